@@ -1,0 +1,33 @@
+# Build the MI355X engine (gfx950) and the CPU oracle.
+#   make            -> ctstraffic_amd/libcts_engine.so + oracle/libcts_oracle.so
+#   make asm        -> ctstraffic_amd/build/cts_kernels-gfx950.s (disassembly for inspection)
+HIPCC     ?= /opt/rocm/bin/hipcc
+ARCH      ?= gfx950
+HIPFLAGS  ?= -O3 -std=c++17 -fPIC -Wall -Wno-unused-result --offload-arch=$(ARCH) -Iinclude -Ictstraffic_amd/csrc
+CSRC      := ctstraffic_amd/csrc
+ENGINE_SO := ctstraffic_amd/libcts_engine.so
+HDRS      := include/cts_engine.h include/cts_pattern.h $(CSRC)/cts_internal.hpp $(wildcard $(CSRC)/*.hpp)
+SRCS      := $(CSRC)/cts_kernels.hip $(CSRC)/cts_engine.cpp $(wildcard $(CSRC)/cts_pattern*.cpp)
+OBJS      := $(patsubst $(CSRC)/%,ctstraffic_amd/build/%.o,$(SRCS))
+
+all: $(ENGINE_SO) oracle
+
+ctstraffic_amd/build/%.o: $(CSRC)/% $(HDRS)
+	@mkdir -p ctstraffic_amd/build
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(ENGINE_SO): $(OBJS)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJS) -Wl,-soname,libcts_engine.so
+
+oracle:
+	$(MAKE) -s -C oracle
+
+asm: $(CSRC)/cts_kernels.hip $(HDRS)
+	@mkdir -p ctstraffic_amd/build
+	$(HIPCC) $(HIPFLAGS) --cuda-device-only -S $< -o ctstraffic_amd/build/cts_kernels-$(ARCH).s
+
+clean:
+	rm -rf ctstraffic_amd/build $(ENGINE_SO)
+	$(MAKE) -s -C oracle clean
+
+.PHONY: all oracle asm clean

@@ -1,0 +1,331 @@
+#!/usr/bin/env python3
+"""bench.py — headline benchmark for the ctsTraffic data-integrity path on MI355X.
+
+Metric (BASELINE.json): "GiB/s verified, 64 KiB buffers device-resident; % MI355X
+HBM roofline". Workload (BASELINE configs[1]): per GPU,
+4096 x 64 KiB received buffers resident in HBM (expected offsets 75 % phase 0,
+25 % random, seed 0xC75; 1 in 1024 buffers carries a one-byte corruption,
+seed 0xBAD). A step = one cts_verify pass over one such batch. The batch
+rotates over R >= 8 identical arenas (2 GiB) so every pass streams from HBM
+rather than the 256 MiB Infinity Cache. The fill kernel (the sender's
+materialisation, InitOnceIoPatternCallback's role) builds the arenas untimed.
+
+Usage:  python bench.py [--gpus N] [--steps K] [--warmup W]
+        N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+Each rank verifies its own shard (no data-path collective: "scaling": "weak");
+one RCCL all-reduce of the 5 ctsStatistics-style counters closes the timed region.
+Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+GIB = float(1 << 30)
+METRIC = "GiB/s verified, 64 KiB buffers device-resident; % MI355X HBM roofline"
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--arenas", type=int, default=8, help="rotated copies of the batch (defeat the 256 MiB MALL)")
+    p.add_argument("--buffers", type=int, default=4096)
+    p.add_argument("--cpu-seconds", type=float, default=8.0, help="budget per CPU-baseline leg")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-extras", action="store_true", help="skip fill / datagram / host-path extras")
+    p.add_argument("--extras-only", default="", help="comma list: fill,datagram,host")
+    return p.parse_args()
+
+
+def dist_env():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return world, rank, local
+
+
+def main():
+    args = parse()
+    world, rank, local = dist_env()
+    import torch
+    import torch.distributed as dist
+
+    if not torch.cuda.is_available():
+        print("bench.py: no HIP device visible", file=sys.stderr)
+        sys.exit(2)
+    torch.cuda.set_device(local)
+    dev = "cuda:%d" % local
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device(dev))
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from ctstraffic_amd import Engine, workload as W
+
+    engine = Engine(local)
+    stream = torch.cuda.current_stream()
+
+    # ---- workload (per rank: weak scaling) --------------------------------------------------
+    w = W.tcp_resident(n_buffers=args.buffers)
+    R = max(1, args.arenas)
+    arenas = []
+    descs = None
+    for _ in range(R):
+        a, d = W.materialize(engine, w, device=dev)
+        arenas.append(a)
+        descs = d
+    first, count, exp_ctr, _ = W.expected_results(w)
+    bytes_per_step = w.verified_bytes()
+    counters = engine.new_counters()
+    torch.cuda.synchronize()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    # ---- warmup -------------------------------------------------------------------------------
+    for i in range(args.warmup):
+        engine.verify(arenas[i % R], descs, max_length_hint=w.max_length, counters=counters)
+    torch.cuda.synchronize()
+    engine.reset_counters(counters)
+    torch.cuda.synchronize()
+
+    # ---- timed region -----------------------------------------------------------------------------
+    K = args.steps
+    ev_s = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
+    ev_e = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
+    ctr_reduced = torch.zeros(5, dtype=torch.int64, device=dev)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(K):
+        ev_s[k].record(stream)
+        engine.verify(arenas[k % R], descs, max_length_hint=w.max_length, counters=counters)
+        ev_e[k].record(stream)
+    if world > 1:
+        # fold the shards on-device and all-reduce the 5 counters over RCCL/xGMI
+        ctr_reduced.copy_(counters.view(-1, 8)[:, :5].sum(0))
+        dist.all_reduce(ctr_reduced)
+    torch.cuda.synchronize()
+    barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    kern_ms = np.array([ev_s[k].elapsed_time(ev_e[k]) for k in range(K)])
+    avg_kernel_s = float(kern_ms.mean()) / 1e3
+    local_ctr = engine.read_counters(counters)
+    parity_ok = local_ctr == {k: v * K for k, v in exp_ctr.items()}
+    if world > 1:
+        glob = ctr_reduced.cpu().tolist()
+        exp_glob = [exp_ctr[f] * K * world for f in ("bytes_checked", "bytes_ok", "buffers_checked",
+                                                      "buffers_failed", "mismatched_bytes")]
+        parity_ok = parity_ok and glob == exp_glob
+        ok_t = torch.tensor([1 if parity_ok else 0], device=dev)
+        dist.all_reduce(ok_t, op=dist.ReduceOp.MIN)
+        parity_ok = bool(ok_t.item())
+
+    total_bytes = bytes_per_step * K * world
+    value = total_bytes / elapsed / GIB
+    achieved_gbps = bytes_per_step / avg_kernel_s / 1e9
+
+    # allreduce latency (separately, outside the headline)
+    allreduce_us = None
+    if world > 1:
+        torch.cuda.synchronize()
+        ta = time.perf_counter()
+        for _ in range(20):
+            dist.all_reduce(ctr_reduced)
+        torch.cuda.synchronize()
+        allreduce_us = (time.perf_counter() - ta) / 20 * 1e6
+
+    extras = {}
+    cpu = None
+    if rank == 0 and world == 1:
+        want = set(x for x in args.extras_only.split(",") if x) or {"fill", "datagram", "host"}
+        if not args.no_extras:
+            extras = run_extras(engine, torch, W, w, arenas, descs, dev, want)
+        if not args.no_cpu_baseline:
+            cpu = cpu_baseline(arenas[0], w, args.cpu_seconds)
+
+    traffic = None
+    tp = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_traffic.json")
+    if os.path.exists(tp):
+        try:
+            tj = json.load(open(tp))
+            if tj.get("workload") == w.name and tj.get("buffers") == args.buffers:
+                traffic = tj.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / K * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (seeded pattern fill + 1/1024 one-byte corruptions, seeds 0xC75/0xBAD)",
+            "config": {
+                "workload": "config2: %d x 64 KiB received buffers resident in HBM per GPU, cts_verify "
+                            "(RtlCompareMemory semantics), %d rotated arenas" % (args.buffers, R),
+                "buffers_per_gpu": args.buffers,
+                "buffer_bytes": 65536,
+                "verified_bytes_per_step_per_gpu": bytes_per_step,
+                "arenas_rotated": R,
+                "parallelism": "hash-sharded, %d rank(s), no data-path collective" % world,
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved_gbps, 1),
+                "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s",
+                "frac": round(achieved_gbps / HBM_PEAK_GBPS, 4),
+                "traffic": traffic,
+                "kernel": "cts::verify_kernel<256,8,true>",
+                "avg_kernel_us": round(avg_kernel_s * 1e6, 2),
+                "algorithmic_bytes_per_launch": bytes_per_step,
+            },
+            "cpu_baseline": cpu,
+            "parity": {"counters_match_expected": bool(parity_ok), "counters": local_ctr},
+        }
+        if allreduce_us is not None:
+            line["allreduce_counters_us"] = round(allreduce_us, 1)
+        if extras:
+            line["extras"] = extras
+        print(json.dumps(line), flush=True)
+    engine.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def _time_kernel(torch, fn, steps):
+    s = torch.cuda.current_stream()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    for i in range(steps):
+        evs[i][0].record(s)
+        fn(i)
+        evs[i][1].record(s)
+    torch.cuda.synchronize()
+    return float(np.mean([a.elapsed_time(b) for a, b in evs])) / 1e3
+
+
+def run_extras(engine, torch, W, w, arenas, descs, dev, want):
+    out = {}
+    R = len(arenas)
+    nbytes = w.verified_bytes()
+    if "fill" in want:
+        # fill kernel over the same batch (write-bound twin); re-materialise corruptions afterwards
+        t = _time_kernel(torch, lambda i: engine.fill(arenas[i % R], descs, max_length_hint=w.max_length), 100)
+        out["fill_GiBps"] = round(nbytes / t / GIB, 1)
+        out["fill_GBps"] = round(nbytes / t / 1e9, 1)
+        # fused view: fill + verify of the same batch back to back
+        ctr = engine.new_counters()
+
+        def fv(i):
+            engine.fill(arenas[i % R], descs, max_length_hint=w.max_length)
+            engine.verify(arenas[i % R], descs, max_length_hint=w.max_length, counters=ctr)
+
+        t = _time_kernel(torch, fv, 50)
+        out["fill_then_verify_GiBps_verified"] = round(nbytes / t / GIB, 1)
+        for a in arenas:  # restore the corruption plan
+            pos = torch.from_numpy(w.corrupt_abs_offsets()).to(dev)
+            a[pos] = a[pos] ^ torch.from_numpy(w.corrupt_xor).to(dev)
+    if "datagram" in want:
+        try:
+            wd = W.udp_datagrams(n_datagrams=4 * 1024 * 1024)
+            ad, dd = W.materialize(engine, wd, device=dev)
+            ctr = engine.new_counters()
+            t = _time_kernel(torch, lambda i: engine.verify(ad, dd, max_length_hint=wd.max_length, counters=ctr), 20)
+            out["datagram_1472_verify_GiBps"] = round(wd.verified_bytes() / t / GIB, 1)
+            out["datagram_1472_verify_Mdgram_per_s"] = round(wd.n / t / 1e6, 1)
+            out["datagram_config"] = "4M x 1472 B (26 B header skipped), 1/4 of config 3"
+            del ad, dd
+        except Exception as e:  # pragma: no cover
+            out["datagram_error"] = repr(e)
+    if "host" in want:
+        try:
+            # pinned, device-mapped host arena = the recv-buffer container of a GPU-verified ctsIoPattern
+            hview, hptr, dptr = engine.host_alloc(arenas[0].numel())
+            hview[:] = arenas[0].cpu().numpy()
+            ctr = engine.new_counters()
+            # (a) zero-copy: the verify kernel reads the pinned host arena in place over PCIe
+            t = _time_kernel(torch, lambda i: engine.verify_ptr(dptr, hview.size, descs, max_length_hint=w.max_length,
+                                                                 counters=ctr), 5)
+            out["host_zero_copy_verify_GiBps"] = round(nbytes / t / GIB, 2)
+            ok = engine.read_counters(ctr)["buffers_failed"] == 5 * len(np.unique(w.corrupt_buf))
+            out["host_zero_copy_parity"] = bool(ok)
+            # (b) pinned hipMemcpyAsync H2D then device verify
+            host_t = torch.from_numpy(hview)
+            dst = torch.empty_like(arenas[0])
+
+            def h2d(i):
+                dst.copy_(host_t, non_blocking=True)
+                engine.verify(dst, descs, max_length_hint=w.max_length, counters=ctr)
+
+            t = _time_kernel(torch, h2d, 5)
+            out["host_h2d_then_verify_GiBps"] = round(nbytes / t / GIB, 2)
+            del dst, host_t
+            torch.cuda.synchronize()
+            engine.host_free(hptr)
+        except Exception as e:  # pragma: no cover
+            out["host_error"] = repr(e)
+    return out
+
+
+def cpu_baseline(arena, w, seconds):
+    """The oracle (g++/gcc restatement of VerifyBuffer, RtlCompareMemory semantics) on this host's
+    cores over a host copy of the same batch. Bounded: ~`seconds` per leg."""
+    import oracle
+
+    host = arena.cpu().numpy()
+    nthreads = max(1, min(16, os.cpu_count() or 1))
+    legs = {}
+    for nt in (1, nthreads):
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            oracle.verify_batch(host, w.descs, nthreads=nt, want_results=False)
+            reps += 1
+            if time.perf_counter() - t0 >= seconds:
+                break
+        el = time.perf_counter() - t0
+        legs[nt] = w.verified_bytes() * reps / el / GIB
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except Exception:
+        pass
+    return {
+        "value": round(legs[nthreads], 2),
+        "unit": "GiB/s",
+        "cores": nthreads,
+        "kind": "port",
+        "sample": "config2 batch (%d x 64 KiB, 256 MiB host copy of the same arena), repeated for ~%.0f s per leg"
+                  % (w.n, seconds),
+        "single_thread_value": round(legs[1], 2),
+        "cpu_model": model,
+    }
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,372 @@
+// cts_engine.cpp — the C ABI (include/cts_engine.h) over the gfx950 kernels.
+//
+// Every entry point is noexcept and returns a cts_status, mirroring the
+// reference's noexcept IO surface (ctsIOPattern.h:143-144) while replacing its
+// FAIL_FAST process aborts with error codes a foreign caller can handle.
+#include <hip/hip_runtime_api.h>
+
+#include <atomic>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "cts_engine.h"
+#include "cts_internal.hpp"
+
+struct cts_engine {
+    int device = 0;
+    cts::LaunchGeometry geo;
+    std::mutex host_mu;  // serialises the single-buffer host path (shared staging)
+    hipStream_t stream = nullptr;
+    // single-buffer host staging: pinned, device-mapped (zero-copy reads over PCIe)
+    uint8_t* stage = nullptr;
+    size_t stage_cap = 0;
+    cts_buf_desc* stage_desc = nullptr;       // pinned, device-mapped
+    cts_verify_result* stage_res = nullptr;   // pinned, device-mapped
+};
+
+namespace {
+
+int env_int(const char* name, int dflt)
+{
+    const char* v = std::getenv(name);
+    if (v == nullptr || *v == 0) return dflt;
+    return std::atoi(v);
+}
+
+struct DeviceGuard {
+    int prev = -1;
+    bool ok = false;
+    explicit DeviceGuard(int dev)
+    {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        ok = (prev == dev) || (hipSetDevice(dev) == hipSuccess);
+    }
+    ~DeviceGuard()
+    {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+inline int hip_status(hipError_t e) { return e == hipSuccess ? CTS_OK : CTS_E_HIP; }
+
+// Pinned host memory that the device reads directly (hipHostMalloc memory is
+// mapped into the device address space).
+int host_alloc_mapped(size_t bytes, void** out)
+{
+    void* p = nullptr;
+    if (hipHostMalloc(&p, bytes, hipHostMallocMapped | hipHostMallocPortable) != hipSuccess) return CTS_E_NOMEM;
+    *out = p;
+    return CTS_OK;
+}
+
+template <typename T>
+T* device_view(T* host)
+{
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, host, 0) != hipSuccess) return nullptr;
+    return static_cast<T*>(d);
+}
+
+int ensure_stage(cts_engine* e, size_t bytes)
+{
+    if (e->stage_cap >= bytes) return CTS_OK;
+    if (e->stage) (void)hipHostFree(e->stage);
+    e->stage = nullptr;
+    e->stage_cap = 0;
+    size_t cap = 1u << 20;
+    while (cap < bytes) cap <<= 1;
+    void* p = nullptr;
+    const int rc = host_alloc_mapped(cap, &p);
+    if (rc != CTS_OK) return rc;
+    e->stage = static_cast<uint8_t*>(p);
+    e->stage_cap = cap;
+    return CTS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* cts_version(void) { return "ctstraffic_amd 0.1.0 (gfx950)"; }
+
+const char* cts_status_string(int status)
+{
+    switch (status) {
+    case CTS_OK: return "ok";
+    case CTS_E_INVALID: return "invalid argument";
+    case CTS_E_HIP: return "HIP runtime error";
+    case CTS_E_NOMEM: return "out of memory";
+    case CTS_E_NO_DEVICE: return "no such HIP device";
+    default: return "unknown status";
+    }
+}
+
+uint8_t cts_pattern_byte(uint64_t stream_offset)
+{
+    const uint32_t j = (uint32_t)(stream_offset & 0xFFFFu);
+    return (uint8_t)((j & 1u) ? (j >> 9) : ((j >> 1) & 0xFFu));
+}
+
+uint64_t cts_sender_buffer_size(uint32_t max_buffer_size) { return (uint64_t)CTS_PATTERN_PERIOD + max_buffer_size; }
+
+int cts_engine_create(int device, cts_engine** out)
+{
+    if (out == nullptr) return CTS_E_INVALID;
+    *out = nullptr;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return CTS_E_NO_DEVICE;
+    if (device < 0 || device >= count) return CTS_E_NO_DEVICE;
+    DeviceGuard g(device);
+    if (!g.ok) return CTS_E_HIP;
+    cts_engine* e = new (std::nothrow) cts_engine();
+    if (e == nullptr) return CTS_E_NOMEM;
+    e->device = device;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
+        e->geo.num_cus = cus;
+    e->geo.blocks_per_cu = env_int("CTS_BLOCKS_PER_CU", e->geo.blocks_per_cu);
+    e->geo.nontemporal = env_int("CTS_NT_LOADS", e->geo.nontemporal);
+    e->geo.small_threshold = env_int("CTS_SMALL_THRESHOLD", e->geo.small_threshold);
+    if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete e;
+        return CTS_E_HIP;
+    }
+    void* p = nullptr;
+    if (host_alloc_mapped(sizeof(cts_buf_desc), &p) != CTS_OK) {
+        cts_engine_destroy(e);
+        return CTS_E_NOMEM;
+    }
+    e->stage_desc = static_cast<cts_buf_desc*>(p);
+    if (host_alloc_mapped(sizeof(cts_verify_result), &p) != CTS_OK) {
+        cts_engine_destroy(e);
+        return CTS_E_NOMEM;
+    }
+    e->stage_res = static_cast<cts_verify_result*>(p);
+    *out = e;
+    return CTS_OK;
+}
+
+int cts_engine_destroy(cts_engine* e)
+{
+    if (e == nullptr) return CTS_E_INVALID;
+    {
+        DeviceGuard g(e->device);
+        if (e->stream) {
+            (void)hipStreamSynchronize(e->stream);
+            (void)hipStreamDestroy(e->stream);
+        }
+        if (e->stage) (void)hipHostFree(e->stage);
+        if (e->stage_desc) (void)hipHostFree(e->stage_desc);
+        if (e->stage_res) (void)hipHostFree(e->stage_res);
+    }
+    delete e;
+    return CTS_OK;
+}
+
+int cts_engine_device(const cts_engine* e) { return e ? e->device : CTS_E_INVALID; }
+
+int cts_sender_buffer_fill(cts_engine* e, void* dev_dst, uint32_t max_buffer_size, void* stream)
+{
+    if (e == nullptr || dev_dst == nullptr || ((uintptr_t)dev_dst & 15u) != 0) return CTS_E_INVALID;
+    DeviceGuard g(e->device);
+    if (!g.ok) return CTS_E_HIP;
+    return hip_status(cts::launch_fill_span(static_cast<uint8_t*>(dev_dst), cts_sender_buffer_size(max_buffer_size), 0,
+                                            static_cast<hipStream_t>(stream), e->geo));
+}
+
+int cts_fill(cts_engine* e, void* dev_arena, uint64_t arena_bytes, const cts_buf_desc* dev_descs, uint32_t n,
+             uint32_t max_length_hint, void* stream)
+{
+    if (e == nullptr) return CTS_E_INVALID;
+    if (n == 0) return CTS_OK;
+    if (dev_arena == nullptr || dev_descs == nullptr || ((uintptr_t)dev_arena & 15u) != 0) return CTS_E_INVALID;
+    DeviceGuard g(e->device);
+    if (!g.ok) return CTS_E_HIP;
+    return hip_status(cts::launch_fill(static_cast<uint8_t*>(dev_arena), arena_bytes, dev_descs, n, max_length_hint,
+                                       static_cast<hipStream_t>(stream), e->geo));
+}
+
+int cts_verify(cts_engine* e, const void* dev_arena, uint64_t arena_bytes, const cts_buf_desc* dev_descs, uint32_t n,
+               uint32_t max_length_hint, cts_verify_result* dev_results, void* dev_counters,
+               uint32_t* dev_conn_first_fail, uint32_t n_conns, void* stream)
+{
+    if (e == nullptr) return CTS_E_INVALID;
+    if (n == 0) return CTS_OK;
+    if (dev_arena == nullptr || dev_descs == nullptr || ((uintptr_t)dev_arena & 15u) != 0) return CTS_E_INVALID;
+    if (dev_conn_first_fail == nullptr && n_conns != 0) return CTS_E_INVALID;
+    DeviceGuard g(e->device);
+    if (!g.ok) return CTS_E_HIP;
+    return hip_status(cts::launch_verify(static_cast<const uint8_t*>(dev_arena), arena_bytes, dev_descs, n,
+                                         max_length_hint, dev_results, static_cast<uint64_t*>(dev_counters),
+                                         dev_conn_first_fail, n_conns, static_cast<hipStream_t>(stream), e->geo));
+}
+
+size_t cts_counters_device_bytes(void) { return (size_t)CTS_COUNTER_SHARDS * cts::kCounterSlots * sizeof(uint64_t); }
+
+int cts_counters_reset(cts_engine* e, void* dev_counters, void* stream)
+{
+    if (e == nullptr || dev_counters == nullptr) return CTS_E_INVALID;
+    DeviceGuard g(e->device);
+    if (!g.ok) return CTS_E_HIP;
+    return hip_status(hipMemsetAsync(dev_counters, 0, cts_counters_device_bytes(), static_cast<hipStream_t>(stream)));
+}
+
+int cts_counters_read(cts_engine* e, const void* dev_counters, cts_counters* out, void* stream)
+{
+    if (e == nullptr || dev_counters == nullptr || out == nullptr) return CTS_E_INVALID;
+    DeviceGuard g(e->device);
+    if (!g.ok) return CTS_E_HIP;
+    std::vector<uint64_t> h(CTS_COUNTER_SHARDS * cts::kCounterSlots);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (hipMemcpyAsync(h.data(), dev_counters, cts_counters_device_bytes(), hipMemcpyDeviceToHost, s) != hipSuccess)
+        return CTS_E_HIP;
+    if (hipStreamSynchronize(s) != hipSuccess) return CTS_E_HIP;
+    uint64_t v[5] = {0, 0, 0, 0, 0};
+    for (uint32_t sh = 0; sh < CTS_COUNTER_SHARDS; ++sh)
+        for (int k = 0; k < 5; ++k) v[k] += h[sh * cts::kCounterSlots + k];
+    out->bytes_checked = v[cts::kBytesChecked];
+    out->bytes_ok = v[cts::kBytesOk];
+    out->buffers_checked = v[cts::kBuffersChecked];
+    out->buffers_failed = v[cts::kBuffersFailed];
+    out->mismatched_bytes = v[cts::kMismatchedBytes];
+    return CTS_OK;
+}
+
+int cts_host_alloc(cts_engine* e, uint64_t bytes, void** host_ptr, void** dev_view)
+{
+    if (e == nullptr || host_ptr == nullptr || bytes == 0) return CTS_E_INVALID;
+    DeviceGuard g(e->device);
+    if (!g.ok) return CTS_E_HIP;
+    void* p = nullptr;
+    const int rc = host_alloc_mapped((size_t)((bytes + 15u) & ~(uint64_t)15u), &p);
+    if (rc != CTS_OK) return rc;
+    *host_ptr = p;
+    if (dev_view != nullptr) {
+        void* d = nullptr;
+        if (hipHostGetDevicePointer(&d, p, 0) != hipSuccess) {
+            (void)hipHostFree(p);
+            *host_ptr = nullptr;
+            return CTS_E_HIP;
+        }
+        *dev_view = d;
+    }
+    return CTS_OK;
+}
+
+int cts_host_free(cts_engine* e, void* host_ptr)
+{
+    if (e == nullptr || host_ptr == nullptr) return CTS_E_INVALID;
+    DeviceGuard g(e->device);
+    return hip_status(hipHostFree(host_ptr));
+}
+
+int cts_host_device_pointer(void* host_ptr, void** dev_view)
+{
+    if (host_ptr == nullptr || dev_view == nullptr) return CTS_E_INVALID;
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, host_ptr, 0) != hipSuccess) return CTS_E_INVALID;
+    *dev_view = d;
+    return CTS_OK;
+}
+
+int cts_verify_host(cts_engine* e, const void* host_buf, uint32_t len, uint32_t expected_offset, cts_verify_result* out)
+{
+    if (e == nullptr || out == nullptr || (host_buf == nullptr && len != 0)) return CTS_E_INVALID;
+    if (expected_offset >= CTS_PATTERN_PERIOD) return CTS_E_INVALID;
+    std::lock_guard<std::mutex> lk(e->host_mu);
+    DeviceGuard g(e->device);
+    if (!g.ok) return CTS_E_HIP;
+    int rc = ensure_stage(e, (size_t)len + 16);
+    if (rc != CTS_OK) return rc;
+    if (len) std::memcpy(e->stage, host_buf, len);
+    cts_buf_desc d;
+    d.byte_offset = 0;
+    d.length = len;
+    d.expected_pattern_offset = expected_offset;
+    d.conn_index = 0;
+    d.skip_head = 0;
+    *e->stage_desc = d;
+    const uint8_t* arena = device_view(e->stage);
+    const cts_buf_desc* dd = device_view(e->stage_desc);
+    cts_verify_result* dr = device_view(e->stage_res);
+    if (!arena || !dd || !dr) return CTS_E_HIP;
+    hipError_t err = cts::launch_verify(arena, e->stage_cap, dd, 1, len, dr, nullptr, nullptr, 0, e->stream, e->geo);
+    if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
+    if (err != hipSuccess) return CTS_E_HIP;
+    *out = *e->stage_res;
+    return CTS_OK;
+}
+
+int cts_verify_host_batch(cts_engine* e, const void* const* bufs, const uint32_t* lens, const uint32_t* expected,
+                          const uint32_t* skip_heads, uint32_t n, cts_verify_result* results, cts_counters* counters)
+{
+    if (e == nullptr) return CTS_E_INVALID;
+    if (n == 0) return CTS_OK;
+    if (bufs == nullptr || lens == nullptr || expected == nullptr || results == nullptr) return CTS_E_INVALID;
+    std::lock_guard<std::mutex> lk(e->host_mu);
+    DeviceGuard g(e->device);
+    if (!g.ok) return CTS_E_HIP;
+    // Stage every buffer into one pinned, device-mapped arena (16-byte aligned
+    // slots), describe it, verify it in place over PCIe, read results.
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        if (bufs[i] == nullptr && lens[i] != 0) return CTS_E_INVALID;
+        total += ((uint64_t)lens[i] + 15u) & ~(uint64_t)15u;
+    }
+    void* pdesc = nullptr;
+    void* pres = nullptr;
+    void* pctr = nullptr;
+    int rc = ensure_stage(e, (size_t)total + 16);
+    if (rc != CTS_OK) return rc;
+    if ((rc = host_alloc_mapped(sizeof(cts_buf_desc) * n, &pdesc)) != CTS_OK) return rc;
+    if ((rc = host_alloc_mapped(sizeof(cts_verify_result) * n, &pres)) != CTS_OK) {
+        (void)hipHostFree(pdesc);
+        return rc;
+    }
+    if (counters && (rc = host_alloc_mapped(cts_counters_device_bytes(), &pctr)) != CTS_OK) {
+        (void)hipHostFree(pdesc);
+        (void)hipHostFree(pres);
+        return rc;
+    }
+    cts_buf_desc* hd = static_cast<cts_buf_desc*>(pdesc);
+    uint64_t off = 0;
+    uint32_t maxlen = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        if (lens[i]) std::memcpy(e->stage + off, bufs[i], lens[i]);
+        hd[i].byte_offset = off;
+        hd[i].length = lens[i];
+        hd[i].expected_pattern_offset = expected[i];
+        hd[i].conn_index = i;
+        hd[i].skip_head = skip_heads ? skip_heads[i] : 0u;
+        maxlen = lens[i] > maxlen ? lens[i] : maxlen;
+        off += ((uint64_t)lens[i] + 15u) & ~(uint64_t)15u;
+    }
+    if (pctr) std::memset(pctr, 0, cts_counters_device_bytes());
+    hipError_t err = cts::launch_verify(device_view(e->stage), e->stage_cap, device_view(hd), n, maxlen,
+                                        device_view(static_cast<cts_verify_result*>(pres)),
+                                        pctr ? device_view(static_cast<uint64_t*>(pctr)) : nullptr, nullptr, 0,
+                                        e->stream, e->geo);
+    if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
+    if (err == hipSuccess) {
+        std::memcpy(results, pres, sizeof(cts_verify_result) * n);
+        if (counters) {
+            const uint64_t* h = static_cast<const uint64_t*>(pctr);
+            for (uint32_t sh = 0; sh < CTS_COUNTER_SHARDS; ++sh) {
+                counters->bytes_checked += h[sh * cts::kCounterSlots + cts::kBytesChecked];
+                counters->bytes_ok += h[sh * cts::kCounterSlots + cts::kBytesOk];
+                counters->buffers_checked += h[sh * cts::kCounterSlots + cts::kBuffersChecked];
+                counters->buffers_failed += h[sh * cts::kCounterSlots + cts::kBuffersFailed];
+                counters->mismatched_bytes += h[sh * cts::kCounterSlots + cts::kMismatchedBytes];
+            }
+        }
+    }
+    (void)hipHostFree(pdesc);
+    (void)hipHostFree(pres);
+    if (pctr) (void)hipHostFree(pctr);
+    return err == hipSuccess ? CTS_OK : CTS_E_HIP;
+}
+
+}  // extern "C"

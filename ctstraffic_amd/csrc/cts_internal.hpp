@@ -1,0 +1,36 @@
+// cts_internal.hpp — launchers shared between the kernel TU and the C-ABI TU.
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+#include <stdint.h>
+
+#include "cts_engine.h"
+
+namespace cts {
+
+// Device counter block: CTS_COUNTER_SHARDS rows of 8 u64 (64 B each); a
+// workgroup adds its totals to row (blockIdx.x % CTS_COUNTER_SHARDS) so the
+// adds of a 2048-block grid spread over 64 lines instead of one.
+constexpr int kCounterSlots = 8;  // 5 used, padded to one 64-byte line
+enum CounterSlot { kBytesChecked = 0, kBytesOk = 1, kBuffersChecked = 2, kBuffersFailed = 3, kMismatchedBytes = 4 };
+
+struct LaunchGeometry {
+    int num_cus = 256;        // hipDeviceAttributeMultiprocessorCount
+    int blocks_per_cu = 8;    // grid cap = num_cus * blocks_per_cu (grid-stride beyond)
+    int nontemporal = 1;      // nt loads for the once-read verify stream
+    int small_threshold = 8192;  // max_length_hint <= this -> one wave per buffer
+};
+
+hipError_t launch_verify(const uint8_t* arena, uint64_t arena_bytes, const cts_buf_desc* descs, uint32_t n,
+                         uint32_t max_length_hint, cts_verify_result* results, uint64_t* counters,
+                         uint32_t* conn_first_fail, uint32_t n_conns, hipStream_t stream,
+                         const LaunchGeometry& geo);
+
+hipError_t launch_fill(uint8_t* arena, uint64_t arena_bytes, const cts_buf_desc* descs, uint32_t n,
+                       uint32_t max_length_hint, hipStream_t stream, const LaunchGeometry& geo);
+
+// dst[i] = P((pattern_offset + i) mod 65536) for i < bytes; many blocks per span.
+hipError_t launch_fill_span(uint8_t* dst, uint64_t bytes, uint32_t pattern_offset, hipStream_t stream,
+                            const LaunchGeometry& geo);
+
+}  // namespace cts

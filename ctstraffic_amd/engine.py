@@ -1,0 +1,185 @@
+"""Python handle over the C ABI (``include/cts_engine.h``).
+
+torch tensors are used only as device-memory/stream plumbing: their
+``data_ptr()`` and the current HIP stream are passed straight through the
+C ABI, which never sees a torch type.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import CtsCounters, CtsVerifyResult, check, lib
+from .types import DESC_DTYPE, RESULT_DTYPE
+
+try:
+    import torch
+except Exception:  # pragma: no cover
+    torch = None
+
+
+def _ptr(x) -> Optional[int]:
+    if x is None:
+        return None
+    if isinstance(x, int):
+        return x
+    if torch is not None and isinstance(x, torch.Tensor):
+        return x.data_ptr()
+    if isinstance(x, np.ndarray):
+        return x.ctypes.data
+    raise TypeError("unsupported buffer type %r" % type(x))
+
+
+def _nbytes(x) -> int:
+    if torch is not None and isinstance(x, torch.Tensor):
+        return x.numel() * x.element_size()
+    if isinstance(x, np.ndarray):
+        return x.nbytes
+    raise TypeError("unsupported buffer type %r" % type(x))
+
+
+def _stream(stream) -> Optional[int]:
+    if stream is None:
+        if torch is not None and torch.cuda.is_available():
+            return torch.cuda.current_stream().cuda_stream
+        return None
+    if isinstance(stream, int):
+        return stream
+    return stream.cuda_stream
+
+
+def pattern_byte(stream_offset: int) -> int:
+    """Byte of g_senderSharedBuffer at a stream offset (ctsIOPattern.cpp:55-80)."""
+    return int(lib().cts_pattern_byte(stream_offset))
+
+
+def sender_buffer_size(max_buffer_size: int) -> int:
+    return int(lib().cts_sender_buffer_size(max_buffer_size))
+
+
+def descs_to_device(descs: np.ndarray, device="cuda"):
+    """Structured DESC_DTYPE array -> uint8 device tensor (24 bytes per descriptor)."""
+    descs = np.ascontiguousarray(descs, dtype=DESC_DTYPE)
+    return torch.from_numpy(descs.view(np.uint8).copy()).to(device)
+
+
+def results_from_device(t) -> np.ndarray:
+    return t.cpu().numpy().view(RESULT_DTYPE)
+
+
+class Engine:
+    """One engine per GPU (cts_engine_create). Thread-safe across streams."""
+
+    def __init__(self, device: int = 0):
+        h = ctypes.c_void_p()
+        check("cts_engine_create", lib().cts_engine_create(device, ctypes.byref(h)))
+        self._h = h
+        self.device = device
+
+    # ---- lifetime ----------------------------------------------------------
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None and self._h.value:
+            lib().cts_engine_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- fill ----------------------------------------------------------------
+    def sender_buffer(self, max_buffer_size: int, stream=None):
+        """Device copy of g_senderSharedBuffer (InitOnceIoPatternCallback, ctsIOPattern.cpp:52-90)."""
+        n = sender_buffer_size(max_buffer_size)
+        out = torch.empty(n + 16, dtype=torch.uint8, device="cuda:%d" % self.device)[:n]
+        check("cts_sender_buffer_fill",
+              lib().cts_sender_buffer_fill(self._h, _ptr(out), max_buffer_size, _stream(stream)))
+        return out
+
+    def fill(self, arena, descs, max_length_hint: int = 0, stream=None) -> None:
+        n = _nbytes(descs) // DESC_DTYPE.itemsize
+        check("cts_fill", lib().cts_fill(self._h, _ptr(arena), _nbytes(arena), _ptr(descs), n, max_length_hint,
+                                         _stream(stream)))
+
+    # ---- verify --------------------------------------------------------------
+    def verify(self, arena, descs, *, max_length_hint: int = 0, results=None, counters=None,
+               conn_first_fail=None, stream=None) -> None:
+        n = _nbytes(descs) // DESC_DTYPE.itemsize
+        n_conns = 0 if conn_first_fail is None else _nbytes(conn_first_fail) // 4
+        check("cts_verify", lib().cts_verify(self._h, _ptr(arena), _nbytes(arena), _ptr(descs), n, max_length_hint,
+                                             _ptr(results), _ptr(counters), _ptr(conn_first_fail), n_conns,
+                                             _stream(stream)))
+
+    def new_results(self, n: int):
+        return torch.zeros(n * RESULT_DTYPE.itemsize, dtype=torch.uint8, device="cuda:%d" % self.device)
+
+    # ---- counters --------------------------------------------------------------
+    def new_counters(self):
+        nbytes = int(lib().cts_counters_device_bytes())
+        return torch.zeros(nbytes // 8, dtype=torch.int64, device="cuda:%d" % self.device)
+
+    def reset_counters(self, counters, stream=None) -> None:
+        check("cts_counters_reset", lib().cts_counters_reset(self._h, _ptr(counters), _stream(stream)))
+
+    def read_counters(self, counters, stream=None) -> dict:
+        c = CtsCounters()
+        check("cts_counters_read", lib().cts_counters_read(self._h, _ptr(counters), ctypes.byref(c),
+                                                           _stream(stream)))
+        return c.as_dict()
+
+    # ---- pinned host arenas ---------------------------------------------------------
+    def host_alloc(self, nbytes: int):
+        """Pinned, device-mapped host arena. Returns (numpy uint8 view, host ptr, device-view ptr)."""
+        h, d = ctypes.c_void_p(), ctypes.c_void_p()
+        check("cts_host_alloc", lib().cts_host_alloc(self._h, nbytes, ctypes.byref(h), ctypes.byref(d)))
+        arr = np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(h.value))
+        return arr, h.value, d.value
+
+    def host_free(self, host_ptr: int) -> None:
+        check("cts_host_free", lib().cts_host_free(self._h, host_ptr))
+
+    def verify_ptr(self, arena_ptr: int, arena_bytes: int, descs, *, max_length_hint: int = 0, results=None,
+                   counters=None, stream=None) -> None:
+        """cts_verify on a raw device address (e.g. the device view of a pinned host arena)."""
+        n = _nbytes(descs) // DESC_DTYPE.itemsize
+        check("cts_verify", lib().cts_verify(self._h, arena_ptr, arena_bytes, _ptr(descs), n, max_length_hint,
+                                             _ptr(results), _ptr(counters), None, 0, _stream(stream)))
+
+    # ---- host buffers (drop-in VerifyBuffer) ------------------------------------
+    def verify_host(self, buf, expected_offset: int) -> dict:
+        a = np.frombuffer(bytes(buf), dtype=np.uint8) if not isinstance(buf, np.ndarray) else buf
+        a = np.ascontiguousarray(a, dtype=np.uint8)
+        r = CtsVerifyResult()
+        check("cts_verify_host", lib().cts_verify_host(self._h, a.ctypes.data if a.size else None, a.size,
+                                                       expected_offset, ctypes.byref(r)))
+        return {"pass": bool(r.pass_), "first_mismatch": r.first_mismatch, "mismatch_bytes": r.mismatch_bytes,
+                "expected": r.expected, "actual": r.actual, "flags": r.flags}
+
+    def verify_host_batch(self, bufs: Sequence[np.ndarray], expected: Sequence[int],
+                          skip_heads: Optional[Sequence[int]] = None):
+        n = len(bufs)
+        arrs = [np.ascontiguousarray(b, dtype=np.uint8) for b in bufs]
+        ptrs = (ctypes.c_void_p * n)(*[a.ctypes.data if a.size else None for a in arrs])
+        lens = np.array([a.size for a in arrs], dtype=np.uint32)
+        exp = np.array(expected, dtype=np.uint32)
+        skips = None if skip_heads is None else np.array(skip_heads, dtype=np.uint32)
+        results = np.zeros(n, dtype=RESULT_DTYPE)
+        c = CtsCounters()
+        check("cts_verify_host_batch",
+              lib().cts_verify_host_batch(self._h, ptrs, lens.ctypes.data, exp.ctypes.data,
+                                          None if skips is None else skips.ctypes.data, n, results.ctypes.data,
+                                          ctypes.byref(c)))
+        return results, c.as_dict()
+
+
+__all__ = ["Engine", "pattern_byte", "sender_buffer_size", "descs_to_device", "results_from_device", "_lib"]

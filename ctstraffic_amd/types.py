@@ -1,0 +1,28 @@
+"""numpy mirrors of the C ABI structs (include/cts_engine.h)."""
+import numpy as np
+
+# cts_buf_desc: the ctsTask fields the hot path reads (ctsIOTask.hpp:37-60)
+DESC_DTYPE = np.dtype(
+    [
+        ("byte_offset", "<u8"),
+        ("length", "<u4"),
+        ("expected_pattern_offset", "<u4"),
+        ("conn_index", "<u4"),
+        ("skip_head", "<u4"),
+    ]
+)
+# cts_verify_result
+RESULT_DTYPE = np.dtype(
+    [
+        ("first_mismatch", "<u4"),
+        ("mismatch_bytes", "<u4"),
+        ("expected", "u1"),
+        ("actual", "u1"),
+        ("pass", "u1"),
+        ("flags", "u1"),
+    ]
+)
+COUNTER_FIELDS = ("bytes_checked", "bytes_ok", "buffers_checked", "buffers_failed", "mismatched_bytes")
+RESULT_FLAG_BAD_DESC = 0x1
+
+assert DESC_DTYPE.itemsize == 24 and RESULT_DTYPE.itemsize == 12

@@ -1,0 +1,189 @@
+/*
+ * cts_engine.h — C ABI of the MI355X-native ctsTraffic data-integrity engine.
+ *
+ * The engine replaces the two hot-path pieces of ctsTraffic's ctsIoPattern
+ * (reference: /root/reference, microsoft/ctsTraffic):
+ *
+ *   fill   = InitOnceIoPatternCallback            ctsTraffic/ctsIOPattern.cpp:52-90
+ *            (+ per-buffer materialisation of the sender stream)
+ *   verify = ctsIoPattern::VerifyBuffer            ctsTraffic/ctsIOPattern.cpp:745-775
+ *            (decl. ctsTraffic/ctsIOPattern.h:329), RtlCompareMemory semantics
+ *
+ * Both are reached in the reference only through ctsIoPattern::CompleteIo
+ * (ctsIOPattern.cpp:364-534) and the ctsIoPattern constructor, so the IO
+ * functors (ctsSendRecvIocp.cpp, ctsRioIocp.cpp, ctsMediaStreamClient.cpp)
+ * stay unchanged; the host-side ctsIoPattern mirror lives in cts_pattern.h.
+ *
+ * Conventions (ctsIOPattern.h:143-144 are noexcept; FAIL_FAST on internal
+ * inconsistency): every entry point is noexcept and returns an int status,
+ * 0 = CTS_OK, negative = error (see cts_status). No entry point throws.
+ * Device pointers are plain pointers obtained from hipMalloc (or any
+ * allocator of the same process/runtime); `stream` is a hipStream_t passed
+ * as void* (NULL = the legacy null stream). No torch types cross this ABI.
+ *
+ * Thread safety: an engine may be used concurrently from many threads as
+ * long as each thread passes its own stream (the reference serialises per
+ * connection under the ctsSocket lock, ctsSocket.h:189, and runs many
+ * connections concurrently on the NT threadpool).
+ */
+#ifndef CTS_ENGINE_H
+#define CTS_ENGINE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* c_bufferPatternSize = 0xffff + 1 (ctsIOPattern.cpp:35). The byte stream
+ * repeats every 65536 bytes: u16 little-endian values 0..32767
+ * (ctsIOPattern.cpp:55-58 build 0..65535, but only the first 65536 bytes are
+ * ever copied into the sender buffer, ctsIOPattern.cpp:72-80). */
+#define CTS_PATTERN_PERIOD 65536u
+/* c_udpDatagramDataHeaderLength = 2 + 8 + 8 + 8 (ctsMediaStreamProtocol.hpp:43-52) */
+#define CTS_UDP_DATA_HEADER_LENGTH 26u
+/* c_statusErrorDataDidNotMatchBitPattern = MAXINT - 3 (ctsIOPattern.h:49) */
+#define CTS_STATUS_ERROR_DATA_DID_NOT_MATCH_BIT_PATTERN 2147483644u
+/* Number of 64-byte counter shards in a device counter block. */
+#define CTS_COUNTER_SHARDS 64u
+
+typedef enum cts_status {
+    CTS_OK = 0,
+    CTS_E_INVALID = -1,   /* bad argument (null, misaligned, out of range) */
+    CTS_E_HIP = -2,       /* a HIP runtime call or kernel launch failed */
+    CTS_E_NOMEM = -3,     /* allocation failed */
+    CTS_E_NO_DEVICE = -4  /* no HIP device / device index out of range */
+} cts_status;
+
+/* One received (verify) or outgoing (fill) buffer inside a device arena.
+ * Mirrors the fields of ctsTask (ctsIOTask.hpp:37-60) that the hot path
+ * reads: m_buffer (as an arena offset), the transferred length, the
+ * m_bufferOffset where payload starts, and m_expectedPatternOffset. */
+typedef struct cts_buf_desc {
+    uint64_t byte_offset;             /* buffer start = arena + byte_offset */
+    uint32_t length;                  /* bytes transferred incl. skip_head (currentTransfer) */
+    uint32_t expected_pattern_offset; /* ctsTask::m_expectedPatternOffset, < 65536 */
+    uint32_t conn_index;              /* connection slot (DataError accounting) */
+    uint32_t skip_head;               /* ctsTask::m_bufferOffset: 0 TCP, 26 MediaStream payload */
+} cts_buf_desc;                       /* 24 bytes */
+
+#define CTS_RESULT_FLAG_BAD_DESC 0x1u /* descriptor out of arena / offset >= 65536 / length < skip_head */
+
+/* Per-buffer verify record. first_mismatch is RtlCompareMemory's return
+ * value (matching-prefix length) over the verified region
+ * [byte_offset+skip_head, byte_offset+length) — ctsIOPattern.cpp:757-760;
+ * pass iff first_mismatch == length - skip_head (ctsIOPattern.cpp:774).
+ * expected/actual are the two bytes ctsIOPattern.cpp:761-772 prints. */
+typedef struct cts_verify_result {
+    uint32_t first_mismatch;
+    uint32_t mismatch_bytes;  /* extension: # of differing bytes (not in the reference) */
+    uint8_t expected;         /* pattern byte at first_mismatch (0 when clean) */
+    uint8_t actual;           /* received byte at first_mismatch (0 when clean) */
+    uint8_t pass;             /* 1 = buffer matched the bit pattern */
+    uint8_t flags;            /* CTS_RESULT_FLAG_* */
+} cts_verify_result;          /* 12 bytes */
+
+/* Aggregate counters (the aggregation target is ctsStatistics.hpp:87-373).
+ * bytes_checked  : sum of verified bytes (length - skip_head)
+ * bytes_ok       : sum of verified bytes of buffers that passed
+ * buffers_checked: # buffers verified (bad descriptors excluded)
+ * buffers_failed : # buffers that did not match
+ * mismatched_bytes: extension, sum of cts_verify_result.mismatch_bytes */
+typedef struct cts_counters {
+    uint64_t bytes_checked;
+    uint64_t bytes_ok;
+    uint64_t buffers_checked;
+    uint64_t buffers_failed;
+    uint64_t mismatched_bytes;
+} cts_counters;
+
+typedef struct cts_engine cts_engine;
+
+/* ---- library / pattern helpers ------------------------------------------ */
+const char* cts_version(void);
+const char* cts_status_string(int status);
+/* P(stream_offset mod 65536): the byte g_senderSharedBuffer holds at that
+ * offset (ctsIOPattern.cpp:55-80). Pure arithmetic, no device needed. */
+uint8_t cts_pattern_byte(uint64_t stream_offset);
+/* g_maximumBufferSize = c_bufferPatternSize + GetMaxBufferSize() (ctsIOPattern.cpp:60) */
+uint64_t cts_sender_buffer_size(uint32_t max_buffer_size);
+
+/* ---- engine lifetime ------------------------------------------------------ */
+int cts_engine_create(int device, cts_engine** out);
+int cts_engine_destroy(cts_engine* engine);
+int cts_engine_device(const cts_engine* engine);
+
+/* ---- fill (write-bound) --------------------------------------------------- */
+/* Materialise g_senderSharedBuffer on the device: dst[i] = P(i) for
+ * i < 65536 + max_buffer_size (InitOnceIoPatternCallback, ctsIOPattern.cpp:52-90).
+ * dst must be 16-byte aligned. */
+int cts_sender_buffer_fill(cts_engine* engine, void* dev_dst, uint32_t max_buffer_size, void* stream);
+
+/* For every descriptor d: arena[d.byte_offset + d.skip_head + b] =
+ * P(d.expected_pattern_offset + b) for b < d.length - d.skip_head, i.e. what a
+ * sender at stream offset d.expected_pattern_offset puts on the wire
+ * (ctsTask{m_buffer = S, m_bufferOffset = m_sendPatternOffset}, ctsIOPattern.cpp:676-697).
+ * Header bytes [0, skip_head) are left untouched. max_length_hint selects the
+ * launch geometry (0 = unknown). dev_arena must be 16-byte aligned. */
+int cts_fill(cts_engine* engine, void* dev_arena, uint64_t arena_bytes,
+             const cts_buf_desc* dev_descs, uint32_t n, uint32_t max_length_hint, void* stream);
+
+/* ---- verify (read-bound, the headline path) -------------------------------- */
+/* Verify n device-resident buffers against the pattern. Any of the three
+ * outputs may be NULL:
+ *   dev_results[i]        : per-buffer record (cts_verify_result)
+ *   dev_counters          : device counter block (cts_counters_device_bytes()),
+ *                           ACCUMULATED into (like ctsStatsTracking::Add)
+ *   dev_conn_first_fail   : n_conns u32 slots; for every failing buffer i of
+ *                           connection c (< n_conns): atomicMin(slot[c], i).
+ *                           Initialise to 0xFFFFFFFF. The DataError count
+ *                           (ctsSocketState.cpp:221-232) is the number of slots
+ *                           != 0xFFFFFFFF when descriptors of one connection are
+ *                           in stream order.
+ * dev_arena must be 16-byte aligned and its allocation must extend to a
+ * multiple of 16 bytes (every hipMalloc allocation does). */
+int cts_verify(cts_engine* engine, const void* dev_arena, uint64_t arena_bytes,
+               const cts_buf_desc* dev_descs, uint32_t n, uint32_t max_length_hint,
+               cts_verify_result* dev_results, void* dev_counters,
+               uint32_t* dev_conn_first_fail, uint32_t n_conns, void* stream);
+
+/* ---- counters --------------------------------------------------------------- */
+size_t cts_counters_device_bytes(void);
+int cts_counters_reset(cts_engine* engine, void* dev_counters, void* stream);
+/* Folds the shards into *out. Synchronises `stream`. */
+int cts_counters_read(cts_engine* engine, const void* dev_counters, cts_counters* out, void* stream);
+
+/* ---- host-buffer drop-in for ctsIoPattern::VerifyBuffer ---------------------- */
+/* Verifies `len` bytes at host_buf + skip_head against the pattern starting at
+ * expected_offset: stages the bytes into pinned memory, runs the verify kernel
+ * on the engine's internal stream and waits. Returns the record in *out
+ * (RtlCompareMemory semantics, ctsIOPattern.cpp:753-774). Thread-safe. */
+int cts_verify_host(cts_engine* engine, const void* host_buf, uint32_t len,
+                    uint32_t expected_offset, cts_verify_result* out);
+
+/* Pinned host arenas (the recv-buffer container of a GPU-verified
+ * ctsIoPattern, ctsIOPattern.cpp:156-175): page-locked and mapped into the
+ * device address space, so cts_verify can read them in place over PCIe
+ * (zero-copy) or hipMemcpyAsync can DMA them. *dev_view receives the device
+ * address to pass as dev_arena. */
+int cts_host_alloc(cts_engine* engine, uint64_t bytes, void** host_ptr, void** dev_view);
+int cts_host_free(cts_engine* engine, void* host_ptr);
+/* Device address of pinned+mapped host memory (hipHostGetDevicePointer);
+ * CTS_E_INVALID if host_ptr is not device-accessible pinned memory. */
+int cts_host_device_pointer(void* host_ptr, void** dev_view);
+
+/* Batched host path (PCIe-inclusive): verifies n host buffers
+ * (bufs[i] + skip_heads[i], lens[i] - skip_heads[i] bytes, expected offsets
+ * expected[i]) with pinned double-buffered staging and hipMemcpyAsync
+ * overlapped with the kernel. skip_heads may be NULL (all 0). results[n] host
+ * memory; counters (host) accumulated into if non-NULL. */
+int cts_verify_host_batch(cts_engine* engine, const void* const* bufs, const uint32_t* lens,
+                          const uint32_t* expected, const uint32_t* skip_heads, uint32_t n,
+                          cts_verify_result* results, cts_counters* counters);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+#endif /* CTS_ENGINE_H */

@@ -1,0 +1,122 @@
+"""CPU: the C-ABI library loads, exports every symbol include/*.h declares, and
+its struct layouts match the Python mirrors. No device compute is issued."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+INCLUDE = os.path.join(ROOT, "include")
+
+
+def declared_functions():
+    names = []
+    for h in sorted(os.listdir(INCLUDE)):
+        if not h.endswith(".h"):
+            continue
+        src = open(os.path.join(INCLUDE, h)).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        src = re.sub(r"//[^\n]*", "", src)
+        for m in re.finditer(r"^[A-Za-z_][\w\s\*]*?\b(cts_\w+)\s*\(", src, flags=re.M):
+            names.append(m.group(1))
+    return sorted(set(names))
+
+
+def test_header_declares_functions():
+    names = declared_functions()
+    assert "cts_verify" in names and "cts_fill" in names and "cts_engine_create" in names
+    assert len(names) >= 15
+
+
+def test_library_exports_every_declared_symbol():
+    from ctstraffic_amd import _lib
+
+    L = _lib.lib()
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True, check=True)
+    exported = {line.split()[-1] for line in out.stdout.splitlines() if line.strip()}
+    missing = [n for n in declared_functions() if n not in exported]
+    assert not missing, missing
+    for n in declared_functions():
+        assert hasattr(L, n)
+
+
+def test_library_is_gfx950_code_object():
+    from ctstraffic_amd import _lib
+
+    blob = open(_lib.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob
+
+
+def test_struct_layouts_match_c():
+    """Compile a probe against include/cts_engine.h and compare sizeof/offsetof."""
+    probe = r"""
+#include <stdio.h>
+#include <stddef.h>
+#include "cts_engine.h"
+int main(void){
+ printf("%zu %zu %zu %zu %zu %zu\n", sizeof(cts_buf_desc), offsetof(cts_buf_desc,length),
+   offsetof(cts_buf_desc,expected_pattern_offset), offsetof(cts_buf_desc,conn_index), offsetof(cts_buf_desc,skip_head),
+   sizeof(cts_verify_result));
+ printf("%zu %zu %zu %zu %zu\n", offsetof(cts_verify_result,mismatch_bytes), offsetof(cts_verify_result,expected),
+   offsetof(cts_verify_result,actual), offsetof(cts_verify_result,pass), offsetof(cts_verify_result,flags));
+ printf("%zu\n", sizeof(cts_counters));
+ return 0; }
+"""
+    import tempfile
+
+    from ctstraffic_amd.types import DESC_DTYPE, RESULT_DTYPE
+
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "p.c")
+        open(c, "w").write(probe)
+        exe = os.path.join(d, "p")
+        subprocess.run(["gcc", "-std=c11", "-I", INCLUDE, c, "-o", exe], check=True)
+        lines = subprocess.run([exe], capture_output=True, text=True, check=True).stdout.split("\n")
+    a = list(map(int, lines[0].split()))
+    b = list(map(int, lines[1].split()))
+    assert a[0] == DESC_DTYPE.itemsize == oracle.DESC_DTYPE.itemsize == 24
+    assert a[1:5] == [DESC_DTYPE.fields[f][1] for f in ("length", "expected_pattern_offset", "conn_index", "skip_head")]
+    assert a[5] == RESULT_DTYPE.itemsize == 12
+    assert b == [RESULT_DTYPE.fields[f][1] for f in ("mismatch_bytes", "expected", "actual", "pass", "flags")]
+    assert int(lines[2]) == 40
+
+
+def test_pattern_byte_helper_matches_oracle():
+    # cts_pattern_byte is the ABI's pure-arithmetic helper (no device involved)
+    from ctstraffic_amd import pattern_byte
+
+    S = oracle.sender_buffer(65536)
+    for p in list(range(0, 64)) + list(range(65500, 65600)) + [131071, 2**33 + 5]:
+        assert pattern_byte(p) == S[p % 65536]
+    from ctstraffic_amd import sender_buffer_size
+
+    assert sender_buffer_size(65536) == 131072
+
+
+def test_status_strings_and_invalid_args_without_device():
+    from ctstraffic_amd import _lib
+
+    L = _lib.lib()
+    assert L.cts_status_string(0) == b"ok"
+    assert L.cts_status_string(-4) == b"no such HIP device"
+    # null engine -> CTS_E_INVALID, never a crash and never a compute call
+    assert L.cts_verify(None, None, 0, None, 1, 0, None, None, None, 0, None) == _lib.CTS_E_INVALID
+    assert L.cts_fill(None, None, 0, None, 1, 0, None) == _lib.CTS_E_INVALID
+    assert L.cts_engine_destroy(None) == _lib.CTS_E_INVALID
+    assert L.cts_counters_device_bytes() == _lib.COUNTER_SHARDS * 64
+
+
+def test_engine_create_without_device_fails_loudly():
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("a device is present")
+    from ctstraffic_amd import CtsError, Engine
+
+    with pytest.raises(CtsError):
+        Engine(0)
