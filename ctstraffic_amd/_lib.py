@@ -34,6 +34,10 @@ PATTERN_PERIOD = 65536
 UDP_DATA_HEADER_LENGTH = 26
 STATUS_ERROR_DATA_DID_NOT_MATCH_BIT_PATTERN = 2147483644  # MAXINT - 3, ctsIOPattern.h:49
 COUNTER_SHARDS = 64
+ATTR_BLOCKS_PER_CU = 1
+ATTR_NT_LOADS = 2
+ATTR_SMALL_THRESHOLD = 3
+ATTR_VERIFY_VARIANT = 4
 
 
 class CtsError(RuntimeError):
@@ -99,6 +103,8 @@ def _declare(L: ctypes.CDLL) -> None:
         "cts_verify_host_batch": ([P, P, P, P, P, u32, P, ctypes.POINTER(CtsCounters)], i32),
         "cts_host_alloc": ([P, u64, ctypes.POINTER(P), ctypes.POINTER(P)], i32),
         "cts_host_free": ([P, P], i32),
+        "cts_engine_set_attr": ([P, i32, i32], i32),
+        "cts_engine_get_attr": ([P, i32, ctypes.POINTER(i32)], i32),
         "cts_host_device_pointer": ([P, ctypes.POINTER(P)], i32),
     }
     for name, (argtypes, restype) in sigs.items():

@@ -130,6 +130,7 @@ int cts_engine_create(int device, cts_engine** out)
     e->geo.blocks_per_cu = env_int("CTS_BLOCKS_PER_CU", e->geo.blocks_per_cu);
     e->geo.nontemporal = env_int("CTS_NT_LOADS", e->geo.nontemporal);
     e->geo.small_threshold = env_int("CTS_SMALL_THRESHOLD", e->geo.small_threshold);
+    e->geo.verify_variant = env_int("CTS_VERIFY_VARIANT", e->geo.verify_variant);
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
         delete e;
         return CTS_E_HIP;
@@ -167,6 +168,39 @@ int cts_engine_destroy(cts_engine* e)
 }
 
 int cts_engine_device(const cts_engine* e) { return e ? e->device : CTS_E_INVALID; }
+
+int cts_engine_set_attr(cts_engine* e, int attr, int value)
+{
+    if (e == nullptr) return CTS_E_INVALID;
+    switch (attr) {
+    case CTS_ATTR_BLOCKS_PER_CU:
+        if (value < 1 || value > 64) return CTS_E_INVALID;
+        e->geo.blocks_per_cu = value;
+        return CTS_OK;
+    case CTS_ATTR_NT_LOADS: e->geo.nontemporal = value ? 1 : 0; return CTS_OK;
+    case CTS_ATTR_SMALL_THRESHOLD:
+        if (value < 0) return CTS_E_INVALID;
+        e->geo.small_threshold = value;
+        return CTS_OK;
+    case CTS_ATTR_VERIFY_VARIANT:
+        if (value < 0 || value >= cts::kVerifyVariants) return CTS_E_INVALID;
+        e->geo.verify_variant = value;
+        return CTS_OK;
+    default: return CTS_E_INVALID;
+    }
+}
+
+int cts_engine_get_attr(const cts_engine* e, int attr, int* value)
+{
+    if (e == nullptr || value == nullptr) return CTS_E_INVALID;
+    switch (attr) {
+    case CTS_ATTR_BLOCKS_PER_CU: *value = e->geo.blocks_per_cu; return CTS_OK;
+    case CTS_ATTR_NT_LOADS: *value = e->geo.nontemporal; return CTS_OK;
+    case CTS_ATTR_SMALL_THRESHOLD: *value = e->geo.small_threshold; return CTS_OK;
+    case CTS_ATTR_VERIFY_VARIANT: *value = e->geo.verify_variant; return CTS_OK;
+    default: return CTS_E_INVALID;
+    }
+}
 
 int cts_sender_buffer_fill(cts_engine* e, void* dev_dst, uint32_t max_buffer_size, void* stream)
 {

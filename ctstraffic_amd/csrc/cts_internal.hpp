@@ -14,11 +14,14 @@ namespace cts {
 constexpr int kCounterSlots = 8;  // 5 used, padded to one 64-byte line
 enum CounterSlot { kBytesChecked = 0, kBytesOk = 1, kBuffersChecked = 2, kBuffersFailed = 3, kMismatchedBytes = 4 };
 
+constexpr int kVerifyVariants = 4;  // workgroup-per-buffer verify variants (launch_verify)
+
 struct LaunchGeometry {
     int num_cus = 256;        // hipDeviceAttributeMultiprocessorCount
-    int blocks_per_cu = 8;    // grid cap = num_cus * blocks_per_cu (grid-stride beyond)
+    int blocks_per_cu = 16;   // grid cap = num_cus * blocks_per_cu (grid-stride beyond)
     int nontemporal = 1;      // nt loads for the once-read verify stream
     int small_threshold = 8192;  // max_length_hint <= this -> one wave per buffer
+    int verify_variant = 0;      // see launch_verify
 };
 
 hipError_t launch_verify(const uint8_t* arena, uint64_t arena_bytes, const cts_buf_desc* descs, uint32_t n,

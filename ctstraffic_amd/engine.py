@@ -97,6 +97,15 @@ class Engine:
         except Exception:
             pass
 
+    # ---- launch attributes ----------------------------------------------------
+    def set_attr(self, attr: int, value: int) -> None:
+        check("cts_engine_set_attr", lib().cts_engine_set_attr(self._h, attr, value))
+
+    def get_attr(self, attr: int) -> int:
+        v = ctypes.c_int()
+        check("cts_engine_get_attr", lib().cts_engine_get_attr(self._h, attr, ctypes.byref(v)))
+        return v.value
+
     # ---- fill ----------------------------------------------------------------
     def sender_buffer(self, max_buffer_size: int, stream=None):
         """Device copy of g_senderSharedBuffer (InitOnceIoPatternCallback, ctsIOPattern.cpp:52-90)."""

@@ -269,3 +269,33 @@ def test_verify_host_batch(engine):
     er, ec, _ = oracle.verify_batch(arena, descs)
     assert_results_equal(r, er)
     assert c == ec
+
+
+# ---- every launch variant / geometry is bit-identical ------------------------------------------
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("nt", [1, 0])
+def test_launch_variants_parity(engine, variant, nt):
+    from ctstraffic_amd import _lib
+
+    try:
+        engine.set_attr(_lib.ATTR_VERIFY_VARIANT, variant)
+        engine.set_attr(_lib.ATTR_NT_LOADS, nt)
+        for seed, n, max_len, hint, skip in [(21, 200, 3000, 1472, True), (22, 64, 140000, 0, False),
+                                             (23, 300, 1472, 1472, True), (24, 100, 70000, 0, True)]:
+            for bpc in (1, 16):
+                engine.set_attr(_lib.ATTR_BLOCKS_PER_CU, bpc)
+                rng = np.random.default_rng(seed)
+                arena, descs = _random_case(rng, n, max_len, skip=skip)
+                r, ctr, cff = run_verify(engine, arena, descs, hint, n_conns=7)
+                er, ectr, ecff = oracle.verify_batch(arena, descs, n_conns=7)
+                assert_results_equal(r, er, "variant %d nt %d seed %d bpc %d" % (variant, nt, seed, bpc))
+                assert ctr == ectr
+                assert np.array_equal(cff, ecff)
+        w = W.udp_datagrams(n_datagrams=4099, corrupt_rate=7)
+        _check_workload(engine, w, with_oracle=True)
+        w = W.tcp_resident(n_buffers=300, corrupt_rate=5)
+        _check_workload(engine, w, with_oracle=True)
+    finally:
+        engine.set_attr(_lib.ATTR_VERIFY_VARIANT, 0)
+        engine.set_attr(_lib.ATTR_NT_LOADS, 1)
+        engine.set_attr(_lib.ATTR_BLOCKS_PER_CU, 16)

@@ -1,0 +1,76 @@
+#!/usr/bin/env python3
+"""Interleaved A/B of verify launch variants in ONE process (methodology rule 24).
+
+For each round, every (variant, blocks_per_cu, nt) configuration runs `--launches`
+back-to-back verify launches over rotated arenas; the per-launch kernel time comes
+from HIP events on the launch stream. Prints a JSON table (median over rounds).
+"""
+import argparse
+import itertools
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from ctstraffic_amd import Engine, _lib, workload as W  # noqa: E402
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--rounds", type=int, default=3)
+    p.add_argument("--launches", type=int, default=40)
+    p.add_argument("--arenas", type=int, default=8)
+    p.add_argument("--variants", default="0,1,2,3")
+    p.add_argument("--bpc", default="4,8,16")
+    p.add_argument("--nt", default="1,0")
+    p.add_argument("--workload", default="config2")
+    args = p.parse_args()
+    torch.cuda.set_device(0)
+    eng = Engine(0)
+    if args.workload == "config2":
+        w = W.tcp_resident()
+    else:
+        w = W.udp_datagrams(n_datagrams=4 * 1024 * 1024)
+    arenas, descs = [], None
+    for _ in range(args.arenas):
+        a, descs = W.materialize(eng, w)
+        arenas.append(a)
+    _, _, exp, _ = W.expected_results(w)
+    ctr = eng.new_counters()
+    s = torch.cuda.current_stream()
+    combos = list(itertools.product([int(x) for x in args.variants.split(",")],
+                                    [int(x) for x in args.bpc.split(",")],
+                                    [int(x) for x in args.nt.split(",")]))
+    times = {c: [] for c in combos}
+    for r in range(args.rounds):
+        for c in combos:
+            v, bpc, nt = c
+            eng.set_attr(_lib.ATTR_VERIFY_VARIANT, v)
+            eng.set_attr(_lib.ATTR_BLOCKS_PER_CU, bpc)
+            eng.set_attr(_lib.ATTR_NT_LOADS, nt)
+            eng.reset_counters(ctr)
+            evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                   for _ in range(args.launches)]
+            for i in range(args.launches):
+                evs[i][0].record(s)
+                eng.verify(arenas[i % len(arenas)], descs, max_length_hint=w.max_length, counters=ctr)
+                evs[i][1].record(s)
+            torch.cuda.synchronize()
+            got = eng.read_counters(ctr)
+            assert got == {k: v_ * args.launches for k, v_ in exp.items()}, (c, got)
+            times[c].append(float(np.median([a.elapsed_time(b) for a, b in evs[2:]])))
+    nbytes = w.verified_bytes()
+    rows = []
+    for c in combos:
+        t = float(np.median(times[c])) / 1e3
+        rows.append({"variant": c[0], "blocks_per_cu": c[1], "nt": c[2], "us": round(t * 1e6, 2),
+                     "GBps": round(nbytes / t / 1e9, 1), "spread_us": round((max(times[c]) - min(times[c])) * 1e3, 2)})
+    rows.sort(key=lambda x: x["us"])
+    print(json.dumps({"workload": w.name, "bytes": nbytes, "rows": rows}, indent=0))
+
+
+if __name__ == "__main__":
+    main()
