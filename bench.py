@@ -199,7 +199,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved_gbps / HBM_PEAK_GBPS, 4),
                 "traffic": traffic,
-                "kernel": "cts::verify_kernel<256,8,true>",
+                "kernel": "cts::verify_wg_kernel<8,true>",
                 "avg_kernel_us": round(avg_kernel_s * 1e6, 2),
                 "algorithmic_bytes_per_launch": bytes_per_step,
             },

@@ -38,6 +38,7 @@ ATTR_BLOCKS_PER_CU = 1
 ATTR_NT_LOADS = 2
 ATTR_SMALL_THRESHOLD = 3
 ATTR_VERIFY_VARIANT = 4
+ATTR_SMALL_BLOCKS_PER_CU = 5
 
 
 class CtsError(RuntimeError):

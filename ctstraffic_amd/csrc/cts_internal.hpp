@@ -18,7 +18,8 @@ constexpr int kVerifyVariants = 4;  // workgroup-per-buffer verify variants (lau
 
 struct LaunchGeometry {
     int num_cus = 256;        // hipDeviceAttributeMultiprocessorCount
-    int blocks_per_cu = 16;   // grid cap = num_cus * blocks_per_cu (grid-stride beyond)
+    int blocks_per_cu = 8;        // workgroup-per-buffer grid cap = num_cus * this (grid-stride beyond)
+    int small_blocks_per_cu = 64; // wave-per-buffer grid cap
     int nontemporal = 1;      // nt loads for the once-read verify stream
     int small_threshold = 8192;  // max_length_hint <= this -> one wave per buffer
     int verify_variant = 0;      // see launch_verify

@@ -20,9 +20,10 @@
 //
 // Paths:
 //   verify_wg_kernel    one 256-lane workgroup per buffer (64 KiB TCP buffers)
-//   verify_wg_lds_kernel the same, chunks land in LDS by LDS-DMA (global_load_lds)
-//   verify_wave_kernel  one wave per buffer, G buffers in flight per wave
-//                       (1472-byte MediaStream datagrams)
+//   verify_wave_kernel  one wave per buffer (1472-byte MediaStream datagrams)
+// An LDS-DMA (global_load_lds_dwordx4) variant of the workgroup path measured
+// 2.9 TB/s against 5.7 TB/s for register loads on this stream and was dropped
+// ("What did not work").
 #include <hip/hip_runtime.h>
 
 #include "cts_internal.hpp"
@@ -149,51 +150,113 @@ __device__ __forceinline__ u32x4 chunk_diff_masked(const Span& s, uint32_t c)
     return x;
 }
 
-// Edge chunks (first and last, possibly partial) by lanes 0 and 1.
-__device__ __forceinline__ uint32_t scan_edges(const Span& s, uint32_t lane)
+// Buffer resource over the span's chunks [0, nchunks): 16-byte buffer loads
+// address it with ONE lane offset VGPR (+ an SGPR offset per unrolled load)
+// instead of a 64-bit address per load, and the hardware range check returns 0
+// for any byte past num_records instead of faulting.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t span_rsrc(const Span& s)
 {
-    uint32_t acc = 0;
-    if (lane < 2u && s.nchunks > 0u && (lane == 0u || s.nchunks > 1u)) {
-        acc = or4(chunk_diff_masked(s, lane == 0u ? 0u : s.nchunks - 1u));
-    }
-    return acc;
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<u32x4*>(s.p), (short)0, (int)(s.nchunks * 16u), 0x00020000);
 }
 
-// Fast pass over interior chunks [c_begin, c_end) (all 16 bytes valid): OR of
-// (received ^ expected) over this lane's chunks. Straight-line rounds of U
-// loads per lane, all issued before the first compare (sched_barrier stops the
-// scheduler from interleaving them with the compares); no load under a branch
-// (a load under an exec branch makes hipcc drain vmcnt(0) at every join). The
-// tail round clamps its chunk index and discards the excess.
-template <int TEAM, int U, bool NT>
-__device__ __forceinline__ uint32_t scan_interior(const Span& s, uint32_t c_begin, uint32_t c_end, uint32_t lane)
+template <bool NT>
+__device__ __forceinline__ u32x4 buf_load(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff)
 {
+    return __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, NT ? 2 : 0);  // aux 2 = nt
+}
+
+// Expected chunk u of a round: k advances by TEAM*8 per unrolled step (16*TEAM
+// bytes / 2), added to the packed base before the per-half wrap mask. The low
+// half stays below 65536 (k <= 32767 + 8*TEAM*(U-1) + 8), so no carry crosses.
+template <int TEAM, int U>
+__device__ __forceinline__ u32x4 expected_step(uint32_t B, int u, uint32_t sh)
+{
+    static_assert(32767 + 8 * TEAM * (U - 1) + 8 < 65536, "packed k must not carry");
+    // B is made opaque so each word is v_add(literal) + v_and: left visible,
+    // hipcc folds the adds into v_mad_u32_u24 whose 32-bit addends (VOP3 takes
+    // no literal on gfx950) it then parks in ~40 VGPRs, halving occupancy.
+    uint32_t bb = B;
+    asm volatile("" : "+v"(bb));
+    const uint32_t b = bb + (uint32_t)u * (uint32_t)(8 * TEAM) * 0x10001u;
+    const uint32_t w0 = b & 0x7FFF7FFFu;
+    const uint32_t w1 = (b + 0x20002u) & 0x7FFF7FFFu;
+    const uint32_t w2 = (b + 0x40004u) & 0x7FFF7FFFu;
+    const uint32_t w3 = (b + 0x60006u) & 0x7FFF7FFFu;
+    const uint32_t w4 = (b + 0x80008u) & 0x7FFF7FFFu;
+    return u32x4{__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
+                 __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh)};
+}
+
+// packed base (k*0x10001 + 0x10000) of the chunk at index c
+__device__ __forceinline__ uint32_t chunk_base(const Span& s, uint32_t c)
+{
+    const uint32_t k = ((s.q0 + 16u * c) & 0xFFFFu) >> 1;
+    return __umul24(k, 0x10001u) + 0x10000u;
+}
+
+// Fast pass over the interior chunks [1, nchunks-1) (all 16 bytes valid): OR
+// of (received ^ expected) over this lane's chunks. Straight-line rounds of U
+// buffer loads per lane, all issued before the first compare (sched_barrier
+// keeps the scheduler from interleaving them with the compares); no load under
+// a branch (a load under an exec branch makes hipcc drain vmcnt(0) at every
+// join). Full rounds use SGPR offsets; the tail round puts the whole offset in
+// the VGPR so the range check (which covers voffset + imm) zero-fills the
+// excess lanes, which are then masked out.
+template <int TEAM, int U, bool NT>
+__device__ __forceinline__ uint32_t scan_interior(const Span& s, __amdgpu_buffer_rsrc_t r, uint32_t lane)
+{
+    if (s.nchunks < 3u) return 0;
+    const uint32_t c_end = s.nchunks - 1u;  // interior = [1, c_end)
     uint32_t acc = 0;
-    if (c_end <= c_begin) return 0;
-    uint32_t cb = c_begin;
+    uint32_t cb = 1u;
+    const uint32_t voff = lane * 16u;
     for (; cb + (uint32_t)(TEAM * U) <= c_end; cb += (uint32_t)(TEAM * U)) {
         u32x4 d[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) d[u] = load_chunk<NT>(s.p + cb + (uint32_t)(u * TEAM) + lane);
+        for (int u = 0; u < U; ++u) d[u] = buf_load<NT>(r, voff, (cb + (uint32_t)(u * TEAM)) * 16u);
         __builtin_amdgcn_sched_barrier(0);
+        const uint32_t B = chunk_base(s, cb + lane);
 #pragma unroll
-        for (int u = 0; u < U; ++u) acc |= or4(chunk_xor(s, cb + (uint32_t)(u * TEAM) + lane, d[u]));
+        for (int u = 0; u < U; ++u) {
+            acc |= or4(d[u] ^ expected_step<TEAM, U>(B, u, s.sh));
+            // one chunk's expected words live at a time (else hipcc hoists all
+            // U*5 of them ahead of the compares: +40 VGPRs, half the occupancy)
+            __builtin_amdgcn_sched_barrier(0);
+        }
     }
     if (cb < c_end) {
         u32x4 d[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t c = cb + (uint32_t)(u * TEAM) + lane;
-            d[u] = load_chunk<NT>(s.p + (c < c_end ? c : c_end - 1u));
-        }
+        for (int u = 0; u < U; ++u) d[u] = buf_load<NT>(r, (cb + (uint32_t)(u * TEAM) + lane) * 16u, 0u);
         __builtin_amdgcn_sched_barrier(0);
+        const uint32_t B = chunk_base(s, cb + lane);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const uint32_t c = cb + (uint32_t)(u * TEAM) + lane;
-            const uint32_t any = or4(chunk_xor(s, c < c_end ? c : c_end - 1u, d[u]));
-            acc |= (c < c_end) ? any : 0u;
+            const uint32_t any = or4(d[u] ^ expected_step<TEAM, U>(B, u, s.sh));
+            acc |= (cb + (uint32_t)(u * TEAM) + lane < c_end) ? any : 0u;
+            __builtin_amdgcn_sched_barrier(0);
         }
     }
+    return acc;
+}
+
+// Fast pass over a whole span: OR of (received ^ expected) over this lane's
+// share. The two edge chunks (first and last, possibly partial) are loaded
+// FIRST by every lane (lane 1 the last chunk, the others chunk 0: the same
+// lines, no extra traffic), so their latency hides under the interior stream
+// instead of adding a dependent round trip per buffer; their byte-masked
+// compare runs at the end, branch-free, on registers. For an empty span the
+// edge offset is out of the resource's range and reads 0.
+template <int TEAM, int U, bool NT>
+__device__ __forceinline__ uint32_t scan_buffer(const Span& s, uint32_t lane)
+{
+    const __amdgpu_buffer_rsrc_t r = span_rsrc(s);
+    const uint32_t ce = (lane == 1u) ? s.nchunks - 1u : 0u;
+    const u32x4 edge = buf_load<NT>(r, ce * 16u, 0u);
+    uint32_t acc = scan_interior<TEAM, U, NT>(s, r, lane);
+    const bool use = lane < 2u && s.nchunks > 0u && (lane == 0u || s.nchunks > 1u);
+    const u32x4 x = chunk_xor(s, ce, edge) & range_mask(ce == 0u ? s.lo : 0u, ce == s.nchunks - 1u ? s.hi_last : 16u);
+    acc |= use ? or4(x) : 0u;
     return acc;
 }
 
@@ -235,10 +298,6 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v)
     return v;
 }
 
-struct TeamCounters {
-    uint64_t v[5];
-};
-
 __device__ __forceinline__ void write_bad(cts_verify_result* results, uint32_t i)
 {
     if (results != nullptr) {
@@ -255,7 +314,7 @@ __device__ __forceinline__ void write_bad(cts_verify_result* results, uint32_t i
 
 // Record one verified buffer (called by the team leader).
 __device__ __forceinline__ void finish_buffer(const Span& s, const cts_buf_desc& d, uint32_t i, uint32_t first,
-                                              uint32_t count, cts_verify_result* results, TeamCounters& tc,
+                                              uint32_t count, cts_verify_result* results, uint64_t* tc,
                                               uint32_t* conn_first_fail, uint32_t n_conns)
 {
     const bool pass = (first == kNone);
@@ -269,33 +328,37 @@ __device__ __forceinline__ void finish_buffer(const Span& s, const cts_buf_desc&
         r.flags = 0;
         results[i] = r;
     }
-    tc.v[kBytesChecked] += s.len;
-    tc.v[kBuffersChecked] += 1;
+    // the team's running counters live in LDS (tc[5]), not in 10 VGPRs across the stream loop
+    tc[kBytesChecked] += s.len;
+    tc[kBuffersChecked] += 1;
     if (pass) {
-        tc.v[kBytesOk] += s.len;
+        tc[kBytesOk] += s.len;
     } else {
-        tc.v[kBuffersFailed] += 1;
-        tc.v[kMismatchedBytes] += count;
+        tc[kBuffersFailed] += 1;
+        tc[kMismatchedBytes] += count;
         if (conn_first_fail != nullptr && d.conn_index < n_conns) atomicMin(&conn_first_fail[d.conn_index], i);
     }
+}
+
+// Per-team running counters in LDS: ctr[team][5], zeroed at kernel start.
+template <int TEAMS>
+__device__ __forceinline__ void zero_counters(uint64_t (*ctr)[5])
+{
+    if (threadIdx.x < (unsigned)(TEAMS * 5)) ctr[threadIdx.x / 5][threadIdx.x % 5] = 0;
+    __syncthreads();
 }
 
 // Fold the per-team counters of a workgroup and add them to the counter shard
 // of this workgroup (one 64-byte line per shard, CTS_COUNTER_SHARDS shards).
 template <int TEAMS>
-__device__ __forceinline__ void flush_counters(uint64_t* counters, const TeamCounters& tc, uint32_t team, bool leader)
+__device__ __forceinline__ void flush_counters(uint64_t* counters, uint64_t (*ctr)[5])
 {
-    __shared__ uint64_t red_ctr[TEAMS][5];
-    if (counters == nullptr) return;
-    if (leader) {
-#pragma unroll
-        for (int k = 0; k < 5; ++k) red_ctr[team][k] = tc.v[k];
-    }
     __syncthreads();
+    if (counters == nullptr) return;
     if (threadIdx.x < 5) {
         uint64_t sum = 0;
 #pragma unroll
-        for (int t = 0; t < TEAMS; ++t) sum += red_ctr[t][threadIdx.x];
+        for (int t = 0; t < TEAMS; ++t) sum += ctr[t][threadIdx.x];
         if (sum)
             atomicAdd((unsigned long long*)&counters[(blockIdx.x % CTS_COUNTER_SHARDS) * kCounterSlots + threadIdx.x],
                       (unsigned long long)sum);
@@ -303,236 +366,104 @@ __device__ __forceinline__ void flush_counters(uint64_t* counters, const TeamCou
 }
 
 // Workgroup-wide reduction of (first, count) when some lane saw a mismatch.
-__device__ __forceinline__ void block_reduce_mismatch(uint32_t& first, uint32_t& count)
+// red = 2 * (kBlock/64) u32 of LDS scratch.
+__device__ __forceinline__ void block_reduce_mismatch_with(uint32_t& first, uint32_t& count, uint32_t* red)
 {
-    __shared__ uint32_t red_first[kBlock / 64];
-    __shared__ uint32_t red_count[kBlock / 64];
     const uint32_t wave = threadIdx.x / 64;
     first = wave_min(first);
     count = wave_sum(count);
     if ((threadIdx.x & 63) == 0) {
-        red_first[wave] = first;
-        red_count[wave] = count;
+        red[wave] = first;
+        red[kBlock / 64 + wave] = count;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
 #pragma unroll
         for (int w = 1; w < kBlock / 64; ++w) {
-            first = red_first[w] < first ? red_first[w] : first;
-            count += red_count[w];
+            first = red[w] < first ? red[w] : first;
+            count += red[kBlock / 64 + w];
         }
     }
-    __syncthreads();  // red_* reused by the next buffer
+    __syncthreads();  // red reused by the next buffer
+}
+
+__device__ __forceinline__ void block_reduce_mismatch(uint32_t& first, uint32_t& count)
+{
+    __shared__ uint32_t red[2 * (kBlock / 64)];
+    block_reduce_mismatch_with(first, count, red);
 }
 
 // ---------------------------------------------------------------------------------------------
-// One 256-lane workgroup per buffer (grid-strides over buffers).
+// One 256-lane workgroup per buffer (grid-strides over buffers). The next
+// buffer's descriptor is fetched while the current one streams.
 template <int U, bool NT>
-__global__ void __launch_bounds__(kBlock) verify_wg_kernel(const uint8_t* __restrict__ arena, uint64_t arena_bytes,
-                                                           const cts_buf_desc* __restrict__ descs, uint32_t n,
-                                                           cts_verify_result* __restrict__ results,
-                                                           uint64_t* __restrict__ counters,
-                                                           uint32_t* __restrict__ conn_first_fail, uint32_t n_conns)
+__global__ void __launch_bounds__(kBlock, (U <= 8 ? 8 : 4))
+    verify_wg_kernel(const uint8_t* __restrict__ arena, uint64_t arena_bytes, const cts_buf_desc* __restrict__ descs,
+                     uint32_t n, cts_verify_result* __restrict__ results, uint64_t* __restrict__ counters,
+                     uint32_t* __restrict__ conn_first_fail, uint32_t n_conns)
 {
+    __shared__ uint64_t ctr[1][5];
     const uint32_t lane = threadIdx.x;
-    TeamCounters tc = {{0, 0, 0, 0, 0}};
-    for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
-        const cts_buf_desc d = descs[i];
+    zero_counters<1>(ctr);
+    uint32_t i = blockIdx.x;
+    cts_buf_desc dn;
+    if (i < n) dn = descs[i];
+    for (; i < n; i += gridDim.x) {
+        const cts_buf_desc d = dn;
+        if (i + gridDim.x < n) dn = descs[i + gridDim.x];
         if (desc_bad(d, arena_bytes)) {
             if (lane == 0) write_bad(results, i);
             continue;
         }
         const Span s = make_span(arena, d);
-        uint32_t acc = s.nchunks >= 3u ? scan_interior<kBlock, U, NT>(s, 1u, s.nchunks - 1u, lane) : 0u;
-        acc |= scan_edges(s, lane);
+        const uint32_t acc = scan_buffer<kBlock, U, NT>(s, lane);
         uint32_t first = kNone, count = 0;
         if (__syncthreads_or(acc != 0u)) {  // rare: exact re-scan + reduction
             scan_exact<kBlock>(s, lane, first, count);
             block_reduce_mismatch(first, count);
         }
-        if (lane == 0) finish_buffer(s, d, i, first, count, results, tc, conn_first_fail, n_conns);
+        if (lane == 0) finish_buffer(s, d, i, first, count, results, ctr[0], conn_first_fail, n_conns);
     }
-    flush_counters<1>(counters, tc, 0, threadIdx.x == 0);
+    flush_counters<1>(counters, ctr);
 }
 
 // ---------------------------------------------------------------------------------------------
-// LDS-DMA variant: each wave streams its chunks with global_load_lds_dwordx4
-// (1 KiB per wave-instruction lands in the wave's private LDS slot, lane i at
-// +16 i) and reads them back with ds_read_b128 behind a counted vmcnt. The
-// in-flight bytes live in LDS, not VGPRs. No cross-wave LDS sharing: no barrier.
-template <int N>
-__device__ __forceinline__ void wait_vmcnt()
-{
-    static_assert(N >= 0 && N < 64, "vmcnt range");
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
+// One wave per buffer (datagram-sized buffers; also any buffer when there are
+// enough of them to fill the chip one wave each). Waves grid-stride over the
+// descriptors, fetching the next descriptor while the current buffer streams.
 template <int U, bool NT>
-__device__ __forceinline__ uint32_t scan_interior_lds(const Span& s, uint32_t c_begin, uint32_t c_end, uint32_t lane,
-                                                      u32x4 (*slot)[64])
+__global__ void __launch_bounds__(kBlock)
+    verify_wave_kernel(const uint8_t* __restrict__ arena, uint64_t arena_bytes, const cts_buf_desc* __restrict__ descs,
+                       uint32_t n, cts_verify_result* __restrict__ results, uint64_t* __restrict__ counters,
+                       uint32_t* __restrict__ conn_first_fail, uint32_t n_conns)
 {
-    typedef __attribute__((address_space(3))) void lds_void;
-    typedef __attribute__((address_space(1))) const void gbl_void;
-    uint32_t acc = 0;
-    if (c_end <= c_begin) return 0;
-    for (uint32_t cb = c_begin; cb < c_end; cb += (uint32_t)(kBlock * U)) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t c = cb + (uint32_t)(u * kBlock) + lane;
-            const u32x4* src = s.p + (c < c_end ? c : c_end - 1u);
-            __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)&slot[u][0], 16, 0, NT ? 2 : 0);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            // wait until the u-th piece has landed (the U-1-u younger ones may still fly)
-            if constexpr (U == 8) {
-                switch (u) {
-                case 0: wait_vmcnt<7>(); break;
-                case 1: wait_vmcnt<6>(); break;
-                case 2: wait_vmcnt<5>(); break;
-                case 3: wait_vmcnt<4>(); break;
-                case 4: wait_vmcnt<3>(); break;
-                case 5: wait_vmcnt<2>(); break;
-                case 6: wait_vmcnt<1>(); break;
-                default: wait_vmcnt<0>(); break;
-                }
-            } else {
-                wait_vmcnt<0>();
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            const uint32_t c = cb + (uint32_t)(u * kBlock) + lane;
-            const u32x4 data = slot[u][lane];
-            const uint32_t any = or4(chunk_xor(s, c < c_end ? c : c_end - 1u, data));
-            acc |= (c < c_end) ? any : 0u;
-        }
-        // every lane has read its slot entries before the next round overwrites them
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    return acc;
-}
-
-template <int U, bool NT>
-__global__ void __launch_bounds__(kBlock) verify_wg_lds_kernel(const uint8_t* __restrict__ arena,
-                                                               uint64_t arena_bytes,
-                                                               const cts_buf_desc* __restrict__ descs, uint32_t n,
-                                                               cts_verify_result* __restrict__ results,
-                                                               uint64_t* __restrict__ counters,
-                                                               uint32_t* __restrict__ conn_first_fail, uint32_t n_conns)
-{
-    __shared__ __attribute__((aligned(16))) u32x4 ring[kBlock / 64][U][64];
-    const uint32_t lane = threadIdx.x;
-    const uint32_t wave = threadIdx.x / 64;
-    TeamCounters tc = {{0, 0, 0, 0, 0}};
-    for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
-        const cts_buf_desc d = descs[i];
+    constexpr int WAVES = kBlock / 64;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t nw = gridDim.x * WAVES;
+    __shared__ uint64_t ctr[WAVES][5];
+    zero_counters<WAVES>(ctr);
+    uint32_t i = blockIdx.x * WAVES + wave;
+    cts_buf_desc dn;
+    if (i < n) dn = descs[i];
+    for (; i < n; i += nw) {
+        const cts_buf_desc d = dn;
+        if (i + nw < n) dn = descs[i + nw];
         if (desc_bad(d, arena_bytes)) {
             if (lane == 0) write_bad(results, i);
             continue;
         }
         const Span s = make_span(arena, d);
-        uint32_t acc = s.nchunks >= 3u ? scan_interior_lds<U, NT>(s, 1u, s.nchunks - 1u, lane, ring[wave]) : 0u;
-        acc |= scan_edges(s, lane);
+        const uint32_t acc = scan_buffer<64, U, NT>(s, lane);
         uint32_t first = kNone, count = 0;
-        if (__syncthreads_or(acc != 0u)) {
-            scan_exact<kBlock>(s, lane, first, count);
-            block_reduce_mismatch(first, count);
+        if (__any(acc != 0u)) {
+            scan_exact<64>(s, lane, first, count);
+            first = wave_min(first);
+            count = wave_sum(count);
         }
-        if (lane == 0) finish_buffer(s, d, i, first, count, results, tc, conn_first_fail, n_conns);
+        if (lane == 0) finish_buffer(s, d, i, first, count, results, ctr[wave], conn_first_fail, n_conns);
     }
-    flush_counters<1>(counters, tc, 0, threadIdx.x == 0);
-}
-
-// ---------------------------------------------------------------------------------------------
-// One wave per buffer, G buffers in flight per wave (datagram-sized buffers).
-// A group of G descriptors whose interiors fit U chunks per lane takes the
-// grouped fast path (G*U loads per lane issued together); any other group is
-// processed buffer by buffer.
-template <int G, int U, bool NT>
-__global__ void __launch_bounds__(kBlock) verify_wave_kernel(const uint8_t* __restrict__ arena, uint64_t arena_bytes,
-                                                             const cts_buf_desc* __restrict__ descs, uint32_t n,
-                                                             cts_verify_result* __restrict__ results,
-                                                             uint64_t* __restrict__ counters,
-                                                             uint32_t* __restrict__ conn_first_fail, uint32_t n_conns)
-{
-    constexpr int WAVES = kBlock / 64;
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t gw = blockIdx.x * WAVES + wave;
-    const uint32_t nw = gridDim.x * WAVES;
-    TeamCounters tc = {{0, 0, 0, 0, 0}};
-
-    for (uint32_t base = gw * G; base < n; base += nw * G) {
-        cts_buf_desc d[G];
-        Span s[G];
-        bool ok[G];
-        bool simple = true;
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-            const uint32_t i = base + (uint32_t)g;
-            ok[g] = false;
-            s[g].nchunks = 0;
-            if (i < n) {
-                d[g] = descs[i];
-                ok[g] = !desc_bad(d[g], arena_bytes);
-                if (ok[g]) s[g] = make_span(arena, d[g]);
-            }
-            simple = simple && ok[g] && s[g].nchunks >= 3u && s[g].nchunks - 2u <= (uint32_t)(64 * U);
-        }
-        uint32_t acc[G];
-        if (simple) {
-            u32x4 x[G][U];
-#pragma unroll
-            for (int g = 0; g < G; ++g) {
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const uint32_t c = 1u + (uint32_t)(u * 64) + lane;
-                    const uint32_t cl = s[g].nchunks - 2u;  // last interior chunk
-                    x[g][u] = load_chunk<NT>(s[g].p + (c < cl ? c : cl));
-                }
-            }
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int g = 0; g < G; ++g) {
-                acc[g] = 0;
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const uint32_t c = 1u + (uint32_t)(u * 64) + lane;
-                    const uint32_t cl = s[g].nchunks - 2u;
-                    const uint32_t any = or4(chunk_xor(s[g], c < cl ? c : cl, x[g][u]));
-                    acc[g] |= (c <= cl) ? any : 0u;
-                }
-                acc[g] |= scan_edges(s[g], lane);
-            }
-        } else {
-#pragma unroll
-            for (int g = 0; g < G; ++g) {
-                acc[g] = 0;
-                if (ok[g]) {
-                    if (s[g].nchunks >= 3u) acc[g] = scan_interior<64, U, NT>(s[g], 1u, s[g].nchunks - 1u, lane);
-                    acc[g] |= scan_edges(s[g], lane);
-                }
-            }
-        }
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-            const uint32_t i = base + (uint32_t)g;
-            if (i >= n) break;
-            if (!ok[g]) {
-                if (lane == 0) write_bad(results, i);
-                continue;
-            }
-            uint32_t first = kNone, count = 0;
-            if (__any(acc[g] != 0u)) {
-                scan_exact<64>(s[g], lane, first, count);
-                first = wave_min(first);
-                count = wave_sum(count);
-            }
-            if (lane == 0) finish_buffer(s[g], d[g], i, first, count, results, tc, conn_first_fail, n_conns);
-        }
-    }
-    flush_counters<WAVES>(counters, tc, wave, lane == 0);
+    flush_counters<WAVES>(counters, ctr);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -593,7 +524,8 @@ __global__ void __launch_bounds__(kBlock) fill_span_kernel(uint8_t* __restrict__
 static inline uint32_t grid_for(uint32_t n, int teams_per_block, const LaunchGeometry& geo)
 {
     const uint64_t want = ((uint64_t)n + teams_per_block - 1) / teams_per_block;
-    const uint64_t cap = (uint64_t)geo.num_cus * (uint64_t)(geo.blocks_per_cu > 0 ? geo.blocks_per_cu : 16);
+    const int bpc = teams_per_block > 1 ? geo.small_blocks_per_cu : geo.blocks_per_cu;
+    const uint64_t cap = (uint64_t)geo.num_cus * (uint64_t)(bpc > 0 ? bpc : 8);
     const uint64_t g = want < cap ? want : cap;
     return (uint32_t)(g == 0 ? 1 : g);
 }
@@ -606,30 +538,20 @@ static void launch_verify_nt(const uint8_t* arena, uint64_t arena_bytes, const c
                              uint32_t n_conns, hipStream_t stream, const LaunchGeometry& geo)
 {
     if (small) {
-        // variant (small path): 0 = G4 U2, 1 = G2 U2, 2 = G8 U2, 3 = G1 U2
-        constexpr int U = 2;
-        int G = 4;
+        // variant (small path): 0 = U2, 1 = U1, 2 = U4 (chunks per lane per round)
+        const uint32_t grid = grid_for(n, kBlock / 64, geo);
         switch (geo.verify_variant) {
-        case 1: G = 2; break;
-        case 2: G = 8; break;
-        case 3: G = 1; break;
-        default: G = 4; break;
-        }
-        const uint32_t grid = grid_for((n + G - 1) / G, kBlock / 64, geo);
-        switch (G) {
-        case 1: verify_wave_kernel<1, U, NT><<<grid, kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
-        case 2: verify_wave_kernel<2, U, NT><<<grid, kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
-        case 8: verify_wave_kernel<8, U, NT><<<grid, kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
-        default: verify_wave_kernel<4, U, NT><<<grid, kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
+        case 1: verify_wave_kernel<1, NT><<<grid, kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
+        case 2: verify_wave_kernel<4, NT><<<grid, kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
+        default: verify_wave_kernel<2, NT><<<grid, kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         }
     } else {
-        // variant (workgroup path): 0 = U8, 1 = U16, 2 = U4, 3 = LDS-DMA U8
-        const uint32_t grid = grid_for(n, 1, geo);
+        // variant (large path): 0 = workgroup/buffer U8, 1 = U4, 2 = U16, 3 = wave/buffer U8
         switch (geo.verify_variant) {
-        case 1: verify_wg_kernel<16, NT><<<grid, kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
-        case 2: verify_wg_kernel<4, NT><<<grid, kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
-        case 3: verify_wg_lds_kernel<8, NT><<<grid, kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
-        default: verify_wg_kernel<8, NT><<<grid, kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
+        case 1: verify_wg_kernel<4, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
+        case 2: verify_wg_kernel<16, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
+        case 3: verify_wave_kernel<8, NT><<<grid_for(n, kBlock / 64, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
+        default: verify_wg_kernel<8, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         }
     }
 }

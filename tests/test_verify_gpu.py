@@ -284,6 +284,7 @@ def test_launch_variants_parity(engine, variant, nt):
                                              (23, 300, 1472, 1472, True), (24, 100, 70000, 0, True)]:
             for bpc in (1, 16):
                 engine.set_attr(_lib.ATTR_BLOCKS_PER_CU, bpc)
+                engine.set_attr(_lib.ATTR_SMALL_BLOCKS_PER_CU, bpc)
                 rng = np.random.default_rng(seed)
                 arena, descs = _random_case(rng, n, max_len, skip=skip)
                 r, ctr, cff = run_verify(engine, arena, descs, hint, n_conns=7)
@@ -298,4 +299,5 @@ def test_launch_variants_parity(engine, variant, nt):
     finally:
         engine.set_attr(_lib.ATTR_VERIFY_VARIANT, 0)
         engine.set_attr(_lib.ATTR_NT_LOADS, 1)
-        engine.set_attr(_lib.ATTR_BLOCKS_PER_CU, 16)
+        engine.set_attr(_lib.ATTR_BLOCKS_PER_CU, 8)
+        engine.set_attr(_lib.ATTR_SMALL_BLOCKS_PER_CU, 64)

@@ -1,0 +1,132 @@
+// hbm_read_ceiling.hip — known-good reference for the verify roofline: how fast
+// can a plain streaming READ kernel pull bytes from HBM on this MI355X?
+// (methodology rule 10: a ceiling claim needs a reference measured on the same
+// hardware). OR-reduces a large buffer with 16-byte loads, sweeping unroll,
+// grid size and cache policy; prints one JSON line per configuration.
+//
+// build: hipcc --offload-arch=gfx950 -O3 tools/hbm_read_ceiling.hip -o tools/hbm_read_ceiling
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+#define CHECK(x)                                                                              \
+    do {                                                                                      \
+        hipError_t e_ = (x);                                                                  \
+        if (e_ != hipSuccess) {                                                               \
+            fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+            exit(1);                                                                          \
+        }                                                                                     \
+    } while (0)
+
+// grid-stride over chunks; each lane issues U loads per round (straight line)
+template <int U, bool NT>
+__global__ void __launch_bounds__(256) read_or(const u32x4* __restrict__ p, uint64_t nchunks, uint32_t* out)
+{
+    uint32_t acc = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * 256u * U;
+    uint64_t c = (uint64_t)blockIdx.x * 256u * U + threadIdx.x;
+    for (; c + 256u * (U - 1) < nchunks; c += stride) {
+        u32x4 d[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) d[u] = NT ? __builtin_nontemporal_load(p + c + u * 256u) : p[c + u * 256u];
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc |= d[u][0] ^ d[u][1] ^ d[u][2] ^ d[u][3];
+    }
+    if (acc == 0x12345678u) out[0] = acc;  // keep the loads alive
+}
+
+// contiguous per-block slabs: block b reads chunks [b*per, (b+1)*per) (like one buffer per block)
+template <int U, bool NT>
+__global__ void __launch_bounds__(256) read_or_slab(const u32x4* __restrict__ p, uint32_t per_block, uint32_t* out)
+{
+    uint32_t acc = 0;
+    const u32x4* q = p + (uint64_t)blockIdx.x * per_block;
+    for (uint32_t c = threadIdx.x; c + 256u * (U - 1) < per_block; c += 256u * U) {
+        u32x4 d[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) d[u] = NT ? __builtin_nontemporal_load(q + c + u * 256u) : q[c + u * 256u];
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc |= d[u][0] ^ d[u][1] ^ d[u][2] ^ d[u][3];
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
+template <typename F>
+static float time_ms(F launch, int reps, hipStream_t s)
+{
+    hipEvent_t a, b;
+    CHECK(hipEventCreate(&a));
+    CHECK(hipEventCreate(&b));
+    launch(0);
+    CHECK(hipStreamSynchronize(s));
+    CHECK(hipEventRecord(a, s));
+    for (int i = 0; i < reps; ++i) launch(i);
+    CHECK(hipEventRecord(b, s));
+    CHECK(hipEventSynchronize(b));
+    float ms = 0;
+    CHECK(hipEventElapsedTime(&ms, a, b));
+    CHECK(hipEventDestroy(a));
+    CHECK(hipEventDestroy(b));
+    return ms / reps;
+}
+
+int main()
+{
+    int cus = 0;
+    CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+    const size_t arena = 256ull << 20;  // 256 MiB, like one config-2 batch
+    const int R = 8;                     // rotate: 2 GiB total, defeats the 256 MiB MALL
+    std::vector<u32x4*> bufs(R);
+    for (int r = 0; r < R; ++r) {
+        CHECK(hipMalloc(&bufs[r], arena));
+        CHECK(hipMemset(bufs[r], r + 1, arena));
+    }
+    uint32_t* out;
+    CHECK(hipMalloc(&out, 64));
+    hipStream_t s;
+    CHECK(hipStreamCreate(&s));
+    const uint64_t nchunks = arena / 16;
+    const int reps = 64;
+
+#define RUN_GS(U, NT, BPC)                                                                                           \
+    do {                                                                                                             \
+        const uint32_t grid = (uint32_t)cus * (BPC);                                                                 \
+        float ms = time_ms([&](int i) { read_or<U, NT><<<grid, 256, 0, s>>>(bufs[i % R], nchunks, out); }, reps, s); \
+        printf("{\"kind\":\"gridstride\",\"U\":%d,\"nt\":%d,\"blocks_per_cu\":%d,\"us\":%.2f,\"GBps\":%.1f}\n", U,     \
+               (int)NT, BPC, ms * 1e3, arena / (ms * 1e-3) / 1e9);                                                    \
+    } while (0)
+#define RUN_SLAB(U, NT, SLAB)                                                                                       \
+    do {                                                                                                            \
+        const uint32_t per = (SLAB) / 16;                                                                           \
+        const uint32_t grid = (uint32_t)(arena / (SLAB));                                                          \
+        float ms = time_ms([&](int i) { read_or_slab<U, NT><<<grid, 256, 0, s>>>(bufs[i % R], per, out); }, reps, s); \
+        printf("{\"kind\":\"slab\",\"U\":%d,\"nt\":%d,\"slab\":%d,\"us\":%.2f,\"GBps\":%.1f}\n", U, (int)NT, SLAB,    \
+               ms * 1e3, arena / (ms * 1e-3) / 1e9);                                                                 \
+    } while (0)
+
+    for (int pass = 0; pass < 2; ++pass) {
+        RUN_GS(4, true, 4);
+        RUN_GS(4, true, 8);
+        RUN_GS(4, true, 16);
+        RUN_GS(8, true, 4);
+        RUN_GS(8, true, 8);
+        RUN_GS(2, true, 8);
+        RUN_GS(2, true, 16);
+        RUN_GS(1, true, 32);
+        RUN_GS(4, false, 8);
+        RUN_GS(8, false, 4);
+        RUN_SLAB(8, true, 65536);
+        RUN_SLAB(4, true, 65536);
+        RUN_SLAB(16, true, 65536);
+        RUN_SLAB(4, true, 32768);
+        RUN_SLAB(8, true, 131072);
+        RUN_SLAB(8, false, 65536);
+    }
+    return 0;
+}

@@ -27,11 +27,12 @@ def main():
     p.add_argument("--bpc", default="4,8,16")
     p.add_argument("--nt", default="1,0")
     p.add_argument("--workload", default="config2")
+    p.add_argument("--buffers", type=int, default=4096)
     args = p.parse_args()
     torch.cuda.set_device(0)
     eng = Engine(0)
     if args.workload == "config2":
-        w = W.tcp_resident()
+        w = W.tcp_resident(n_buffers=args.buffers)
     else:
         w = W.udp_datagrams(n_datagrams=4 * 1024 * 1024)
     arenas, descs = [], None
@@ -50,6 +51,7 @@ def main():
             v, bpc, nt = c
             eng.set_attr(_lib.ATTR_VERIFY_VARIANT, v)
             eng.set_attr(_lib.ATTR_BLOCKS_PER_CU, bpc)
+            eng.set_attr(_lib.ATTR_SMALL_BLOCKS_PER_CU, bpc)
             eng.set_attr(_lib.ATTR_NT_LOADS, nt)
             eng.reset_counters(ctr)
             evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
