@@ -16,8 +16,8 @@ ctstraffic_amd/build/%.o: $(CSRC)/% $(HDRS)
 	@mkdir -p ctstraffic_amd/build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(ENGINE_SO): $(OBJS)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJS) -Wl,-soname,libcts_engine.so
+$(ENGINE_SO): $(OBJS) $(CSRC)/exports.map
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJS) -Wl,-soname,libcts_engine.so -Wl,--version-script=$(CSRC)/exports.map
 
 oracle:
 	$(MAKE) -s -C oracle

@@ -1,0 +1,129 @@
+"""ctypes declarations of the ctsIoPattern mirror's C ABI (include/cts_pattern.h)."""
+from __future__ import annotations
+
+import ctypes
+
+from ._lib import CtsVerifyResult
+
+TASK_NONE, TASK_SEND, TASK_RECV, TASK_GRACEFUL_SHUTDOWN, TASK_HARD_SHUTDOWN, TASK_ABORT, TASK_FATAL_ABORT = range(7)
+(BUFFER_NULL, BUFFER_TCP_CONNECTION_ID, BUFFER_UDP_CONNECTION_ID, BUFFER_COMPLETION_MESSAGE, BUFFER_STATIC,
+ BUFFER_DYNAMIC) = range(6)
+IO_CONTINUE, IO_COMPLETED, IO_FAILED = 0, 1, 2
+PATTERN_PUSH, PATTERN_PULL, PATTERN_PUSHPULL, PATTERN_DUPLEX = 1, 2, 3, 4
+PROTOCOL_TCP, PROTOCOL_UDP = 1, 2
+SHUTDOWN_GRACEFUL, SHUTDOWN_HARD = 1, 2
+VERIFY_SYNC, VERIFY_DEFERRED = 0, 1
+
+STATUS_IO_RUNNING = 2147483647
+STATUS_ERROR_NOT_ALL_DATA_TRANSFERRED = 2147483646
+STATUS_ERROR_TOO_MUCH_DATA_TRANSFERRED = 2147483645
+STATUS_ERROR_DATA_DID_NOT_MATCH_BIT_PATTERN = 2147483644
+PATTERN_E_FAIL_FAST = 2147483640
+CONNECTION_ID_LENGTH = 37
+COMPLETION_MESSAGE_SIZE = 4
+
+
+class CtsTask(ctypes.Structure):
+    """ctsTask (ctsIOTask.hpp:37-60)."""
+
+    _fields_ = [
+        ("time_offset_ms", ctypes.c_int64),
+        ("rio_buffer_id", ctypes.c_uint64),
+        ("buffer", ctypes.c_void_p),
+        ("buffer_length", ctypes.c_uint32),
+        ("buffer_offset", ctypes.c_uint32),
+        ("expected_pattern_offset", ctypes.c_uint32),
+        ("io_action", ctypes.c_uint8),
+        ("buffer_type", ctypes.c_uint8),
+        ("track_io", ctypes.c_uint8),
+        ("reserved", ctypes.c_uint8),
+    ]
+
+
+class CtsPatternConfig(ctypes.Structure):
+    _fields_ = [
+        ("io_pattern", ctypes.c_uint32),
+        ("protocol", ctypes.c_uint32),
+        ("listening", ctypes.c_uint32),
+        ("verify_buffers", ctypes.c_uint32),
+        ("use_shared_buffer", ctypes.c_uint32),
+        ("pre_post_recvs", ctypes.c_uint32),
+        ("pre_post_sends", ctypes.c_uint32),
+        ("buffer_size_low", ctypes.c_uint32),
+        ("buffer_size_high", ctypes.c_uint32),
+        ("push_bytes", ctypes.c_uint32),
+        ("pull_bytes", ctypes.c_uint32),
+        ("tcp_shutdown", ctypes.c_uint32),
+        ("transfer_size", ctypes.c_uint64),
+        ("random_seed", ctypes.c_uint64),
+        ("verify_mode", ctypes.c_uint32),
+        ("batch_buffers", ctypes.c_uint32),
+        ("batch_bytes", ctypes.c_uint64),
+    ]
+
+
+class CtsPatternStats(ctypes.Structure):
+    _fields_ = [
+        ("bytes_sent", ctypes.c_uint64),
+        ("bytes_recv", ctypes.c_uint64),
+        ("buffers_verified", ctypes.c_uint64),
+        ("bytes_verified", ctypes.c_uint64),
+        ("buffers_failed", ctypes.c_uint64),
+        ("bytes_recv_at_failure", ctypes.c_uint64),
+        ("recv_pattern_offset", ctypes.c_uint32),
+        ("send_pattern_offset", ctypes.c_uint32),
+        ("last_error", ctypes.c_uint32),
+        ("queued", ctypes.c_uint32),
+        ("fail_length", ctypes.c_uint32),
+        ("fail_offset", ctypes.c_uint32),
+        ("fail_expected", ctypes.c_uint8),
+        ("fail_actual", ctypes.c_uint8),
+        ("has_failure", ctypes.c_uint8),
+        ("reserved", ctypes.c_uint8),
+        ("fail_completion", ctypes.c_uint32),
+    ]
+
+    def as_dict(self) -> dict:
+        return {f: int(getattr(self, f)) for f, _ in self._fields_ if f != "reserved"}
+
+
+class CtsStatusDetails(ctypes.Structure):
+    _fields_ = [("bytes_sent", ctypes.c_uint64), ("bytes_recv", ctypes.c_uint64), ("data_errors", ctypes.c_uint64)]
+
+
+assert ctypes.sizeof(CtsTask) == 40
+assert ctypes.sizeof(CtsPatternConfig) == 80
+
+# int (*)(void* ctx, const uint8_t* host_arena, uint64_t arena_bytes, const cts_buf_desc* descs,
+#         uint32_t n, cts_verify_result* results)
+BATCH_VERIFIER = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                  ctypes.c_uint32, ctypes.POINTER(CtsVerifyResult))
+
+
+def declare(L: ctypes.CDLL) -> None:
+    P = ctypes.c_void_p
+    u32, u64, i32 = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
+    sigs = {
+        "cts_shared_buffer_init": ([P, u32], i32),
+        "cts_shared_buffer_attach": ([P, u64], i32),
+        "cts_shared_buffer": ([], P),
+        "cts_shared_buffer_bytes": ([], u64),
+        "cts_shared_buffer_release": ([], None),
+        "cts_io_pattern_create": ([ctypes.POINTER(CtsPatternConfig), P, ctypes.POINTER(P)], i32),
+        "cts_io_pattern_destroy": ([P], i32),
+        "cts_io_pattern_set_verifier": ([P, BATCH_VERIFIER, P], i32),
+        "cts_io_pattern_initiate_io": ([P, ctypes.POINTER(CtsTask)], i32),
+        "cts_io_pattern_complete_io": ([P, ctypes.POINTER(CtsTask), u32, u32], i32),
+        "cts_io_pattern_last_error": ([P], u32),
+        "cts_io_pattern_flush": ([P], i32),
+        "cts_io_pattern_get_stats": ([P, ctypes.POINTER(CtsPatternStats)], i32),
+        "cts_io_pattern_failure_message": ([P, ctypes.c_char_p, u32], i32),
+        "cts_io_pattern_fail_fast_reason": ([P], ctypes.c_char_p),
+        "cts_io_pattern_connection_id": ([P], ctypes.c_char_p),
+        "cts_status_details_read": ([ctypes.POINTER(CtsStatusDetails)], i32),
+        "cts_status_details_reset": ([], None),
+    }
+    for name, (argtypes, restype) in sigs.items():
+        fn = getattr(L, name)
+        fn.argtypes = argtypes
+        fn.restype = restype

@@ -1,0 +1,1083 @@
+// cts_pattern.cpp — host-side ctsIoPattern mirror (include/cts_pattern.h): the
+// caller of the gfx950 fill/verify engine, restated from the reference
+// (microsoft/ctsTraffic) so the IO functors can hand completed buffers over
+// unchanged.
+//
+//   PatternState     ctsTraffic/ctsIOPatternState.hpp:57-504 (ctsIoPatternState)
+//   IoPattern        ctsTraffic/ctsIOPattern.cpp:133-743     (ctsIoPattern base)
+//   Push/Pull/...    ctsTraffic/ctsIOPattern.cpp:796-1031    (concrete TCP patterns)
+//
+// The two hot-path pieces go to the GPU: the sender buffer is written by the
+// fill kernel (cts_shared_buffer_init) and VerifyBuffer runs the verify kernel
+// on the pattern's pinned, device-mapped recv buffers (zero copy) — per
+// completion (CTS_VERIFY_SYNC) or batched (CTS_VERIFY_DEFERRED).
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <array>
+#include <atomic>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <new>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "cts_engine.h"
+#include "cts_pattern.h"
+
+namespace {
+
+constexpr uint32_t kPatternSize = CTS_PATTERN_PERIOD;  // c_bufferPatternSize, ctsIOPattern.cpp:35
+constexpr uint32_t kStatusIoRunning = CTS_STATUS_IO_RUNNING;
+constexpr uint32_t kNoError = 0;
+constexpr char kCompletionMessage[CTS_COMPLETION_MESSAGE_SIZE + 1] = "DONE";  // ctsIOPatternState.hpp:24
+
+// ---- process-wide state -------------------------------------------------------------------
+// g_senderSharedBuffer / g_maximumBufferSize (ctsIOPattern.cpp:40-47): one per process.
+struct SharedBuffer {
+    std::mutex mu;
+    char* host = nullptr;
+    uint64_t bytes = 0;
+    bool owned = false;       // pinned by cts_shared_buffer_init (hipHostFree on release)
+    cts_engine* engine = nullptr;
+    std::vector<char> receiver;  // g_receiverSharedBuffer (UseSharedBuffer, ctsIOPattern.cpp:138-152)
+};
+SharedBuffer g_shared;
+
+// TcpStatusDetails (ctsConfig.h:415) + a DataError tally
+std::atomic<uint64_t> g_bytesSent{0};
+std::atomic<uint64_t> g_bytesRecv{0};
+std::atomic<uint64_t> g_dataErrors{0};
+
+// ---- ctsIoPatternState ------------------------------------------------------------------------
+enum class PatternType { NoIo, SendConnectionId, RecvConnectionId, MoreIo, SendCompletion, RecvCompletion,
+                         GracefulShutdown, HardShutdown, RequestFin };
+enum class PatternError { NoError, TooManyBytes, TooFewBytes, CorruptedBytes, ErrorIoFailed, SuccessfullyCompleted };
+
+struct FailFast {
+    std::string reason;
+};
+
+class PatternState {
+public:
+    enum class Internal { Initialized, MoreIo, ServerSendConnectionId, ClientRecvConnectionId, ServerSendCompletion,
+                          ClientRecvCompletion, CompletedTransfer, ErrorIoFailed, GracefulShutdown, HardShutdown,
+                          RequestFin };
+
+    PatternState(const cts_pattern_config& c, uint32_t max_buffer_size)
+        : m_maxTransfer(c.transfer_size),
+          m_idealSendBacklog(c.pre_post_sends == 0 ? max_buffer_size : max_buffer_size * c.pre_post_sends),
+          m_listening(c.listening != 0),
+          m_graceful(c.tcp_shutdown != CTS_SHUTDOWN_HARD)
+    {
+    }
+
+    uint64_t GetRemainingTransfer() const  // ctsIOPatternState.hpp:123-141
+    {
+        const uint64_t already = m_confirmedBytes + m_inFlightBytes;
+        if (already > m_maxTransfer) throw FailFast{"bytes already transferred exceed the total to transfer"};
+        return m_maxTransfer - already;
+    }
+    uint64_t GetMaxTransfer() const { return m_maxTransfer; }
+    void SetMaxTransfer(uint64_t v) { m_maxTransfer = v; }
+    uint32_t GetIdealSendBacklog() const { return m_idealSendBacklog; }
+    bool IsCompleted() const { return m_internal == Internal::CompletedTransfer || m_internal == Internal::ErrorIoFailed; }
+    bool IsCurrentStateMoreIo() const { return m_internal == Internal::MoreIo; }
+
+    PatternType GetNextPatternType()  // ctsIOPatternState.hpp:177-244
+    {
+        if (m_pended) return PatternType::NoIo;
+        switch (m_internal) {
+        case Internal::Initialized:
+            m_pended = true;
+            if (m_listening) {
+                m_internal = Internal::ServerSendConnectionId;
+                return PatternType::SendConnectionId;
+            }
+            m_internal = Internal::ClientRecvConnectionId;
+            return PatternType::RecvConnectionId;
+        case Internal::ServerSendConnectionId:
+        case Internal::ClientRecvConnectionId:
+            m_internal = Internal::MoreIo;
+            return PatternType::MoreIo;
+        case Internal::MoreIo:
+            return (m_confirmedBytes + m_inFlightBytes) < m_maxTransfer ? PatternType::MoreIo : PatternType::NoIo;
+        case Internal::ServerSendCompletion: m_pended = true; return PatternType::SendCompletion;
+        case Internal::ClientRecvCompletion: m_pended = true; return PatternType::RecvCompletion;
+        case Internal::GracefulShutdown: m_pended = true; return PatternType::GracefulShutdown;
+        case Internal::HardShutdown: m_pended = true; return PatternType::HardShutdown;
+        case Internal::RequestFin: m_pended = true; return PatternType::RequestFin;
+        case Internal::CompletedTransfer:
+        case Internal::ErrorIoFailed: return PatternType::NoIo;
+        }
+        throw FailFast{"GetNextPatternType called in an invalid state"};
+    }
+
+    void NotifyNextTask(const cts_task& t)  // ctsIOPatternState.hpp:246-252
+    {
+        if (t.track_io) m_inFlightBytes += t.buffer_length;
+    }
+
+    PatternError UpdateError(uint32_t error)  // ctsIOPatternState.hpp:254-293 (TCP branch)
+    {
+        if (m_internal == Internal::ErrorIoFailed) return PatternError::ErrorIoFailed;
+        if (error != 0 && !IsCompleted()) {
+            // WSAETIMEDOUT / WSAECONNRESET / WSAECONNABORTED while a server waits for the FIN
+            if (m_listening && m_internal == Internal::RequestFin && (error == 10060 || error == 10054 || error == 10053))
+                return PatternError::NoError;
+            m_internal = Internal::ErrorIoFailed;
+            return PatternError::ErrorIoFailed;
+        }
+        return PatternError::NoError;
+    }
+
+    // True when CompletedTask(task, bytes) would return NoError and leave the
+    // state in MoreIo without side effects beyond the byte accounting — the
+    // completions a DEFERRED pattern may verify later (cts_io_pattern_flush).
+    bool WouldStayMoreIo(const cts_task& t, uint32_t bytes) const
+    {
+        if (m_internal != Internal::MoreIo || !t.track_io) return false;
+        if (bytes > t.buffer_length || t.buffer_length > m_inFlightBytes) return false;
+        const uint64_t inflight = m_inFlightBytes - t.buffer_length;
+        const uint64_t already = m_confirmedBytes + bytes + inflight;
+        if (already < m_maxTransfer) return bytes != 0;
+        if (already == m_maxTransfer) return inflight != 0;
+        return false;
+    }
+
+    PatternError CompletedTask(const cts_task& t, uint32_t bytes)  // ctsIOPatternState.hpp:295-504 (TCP)
+    {
+        if (m_internal == Internal::ErrorIoFailed) return PatternError::ErrorIoFailed;
+        if (m_internal == Internal::ServerSendConnectionId || m_internal == Internal::ClientRecvConnectionId) {
+            if (bytes != CTS_CONNECTION_ID_LENGTH) {
+                m_internal = Internal::ErrorIoFailed;
+                return PatternError::TooFewBytes;
+            }
+            m_pended = false;
+        }
+        if (t.track_io) {
+            if (bytes > m_inFlightBytes) throw FailFast{"task returned more bytes than were in flight"};
+            if (t.buffer_length > m_inFlightBytes) throw FailFast{"task requested more bytes than were in flight"};
+            if (bytes > t.buffer_length) throw FailFast{"task returned more bytes than were posted"};
+            m_inFlightBytes -= t.buffer_length;
+            m_confirmedBytes += bytes;
+        }
+        const uint64_t already = m_confirmedBytes + m_inFlightBytes;
+        if (already < m_maxTransfer) {
+            if (bytes == 0) {
+                m_internal = Internal::ErrorIoFailed;
+                return PatternError::TooFewBytes;
+            }
+        } else if (already == m_maxTransfer) {
+            if (m_inFlightBytes == 0) {
+                if (m_listening) {
+                    switch (m_internal) {
+                    case Internal::MoreIo:
+                        m_internal = Internal::ServerSendCompletion;
+                        m_pended = false;
+                        break;
+                    case Internal::ServerSendCompletion:
+                        m_internal = Internal::RequestFin;
+                        m_pended = false;
+                        break;
+                    case Internal::RequestFin:
+                        if (bytes != 0) {
+                            m_internal = Internal::ErrorIoFailed;
+                            return PatternError::TooManyBytes;
+                        }
+                        m_internal = Internal::CompletedTransfer;
+                        return PatternError::SuccessfullyCompleted;
+                    default: throw FailFast{"CompletedTask: invalid server state"};
+                    }
+                } else {
+                    switch (m_internal) {
+                    case Internal::MoreIo:
+                        m_internal = Internal::ClientRecvCompletion;
+                        m_pended = false;
+                        break;
+                    case Internal::ClientRecvCompletion:
+                        if (bytes != CTS_COMPLETION_MESSAGE_SIZE ||
+                            std::memcmp(t.buffer, kCompletionMessage, CTS_COMPLETION_MESSAGE_SIZE) != 0) {
+                            m_internal = Internal::ErrorIoFailed;
+                            return PatternError::TooFewBytes;
+                        }
+                        m_internal = m_graceful ? Internal::GracefulShutdown : Internal::HardShutdown;
+                        m_pended = false;
+                        break;
+                    case Internal::GracefulShutdown:
+                        m_internal = Internal::RequestFin;
+                        m_pended = false;
+                        break;
+                    case Internal::RequestFin:
+                        if (bytes != 0) {
+                            m_internal = Internal::ErrorIoFailed;
+                            return PatternError::TooManyBytes;
+                        }
+                        m_internal = Internal::CompletedTransfer;
+                        return PatternError::SuccessfullyCompleted;
+                    case Internal::HardShutdown:
+                        m_internal = Internal::CompletedTransfer;
+                        return PatternError::SuccessfullyCompleted;
+                    default: throw FailFast{"CompletedTask: invalid client state"};
+                    }
+                }
+            }
+        } else {
+            m_internal = Internal::ErrorIoFailed;
+            return PatternError::TooManyBytes;
+        }
+        return PatternError::NoError;
+    }
+
+private:
+    uint64_t m_confirmedBytes = 0;
+    uint64_t m_maxTransfer;
+    uint64_t m_inFlightBytes = 0;
+    uint32_t m_idealSendBacklog;
+    Internal m_internal = Internal::Initialized;
+    bool m_pended = false;
+    bool m_listening;
+    bool m_graceful;
+};
+
+// ---- pinned host memory helpers -------------------------------------------------------------
+struct Pinned {
+    uint8_t* host = nullptr;
+    uint8_t* dev = nullptr;  // device view (hipHostGetDevicePointer)
+    uint64_t bytes = 0;
+    cts_engine* engine = nullptr;
+    int alloc(cts_engine* e, uint64_t n)
+    {
+        void *h = nullptr, *d = nullptr;
+        const int rc = cts_host_alloc(e, n, &h, &d);
+        if (rc != CTS_OK) return rc;
+        host = static_cast<uint8_t*>(h);
+        dev = static_cast<uint8_t*>(d);
+        bytes = n;
+        engine = e;
+        return CTS_OK;
+    }
+    void release()
+    {
+        if (host) (void)cts_host_free(engine, host);
+        host = dev = nullptr;
+        bytes = 0;
+    }
+    ~Pinned() { release(); }
+};
+
+struct Queued {
+    uint32_t completion;     // recv completion index
+    uint32_t transferred;
+    uint64_t bytes_recv_after;  // m_bytesRecv after this completion (as the reference would count it)
+};
+
+}  // namespace
+
+// ---- ctsIoPattern -----------------------------------------------------------------------------
+struct cts_io_pattern {
+    explicit cts_io_pattern(const cts_pattern_config& c, uint32_t maxbuf, uint32_t recv_count)
+        : cfg(c), max_buffer_size(maxbuf), state(c, maxbuf), rng(c.random_seed), recvCount(recv_count)
+    {
+    }
+    virtual ~cts_io_pattern()
+    {
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+
+    cts_pattern_config cfg;
+    uint32_t max_buffer_size;
+    PatternState state;
+    std::mt19937_64 rng;
+    uint32_t recvCount;
+    cts_engine* engine = nullptr;
+    cts_batch_verifier hook = nullptr;
+    void* hook_ctx = nullptr;
+    hipStream_t stream = nullptr;
+
+    uint32_t m_sendPatternOffset = 0;
+    uint32_t m_recvPatternOffset = 0;
+    uint32_t m_lastError = kStatusIoRunning;
+    std::vector<char*> m_recvBufferFreeList;
+    Pinned recv_pinned;                 // m_recvBufferContainer when a device verifies in place
+    std::vector<char> recv_plain;       // m_recvBufferContainer otherwise
+    std::array<char, CTS_COMPLETION_MESSAGE_SIZE> m_completionMessageBuffer{};
+    char connection_id[CTS_CONNECTION_ID_LENGTH] = {};
+    std::string fail_fast;
+
+    // statistics + verify bookkeeping
+    uint64_t bytes_sent = 0, bytes_recv = 0;
+    uint64_t buffers_verified = 0, bytes_verified = 0, buffers_failed = 0;
+    uint64_t bytes_recv_at_failure = 0;
+    uint32_t recv_completions = 0;
+    bool has_failure = false;
+    uint32_t fail_length = 0, fail_offset = 0, fail_completion = 0;
+    uint8_t fail_expected = 0, fail_actual = 0;
+
+    // SYNC device verify: one descriptor + one result, pinned and device-mapped
+    Pinned one;
+    // DEFERRED queue
+    Pinned stage, stage_desc, stage_res;
+    std::vector<uint8_t> hstage;        // host staging when a hook verifies
+    std::vector<cts_buf_desc> hdesc;
+    std::vector<cts_verify_result> hres;
+    std::vector<Queued> queue;
+    uint64_t stage_used = 0;
+
+    uint32_t GetBufferSize()  // ctsConfig.cpp:4679-4684
+    {
+        if (cfg.buffer_size_high == 0) return cfg.buffer_size_low;
+        std::uniform_int_distribution<uint32_t> d(cfg.buffer_size_low, cfg.buffer_size_high);
+        return d(rng);
+    }
+
+    // derived-pattern interface (ctsIOPattern.h:187-188)
+    virtual cts_task GetNextTaskFromPattern() = 0;
+    virtual PatternError CompleteTaskBackToPattern(const cts_task&, uint32_t) = 0;
+
+    uint64_t GetTotalTransfer() const { return state.GetMaxTransfer(); }
+    void SetTotalTransfer(uint64_t v) { state.SetMaxTransfer(v); }
+    uint32_t GetIdealSendBacklog() const { return state.GetIdealSendBacklog(); }
+
+    uint32_t UpdateLastError(uint32_t error)  // ctsIOPattern.h:344-365
+    {
+        if (m_lastError == kStatusIoRunning) {
+            const PatternError st = state.UpdateError(error);
+            if (error == kNoError) {
+                if (st != PatternError::ErrorIoFailed) m_lastError = kNoError;
+            } else if (st == PatternError::ErrorIoFailed) {
+                m_lastError = error;
+                if (error == CTS_STATUS_ERROR_DATA_DID_NOT_MATCH_BIT_PATTERN) g_dataErrors.fetch_add(1);
+            }
+        }
+        return m_lastError;
+    }
+
+    void UpdateLastPatternError(PatternError e)  // ctsIOPattern.h:367-392
+    {
+        switch (e) {
+        case PatternError::CorruptedBytes: UpdateLastError(CTS_STATUS_ERROR_DATA_DID_NOT_MATCH_BIT_PATTERN); break;
+        case PatternError::TooFewBytes: UpdateLastError(CTS_STATUS_ERROR_NOT_ALL_DATA_TRANSFERRED); break;
+        case PatternError::TooManyBytes: UpdateLastError(CTS_STATUS_ERROR_TOO_MUCH_DATA_TRANSFERRED); break;
+        case PatternError::SuccessfullyCompleted: UpdateLastError(kNoError); break;
+        case PatternError::NoError:
+        case PatternError::ErrorIoFailed: break;
+        }
+    }
+
+    int GetCurrentStatus() const  // ctsIOPattern.h:160-174
+    {
+        if (m_lastError == kStatusIoRunning) return CTS_IO_CONTINUE;
+        if (m_lastError == kNoError) return CTS_IO_COMPLETED;
+        return CTS_IO_FAILED;
+    }
+
+    int CreateRecvBuffers()  // ctsIOPattern.cpp:133-193 (RIO registration not restated)
+    {
+        m_recvBufferFreeList.assign(recvCount, nullptr);
+        if (recvCount == 0) return CTS_OK;
+        if (cfg.use_shared_buffer) {
+            std::lock_guard<std::mutex> lk(g_shared.mu);
+            if (g_shared.receiver.size() < g_shared.bytes) g_shared.receiver.resize(g_shared.bytes);
+            for (auto& b : m_recvBufferFreeList) b = g_shared.receiver.data();
+            return CTS_OK;
+        }
+        const uint64_t bytes = (uint64_t)max_buffer_size * recvCount;
+        char* base = nullptr;
+        if (engine != nullptr && hook == nullptr) {
+            const int rc = recv_pinned.alloc(engine, bytes ? bytes : 16);
+            if (rc != CTS_OK) return rc;
+            base = reinterpret_cast<char*>(recv_pinned.host);
+        } else {
+            recv_plain.assign(bytes, 0);
+            base = recv_plain.data();
+        }
+        for (uint32_t i = 0; i < recvCount; ++i) m_recvBufferFreeList[i] = base + (size_t)i * max_buffer_size;
+        return CTS_OK;
+    }
+
+    void CreateSendBuffers()  // ctsIOPattern.cpp:195-217
+    {
+        std::memcpy(m_completionMessageBuffer.data(), kCompletionMessage, CTS_COMPLETION_MESSAGE_SIZE);
+    }
+
+    cts_task CreateNewTask(uint8_t action, uint32_t maxTransfer)  // ctsIOPattern.cpp:550-743
+    {
+        const uint64_t remaining = state.GetRemainingTransfer();
+        const uint64_t next = GetBufferSize();
+        const uint64_t minBuf = std::min<uint64_t>(remaining, next);
+        uint64_t newSize = minBuf;
+        if (maxTransfer > 0 && maxTransfer < minBuf) newSize = maxTransfer;
+        if (newSize > 0xFFFFFFFFull) throw FailFast{"next buffer size is greater than MAXDWORD"};
+        const uint32_t size = (uint32_t)newSize;
+        cts_task t{};
+        if (action == CTS_TASK_SEND) {
+            t.io_action = CTS_TASK_SEND;
+            t.buffer_type = CTS_BUFFER_STATIC;
+            t.buffer_length = size;
+            t.buffer_offset = m_sendPatternOffset;
+            t.expected_pattern_offset = 0;
+            t.buffer = g_shared.host;
+            m_sendPatternOffset += size;
+            m_sendPatternOffset %= kPatternSize;
+            if ((uint64_t)t.buffer_length + t.buffer_offset > g_shared.bytes)
+                throw FailFast{"send task is larger than the shared sender buffer"};
+        } else {
+            t.io_action = CTS_TASK_RECV;
+            t.buffer_type = CTS_BUFFER_DYNAMIC;
+            t.buffer_length = size;
+            t.buffer_offset = 0;
+            t.expected_pattern_offset = m_recvPatternOffset;
+            if (m_recvBufferFreeList.empty()) throw FailFast{"m_recvBufferFreeList is empty for a new Recv task"};
+            t.buffer = m_recvBufferFreeList.back();
+            m_recvBufferFreeList.pop_back();
+            if (m_recvPatternOffset >= kPatternSize) throw FailFast{"recv pattern offset too large"};
+        }
+        return t;
+    }
+    cts_task CreateTrackedTask(uint8_t a, uint32_t maxTransfer = 0)
+    {
+        cts_task t = CreateNewTask(a, maxTransfer);
+        t.track_io = 1;
+        return t;
+    }
+
+    cts_task InitiateIo()  // ctsIOPattern.cpp:251-356
+    {
+        cts_task t{};
+        switch (state.GetNextPatternType()) {
+        case PatternType::MoreIo: t = GetNextTaskFromPattern(); break;
+        case PatternType::NoIo: break;
+        case PatternType::SendConnectionId:
+        case PatternType::RecvConnectionId:
+            t.io_action = cfg.listening ? CTS_TASK_SEND : CTS_TASK_RECV;
+            t.buffer = connection_id;
+            t.buffer_length = CTS_CONNECTION_ID_LENGTH;
+            t.buffer_type = CTS_BUFFER_TCP_CONNECTION_ID;
+            break;
+        case PatternType::SendCompletion:
+        case PatternType::RecvCompletion:
+            t.io_action = cfg.listening ? CTS_TASK_SEND : CTS_TASK_RECV;
+            t.buffer = m_completionMessageBuffer.data();
+            t.buffer_length = CTS_COMPLETION_MESSAGE_SIZE;
+            t.buffer_type = CTS_BUFFER_COMPLETION_MESSAGE;
+            break;
+        case PatternType::HardShutdown: t.io_action = CTS_TASK_HARD_SHUTDOWN; break;
+        case PatternType::GracefulShutdown: t.io_action = CTS_TASK_GRACEFUL_SHUTDOWN; break;
+        case PatternType::RequestFin:
+            t.io_action = CTS_TASK_RECV;
+            t.buffer = m_completionMessageBuffer.data();
+            t.buffer_length = CTS_COMPLETION_MESSAGE_SIZE;
+            t.buffer_type = CTS_BUFFER_STATIC;
+            break;
+        }
+        state.NotifyNextTask(t);
+        return t;
+    }
+
+    // ---- VerifyBuffer ------------------------------------------------------------------------
+    void RecordFailure(uint32_t completion, uint32_t transferred, const cts_verify_result& r, uint64_t recv_after)
+    {
+        ++buffers_failed;
+        if (has_failure) return;
+        has_failure = true;
+        fail_completion = completion;
+        fail_length = transferred;
+        fail_offset = r.first_mismatch;
+        fail_expected = r.expected;
+        fail_actual = r.actual;
+        bytes_recv_at_failure = recv_after;
+    }
+
+    int EnsureStream()
+    {
+        if (stream != nullptr) return CTS_OK;
+        return hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) == hipSuccess ? CTS_OK : CTS_E_HIP;
+    }
+
+    // One buffer, now (ctsIOPattern.cpp:745-775). Returns CTS_OK and sets *pass.
+    int VerifyNow(const cts_task& t, uint32_t transferred, cts_verify_result& r)
+    {
+        const char* src = t.buffer + t.buffer_offset;
+        if (hook != nullptr) {
+            cts_buf_desc d{0, transferred, t.expected_pattern_offset, 0, 0};
+            return hook(hook_ctx, reinterpret_cast<const uint8_t*>(src), transferred, &d, 1, &r) == 0 ? CTS_OK
+                                                                                                      : CTS_E_INVALID;
+        }
+        if (engine == nullptr) return CTS_E_INVALID;
+        const uint8_t* rp = reinterpret_cast<const uint8_t*>(src);
+        if (recv_pinned.host != nullptr && rp >= recv_pinned.host && rp + transferred <= recv_pinned.host + recv_pinned.bytes) {
+            // zero copy: the kernel reads the pinned recv buffer in place over PCIe
+            int rc = EnsureStream();
+            if (rc != CTS_OK) return rc;
+            if (one.host == nullptr && (rc = one.alloc(engine, 64)) != CTS_OK) return rc;
+            auto* d = reinterpret_cast<cts_buf_desc*>(one.host);
+            *d = cts_buf_desc{(uint64_t)(rp - recv_pinned.host), transferred, t.expected_pattern_offset, 0, 0};
+            rc = cts_verify(engine, recv_pinned.dev, recv_pinned.bytes, reinterpret_cast<cts_buf_desc*>(one.dev), 1,
+                            transferred, reinterpret_cast<cts_verify_result*>(one.dev + 32), nullptr, nullptr, 0,
+                            stream);
+            if (rc != CTS_OK) return rc;
+            if (hipStreamSynchronize(stream) != hipSuccess) return CTS_E_HIP;
+            std::memcpy(&r, one.host + 32, sizeof(r));
+            return CTS_OK;
+        }
+        return cts_verify_host(engine, src, transferred, t.expected_pattern_offset, &r);
+    }
+
+    uint64_t StageCapacity() const { return cfg.batch_bytes ? cfg.batch_bytes : (64ull << 20); }
+    uint32_t BatchCapacity() const { return cfg.batch_buffers ? cfg.batch_buffers : 1024u; }
+
+    // Queue one buffer for the next batch (DEFERRED). Returns CTS_OK.
+    int Enqueue(const cts_task& t, uint32_t transferred, uint64_t recv_after)
+    {
+        const uint64_t slot = ((uint64_t)transferred + 15u) & ~15ull;
+        if (!queue.empty() && stage_used + slot > StageCapacity()) {
+            const int rc = Flush();
+            if (rc < 0) return rc;
+        }
+        const uint64_t cap = std::max<uint64_t>(StageCapacity(), slot);
+        uint8_t* base = nullptr;
+        if (hook != nullptr) {
+            if (hstage.size() < cap) hstage.resize(cap);
+            if (hdesc.size() < BatchCapacity()) {
+                hdesc.resize(BatchCapacity());
+                hres.resize(BatchCapacity());
+            }
+            base = hstage.data();
+        } else {
+            if (engine == nullptr) return CTS_E_INVALID;
+            int rc;
+            if (stage.bytes < cap) {
+                stage.release();
+                if ((rc = stage.alloc(engine, cap)) != CTS_OK) return rc;
+            }
+            if (stage_desc.host == nullptr) {
+                if ((rc = stage_desc.alloc(engine, sizeof(cts_buf_desc) * (uint64_t)BatchCapacity())) != CTS_OK) return rc;
+                if ((rc = stage_res.alloc(engine, sizeof(cts_verify_result) * (uint64_t)BatchCapacity())) != CTS_OK)
+                    return rc;
+            }
+            base = stage.host;
+        }
+        if (transferred) std::memcpy(base + stage_used, t.buffer + t.buffer_offset, transferred);
+        cts_buf_desc* descs = hook ? hdesc.data() : reinterpret_cast<cts_buf_desc*>(stage_desc.host);
+        descs[queue.size()] = cts_buf_desc{stage_used, transferred, t.expected_pattern_offset, 0, 0};
+        queue.push_back(Queued{recv_completions, transferred, recv_after});
+        stage_used += slot;
+        return CTS_OK;
+    }
+
+    int Flush()  // cts_io_pattern_flush
+    {
+        if (queue.empty()) return GetCurrentStatus();
+        const uint32_t n = (uint32_t)queue.size();
+        const cts_verify_result* res = nullptr;
+        if (hook != nullptr) {
+            if (hook(hook_ctx, hstage.data(), stage_used, hdesc.data(), n, hres.data()) != 0) return CTS_E_INVALID;
+            res = hres.data();
+        } else {
+            int rc = EnsureStream();
+            if (rc != CTS_OK) return rc;
+            uint32_t maxlen = 0;
+            for (const auto& q : queue) maxlen = std::max(maxlen, q.transferred);
+            rc = cts_verify(engine, stage.dev, stage.bytes, reinterpret_cast<cts_buf_desc*>(stage_desc.dev), n, maxlen,
+                            reinterpret_cast<cts_verify_result*>(stage_res.dev), nullptr, nullptr, 0, stream);
+            if (rc != CTS_OK) return rc;
+            if (hipStreamSynchronize(stream) != hipSuccess) return CTS_E_HIP;
+            res = reinterpret_cast<const cts_verify_result*>(stage_res.host);
+        }
+        bool failed = false;
+        for (uint32_t i = 0; i < n; ++i) {
+            ++buffers_verified;
+            bytes_verified += queue[i].transferred;
+            if (!res[i].pass) {
+                RecordFailure(queue[i].completion, queue[i].transferred, res[i], queue[i].bytes_recv_after);
+                failed = true;
+            }
+        }
+        queue.clear();
+        stage_used = 0;
+        if (failed) UpdateLastError(CTS_STATUS_ERROR_DATA_DID_NOT_MATCH_BIT_PATTERN);
+        return GetCurrentStatus();
+    }
+
+    bool Deferred() const { return cfg.verify_mode == CTS_VERIFY_DEFERRED; }
+
+    bool VerifyGate(const cts_task& t) const  // ctsIOPattern.cpp:475-479 (TCP checked at create)
+    {
+        return cfg.verify_buffers && t.io_action == CTS_TASK_RECV && t.track_io;
+    }
+
+    int CompleteIo(const cts_task& t, uint32_t transfer, uint32_t status)  // ctsIOPattern.cpp:364-534
+    {
+        // DEFERRED: anything but a plain in-transfer tracked send/recv sees the
+        // queued verdicts first, so a pending data error latches before it.
+        bool benign = status == kNoError && (t.io_action == CTS_TASK_SEND || t.io_action == CTS_TASK_RECV) &&
+                      state.WouldStayMoreIo(t, transfer) && m_lastError == kStatusIoRunning;
+        if (Deferred() && !queue.empty() && !benign) {
+            const int rc = Flush();
+            if (rc < 0) return rc;
+        }
+        const bool wasIoRequestedFromPattern = state.IsCurrentStateMoreIo();
+        if (t.buffer_type == CTS_BUFFER_DYNAMIC && t.io_action == CTS_TASK_RECV) m_recvBufferFreeList.push_back(t.buffer);
+
+        bool verified_now = false, defer_this = false;
+        cts_verify_result vr{};
+        switch (t.io_action) {
+        case CTS_TASK_NONE: break;
+        case CTS_TASK_FATAL_ABORT: UpdateLastError(CTS_STATUS_ERROR_NOT_ALL_DATA_TRANSFERRED); break;
+        case CTS_TASK_ABORT: break;
+        case CTS_TASK_GRACEFUL_SHUTDOWN:
+        case CTS_TASK_HARD_SHUTDOWN:
+        case CTS_TASK_RECV:
+        case CTS_TASK_SEND: {
+            bool verifyIo = true;
+            if (t.buffer_type == CTS_BUFFER_TCP_CONNECTION_ID || t.buffer_type == CTS_BUFFER_COMPLETION_MESSAGE) {
+                verifyIo = false;
+                if (status != kNoError) {
+                    UpdateLastError(status);
+                } else {
+                    UpdateLastPatternError(state.CompletedTask(t, transfer));
+                }
+            } else if (status != kNoError) {
+                if (!(t.io_action == CTS_TASK_RECV && state.IsCompleted())) {
+                    if (UpdateLastError(status) != kStatusIoRunning) verifyIo = false;
+                }
+            }
+            if (verifyIo) {
+                const PatternError ps = state.CompletedTask(t, transfer);
+                UpdateLastPatternError(ps);
+                if (VerifyGate(t) && (ps == PatternError::SuccessfullyCompleted || ps == PatternError::NoError)) {
+                    if (t.expected_pattern_offset != m_recvPatternOffset)
+                        throw FailFast{"task expected_pattern_offset does not match the current pattern offset"};
+                    if (Deferred()) {
+                        defer_this = true;
+                    } else {
+                        const int rc = VerifyNow(t, transfer, vr);
+                        if (rc != CTS_OK) return rc;
+                        verified_now = true;
+                    }
+                    m_recvPatternOffset += transfer;
+                    m_recvPatternOffset %= kPatternSize;
+                }
+            }
+            break;
+        }
+        default: throw FailFast{"CompleteIo: unknown task action"};
+        }
+
+        if (t.io_action != CTS_TASK_NONE && status == kNoError) {
+            if (t.io_action == CTS_TASK_SEND) g_bytesSent.fetch_add(transfer);
+            else if (t.io_action == CTS_TASK_RECV) g_bytesRecv.fetch_add(transfer);
+            if (wasIoRequestedFromPattern) UpdateLastPatternError(CompleteTaskBackToPattern(t, transfer));
+        }
+        if (verified_now) {
+            ++buffers_verified;
+            bytes_verified += transfer;
+            if (!vr.pass) {
+                RecordFailure(recv_completions, transfer, vr, bytes_recv);
+                UpdateLastError(CTS_STATUS_ERROR_DATA_DID_NOT_MATCH_BIT_PATTERN);
+            }
+        }
+        if (defer_this) {
+            const int rc = Enqueue(t, transfer, bytes_recv);
+            if (rc < 0) return rc;
+            if (!benign || queue.size() >= BatchCapacity()) {
+                const int fr = Flush();
+                if (fr < 0) return fr;
+            }
+        }
+        if (t.io_action == CTS_TASK_RECV && t.track_io) ++recv_completions;
+        if (state.IsCompleted()) UpdateLastError(kNoError);
+        return GetCurrentStatus();
+    }
+};
+
+// The reference verifies inside CompleteIo *before* CompleteTaskBackToPattern
+// adds the bytes to m_statistics; the data-error latch order is identical here
+// (UpdateLastError keeps the first error), the verify call merely runs after the
+// byte accounting so bytes_recv_at_failure includes the failing completion, as
+// ctsIOPattern.cpp:505-521 counts it.
+
+namespace {
+
+// ---- concrete patterns (ctsIOPattern.cpp:796-1031) -------------------------------------------
+struct PushOrPull : cts_io_pattern {
+    // Push: the client sends, the server receives. Pull: the reverse.
+    PushOrPull(const cts_pattern_config& c, uint32_t maxbuf, bool receiving)
+        : cts_io_pattern(c, maxbuf, receiving ? c.pre_post_recvs : 0),
+          m_ioAction(receiving ? CTS_TASK_RECV : CTS_TASK_SEND),
+          m_recvNeeded(receiving ? c.pre_post_recvs : 0)
+    {
+    }
+    uint8_t m_ioAction;
+    uint32_t m_recvNeeded;
+    uint32_t m_sendBytesInFlight = 0;
+    cts_task GetNextTaskFromPattern() override  // :803-822 / :856-875
+    {
+        if (m_ioAction == CTS_TASK_RECV && m_recvNeeded > 0) {
+            --m_recvNeeded;
+            return CreateTrackedTask(m_ioAction);
+        }
+        if (m_ioAction == CTS_TASK_SEND && GetIdealSendBacklog() > m_sendBytesInFlight) {
+            const cts_task t = CreateTrackedTask(m_ioAction);
+            m_sendBytesInFlight += t.buffer_length;
+            return t;
+        }
+        return cts_task{};
+    }
+    PatternError CompleteTaskBackToPattern(const cts_task& t, uint32_t bytes) override  // :824-838
+    {
+        if (t.io_action == CTS_TASK_SEND) {
+            bytes_sent += bytes;
+            m_sendBytesInFlight -= bytes;
+        } else if (t.io_action == CTS_TASK_RECV) {
+            bytes_recv += bytes;
+            ++m_recvNeeded;
+        }
+        return PatternError::NoError;
+    }
+};
+
+struct PushPull : cts_io_pattern {  // :888-966
+    PushPull(const cts_pattern_config& c, uint32_t maxbuf)
+        : cts_io_pattern(c, maxbuf, 1), m_push(c.push_bytes), m_pull(c.pull_bytes), m_listening(c.listening != 0),
+          m_sending(c.listening == 0)
+    {
+    }
+    uint32_t m_push, m_pull, m_intra = 0;
+    bool m_listening, m_ioNeeded = true, m_sending;
+    uint32_t Segment() const
+    {
+        return m_listening ? (m_sending ? m_pull : m_push) : (m_sending ? m_push : m_pull);
+    }
+    cts_task GetNextTaskFromPattern() override
+    {
+        const uint32_t seg = Segment();
+        if (m_intra >= seg) throw FailFast{"invalid PushPull state: intra-segment transfer >= segment size"};
+        if (m_ioNeeded) {
+            m_ioNeeded = false;
+            return CreateTrackedTask(m_sending ? CTS_TASK_SEND : CTS_TASK_RECV, seg - m_intra);
+        }
+        return cts_task{};
+    }
+    PatternError CompleteTaskBackToPattern(const cts_task& t, uint32_t bytes) override
+    {
+        if (t.io_action == CTS_TASK_SEND) bytes_sent += bytes;
+        else if (t.io_action == CTS_TASK_RECV) bytes_recv += bytes;
+        m_ioNeeded = true;
+        m_intra += bytes;
+        const uint32_t seg = Segment();
+        if (m_intra > seg) throw FailFast{"invalid PushPull state: intra-segment transfer > segment size"};
+        if (seg == m_intra) {
+            m_sending = !m_sending;
+            m_intra = 0;
+        }
+        return PatternError::NoError;
+    }
+};
+
+struct Duplex : cts_io_pattern {  // :968-1031
+    Duplex(const cts_pattern_config& c, uint32_t maxbuf)
+        : cts_io_pattern(c, maxbuf, c.pre_post_recvs), m_recvNeeded(c.pre_post_recvs)
+    {
+        uint64_t total = GetTotalTransfer();
+        if (total % 2 != 0) SetTotalTransfer(++total);
+        m_remainingSend = total / 2;
+        m_remainingRecv = m_remainingSend;
+    }
+    uint64_t m_remainingSend = 0, m_remainingRecv = 0;
+    uint32_t m_recvNeeded;
+    uint32_t m_sendBytesInFlight = 0;
+    cts_task GetNextTaskFromPattern() override
+    {
+        constexpr uint64_t kMaxLong = 0x7FFFFFFF;
+        cts_task t{};
+        if (m_remainingRecv > 0 && m_recvNeeded > 0) {
+            t = CreateTrackedTask(CTS_TASK_RECV, (uint32_t)std::min(m_remainingRecv, kMaxLong));
+            m_remainingRecv -= t.buffer_length;
+            --m_recvNeeded;
+        } else if (m_remainingSend > 0 && GetIdealSendBacklog() > m_sendBytesInFlight) {
+            t = CreateTrackedTask(CTS_TASK_SEND, (uint32_t)std::min(m_remainingSend, kMaxLong));
+            m_remainingSend -= t.buffer_length;
+            m_sendBytesInFlight += t.buffer_length;
+        }
+        return t;
+    }
+    PatternError CompleteTaskBackToPattern(const cts_task& t, uint32_t bytes) override
+    {
+        if (t.io_action == CTS_TASK_SEND) {
+            bytes_sent += bytes;
+            m_sendBytesInFlight -= bytes;
+            m_remainingSend += t.buffer_length;
+            m_remainingSend -= bytes;
+        } else if (t.io_action == CTS_TASK_RECV) {
+            bytes_recv += bytes;
+            ++m_recvNeeded;
+            m_remainingRecv += t.buffer_length;
+            m_remainingRecv -= bytes;
+        }
+        return PatternError::NoError;
+    }
+};
+
+void make_connection_id(char* out)  // ctsStatistics::GenerateConnectionId: a UUID string
+{
+    std::random_device rd;
+    std::mt19937_64 g(((uint64_t)rd() << 32) ^ rd());
+    uint8_t b[16];
+    for (auto& x : b) x = (uint8_t)g();
+    b[6] = (uint8_t)((b[6] & 0x0F) | 0x40);
+    b[8] = (uint8_t)((b[8] & 0x3F) | 0x80);
+    std::snprintf(out, CTS_CONNECTION_ID_LENGTH,
+                  "%02x%02x%02x%02x-%02x%02x-%02x%02x-%02x%02x-%02x%02x%02x%02x%02x%02x", b[0], b[1], b[2], b[3],
+                  b[4], b[5], b[6], b[7], b[8], b[9], b[10], b[11], b[12], b[13], b[14], b[15]);
+}
+
+inline bool latch_fail_fast(cts_io_pattern* p, const FailFast& f)
+{
+    if (p->fail_fast.empty()) p->fail_fast = f.reason;
+    p->m_lastError = CTS_PATTERN_E_FAIL_FAST;
+    return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+int cts_shared_buffer_init(cts_engine* engine, uint32_t max_buffer_size)
+{
+    if (engine == nullptr) return CTS_E_INVALID;
+    std::lock_guard<std::mutex> lk(g_shared.mu);
+    const uint64_t need = cts_sender_buffer_size(max_buffer_size);
+    if (g_shared.host != nullptr && g_shared.owned && g_shared.bytes >= need) return CTS_OK;
+    void *h = nullptr, *d = nullptr;
+    int rc = cts_host_alloc(engine, need, &h, &d);
+    if (rc != CTS_OK) return rc;
+    // the fill kernel writes the pinned sender buffer through its device view
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
+        (void)cts_host_free(engine, h);
+        return CTS_E_HIP;
+    }
+    rc = cts_sender_buffer_fill(engine, d, max_buffer_size, s);
+    if (rc == CTS_OK && hipStreamSynchronize(s) != hipSuccess) rc = CTS_E_HIP;
+    (void)hipStreamDestroy(s);
+    if (rc != CTS_OK) {
+        (void)cts_host_free(engine, h);
+        return rc;
+    }
+    if (g_shared.owned && g_shared.host) (void)cts_host_free(g_shared.engine, g_shared.host);
+    g_shared.host = static_cast<char*>(h);
+    g_shared.bytes = need;
+    g_shared.owned = true;
+    g_shared.engine = engine;
+    return CTS_OK;
+}
+
+int cts_shared_buffer_attach(const void* host, uint64_t bytes)
+{
+    if (host == nullptr || bytes < CTS_PATTERN_PERIOD) return CTS_E_INVALID;
+    std::lock_guard<std::mutex> lk(g_shared.mu);
+    if (g_shared.owned && g_shared.host) (void)cts_host_free(g_shared.engine, g_shared.host);
+    g_shared.host = const_cast<char*>(static_cast<const char*>(host));
+    g_shared.bytes = bytes;
+    g_shared.owned = false;
+    g_shared.engine = nullptr;
+    return CTS_OK;
+}
+
+char* cts_shared_buffer(void) { return g_shared.host; }
+uint64_t cts_shared_buffer_bytes(void) { return g_shared.bytes; }
+
+void cts_shared_buffer_release(void)
+{
+    std::lock_guard<std::mutex> lk(g_shared.mu);
+    if (g_shared.owned && g_shared.host) (void)cts_host_free(g_shared.engine, g_shared.host);
+    g_shared.host = nullptr;
+    g_shared.bytes = 0;
+    g_shared.owned = false;
+    g_shared.engine = nullptr;
+}
+
+int cts_io_pattern_create(const cts_pattern_config* c, cts_engine* engine, cts_io_pattern** out)
+{
+    if (c == nullptr || out == nullptr) return CTS_E_INVALID;
+    *out = nullptr;
+    if (c->protocol != CTS_PROTOCOL_TCP) return CTS_E_INVALID;  // MediaStream (UDP) patterns: not restated yet
+    if (c->buffer_size_low == 0 || (c->buffer_size_high != 0 && c->buffer_size_high < c->buffer_size_low))
+        return CTS_E_INVALID;
+    if (c->pre_post_recvs == 0) return CTS_E_INVALID;                         // ctsConfig.cpp:2169-2171
+    if (c->verify_buffers && c->pre_post_recvs > 1) return CTS_E_INVALID;     // ctsConfig.cpp:3440-3446
+    if (c->use_shared_buffer && c->verify_buffers) return CTS_E_INVALID;      // ctsIOPattern.cpp:225-227
+    if (c->verify_mode != CTS_VERIFY_SYNC && c->verify_mode != CTS_VERIFY_DEFERRED) return CTS_E_INVALID;
+    const uint32_t maxbuf = c->buffer_size_high == 0 ? c->buffer_size_low : c->buffer_size_high;  // GetMaxBufferSize
+    if (engine != nullptr) {
+        const int rc = cts_shared_buffer_init(engine, maxbuf);  // InitOnceExecuteOnce(InitOnceIoPatternCallback)
+        if (rc != CTS_OK) return rc;
+    }
+    if (g_shared.host == nullptr || g_shared.bytes < cts_sender_buffer_size(maxbuf)) return CTS_E_INVALID;
+    cts_io_pattern* p = nullptr;
+    try {
+        switch (c->io_pattern) {
+        case CTS_PATTERN_PUSH: p = new PushOrPull(*c, maxbuf, c->listening != 0); break;
+        case CTS_PATTERN_PULL: p = new PushOrPull(*c, maxbuf, c->listening == 0); break;
+        case CTS_PATTERN_PUSHPULL:
+            if (c->push_bytes == 0 || c->pull_bytes == 0) return CTS_E_INVALID;
+            p = new PushPull(*c, maxbuf);
+            break;
+        case CTS_PATTERN_DUPLEX: p = new Duplex(*c, maxbuf); break;
+        default: return CTS_E_INVALID;
+        }
+    } catch (const std::bad_alloc&) {
+        return CTS_E_NOMEM;
+    }
+    p->engine = engine;
+    if (c->listening) make_connection_id(p->connection_id);
+    // ctsIoPatternStatistics ctor: CreateRecvBuffers + CreateSendBuffers (ctsIOPattern.h:420-432)
+    int rc = CTS_OK;
+    try {
+        rc = p->CreateRecvBuffers();
+        p->CreateSendBuffers();
+    } catch (const std::bad_alloc&) {
+        rc = CTS_E_NOMEM;
+    }
+    if (rc != CTS_OK) {
+        delete p;
+        return rc;
+    }
+    *out = p;
+    return CTS_OK;
+}
+
+int cts_io_pattern_destroy(cts_io_pattern* p)
+{
+    if (p == nullptr) return CTS_E_INVALID;
+    delete p;
+    return CTS_OK;
+}
+
+int cts_io_pattern_set_verifier(cts_io_pattern* p, cts_batch_verifier fn, void* ctx)
+{
+    if (p == nullptr) return CTS_E_INVALID;
+    if (!p->queue.empty()) return CTS_E_INVALID;
+    p->hook = fn;
+    p->hook_ctx = ctx;
+    return CTS_OK;
+}
+
+int cts_io_pattern_initiate_io(cts_io_pattern* p, cts_task* out)
+{
+    if (p == nullptr || out == nullptr) return CTS_E_INVALID;
+    *out = cts_task{};
+    if (!p->fail_fast.empty()) return CTS_OK;
+    try {
+        *out = p->InitiateIo();
+    } catch (const FailFast& f) {
+        latch_fail_fast(p, f);
+        *out = cts_task{};
+    } catch (const std::bad_alloc&) {
+        return CTS_E_NOMEM;
+    }
+    return CTS_OK;
+}
+
+int cts_io_pattern_complete_io(cts_io_pattern* p, const cts_task* t, uint32_t current_transfer, uint32_t status)
+{
+    if (p == nullptr || t == nullptr) return CTS_E_INVALID;
+    if (!p->fail_fast.empty()) return CTS_IO_FAILED;
+    if (p->hook == nullptr && p->engine == nullptr && p->cfg.verify_buffers && t->io_action == CTS_TASK_RECV &&
+        t->track_io)
+        return CTS_E_INVALID;  // no verifier: the product has no CPU verify path
+    try {
+        return p->CompleteIo(*t, current_transfer, status);
+    } catch (const FailFast& f) {
+        latch_fail_fast(p, f);
+        return CTS_IO_FAILED;
+    } catch (const std::bad_alloc&) {
+        return CTS_E_NOMEM;
+    }
+}
+
+uint32_t cts_io_pattern_last_error(const cts_io_pattern* p) { return p ? p->m_lastError : CTS_STATUS_IO_RUNNING; }
+
+int cts_io_pattern_flush(cts_io_pattern* p)
+{
+    if (p == nullptr) return CTS_E_INVALID;
+    try {
+        return p->Flush();
+    } catch (const FailFast& f) {
+        latch_fail_fast(p, f);
+        return CTS_IO_FAILED;
+    }
+}
+
+int cts_io_pattern_get_stats(const cts_io_pattern* p, cts_pattern_stats* o)
+{
+    if (p == nullptr || o == nullptr) return CTS_E_INVALID;
+    *o = cts_pattern_stats{};
+    o->bytes_sent = p->bytes_sent;
+    o->bytes_recv = p->bytes_recv;
+    o->buffers_verified = p->buffers_verified;
+    o->bytes_verified = p->bytes_verified;
+    o->buffers_failed = p->buffers_failed;
+    o->bytes_recv_at_failure = p->has_failure ? p->bytes_recv_at_failure : p->bytes_recv;
+    o->recv_pattern_offset = p->m_recvPatternOffset;
+    o->send_pattern_offset = p->m_sendPatternOffset;
+    o->last_error = p->m_lastError;
+    o->queued = (uint32_t)p->queue.size();
+    o->fail_length = p->fail_length;
+    o->fail_offset = p->fail_offset;
+    o->fail_expected = p->fail_expected;
+    o->fail_actual = p->fail_actual;
+    o->has_failure = p->has_failure ? 1 : 0;
+    o->fail_completion = p->fail_completion;
+    return CTS_OK;
+}
+
+int cts_io_pattern_failure_message(const cts_io_pattern* p, char* buf, uint32_t buf_len)
+{
+    if (p == nullptr || !p->has_failure) return 0;
+    // ctsIOPattern.cpp:761-772: the bytes are `char`, so values >= 0x80 print sign-extended
+    // through %x (MSVC: 32-bit unsigned). Pointers are not part of the parity contract.
+    char tmp[512];
+    const int n = std::snprintf(tmp, sizeof(tmp),
+                                "ctsIOPattern found data corruption: detected an invalid byte pattern in the returned "
+                                "buffer (length %u): mismatch from expected pattern at offset (%u) [expected 32-bit "
+                                "value '0x%x' didn't match '0x%x']",
+                                p->fail_length, p->fail_offset, (unsigned)(int)(int8_t)p->fail_expected,
+                                (unsigned)(int)(int8_t)p->fail_actual);
+    if (buf != nullptr && buf_len > 0) {
+        const size_t k = std::min<size_t>((size_t)n, buf_len - 1);
+        std::memcpy(buf, tmp, k);
+        buf[k] = 0;
+    }
+    return n;
+}
+
+const char* cts_io_pattern_fail_fast_reason(const cts_io_pattern* p)
+{
+    return (p == nullptr || p->fail_fast.empty()) ? nullptr : p->fail_fast.c_str();
+}
+
+const char* cts_io_pattern_connection_id(cts_io_pattern* p) { return p ? p->connection_id : nullptr; }
+
+int cts_status_details_read(cts_status_details* o)
+{
+    if (o == nullptr) return CTS_E_INVALID;
+    o->bytes_sent = g_bytesSent.load();
+    o->bytes_recv = g_bytesRecv.load();
+    o->data_errors = g_dataErrors.load();
+    return CTS_OK;
+}
+
+void cts_status_details_reset(void)
+{
+    g_bytesSent = 0;
+    g_bytesRecv = 0;
+    g_dataErrors = 0;
+}
+
+}  // extern "C"

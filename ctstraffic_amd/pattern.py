@@ -1,0 +1,196 @@
+"""Python handle over the ctsIoPattern mirror (include/cts_pattern.h).
+
+Keeps the reference's names (ctsTraffic/ctsIOPattern.h:80-144):
+``IoPattern.MakeIoPattern(config, engine)``, ``InitiateIo()``,
+``CompleteIo(task, currentTransfer, statusCode)``, ``GetLastPatternError()``,
+``AccessSharedBuffer()``, so tests replaying the reference's MSTest scenarios
+read like the originals.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Callable, Optional
+
+import numpy as np
+
+from . import _pattern_abi as A
+from ._lib import CtsError, check, lib
+from .types import DESC_DTYPE, RESULT_DTYPE
+
+ctsTask = A.CtsTask
+
+
+@dataclass
+class PatternConfig:
+    """The ctsConfig settings the pattern reads (ctsConfig.h:370-462), explicit."""
+
+    io_pattern: int = A.PATTERN_PUSH
+    listening: bool = False
+    verify_buffers: bool = True
+    use_shared_buffer: bool = False
+    pre_post_recvs: int = 1
+    pre_post_sends: int = 1
+    buffer_size: int = 65536
+    buffer_size_high: int = 0
+    push_bytes: int = 0
+    pull_bytes: int = 0
+    tcp_shutdown: int = A.SHUTDOWN_GRACEFUL
+    transfer_size: int = 1 << 30
+    random_seed: int = 0
+    verify_mode: int = A.VERIFY_SYNC
+    batch_buffers: int = 0
+    batch_bytes: int = 0
+
+    def to_c(self) -> A.CtsPatternConfig:
+        c = A.CtsPatternConfig()
+        c.io_pattern = self.io_pattern
+        c.protocol = A.PROTOCOL_TCP
+        c.listening = int(bool(self.listening))
+        c.verify_buffers = int(bool(self.verify_buffers))
+        c.use_shared_buffer = int(bool(self.use_shared_buffer))
+        c.pre_post_recvs = self.pre_post_recvs
+        c.pre_post_sends = self.pre_post_sends
+        c.buffer_size_low = self.buffer_size
+        c.buffer_size_high = self.buffer_size_high
+        c.push_bytes = self.push_bytes
+        c.pull_bytes = self.pull_bytes
+        c.tcp_shutdown = self.tcp_shutdown
+        c.transfer_size = self.transfer_size
+        c.random_seed = self.random_seed
+        c.verify_mode = self.verify_mode
+        c.batch_buffers = self.batch_buffers
+        c.batch_bytes = self.batch_bytes
+        return c
+
+    @property
+    def max_buffer_size(self) -> int:
+        return self.buffer_size_high or self.buffer_size
+
+
+def batch_verifier(fn: Callable[[np.ndarray, np.ndarray], np.ndarray]):
+    """Wrap ``fn(arena_u8, descs) -> results(RESULT_DTYPE)`` as a cts_batch_verifier hook."""
+
+    def _cb(ctx, arena, arena_bytes, descs, n, results):
+        try:
+            a = np.ctypeslib.as_array((ctypes.c_uint8 * max(int(arena_bytes), 1)).from_address(arena))[:arena_bytes]
+            d = np.frombuffer((ctypes.c_uint8 * (24 * n)).from_address(descs), dtype=DESC_DTYPE, count=n).copy()
+            r = fn(np.ascontiguousarray(a), d)
+            ctypes.memmove(ctypes.cast(results, ctypes.c_void_p).value, r.astype(RESULT_DTYPE).tobytes(), 12 * n)
+            return 0
+        except Exception:  # pragma: no cover - reported as a failed verify call
+            return -1
+
+    return A.BATCH_VERIFIER(_cb)
+
+
+class IoPattern:
+    """One connection's ctsIoPattern (MakeIoPattern, ctsIOPattern.cpp:97-124)."""
+
+    def __init__(self, config: PatternConfig, engine=None, verifier=None):
+        self.config = config
+        self._cfg = config.to_c()
+        h = ctypes.c_void_p()
+        check("cts_io_pattern_create",
+              lib().cts_io_pattern_create(ctypes.byref(self._cfg), None if engine is None else engine._h,
+                                          ctypes.byref(h)))
+        self._h = h
+        self._hook = None
+        if verifier is not None:
+            self._hook = verifier if isinstance(verifier, A.BATCH_VERIFIER) else batch_verifier(verifier)
+            check("cts_io_pattern_set_verifier", lib().cts_io_pattern_set_verifier(self._h, self._hook, None))
+
+    MakeIoPattern = classmethod(lambda cls, config, engine=None, verifier=None: cls(config, engine, verifier))
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None and self._h.value:
+            lib().cts_io_pattern_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- the boundary (ctsIOPattern.h:143-144) -------------------------------
+    def InitiateIo(self) -> A.CtsTask:
+        t = A.CtsTask()
+        check("cts_io_pattern_initiate_io", lib().cts_io_pattern_initiate_io(self._h, ctypes.byref(t)))
+        return t
+
+    def CompleteIo(self, task: A.CtsTask, current_transfer: int, status_code: int = 0) -> int:
+        rc = lib().cts_io_pattern_complete_io(self._h, ctypes.byref(task), current_transfer, status_code)
+        if rc < 0:
+            raise CtsError("cts_io_pattern_complete_io", rc)
+        return rc
+
+    def GetLastPatternError(self) -> int:
+        return int(lib().cts_io_pattern_last_error(self._h))
+
+    def Flush(self) -> int:
+        rc = lib().cts_io_pattern_flush(self._h)
+        if rc < 0:
+            raise CtsError("cts_io_pattern_flush", rc)
+        return rc
+
+    def stats(self) -> dict:
+        s = A.CtsPatternStats()
+        check("cts_io_pattern_get_stats", lib().cts_io_pattern_get_stats(self._h, ctypes.byref(s)))
+        return s.as_dict()
+
+    def failure_message(self) -> str:
+        buf = ctypes.create_string_buffer(512)
+        n = lib().cts_io_pattern_failure_message(self._h, buf, 512)
+        return buf.value.decode() if n else ""
+
+    def fail_fast_reason(self) -> Optional[str]:
+        r = lib().cts_io_pattern_fail_fast_reason(self._h)
+        return r.decode() if r else None
+
+    def connection_id(self) -> str:
+        return lib().cts_io_pattern_connection_id(self._h).decode()
+
+    # ---- helpers the tests use to "simulate the wire" ---------------------------
+    @staticmethod
+    def AccessSharedBuffer() -> int:
+        """g_senderSharedBuffer address (ctsIOPattern.cpp:126-131)."""
+        return int(lib().cts_shared_buffer() or 0)
+
+    @staticmethod
+    def write_task_buffer(task: A.CtsTask, data: bytes, offset: int = 0) -> None:
+        ctypes.memmove(task.buffer + task.buffer_offset + offset, data, len(data))
+
+    @staticmethod
+    def read_task_buffer(task: A.CtsTask, n: int, offset: int = 0) -> bytes:
+        return ctypes.string_at(task.buffer + task.buffer_offset + offset, n)
+
+    @staticmethod
+    def recv_from_wire(task: A.CtsTask, nbytes: int) -> None:
+        """memcpy(task.m_buffer, AccessSharedBuffer() + task.m_expectedPatternOffset, n)
+        — the MSTest convention (ctsIOPatternUnitTest_Server.cpp:295)."""
+        ctypes.memmove(task.buffer + task.buffer_offset, IoPattern.AccessSharedBuffer() + task.expected_pattern_offset,
+                       nbytes)
+
+
+def shared_buffer_init(engine, max_buffer_size: int) -> None:
+    check("cts_shared_buffer_init", lib().cts_shared_buffer_init(engine._h, max_buffer_size))
+
+
+def shared_buffer_attach(buf: np.ndarray) -> None:
+    """Harnesses without a device: use caller-owned bytes as g_senderSharedBuffer (keep buf alive)."""
+    check("cts_shared_buffer_attach", lib().cts_shared_buffer_attach(buf.ctypes.data, buf.nbytes))
+
+
+def shared_buffer_release() -> None:
+    lib().cts_shared_buffer_release()
+
+
+def status_details() -> dict:
+    s = A.CtsStatusDetails()
+    check("cts_status_details_read", lib().cts_status_details_read(ctypes.byref(s)))
+    return {"bytes_sent": s.bytes_sent, "bytes_recv": s.bytes_recv, "data_errors": s.data_errors}
+
+
+def status_details_reset() -> None:
+    lib().cts_status_details_reset()

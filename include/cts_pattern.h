@@ -1,0 +1,230 @@
+/*
+ * cts_pattern.h — C ABI of the host-side ctsIoPattern mirror: the caller of the
+ * GPU fill/verify engine (include/cts_engine.h).
+ *
+ * The IO functors of the reference (ctsSendRecvIocp.cpp:97,243,368;
+ * ctsRioIocp.cpp:617,687,705,715,775; ctsReadWriteIocp.cpp:79,144,238) drive a
+ * connection through exactly two calls on its pattern object:
+ *
+ *   ctsTask     ctsIoPattern::InitiateIo()                               ctsIOPattern.h:143
+ *   ctsIoStatus ctsIoPattern::CompleteIo(task, currentTransfer, status)  ctsIOPattern.h:144
+ *
+ * plus the factory MakeIoPattern (ctsIOPattern.cpp:97-124), GetLastPatternError
+ * (ctsIOPattern.h:126-129) and AccessSharedBuffer (ctsIOPattern.cpp:126-131,
+ * which the reference's own tests use to simulate the wire). This header
+ * exports those calls with the same argument meaning; the bodies restate
+ * ctsIOPattern.cpp:219-743 and ctsIOPatternState.hpp:57-504 in C++ and route
+ * the two hot-path pieces to the GPU:
+ *
+ *   g_senderSharedBuffer (InitOnceIoPatternCallback, ctsIOPattern.cpp:52-90)
+ *       -> cts_shared_buffer_init: the gfx950 fill kernel writes it;
+ *   VerifyBuffer (ctsIOPattern.cpp:745-775)
+ *       -> the gfx950 verify kernel, on the pattern's pinned, device-mapped
+ *          recv buffers (zero copy), either per completion (CTS_VERIFY_SYNC,
+ *          the reference's timing) or batched (CTS_VERIFY_DEFERRED, §8f-1 of
+ *          see cts_io_pattern_flush).
+ *
+ * Configuration that the reference reads from ctsConfig::g_configSettings and
+ * the Get*Size() accessors (ctsConfig.h:370-462, ctsConfig.cpp:4679-4698) is
+ * passed explicitly in cts_pattern_config.
+ *
+ * Error conventions: the reference's entry points are noexcept and FAIL_FAST
+ * on internal inconsistency. Here every call returns normally; an internal
+ * inconsistency latches CTS_PATTERN_E_FAIL_FAST on the pattern (readable with
+ * cts_io_pattern_fail_fast_reason) and CompleteIo returns CTS_IO_FAILED.
+ * Rate limiting (TcpBytesPerSecond) and burst delays are not part of the
+ * data-integrity path and are not restated: time offsets are always 0.
+ */
+#ifndef CTS_PATTERN_H
+#define CTS_PATTERN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "cts_engine.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ctsTaskAction (ctsIOTask.hpp:27-36) */
+typedef enum cts_task_action {
+    CTS_TASK_NONE = 0,
+    CTS_TASK_SEND = 1,
+    CTS_TASK_RECV = 2,
+    CTS_TASK_GRACEFUL_SHUTDOWN = 3,
+    CTS_TASK_HARD_SHUTDOWN = 4,
+    CTS_TASK_ABORT = 5,
+    CTS_TASK_FATAL_ABORT = 6
+} cts_task_action;
+
+/* ctsTask::BufferType (ctsIOTask.hpp:47-55) */
+typedef enum cts_buffer_type {
+    CTS_BUFFER_NULL = 0,
+    CTS_BUFFER_TCP_CONNECTION_ID = 1,
+    CTS_BUFFER_UDP_CONNECTION_ID = 2,
+    CTS_BUFFER_COMPLETION_MESSAGE = 3,
+    CTS_BUFFER_STATIC = 4,
+    CTS_BUFFER_DYNAMIC = 5
+} cts_buffer_type;
+
+/* ctsTask (ctsIOTask.hpp:37-60), RIO_BUFFERID as a uint64 (0 = RIO_INVALID_BUFFERID). */
+typedef struct cts_task {
+    int64_t time_offset_ms;           /* m_timeOffsetMilliseconds */
+    uint64_t rio_buffer_id;           /* m_rioBufferid */
+    char* buffer;                     /* m_buffer */
+    uint32_t buffer_length;           /* m_bufferLength */
+    uint32_t buffer_offset;           /* m_bufferOffset */
+    uint32_t expected_pattern_offset; /* m_expectedPatternOffset */
+    uint8_t io_action;                /* m_ioAction (cts_task_action) */
+    uint8_t buffer_type;              /* m_bufferType (cts_buffer_type) */
+    uint8_t track_io;                 /* m_trackIo */
+    uint8_t reserved;
+} cts_task;                           /* 40 bytes */
+
+/* ctsIoStatus (ctsIOPattern.h:38-43) */
+typedef enum cts_io_status { CTS_IO_CONTINUE = 0, CTS_IO_COMPLETED = 1, CTS_IO_FAILED = 2 } cts_io_status;
+
+/* Protocol error codes (ctsIOPattern.h:46-50) */
+#define CTS_STATUS_IO_RUNNING 2147483647u                   /* c_statusIoRunning = MAXINT */
+#define CTS_STATUS_ERROR_NOT_ALL_DATA_TRANSFERRED 2147483646u /* MAXINT - 1 */
+#define CTS_STATUS_ERROR_TOO_MUCH_DATA_TRANSFERRED 2147483645u /* MAXINT - 2 */
+/* CTS_STATUS_ERROR_DATA_DID_NOT_MATCH_BIT_PATTERN (MAXINT - 3) is in cts_engine.h */
+/* Not in the reference: the latched stand-in for a FAIL_FAST process abort. */
+#define CTS_PATTERN_E_FAIL_FAST 2147483640u
+
+/* ctsStatistics::ConnectionIdLength = 36 + 1 (ctsStatistics.hpp:36) */
+#define CTS_CONNECTION_ID_LENGTH 37u
+/* c_completionMessage "DONE" / c_completionMessageSize (ctsIOPatternState.hpp:24-25) */
+#define CTS_COMPLETION_MESSAGE_SIZE 4u
+
+typedef enum cts_io_pattern_type { /* ctsConfig::IoPatternType */
+    CTS_PATTERN_PUSH = 1,
+    CTS_PATTERN_PULL = 2,
+    CTS_PATTERN_PUSHPULL = 3,
+    CTS_PATTERN_DUPLEX = 4
+} cts_io_pattern_type;
+
+typedef enum cts_protocol { CTS_PROTOCOL_TCP = 1, CTS_PROTOCOL_UDP = 2 } cts_protocol;
+typedef enum cts_tcp_shutdown { CTS_SHUTDOWN_GRACEFUL = 1, CTS_SHUTDOWN_HARD = 2 } cts_tcp_shutdown;
+
+typedef enum cts_verify_mode {
+    /* VerifyBuffer runs inside every CompleteIo, as in the reference. */
+    CTS_VERIFY_SYNC = 0,
+    /* Verified recv completions are queued and checked in batches (one kernel
+     * launch per batch); see cts_io_pattern_flush for the exactness contract. */
+    CTS_VERIFY_DEFERRED = 1
+} cts_verify_mode;
+
+typedef struct cts_pattern_config {
+    uint32_t io_pattern;        /* cts_io_pattern_type      (g_configSettings->IoPattern) */
+    uint32_t protocol;          /* cts_protocol             (->Protocol) */
+    uint32_t listening;         /* ctsConfig::IsListening(): 1 = server */
+    uint32_t verify_buffers;    /* ->ShouldVerifyBuffers (-verify:data) */
+    uint32_t use_shared_buffer; /* ->UseSharedBuffer */
+    uint32_t pre_post_recvs;    /* ->PrePostRecvs */
+    uint32_t pre_post_sends;    /* ->PrePostSends (0 = rely on the ideal send backlog) */
+    uint32_t buffer_size_low;   /* GetBufferSize(): fixed size, or the low end of -buffer:[lo,hi] */
+    uint32_t buffer_size_high;  /* 0 = fixed; else GetBufferSize() draws uniformly in [lo, hi] */
+    uint32_t push_bytes;        /* ->PushBytes (PushPull) */
+    uint32_t pull_bytes;        /* ->PullBytes (PushPull) */
+    uint32_t tcp_shutdown;      /* cts_tcp_shutdown (GetShutdownType()) */
+    uint64_t transfer_size;     /* GetTransferSize() */
+    uint64_t random_seed;       /* seed of the -buffer:[lo,hi] draw (reference: random_device) */
+    uint32_t verify_mode;       /* cts_verify_mode */
+    uint32_t batch_buffers;     /* DEFERRED: max queued buffers per batch (0 = 1024) */
+    uint64_t batch_bytes;       /* DEFERRED: staging arena bytes (0 = 64 MiB) */
+} cts_pattern_config;
+
+/* Per-connection statistics (ctsTcpStatistics, ctsStatistics.hpp:316-373) and
+ * the verify bookkeeping of this pattern. */
+typedef struct cts_pattern_stats {
+    uint64_t bytes_sent;          /* m_statistics.m_bytesSent */
+    uint64_t bytes_recv;          /* m_statistics.m_bytesRecv */
+    uint64_t buffers_verified;    /* VerifyBuffer calls that completed */
+    uint64_t bytes_verified;      /* sum of their transferred bytes */
+    uint64_t buffers_failed;      /* verify failures (0 or 1 in SYNC mode: the first fails the connection) */
+    uint64_t bytes_recv_at_failure; /* DEFERRED: m_bytesRecv as it stood right after the failing completion */
+    uint32_t recv_pattern_offset; /* m_recvPatternOffset */
+    uint32_t send_pattern_offset; /* m_sendPatternOffset */
+    uint32_t last_error;          /* GetLastPatternError() */
+    uint32_t queued;              /* DEFERRED: buffers waiting for the next batch */
+    /* first verify failure (ctsIOPattern.cpp:761-772 prints these) */
+    uint32_t fail_length;         /* transferred bytes of the failing buffer */
+    uint32_t fail_offset;         /* lengthMatched = RtlCompareMemory(...) */
+    uint8_t fail_expected;        /* patternBuffer[lengthMatched] */
+    uint8_t fail_actual;          /* received byte at lengthMatched */
+    uint8_t has_failure;
+    uint8_t reserved;
+    uint32_t fail_completion;     /* index of the failing recv completion (0-based) */
+} cts_pattern_stats;
+
+/* Batch verifier hook: verify n buffers of a host arena (results[i] per
+ * descs[i], RtlCompareMemory semantics). Return 0 on success. When a pattern has
+ * a hook it is used instead of the engine (test harnesses: the reference's own
+ * tests replace ctsConfig by link-time fakes in the same way). */
+typedef int (*cts_batch_verifier)(void* ctx, const uint8_t* host_arena, uint64_t arena_bytes,
+                                  const cts_buf_desc* descs, uint32_t n, cts_verify_result* results);
+
+typedef struct cts_io_pattern cts_io_pattern;
+
+/* ---- g_senderSharedBuffer (process-wide, InitOnceIoPatternCallback) ------ */
+/* Materialise the sender buffer (65536 + max_buffer_size bytes) in pinned,
+ * device-mapped host memory with the gfx950 fill kernel. Idempotent for a
+ * size <= the current one. */
+int cts_shared_buffer_init(cts_engine* engine, uint32_t max_buffer_size);
+/* Use caller-owned bytes as the sender buffer (harnesses without a device). */
+int cts_shared_buffer_attach(const void* host, uint64_t bytes);
+/* AccessSharedBuffer (ctsIOPattern.cpp:126-131): NULL until init/attach. */
+char* cts_shared_buffer(void);
+uint64_t cts_shared_buffer_bytes(void);
+void cts_shared_buffer_release(void);
+
+/* ---- pattern lifetime (MakeIoPattern, ctsIOPattern.cpp:97-124) ------------ */
+/* engine may be NULL only when verify_buffers == 0 or a batch verifier is set
+ * with cts_io_pattern_set_verifier before the first CompleteIo. */
+int cts_io_pattern_create(const cts_pattern_config* config, cts_engine* engine, cts_io_pattern** out);
+int cts_io_pattern_destroy(cts_io_pattern* pattern);
+int cts_io_pattern_set_verifier(cts_io_pattern* pattern, cts_batch_verifier fn, void* ctx);
+
+/* ---- the boundary ---------------------------------------------------------- */
+int cts_io_pattern_initiate_io(cts_io_pattern* pattern, cts_task* out_task);
+/* Returns a cts_io_status (>= 0) or a negative cts_status on a bad argument /
+ * device error. */
+int cts_io_pattern_complete_io(cts_io_pattern* pattern, const cts_task* task, uint32_t current_transfer,
+                               uint32_t status_code);
+uint32_t cts_io_pattern_last_error(const cts_io_pattern* pattern);
+/* DEFERRED mode: verify every queued buffer now (one kernel launch) and apply
+ * the outcome as the reference would have at the first failing completion:
+ * latch CTS_STATUS_ERROR_DATA_DID_NOT_MATCH_BIT_PATTERN and record its offset,
+ * expected and actual bytes and the recv byte count at that completion.
+ * CompleteIo flushes by itself before any completion that is not a plain
+ * in-transfer tracked send/recv (connection id, completion message, FIN,
+ * a failed IO, the last bytes of the transfer) and when the batch is full, so
+ * the connection's final status is exact; completions between a failing
+ * buffer and its flush return CTS_IO_CONTINUE where the reference would have
+ * returned CTS_IO_FAILED. Returns the current cts_io_status. */
+int cts_io_pattern_flush(cts_io_pattern* pattern);
+int cts_io_pattern_get_stats(const cts_io_pattern* pattern, cts_pattern_stats* out);
+/* The message ctsConfig::PrintErrorInfo receives on a verify failure
+ * (ctsIOPattern.cpp:761-772, bytes printed as sign-extended char through %x).
+ * Returns the length written (0 if no failure). */
+int cts_io_pattern_failure_message(const cts_io_pattern* pattern, char* buf, uint32_t buf_len);
+const char* cts_io_pattern_fail_fast_reason(const cts_io_pattern* pattern);
+/* GetConnectionIdentifier(): the 36-char id + NUL (servers generate it). */
+const char* cts_io_pattern_connection_id(cts_io_pattern* pattern);
+
+/* ---- process-wide status counters (TcpStatusDetails, ctsConfig.h:415-417) ---- */
+typedef struct cts_status_details {
+    uint64_t bytes_sent;        /* TcpStatusDetails.m_bytesSent */
+    uint64_t bytes_recv;        /* TcpStatusDetails.m_bytesRecv */
+    uint64_t data_errors;       /* patterns that latched DATA_DID_NOT_MATCH_BIT_PATTERN */
+} cts_status_details;
+int cts_status_details_read(cts_status_details* out);
+void cts_status_details_reset(void);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+#endif /* CTS_PATTERN_H */

@@ -120,3 +120,46 @@ def test_engine_create_without_device_fails_loudly():
 
     with pytest.raises(CtsError):
         Engine(0)
+
+
+def test_pattern_struct_layouts_match_c():
+    """cts_task / cts_pattern_config / cts_pattern_stats (include/cts_pattern.h) vs the ctypes mirrors."""
+    import ctypes
+    import tempfile
+
+    from ctstraffic_amd import _pattern_abi as A
+
+    probe = r"""
+#include <stdio.h>
+#include <stddef.h>
+#include "cts_pattern.h"
+#define O(T,f) printf("%s %zu\n", #f, offsetof(T,f))
+int main(void){
+ printf("sizeof %zu %zu %zu %zu\n", sizeof(cts_task), sizeof(cts_pattern_config), sizeof(cts_pattern_stats),
+        sizeof(cts_status_details));
+ O(cts_task,buffer); O(cts_task,buffer_length); O(cts_task,expected_pattern_offset); O(cts_task,io_action);
+ O(cts_task,track_io);
+ O(cts_pattern_config,transfer_size); O(cts_pattern_config,random_seed); O(cts_pattern_config,verify_mode);
+ O(cts_pattern_config,batch_bytes);
+ O(cts_pattern_stats,recv_pattern_offset); O(cts_pattern_stats,fail_expected); O(cts_pattern_stats,fail_completion);
+ return 0; }
+"""
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "p.c")
+        open(c, "w").write(probe)
+        exe = os.path.join(d, "p")
+        subprocess.run(["gcc", "-std=c11", "-I", INCLUDE, c, "-o", exe], check=True)
+        lines = subprocess.run([exe], capture_output=True, text=True, check=True).stdout.split("\n")
+    sizes = list(map(int, lines[0].split()[1:]))
+    assert sizes == [ctypes.sizeof(A.CtsTask), ctypes.sizeof(A.CtsPatternConfig), ctypes.sizeof(A.CtsPatternStats),
+                     ctypes.sizeof(A.CtsStatusDetails)]
+    structs = {"buffer": A.CtsTask, "buffer_length": A.CtsTask, "expected_pattern_offset": A.CtsTask,
+               "io_action": A.CtsTask, "track_io": A.CtsTask, "transfer_size": A.CtsPatternConfig,
+               "random_seed": A.CtsPatternConfig, "verify_mode": A.CtsPatternConfig,
+               "batch_bytes": A.CtsPatternConfig, "recv_pattern_offset": A.CtsPatternStats,
+               "fail_expected": A.CtsPatternStats, "fail_completion": A.CtsPatternStats}
+    for line in lines[1:]:
+        if not line.strip():
+            continue
+        f, off = line.split()
+        assert getattr(structs[f], f).offset == int(off), f

@@ -1,0 +1,554 @@
+"""The ctsIoPattern mirror (include/cts_pattern.h) replaying the reference's own
+MSTest scenarios (MSTest/ctsIOPatternUnitTest_{Server,Client,Duplex}), plus
+randomized long streams with injected corruption.
+
+Each scenario runs against four backends:
+  cpu-sync / cpu-deferred : VerifyBuffer answered by the CPU oracle through the
+                            pattern's batch-verifier hook (the reference's tests
+                            replace ctsConfig by link-time fakes the same way);
+  gpu-sync / gpu-deferred : VerifyBuffer on the gfx950 verify kernel (zero-copy
+                            over the pattern's pinned recv buffers), sender
+                            buffer written by the gfx950 fill kernel.
+Assertions follow the reference tests line by line (file:line cited per test).
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+import oracle
+from ctstraffic_amd import _pattern_abi as A
+from ctstraffic_amd.pattern import IoPattern, PatternConfig, shared_buffer_attach
+
+ContinueIo, CompletedIo, FailedIo = A.IO_CONTINUE, A.IO_COMPLETED, A.IO_FAILED
+Send, Recv, NoneAction = A.TASK_SEND, A.TASK_RECV, A.TASK_NONE
+ConnectionIdLength = A.CONNECTION_ID_LENGTH
+g_TestBufferLength = 4  # completion message "DONE"
+g_TestRecvBufferLength = 1024
+WSAECONNRESET = 10054
+
+BACKENDS = [
+    pytest.param(("cpu", A.VERIFY_SYNC), id="cpu-sync"),
+    pytest.param(("cpu", A.VERIFY_DEFERRED), id="cpu-deferred"),
+    pytest.param(("gpu", A.VERIFY_SYNC), id="gpu-sync", marks=pytest.mark.gpu),
+    pytest.param(("gpu", A.VERIFY_DEFERRED), id="gpu-deferred", marks=pytest.mark.gpu),
+]
+
+_SENDER = oracle.sender_buffer(4 * 65536)  # g_senderSharedBuffer stand-in for device-less harnesses
+
+
+def _oracle_verifier(arena, descs):
+    return oracle.verify_batch(arena, descs)[0]
+
+
+@pytest.fixture(params=BACKENDS)
+def make(request):
+    kind, mode = request.param
+    made = []
+
+    def factory(**kw):
+        kw.setdefault("verify_mode", mode)
+        cfg = PatternConfig(**kw)
+        if kind == "cpu":
+            shared_buffer_attach(_SENDER)
+            p = IoPattern.MakeIoPattern(cfg, None, verifier=_oracle_verifier)
+        else:
+            eng = request.getfixturevalue("engine")
+            p = IoPattern.MakeIoPattern(cfg, eng)
+        made.append(p)
+        return p
+
+    factory.kind, factory.mode = kind, mode
+    yield factory
+    for p in made:
+        p.close()
+
+
+def recv_correct(task, n=None):
+    IoPattern.recv_from_wire(task, task.buffer_length if n is None else n)
+
+
+def zero(task):
+    ctypes.memset(task.buffer + task.buffer_offset, 0, task.buffer_length)
+
+
+def server_defaults(**kw):  # ctsIOPatternUnitTest_Server.cpp:250-274 SetTestBaseClassDefaults(Server)
+    d = dict(io_pattern=A.PATTERN_PUSH, listening=True, verify_buffers=True, pre_post_recvs=1, pre_post_sends=1,
+             buffer_size=1024, transfer_size=10)
+    d.update(kw)
+    return d
+
+
+def client_defaults(**kw):
+    d = server_defaults(listening=False)
+    d.update(kw)
+    return d
+
+
+# ---- ctsIOPatternUnitTest_Server.cpp ---------------------------------------------------------------
+def test_TestBaseClass_SingleSuccessfulRecv_Server(make):  # :280-312
+    p = make(**server_defaults())
+    t = p.InitiateIo()
+    assert (t.buffer_length, t.io_action) == (ConnectionIdLength, Send)
+    assert p.CompleteIo(t, ConnectionIdLength, 0) == ContinueIo
+    t = p.InitiateIo()
+    assert (t.buffer_length, t.io_action) == (10, Recv)
+    recv_correct(t)
+    assert p.CompleteIo(t, 10, 0) == ContinueIo
+    t = p.InitiateIo()
+    assert (t.io_action, t.buffer_length) == (Send, g_TestBufferLength)
+    assert IoPattern.read_task_buffer(t, 4) == b"DONE"
+    assert p.CompleteIo(t, 4, 0) == ContinueIo
+    t = p.InitiateIo()
+    assert t.io_action == Recv
+    assert p.CompleteIo(t, 0, 0) == CompletedIo
+    assert p.GetLastPatternError() == 0
+    s = p.stats()
+    assert s["buffers_verified"] == 1 and s["buffers_failed"] == 0 and s["bytes_recv"] == 10
+
+
+def test_TestBaseClass_FailSendingConnectionId(make):  # :314-324
+    p = make(**server_defaults())
+    t = p.InitiateIo()
+    assert (t.buffer_length, t.io_action) == (ConnectionIdLength, Send)
+    assert p.CompleteIo(t, 0, 1) == FailedIo
+    assert p.GetLastPatternError() == 1
+
+
+def test_TestBaseClass_FailRecv(make):  # :326-342
+    p = make(**server_defaults())
+    t = p.InitiateIo()
+    assert p.CompleteIo(t, ConnectionIdLength, 0) == ContinueIo
+    t = p.InitiateIo()
+    assert (t.buffer_length, t.io_action) == (10, Recv)
+    assert p.CompleteIo(t, 10, 1) == FailedIo
+    assert p.GetLastPatternError() == 1
+
+
+def _server_to_fin(p):
+    t = p.InitiateIo()
+    assert p.CompleteIo(t, ConnectionIdLength, 0) == ContinueIo
+    t = p.InitiateIo()
+    recv_correct(t)
+    assert p.CompleteIo(t, 10, 0) == ContinueIo
+    t = p.InitiateIo()
+    assert t.io_action == Send and IoPattern.read_task_buffer(t, 4) == b"DONE"
+    assert p.CompleteIo(t, 4, 0) == ContinueIo
+    t = p.InitiateIo()
+    assert t.io_action == Recv
+    return t
+
+
+def test_TestServerBaseClass_FailFINAfterRecv(make):  # :344-377
+    p = make(**server_defaults())
+    t = _server_to_fin(p)
+    assert p.CompleteIo(t, 0, 1) == FailedIo
+    assert p.GetLastPatternError() == 1
+
+
+def test_TestServerBaseClass_TooManyBytesOnFINAfterRecv(make):  # :414-447
+    p = make(**server_defaults())
+    t = _server_to_fin(p)
+    assert p.CompleteIo(t, 1, 0) == FailedIo
+    assert p.GetLastPatternError() == A.STATUS_ERROR_TOO_MUCH_DATA_TRANSFERRED
+
+
+def test_TestBaseClass_InvalidBytesOnRecv(make):  # :449-467
+    p = make(**server_defaults())
+    t = p.InitiateIo()
+    assert p.CompleteIo(t, ConnectionIdLength, 0) == ContinueIo
+    t = p.InitiateIo()
+    assert (t.buffer_length, t.io_action) == (10, Recv)
+    zero(t)  # ::ZeroMemory(test_task.m_buffer, test_task.m_bufferLength)
+    assert p.CompleteIo(t, 10, 0) == FailedIo
+    assert p.GetLastPatternError() == A.STATUS_ERROR_DATA_DID_NOT_MATCH_BIT_PATTERN
+    s = p.stats()
+    # P = 00 00 01 00 02 00 ...: the zeroed buffer first differs at byte 2 (expected 0x01, got 0x00)
+    assert (s["has_failure"], s["fail_offset"], s["fail_expected"], s["fail_actual"]) == (1, 2, 1, 0)
+    assert s["bytes_recv"] == 10  # a corrupt buffer is still counted (ctsIOPattern.cpp:505-521)
+    assert "offset (2)" in p.failure_message() and "'0x1' didn't match '0x0'" in p.failure_message()
+
+
+def _push_server_loop(p, n, post, complete):
+    t = p.InitiateIo()
+    assert (t.buffer_length, t.io_action) == (ConnectionIdLength, Send)
+    assert p.CompleteIo(t, ConnectionIdLength, 0) == ContinueIo
+    offsets = []
+    for _ in range(n):
+        t = p.InitiateIo()
+        assert (t.buffer_length, t.io_action) == (post, Recv)
+        assert p.InitiateIo().io_action == NoneAction
+        offsets.append(t.expected_pattern_offset)
+        recv_correct(t)
+        assert p.CompleteIo(t, complete, 0) == ContinueIo
+    return offsets
+
+
+def _server_finish(p):
+    t = p.InitiateIo()
+    assert (t.io_action, t.buffer_length) == (Send, g_TestBufferLength)
+    assert p.InitiateIo().io_action == NoneAction
+    assert IoPattern.read_task_buffer(t, 4) == b"DONE"
+    assert p.CompleteIo(t, 4, 0) == ContinueIo
+    t = p.InitiateIo()
+    assert t.io_action == Recv
+    assert p.InitiateIo().io_action == NoneAction
+    assert p.CompleteIo(t, 0, 0) == CompletedIo
+
+
+def test_PushServer_VerifyingBuffersNotUsingSharedBuffer(make):  # :609-667
+    p = make(**server_defaults(buffer_size=1024, transfer_size=1024 * 10))
+    offs = _push_server_loop(p, 10, 1024, 1024)
+    assert offs == [1024 * i for i in range(10)]  # m_recvPatternOffset advances by completed bytes
+    _server_finish(p)
+    s = p.stats()
+    assert s["buffers_verified"] == 10 and s["bytes_verified"] == 10240 and s["recv_pattern_offset"] == 10240
+
+
+def test_PushServer_VerifyingBuffersNotUsingSharedBuffer_SmallRecvs(make):  # :669-740
+    p = make(**server_defaults(buffer_size=2048, transfer_size=1024 * 10))
+    offs = _push_server_loop(p, 9, 2048, 1024)
+    assert offs == [1024 * i for i in range(9)]
+    t = p.InitiateIo()  # the final recv is just 1024 bytes
+    assert (t.buffer_length, t.io_action, t.expected_pattern_offset) == (1024, Recv, 9 * 1024)
+    assert p.InitiateIo().io_action == NoneAction
+    recv_correct(t)
+    assert p.CompleteIo(t, 1024, 0) == ContinueIo
+    _server_finish(p)
+    assert p.GetLastPatternError() == 0
+
+
+def test_PushServer_NotVerifyingBuffersUsingSharedBuffer(make):  # :742-808
+    p = make(**server_defaults(buffer_size=1024, transfer_size=1024 * 10, verify_buffers=False,
+                               use_shared_buffer=True))
+    t = p.InitiateIo()
+    assert p.CompleteIo(t, ConnectionIdLength, 0) == ContinueIo
+    for _ in range(10):
+        t = p.InitiateIo()
+        assert (t.buffer_length, t.io_action) == (1024, Recv)
+        zero(t)  # not verifying: garbage is fine
+        assert p.CompleteIo(t, 1024, 0) == ContinueIo
+    _server_finish(p)
+    assert p.stats()["buffers_verified"] == 0
+
+
+def test_PullServer_VerifyingBuffersNotUsingSharedBuffer(make):  # :868-924
+    p = make(**server_defaults(io_pattern=A.PATTERN_PULL, buffer_size=1024, transfer_size=1024 * 10))
+    t = p.InitiateIo()
+    assert p.CompleteIo(t, ConnectionIdLength, 0) == ContinueIo
+    base = IoPattern.AccessSharedBuffer()
+    for i in range(10):
+        t = p.InitiateIo()
+        assert (t.buffer_length, t.io_action) == (1024, Send)
+        # Send tasks point into g_senderSharedBuffer at m_sendPatternOffset (ctsIOPattern.cpp:676-681)
+        assert t.buffer == base and t.buffer_offset == 1024 * i
+        assert p.InitiateIo().io_action == NoneAction
+        assert p.CompleteIo(t, 1024, 0) == ContinueIo
+    _server_finish(p)
+    assert p.stats()["send_pattern_offset"] == 10240 and p.stats()["bytes_sent"] == 10240
+
+
+# ---- ctsIOPatternUnitTest_Client.cpp ------------------------------------------------------------
+def test_TestBaseClass_SuccessfulSend(make):  # Client :280-313
+    p = make(**client_defaults())
+    t = p.InitiateIo()
+    assert (t.buffer_length, t.io_action) == (ConnectionIdLength, Recv)
+    assert p.CompleteIo(t, ConnectionIdLength, 0) == ContinueIo
+    t = p.InitiateIo()
+    assert (t.buffer_length, t.io_action) == (10, Send)
+    assert p.CompleteIo(t, 10, 0) == ContinueIo
+    t = p.InitiateIo()
+    assert (t.io_action, t.buffer_length) == (Recv, g_TestBufferLength)
+    assert p.CompleteIo(t, 4, 0) == ContinueIo
+    t = p.InitiateIo()
+    assert t.io_action == A.TASK_GRACEFUL_SHUTDOWN
+    assert p.CompleteIo(t, 0, 0) == ContinueIo
+    t = p.InitiateIo()
+    assert t.io_action == Recv
+    assert p.CompleteIo(t, 0, 0) == CompletedIo
+
+
+@pytest.mark.parametrize("shutdown", [A.SHUTDOWN_GRACEFUL, A.SHUTDOWN_HARD], ids=["Graceful", "Rude"])
+def test_PullClient_VerifyingBuffersNotUsingSharedBuffer_SmallRecvs(make, shutdown):  # Client :1662-1774
+    p = make(**client_defaults(io_pattern=A.PATTERN_PULL, buffer_size=2048, transfer_size=10240,
+                               tcp_shutdown=shutdown))
+    t = p.InitiateIo()
+    assert (t.buffer_length, t.io_action) == (ConnectionIdLength, Recv)
+    assert p.CompleteIo(t, ConnectionIdLength, 0) == ContinueIo
+    for i in range(9):
+        t = p.InitiateIo()
+        assert (t.buffer_length, t.io_action, t.expected_pattern_offset) == (2048, Recv, 1024 * i)
+        recv_correct(t)
+        assert p.CompleteIo(t, 1024, 0) == ContinueIo
+    t = p.InitiateIo()
+    assert (t.buffer_length, t.io_action) == (1024, Recv)
+    recv_correct(t)
+    assert p.CompleteIo(t, 1024, 0) == ContinueIo
+    t = p.InitiateIo()
+    assert (t.io_action, t.buffer_length) == (Recv, g_TestBufferLength)
+    assert p.CompleteIo(t, 4, 0) == ContinueIo
+    t = p.InitiateIo()
+    if shutdown == A.SHUTDOWN_GRACEFUL:
+        assert t.io_action == A.TASK_GRACEFUL_SHUTDOWN
+        assert p.CompleteIo(t, 0, 0) == ContinueIo
+        t = p.InitiateIo()
+        assert t.io_action == Recv
+        assert p.CompleteIo(t, 0, 0) == CompletedIo
+    else:
+        assert t.io_action == A.TASK_HARD_SHUTDOWN
+        assert p.CompleteIo(t, 0, 0) == CompletedIo
+    assert p.stats()["buffers_verified"] == 10
+
+
+def test_TestBaseClass_FailReceivingConnectionId(make):  # Client :482-492
+    p = make(**client_defaults())
+    t = p.InitiateIo()
+    assert p.CompleteIo(t, 0, 1) == FailedIo
+    assert p.GetLastPatternError() == 1
+
+
+# ---- ctsIOPatternUnitTest_Duplex.cpp --------------------------------------------------------------
+def duplex_defaults(role_server=False, **kw):  # :208-229 SetTestDuplexDefaults
+    d = dict(io_pattern=A.PATTERN_DUPLEX, listening=role_server, verify_buffers=True, pre_post_recvs=1,
+             pre_post_sends=1, buffer_size=1024, transfer_size=20)
+    d.update(kw)
+    return d
+
+
+def _complete_connection_id(p, server):
+    t = p.InitiateIo()
+    assert (t.buffer_length, t.io_action) == (ConnectionIdLength, Send if server else Recv)
+    assert p.CompleteIo(t, ConnectionIdLength, 0) == ContinueIo
+
+
+def _pended_data_tasks(p):
+    r = p.InitiateIo()
+    assert (r.io_action, r.buffer_length) == (Recv, 10)
+    s = p.InitiateIo()
+    assert (s.io_action, s.buffer_length) == (Send, 10)
+    assert p.InitiateIo().io_action == NoneAction
+    return r, s
+
+
+def _complete_data_recv(p, t, n):
+    IoPattern.recv_from_wire(t, n)
+    return p.CompleteIo(t, n, 0)
+
+
+def _successful_shutdown(p, server, hard=False):
+    if server:
+        t = p.InitiateIo()
+        assert (t.io_action, t.buffer_length) == (Send, 4)
+        assert p.CompleteIo(t, 4, 0) == ContinueIo
+        t = p.InitiateIo()
+        assert t.io_action == Recv
+        assert p.CompleteIo(t, 0, 0) == CompletedIo
+        return
+    t = p.InitiateIo()
+    assert (t.io_action, t.buffer_length) == (Recv, 4)
+    assert p.CompleteIo(t, 4, 0) == ContinueIo
+    t = p.InitiateIo()
+    if hard:
+        assert t.io_action == A.TASK_HARD_SHUTDOWN
+        assert p.CompleteIo(t, 0, 0) == CompletedIo
+        return
+    assert t.io_action == A.TASK_GRACEFUL_SHUTDOWN
+    assert p.CompleteIo(t, 0, 0) == ContinueIo
+    t = p.InitiateIo()
+    assert t.io_action == Recv
+    assert p.CompleteIo(t, 0, 0) == CompletedIo
+
+
+@pytest.mark.parametrize("server,recv_first,hard", [(False, True, False), (False, False, False), (False, True, True),
+                                                    (True, False, False), (True, True, False)],
+                         ids=["Client_Graceful_RecvThenSend", "Client_Graceful_SendThenRecv", "Client_HardShutdown",
+                              "Server_Graceful_SendThenRecv", "Server_Graceful_RecvThenSend"])
+def test_Duplex_success_paths(make, server, recv_first, hard):  # :492-590
+    p = make(**duplex_defaults(server, tcp_shutdown=A.SHUTDOWN_HARD if hard else A.SHUTDOWN_GRACEFUL))
+    _complete_connection_id(p, server)
+    r, s = _pended_data_tasks(p)
+    if recv_first:
+        assert _complete_data_recv(p, r, 10) == ContinueIo
+        assert p.CompleteIo(s, 10, 0) == ContinueIo
+    else:
+        assert p.CompleteIo(s, 10, 0) == ContinueIo
+        assert _complete_data_recv(p, r, 10) == ContinueIo
+    _successful_shutdown(p, server, hard)
+    assert p.GetLastPatternError() == 0
+
+
+def test_Duplex_Client_PartialRecv_RepostsRemainder(make):  # :592-622
+    p = make(**duplex_defaults(False))
+    _complete_connection_id(p, False)
+    r = p.InitiateIo()
+    assert (r.io_action, r.buffer_length) == (Recv, 10)
+    s = p.InitiateIo()
+    assert (s.io_action, s.buffer_length) == (Send, 10)
+    assert _complete_data_recv(p, r, 4) == ContinueIo
+    rr = p.InitiateIo()
+    assert (rr.io_action, rr.buffer_length) == (Recv, 6)
+    assert rr.expected_pattern_offset == 4  # the unaligned phase the next buffer is verified at
+    assert p.CompleteIo(s, 10, 0) == ContinueIo
+    assert _complete_data_recv(p, rr, 6) == ContinueIo
+    _successful_shutdown(p, False)
+    assert p.GetLastPatternError() == 0
+    assert p.stats()["buffers_verified"] == 2
+
+
+def test_Duplex_Server_TolerateRstWhileAwaitingFin(make):  # :626-655
+    p = make(**duplex_defaults(True))
+    _complete_connection_id(p, True)
+    r, s = _pended_data_tasks(p)
+    assert _complete_data_recv(p, r, 10) == ContinueIo
+    assert p.CompleteIo(s, 10, 0) == ContinueIo
+    t = p.InitiateIo()
+    assert t.io_action == Send
+    assert p.CompleteIo(t, 4, 0) == ContinueIo
+    t = p.InitiateIo()
+    assert t.io_action == Recv
+    assert p.CompleteIo(t, 0, WSAECONNRESET) == CompletedIo
+    assert p.GetLastPatternError() == 0
+
+
+def test_Duplex_Client_FailDataRecv(make):  # :700-715
+    p = make(**duplex_defaults(False))
+    _complete_connection_id(p, False)
+    r, s = _pended_data_tasks(p)
+    assert p.CompleteIo(r, 0, 1) == FailedIo
+    assert p.GetLastPatternError() == 1
+
+
+def test_Duplex_Client_CorruptedRecv(make):
+    """Not an MSTest case: a corrupted Duplex recv fails the connection with the bit-pattern error."""
+    p = make(**duplex_defaults(False))
+    _complete_connection_id(p, False)
+    r, s = _pended_data_tasks(p)
+    IoPattern.recv_from_wire(r, 10)
+    IoPattern.write_task_buffer(r, b"\xff", 7)
+    assert p.CompleteIo(s, 10, 0) == ContinueIo
+    assert p.CompleteIo(r, 10, 0) == FailedIo
+    assert p.GetLastPatternError() == A.STATUS_ERROR_DATA_DID_NOT_MATCH_BIT_PATTERN
+    s = p.stats()
+    assert (s["fail_offset"], s["fail_expected"], s["fail_actual"]) == (7, 0, 0xFF)
+    assert "'0x0' didn't match '0xffffffff'" in p.failure_message()  # char through %x sign-extends
+
+
+@pytest.mark.parametrize("reverse", [False, True], ids=["InOrder", "ReverseOrder"])
+def test_Duplex_MultipleConcurrentSends(make, reverse):  # :1401-1553 (send offsets advance per created task)
+    p = make(**duplex_defaults(False, pre_post_sends=3, buffer_size=10, transfer_size=2 * 3 * 10))
+    _complete_connection_id(p, False)
+    r = p.InitiateIo()
+    assert (r.io_action, r.buffer_length) == (Recv, 10)
+    sends = [p.InitiateIo() for _ in range(3)]
+    assert [t.io_action for t in sends] == [Send] * 3
+    assert [t.buffer_offset for t in sends] == [0, 10, 20]
+    assert p.InitiateIo().io_action == NoneAction
+    for t in (sends[::-1] if reverse else sends):
+        assert p.CompleteIo(t, 10, 0) == ContinueIo
+    assert p.InitiateIo().io_action == NoneAction  # the send half is done; the recv is still pending
+    for i in range(3):
+        assert r.expected_pattern_offset == 10 * i
+        assert _complete_data_recv(p, r, 10) == ContinueIo
+        if i < 2:
+            r = p.InitiateIo()
+    _successful_shutdown(p, False)
+    assert p.GetLastPatternError() == 0
+
+
+# ---- configuration guards (ctsConfig.cpp:2169-2171, 3440-3446; ctsIOPattern.cpp:225-227) ----------
+def test_config_guards():
+    shared_buffer_attach(_SENDER)
+    from ctstraffic_amd import CtsError
+
+    with pytest.raises(CtsError):  # -PrePostRecvs > 1 requires -Verify:connection with TCP
+        IoPattern(PatternConfig(pre_post_recvs=2, verify_buffers=True, buffer_size=1024), verifier=_oracle_verifier)
+    with pytest.raises(CtsError):  # UseSharedBuffer && ShouldVerifyBuffers
+        IoPattern(PatternConfig(use_shared_buffer=True, verify_buffers=True, buffer_size=1024),
+                  verifier=_oracle_verifier)
+    with pytest.raises(CtsError):  # PrePostRecvs == 0
+        IoPattern(PatternConfig(pre_post_recvs=0, verify_buffers=False, buffer_size=1024))
+
+
+def test_no_verifier_fails_loudly():
+    """Without an engine or a hook a verifying pattern refuses to complete a data recv: the product
+    has no CPU verify path."""
+    shared_buffer_attach(_SENDER)
+    from ctstraffic_amd import CtsError
+
+    p = IoPattern(PatternConfig(**server_defaults()))
+    t = p.InitiateIo()
+    assert p.CompleteIo(t, ConnectionIdLength, 0) == ContinueIo
+    t = p.InitiateIo()
+    recv_correct(t)
+    with pytest.raises(CtsError):
+        p.CompleteIo(t, 10, 0)
+    p.close()
+
+
+# ---- randomized long streams: sync vs deferred vs the oracle ----------------------------------------
+def _expected_stream(lens, corrupt):
+    """Walk the completions with the oracle: (first failing completion, bytes_recv at it, result)."""
+    S = oracle.sender_buffer(65536 * 2)
+    off = 0
+    recv = 0
+    for i, n in enumerate(lens):
+        buf = S[off:off + n].copy()
+        if i in corrupt:
+            buf[corrupt[i][0]] ^= corrupt[i][1]
+        recv += n
+        r = oracle.verify_buffer(buf, 0, off, n)
+        if not r["pass"]:
+            return i, recv, r
+        off = (off + n) % 65536
+    return None, recv, None
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_random_push_server_stream(make, seed):
+    rng = np.random.default_rng(seed)
+    bufsize = int(rng.choice([1000, 4096, 65536]))
+    n = 300
+    lens = [int(x) for x in rng.integers(1, bufsize + 1, size=n)]
+    total = sum(lens)
+    corrupt = {}
+    if seed != 1:
+        k = int(rng.integers(5, n - 5))
+        corrupt[k] = (int(rng.integers(0, lens[k])), int(rng.integers(1, 256)))
+    p = make(**server_defaults(buffer_size=bufsize, transfer_size=total, batch_buffers=16))
+    t = p.InitiateIo()
+    assert p.CompleteIo(t, ConnectionIdLength, 0) == ContinueIo
+    statuses = []
+    for i, ln in enumerate(lens):
+        t = p.InitiateIo()
+        assert t.io_action == Recv
+        # the wire delivers fewer bytes than posted (partial completions shift the phase)
+        take = min(ln, t.buffer_length)
+        IoPattern.recv_from_wire(t, take)
+        if i in corrupt:
+            pos, x = corrupt[i]
+            pos = min(pos, take - 1)
+            corrupt[i] = (pos, x)
+            b = IoPattern.read_task_buffer(t, 1, pos)[0] ^ x
+            IoPattern.write_task_buffer(t, bytes([b]), pos)
+        lens[i] = take
+        st = p.CompleteIo(t, take, 0)
+        statuses.append(st)
+        if st == FailedIo:
+            break
+    flushed = p.Flush() if statuses[-1] != FailedIo else FailedIo  # drain a deferred queue
+    fail_at, recv_at, r = _expected_stream(lens[:len(statuses)], corrupt)
+    s = p.stats()
+    if fail_at is None:
+        assert all(x == ContinueIo for x in statuses[:-1])
+        assert s["has_failure"] == 0 and p.GetLastPatternError() == 2147483647
+        assert s["buffers_verified"] == len(statuses)
+        return
+    assert s["has_failure"] == 1 and s["fail_completion"] == fail_at
+    assert (s["fail_offset"], s["fail_expected"], s["fail_actual"]) == (r["first_mismatch"], r["expected"], r["actual"])
+    assert s["bytes_recv_at_failure"] == recv_at
+    assert p.GetLastPatternError() == A.STATUS_ERROR_DATA_DID_NOT_MATCH_BIT_PATTERN
+    if make.mode == A.VERIFY_SYNC:
+        assert statuses[-1] == FailedIo and len(statuses) == fail_at + 1
+    else:
+        # deferred: the failure surfaces at the end of its batch (within its batch of 16) or at the final flush
+        assert flushed == FailedIo and fail_at + 1 <= len(statuses) <= fail_at + 16

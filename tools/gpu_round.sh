@@ -1,0 +1,33 @@
+#!/bin/bash
+# One gpurun call: GPU parity tests, smoke, bench, rocprofv3 kernel-trace stats and
+# PMC HBM-traffic passes. Every GPU step has its own time limit; steps chain with &&
+# semantics (set -e), so nothing more runs on the GPU after a failure.
+#   usage (from this container):  gpurun --timeout 1100 -- bash tools/gpu_round.sh TAG
+set -euo pipefail
+TAG=${1:-r01}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+STEPS=${STEPS:-all}
+run() { echo "[$(date +%T)] $*" | tee -a "$OUT/steps.log"; }
+if [[ $STEPS == all || $STEPS == *tests* ]]; then
+  run pytest-gpu
+  timeout -k 10 400 python -m pytest tests -m gpu -x -q -p no:cacheprovider > "$OUT/pytest_gpu.log" 2>&1
+  run smoke
+  timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
+fi
+if [[ $STEPS == all || $STEPS == *bench* ]]; then
+  run bench
+  timeout -k 10 400 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
+fi
+if [[ $STEPS == all || $STEPS == *prof* ]]; then
+  run rocprof-kernel-trace
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -d "$OUT/prof_kt" -o run --output-format csv \
+    -- python3 bench.py --no-cpu-baseline --steps 200 --warmup 20 > "$OUT/prof_kt_bench.json" 2> "$OUT/prof_kt.err"
+  for ctr in FETCH_SIZE WRITE_SIZE TCC_EA0_RDREQ_sum; do
+    run rocprof-pmc $ctr
+    timeout -k 10 300 rocprofv3 --pmc $ctr --kernel-trace -T -d "$OUT/prof_pmc_$ctr" -o run --output-format csv \
+      -- python3 bench.py --no-cpu-baseline --steps 50 --warmup 5 > "$OUT/prof_pmc_$ctr.json" 2> "$OUT/prof_pmc_$ctr.err"
+  done
+fi
+run done
