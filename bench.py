@@ -42,20 +42,18 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extras", action="store_true", help="skip fill / datagram / host-path extras")
     p.add_argument("--extras-only", default="", help="comma list: fill,datagram,host")
+    p.add_argument("--no-graph", action="store_true", help="launch every step from the host (no HIP graph)")
     return p.parse_args()
-
-
-def dist_env():
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    return world, rank, local
 
 
 def main():
     args = parse()
-    world, rank, local = dist_env()
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     import torch
+
+    from ctstraffic_amd.distributed import dist_env
+
+    world, rank, local = dist_env()
     import torch.distributed as dist
 
     if not torch.cuda.is_available():
@@ -63,17 +61,17 @@ def main():
         sys.exit(2)
     torch.cuda.set_device(local)
     dev = "cuda:%d" % local
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device(dev))
-
-    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from ctstraffic_amd import Engine, workload as W
+    from ctstraffic_amd import distributed as D
+
+    if world > 1:
+        D.init("nccl", device=torch.device(dev))
 
     engine = Engine(local)
-    stream = torch.cuda.current_stream()
+    stream = torch.cuda.Stream()
 
     # ---- workload (per rank: weak scaling) --------------------------------------------------
+    # each rank verifies its own shard of connections (hash(conn) mod G): config 2's batch per GPU
     w = W.tcp_resident(n_buffers=args.buffers)
     R = max(1, args.arenas)
     arenas = []
@@ -91,46 +89,64 @@ def main():
         if world > 1:
             dist.barrier()
 
+    # ---- HIP graph of one rotation (R launches), replayed in the timed region ----------------
+    graph = None
+    if not args.no_graph:
+        for i in range(R):  # first launches outside capture (module load, allocator)
+            engine.verify(arenas[i], descs, max_length_hint=w.max_length, counters=counters, stream=stream)
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=stream):
+            for i in range(R):
+                engine.verify(arenas[i], descs, max_length_hint=w.max_length, counters=counters, stream=stream)
+        torch.cuda.synchronize()
+
+    def run_steps(k0, k):
+        """k verify steps starting at rotation index k0 (graph replays for whole rotations)."""
+        done = 0
+        with torch.cuda.stream(stream):
+            if graph is not None and k0 % R == 0:
+                for _ in range(k // R):
+                    graph.replay()
+                done = (k // R) * R
+            for i in range(done, k):
+                engine.verify(arenas[(k0 + i) % R], descs, max_length_hint=w.max_length, counters=counters,
+                              stream=stream)
+
     # ---- warmup -------------------------------------------------------------------------------
-    for i in range(args.warmup):
-        engine.verify(arenas[i % R], descs, max_length_hint=w.max_length, counters=counters)
+    run_steps(0, max(args.warmup, 1))
     torch.cuda.synchronize()
-    engine.reset_counters(counters)
+    engine.reset_counters(counters, stream=stream)
     torch.cuda.synchronize()
 
     # ---- timed region -----------------------------------------------------------------------------
     K = args.steps
-    ev_s = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
-    ev_e = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
-    ctr_reduced = torch.zeros(5, dtype=torch.int64, device=dev)
+    ev_a = torch.cuda.Event(enable_timing=True)
+    ev_b = torch.cuda.Event(enable_timing=True)
+    ctr_reduced = None
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(K):
-        ev_s[k].record(stream)
-        engine.verify(arenas[k % R], descs, max_length_hint=w.max_length, counters=counters)
-        ev_e[k].record(stream)
+    ev_a.record(stream)
+    run_steps(0, K)
+    ev_b.record(stream)
     if world > 1:
         # fold the shards on-device and all-reduce the 5 counters over RCCL/xGMI
-        ctr_reduced.copy_(counters.view(-1, 8)[:, :5].sum(0))
-        dist.all_reduce(ctr_reduced)
+        with torch.cuda.stream(stream):
+            ctr_reduced = D.allreduce_counters(D.fold_counters(counters))
     torch.cuda.synchronize()
     barrier()
     t1 = time.perf_counter()
-    elapsed = t1 - t0
-    if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    elapsed = D.max_over_ranks(t1 - t0, device=dev)
 
-    kern_ms = np.array([ev_s[k].elapsed_time(ev_e[k]) for k in range(K)])
-    avg_kernel_s = float(kern_ms.mean()) / 1e3
+    # events on the launch stream bracket exactly the K launches: the average launch duration
+    # includes the (graph) dispatch gaps, so it is an upper bound of the kernel time rocprof reports
+    avg_kernel_s = ev_a.elapsed_time(ev_b) / 1e3 / K
     local_ctr = engine.read_counters(counters)
     parity_ok = local_ctr == {k: v * K for k, v in exp_ctr.items()}
     if world > 1:
-        glob = ctr_reduced.cpu().tolist()
-        exp_glob = [exp_ctr[f] * K * world for f in ("bytes_checked", "bytes_ok", "buffers_checked",
-                                                      "buffers_failed", "mismatched_bytes")]
+        glob = D.counters_dict(ctr_reduced)
+        exp_glob = {f: exp_ctr[f] * K * world for f in exp_ctr}
         parity_ok = parity_ok and glob == exp_glob
         ok_t = torch.tensor([1 if parity_ok else 0], device=dev)
         dist.all_reduce(ok_t, op=dist.ReduceOp.MIN)
@@ -146,7 +162,7 @@ def main():
         torch.cuda.synchronize()
         ta = time.perf_counter()
         for _ in range(20):
-            dist.all_reduce(ctr_reduced)
+            D.allreduce_counters(ctr_reduced)
         torch.cuda.synchronize()
         allreduce_us = (time.perf_counter() - ta) / 20 * 1e6
 
@@ -159,15 +175,11 @@ def main():
         if not args.no_cpu_baseline:
             cpu = cpu_baseline(arenas[0], w, args.cpu_seconds)
 
-    traffic = None
-    tp = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_traffic.json")
-    if os.path.exists(tp):
-        try:
-            tj = json.load(open(tp))
-            if tj.get("workload") == w.name and tj.get("buffers") == args.buffers:
-                traffic = tj.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+    traffic, traffic_src = pmc_traffic(w.name, args.buffers)
+    from ctstraffic_amd import _lib
+
+    variant = engine.get_attr(_lib.ATTR_VERIFY_VARIANT)
+    kernel = VERIFY_KERNELS.get(variant, "variant %d" % variant)
 
     if rank == 0:
         line = {
@@ -199,8 +211,11 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved_gbps / HBM_PEAK_GBPS, 4),
                 "traffic": traffic,
-                "kernel": "cts::verify_wg_kernel<8,true>",
+                "traffic_source": traffic_src,
+                "kernel": kernel,
                 "avg_kernel_us": round(avg_kernel_s * 1e6, 2),
+                "timing": "HIP events on the launch stream around the K timed launches (%s), / K"
+                          % ("HIP-graph replays" if graph is not None else "host launches"),
                 "algorithmic_bytes_per_launch": bytes_per_step,
             },
             "cpu_baseline": cpu,
@@ -217,14 +232,40 @@ def main():
 
 
 def _time_kernel(torch, fn, steps):
+    """Average time per launch: events around `steps` back-to-back launches (per-launch event pairs
+    would add ~2.5 us to every launch)."""
     s = torch.cuda.current_stream()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    fn(0)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(s)
     for i in range(steps):
-        evs[i][0].record(s)
         fn(i)
-        evs[i][1].record(s)
+    b.record(s)
     torch.cuda.synchronize()
-    return float(np.mean([a.elapsed_time(b) for a, b in evs])) / 1e3
+    return a.elapsed_time(b) / 1e3 / steps
+
+
+VERIFY_KERNELS = {0: "cts::verify_wg_kernel<8,true>", 1: "cts::verify_wg_kernel<4,true>",
+                  2: "cts::verify_wg_kernel<16,true>", 3: "cts::verify_wave_kernel<8,true>",
+                  4: "cts::verify_wg_nb_kernel<8,true>", 5: "cts::verify_wg_nb_kernel<4,true>"}
+
+
+def pmc_traffic(workload, buffers):
+    """HBM bytes per verify launch from the newest profiles/<round>/pmc_traffic.json (rocprofv3 PMC,
+    corrected per MI355X_MICROARCH.md; written by tools/prof_summary.py), or None."""
+    root = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles")
+    try:
+        rounds = sorted(d for d in os.listdir(root) if os.path.exists(os.path.join(root, d, "pmc_traffic.json")))
+    except OSError:
+        return None, None
+    for d in reversed(rounds):
+        try:
+            tj = json.load(open(os.path.join(root, d, "pmc_traffic.json")))
+        except Exception:
+            continue
+        if tj.get("workload") == workload and tj.get("buffers") == buffers and tj.get("hbm_bytes_per_launch"):
+            return int(tj["hbm_bytes_per_launch"]), "profiles/%s/pmc_traffic.json" % d
+    return None, None
 
 
 def run_extras(engine, torch, W, w, arenas, descs, dev, want):

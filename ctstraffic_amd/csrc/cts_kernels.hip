@@ -281,6 +281,33 @@ __device__ __forceinline__ void scan_exact(const Span& s, uint32_t lane, uint32_
     }
 }
 
+// Exact scan of exactly the chunks this lane owns in scan_buffer: interior chunk
+// c (1 <= c < nchunks-1) belongs to lane (c-1) % TEAM, chunk 0 to lane 0 and the
+// last chunk to lane 1. A team that splits a buffer's verdict across waves needs
+// each wave's exact share to cover exactly what that wave's fast pass flagged.
+template <int TEAM>
+__device__ __forceinline__ void scan_exact_owned(const Span& s, uint32_t lane, uint32_t& first, uint32_t& count)
+{
+    auto take = [&](uint32_t c) {
+        const u32x4 x = chunk_diff_masked(s, c);
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            const uint32_t nz = nonzero_bytes(x[w]);
+            if (nz) {
+                const uint32_t idx = 4u * (uint32_t)w + ((uint32_t)__builtin_ctz(nz) >> 3);
+                const uint32_t pos = 16u * c + idx - s.lo;
+                first = pos < first ? pos : first;
+                count += (uint32_t)__builtin_popcount(nz);
+            }
+        }
+    };
+    if (s.nchunks == 0) return;
+    if (s.nchunks >= 3)
+        for (uint32_t c = 1u + lane; c < s.nchunks - 1u; c += TEAM) take(c);
+    if (lane == 0u) take(0u);
+    if (lane == 1u && s.nchunks > 1u) take(s.nchunks - 1u);
+}
+
 __device__ __forceinline__ uint32_t wave_min(uint32_t v)
 {
 #pragma unroll
@@ -428,6 +455,89 @@ __global__ void __launch_bounds__(kBlock, (U <= 8 ? 8 : 4))
 }
 
 // ---------------------------------------------------------------------------------------------
+// Barrier-free workgroup-per-buffer verify. verify_wg_kernel ends every buffer
+// with __syncthreads_or: each wave drains its loads (vmcnt(0)) and then waits
+// for the slowest wave before the next buffer's loads go out — one HBM latency
+// of dead time per buffer per workgroup. Here the four waves of a workgroup
+// only meet through an LDS arrival word per buffer: a wave that saw a mismatch
+// in its own chunks computes its exact (first, count) share first and merges it
+// with LDS atomics, then every wave adds one arrival (count | flag << 8); the
+// wave that arrives last writes the record and resets the slot. Waves run
+// ahead into the next buffer immediately. Slots form a ring of kRing; a
+// barrier every kRing buffers bounds the skew between waves so a slot is
+// never reused while a slower wave still owns it.
+constexpr uint32_t kRing = 16;
+
+struct ArriveSlot {
+    uint32_t arrive;  // arrivals (low 8 bits) | flagged waves << 8
+    uint32_t first;   // min first-mismatch over flagged waves
+    uint32_t count;   // sum of differing bytes over flagged waves
+};
+
+template <int U, bool NT>
+__global__ void __launch_bounds__(kBlock, (U <= 8 ? 8 : 4))
+    verify_wg_nb_kernel(const uint8_t* __restrict__ arena, uint64_t arena_bytes, const cts_buf_desc* __restrict__ descs,
+                        uint32_t n, cts_verify_result* __restrict__ results, uint64_t* __restrict__ counters,
+                        uint32_t* __restrict__ conn_first_fail, uint32_t n_conns)
+{
+    constexpr int WAVES = kBlock / 64;
+    __shared__ uint64_t ctr[WAVES][5];
+    __shared__ ArriveSlot slots[kRing];
+    const uint32_t lane = threadIdx.x;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (threadIdx.x < kRing) slots[threadIdx.x] = ArriveSlot{0u, kNone, 0u};
+    zero_counters<WAVES>(ctr);  // ends with __syncthreads
+    uint32_t i = blockIdx.x;
+    uint32_t j = 0;
+    cts_buf_desc dn;
+    if (i < n) dn = descs[i];
+    for (; i < n; i += gridDim.x, ++j) {
+        const cts_buf_desc d = dn;
+        if (i + gridDim.x < n) dn = descs[i + gridDim.x];
+        if (j != 0 && (j % kRing) == 0) __syncthreads();  // bound inter-wave skew (slot reuse)
+        if (desc_bad(d, arena_bytes)) {
+            if (lane == 0) write_bad(results, i);
+            continue;
+        }
+        const Span s = make_span(arena, d);
+        const uint32_t acc = scan_buffer<kBlock, U, NT>(s, lane);
+        ArriveSlot* slot = &slots[j % kRing];
+        uint32_t flag = 0;
+        if (__any(acc != 0u)) {  // rare: exact share of this wave's chunks
+            uint32_t first = kNone, count = 0;
+            scan_exact_owned<kBlock>(s, lane, first, count);
+            first = wave_min(first);
+            count = wave_sum(count);
+            if ((lane & 63u) == 0) {
+                atomicMin(&slot->first, first);
+                atomicAdd(&slot->count, count);
+            }
+            flag = 0x100u;
+        }
+        uint32_t old = 0;
+        if ((lane & 63u) == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            old = atomicAdd(&slot->arrive, 1u | flag);
+        }
+        old = (uint32_t)__builtin_amdgcn_readfirstlane((int)__shfl((int)old, 0, 64));
+        if ((old & 0xFFu) == (uint32_t)(WAVES - 1) && (lane & 63u) == 0) {  // last arrival finishes the buffer
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            const bool any = ((old >> 8) + (flag >> 8)) != 0u;
+            uint32_t first = kNone, count = 0;
+            if (any) {
+                first = __hip_atomic_load(&slot->first, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                count = __hip_atomic_load(&slot->count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            slot->first = kNone;
+            slot->count = 0;
+            slot->arrive = 0;
+            finish_buffer(s, d, i, first, count, results, ctr[wave], conn_first_fail, n_conns);
+        }
+    }
+    flush_counters<WAVES>(counters, ctr);
+}
+
+// ---------------------------------------------------------------------------------------------
 // One wave per buffer (datagram-sized buffers; also any buffer when there are
 // enough of them to fill the chip one wave each). Waves grid-stride over the
 // descriptors, fetching the next descriptor while the current buffer streams.
@@ -546,8 +656,11 @@ static void launch_verify_nt(const uint8_t* arena, uint64_t arena_bytes, const c
         default: verify_wave_kernel<2, NT><<<grid, kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         }
     } else {
-        // variant (large path): 0 = workgroup/buffer U8, 1 = U4, 2 = U16, 3 = wave/buffer U8
+        // variant (large path): 0 = workgroup/buffer U8, 1 = U4, 2 = U16, 3 = wave/buffer U8,
+        // 4 = barrier-free workgroup/buffer U8, 5 = barrier-free U4
         switch (geo.verify_variant) {
+        case 4: verify_wg_nb_kernel<8, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
+        case 5: verify_wg_nb_kernel<4, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 1: verify_wg_kernel<4, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 2: verify_wg_kernel<16, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 3: verify_wave_kernel<8, NT><<<grid_for(n, kBlock / 64, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;

@@ -1,0 +1,85 @@
+"""Multi-GPU plumbing for the verify path.
+
+The path shards embarrassingly: each buffer carries its own expected pattern
+offset, and connections are assigned to ranks by ``fmix32(conn_index) mod G``
+(:func:`ctstraffic_amd.workload.shard_of`), so a connection's first failing
+buffer and its DataError decision (ctsSocketState.cpp:221-232) stay on one
+rank. The only collective is an optional all-reduce (sum) of the five
+ctsStatistics-style counters (ctsStatistics.hpp:87-198) — 40 bytes over
+RCCL/xGMI (backend "nccl") or gloo on CPU.
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+from .types import COUNTER_FIELDS
+
+COUNTER_SLOTS = 8  # u64 per 64-byte counter shard (cts_internal.hpp kCounterSlots)
+
+
+def dist_env():
+    """(world, rank, local_rank) from the torch.distributed.run environment."""
+    return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def init(backend: str, device=None):
+    """init_process_group from the env; MASTER_ADDR defaults to 127.0.0.1."""
+    import torch.distributed as dist
+
+    world, rank, _ = dist_env()
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    kw = {}
+    if device is not None:
+        kw["device_id"] = device
+    dist.init_process_group(backend, rank=rank, world_size=world, **kw)
+    return world, rank
+
+
+def fold_counters(counter_block):
+    """Device counter block (CTS_COUNTER_SHARDS x 8 int64, cts_counters_device_bytes) -> int64[5],
+    on the block's own device (no host round trip)."""
+    return counter_block.view(-1, COUNTER_SLOTS)[:, : len(COUNTER_FIELDS)].sum(0)
+
+
+def allreduce_counters(counters5, group=None):
+    """In-place sum of the five counters over all ranks (ctsStatsTracking::Add across GPUs)."""
+    import torch.distributed as dist
+
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(counters5, op=dist.ReduceOp.SUM, group=group)
+    return counters5
+
+
+def counters_dict(counters5) -> dict:
+    vals = [int(x) for x in counters5.tolist()]
+    return dict(zip(COUNTER_FIELDS, vals))
+
+
+def max_over_ranks(value: float, device=None, group=None) -> float:
+    """Max of a float over ranks (the timed region's wall time)."""
+    import torch
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        return value
+    t = torch.tensor([value], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return float(t.item())
+
+
+def data_error_count(conn_first_fail, group=None) -> int:
+    """DataError count: connections whose first failing buffer exists (slot != 0xFFFFFFFF),
+    summed over ranks (connections are rank-local, so the sum is exact)."""
+    import torch
+    import torch.distributed as dist
+
+    n = (conn_first_fail.view(torch.int32) != -1).sum().to(torch.int64).reshape(1)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(n, op=dist.ReduceOp.SUM, group=group)
+    return int(n.item())
+
+
+__all__ = ["dist_env", "init", "fold_counters", "allreduce_counters", "counters_dict", "max_over_ranks",
+           "data_error_count"]

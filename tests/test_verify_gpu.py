@@ -101,8 +101,10 @@ def _random_case(rng, n, max_len, align_mix=True, corrupt_frac=0.3, skip=False):
         if v <= 0 or rng.random() > corrupt_frac:
             continue
         base = int(descs[i]["byte_offset"]) + int(descs[i]["skip_head"])
-        kind = rng.integers(0, 4)
-        if kind == 0:
+        kind = rng.integers(0, 5)
+        if kind == 4:  # scattered bytes: several waves / lanes of one team see mismatches
+            ps = sorted(set(int(x) for x in rng.integers(0, v, size=int(rng.integers(2, 9)))))
+        elif kind == 0:
             ps = [int(rng.integers(0, v))]
         elif kind == 1:
             s = int(rng.integers(0, v))
@@ -272,7 +274,7 @@ def test_verify_host_batch(engine):
 
 
 # ---- every launch variant / geometry is bit-identical ------------------------------------------
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
 @pytest.mark.parametrize("nt", [1, 0])
 def test_launch_variants_parity(engine, variant, nt):
     from ctstraffic_amd import _lib
@@ -281,7 +283,8 @@ def test_launch_variants_parity(engine, variant, nt):
         engine.set_attr(_lib.ATTR_VERIFY_VARIANT, variant)
         engine.set_attr(_lib.ATTR_NT_LOADS, nt)
         for seed, n, max_len, hint, skip in [(21, 200, 3000, 1472, True), (22, 64, 140000, 0, False),
-                                             (23, 300, 1472, 1472, True), (24, 100, 70000, 0, True)]:
+                                             (23, 300, 1472, 1472, True), (24, 100, 70000, 0, True),
+                                             (25, 6000, 9000, 0, False)]:  # > kRing buffers per workgroup
             for bpc in (1, 16):
                 engine.set_attr(_lib.ATTR_BLOCKS_PER_CU, bpc)
                 engine.set_attr(_lib.ATTR_SMALL_BLOCKS_PER_CU, bpc)
