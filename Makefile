@@ -6,8 +6,8 @@ ARCH      ?= gfx950
 HIPFLAGS  ?= -O3 -std=c++17 -fPIC -Wall -Wno-unused-result --offload-arch=$(ARCH) -Iinclude -Ictstraffic_amd/csrc
 CSRC      := ctstraffic_amd/csrc
 ENGINE_SO := ctstraffic_amd/libcts_engine.so
-HDRS      := include/cts_engine.h include/cts_pattern.h $(CSRC)/cts_internal.hpp $(wildcard $(CSRC)/*.hpp)
-SRCS      := $(CSRC)/cts_kernels.hip $(CSRC)/cts_engine.cpp $(wildcard $(CSRC)/cts_pattern*.cpp)
+HDRS      := $(wildcard include/*.h) $(wildcard $(CSRC)/*.hpp)
+SRCS      := $(wildcard $(CSRC)/*.hip) $(wildcard $(CSRC)/*.cpp)
 OBJS      := $(patsubst $(CSRC)/%,ctstraffic_amd/build/%.o,$(SRCS))
 
 all: $(ENGINE_SO) oracle

@@ -112,12 +112,10 @@ def _declare(L: ctypes.CDLL) -> None:
         fn = getattr(L, name)
         fn.argtypes = argtypes
         fn.restype = restype
-    try:
-        from . import _pattern_abi
+    from . import _pattern_abi, media_stream
 
-        _pattern_abi.declare(L)
-    except ImportError:
-        pass
+    _pattern_abi.declare(L)
+    media_stream.declare(L)
 
 
 def lib() -> ctypes.CDLL:

@@ -244,6 +244,33 @@ int cts_verify(cts_engine* e, const void* dev_arena, uint64_t arena_bytes, const
                                          dev_conn_first_fail, n_conns, static_cast<hipStream_t>(stream), e->geo));
 }
 
+int cts_media_stream_fill(cts_engine* e, void* dev_arena, uint64_t arena_bytes, const cts_buf_desc* dev_descs,
+                          const cts_datagram_header* dev_headers, uint32_t n, void* stream)
+{
+    if (e == nullptr) return CTS_E_INVALID;
+    if (n == 0) return CTS_OK;
+    if (dev_arena == nullptr || dev_descs == nullptr || dev_headers == nullptr) return CTS_E_INVALID;
+    DeviceGuard g(e->device);
+    if (!g.ok) return CTS_E_HIP;
+    return hip_status(cts::launch_media_stream_fill(static_cast<uint8_t*>(dev_arena), arena_bytes, dev_descs,
+                                                    dev_headers, n, static_cast<hipStream_t>(stream), e->geo));
+}
+
+int cts_media_stream_verify(cts_engine* e, const void* dev_arena, uint64_t arena_bytes, const cts_buf_desc* dev_descs,
+                            uint32_t n, cts_datagram_record* dev_records, cts_verify_result* dev_results,
+                            void* dev_counters, void* stream)
+{
+    if (e == nullptr) return CTS_E_INVALID;
+    if (n == 0) return CTS_OK;
+    if (dev_arena == nullptr || dev_descs == nullptr || ((uintptr_t)dev_arena & 15u) != 0) return CTS_E_INVALID;
+    DeviceGuard g(e->device);
+    if (!g.ok) return CTS_E_HIP;
+    return hip_status(cts::launch_media_stream_verify(static_cast<const uint8_t*>(dev_arena), arena_bytes, dev_descs,
+                                                      n, dev_records, dev_results,
+                                                      static_cast<uint64_t*>(dev_counters),
+                                                      static_cast<hipStream_t>(stream), e->geo));
+}
+
 size_t cts_counters_device_bytes(void) { return (size_t)CTS_COUNTER_SHARDS * cts::kCounterSlots * sizeof(uint64_t); }
 
 int cts_counters_reset(cts_engine* e, void* dev_counters, void* stream)

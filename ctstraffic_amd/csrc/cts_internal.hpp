@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include "cts_engine.h"
+#include "cts_media_stream.h"
 
 namespace cts {
 
@@ -14,7 +15,7 @@ namespace cts {
 constexpr int kCounterSlots = 8;  // 5 used, padded to one 64-byte line
 enum CounterSlot { kBytesChecked = 0, kBytesOk = 1, kBuffersChecked = 2, kBuffersFailed = 3, kMismatchedBytes = 4 };
 
-constexpr int kVerifyVariants = 6;  // workgroup-per-buffer verify variants (launch_verify)
+constexpr int kVerifyVariants = 8;  // workgroup-per-buffer verify variants (launch_verify)
 
 struct LaunchGeometry {
     int num_cus = 256;        // hipDeviceAttributeMultiprocessorCount
@@ -36,5 +37,13 @@ hipError_t launch_fill(uint8_t* arena, uint64_t arena_bytes, const cts_buf_desc*
 // dst[i] = P((pattern_offset + i) mod 65536) for i < bytes; many blocks per span.
 hipError_t launch_fill_span(uint8_t* dst, uint64_t bytes, uint32_t pattern_offset, hipStream_t stream,
                             const LaunchGeometry& geo);
+
+hipError_t launch_media_stream_verify(const uint8_t* arena, uint64_t arena_bytes, const cts_buf_desc* descs, uint32_t n,
+                                     cts_datagram_record* records, cts_verify_result* results, uint64_t* counters,
+                                     hipStream_t stream, const LaunchGeometry& geo);
+
+hipError_t launch_media_stream_fill(uint8_t* arena, uint64_t arena_bytes, const cts_buf_desc* descs,
+                                   const cts_datagram_header* headers, uint32_t n, hipStream_t stream,
+                                   const LaunchGeometry& geo);
 
 }  // namespace cts

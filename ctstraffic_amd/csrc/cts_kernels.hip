@@ -108,6 +108,7 @@ struct Span {
     uint32_t lo;       // bytes of chunk 0 before the span
     uint32_t hi_last;  // bytes of the last chunk inside the span (1..16)
     uint32_t expected; // ctsTask::m_expectedPatternOffset
+    uint32_t cb0;      // first interior chunk on a 128-byte line boundary (1..8)
 };
 
 __device__ __forceinline__ bool desc_bad(const cts_buf_desc& d, uint64_t arena_bytes)
@@ -133,6 +134,10 @@ __device__ __forceinline__ Span make_span(const uint8_t* __restrict__ arena, con
     s.sh = s.q0 & 1u;
     s.p = reinterpret_cast<const u32x4*>(s.sp - s.lo);
     s.expected = d.expected_pattern_offset;
+    // Interior rounds start on a 128-byte line: a wave's 1 KiB load then covers 8
+    // lines instead of straddling 9 (chunks [1, cb0) are head chunks, see scan_buffer).
+    const uint32_t a = (uint32_t)(((uintptr_t)s.p >> 4) & 7u);  // chunk 0's slot in its line
+    s.cb0 = 8u - a;                                             // (a + cb0) % 8 == 0, cb0 in [1, 8]
     return s;
 }
 
@@ -168,7 +173,7 @@ __device__ __forceinline__ u32x4 buf_load(__amdgpu_buffer_rsrc_t r, uint32_t vof
 // Expected chunk u of a round: k advances by TEAM*8 per unrolled step (16*TEAM
 // bytes / 2), added to the packed base before the per-half wrap mask. The low
 // half stays below 65536 (k <= 32767 + 8*TEAM*(U-1) + 8), so no carry crosses.
-template <int TEAM, int U>
+template <int TEAM, int U, bool EVEN = false>
 __device__ __forceinline__ u32x4 expected_step(uint32_t B, int u, uint32_t sh)
 {
     static_assert(32767 + 8 * TEAM * (U - 1) + 8 < 65536, "packed k must not carry");
@@ -182,9 +187,15 @@ __device__ __forceinline__ u32x4 expected_step(uint32_t B, int u, uint32_t sh)
     const uint32_t w1 = (b + 0x20002u) & 0x7FFF7FFFu;
     const uint32_t w2 = (b + 0x40004u) & 0x7FFF7FFFu;
     const uint32_t w3 = (b + 0x60006u) & 0x7FFF7FFFu;
-    const uint32_t w4 = (b + 0x80008u) & 0x7FFF7FFFu;
-    return u32x4{__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
-                 __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh)};
+    if constexpr (EVEN) {
+        // byte phase 0 (every 16-aligned expected offset, 75 % of config 2): the chunk IS
+        // the four packed pairs, no funnel shift and no fifth word
+        return u32x4{w0, w1, w2, w3};
+    } else {
+        const uint32_t w4 = (b + 0x80008u) & 0x7FFF7FFFu;
+        return u32x4{__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
+                     __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh)};
+    }
 }
 
 // packed base (k*0x10001 + 0x10000) of the chunk at index c
@@ -202,13 +213,13 @@ __device__ __forceinline__ uint32_t chunk_base(const Span& s, uint32_t c)
 // join). Full rounds use SGPR offsets; the tail round puts the whole offset in
 // the VGPR so the range check (which covers voffset + imm) zero-fills the
 // excess lanes, which are then masked out.
-template <int TEAM, int U, bool NT>
-__device__ __forceinline__ uint32_t scan_interior(const Span& s, __amdgpu_buffer_rsrc_t r, uint32_t lane)
+template <int TEAM, int U, bool NT, bool EVEN>
+__device__ __forceinline__ uint32_t scan_interior_impl(const Span& s, __amdgpu_buffer_rsrc_t r, uint32_t lane)
 {
     if (s.nchunks < 3u) return 0;
-    const uint32_t c_end = s.nchunks - 1u;  // interior = [1, c_end)
+    const uint32_t c_end = s.nchunks - 1u;  // interior = [cb0, c_end); [1, cb0) are head chunks
     uint32_t acc = 0;
-    uint32_t cb = 1u;
+    uint32_t cb = s.cb0;
     const uint32_t voff = lane * 16u;
     for (; cb + (uint32_t)(TEAM * U) <= c_end; cb += (uint32_t)(TEAM * U)) {
         u32x4 d[U];
@@ -218,7 +229,7 @@ __device__ __forceinline__ uint32_t scan_interior(const Span& s, __amdgpu_buffer
         const uint32_t B = chunk_base(s, cb + lane);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            acc |= or4(d[u] ^ expected_step<TEAM, U>(B, u, s.sh));
+            acc |= or4(d[u] ^ expected_step<TEAM, U, EVEN>(B, u, s.sh));
             // one chunk's expected words live at a time (else hipcc hoists all
             // U*5 of them ahead of the compares: +40 VGPRs, half the occupancy)
             __builtin_amdgcn_sched_barrier(0);
@@ -232,12 +243,23 @@ __device__ __forceinline__ uint32_t scan_interior(const Span& s, __amdgpu_buffer
         const uint32_t B = chunk_base(s, cb + lane);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const uint32_t any = or4(d[u] ^ expected_step<TEAM, U>(B, u, s.sh));
+            const uint32_t any = or4(d[u] ^ expected_step<TEAM, U, EVEN>(B, u, s.sh));
             acc |= (cb + (uint32_t)(u * TEAM) + lane < c_end) ? any : 0u;
             __builtin_amdgcn_sched_barrier(0);
         }
     }
     return acc;
+}
+
+// SPLIT: a span-uniform (scalar) branch on the byte phase selects the
+// funnel-shift-free even-phase stream.
+template <int TEAM, int U, bool NT, bool SPLIT>
+__device__ __forceinline__ uint32_t scan_interior(const Span& s, __amdgpu_buffer_rsrc_t r, uint32_t lane)
+{
+    if constexpr (SPLIT) {
+        if (__builtin_amdgcn_readfirstlane(s.sh) == 0u) return scan_interior_impl<TEAM, U, NT, true>(s, r, lane);
+    }
+    return scan_interior_impl<TEAM, U, NT, false>(s, r, lane);
 }
 
 // Fast pass over a whole span: OR of (received ^ expected) over this lane's
@@ -247,16 +269,31 @@ __device__ __forceinline__ uint32_t scan_interior(const Span& s, __amdgpu_buffer
 // instead of adding a dependent round trip per buffer; their byte-masked
 // compare runs at the end, branch-free, on registers. For an empty span the
 // edge offset is out of the resource's range and reads 0.
-template <int TEAM, int U, bool NT>
+// Edge/head chunk of a lane: lane 0 = chunk 0, lane 1 = the last chunk, lanes
+// 2..8 = head chunks 1..7 (those below cb0 and the last chunk); other lanes
+// re-load chunk 0 (same line, no extra traffic) and discard it.
+__device__ __forceinline__ uint32_t edge_chunk_of(const Span& s, uint32_t lane)
+{
+    return lane == 1u ? s.nchunks - 1u : ((lane >= 2u && lane <= 8u) ? lane - 1u : 0u);
+}
+__device__ __forceinline__ bool edge_chunk_used(const Span& s, uint32_t lane)
+{
+    if (s.nchunks == 0u) return false;
+    if (lane == 0u) return true;
+    if (lane == 1u) return s.nchunks > 1u;
+    const uint32_t h = s.nchunks - 1u < s.cb0 ? s.nchunks - 1u : s.cb0;  // head = [1, min(cb0, nchunks-1))
+    return lane >= 2u && lane <= 8u && lane - 1u < h;
+}
+
+template <int TEAM, int U, bool NT, bool SPLIT = false>
 __device__ __forceinline__ uint32_t scan_buffer(const Span& s, uint32_t lane)
 {
     const __amdgpu_buffer_rsrc_t r = span_rsrc(s);
-    const uint32_t ce = (lane == 1u) ? s.nchunks - 1u : 0u;
+    const uint32_t ce = edge_chunk_of(s, lane);
     const u32x4 edge = buf_load<NT>(r, ce * 16u, 0u);
-    uint32_t acc = scan_interior<TEAM, U, NT>(s, r, lane);
-    const bool use = lane < 2u && s.nchunks > 0u && (lane == 0u || s.nchunks > 1u);
+    uint32_t acc = scan_interior<TEAM, U, NT, SPLIT>(s, r, lane);
     const u32x4 x = chunk_xor(s, ce, edge) & range_mask(ce == 0u ? s.lo : 0u, ce == s.nchunks - 1u ? s.hi_last : 16u);
-    acc |= use ? or4(x) : 0u;
+    acc |= edge_chunk_used(s, lane) ? or4(x) : 0u;
     return acc;
 }
 
@@ -282,8 +319,8 @@ __device__ __forceinline__ void scan_exact(const Span& s, uint32_t lane, uint32_
 }
 
 // Exact scan of exactly the chunks this lane owns in scan_buffer: interior chunk
-// c (1 <= c < nchunks-1) belongs to lane (c-1) % TEAM, chunk 0 to lane 0 and the
-// last chunk to lane 1. A team that splits a buffer's verdict across waves needs
+// c (cb0 <= c < nchunks-1) belongs to lane (c-cb0) % TEAM, the edge and head
+// chunks to lanes 0..8 (edge_chunk_of). A team that splits a buffer's verdict across waves needs
 // each wave's exact share to cover exactly what that wave's fast pass flagged.
 template <int TEAM>
 __device__ __forceinline__ void scan_exact_owned(const Span& s, uint32_t lane, uint32_t& first, uint32_t& count)
@@ -303,9 +340,8 @@ __device__ __forceinline__ void scan_exact_owned(const Span& s, uint32_t lane, u
     };
     if (s.nchunks == 0) return;
     if (s.nchunks >= 3)
-        for (uint32_t c = 1u + lane; c < s.nchunks - 1u; c += TEAM) take(c);
-    if (lane == 0u) take(0u);
-    if (lane == 1u && s.nchunks > 1u) take(s.nchunks - 1u);
+        for (uint32_t c = s.cb0 + lane; c < s.nchunks - 1u; c += TEAM) take(c);
+    if (edge_chunk_used(s, lane)) take(edge_chunk_of(s, lane));
 }
 
 __device__ __forceinline__ uint32_t wave_min(uint32_t v)
@@ -423,7 +459,7 @@ __device__ __forceinline__ void block_reduce_mismatch(uint32_t& first, uint32_t&
 // ---------------------------------------------------------------------------------------------
 // One 256-lane workgroup per buffer (grid-strides over buffers). The next
 // buffer's descriptor is fetched while the current one streams.
-template <int U, bool NT>
+template <int U, bool NT, bool SPLIT = false>
 __global__ void __launch_bounds__(kBlock, (U <= 8 ? 8 : 4))
     verify_wg_kernel(const uint8_t* __restrict__ arena, uint64_t arena_bytes, const cts_buf_desc* __restrict__ descs,
                      uint32_t n, cts_verify_result* __restrict__ results, uint64_t* __restrict__ counters,
@@ -443,7 +479,7 @@ __global__ void __launch_bounds__(kBlock, (U <= 8 ? 8 : 4))
             continue;
         }
         const Span s = make_span(arena, d);
-        const uint32_t acc = scan_buffer<kBlock, U, NT>(s, lane);
+        const uint32_t acc = scan_buffer<kBlock, U, NT, SPLIT>(s, lane);
         uint32_t first = kNone, count = 0;
         if (__syncthreads_or(acc != 0u)) {  // rare: exact re-scan + reduction
             scan_exact<kBlock>(s, lane, first, count);
@@ -631,6 +667,125 @@ __global__ void __launch_bounds__(kBlock) fill_span_kernel(uint8_t* __restrict__
 }
 
 // ---------------------------------------------------------------------------------------------
+// MediaStream (UDP) datagrams: one wave per datagram, like verify_wave_kernel.
+// Receive: parse + validate the header (ctsMediaStreamProtocol.hpp:284-329), then
+// verify the payload of DATA datagrams at pattern offset 0 after the 26-byte
+// header (ctsIOPatternMediaStream.cpp:185-192).
+__device__ __forceinline__ int64_t load_i64_unaligned(const uint8_t* p)
+{
+    uint64_t v = 0;
+#pragma unroll
+    for (int b = 0; b < 8; ++b) v |= (uint64_t)p[b] << (8 * b);
+    return (int64_t)v;
+}
+
+template <int U, bool NT>
+__global__ void __launch_bounds__(kBlock)
+    media_stream_verify_kernel(const uint8_t* __restrict__ arena, uint64_t arena_bytes,
+                               const cts_buf_desc* __restrict__ descs, uint32_t n,
+                               cts_datagram_record* __restrict__ records, cts_verify_result* __restrict__ results,
+                               uint64_t* __restrict__ counters)
+{
+    constexpr int WAVES = kBlock / 64;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t nw = gridDim.x * WAVES;
+    __shared__ uint64_t ctr[WAVES][5];
+    zero_counters<WAVES>(ctr);
+    for (uint32_t i = blockIdx.x * WAVES + wave; i < n; i += nw) {
+        cts_buf_desc d = descs[i];
+        const uint32_t completed = d.length;
+        const bool bad = d.byte_offset > arena_bytes || arena_bytes - d.byte_offset < (uint64_t)completed;
+        const uint8_t* dg = arena + d.byte_offset;
+        // header: every lane computes the same scalar answer from the first bytes
+        uint32_t flag = 0, kind;
+        if (bad) {
+            kind = CTS_DGRAM_BAD_DESC;
+        } else if (completed == 0u) {
+            kind = CTS_DGRAM_ZERO;
+        } else if (completed < CTS_UDP_FLAG_LENGTH) {
+            kind = CTS_DGRAM_SHORT;
+        } else {
+            flag = (uint32_t)dg[0] | ((uint32_t)dg[1] << 8);
+            if (flag == CTS_UDP_FLAG_DATA)
+                kind = completed < CTS_UDP_DATA_HEADER_LENGTH ? CTS_DGRAM_SHORT : CTS_DGRAM_DATA;
+            else if (flag == CTS_UDP_FLAG_ID)
+                kind = completed < CTS_UDP_CONNECTION_ID_HEADER_LENGTH ? CTS_DGRAM_SHORT : CTS_DGRAM_ID;
+            else
+                kind = CTS_DGRAM_UNKNOWN;
+        }
+        kind = (uint32_t)__builtin_amdgcn_readfirstlane((int)kind);
+        if (records != nullptr && lane == 0) {
+            cts_datagram_record rec;
+            const bool data = kind == CTS_DGRAM_DATA;
+            rec.sequence_number = data ? load_i64_unaligned(dg + 2) : 0;
+            rec.sender_qpc = data ? load_i64_unaligned(dg + 8) : 0;
+            rec.sender_qpf = data ? load_i64_unaligned(dg + 16) : 0;
+            rec.flag = (uint16_t)flag;
+            rec.kind = (uint8_t)kind;
+            rec.reserved = 0;
+            rec.completed_bytes = completed;
+            records[i] = rec;
+        }
+        if (kind != CTS_DGRAM_DATA) {
+            if (results != nullptr && lane == 0) {
+                cts_verify_result r{};
+                r.flags = kind == CTS_DGRAM_BAD_DESC ? CTS_RESULT_FLAG_BAD_DESC : CTS_RESULT_FLAG_NOT_DATA;
+                results[i] = r;
+            }
+            continue;
+        }
+        d.skip_head = CTS_UDP_DATA_HEADER_LENGTH;
+        d.expected_pattern_offset = 0;
+        const Span s = make_span(arena, d);
+        const uint32_t acc = scan_buffer<64, U, NT>(s, lane);
+        uint32_t first = kNone, count = 0;
+        if (__any(acc != 0u)) {
+            scan_exact<64>(s, lane, first, count);
+            first = wave_min(first);
+            count = wave_sum(count);
+        }
+        if (lane == 0) finish_buffer(s, d, i, first, count, results, ctr[wave], nullptr, 0);
+    }
+    flush_counters<WAVES>(counters, ctr);
+}
+
+// Send: header {u16 0, i64 seq, i64 qpc, i64 qpf} + P[0 .. length-26) per datagram
+// (ctsMediaStreamSendRequests' WSABUF array, ctsMediaStreamProtocol.hpp:230-243).
+__global__ void __launch_bounds__(kBlock)
+    media_stream_fill_kernel(uint8_t* __restrict__ arena, uint64_t arena_bytes, const cts_buf_desc* __restrict__ descs,
+                             const cts_datagram_header* __restrict__ headers, uint32_t n)
+{
+    constexpr int WAVES = kBlock / 64;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    for (uint32_t i = blockIdx.x * WAVES + wave; i < n; i += gridDim.x * WAVES) {
+        const cts_buf_desc d = descs[i];
+        if (d.length < CTS_UDP_DATA_HEADER_LENGTH || d.byte_offset > arena_bytes ||
+            arena_bytes - d.byte_offset < (uint64_t)d.length)
+            continue;
+        uint8_t* dg = arena + d.byte_offset;
+        if (lane < CTS_UDP_DATA_HEADER_LENGTH) {
+            const cts_datagram_header h = headers[i];
+            uint8_t b = 0;
+            if (lane >= 2u && lane < 10u) b = (uint8_t)((uint64_t)h.sequence_number >> (8 * (lane - 2u)));
+            else if (lane >= 10u && lane < 18u) b = (uint8_t)((uint64_t)h.qpc >> (8 * (lane - 10u)));
+            else if (lane >= 18u) b = (uint8_t)((uint64_t)h.qpf >> (8 * (lane - 18u)));
+            dg[lane] = b;  // flag bytes 0..1 = c_udpDatagramProtocolHeaderFlagData = 0
+        }
+        const uint32_t len = d.length - CTS_UDP_DATA_HEADER_LENGTH;
+        if (len == 0) continue;
+        uint8_t* sp = dg + CTS_UDP_DATA_HEADER_LENGTH;
+        const uint32_t lo = (uint32_t)((uintptr_t)sp & 15u);
+        const uint32_t nchunks = (uint32_t)(((uint64_t)lo + len + 15u) >> 4);
+        const uint32_t hi_last = (uint32_t)((uint64_t)lo + len - 16ull * (nchunks - 1u));
+        const uint32_t q0 = (0u - lo) & 0xFFFFu;
+        u32x4* p = reinterpret_cast<u32x4*>(sp - lo);
+        for (uint32_t c = lane; c < nchunks; c += 64u) fill_chunk(p, c, nchunks, q0, lo, hi_last);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 static inline uint32_t grid_for(uint32_t n, int teams_per_block, const LaunchGeometry& geo)
 {
     const uint64_t want = ((uint64_t)n + teams_per_block - 1) / teams_per_block;
@@ -657,10 +812,13 @@ static void launch_verify_nt(const uint8_t* arena, uint64_t arena_bytes, const c
         }
     } else {
         // variant (large path): 0 = workgroup/buffer U8, 1 = U4, 2 = U16, 3 = wave/buffer U8,
-        // 4 = barrier-free workgroup/buffer U8, 5 = barrier-free U4
+        // 4 = barrier-free workgroup/buffer U8, 5 = barrier-free U4,
+        // 6 = workgroup/buffer U8 with an even-phase fast stream, 7 = same U4
         switch (geo.verify_variant) {
         case 4: verify_wg_nb_kernel<8, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 5: verify_wg_nb_kernel<4, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
+        case 6: verify_wg_kernel<8, NT, true><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
+        case 7: verify_wg_kernel<4, NT, true><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 1: verify_wg_kernel<4, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 2: verify_wg_kernel<16, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 3: verify_wave_kernel<8, NT><<<grid_for(n, kBlock / 64, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
@@ -696,6 +854,31 @@ hipError_t launch_fill(uint8_t* arena, uint64_t arena_bytes, const cts_buf_desc*
     } else {
         fill_kernel<kBlock><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(arena, arena_bytes, descs, n);
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_media_stream_verify(const uint8_t* arena, uint64_t arena_bytes, const cts_buf_desc* descs, uint32_t n,
+                                     cts_datagram_record* records, cts_verify_result* results, uint64_t* counters,
+                                     hipStream_t stream, const LaunchGeometry& geo)
+{
+    if (n == 0) return hipSuccess;
+    const uint32_t grid = grid_for(n, kBlock / 64, geo);
+    if (geo.nontemporal)
+        media_stream_verify_kernel<2, true><<<grid, kBlock, 0, stream>>>(arena, arena_bytes, descs, n, records, results,
+                                                                         counters);
+    else
+        media_stream_verify_kernel<2, false><<<grid, kBlock, 0, stream>>>(arena, arena_bytes, descs, n, records,
+                                                                          results, counters);
+    return hipGetLastError();
+}
+
+hipError_t launch_media_stream_fill(uint8_t* arena, uint64_t arena_bytes, const cts_buf_desc* descs,
+                                   const cts_datagram_header* headers, uint32_t n, hipStream_t stream,
+                                   const LaunchGeometry& geo)
+{
+    if (n == 0) return hipSuccess;
+    media_stream_fill_kernel<<<grid_for(n, kBlock / 64, geo), kBlock, 0, stream>>>(arena, arena_bytes, descs, headers,
+                                                                                    n);
     return hipGetLastError();
 }
 

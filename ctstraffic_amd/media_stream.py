@@ -1,0 +1,152 @@
+"""MediaStream (UDP) framing around the verify path — Python handle over
+include/cts_media_stream.h.
+
+* :func:`split` — ctsMediaStreamSendRequests' datagram sizes for one frame
+  (ctsMediaStreamProtocol.hpp:151-205);
+* :func:`fill` / :func:`verify` — the gfx950 datagram kernels (sender
+  materialisation; receiver header parse + validate + payload verify);
+* :class:`MediaStreamClient` — ctsIoPatternMediaStreamClient's frame accounting
+  (ctsIOPatternMediaStream.cpp), driven by explicit render ticks.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from ._lib import CtsError, check, lib
+from .types import DESC_DTYPE, DGRAM_HEADER_DTYPE, DGRAM_RECORD_DTYPE, RESULT_DTYPE
+
+DGRAM_DATA, DGRAM_ID, DGRAM_ZERO, DGRAM_SHORT, DGRAM_UNKNOWN, DGRAM_BAD_DESC = range(6)
+FLAG_DATA, FLAG_ID = 0x0000, 0x1000
+DATA_HEADER_LENGTH = 26
+CONNECTION_ID_HEADER_LENGTH = 39
+
+
+class Settings(ctypes.Structure):
+    """ctsConfig::MediaStreamSettings (the fields the client reads)."""
+
+    _fields_ = [("frame_size_bytes", ctypes.c_uint32), ("datagram_max_size", ctypes.c_uint32),
+                ("frames_per_second", ctypes.c_uint32), ("buffered_frames", ctypes.c_uint32),
+                ("stream_length_frames", ctypes.c_int64)]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [("bits_received", ctypes.c_int64), ("successful_frames", ctypes.c_int64),
+                ("dropped_frames", ctypes.c_int64), ("duplicate_frames", ctypes.c_int64),
+                ("error_frames", ctypes.c_int64), ("datagrams", ctypes.c_uint64), ("last_error", ctypes.c_uint32),
+                ("finished", ctypes.c_uint32), ("head_sequence_number", ctypes.c_int64),
+                ("fail_datagram", ctypes.c_uint32), ("has_failure", ctypes.c_uint32)]
+
+    def as_dict(self) -> dict:
+        return {f: int(getattr(self, f)) for f, _ in self._fields_}
+
+
+def declare(L: ctypes.CDLL) -> None:
+    P = ctypes.c_void_p
+    u32, u64, i32, i64 = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int, ctypes.c_int64
+    sigs = {
+        "cts_media_stream_split": ([u64, u32, P, u64], u64),
+        "cts_media_stream_fill": ([P, P, u64, P, P, u32, P], i32),
+        "cts_media_stream_verify": ([P, P, u64, P, u32, P, P, P, P], i32),
+        "cts_media_stream_client_create": ([ctypes.POINTER(Settings), ctypes.POINTER(P)], i32),
+        "cts_media_stream_client_destroy": ([P], i32),
+        "cts_media_stream_client_complete": ([P, P, P, u32, i64, i64, ctypes.POINTER(u32)], i32),
+        "cts_media_stream_client_set_connection_id": ([P, ctypes.c_char_p, u32], i32),
+        "cts_media_stream_client_render": ([P], i32),
+        "cts_media_stream_client_stats": ([P, ctypes.POINTER(Stats)], i32),
+        "cts_media_stream_client_connection_id": ([P], ctypes.c_char_p),
+    }
+    for name, (argtypes, restype) in sigs.items():
+        fn = getattr(L, name)
+        fn.argtypes = argtypes
+        fn.restype = restype
+
+
+def split(frame_bytes: int, max_datagram: int) -> np.ndarray:
+    """Total lengths (26-byte header included) of the datagrams one frame is sent as."""
+    n = int(lib().cts_media_stream_split(frame_bytes, max_datagram, None, 0))
+    out = np.zeros(n, dtype=np.uint32)
+    if n:
+        lib().cts_media_stream_split(frame_bytes, max_datagram, out.ctypes.data, n)
+    return out
+
+
+def _ptr(x):
+    from .engine import _ptr as p
+
+    return p(x)
+
+
+def fill(engine, arena, descs, headers, stream=None) -> None:
+    """cts_media_stream_fill: descs (uint8 device tensor of DESC_DTYPE), headers (uint8 device tensor of
+    DGRAM_HEADER_DTYPE)."""
+    from .engine import _nbytes, _stream
+
+    n = _nbytes(descs) // DESC_DTYPE.itemsize
+    assert _nbytes(headers) // DGRAM_HEADER_DTYPE.itemsize == n
+    check("cts_media_stream_fill", lib().cts_media_stream_fill(engine._h, _ptr(arena), _nbytes(arena), _ptr(descs),
+                                                               _ptr(headers), n, _stream(stream)))
+
+
+def verify(engine, arena, descs, records=None, results=None, counters=None, stream=None) -> None:
+    from .engine import _nbytes, _stream
+
+    n = _nbytes(descs) // DESC_DTYPE.itemsize
+    check("cts_media_stream_verify",
+          lib().cts_media_stream_verify(engine._h, _ptr(arena), _nbytes(arena), _ptr(descs), n, _ptr(records),
+                                        _ptr(results), _ptr(counters), _stream(stream)))
+
+
+class MediaStreamClient:
+    """ctsIoPatternMediaStreamClient's frame accounting (ctsIOPatternMediaStream.cpp:46-530)."""
+
+    def __init__(self, frame_size_bytes: int, buffered_frames: int, stream_length_frames: int,
+                 datagram_max_size: int = 1400, frames_per_second: int = 60):
+        self._s = Settings(frame_size_bytes, datagram_max_size, frames_per_second, buffered_frames,
+                           stream_length_frames)
+        h = ctypes.c_void_p()
+        check("cts_media_stream_client_create", lib().cts_media_stream_client_create(ctypes.byref(self._s),
+                                                                                       ctypes.byref(h)))
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            lib().cts_media_stream_client_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def complete(self, records: np.ndarray, results: np.ndarray, receiver_qpc: int = 0, receiver_qpf: int = 0):
+        """Returns (cts_io_status, consumed)."""
+        records = np.ascontiguousarray(records, dtype=DGRAM_RECORD_DTYPE)
+        results = np.ascontiguousarray(results, dtype=RESULT_DTYPE)
+        assert len(records) == len(results)
+        consumed = ctypes.c_uint32()
+        rc = lib().cts_media_stream_client_complete(self._h, records.ctypes.data, results.ctypes.data, len(records),
+                                                    receiver_qpc, receiver_qpf, ctypes.byref(consumed))
+        if rc < 0:
+            raise CtsError("cts_media_stream_client_complete", rc)
+        return rc, consumed.value
+
+    def set_connection_id(self, datagram: bytes) -> None:
+        check("cts_media_stream_client_set_connection_id",
+              lib().cts_media_stream_client_set_connection_id(self._h, datagram, len(datagram)))
+
+    def render(self) -> int:
+        rc = lib().cts_media_stream_client_render(self._h)
+        if rc < 0:
+            raise CtsError("cts_media_stream_client_render", rc)
+        return rc
+
+    def stats(self) -> dict:
+        s = Stats()
+        check("cts_media_stream_client_stats", lib().cts_media_stream_client_stats(self._h, ctypes.byref(s)))
+        return s.as_dict()
+
+    def connection_id(self) -> str:
+        return lib().cts_media_stream_client_connection_id(self._h).decode()

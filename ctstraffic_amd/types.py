@@ -26,3 +26,19 @@ COUNTER_FIELDS = ("bytes_checked", "bytes_ok", "buffers_checked", "buffers_faile
 RESULT_FLAG_BAD_DESC = 0x1
 
 assert DESC_DTYPE.itemsize == 24 and RESULT_DTYPE.itemsize == 12
+# cts_datagram_record (include/cts_media_stream.h)
+DGRAM_RECORD_DTYPE = np.dtype(
+    [
+        ("sequence_number", "<i8"),
+        ("sender_qpc", "<i8"),
+        ("sender_qpf", "<i8"),
+        ("flag", "<u2"),
+        ("kind", "u1"),
+        ("reserved", "u1"),
+        ("completed_bytes", "<u4"),
+    ]
+)
+# cts_datagram_header
+DGRAM_HEADER_DTYPE = np.dtype([("sequence_number", "<i8"), ("qpc", "<i8"), ("qpf", "<i8")])
+RESULT_FLAG_NOT_DATA = 0x2
+assert DGRAM_RECORD_DTYPE.itemsize == 32 and DGRAM_HEADER_DTYPE.itemsize == 24

@@ -1,0 +1,151 @@
+/*
+ * cts_media_stream.h — C ABI of the MediaStream (UDP) datagram framing around
+ * the verify path.
+ *
+ * A MediaStream server sends every frame of FrameSizeBytes as datagrams of at
+ * most DatagramMaxSize bytes. Each datagram is a 26-byte data header
+ * {u16 flag = 0, i64 sequence number (the frame), i64 QPC, i64 QPF} followed by
+ * the first (length - 26) bytes of g_senderSharedBuffer
+ * (ctsMediaStreamProtocol.hpp:43-52, 171-205, 242; ctsMediaStreamServer.cpp:559-563).
+ * The client validates the header, verifies the payload against the pattern at
+ * offset 0, and books the bytes to a frame of its jitter queue
+ * (ctsIOPatternMediaStream.cpp:140-272), which a renderer timer drains
+ * (:360-530).
+ *
+ * GPU side (batched, device-resident): cts_media_stream_fill writes whole data
+ * datagrams; cts_media_stream_verify parses + validates every received
+ * datagram and verifies the data payloads in one pass.
+ * Host side: cts_media_stream_split (frame -> datagram sizes) and the client's
+ * frame accounting (cts_media_stream_client_*), fed with the GPU's records.
+ */
+#ifndef CTS_MEDIA_STREAM_H
+#define CTS_MEDIA_STREAM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "cts_engine.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CTS_UDP_FLAG_DATA 0x0000u                 /* c_udpDatagramProtocolHeaderFlagData */
+#define CTS_UDP_FLAG_ID 0x1000u                   /* c_udpDatagramProtocolHeaderFlagId */
+#define CTS_UDP_FLAG_LENGTH 2u                    /* c_udpDatagramProtocolHeaderFlagLength */
+#define CTS_UDP_CONNECTION_ID_HEADER_LENGTH 39u   /* flag + ctsStatistics::ConnectionIdLength */
+/* CTS_UDP_DATA_HEADER_LENGTH (26) is in cts_engine.h */
+
+/* kind of a received datagram (ctsMediaStreamMessage::ValidateBufferLengthFromTask,
+ * ctsMediaStreamProtocol.hpp:284-329, plus the zero-byte case of
+ * ctsIOPatternMediaStream.cpp:158-167) */
+typedef enum cts_datagram_kind {
+    CTS_DGRAM_DATA = 0,      /* flag 0, >= 26 bytes: payload verified */
+    CTS_DGRAM_ID = 1,        /* flag 0x1000, >= 39 bytes: carries the connection id */
+    CTS_DGRAM_ZERO = 2,      /* 0 bytes */
+    CTS_DGRAM_SHORT = 3,     /* shorter than its header (rejected: TooFewBytes) */
+    CTS_DGRAM_UNKNOWN = 4,   /* unknown flag (rejected: TooFewBytes) */
+    CTS_DGRAM_BAD_DESC = 5   /* descriptor outside the arena */
+} cts_datagram_kind;
+
+/* Header values of one outgoing data datagram. */
+typedef struct cts_datagram_header {
+    int64_t sequence_number;
+    int64_t qpc;
+    int64_t qpf;
+} cts_datagram_header;
+
+/* What the client reads out of one received datagram. Field offsets follow the
+ * reference's reads, including its two overlapping ones:
+ *   sequence_number = *(int64*)(buf + 2)   GetSequenceNumberFromTask (ctsMediaStreamProtocol.hpp:352-366)
+ *   sender_qpc      = *(int64*)(buf + 8)   ctsIOPatternMediaStream.cpp:218
+ *   sender_qpf      = *(int64*)(buf + 16)  ctsIOPatternMediaStream.cpp:219
+ * (the header itself carries qpc at +10 and qpf at +18). */
+typedef struct cts_datagram_record {
+    int64_t sequence_number;
+    int64_t sender_qpc;
+    int64_t sender_qpf;
+    uint16_t flag;            /* GetProtocolHeaderFromTask: u16 at +0 (0 when < 2 bytes) */
+    uint8_t kind;             /* cts_datagram_kind */
+    uint8_t reserved;
+    uint32_t completed_bytes;
+} cts_datagram_record;        /* 32 bytes */
+
+/* Set in cts_verify_result.flags for datagrams that carry no verified payload (not DATA). */
+#define CTS_RESULT_FLAG_NOT_DATA 0x2u
+
+/* ctsMediaStreamSendRequests iteration (ctsMediaStreamProtocol.hpp:151-205):
+ * the total lengths (header included) of the datagrams one frame of
+ * frame_bytes is sent as. Writes min(count, cap) lengths and returns count,
+ * or 0 when frame_bytes <= 26 (the reference FAIL_FASTs) or max_datagram <= 26. */
+uint64_t cts_media_stream_split(uint64_t frame_bytes, uint32_t max_datagram, uint32_t* out_lengths, uint64_t cap);
+
+/* Sender: for every descriptor d (one data datagram of d.length bytes at
+ * d.byte_offset; skip_head/expected ignored), write the 26-byte header
+ * {0, headers[i]} and the payload P[0 .. d.length - 26). */
+int cts_media_stream_fill(cts_engine* engine, void* dev_arena, uint64_t arena_bytes, const cts_buf_desc* dev_descs,
+                          const cts_datagram_header* dev_headers, uint32_t n, void* stream);
+
+/* Receiver: d.length = completed bytes of datagram i at d.byte_offset
+ * (skip_head/expected ignored). records[i] gets the parsed header; for DATA
+ * datagrams results[i] is the payload verify (skip 26, expected offset 0,
+ * RtlCompareMemory semantics, ctsIOPatternMediaStream.cpp:185-192) and the
+ * counters (cts_counters_device_bytes block, accumulated) count it; for other
+ * kinds results[i].flags = CTS_RESULT_FLAG_NOT_DATA and nothing is counted.
+ * Any output may be NULL. */
+int cts_media_stream_verify(cts_engine* engine, const void* dev_arena, uint64_t arena_bytes,
+                            const cts_buf_desc* dev_descs, uint32_t n, cts_datagram_record* dev_records,
+                            cts_verify_result* dev_results, void* dev_counters, void* stream);
+
+/* ---- client frame accounting (ctsIoPatternMediaStreamClient) ---------------- */
+typedef struct cts_media_stream_settings { /* ctsConfig::MediaStreamSettings */
+    uint32_t frame_size_bytes;
+    uint32_t datagram_max_size;
+    uint32_t frames_per_second;
+    uint32_t buffered_frames;
+    int64_t stream_length_frames;
+} cts_media_stream_settings;
+
+/* ctsUdpStatistics (ctsStatistics.hpp:249-314) + the first failure */
+typedef struct cts_media_stream_stats {
+    int64_t bits_received;
+    int64_t successful_frames;
+    int64_t dropped_frames;
+    int64_t duplicate_frames;
+    int64_t error_frames;
+    uint64_t datagrams;          /* datagrams completed into the pattern */
+    uint32_t last_error;         /* GetLastPatternError(): 0 / running / protocol error */
+    uint32_t finished;           /* 1 = stream rendered to its final frame (Abort), 2 = FatalAbort */
+    int64_t head_sequence_number;
+    uint32_t fail_datagram;      /* index (in completion order) of the datagram that failed the stream */
+    uint32_t has_failure;
+} cts_media_stream_stats;
+
+typedef struct cts_media_stream_client cts_media_stream_client;
+
+int cts_media_stream_client_create(const cts_media_stream_settings* settings, cts_media_stream_client** out);
+int cts_media_stream_client_destroy(cts_media_stream_client* client);
+/* CompleteIo of n received datagrams in completion order (records/results from
+ * cts_media_stream_verify, copied to host). Stops at the first datagram that
+ * fails the stream (zero bytes before the end, a rejected header, a corrupted
+ * payload), as the reference's FailedIo would. *consumed = datagrams applied.
+ * Returns a cts_io_status (cts_pattern.h) or a negative cts_status.
+ * An ID datagram's connection id must be handed over with
+ * cts_media_stream_client_set_connection_id (the record does not carry it). */
+int cts_media_stream_client_complete(cts_media_stream_client* client, const cts_datagram_record* records,
+                                     const cts_verify_result* results, uint32_t n, int64_t receiver_qpc,
+                                     int64_t receiver_qpf, uint32_t* consumed);
+int cts_media_stream_client_set_connection_id(cts_media_stream_client* client, const char* datagram, uint32_t len);
+/* One renderer-timer tick (TimerCallback, ctsIOPatternMediaStream.cpp:470-530,
+ * without the wall-clock scheduling): returns 0 = keep rendering, 1 = the stream
+ * finished (Abort), 2 = nothing was ever received (FatalAbort). */
+int cts_media_stream_client_render(cts_media_stream_client* client);
+int cts_media_stream_client_stats(const cts_media_stream_client* client, cts_media_stream_stats* out);
+/* The client's connection id (37 bytes incl. NUL) once an ID datagram was applied. */
+const char* cts_media_stream_client_connection_id(const cts_media_stream_client* client);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+#endif /* CTS_MEDIA_STREAM_H */

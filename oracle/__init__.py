@@ -48,6 +48,17 @@ RESULT_DTYPE = np.dtype(
         ("flags", "u1"),
     ]
 )
+DGRAM_RECORD_DTYPE = np.dtype(
+    [
+        ("sequence_number", "<i8"),
+        ("sender_qpc", "<i8"),
+        ("sender_qpf", "<i8"),
+        ("flag", "<u2"),
+        ("kind", "u1"),
+        ("reserved", "u1"),
+        ("completed_bytes", "<u4"),
+    ]
+)
 COUNTER_FIELDS = ("bytes_checked", "bytes_ok", "buffers_checked", "buffers_failed", "mismatched_bytes")
 assert DESC_DTYPE.itemsize == 24 and RESULT_DTYPE.itemsize == 12
 
@@ -103,6 +114,9 @@ def lib() -> ctypes.CDLL:
         L.ora_verify_batch.argtypes = [P, ctypes.c_uint64, P, ctypes.c_uint32, P,
                                        ctypes.POINTER(OraCounters), P, ctypes.c_uint32, ctypes.c_int]
         L.ora_verify_batch.restype = ctypes.c_int
+        L.ora_media_stream_verify.argtypes = [P, ctypes.c_uint64, P, ctypes.c_uint32, P, P,
+                                              ctypes.POINTER(OraCounters)]
+        L.ora_media_stream_verify.restype = None
         L.ora_fnv1a64.argtypes = [P, ctypes.c_size_t]
         L.ora_fnv1a64.restype = ctypes.c_uint64
         _lib = L
@@ -182,3 +196,15 @@ def verify_batch(arena: np.ndarray, descs: np.ndarray, n_conns: int = 0, nthread
 def fnv1a64(data: np.ndarray) -> int:
     data = np.ascontiguousarray(data, dtype=np.uint8)
     return int(lib().ora_fnv1a64(_ptr(data), data.size))
+
+
+def media_stream_verify(arena: np.ndarray, descs: np.ndarray):
+    """MediaStream client receive path per datagram: (records DGRAM_RECORD_DTYPE, results, counters)."""
+    assert arena.dtype == np.uint8 and arena.flags.c_contiguous
+    descs = np.ascontiguousarray(descs, dtype=DESC_DTYPE)
+    n = len(descs)
+    recs = np.zeros(n, dtype=DGRAM_RECORD_DTYPE)
+    results = np.zeros(n, dtype=RESULT_DTYPE)
+    c = OraCounters()
+    lib().ora_media_stream_verify(_ptr(arena), arena.size, _ptr(descs), n, _ptr(recs), _ptr(results), ctypes.byref(c))
+    return recs, results, c.as_dict()

@@ -248,3 +248,67 @@ uint64_t ora_fnv1a64(const uint8_t* p, size_t n)
     }
     return h;
 }
+
+static int64_t ora_i64le(const uint8_t* p)
+{
+    uint64_t v = 0;
+    for (int b = 0; b < 8; ++b) v |= (uint64_t)p[b] << (8 * b);
+    return (int64_t)v;
+}
+
+void ora_media_stream_verify(const uint8_t* arena, uint64_t arena_bytes, const ora_desc* descs, uint32_t n,
+                             ora_dgram_record* records, ora_result* results, ora_counters* counters)
+{
+    uint32_t maxlen = 0;
+    for (uint32_t i = 0; i < n; ++i) maxlen = descs[i].length > maxlen ? descs[i].length : maxlen;
+    uint8_t* S = (uint8_t*)malloc((size_t)ora_sender_buffer_size(maxlen));
+    if (!S) return;
+    ora_build_sender_buffer(S, maxlen);
+    for (uint32_t i = 0; i < n; ++i) {
+        const ora_desc* d = &descs[i];
+        const uint32_t completed = d->length;
+        ora_dgram_record rec;
+        memset(&rec, 0, sizeof(rec));
+        rec.completed_bytes = completed;
+        ora_result r;
+        memset(&r, 0, sizeof(r));
+        const uint8_t* buf = arena + d->byte_offset;
+        if (d->byte_offset > arena_bytes || arena_bytes - d->byte_offset < completed) {
+            rec.kind = 5;
+        } else if (completed == 0) {
+            rec.kind = 2;                                   /* zero-byte datagram, :158-167 */
+        } else if (completed < 2) {                         /* < c_udpDatagramProtocolHeaderFlagLength */
+            rec.kind = 3;
+        } else {
+            rec.flag = (uint16_t)(buf[0] | (buf[1] << 8));  /* *reinterpret_cast<unsigned short*>(m_buffer) */
+            if (rec.flag == 0x0000)
+                rec.kind = completed < 26 ? 3 : 0;           /* c_udpDatagramDataHeaderLength */
+            else if (rec.flag == 0x1000)
+                rec.kind = completed < 39 ? 3 : 1;           /* c_udpDatagramConnectionIdHeaderLength */
+            else
+                rec.kind = 4;
+        }
+        if (rec.kind == 0) {
+            rec.sequence_number = ora_i64le(buf + 2);
+            rec.sender_qpc = ora_i64le(buf + 8);
+            rec.sender_qpf = ora_i64le(buf + 16);
+            const uint32_t transferred = completed - 26;
+            ora_verify_buffer(S, buf, 26, 0, transferred, &r);
+            if (counters) {
+                counters->bytes_checked += transferred;
+                counters->buffers_checked += 1;
+                if (r.pass) {
+                    counters->bytes_ok += transferred;
+                } else {
+                    counters->buffers_failed += 1;
+                    counters->mismatched_bytes += r.mismatch_bytes;
+                }
+            }
+        } else {
+            r.flags = rec.kind == 5 ? 1 : 2;
+        }
+        if (records) records[i] = rec;
+        if (results) results[i] = r;
+    }
+    free(S);
+}

@@ -163,3 +163,36 @@ int main(void){
             continue
         f, off = line.split()
         assert getattr(structs[f], f).offset == int(off), f
+
+
+def test_media_stream_struct_layouts_match_c():
+    import ctypes
+    import tempfile
+
+    from ctstraffic_amd import media_stream as M
+    from ctstraffic_amd.types import DGRAM_HEADER_DTYPE, DGRAM_RECORD_DTYPE
+
+    probe = r"""
+#include <stdio.h>
+#include <stddef.h>
+#include "cts_media_stream.h"
+int main(void){
+ printf("%zu %zu %zu %zu\n", sizeof(cts_datagram_record), sizeof(cts_datagram_header),
+        sizeof(cts_media_stream_settings), sizeof(cts_media_stream_stats));
+ printf("%zu %zu %zu %zu\n", offsetof(cts_datagram_record,flag), offsetof(cts_datagram_record,kind),
+        offsetof(cts_datagram_record,completed_bytes), offsetof(cts_media_stream_stats,head_sequence_number));
+ return 0; }
+"""
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "p.c")
+        open(c, "w").write(probe)
+        exe = os.path.join(d, "p")
+        subprocess.run(["gcc", "-std=c11", "-I", INCLUDE, c, "-o", exe], check=True)
+        lines = subprocess.run([exe], capture_output=True, text=True, check=True).stdout.split("\n")
+    a = list(map(int, lines[0].split()))
+    b = list(map(int, lines[1].split()))
+    assert a == [DGRAM_RECORD_DTYPE.itemsize, DGRAM_HEADER_DTYPE.itemsize, ctypes.sizeof(M.Settings),
+                 ctypes.sizeof(M.Stats)]
+    assert b == [DGRAM_RECORD_DTYPE.fields["flag"][1], DGRAM_RECORD_DTYPE.fields["kind"][1],
+                 DGRAM_RECORD_DTYPE.fields["completed_bytes"][1], M.Stats.head_sequence_number.offset]
+    assert DGRAM_RECORD_DTYPE == oracle.DGRAM_RECORD_DTYPE

@@ -76,7 +76,7 @@ static float time_ms(F launch, int reps, hipStream_t s)
     return ms / reps;
 }
 
-int main()
+int main(int argc, char** argv)
 {
     int cus = 0;
     CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
@@ -92,7 +92,7 @@ int main()
     hipStream_t s;
     CHECK(hipStreamCreate(&s));
     const uint64_t nchunks = arena / 16;
-    const int reps = 64;
+    const int reps = argc > 1 ? atoi(argv[1]) : 64;
 
 #define RUN_GS(U, NT, BPC)                                                                                           \
     do {                                                                                                             \
