@@ -169,7 +169,7 @@ def main():
     extras = {}
     cpu = None
     if rank == 0 and world == 1:
-        want = set(x for x in args.extras_only.split(",") if x) or {"fill", "datagram", "host"}
+        want = set(x for x in args.extras_only.split(",") if x) or {"fill", "datagram", "host", "loopback"}
         if not args.no_extras:
             extras = run_extras(engine, torch, W, w, arenas, descs, dev, want)
         if not args.no_cpu_baseline:
@@ -292,16 +292,44 @@ def run_extras(engine, torch, W, w, arenas, descs, dev, want):
             a[pos] = a[pos] ^ torch.from_numpy(w.corrupt_xor).to(dev)
     if "datagram" in want:
         try:
-            wd = W.udp_datagrams(n_datagrams=4 * 1024 * 1024)
+            # config 3 in full: 16 M x 1472-byte MediaStream datagrams (23 GiB resident)
+            from ctstraffic_amd import media_stream as MS
+
+            wd = W.udp_datagrams(n_datagrams=16 * 1024 * 1024)
             ad, dd = W.materialize(engine, wd, device=dev)
             ctr = engine.new_counters()
-            t = _time_kernel(torch, lambda i: engine.verify(ad, dd, max_length_hint=wd.max_length, counters=ctr), 20)
+            t = _time_kernel(torch, lambda i: engine.verify(ad, dd, max_length_hint=wd.max_length, counters=ctr), 10)
             out["datagram_1472_verify_GiBps"] = round(wd.verified_bytes() / t / GIB, 1)
+            out["datagram_1472_verify_GBps_payload"] = round(wd.verified_bytes() / t / 1e9, 1)
             out["datagram_1472_verify_Mdgram_per_s"] = round(wd.n / t / 1e6, 1)
-            out["datagram_config"] = "4M x 1472 B (26 B header skipped), 1/4 of config 3"
+            out["datagram_config"] = "config3: 16M x 1472 B (26 B header skipped; payload bytes counted)"
+            ok = engine.read_counters(ctr)["buffers_failed"] == 11 * len(np.unique(wd.corrupt_buf))
+            out["datagram_parity"] = bool(ok)
+            # the MediaStream client path: header parse + validate + payload verify + 32-byte record
+            recs = torch.empty(wd.n * 32, dtype=torch.uint8, device=dev)
+            res = engine.new_results(wd.n)
+            t = _time_kernel(torch, lambda i: MS.verify(engine, ad, dd, records=recs, results=res), 10)
+            out["media_stream_verify_GiBps"] = round(wd.verified_bytes() / t / GIB, 1)
+            out["media_stream_verify_Mdgram_per_s"] = round(wd.n / t / 1e6, 1)
+            del recs, res
             del ad, dd
         except Exception as e:  # pragma: no cover
             out["datagram_error"] = repr(e)
+    if "loopback" in want:
+        try:
+            # config 1 end to end: loopback TCP push, 8 conns, 64 KiB IO, 1 GiB/conn, -verify:data; the
+            # sender buffer comes from the fill kernel, every received buffer is verified on the GPU
+            from ctstraffic_amd import _pattern_abi as PA
+            from ctstraffic_amd import loopback as LB
+
+            for name, mode in (("deferred", PA.VERIFY_DEFERRED), ("sync", PA.VERIFY_SYNC)):
+                r = LB.run(connections=8, buffer_size=65536, transfer_size=1 << 30, engine=engine, verify_mode=mode)
+                out["loopback_config1_%s" % name] = {
+                    "GBps_recv": round(r["GBps_recv"], 3), "seconds": round(r["seconds"], 3),
+                    "connections_ok": r["connections_ok"], "data_errors": r["data_errors"],
+                    "buffers_verified": r["buffers_verified"]}
+        except Exception as e:  # pragma: no cover
+            out["loopback_error"] = repr(e)
     if "host" in want:
         try:
             # pinned, device-mapped host arena = the recv-buffer container of a GPU-verified ctsIoPattern
@@ -349,6 +377,25 @@ def cpu_baseline(arena, w, seconds):
                 break
         el = time.perf_counter() - t0
         legs[nt] = w.verified_bytes() * reps / el / GIB
+    loop = None
+    try:
+        # the same config-1 loopback run with the oracle answering VerifyBuffer on the CPU (one
+        # verifying thread per connection), i.e. the reference's own arrangement
+        from ctstraffic_amd import _pattern_abi as PA
+        from ctstraffic_amd import loopback as LB
+        from ctstraffic_amd.pattern import shared_buffer_attach
+
+        S = oracle.sender_buffer(65536)
+        shared_buffer_attach(S)
+        hook = PA.BATCH_VERIFIER(oracle.batch_verifier_address())
+        r = LB.run(connections=8, buffer_size=65536, transfer_size=1 << 30, verifier=hook,
+                   verify_mode=PA.VERIFY_SYNC)
+        loop = {"GBps_recv": round(r["GBps_recv"], 3), "connections_ok": r["connections_ok"],
+                "seconds": round(r["seconds"], 3),
+                "sample": "config 1: 8 conns x 1 GiB loopback push, 64 KiB, oracle VerifyBuffer (C) per completion "
+                          "on each connection's receive thread"}
+    except Exception as e:  # pragma: no cover
+        loop = {"error": repr(e)}
     model = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -366,6 +413,7 @@ def cpu_baseline(arena, w, seconds):
                   % (w.n, seconds),
         "single_thread_value": round(legs[1], 2),
         "cpu_model": model,
+        "loopback_config1": loop,
     }
 
 

@@ -290,7 +290,9 @@ __device__ __forceinline__ uint32_t scan_buffer(const Span& s, uint32_t lane)
 {
     const __amdgpu_buffer_rsrc_t r = span_rsrc(s);
     const uint32_t ce = edge_chunk_of(s, lane);
-    const u32x4 edge = buf_load<NT>(r, ce * 16u, 0u);
+    // lanes without an edge/head chunk address past the resource: the range check
+    // returns 0 without a memory request (waves 1..3 of a workgroup fetch nothing)
+    const u32x4 edge = buf_load<NT>(r, edge_chunk_used(s, lane) ? ce * 16u : 0x7FFFFFF0u, 0u);
     uint32_t acc = scan_interior<TEAM, U, NT, SPLIT>(s, r, lane);
     const u32x4 x = chunk_xor(s, ce, edge) & range_mask(ce == 0u ? s.lo : 0u, ce == s.nchunks - 1u ? s.hi_last : 16u);
     acc |= edge_chunk_used(s, lane) ? or4(x) : 0u;
@@ -300,48 +302,51 @@ __device__ __forceinline__ uint32_t scan_buffer(const Span& s, uint32_t lane)
 // Exact scan of a whole span (rare path: a span the fast pass flagged): first
 // differing byte position (relative to the span start) and # differing bytes
 // over this lane's chunks.
-template <int TEAM>
-__device__ __forceinline__ void scan_exact(const Span& s, uint32_t lane, uint32_t& first, uint32_t& count)
+// Exact diff of one chunk's XOR: first differing byte (span-relative) and count.
+__device__ __forceinline__ void take_diff(const Span& s, uint32_t c, u32x4 x, uint32_t& first, uint32_t& count)
 {
-    for (uint32_t c = lane; c < s.nchunks; c += TEAM) {
-        const u32x4 x = chunk_diff_masked(s, c);
 #pragma unroll
-        for (int w = 0; w < 4; ++w) {
-            const uint32_t nz = nonzero_bytes(x[w]);
-            if (nz) {
-                const uint32_t idx = 4u * (uint32_t)w + ((uint32_t)__builtin_ctz(nz) >> 3);
-                const uint32_t pos = 16u * c + idx - s.lo;
-                first = pos < first ? pos : first;
-                count += (uint32_t)__builtin_popcount(nz);
-            }
+    for (int w = 0; w < 4; ++w) {
+        const uint32_t nz = nonzero_bytes(x[w]);
+        if (nz) {
+            const uint32_t idx = 4u * (uint32_t)w + ((uint32_t)__builtin_ctz(nz) >> 3);
+            const uint32_t pos = 16u * c + idx - s.lo;
+            first = pos < first ? pos : first;
+            count += (uint32_t)__builtin_popcount(nz);
         }
     }
 }
 
-// Exact scan of exactly the chunks this lane owns in scan_buffer: interior chunk
-// c (cb0 <= c < nchunks-1) belongs to lane (c-cb0) % TEAM, the edge and head
-// chunks to lanes 0..8 (edge_chunk_of). A team that splits a buffer's verdict across waves needs
-// each wave's exact share to cover exactly what that wave's fast pass flagged.
-template <int TEAM>
+// Exact re-scan of exactly the chunks this lane owns in scan_buffer (interior
+// chunk c in [cb0, nchunks-1) -> lane (c-cb0) % TEAM; edge/head chunks -> lanes
+// 0..8, edge_chunk_of). Only lanes whose fast pass saw a difference call it, so
+// a corrupt buffer costs one lane's re-read, not the team's; the loads go out U
+// at a time like the fast pass, so the re-read is a few round trips, not one per
+// chunk. Yields the lane's first differing byte and differing-byte count.
+template <int TEAM, int U, bool NT>
 __device__ __forceinline__ void scan_exact_owned(const Span& s, uint32_t lane, uint32_t& first, uint32_t& count)
 {
-    auto take = [&](uint32_t c) {
-        const u32x4 x = chunk_diff_masked(s, c);
+    if (s.nchunks == 0) return;
+    const __amdgpu_buffer_rsrc_t r = span_rsrc(s);
+    if (s.nchunks >= 3u) {
+        const uint32_t c_end = s.nchunks - 1u;
+        for (uint32_t cb = s.cb0; cb < c_end; cb += (uint32_t)(TEAM * U)) {
+            u32x4 d[U];
 #pragma unroll
-        for (int w = 0; w < 4; ++w) {
-            const uint32_t nz = nonzero_bytes(x[w]);
-            if (nz) {
-                const uint32_t idx = 4u * (uint32_t)w + ((uint32_t)__builtin_ctz(nz) >> 3);
-                const uint32_t pos = 16u * c + idx - s.lo;
-                first = pos < first ? pos : first;
-                count += (uint32_t)__builtin_popcount(nz);
+            for (int u = 0; u < U; ++u) d[u] = buf_load<NT>(r, (cb + (uint32_t)(u * TEAM) + lane) * 16u, 0u);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t c = cb + (uint32_t)(u * TEAM) + lane;
+                if (c < c_end) take_diff(s, c, chunk_xor(s, c, d[u]), first, count);
             }
         }
-    };
-    if (s.nchunks == 0) return;
-    if (s.nchunks >= 3)
-        for (uint32_t c = s.cb0 + lane; c < s.nchunks - 1u; c += TEAM) take(c);
-    if (edge_chunk_used(s, lane)) take(edge_chunk_of(s, lane));
+    }
+    if (edge_chunk_used(s, lane)) {
+        const uint32_t c = edge_chunk_of(s, lane);
+        const u32x4 x = chunk_xor(s, c, buf_load<NT>(r, c * 16u, 0u)) &
+                        range_mask(c == 0u ? s.lo : 0u, c == s.nchunks - 1u ? s.hi_last : 16u);
+        take_diff(s, c, x, first, count);
+    }
 }
 
 __device__ __forceinline__ uint32_t wave_min(uint32_t v)
@@ -481,8 +486,8 @@ __global__ void __launch_bounds__(kBlock, (U <= 8 ? 8 : 4))
         const Span s = make_span(arena, d);
         const uint32_t acc = scan_buffer<kBlock, U, NT, SPLIT>(s, lane);
         uint32_t first = kNone, count = 0;
-        if (__syncthreads_or(acc != 0u)) {  // rare: exact re-scan + reduction
-            scan_exact<kBlock>(s, lane, first, count);
+        if (__syncthreads_or(acc != 0u)) {  // rare: exact re-scan by the dirty lanes + reduction
+            if (acc != 0u) scan_exact_owned<kBlock, 2, NT>(s, lane, first, count);
             block_reduce_mismatch(first, count);
         }
         if (lane == 0) finish_buffer(s, d, i, first, count, results, ctr[0], conn_first_fail, n_conns);
@@ -541,7 +546,7 @@ __global__ void __launch_bounds__(kBlock, (U <= 8 ? 8 : 4))
         uint32_t flag = 0;
         if (__any(acc != 0u)) {  // rare: exact share of this wave's chunks
             uint32_t first = kNone, count = 0;
-            scan_exact_owned<kBlock>(s, lane, first, count);
+            if (acc != 0u) scan_exact_owned<kBlock, 2, NT>(s, lane, first, count);
             first = wave_min(first);
             count = wave_sum(count);
             if ((lane & 63u) == 0) {
@@ -603,7 +608,7 @@ __global__ void __launch_bounds__(kBlock)
         const uint32_t acc = scan_buffer<64, U, NT>(s, lane);
         uint32_t first = kNone, count = 0;
         if (__any(acc != 0u)) {
-            scan_exact<64>(s, lane, first, count);
+            if (acc != 0u) scan_exact_owned<64, 2, NT>(s, lane, first, count);
             first = wave_min(first);
             count = wave_sum(count);
         }
@@ -741,7 +746,7 @@ __global__ void __launch_bounds__(kBlock)
         const uint32_t acc = scan_buffer<64, U, NT>(s, lane);
         uint32_t first = kNone, count = 0;
         if (__any(acc != 0u)) {
-            scan_exact<64>(s, lane, first, count);
+            if (acc != 0u) scan_exact_owned<64, 2, NT>(s, lane, first, count);
             first = wave_min(first);
             count = wave_sum(count);
         }

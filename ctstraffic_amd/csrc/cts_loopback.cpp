@@ -1,0 +1,259 @@
+// cts_loopback.cpp — loopback-TCP feeder (include/cts_loopback.h): blocking
+// POSIX sockets, one thread per connection side, each driving a cts_io_pattern
+// exactly as the reference's IOCP functor drives ctsIoPattern:
+// InitiateIo -> post the IO -> CompleteIo(task, transferred, status)
+// (ctsTraffic/ctsSendRecvIocp.cpp:130-300, 335-415). One IO is in flight per
+// side (PrePostRecvs = PrePostSends = 1, what -Verify:data requires for TCP,
+// ctsConfig.cpp:3440-3446), so blocking calls preserve the reference's ordering.
+#include <arpa/inet.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <cerrno>
+#include <chrono>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "cts_loopback.h"
+
+namespace {
+
+// Winsock codes the pattern's state machine distinguishes (ctsIOPatternState.hpp:269-275)
+uint32_t wsa_status(int err)
+{
+    switch (err) {
+    case ECONNRESET: return 10054;    // WSAECONNRESET
+    case ECONNABORTED: return 10053;  // WSAECONNABORTED
+    case ETIMEDOUT: return 10060;     // WSAETIMEDOUT
+    case EPIPE: return 10054;
+    default: return 20000u + (uint32_t)err;
+    }
+}
+
+// returns 0 or a wsa_status
+uint32_t send_all(int fd, const char* p, uint32_t n)
+{
+    while (n > 0) {
+        const ssize_t k = ::send(fd, p, n, MSG_NOSIGNAL);
+        if (k < 0) {
+            if (errno == EINTR) continue;
+            return wsa_status(errno);
+        }
+        p += k;
+        n -= (uint32_t)k;
+    }
+    return 0;
+}
+
+// one recv (partial completions are part of the path: they shift the next buffer's phase)
+uint32_t recv_some(int fd, char* p, uint32_t n, uint32_t* got, bool wait_all)
+{
+    *got = 0;
+    for (;;) {
+        const ssize_t k = ::recv(fd, p + *got, n - *got, 0);
+        if (k < 0) {
+            if (errno == EINTR) continue;
+            return wsa_status(errno);
+        }
+        *got += (uint32_t)k;
+        if (k == 0 || !wait_all || *got == n) return 0;
+    }
+}
+
+struct SideResult {
+    int status = CTS_IO_FAILED;
+    uint32_t last_error = 0;
+    cts_pattern_stats stats{};
+};
+
+void run_side(int* fdslot, cts_io_pattern* p, bool inject, uint32_t inject_index, SideResult* out)
+{
+    const int fd = *fdslot;
+    std::vector<char> scratch;
+    uint32_t data_sends = 0;
+    int st = CTS_IO_CONTINUE;
+    for (;;) {
+        cts_task t{};
+        if (cts_io_pattern_initiate_io(p, &t) != CTS_OK) {
+            st = CTS_IO_FAILED;
+            break;
+        }
+        uint32_t transferred = 0, status = 0;
+        switch (t.io_action) {
+        case CTS_TASK_SEND: {
+            const char* src = t.buffer + t.buffer_offset;
+            if (inject && t.track_io && data_sends++ == inject_index && t.buffer_length > 0) {
+                scratch.assign(src, src + t.buffer_length);  // fault injection: one flipped byte on the wire
+                scratch[t.buffer_length / 2] ^= 0x5A;
+                src = scratch.data();
+            }
+            status = send_all(fd, src, t.buffer_length);
+            transferred = status == 0 ? t.buffer_length : 0;
+            break;
+        }
+        case CTS_TASK_RECV: {
+            // protocol messages are fixed-size; data recvs complete with whatever arrived
+            const bool whole = t.buffer_type == CTS_BUFFER_TCP_CONNECTION_ID ||
+                               t.buffer_type == CTS_BUFFER_COMPLETION_MESSAGE;
+            status = recv_some(fd, t.buffer + t.buffer_offset, t.buffer_length, &transferred, whole);
+            break;
+        }
+        case CTS_TASK_GRACEFUL_SHUTDOWN:
+            if (::shutdown(fd, SHUT_WR) != 0) status = wsa_status(errno);
+            break;
+        case CTS_TASK_HARD_SHUTDOWN: {
+            linger l{1, 0};  // RST on close
+            (void)::setsockopt(fd, SOL_SOCKET, SO_LINGER, &l, sizeof(l));
+            break;
+        }
+        case CTS_TASK_NONE:
+            // one IO at a time: nothing to post means the pattern is waiting on nothing -> done
+            break;
+        default: break;
+        }
+        if (t.io_action == CTS_TASK_NONE) {
+            st = cts_io_pattern_flush(p);
+            break;
+        }
+        st = cts_io_pattern_complete_io(p, &t, transferred, status);
+        if (st != CTS_IO_CONTINUE) break;
+    }
+    // the side closes its socket as soon as its pattern is done (ctsSocketState
+    // Closing, ctsSocketState.cpp:213-264): gracefully after CompletedIo — the
+    // peer may still be waiting for this FIN — and with RST after a failure, which
+    // unblocks a peer stuck in send/recv
+    if (st != CTS_IO_COMPLETED) {
+        linger l{1, 0};
+        (void)::setsockopt(fd, SOL_SOCKET, SO_LINGER, &l, sizeof(l));
+    }
+    ::close(fd);
+    *fdslot = -1;
+    out->status = st;
+    out->last_error = cts_io_pattern_last_error(p);
+    (void)cts_io_pattern_get_stats(p, &out->stats);
+}
+
+}  // namespace
+
+extern "C" int cts_loopback_run(const cts_loopback_config* cfg, cts_engine* engine, cts_batch_verifier hook,
+                                void* hook_ctx, cts_loopback_result* out)
+{
+    if (cfg == nullptr || out == nullptr || cfg->connections == 0 || cfg->buffer_size == 0) return CTS_E_INVALID;
+    // one blocking IO per side: Duplex (concurrent send + recv on one socket) needs an async functor
+    if (cfg->io_pattern != 0 && cfg->io_pattern != CTS_PATTERN_PUSH && cfg->io_pattern != CTS_PATTERN_PULL)
+        return CTS_E_INVALID;
+    if (engine == nullptr && hook == nullptr && cfg->verify_buffers) return CTS_E_INVALID;
+    *out = cts_loopback_result{};
+    if (engine != nullptr) {
+        const int rc = cts_shared_buffer_init(engine, cfg->buffer_size);
+        if (rc != CTS_OK) return rc;
+    }
+    const int lfd = ::socket(AF_INET, SOCK_STREAM, 0);
+    if (lfd < 0) return CTS_E_INVALID;
+    int one = 1;
+    (void)::setsockopt(lfd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+    sockaddr_in addr{};
+    addr.sin_family = AF_INET;
+    addr.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+    addr.sin_port = 0;
+    socklen_t alen = sizeof(addr);
+    if (::bind(lfd, (sockaddr*)&addr, sizeof(addr)) != 0 || ::listen(lfd, (int)cfg->connections) != 0 ||
+        ::getsockname(lfd, (sockaddr*)&addr, &alen) != 0) {
+        ::close(lfd);
+        return CTS_E_INVALID;
+    }
+    const uint32_t n = cfg->connections;
+    auto make_cfg = [&](bool listening) {
+        cts_pattern_config c{};
+        c.io_pattern = cfg->io_pattern ? cfg->io_pattern : CTS_PATTERN_PUSH;
+        c.protocol = CTS_PROTOCOL_TCP;
+        c.listening = listening ? 1u : 0u;
+        c.verify_buffers = cfg->verify_buffers;
+        c.pre_post_recvs = 1;
+        c.pre_post_sends = 1;
+        c.buffer_size_low = cfg->buffer_size;
+        c.tcp_shutdown = CTS_SHUTDOWN_GRACEFUL;
+        c.transfer_size = cfg->transfer_size;
+        c.verify_mode = cfg->verify_mode;
+        c.batch_buffers = cfg->batch_buffers ? cfg->batch_buffers : 256u;
+        c.batch_bytes = (uint64_t)c.batch_buffers * cfg->buffer_size;
+        return c;
+    };
+    std::vector<cts_io_pattern*> pats(2 * n, nullptr);
+    int rc = CTS_OK;
+    for (uint32_t i = 0; i < 2 * n && rc == CTS_OK; ++i) {
+        const cts_pattern_config c = make_cfg(i >= n);  // [0,n) clients, [n,2n) servers
+        rc = cts_io_pattern_create(&c, engine, &pats[i]);
+        if (rc == CTS_OK && hook != nullptr) rc = cts_io_pattern_set_verifier(pats[i], hook, hook_ctx);
+    }
+    if (rc != CTS_OK) {
+        for (auto* p : pats)
+            if (p) cts_io_pattern_destroy(p);
+        ::close(lfd);
+        return rc;
+    }
+    cts_status_details before{};
+    (void)cts_status_details_read(&before);
+    std::vector<SideResult> res(2 * n);
+    std::vector<int> fds(2 * n, -1);
+    std::vector<std::thread> threads;
+    const auto t0 = std::chrono::steady_clock::now();
+    auto tune = [&](int fd) {
+        (void)::setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+        if (cfg->socket_buffer_bytes) {
+            const int b = (int)cfg->socket_buffer_bytes;
+            (void)::setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &b, sizeof(b));
+            (void)::setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &b, sizeof(b));
+        }
+    };
+    for (uint32_t i = 0; i < n; ++i) {  // clients connect; the listen backlog holds them
+        const int fd = ::socket(AF_INET, SOCK_STREAM, 0);
+        if (fd < 0 || ::connect(fd, (sockaddr*)&addr, sizeof(addr)) != 0) {
+            if (fd >= 0) ::close(fd);
+            continue;
+        }
+        tune(fd);
+        fds[i] = fd;
+    }
+    for (uint32_t i = 0; i < n; ++i) {  // servers accept in connect order
+        const int fd = ::accept(lfd, nullptr, nullptr);
+        if (fd < 0) break;
+        tune(fd);
+        fds[n + i] = fd;
+    }
+    std::vector<bool> connected0(2 * n);
+    for (uint32_t i = 0; i < 2 * n; ++i) connected0[i] = fds[i] >= 0;
+    for (uint32_t i = 0; i < 2 * n; ++i) {
+        if (fds[i] < 0) continue;
+        const bool inject = i < n && i == cfg->corrupt_connection;
+        threads.emplace_back(run_side, &fds[i], pats[i], inject, cfg->corrupt_send_index, &res[i]);
+    }
+    const std::vector<bool>& connected = connected0;
+    for (auto& t : threads) t.join();
+    const auto t1 = std::chrono::steady_clock::now();
+    for (int fd : fds)
+        if (fd >= 0) ::close(fd);
+    ::close(lfd);
+    cts_status_details after{};
+    (void)cts_status_details_read(&after);
+    out->seconds = std::chrono::duration<double>(t1 - t0).count();
+    out->bytes_sent = after.bytes_sent - before.bytes_sent;
+    out->bytes_recv = after.bytes_recv - before.bytes_recv;
+    for (uint32_t i = 0; i < n; ++i) {
+        const SideResult& c = res[i];
+        const SideResult& s = res[n + i];
+        const bool ok = connected[i] && connected[n + i] && c.status == CTS_IO_COMPLETED && s.status == CTS_IO_COMPLETED;
+        if (ok) ++out->connections_ok;
+        else ++out->connections_failed;
+        if (c.last_error == CTS_STATUS_ERROR_DATA_DID_NOT_MATCH_BIT_PATTERN ||
+            s.last_error == CTS_STATUS_ERROR_DATA_DID_NOT_MATCH_BIT_PATTERN)
+            ++out->data_errors;
+        out->buffers_verified += c.stats.buffers_verified + s.stats.buffers_verified;
+    }
+    for (auto* p : pats) cts_io_pattern_destroy(p);
+    return CTS_OK;
+}

@@ -1,0 +1,57 @@
+"""Loopback-TCP feeder (include/cts_loopback.h): the reference's config 1 end to end
+("-Pattern:push -Connections:8 -Buffer:65536 -Transfer:1GiB -Verify:data" over
+loopback) with the sender buffer written by the fill kernel and every received
+buffer verified by the verify kernel."""
+from __future__ import annotations
+
+import ctypes
+
+from . import _pattern_abi as A
+from ._lib import check, lib
+
+
+class LoopbackConfig(ctypes.Structure):
+    _fields_ = [("connections", ctypes.c_uint32), ("io_pattern", ctypes.c_uint32), ("buffer_size", ctypes.c_uint32),
+                ("verify_buffers", ctypes.c_uint32), ("transfer_size", ctypes.c_uint64),
+                ("verify_mode", ctypes.c_uint32), ("batch_buffers", ctypes.c_uint32),
+                ("corrupt_connection", ctypes.c_uint32), ("corrupt_send_index", ctypes.c_uint32),
+                ("socket_buffer_bytes", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+
+
+class LoopbackResult(ctypes.Structure):
+    _fields_ = [("seconds", ctypes.c_double), ("bytes_sent", ctypes.c_uint64), ("bytes_recv", ctypes.c_uint64),
+                ("buffers_verified", ctypes.c_uint64), ("connections_ok", ctypes.c_uint32),
+                ("connections_failed", ctypes.c_uint32), ("data_errors", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32)]
+
+    def as_dict(self) -> dict:
+        d = {f: getattr(self, f) for f, _ in self._fields_ if f != "reserved"}
+        d["GBps_recv"] = self.bytes_recv / self.seconds / 1e9 if self.seconds > 0 else 0.0
+        return d
+
+
+def declare(L: ctypes.CDLL) -> None:
+    fn = L.cts_loopback_run
+    fn.argtypes = [ctypes.POINTER(LoopbackConfig), ctypes.c_void_p, A.BATCH_VERIFIER, ctypes.c_void_p,
+                   ctypes.POINTER(LoopbackResult)]
+    fn.restype = ctypes.c_int
+
+
+def run(connections=8, buffer_size=65536, transfer_size=1 << 30, engine=None, verifier=None,
+        io_pattern=A.PATTERN_PUSH, verify=True, verify_mode=A.VERIFY_DEFERRED, batch_buffers=0,
+        corrupt_connection=None, corrupt_send_index=0, socket_buffer_bytes=0) -> dict:
+    """One loopback run. ``verifier`` (a cts_batch_verifier or a python fn(arena, descs) -> results) replaces the
+    engine's kernel (test harnesses / the CPU baseline)."""
+    from .pattern import batch_verifier
+
+    cfg = LoopbackConfig(connections, io_pattern, buffer_size, int(verify), transfer_size, verify_mode, batch_buffers,
+                         0xFFFFFFFF if corrupt_connection is None else corrupt_connection, corrupt_send_index,
+                         socket_buffer_bytes, 0)
+    hook = None
+    if verifier is not None:
+        hook = verifier if isinstance(verifier, A.BATCH_VERIFIER) else batch_verifier(verifier)
+    res = LoopbackResult()
+    check("cts_loopback_run", lib().cts_loopback_run(ctypes.byref(cfg), None if engine is None else engine._h,
+                                                     hook if hook is not None else A.BATCH_VERIFIER(), None,
+                                                     ctypes.byref(res)))
+    return res.as_dict()

@@ -1,0 +1,59 @@
+/*
+ * cts_loopback.h — a Linux loopback-TCP feeder for the data-integrity path
+ * (SURVEY.md §8f-3): the role of the reference's IOCP IO functor
+ * (ctsTraffic/ctsSendRecvIocp.cpp:335-415, ctsSendRecvProcessTask :130-300)
+ * played with blocking POSIX sockets, one thread per connection side, over the
+ * ctsIoPattern mirror of cts_pattern.h. Clients send g_senderSharedBuffer
+ * (written by the gfx950 fill kernel) and servers verify every received buffer
+ * on the GPU, so a run is the reference's config 1 end to end
+ * ("-Pattern:push -Connections:8 -Buffer:65536 -Transfer:1GiB -Verify:data"
+ * over loopback), host memory and the kernel stack included.
+ */
+#ifndef CTS_LOOPBACK_H
+#define CTS_LOOPBACK_H
+
+#include <stdint.h>
+
+#include "cts_engine.h"
+#include "cts_pattern.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct cts_loopback_config {
+    uint32_t connections;           /* -Connections (client/server pairs) */
+    uint32_t io_pattern;            /* CTS_PATTERN_PUSH / PULL (one blocking IO per side: no Duplex) */
+    uint32_t buffer_size;           /* -Buffer */
+    uint32_t verify_buffers;        /* -Verify:data */
+    uint64_t transfer_size;         /* -Transfer, per connection */
+    uint32_t verify_mode;           /* CTS_VERIFY_SYNC / CTS_VERIFY_DEFERRED */
+    uint32_t batch_buffers;         /* DEFERRED batch (0 = default) */
+    uint32_t corrupt_connection;    /* fault injection: connection index whose sender flips a byte, or ~0u */
+    uint32_t corrupt_send_index;    /* ... in its n-th data send (0-based) */
+    uint32_t socket_buffer_bytes;   /* SO_SNDBUF / SO_RCVBUF (0 = system default) */
+    uint32_t reserved;
+} cts_loopback_config;
+
+typedef struct cts_loopback_result {
+    double seconds;                 /* wall time from the first connect to the last completed connection */
+    uint64_t bytes_sent;            /* TcpStatusDetails.m_bytesSent delta */
+    uint64_t bytes_recv;            /* TcpStatusDetails.m_bytesRecv delta */
+    uint64_t buffers_verified;      /* sum over server patterns */
+    uint32_t connections_ok;        /* both sides CompletedIo */
+    uint32_t connections_failed;    /* any side FailedIo or a socket error */
+    uint32_t data_errors;           /* patterns that latched DATA_DID_NOT_MATCH_BIT_PATTERN (README "DataError") */
+    uint32_t reserved;
+} cts_loopback_result;
+
+/* Runs cfg->connections loopback connections to completion. engine may be NULL
+ * only when verify_buffers == 0 or hook != NULL (hook: see cts_batch_verifier).
+ * Returns CTS_OK when the run finished (connection outcomes are in *out). */
+int cts_loopback_run(const cts_loopback_config* cfg, cts_engine* engine, cts_batch_verifier hook, void* hook_ctx,
+                     cts_loopback_result* out);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+#endif /* CTS_LOOPBACK_H */

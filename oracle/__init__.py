@@ -208,3 +208,8 @@ def media_stream_verify(arena: np.ndarray, descs: np.ndarray):
     c = OraCounters()
     lib().ora_media_stream_verify(_ptr(arena), arena.size, _ptr(descs), n, _ptr(recs), _ptr(results), ctypes.byref(c))
     return recs, results, c.as_dict()
+
+
+def batch_verifier_address() -> int:
+    """Address of ora_batch_verifier (a cts_batch_verifier): the CPU VerifyBuffer for C callers."""
+    return ctypes.cast(lib().ora_batch_verifier, ctypes.c_void_p).value

@@ -312,3 +312,34 @@ void ora_media_stream_verify(const uint8_t* arena, uint64_t arena_bytes, const o
     }
     free(S);
 }
+
+/* g_senderSharedBuffer as the reference keeps it: built once per process (InitOnceIoPatternCallback),
+ * here for buffers up to 1 MiB. */
+#define ORA_HOOK_MAX_BUFFER (1u << 20)
+static uint8_t* g_hook_sender;
+static pthread_once_t g_hook_once = PTHREAD_ONCE_INIT;
+static void build_hook_sender(void)
+{
+    g_hook_sender = (uint8_t*)malloc((size_t)ora_sender_buffer_size(ORA_HOOK_MAX_BUFFER));
+    if (g_hook_sender) ora_build_sender_buffer(g_hook_sender, ORA_HOOK_MAX_BUFFER);
+}
+
+int ora_batch_verifier(void* ctx, const uint8_t* arena, uint64_t arena_bytes, const ora_desc* descs, uint32_t n,
+                       ora_result* results)
+{
+    (void)ctx;
+    pthread_once(&g_hook_once, build_hook_sender);
+    if (!g_hook_sender || max_verified_len(descs, n) > ORA_HOOK_MAX_BUFFER)
+        return ora_verify_batch(arena, arena_bytes, descs, n, results, NULL, NULL, 0, 1);
+    for (uint32_t i = 0; i < n; ++i) {
+        const ora_desc* d = &descs[i];
+        if (desc_bad(d, arena_bytes)) {
+            memset(&results[i], 0, sizeof(results[i]));
+            results[i].flags = 1;
+            continue;
+        }
+        ora_verify_buffer(g_hook_sender, arena + d->byte_offset, d->skip_head, d->expected_pattern_offset,
+                          d->length - d->skip_head, &results[i]);
+    }
+    return 0;
+}

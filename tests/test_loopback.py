@@ -1,0 +1,64 @@
+"""Loopback-TCP feeder: whole connections over 127.0.0.1
+through the ctsIoPattern mirror, the reference's config 1 in miniature.
+
+CPU: the oracle answers VerifyBuffer through the pattern's batch-verifier hook
+(the reference's tests replace ctsConfig with fakes the same way); GPU: the
+fill kernel writes the sender buffer and the verify kernel checks every
+received buffer. A fault-injection knob flips one byte on the wire.
+"""
+import pytest
+
+import oracle
+from ctstraffic_amd import _pattern_abi as A
+from ctstraffic_amd import loopback
+from ctstraffic_amd.pattern import shared_buffer_attach
+
+_SENDER = oracle.sender_buffer(2 * 65536)
+
+
+def _oracle_verifier(arena, descs):
+    return oracle.verify_batch(arena, descs)[0]
+
+
+@pytest.mark.parametrize("mode", [A.VERIFY_SYNC, A.VERIFY_DEFERRED], ids=["sync", "deferred"])
+@pytest.mark.parametrize("pattern", [A.PATTERN_PUSH, A.PATTERN_PULL], ids=["push", "pull"])
+def test_loopback_clean_cpu(mode, pattern):
+    shared_buffer_attach(_SENDER)
+    r = loopback.run(connections=4, buffer_size=65536, transfer_size=3 * 1024 * 1024 + 12345, verifier=_oracle_verifier,
+                     io_pattern=pattern, verify_mode=mode, batch_buffers=16)
+    assert r["connections_ok"] == 4 and r["connections_failed"] == 0 and r["data_errors"] == 0
+    # every data byte crosses once; connection ids (37 B) and DONE (4 B) are counted too (ctsIOPattern.cpp:505-516)
+    data = 4 * (3 * 1024 * 1024 + 12345)
+    assert r["bytes_recv"] == data + 4 * (37 + 4)
+    assert r["buffers_verified"] >= data // 65536
+
+
+@pytest.mark.parametrize("mode", [A.VERIFY_SYNC, A.VERIFY_DEFERRED], ids=["sync", "deferred"])
+def test_loopback_detects_wire_corruption_cpu(mode):
+    shared_buffer_attach(_SENDER)
+    r = loopback.run(connections=3, buffer_size=16384, transfer_size=2 * 1024 * 1024, verifier=_oracle_verifier,
+                     verify_mode=mode, batch_buffers=8, corrupt_connection=1, corrupt_send_index=17)
+    assert r["data_errors"] == 1 and r["connections_failed"] == 1 and r["connections_ok"] == 2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [A.VERIFY_SYNC, A.VERIFY_DEFERRED], ids=["sync", "deferred"])
+def test_loopback_gpu(engine, mode):
+    r = loopback.run(connections=4, buffer_size=65536, transfer_size=16 * 1024 * 1024 + 7, engine=engine,
+                     verify_mode=mode)
+    assert r["connections_ok"] == 4 and r["data_errors"] == 0
+    r = loopback.run(connections=4, buffer_size=65536, transfer_size=8 * 1024 * 1024, engine=engine, verify_mode=mode,
+                     corrupt_connection=2, corrupt_send_index=40)
+    assert r["data_errors"] == 1 and r["connections_ok"] == 3
+
+
+def test_loopback_with_c_oracle_hook():
+    """The CPU baseline's arrangement: the oracle's C entry point as the pattern's verifier."""
+    shared_buffer_attach(_SENDER)
+    hook = A.BATCH_VERIFIER(oracle.batch_verifier_address())
+    r = loopback.run(connections=8, buffer_size=65536, transfer_size=8 * 1024 * 1024, verifier=hook,
+                     verify_mode=A.VERIFY_SYNC)
+    assert r["connections_ok"] == 8 and r["data_errors"] == 0
+    r = loopback.run(connections=2, buffer_size=65536, transfer_size=8 * 1024 * 1024, verifier=hook,
+                     verify_mode=A.VERIFY_SYNC, corrupt_connection=0, corrupt_send_index=3)
+    assert r["data_errors"] == 1

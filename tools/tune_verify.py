@@ -28,13 +28,14 @@ def main():
     p.add_argument("--nt", default="1,0")
     p.add_argument("--workload", default="config2")
     p.add_argument("--buffers", type=int, default=4096)
+    p.add_argument("--corrupt-rate", type=int, default=1024, help="1 in N buffers corrupted (0 = none)")
     args = p.parse_args()
     torch.cuda.set_device(0)
     eng = Engine(0)
     if args.workload == "config2":
-        w = W.tcp_resident(n_buffers=args.buffers)
+        w = W.tcp_resident(n_buffers=args.buffers, corrupt_rate=args.corrupt_rate)
     else:
-        w = W.udp_datagrams(n_datagrams=4 * 1024 * 1024)
+        w = W.udp_datagrams(n_datagrams=4 * 1024 * 1024, corrupt_rate=args.corrupt_rate)
     arenas, descs = [], None
     for _ in range(args.arenas):
         a, descs = W.materialize(eng, w)
