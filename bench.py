@@ -42,6 +42,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extras", action="store_true", help="skip fill / datagram / host-path extras")
     p.add_argument("--extras-only", default="", help="comma list: fill,datagram,host")
+    p.add_argument("--stream", choices=["new", "default"], default="new",
+                   help="launch stream: a new HIP stream or the device's default stream")
     p.add_argument("--graph", action="store_true", help="replay the timed steps from a HIP graph (measured: no gain)")
     return p.parse_args()
 
@@ -68,7 +70,7 @@ def main():
         D.init("nccl", device=torch.device(dev))
 
     engine = Engine(local)
-    stream = torch.cuda.Stream()
+    stream = torch.cuda.Stream() if args.stream == "new" else torch.cuda.current_stream()
 
     # ---- workload (per rank: weak scaling) --------------------------------------------------
     # each rank verifies its own shard of connections (hash(conn) mod G): config 2's batch per GPU

@@ -684,6 +684,16 @@ __device__ __forceinline__ int64_t load_i64_unaligned(const uint8_t* p)
     return (int64_t)v;
 }
 
+// Lane l (< 26) holds header byte l (0 past the completed bytes); returns the
+// little-endian i64 at byte offset `at` via v_readlane (wave-uniform, no memory).
+__device__ __forceinline__ int64_t header_i64(uint32_t hb, int at)
+{
+    uint64_t v = 0;
+#pragma unroll
+    for (int b = 0; b < 8; ++b) v |= (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hb, at + b) << (8 * b);
+    return (int64_t)v;
+}
+
 template <int U, bool NT>
 __global__ void __launch_bounds__(kBlock)
     media_stream_verify_kernel(const uint8_t* __restrict__ arena, uint64_t arena_bytes,
@@ -697,12 +707,32 @@ __global__ void __launch_bounds__(kBlock)
     const uint32_t nw = gridDim.x * WAVES;
     __shared__ uint64_t ctr[WAVES][5];
     zero_counters<WAVES>(ctr);
-    for (uint32_t i = blockIdx.x * WAVES + wave; i < n; i += nw) {
-        cts_buf_desc d = descs[i];
+    uint32_t i = blockIdx.x * WAVES + wave;
+    cts_buf_desc dn;
+    if (i < n) dn = descs[i];
+    for (; i < n; i += nw) {
+        cts_buf_desc d = dn;
+        if (i + nw < n) dn = descs[i + nw];
         const uint32_t completed = d.length;
         const bool bad = d.byte_offset > arena_bytes || arena_bytes - d.byte_offset < (uint64_t)completed;
-        const uint8_t* dg = arena + d.byte_offset;
-        // header: every lane computes the same scalar answer from the first bytes
+        // The header bytes and the payload stream are loaded together: the payload is
+        // verified speculatively (as a DATA datagram) while the header is in flight, and
+        // discarded if the header says otherwise — no dependent round trip per datagram.
+        // Lane l < 26 loads header byte l through a resource covering only the completed
+        // bytes (out of range -> 0, no request).
+        const __amdgpu_buffer_rsrc_t hr = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint8_t*>(arena + (bad ? 0 : d.byte_offset)), (short)0, (int)(bad ? 0u : completed), 0x00020000);
+        const uint32_t hb = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(hr, lane < CTS_UDP_DATA_HEADER_LENGTH ? lane : 0x7FFFFFF0u, 0u, 0);
+        const bool maybe_data = !bad && completed >= CTS_UDP_DATA_HEADER_LENGTH;
+        d.skip_head = CTS_UDP_DATA_HEADER_LENGTH;
+        d.expected_pattern_offset = 0;
+        if (!maybe_data) {
+            d.byte_offset = 0;  // an empty span: scan_buffer issues no in-range loads
+            d.length = CTS_UDP_DATA_HEADER_LENGTH;
+        }
+        const Span s = make_span(arena, d);
+        const uint32_t acc = scan_buffer<64, U, NT>(s, lane);
+        // header: ctsMediaStreamMessage::ValidateBufferLengthFromTask (ctsMediaStreamProtocol.hpp:284-329)
         uint32_t flag = 0, kind;
         if (bad) {
             kind = CTS_DGRAM_BAD_DESC;
@@ -711,7 +741,7 @@ __global__ void __launch_bounds__(kBlock)
         } else if (completed < CTS_UDP_FLAG_LENGTH) {
             kind = CTS_DGRAM_SHORT;
         } else {
-            flag = (uint32_t)dg[0] | ((uint32_t)dg[1] << 8);
+            flag = (uint32_t)__builtin_amdgcn_readlane((int)hb, 0) | ((uint32_t)__builtin_amdgcn_readlane((int)hb, 1) << 8);
             if (flag == CTS_UDP_FLAG_DATA)
                 kind = completed < CTS_UDP_DATA_HEADER_LENGTH ? CTS_DGRAM_SHORT : CTS_DGRAM_DATA;
             else if (flag == CTS_UDP_FLAG_ID)
@@ -719,20 +749,19 @@ __global__ void __launch_bounds__(kBlock)
             else
                 kind = CTS_DGRAM_UNKNOWN;
         }
-        kind = (uint32_t)__builtin_amdgcn_readfirstlane((int)kind);
+        const bool data = kind == CTS_DGRAM_DATA;
         if (records != nullptr && lane == 0) {
             cts_datagram_record rec;
-            const bool data = kind == CTS_DGRAM_DATA;
-            rec.sequence_number = data ? load_i64_unaligned(dg + 2) : 0;
-            rec.sender_qpc = data ? load_i64_unaligned(dg + 8) : 0;
-            rec.sender_qpf = data ? load_i64_unaligned(dg + 16) : 0;
+            rec.sequence_number = data ? header_i64(hb, 2) : 0;   // GetSequenceNumberFromTask
+            rec.sender_qpc = data ? header_i64(hb, 8) : 0;        // ctsIOPatternMediaStream.cpp:218
+            rec.sender_qpf = data ? header_i64(hb, 16) : 0;       // :219
             rec.flag = (uint16_t)flag;
             rec.kind = (uint8_t)kind;
             rec.reserved = 0;
             rec.completed_bytes = completed;
             records[i] = rec;
         }
-        if (kind != CTS_DGRAM_DATA) {
+        if (!data) {
             if (results != nullptr && lane == 0) {
                 cts_verify_result r{};
                 r.flags = kind == CTS_DGRAM_BAD_DESC ? CTS_RESULT_FLAG_BAD_DESC : CTS_RESULT_FLAG_NOT_DATA;
@@ -740,10 +769,6 @@ __global__ void __launch_bounds__(kBlock)
             }
             continue;
         }
-        d.skip_head = CTS_UDP_DATA_HEADER_LENGTH;
-        d.expected_pattern_offset = 0;
-        const Span s = make_span(arena, d);
-        const uint32_t acc = scan_buffer<64, U, NT>(s, lane);
         uint32_t first = kNone, count = 0;
         if (__any(acc != 0u)) {
             if (acc != 0u) scan_exact_owned<64, 2, NT>(s, lane, first, count);

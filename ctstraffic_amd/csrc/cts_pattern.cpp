@@ -326,6 +326,13 @@ struct cts_io_pattern {
     std::vector<cts_verify_result> hres;
     std::vector<Queued> queue;
     uint64_t stage_used = 0;
+    // DEFERRED zero-copy ring: the recv container holds BatchCapacity()+2 buffer slots and a
+    // completed buffer's slot is not handed out again before its batch was verified, so a
+    // batch is verified in place (no staging copy)
+    bool ring = false, queue_in_ring = false;
+    uint32_t ring_slots = 0, ring_next = 0;
+    char* ring_base = nullptr;
+    uint64_t ring_bytes = 0;
 
     uint32_t GetBufferSize()  // ctsConfig.cpp:4679-4684
     {
@@ -385,7 +392,9 @@ struct cts_io_pattern {
             for (auto& b : m_recvBufferFreeList) b = g_shared.receiver.data();
             return CTS_OK;
         }
-        const uint64_t bytes = (uint64_t)max_buffer_size * recvCount;
+        ring = Deferred();
+        ring_slots = ring ? BatchCapacity() + recvCount + 1 : recvCount;
+        const uint64_t bytes = (uint64_t)max_buffer_size * ring_slots;
         char* base = nullptr;
         if (engine != nullptr && hook == nullptr) {
             const int rc = recv_pinned.alloc(engine, bytes ? bytes : 16);
@@ -396,7 +405,20 @@ struct cts_io_pattern {
             base = recv_plain.data();
         }
         for (uint32_t i = 0; i < recvCount; ++i) m_recvBufferFreeList[i] = base + (size_t)i * max_buffer_size;
+        ring_base = base;
+        ring_bytes = bytes;
+        ring_next = recvCount;
         return CTS_OK;
+    }
+
+    // the buffer to put back on the free list after a completion (ctsIOPattern.cpp:371-376):
+    // the completed one, or in ring mode the next ring slot (the completed one waits for its batch)
+    char* RecycledRecvBuffer(char* completed)
+    {
+        if (!ring) return completed;
+        char* b = ring_base + (size_t)(ring_next % ring_slots) * max_buffer_size;
+        ++ring_next;
+        return b;
     }
 
     void CreateSendBuffers()  // ctsIOPattern.cpp:195-217
@@ -531,8 +553,47 @@ struct cts_io_pattern {
     uint32_t BatchCapacity() const { return cfg.batch_buffers ? cfg.batch_buffers : 1024u; }
 
     // Queue one buffer for the next batch (DEFERRED). Returns CTS_OK.
+    bool InRing(const char* p, uint32_t n) const
+    {
+        return ring && p >= ring_base && p + n <= ring_base + ring_bytes;
+    }
+
+    int EnsureBatchDescs()
+    {
+        if (hook != nullptr) {
+            if (hdesc.size() < BatchCapacity()) {
+                hdesc.resize(BatchCapacity());
+                hres.resize(BatchCapacity());
+            }
+            return CTS_OK;
+        }
+        if (engine == nullptr) return CTS_E_INVALID;
+        int rc;
+        if (stage_desc.host == nullptr) {
+            if ((rc = stage_desc.alloc(engine, sizeof(cts_buf_desc) * (uint64_t)BatchCapacity())) != CTS_OK) return rc;
+            if ((rc = stage_res.alloc(engine, sizeof(cts_verify_result) * (uint64_t)BatchCapacity())) != CTS_OK) return rc;
+        }
+        return CTS_OK;
+    }
+
     int Enqueue(const cts_task& t, uint32_t transferred, uint64_t recv_after)
     {
+        const char* src = t.buffer + t.buffer_offset;
+        if (InRing(src, transferred) && (queue.empty() || queue_in_ring)) {
+            // zero copy: the batch descriptor points at the recv buffer itself
+            const int rc = EnsureBatchDescs();
+            if (rc != CTS_OK) return rc;
+            cts_buf_desc* descs = hook ? hdesc.data() : reinterpret_cast<cts_buf_desc*>(stage_desc.host);
+            descs[queue.size()] = cts_buf_desc{(uint64_t)(src - ring_base), transferred, t.expected_pattern_offset, 0, 0};
+            queue.push_back(Queued{recv_completions, transferred, recv_after});
+            queue_in_ring = true;
+            return CTS_OK;
+        }
+        if (!queue.empty() && queue_in_ring) {  // never mix ring and staged entries in one batch
+            const int rc = Flush();
+            if (rc < 0) return rc;
+        }
+        queue_in_ring = false;
         const uint64_t slot = ((uint64_t)transferred + 15u) & ~15ull;
         if (!queue.empty() && stage_used + slot > StageCapacity()) {
             const int rc = Flush();
@@ -575,14 +636,18 @@ struct cts_io_pattern {
         const uint32_t n = (uint32_t)queue.size();
         const cts_verify_result* res = nullptr;
         if (hook != nullptr) {
-            if (hook(hook_ctx, hstage.data(), stage_used, hdesc.data(), n, hres.data()) != 0) return CTS_E_INVALID;
+            const uint8_t* arena = queue_in_ring ? reinterpret_cast<const uint8_t*>(ring_base) : hstage.data();
+            const uint64_t bytes = queue_in_ring ? ring_bytes : stage_used;
+            if (hook(hook_ctx, arena, bytes, hdesc.data(), n, hres.data()) != 0) return CTS_E_INVALID;
             res = hres.data();
         } else {
             int rc = EnsureStream();
             if (rc != CTS_OK) return rc;
             uint32_t maxlen = 0;
             for (const auto& q : queue) maxlen = std::max(maxlen, q.transferred);
-            rc = cts_verify(engine, stage.dev, stage.bytes, reinterpret_cast<cts_buf_desc*>(stage_desc.dev), n, maxlen,
+            const uint8_t* arena = queue_in_ring ? recv_pinned.dev : stage.dev;
+            const uint64_t bytes = queue_in_ring ? recv_pinned.bytes : stage.bytes;
+            rc = cts_verify(engine, arena, bytes, reinterpret_cast<cts_buf_desc*>(stage_desc.dev), n, maxlen,
                             reinterpret_cast<cts_verify_result*>(stage_res.dev), nullptr, nullptr, 0, stream);
             if (rc != CTS_OK) return rc;
             if (hipStreamSynchronize(stream) != hipSuccess) return CTS_E_HIP;
@@ -621,7 +686,8 @@ struct cts_io_pattern {
             if (rc < 0) return rc;
         }
         const bool wasIoRequestedFromPattern = state.IsCurrentStateMoreIo();
-        if (t.buffer_type == CTS_BUFFER_DYNAMIC && t.io_action == CTS_TASK_RECV) m_recvBufferFreeList.push_back(t.buffer);
+        if (t.buffer_type == CTS_BUFFER_DYNAMIC && t.io_action == CTS_TASK_RECV)
+            m_recvBufferFreeList.push_back(RecycledRecvBuffer(t.buffer));
 
         bool verified_now = false, defer_this = false;
         cts_verify_result vr{};

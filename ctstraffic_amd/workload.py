@@ -79,9 +79,10 @@ def _corruption_plan(lengths: np.ndarray, rate: int, seed: int, rng_count: Optio
     """Choose n // rate distinct buffers (none when rate <= 0), one corrupted byte each."""
     n = len(lengths)
     rng = np.random.default_rng(seed)
-    k = (n // rate) if rng_count is None else rng_count
     if rate <= 0 or n == 0:
         k = 0
+    else:
+        k = (n // rate) if rng_count is None else rng_count
     eligible = np.nonzero(lengths > 0)[0]
     k = min(k, len(eligible))
     bufs = np.sort(rng.choice(eligible, size=k, replace=False)) if k else np.zeros(0, np.int64)
