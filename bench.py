@@ -42,7 +42,7 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extras", action="store_true", help="skip fill / datagram / host-path extras")
     p.add_argument("--extras-only", default="", help="comma list: fill,datagram,host")
-    p.add_argument("--stream", choices=["new", "default"], default="new",
+    p.add_argument("--stream", choices=["new", "default"], default="default",
                    help="launch stream: a new HIP stream or the device's default stream")
     p.add_argument("--graph", action="store_true", help="replay the timed steps from a HIP graph (measured: no gain)")
     return p.parse_args()
@@ -250,7 +250,8 @@ def _time_kernel(torch, fn, steps):
 VERIFY_KERNELS = {0: "cts::verify_wg_kernel<8,true>", 1: "cts::verify_wg_kernel<4,true>",
                   2: "cts::verify_wg_kernel<16,true>", 3: "cts::verify_wave_kernel<8,true>",
                   4: "cts::verify_wg_nb_kernel<8,true>", 5: "cts::verify_wg_nb_kernel<4,true>",
-                  6: "cts::verify_wg_kernel<8,true,true>", 7: "cts::verify_wg_kernel<4,true,true>"}
+                  6: "cts::verify_wg_kernel<8,true,true>", 7: "cts::verify_wg_kernel<4,true,true>",
+                  8: "cts::verify_wg_kernel<8,true,true,true>"}
 
 
 def pmc_traffic(workload, buffers):

@@ -112,11 +112,12 @@ def _declare(L: ctypes.CDLL) -> None:
         fn = getattr(L, name)
         fn.argtypes = argtypes
         fn.restype = restype
-    from . import _pattern_abi, loopback, media_stream
+    from . import _pattern_abi, loopback, media_stream, status
 
     _pattern_abi.declare(L)
     media_stream.declare(L)
     loopback.declare(L)
+    status.declare(L)
 
 
 def lib() -> ctypes.CDLL:

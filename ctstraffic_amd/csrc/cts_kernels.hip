@@ -464,7 +464,10 @@ __device__ __forceinline__ void block_reduce_mismatch(uint32_t& first, uint32_t&
 // ---------------------------------------------------------------------------------------------
 // One 256-lane workgroup per buffer (grid-strides over buffers). The next
 // buffer's descriptor is fetched while the current one streams.
-template <int U, bool NT, bool SPLIT = false>
+// SCTR: the per-buffer verdict is workgroup-uniform (__syncthreads_or), so the
+// counters of clean buffers are kept in SGPRs by every wave (scalar adds, no LDS
+// round trip per buffer); only a corrupt buffer goes through lane 0 + LDS.
+template <int U, bool NT, bool SPLIT = false, bool SCTR = false>
 __global__ void __launch_bounds__(kBlock, (U <= 8 ? 8 : 4))
     verify_wg_kernel(const uint8_t* __restrict__ arena, uint64_t arena_bytes, const cts_buf_desc* __restrict__ descs,
                      uint32_t n, cts_verify_result* __restrict__ results, uint64_t* __restrict__ counters,
@@ -473,6 +476,8 @@ __global__ void __launch_bounds__(kBlock, (U <= 8 ? 8 : 4))
     __shared__ uint64_t ctr[1][5];
     const uint32_t lane = threadIdx.x;
     zero_counters<1>(ctr);
+    uint64_t ok_bytes = 0;     // SCTR: bytes of clean buffers (uniform)
+    uint32_t ok_buffers = 0;   // SCTR: clean buffers (uniform)
     uint32_t i = blockIdx.x;
     cts_buf_desc dn;
     if (i < n) dn = descs[i];
@@ -486,11 +491,32 @@ __global__ void __launch_bounds__(kBlock, (U <= 8 ? 8 : 4))
         const Span s = make_span(arena, d);
         const uint32_t acc = scan_buffer<kBlock, U, NT, SPLIT>(s, lane);
         uint32_t first = kNone, count = 0;
-        if (__syncthreads_or(acc != 0u)) {  // rare: exact re-scan by the dirty lanes + reduction
+        const bool dirty = __builtin_amdgcn_readfirstlane(__syncthreads_or(acc != 0u)) != 0;
+        if (dirty) {  // rare: exact re-scan by the dirty lanes + reduction
             if (acc != 0u) scan_exact_owned<kBlock, 2, NT>(s, lane, first, count);
             block_reduce_mismatch(first, count);
         }
+        if constexpr (SCTR) {
+            if (!dirty) {
+                ok_bytes += s.len;
+                ok_buffers += 1;
+                if (results != nullptr && lane == 0) {
+                    cts_verify_result r{};
+                    r.first_mismatch = s.len;
+                    r.pass = 1;
+                    results[i] = r;
+                }
+                continue;
+            }
+        }
         if (lane == 0) finish_buffer(s, d, i, first, count, results, ctr[0], conn_first_fail, n_conns);
+    }
+    if constexpr (SCTR) {
+        if (lane == 0) {
+            ctr[0][kBytesChecked] += ok_bytes;
+            ctr[0][kBytesOk] += ok_bytes;
+            ctr[0][kBuffersChecked] += ok_buffers;
+        }
     }
     flush_counters<1>(counters, ctr);
 }
@@ -613,6 +639,123 @@ __global__ void __launch_bounds__(kBlock)
             count = wave_sum(count);
         }
         if (lane == 0) finish_buffer(s, d, i, first, count, results, ctr[wave], conn_first_fail, n_conns);
+    }
+    flush_counters<WAVES>(counters, ctr);
+}
+
+// ---------------------------------------------------------------------------------------------
+// One wave per buffer, software-pipelined across buffers (datagram-sized spans):
+// the loads of the next buffer (edge/head chunks + one interior round of U
+// chunks per lane) are in flight while the current buffer is compared, so a wave
+// keeps two buffers' bytes in the memory system instead of one. A span whose
+// interior does not fit one round finishes its remaining rounds synchronously.
+template <int U, bool NT>
+struct Pending {
+    Span s;
+    u32x4 edge;
+    u32x4 d[U];
+    bool one_round;
+};
+
+template <int U, bool NT>
+__device__ __forceinline__ void pipe_issue(const Span& s, uint32_t lane, Pending<U, NT>& p)
+{
+    p.s = s;
+    const __amdgpu_buffer_rsrc_t r = span_rsrc(s);
+    const uint32_t ce = edge_chunk_of(s, lane);
+    p.edge = buf_load<NT>(r, edge_chunk_used(s, lane) ? ce * 16u : 0x7FFFFFF0u, 0u);
+    const uint32_t c_end = s.nchunks > 0u ? s.nchunks - 1u : 0u;
+    p.one_round = s.nchunks < 3u || c_end <= s.cb0 + (uint32_t)(64 * U);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        // interior chunk cb0 + u*64 + lane; past the span -> out of range -> 0, no request
+        const uint32_t c = s.cb0 + (uint32_t)(u * 64) + lane;
+        p.d[u] = buf_load<NT>(r, (s.nchunks >= 3u && c < c_end) ? c * 16u : 0x7FFFFFF0u, 0u);
+    }
+}
+
+template <int U, bool NT>
+__device__ __forceinline__ uint32_t pipe_consume(const Pending<U, NT>& p, uint32_t lane)
+{
+    const Span& s = p.s;
+    uint32_t acc = 0;
+    if (s.nchunks >= 3u) {
+        const uint32_t c_end = s.nchunks - 1u;
+        const uint32_t B = chunk_base(s, s.cb0 + lane);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t c = s.cb0 + (uint32_t)(u * 64) + lane;
+            const uint32_t any = or4(p.d[u] ^ expected_step<64, U>(B, u, s.sh));
+            acc |= c < c_end ? any : 0u;
+        }
+        if (!p.one_round) {  // rare for datagrams: the rest of the interior, round by round
+            Span t = s;
+            t.cb0 = s.cb0 + (uint32_t)(64 * U);
+            acc |= scan_interior<64, U, NT, false>(t, span_rsrc(s), lane);
+        }
+    }
+    const uint32_t ce = edge_chunk_of(s, lane);
+    const u32x4 x = chunk_xor(s, ce, p.edge) & range_mask(ce == 0u ? s.lo : 0u, ce == s.nchunks - 1u ? s.hi_last : 16u);
+    acc |= edge_chunk_used(s, lane) ? or4(x) : 0u;
+    return acc;
+}
+
+template <int U, bool NT>
+__global__ void __launch_bounds__(kBlock)
+    verify_wave_pipe_kernel(const uint8_t* __restrict__ arena, uint64_t arena_bytes,
+                            const cts_buf_desc* __restrict__ descs, uint32_t n, cts_verify_result* __restrict__ results,
+                            uint64_t* __restrict__ counters, uint32_t* __restrict__ conn_first_fail, uint32_t n_conns)
+{
+    constexpr int WAVES = kBlock / 64;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t nw = gridDim.x * WAVES;
+    __shared__ uint64_t ctr[WAVES][5];
+    zero_counters<WAVES>(ctr);
+    uint32_t i = blockIdx.x * WAVES + wave;
+    if (i < n) {
+        // a bad descriptor becomes an empty span (no loads); its record is written at consume time
+        auto span_of = [&](const cts_buf_desc& d, bool& bad) {
+            bad = desc_bad(d, arena_bytes);
+            cts_buf_desc e = d;
+            if (bad) {
+                e.byte_offset = 0;
+                e.length = 0;
+                e.skip_head = 0;
+            }
+            return make_span(arena, e);
+        };
+        cts_buf_desc dc = descs[i];
+        bool bad_c;
+        Pending<U, NT> cur;
+        pipe_issue<U, NT>(span_of(dc, bad_c), lane, cur);
+        cts_buf_desc dn;
+        if (i + nw < n) dn = descs[i + nw];
+        for (; i < n; i += nw) {
+            Pending<U, NT> nxt;
+            bool bad_n = true;
+            const cts_buf_desc dnn = dn;
+            if (i + nw < n) {
+                pipe_issue<U, NT>(span_of(dnn, bad_n), lane, nxt);
+                if (i + 2 * nw < n) dn = descs[i + 2 * nw];
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            if (bad_c) {
+                if (lane == 0) write_bad(results, i);
+            } else {
+                const uint32_t acc = pipe_consume<U, NT>(cur, lane);
+                uint32_t first = kNone, count = 0;
+                if (__any(acc != 0u)) {
+                    if (acc != 0u) scan_exact_owned<64, 2, NT>(cur.s, lane, first, count);
+                    first = wave_min(first);
+                    count = wave_sum(count);
+                }
+                if (lane == 0) finish_buffer(cur.s, dc, i, first, count, results, ctr[wave], conn_first_fail, n_conns);
+            }
+            cur = nxt;
+            dc = dnn;
+            bad_c = bad_n;
+        }
     }
     flush_counters<WAVES>(counters, ctr);
 }
@@ -833,21 +976,26 @@ static void launch_verify_nt(const uint8_t* arena, uint64_t arena_bytes, const c
                              uint32_t n_conns, hipStream_t stream, const LaunchGeometry& geo)
 {
     if (small) {
-        // variant (small path): 0 = U2, 1 = U1, 2 = U4 (chunks per lane per round)
+        // variant (small path): 0 = U2, 1 = U1, 2 = U4 (chunks per lane per round),
+        // 3 = pipelined across buffers U2, 4 = pipelined U1
         const uint32_t grid = grid_for(n, kBlock / 64, geo);
         switch (geo.verify_variant) {
         case 1: verify_wave_kernel<1, NT><<<grid, kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 2: verify_wave_kernel<4, NT><<<grid, kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
+        case 3: verify_wave_pipe_kernel<2, NT><<<grid, kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
+        case 4: verify_wave_pipe_kernel<1, NT><<<grid, kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         default: verify_wave_kernel<2, NT><<<grid, kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         }
     } else {
         // variant (large path): 0 = workgroup/buffer U8, 1 = U4, 2 = U16, 3 = wave/buffer U8,
         // 4 = barrier-free workgroup/buffer U8, 5 = barrier-free U4,
-        // 6 = workgroup/buffer U8 with an even-phase fast stream, 7 = same U4
+        // 6 = workgroup/buffer U8 with an even-phase fast stream, 7 = same U4,
+        // 8 = variant 6 with clean-buffer counters in SGPRs
         switch (geo.verify_variant) {
         case 4: verify_wg_nb_kernel<8, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 5: verify_wg_nb_kernel<4, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 6: verify_wg_kernel<8, NT, true><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
+        case 8: verify_wg_kernel<8, NT, true, true><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 7: verify_wg_kernel<4, NT, true><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 1: verify_wg_kernel<4, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 2: verify_wg_kernel<16, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;

@@ -274,7 +274,7 @@ def test_verify_host_batch(engine):
 
 
 # ---- every launch variant / geometry is bit-identical ------------------------------------------
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8])
 @pytest.mark.parametrize("nt", [1, 0])
 def test_launch_variants_parity(engine, variant, nt):
     from ctstraffic_amd import _lib
@@ -300,7 +300,7 @@ def test_launch_variants_parity(engine, variant, nt):
         w = W.tcp_resident(n_buffers=300, corrupt_rate=5)
         _check_workload(engine, w, with_oracle=True)
     finally:
-        engine.set_attr(_lib.ATTR_VERIFY_VARIANT, 0)
+        engine.set_attr(_lib.ATTR_VERIFY_VARIANT, 6)
         engine.set_attr(_lib.ATTR_NT_LOADS, 1)
         engine.set_attr(_lib.ATTR_BLOCKS_PER_CU, 8)
         engine.set_attr(_lib.ATTR_SMALL_BLOCKS_PER_CU, 64)
