@@ -44,6 +44,8 @@ def parse():
     p.add_argument("--extras-only", default="", help="comma list: fill,datagram,host")
     p.add_argument("--stream", choices=["new", "default"], default="default",
                    help="launch stream: a new HIP stream or the device's default stream")
+    p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                   help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI)")
     p.add_argument("--graph", action="store_true", help="replay the timed steps from a HIP graph (measured: no gain)")
     return p.parse_args()
 
@@ -61,20 +63,22 @@ def main():
     if not torch.cuda.is_available():
         print("bench.py: no HIP device visible", file=sys.stderr)
         sys.exit(2)
-    torch.cuda.set_device(local)
-    dev = "cuda:%d" % local
+    gpu = local % torch.cuda.device_count()  # one rank per GPU; ranks share a GPU only in rehearsals
+    torch.cuda.set_device(gpu)
+    dev = "cuda:%d" % gpu
     from ctstraffic_amd import Engine, workload as W
     from ctstraffic_amd import distributed as D
 
     if world > 1:
-        D.init("nccl", device=torch.device(dev))
+        D.init(args.dist_backend, device=torch.device(dev) if args.dist_backend == "nccl" else None)
 
-    engine = Engine(local)
+    engine = Engine(gpu)
     stream = torch.cuda.Stream() if args.stream == "new" else torch.cuda.current_stream()
 
     # ---- workload (per rank: weak scaling) --------------------------------------------------
-    # each rank verifies its own shard of connections (hash(conn) mod G): config 2's batch per GPU
-    w = W.tcp_resident(n_buffers=args.buffers)
+    # weak scaling: every rank verifies a config-2 batch of its own connections (rank-disjoint
+    # connection ids, so the per-connection DataError decisions never span GPUs)
+    w = W.tcp_resident(n_buffers=args.buffers, conn_base=rank * args.buffers)
     R = max(1, args.arenas)
     arenas = []
     descs = None
@@ -204,7 +208,8 @@ def main():
                 "buffer_bytes": 65536,
                 "verified_bytes_per_step_per_gpu": bytes_per_step,
                 "arenas_rotated": R,
-                "parallelism": "hash-sharded, %d rank(s), no data-path collective" % world,
+                "parallelism": "%d rank(s), one config-2 batch of its own connections each, no data-path "
+                               "collective; RCCL all-reduce of the 5 counters closes the timed region" % world,
             },
             "roofline": {
                 "bound": "hbm",

@@ -93,7 +93,7 @@ def _corruption_plan(lengths: np.ndarray, rate: int, seed: int, rng_count: Optio
 
 def tcp_resident(n_buffers: int = 4096, length: int = 65536, corrupt_rate: int = 1024,
                  random_phase_frac: float = 0.25, seed_offsets: int = SEED_OFFSETS,
-                 seed_corrupt: int = SEED_CORRUPT, name: str = "config2") -> Workload:
+                 seed_corrupt: int = SEED_CORRUPT, name: str = "config2", conn_base: int = 0) -> Workload:
     """Config 2: n x 64 KiB device-resident buffers, mixed phases, sparse corruption."""
     rng = np.random.default_rng(seed_offsets)
     d = np.zeros(n_buffers, dtype=DESC_DTYPE)
@@ -102,7 +102,7 @@ def tcp_resident(n_buffers: int = 4096, length: int = 65536, corrupt_rate: int =
     rand = rng.random(n_buffers) < random_phase_frac
     offs = rng.integers(0, PATTERN_PERIOD, size=n_buffers)
     d["expected_pattern_offset"] = np.where(rand, offs, 0).astype(np.uint32)
-    d["conn_index"] = np.arange(n_buffers, dtype=np.uint32)
+    d["conn_index"] = np.arange(n_buffers, dtype=np.uint32) + np.uint32(conn_base)  # rank-disjoint connections
     d["skip_head"] = 0
     lens = d["length"].astype(np.int64)
     cb, cp, cx = _corruption_plan(lens, corrupt_rate, seed_corrupt)

@@ -20,14 +20,21 @@ if [[ $STEPS == all || $STEPS == *bench* ]]; then
   run bench
   timeout -k 10 400 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
 fi
+if [[ $STEPS == all || $STEPS == *dist* ]]; then
+  # 2-rank rehearsal of the multi-GPU path on this one GPU (gloo; both ranks on cuda:0)
+  run dist-rehearsal
+  timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+    --master-port 29517 bench.py --gpus 2 --dist-backend gloo --no-cpu-baseline --no-extras --steps 50 --warmup 5 \
+    > "$OUT/dist2_gloo.json" 2> "$OUT/dist2_gloo.err"
+fi
 if [[ $STEPS == all || $STEPS == *prof* ]]; then
   run rocprof-kernel-trace
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -d "$OUT/prof_kt" -o run --output-format csv \
-    -- python3 bench.py --no-cpu-baseline --steps 200 --warmup 20 > "$OUT/prof_kt_bench.json" 2> "$OUT/prof_kt.err"
+    -- python3 bench.py --no-cpu-baseline --no-extras --steps 200 --warmup 20 > "$OUT/prof_kt_bench.json" 2> "$OUT/prof_kt.err"
   for ctr in FETCH_SIZE WRITE_SIZE TCC_EA0_RDREQ_sum; do
     run rocprof-pmc $ctr
     timeout -k 10 300 rocprofv3 --pmc $ctr --kernel-trace -T -d "$OUT/prof_pmc_$ctr" -o run --output-format csv \
-      -- python3 bench.py --no-cpu-baseline --steps 50 --warmup 5 > "$OUT/prof_pmc_$ctr.json" 2> "$OUT/prof_pmc_$ctr.err"
+      -- python3 bench.py --no-cpu-baseline --no-extras --steps 50 --warmup 5 > "$OUT/prof_pmc_$ctr.json" 2> "$OUT/prof_pmc_$ctr.err"
   done
 fi
 run done
