@@ -522,6 +522,153 @@ __global__ void __launch_bounds__(kBlock, (U <= 8 ? 8 : 4))
 }
 
 // ---------------------------------------------------------------------------------------------
+// Software-pipelined workgroup verify: the workgroup's buffers form one stream of
+// rounds (U chunks per lane each; a buffer is max(1, ceil(interior / (256*U)))
+// rounds, its edge/head chunks ride on its first round). Round r+1 — possibly the
+// next buffer's first round — is issued before round r is compared, so the
+// per-buffer __syncthreads_or (which needs only round r's data) overlaps the next
+// buffer's loads instead of draining the memory pipe. Every iteration issues the
+// same U+1 loads (out of range when there is nothing to fetch: no request), so
+// the loads never sit under a branch.
+struct PipeBuf {
+    Span s;
+    uint32_t rounds;  // >= 1
+    uint32_t i;       // buffer index (>= n: none)
+    bool bad;
+};
+
+template <int U>
+__device__ __forceinline__ PipeBuf pipe_buf(const uint8_t* arena, uint64_t arena_bytes, const cts_buf_desc& d,
+                                            uint32_t i, uint32_t n)
+{
+    PipeBuf b;
+    b.i = i;
+    b.bad = i < n && desc_bad(d, arena_bytes);
+    cts_buf_desc e = d;
+    if (i >= n || b.bad) {
+        e.byte_offset = 0;
+        e.length = 0;
+        e.skip_head = 0;
+        e.expected_pattern_offset = 0;
+    }
+    b.s = make_span(arena, e);
+    const uint32_t per = 256u * (uint32_t)U;
+    const uint32_t c_end = b.s.nchunks > 0u ? b.s.nchunks - 1u : 0u;
+    const uint32_t interior = (b.s.nchunks >= 3u && c_end > b.s.cb0) ? c_end - b.s.cb0 : 0u;
+    b.rounds = interior == 0u ? 1u : (interior + per - 1u) / per;
+    return b;
+}
+
+// loads of round k of buffer b (+ its edge/head chunk when k == 0)
+template <int U, bool NT>
+__device__ __forceinline__ void pipe_round_issue(const PipeBuf& b, uint32_t k, bool live, uint32_t lane, u32x4 (&d)[U],
+                                                 u32x4& edge)
+{
+    const __amdgpu_buffer_rsrc_t r = span_rsrc(b.s);
+    const uint32_t c_end = b.s.nchunks > 0u ? b.s.nchunks - 1u : 0u;
+    const uint32_t cb = b.s.cb0 + k * 256u * (uint32_t)U;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint32_t c = cb + (uint32_t)(u * 256) + lane;
+        d[u] = buf_load<NT>(r, (live && b.s.nchunks >= 3u && c < c_end) ? c * 16u : 0x7FFFFFF0u, 0u);
+    }
+    const uint32_t ce = edge_chunk_of(b.s, lane);
+    const bool e = live && k == 0u && edge_chunk_used(b.s, lane);
+    const u32x4 v = buf_load<NT>(r, e ? ce * 16u : 0x7FFFFFF0u, 0u);
+    if (k == 0u) edge = v;
+}
+
+template <int U>
+__device__ __forceinline__ uint32_t pipe_round_consume(const PipeBuf& b, uint32_t k, uint32_t lane, const u32x4 (&d)[U])
+{
+    if (b.s.nchunks < 3u) return 0u;
+    const uint32_t c_end = b.s.nchunks - 1u;
+    const uint32_t cb = b.s.cb0 + k * 256u * (uint32_t)U;
+    const uint32_t B = chunk_base(b.s, cb + lane);
+    uint32_t acc = 0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint32_t c = cb + (uint32_t)(u * 256) + lane;
+        const uint32_t any = or4(d[u] ^ expected_step<256, U>(B, u, b.s.sh));
+        acc |= c < c_end ? any : 0u;
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    return acc;
+}
+
+template <int U, bool NT>
+__global__ void __launch_bounds__(kBlock, (U <= 2 ? 8 : 7))
+    verify_wg_pipe_kernel(const uint8_t* __restrict__ arena, uint64_t arena_bytes,
+                          const cts_buf_desc* __restrict__ descs, uint32_t n, cts_verify_result* __restrict__ results,
+                          uint64_t* __restrict__ counters, uint32_t* __restrict__ conn_first_fail, uint32_t n_conns)
+{
+    __shared__ uint64_t ctr[1][5];
+    const uint32_t lane = threadIdx.x;
+    zero_counters<1>(ctr);
+    const uint32_t g = gridDim.x;
+    uint32_t i0 = blockIdx.x;
+    if (i0 >= n) {
+        flush_counters<1>(counters, ctr);
+        return;
+    }
+    cts_buf_desc dcur = descs[i0];
+    PipeBuf cur = pipe_buf<U>(arena, arena_bytes, dcur, i0, n);
+    cts_buf_desc dnext{};
+    if (i0 + g < n) dnext = descs[i0 + g];
+    u32x4 ra[U], rb[U];
+    u32x4 ecur = {0u, 0u, 0u, 0u};
+    pipe_round_issue<U, NT>(cur, 0u, !cur.bad, lane, ra, ecur);
+    uint32_t k = 0, acc = 0;
+    // one pipeline step: issue the round after (cur, k) into `nx`, compare `now`
+    auto step = [&](u32x4 (&now)[U], u32x4 (&nx)[U]) -> bool {
+        const bool last = k + 1u == cur.rounds;
+        PipeBuf nb = cur;
+        cts_buf_desc dnb = dcur;
+        uint32_t nk = k + 1u;
+        if (last) {
+            nb = pipe_buf<U>(arena, arena_bytes, dnext, cur.i + g, n);
+            dnb = dnext;
+            nk = 0u;
+        }
+        u32x4 e_new = {0u, 0u, 0u, 0u};
+        pipe_round_issue<U, NT>(nb, nk, nb.i < n && !nb.bad, lane, nx, e_new);
+        __builtin_amdgcn_sched_barrier(0);
+        if (!cur.bad) acc |= pipe_round_consume<U>(cur, k, lane, now);
+        if (!last) {
+            k = nk;
+            return true;
+        }
+        // buffer complete: edges, verdict, record (the next buffer's first round is in flight)
+        if (cur.bad) {
+            if (lane == 0) write_bad(results, cur.i);
+        } else {
+            const uint32_t ce = edge_chunk_of(cur.s, lane);
+            const u32x4 x = chunk_xor(cur.s, ce, ecur) &
+                            range_mask(ce == 0u ? cur.s.lo : 0u, ce == cur.s.nchunks - 1u ? cur.s.hi_last : 16u);
+            acc |= edge_chunk_used(cur.s, lane) ? or4(x) : 0u;
+            uint32_t first = kNone, count = 0;
+            if (__syncthreads_or(acc != 0u)) {
+                if (acc != 0u) scan_exact_owned<kBlock, 2, NT>(cur.s, lane, first, count);
+                block_reduce_mismatch(first, count);
+            }
+            if (lane == 0) finish_buffer(cur.s, dcur, cur.i, first, count, results, ctr[0], conn_first_fail, n_conns);
+        }
+        acc = 0u;
+        ecur = e_new;
+        cur = nb;
+        dcur = dnb;
+        k = 0u;
+        if (cur.i + g < n) dnext = descs[cur.i + g];
+        return cur.i < n;
+    };
+    for (;;) {
+        if (!step(ra, rb)) break;
+        if (!step(rb, ra)) break;
+    }
+    flush_counters<1>(counters, ctr);
+}
+
+// ---------------------------------------------------------------------------------------------
 // Barrier-free workgroup-per-buffer verify. verify_wg_kernel ends every buffer
 // with __syncthreads_or: each wave drains its loads (vmcnt(0)) and then waits
 // for the slowest wave before the next buffer's loads go out — one HBM latency
@@ -990,12 +1137,15 @@ static void launch_verify_nt(const uint8_t* arena, uint64_t arena_bytes, const c
         // variant (large path): 0 = workgroup/buffer U8, 1 = U4, 2 = U16, 3 = wave/buffer U8,
         // 4 = barrier-free workgroup/buffer U8, 5 = barrier-free U4,
         // 6 = workgroup/buffer U8 with an even-phase fast stream, 7 = same U4,
-        // 8 = variant 6 with clean-buffer counters in SGPRs
+        // 8 = variant 6 with clean-buffer counters in SGPRs,
+        // 9 = software-pipelined round stream U4, 10 = same U2
         switch (geo.verify_variant) {
         case 4: verify_wg_nb_kernel<8, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 5: verify_wg_nb_kernel<4, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 6: verify_wg_kernel<8, NT, true><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 8: verify_wg_kernel<8, NT, true, true><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
+        case 9: verify_wg_pipe_kernel<4, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
+        case 10: verify_wg_pipe_kernel<2, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 7: verify_wg_kernel<4, NT, true><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 1: verify_wg_kernel<4, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 2: verify_wg_kernel<16, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;

@@ -274,7 +274,7 @@ def test_verify_host_batch(engine):
 
 
 # ---- every launch variant / geometry is bit-identical ------------------------------------------
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10])
 @pytest.mark.parametrize("nt", [1, 0])
 def test_launch_variants_parity(engine, variant, nt):
     from ctstraffic_amd import _lib

@@ -30,6 +30,10 @@ ALGO_BYTES = {("verify_wg_kernel", "524288"): 268435456, ("verify_wave_kernel", 
               ("fill_kernel", "524288"): 268435456}
 
 
+def _kname(name):
+    return name.split("(")[0].split("<")[0].split("::")[-1].strip()
+
+
 def _grid(r):
     return r.get("Grid_Size") or r.get("Grid_Size_X")
 
@@ -44,8 +48,7 @@ def main(src, dst):
     if os.path.exists(tr):
         by = defaultdict(list)
         for r in csv.DictReader(open(tr)):
-            by[(r["Kernel_Name"].split("(")[0].split("<")[0].split("::")[-1], _grid(r))].append(
-                int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+            by[(_kname(r["Kernel_Name"]), _grid(r))].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
         for k, d in by.items():
             if k not in WORKLOADS:
                 continue
@@ -62,7 +65,7 @@ def main(src, dst):
             continue
         by = defaultdict(list)
         for r in csv.DictReader(open(p)):
-            by[(r["Kernel_Name"].split("(")[0].split("<")[0].split("::")[-1], _grid(r))].append(float(r["Counter_Value"]))
+            by[(_kname(r["Kernel_Name"]), _grid(r))].append(float(r["Counter_Value"]))
         for k, v in by.items():
             if k not in WORKLOADS:
                 continue
