@@ -22,7 +22,8 @@ except Exception:  # pragma: no cover - torch is part of the image
     torch = None
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libcts_engine.so")
+# CTS_ENGINE_LIB: an alternative in-tree build of the same library (tools/ A/B runs)
+LIB_PATH = os.environ.get("CTS_ENGINE_LIB") or os.path.join(_HERE, "libcts_engine.so")
 
 CTS_OK = 0
 CTS_E_INVALID = -1

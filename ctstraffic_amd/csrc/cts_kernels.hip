@@ -214,12 +214,10 @@ __device__ __forceinline__ uint32_t chunk_base(const Span& s, uint32_t c)
 // the VGPR so the range check (which covers voffset + imm) zero-fills the
 // excess lanes, which are then masked out.
 template <int TEAM, int U, bool NT, bool EVEN>
-__device__ __forceinline__ uint32_t scan_interior_impl(const Span& s, __amdgpu_buffer_rsrc_t r, uint32_t lane)
+__device__ __forceinline__ uint32_t scan_rounds(const Span& s, __amdgpu_buffer_rsrc_t r, uint32_t lane, uint32_t cb,
+                                                uint32_t c_end)
 {
-    if (s.nchunks < 3u) return 0;
-    const uint32_t c_end = s.nchunks - 1u;  // interior = [cb0, c_end); [1, cb0) are head chunks
     uint32_t acc = 0;
-    uint32_t cb = s.cb0;
     const uint32_t voff = lane * 16u;
     for (; cb + (uint32_t)(TEAM * U) <= c_end; cb += (uint32_t)(TEAM * U)) {
         u32x4 d[U];
@@ -251,6 +249,14 @@ __device__ __forceinline__ uint32_t scan_interior_impl(const Span& s, __amdgpu_b
     return acc;
 }
 
+// interior = [cb0, nchunks-1); [1, cb0) are head chunks
+template <int TEAM, int U, bool NT, bool EVEN>
+__device__ __forceinline__ uint32_t scan_interior_impl(const Span& s, __amdgpu_buffer_rsrc_t r, uint32_t lane)
+{
+    if (s.nchunks < 3u) return 0;
+    return scan_rounds<TEAM, U, NT, EVEN>(s, r, lane, s.cb0, s.nchunks - 1u);
+}
+
 // SPLIT: a span-uniform (scalar) branch on the byte phase selects the
 // funnel-shift-free even-phase stream.
 template <int TEAM, int U, bool NT, bool SPLIT>
@@ -260,6 +266,25 @@ __device__ __forceinline__ uint32_t scan_interior(const Span& s, __amdgpu_buffer
         if (__builtin_amdgcn_readfirstlane(s.sh) == 0u) return scan_interior_impl<TEAM, U, NT, true>(s, r, lane);
     }
     return scan_interior_impl<TEAM, U, NT, false>(s, r, lane);
+}
+
+// A span of whole chunks starting on a 128-byte line (lo == 0, hi_last == 16,
+// chunk 0 line-aligned: every buffer of a 64 KiB-strided arena or recv ring
+// whose completion is a multiple of 16 bytes) has no partial chunk to mask: all
+// of [0, nchunks) streams in rounds, with no edge/head load and, for 64 KiB, no
+// tail round (4096 chunks = 2 full rounds of 256 lanes x U8).
+__device__ __forceinline__ bool span_whole_lines(const Span& s)
+{
+    return s.lo == 0u && s.hi_last == 16u && s.cb0 == 8u;
+}
+
+template <int TEAM, int U, bool NT, bool SPLIT>
+__device__ __forceinline__ uint32_t scan_whole(const Span& s, __amdgpu_buffer_rsrc_t r, uint32_t lane)
+{
+    if constexpr (SPLIT) {
+        if (__builtin_amdgcn_readfirstlane(s.sh) == 0u) return scan_rounds<TEAM, U, NT, true>(s, r, lane, 0u, s.nchunks);
+    }
+    return scan_rounds<TEAM, U, NT, false>(s, r, lane, 0u, s.nchunks);
 }
 
 // Fast pass over a whole span: OR of (received ^ expected) over this lane's
@@ -285,10 +310,13 @@ __device__ __forceinline__ bool edge_chunk_used(const Span& s, uint32_t lane)
     return lane >= 2u && lane <= 8u && lane - 1u < h;
 }
 
-template <int TEAM, int U, bool NT, bool SPLIT = false>
+template <int TEAM, int U, bool NT, bool SPLIT = false, bool WHOLE = false>
 __device__ __forceinline__ uint32_t scan_buffer(const Span& s, uint32_t lane)
 {
     const __amdgpu_buffer_rsrc_t r = span_rsrc(s);
+    if constexpr (WHOLE) {
+        if (__builtin_amdgcn_readfirstlane(span_whole_lines(s) ? 1u : 0u)) return scan_whole<TEAM, U, NT, SPLIT>(s, r, lane);
+    }
     const uint32_t ce = edge_chunk_of(s, lane);
     // lanes without an edge/head chunk address past the resource: the range check
     // returns 0 without a memory request (waves 1..3 of a workgroup fetch nothing)
@@ -346,6 +374,23 @@ __device__ __forceinline__ void scan_exact_owned(const Span& s, uint32_t lane, u
         const u32x4 x = chunk_xor(s, c, buf_load<NT>(r, c * 16u, 0u)) &
                         range_mask(c == 0u ? s.lo : 0u, c == s.nchunks - 1u ? s.hi_last : 16u);
         take_diff(s, c, x, first, count);
+    }
+}
+
+// scan_exact_owned for a span scan_whole streamed: chunk c -> lane c % TEAM, no edges
+template <int TEAM, int U, bool NT>
+__device__ __forceinline__ void scan_exact_whole(const Span& s, uint32_t lane, uint32_t& first, uint32_t& count)
+{
+    const __amdgpu_buffer_rsrc_t r = span_rsrc(s);
+    for (uint32_t cb = 0; cb < s.nchunks; cb += (uint32_t)(TEAM * U)) {
+        u32x4 d[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) d[u] = buf_load<NT>(r, (cb + (uint32_t)(u * TEAM) + lane) * 16u, 0u);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t c = cb + (uint32_t)(u * TEAM) + lane;
+            if (c < s.nchunks) take_diff(s, c, chunk_xor(s, c, d[u]), first, count);
+        }
     }
 }
 
@@ -467,7 +512,7 @@ __device__ __forceinline__ void block_reduce_mismatch(uint32_t& first, uint32_t&
 // SCTR: the per-buffer verdict is workgroup-uniform (__syncthreads_or), so the
 // counters of clean buffers are kept in SGPRs by every wave (scalar adds, no LDS
 // round trip per buffer); only a corrupt buffer goes through lane 0 + LDS.
-template <int U, bool NT, bool SPLIT = false, bool SCTR = false>
+template <int U, bool NT, bool SPLIT = false, bool SCTR = false, bool WHOLE = false>
 __global__ void __launch_bounds__(kBlock, (U <= 8 ? 8 : 4))
     verify_wg_kernel(const uint8_t* __restrict__ arena, uint64_t arena_bytes, const cts_buf_desc* __restrict__ descs,
                      uint32_t n, cts_verify_result* __restrict__ results, uint64_t* __restrict__ counters,
@@ -489,11 +534,14 @@ __global__ void __launch_bounds__(kBlock, (U <= 8 ? 8 : 4))
             continue;
         }
         const Span s = make_span(arena, d);
-        const uint32_t acc = scan_buffer<kBlock, U, NT, SPLIT>(s, lane);
+        const uint32_t acc = scan_buffer<kBlock, U, NT, SPLIT, WHOLE>(s, lane);
         uint32_t first = kNone, count = 0;
         const bool dirty = __builtin_amdgcn_readfirstlane(__syncthreads_or(acc != 0u)) != 0;
         if (dirty) {  // rare: exact re-scan by the dirty lanes + reduction
-            if (acc != 0u) scan_exact_owned<kBlock, 2, NT>(s, lane, first, count);
+            if (acc != 0u) {
+                if (WHOLE && span_whole_lines(s)) scan_exact_whole<kBlock, 2, NT>(s, lane, first, count);
+                else scan_exact_owned<kBlock, 2, NT>(s, lane, first, count);
+            }
             block_reduce_mismatch(first, count);
         }
         if constexpr (SCTR) {
@@ -517,153 +565,6 @@ __global__ void __launch_bounds__(kBlock, (U <= 8 ? 8 : 4))
             ctr[0][kBytesOk] += ok_bytes;
             ctr[0][kBuffersChecked] += ok_buffers;
         }
-    }
-    flush_counters<1>(counters, ctr);
-}
-
-// ---------------------------------------------------------------------------------------------
-// Software-pipelined workgroup verify: the workgroup's buffers form one stream of
-// rounds (U chunks per lane each; a buffer is max(1, ceil(interior / (256*U)))
-// rounds, its edge/head chunks ride on its first round). Round r+1 — possibly the
-// next buffer's first round — is issued before round r is compared, so the
-// per-buffer __syncthreads_or (which needs only round r's data) overlaps the next
-// buffer's loads instead of draining the memory pipe. Every iteration issues the
-// same U+1 loads (out of range when there is nothing to fetch: no request), so
-// the loads never sit under a branch.
-struct PipeBuf {
-    Span s;
-    uint32_t rounds;  // >= 1
-    uint32_t i;       // buffer index (>= n: none)
-    bool bad;
-};
-
-template <int U>
-__device__ __forceinline__ PipeBuf pipe_buf(const uint8_t* arena, uint64_t arena_bytes, const cts_buf_desc& d,
-                                            uint32_t i, uint32_t n)
-{
-    PipeBuf b;
-    b.i = i;
-    b.bad = i < n && desc_bad(d, arena_bytes);
-    cts_buf_desc e = d;
-    if (i >= n || b.bad) {
-        e.byte_offset = 0;
-        e.length = 0;
-        e.skip_head = 0;
-        e.expected_pattern_offset = 0;
-    }
-    b.s = make_span(arena, e);
-    const uint32_t per = 256u * (uint32_t)U;
-    const uint32_t c_end = b.s.nchunks > 0u ? b.s.nchunks - 1u : 0u;
-    const uint32_t interior = (b.s.nchunks >= 3u && c_end > b.s.cb0) ? c_end - b.s.cb0 : 0u;
-    b.rounds = interior == 0u ? 1u : (interior + per - 1u) / per;
-    return b;
-}
-
-// loads of round k of buffer b (+ its edge/head chunk when k == 0)
-template <int U, bool NT>
-__device__ __forceinline__ void pipe_round_issue(const PipeBuf& b, uint32_t k, bool live, uint32_t lane, u32x4 (&d)[U],
-                                                 u32x4& edge)
-{
-    const __amdgpu_buffer_rsrc_t r = span_rsrc(b.s);
-    const uint32_t c_end = b.s.nchunks > 0u ? b.s.nchunks - 1u : 0u;
-    const uint32_t cb = b.s.cb0 + k * 256u * (uint32_t)U;
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const uint32_t c = cb + (uint32_t)(u * 256) + lane;
-        d[u] = buf_load<NT>(r, (live && b.s.nchunks >= 3u && c < c_end) ? c * 16u : 0x7FFFFFF0u, 0u);
-    }
-    const uint32_t ce = edge_chunk_of(b.s, lane);
-    const bool e = live && k == 0u && edge_chunk_used(b.s, lane);
-    const u32x4 v = buf_load<NT>(r, e ? ce * 16u : 0x7FFFFFF0u, 0u);
-    if (k == 0u) edge = v;
-}
-
-template <int U>
-__device__ __forceinline__ uint32_t pipe_round_consume(const PipeBuf& b, uint32_t k, uint32_t lane, const u32x4 (&d)[U])
-{
-    if (b.s.nchunks < 3u) return 0u;
-    const uint32_t c_end = b.s.nchunks - 1u;
-    const uint32_t cb = b.s.cb0 + k * 256u * (uint32_t)U;
-    const uint32_t B = chunk_base(b.s, cb + lane);
-    uint32_t acc = 0;
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const uint32_t c = cb + (uint32_t)(u * 256) + lane;
-        const uint32_t any = or4(d[u] ^ expected_step<256, U>(B, u, b.s.sh));
-        acc |= c < c_end ? any : 0u;
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    return acc;
-}
-
-template <int U, bool NT>
-__global__ void __launch_bounds__(kBlock, (U <= 2 ? 8 : 7))
-    verify_wg_pipe_kernel(const uint8_t* __restrict__ arena, uint64_t arena_bytes,
-                          const cts_buf_desc* __restrict__ descs, uint32_t n, cts_verify_result* __restrict__ results,
-                          uint64_t* __restrict__ counters, uint32_t* __restrict__ conn_first_fail, uint32_t n_conns)
-{
-    __shared__ uint64_t ctr[1][5];
-    const uint32_t lane = threadIdx.x;
-    zero_counters<1>(ctr);
-    const uint32_t g = gridDim.x;
-    uint32_t i0 = blockIdx.x;
-    if (i0 >= n) {
-        flush_counters<1>(counters, ctr);
-        return;
-    }
-    cts_buf_desc dcur = descs[i0];
-    PipeBuf cur = pipe_buf<U>(arena, arena_bytes, dcur, i0, n);
-    cts_buf_desc dnext{};
-    if (i0 + g < n) dnext = descs[i0 + g];
-    u32x4 ra[U], rb[U];
-    u32x4 ecur = {0u, 0u, 0u, 0u};
-    pipe_round_issue<U, NT>(cur, 0u, !cur.bad, lane, ra, ecur);
-    uint32_t k = 0, acc = 0;
-    // one pipeline step: issue the round after (cur, k) into `nx`, compare `now`
-    auto step = [&](u32x4 (&now)[U], u32x4 (&nx)[U]) -> bool {
-        const bool last = k + 1u == cur.rounds;
-        PipeBuf nb = cur;
-        cts_buf_desc dnb = dcur;
-        uint32_t nk = k + 1u;
-        if (last) {
-            nb = pipe_buf<U>(arena, arena_bytes, dnext, cur.i + g, n);
-            dnb = dnext;
-            nk = 0u;
-        }
-        u32x4 e_new = {0u, 0u, 0u, 0u};
-        pipe_round_issue<U, NT>(nb, nk, nb.i < n && !nb.bad, lane, nx, e_new);
-        __builtin_amdgcn_sched_barrier(0);
-        if (!cur.bad) acc |= pipe_round_consume<U>(cur, k, lane, now);
-        if (!last) {
-            k = nk;
-            return true;
-        }
-        // buffer complete: edges, verdict, record (the next buffer's first round is in flight)
-        if (cur.bad) {
-            if (lane == 0) write_bad(results, cur.i);
-        } else {
-            const uint32_t ce = edge_chunk_of(cur.s, lane);
-            const u32x4 x = chunk_xor(cur.s, ce, ecur) &
-                            range_mask(ce == 0u ? cur.s.lo : 0u, ce == cur.s.nchunks - 1u ? cur.s.hi_last : 16u);
-            acc |= edge_chunk_used(cur.s, lane) ? or4(x) : 0u;
-            uint32_t first = kNone, count = 0;
-            if (__syncthreads_or(acc != 0u)) {
-                if (acc != 0u) scan_exact_owned<kBlock, 2, NT>(cur.s, lane, first, count);
-                block_reduce_mismatch(first, count);
-            }
-            if (lane == 0) finish_buffer(cur.s, dcur, cur.i, first, count, results, ctr[0], conn_first_fail, n_conns);
-        }
-        acc = 0u;
-        ecur = e_new;
-        cur = nb;
-        dcur = dnb;
-        k = 0u;
-        if (cur.i + g < n) dnext = descs[cur.i + g];
-        return cur.i < n;
-    };
-    for (;;) {
-        if (!step(ra, rb)) break;
-        if (!step(rb, ra)) break;
     }
     flush_counters<1>(counters, ctr);
 }
@@ -1138,14 +1039,14 @@ static void launch_verify_nt(const uint8_t* arena, uint64_t arena_bytes, const c
         // 4 = barrier-free workgroup/buffer U8, 5 = barrier-free U4,
         // 6 = workgroup/buffer U8 with an even-phase fast stream, 7 = same U4,
         // 8 = variant 6 with clean-buffer counters in SGPRs,
-        // 9 = software-pipelined round stream U4, 10 = same U2
+        // 9 = variant 6 + whole-line spans streamed without edge/head/tail handling, 10 = same U4
         switch (geo.verify_variant) {
         case 4: verify_wg_nb_kernel<8, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 5: verify_wg_nb_kernel<4, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 6: verify_wg_kernel<8, NT, true><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 8: verify_wg_kernel<8, NT, true, true><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
-        case 9: verify_wg_pipe_kernel<4, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
-        case 10: verify_wg_pipe_kernel<2, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
+        case 9: verify_wg_kernel<8, NT, true, false, true><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
+        case 10: verify_wg_kernel<4, NT, true, false, true><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 7: verify_wg_kernel<4, NT, true><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 1: verify_wg_kernel<4, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 2: verify_wg_kernel<16, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;

@@ -80,12 +80,20 @@ def test_sender_buffer_fill(engine, max_buf):
     assert np.array_equal(S.cpu().numpy(), oracle.sender_buffer(max_buf))
 
 
-def _random_case(rng, n, max_len, align_mix=True, corrupt_frac=0.3, skip=False):
+def _random_case(rng, n, max_len, align_mix=True, corrupt_frac=0.3, skip=False, whole=False):
+    """whole: every span starts on a 128-byte line and is a multiple of 16 bytes
+    (the streamed-without-edges path of verify variants 9/10; a third are 64 KiB)."""
     lens = rng.integers(0, max_len + 1, size=n)
+    if whole:
+        lens = np.where(rng.random(n) < 0.33, 65536, lens // 16 * 16)
+        skip = False
     descs = np.zeros(n, dtype=DESC_DTYPE)
     off = 0
     for i in range(n):
-        off += int(rng.integers(0, 17)) if align_mix else (-off) % 16
+        if whole:
+            off += (-off) % 128
+        else:
+            off += int(rng.integers(0, 17)) if align_mix else (-off) % 16
         descs[i]["byte_offset"] = off
         descs[i]["length"] = lens[i]
         descs[i]["skip_head"] = min(int(lens[i]), int(rng.integers(0, 40))) if skip else 0
@@ -282,14 +290,16 @@ def test_launch_variants_parity(engine, variant, nt):
     try:
         engine.set_attr(_lib.ATTR_VERIFY_VARIANT, variant)
         engine.set_attr(_lib.ATTR_NT_LOADS, nt)
-        for seed, n, max_len, hint, skip in [(21, 200, 3000, 1472, True), (22, 64, 140000, 0, False),
-                                             (23, 300, 1472, 1472, True), (24, 100, 70000, 0, True),
-                                             (25, 6000, 9000, 0, False)]:  # > kRing buffers per workgroup
+        for seed, n, max_len, hint, skip, whole in [
+                (21, 200, 3000, 1472, True, False), (22, 64, 140000, 0, False, False),
+                (23, 300, 1472, 1472, True, False), (24, 100, 70000, 0, True, False),
+                (25, 6000, 9000, 0, False, False),  # > kRing buffers per workgroup
+                (26, 400, 140000, 0, False, True), (27, 300, 2000, 1472, False, True)]:
             for bpc in (1, 16):
                 engine.set_attr(_lib.ATTR_BLOCKS_PER_CU, bpc)
                 engine.set_attr(_lib.ATTR_SMALL_BLOCKS_PER_CU, bpc)
                 rng = np.random.default_rng(seed)
-                arena, descs = _random_case(rng, n, max_len, skip=skip)
+                arena, descs = _random_case(rng, n, max_len, skip=skip, whole=whole)
                 r, ctr, cff = run_verify(engine, arena, descs, hint, n_conns=7)
                 er, ectr, ecff = oracle.verify_batch(arena, descs, n_conns=7)
                 assert_results_equal(r, er, "variant %d nt %d seed %d bpc %d" % (variant, nt, seed, bpc))
@@ -300,7 +310,7 @@ def test_launch_variants_parity(engine, variant, nt):
         w = W.tcp_resident(n_buffers=300, corrupt_rate=5)
         _check_workload(engine, w, with_oracle=True)
     finally:
-        engine.set_attr(_lib.ATTR_VERIFY_VARIANT, 6)
+        engine.set_attr(_lib.ATTR_VERIFY_VARIANT, 10)
         engine.set_attr(_lib.ATTR_NT_LOADS, 1)
         engine.set_attr(_lib.ATTR_BLOCKS_PER_CU, 8)
         engine.set_attr(_lib.ATTR_SMALL_BLOCKS_PER_CU, 64)

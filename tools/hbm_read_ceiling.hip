@@ -80,7 +80,9 @@ int main(int argc, char** argv)
 {
     int cus = 0;
     CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
-    const size_t arena = 256ull << 20;  // 256 MiB, like one config-2 batch
+    // argv: [reps] [arena MiB (256 = one config-2 batch)] [quick: 1 = two configs only]
+    const size_t arena = (size_t)(argc > 2 ? atoi(argv[2]) : 256) << 20;
+    const bool quick = argc > 3 && atoi(argv[3]) != 0;
     const int R = 8;                     // rotate: 2 GiB total, defeats the 256 MiB MALL
     std::vector<u32x4*> bufs(R);
     for (int r = 0; r < R; ++r) {
@@ -110,6 +112,13 @@ int main(int argc, char** argv)
                ms * 1e3, arena / (ms * 1e-3) / 1e9);                                                                 \
     } while (0)
 
+    if (quick) {
+        for (int pass = 0; pass < 2; ++pass) {
+            RUN_GS(8, true, 8);
+            RUN_SLAB(8, true, 65536);
+        }
+        return 0;
+    }
     for (int pass = 0; pass < 2; ++pass) {
         RUN_GS(4, true, 4);
         RUN_GS(4, true, 8);
