@@ -257,7 +257,9 @@ VERIFY_KERNELS = {0: "cts::verify_wg_kernel<8,true>", 1: "cts::verify_wg_kernel<
                   4: "cts::verify_wg_nb_kernel<8,true>", 5: "cts::verify_wg_nb_kernel<4,true>",
                   6: "cts::verify_wg_kernel<8,true,true>", 7: "cts::verify_wg_kernel<4,true,true>",
                   8: "cts::verify_wg_kernel<8,true,true,true>", 9: "cts::verify_wg_kernel<8,true,true,false,true>",
-                  10: "cts::verify_wg_kernel<4,true,true,false,true>"}
+                  10: "cts::verify_wg_kernel<4,true,true,false,true>",
+                  11: "cts::verify_wg_kernel<4,true,true,false,true,true>",
+                  12: "cts::verify_wg_kernel<8,true,true,false,true,true>"}
 
 
 def pmc_traffic(workload, buffers):

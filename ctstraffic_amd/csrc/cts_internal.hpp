@@ -15,7 +15,7 @@ namespace cts {
 constexpr int kCounterSlots = 8;  // 5 used, padded to one 64-byte line
 enum CounterSlot { kBytesChecked = 0, kBytesOk = 1, kBuffersChecked = 2, kBuffersFailed = 3, kMismatchedBytes = 4 };
 
-constexpr int kVerifyVariants = 11;  // workgroup-per-buffer verify variants (launch_verify)
+constexpr int kVerifyVariants = 13;  // workgroup-per-buffer verify variants (launch_verify)
 
 struct LaunchGeometry {
     int num_cus = 256;        // hipDeviceAttributeMultiprocessorCount
@@ -23,7 +23,7 @@ struct LaunchGeometry {
     int small_blocks_per_cu = 64; // wave-per-buffer grid cap
     int nontemporal = 1;      // nt loads for the once-read verify stream
     int small_threshold = 8192;  // max_length_hint <= this -> one wave per buffer
-    int verify_variant = 10;     // see launch_verify (10: even-phase stream + whole-line spans, U4;
+    int verify_variant = 11;     // see launch_verify (11: variant 10 + in-register exact diff; 10: even-phase stream + whole-line spans, U4;
                                  // measured 1.3-3 % faster than 6, which was +0.3-0.7 % over 0)
 };
 

@@ -327,9 +327,6 @@ __device__ __forceinline__ uint32_t scan_buffer(const Span& s, uint32_t lane)
     return acc;
 }
 
-// Exact scan of a whole span (rare path: a span the fast pass flagged): first
-// differing byte position (relative to the span start) and # differing bytes
-// over this lane's chunks.
 // Exact diff of one chunk's XOR: first differing byte (span-relative) and count.
 __device__ __forceinline__ void take_diff(const Span& s, uint32_t c, u32x4 x, uint32_t& first, uint32_t& count)
 {
@@ -392,6 +389,72 @@ __device__ __forceinline__ void scan_exact_whole(const Span& s, uint32_t lane, u
             if (c < s.nchunks) take_diff(s, c, chunk_xor(s, c, d[u]), first, count);
         }
     }
+}
+
+// The whole-span stream with the exact diff done in registers: a lane whose round
+// saw a difference computes its first differing byte and differing-byte count from
+// the XORs it still holds, so a corrupt buffer costs no re-read. (The re-read of
+// scan_exact_whole is 8 dependent rounds for a 64 KiB buffer: several microseconds
+// during which the workgroup's next buffer waits, and with one corrupt buffer in a
+// thousand that workgroup is the launch's last to finish.) The clean-path cost is
+// one compare and branch per round.
+template <int TEAM, int U, bool NT, bool EVEN>
+__device__ __forceinline__ void scan_whole_exact_impl(const Span& s, __amdgpu_buffer_rsrc_t r, uint32_t lane,
+                                                      uint32_t& first, uint32_t& count)
+{
+    const uint32_t voff = lane * 16u;
+    uint32_t cb = 0;
+    const uint32_t c_end = s.nchunks;
+    for (; cb + (uint32_t)(TEAM * U) <= c_end; cb += (uint32_t)(TEAM * U)) {
+        u32x4 d[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) d[u] = buf_load<NT>(r, voff, (cb + (uint32_t)(u * TEAM)) * 16u);
+        __builtin_amdgcn_sched_barrier(0);
+        const uint32_t B = chunk_base(s, cb + lane);
+        uint32_t any = 0;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            d[u] ^= expected_step<TEAM, U, EVEN>(B, u, s.sh);
+            any |= or4(d[u]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if (any != 0u) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) take_diff(s, cb + (uint32_t)(u * TEAM) + lane, d[u], first, count);
+        }
+    }
+    if (cb < c_end) {
+        u32x4 d[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) d[u] = buf_load<NT>(r, (cb + (uint32_t)(u * TEAM) + lane) * 16u, 0u);
+        __builtin_amdgcn_sched_barrier(0);
+        const uint32_t B = chunk_base(s, cb + lane);
+        uint32_t any = 0;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool in = cb + (uint32_t)(u * TEAM) + lane < c_end;
+            d[u] = in ? (d[u] ^ expected_step<TEAM, U, EVEN>(B, u, s.sh)) : u32x4{0u, 0u, 0u, 0u};
+            any |= or4(d[u]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if (any != 0u) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) take_diff(s, cb + (uint32_t)(u * TEAM) + lane, d[u], first, count);
+        }
+    }
+}
+
+template <int TEAM, int U, bool NT, bool SPLIT>
+__device__ __forceinline__ void scan_whole_exact(const Span& s, uint32_t lane, uint32_t& first, uint32_t& count)
+{
+    const __amdgpu_buffer_rsrc_t r = span_rsrc(s);
+    if constexpr (SPLIT) {
+        if (__builtin_amdgcn_readfirstlane(s.sh) == 0u) {
+            scan_whole_exact_impl<TEAM, U, NT, true>(s, r, lane, first, count);
+            return;
+        }
+    }
+    scan_whole_exact_impl<TEAM, U, NT, false>(s, r, lane, first, count);
 }
 
 __device__ __forceinline__ uint32_t wave_min(uint32_t v)
@@ -512,7 +575,7 @@ __device__ __forceinline__ void block_reduce_mismatch(uint32_t& first, uint32_t&
 // SCTR: the per-buffer verdict is workgroup-uniform (__syncthreads_or), so the
 // counters of clean buffers are kept in SGPRs by every wave (scalar adds, no LDS
 // round trip per buffer); only a corrupt buffer goes through lane 0 + LDS.
-template <int U, bool NT, bool SPLIT = false, bool SCTR = false, bool WHOLE = false>
+template <int U, bool NT, bool SPLIT = false, bool SCTR = false, bool WHOLE = false, bool XD = false>
 __global__ void __launch_bounds__(kBlock, (U <= 8 ? 8 : 4))
     verify_wg_kernel(const uint8_t* __restrict__ arena, uint64_t arena_bytes, const cts_buf_desc* __restrict__ descs,
                      uint32_t n, cts_verify_result* __restrict__ results, uint64_t* __restrict__ counters,
@@ -534,15 +597,23 @@ __global__ void __launch_bounds__(kBlock, (U <= 8 ? 8 : 4))
             continue;
         }
         const Span s = make_span(arena, d);
-        const uint32_t acc = scan_buffer<kBlock, U, NT, SPLIT, WHOLE>(s, lane);
         uint32_t first = kNone, count = 0;
-        const bool dirty = __builtin_amdgcn_readfirstlane(__syncthreads_or(acc != 0u)) != 0;
-        if (dirty) {  // rare: exact re-scan by the dirty lanes + reduction
-            if (acc != 0u) {
-                if (WHOLE && span_whole_lines(s)) scan_exact_whole<kBlock, 2, NT>(s, lane, first, count);
-                else scan_exact_owned<kBlock, 2, NT>(s, lane, first, count);
+        bool dirty;
+        if (XD && __builtin_amdgcn_readfirstlane(span_whole_lines(s) ? 1u : 0u)) {
+            // whole-line span, exact diff in registers: only the reduction is left
+            scan_whole_exact<kBlock, U, NT, SPLIT>(s, lane, first, count);
+            dirty = __builtin_amdgcn_readfirstlane(__syncthreads_or(first != kNone)) != 0;
+            if (dirty) block_reduce_mismatch(first, count);
+        } else {
+            const uint32_t acc = scan_buffer<kBlock, U, NT, SPLIT, WHOLE>(s, lane);
+            dirty = __builtin_amdgcn_readfirstlane(__syncthreads_or(acc != 0u)) != 0;
+            if (dirty) {  // rare: exact re-scan by the dirty lanes + reduction
+                if (acc != 0u) {
+                    if (WHOLE && span_whole_lines(s)) scan_exact_whole<kBlock, 2, NT>(s, lane, first, count);
+                    else scan_exact_owned<kBlock, 2, NT>(s, lane, first, count);
+                }
+                block_reduce_mismatch(first, count);
             }
-            block_reduce_mismatch(first, count);
         }
         if constexpr (SCTR) {
             if (!dirty) {
@@ -828,11 +899,30 @@ __device__ __forceinline__ void fill_chunk(u32x4* a0, uint32_t c, uint32_t nchun
     }
 }
 
+// A span of whole 16-byte chunks (lo == 0, last chunk full): straight-line rounds of
+// U 16-byte buffer stores per lane, the expected words stepped like the verify
+// stream; the tail round needs no mask (stores past num_records are dropped).
+template <int TEAM, int U, bool EVEN>
+__device__ __forceinline__ void fill_whole_rounds(u32x4* p, uint32_t nchunks, uint32_t q0, uint32_t lane)
+{
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(p, (short)0, (int)(nchunks * 16u), 0x00020000);
+    const uint32_t sh = q0 & 1u;
+    for (uint32_t cb = 0; cb < nchunks; cb += (uint32_t)(TEAM * U)) {
+        const uint32_t k = ((q0 + 16u * (cb + lane)) & 0xFFFFu) >> 1;
+        const uint32_t B = __umul24(k, 0x10001u) + 0x10000u;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            __builtin_amdgcn_raw_buffer_store_b128(expected_step<TEAM, U, EVEN>(B, u, sh), r,
+                                                   (cb + (uint32_t)(u * TEAM) + lane) * 16u, 0u, 2);  // aux 2 = nt
+    }
+}
+
 template <int TEAM>
 __global__ void __launch_bounds__(kBlock) fill_kernel(uint8_t* __restrict__ arena, uint64_t arena_bytes,
                                                       const cts_buf_desc* __restrict__ descs, uint32_t n)
 {
     constexpr int TEAMS = kBlock / TEAM;
+    constexpr int FU = TEAM == kBlock ? 4 : 2;  // stores per lane per whole-span round
     const uint32_t lane = threadIdx.x % TEAM;
     const uint32_t team = (TEAM == kBlock) ? 0u : (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x / TEAM);
     for (uint32_t i = blockIdx.x * TEAMS + team; i < n; i += gridDim.x * TEAMS) {
@@ -846,6 +936,11 @@ __global__ void __launch_bounds__(kBlock) fill_kernel(uint8_t* __restrict__ aren
         const uint32_t hi_last = (uint32_t)((uint64_t)lo + len - 16ull * (nchunks - 1u));
         const uint32_t q0 = (d.expected_pattern_offset - lo) & 0xFFFFu;
         u32x4* p = reinterpret_cast<u32x4*>(sp - lo);
+        if (__builtin_amdgcn_readfirstlane((lo == 0u && hi_last == 16u) ? 1u : 0u)) {
+            if (__builtin_amdgcn_readfirstlane(q0 & 1u) == 0u) fill_whole_rounds<TEAM, FU, true>(p, nchunks, q0, lane);
+            else fill_whole_rounds<TEAM, FU, false>(p, nchunks, q0, lane);
+            continue;
+        }
         for (uint32_t c = lane; c < nchunks; c += TEAM) fill_chunk(p, c, nchunks, q0, lo, hi_last);
     }
 }
@@ -1039,7 +1134,8 @@ static void launch_verify_nt(const uint8_t* arena, uint64_t arena_bytes, const c
         // 4 = barrier-free workgroup/buffer U8, 5 = barrier-free U4,
         // 6 = workgroup/buffer U8 with an even-phase fast stream, 7 = same U4,
         // 8 = variant 6 with clean-buffer counters in SGPRs,
-        // 9 = variant 6 + whole-line spans streamed without edge/head/tail handling, 10 = same U4
+        // 9 = variant 6 + whole-line spans streamed without edge/head/tail handling, 10 = same U4,
+        // 11 = variant 10 with the exact diff of whole-line spans in registers (no re-read), 12 = same U8
         switch (geo.verify_variant) {
         case 4: verify_wg_nb_kernel<8, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 5: verify_wg_nb_kernel<4, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
@@ -1047,6 +1143,8 @@ static void launch_verify_nt(const uint8_t* arena, uint64_t arena_bytes, const c
         case 8: verify_wg_kernel<8, NT, true, true><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 9: verify_wg_kernel<8, NT, true, false, true><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 10: verify_wg_kernel<4, NT, true, false, true><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
+        case 11: verify_wg_kernel<4, NT, true, false, true, true><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
+        case 12: verify_wg_kernel<8, NT, true, false, true, true><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 7: verify_wg_kernel<4, NT, true><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 1: verify_wg_kernel<4, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 2: verify_wg_kernel<16, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;

@@ -57,6 +57,44 @@ __global__ void __launch_bounds__(256) read_or_slab(const u32x4* __restrict__ p,
     if (acc == 0x12345678u) out[0] = acc;
 }
 
+// verify's access shape: grid = G blocks, block b reads slabs b, b+G, ... (64 KiB each,
+// U*4 KiB rounds); STAG rotates the round order by block so concurrently active blocks
+// do not all start at the same 4 KiB offset of their slab (HBM channel/bank spread).
+template <int U, bool NT, bool STAG>
+__global__ void __launch_bounds__(256) read_or_slab_gs(const u32x4* __restrict__ p, uint32_t per_block,
+                                                       uint32_t nslabs, uint32_t* out)
+{
+    uint32_t acc = 0;
+    const uint32_t rounds = per_block / (256u * U);
+    for (uint32_t sl = blockIdx.x; sl < nslabs; sl += gridDim.x) {
+        const u32x4* q = p + (uint64_t)sl * per_block;
+        const uint32_t r0 = STAG ? (sl / 8u) % rounds : 0u;  // blocks b..b+7 land on 8 XCDs
+        for (uint32_t k = 0; k < rounds; ++k) {
+            uint32_t r = r0 + k;
+            r = r >= rounds ? r - rounds : r;
+            const uint32_t c = r * 256u * U + threadIdx.x;
+            u32x4 d[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) d[u] = NT ? __builtin_nontemporal_load(q + c + u * 256u) : q[c + u * 256u];
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc |= d[u][0] ^ d[u][1] ^ d[u][2] ^ d[u][3];
+        }
+        acc = __syncthreads_or(acc == 0x12345678u) ? 1u : acc;  // verify's per-buffer barrier
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
+// ctsTraffic's byte pattern (u16 ramp mod 32768, 64 KiB period) instead of a constant:
+// the verify stream reads bytes that toggle; a memset arena does not
+__global__ void fill_ramp(uint32_t* p, uint64_t nwords)
+{
+    for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nwords; w += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t k = (uint32_t)((2 * w) & 0x7FFFu);
+        p[w] = k | ((k + 1u) << 16);
+    }
+}
+
 template <typename F>
 static float time_ms(F launch, int reps, hipStream_t s)
 {
@@ -83,11 +121,13 @@ int main(int argc, char** argv)
     // argv: [reps] [arena MiB (256 = one config-2 batch)] [quick: 1 = two configs only]
     const size_t arena = (size_t)(argc > 2 ? atoi(argv[2]) : 256) << 20;
     const bool quick = argc > 3 && atoi(argv[3]) != 0;
+    const bool ramp = argc > 4 && atoi(argv[4]) != 0;  // arena holds the ctsTraffic pattern
     const int R = 8;                     // rotate: 2 GiB total, defeats the 256 MiB MALL
     std::vector<u32x4*> bufs(R);
     for (int r = 0; r < R; ++r) {
         CHECK(hipMalloc(&bufs[r], arena));
-        CHECK(hipMemset(bufs[r], r + 1, arena));
+        if (ramp) fill_ramp<<<2048, 256>>>(reinterpret_cast<uint32_t*>(bufs[r]), arena / 4);
+        else CHECK(hipMemset(bufs[r], r + 1, arena));
     }
     uint32_t* out;
     CHECK(hipMalloc(&out, 64));
@@ -112,10 +152,31 @@ int main(int argc, char** argv)
                ms * 1e3, arena / (ms * 1e-3) / 1e9);                                                                 \
     } while (0)
 
+#define RUN_SLABGS(U, NT, STAG, BPC)                                                                             \
+    do {                                                                                                         \
+        const uint32_t per = 65536 / 16;                                                                         \
+        const uint32_t nsl = (uint32_t)(arena / 65536);                                                          \
+        const uint32_t grid = (uint32_t)cus * (BPC);                                                             \
+        float ms = time_ms(                                                                                      \
+            [&](int i) { read_or_slab_gs<U, NT, STAG><<<grid, 256, 0, s>>>(bufs[i % R], per, nsl, out); }, reps, \
+            s);                                                                                                  \
+        printf("{\"kind\":\"slab_gs\",\"U\":%d,\"nt\":%d,\"stagger\":%d,\"blocks_per_cu\":%d,\"us\":%.2f,"        \
+               "\"GBps\":%.1f}\n",                                                                               \
+               U, (int)NT, (int)STAG, BPC, ms * 1e3, arena / (ms * 1e-3) / 1e9);                                 \
+    } while (0)
+
     if (quick) {
         for (int pass = 0; pass < 2; ++pass) {
             RUN_GS(8, true, 8);
+            RUN_GS(4, true, 8);
             RUN_SLAB(8, true, 65536);
+            RUN_SLAB(4, true, 65536);
+            RUN_SLABGS(4, true, false, 8);
+            RUN_SLABGS(4, true, true, 8);
+            RUN_SLABGS(8, true, false, 8);
+            RUN_SLABGS(8, true, true, 8);
+            RUN_SLABGS(4, true, false, 4);
+            RUN_SLABGS(4, true, true, 4);
         }
         return 0;
     }

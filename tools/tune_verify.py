@@ -29,6 +29,7 @@ def main():
     p.add_argument("--workload", default="config2")
     p.add_argument("--buffers", type=int, default=4096)
     p.add_argument("--corrupt-rate", type=int, default=1024, help="1 in N buffers corrupted (0 = none)")
+    p.add_argument("--results", action="store_true", help="also write the per-buffer result records")
     args = p.parse_args()
     torch.cuda.set_device(0)
     eng = Engine(0)
@@ -42,6 +43,7 @@ def main():
         arenas.append(a)
     _, _, exp, _ = W.expected_results(w)
     ctr = eng.new_counters()
+    res = eng.new_results(w.n) if args.results else None
     s = torch.cuda.current_stream()
     combos = list(itertools.product([int(x) for x in args.variants.split(",")],
                                     [int(x) for x in args.bpc.split(",")],
@@ -57,10 +59,11 @@ def main():
             eng.reset_counters(ctr)
             # region timing: per-launch event pairs add ~2.5 us to every launch on this stack
             ea, eb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            eng.verify(arenas[0], descs, max_length_hint=w.max_length, counters=ctr)
+            eng.verify(arenas[0], descs, max_length_hint=w.max_length, counters=ctr, results=res)
             ea.record(s)
             for i in range(args.launches - 1):
-                eng.verify(arenas[(i + 1) % len(arenas)], descs, max_length_hint=w.max_length, counters=ctr)
+                eng.verify(arenas[(i + 1) % len(arenas)], descs, max_length_hint=w.max_length, counters=ctr,
+                           results=res)
             eb.record(s)
             torch.cuda.synchronize()
             got = eng.read_counters(ctr)
@@ -73,7 +76,7 @@ def main():
         rows.append({"variant": c[0], "blocks_per_cu": c[1], "nt": c[2], "us": round(t * 1e6, 2),
                      "GBps": round(nbytes / t / 1e9, 1), "spread_us": round((max(times[c]) - min(times[c])) * 1e3, 2)})
     rows.sort(key=lambda x: x["us"])
-    print(json.dumps({"workload": w.name, "bytes": nbytes, "rows": rows}, indent=0))
+    print(json.dumps({"workload": w.name, "bytes": nbytes, "results": bool(args.results), "rows": rows}, indent=0))
 
 
 if __name__ == "__main__":

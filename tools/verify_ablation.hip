@@ -193,6 +193,20 @@ int main(int argc, char** argv)
                arena / (ms * 1e-3) / 1e9);                                                                     \
     } while (0)
 
+    const bool isolate = argc > 2 && atoi(argv[2]) != 0;
+    if (isolate) {  // one piece at a time over the plain read (U4 = verify's default round)
+        for (int pass = 0; pass < 2; ++pass) {
+            RUN(4, false, false, false, false, false, 8);
+            RUN(4, true, false, false, false, false, 8);
+            RUN(4, false, true, false, false, false, 8);
+            RUN(4, false, false, true, false, false, 8);
+            RUN(4, true, true, false, false, false, 8);
+            RUN(4, true, true, true, false, false, 8);
+            RUN(8, false, true, false, false, false, 8);
+            RUN(8, false, false, true, false, false, 8);
+        }
+        return 0;
+    }
     for (int pass = 0; pass < 2; ++pass) {
         RUN(8, false, false, false, false, false, 8);
         RUN(8, true, true, true, false, false, 8);
