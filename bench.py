@@ -259,7 +259,9 @@ VERIFY_KERNELS = {0: "cts::verify_wg_kernel<8,true>", 1: "cts::verify_wg_kernel<
                   8: "cts::verify_wg_kernel<8,true,true,true>", 9: "cts::verify_wg_kernel<8,true,true,false,true>",
                   10: "cts::verify_wg_kernel<4,true,true,false,true>",
                   11: "cts::verify_wg_kernel<4,true,true,false,true,true>",
-                  12: "cts::verify_wg_kernel<8,true,true,false,true,true>"}
+                  12: "cts::verify_wg_kernel<8,true,true,false,true,true>",
+                  13: "cts::verify_wg_kernel<2,true,true,false,true,true>",
+                  14: "cts::verify_wg_kernel<1,true,true,false,true,true>"}
 
 
 def pmc_traffic(workload, buffers):

@@ -15,16 +15,19 @@ namespace cts {
 constexpr int kCounterSlots = 8;  // 5 used, padded to one 64-byte line
 enum CounterSlot { kBytesChecked = 0, kBytesOk = 1, kBuffersChecked = 2, kBuffersFailed = 3, kMismatchedBytes = 4 };
 
-constexpr int kVerifyVariants = 13;  // workgroup-per-buffer verify variants (launch_verify)
+constexpr int kVerifyVariants = 15;  // workgroup-per-buffer verify variants (launch_verify)
 
 struct LaunchGeometry {
     int num_cus = 256;        // hipDeviceAttributeMultiprocessorCount
-    int blocks_per_cu = 8;        // workgroup-per-buffer grid cap = num_cus * this (grid-stride beyond)
+    int blocks_per_cu = 4;        // workgroup-per-buffer grid cap = num_cus * this (grid-stride beyond);
+                                  // 4 x 4 waves x U2 = 32 KiB of loads in flight per CU measured best
+                                  // (config 2: 41.0-41.2 us vs 42.6-43.9 at 8; tools/tune_verify.py)
     int small_blocks_per_cu = 64; // wave-per-buffer grid cap
     int nontemporal = 1;      // nt loads for the once-read verify stream
     int small_threshold = 8192;  // max_length_hint <= this -> one wave per buffer
-    int verify_variant = 11;     // see launch_verify (11: variant 10 + in-register exact diff; 10: even-phase stream + whole-line spans, U4;
-                                 // measured 1.3-3 % faster than 6, which was +0.3-0.7 % over 0)
+    int verify_variant = 13;     // see launch_verify (13: variant 11 at U2; 11: variant 10 + in-register exact diff;
+                                 // 10: even-phase stream + whole-line spans, U4, measured 1.3-3 % faster than 6,
+                                 // which was +0.3-0.7 % over 0)
 };
 
 hipError_t launch_verify(const uint8_t* arena, uint64_t arena_bytes, const cts_buf_desc* descs, uint32_t n,

@@ -1107,7 +1107,12 @@ static inline uint32_t grid_for(uint32_t n, int teams_per_block, const LaunchGeo
     const uint64_t want = ((uint64_t)n + teams_per_block - 1) / teams_per_block;
     const int bpc = teams_per_block > 1 ? geo.small_blocks_per_cu : geo.blocks_per_cu;
     const uint64_t cap = (uint64_t)geo.num_cus * (uint64_t)(bpc > 0 ? bpc : 8);
-    const uint64_t g = want < cap ? want : cap;
+    // grid-stride with the same number of teams' worth of work per workgroup: past the cap
+    // the grid shrinks to ceil(want / per) so no workgroup runs one buffer more than the
+    // rest (an uneven split, e.g. 4096 buffers over 1280 workgroups, leaves a tail of
+    // workgroups with an extra buffer that alone sets the launch's end)
+    const uint64_t per = want <= cap ? 1 : (want + cap - 1) / cap;
+    const uint64_t g = (want + per - 1) / per;
     return (uint32_t)(g == 0 ? 1 : g);
 }
 
@@ -1135,7 +1140,8 @@ static void launch_verify_nt(const uint8_t* arena, uint64_t arena_bytes, const c
         // 6 = workgroup/buffer U8 with an even-phase fast stream, 7 = same U4,
         // 8 = variant 6 with clean-buffer counters in SGPRs,
         // 9 = variant 6 + whole-line spans streamed without edge/head/tail handling, 10 = same U4,
-        // 11 = variant 10 with the exact diff of whole-line spans in registers (no re-read), 12 = same U8
+        // 11 = variant 10 with the exact diff of whole-line spans in registers (no re-read), 12 = same U8,
+        // 13 = same U2, 14 = same U1
         switch (geo.verify_variant) {
         case 4: verify_wg_nb_kernel<8, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 5: verify_wg_nb_kernel<4, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
@@ -1145,6 +1151,8 @@ static void launch_verify_nt(const uint8_t* arena, uint64_t arena_bytes, const c
         case 10: verify_wg_kernel<4, NT, true, false, true><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 11: verify_wg_kernel<4, NT, true, false, true, true><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 12: verify_wg_kernel<8, NT, true, false, true, true><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
+        case 13: verify_wg_kernel<2, NT, true, false, true, true><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
+        case 14: verify_wg_kernel<1, NT, true, false, true, true><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 7: verify_wg_kernel<4, NT, true><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 1: verify_wg_kernel<4, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 2: verify_wg_kernel<16, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;

@@ -289,12 +289,14 @@ def test_verify_host_batch(engine):
 
 
 # ---- every launch variant / geometry is bit-identical ------------------------------------------
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14])
 @pytest.mark.parametrize("nt", [1, 0])
 def test_launch_variants_parity(engine, variant, nt):
     from ctstraffic_amd import _lib
 
     default_variant = engine.get_attr(_lib.ATTR_VERIFY_VARIANT)
+    default_bpc = engine.get_attr(_lib.ATTR_BLOCKS_PER_CU)
+    default_small_bpc = engine.get_attr(_lib.ATTR_SMALL_BLOCKS_PER_CU)
     try:
         engine.set_attr(_lib.ATTR_VERIFY_VARIANT, variant)
         engine.set_attr(_lib.ATTR_NT_LOADS, nt)
@@ -320,5 +322,5 @@ def test_launch_variants_parity(engine, variant, nt):
     finally:
         engine.set_attr(_lib.ATTR_VERIFY_VARIANT, default_variant)
         engine.set_attr(_lib.ATTR_NT_LOADS, 1)
-        engine.set_attr(_lib.ATTR_BLOCKS_PER_CU, 8)
-        engine.set_attr(_lib.ATTR_SMALL_BLOCKS_PER_CU, 64)
+        engine.set_attr(_lib.ATTR_BLOCKS_PER_CU, default_bpc)
+        engine.set_attr(_lib.ATTR_SMALL_BLOCKS_PER_CU, default_small_bpc)

@@ -20,6 +20,11 @@ if [[ $STEPS == all || $STEPS == *bench* ]]; then
   run bench
   timeout -k 10 400 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
 fi
+if [[ $STEPS == all || $STEPS == *ceiling* ]]; then
+  # plain streaming-read reference on the same box (build: see tools/hbm_read_ceiling.hip)
+  run ceiling
+  timeout -k 10 120 tools/hbm_read_ceiling 64 256 1 1 > "$OUT/ceiling.jsonl" 2> "$OUT/ceiling.err"
+fi
 if [[ $STEPS == all || $STEPS == *dist* ]]; then
   # 2-rank rehearsal of the multi-GPU path on this one GPU (gloo; both ranks on cuda:0)
   run dist-rehearsal

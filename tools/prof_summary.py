@@ -20,14 +20,14 @@ from collections import defaultdict
 
 import numpy as np
 
-# (kernel name prefix, grid size) -> workload tag, per bench.py's launches
+# kernel name -> workload tag, per bench.py's launches (the profiled runs pass --no-extras, so
+# each kernel has one workload; the grid depends on the launch geometry and is only reported)
 WORKLOADS = {
-    ("verify_wg_kernel", "524288"): "config2 verify: 4096 x 64 KiB (268435456 B read)",
-    ("verify_wave_kernel", "4194304"): "config3/4 verify: 4M x 1472 B datagrams (6065743872 B payload read)",
-    ("fill_kernel", "524288"): "config2 fill: 4096 x 64 KiB (268435456 B written)",
+    "verify_wg_kernel": "config2 verify: 4096 x 64 KiB (268435456 B read)",
+    "verify_wave_kernel": "config3/4 verify: 4M x 1472 B datagrams (6065743872 B payload read)",
+    "fill_kernel": "config2 fill: 4096 x 64 KiB (268435456 B written)",
 }
-ALGO_BYTES = {("verify_wg_kernel", "524288"): 268435456, ("verify_wave_kernel", "4194304"): 4194304 * 1446,
-              ("fill_kernel", "524288"): 268435456}
+ALGO_BYTES = {"verify_wg_kernel": 268435456, "verify_wave_kernel": 4194304 * 1446, "fill_kernel": 268435456}
 
 
 def _kname(name):
@@ -50,13 +50,16 @@ def main(src, dst):
         for r in csv.DictReader(open(tr)):
             by[(_kname(r["Kernel_Name"]), _grid(r))].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
         for k, d in by.items():
-            if k not in WORKLOADS:
+            if k[0] not in WORKLOADS:
+                continue
+            # one grid per kernel: the one launched most often
+            if len(d) < max(len(v) for kk, v in by.items() if kk[0] == k[0]):
                 continue
             d = np.array(d)
-            out[WORKLOADS[k]] = {"kernel": k[0], "grid": int(k[1]), "launches": int(d.size),
+            out[WORKLOADS[k[0]]] = {"kernel": k[0], "grid": int(k[1]), "launches": int(d.size),
                                  "avg_us": round(float(d.mean()) / 1e3, 2), "median_us": round(float(np.median(d)) / 1e3, 2),
                                  "min_us": round(float(d.min()) / 1e3, 2),
-                                 "algorithmic_GBps_at_avg": round(ALGO_BYTES[k] / float(d.mean()), 1)}
+                                 "algorithmic_GBps_at_avg": round(ALGO_BYTES[k[0]] / float(d.mean()), 1)}
         json.dump(out, open(os.path.join(dst, "kernel_trace_summary.json"), "w"), indent=1)
     pmc = {}
     for ctr in ("FETCH_SIZE", "WRITE_SIZE", "TCC_EA0_RDREQ_sum"):
@@ -67,9 +70,11 @@ def main(src, dst):
         for r in csv.DictReader(open(p)):
             by[(_kname(r["Kernel_Name"]), _grid(r))].append(float(r["Counter_Value"]))
         for k, v in by.items():
-            if k not in WORKLOADS:
+            if k[0] not in WORKLOADS:
                 continue
-            e = pmc.setdefault(WORKLOADS[k], {"kernel": k[0], "algorithmic_bytes": ALGO_BYTES[k]})
+            if len(v) < max(len(vv) for kk, vv in by.items() if kk[0] == k[0]):
+                continue
+            e = pmc.setdefault(WORKLOADS[k[0]], {"kernel": k[0], "grid": int(k[1]), "algorithmic_bytes": ALGO_BYTES[k[0]]})
             e[ctr + "_median"] = float(np.median(v))
             e["launches_" + ctr] = len(v)
     for name, e in pmc.items():
@@ -84,7 +89,7 @@ def main(src, dst):
         if main_bytes:
             e["traffic_over_algorithmic"] = round(main_bytes / e["algorithmic_bytes"], 4)
     if pmc:
-        v = pmc.get(WORKLOADS[("verify_wg_kernel", "524288")], {})
+        v = pmc.get(WORKLOADS["verify_wg_kernel"], {})
         pmc_out = {"workload": "config2", "buffers": 4096, "hbm_bytes_per_launch": v.get("hbm_read_bytes_per_launch"),
                    "correction": "bytes = 2 x 1024 x FETCH_SIZE(KiB) (gfx950 streaming-read halving)",
                    "kernels": pmc}
