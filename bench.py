@@ -123,6 +123,10 @@ def main():
     run_steps(0, max(args.warmup, 1))
     torch.cuda.synchronize()
     engine.reset_counters(counters, stream=stream)
+    if world > 1:
+        # the counter all-reduce once before the clock starts (communicator and kernel set-up)
+        with torch.cuda.stream(stream):
+            D.allreduce_counters(D.fold_counters(counters))
     torch.cuda.synchronize()
 
     # ---- timed region -----------------------------------------------------------------------------

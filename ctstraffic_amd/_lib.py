@@ -40,6 +40,8 @@ ATTR_NT_LOADS = 2
 ATTR_SMALL_THRESHOLD = 3
 ATTR_VERIFY_VARIANT = 4
 ATTR_SMALL_BLOCKS_PER_CU = 5
+ATTR_SMALL_VARIANT = 6
+ATTR_FILL_BLOCKS_PER_CU = 7
 
 
 class CtsError(RuntimeError):

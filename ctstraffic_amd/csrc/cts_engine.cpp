@@ -132,6 +132,8 @@ int cts_engine_create(int device, cts_engine** out)
     e->geo.small_threshold = env_int("CTS_SMALL_THRESHOLD", e->geo.small_threshold);
     e->geo.verify_variant = env_int("CTS_VERIFY_VARIANT", e->geo.verify_variant);
     e->geo.small_blocks_per_cu = env_int("CTS_SMALL_BLOCKS_PER_CU", e->geo.small_blocks_per_cu);
+    e->geo.small_variant = env_int("CTS_SMALL_VARIANT", e->geo.small_variant);
+    e->geo.fill_blocks_per_cu = env_int("CTS_FILL_BLOCKS_PER_CU", e->geo.fill_blocks_per_cu);
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
         delete e;
         return CTS_E_HIP;
@@ -191,6 +193,14 @@ int cts_engine_set_attr(cts_engine* e, int attr, int value)
         if (value < 1 || value > 256) return CTS_E_INVALID;
         e->geo.small_blocks_per_cu = value;
         return CTS_OK;
+    case CTS_ATTR_SMALL_VARIANT:
+        if (value < 0 || value >= cts::kSmallVariants) return CTS_E_INVALID;
+        e->geo.small_variant = value;
+        return CTS_OK;
+    case CTS_ATTR_FILL_BLOCKS_PER_CU:
+        if (value < 1 || value > 64) return CTS_E_INVALID;
+        e->geo.fill_blocks_per_cu = value;
+        return CTS_OK;
     default: return CTS_E_INVALID;
     }
 }
@@ -204,6 +214,8 @@ int cts_engine_get_attr(const cts_engine* e, int attr, int* value)
     case CTS_ATTR_SMALL_THRESHOLD: *value = e->geo.small_threshold; return CTS_OK;
     case CTS_ATTR_VERIFY_VARIANT: *value = e->geo.verify_variant; return CTS_OK;
     case CTS_ATTR_SMALL_BLOCKS_PER_CU: *value = e->geo.small_blocks_per_cu; return CTS_OK;
+    case CTS_ATTR_SMALL_VARIANT: *value = e->geo.small_variant; return CTS_OK;
+    case CTS_ATTR_FILL_BLOCKS_PER_CU: *value = e->geo.fill_blocks_per_cu; return CTS_OK;
     default: return CTS_E_INVALID;
     }
 }

@@ -16,6 +16,7 @@ constexpr int kCounterSlots = 8;  // 5 used, padded to one 64-byte line
 enum CounterSlot { kBytesChecked = 0, kBytesOk = 1, kBuffersChecked = 2, kBuffersFailed = 3, kMismatchedBytes = 4 };
 
 constexpr int kVerifyVariants = 15;  // workgroup-per-buffer verify variants (launch_verify)
+constexpr int kSmallVariants = 9;    // small-buffer (datagram) verify variants
 
 struct LaunchGeometry {
     int num_cus = 256;        // hipDeviceAttributeMultiprocessorCount
@@ -24,7 +25,10 @@ struct LaunchGeometry {
                                   // (config 2: 41.0-41.2 us vs 42.6-43.9 at 8; tools/tune_verify.py)
     int small_blocks_per_cu = 64; // wave-per-buffer grid cap
     int nontemporal = 1;      // nt loads for the once-read verify stream
-    int small_threshold = 8192;  // max_length_hint <= this -> one wave per buffer
+    int small_threshold = 8192;  // max_length_hint <= this -> small-buffer path
+    int small_variant = 7;       // small-buffer path kernel (launch_verify_nt; 7 = four buffers per wave, line-aligned U6:
+                                 // config 3 at 5.95 TB/s of payload vs 4.71 for one wave per datagram)
+    int fill_blocks_per_cu = 2;  // fill grid cap (write-bound: 2 measured best, tools/tune_verify.py --op fill)
     int verify_variant = 13;     // see launch_verify (13: variant 11 at U2; 11: variant 10 + in-register exact diff;
                                  // 10: even-phase stream + whole-line spans, U4, measured 1.3-3 % faster than 6,
                                  // which was +0.3-0.7 % over 0)

@@ -97,6 +97,21 @@ __device__ __forceinline__ u32x4 load_chunk(const u32x4* p)
 
 __device__ __forceinline__ uint32_t or4(u32x4 x) { return x[0] | x[1] | x[2] | x[3]; }
 
+// load_chunk through an explicitly global (address space 1) pointer: a pointer that
+// went through a select or a phi can lose its address space and become a flat load,
+// which also counts in lgkmcnt and forces full drains
+typedef const u32x4 __attribute__((address_space(1)))* gchunk_ptr;
+template <bool NT>
+__device__ __forceinline__ u32x4 load_chunk_g(const u32x4* p)
+{
+    const gchunk_ptr g = (gchunk_ptr)p;
+    if constexpr (NT) {
+        return __builtin_nontemporal_load(g);
+    } else {
+        return *g;
+    }
+}
+
 // A buffer's verified span [sp, sp + len) as 16-byte chunks of p = sp - lo.
 struct Span {
     const u32x4* p;
@@ -763,6 +778,226 @@ __global__ void __launch_bounds__(kBlock)
 }
 
 // ---------------------------------------------------------------------------------------------
+// Four buffers per wave: 16-lane teams, one buffer each (datagram-sized spans).
+// verify_wave_kernel spends a whole wave per 1472-byte datagram: its per-buffer
+// scalar work (descriptor, span set-up, edge lanes, record, counters) is issued once
+// per datagram and a third of its lanes' loads fall past the span. Here a wave's
+// instructions serve four datagrams at once: the span fields live in VGPRs (one
+// descriptor per team), each load instruction fetches four 256-byte runs, and
+// U loads per lane cover 16*U chunks per round (U = 6: 1536 B, one round for a
+// 1446-byte payload at any alignment). Loads are global (per-lane 64-bit
+// addresses: a buffer resource must be wave-uniform); addresses of chunks outside
+// a span are clamped into it (same lines, no extra traffic) and their compare is
+// discarded. ALIGN starts the rounds on the 128-byte line of chunk 0 (the
+// line-aligned interior of scan_buffer), so a team's run covers 2 lines, not 3.
+// A team whose OR is nonzero (rare; the verdict is a wave ballot) re-reads its own
+// chunks exactly and reduces (first, count) over its 16 lanes.
+__device__ __forceinline__ void take_diff_at(uint32_t c, uint32_t lo, u32x4 x, uint32_t& first, uint32_t& count)
+{
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        const uint32_t nz = nonzero_bytes(x[w]);
+        if (nz) {
+            const uint32_t pos = 16u * c + 4u * (uint32_t)w + ((uint32_t)__builtin_ctz(nz) >> 3) - lo;
+            first = pos < first ? pos : first;
+            count += (uint32_t)__builtin_popcount(nz);
+        }
+    }
+}
+
+constexpr int kQuadTeam = 16;  // lanes per buffer in the four-buffers-per-wave kernels
+
+// A team's span, all fields per lane (VGPRs): the four teams of a wave hold four buffers.
+struct QSpan {
+    const u32x4* p;     // chunk 0 (16-byte aligned)
+    const uint8_t* sp;  // first verified byte
+    uint32_t len, nch, hi_last, lo, q0, sh;
+    int last;  // address clamp: the last chunk (0 for an empty span)
+    int cs;    // first chunk of round 0 (line-aligned with ALIGN, else 1)
+    int c_hi;  // last interior chunk (nch - 2)
+};
+
+// Span of [sp, sp + len) at pattern offset `expected`; an empty span (len 0: an idle
+// team, a bad descriptor, a non-DATA datagram) points at `dummy`, 16-byte-aligned
+// memory the clamped loads may read (every compare of an empty span is discarded).
+template <bool ALIGN>
+__device__ __forceinline__ QSpan quad_span(const uint8_t* sp, uint32_t len, uint32_t expected, const void* dummy)
+{
+    QSpan q;
+    q.sp = len ? sp : reinterpret_cast<const uint8_t*>(dummy);
+    q.len = len;
+    q.lo = (uint32_t)((uintptr_t)q.sp & 15u);
+    q.nch = len == 0u ? 0u : (uint32_t)(((uint64_t)q.lo + len + 15u) >> 4);
+    q.hi_last = len == 0u ? 0u : (uint32_t)((uint64_t)q.lo + len - 16ull * (q.nch - 1u));
+    q.q0 = (expected - q.lo) & 0xFFFFu;
+    q.sh = q.q0 & 1u;
+    q.p = reinterpret_cast<const u32x4*>(q.sp - q.lo);
+    q.last = q.nch == 0u ? 0 : (int)q.nch - 1;
+    q.cs = ALIGN ? -(int)(((uintptr_t)q.p >> 4) & 7u) : 1;
+    q.c_hi = (int)q.nch - 2;
+    return q;
+}
+
+// Edge chunk of a team lane: lane 0 chunk 0, lane 1 the last chunk (others: none).
+__device__ __forceinline__ bool quad_edge_used(const QSpan& q, uint32_t lane)
+{
+    return (lane == 0u && q.nch >= 1u) || (lane == 1u && q.nch >= 2u);
+}
+__device__ __forceinline__ uint32_t quad_edge_chunk(const QSpan& q, uint32_t lane) { return lane == 1u ? (uint32_t)q.last : 0u; }
+__device__ __forceinline__ u32x4 quad_edge_xor(const QSpan& q, uint32_t ce, u32x4 data)
+{
+    return (data ^ expected_chunk((q.q0 + 16u * ce) & 0xFFFFu, q.sh)) &
+           range_mask(ce == 0u ? q.lo : 0u, ce == (uint32_t)q.last ? q.hi_last : 16u);
+}
+
+// Interior [1, nch-1) in rounds of U loads per lane starting at chunk cs (the wave loops
+// while any of its teams has chunks left); returns the OR of this lane's differences.
+template <int U, bool NT>
+__device__ __forceinline__ uint32_t quad_scan_interior(const QSpan& q, uint32_t lane)
+{
+    constexpr int ROUND = kQuadTeam * U;
+    uint32_t acc = 0;
+    for (int r = 0; __any(q.cs + r * ROUND <= q.c_hi); ++r) {
+        const int cb = q.cs + r * ROUND + (int)lane;
+        u32x4 dd[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            int c = cb + u * kQuadTeam;
+            c = c < 0 ? 0 : (c > q.last ? q.last : c);
+            dd[u] = load_chunk_g<NT>(q.p + c);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        const uint32_t k = ((q.q0 + 16u * (uint32_t)cb) & 0xFFFFu) >> 1;
+        const uint32_t B = __umul24(k, 0x10001u) + 0x10000u;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int c = cb + u * kQuadTeam;
+            const uint32_t any = or4(dd[u] ^ expected_step<kQuadTeam, U>(B, u, q.sh));
+            acc |= (c >= 1 && c <= q.c_hi) ? any : 0u;
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    return acc;
+}
+
+// Exact re-read of exactly the chunks this lane owns (interior chunks = cs + lane mod 16,
+// plus its edge chunk): first differing byte (span-relative) and differing-byte count.
+template <bool NT>
+__device__ __forceinline__ void quad_scan_exact(const QSpan& q, uint32_t lane, uint32_t& first, uint32_t& count)
+{
+    for (int c = q.cs + (int)lane; c <= q.c_hi; c += kQuadTeam) {
+        if (c >= 1)
+            take_diff_at((uint32_t)c, q.lo,
+                         load_chunk_g<NT>(q.p + c) ^ expected_chunk((q.q0 + 16u * (uint32_t)c) & 0xFFFFu, q.sh), first,
+                         count);
+    }
+    if (quad_edge_used(q, lane)) {
+        const uint32_t ce = quad_edge_chunk(q, lane);
+        take_diff_at(ce, q.lo, quad_edge_xor(q, ce, load_chunk_g<NT>(q.p + ce)), first, count);
+    }
+}
+
+// min / sum over the 16 lanes of each team (all lanes of the wave take part)
+__device__ __forceinline__ void quad_team_reduce(uint32_t& first, uint32_t& count)
+{
+#pragma unroll
+    for (int off = kQuadTeam / 2; off > 0; off >>= 1) {
+        const uint32_t of = (uint32_t)__shfl_xor((int)first, off, kQuadTeam);
+        first = of < first ? of : first;
+        count += (uint32_t)__shfl_xor((int)count, off, kQuadTeam);
+    }
+}
+
+// Team-leader running counters (registers), written to LDS once at the end.
+struct QCounters {
+    uint64_t bytes = 0, ok = 0, mism = 0;
+    uint32_t bufs = 0, fail = 0;
+    __device__ __forceinline__ void add(uint32_t len, bool pass, uint32_t count)
+    {
+        bytes += len;
+        bufs += 1u;
+        if (pass) {
+            ok += len;
+        } else {
+            fail += 1u;
+            mism += count;
+        }
+    }
+    template <int TEAMS>
+    __device__ __forceinline__ void flush(uint64_t (*ctr)[5], uint32_t team, uint32_t lane, uint64_t* counters) const
+    {
+        if (lane == 0u) {
+            ctr[team][kBytesChecked] = bytes;
+            ctr[team][kBytesOk] = ok;
+            ctr[team][kBuffersChecked] = bufs;
+            ctr[team][kBuffersFailed] = fail;
+            ctr[team][kMismatchedBytes] = mism;
+        }
+        flush_counters<TEAMS>(counters, ctr);
+    }
+};
+
+template <int U, bool NT, bool ALIGN>
+__global__ void __launch_bounds__(kBlock)
+    verify_quad_kernel(const uint8_t* __restrict__ arena, uint64_t arena_bytes, const cts_buf_desc* __restrict__ descs,
+                       uint32_t n, cts_verify_result* __restrict__ results, uint64_t* __restrict__ counters,
+                       uint32_t* __restrict__ conn_first_fail, uint32_t n_conns)
+{
+    constexpr int TEAMS = kBlock / kQuadTeam;
+    __shared__ uint64_t ctr[TEAMS][5];
+    const uint32_t lane = threadIdx.x & (kQuadTeam - 1);
+    const uint32_t team = threadIdx.x / kQuadTeam;
+    const uint32_t nteams = gridDim.x * TEAMS;
+    // the descriptor array holds >= 24 bytes: its first 16-byte-aligned chunk is the
+    // dummy target of an empty span's clamped loads
+    const void* dummy = reinterpret_cast<const void*>(((uintptr_t)descs + 15u) & ~(uintptr_t)15u);
+    QCounters qc;
+    uint32_t i = blockIdx.x * TEAMS + team;
+    cts_buf_desc dn = descs[i < n ? i : n - 1u];  // n >= 1 (launch_verify returns early on 0)
+    while (__any(i < n)) {
+        const cts_buf_desc d = dn;
+        const uint32_t inext = i + nteams > i ? i + nteams : n;  // (wrap guard)
+        dn = descs[inext < n ? inext : n - 1u];                  // clamped: no load under a branch
+        const bool live = i < n;
+        const bool ok = live && !desc_bad(d, arena_bytes);
+        const QSpan q = quad_span<ALIGN>(arena + d.byte_offset + d.skip_head, ok ? d.length - d.skip_head : 0u,
+                                         d.expected_pattern_offset, dummy);
+        // edge chunks first (their latency hides under the interior rounds)
+        const uint32_t ce = quad_edge_chunk(q, lane);
+        const u32x4 edge = load_chunk_g<NT>(q.p + ce);
+        uint32_t acc = quad_scan_interior<U, NT>(q, lane);
+        acc |= quad_edge_used(q, lane) ? or4(quad_edge_xor(q, ce, edge)) : 0u;
+        uint32_t first = kNone, count = 0;
+        if (__any(acc != 0u)) {  // rare: exact re-read of the dirty lanes' own chunks
+            if (acc != 0u) quad_scan_exact<NT>(q, lane, first, count);
+            quad_team_reduce(first, count);
+        }
+        if (lane == 0u && live) {
+            if (!ok) {
+                write_bad(results, i);
+            } else {
+                const bool pass = first == kNone;
+                if (results != nullptr) {
+                    cts_verify_result rec;
+                    rec.first_mismatch = pass ? q.len : first;
+                    rec.mismatch_bytes = pass ? 0u : count;
+                    rec.expected = pass ? 0 : (uint8_t)pattern_byte_dev(d.expected_pattern_offset + first);
+                    rec.actual = pass ? 0 : q.sp[first];
+                    rec.pass = pass ? 1 : 0;
+                    rec.flags = 0;
+                    results[i] = rec;
+                }
+                qc.add(q.len, pass, count);
+                if (!pass && conn_first_fail != nullptr && d.conn_index < n_conns)
+                    atomicMin(&conn_first_fail[d.conn_index], i);
+            }
+        }
+        i = inext;
+    }
+    qc.flush<TEAMS>(ctr, team, lane, counters);
+}
+
+// ---------------------------------------------------------------------------------------------
 // One wave per buffer, software-pipelined across buffers (datagram-sized spans):
 // the loads of the next buffer (edge/head chunks + one interior round of U
 // chunks per lane) are in flight while the current buffer is compared, so a wave
@@ -1066,6 +1301,134 @@ __global__ void __launch_bounds__(kBlock)
     flush_counters<WAVES>(counters, ctr);
 }
 
+// MediaStream receive, four datagrams per wave (16-lane teams; see verify_quad_kernel).
+// Team lane j loads header bytes j and j + 16 (bytes past the completed length read as 0,
+// from the dummy address) alongside the speculative DATA payload stream; the header dwords
+// reach the team leader through lane shuffles, with no dependent memory round trip.
+__device__ __forceinline__ uint8_t load_byte_g(const uint8_t* p)
+{
+    return *(const uint8_t __attribute__((address_space(1)))*)p;
+}
+
+template <int U, bool NT, bool ALIGN>
+__global__ void __launch_bounds__(kBlock)
+    media_stream_verify_quad_kernel(const uint8_t* __restrict__ arena, uint64_t arena_bytes,
+                                    const cts_buf_desc* __restrict__ descs, uint32_t n,
+                                    cts_datagram_record* __restrict__ records, cts_verify_result* __restrict__ results,
+                                    uint64_t* __restrict__ counters)
+{
+    constexpr int TEAMS = kBlock / kQuadTeam;
+    __shared__ uint64_t ctr[TEAMS][5];
+    const uint32_t lane = threadIdx.x & (kQuadTeam - 1);
+    const uint32_t team = threadIdx.x / kQuadTeam;
+    const uint32_t nteams = gridDim.x * TEAMS;
+    const void* dummy = reinterpret_cast<const void*>(((uintptr_t)descs + 15u) & ~(uintptr_t)15u);
+    const uint8_t* dummy8 = reinterpret_cast<const uint8_t*>(dummy);
+    QCounters qc;
+    uint32_t i = blockIdx.x * TEAMS + team;
+    cts_buf_desc dn = descs[i < n ? i : n - 1u];
+    while (__any(i < n)) {
+        const cts_buf_desc d = dn;
+        const uint32_t inext = i + nteams > i ? i + nteams : n;
+        dn = descs[inext < n ? inext : n - 1u];
+        const bool live = i < n;
+        const uint32_t completed = d.length;
+        const bool bad = d.byte_offset > arena_bytes || arena_bytes - d.byte_offset < (uint64_t)completed;
+        const bool in = live && !bad;
+        const uint8_t* dg = arena + d.byte_offset;
+        // header bytes j and j + 16 of this team's datagram (0 past the completed bytes)
+        const bool h0 = in && lane < completed;
+        const bool h1 = in && lane + 16u < CTS_UDP_DATA_HEADER_LENGTH && lane + 16u < completed;
+        uint32_t hb0 = load_byte_g(h0 ? dg + lane : dummy8);
+        uint32_t hb1 = load_byte_g(h1 ? dg + lane + 16u : dummy8);
+        // speculative DATA payload: [26, completed) at pattern offset 0
+        const bool maybe_data = in && completed >= CTS_UDP_DATA_HEADER_LENGTH;
+        const QSpan q = quad_span<ALIGN>(dg + CTS_UDP_DATA_HEADER_LENGTH,
+                                         maybe_data ? completed - CTS_UDP_DATA_HEADER_LENGTH : 0u, 0u, dummy);
+        const uint32_t ce = quad_edge_chunk(q, lane);
+        const u32x4 edge = load_chunk_g<NT>(q.p + ce);
+        uint32_t acc = quad_scan_interior<U, NT>(q, lane);
+        acc |= quad_edge_used(q, lane) ? or4(quad_edge_xor(q, ce, edge)) : 0u;
+        // header dwords: lane 4k packs bytes 4k..4k+3 of each half; every lane gathers
+        hb0 = h0 ? hb0 : 0u;
+        hb1 = h1 ? hb1 : 0u;
+        uint32_t w0 = hb0, w1 = hb1;
+#pragma unroll
+        for (int b = 1; b < 4; ++b) {
+            w0 |= (uint32_t)__shfl_down((int)hb0, b, kQuadTeam) << (8 * b);
+            w1 |= (uint32_t)__shfl_down((int)hb1, b, kQuadTeam) << (8 * b);
+        }
+        // (every lane needs them: the DATA verdict gates each lane's differences)
+        const uint32_t H0 = (uint32_t)__shfl((int)w0, 0, kQuadTeam);     // bytes 0..3
+        const uint32_t H1 = (uint32_t)__shfl((int)w0, 4, kQuadTeam);     // 4..7
+        const uint32_t H2 = (uint32_t)__shfl((int)w0, 8, kQuadTeam);     // 8..11
+        const uint32_t H3 = (uint32_t)__shfl((int)w0, 12, kQuadTeam);    // 12..15
+        const uint32_t H4 = (uint32_t)__shfl((int)w1, 0, kQuadTeam);     // 16..19
+        const uint32_t H5 = (uint32_t)__shfl((int)w1, 4, kQuadTeam);     // 20..23
+        // header: ctsMediaStreamMessage::ValidateBufferLengthFromTask (ctsMediaStreamProtocol.hpp:284-329)
+        uint32_t flag = 0, kind;
+        if (bad) {
+            kind = CTS_DGRAM_BAD_DESC;
+        } else if (completed == 0u) {
+            kind = CTS_DGRAM_ZERO;
+        } else if (completed < CTS_UDP_FLAG_LENGTH) {
+            kind = CTS_DGRAM_SHORT;
+        } else {
+            flag = H0 & 0xFFFFu;
+            if (flag == CTS_UDP_FLAG_DATA)
+                kind = completed < CTS_UDP_DATA_HEADER_LENGTH ? CTS_DGRAM_SHORT : CTS_DGRAM_DATA;
+            else if (flag == CTS_UDP_FLAG_ID)
+                kind = completed < CTS_UDP_CONNECTION_ID_HEADER_LENGTH ? CTS_DGRAM_SHORT : CTS_DGRAM_ID;
+            else
+                kind = CTS_DGRAM_UNKNOWN;
+        }
+        const bool data = kind == CTS_DGRAM_DATA;
+        uint32_t first = kNone, count = 0;
+        if (__any(acc != 0u && data)) {  // rare: exact re-read (non-DATA teams' differences are discarded)
+            if (acc != 0u && data) quad_scan_exact<NT>(q, lane, first, count);
+            quad_team_reduce(first, count);
+        }
+        if (lane == 0u && live) {
+            if (records != nullptr) {
+                cts_datagram_record rec;
+                // GetSequenceNumberFromTask: i64 at byte 2; ctsIOPatternMediaStream.cpp:218-219 read
+                // the sender qpc / qpf at bytes 8 and 16 of the buffer
+                const uint64_t seq = (uint64_t)((H0 >> 16) | (H1 << 16)) | ((uint64_t)((H1 >> 16) | (H2 << 16)) << 32);
+                rec.sequence_number = data ? (int64_t)seq : 0;
+                rec.sender_qpc = data ? (int64_t)((uint64_t)H2 | ((uint64_t)H3 << 32)) : 0;
+                rec.sender_qpf = data ? (int64_t)((uint64_t)H4 | ((uint64_t)H5 << 32)) : 0;
+                rec.flag = (uint16_t)flag;
+                rec.kind = (uint8_t)kind;
+                rec.reserved = 0;
+                rec.completed_bytes = completed;
+                records[i] = rec;
+            }
+            if (!data) {
+                if (results != nullptr) {
+                    cts_verify_result r{};
+                    r.flags = kind == CTS_DGRAM_BAD_DESC ? CTS_RESULT_FLAG_BAD_DESC : CTS_RESULT_FLAG_NOT_DATA;
+                    results[i] = r;
+                }
+            } else {
+                const bool pass = first == kNone;
+                if (results != nullptr) {
+                    cts_verify_result rec;
+                    rec.first_mismatch = pass ? q.len : first;
+                    rec.mismatch_bytes = pass ? 0u : count;
+                    rec.expected = pass ? 0 : (uint8_t)pattern_byte_dev(first);
+                    rec.actual = pass ? 0 : q.sp[first];
+                    rec.pass = pass ? 1 : 0;
+                    rec.flags = 0;
+                    results[i] = rec;
+                }
+                qc.add(q.len, pass, count);
+            }
+        }
+        i = inext;
+    }
+    qc.flush<TEAMS>(ctr, team, lane, counters);
+}
+
 // Send: header {u16 0, i64 seq, i64 qpc, i64 qpf} + P[0 .. length-26) per datagram
 // (ctsMediaStreamSendRequests' WSABUF array, ctsMediaStreamProtocol.hpp:230-243).
 __global__ void __launch_bounds__(kBlock)
@@ -1102,10 +1465,10 @@ __global__ void __launch_bounds__(kBlock)
 }
 
 // ---------------------------------------------------------------------------------------------
-static inline uint32_t grid_for(uint32_t n, int teams_per_block, const LaunchGeometry& geo)
+static inline uint32_t grid_for(uint32_t n, int teams_per_block, const LaunchGeometry& geo, int bpc_cap = 0)
 {
     const uint64_t want = ((uint64_t)n + teams_per_block - 1) / teams_per_block;
-    const int bpc = teams_per_block > 1 ? geo.small_blocks_per_cu : geo.blocks_per_cu;
+    const int bpc = bpc_cap > 0 ? bpc_cap : (teams_per_block > 1 ? geo.small_blocks_per_cu : geo.blocks_per_cu);
     const uint64_t cap = (uint64_t)geo.num_cus * (uint64_t)(bpc > 0 ? bpc : 8);
     // grid-stride with the same number of teams' worth of work per workgroup: past the cap
     // the grid shrinks to ceil(want / per) so no workgroup runs one buffer more than the
@@ -1124,10 +1487,17 @@ static void launch_verify_nt(const uint8_t* arena, uint64_t arena_bytes, const c
                              uint32_t n_conns, hipStream_t stream, const LaunchGeometry& geo)
 {
     if (small) {
-        // variant (small path): 0 = U2, 1 = U1, 2 = U4 (chunks per lane per round),
-        // 3 = pipelined across buffers U2, 4 = pipelined U1
+        // small_variant: 0 = one wave per buffer U2, 1 = U1, 2 = U4 (chunks per lane per round),
+        // 3 = pipelined across buffers U2, 4 = pipelined U1,
+        // 5 = four buffers per wave (16-lane teams) U6, 6 = same, line-aligned rounds U7,
+        // 7 = line-aligned U6, 8 = U4
         const uint32_t grid = grid_for(n, kBlock / 64, geo);
-        switch (geo.verify_variant) {
+        const uint32_t qgrid = grid_for(n, kBlock / kQuadTeam, geo);
+        switch (geo.small_variant) {
+        case 5: verify_quad_kernel<6, NT, false><<<qgrid, kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
+        case 6: verify_quad_kernel<7, NT, true><<<qgrid, kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
+        case 7: verify_quad_kernel<6, NT, true><<<qgrid, kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
+        case 8: verify_quad_kernel<4, NT, false><<<qgrid, kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 1: verify_wave_kernel<1, NT><<<grid, kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 2: verify_wave_kernel<4, NT><<<grid, kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 3: verify_wave_pipe_kernel<2, NT><<<grid, kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
@@ -1187,7 +1557,7 @@ hipError_t launch_fill(uint8_t* arena, uint64_t arena_bytes, const cts_buf_desc*
     if (small) {
         fill_kernel<64><<<grid_for(n, kBlock / 64, geo), kBlock, 0, stream>>>(arena, arena_bytes, descs, n);
     } else {
-        fill_kernel<kBlock><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(arena, arena_bytes, descs, n);
+        fill_kernel<kBlock><<<grid_for(n, 1, geo, geo.fill_blocks_per_cu), kBlock, 0, stream>>>(arena, arena_bytes, descs, n);
     }
     return hipGetLastError();
 }
@@ -1197,6 +1567,16 @@ hipError_t launch_media_stream_verify(const uint8_t* arena, uint64_t arena_bytes
                                      hipStream_t stream, const LaunchGeometry& geo)
 {
     if (n == 0) return hipSuccess;
+    if (geo.small_variant >= 5) {  // four datagrams per wave (the small-path default)
+        const uint32_t qgrid = grid_for(n, kBlock / kQuadTeam, geo);
+        if (geo.nontemporal)
+            media_stream_verify_quad_kernel<6, true, true><<<qgrid, kBlock, 0, stream>>>(arena, arena_bytes, descs, n,
+                                                                                        records, results, counters);
+        else
+            media_stream_verify_quad_kernel<6, false, true><<<qgrid, kBlock, 0, stream>>>(arena, arena_bytes, descs, n,
+                                                                                         records, results, counters);
+        return hipGetLastError();
+    }
     const uint32_t grid = grid_for(n, kBlock / 64, geo);
     if (geo.nontemporal)
         media_stream_verify_kernel<2, true><<<grid, kBlock, 0, stream>>>(arena, arena_bytes, descs, n, records, results,

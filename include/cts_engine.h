@@ -116,14 +116,16 @@ int cts_engine_device(const cts_engine* engine);
 
 /* Launch-geometry attributes (defaults tuned for MI355X; env overrides
  * CTS_BLOCKS_PER_CU / CTS_NT_LOADS / CTS_SMALL_THRESHOLD / CTS_VERIFY_VARIANT /
- * CTS_SMALL_BLOCKS_PER_CU
+ * CTS_SMALL_BLOCKS_PER_CU / CTS_SMALL_VARIANT / CTS_FILL_BLOCKS_PER_CU
  * are read at create time). */
 typedef enum cts_engine_attr {
     CTS_ATTR_BLOCKS_PER_CU = 1,   /* grid cap = CUs x this (grid-strides beyond) */
     CTS_ATTR_NT_LOADS = 2,        /* 1 = nontemporal loads on the verify stream */
     CTS_ATTR_SMALL_THRESHOLD = 3, /* max_length_hint <= this -> one wave per buffer */
     CTS_ATTR_VERIFY_VARIANT = 4,  /* kernel variant (see cts_kernels.hip launch_verify) */
-    CTS_ATTR_SMALL_BLOCKS_PER_CU = 5 /* grid cap of the wave-per-buffer (small) path */
+    CTS_ATTR_SMALL_BLOCKS_PER_CU = 5, /* grid cap of the small-buffer path */
+    CTS_ATTR_SMALL_VARIANT = 6,       /* small-buffer (datagram) kernel variant */
+    CTS_ATTR_FILL_BLOCKS_PER_CU = 7   /* grid cap of the fill kernels */
 } cts_engine_attr;
 int cts_engine_set_attr(cts_engine* engine, int attr, int value);
 int cts_engine_get_attr(const cts_engine* engine, int attr, int* value);

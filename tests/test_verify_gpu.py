@@ -324,3 +324,47 @@ def test_launch_variants_parity(engine, variant, nt):
         engine.set_attr(_lib.ATTR_NT_LOADS, 1)
         engine.set_attr(_lib.ATTR_BLOCKS_PER_CU, default_bpc)
         engine.set_attr(_lib.ATTR_SMALL_BLOCKS_PER_CU, default_small_bpc)
+
+
+# ---- every small-buffer (datagram) kernel is bit-identical --------------------------------------
+@pytest.mark.parametrize("small_variant", list(range(9)))
+def test_small_variants_parity(engine, small_variant):
+    """Small-buffer path (max_length_hint <= 8192): one wave per buffer (0-4) and four
+    buffers per wave in 16-lane teams (5-8), vs the oracle. Includes spans longer than the
+    hint (multi-round teams), empty spans, all start alignments, bad descriptors, a batch
+    whose size is not a multiple of the team count, and config-3 datagrams."""
+    from ctstraffic_amd import _lib
+
+    default_sv = engine.get_attr(_lib.ATTR_SMALL_VARIANT)
+    default_sbpc = engine.get_attr(_lib.ATTR_SMALL_BLOCKS_PER_CU)
+    try:
+        engine.set_attr(_lib.ATTR_SMALL_VARIANT, small_variant)
+        for seed, n, max_len, hint, skip in [(31, 301, 1500, 1472, True), (32, 257, 200, 64, False),
+                                             (33, 120, 20000, 1472, True), (34, 1000, 3000, 8192, False),
+                                             (35, 7, 40, 40, True)]:
+            for sbpc in (1, 64):
+                engine.set_attr(_lib.ATTR_SMALL_BLOCKS_PER_CU, sbpc)
+                rng = np.random.default_rng(seed)
+                arena, descs = _random_case(rng, n, max_len, skip=skip)
+                r, ctr, cff = run_verify(engine, arena, descs, hint, n_conns=7)
+                er, ectr, ecff = oracle.verify_batch(arena, descs, n_conns=7)
+                assert_results_equal(r, er, "small variant %d seed %d sbpc %d" % (small_variant, seed, sbpc))
+                assert ctr == ectr
+                assert np.array_equal(cff, ecff)
+        arena = np.zeros(256, np.uint8)
+        oracle.fill(arena, np.array([(0, 256, 0, 0, 0)], dtype=oracle.DESC_DTYPE))
+        d = np.zeros(5, dtype=DESC_DTYPE)
+        d[0] = (0, 10, 65536, 0, 0)
+        d[1] = (0, 10, 0, 0, 11)
+        d[2] = (250, 10, 0, 0, 0)
+        d[3] = (2**40, 1, 0, 0, 0)
+        d[4] = (16, 32, 16, 0, 0)
+        r, ctr, _ = run_verify(engine, arena, d, 1472)
+        er, ectr, _ = oracle.verify_batch(arena, d)
+        assert_results_equal(r, er)
+        assert ctr == ectr and ctr["buffers_checked"] == 1
+        w = W.udp_datagrams(n_datagrams=4099, corrupt_rate=7)
+        _check_workload(engine, w, with_oracle=True)
+    finally:
+        engine.set_attr(_lib.ATTR_SMALL_VARIANT, default_sv)
+        engine.set_attr(_lib.ATTR_SMALL_BLOCKS_PER_CU, default_sbpc)

@@ -85,6 +85,22 @@ __global__ void __launch_bounds__(256) read_or_slab_gs(const u32x4* __restrict__
     if (acc == 0x12345678u) out[0] = acc;
 }
 
+// write reference for the fill kernel: the same slab shape, 16-byte nontemporal stores
+template <int U>
+__global__ void __launch_bounds__(256) write_slab_gs(u32x4* __restrict__ p, uint32_t per_block, uint32_t nslabs)
+{
+    for (uint32_t sl = blockIdx.x; sl < nslabs; sl += gridDim.x) {
+        u32x4* q = p + (uint64_t)sl * per_block;
+        for (uint32_t c = threadIdx.x; c < per_block; c += 256u * U) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t v = sl + c + (uint32_t)u;
+                __builtin_nontemporal_store(u32x4{v, v + 1u, v + 2u, v + 3u}, q + c + u * 256u);
+            }
+        }
+    }
+}
+
 // ctsTraffic's byte pattern (u16 ramp mod 32768, 64 KiB period) instead of a constant:
 // the verify stream reads bytes that toggle; a memset arena does not
 __global__ void fill_ramp(uint32_t* p, uint64_t nwords)
@@ -118,7 +134,7 @@ int main(int argc, char** argv)
 {
     int cus = 0;
     CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
-    // argv: [reps] [arena MiB (256 = one config-2 batch)] [quick: 1 = two configs only]
+    // argv: [reps] [arena MiB (256 = one config-2 batch)] [quick: 1 = two configs only] [ramp] [writes: 1 = store sweep]
     const size_t arena = (size_t)(argc > 2 ? atoi(argv[2]) : 256) << 20;
     const bool quick = argc > 3 && atoi(argv[3]) != 0;
     const bool ramp = argc > 4 && atoi(argv[4]) != 0;  // arena holds the ctsTraffic pattern
@@ -165,6 +181,29 @@ int main(int argc, char** argv)
                U, (int)NT, (int)STAG, BPC, ms * 1e3, arena / (ms * 1e-3) / 1e9);                                 \
     } while (0)
 
+#define RUN_WR(U, BPC)                                                                                        \
+    do {                                                                                                      \
+        const uint32_t nsl = (uint32_t)(arena / 65536);                                                       \
+        const uint32_t grid = (uint32_t)cus * (BPC);                                                          \
+        float ms = time_ms([&](int i) { write_slab_gs<U><<<grid, 256, 0, s>>>(bufs[i % R], 4096u, nsl); }, reps, s); \
+        printf("{\"kind\":\"write_slab_gs\",\"U\":%d,\"nt\":1,\"blocks_per_cu\":%d,\"us\":%.2f,\"GBps\":%.1f}\n", U, \
+               BPC, ms * 1e3, arena / (ms * 1e-3) / 1e9);                                                     \
+    } while (0)
+
+    const bool writes = argc > 5 && atoi(argv[5]) != 0;
+    if (writes) {
+        for (int pass = 0; pass < 2; ++pass) {
+            RUN_WR(1, 4);
+            RUN_WR(2, 4);
+            RUN_WR(4, 4);
+            RUN_WR(4, 8);
+            RUN_WR(2, 8);
+            RUN_WR(1, 8);
+            RUN_WR(4, 2);
+            RUN_WR(4, 16);
+        }
+        return 0;
+    }
     if (quick) {
         for (int pass = 0; pass < 2; ++pass) {
             RUN_GS(8, true, 8);

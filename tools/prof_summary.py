@@ -25,9 +25,11 @@ import numpy as np
 WORKLOADS = {
     "verify_wg_kernel": "config2 verify: 4096 x 64 KiB (268435456 B read)",
     "verify_wave_kernel": "config3/4 verify: 4M x 1472 B datagrams (6065743872 B payload read)",
+    "verify_quad_kernel": "config3/4 verify: 4M x 1472 B datagrams (6065743872 B payload read)",
     "fill_kernel": "config2 fill: 4096 x 64 KiB (268435456 B written)",
 }
-ALGO_BYTES = {"verify_wg_kernel": 268435456, "verify_wave_kernel": 4194304 * 1446, "fill_kernel": 268435456}
+ALGO_BYTES = {"verify_wg_kernel": 268435456, "verify_wave_kernel": 4194304 * 1446, "verify_quad_kernel": 4194304 * 1446,
+              "fill_kernel": 268435456}
 
 
 def _kname(name):

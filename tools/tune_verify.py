@@ -30,6 +30,8 @@ def main():
     p.add_argument("--buffers", type=int, default=4096)
     p.add_argument("--corrupt-rate", type=int, default=1024, help="1 in N buffers corrupted (0 = none)")
     p.add_argument("--results", action="store_true", help="also write the per-buffer result records")
+    p.add_argument("--op", default="verify", choices=["verify", "fill"],
+                   help="fill: time cts_fill over the same descriptors (write-bound twin)")
     args = p.parse_args()
     torch.cuda.set_device(0)
     eng = Engine(0)
@@ -52,22 +54,32 @@ def main():
     for r in range(args.rounds):
         for c in combos:
             v, bpc, nt = c
-            eng.set_attr(_lib.ATTR_VERIFY_VARIANT, v)
+            # the variant list names small-path kernels for config3 (datagrams), else large-path ones
+            eng.set_attr(_lib.ATTR_SMALL_VARIANT if args.workload == "config3" else _lib.ATTR_VERIFY_VARIANT, v)
             eng.set_attr(_lib.ATTR_BLOCKS_PER_CU, bpc)
+            eng.set_attr(_lib.ATTR_FILL_BLOCKS_PER_CU, bpc)
             eng.set_attr(_lib.ATTR_SMALL_BLOCKS_PER_CU, bpc)
             eng.set_attr(_lib.ATTR_NT_LOADS, nt)
             eng.reset_counters(ctr)
             # region timing: per-launch event pairs add ~2.5 us to every launch on this stack
             ea, eb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            eng.verify(arenas[0], descs, max_length_hint=w.max_length, counters=ctr, results=res)
-            ea.record(s)
-            for i in range(args.launches - 1):
-                eng.verify(arenas[(i + 1) % len(arenas)], descs, max_length_hint=w.max_length, counters=ctr,
-                           results=res)
-            eb.record(s)
-            torch.cuda.synchronize()
-            got = eng.read_counters(ctr)
-            assert got == {k: v_ * args.launches for k, v_ in exp.items()}, (c, got)
+            if args.op == "fill":
+                eng.fill(arenas[0], descs, max_length_hint=w.max_length)
+                ea.record(s)
+                for i in range(args.launches - 1):
+                    eng.fill(arenas[(i + 1) % len(arenas)], descs, max_length_hint=w.max_length)
+                eb.record(s)
+                torch.cuda.synchronize()
+            else:
+                eng.verify(arenas[0], descs, max_length_hint=w.max_length, counters=ctr, results=res)
+                ea.record(s)
+                for i in range(args.launches - 1):
+                    eng.verify(arenas[(i + 1) % len(arenas)], descs, max_length_hint=w.max_length, counters=ctr,
+                               results=res)
+                eb.record(s)
+                torch.cuda.synchronize()
+                got = eng.read_counters(ctr)
+                assert got == {k: v_ * args.launches for k, v_ in exp.items()}, (c, got)
             times[c].append(ea.elapsed_time(eb) / (args.launches - 1))
     nbytes = w.verified_bytes()
     rows = []
@@ -76,7 +88,7 @@ def main():
         rows.append({"variant": c[0], "blocks_per_cu": c[1], "nt": c[2], "us": round(t * 1e6, 2),
                      "GBps": round(nbytes / t / 1e9, 1), "spread_us": round((max(times[c]) - min(times[c])) * 1e3, 2)})
     rows.sort(key=lambda x: x["us"])
-    print(json.dumps({"workload": w.name, "bytes": nbytes, "results": bool(args.results), "rows": rows}, indent=0))
+    print(json.dumps({"workload": w.name, "op": args.op, "bytes": nbytes, "results": bool(args.results), "rows": rows}, indent=0))
 
 
 if __name__ == "__main__":
