@@ -260,6 +260,15 @@ def test_config4_full_shard(engine):
     _check_workload(engine, W.connection_streams(world=4, rank=0), with_oracle=False)
 
 
+def test_config5_full_shard(engine):
+    """8 M x 64 KiB over 8 GPUs (512 GiB): this GPU verifies rank 0's hash shard, ~1 M buffers = ~64 GiB
+    resident at once, checked against the analytic outcome (per-buffer records, counters, DataError slots)."""
+    w = W.connection_streams(n_conns=8192, buffers_per_conn=1024, world=8, rank=0, name="config5")
+    assert w.verified_bytes() > 60 * 2**30
+    _check_workload(engine, w, with_oracle=False)
+    torch.cuda.empty_cache()
+
+
 # ---- host-buffer paths ------------------------------------------------------------------------------
 def test_verify_host_single(engine):
     S = oracle.sender_buffer(70000)

@@ -20,16 +20,21 @@ from collections import defaultdict
 
 import numpy as np
 
-# kernel name -> workload tag, per bench.py's launches (the profiled runs pass --no-extras, so
-# each kernel has one workload; the grid depends on the launch geometry and is only reported)
+# kernel name -> workload tag, per bench.py's launches. Two profiled runs: prof_* is the config-2
+# headline (bench.py --no-extras), prof_dg_* the config-3 datagram extras (--extras-only datagram);
+# each kernel is summarised from the first run that launched it most, and reports its grid.
+DG = 16 * 1024 * 1024
 WORKLOADS = {
     "verify_wg_kernel": "config2 verify: 4096 x 64 KiB (268435456 B read)",
-    "verify_wave_kernel": "config3/4 verify: 4M x 1472 B datagrams (6065743872 B payload read)",
-    "verify_quad_kernel": "config3/4 verify: 4M x 1472 B datagrams (6065743872 B payload read)",
     "fill_kernel": "config2 fill: 4096 x 64 KiB (268435456 B written)",
+    "verify_quad_kernel": "config3 verify: 16M x 1472 B datagrams (%d B payload read)" % (DG * 1446),
+    "verify_wave_kernel": "config3 verify: 16M x 1472 B datagrams (%d B payload read)" % (DG * 1446),
+    "media_stream_verify_quad_kernel": "config3 MediaStream receive: 16M x 1472 B datagrams (%d B payload read)" % (
+        DG * 1446),
 }
-ALGO_BYTES = {"verify_wg_kernel": 268435456, "verify_wave_kernel": 4194304 * 1446, "verify_quad_kernel": 4194304 * 1446,
-              "fill_kernel": 268435456}
+ALGO_BYTES = {"verify_wg_kernel": 268435456, "fill_kernel": 268435456, "verify_quad_kernel": DG * 1446,
+              "verify_wave_kernel": DG * 1446, "media_stream_verify_quad_kernel": DG * 1446}
+RUNS = ("prof", "prof_dg")
 
 
 def _kname(name):
@@ -40,45 +45,56 @@ def _grid(r):
     return r.get("Grid_Size") or r.get("Grid_Size_X")
 
 
+def _by_kernel(rows, value):
+    """{kernel: (grid, [values])} keeping, per kernel, the grid launched most often."""
+    by = defaultdict(list)
+    for r in rows:
+        k = _kname(r["Kernel_Name"])
+        if k in WORKLOADS:
+            by[(k, _grid(r))].append(value(r))
+    best = {}
+    for (k, g), v in by.items():
+        if k not in best or len(v) > len(best[k][1]):
+            best[k] = (g, v)
+    return best
+
+
 def main(src, dst):
     os.makedirs(dst, exist_ok=True)
-    ks = os.path.join(src, "prof_kt", "run_kernel_stats.csv")
-    if os.path.exists(ks):
-        shutil.copy(ks, os.path.join(dst, "kernel_stats.csv"))
+    for run in RUNS:
+        ks = os.path.join(src, run + "_kt", "run_kernel_stats.csv")
+        if os.path.exists(ks):
+            shutil.copy(ks, os.path.join(dst, "kernel_stats.csv" if run == "prof" else "kernel_stats_datagram.csv"))
     out = {}
-    tr = os.path.join(src, "prof_kt", "run_kernel_trace.csv")
-    if os.path.exists(tr):
-        by = defaultdict(list)
-        for r in csv.DictReader(open(tr)):
-            by[(_kname(r["Kernel_Name"]), _grid(r))].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
-        for k, d in by.items():
-            if k[0] not in WORKLOADS:
-                continue
-            # one grid per kernel: the one launched most often
-            if len(d) < max(len(v) for kk, v in by.items() if kk[0] == k[0]):
+    for run in RUNS:
+        tr = os.path.join(src, run + "_kt", "run_kernel_trace.csv")
+        if not os.path.exists(tr):
+            continue
+        best = _by_kernel(csv.DictReader(open(tr)), lambda r: int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+        for k, (g, d) in best.items():
+            if WORKLOADS[k] in out:
                 continue
             d = np.array(d)
-            out[WORKLOADS[k[0]]] = {"kernel": k[0], "grid": int(k[1]), "launches": int(d.size),
+            out[WORKLOADS[k]] = {"kernel": k, "grid": int(g), "launches": int(d.size), "run": run,
                                  "avg_us": round(float(d.mean()) / 1e3, 2), "median_us": round(float(np.median(d)) / 1e3, 2),
                                  "min_us": round(float(d.min()) / 1e3, 2),
-                                 "algorithmic_GBps_at_avg": round(ALGO_BYTES[k[0]] / float(d.mean()), 1)}
+                                 "algorithmic_GBps_at_avg": round(ALGO_BYTES[k] / float(d.mean()), 1)}
+    if out:
         json.dump(out, open(os.path.join(dst, "kernel_trace_summary.json"), "w"), indent=1)
     pmc = {}
-    for ctr in ("FETCH_SIZE", "WRITE_SIZE", "TCC_EA0_RDREQ_sum"):
-        p = os.path.join(src, "prof_pmc_%s" % ctr, "run_counter_collection.csv")
-        if not os.path.exists(p):
-            continue
-        by = defaultdict(list)
-        for r in csv.DictReader(open(p)):
-            by[(_kname(r["Kernel_Name"]), _grid(r))].append(float(r["Counter_Value"]))
-        for k, v in by.items():
-            if k[0] not in WORKLOADS:
+    for run in RUNS:
+        for ctr in ("FETCH_SIZE", "WRITE_SIZE", "TCC_EA0_RDREQ_sum"):
+            p = os.path.join(src, "%s_pmc_%s" % (run, ctr), "run_counter_collection.csv")
+            if not os.path.exists(p):
                 continue
-            if len(v) < max(len(vv) for kk, vv in by.items() if kk[0] == k[0]):
-                continue
-            e = pmc.setdefault(WORKLOADS[k[0]], {"kernel": k[0], "grid": int(k[1]), "algorithmic_bytes": ALGO_BYTES[k[0]]})
-            e[ctr + "_median"] = float(np.median(v))
-            e["launches_" + ctr] = len(v)
+            best = _by_kernel(csv.DictReader(open(p)), lambda r: float(r["Counter_Value"]))
+            for k, (g, v) in best.items():
+                e = pmc.setdefault(WORKLOADS[k], {"kernel": k, "grid": int(g), "run": run,
+                                                  "algorithmic_bytes": ALGO_BYTES[k]})
+                if e["run"] != run or ctr + "_median" in e:
+                    continue
+                e[ctr + "_median"] = float(np.median(v))
+                e["launches_" + ctr] = len(v)
     for name, e in pmc.items():
         if "FETCH_SIZE_median" in e:
             e["hbm_read_bytes_per_launch"] = int(2 * 1024 * e["FETCH_SIZE_median"])
