@@ -234,7 +234,7 @@ int cts_fill(cts_engine* e, void* dev_arena, uint64_t arena_bytes, const cts_buf
 {
     if (e == nullptr) return CTS_E_INVALID;
     if (n == 0) return CTS_OK;
-    if (dev_arena == nullptr || dev_descs == nullptr || ((uintptr_t)dev_arena & 15u) != 0) return CTS_E_INVALID;
+    if (dev_arena == nullptr || dev_descs == nullptr || ((uintptr_t)dev_descs & 7u) != 0 || ((uintptr_t)dev_arena & 15u) != 0) return CTS_E_INVALID;
     DeviceGuard g(e->device);
     if (!g.ok) return CTS_E_HIP;
     return hip_status(cts::launch_fill(static_cast<uint8_t*>(dev_arena), arena_bytes, dev_descs, n, max_length_hint,
@@ -247,7 +247,7 @@ int cts_verify(cts_engine* e, const void* dev_arena, uint64_t arena_bytes, const
 {
     if (e == nullptr) return CTS_E_INVALID;
     if (n == 0) return CTS_OK;
-    if (dev_arena == nullptr || dev_descs == nullptr || ((uintptr_t)dev_arena & 15u) != 0) return CTS_E_INVALID;
+    if (dev_arena == nullptr || dev_descs == nullptr || ((uintptr_t)dev_descs & 7u) != 0 || ((uintptr_t)dev_arena & 15u) != 0) return CTS_E_INVALID;
     if (dev_conn_first_fail == nullptr && n_conns != 0) return CTS_E_INVALID;
     DeviceGuard g(e->device);
     if (!g.ok) return CTS_E_HIP;
@@ -261,7 +261,7 @@ int cts_media_stream_fill(cts_engine* e, void* dev_arena, uint64_t arena_bytes, 
 {
     if (e == nullptr) return CTS_E_INVALID;
     if (n == 0) return CTS_OK;
-    if (dev_arena == nullptr || dev_descs == nullptr || dev_headers == nullptr) return CTS_E_INVALID;
+    if (dev_arena == nullptr || dev_descs == nullptr || ((uintptr_t)dev_descs & 7u) != 0 || dev_headers == nullptr) return CTS_E_INVALID;
     DeviceGuard g(e->device);
     if (!g.ok) return CTS_E_HIP;
     return hip_status(cts::launch_media_stream_fill(static_cast<uint8_t*>(dev_arena), arena_bytes, dev_descs,
@@ -274,7 +274,7 @@ int cts_media_stream_verify(cts_engine* e, const void* dev_arena, uint64_t arena
 {
     if (e == nullptr) return CTS_E_INVALID;
     if (n == 0) return CTS_OK;
-    if (dev_arena == nullptr || dev_descs == nullptr || ((uintptr_t)dev_arena & 15u) != 0) return CTS_E_INVALID;
+    if (dev_arena == nullptr || dev_descs == nullptr || ((uintptr_t)dev_descs & 7u) != 0 || ((uintptr_t)dev_arena & 15u) != 0) return CTS_E_INVALID;
     DeviceGuard g(e->device);
     if (!g.ok) return CTS_E_HIP;
     return hip_status(cts::launch_media_stream_verify(static_cast<const uint8_t*>(dev_arena), arena_bytes, dev_descs,

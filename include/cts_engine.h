@@ -141,7 +141,8 @@ int cts_sender_buffer_fill(cts_engine* engine, void* dev_dst, uint32_t max_buffe
  * sender at stream offset d.expected_pattern_offset puts on the wire
  * (ctsTask{m_buffer = S, m_bufferOffset = m_sendPatternOffset}, ctsIOPattern.cpp:676-697).
  * Header bytes [0, skip_head) are left untouched. max_length_hint selects the
- * launch geometry (0 = unknown). dev_arena must be 16-byte aligned. */
+ * launch geometry (0 = unknown). dev_arena must be 16-byte aligned, dev_descs
+ * 8-byte aligned (CTS_E_INVALID otherwise). */
 int cts_fill(cts_engine* engine, void* dev_arena, uint64_t arena_bytes,
              const cts_buf_desc* dev_descs, uint32_t n, uint32_t max_length_hint, void* stream);
 
@@ -158,7 +159,8 @@ int cts_fill(cts_engine* engine, void* dev_arena, uint64_t arena_bytes,
  *                           != 0xFFFFFFFF when descriptors of one connection are
  *                           in stream order.
  * dev_arena must be 16-byte aligned and its allocation must extend to a
- * multiple of 16 bytes (every hipMalloc allocation does). */
+ * multiple of 16 bytes (every hipMalloc allocation does); dev_descs must be
+ * 8-byte aligned (CTS_E_INVALID otherwise). */
 int cts_verify(cts_engine* engine, const void* dev_arena, uint64_t arena_bytes,
                const cts_buf_desc* dev_descs, uint32_t n, uint32_t max_length_hint,
                cts_verify_result* dev_results, void* dev_counters,

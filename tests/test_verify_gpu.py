@@ -161,6 +161,19 @@ def test_bad_descriptors(engine):
     assert ctr == ectr and ctr["buffers_checked"] == 1
 
 
+def test_misaligned_descriptor_array_is_rejected(engine):
+    """The kernels read descriptors as u64 fields: a descriptor array that is not
+    8-byte aligned is refused with CTS_E_INVALID, before any launch."""
+    from ctstraffic_amd._lib import CtsError
+
+    arena = torch.zeros(256, dtype=torch.uint8, device=DEV)
+    raw = torch.zeros(DESC_DTYPE.itemsize * 2 + 8, dtype=torch.uint8, device=DEV)
+    with pytest.raises(CtsError):
+        engine.verify(arena, raw[4:4 + DESC_DTYPE.itemsize], max_length_hint=0)
+    with pytest.raises(CtsError):
+        engine.fill(arena, raw[4:4 + DESC_DTYPE.itemsize], max_length_hint=0)
+
+
 def test_fill_matches_oracle_and_leaves_neighbours(engine):
     rng = np.random.default_rng(11)
     # aligned: 16-byte-aligned spans of whole chunks (the fill's straight-line store rounds;
