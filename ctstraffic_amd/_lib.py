@@ -42,6 +42,8 @@ ATTR_VERIFY_VARIANT = 4
 ATTR_SMALL_BLOCKS_PER_CU = 5
 ATTR_SMALL_VARIANT = 6
 ATTR_FILL_BLOCKS_PER_CU = 7
+ATTR_MS_VARIANT = 8
+ATTR_SMALL_CHUNK = 9
 
 
 class CtsError(RuntimeError):

@@ -134,6 +134,8 @@ int cts_engine_create(int device, cts_engine** out)
     e->geo.small_blocks_per_cu = env_int("CTS_SMALL_BLOCKS_PER_CU", e->geo.small_blocks_per_cu);
     e->geo.small_variant = env_int("CTS_SMALL_VARIANT", e->geo.small_variant);
     e->geo.fill_blocks_per_cu = env_int("CTS_FILL_BLOCKS_PER_CU", e->geo.fill_blocks_per_cu);
+    e->geo.ms_variant = env_int("CTS_MS_VARIANT", e->geo.ms_variant);
+    e->geo.small_chunk = env_int("CTS_SMALL_CHUNK", e->geo.small_chunk);
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
         delete e;
         return CTS_E_HIP;
@@ -201,6 +203,14 @@ int cts_engine_set_attr(cts_engine* e, int attr, int value)
         if (value < 1 || value > 64) return CTS_E_INVALID;
         e->geo.fill_blocks_per_cu = value;
         return CTS_OK;
+    case CTS_ATTR_MS_VARIANT:
+        if (value < 0 || value >= cts::kMediaStreamVariants) return CTS_E_INVALID;
+        e->geo.ms_variant = value;
+        return CTS_OK;
+    case CTS_ATTR_SMALL_CHUNK:
+        if (value < 0 || value > (1 << 24)) return CTS_E_INVALID;
+        e->geo.small_chunk = value;
+        return CTS_OK;
     default: return CTS_E_INVALID;
     }
 }
@@ -216,6 +226,8 @@ int cts_engine_get_attr(const cts_engine* e, int attr, int* value)
     case CTS_ATTR_SMALL_BLOCKS_PER_CU: *value = e->geo.small_blocks_per_cu; return CTS_OK;
     case CTS_ATTR_SMALL_VARIANT: *value = e->geo.small_variant; return CTS_OK;
     case CTS_ATTR_FILL_BLOCKS_PER_CU: *value = e->geo.fill_blocks_per_cu; return CTS_OK;
+    case CTS_ATTR_MS_VARIANT: *value = e->geo.ms_variant; return CTS_OK;
+    case CTS_ATTR_SMALL_CHUNK: *value = e->geo.small_chunk; return CTS_OK;
     default: return CTS_E_INVALID;
     }
 }

@@ -16,7 +16,8 @@ constexpr int kCounterSlots = 8;  // 5 used, padded to one 64-byte line
 enum CounterSlot { kBytesChecked = 0, kBytesOk = 1, kBuffersChecked = 2, kBuffersFailed = 3, kMismatchedBytes = 4 };
 
 constexpr int kVerifyVariants = 15;  // workgroup-per-buffer verify variants (launch_verify)
-constexpr int kSmallVariants = 9;    // small-buffer (datagram) verify variants
+constexpr int kSmallVariants = 10;   // small-buffer (datagram) verify variants
+constexpr int kMediaStreamVariants = 4;  // MediaStream receive kernels (launch_media_stream_verify)
 
 struct LaunchGeometry {
     int num_cus = 256;        // hipDeviceAttributeMultiprocessorCount
@@ -26,8 +27,14 @@ struct LaunchGeometry {
     int small_blocks_per_cu = 64; // wave-per-buffer grid cap
     int nontemporal = 1;      // nt loads for the once-read verify stream
     int small_threshold = 8192;  // max_length_hint <= this -> small-buffer path
-    int small_variant = 7;       // small-buffer path kernel (launch_verify_nt; 7 = four buffers per wave, line-aligned U6:
-                                 // config 3 at 5.95 TB/s of payload vs 4.71 for one wave per datagram)
+    int small_variant = 9;       // small-buffer path kernel (launch_verify_nt; 7 = four buffers per wave, line-aligned U6:
+                                 // config 3 at 5.95 TB/s of payload vs 4.71 for one wave per datagram; 9 = 7 walking
+                                 // block-contiguous ranges: 0-5 % faster, results +2 %; tools/media_stream_probe.py)
+    int ms_variant = 3;          // MediaStream receive kernel (launch_media_stream_verify; 3 = four datagrams per wave,
+                                 // 16-B header chunks + DPP, block-contiguous: with records + results 1.04-1.08 ms per
+                                 // 4 M datagrams vs 1.24 ms for variant 1 before output staging)
+    int small_chunk = 0;         // chunked walk of small variant 9 / MediaStream variant 3: buffers per chunk (0 = one
+                                 // contiguous range per workgroup)
     int fill_blocks_per_cu = 2;  // fill grid cap (write-bound: 2 measured best, tools/tune_verify.py --op fill)
     int verify_variant = 13;     // see launch_verify (13: variant 11 at U2; 11: variant 10 + in-register exact diff;
                                  // 10: even-phase stream + whole-line spans, U4, measured 1.3-3 % faster than 6,

@@ -937,28 +937,117 @@ struct QCounters {
     }
 };
 
-template <int U, bool NT, bool ALIGN>
+// Per-wave output staging for the four-buffers-per-wave kernels. Each team leader puts its
+// 12-byte result (and, for MediaStream, its 32-byte record) in LDS as whole dwords; the wave
+// then writes the four teams' outputs from consecutive lanes: one coalesced dword store covers
+// 4 x 12 = 48 contiguous result bytes, one covers 4 x 32 = 128 record bytes. Written directly,
+// each leader's struct became 4-lane sub-dword and unaligned stores (global_store_short/byte,
+// dword at +7): on 4 M datagrams the records alone added 265 us to a 920 us launch
+// (tools/media_stream_probe.py). Nontemporal stores here measured 2-4 % slower; write-through
+// (sc1) stores helped the records and hurt the results, and deferring the stores until the next
+// buffer's loads were in flight changed nothing (+-0.5 %).
+struct QuadOut {
+    uint32_t res[4][3];
+    uint32_t rec[4][8];
+};
+
+__device__ __forceinline__ uint32_t result_dw2(uint32_t expected, uint32_t actual, uint32_t pass, uint32_t flags)
+{
+    return (expected & 0xFFu) | ((actual & 0xFFu) << 8) | (pass << 16) | (flags << 24);  // bytes 8..11
+}
+
+__device__ __forceinline__ void quad_stage_result(QuadOut& o, uint32_t t, uint32_t first_mismatch,
+                                                  uint32_t mismatch_bytes, uint32_t dw2)
+{
+    o.res[t][0] = first_mismatch;
+    o.res[t][1] = mismatch_bytes;
+    o.res[t][2] = dw2;
+}
+
+// All 64 lanes of the wave call this after the leaders staged; i = this lane's buffer index
+// (the wave's four teams hold i0 .. i0 + 3, i0 = lane 0's), n = buffers in the launch.
+__device__ __forceinline__ void quad_flush_outputs(const QuadOut& o, uint32_t i, uint32_t n,
+                                                   cts_verify_result* results, cts_datagram_record* records)
+{
+    __builtin_amdgcn_wave_barrier();
+    // (64-bit: i0 + t may pass 2^32 on the wave's last round when n is close to it)
+    const uint64_t i0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)i);
+    const uint32_t l = threadIdx.x & 63u;
+    if (results != nullptr && l < 12u) {
+        const uint32_t t = l / 3u;
+        const uint32_t v = o.res[t][l - 3u * t];
+        if (i0 + t < n) reinterpret_cast<uint32_t*>(results)[3ull * i0 + l] = v;
+    }
+    if (records != nullptr && l < 32u) {
+        const uint32_t t = l >> 3;
+        const uint32_t v = o.rec[t][l & 7u];
+        if (i0 + t < n) reinterpret_cast<uint32_t*>(records)[8ull * i0 + l] = v;
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
+// Which buffers a team visits. Grid-stride (CONTIG = false): team k of block b takes
+// b * TEAMS + k, then steps by the grid's team count. Chunked (CONTIG = true): the buffers are cut
+// into chunks of `per` consecutive buffers (a multiple of TEAMS); block b walks chunks b, b + grid,
+// ... TEAMS buffers at a time, so the rounds of a wave write adjacent outputs and a 128-byte line
+// of 12-byte results fills up in ONE CU's L2 (grid-stride spreads a line over workgroups on
+// different XCDs: partial-line writes). per = TEAMS is the grid-stride walk; one chunk per block
+// is a fully block-contiguous walk.
+template <bool CONTIG, int TEAMS>
+struct QuadWalk {
+    uint32_t i, end;
+    uint64_t cbase;  // first buffer of the current chunk (CONTIG)
+    uint32_t per, team;
+    __device__ __forceinline__ QuadWalk(uint32_t n, uint32_t per_, uint32_t team_) : end(n), per(per_), team(team_)
+    {
+        if constexpr (CONTIG) {
+            cbase = (uint64_t)blockIdx.x * per;
+            i = cbase + team < (uint64_t)n ? (uint32_t)(cbase + team) : n;
+        } else {
+            cbase = 0;
+            i = blockIdx.x * TEAMS + team;
+        }
+    }
+    // the buffer after i (end when none); moves to the block's next chunk at a chunk's end
+    __device__ __forceinline__ uint32_t next()
+    {
+        uint64_t nx;
+        if constexpr (CONTIG) {
+            nx = (uint64_t)i + TEAMS;
+            if (nx - cbase >= per) {
+                cbase += (uint64_t)gridDim.x * per;
+                nx = cbase + team;
+            }
+        } else {
+            nx = (uint64_t)i + (uint64_t)gridDim.x * TEAMS;
+        }
+        return nx < (uint64_t)end ? (uint32_t)nx : end;
+    }
+};
+
+template <int U, bool NT, bool ALIGN, bool CONTIG = false>
 __global__ void __launch_bounds__(kBlock)
     verify_quad_kernel(const uint8_t* __restrict__ arena, uint64_t arena_bytes, const cts_buf_desc* __restrict__ descs,
                        uint32_t n, cts_verify_result* __restrict__ results, uint64_t* __restrict__ counters,
-                       uint32_t* __restrict__ conn_first_fail, uint32_t n_conns)
+                       uint32_t* __restrict__ conn_first_fail, uint32_t n_conns, uint32_t per = 0)
 {
     constexpr int TEAMS = kBlock / kQuadTeam;
     __shared__ uint64_t ctr[TEAMS][5];
+    __shared__ QuadOut qout[kBlock / 64];
     const uint32_t lane = threadIdx.x & (kQuadTeam - 1);
     const uint32_t team = threadIdx.x / kQuadTeam;
-    const uint32_t nteams = gridDim.x * TEAMS;
     // the descriptor array holds >= 24 bytes: its first 16-byte-aligned chunk is the
     // dummy target of an empty span's clamped loads
     const void* dummy = reinterpret_cast<const void*>(((uintptr_t)descs + 15u) & ~(uintptr_t)15u);
     QCounters qc;
-    uint32_t i = blockIdx.x * TEAMS + team;
-    cts_buf_desc dn = descs[i < n ? i : n - 1u];  // n >= 1 (launch_verify returns early on 0)
-    while (__any(i < n)) {
+    QuadWalk<CONTIG, TEAMS> w(n, per, team);
+    cts_buf_desc dn = descs[w.i < n ? w.i : n - 1u];  // n >= 1 (launch_verify returns early on 0)
+    while (__any(w.i < w.end)) {
+        const uint32_t i = w.i;
         const cts_buf_desc d = dn;
-        const uint32_t inext = i + nteams > i ? i + nteams : n;  // (wrap guard)
-        dn = descs[inext < n ? inext : n - 1u];                  // clamped: no load under a branch
-        const bool live = i < n;
+        const uint32_t inext = w.next();
+        dn = descs[inext < n ? inext : n - 1u];  // clamped: no load under a branch
+        const bool live = i < w.end;
         const bool ok = live && !desc_bad(d, arena_bytes);
         const QSpan q = quad_span<ALIGN>(arena + d.byte_offset + d.skip_head, ok ? d.length - d.skip_head : 0u,
                                          d.expected_pattern_offset, dummy);
@@ -973,26 +1062,23 @@ __global__ void __launch_bounds__(kBlock)
             quad_team_reduce(first, count);
         }
         if (lane == 0u && live) {
+            QuadOut& o = qout[team >> 2];
             if (!ok) {
-                write_bad(results, i);
+                quad_stage_result(o, team & 3u, 0u, 0u, result_dw2(0u, 0u, 0u, CTS_RESULT_FLAG_BAD_DESC));
             } else {
                 const bool pass = first == kNone;
-                if (results != nullptr) {
-                    cts_verify_result rec;
-                    rec.first_mismatch = pass ? q.len : first;
-                    rec.mismatch_bytes = pass ? 0u : count;
-                    rec.expected = pass ? 0 : (uint8_t)pattern_byte_dev(d.expected_pattern_offset + first);
-                    rec.actual = pass ? 0 : q.sp[first];
-                    rec.pass = pass ? 1 : 0;
-                    rec.flags = 0;
-                    results[i] = rec;
-                }
+                if (results != nullptr)
+                    quad_stage_result(o, team & 3u, pass ? q.len : first, pass ? 0u : count,
+                                      pass ? result_dw2(0u, 0u, 1u, 0u)
+                                           : result_dw2(pattern_byte_dev(d.expected_pattern_offset + first),
+                                                        q.sp[first], 0u, 0u));
                 qc.add(q.len, pass, count);
                 if (!pass && conn_first_fail != nullptr && d.conn_index < n_conns)
                     atomicMin(&conn_first_fail[d.conn_index], i);
             }
         }
-        i = inext;
+        quad_flush_outputs(qout[team >> 2], i, w.end, results, nullptr);
+        w.i = inext;
     }
     qc.flush<TEAMS>(ctr, team, lane, counters);
 }
@@ -1310,37 +1396,83 @@ __device__ __forceinline__ uint8_t load_byte_g(const uint8_t* p)
     return *(const uint8_t __attribute__((address_space(1)))*)p;
 }
 
-template <int U, bool NT, bool ALIGN>
+// Team lane 0 receives dword c of lane `from`'s u32x4 (from = 1, 2) within its 16-lane DPP
+// row (row_shl:from; a VALU move, no LDS round trip).
+template <int FROM>
+__device__ __forceinline__ uint32_t row_shl(uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x100 | FROM, 0xF, 0xF, true);
+}
+
+// Header dwords of the 16-B-chunk form (HDR16): team lanes 0..2 each hold one 16-byte chunk of
+// the 48-byte window starting at the datagram's 16-byte-aligned base; header byte b sits at
+// window byte ho + b. Returns dwords H[0..5] = header bytes 0..23 on team lane 0.
+__device__ __forceinline__ void header_dwords_hdr16(u32x4 own, uint32_t ho, uint32_t (&H)[6])
+{
+    uint32_t W[12];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        W[c] = own[c];
+        W[4 + c] = row_shl<1>(own[c]);
+        W[8 + c] = row_shl<2>(own[c]);
+    }
+    // the 7 dwords starting at ho / 4 (a 4-way select each), then a byte funnel by ho % 4
+    const uint32_t j0 = ho >> 2, s = ho & 3u;
+    uint32_t V[7];
+#pragma unroll
+    for (int m = 0; m < 7; ++m)
+        V[m] = j0 == 0u ? W[m] : (j0 == 1u ? W[m + 1] : (j0 == 2u ? W[m + 2] : W[m + 3]));
+#pragma unroll
+    for (int k = 0; k < 6; ++k) H[k] = __builtin_amdgcn_alignbyte(V[k + 1], V[k], s);
+}
+
+// HDR16 = false: header bytes j and j + 16 by byte loads on every team lane, dwords gathered by
+// lane shuffles (ms_variant 1). HDR16 = true: three 16-byte header chunk loads on team lanes
+// 0..2, gathered on lane 0 by DPP row shifts; the DATA verdict is broadcast (ms_variant 2).
+template <int U, bool NT, bool ALIGN, bool HDR16, bool CONTIG = false>
 __global__ void __launch_bounds__(kBlock)
     media_stream_verify_quad_kernel(const uint8_t* __restrict__ arena, uint64_t arena_bytes,
                                     const cts_buf_desc* __restrict__ descs, uint32_t n,
                                     cts_datagram_record* __restrict__ records, cts_verify_result* __restrict__ results,
-                                    uint64_t* __restrict__ counters)
+                                    uint64_t* __restrict__ counters, uint32_t per = 0)
 {
     constexpr int TEAMS = kBlock / kQuadTeam;
     __shared__ uint64_t ctr[TEAMS][5];
+    __shared__ QuadOut qout[kBlock / 64];
     const uint32_t lane = threadIdx.x & (kQuadTeam - 1);
     const uint32_t team = threadIdx.x / kQuadTeam;
-    const uint32_t nteams = gridDim.x * TEAMS;
     const void* dummy = reinterpret_cast<const void*>(((uintptr_t)descs + 15u) & ~(uintptr_t)15u);
     const uint8_t* dummy8 = reinterpret_cast<const uint8_t*>(dummy);
     QCounters qc;
-    uint32_t i = blockIdx.x * TEAMS + team;
-    cts_buf_desc dn = descs[i < n ? i : n - 1u];
-    while (__any(i < n)) {
+    QuadWalk<CONTIG, TEAMS> w(n, per, team);
+    cts_buf_desc dn = descs[w.i < n ? w.i : n - 1u];
+    while (__any(w.i < w.end)) {
+        const uint32_t i = w.i;
         const cts_buf_desc d = dn;
-        const uint32_t inext = i + nteams > i ? i + nteams : n;
+        const uint32_t inext = w.next();
         dn = descs[inext < n ? inext : n - 1u];
-        const bool live = i < n;
+        const bool live = i < w.end;
         const uint32_t completed = d.length;
         const bool bad = d.byte_offset > arena_bytes || arena_bytes - d.byte_offset < (uint64_t)completed;
         const bool in = live && !bad;
         const uint8_t* dg = arena + d.byte_offset;
-        // header bytes j and j + 16 of this team's datagram (0 past the completed bytes)
-        const bool h0 = in && lane < completed;
-        const bool h1 = in && lane + 16u < CTS_UDP_DATA_HEADER_LENGTH && lane + 16u < completed;
-        uint32_t hb0 = load_byte_g(h0 ? dg + lane : dummy8);
-        uint32_t hb1 = load_byte_g(h1 ? dg + lane + 16u : dummy8);
+        uint32_t hb0 = 0, hb1 = 0;
+        bool h0 = false, h1 = false;
+        u32x4 hch = u32x4{0u, 0u, 0u, 0u};
+        const uint32_t ho = (uint32_t)((uintptr_t)dg & 15u);
+        if constexpr (HDR16) {
+            // header chunks: the 16-byte-aligned chunks holding bytes [0, min(completed, 26)); a
+            // chunk is loaded only if it holds one of those bytes (never past the datagram's page)
+            const uint32_t hbytes = completed < CTS_UDP_DATA_HEADER_LENGTH ? completed : CTS_UDP_DATA_HEADER_LENGTH;
+            if (in && 16u * lane < ho + hbytes)
+                hch = load_chunk_g<NT>(reinterpret_cast<const u32x4*>(dg - ho) + lane);
+        } else {
+            // header bytes j and j + 16 of this team's datagram (0 past the completed bytes)
+            h0 = in && lane < completed;
+            h1 = in && lane + 16u < CTS_UDP_DATA_HEADER_LENGTH && lane + 16u < completed;
+            hb0 = load_byte_g(h0 ? dg + lane : dummy8);
+            hb1 = load_byte_g(h1 ? dg + lane + 16u : dummy8);
+        }
         // speculative DATA payload: [26, completed) at pattern offset 0
         const bool maybe_data = in && completed >= CTS_UDP_DATA_HEADER_LENGTH;
         const QSpan q = quad_span<ALIGN>(dg + CTS_UDP_DATA_HEADER_LENGTH,
@@ -1349,22 +1481,29 @@ __global__ void __launch_bounds__(kBlock)
         const u32x4 edge = load_chunk_g<NT>(q.p + ce);
         uint32_t acc = quad_scan_interior<U, NT>(q, lane);
         acc |= quad_edge_used(q, lane) ? or4(quad_edge_xor(q, ce, edge)) : 0u;
-        // header dwords: lane 4k packs bytes 4k..4k+3 of each half; every lane gathers
-        hb0 = h0 ? hb0 : 0u;
-        hb1 = h1 ? hb1 : 0u;
-        uint32_t w0 = hb0, w1 = hb1;
+        uint32_t H[6];
+        if constexpr (HDR16) {
+            // valid on team lane 0; bytes past the completed length are never read (the flag needs
+            // completed >= 2, the DATA fields completed >= 26)
+            header_dwords_hdr16(hch, ho, H);
+        } else {
+            // header dwords: lane 4k packs bytes 4k..4k+3 of each half; every lane gathers
+            hb0 = h0 ? hb0 : 0u;
+            hb1 = h1 ? hb1 : 0u;
+            uint32_t w0 = hb0, w1 = hb1;
 #pragma unroll
-        for (int b = 1; b < 4; ++b) {
-            w0 |= (uint32_t)__shfl_down((int)hb0, b, kQuadTeam) << (8 * b);
-            w1 |= (uint32_t)__shfl_down((int)hb1, b, kQuadTeam) << (8 * b);
+            for (int b = 1; b < 4; ++b) {
+                w0 |= (uint32_t)__shfl_down((int)hb0, b, kQuadTeam) << (8 * b);
+                w1 |= (uint32_t)__shfl_down((int)hb1, b, kQuadTeam) << (8 * b);
+            }
+            // (every lane needs them: the DATA verdict gates each lane's differences)
+            H[0] = (uint32_t)__shfl((int)w0, 0, kQuadTeam);     // bytes 0..3
+            H[1] = (uint32_t)__shfl((int)w0, 4, kQuadTeam);     // 4..7
+            H[2] = (uint32_t)__shfl((int)w0, 8, kQuadTeam);     // 8..11
+            H[3] = (uint32_t)__shfl((int)w0, 12, kQuadTeam);    // 12..15
+            H[4] = (uint32_t)__shfl((int)w1, 0, kQuadTeam);     // 16..19
+            H[5] = (uint32_t)__shfl((int)w1, 4, kQuadTeam);     // 20..23
         }
-        // (every lane needs them: the DATA verdict gates each lane's differences)
-        const uint32_t H0 = (uint32_t)__shfl((int)w0, 0, kQuadTeam);     // bytes 0..3
-        const uint32_t H1 = (uint32_t)__shfl((int)w0, 4, kQuadTeam);     // 4..7
-        const uint32_t H2 = (uint32_t)__shfl((int)w0, 8, kQuadTeam);     // 8..11
-        const uint32_t H3 = (uint32_t)__shfl((int)w0, 12, kQuadTeam);    // 12..15
-        const uint32_t H4 = (uint32_t)__shfl((int)w1, 0, kQuadTeam);     // 16..19
-        const uint32_t H5 = (uint32_t)__shfl((int)w1, 4, kQuadTeam);     // 20..23
         // header: ctsMediaStreamMessage::ValidateBufferLengthFromTask (ctsMediaStreamProtocol.hpp:284-329)
         uint32_t flag = 0, kind;
         if (bad) {
@@ -1374,7 +1513,7 @@ __global__ void __launch_bounds__(kBlock)
         } else if (completed < CTS_UDP_FLAG_LENGTH) {
             kind = CTS_DGRAM_SHORT;
         } else {
-            flag = H0 & 0xFFFFu;
+            flag = H[0] & 0xFFFFu;
             if (flag == CTS_UDP_FLAG_DATA)
                 kind = completed < CTS_UDP_DATA_HEADER_LENGTH ? CTS_DGRAM_SHORT : CTS_DGRAM_DATA;
             else if (flag == CTS_UDP_FLAG_ID)
@@ -1382,6 +1521,7 @@ __global__ void __launch_bounds__(kBlock)
             else
                 kind = CTS_DGRAM_UNKNOWN;
         }
+        if constexpr (HDR16) kind = (uint32_t)__shfl((int)kind, 0, kQuadTeam);  // lane 0's verdict
         const bool data = kind == CTS_DGRAM_DATA;
         uint32_t first = kNone, count = 0;
         if (__any(acc != 0u && data)) {  // rare: exact re-read (non-DATA teams' differences are discarded)
@@ -1389,42 +1529,35 @@ __global__ void __launch_bounds__(kBlock)
             quad_team_reduce(first, count);
         }
         if (lane == 0u && live) {
+            QuadOut& o = qout[team >> 2];
+            const uint32_t t = team & 3u;
             if (records != nullptr) {
-                cts_datagram_record rec;
-                // GetSequenceNumberFromTask: i64 at byte 2; ctsIOPatternMediaStream.cpp:218-219 read
-                // the sender qpc / qpf at bytes 8 and 16 of the buffer
-                const uint64_t seq = (uint64_t)((H0 >> 16) | (H1 << 16)) | ((uint64_t)((H1 >> 16) | (H2 << 16)) << 32);
-                rec.sequence_number = data ? (int64_t)seq : 0;
-                rec.sender_qpc = data ? (int64_t)((uint64_t)H2 | ((uint64_t)H3 << 32)) : 0;
-                rec.sender_qpf = data ? (int64_t)((uint64_t)H4 | ((uint64_t)H5 << 32)) : 0;
-                rec.flag = (uint16_t)flag;
-                rec.kind = (uint8_t)kind;
-                rec.reserved = 0;
-                rec.completed_bytes = completed;
-                records[i] = rec;
+                // cts_datagram_record as dwords: seq = header bytes 2..9 (GetSequenceNumberFromTask);
+                // ctsIOPatternMediaStream.cpp:218-219 read the sender qpc / qpf at bytes 8 and 16
+                o.rec[t][0] = data ? (H[0] >> 16) | (H[1] << 16) : 0u;
+                o.rec[t][1] = data ? (H[1] >> 16) | (H[2] << 16) : 0u;
+                o.rec[t][2] = data ? H[2] : 0u;
+                o.rec[t][3] = data ? H[3] : 0u;
+                o.rec[t][4] = data ? H[4] : 0u;
+                o.rec[t][5] = data ? H[5] : 0u;
+                o.rec[t][6] = (flag & 0xFFFFu) | (kind << 16);  // flag, kind, reserved = 0
+                o.rec[t][7] = completed;
             }
             if (!data) {
-                if (results != nullptr) {
-                    cts_verify_result r{};
-                    r.flags = kind == CTS_DGRAM_BAD_DESC ? CTS_RESULT_FLAG_BAD_DESC : CTS_RESULT_FLAG_NOT_DATA;
-                    results[i] = r;
-                }
+                quad_stage_result(o, t, 0u, 0u,
+                                  result_dw2(0u, 0u, 0u, kind == CTS_DGRAM_BAD_DESC ? CTS_RESULT_FLAG_BAD_DESC
+                                                                                   : CTS_RESULT_FLAG_NOT_DATA));
             } else {
                 const bool pass = first == kNone;
-                if (results != nullptr) {
-                    cts_verify_result rec;
-                    rec.first_mismatch = pass ? q.len : first;
-                    rec.mismatch_bytes = pass ? 0u : count;
-                    rec.expected = pass ? 0 : (uint8_t)pattern_byte_dev(first);
-                    rec.actual = pass ? 0 : q.sp[first];
-                    rec.pass = pass ? 1 : 0;
-                    rec.flags = 0;
-                    results[i] = rec;
-                }
+                if (results != nullptr)
+                    quad_stage_result(o, t, pass ? q.len : first, pass ? 0u : count,
+                                      pass ? result_dw2(0u, 0u, 1u, 0u)
+                                           : result_dw2(pattern_byte_dev(first), q.sp[first], 0u, 0u));
                 qc.add(q.len, pass, count);
             }
         }
-        i = inext;
+        quad_flush_outputs(qout[team >> 2], i, w.end, results, records);
+        w.i = inext;
     }
     qc.flush<TEAMS>(ctr, team, lane, counters);
 }
@@ -1481,6 +1614,26 @@ static inline uint32_t grid_for(uint32_t n, int teams_per_block, const LaunchGeo
 
 #define CTS_VERIFY_ARGS arena, arena_bytes, descs, n, results, counters, conn_first_fail, n_conns
 
+// Chunked launch of a four-buffers-per-wave kernel (QuadWalk<true>): chunk = geo.small_chunk
+// buffers (rounded up to the block's 16 teams); 0 = one block-contiguous range per block, every
+// block but the last with the same count.
+struct ContigGrid {
+    uint32_t grid, per;
+};
+static inline ContigGrid contig_grid(uint32_t n, const LaunchGeometry& geo)
+{
+    const uint32_t teams = kBlock / kQuadTeam;
+    const uint32_t g = grid_for(n, teams, geo);
+    if (geo.small_chunk > 0) {
+        const uint64_t per = ((uint64_t)geo.small_chunk + teams - 1) / teams * teams;
+        const uint64_t chunks = ((uint64_t)n + per - 1) / per;
+        return ContigGrid{(uint32_t)(chunks < g ? chunks : g), (uint32_t)per};
+    }
+    const uint64_t groups = ((uint64_t)n + teams - 1) / teams;
+    const uint64_t per = (groups + g - 1) / g * teams;
+    return ContigGrid{(uint32_t)(((uint64_t)n + per - 1) / per), (uint32_t)per};
+}
+
 template <bool NT>
 static void launch_verify_nt(const uint8_t* arena, uint64_t arena_bytes, const cts_buf_desc* descs, uint32_t n,
                              bool small, cts_verify_result* results, uint64_t* counters, uint32_t* conn_first_fail,
@@ -1490,7 +1643,7 @@ static void launch_verify_nt(const uint8_t* arena, uint64_t arena_bytes, const c
         // small_variant: 0 = one wave per buffer U2, 1 = U1, 2 = U4 (chunks per lane per round),
         // 3 = pipelined across buffers U2, 4 = pipelined U1,
         // 5 = four buffers per wave (16-lane teams) U6, 6 = same, line-aligned rounds U7,
-        // 7 = line-aligned U6, 8 = U4
+        // 7 = line-aligned U6, 8 = U4, 9 = variant 7 walking block-contiguous buffer ranges
         const uint32_t grid = grid_for(n, kBlock / 64, geo);
         const uint32_t qgrid = grid_for(n, kBlock / kQuadTeam, geo);
         switch (geo.small_variant) {
@@ -1498,6 +1651,11 @@ static void launch_verify_nt(const uint8_t* arena, uint64_t arena_bytes, const c
         case 6: verify_quad_kernel<7, NT, true><<<qgrid, kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 7: verify_quad_kernel<6, NT, true><<<qgrid, kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 8: verify_quad_kernel<4, NT, false><<<qgrid, kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
+        case 9: {
+            const ContigGrid cg = contig_grid(n, geo);
+            verify_quad_kernel<6, NT, true, true><<<cg.grid, kBlock, 0, stream>>>(CTS_VERIFY_ARGS, cg.per);
+            break;
+        }
         case 1: verify_wave_kernel<1, NT><<<grid, kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 2: verify_wave_kernel<4, NT><<<grid, kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 3: verify_wave_pipe_kernel<2, NT><<<grid, kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
@@ -1567,23 +1725,38 @@ hipError_t launch_media_stream_verify(const uint8_t* arena, uint64_t arena_bytes
                                      hipStream_t stream, const LaunchGeometry& geo)
 {
     if (n == 0) return hipSuccess;
-    if (geo.small_variant >= 5) {  // four datagrams per wave (the small-path default)
-        const uint32_t qgrid = grid_for(n, kBlock / kQuadTeam, geo);
-        if (geo.nontemporal)
-            media_stream_verify_quad_kernel<6, true, true><<<qgrid, kBlock, 0, stream>>>(arena, arena_bytes, descs, n,
-                                                                                        records, results, counters);
-        else
-            media_stream_verify_quad_kernel<6, false, true><<<qgrid, kBlock, 0, stream>>>(arena, arena_bytes, descs, n,
-                                                                                         records, results, counters);
-        return hipGetLastError();
-    }
+#define CTS_MS_ARGS arena, arena_bytes, descs, n, records, results, counters
+    // ms_variant: 0 = one wave per datagram, 1 = four datagrams per wave (header by byte loads),
+    // 2 = four per wave, header by three 16-byte chunk loads + DPP, 3 = variant 2 walking
+    // block-contiguous datagram ranges (default)
+    const uint32_t qgrid = grid_for(n, kBlock / kQuadTeam, geo);
     const uint32_t grid = grid_for(n, kBlock / 64, geo);
-    if (geo.nontemporal)
-        media_stream_verify_kernel<2, true><<<grid, kBlock, 0, stream>>>(arena, arena_bytes, descs, n, records, results,
-                                                                         counters);
-    else
-        media_stream_verify_kernel<2, false><<<grid, kBlock, 0, stream>>>(arena, arena_bytes, descs, n, records,
-                                                                          results, counters);
+    const bool nt = geo.nontemporal != 0;
+    switch (geo.ms_variant) {
+    case 0:
+        if (nt) media_stream_verify_kernel<2, true><<<grid, kBlock, 0, stream>>>(CTS_MS_ARGS);
+        else media_stream_verify_kernel<2, false><<<grid, kBlock, 0, stream>>>(CTS_MS_ARGS);
+        break;
+    case 1:
+        if (nt) media_stream_verify_quad_kernel<6, true, true, false><<<qgrid, kBlock, 0, stream>>>(CTS_MS_ARGS);
+        else media_stream_verify_quad_kernel<6, false, true, false><<<qgrid, kBlock, 0, stream>>>(CTS_MS_ARGS);
+        break;
+    case 2:
+        if (nt) media_stream_verify_quad_kernel<6, true, true, true><<<qgrid, kBlock, 0, stream>>>(CTS_MS_ARGS);
+        else media_stream_verify_quad_kernel<6, false, true, true><<<qgrid, kBlock, 0, stream>>>(CTS_MS_ARGS);
+        break;
+    default: {
+        const ContigGrid cg = contig_grid(n, geo);
+        if (nt)
+            media_stream_verify_quad_kernel<6, true, true, true, true><<<cg.grid, kBlock, 0, stream>>>(CTS_MS_ARGS,
+                                                                                                     cg.per);
+        else
+            media_stream_verify_quad_kernel<6, false, true, true, true><<<cg.grid, kBlock, 0, stream>>>(CTS_MS_ARGS,
+                                                                                                      cg.per);
+        break;
+    }
+    }
+#undef CTS_MS_ARGS
     return hipGetLastError();
 }
 

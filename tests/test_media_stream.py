@@ -192,17 +192,29 @@ def _to_dev(a, torch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("small_variant", [0, 7])
-def test_gpu_media_stream_verify_matches_oracle(engine, small_variant):
-    """small_variant 0: one wave per datagram; 7 (default): four datagrams per wave."""
+@pytest.mark.parametrize("ms_variant", [0, 1, 2, 3])
+def test_gpu_media_stream_verify_matches_oracle(engine, ms_variant):
+    """ms_variant 0: one wave per datagram; 1: four datagrams per wave, header by byte loads;
+    2: four per wave, header by 16-byte chunk loads gathered with DPP row shifts; 3: variant 2
+    walking block-contiguous datagram ranges (the default)."""
     from ctstraffic_amd import _lib
 
-    default_sv = engine.get_attr(_lib.ATTR_SMALL_VARIANT)
-    engine.set_attr(_lib.ATTR_SMALL_VARIANT, small_variant)
+    default = engine.get_attr(_lib.ATTR_MS_VARIANT)
+    default_sbpc = engine.get_attr(_lib.ATTR_SMALL_BLOCKS_PER_CU)
+    default_chunk = engine.get_attr(_lib.ATTR_SMALL_CHUNK)
+    engine.set_attr(_lib.ATTR_MS_VARIANT, ms_variant)
     try:
-        _media_stream_verify_vs_oracle(engine)
+        # sbpc 1: several rounds per workgroup (5 000+ datagrams over 256 workgroups); chunked walks
+        for sbpc, chunk in ((1, 0), (64, 0), (1, 16), (2, 48)):
+            if chunk and ms_variant != 3:
+                continue
+            engine.set_attr(_lib.ATTR_SMALL_BLOCKS_PER_CU, sbpc)
+            engine.set_attr(_lib.ATTR_SMALL_CHUNK, chunk)
+            _media_stream_verify_vs_oracle(engine)
     finally:
-        engine.set_attr(_lib.ATTR_SMALL_VARIANT, default_sv)
+        engine.set_attr(_lib.ATTR_MS_VARIANT, default)
+        engine.set_attr(_lib.ATTR_SMALL_BLOCKS_PER_CU, default_sbpc)
+        engine.set_attr(_lib.ATTR_SMALL_CHUNK, default_chunk)
 
 
 def _media_stream_verify_vs_oracle(engine):
@@ -211,7 +223,7 @@ def _media_stream_verify_vs_oracle(engine):
     rng = np.random.default_rng(11)
     dgs = _crafted()
     S = oracle.sender_buffer(9000)
-    for _ in range(3000):  # random valid/corrupt data datagrams of random sizes
+    for _ in range(5000):  # random valid/corrupt data datagrams of random sizes
         ln = int(rng.integers(26, 9000))
         d = bytearray(np.array([0], "<u2").tobytes() + np.array([rng.integers(-9, 1 << 40), rng.integers(0, 1 << 62),
                                                                  rng.integers(0, 1 << 62)], "<i8").tobytes())

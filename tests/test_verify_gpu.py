@@ -349,28 +349,33 @@ def test_launch_variants_parity(engine, variant, nt):
 
 
 # ---- every small-buffer (datagram) kernel is bit-identical --------------------------------------
-@pytest.mark.parametrize("small_variant", list(range(9)))
+@pytest.mark.parametrize("small_variant", list(range(10)))
 def test_small_variants_parity(engine, small_variant):
     """Small-buffer path (max_length_hint <= 8192): one wave per buffer (0-4) and four
-    buffers per wave in 16-lane teams (5-8), vs the oracle. Includes spans longer than the
+    buffers per wave in 16-lane teams (5-8; 9 walking block-contiguous ranges), vs the oracle. Includes spans longer than the
     hint (multi-round teams), empty spans, all start alignments, bad descriptors, a batch
     whose size is not a multiple of the team count, and config-3 datagrams."""
     from ctstraffic_amd import _lib
 
     default_sv = engine.get_attr(_lib.ATTR_SMALL_VARIANT)
     default_sbpc = engine.get_attr(_lib.ATTR_SMALL_BLOCKS_PER_CU)
+    default_chunk = engine.get_attr(_lib.ATTR_SMALL_CHUNK)
     try:
         engine.set_attr(_lib.ATTR_SMALL_VARIANT, small_variant)
         for seed, n, max_len, hint, skip in [(31, 301, 1500, 1472, True), (32, 257, 200, 64, False),
                                              (33, 120, 20000, 1472, True), (34, 1000, 3000, 8192, False),
                                              (35, 7, 40, 40, True)]:
-            for sbpc in (1, 64):
+            for sbpc, chunk in ((1, 0), (64, 0), (1, 16), (2, 48)):
+                if chunk and small_variant != 9:  # (only variant 9 walks chunks)
+                    continue
                 engine.set_attr(_lib.ATTR_SMALL_BLOCKS_PER_CU, sbpc)
+                engine.set_attr(_lib.ATTR_SMALL_CHUNK, chunk)
                 rng = np.random.default_rng(seed)
                 arena, descs = _random_case(rng, n, max_len, skip=skip)
                 r, ctr, cff = run_verify(engine, arena, descs, hint, n_conns=7)
                 er, ectr, ecff = oracle.verify_batch(arena, descs, n_conns=7)
-                assert_results_equal(r, er, "small variant %d seed %d sbpc %d" % (small_variant, seed, sbpc))
+                assert_results_equal(r, er, "small variant %d seed %d sbpc %d chunk %d" % (small_variant, seed, sbpc,
+                                                                                           chunk))
                 assert ctr == ectr
                 assert np.array_equal(cff, ecff)
         arena = np.zeros(256, np.uint8)
@@ -390,3 +395,4 @@ def test_small_variants_parity(engine, small_variant):
     finally:
         engine.set_attr(_lib.ATTR_SMALL_VARIANT, default_sv)
         engine.set_attr(_lib.ATTR_SMALL_BLOCKS_PER_CU, default_sbpc)
+        engine.set_attr(_lib.ATTR_SMALL_CHUNK, default_chunk)

@@ -1,0 +1,80 @@
+#!/usr/bin/env python3
+"""Where does MediaStream receive time go? Interleaved A/B in one process over config-3-shaped
+datagrams (4 M x 1472 B by default): plain datagram verify with/without per-datagram results,
+and cts_media_stream_verify with/without records and results, for each small-path variant
+given. Prints one JSON line per (case, round).
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from ctstraffic_amd import Engine, _lib, media_stream as MS, workload as W  # noqa: E402
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--datagrams", type=int, default=4 * 1024 * 1024)
+    p.add_argument("--launches", type=int, default=20)
+    p.add_argument("--rounds", type=int, default=3)
+    p.add_argument("--ms-variants", default="", help="comma list of ATTR_MS_VARIANT values to A/B")
+    p.add_argument("--small-variants", default="", help="comma list of ATTR_SMALL_VARIANT values to A/B")
+    p.add_argument("--chunks", default="", help="comma list of ATTR_SMALL_CHUNK values (chunked walks)")
+    p.add_argument("--arenas", type=int, default=4)
+    p.add_argument("--only", default="", help="comma list of case names to run (default: all)")
+    args = p.parse_args()
+    torch.cuda.set_device(0)
+    eng = Engine(0)
+    w = W.udp_datagrams(n_datagrams=args.datagrams)
+    arenas = []
+    for _ in range(args.arenas):
+        a, d = W.materialize(eng, w)
+        arenas.append(a)
+    recs = torch.empty(w.n * 32, dtype=torch.uint8, device="cuda")
+    res = eng.new_results(w.n)
+    ctr = eng.new_counters()
+    s = torch.cuda.current_stream()
+    msv = [int(x) for x in args.ms_variants.split(",") if x] or [None]
+    svs = [int(x) for x in args.small_variants.split(",") if x] or [None]
+    chunks = [int(x) for x in args.chunks.split(",") if x] or [None]
+    only = set(x for x in args.only.split(",") if x)
+    cases = []
+    for ch in chunks:
+        for sv in svs:
+            cases += [("verify", ("small", sv, ch),
+                       lambda a: eng.verify(a, d, max_length_hint=w.max_length, counters=ctr)),
+                      ("verify+results", ("small", sv, ch),
+                       lambda a: eng.verify(a, d, max_length_hint=w.max_length, counters=ctr, results=res))]
+        for v in msv:
+            cases += [("ms", ("ms", v, ch), lambda a: MS.verify(eng, a, d)),
+                      ("ms+results", ("ms", v, ch), lambda a: MS.verify(eng, a, d, results=res)),
+                      ("ms+records", ("ms", v, ch), lambda a: MS.verify(eng, a, d, records=recs)),
+                      ("ms+records+results", ("ms", v, ch),
+                       lambda a: MS.verify(eng, a, d, records=recs, results=res))]
+    cases = [c for c in cases if not only or c[0] in only]
+    for r in range(args.rounds):
+        for name, v, fn in cases:
+            kind, var, ch = v
+            if var is not None:
+                eng.set_attr(_lib.ATTR_SMALL_VARIANT if kind == "small" else _lib.ATTR_MS_VARIANT, var)
+            if ch is not None:
+                eng.set_attr(_lib.ATTR_SMALL_CHUNK, ch)
+            fn(arenas[0])
+            ea, eb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ea.record(s)
+            for i in range(args.launches):
+                fn(arenas[(i + 1) % len(arenas)])
+            eb.record(s)
+            torch.cuda.synchronize()
+            us = ea.elapsed_time(eb) * 1e3 / args.launches
+            print(json.dumps({"round": r, "case": name, "variant": v, "us": round(us, 1),
+                              "GBps_payload": round(w.verified_bytes() / us / 1e3, 1),
+                              "Mdgram_per_s": round(w.n / us, 1)}), flush=True)
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()
