@@ -339,8 +339,12 @@ def run_extras(engine, torch, W, w, arenas, descs, dev, want):
             from ctstraffic_amd import _pattern_abi as PA
             from ctstraffic_amd import loopback as LB
 
-            for name, mode in (("deferred", PA.VERIFY_DEFERRED), ("sync", PA.VERIFY_SYNC)):
-                r = LB.run(connections=8, buffer_size=65536, transfer_size=1 << 30, engine=engine, verify_mode=mode)
+            for name, mode, pat in (("deferred", PA.VERIFY_DEFERRED, PA.PATTERN_PUSH),
+                                    ("sync", PA.VERIFY_SYNC, PA.PATTERN_PUSH),
+                                    ("duplex_deferred", PA.VERIFY_DEFERRED, PA.PATTERN_DUPLEX)):
+                # (duplex: each side sends and receives half of the 1 GiB at once, both directions verified)
+                r = LB.run(connections=8, buffer_size=65536, transfer_size=1 << 30, engine=engine, verify_mode=mode,
+                           io_pattern=pat)
                 out["loopback_config1_%s" % name] = {
                     "GBps_recv": round(r["GBps_recv"], 3), "seconds": round(r["seconds"], 3),
                     "connections_ok": r["connections_ok"], "data_errors": r["data_errors"],

@@ -1,10 +1,15 @@
 // cts_loopback.cpp — loopback-TCP feeder (include/cts_loopback.h): blocking
-// POSIX sockets, one thread per connection side, each driving a cts_io_pattern
-// exactly as the reference's IOCP functor drives ctsIoPattern:
-// InitiateIo -> post the IO -> CompleteIo(task, transferred, status)
-// (ctsTraffic/ctsSendRecvIocp.cpp:130-300, 335-415). One IO is in flight per
-// side (PrePostRecvs = PrePostSends = 1, what -Verify:data requires for TCP,
-// ctsConfig.cpp:3440-3446), so blocking calls preserve the reference's ordering.
+// POSIX sockets driving a cts_io_pattern exactly as the reference's IOCP functor
+// drives ctsIoPattern: InitiateIo -> post the IO -> CompleteIo(task, transferred,
+// status) (ctsTraffic/ctsSendRecvIocp.cpp:130-300, 335-415).
+//   sync functor  (run_side): one thread per connection side, one IO at a time
+//                 (PrePostRecvs = PrePostSends = 1, what -Verify:data requires for
+//                 TCP, ctsConfig.cpp:3440-3446) — Push, Pull, PushPull.
+//   async functor (AsyncSide): a send thread and a recv thread per side, so a send
+//                 and a recv are in flight together (Duplex). Completions run under
+//                 the connection's lock and re-pump InitiateIo until it returns
+//                 None, as ctsSendRecvCompletionCallback / ctsSendRecvIocp do
+//                 (:47-127, :335-415); the side is done when its IO count drops to 0.
 #include <arpa/inet.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
@@ -14,7 +19,10 @@
 #include <atomic>
 #include <cerrno>
 #include <chrono>
+#include <condition_variable>
 #include <cstring>
+#include <deque>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -137,15 +145,153 @@ void run_side(int* fdslot, cts_io_pattern* p, bool inject, uint32_t inject_index
     (void)cts_io_pattern_get_stats(p, &out->stats);
 }
 
+// ---- async functor (Duplex): one send and one recv thread per connection side -----------------
+struct AsyncSide {
+    int fd;
+    cts_io_pattern* p;
+    bool inject;
+    uint32_t inject_index;
+    uint32_t data_sends = 0;
+    std::mutex mu;  // the ctsSocket lock: every pattern call runs under it (ctsSocket.h:189)
+    std::condition_variable cv;
+    std::deque<cts_task> sends, recvs;
+    uint32_t io = 0;       // posted IOs + the pump's own hold (sharedSocket->IncrementIo)
+    bool finished = false; // io dropped to 0 (CompleteState)
+    bool aborted = false;  // the pattern failed: queued IO completes as aborted, blocked IO is unblocked
+    int status = CTS_IO_CONTINUE;
+
+    void fail_socket()
+    {
+        aborted = true;
+        (void)::shutdown(fd, SHUT_RDWR);  // wakes a send/recv blocked in the other thread
+    }
+    void on_status(int st)
+    {
+        if (st == CTS_IO_FAILED) {
+            status = CTS_IO_FAILED;
+            fail_socket();
+        } else if (st == CTS_IO_COMPLETED && status != CTS_IO_FAILED) {
+            status = CTS_IO_COMPLETED;
+        }
+    }
+    void release()  // DecrementIo; at 0 the side is done
+    {
+        if (--io == 0) {
+            finished = true;
+            cv.notify_all();
+        }
+    }
+    // ctsSendRecvIocp (:335-415): post IO until InitiateIo returns None. Shutdown tasks run inline.
+    void pump()
+    {
+        ++io;
+        while (!aborted) {
+            cts_task t{};
+            if (cts_io_pattern_initiate_io(p, &t) != CTS_OK) {
+                on_status(CTS_IO_FAILED);
+                break;
+            }
+            if (t.io_action == CTS_TASK_NONE) break;
+            if (t.io_action == CTS_TASK_SEND || t.io_action == CTS_TASK_RECV) {
+                (t.io_action == CTS_TASK_SEND ? sends : recvs).push_back(t);
+                ++io;
+                cv.notify_all();
+                continue;
+            }
+            uint32_t err = 0;
+            if (t.io_action == CTS_TASK_GRACEFUL_SHUTDOWN) {
+                if (::shutdown(fd, SHUT_WR) != 0) err = wsa_status(errno);
+            } else if (t.io_action == CTS_TASK_HARD_SHUTDOWN) {
+                linger l{1, 0};  // RST on close
+                (void)::setsockopt(fd, SOL_SOCKET, SO_LINGER, &l, sizeof(l));
+            }
+            const int st = cts_io_pattern_complete_io(p, &t, 0, err);
+            on_status(st);
+            if (st != CTS_IO_CONTINUE) break;
+        }
+        release();
+    }
+    void worker(bool sending)
+    {
+        std::deque<cts_task>& q = sending ? sends : recvs;
+        std::vector<char> scratch;
+        std::unique_lock<std::mutex> lk(mu);
+        for (;;) {
+            cv.wait(lk, [&] { return finished || !q.empty(); });
+            if (q.empty()) return;  // finished
+            cts_task t = q.front();
+            q.pop_front();
+            uint32_t transferred = 0, err = 0;
+            if (aborted) {
+                err = 10053;  // WSAECONNABORTED: the socket was closed under this IO
+            } else {
+                const bool inj = sending && inject && t.track_io && data_sends++ == inject_index && t.buffer_length > 0;
+                lk.unlock();
+                if (sending) {
+                    const char* src = t.buffer + t.buffer_offset;
+                    if (inj) {  // fault injection: one flipped byte on the wire
+                        scratch.assign(src, src + t.buffer_length);
+                        scratch[t.buffer_length / 2] ^= 0x5A;
+                        src = scratch.data();
+                    }
+                    err = send_all(fd, src, t.buffer_length);
+                    transferred = err == 0 ? t.buffer_length : 0;
+                } else {
+                    const bool whole = t.buffer_type == CTS_BUFFER_TCP_CONNECTION_ID ||
+                                       t.buffer_type == CTS_BUFFER_COMPLETION_MESSAGE;
+                    err = recv_some(fd, t.buffer + t.buffer_offset, t.buffer_length, &transferred, whole);
+                }
+                lk.lock();
+            }
+            // ctsSendRecvCompletionCallback (:47-127): CompleteIo, then more IO if it asks for it
+            const int st = cts_io_pattern_complete_io(p, &t, transferred, err);
+            on_status(st);
+            if (st == CTS_IO_CONTINUE) pump();
+            release();
+        }
+    }
+};
+
+void run_side_async(int* fdslot, cts_io_pattern* p, bool inject, uint32_t inject_index, SideResult* out)
+{
+    AsyncSide a;
+    a.fd = *fdslot;
+    a.p = p;
+    a.inject = inject;
+    a.inject_index = inject_index;
+    {
+        std::lock_guard<std::mutex> lk(a.mu);
+        a.pump();
+    }
+    std::thread ts([&] { a.worker(true); });
+    a.worker(false);
+    ts.join();
+    int st = a.status;
+    if (st == CTS_IO_CONTINUE) st = cts_io_pattern_flush(p);  // nothing left to post: settle the pattern
+    if (st != CTS_IO_COMPLETED) {
+        linger l{1, 0};
+        (void)::setsockopt(a.fd, SOL_SOCKET, SO_LINGER, &l, sizeof(l));
+    }
+    ::close(a.fd);
+    *fdslot = -1;
+    out->status = st;
+    out->last_error = cts_io_pattern_last_error(p);
+    (void)cts_io_pattern_get_stats(p, &out->stats);
+}
+
 }  // namespace
 
 extern "C" int cts_loopback_run(const cts_loopback_config* cfg, cts_engine* engine, cts_batch_verifier hook,
                                 void* hook_ctx, cts_loopback_result* out)
 {
     if (cfg == nullptr || out == nullptr || cfg->connections == 0 || cfg->buffer_size == 0) return CTS_E_INVALID;
-    // one blocking IO per side: Duplex (concurrent send + recv on one socket) needs an async functor
-    if (cfg->io_pattern != 0 && cfg->io_pattern != CTS_PATTERN_PUSH && cfg->io_pattern != CTS_PATTERN_PULL)
+    const uint32_t pattern = cfg->io_pattern ? cfg->io_pattern : CTS_PATTERN_PUSH;
+    if (pattern < CTS_PATTERN_PUSH || pattern > CTS_PATTERN_DUPLEX || cfg->functor > CTS_LOOPBACK_FUNCTOR_ASYNC)
         return CTS_E_INVALID;
+    // one blocking IO per side cannot run Duplex (a send and a recv in flight together)
+    const bool async = cfg->functor == CTS_LOOPBACK_FUNCTOR_ASYNC ||
+                       (cfg->functor == CTS_LOOPBACK_FUNCTOR_AUTO && pattern == CTS_PATTERN_DUPLEX);
+    if (pattern == CTS_PATTERN_DUPLEX && !async) return CTS_E_INVALID;
     if (engine == nullptr && hook == nullptr && cfg->verify_buffers) return CTS_E_INVALID;
     *out = cts_loopback_result{};
     if (engine != nullptr) {
@@ -169,7 +315,9 @@ extern "C" int cts_loopback_run(const cts_loopback_config* cfg, cts_engine* engi
     const uint32_t n = cfg->connections;
     auto make_cfg = [&](bool listening) {
         cts_pattern_config c{};
-        c.io_pattern = cfg->io_pattern ? cfg->io_pattern : CTS_PATTERN_PUSH;
+        c.io_pattern = pattern;
+        c.push_bytes = cfg->push_bytes ? cfg->push_bytes : cfg->buffer_size;  // PushPull segments
+        c.pull_bytes = cfg->pull_bytes ? cfg->pull_bytes : cfg->buffer_size;
         c.protocol = CTS_PROTOCOL_TCP;
         c.listening = listening ? 1u : 0u;
         c.verify_buffers = cfg->verify_buffers;
@@ -230,7 +378,8 @@ extern "C" int cts_loopback_run(const cts_loopback_config* cfg, cts_engine* engi
     for (uint32_t i = 0; i < 2 * n; ++i) {
         if (fds[i] < 0) continue;
         const bool inject = i < n && i == cfg->corrupt_connection;
-        threads.emplace_back(run_side, &fds[i], pats[i], inject, cfg->corrupt_send_index, &res[i]);
+        threads.emplace_back(async ? run_side_async : run_side, &fds[i], pats[i], inject, cfg->corrupt_send_index,
+                             &res[i]);
     }
     const std::vector<bool>& connected = connected0;
     for (auto& t : threads) t.join();

@@ -15,7 +15,11 @@ class LoopbackConfig(ctypes.Structure):
                 ("verify_buffers", ctypes.c_uint32), ("transfer_size", ctypes.c_uint64),
                 ("verify_mode", ctypes.c_uint32), ("batch_buffers", ctypes.c_uint32),
                 ("corrupt_connection", ctypes.c_uint32), ("corrupt_send_index", ctypes.c_uint32),
-                ("socket_buffer_bytes", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+                ("socket_buffer_bytes", ctypes.c_uint32), ("push_bytes", ctypes.c_uint32),
+                ("pull_bytes", ctypes.c_uint32), ("functor", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+
+
+FUNCTOR_AUTO, FUNCTOR_SYNC, FUNCTOR_ASYNC = 0, 1, 2
 
 
 class LoopbackResult(ctypes.Structure):
@@ -39,14 +43,15 @@ def declare(L: ctypes.CDLL) -> None:
 
 def run(connections=8, buffer_size=65536, transfer_size=1 << 30, engine=None, verifier=None,
         io_pattern=A.PATTERN_PUSH, verify=True, verify_mode=A.VERIFY_DEFERRED, batch_buffers=0,
-        corrupt_connection=None, corrupt_send_index=0, socket_buffer_bytes=0) -> dict:
+        corrupt_connection=None, corrupt_send_index=0, socket_buffer_bytes=0, push_bytes=0, pull_bytes=0,
+        functor=FUNCTOR_AUTO) -> dict:
     """One loopback run. ``verifier`` (a cts_batch_verifier or a python fn(arena, descs) -> results) replaces the
     engine's kernel (test harnesses / the CPU baseline)."""
     from .pattern import batch_verifier
 
     cfg = LoopbackConfig(connections, io_pattern, buffer_size, int(verify), transfer_size, verify_mode, batch_buffers,
                          0xFFFFFFFF if corrupt_connection is None else corrupt_connection, corrupt_send_index,
-                         socket_buffer_bytes, 0)
+                         socket_buffer_bytes, push_bytes, pull_bytes, functor, 0)
     hook = None
     if verifier is not None:
         hook = verifier if isinstance(verifier, A.BATCH_VERIFIER) else batch_verifier(verifier)

@@ -2,10 +2,12 @@
  * cts_loopback.h — a Linux loopback-TCP feeder for the data-integrity path
  * (SURVEY.md §8f-3): the role of the reference's IOCP IO functor
  * (ctsTraffic/ctsSendRecvIocp.cpp:335-415, ctsSendRecvProcessTask :130-300)
- * played with blocking POSIX sockets, one thread per connection side, over the
- * ctsIoPattern mirror of cts_pattern.h. Clients send g_senderSharedBuffer
- * (written by the gfx950 fill kernel) and servers verify every received buffer
- * on the GPU, so a run is the reference's config 1 end to end
+ * played with blocking POSIX sockets over the ctsIoPattern mirror of
+ * cts_pattern.h: one thread per connection side (Push, Pull, PushPull), or a
+ * send and a recv thread per side (Duplex; see cts_loopback_functor). Senders
+ * send g_senderSharedBuffer (written by the gfx950 fill kernel) and receivers
+ * verify every received buffer on the GPU, so a push run is the reference's
+ * config 1 end to end
  * ("-Pattern:push -Connections:8 -Buffer:65536 -Transfer:1GiB -Verify:data"
  * over loopback), host memory and the kernel stack included.
  */
@@ -23,7 +25,7 @@ extern "C" {
 
 typedef struct cts_loopback_config {
     uint32_t connections;           /* -Connections (client/server pairs) */
-    uint32_t io_pattern;            /* CTS_PATTERN_PUSH / PULL (one blocking IO per side: no Duplex) */
+    uint32_t io_pattern;            /* cts_io_pattern_type (0 = Push) */
     uint32_t buffer_size;           /* -Buffer */
     uint32_t verify_buffers;        /* -Verify:data */
     uint64_t transfer_size;         /* -Transfer, per connection */
@@ -32,8 +34,18 @@ typedef struct cts_loopback_config {
     uint32_t corrupt_connection;    /* fault injection: connection index whose sender flips a byte, or ~0u */
     uint32_t corrupt_send_index;    /* ... in its n-th data send (0-based) */
     uint32_t socket_buffer_bytes;   /* SO_SNDBUF / SO_RCVBUF (0 = system default) */
+    uint32_t push_bytes;            /* -PushBytes (PushPull; 0 = buffer_size) */
+    uint32_t pull_bytes;            /* -PullBytes (PushPull; 0 = buffer_size) */
+    uint32_t functor;               /* cts_loopback_functor */
     uint32_t reserved;
 } cts_loopback_config;
+
+typedef enum cts_loopback_functor {
+    CTS_LOOPBACK_FUNCTOR_AUTO = 0,  /* async for Duplex, sync otherwise */
+    CTS_LOOPBACK_FUNCTOR_SYNC = 1,  /* one thread per side, one blocking IO at a time (Push, Pull, PushPull) */
+    CTS_LOOPBACK_FUNCTOR_ASYNC = 2  /* a send and a recv thread per side; completions re-pump InitiateIo
+                                       under the connection lock (ctsSendRecvIocp.cpp:47-127, 335-415) */
+} cts_loopback_functor;
 
 typedef struct cts_loopback_result {
     double seconds;                 /* wall time from the first connect to the last completed connection */

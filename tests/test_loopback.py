@@ -62,3 +62,63 @@ def test_loopback_with_c_oracle_hook():
     r = loopback.run(connections=2, buffer_size=65536, transfer_size=8 * 1024 * 1024, verifier=hook,
                      verify_mode=A.VERIFY_SYNC, corrupt_connection=0, corrupt_send_index=3)
     assert r["data_errors"] == 1
+
+
+# ---- PushPull (sync functor) and Duplex (async functor: a send and a recv in flight per side) -----------------
+@pytest.mark.parametrize("mode", [A.VERIFY_SYNC, A.VERIFY_DEFERRED], ids=["sync", "deferred"])
+def test_loopback_pushpull_cpu(mode):
+    """-Pattern:pushpull: the client pushes PushBytes, then pulls PullBytes, alternating (ctsIOPattern.cpp:888-966);
+    both directions are verified, and segment ends shift the receive phase (odd sizes)."""
+    shared_buffer_attach(_SENDER)
+    total = 5 * 1024 * 1024 + 333
+    r = loopback.run(connections=3, buffer_size=65536, transfer_size=total, verifier=_oracle_verifier,
+                     io_pattern=A.PATTERN_PUSHPULL, verify_mode=mode, batch_buffers=8, push_bytes=100003,
+                     pull_bytes=65537)
+    assert r["connections_ok"] == 3 and r["data_errors"] == 0
+    assert r["bytes_recv"] == 3 * (total + 37 + 4)
+    r = loopback.run(connections=2, buffer_size=65536, transfer_size=total, verifier=_oracle_verifier,
+                     io_pattern=A.PATTERN_PUSHPULL, verify_mode=mode, batch_buffers=8, push_bytes=100003,
+                     pull_bytes=65537, corrupt_connection=1, corrupt_send_index=9)
+    assert r["data_errors"] == 1 and r["connections_ok"] == 1
+
+
+@pytest.mark.parametrize("mode", [A.VERIFY_SYNC, A.VERIFY_DEFERRED], ids=["sync", "deferred"])
+def test_loopback_duplex_cpu(mode):
+    """-Pattern:duplex: each side sends and receives half the transfer at once (ctsIOPattern.cpp:968-1031), which
+    only the async functor can run; both receive directions are verified."""
+    shared_buffer_attach(_SENDER)
+    total = 6 * 1024 * 1024 + 10
+    r = loopback.run(connections=4, buffer_size=65536, transfer_size=total, verifier=_oracle_verifier,
+                     io_pattern=A.PATTERN_DUPLEX, verify_mode=mode, batch_buffers=8)
+    assert r["connections_ok"] == 4 and r["connections_failed"] == 0 and r["data_errors"] == 0
+    assert r["bytes_recv"] == 4 * (total + 37 + 4)
+    assert r["bytes_sent"] == r["bytes_recv"]
+    # a flipped byte in either direction fails that connection only
+    r = loopback.run(connections=3, buffer_size=65536, transfer_size=total, verifier=_oracle_verifier,
+                     io_pattern=A.PATTERN_DUPLEX, verify_mode=mode, batch_buffers=8, corrupt_connection=1,
+                     corrupt_send_index=21)
+    assert r["data_errors"] == 1 and r["connections_failed"] == 1 and r["connections_ok"] == 2
+
+
+def test_loopback_functor_choice():
+    """The async functor runs the one-IO-at-a-time patterns too; Duplex refuses the sync functor."""
+    from ctstraffic_amd._lib import CtsError
+
+    shared_buffer_attach(_SENDER)
+    r = loopback.run(connections=2, buffer_size=32768, transfer_size=3 * 1024 * 1024, verifier=_oracle_verifier,
+                     io_pattern=A.PATTERN_PULL, verify_mode=A.VERIFY_SYNC, functor=loopback.FUNCTOR_ASYNC)
+    assert r["connections_ok"] == 2 and r["data_errors"] == 0
+    with pytest.raises(CtsError):
+        loopback.run(connections=1, buffer_size=65536, transfer_size=1 << 20, verifier=_oracle_verifier,
+                     io_pattern=A.PATTERN_DUPLEX, functor=loopback.FUNCTOR_SYNC)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [A.VERIFY_SYNC, A.VERIFY_DEFERRED], ids=["sync", "deferred"])
+def test_loopback_duplex_gpu(engine, mode):
+    r = loopback.run(connections=4, buffer_size=65536, transfer_size=16 * 1024 * 1024 + 6, engine=engine,
+                     io_pattern=A.PATTERN_DUPLEX, verify_mode=mode)
+    assert r["connections_ok"] == 4 and r["data_errors"] == 0
+    r = loopback.run(connections=4, buffer_size=65536, transfer_size=8 * 1024 * 1024, engine=engine,
+                     io_pattern=A.PATTERN_DUPLEX, verify_mode=mode, corrupt_connection=3, corrupt_send_index=30)
+    assert r["data_errors"] == 1 and r["connections_ok"] == 3
