@@ -377,7 +377,7 @@ extern "C" int cts_loopback_run(const cts_loopback_config* cfg, cts_engine* engi
     for (uint32_t i = 0; i < 2 * n; ++i) connected0[i] = fds[i] >= 0;
     for (uint32_t i = 0; i < 2 * n; ++i) {
         if (fds[i] < 0) continue;
-        const bool inject = i < n && i == cfg->corrupt_connection;
+        const bool inject = i % n == cfg->corrupt_connection;  // whichever side(s) send data
         threads.emplace_back(async ? run_side_async : run_side, &fds[i], pats[i], inject, cfg->corrupt_send_index,
                              &res[i]);
     }

@@ -31,8 +31,8 @@ typedef struct cts_loopback_config {
     uint64_t transfer_size;         /* -Transfer, per connection */
     uint32_t verify_mode;           /* CTS_VERIFY_SYNC / CTS_VERIFY_DEFERRED */
     uint32_t batch_buffers;         /* DEFERRED batch (0 = default) */
-    uint32_t corrupt_connection;    /* fault injection: connection index whose sender flips a byte, or ~0u */
-    uint32_t corrupt_send_index;    /* ... in its n-th data send (0-based) */
+    uint32_t corrupt_connection;    /* fault injection: connection whose data senders flip a byte, or ~0u */
+    uint32_t corrupt_send_index;    /* ... in their n-th data send (0-based; each side counts its own) */
     uint32_t socket_buffer_bytes;   /* SO_SNDBUF / SO_RCVBUF (0 = system default) */
     uint32_t push_bytes;            /* -PushBytes (PushPull; 0 = buffer_size) */
     uint32_t pull_bytes;            /* -PullBytes (PushPull; 0 = buffer_size) */

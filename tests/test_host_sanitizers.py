@@ -1,0 +1,56 @@
+"""Host C++ under sanitizers (the reference has none; "ASan/UBSan on host code").
+
+The host half of the engine — the ctsIoPattern mirror (cts_pattern.cpp), MediaStream framing and
+client accounting (cts_media_stream.cpp), status output (cts_status.cpp) and the loopback feeder
+with its sync and async functors (cts_loopback.cpp) — is built from source with g++ against
+link-time fakes of the device entry points (tests/cpp/engine_stub.cpp), with the oracle's C
+verifier as every pattern's hook. Two builds run the MSTest replay (tests/cpp/pattern_replay.cpp)
+and whole loopback connections of every TCP pattern (tests/cpp/loopback_stress.cpp):
+AddressSanitizer + UndefinedBehaviorSanitizer, and ThreadSanitizer (the async functor's send and
+recv threads share one pattern under the connection lock). Any report fails the test.
+"""
+import os
+import subprocess
+import tempfile
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HOST_SRCS = ["cts_pattern.cpp", "cts_media_stream.cpp", "cts_status.cpp", "cts_loopback.cpp"]
+SAN = {
+    "asan-ubsan": ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"],
+    "tsan": ["-fsanitize=thread"],
+}
+ENV = {"ASAN_OPTIONS": "detect_leaks=1:abort_on_error=0:exitcode=23",
+       "UBSAN_OPTIONS": "halt_on_error=1:print_stacktrace=1:exitcode=24",
+       "TSAN_OPTIONS": "halt_on_error=1:exitcode=25"}
+
+
+def _build(d, san, driver):
+    flags = ["-g", "-O1", "-fno-omit-frame-pointer", "-pthread"] + SAN[san]
+    inc = ["-I", os.path.join(ROOT, "include"), "-I", os.path.join(ROOT, "ctstraffic_amd", "csrc"),
+           "-I", "/opt/rocm/include", "-D__HIP_PLATFORM_AMD__"]
+    objs = []
+    for src in [os.path.join(ROOT, "ctstraffic_amd", "csrc", s) for s in HOST_SRCS] + [
+            os.path.join(ROOT, "tests", "cpp", "engine_stub.cpp"), os.path.join(ROOT, "tests", "cpp", driver)]:
+        o = os.path.join(d, os.path.basename(src) + ".o")
+        subprocess.run(["g++", "-std=c++17", *flags, *inc, "-c", src, "-o", o], check=True)
+        objs.append(o)
+    o = os.path.join(d, "cts_oracle.o")
+    subprocess.run(["gcc", "-std=c11", *flags, "-I", os.path.join(ROOT, "oracle"), "-c",
+                    os.path.join(ROOT, "oracle", "cts_oracle.c"), "-o", o], check=True)
+    objs.append(o)
+    exe = os.path.join(d, driver[:-4])
+    subprocess.run(["g++", *flags, *objs, "-o", exe], check=True)
+    return exe
+
+
+@pytest.mark.parametrize("san", sorted(SAN))
+@pytest.mark.parametrize("driver", ["pattern_replay.cpp", "loopback_stress.cpp"])
+def test_host_code_under_sanitizer(san, driver):
+    with tempfile.TemporaryDirectory() as d:
+        exe = _build(d, san, driver)
+        out = subprocess.run([exe], capture_output=True, text=True, timeout=300, env={**os.environ, **ENV})
+        assert out.returncode == 0, (out.returncode, out.stderr[-4000:])
+        assert ": ok" in out.stdout
+        assert "runtime error" not in out.stderr and "WARNING: ThreadSanitizer" not in out.stderr, out.stderr[-4000:]
