@@ -96,6 +96,7 @@ def _declare(L: ctypes.CDLL) -> None:
         "cts_status_string": ([i32], ctypes.c_char_p),
         "cts_pattern_byte": ([u64], ctypes.c_uint8),
         "cts_sender_buffer_size": ([u32], u64),
+        "cts_shard_of": ([u32, u32], u32),
         "cts_engine_create": ([i32, ctypes.POINTER(P)], i32),
         "cts_engine_destroy": ([P], i32),
         "cts_engine_device": ([P], i32),

@@ -104,14 +104,6 @@ const char* cts_status_string(int status)
     }
 }
 
-uint8_t cts_pattern_byte(uint64_t stream_offset)
-{
-    const uint32_t j = (uint32_t)(stream_offset & 0xFFFFu);
-    return (uint8_t)((j & 1u) ? (j >> 9) : ((j >> 1) & 0xFFu));
-}
-
-uint64_t cts_sender_buffer_size(uint32_t max_buffer_size) { return (uint64_t)CTS_PATTERN_PERIOD + max_buffer_size; }
-
 int cts_engine_create(int device, cts_engine** out)
 {
     if (out == nullptr) return CTS_E_INVALID;

@@ -284,7 +284,17 @@ void run_side_async(int* fdslot, cts_io_pattern* p, bool inject, uint32_t inject
 extern "C" int cts_loopback_run(const cts_loopback_config* cfg, cts_engine* engine, cts_batch_verifier hook,
                                 void* hook_ctx, cts_loopback_result* out)
 {
+    return cts_loopback_run_multi(cfg, engine ? &engine : nullptr, engine ? 1u : 0u, hook, hook_ctx, out);
+}
+
+extern "C" int cts_loopback_run_multi(const cts_loopback_config* cfg, cts_engine* const* engines, uint32_t n_engines,
+                                      cts_batch_verifier hook, void* hook_ctx, cts_loopback_result* out)
+{
     if (cfg == nullptr || out == nullptr || cfg->connections == 0 || cfg->buffer_size == 0) return CTS_E_INVALID;
+    if (n_engines > 0 && engines == nullptr) return CTS_E_INVALID;
+    for (uint32_t k = 0; k < n_engines; ++k)
+        if (engines[k] == nullptr) return CTS_E_INVALID;
+    cts_engine* const engine = n_engines ? engines[0] : nullptr;  // fills the process-wide sender buffer
     const uint32_t pattern = cfg->io_pattern ? cfg->io_pattern : CTS_PATTERN_PUSH;
     if (pattern < CTS_PATTERN_PUSH || pattern > CTS_PATTERN_DUPLEX || cfg->functor > CTS_LOOPBACK_FUNCTOR_ASYNC)
         return CTS_E_INVALID;
@@ -335,7 +345,8 @@ extern "C" int cts_loopback_run(const cts_loopback_config* cfg, cts_engine* engi
     int rc = CTS_OK;
     for (uint32_t i = 0; i < 2 * n && rc == CTS_OK; ++i) {
         const cts_pattern_config c = make_cfg(i >= n);  // [0,n) clients, [n,2n) servers
-        rc = cts_io_pattern_create(&c, engine, &pats[i]);
+        cts_engine* const eng = n_engines ? engines[cts_shard_of(i % n, n_engines)] : nullptr;
+        rc = cts_io_pattern_create(&c, eng, &pats[i]);
         if (rc == CTS_OK && hook != nullptr) rc = cts_io_pattern_set_verifier(pats[i], hook, hook_ctx);
     }
     if (rc != CTS_OK) {

@@ -39,14 +39,19 @@ def declare(L: ctypes.CDLL) -> None:
     fn.argtypes = [ctypes.POINTER(LoopbackConfig), ctypes.c_void_p, A.BATCH_VERIFIER, ctypes.c_void_p,
                    ctypes.POINTER(LoopbackResult)]
     fn.restype = ctypes.c_int
+    fn = L.cts_loopback_run_multi
+    fn.argtypes = [ctypes.POINTER(LoopbackConfig), ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint32,
+                   A.BATCH_VERIFIER, ctypes.c_void_p, ctypes.POINTER(LoopbackResult)]
+    fn.restype = ctypes.c_int
 
 
 def run(connections=8, buffer_size=65536, transfer_size=1 << 30, engine=None, verifier=None,
         io_pattern=A.PATTERN_PUSH, verify=True, verify_mode=A.VERIFY_DEFERRED, batch_buffers=0,
         corrupt_connection=None, corrupt_send_index=0, socket_buffer_bytes=0, push_bytes=0, pull_bytes=0,
         functor=FUNCTOR_AUTO) -> dict:
-    """One loopback run. ``verifier`` (a cts_batch_verifier or a python fn(arena, descs) -> results) replaces the
-    engine's kernel (test harnesses / the CPU baseline)."""
+    """One loopback run. ``engine`` is one Engine or a list of them (one per GPU: connection i verifies on
+    engine[cts_shard_of(i, len)]). ``verifier`` (a cts_batch_verifier or a python fn(arena, descs) -> results)
+    replaces the engines' kernel (test harnesses / the CPU baseline)."""
     from .pattern import batch_verifier
 
     cfg = LoopbackConfig(connections, io_pattern, buffer_size, int(verify), transfer_size, verify_mode, batch_buffers,
@@ -56,7 +61,9 @@ def run(connections=8, buffer_size=65536, transfer_size=1 << 30, engine=None, ve
     if verifier is not None:
         hook = verifier if isinstance(verifier, A.BATCH_VERIFIER) else batch_verifier(verifier)
     res = LoopbackResult()
-    check("cts_loopback_run", lib().cts_loopback_run(ctypes.byref(cfg), None if engine is None else engine._h,
-                                                     hook if hook is not None else A.BATCH_VERIFIER(), None,
-                                                     ctypes.byref(res)))
+    engines = engine if isinstance(engine, (list, tuple)) else ([] if engine is None else [engine])
+    arr = (ctypes.c_void_p * max(1, len(engines)))(*[e._h.value for e in engines])
+    check("cts_loopback_run_multi",
+          lib().cts_loopback_run_multi(ctypes.byref(cfg), arr if engines else None, len(engines),
+                                       hook if hook is not None else A.BATCH_VERIFIER(), None, ctypes.byref(res)))
     return res.as_dict()

@@ -109,6 +109,11 @@ uint8_t cts_pattern_byte(uint64_t stream_offset);
 /* g_maximumBufferSize = c_bufferPatternSize + GetMaxBufferSize() (ctsIOPattern.cpp:60) */
 uint64_t cts_sender_buffer_size(uint32_t max_buffer_size);
 
+/* Which of n_shards GPUs owns a connection: fmix32(conn_index) mod n_shards (the murmur3
+ * finaliser). Every buffer of a connection goes to one GPU, so its first failing buffer and its
+ * DataError decision (ctsSocketState.cpp:221-232) stay GPU-local. */
+uint32_t cts_shard_of(uint32_t conn_index, uint32_t n_shards);
+
 /* ---- engine lifetime ------------------------------------------------------ */
 int cts_engine_create(int device, cts_engine** out);
 int cts_engine_destroy(cts_engine* engine);

@@ -64,6 +64,12 @@ typedef struct cts_loopback_result {
 int cts_loopback_run(const cts_loopback_config* cfg, cts_engine* engine, cts_batch_verifier hook, void* hook_ctx,
                      cts_loopback_result* out);
 
+/* The same over several engines (one per GPU): connection i's patterns verify on
+ * engines[cts_shard_of(i, n_engines)], so a host's receive traffic spreads over its GPUs' PCIe
+ * links with each connection on one GPU. n_engines == 0 runs on the hook alone. */
+int cts_loopback_run_multi(const cts_loopback_config* cfg, cts_engine* const* engines, uint32_t n_engines,
+                           cts_batch_verifier hook, void* hook_ctx, cts_loopback_result* out);
+
 #ifdef __cplusplus
 } /* extern "C" */
 #endif

@@ -29,8 +29,6 @@ int cts_host_free(cts_engine*, void* host_ptr)
     return CTS_OK;
 }
 
-uint64_t cts_sender_buffer_size(uint32_t max_buffer_size) { return (uint64_t)CTS_PATTERN_PERIOD + max_buffer_size; }
-
 int cts_sender_buffer_fill(cts_engine*, void*, uint32_t, void*) { return CTS_E_NO_DEVICE; }
 
 int cts_verify(cts_engine*, const void*, uint64_t, const cts_buf_desc*, uint32_t, uint32_t, cts_verify_result*, void*,

@@ -196,3 +196,18 @@ int main(void){
     assert b == [DGRAM_RECORD_DTYPE.fields["flag"][1], DGRAM_RECORD_DTYPE.fields["kind"][1],
                  DGRAM_RECORD_DTYPE.fields["completed_bytes"][1], M.Stats.head_sequence_number.offset]
     assert DGRAM_RECORD_DTYPE == oracle.DGRAM_RECORD_DTYPE
+
+
+def test_shard_of_matches_workload_sharding():
+    """cts_shard_of (the C ABI's connection -> GPU map) is workload.shard_of: fmix32(conn) mod G."""
+    import numpy as np
+
+    from ctstraffic_amd import _lib
+    from ctstraffic_amd import workload as W
+
+    conns = np.concatenate([np.arange(5000), np.array([2**31 - 1, 2**31, 2**32 - 1])]).astype(np.uint32)
+    for g in (1, 2, 3, 4, 8):
+        want = W.shard_of(conns, g)
+        got = np.array([_lib.lib().cts_shard_of(int(c), g) for c in conns])
+        assert np.array_equal(got, want), g
+    assert _lib.lib().cts_shard_of(12345, 0) == 0

@@ -16,7 +16,7 @@ import tempfile
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HOST_SRCS = ["cts_pattern.cpp", "cts_media_stream.cpp", "cts_status.cpp", "cts_loopback.cpp"]
+HOST_SRCS = ["cts_pattern.cpp", "cts_media_stream.cpp", "cts_status.cpp", "cts_loopback.cpp", "cts_host_util.cpp"]
 SAN = {
     "asan-ubsan": ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"],
     "tsan": ["-fsanitize=thread"],

@@ -122,3 +122,31 @@ def test_loopback_duplex_gpu(engine, mode):
     r = loopback.run(connections=4, buffer_size=65536, transfer_size=8 * 1024 * 1024, engine=engine,
                      io_pattern=A.PATTERN_DUPLEX, verify_mode=mode, corrupt_connection=3, corrupt_send_index=30)
     assert r["data_errors"] == 1 and r["connections_ok"] == 3
+
+
+def test_loopback_multi_engine_validation():
+    from ctstraffic_amd._lib import CtsError
+
+    shared_buffer_attach(_SENDER)
+    # no engines + a hook: the hook verifies (n_engines == 0)
+    r = loopback.run(connections=2, buffer_size=65536, transfer_size=1 << 20, verifier=_oracle_verifier, engine=[])
+    assert r["connections_ok"] == 2
+    with pytest.raises(CtsError):  # nothing to verify with
+        loopback.run(connections=1, buffer_size=65536, transfer_size=1 << 20, engine=[])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pattern", [A.PATTERN_PUSH, A.PATTERN_DUPLEX], ids=["push", "duplex"])
+def test_loopback_two_engines_gpu(engine, pattern):
+    """Connections spread over two engines by cts_shard_of (two engines on one GPU here; one per GPU on a node)."""
+    from ctstraffic_amd import Engine
+
+    with Engine(0) as e2:
+        r = loopback.run(connections=8, buffer_size=65536, transfer_size=8 * 1024 * 1024 + 2, engine=[engine, e2],
+                         io_pattern=pattern, verify_mode=A.VERIFY_DEFERRED)
+        assert r["connections_ok"] == 8 and r["data_errors"] == 0
+        for bad in (0, 5):  # connections on either engine (cts_shard_of(0, 2) != cts_shard_of(5, 2))
+            r = loopback.run(connections=8, buffer_size=65536, transfer_size=4 * 1024 * 1024, engine=[engine, e2],
+                             io_pattern=pattern, verify_mode=A.VERIFY_DEFERRED, corrupt_connection=bad,
+                             corrupt_send_index=11)
+            assert r["data_errors"] == 1 and r["connections_ok"] == 7
