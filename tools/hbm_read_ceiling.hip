@@ -85,6 +85,36 @@ __global__ void __launch_bounds__(256) read_or_slab_gs(const u32x4* __restrict__
     if (acc == 0x12345678u) out[0] = acc;
 }
 
+// LDS-DMA stream (global_load_lds_dwordx4): each wave reads its own contiguous region through a
+// ring of D 1-KiB LDS slots, D DMAs in flight; lane l reads back the 16 bytes it requested
+// (the DMA destination is lane-linear), so no barrier is needed, only counted vmcnt waits.
+template <int D, int AUX>
+__global__ void __launch_bounds__(256) read_ldsdma(const u32x4* __restrict__ p, uint32_t per_wave, uint32_t* out)
+{
+    __shared__ u32x4 ring[4][D][64];
+    const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63u;
+    const u32x4* base = p + ((uint64_t)blockIdx.x * 4u + w) * per_wave * 64u + l;
+    typedef __attribute__((address_space(3))) void* lds_ptr;
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+        __builtin_amdgcn_global_load_lds(base + d * 64, (lds_ptr)&ring[w][d][0], 16, 0, AUX);
+    uint32_t acc = 0;
+    uint32_t k = 0;
+    for (; k + D < per_wave; ++k) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D - 1) : "memory");
+        const u32x4 v = ring[w][k % D][l];
+        acc |= v[0] ^ v[1] ^ v[2] ^ v[3];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_global_load_lds(base + (uint64_t)(k + D) * 64, (lds_ptr)&ring[w][k % D][0], 16, 0, AUX);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (; k < per_wave; ++k) {
+        const u32x4 v = ring[w][k % D][l];
+        acc |= v[0] ^ v[1] ^ v[2] ^ v[3];
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
 // write reference for the fill kernel: the same slab shape, 16-byte nontemporal stores
 template <int U>
 __global__ void __launch_bounds__(256) write_slab_gs(u32x4* __restrict__ p, uint32_t per_block, uint32_t nslabs)
@@ -135,6 +165,7 @@ int main(int argc, char** argv)
     int cus = 0;
     CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
     // argv: [reps] [arena MiB (256 = one config-2 batch)] [quick: 1 = two configs only] [ramp] [writes: 1 = store sweep]
+    //       [dma: 1 = LDS-DMA sweep]
     const size_t arena = (size_t)(argc > 2 ? atoi(argv[2]) : 256) << 20;
     const bool quick = argc > 3 && atoi(argv[3]) != 0;
     const bool ramp = argc > 4 && atoi(argv[4]) != 0;  // arena holds the ctsTraffic pattern
@@ -190,6 +221,32 @@ int main(int argc, char** argv)
                BPC, ms * 1e3, arena / (ms * 1e-3) / 1e9);                                                     \
     } while (0)
 
+#define RUN_DMA(D, AUX, BPC)                                                                                   \
+    do {                                                                                                       \
+        const uint32_t grid = (uint32_t)cus * (BPC);                                                           \
+        const uint32_t per_wave = (uint32_t)(nchunks / 64 / (grid * 4u));                                      \
+        const double bytes = (double)per_wave * 64 * 16 * grid * 4;                                            \
+        float ms = time_ms([&](int i) { read_ldsdma<D, AUX><<<grid, 256, 0, s>>>(bufs[i % R], per_wave, out); }, \
+                           reps, s);                                                                           \
+        printf("{\"kind\":\"ldsdma\",\"D\":%d,\"aux\":%d,\"blocks_per_cu\":%d,\"us\":%.2f,\"GBps\":%.1f}\n", D, AUX, \
+               BPC, ms * 1e3, bytes / (ms * 1e-3) / 1e9);                                                       \
+    } while (0)
+
+    const bool dma = argc > 6 && atoi(argv[6]) != 0;
+    if (dma) {
+        for (int pass = 0; pass < 2; ++pass) {
+            RUN_GS(4, true, 8);
+            RUN_SLAB(4, true, 65536);
+            RUN_DMA(4, 2, 2);
+            RUN_DMA(8, 2, 2);
+            RUN_DMA(8, 2, 1);
+            RUN_DMA(16, 2, 1);
+            RUN_DMA(8, 0, 2);
+            RUN_DMA(4, 2, 4);
+            RUN_DMA(16, 2, 2);
+        }
+        return 0;
+    }
     const bool writes = argc > 5 && atoi(argv[5]) != 0;
     if (writes) {
         for (int pass = 0; pass < 2; ++pass) {
