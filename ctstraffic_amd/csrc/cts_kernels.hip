@@ -472,6 +472,41 @@ __device__ __forceinline__ void scan_whole_exact(const Span& s, uint32_t lane, u
     scan_whole_exact_impl<TEAM, U, NT, false>(s, r, lane, first, count);
 }
 
+// Spans of 2 GiB or more (a u32 ctsTask length allows 4 GiB - 1). The buffer-resource streams above
+// address a span with 32-bit byte offsets and a 32-bit num_records (and use 0x7FFFFFF0 as an
+// out-of-range offset), so such spans take this plain pass instead: 64-bit pointers, exact from the
+// start (first differing byte and count, RtlCompareMemory semantics), TEAM lanes striding the chunks
+// G loads at a time (2: the pass must not raise the hot kernels' register count). Positions are span-relative u32 (16c + idx - lo < 2^32 even when 16c wraps).
+constexpr uint32_t kGiantChunks = 1u << 27;
+
+__device__ __forceinline__ bool span_giant(const Span& s)
+{
+    return __builtin_amdgcn_readfirstlane(s.nchunks >= kGiantChunks ? 1u : 0u) != 0u;
+}
+
+template <int TEAM, bool NT, uint32_t G = 2>
+__device__ __forceinline__ void scan_giant_exact(const Span& s, uint32_t lane, uint32_t& first, uint32_t& count)
+{
+    for (uint32_t cb = 0; cb < s.nchunks; cb += G * TEAM) {
+        u32x4 d[G];
+#pragma unroll
+        for (uint32_t g = 0; g < G; ++g) {
+            const uint32_t c = cb + g * TEAM + lane;
+            d[g] = load_chunk_g<NT>(s.p + (c < s.nchunks ? c : 0u));
+        }
+#pragma unroll
+        for (uint32_t g = 0; g < G; ++g) {
+            const uint32_t c = cb + g * TEAM + lane;
+            if (c < s.nchunks) {
+                u32x4 x = chunk_xor(s, c, d[g]);
+                if (c == 0u || c == s.nchunks - 1u)
+                    x &= range_mask(c == 0u ? s.lo : 0u, c == s.nchunks - 1u ? s.hi_last : 16u);
+                take_diff(s, c, x, first, count);
+            }
+        }
+    }
+}
+
 __device__ __forceinline__ uint32_t wave_min(uint32_t v)
 {
 #pragma unroll
@@ -614,7 +649,11 @@ __global__ void __launch_bounds__(kBlock, (U <= 8 ? 8 : 4))
         const Span s = make_span(arena, d);
         uint32_t first = kNone, count = 0;
         bool dirty;
-        if (XD && __builtin_amdgcn_readfirstlane(span_whole_lines(s) ? 1u : 0u)) {
+        if (span_giant(s)) {  // >= 2 GiB: 64-bit exact pass
+            scan_giant_exact<kBlock, NT>(s, lane, first, count);
+            dirty = __builtin_amdgcn_readfirstlane(__syncthreads_or(first != kNone)) != 0;
+            if (dirty) block_reduce_mismatch(first, count);
+        } else if (XD && __builtin_amdgcn_readfirstlane(span_whole_lines(s) ? 1u : 0u)) {
             // whole-line span, exact diff in registers: only the reduction is left
             scan_whole_exact<kBlock, U, NT, SPLIT>(s, lane, first, count);
             dirty = __builtin_amdgcn_readfirstlane(__syncthreads_or(first != kNone)) != 0;
@@ -701,12 +740,15 @@ __global__ void __launch_bounds__(kBlock, (U <= 8 ? 8 : 4))
             continue;
         }
         const Span s = make_span(arena, d);
-        const uint32_t acc = scan_buffer<kBlock, U, NT>(s, lane);
+        const bool giant = span_giant(s);
+        uint32_t gfirst = kNone, gcount = 0;
+        if (giant) scan_giant_exact<kBlock, NT>(s, lane, gfirst, gcount);  // >= 2 GiB: 64-bit exact pass
+        const uint32_t acc = giant ? (gfirst != kNone ? 1u : 0u) : scan_buffer<kBlock, U, NT>(s, lane);
         ArriveSlot* slot = &slots[j % kRing];
         uint32_t flag = 0;
         if (__any(acc != 0u)) {  // rare: exact share of this wave's chunks
-            uint32_t first = kNone, count = 0;
-            if (acc != 0u) scan_exact_owned<kBlock, 2, NT>(s, lane, first, count);
+            uint32_t first = gfirst, count = gcount;
+            if (acc != 0u && !giant) scan_exact_owned<kBlock, 2, NT>(s, lane, first, count);
             first = wave_min(first);
             count = wave_sum(count);
             if ((lane & 63u) == 0) {
@@ -765,12 +807,18 @@ __global__ void __launch_bounds__(kBlock)
             continue;
         }
         const Span s = make_span(arena, d);
-        const uint32_t acc = scan_buffer<64, U, NT>(s, lane);
         uint32_t first = kNone, count = 0;
-        if (__any(acc != 0u)) {
-            if (acc != 0u) scan_exact_owned<64, 2, NT>(s, lane, first, count);
+        if (span_giant(s)) {  // >= 2 GiB: 64-bit exact pass
+            scan_giant_exact<64, NT>(s, lane, first, count);
             first = wave_min(first);
             count = wave_sum(count);
+        } else {
+            const uint32_t acc = scan_buffer<64, U, NT>(s, lane);
+            if (__any(acc != 0u)) {
+                if (acc != 0u) scan_exact_owned<64, 2, NT>(s, lane, first, count);
+                first = wave_min(first);
+                count = wave_sum(count);
+            }
         }
         if (lane == 0) finish_buffer(s, d, i, first, count, results, ctr[wave], conn_first_fail, n_conns);
     }
@@ -1185,7 +1233,11 @@ __global__ void __launch_bounds__(kBlock)
             } else {
                 const uint32_t acc = pipe_consume<U, NT>(cur, lane);
                 uint32_t first = kNone, count = 0;
-                if (__any(acc != 0u)) {
+                if (span_giant(cur.s)) {  // >= 2 GiB: the prefetched round is discarded, 64-bit exact pass
+                    scan_giant_exact<64, NT>(cur.s, lane, first, count);
+                    first = wave_min(first);
+                    count = wave_sum(count);
+                } else if (__any(acc != 0u)) {
                     if (acc != 0u) scan_exact_owned<64, 2, NT>(cur.s, lane, first, count);
                     first = wave_min(first);
                     count = wave_sum(count);
@@ -1257,7 +1309,8 @@ __global__ void __launch_bounds__(kBlock) fill_kernel(uint8_t* __restrict__ aren
         const uint32_t hi_last = (uint32_t)((uint64_t)lo + len - 16ull * (nchunks - 1u));
         const uint32_t q0 = (d.expected_pattern_offset - lo) & 0xFFFFu;
         u32x4* p = reinterpret_cast<u32x4*>(sp - lo);
-        if (__builtin_amdgcn_readfirstlane((lo == 0u && hi_last == 16u) ? 1u : 0u)) {
+        // (whole-chunk spans stream buffer stores: 32-bit offsets, so spans >= 2 GiB take the pointer loop)
+        if (__builtin_amdgcn_readfirstlane((lo == 0u && hi_last == 16u && nchunks < kGiantChunks) ? 1u : 0u)) {
             if (__builtin_amdgcn_readfirstlane(q0 & 1u) == 0u) fill_whole_rounds<TEAM, FU, true>(p, nchunks, q0, lane);
             else fill_whole_rounds<TEAM, FU, false>(p, nchunks, q0, lane);
             continue;
@@ -1338,7 +1391,8 @@ __global__ void __launch_bounds__(kBlock)
             d.length = CTS_UDP_DATA_HEADER_LENGTH;
         }
         const Span s = make_span(arena, d);
-        const uint32_t acc = scan_buffer<64, U, NT>(s, lane);
+        const bool giant = span_giant(s);  // >= 2 GiB: 64-bit exact pass (below)
+        const uint32_t acc = giant ? 0u : scan_buffer<64, U, NT>(s, lane);
         // header: ctsMediaStreamMessage::ValidateBufferLengthFromTask (ctsMediaStreamProtocol.hpp:284-329)
         uint32_t flag = 0, kind;
         if (bad) {
@@ -1377,7 +1431,11 @@ __global__ void __launch_bounds__(kBlock)
             continue;
         }
         uint32_t first = kNone, count = 0;
-        if (__any(acc != 0u)) {
+        if (giant) {
+            scan_giant_exact<64, NT>(s, lane, first, count);
+            first = wave_min(first);
+            count = wave_sum(count);
+        } else if (__any(acc != 0u)) {
             if (acc != 0u) scan_exact_owned<64, 2, NT>(s, lane, first, count);
             first = wave_min(first);
             count = wave_sum(count);

@@ -396,3 +396,50 @@ def test_small_variants_parity(engine, small_variant):
         engine.set_attr(_lib.ATTR_SMALL_VARIANT, default_sv)
         engine.set_attr(_lib.ATTR_SMALL_BLOCKS_PER_CU, default_sbpc)
         engine.set_attr(_lib.ATTR_SMALL_CHUNK, default_chunk)
+
+
+# ---- maximum sizes: one buffer of 2^32 - 1 bytes, buffers past the 4 GiB arena offset -----------------------
+def test_max_length_buffers(engine):
+    """ctsTask::m_bufferLength is a u32: a single 2^32 - 1-byte buffer (last byte corrupted) and a 2^31 + 77-byte
+    buffer starting past 2^32 in the arena at an odd address with the MediaStream skip. Both kernels paths; the fill
+    writes them first (its 64-bit offsets are checked at sampled positions against the oracle's pattern)."""
+    L0, L1 = 2**32 - 1, 2**31 + 77
+    off1 = 2**32 + 3
+    total = off1 + L1 + 64
+    try:
+        arena = torch.zeros(total, dtype=torch.uint8, device=DEV)
+    except RuntimeError:  # pragma: no cover
+        pytest.skip("not enough device memory")
+    descs = np.zeros(2, dtype=DESC_DTYPE)
+    descs[0] = (0, L0, 12345, 0, 0)
+    descs[1] = (off1, L1, 65535, 1, 26)
+    d = to_dev(descs)
+    engine.fill(arena, d, max_length_hint=0)
+    torch.cuda.synchronize()
+    pat = oracle.sender_buffer(65536)  # P(j) for j < 65536 + 65536
+    for b, (off, ln, exp, skip) in enumerate([(0, L0, 12345, 0), (off1, L1, 65535, 26)]):
+        for rel in (0, 1, 2**31 - 5, 2**32 - 2 - 2 * skip if b == 0 else ln - skip - 1, ln - skip - 1):
+            got = int(arena[off + skip + rel].item())
+            assert got == int(pat[(exp + rel) % 65536]), (b, rel)
+        assert int(arena[off + ln].item()) == 0 if b == 1 else True  # the byte after the buffer is untouched
+    # corrupt: buffer 0 at its last byte, buffer 1 at span byte 2^31 + 9 (past 2^31)
+    c0, c1 = L0 - 1, 2**31 + 9
+    arena[c0] ^= 0x5A
+    arena[off1 + 26 + c1] ^= 0xFF
+    exp_first = [c0, c1]
+    exp_bytes = [int(pat[(12345 + c0) % 65536]), int(pat[(65535 + c1) % 65536])]
+    act_bytes = [exp_bytes[0] ^ 0x5A, exp_bytes[1] ^ 0xFF]
+    for hint in (0, 1472):  # workgroup path, and the four-per-wave team path walking one giant span
+        res = engine.new_results(2)
+        ctr = engine.new_counters()
+        engine.verify(arena, d, max_length_hint=hint, results=res, counters=ctr)
+        torch.cuda.synchronize()
+        r = res.cpu().numpy().view(RESULT_DTYPE)
+        for b in range(2):
+            assert (int(r[b]["first_mismatch"]), int(r[b]["mismatch_bytes"]), int(r[b]["expected"]),
+                    int(r[b]["actual"]), int(r[b]["pass"])) == (exp_first[b], 1, exp_bytes[b], act_bytes[b], 0), (hint, b)
+        c = engine.read_counters(ctr)
+        assert c == {"bytes_checked": L0 + L1 - 26, "bytes_ok": 0, "buffers_checked": 2, "buffers_failed": 2,
+                     "mismatched_bytes": 2}
+    del arena
+    torch.cuda.empty_cache()
