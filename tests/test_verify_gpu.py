@@ -402,7 +402,8 @@ def test_small_variants_parity(engine, small_variant):
 def test_max_length_buffers(engine):
     """ctsTask::m_bufferLength is a u32: a single 2^32 - 1-byte buffer (last byte corrupted) and a 2^31 + 77-byte
     buffer starting past 2^32 in the arena at an odd address with the MediaStream skip. Both kernels paths; the fill
-    writes them first (its 64-bit offsets are checked at sampled positions against the oracle's pattern)."""
+    writes them first (its 64-bit offsets are checked at sampled positions against the oracle's pattern). Every
+    kernel family: workgroup, barrier-free workgroup, wave, pipelined wave, four-per-wave."""
     L0, L1 = 2**32 - 1, 2**31 + 77
     off1 = 2**32 + 3
     total = off1 + L1 + 64
@@ -429,7 +430,13 @@ def test_max_length_buffers(engine):
     exp_first = [c0, c1]
     exp_bytes = [int(pat[(12345 + c0) % 65536]), int(pat[(65535 + c1) % 65536])]
     act_bytes = [exp_bytes[0] ^ 0x5A, exp_bytes[1] ^ 0xFF]
-    for hint in (0, 1472):  # workgroup path, and the four-per-wave team path walking one giant span
+    from ctstraffic_amd import _lib
+
+    cases = [(_lib.ATTR_VERIFY_VARIANT, 13, 0), (_lib.ATTR_VERIFY_VARIANT, 4, 0), (_lib.ATTR_VERIFY_VARIANT, 3, 0),
+             (_lib.ATTR_SMALL_VARIANT, 9, 1472), (_lib.ATTR_SMALL_VARIANT, 0, 1472), (_lib.ATTR_SMALL_VARIANT, 3, 1472)]
+    defaults = {a: engine.get_attr(a) for a, _, _ in cases}
+    for attr, variant, hint in cases:  # workgroup, barrier-free workgroup, wave, four-per-wave, wave, pipelined wave
+        engine.set_attr(attr, variant)
         res = engine.new_results(2)
         ctr = engine.new_counters()
         engine.verify(arena, d, max_length_hint=hint, results=res, counters=ctr)
@@ -437,9 +444,11 @@ def test_max_length_buffers(engine):
         r = res.cpu().numpy().view(RESULT_DTYPE)
         for b in range(2):
             assert (int(r[b]["first_mismatch"]), int(r[b]["mismatch_bytes"]), int(r[b]["expected"]),
-                    int(r[b]["actual"]), int(r[b]["pass"])) == (exp_first[b], 1, exp_bytes[b], act_bytes[b], 0), (hint, b)
+                    int(r[b]["actual"]), int(r[b]["pass"])) == (exp_first[b], 1, exp_bytes[b], act_bytes[b], 0), (
+                        attr, variant, b)
         c = engine.read_counters(ctr)
         assert c == {"bytes_checked": L0 + L1 - 26, "bytes_ok": 0, "buffers_checked": 2, "buffers_failed": 2,
                      "mismatched_bytes": 2}
+        engine.set_attr(attr, defaults[attr])
     del arena
     torch.cuda.empty_cache()
