@@ -25,6 +25,12 @@ struct cts_engine {
     size_t stage_cap = 0;
     cts_buf_desc* stage_desc = nullptr;       // pinned, device-mapped
     cts_verify_result* stage_res = nullptr;   // pinned, device-mapped
+    // cts_verify_host_batch staging (pinned, device-mapped), grown on demand and kept
+    void* batch_desc = nullptr;
+    size_t batch_desc_cap = 0;
+    void* batch_res = nullptr;
+    size_t batch_res_cap = 0;
+    void* batch_ctr = nullptr;
 };
 
 namespace {
@@ -70,20 +76,27 @@ T* device_view(T* host)
     return static_cast<T*>(d);
 }
 
+// Grow a pinned, device-mapped staging area to >= bytes (powers of two from `floor`).
+int ensure_pinned(void** p, size_t* cap, size_t bytes, size_t floor)
+{
+    if (*cap >= bytes && *p != nullptr) return CTS_OK;
+    if (*p) (void)hipHostFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    size_t c = floor;
+    while (c < bytes) c <<= 1;
+    const int rc = host_alloc_mapped(c, p);
+    if (rc != CTS_OK) return rc;
+    *cap = c;
+    return CTS_OK;
+}
+
 int ensure_stage(cts_engine* e, size_t bytes)
 {
-    if (e->stage_cap >= bytes) return CTS_OK;
-    if (e->stage) (void)hipHostFree(e->stage);
-    e->stage = nullptr;
-    e->stage_cap = 0;
-    size_t cap = 1u << 20;
-    while (cap < bytes) cap <<= 1;
-    void* p = nullptr;
-    const int rc = host_alloc_mapped(cap, &p);
-    if (rc != CTS_OK) return rc;
+    void* p = e->stage;
+    const int rc = ensure_pinned(&p, &e->stage_cap, bytes, 1u << 20);
     e->stage = static_cast<uint8_t*>(p);
-    e->stage_cap = cap;
-    return CTS_OK;
+    return rc;
 }
 
 }  // namespace
@@ -159,6 +172,9 @@ int cts_engine_destroy(cts_engine* e)
         if (e->stage) (void)hipHostFree(e->stage);
         if (e->stage_desc) (void)hipHostFree(e->stage_desc);
         if (e->stage_res) (void)hipHostFree(e->stage_res);
+        if (e->batch_desc) (void)hipHostFree(e->batch_desc);
+        if (e->batch_res) (void)hipHostFree(e->batch_res);
+        if (e->batch_ctr) (void)hipHostFree(e->batch_ctr);
     }
     delete e;
     return CTS_OK;
@@ -399,22 +415,16 @@ int cts_verify_host_batch(cts_engine* e, const void* const* bufs, const uint32_t
         if (bufs[i] == nullptr && lens[i] != 0) return CTS_E_INVALID;
         total += ((uint64_t)lens[i] + 15u) & ~(uint64_t)15u;
     }
-    void* pdesc = nullptr;
-    void* pres = nullptr;
-    void* pctr = nullptr;
     int rc = ensure_stage(e, (size_t)total + 16);
     if (rc != CTS_OK) return rc;
-    if ((rc = host_alloc_mapped(sizeof(cts_buf_desc) * n, &pdesc)) != CTS_OK) return rc;
-    if ((rc = host_alloc_mapped(sizeof(cts_verify_result) * n, &pres)) != CTS_OK) {
-        (void)hipHostFree(pdesc);
+    if ((rc = ensure_pinned(&e->batch_desc, &e->batch_desc_cap, sizeof(cts_buf_desc) * n, 4096)) != CTS_OK) return rc;
+    if ((rc = ensure_pinned(&e->batch_res, &e->batch_res_cap, sizeof(cts_verify_result) * n, 4096)) != CTS_OK) return rc;
+    if (counters && e->batch_ctr == nullptr &&
+        (rc = host_alloc_mapped(cts_counters_device_bytes(), &e->batch_ctr)) != CTS_OK)
         return rc;
-    }
-    if (counters && (rc = host_alloc_mapped(cts_counters_device_bytes(), &pctr)) != CTS_OK) {
-        (void)hipHostFree(pdesc);
-        (void)hipHostFree(pres);
-        return rc;
-    }
-    cts_buf_desc* hd = static_cast<cts_buf_desc*>(pdesc);
+    void* const pres = e->batch_res;
+    void* const pctr = counters ? e->batch_ctr : nullptr;
+    cts_buf_desc* hd = static_cast<cts_buf_desc*>(e->batch_desc);
     uint64_t off = 0;
     uint32_t maxlen = 0;
     for (uint32_t i = 0; i < n; ++i) {
@@ -446,9 +456,6 @@ int cts_verify_host_batch(cts_engine* e, const void* const* bufs, const uint32_t
             }
         }
     }
-    (void)hipHostFree(pdesc);
-    (void)hipHostFree(pres);
-    if (pctr) (void)hipHostFree(pctr);
     return err == hipSuccess ? CTS_OK : CTS_E_HIP;
 }
 

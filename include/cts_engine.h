@@ -201,9 +201,11 @@ int cts_host_device_pointer(void* host_ptr, void** dev_view);
 
 /* Batched host path (PCIe-inclusive): verifies n host buffers
  * (bufs[i] + skip_heads[i], lens[i] - skip_heads[i] bytes, expected offsets
- * expected[i]) with pinned double-buffered staging and hipMemcpyAsync
- * overlapped with the kernel. skip_heads may be NULL (all 0). results[n] host
- * memory; counters (host) accumulated into if non-NULL. */
+ * expected[i]) in one kernel launch: the buffers are copied into the engine's
+ * pinned, device-mapped staging arena (kept and grown across calls) and the
+ * kernel reads them in place over PCIe (zero copy). skip_heads may be NULL
+ * (all 0). results[n] host memory; counters (host) accumulated into if
+ * non-NULL. Thread-safe (serialised per engine); synchronous. */
 int cts_verify_host_batch(cts_engine* engine, const void* const* bufs, const uint32_t* lens,
                           const uint32_t* expected, const uint32_t* skip_heads, uint32_t n,
                           cts_verify_result* results, cts_counters* counters);

@@ -301,13 +301,15 @@ def test_verify_host_single(engine):
 
 
 def test_verify_host_batch(engine):
-    rng = np.random.default_rng(5)
-    arena, descs = _random_case(rng, 100, 3000, skip=True)
-    bufs = [arena[int(d["byte_offset"]): int(d["byte_offset"]) + int(d["length"])] for d in descs]
-    r, c = engine.verify_host_batch(bufs, descs["expected_pattern_offset"], descs["skip_head"])
-    er, ec, _ = oracle.verify_batch(arena, descs)
-    assert_results_equal(r, er)
-    assert c == ec
+    """Repeated calls reuse (and grow) the engine's pinned staging: small, larger, small again."""
+    for seed, n, max_len in ((5, 100, 3000), (6, 3000, 70000), (7, 17, 200)):
+        rng = np.random.default_rng(seed)
+        arena, descs = _random_case(rng, n, max_len, skip=True)
+        bufs = [arena[int(d["byte_offset"]): int(d["byte_offset"]) + int(d["length"])] for d in descs]
+        r, c = engine.verify_host_batch(bufs, descs["expected_pattern_offset"], descs["skip_head"])
+        er, ec, _ = oracle.verify_batch(arena, descs)
+        assert_results_equal(r, er, "seed %d" % seed)
+        assert c == ec
 
 
 # ---- every launch variant / geometry is bit-identical ------------------------------------------
