@@ -112,6 +112,8 @@ def _declare(L: ctypes.CDLL) -> None:
         "cts_host_free": ([P, P], i32),
         "cts_engine_set_attr": ([P, i32, i32], i32),
         "cts_engine_get_attr": ([P, i32, ctypes.POINTER(i32)], i32),
+        "cts_engine_stream_create": ([P, ctypes.POINTER(P)], i32),
+        "cts_engine_stream_destroy": ([P, P], i32),
         "cts_host_device_pointer": ([P, ctypes.POINTER(P)], i32),
     }
     for name, (argtypes, restype) in sigs.items():

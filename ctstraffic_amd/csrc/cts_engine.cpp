@@ -182,6 +182,24 @@ int cts_engine_destroy(cts_engine* e)
 
 int cts_engine_device(const cts_engine* e) { return e ? e->device : CTS_E_INVALID; }
 
+int cts_engine_stream_create(cts_engine* e, void** stream)
+{
+    if (e == nullptr || stream == nullptr) return CTS_E_INVALID;
+    DeviceGuard g(e->device);
+    if (!g.ok) return CTS_E_HIP;
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return CTS_E_HIP;
+    *stream = s;
+    return CTS_OK;
+}
+
+int cts_engine_stream_destroy(cts_engine* e, void* stream)
+{
+    if (e == nullptr || stream == nullptr) return CTS_E_INVALID;
+    DeviceGuard g(e->device);
+    return hip_status(hipStreamDestroy(static_cast<hipStream_t>(stream)));
+}
+
 int cts_engine_set_attr(cts_engine* e, int attr, int value)
 {
     if (e == nullptr) return CTS_E_INVALID;

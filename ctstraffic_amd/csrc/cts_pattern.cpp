@@ -285,7 +285,7 @@ struct cts_io_pattern {
     }
     virtual ~cts_io_pattern()
     {
-        if (stream) (void)hipStreamDestroy(stream);
+        if (stream) (void)cts_engine_stream_destroy(engine, stream);
     }
 
     cts_pattern_config cfg;
@@ -514,10 +514,13 @@ struct cts_io_pattern {
         bytes_recv_at_failure = recv_after;
     }
 
-    int EnsureStream()
+    int EnsureStream()  // on the engine's device, not the calling thread's current one
     {
         if (stream != nullptr) return CTS_OK;
-        return hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) == hipSuccess ? CTS_OK : CTS_E_HIP;
+        void* s = nullptr;
+        const int rc = cts_engine_stream_create(engine, &s);
+        stream = static_cast<hipStream_t>(s);
+        return rc;
     }
 
     // One buffer, now (ctsIOPattern.cpp:745-775). Returns CTS_OK and sets *pass.
@@ -923,14 +926,14 @@ int cts_shared_buffer_init(cts_engine* engine, uint32_t max_buffer_size)
     int rc = cts_host_alloc(engine, need, &h, &d);
     if (rc != CTS_OK) return rc;
     // the fill kernel writes the pinned sender buffer through its device view
-    hipStream_t s = nullptr;
-    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
+    void* s = nullptr;
+    if ((rc = cts_engine_stream_create(engine, &s)) != CTS_OK) {
         (void)cts_host_free(engine, h);
-        return CTS_E_HIP;
+        return rc;
     }
     rc = cts_sender_buffer_fill(engine, d, max_buffer_size, s);
-    if (rc == CTS_OK && hipStreamSynchronize(s) != hipSuccess) rc = CTS_E_HIP;
-    (void)hipStreamDestroy(s);
+    if (rc == CTS_OK && hipStreamSynchronize(static_cast<hipStream_t>(s)) != hipSuccess) rc = CTS_E_HIP;
+    (void)cts_engine_stream_destroy(engine, s);
     if (rc != CTS_OK) {
         (void)cts_host_free(engine, h);
         return rc;

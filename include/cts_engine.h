@@ -136,6 +136,11 @@ typedef enum cts_engine_attr {
     CTS_ATTR_SMALL_CHUNK = 9          /* chunked small-buffer walk: buffers per chunk (0 = contiguous) */
 } cts_engine_attr;
 int cts_engine_set_attr(cts_engine* engine, int attr, int value);
+/* A non-blocking HIP stream on the engine's device, whatever device the calling
+ * thread has current (one per connection: the reference serialises IO per
+ * connection under the ctsSocket lock, ctsSocket.h:189). */
+int cts_engine_stream_create(cts_engine* engine, void** stream);
+int cts_engine_stream_destroy(cts_engine* engine, void* stream);
 int cts_engine_get_attr(const cts_engine* engine, int attr, int* value);
 
 /* ---- fill (write-bound) --------------------------------------------------- */

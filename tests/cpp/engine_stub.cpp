@@ -39,8 +39,9 @@ int cts_verify(cts_engine*, const void*, uint64_t, const cts_buf_desc*, uint32_t
 
 int cts_verify_host(cts_engine*, const void*, uint32_t, uint32_t, cts_verify_result*) { return CTS_E_NO_DEVICE; }
 
-hipError_t hipStreamCreateWithFlags(hipStream_t*, unsigned int) { return hipErrorNoDevice; }
-hipError_t hipStreamDestroy(hipStream_t) { return hipErrorNoDevice; }
+int cts_engine_stream_create(cts_engine*, void**) { return CTS_E_NO_DEVICE; }
+int cts_engine_stream_destroy(cts_engine*, void*) { return CTS_E_NO_DEVICE; }
+
 hipError_t hipStreamSynchronize(hipStream_t) { return hipErrorNoDevice; }
 
 }  // extern "C"

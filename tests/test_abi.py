@@ -211,3 +211,13 @@ def test_shard_of_matches_workload_sharding():
         got = np.array([_lib.lib().cts_shard_of(int(c), g) for c in conns])
         assert np.array_equal(got, want), g
     assert _lib.lib().cts_shard_of(12345, 0) == 0
+
+
+def test_engine_stream_create_rejects_null():
+    import ctypes
+
+    from ctstraffic_amd import _lib
+
+    s = ctypes.c_void_p()
+    assert _lib.lib().cts_engine_stream_create(None, ctypes.byref(s)) == _lib.CTS_E_INVALID
+    assert _lib.lib().cts_engine_stream_destroy(None, None) == _lib.CTS_E_INVALID

@@ -454,3 +454,21 @@ def test_max_length_buffers(engine):
         engine.set_attr(attr, defaults[attr])
     del arena
     torch.cuda.empty_cache()
+
+
+def test_engine_stream(engine):
+    """cts_engine_stream_create: a stream on the engine's device that cts_verify runs on."""
+    import ctypes
+
+    from ctstraffic_amd import _lib
+
+    s = ctypes.c_void_p()
+    assert _lib.lib().cts_engine_stream_create(engine._h, ctypes.byref(s)) == 0 and s.value
+    w = W.tcp_resident(n_buffers=32, corrupt_rate=8)
+    arena, descs = W.materialize(engine, w, device=DEV)
+    ctr = engine.new_counters()
+    torch.cuda.synchronize()
+    engine.verify(arena, descs, max_length_hint=w.max_length, counters=ctr, stream=s.value)
+    exp = W.expected_results(w)[2]
+    assert engine.read_counters(ctr, stream=s.value) == exp
+    assert _lib.lib().cts_engine_stream_destroy(engine._h, s) == 0
