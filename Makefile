@@ -10,7 +10,14 @@ HDRS      := $(wildcard include/*.h) $(wildcard $(CSRC)/*.hpp)
 SRCS      := $(wildcard $(CSRC)/*.hip) $(wildcard $(CSRC)/*.cpp)
 OBJS      := $(patsubst $(CSRC)/%,ctstraffic_amd/build/%.o,$(SRCS))
 
-all: $(ENGINE_SO) oracle
+DEVICE_VERIFY := ctstraffic_amd/build/device_verify
+
+all: $(ENGINE_SO) oracle $(DEVICE_VERIFY)
+
+# C++ device-resident sample against the C ABI (run on the GPU box by tests/test_cpp_abi.py)
+$(DEVICE_VERIFY): tests/cpp/device_verify.cpp $(ENGINE_SO) include/cts_engine.h
+	@mkdir -p ctstraffic_amd/build
+	$(HIPCC) -O2 -std=c++17 -Iinclude $< -o $@ -Lctstraffic_amd -lcts_engine -Wl,-rpath,'$$ORIGIN/..'
 
 ctstraffic_amd/build/%.o: $(CSRC)/% $(HDRS)
 	@mkdir -p ctstraffic_amd/build
