@@ -44,6 +44,7 @@ ATTR_SMALL_VARIANT = 6
 ATTR_FILL_BLOCKS_PER_CU = 7
 ATTR_MS_VARIANT = 8
 ATTR_SMALL_CHUNK = 9
+ATTR_FILL_NT = 10
 
 
 class CtsError(RuntimeError):

@@ -141,6 +141,7 @@ int cts_engine_create(int device, cts_engine** out)
     e->geo.fill_blocks_per_cu = env_int("CTS_FILL_BLOCKS_PER_CU", e->geo.fill_blocks_per_cu);
     e->geo.ms_variant = env_int("CTS_MS_VARIANT", e->geo.ms_variant);
     e->geo.small_chunk = env_int("CTS_SMALL_CHUNK", e->geo.small_chunk);
+    e->geo.fill_nt = env_int("CTS_FILL_NT", e->geo.fill_nt);
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
         delete e;
         return CTS_E_HIP;
@@ -237,6 +238,10 @@ int cts_engine_set_attr(cts_engine* e, int attr, int value)
         if (value < 0 || value > (1 << 24)) return CTS_E_INVALID;
         e->geo.small_chunk = value;
         return CTS_OK;
+    case CTS_ATTR_FILL_NT:
+        if (value < 0 || value > 2) return CTS_E_INVALID;
+        e->geo.fill_nt = value;
+        return CTS_OK;
     default: return CTS_E_INVALID;
     }
 }
@@ -254,6 +259,7 @@ int cts_engine_get_attr(const cts_engine* e, int attr, int* value)
     case CTS_ATTR_FILL_BLOCKS_PER_CU: *value = e->geo.fill_blocks_per_cu; return CTS_OK;
     case CTS_ATTR_MS_VARIANT: *value = e->geo.ms_variant; return CTS_OK;
     case CTS_ATTR_SMALL_CHUNK: *value = e->geo.small_chunk; return CTS_OK;
+    case CTS_ATTR_FILL_NT: *value = e->geo.fill_nt; return CTS_OK;
     default: return CTS_E_INVALID;
     }
 }

@@ -35,7 +35,9 @@ struct LaunchGeometry {
                                  // 4 M datagrams vs 1.24 ms for variant 1 before output staging)
     int small_chunk = 0;         // chunked walk of small variant 9 / MediaStream variant 3: buffers per chunk (0 = one
                                  // contiguous range per workgroup)
-    int fill_blocks_per_cu = 2;  // fill grid cap (write-bound: 2 measured best, tools/tune_verify.py --op fill)
+    int fill_nt = 2;             // fill store policy: 0 plain, 1 nontemporal, 2 by path (plain for the workgroup
+                                 // path, nontemporal for datagrams; tools/tune_verify.py --op fill)
+    int fill_blocks_per_cu = 1;  // fill grid cap (write-bound; plain stores: 1 measured best, 48.7 vs 49.1-49.4 us)
     int verify_variant = 13;     // see launch_verify (13: variant 11 at U2; 11: variant 10 + in-register exact diff;
                                  // 10: even-phase stream + whole-line spans, U4, measured 1.3-3 % faster than 6,
                                  // which was +0.3-0.7 % over 0)

@@ -1256,6 +1256,7 @@ __global__ void __launch_bounds__(kBlock)
 // fill: the write-bound twin. Interior chunks are 16-byte stores; the (at most
 // two) edge chunks of a span are written bytewise so neighbouring buffers
 // sharing a 16-byte line are never touched.
+template <bool NTS = false>
 __device__ __forceinline__ void fill_chunk(u32x4* a0, uint32_t c, uint32_t nchunks, uint32_t q0, uint32_t lo,
                                            uint32_t hi_last)
 {
@@ -1265,7 +1266,8 @@ __device__ __forceinline__ void fill_chunk(u32x4* a0, uint32_t c, uint32_t nchun
     const uint32_t b0 = first_c ? lo : 0u;
     const uint32_t b1 = last_c ? hi_last : 16u;
     if (b0 == 0u && b1 == 16u) {
-        __builtin_nontemporal_store(e, a0 + c);
+        if constexpr (NTS) __builtin_nontemporal_store(e, a0 + c);
+        else a0[c] = e;
     } else {
         uint8_t* dst = reinterpret_cast<uint8_t*>(a0 + c);
         for (uint32_t b = b0; b < b1; ++b) dst[b] = (uint8_t)(e[b >> 2] >> (8 * (b & 3)));
@@ -1275,7 +1277,7 @@ __device__ __forceinline__ void fill_chunk(u32x4* a0, uint32_t c, uint32_t nchun
 // A span of whole 16-byte chunks (lo == 0, last chunk full): straight-line rounds of
 // U 16-byte buffer stores per lane, the expected words stepped like the verify
 // stream; the tail round needs no mask (stores past num_records are dropped).
-template <int TEAM, int U, bool EVEN>
+template <int TEAM, int U, bool EVEN, bool NTS>
 __device__ __forceinline__ void fill_whole_rounds(u32x4* p, uint32_t nchunks, uint32_t q0, uint32_t lane)
 {
     const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(p, (short)0, (int)(nchunks * 16u), 0x00020000);
@@ -1286,11 +1288,13 @@ __device__ __forceinline__ void fill_whole_rounds(u32x4* p, uint32_t nchunks, ui
 #pragma unroll
         for (int u = 0; u < U; ++u)
             __builtin_amdgcn_raw_buffer_store_b128(expected_step<TEAM, U, EVEN>(B, u, sh), r,
-                                                   (cb + (uint32_t)(u * TEAM) + lane) * 16u, 0u, 2);  // aux 2 = nt
+                                                   (cb + (uint32_t)(u * TEAM) + lane) * 16u, 0u, NTS ? 2 : 0);
     }
 }
 
-template <int TEAM>
+// NTS: nontemporal stores. Plain stores measured faster for whole 64 KiB buffers (tools/hbm_read_ceiling
+// writes: 5.51-5.60 TB/s plain vs 4.98-5.35 nt on the same slab shape), nontemporal for datagrams.
+template <int TEAM, bool NTS = false>
 __global__ void __launch_bounds__(kBlock) fill_kernel(uint8_t* __restrict__ arena, uint64_t arena_bytes,
                                                       const cts_buf_desc* __restrict__ descs, uint32_t n)
 {
@@ -1311,11 +1315,11 @@ __global__ void __launch_bounds__(kBlock) fill_kernel(uint8_t* __restrict__ aren
         u32x4* p = reinterpret_cast<u32x4*>(sp - lo);
         // (whole-chunk spans stream buffer stores: 32-bit offsets, so spans >= 2 GiB take the pointer loop)
         if (__builtin_amdgcn_readfirstlane((lo == 0u && hi_last == 16u && nchunks < kGiantChunks) ? 1u : 0u)) {
-            if (__builtin_amdgcn_readfirstlane(q0 & 1u) == 0u) fill_whole_rounds<TEAM, FU, true>(p, nchunks, q0, lane);
-            else fill_whole_rounds<TEAM, FU, false>(p, nchunks, q0, lane);
+            if (__builtin_amdgcn_readfirstlane(q0 & 1u) == 0u) fill_whole_rounds<TEAM, FU, true, NTS>(p, nchunks, q0, lane);
+            else fill_whole_rounds<TEAM, FU, false, NTS>(p, nchunks, q0, lane);
             continue;
         }
-        for (uint32_t c = lane; c < nchunks; c += TEAM) fill_chunk(p, c, nchunks, q0, lo, hi_last);
+        for (uint32_t c = lane; c < nchunks; c += TEAM) fill_chunk<NTS>(p, c, nchunks, q0, lo, hi_last);
     }
 }
 
@@ -1651,7 +1655,7 @@ __global__ void __launch_bounds__(kBlock)
         const uint32_t hi_last = (uint32_t)((uint64_t)lo + len - 16ull * (nchunks - 1u));
         const uint32_t q0 = (0u - lo) & 0xFFFFu;
         u32x4* p = reinterpret_cast<u32x4*>(sp - lo);
-        for (uint32_t c = lane; c < nchunks; c += 64u) fill_chunk(p, c, nchunks, q0, lo, hi_last);
+        for (uint32_t c = lane; c < nchunks; c += 64u) fill_chunk<true>(p, c, nchunks, q0, lo, hi_last);
     }
 }
 
@@ -1770,10 +1774,16 @@ hipError_t launch_fill(uint8_t* arena, uint64_t arena_bytes, const cts_buf_desc*
 {
     if (n == 0) return hipSuccess;
     const bool small = max_length_hint != 0 && max_length_hint <= (uint32_t)geo.small_threshold;
-    if (small) {
-        fill_kernel<64><<<grid_for(n, kBlock / 64, geo), kBlock, 0, stream>>>(arena, arena_bytes, descs, n);
+    // store policy: fill_nt 0 = plain, 1 = nontemporal, 2 = by path (plain for the workgroup path:
+    // config 2 48.7 vs 51.1 us; nontemporal for datagrams: 1.46 vs 1.68 ms per 4 M; tools/tune_verify.py --op fill)
+    const bool nts = geo.fill_nt == 2 ? small : geo.fill_nt != 0;
+    const uint32_t sgrid = grid_for(n, kBlock / 64, geo), lgrid = grid_for(n, 1, geo, geo.fill_blocks_per_cu);
+    if (nts) {
+        if (small) fill_kernel<64, true><<<sgrid, kBlock, 0, stream>>>(arena, arena_bytes, descs, n);
+        else fill_kernel<kBlock, true><<<lgrid, kBlock, 0, stream>>>(arena, arena_bytes, descs, n);
     } else {
-        fill_kernel<kBlock><<<grid_for(n, 1, geo, geo.fill_blocks_per_cu), kBlock, 0, stream>>>(arena, arena_bytes, descs, n);
+        if (small) fill_kernel<64><<<sgrid, kBlock, 0, stream>>>(arena, arena_bytes, descs, n);
+        else fill_kernel<kBlock><<<lgrid, kBlock, 0, stream>>>(arena, arena_bytes, descs, n);
     }
     return hipGetLastError();
 }

@@ -122,7 +122,7 @@ int cts_engine_device(const cts_engine* engine);
 /* Launch-geometry attributes (defaults tuned for MI355X; env overrides
  * CTS_BLOCKS_PER_CU / CTS_NT_LOADS / CTS_SMALL_THRESHOLD / CTS_VERIFY_VARIANT /
  * CTS_SMALL_BLOCKS_PER_CU / CTS_SMALL_VARIANT / CTS_FILL_BLOCKS_PER_CU / CTS_MS_VARIANT /
- * CTS_SMALL_CHUNK
+ * CTS_SMALL_CHUNK / CTS_FILL_NT
  * are read at create time). */
 typedef enum cts_engine_attr {
     CTS_ATTR_BLOCKS_PER_CU = 1,   /* grid cap = CUs x this (grid-strides beyond) */
@@ -133,7 +133,8 @@ typedef enum cts_engine_attr {
     CTS_ATTR_SMALL_VARIANT = 6,       /* small-buffer (datagram) kernel variant */
     CTS_ATTR_FILL_BLOCKS_PER_CU = 7,  /* grid cap of the fill kernels */
     CTS_ATTR_MS_VARIANT = 8,          /* MediaStream receive kernel (cts_media_stream_verify) */
-    CTS_ATTR_SMALL_CHUNK = 9          /* chunked small-buffer walk: buffers per chunk (0 = contiguous) */
+    CTS_ATTR_SMALL_CHUNK = 9,         /* chunked small-buffer walk: buffers per chunk (0 = contiguous) */
+    CTS_ATTR_FILL_NT = 10             /* cts_fill stores: 0 plain, 1 nontemporal, 2 by path (default) */
 } cts_engine_attr;
 int cts_engine_set_attr(cts_engine* engine, int attr, int value);
 /* A non-blocking HIP stream on the engine's device, whatever device the calling

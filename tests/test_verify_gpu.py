@@ -174,7 +174,19 @@ def test_misaligned_descriptor_array_is_rejected(engine):
         engine.fill(arena, raw[4:4 + DESC_DTYPE.itemsize], max_length_hint=0)
 
 
-def test_fill_matches_oracle_and_leaves_neighbours(engine):
+@pytest.mark.parametrize("fill_nt", [0, 1, 2])
+def test_fill_matches_oracle_and_leaves_neighbours(engine, fill_nt):
+    from ctstraffic_amd import _lib
+
+    default_nt = engine.get_attr(_lib.ATTR_FILL_NT)
+    engine.set_attr(_lib.ATTR_FILL_NT, fill_nt)
+    try:
+        _fill_vs_oracle(engine)
+    finally:
+        engine.set_attr(_lib.ATTR_FILL_NT, default_nt)
+
+
+def _fill_vs_oracle(engine):
     rng = np.random.default_rng(11)
     # aligned: 16-byte-aligned spans of whole chunks (the fill's straight-line store rounds;
     # a third are 64 KiB, phases odd and even), with 16-byte gaps that must stay untouched

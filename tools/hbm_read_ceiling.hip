@@ -115,8 +115,9 @@ __global__ void __launch_bounds__(256) read_ldsdma(const u32x4* __restrict__ p, 
     if (acc == 0x12345678u) out[0] = acc;
 }
 
-// write reference for the fill kernel: the same slab shape, 16-byte nontemporal stores
-template <int U>
+// write reference for the fill kernel: the same slab shape, 16-byte stores (POL 0 = nontemporal,
+// 1 = plain, 2 = write-through sc1 via an agent-scope relaxed atomic store of each dword)
+template <int U, int POL = 0>
 __global__ void __launch_bounds__(256) write_slab_gs(u32x4* __restrict__ p, uint32_t per_block, uint32_t nslabs)
 {
     for (uint32_t sl = blockIdx.x; sl < nslabs; sl += gridDim.x) {
@@ -125,7 +126,9 @@ __global__ void __launch_bounds__(256) write_slab_gs(u32x4* __restrict__ p, uint
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const uint32_t v = sl + c + (uint32_t)u;
-                __builtin_nontemporal_store(u32x4{v, v + 1u, v + 2u, v + 3u}, q + c + u * 256u);
+                const u32x4 x = u32x4{v, v + 1u, v + 2u, v + 3u};
+                if constexpr (POL == 0) __builtin_nontemporal_store(x, q + c + u * 256u);
+                else q[c + u * 256u] = x;
             }
         }
     }
@@ -212,14 +215,16 @@ int main(int argc, char** argv)
                U, (int)NT, (int)STAG, BPC, ms * 1e3, arena / (ms * 1e-3) / 1e9);                                 \
     } while (0)
 
-#define RUN_WR(U, BPC)                                                                                        \
+#define RUN_WRP(U, BPC, POL)                                                                                  \
     do {                                                                                                      \
         const uint32_t nsl = (uint32_t)(arena / 65536);                                                       \
         const uint32_t grid = (uint32_t)cus * (BPC);                                                          \
-        float ms = time_ms([&](int i) { write_slab_gs<U><<<grid, 256, 0, s>>>(bufs[i % R], 4096u, nsl); }, reps, s); \
-        printf("{\"kind\":\"write_slab_gs\",\"U\":%d,\"nt\":1,\"blocks_per_cu\":%d,\"us\":%.2f,\"GBps\":%.1f}\n", U, \
-               BPC, ms * 1e3, arena / (ms * 1e-3) / 1e9);                                                     \
+        float ms = time_ms([&](int i) { write_slab_gs<U, POL><<<grid, 256, 0, s>>>(bufs[i % R], 4096u, nsl); }, reps, \
+                           s);                                                                                \
+        printf("{\"kind\":\"write_slab_gs\",\"U\":%d,\"nt\":%d,\"blocks_per_cu\":%d,\"us\":%.2f,\"GBps\":%.1f}\n", U, \
+               POL == 0 ? 1 : 0, BPC, ms * 1e3, arena / (ms * 1e-3) / 1e9);                                 \
     } while (0)
+#define RUN_WR(U, BPC) RUN_WRP(U, BPC, 0)
 
 #define RUN_DMA(D, AUX, BPC)                                                                                   \
     do {                                                                                                       \
@@ -250,6 +255,10 @@ int main(int argc, char** argv)
     const bool writes = argc > 5 && atoi(argv[5]) != 0;
     if (writes) {
         for (int pass = 0; pass < 2; ++pass) {
+            RUN_WRP(4, 2, 1);
+            RUN_WRP(4, 4, 1);
+            RUN_WRP(2, 8, 1);
+            RUN_WRP(4, 2, 0);
             RUN_WR(1, 4);
             RUN_WR(2, 4);
             RUN_WR(4, 4);

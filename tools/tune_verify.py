@@ -59,7 +59,8 @@ def main():
             eng.set_attr(_lib.ATTR_BLOCKS_PER_CU, bpc)
             eng.set_attr(_lib.ATTR_FILL_BLOCKS_PER_CU, bpc)
             eng.set_attr(_lib.ATTR_SMALL_BLOCKS_PER_CU, bpc)
-            eng.set_attr(_lib.ATTR_NT_LOADS, nt)
+            # (--op fill: the nt dimension is the fill's store policy)
+            eng.set_attr(_lib.ATTR_FILL_NT if args.op == "fill" else _lib.ATTR_NT_LOADS, nt)
             eng.reset_counters(ctr)
             # region timing: per-launch event pairs add ~2.5 us to every launch on this stack
             ea, eb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
