@@ -1,5 +1,6 @@
 # Build the MI355X engine (gfx950) and the CPU oracle.
-#   make            -> ctstraffic_amd/libcts_engine.so + oracle/libcts_oracle.so
+#   make            -> ctstraffic_amd/libcts_engine.so + oracle/libcts_oracle.so + the C++ device sample
+#                      (ctstraffic_amd/build/device_verify) + the ceiling/ablation tools
 #   make asm        -> ctstraffic_amd/build/cts_kernels-gfx950.s (disassembly for inspection)
 HIPCC     ?= /opt/rocm/bin/hipcc
 ARCH      ?= gfx950
@@ -11,8 +12,13 @@ SRCS      := $(wildcard $(CSRC)/*.hip) $(wildcard $(CSRC)/*.cpp)
 OBJS      := $(patsubst $(CSRC)/%,ctstraffic_amd/build/%.o,$(SRCS))
 
 DEVICE_VERIFY := ctstraffic_amd/build/device_verify
+TOOLS := tools/hbm_read_ceiling tools/verify_ablation
 
-all: $(ENGINE_SO) oracle $(DEVICE_VERIFY)
+all: $(ENGINE_SO) oracle $(DEVICE_VERIFY) $(TOOLS)
+
+# measurement references used by tools/gpu_round.sh (plain streaming read/write ceilings, verify ablation)
+tools/%: tools/%.hip
+	$(HIPCC) --offload-arch=$(ARCH) -O3 $< -o $@
 
 # C++ device-resident sample against the C ABI (run on the GPU box by tests/test_cpp_abi.py)
 $(DEVICE_VERIFY): tests/cpp/device_verify.cpp $(ENGINE_SO) include/cts_engine.h
@@ -34,7 +40,7 @@ asm: $(CSRC)/cts_kernels.hip $(HDRS)
 	$(HIPCC) $(HIPFLAGS) --cuda-device-only -S $< -o ctstraffic_amd/build/cts_kernels-$(ARCH).s
 
 clean:
-	rm -rf ctstraffic_amd/build $(ENGINE_SO)
+	rm -rf ctstraffic_amd/build $(ENGINE_SO) $(TOOLS)
 	$(MAKE) -s -C oracle clean
 
 .PHONY: all oracle asm clean
