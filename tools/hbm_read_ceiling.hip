@@ -7,6 +7,7 @@
 // build: hipcc --offload-arch=gfx950 -O3 tools/hbm_read_ceiling.hip -o tools/hbm_read_ceiling
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -81,6 +82,40 @@ __global__ void __launch_bounds__(256) read_or_slab_gs(const u32x4* __restrict__
             for (int u = 0; u < U; ++u) acc |= d[u][0] ^ d[u][1] ^ d[u][2] ^ d[u][3];
         }
         acc = __syncthreads_or(acc == 0x12345678u) ? 1u : acc;  // verify's per-buffer barrier
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
+// Timeline of the verify-shaped read (grid = BPC x CUs, block b reads 64-KiB slabs b, b + grid, ...):
+// s_memrealtime (100 MHz) stamps per workgroup at start, after each slab, at the end, and the XCC id,
+// to see where a 256 MiB launch's fixed cost goes (ramp-up, uneven finish).
+template <int U>
+__global__ void __launch_bounds__(256) read_slab_timeline(const u32x4* __restrict__ p, uint32_t per_block,
+                                                          uint32_t nslabs, uint64_t* stamps, uint32_t* out)
+{
+    uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    uint32_t acc = 0;
+    const uint32_t rounds = per_block / (256u * U);
+    uint32_t k = 0;
+    for (uint32_t sl = blockIdx.x; sl < nslabs; sl += gridDim.x, ++k) {
+        const u32x4* q = p + (uint64_t)sl * per_block;
+        for (uint32_t r = 0; r < rounds; ++r) {
+            const uint32_t c = r * 256u * U + threadIdx.x;
+            u32x4 d[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) d[u] = __builtin_nontemporal_load(q + c + u * 256u);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc |= d[u][0] ^ d[u][1] ^ d[u][2] ^ d[u][3];
+        }
+        acc = __syncthreads_or(acc == 0x12345678u) ? 1u : acc;
+        if (threadIdx.x == 0 && k < 6) stamps[(uint64_t)blockIdx.x * 8 + 1 + k] = __builtin_amdgcn_s_memrealtime();
+    }
+    if (threadIdx.x == 0) {
+        stamps[(uint64_t)blockIdx.x * 8] = t0;
+        uint32_t xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        stamps[(uint64_t)blockIdx.x * 8 + 7] = (uint64_t)(xcc & 0xFu) | ((uint64_t)k << 8);
     }
     if (acc == 0x12345678u) out[0] = acc;
 }
@@ -168,7 +203,7 @@ int main(int argc, char** argv)
     int cus = 0;
     CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
     // argv: [reps] [arena MiB (256 = one config-2 batch)] [quick: 1 = two configs only] [ramp] [writes: 1 = store sweep]
-    //       [dma: 1 = LDS-DMA sweep]
+    //       [dma: 1 = LDS-DMA sweep] [timeline: 1 = per-workgroup s_memrealtime stamps]
     const size_t arena = (size_t)(argc > 2 ? atoi(argv[2]) : 256) << 20;
     const bool quick = argc > 3 && atoi(argv[3]) != 0;
     const bool ramp = argc > 4 && atoi(argv[4]) != 0;  // arena holds the ctsTraffic pattern
@@ -237,6 +272,44 @@ int main(int argc, char** argv)
                BPC, ms * 1e3, bytes / (ms * 1e-3) / 1e9);                                                       \
     } while (0)
 
+    const bool timeline = argc > 7 && atoi(argv[7]) != 0;
+    if (timeline) {
+        // one timeline per (U, blocks per CU): 3 launches each, the last one's stamps printed as percentiles
+        uint64_t* st;
+        const int maxgrid = cus * 16;
+        CHECK(hipMalloc(&st, (size_t)maxgrid * 8 * sizeof(uint64_t)));
+        const int cfg[][2] = {{4, 4}, {2, 4}, {4, 8}, {4, 2}};
+        for (auto& c : cfg) {
+            const uint32_t grid = (uint32_t)cus * c[1];
+            const uint32_t nsl = (uint32_t)(arena / 65536);
+            for (int rep = 0; rep < 3; ++rep) {
+                CHECK(hipMemsetAsync(st, 0, (size_t)grid * 8 * sizeof(uint64_t), s));
+                if (c[0] == 4) read_slab_timeline<4><<<grid, 256, 0, s>>>(bufs[rep % R], 4096u, nsl, st, out);
+                else read_slab_timeline<2><<<grid, 256, 0, s>>>(bufs[rep % R], 4096u, nsl, st, out);
+                CHECK(hipStreamSynchronize(s));
+            }
+            std::vector<uint64_t> h((size_t)grid * 8);
+            CHECK(hipMemcpy(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost));
+            uint64_t t_min = ~0ull;
+            for (uint32_t b = 0; b < grid; ++b) t_min = h[b * 8] < t_min ? h[b * 8] : t_min;
+            std::vector<double> starts, ends, firsts;
+            for (uint32_t b = 0; b < grid; ++b) {
+                const uint32_t k = (uint32_t)(h[b * 8 + 7] >> 8);
+                starts.push_back((h[b * 8] - t_min) * 0.01);
+                ends.push_back((h[b * 8 + (k < 6 ? k : 6)] - t_min) * 0.01);
+                firsts.push_back((h[b * 8 + 1] - h[b * 8]) * 0.01);
+            }
+            auto pct = [](std::vector<double> v, double q) {
+                std::sort(v.begin(), v.end());
+                return v[(size_t)(q * (v.size() - 1))];
+            };
+            printf("{\"kind\":\"timeline\",\"U\":%d,\"blocks_per_cu\":%d,\"start_us\":[%.2f,%.2f,%.2f],"
+                   "\"first_slab_us\":[%.2f,%.2f,%.2f],\"end_us\":[%.2f,%.2f,%.2f,%.2f,%.2f]}\n",
+                   c[0], c[1], pct(starts, 0), pct(starts, 0.5), pct(starts, 1.0), pct(firsts, 0), pct(firsts, 0.5),
+                   pct(firsts, 1.0), pct(ends, 0), pct(ends, 0.1), pct(ends, 0.5), pct(ends, 0.9), pct(ends, 1.0));
+        }
+        return 0;
+    }
     const bool dma = argc > 6 && atoi(argv[6]) != 0;
     if (dma) {
         for (int pass = 0; pass < 2; ++pass) {
