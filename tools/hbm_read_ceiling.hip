@@ -278,7 +278,7 @@ int main(int argc, char** argv)
         uint64_t* st;
         const int maxgrid = cus * 16;
         CHECK(hipMalloc(&st, (size_t)maxgrid * 8 * sizeof(uint64_t)));
-        const int cfg[][2] = {{4, 4}, {2, 4}, {4, 8}, {4, 2}};
+        const int cfg[][2] = {{4, 4}, {2, 4}};
         for (auto& c : cfg) {
             const uint32_t grid = (uint32_t)cus * c[1];
             const uint32_t nsl = (uint32_t)(arena / 65536);
@@ -304,9 +304,17 @@ int main(int argc, char** argv)
                 return v[(size_t)(q * (v.size() - 1))];
             };
             printf("{\"kind\":\"timeline\",\"U\":%d,\"blocks_per_cu\":%d,\"start_us\":[%.2f,%.2f,%.2f],"
-                   "\"first_slab_us\":[%.2f,%.2f,%.2f],\"end_us\":[%.2f,%.2f,%.2f,%.2f,%.2f]}\n",
+                   "\"first_slab_us\":[%.2f,%.2f,%.2f],\"end_us\":[%.2f,%.2f,%.2f,%.2f,%.2f],\"end_by_xcc\":[",
                    c[0], c[1], pct(starts, 0), pct(starts, 0.5), pct(starts, 1.0), pct(firsts, 0), pct(firsts, 0.5),
                    pct(firsts, 1.0), pct(ends, 0), pct(ends, 0.1), pct(ends, 0.5), pct(ends, 0.9), pct(ends, 1.0));
+            for (uint32_t x = 0; x < 8; ++x) {  // per XCC: min / median / max end
+                std::vector<double> ex;
+                for (uint32_t b = 0; b < grid; ++b)
+                    if ((h[b * 8 + 7] & 0xFu) == x) ex.push_back(ends[b]);
+                if (ex.empty()) continue;
+                printf("%s[%u,%.2f,%.2f,%.2f]", x ? "," : "", x, pct(ex, 0), pct(ex, 0.5), pct(ex, 1.0));
+            }
+            printf("]}\n");
         }
         return 0;
     }
