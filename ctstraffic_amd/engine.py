@@ -70,6 +70,17 @@ def results_from_device(t) -> np.ndarray:
     return t.cpu().numpy().view(RESULT_DTYPE)
 
 
+def _check_outputs(n: int, results, counters) -> None:
+    """The C ABI takes raw device pointers and cannot see their sizes: a results tensor shorter than n records or
+    a counter block shorter than cts_counters_device_bytes() would be written past its end, so refuse them here."""
+    if results is not None and _nbytes(results) < n * RESULT_DTYPE.itemsize:
+        raise ValueError("results holds %d bytes, %d buffers need %d" % (_nbytes(results), n,
+                                                                        n * RESULT_DTYPE.itemsize))
+    if counters is not None and _nbytes(counters) < int(lib().cts_counters_device_bytes()):
+        raise ValueError("counters holds %d bytes, the device block is %d" % (_nbytes(counters),
+                                                                             int(lib().cts_counters_device_bytes())))
+
+
 class Engine:
     """One engine per GPU (cts_engine_create). Thread-safe across streams."""
 
@@ -125,6 +136,7 @@ class Engine:
                conn_first_fail=None, stream=None) -> None:
         n = _nbytes(descs) // DESC_DTYPE.itemsize
         n_conns = 0 if conn_first_fail is None else _nbytes(conn_first_fail) // 4
+        _check_outputs(n, results, counters)
         check("cts_verify", lib().cts_verify(self._h, _ptr(arena), _nbytes(arena), _ptr(descs), n, max_length_hint,
                                              _ptr(results), _ptr(counters), _ptr(conn_first_fail), n_conns,
                                              _stream(stream)))
@@ -161,6 +173,7 @@ class Engine:
                    counters=None, stream=None) -> None:
         """cts_verify on a raw device address (e.g. the device view of a pinned host arena)."""
         n = _nbytes(descs) // DESC_DTYPE.itemsize
+        _check_outputs(n, results, counters)
         check("cts_verify", lib().cts_verify(self._h, arena_ptr, arena_bytes, _ptr(descs), n, max_length_hint,
                                              _ptr(results), _ptr(counters), None, 0, _stream(stream)))
 

@@ -90,9 +90,13 @@ def fill(engine, arena, descs, headers, stream=None) -> None:
 
 
 def verify(engine, arena, descs, records=None, results=None, counters=None, stream=None) -> None:
-    from .engine import _nbytes, _stream
+    from .engine import _check_outputs, _nbytes, _stream
 
     n = _nbytes(descs) // DESC_DTYPE.itemsize
+    _check_outputs(n, results, counters)
+    if records is not None and _nbytes(records) < n * DGRAM_RECORD_DTYPE.itemsize:
+        raise ValueError("records holds %d bytes, %d datagrams need %d" % (_nbytes(records), n,
+                                                                          n * DGRAM_RECORD_DTYPE.itemsize))
     check("cts_media_stream_verify",
           lib().cts_media_stream_verify(engine._h, _ptr(arena), _nbytes(arena), _ptr(descs), n, _ptr(records),
                                         _ptr(results), _ptr(counters), _stream(stream)))

@@ -221,3 +221,18 @@ def test_engine_stream_create_rejects_null():
     s = ctypes.c_void_p()
     assert _lib.lib().cts_engine_stream_create(None, ctypes.byref(s)) == _lib.CTS_E_INVALID
     assert _lib.lib().cts_engine_stream_destroy(None, None) == _lib.CTS_E_INVALID
+
+
+def test_python_handle_refuses_short_output_buffers():
+    """The ABI cannot see buffer sizes; the Python handle checks them before any launch (no device needed)."""
+    import numpy as np
+    import pytest
+
+    from ctstraffic_amd import engine as E
+    from ctstraffic_amd.types import RESULT_DTYPE
+
+    with pytest.raises(ValueError):
+        E._check_outputs(10, np.zeros(9 * RESULT_DTYPE.itemsize, np.uint8), None)
+    with pytest.raises(ValueError):
+        E._check_outputs(1, None, np.zeros(8, np.uint8))
+    E._check_outputs(10, np.zeros(10 * RESULT_DTYPE.itemsize, np.uint8), np.zeros(64 * 64, np.uint8))
