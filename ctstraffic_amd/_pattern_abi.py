@@ -115,6 +115,7 @@ def declare(L: ctypes.CDLL) -> None:
         "cts_io_pattern_initiate_io": ([P, ctypes.POINTER(CtsTask)], i32),
         "cts_io_pattern_complete_io": ([P, ctypes.POINTER(CtsTask), u32, u32], i32),
         "cts_io_pattern_last_error": ([P], u32),
+        "cts_io_pattern_set_ideal_send_backlog": ([P, u32], i32),
         "cts_io_pattern_flush": ([P], i32),
         "cts_io_pattern_get_stats": ([P, ctypes.POINTER(CtsPatternStats)], i32),
         "cts_io_pattern_failure_message": ([P, ctypes.c_char_p, u32], i32),

@@ -84,6 +84,7 @@ public:
     uint64_t GetMaxTransfer() const { return m_maxTransfer; }
     void SetMaxTransfer(uint64_t v) { m_maxTransfer = v; }
     uint32_t GetIdealSendBacklog() const { return m_idealSendBacklog; }
+    void SetIdealSendBacklog(uint32_t isb) { m_idealSendBacklog = isb; }  // ctsIOPatternState.hpp:155-158
     bool IsCompleted() const { return m_internal == Internal::CompletedTransfer || m_internal == Internal::ErrorIoFailed; }
     bool IsCurrentStateMoreIo() const { return m_internal == Internal::MoreIo; }
 
@@ -1071,6 +1072,13 @@ int cts_io_pattern_complete_io(cts_io_pattern* p, const cts_task* t, uint32_t cu
 }
 
 uint32_t cts_io_pattern_last_error(const cts_io_pattern* p) { return p ? p->m_lastError : CTS_STATUS_IO_RUNNING; }
+
+int cts_io_pattern_set_ideal_send_backlog(cts_io_pattern* p, uint32_t bytes)
+{
+    if (p == nullptr) return CTS_E_INVALID;
+    p->state.SetIdealSendBacklog(bytes);
+    return CTS_OK;
+}
 
 int cts_io_pattern_flush(cts_io_pattern* p)
 {

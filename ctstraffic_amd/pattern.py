@@ -128,6 +128,9 @@ class IoPattern:
     def GetLastPatternError(self) -> int:
         return int(lib().cts_io_pattern_last_error(self._h))
 
+    def SetIdealSendBacklog(self, isb: int) -> None:
+        check("cts_io_pattern_set_ideal_send_backlog", lib().cts_io_pattern_set_ideal_send_backlog(self._h, isb))
+
     def Flush(self) -> int:
         rc = lib().cts_io_pattern_flush(self._h)
         if rc < 0:

@@ -194,6 +194,10 @@ int cts_io_pattern_initiate_io(cts_io_pattern* pattern, cts_task* out_task);
 int cts_io_pattern_complete_io(cts_io_pattern* pattern, const cts_task* task, uint32_t current_transfer,
                                uint32_t status_code);
 uint32_t cts_io_pattern_last_error(const cts_io_pattern* pattern);
+/* ctsIoPattern::SetIdealSendBacklog (ctsIOPattern.h:109-112): the socket's ideal send backlog
+ * (SIO_IDEAL_SEND_BACKLOG_QUERY, ctsSocket.cpp:249) bounds the bytes of sends in flight when
+ * pre_post_sends == 0. */
+int cts_io_pattern_set_ideal_send_backlog(cts_io_pattern* pattern, uint32_t bytes);
 /* DEFERRED mode: verify every queued buffer now (one kernel launch) and apply
  * the outcome as the reference would have at the first failing completion:
  * latch CTS_STATUS_ERROR_DATA_DID_NOT_MATCH_BIT_PATTERN and record its offset,

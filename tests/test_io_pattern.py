@@ -300,6 +300,254 @@ def test_PullClient_VerifyingBuffersNotUsingSharedBuffer_SmallRecvs(make, shutdo
     assert p.stats()["buffers_verified"] == 10
 
 
+def _client_to_status(p):
+    """Connection id in, the 10-byte send out, then the server's 4-byte status recv (the common prefix of the
+    client base-class tests, ctsIOPatternUnitTest_Client.cpp:360-760)."""
+    t = p.InitiateIo()
+    assert (t.buffer_length, t.io_action) == (ConnectionIdLength, Recv)
+    assert p.CompleteIo(t, ConnectionIdLength, 0) == ContinueIo
+    t = p.InitiateIo()
+    assert (t.buffer_length, t.io_action) == (10, Send)
+    assert p.CompleteIo(t, 10, 0) == ContinueIo
+    t = p.InitiateIo()
+    assert (t.io_action, t.buffer_length) == (Recv, g_TestBufferLength)
+    return t
+
+
+def test_TestBaseClass_SuccessfulMultipleSends(make):  # Client :315-358
+    p = make(**client_defaults(pre_post_sends=2, buffer_size=10, transfer_size=20))
+    t = p.InitiateIo()
+    assert (t.buffer_length, t.io_action) == (ConnectionIdLength, Recv)
+    assert p.CompleteIo(t, ConnectionIdLength, 0) == ContinueIo
+    t1 = p.InitiateIo()
+    t2 = p.InitiateIo()  # two sends in flight (PrePostSends = 2)
+    assert (t1.buffer_length, t1.io_action, t2.buffer_length, t2.io_action) == (10, Send, 10, Send)
+    assert t2.buffer_offset == t1.buffer_offset + 10  # m_sendPatternOffset advances per created task (:695-697)
+    assert p.CompleteIo(t1, 10, 0) == ContinueIo
+    assert p.CompleteIo(t2, 10, 0) == ContinueIo
+    t = p.InitiateIo()
+    assert (t.io_action, t.buffer_length) == (Recv, g_TestBufferLength)
+    assert p.CompleteIo(t, 4, 0) == ContinueIo
+    t = p.InitiateIo()
+    assert t.io_action == A.TASK_GRACEFUL_SHUTDOWN
+    assert p.CompleteIo(t, 0, 0) == ContinueIo
+    t = p.InitiateIo()
+    assert t.io_action == Recv
+    assert p.CompleteIo(t, 0, 0) == CompletedIo
+
+
+def test_TestBaseClass_SuccessfulSend_HardShutdown(make):  # Client :360-387
+    p = make(**client_defaults(tcp_shutdown=A.SHUTDOWN_HARD))
+    t = _client_to_status(p)
+    assert p.CompleteIo(t, 4, 0) == ContinueIo
+    t = p.InitiateIo()
+    assert t.io_action == A.TASK_HARD_SHUTDOWN
+    assert p.CompleteIo(t, 0, 0) == CompletedIo
+
+
+@pytest.mark.parametrize("transferred,status", [(0, 0), (0, 1)], ids=["NoBytes", "Failed"])
+def test_TestBaseClass_ServerStatusRecv(make, transferred, status):
+    """ReceivedNoBytesWithServerStatus (Client :389-410) and FailedReceivingServerStatus (:412-433)."""
+    p = make(**client_defaults())
+    t = _client_to_status(p)
+    assert p.CompleteIo(t, transferred, status) == FailedIo
+    if status:
+        assert p.GetLastPatternError() == status
+
+
+def test_TestBaseClass_FailSend(make):  # Client :435-451
+    p = make(**client_defaults())
+    t = p.InitiateIo()
+    assert p.CompleteIo(t, ConnectionIdLength, 0) == ContinueIo
+    t = p.InitiateIo()
+    assert (t.buffer_length, t.io_action) == (10, Send)
+    assert p.CompleteIo(t, 10, 1) == FailedIo
+    assert p.GetLastPatternError() == 1
+
+
+def test_TestBaseClass_FailMultipleSends(make):  # Client :453-480
+    p = make(**client_defaults(pre_post_sends=2, buffer_size=10, transfer_size=20))
+    t = p.InitiateIo()
+    assert p.CompleteIo(t, ConnectionIdLength, 0) == ContinueIo
+    t1, t2 = p.InitiateIo(), p.InitiateIo()
+    assert (t1.io_action, t2.io_action) == (Send, Send)
+    assert p.CompleteIo(t1, 10, 1) == FailedIo
+    assert p.GetLastPatternError() == 1
+    assert p.CompleteIo(t2, 10, 1) == FailedIo
+    assert p.GetLastPatternError() == 1
+
+
+@pytest.mark.parametrize("shutdown", [A.SHUTDOWN_GRACEFUL, A.SHUTDOWN_HARD], ids=["Graceful", "Hard"])
+def test_TestBaseClass_FailShutdown(make, shutdown):
+    """FailGracefulShutdownAfterSend/-AFterRecv (Client :494-520, :554-580) and FailHardShutdownAfterSend/-AFterRecv
+    (:524-550, :584-610): the shutdown task completes with an error."""
+    p = make(**client_defaults(tcp_shutdown=shutdown))
+    t = _client_to_status(p)
+    assert p.CompleteIo(t, 4, 0) == ContinueIo
+    t = p.InitiateIo()
+    assert t.io_action == (A.TASK_GRACEFUL_SHUTDOWN if shutdown == A.SHUTDOWN_GRACEFUL else A.TASK_HARD_SHUTDOWN)
+    assert p.CompleteIo(t, 0, 1) == FailedIo
+    assert p.GetLastPatternError() == 1
+
+
+@pytest.mark.parametrize("transferred,status,err", [(0, 1, 1), (1, 0, A.STATUS_ERROR_TOO_MUCH_DATA_TRANSFERRED)],
+                         ids=["FailFIN", "TooManyBytesOnFIN"])
+def test_TestClientBaseClass_FinalFin(make, transferred, status, err):
+    """FailFINAfterSend / FailFINAfterRecv (Client :614-684) and TooManyBytesOnFINAfterSend / -AfterRecv (:686-760):
+    the recv that waits for the server's FIN fails, or returns data."""
+    p = make(**client_defaults())
+    t = _client_to_status(p)
+    assert p.CompleteIo(t, 4, 0) == ContinueIo
+    t = p.InitiateIo()
+    assert t.io_action == A.TASK_GRACEFUL_SHUTDOWN
+    assert p.CompleteIo(t, 0, 0) == ContinueIo
+    t = p.InitiateIo()
+    assert t.io_action == Recv
+    assert p.CompleteIo(t, transferred, status) == FailedIo
+    assert p.GetLastPatternError() == err
+
+
+def _client_finish(p, shutdown=A.SHUTDOWN_GRACEFUL):
+    """Server status in, then the client's shutdown (graceful: FIN + wait for the server's FIN; rude: RST)."""
+    t = p.InitiateIo()
+    assert (t.io_action, t.buffer_length) == (Recv, g_TestBufferLength)
+    assert p.CompleteIo(t, 4, 0) == ContinueIo
+    t = p.InitiateIo()
+    if shutdown == A.SHUTDOWN_GRACEFUL:
+        assert t.io_action == A.TASK_GRACEFUL_SHUTDOWN
+        assert p.CompleteIo(t, 0, 0) == ContinueIo
+        t = p.InitiateIo()
+        assert t.io_action == Recv
+        assert p.CompleteIo(t, 0, 0) == CompletedIo
+    else:
+        assert t.io_action == A.TASK_HARD_SHUTDOWN
+        assert p.CompleteIo(t, 0, 0) == CompletedIo
+
+
+_CLIENT_VARIANTS = [pytest.param(False, False, id="NotVerifyingBuffersNotUsingSharedBuffer"),
+                    pytest.param(True, False, id="VerifyingBuffersNotUsingSharedBuffer"),
+                    pytest.param(False, True, id="NotVerifyingBuffersUsingSharedBuffer")]
+
+
+@pytest.mark.parametrize("shutdown", [A.SHUTDOWN_GRACEFUL, A.SHUTDOWN_HARD], ids=["Graceful", "Rude"])
+@pytest.mark.parametrize("verify,shared", _CLIENT_VARIANTS)
+def test_PushClient(make, verify, shared, shutdown):
+    """PushClient_{Not,}VerifyingBuffers{Not,}UsingSharedBuffer_{Graceful,Rude} (Client :765-1036): ten 1024-byte
+    sends out of g_senderSharedBuffer at the advancing send offset, then status and shutdown."""
+    p = make(**client_defaults(buffer_size=1024, transfer_size=10240, verify_buffers=verify, use_shared_buffer=shared,
+                               tcp_shutdown=shutdown))
+    t = p.InitiateIo()
+    assert (t.buffer_length, t.io_action) == (ConnectionIdLength, Recv)
+    assert p.CompleteIo(t, ConnectionIdLength, 0) == ContinueIo
+    base = IoPattern.AccessSharedBuffer()
+    for i in range(10):
+        t = p.InitiateIo()
+        assert (t.buffer_length, t.io_action) == (1024, Send)
+        assert t.buffer == base and t.buffer_offset == 1024 * i
+        assert p.CompleteIo(t, 1024, 0) == ContinueIo
+    _client_finish(p, shutdown)
+    assert p.stats()["bytes_sent"] == 10240
+
+
+@pytest.mark.parametrize("shutdown", [A.SHUTDOWN_GRACEFUL, A.SHUTDOWN_HARD], ids=["Graceful", "Rude"])
+@pytest.mark.parametrize("verify,shared", _CLIENT_VARIANTS)
+def test_PullClient(make, verify, shared, shutdown):
+    """PullClient_{Not,}VerifyingBuffers{Not,}UsingSharedBuffer_{Graceful,Rude} (Client :1359-1452, :1567-1660,
+    :1775-1870): ten 1024-byte recvs; verified at expected offsets 0, 1024, ... when verifying, garbage accepted
+    (and the offset left at 0) when not."""
+    p = make(**client_defaults(io_pattern=A.PATTERN_PULL, buffer_size=1024, transfer_size=10240, verify_buffers=verify,
+                               use_shared_buffer=shared, tcp_shutdown=shutdown))
+    t = p.InitiateIo()
+    assert (t.buffer_length, t.io_action) == (ConnectionIdLength, Recv)
+    assert p.CompleteIo(t, ConnectionIdLength, 0) == ContinueIo
+    for i in range(10):
+        t = p.InitiateIo()
+        # m_recvPatternOffset advances only inside the verify gate (ctsIOPattern.cpp:475-493)
+        assert (t.buffer_length, t.io_action, t.expected_pattern_offset) == (1024, Recv, 1024 * i if verify else 0)
+        recv_correct(t) if verify else zero(t)
+        assert p.CompleteIo(t, 1024, 0) == ContinueIo
+    _client_finish(p, shutdown)
+    s = p.stats()
+    # per-connection statistics count the pattern's own IO only; the status message goes to TcpStatusDetails
+    # (ctsIOPattern.cpp:505-520)
+    assert s["bytes_recv"] == 10240 and s["buffers_verified"] == (10 if verify else 0)
+
+
+@pytest.mark.parametrize("shutdown", [A.SHUTDOWN_GRACEFUL, A.SHUTDOWN_HARD], ids=["Graceful", "Rude"])
+def test_PullClient_NotVerifyingBuffersNotUsingSharedBuffer_SmallRecvs(make, shutdown):  # Client :1454-1565
+    p = make(**client_defaults(io_pattern=A.PATTERN_PULL, buffer_size=2048, transfer_size=10240, verify_buffers=False,
+                               tcp_shutdown=shutdown))
+    t = p.InitiateIo()
+    assert p.CompleteIo(t, ConnectionIdLength, 0) == ContinueIo
+    for _ in range(9):
+        t = p.InitiateIo()
+        assert (t.buffer_length, t.io_action) == (2048, Recv)
+        assert p.CompleteIo(t, 1024, 0) == ContinueIo
+    t = p.InitiateIo()
+    assert (t.buffer_length, t.io_action) == (1024, Recv)
+    assert p.CompleteIo(t, 1024, 0) == ContinueIo
+    _client_finish(p, shutdown)
+
+
+# ideal send backlog (SetIdealSendBacklog, PrePostSends = 0): Client :1038-1357
+def _isb_client(make, isb):
+    p = make(**client_defaults(buffer_size=1024, transfer_size=10240, verify_buffers=False, pre_post_sends=0))
+    p.SetIdealSendBacklog(isb)
+    t = p.InitiateIo()
+    assert (t.buffer_length, t.io_action) == (ConnectionIdLength, Recv)
+    assert p.CompleteIo(t, ConnectionIdLength, 0) == ContinueIo
+    return p
+
+
+@pytest.mark.parametrize("isb", [2048, 2047], ids=["MultipleSendsWithISBEnabled", "OffsetFromBufferSize"])
+def test_PushClient_MultipleSendsWithISB(make, isb):  # Client :1038-1098, :1290-1357
+    p = _isb_client(make, isb)
+    for _ in range(5):  # two sends in flight, then nothing until one completes
+        t1, t2 = p.InitiateIo(), p.InitiateIo()
+        assert (t1.buffer_length, t1.io_action, t2.buffer_length, t2.io_action) == (1024, Send, 1024, Send)
+        t3 = p.InitiateIo()
+        assert (t3.buffer_length, t3.io_action) == (0, NoneAction)
+        assert p.CompleteIo(t1, 1024, 0) == ContinueIo
+        assert p.CompleteIo(t2, 1024, 0) == ContinueIo
+    _client_finish(p)
+
+
+def test_PushClient_MultipleSendsWithISBEnabledInterleaving(make):  # Client :1100-1161
+    p = _isb_client(make, 2048)
+    first = p.InitiateIo()
+    assert (first.buffer_length, first.io_action) == (1024, Send)
+    for _ in range(1, 10):
+        t = p.InitiateIo()
+        assert (t.buffer_length, t.io_action) == (1024, Send)
+        assert p.InitiateIo().io_action == NoneAction
+        assert p.CompleteIo(t, 1024, 0) == ContinueIo
+    assert p.CompleteIo(first, 1024, 0) == ContinueIo
+    _client_finish(p)
+
+
+def test_PushClient_LargeNumberOfSendsWithISBEnabled(make):  # Client :1163-1232
+    p = _isb_client(make, 10240)
+    pended = [p.InitiateIo() for _ in range(10)]
+    assert all((t.buffer_length, t.io_action) == (1024, Send) for t in pended)
+    assert p.InitiateIo().io_action == NoneAction
+    for i, t in enumerate(pended):
+        assert p.CompleteIo(t, 1024, 0) == ContinueIo
+        if i < 9:
+            assert p.InitiateIo().io_action == NoneAction
+    _client_finish(p)
+
+
+def test_PushClient_OneSendInFlightWithISBEnabledWhenISBIsSmallerThanBufferSize(make):  # Client :1234-1288
+    p = _isb_client(make, 512)
+    for _ in range(10):
+        t = p.InitiateIo()
+        assert (t.buffer_length, t.io_action) == (1024, Send)
+        t2 = p.InitiateIo()
+        assert (t2.buffer_length, t2.io_action) == (0, NoneAction)
+        assert p.CompleteIo(t, 1024, 0) == ContinueIo
+    _client_finish(p)
+
+
 def test_TestBaseClass_FailReceivingConnectionId(make):  # Client :482-492
     p = make(**client_defaults())
     t = p.InitiateIo()
