@@ -9,7 +9,8 @@ Each scenario runs against four backends:
   gpu-sync / gpu-deferred : VerifyBuffer on the gfx950 verify kernel (zero-copy
                             over the pattern's pinned recv buffers), sender
                             buffer written by the gfx950 fill kernel.
-Assertions follow the reference tests line by line (file:line cited per test).
+Assertions follow the reference tests line by line (file:line cited per test); all 101 TEST_METHODs of
+the three MSTest projects are replayed (identical flows folded into parametrized cases).
 """
 import ctypes
 
@@ -146,7 +147,8 @@ def test_TestServerBaseClass_FailFINAfterRecv(make):  # :344-377
     assert p.GetLastPatternError() == 1
 
 
-def test_TestServerBaseClass_TooManyBytesOnFINAfterRecv(make):  # :414-447
+@pytest.mark.parametrize("case", ["AfterSend", "AfterRecv"])
+def test_TestServerBaseClass_TooManyBytesOnFIN(make, case):  # :379-412 (AfterSend), :414-447 (AfterRecv)
     p = make(**server_defaults())
     t = _server_to_fin(p)
     assert p.CompleteIo(t, 1, 0) == FailedIo
@@ -230,6 +232,35 @@ def test_PushServer_NotVerifyingBuffersUsingSharedBuffer(make):  # :742-808
         assert p.CompleteIo(t, 1024, 0) == ContinueIo
     _server_finish(p)
     assert p.stats()["buffers_verified"] == 0
+
+
+@pytest.mark.parametrize("post,complete", [(1024, 1024), (2048, 1024)], ids=["", "SmallRecvs"])
+def test_PushServer_NotVerifyingBuffersNotUsingSharedBuffer(make, post, complete):  # :476-607
+    p = make(**server_defaults(buffer_size=post, transfer_size=1024 * 10, verify_buffers=False))
+    t = p.InitiateIo()
+    assert p.CompleteIo(t, ConnectionIdLength, 0) == ContinueIo
+    for i in range(10):
+        t = p.InitiateIo()
+        # the last small recv is capped to the 1024 bytes left
+        assert (t.buffer_length, t.io_action) == (post if (post == complete or i < 9) else 1024, Recv)
+        zero(t)  # not verifying: any bytes are accepted
+        assert p.CompleteIo(t, complete, 0) == ContinueIo
+    _server_finish(p)
+    assert p.stats()["buffers_verified"] == 0 and p.stats()["bytes_recv"] == 10240
+
+
+@pytest.mark.parametrize("shared", [False, True], ids=["NotUsingSharedBuffer", "UsingSharedBuffer"])
+def test_PullServer_NotVerifyingBuffers(make, shared):  # :810-866, :926-990
+    p = make(**server_defaults(io_pattern=A.PATTERN_PULL, buffer_size=1024, transfer_size=1024 * 10,
+                               verify_buffers=False, use_shared_buffer=shared))
+    t = p.InitiateIo()
+    assert p.CompleteIo(t, ConnectionIdLength, 0) == ContinueIo
+    for i in range(10):
+        t = p.InitiateIo()
+        assert (t.buffer_length, t.io_action, t.buffer_offset) == (1024, Send, 1024 * i)
+        assert p.CompleteIo(t, 1024, 0) == ContinueIo
+    _server_finish(p)
+    assert p.stats()["bytes_sent"] == 10240
 
 
 def test_PullServer_VerifyingBuffersNotUsingSharedBuffer(make):  # :868-924
@@ -679,6 +710,325 @@ def test_Duplex_Client_CorruptedRecv(make):
     s = p.stats()
     assert (s["fail_offset"], s["fail_expected"], s["fail_actual"]) == (7, 0, 0xFF)
     assert "'0x0' didn't match '0xffffffff'" in p.failure_message()  # char through %x sign-extends
+
+
+WSAECONNABORTED, WSAETIMEDOUT = 10053, 10060
+
+
+def _duplex_data_phase(p, server, send_last):  # :318-336 CompleteDataPhase
+    _complete_connection_id(p, server)
+    r, s = _pended_data_tasks(p)
+    if send_last:
+        assert _complete_data_recv(p, r, 10) == ContinueIo
+        assert p.CompleteIo(s, 10, 0) == ContinueIo
+    else:
+        assert p.CompleteIo(s, 10, 0) == ContinueIo
+        assert _complete_data_recv(p, r, 10) == ContinueIo
+
+
+def _duplex_client_to_fin(p):  # :341-354 DriveClientToFinRecv
+    t = p.InitiateIo()
+    assert t.io_action == Recv
+    IoPattern.write_task_buffer(t, b"DONE", 0)
+    assert p.CompleteIo(t, 4, 0) == ContinueIo
+    t = p.InitiateIo()
+    assert t.io_action == A.TASK_GRACEFUL_SHUTDOWN
+    assert p.CompleteIo(t, 0, 0) == ContinueIo
+    t = p.InitiateIo()
+    assert t.io_action == Recv
+    return t
+
+
+def _duplex_server_to_fin(p):  # :358-367 DriveServerToFinRecv
+    t = p.InitiateIo()
+    assert t.io_action == Send
+    assert p.CompleteIo(t, 4, 0) == ContinueIo
+    t = p.InitiateIo()
+    assert t.io_action == Recv
+    return t
+
+
+@pytest.mark.parametrize("server", [False, True], ids=["Client", "Server"])
+def test_Duplex_FailConnectionId(make, server):  # :657-681
+    p = make(**duplex_defaults(server))
+    t = p.InitiateIo()
+    assert (t.buffer_length, t.io_action) == (ConnectionIdLength, Send if server else Recv)
+    assert p.CompleteIo(t, 0, 1) == FailedIo
+    assert p.GetLastPatternError() == 1
+
+
+def test_Duplex_Client_FailDataSend(make):  # :683-698 (the recv is still outstanding)
+    p = make(**duplex_defaults(False))
+    _complete_connection_id(p, False)
+    r, s = _pended_data_tasks(p)
+    assert p.CompleteIo(s, 0, 1) == FailedIo
+    assert p.GetLastPatternError() == 1
+
+
+def test_Duplex_Client_PrematureFinDuringTransfer(make):  # :717-737
+    p = make(**duplex_defaults(False))
+    _complete_connection_id(p, False)
+    r, s = _pended_data_tasks(p)
+    assert p.CompleteIo(s, 10, 0) == ContinueIo
+    assert p.CompleteIo(r, 0, 0) == FailedIo  # a FIN before the expected data
+    assert p.GetLastPatternError() == A.STATUS_ERROR_NOT_ALL_DATA_TRANSFERRED
+
+
+def test_Duplex_Client_ExtraBytesWhenExpectingFin(make):  # :739-769
+    p = make(**duplex_defaults(False))
+    _duplex_data_phase(p, False, send_last=True)
+    t = _duplex_client_to_fin(p)
+    assert p.CompleteIo(t, 1, 0) == FailedIo
+    assert p.GetLastPatternError() == A.STATUS_ERROR_TOO_MUCH_DATA_TRANSFERRED
+
+
+def test_Duplex_Client_FailReceivingServerCompletion(make):  # :771-790
+    p = make(**duplex_defaults(False))
+    _duplex_data_phase(p, False, send_last=True)
+    t = p.InitiateIo()
+    assert t.io_action == Recv
+    assert p.CompleteIo(t, 0, 1) == FailedIo
+    assert p.GetLastPatternError() == 1
+
+
+@pytest.mark.parametrize("hard", [False, True], ids=["FailGracefulShutdown", "HardShutdown_Fails"])
+def test_Duplex_Client_ShutdownFails(make, hard):  # :792-816, :1000-1021
+    p = make(**duplex_defaults(False, tcp_shutdown=A.SHUTDOWN_HARD if hard else A.SHUTDOWN_GRACEFUL))
+    _duplex_data_phase(p, False, send_last=not hard)
+    t = p.InitiateIo()
+    assert t.io_action == Recv
+    IoPattern.write_task_buffer(t, b"DONE", 0)
+    assert p.CompleteIo(t, 4, 0) == ContinueIo
+    t = p.InitiateIo()
+    assert t.io_action == (A.TASK_HARD_SHUTDOWN if hard else A.TASK_GRACEFUL_SHUTDOWN)
+    assert p.CompleteIo(t, 0, 1) == FailedIo
+    assert p.GetLastPatternError() == 1
+
+
+@pytest.mark.parametrize("status,completed,err", [(WSAECONNRESET, FailedIo, WSAECONNRESET),
+                                                  (WSAECONNABORTED, FailedIo, WSAECONNABORTED),
+                                                  (WSAETIMEDOUT, FailedIo, WSAETIMEDOUT), (0, CompletedIo, 0)],
+                         ids=["FailFinWithRst", "FailFinWithConnAborted", "FailFinWithTimeout", "CleanFin_RecvLast"])
+def test_Duplex_Client_FinStatus(make, status, completed, err):  # :818-850, :1060-1099: the client tolerates none
+    p = make(**duplex_defaults(False))
+    _duplex_data_phase(p, False, send_last=False)
+    t = _duplex_client_to_fin(p)
+    assert p.CompleteIo(t, 0, status) == completed
+    assert p.GetLastPatternError() == err
+
+
+@pytest.mark.parametrize("server,status", [(False, 1), (False, WSAECONNRESET), (True, 1)],
+                         ids=["Client_SendLast_SendFails", "Client_SendLast_SendRst", "Server_SendLast_SendFails"])
+def test_Duplex_SendLast_Fails(make, server, status):  # :852-906
+    p = make(**duplex_defaults(server))
+    _complete_connection_id(p, server)
+    r, s = _pended_data_tasks(p)
+    assert _complete_data_recv(p, r, 10) == ContinueIo
+    assert p.CompleteIo(s, 0, status) == FailedIo
+    assert p.GetLastPatternError() == status
+
+
+@pytest.mark.parametrize("server,status", [(False, 1), (False, WSAECONNRESET), (True, 1)],
+                         ids=["Client_RecvLast_RecvFails", "Client_RecvLast_RecvRst", "Server_RecvLast_RecvFails"])
+def test_Duplex_RecvLast_Fails(make, server, status):  # :908-941, :968-987
+    p = make(**duplex_defaults(server))
+    _complete_connection_id(p, server)
+    r, s = _pended_data_tasks(p)
+    assert p.CompleteIo(s, 10, 0) == ContinueIo
+    assert p.CompleteIo(r, 0, status) == FailedIo
+    assert p.GetLastPatternError() == status
+
+
+def test_Duplex_Client_RecvLast_PartialThenComplete(make):  # :943-966
+    p = make(**duplex_defaults(False))
+    _complete_connection_id(p, False)
+    r, s = _pended_data_tasks(p)
+    assert p.CompleteIo(s, 10, 0) == ContinueIo
+    assert _complete_data_recv(p, r, 4) == ContinueIo
+    rr = p.InitiateIo()
+    assert (rr.io_action, rr.buffer_length, rr.expected_pattern_offset) == (Recv, 6, 4)
+    assert _complete_data_recv(p, rr, 6) == ContinueIo
+    _successful_shutdown(p, False)
+    assert p.GetLastPatternError() == 0 and p.stats()["buffers_verified"] == 2
+
+
+def test_Duplex_Client_HardShutdown_SendLast(make):  # :989-998
+    p = make(**duplex_defaults(False, tcp_shutdown=A.SHUTDOWN_HARD))
+    _duplex_data_phase(p, False, send_last=True)
+    _successful_shutdown(p, False, hard=True)
+    assert p.GetLastPatternError() == 0
+
+
+@pytest.mark.parametrize("n,content", [(2, b"DONE"), (4, b"FAIL")], ids=["CompletionTooFewBytes",
+                                                                          "CompletionWrongContent"])
+def test_Duplex_Client_BadCompletion(make, n, content):  # :1023-1058
+    p = make(**duplex_defaults(False))
+    _duplex_data_phase(p, False, send_last=True)
+    t = p.InitiateIo()
+    assert (t.io_action, t.buffer_length) == (Recv, 4)
+    IoPattern.write_task_buffer(t, content, 0)
+    assert p.CompleteIo(t, n, 0) == FailedIo
+    assert p.GetLastPatternError() == A.STATUS_ERROR_NOT_ALL_DATA_TRANSFERRED
+
+
+@pytest.mark.parametrize("send_last,status,completed,err",
+                         [(False, WSAETIMEDOUT, CompletedIo, 0), (True, WSAECONNABORTED, CompletedIo, 0),
+                          (False, 1, FailedIo, 1)],
+                         ids=["TolerateTimeoutAwaitingFin", "TolerateConnAbortedAwaitingFin", "FailFinWithError"])
+def test_Duplex_Server_FinStatus(make, send_last, status, completed, err):  # :1101-1136
+    p = make(**duplex_defaults(True))
+    _duplex_data_phase(p, True, send_last)
+    t = _duplex_server_to_fin(p)
+    assert p.CompleteIo(t, 0, status) == completed
+    assert p.GetLastPatternError() == err
+
+
+def test_Duplex_Server_ExtraBytesWhenExpectingFin(make):  # :1138-1148
+    p = make(**duplex_defaults(True))
+    _duplex_data_phase(p, True, send_last=True)
+    t = _duplex_server_to_fin(p)
+    assert p.CompleteIo(t, 1, 0) == FailedIo
+    assert p.GetLastPatternError() == A.STATUS_ERROR_TOO_MUCH_DATA_TRANSFERRED
+
+
+def test_Duplex_Server_FailSendingCompletion(make):  # :1150-1162
+    p = make(**duplex_defaults(True))
+    _duplex_data_phase(p, True, send_last=False)
+    t = p.InitiateIo()
+    assert (t.io_action, t.buffer_length) == (Send, 4)
+    assert p.CompleteIo(t, 0, 1) == FailedIo
+    assert p.GetLastPatternError() == 1
+
+
+@pytest.mark.parametrize("n", [1, 2, 3], ids=["OneByteFails", "ShortFirstPieceFailsWithoutReassembly",
+                                             "ThreeBytesFails"])
+def test_Duplex_Client_CompletionDoneSplitRecv(make, n):  # :1178-1228: a split 'DONE' is not reassembled
+    p = make(**duplex_defaults(False))
+    _duplex_data_phase(p, False, send_last=True)
+    t = p.InitiateIo()
+    assert (t.io_action, t.buffer_length) == (Recv, 4)
+    assert p.CompleteIo(t, n, 0) == FailedIo
+    assert p.GetLastPatternError() == A.STATUS_ERROR_NOT_ALL_DATA_TRANSFERRED
+    assert p.InitiateIo().io_action == NoneAction
+
+
+@pytest.mark.parametrize("n,send_last", [(2, False), (1, True)], ids=["ShortSendAdvancesWithoutResend",
+                                                                      "OneByteAdvances"])
+def test_Duplex_Server_CompletionDoneSplitSend(make, n, send_last):  # :1230-1265: a short 'DONE' send advances
+    p = make(**duplex_defaults(True))
+    _duplex_data_phase(p, True, send_last)
+    t = p.InitiateIo()
+    assert (t.io_action, t.buffer_length) == (Send, 4)
+    assert p.CompleteIo(t, n, 0) == ContinueIo
+    t = p.InitiateIo()
+    assert t.io_action == Recv
+    assert p.CompleteIo(t, 0, 0) == CompletedIo
+    assert p.GetLastPatternError() == 0
+
+
+def test_Duplex_Client_DataRecvCappedBelowSocketBuffer_DoneCannotCoalesce(make):  # :1284-1310
+    p = make(**duplex_defaults(False))
+    _complete_connection_id(p, False)
+    r, s = _pended_data_tasks(p)
+    assert r.buffer_length < 1024  # capped to the outstanding data, not the buffer size: 'DONE' cannot ride along
+    assert _complete_data_recv(p, r, 10) == ContinueIo
+    assert p.CompleteIo(s, 10, 0) == ContinueIo
+    _successful_shutdown(p, False)
+    assert p.GetLastPatternError() == 0
+
+
+def test_Duplex_Client_PartialFinalData_ThenDone_Deframed(make):  # :1312-1353
+    p = make(**duplex_defaults(False))
+    _complete_connection_id(p, False)
+    r, s = _pended_data_tasks(p)
+    assert _complete_data_recv(p, r, 6) == ContinueIo
+    rr = p.InitiateIo()
+    assert (rr.io_action, rr.buffer_length, rr.expected_pattern_offset) == (Recv, 4, 6)
+    assert p.CompleteIo(s, 10, 0) == ContinueIo
+    assert _complete_data_recv(p, rr, 4) == ContinueIo
+    _successful_shutdown(p, False)
+    assert p.GetLastPatternError() == 0 and p.stats()["buffers_verified"] == 2
+
+
+def test_Duplex_Server_DataRecvCapped_FinCannotCoalesce(make):  # :1355-1393
+    p = make(**duplex_defaults(True))
+    _complete_connection_id(p, True)
+    r = p.InitiateIo()
+    assert (r.io_action, r.buffer_length) == (Recv, 10) and r.buffer_length < 1024
+    s = p.InitiateIo()
+    assert s.io_action == Send
+    assert _complete_data_recv(p, r, 10) == ContinueIo
+    assert p.CompleteIo(s, 10, 0) == ContinueIo
+    _successful_shutdown(p, True)
+    assert p.GetLastPatternError() == 0
+
+
+def _multi_send_defaults(server, pre_post_sends, chunks):  # :384-394 SetTestDuplexMultiSendDefaults
+    return duplex_defaults(server, pre_post_sends=pre_post_sends, buffer_size=10, transfer_size=2 * chunks * 10)
+
+
+def _recv_half(p, r, chunks):  # CompleteMultiSendRecvHalf: the recv half, one 10-byte chunk at a time
+    for i in range(chunks):
+        assert r.expected_pattern_offset == 10 * i
+        assert _complete_data_recv(p, r, 10) == ContinueIo
+        if i < chunks - 1:
+            r = p.InitiateIo()
+            assert (r.io_action, r.buffer_length) == (Recv, 10)
+
+
+def test_Duplex_Client_MultipleConcurrentSends_ReDriveAfterCompletion(make):  # :1443-1475
+    p = make(**_multi_send_defaults(False, 3, 4))
+    _complete_connection_id(p, False)
+    r = p.InitiateIo()
+    assert (r.io_action, r.buffer_length) == (Recv, 10)
+    sends = [p.InitiateIo() for _ in range(3)]  # only three fit the backlog though four chunks remain
+    assert [t.io_action for t in sends] == [Send] * 3
+    assert p.InitiateIo().io_action == NoneAction
+    assert p.CompleteIo(sends[0], 10, 0) == ContinueIo
+    again = p.InitiateIo()  # the freed backlog re-drives the fourth send
+    assert (again.io_action, again.buffer_length, again.buffer_offset) == (Send, 10, 30)
+    assert p.CompleteIo(again, 10, 0) == ContinueIo
+    assert p.CompleteIo(sends[1], 10, 0) == ContinueIo
+    assert p.CompleteIo(sends[2], 10, 0) == ContinueIo
+    assert p.InitiateIo().io_action == NoneAction
+    _recv_half(p, r, 4)
+    _successful_shutdown(p, False)
+    assert p.GetLastPatternError() == 0
+
+
+def test_Duplex_Client_IsbMode_DynamicBacklogGatesSends(make):  # :1477-1513
+    p = make(**_multi_send_defaults(False, 0, 3))
+    _complete_connection_id(p, False)
+    r = p.InitiateIo()
+    assert (r.io_action, r.buffer_length) == (Recv, 10)
+    s1 = p.InitiateIo()
+    assert (s1.io_action, s1.buffer_length) == (Send, 10)
+    assert p.InitiateIo().io_action == NoneAction  # the initial backlog is one chunk
+    p.SetIdealSendBacklog(30)  # the stack raises the ideal send backlog
+    s2, s3 = p.InitiateIo(), p.InitiateIo()
+    assert (s2.io_action, s3.io_action) == (Send, Send)
+    assert p.InitiateIo().io_action == NoneAction
+    for t in (s1, s2, s3):
+        assert p.CompleteIo(t, 10, 0) == ContinueIo
+    _recv_half(p, r, 3)
+    _successful_shutdown(p, False)
+    assert p.GetLastPatternError() == 0
+
+
+@pytest.mark.parametrize("reverse", [False, True], ids=["CompleteInOrder", "CompleteReverseOrder"])
+def test_Duplex_Server_MultipleConcurrentSends(make, reverse):  # :1515-1553
+    p = make(**_multi_send_defaults(True, 3, 3))
+    _complete_connection_id(p, True)
+    r = p.InitiateIo()
+    assert (r.io_action, r.buffer_length) == (Recv, 10)
+    sends = [p.InitiateIo() for _ in range(3)]
+    assert [t.io_action for t in sends] == [Send] * 3
+    assert p.InitiateIo().io_action == NoneAction
+    for t in (sends[::-1] if reverse else sends):
+        assert p.CompleteIo(t, 10, 0) == ContinueIo
+    _recv_half(p, r, 3)
+    _successful_shutdown(p, True)
+    assert p.GetLastPatternError() == 0
 
 
 @pytest.mark.parametrize("reverse", [False, True], ids=["InOrder", "ReverseOrder"])
