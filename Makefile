@@ -14,7 +14,13 @@ OBJS      := $(patsubst $(CSRC)/%,ctstraffic_amd/build/%.o,$(SRCS))
 DEVICE_VERIFY := ctstraffic_amd/build/device_verify
 TOOLS := tools/hbm_read_ceiling tools/verify_ablation
 
-all: $(ENGINE_SO) oracle $(DEVICE_VERIFY) $(TOOLS)
+SYNC_PROBE := tools/sync_probe
+
+all: $(ENGINE_SO) oracle $(DEVICE_VERIFY) $(TOOLS) $(SYNC_PROBE)
+
+# SYNC-mode (per-completion) verify latency probe against the C ABI
+$(SYNC_PROBE): tools/sync_probe.cpp $(ENGINE_SO) include/cts_engine.h
+	$(HIPCC) -O2 -std=c++17 -Iinclude $< -o $@ -Lctstraffic_amd -lcts_engine -Wl,-rpath,'$$ORIGIN/../ctstraffic_amd' -lpthread
 
 # measurement references used by tools/gpu_round.sh (plain streaming read/write ceilings, verify ablation)
 tools/%: tools/%.hip
@@ -40,7 +46,7 @@ asm: $(CSRC)/cts_kernels.hip $(HDRS)
 	$(HIPCC) $(HIPFLAGS) --cuda-device-only -S $< -o ctstraffic_amd/build/cts_kernels-$(ARCH).s
 
 clean:
-	rm -rf ctstraffic_amd/build $(ENGINE_SO) $(TOOLS)
+	rm -rf ctstraffic_amd/build $(ENGINE_SO) $(TOOLS) $(SYNC_PROBE)
 	$(MAKE) -s -C oracle clean
 
 .PHONY: all oracle asm clean

@@ -14,6 +14,7 @@
 
 #include "cts_engine.h"
 #include "cts_internal.hpp"
+#include "cts_slices.hpp"
 
 struct cts_engine {
     int device = 0;
@@ -147,12 +148,12 @@ int cts_engine_create(int device, cts_engine** out)
         return CTS_E_HIP;
     }
     void* p = nullptr;
-    if (host_alloc_mapped(sizeof(cts_buf_desc), &p) != CTS_OK) {
+    if (host_alloc_mapped(cts::kSliceMax * sizeof(cts_buf_desc), &p) != CTS_OK) {
         cts_engine_destroy(e);
         return CTS_E_NOMEM;
     }
     e->stage_desc = static_cast<cts_buf_desc*>(p);
-    if (host_alloc_mapped(sizeof(cts_verify_result), &p) != CTS_OK) {
+    if (host_alloc_mapped(cts::kSliceMax * sizeof(cts_verify_result), &p) != CTS_OK) {
         cts_engine_destroy(e);
         return CTS_E_NOMEM;
     }
@@ -405,21 +406,18 @@ int cts_verify_host(cts_engine* e, const void* host_buf, uint32_t len, uint32_t 
     int rc = ensure_stage(e, (size_t)len + 16);
     if (rc != CTS_OK) return rc;
     if (len) std::memcpy(e->stage, host_buf, len);
-    cts_buf_desc d;
-    d.byte_offset = 0;
-    d.length = len;
-    d.expected_pattern_offset = expected_offset;
-    d.conn_index = 0;
-    d.skip_head = 0;
-    *e->stage_desc = d;
+    // latency-bound single buffer: verified as up to cts::kSliceMax slices read at once (cts_slices.hpp)
+    uint32_t slice_len = 0;
+    const uint32_t ns = cts::slice_plan(0, len, expected_offset, 0, e->stage_desc, &slice_len);
     const uint8_t* arena = device_view(e->stage);
     const cts_buf_desc* dd = device_view(e->stage_desc);
     cts_verify_result* dr = device_view(e->stage_res);
     if (!arena || !dd || !dr) return CTS_E_HIP;
-    hipError_t err = cts::launch_verify(arena, e->stage_cap, dd, 1, len, dr, nullptr, nullptr, 0, e->stream, e->geo);
+    hipError_t err = cts::launch_verify(arena, e->stage_cap, dd, ns, slice_len, dr, nullptr, nullptr, 0, e->stream,
+                                        e->geo);
     if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
     if (err != hipSuccess) return CTS_E_HIP;
-    *out = *e->stage_res;
+    *out = cts::slice_merge(e->stage_res, ns, slice_len, len);
     return CTS_OK;
 }
 

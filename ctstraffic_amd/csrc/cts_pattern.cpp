@@ -27,6 +27,7 @@
 
 #include "cts_engine.h"
 #include "cts_pattern.h"
+#include "cts_slices.hpp"
 
 namespace {
 
@@ -536,18 +537,25 @@ struct cts_io_pattern {
         if (engine == nullptr) return CTS_E_INVALID;
         const uint8_t* rp = reinterpret_cast<const uint8_t*>(src);
         if (recv_pinned.host != nullptr && rp >= recv_pinned.host && rp + transferred <= recv_pinned.host + recv_pinned.bytes) {
-            // zero copy: the kernel reads the pinned recv buffer in place over PCIe
+            // zero copy: the kernel reads the pinned recv buffer in place over PCIe, as up to
+            // cts::kSliceMax slices so the reads go out together (latency-bound; cts_slices.hpp)
             int rc = EnsureStream();
             if (rc != CTS_OK) return rc;
-            if (one.host == nullptr && (rc = one.alloc(engine, 64)) != CTS_OK) return rc;
-            auto* d = reinterpret_cast<cts_buf_desc*>(one.host);
-            *d = cts_buf_desc{(uint64_t)(rp - recv_pinned.host), transferred, t.expected_pattern_offset, 0, 0};
-            rc = cts_verify(engine, recv_pinned.dev, recv_pinned.bytes, reinterpret_cast<cts_buf_desc*>(one.dev), 1,
-                            transferred, reinterpret_cast<cts_verify_result*>(one.dev + 32), nullptr, nullptr, 0,
+            constexpr uint32_t kResAt = cts::kSliceMax * sizeof(cts_buf_desc);
+            if (one.host == nullptr &&
+                (rc = one.alloc(engine, kResAt + cts::kSliceMax * sizeof(cts_verify_result))) != CTS_OK)
+                return rc;
+            uint32_t slice_len = 0;
+            const uint32_t ns = cts::slice_plan((uint64_t)(rp - recv_pinned.host), transferred,
+                                                t.expected_pattern_offset, 0, reinterpret_cast<cts_buf_desc*>(one.host),
+                                                &slice_len);
+            rc = cts_verify(engine, recv_pinned.dev, recv_pinned.bytes, reinterpret_cast<cts_buf_desc*>(one.dev), ns,
+                            slice_len, reinterpret_cast<cts_verify_result*>(one.dev + kResAt), nullptr, nullptr, 0,
                             stream);
             if (rc != CTS_OK) return rc;
             if (hipStreamSynchronize(stream) != hipSuccess) return CTS_E_HIP;
-            std::memcpy(&r, one.host + 32, sizeof(r));
+            r = cts::slice_merge(reinterpret_cast<const cts_verify_result*>(one.host + kResAt), ns, slice_len,
+                                 transferred);
             return CTS_OK;
         }
         return cts_verify_host(engine, src, transferred, t.expected_pattern_offset, &r);

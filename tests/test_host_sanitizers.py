@@ -29,7 +29,7 @@ ENV = {"ASAN_OPTIONS": "detect_leaks=1:abort_on_error=0:exitcode=23",
 def _build(d, san, driver):
     flags = ["-g", "-O1", "-fno-omit-frame-pointer", "-pthread"] + SAN[san]
     inc = ["-I", os.path.join(ROOT, "include"), "-I", os.path.join(ROOT, "ctstraffic_amd", "csrc"),
-           "-I", "/opt/rocm/include", "-D__HIP_PLATFORM_AMD__"]
+           "-I", os.path.join(ROOT, "oracle"), "-I", "/opt/rocm/include", "-D__HIP_PLATFORM_AMD__"]
     objs = []
     for src in [os.path.join(ROOT, "ctstraffic_amd", "csrc", s) for s in HOST_SRCS] + [
             os.path.join(ROOT, "tests", "cpp", "engine_stub.cpp"), os.path.join(ROOT, "tests", "cpp", driver)]:
@@ -46,7 +46,7 @@ def _build(d, san, driver):
 
 
 @pytest.mark.parametrize("san", sorted(SAN))
-@pytest.mark.parametrize("driver", ["pattern_replay.cpp", "loopback_stress.cpp"])
+@pytest.mark.parametrize("driver", ["pattern_replay.cpp", "loopback_stress.cpp", "slices_check.cpp"])
 def test_host_code_under_sanitizer(san, driver):
     with tempfile.TemporaryDirectory() as d:
         exe = _build(d, san, driver)

@@ -1,0 +1,92 @@
+// sync_probe.cpp — latency of one SYNC-mode verify (ctsIOPattern.cpp:745-775 called per CompleteIo):
+// a 64 KiB buffer in pinned, device-mapped host memory verified in place over PCIe and waited for,
+// exactly as cts_pattern.cpp VerifyNow does (cts_verify on the pattern's own stream + synchronize).
+// Variants: the buffer described as S slices (S descriptors of 64 KiB / S, expected offsets advanced,
+// so S workgroups/waves issue their PCIe reads at once) and T threads, each with its own stream,
+// buffer, descriptor and result (T connections completing concurrently). Wait = hipStreamSynchronize
+// or a hipStreamQuery spin. Prints one JSON line per variant: us per verify (per thread).
+//   build: make tools/sync_probe      run: tools/sync_probe [iters]
+#include <hip/hip_runtime_api.h>
+
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "cts_engine.h"
+
+static int run_thread(cts_engine* e, uint32_t slices, bool spin, int iters, double* us_out, int* bad)
+{
+    void* stream = nullptr;
+    if (cts_engine_stream_create(e, &stream) != CTS_OK) return 1;
+    const uint32_t len = 65536, per = len / slices;
+    void *host = nullptr, *dev = nullptr, *hd = nullptr, *dd = nullptr;
+    if (cts_host_alloc(e, len, &host, &dev) != CTS_OK) return 1;
+    if (cts_host_alloc(e, 4096 + slices * 64, &hd, &dd) != CTS_OK) return 1;
+    for (uint32_t b = 0; b < len; ++b) static_cast<uint8_t*>(host)[b] = cts_pattern_byte(b + 1000);
+    auto* desc = static_cast<cts_buf_desc*>(hd);
+    for (uint32_t k = 0; k < slices; ++k)
+        desc[k] = cts_buf_desc{(uint64_t)k * per, per, (1000 + k * per) % CTS_PATTERN_PERIOD, k, 0};
+    auto* res_h = reinterpret_cast<cts_verify_result*>(static_cast<uint8_t*>(hd) + 2048);
+    auto* res_d = reinterpret_cast<cts_verify_result*>(static_cast<uint8_t*>(dd) + 2048);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    auto once = [&]() {
+        if (cts_verify(e, dev, len, static_cast<cts_buf_desc*>(dd), slices, per, res_d, nullptr, nullptr, 0, stream) !=
+            CTS_OK)
+            return false;
+        if (spin) {
+            while (hipStreamQuery(s) == hipErrorNotReady) {
+            }
+        } else if (hipStreamSynchronize(s) != hipSuccess) {
+            return false;
+        }
+        for (uint32_t k = 0; k < slices; ++k)
+            if (!res_h[k].pass) return false;
+        return true;
+    };
+    for (int i = 0; i < 50; ++i)
+        if (!once()) ++*bad;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int i = 0; i < iters; ++i)
+        if (!once()) ++*bad;
+    const auto t1 = std::chrono::steady_clock::now();
+    *us_out = std::chrono::duration<double, std::micro>(t1 - t0).count() / iters;
+    cts_host_free(e, host);
+    cts_host_free(e, hd);
+    cts_engine_stream_destroy(e, stream);
+    return 0;
+}
+
+int main(int argc, char** argv)
+{
+    const int iters = argc > 1 ? std::atoi(argv[1]) : 2000;
+    cts_engine* e = nullptr;
+    if (cts_engine_create(0, &e) != CTS_OK) return 1;
+    for (int spin = 0; spin < 2; ++spin)
+        for (uint32_t threads : {1u, 8u})
+            for (uint32_t slices : {1u, 2u, 4u, 8u, 16u, 32u, 64u}) {
+                std::vector<double> us(threads, 0.0);
+                std::vector<int> bad(threads, 0), rc(threads, 0);
+                std::vector<std::thread> th;
+                for (uint32_t t = 0; t < threads; ++t)
+                    th.emplace_back([&, t] { rc[t] = run_thread(e, slices, spin != 0, iters, &us[t], &bad[t]); });
+                for (auto& x : th) x.join();
+                double mean = 0;
+                int nbad = 0, nrc = 0;
+                for (uint32_t t = 0; t < threads; ++t) {
+                    mean += us[t] / threads;
+                    nbad += bad[t];
+                    nrc += rc[t];
+                }
+                std::printf("{\"wait\": \"%s\", \"threads\": %u, \"slices\": %u, \"us_per_verify\": %.2f, "
+                            "\"GBps_total\": %.2f, \"bad\": %d, \"rc\": %d}\n",
+                            spin ? "query_spin" : "stream_sync", threads, slices, mean,
+                            threads * 65536.0 / (mean * 1e3), nbad, nrc);
+                std::fflush(stdout);
+            }
+    cts_engine_destroy(e);
+    return 0;
+}
