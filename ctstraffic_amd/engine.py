@@ -117,6 +117,16 @@ class Engine:
         check("cts_engine_get_attr", lib().cts_engine_get_attr(self._h, attr, ctypes.byref(v)))
         return v.value
 
+    # ---- streams ---------------------------------------------------------------
+    def stream_create(self) -> int:
+        """A non-blocking HIP stream on the engine's device (cts_engine_stream_create); raw handle."""
+        p = ctypes.c_void_p()
+        check("cts_engine_stream_create", lib().cts_engine_stream_create(self._h, ctypes.byref(p)))
+        return p.value
+
+    def stream_destroy(self, stream: int) -> None:
+        check("cts_engine_stream_destroy", lib().cts_engine_stream_destroy(self._h, stream))
+
     # ---- fill ----------------------------------------------------------------
     def sender_buffer(self, max_buffer_size: int, stream=None):
         """Device copy of g_senderSharedBuffer (InitOnceIoPatternCallback, ctsIOPattern.cpp:52-90)."""

@@ -35,12 +35,17 @@ fi
 if [[ $STEPS == all || $STEPS == *prof* ]]; then
   run rocprof-kernel-trace
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -d "$OUT/prof_kt" -o run --output-format csv \
-    -- python3 bench.py --no-cpu-baseline --no-extras --steps 200 --warmup 20 > "$OUT/prof_kt_bench.json" 2> "$OUT/prof_kt.err"
+    -- python3 bench.py --no-cpu-baseline --no-extras --pipeline-streams 1 --steps 200 --warmup 20 > "$OUT/prof_kt_bench.json" 2> "$OUT/prof_kt.err"
   for ctr in FETCH_SIZE WRITE_SIZE TCC_EA0_RDREQ_sum; do
     run rocprof-pmc $ctr
     timeout -k 10 300 rocprofv3 --pmc $ctr --kernel-trace -T -d "$OUT/prof_pmc_$ctr" -o run --output-format csv \
-      -- python3 bench.py --no-cpu-baseline --no-extras --steps 50 --warmup 5 > "$OUT/prof_pmc_$ctr.json" 2> "$OUT/prof_pmc_$ctr.err"
+      -- python3 bench.py --no-cpu-baseline --no-extras --pipeline-streams 1 --steps 50 --warmup 5 > "$OUT/prof_pmc_$ctr.json" 2> "$OUT/prof_pmc_$ctr.err"
   done
+  # the default (pipelined) headline command under the kernel trace: its serialized roofline leg and
+  # its pipelined leg as two bursts (tools/prof_summary.py: wall per launch, overlap)
+  run rocprof-pipelined-kernel-trace
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -d "$OUT/prof_pipe_kt" -o run --output-format csv \
+    -- python3 bench.py --no-cpu-baseline --no-extras --steps 200 --warmup 20 > "$OUT/prof_pipe_kt_bench.json" 2> "$OUT/prof_pipe_kt.err"
 fi
 if [[ $STEPS == all || $STEPS == *dgprof* ]]; then
   # config 3 (16 M datagrams): the bench's datagram extras under the same two profilers

@@ -59,6 +59,36 @@ def _by_kernel(rows, value):
     return best
 
 
+def _pipelined(tr):
+    """Bursts of config-2 verify launches (gaps > 200 us split them) in a default bench.py run: the
+    serialized roofline leg and the pipelined headline leg. Per burst: launches, wall span / launch
+    (first start to last end), mean kernel duration, and how many launches start before the previous
+    one ends (overlap)."""
+    if not os.path.exists(tr):
+        return None
+    iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in csv.DictReader(open(tr))
+                if _kname(r["Kernel_Name"]) == "verify_wg_kernel" and int(_grid(r)) == 262144)
+    bursts, cur = [], []
+    for a, b in iv:
+        if cur and a - max(e for _, e in cur) > 200_000:
+            bursts.append(cur)
+            cur = []
+        cur.append((a, b))
+    if cur:
+        bursts.append(cur)
+    res = []
+    for bu in bursts:
+        if len(bu) < 50:
+            continue
+        span = max(e for _, e in bu) - bu[0][0]
+        over = sum(1 for i in range(1, len(bu)) if bu[i][0] < max(e for _, e in bu[:i]))
+        res.append({"launches": len(bu), "wall_us_per_launch": round(span / len(bu) / 1e3, 2),
+                    "algorithmic_GBps_at_wall": round(ALGO_BYTES["verify_wg_kernel"] * len(bu) / span, 1),
+                    "mean_kernel_us": round(float(np.mean([b - a for a, b in bu])) / 1e3, 2),
+                    "launches_overlapping_previous": over})
+    return {"kernel": "verify_wg_kernel", "grid": 262144, "run": "prof_pipe", "bursts": res} if res else None
+
+
 def main(src, dst):
     os.makedirs(dst, exist_ok=True)
     for run in RUNS:
@@ -79,6 +109,11 @@ def main(src, dst):
                                  "avg_us": round(float(d.mean()) / 1e3, 2), "median_us": round(float(np.median(d)) / 1e3, 2),
                                  "min_us": round(float(d.min()) / 1e3, 2),
                                  "algorithmic_GBps_at_avg": round(ALGO_BYTES[k] / float(d.mean()), 1)}
+    pipe = _pipelined(os.path.join(src, "prof_pipe_kt", "run_kernel_trace.csv"))
+    if pipe:
+        out["config2 verify, pipelined headline leg (bench.py default, streams round-robin)"] = pipe
+        shutil.copy(os.path.join(src, "prof_pipe_kt", "run_kernel_stats.csv"),
+                    os.path.join(dst, "kernel_stats_pipelined.csv"))
     if out:
         json.dump(out, open(os.path.join(dst, "kernel_trace_summary.json"), "w"), indent=1)
     pmc = {}
