@@ -312,6 +312,26 @@ def test_verify_host_single(engine):
     assert not r["pass"] and r["first_mismatch"] == 2
 
 
+def test_verify_host_single_slice_edges(engine):
+    """cts_verify_host reads one buffer as up to 64 slices (csrc/cts_slices.hpp); corruptions on slice
+    edges, in two slices at once, and ragged last slices fold back to the oracle's whole-buffer result."""
+    S = oracle.sender_buffer(140000)
+    rng = np.random.default_rng(0x51CE)
+    for n in (1023, 1024, 1025, 4097, 65536, 65537, 100000, 131072):
+        sl = max(1024, ((n + 63) // 64 + 15) // 16 * 16)
+        for trial in range(6):
+            e = int(rng.integers(0, 65536))
+            buf = S[e:e + n].copy()
+            picks = {0: [0], 1: [n - 1], 2: [min(sl, n - 1)], 3: [min(sl - 1, n - 1)],
+                     4: [n - 1, int(rng.integers(0, n))], 5: sorted({int(x) for x in rng.integers(0, n, 3)})}[trial]
+            for k in picks:
+                buf[k] ^= int(rng.integers(1, 256))
+            r = engine.verify_host(buf, e)
+            o = oracle.verify_buffer(buf, 0, e, n)
+            assert (r["pass"], r["first_mismatch"], r["expected"], r["actual"], r["mismatch_bytes"]) == (
+                o["pass"], o["first_mismatch"], o["expected"], o["actual"], o["mismatch_bytes"]), (n, trial)
+
+
 def test_verify_host_batch(engine):
     """Repeated calls reuse (and grow) the engine's pinned staging: small, larger, small again."""
     for seed, n, max_len in ((5, 100, 3000), (6, 3000, 70000), (7, 17, 200)):
