@@ -55,6 +55,9 @@ def parse():
     p.add_argument("--pipeline-streams", type=int, default=3,
                    help="headline leg: steps round-robin over S engine streams, so one batch's tail overlaps the "
                         "next batch's ramp-up (1 = serialized launches; tools/overlap_probe.py)")
+    p.add_argument("--pipeline-blocks-per-cu", type=int, default=0,
+                   help="verify grid cap (CTS_ATTR_BLOCKS_PER_CU) for the pipelined leg; 0 = engine default (4). "
+                        "In bench.py A/B on one box 4 beat 3 (39.3-40.0 vs 39.8-40.3 us per step) and 2 (42.9-43.5)")
     return p.parse_args()
 
 
@@ -132,10 +135,16 @@ def main():
     S = 1 if graph is not None else max(1, args.pipeline_streams)
     pipe = [torch.cuda.ExternalStream(engine.stream_create(), device=dev) for _ in range(S)] if S > 1 else []
 
+    from ctstraffic_amd import _lib
+
+    default_bpc = engine.get_attr(_lib.ATTR_BLOCKS_PER_CU)
+    pipe_bpc = args.pipeline_blocks_per_cu if pipe and args.pipeline_blocks_per_cu > 0 else default_bpc
+
     def run_pipelined(k0, k):
         if not pipe:
             run_steps(k0, k)
             return
+        engine.set_attr(_lib.ATTR_BLOCKS_PER_CU, pipe_bpc)  # read at launch time; launches below are queued
         start = torch.cuda.Event()
         start.record(stream)
         for ps in pipe:
@@ -147,6 +156,7 @@ def main():
             ev = torch.cuda.Event()
             ev.record(ps)
             stream.wait_event(ev)
+        engine.set_attr(_lib.ATTR_BLOCKS_PER_CU, default_bpc)
 
     # ---- warmup -------------------------------------------------------------------------------
     run_steps(0, max(args.warmup, 1))
@@ -283,6 +293,7 @@ def main():
                 "algorithmic_bytes_per_launch": bytes_per_step,
                 "pipelined": {
                     "streams": S,
+                    "blocks_per_cu": pipe_bpc,
                     "us_per_step": round(pipe_step_s * 1e6, 2),
                     "effective_GBps": round(bytes_per_step / pipe_step_s / 1e9, 1),
                     "frac": round(bytes_per_step / pipe_step_s / 1e9 / HBM_PEAK_GBPS, 4),

@@ -57,6 +57,31 @@ def main():
             engine.verify(arenas[i % R], descs, max_length_hint=w.max_length, counters=counters, stream=s)
 
     mode = sys.argv[2] if len(sys.argv) > 2 else "sweep"
+    if mode == "bpc":  # workgroup-per-buffer grid cap x streams
+        from ctstraffic_amd import _lib
+        default_bpc = engine.get_attr(_lib.ATTR_BLOCKS_PER_CU)
+        for trial in range(2):
+            for bpc in (2, 3, 4, 6, 8):
+                engine.set_attr(_lib.ATTR_BLOCKS_PER_CU, bpc)
+                for S in (1, 2, 3):
+                    streams = [engine_stream() for _ in range(S)]
+                    for i in range(2 * R):
+                        launch(i, streams[i % S], True)
+                    torch.cuda.synchronize()
+                    engine.reset_counters(counters)
+                    torch.cuda.synchronize()
+                    t0 = time.perf_counter()
+                    for i in range(K):
+                        launch(i, streams[i % S], True)
+                    torch.cuda.synchronize()
+                    t = time.perf_counter() - t0
+                    ok = engine.read_counters(counters) == {k: v * K for k, v in exp_ctr.items()}
+                    print(json.dumps({"trial": trial, "blocks_per_cu": bpc, "streams": S, "steps": K,
+                                      "us_per_step": round(t / K * 1e6, 2),
+                                      "TBps": round(w.verified_bytes() * K / t / 1e12, 3), "counters_ok": ok}),
+                          flush=True)
+        engine.set_attr(_lib.ATTR_BLOCKS_PER_CU, default_bpc)
+        return
     kinds = ("torch", "engine") if mode == "sweep" else ("engine",)
     sweep = (1, 2, 3, 4, 6, 8) if mode == "sweep" else (1, 2, 3)
     for trial in range(3):

@@ -61,32 +61,30 @@ def _by_kernel(rows, value):
 
 def _pipelined(tr):
     """Bursts of config-2 verify launches (gaps > 200 us split them) in a default bench.py run: the
-    serialized roofline leg and the pipelined headline leg. Per burst: launches, wall span / launch
-    (first start to last end), mean kernel duration, and how many launches start before the previous
-    one ends (overlap)."""
+    serialized roofline leg and the pipelined headline leg. Per burst: launches, grids, wall span /
+    launch (first start to last end), mean kernel duration, and how many launches start before the
+    previous one ends (overlap)."""
     if not os.path.exists(tr):
         return None
-    iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in csv.DictReader(open(tr))
-                if _kname(r["Kernel_Name"]) == "verify_wg_kernel" and int(_grid(r)) == 262144)
-    bursts, cur = [], []
-    for a, b in iv:
-        if cur and a - max(e for _, e in cur) > 200_000:
-            bursts.append(cur)
-            cur = []
-        cur.append((a, b))
-    if cur:
-        bursts.append(cur)
+    iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), int(_grid(r))) for r in csv.DictReader(open(tr))
+                if _kname(r["Kernel_Name"]) == "verify_wg_kernel" and int(_grid(r)) >= 65536)
+    bursts = []
+    for a, b, g in iv:
+        if not bursts or a - max(e for _, e, _ in bursts[-1]) > 200_000:
+            bursts.append([])
+        bursts[-1].append((a, b, g))
     res = []
     for bu in bursts:
         if len(bu) < 50:
             continue
-        span = max(e for _, e in bu) - bu[0][0]
-        over = sum(1 for i in range(1, len(bu)) if bu[i][0] < max(e for _, e in bu[:i]))
-        res.append({"launches": len(bu), "wall_us_per_launch": round(span / len(bu) / 1e3, 2),
+        span = max(e for _, e, _ in bu) - bu[0][0]
+        over = sum(1 for i in range(1, len(bu)) if bu[i][0] < max(e for _, e, _ in bu[:i]))
+        res.append({"launches": len(bu), "grids": sorted({g for _, _, g in bu}),
+                    "wall_us_per_launch": round(span / len(bu) / 1e3, 2),
                     "algorithmic_GBps_at_wall": round(ALGO_BYTES["verify_wg_kernel"] * len(bu) / span, 1),
-                    "mean_kernel_us": round(float(np.mean([b - a for a, b in bu])) / 1e3, 2),
+                    "mean_kernel_us": round(float(np.mean([b - a for a, b, _ in bu])) / 1e3, 2),
                     "launches_overlapping_previous": over})
-    return {"kernel": "verify_wg_kernel", "grid": 262144, "run": "prof_pipe", "bursts": res} if res else None
+    return {"kernel": "verify_wg_kernel", "run": "prof_pipe", "bursts": res} if res else None
 
 
 def main(src, dst):
