@@ -55,6 +55,8 @@ def parse():
     p.add_argument("--pipeline-streams", type=int, default=3,
                    help="headline leg: steps round-robin over S engine streams, so one batch's tail overlaps the "
                         "next batch's ramp-up (1 = serialized launches; tools/overlap_probe.py)")
+    p.add_argument("--verify-variant", type=int, default=-1,
+                   help="CTS_ATTR_VERIFY_VARIANT for both legs (-1 = engine default; tools/tune_verify.py)")
     p.add_argument("--pipeline-blocks-per-cu", type=int, default=0,
                    help="verify grid cap (CTS_ATTR_BLOCKS_PER_CU) for the pipelined leg; 0 = engine default (4). "
                         "In bench.py A/B on one box 4 beat 3 (39.3-40.0 vs 39.8-40.3 us per step) and 2 (42.9-43.5)")
@@ -84,6 +86,10 @@ def main():
         D.init(args.dist_backend, device=torch.device(dev) if args.dist_backend == "nccl" else None)
 
     engine = Engine(gpu)
+    if args.verify_variant >= 0:
+        from ctstraffic_amd import _lib as L
+
+        engine.set_attr(L.ATTR_VERIFY_VARIANT, args.verify_variant)
     stream = torch.cuda.Stream() if args.stream == "new" else torch.cuda.current_stream()
 
     # ---- workload (per rank: weak scaling) --------------------------------------------------

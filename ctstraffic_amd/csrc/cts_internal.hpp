@@ -15,7 +15,7 @@ namespace cts {
 constexpr int kCounterSlots = 8;  // 5 used, padded to one 64-byte line
 enum CounterSlot { kBytesChecked = 0, kBytesOk = 1, kBuffersChecked = 2, kBuffersFailed = 3, kMismatchedBytes = 4 };
 
-constexpr int kVerifyVariants = 15;  // workgroup-per-buffer verify variants (launch_verify)
+constexpr int kVerifyVariants = 18;  // workgroup-per-buffer verify variants (launch_verify)
 constexpr int kSmallVariants = 10;   // small-buffer (datagram) verify variants
 constexpr int kMediaStreamVariants = 4;  // MediaStream receive kernels (launch_media_stream_verify)
 

@@ -625,7 +625,10 @@ __device__ __forceinline__ void block_reduce_mismatch(uint32_t& first, uint32_t&
 // SCTR: the per-buffer verdict is workgroup-uniform (__syncthreads_or), so the
 // counters of clean buffers are kept in SGPRs by every wave (scalar adds, no LDS
 // round trip per buffer); only a corrupt buffer goes through lane 0 + LDS.
-template <int U, bool NT, bool SPLIT = false, bool SCTR = false, bool WHOLE = false, bool XD = false>
+// WIN > 1: the descriptor list is cut into WIN contiguous windows and workgroup b walks window
+// b % WIN with stride gridDim.x / WIN (the launcher makes the grid a multiple of WIN), so WIN
+// far-apart regions of the arena stream at once instead of one 1024-buffer front.
+template <int U, bool NT, bool SPLIT = false, bool SCTR = false, bool WHOLE = false, bool XD = false, int WIN = 1>
 __global__ void __launch_bounds__(kBlock, (U <= 8 ? 8 : 4))
     verify_wg_kernel(const uint8_t* __restrict__ arena, uint64_t arena_bytes, const cts_buf_desc* __restrict__ descs,
                      uint32_t n, cts_verify_result* __restrict__ results, uint64_t* __restrict__ counters,
@@ -636,12 +639,21 @@ __global__ void __launch_bounds__(kBlock, (U <= 8 ? 8 : 4))
     zero_counters<1>(ctr);
     uint64_t ok_bytes = 0;     // SCTR: bytes of clean buffers (uniform)
     uint32_t ok_buffers = 0;   // SCTR: clean buffers (uniform)
-    uint32_t i = blockIdx.x;
+    uint32_t i = blockIdx.x, end = n, step = gridDim.x;
+    if constexpr (WIN > 1) {
+        const uint32_t per = (uint32_t)(((uint64_t)n + WIN - 1) / WIN);
+        const uint32_t g = blockIdx.x % WIN;
+        const uint64_t e = (uint64_t)(g + 1) * per;
+        end = e < n ? (uint32_t)e : n;
+        const uint64_t s0 = (uint64_t)g * per + blockIdx.x / WIN;
+        i = s0 < end ? (uint32_t)s0 : end;
+        step = gridDim.x / WIN;
+    }
     cts_buf_desc dn;
-    if (i < n) dn = descs[i];
-    for (; i < n; i += gridDim.x) {
+    if (i < end) dn = descs[i];
+    for (; i < end; i = (uint64_t)i + step < end ? i + step : end) {
         const cts_buf_desc d = dn;
-        if (i + gridDim.x < n) dn = descs[i + gridDim.x];
+        if ((uint64_t)i + step < end) dn = descs[i + step];
         if (desc_bad(d, arena_bytes)) {
             if (lane == 0) write_bad(results, i);
             continue;
@@ -1674,6 +1686,14 @@ static inline uint32_t grid_for(uint32_t n, int teams_per_block, const LaunchGeo
     return (uint32_t)(g == 0 ? 1 : g);
 }
 
+// workgroup-per-buffer grid for a WIN-window walk: grid_for's size rounded down to a multiple of
+// WIN (at least WIN), so every window gets gridDim.x / WIN workgroups
+static inline uint32_t grid_win(uint32_t n, uint32_t win, const LaunchGeometry& geo)
+{
+    const uint32_t g = grid_for(n, 1, geo);
+    return g < win ? win : g - g % win;
+}
+
 #define CTS_VERIFY_ARGS arena, arena_bytes, descs, n, results, counters, conn_first_fail, n_conns
 
 // Chunked launch of a four-buffers-per-wave kernel (QuadWalk<true>): chunk = geo.small_chunk
@@ -1731,7 +1751,7 @@ static void launch_verify_nt(const uint8_t* arena, uint64_t arena_bytes, const c
         // 8 = variant 6 with clean-buffer counters in SGPRs,
         // 9 = variant 6 + whole-line spans streamed without edge/head/tail handling, 10 = same U4,
         // 11 = variant 10 with the exact diff of whole-line spans in registers (no re-read), 12 = same U8,
-        // 13 = same U2, 14 = same U1
+        // 13 = same U2, 14 = same U1, 15/16/17 = variant 13 walking 2/4/8 windows of the descriptor list
         switch (geo.verify_variant) {
         case 4: verify_wg_nb_kernel<8, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 5: verify_wg_nb_kernel<4, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
@@ -1743,6 +1763,9 @@ static void launch_verify_nt(const uint8_t* arena, uint64_t arena_bytes, const c
         case 12: verify_wg_kernel<8, NT, true, false, true, true><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 13: verify_wg_kernel<2, NT, true, false, true, true><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 14: verify_wg_kernel<1, NT, true, false, true, true><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
+        case 15: verify_wg_kernel<2, NT, true, false, true, true, 2><<<grid_win(n, 2, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
+        case 16: verify_wg_kernel<2, NT, true, false, true, true, 4><<<grid_win(n, 4, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
+        case 17: verify_wg_kernel<2, NT, true, false, true, true, 8><<<grid_win(n, 8, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 7: verify_wg_kernel<4, NT, true><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 1: verify_wg_kernel<4, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 2: verify_wg_kernel<16, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;

@@ -345,7 +345,7 @@ def test_verify_host_batch(engine):
 
 
 # ---- every launch variant / geometry is bit-identical ------------------------------------------
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17])
 @pytest.mark.parametrize("nt", [1, 0])
 def test_launch_variants_parity(engine, variant, nt):
     from ctstraffic_amd import _lib
@@ -360,7 +360,8 @@ def test_launch_variants_parity(engine, variant, nt):
                 (21, 200, 3000, 1472, True, False), (22, 64, 140000, 0, False, False),
                 (23, 300, 1472, 1472, True, False), (24, 100, 70000, 0, True, False),
                 (25, 6000, 9000, 0, False, False),  # > kRing buffers per workgroup
-                (26, 400, 140000, 0, False, True), (27, 300, 2000, 1472, False, True)]:
+                (26, 400, 140000, 0, False, True), (27, 300, 2000, 1472, False, True),
+                (28, 3, 70000, 0, False, False)]:  # fewer buffers than windows (variants 15-17)
             for bpc in (1, 16):
                 engine.set_attr(_lib.ATTR_BLOCKS_PER_CU, bpc)
                 engine.set_attr(_lib.ATTR_SMALL_BLOCKS_PER_CU, bpc)
