@@ -45,6 +45,7 @@ ATTR_FILL_BLOCKS_PER_CU = 7
 ATTR_MS_VARIANT = 8
 ATTR_SMALL_CHUNK = 9
 ATTR_FILL_NT = 10
+ATTR_SYNC_COALESCE = 11
 
 
 class CtsError(RuntimeError):
@@ -108,6 +109,7 @@ def _declare(L: ctypes.CDLL) -> None:
         "cts_counters_reset": ([P, P, P], i32),
         "cts_counters_read": ([P, P, ctypes.POINTER(CtsCounters), P], i32),
         "cts_verify_host": ([P, P, u32, u32, ctypes.POINTER(CtsVerifyResult)], i32),
+        "cts_verify_mapped": ([P, P, u32, u32, ctypes.POINTER(CtsVerifyResult)], i32),
         "cts_verify_host_batch": ([P, P, P, P, P, u32, P, ctypes.POINTER(CtsCounters)], i32),
         "cts_host_alloc": ([P, u64, ctypes.POINTER(P), ctypes.POINTER(P)], i32),
         "cts_host_free": ([P, P], i32),

@@ -5,7 +5,9 @@
 // FAIL_FAST process aborts with error codes a foreign caller can handle.
 #include <hip/hip_runtime_api.h>
 
+#include <algorithm>
 #include <atomic>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -32,6 +34,27 @@ struct cts_engine {
     void* batch_res = nullptr;
     size_t batch_res_cap = 0;
     void* batch_ctr = nullptr;
+    // cts_verify_mapped: concurrent SYNC verifies combined into one launch (flat combining)
+    std::mutex comb_mu;
+    std::condition_variable comb_cv;
+    std::vector<struct cts_sync_req*> comb_q;  // waiting for the next launch
+    bool comb_busy = false;
+    int sync_coalesce = 0;                     // CTS_ATTR_SYNC_COALESCE (read by cts_pattern's SYNC verify)                    // a leader owns comb_stream and the comb_* staging
+    hipStream_t comb_stream = nullptr;
+    void* comb_desc = nullptr;
+    size_t comb_desc_cap = 0;
+    void* comb_res = nullptr;
+    size_t comb_res_cap = 0;
+};
+
+// One caller of cts_verify_mapped: its buffer, and its answer once `done`.
+struct cts_sync_req {
+    const uint8_t* dev;
+    uint32_t len;
+    uint32_t expected;
+    cts_verify_result out;
+    int rc;
+    bool done;
 };
 
 namespace {
@@ -100,6 +123,57 @@ int ensure_stage(cts_engine* e, size_t bytes)
     return rc;
 }
 
+// The leader's half of cts_verify_mapped: every request of `batch` as slices of one launch.
+// Descriptors address the group relative to its lowest buffer (one flat device address range:
+// mapped pinned host memory and HBM share the GPU's virtual address space; only the described
+// bytes are read). Per-request verdicts fold back with slice_merge, so each caller gets exactly
+// what a launch of its own would have returned (ctsIOPattern.cpp:745-775).
+void run_sync_group(cts_engine* e, const std::vector<cts_sync_req*>& batch)
+{
+    int rc = CTS_OK;
+    DeviceGuard g(e->device);
+    if (!g.ok) rc = CTS_E_HIP;
+    if (rc == CTS_OK && e->comb_stream == nullptr &&
+        hipStreamCreateWithFlags(&e->comb_stream, hipStreamNonBlocking) != hipSuccess) {
+        e->comb_stream = nullptr;
+        rc = CTS_E_HIP;
+    }
+    const size_t maxd = (size_t)cts::kSliceMax * batch.size();
+    if (rc == CTS_OK) rc = ensure_pinned(&e->comb_desc, &e->comb_desc_cap, maxd * sizeof(cts_buf_desc), 4096);
+    if (rc == CTS_OK) rc = ensure_pinned(&e->comb_res, &e->comb_res_cap, maxd * sizeof(cts_verify_result), 4096);
+    std::vector<uint32_t> first(batch.size()), count(batch.size()), slen(batch.size());
+    if (rc == CTS_OK) {
+        const uint8_t* base = batch[0]->dev;
+        const uint8_t* end = batch[0]->dev + batch[0]->len;
+        for (const cts_sync_req* r : batch) {
+            base = std::min(base, r->dev);
+            end = std::max(end, r->dev + r->len);
+        }
+        base -= reinterpret_cast<uintptr_t>(base) & 15u;  // the kernels align loads from a 16-B arena base
+        auto* hd = static_cast<cts_buf_desc*>(e->comb_desc);
+        uint32_t nd = 0, maxsl = 0;
+        for (size_t i = 0; i < batch.size(); ++i) {
+            first[i] = nd;
+            count[i] = cts::slice_plan((uint64_t)(batch[i]->dev - base), batch[i]->len, batch[i]->expected,
+                                       (uint32_t)i, hd + nd, &slen[i]);
+            nd += count[i];
+            maxsl = std::max(maxsl, slen[i]);
+        }
+        const cts_buf_desc* dd = device_view(hd);
+        cts_verify_result* dr = device_view(static_cast<cts_verify_result*>(e->comb_res));
+        hipError_t err = (dd && dr) ? cts::launch_verify(base, (uint64_t)(end - base), dd, nd, maxsl, dr, nullptr,
+                                                         nullptr, 0, e->comb_stream, e->geo)
+                                    : hipErrorInvalidValue;
+        if (err == hipSuccess) err = hipStreamSynchronize(e->comb_stream);
+        if (err != hipSuccess) rc = CTS_E_HIP;
+    }
+    const auto* res = static_cast<const cts_verify_result*>(e->comb_res);
+    for (size_t i = 0; i < batch.size(); ++i) {
+        batch[i]->rc = rc;
+        if (rc == CTS_OK) batch[i]->out = cts::slice_merge(res + first[i], count[i], slen[i], batch[i]->len);
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -143,6 +217,7 @@ int cts_engine_create(int device, cts_engine** out)
     e->geo.ms_variant = env_int("CTS_MS_VARIANT", e->geo.ms_variant);
     e->geo.small_chunk = env_int("CTS_SMALL_CHUNK", e->geo.small_chunk);
     e->geo.fill_nt = env_int("CTS_FILL_NT", e->geo.fill_nt);
+    e->sync_coalesce = env_int("CTS_SYNC_COALESCE", e->sync_coalesce) ? 1 : 0;
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
         delete e;
         return CTS_E_HIP;
@@ -177,6 +252,12 @@ int cts_engine_destroy(cts_engine* e)
         if (e->batch_desc) (void)hipHostFree(e->batch_desc);
         if (e->batch_res) (void)hipHostFree(e->batch_res);
         if (e->batch_ctr) (void)hipHostFree(e->batch_ctr);
+        if (e->comb_stream) {
+            (void)hipStreamSynchronize(e->comb_stream);
+            (void)hipStreamDestroy(e->comb_stream);
+        }
+        if (e->comb_desc) (void)hipHostFree(e->comb_desc);
+        if (e->comb_res) (void)hipHostFree(e->comb_res);
     }
     delete e;
     return CTS_OK;
@@ -239,6 +320,7 @@ int cts_engine_set_attr(cts_engine* e, int attr, int value)
         if (value < 0 || value > (1 << 24)) return CTS_E_INVALID;
         e->geo.small_chunk = value;
         return CTS_OK;
+    case CTS_ATTR_SYNC_COALESCE: e->sync_coalesce = value ? 1 : 0; return CTS_OK;
     case CTS_ATTR_FILL_NT:
         if (value < 0 || value > 2) return CTS_E_INVALID;
         e->geo.fill_nt = value;
@@ -261,6 +343,7 @@ int cts_engine_get_attr(const cts_engine* e, int attr, int* value)
     case CTS_ATTR_MS_VARIANT: *value = e->geo.ms_variant; return CTS_OK;
     case CTS_ATTR_SMALL_CHUNK: *value = e->geo.small_chunk; return CTS_OK;
     case CTS_ATTR_FILL_NT: *value = e->geo.fill_nt; return CTS_OK;
+    case CTS_ATTR_SYNC_COALESCE: *value = e->sync_coalesce; return CTS_OK;
     default: return CTS_E_INVALID;
     }
 }
@@ -479,6 +562,34 @@ int cts_verify_host_batch(cts_engine* e, const void* const* bufs, const uint32_t
         }
     }
     return err == hipSuccess ? CTS_OK : CTS_E_HIP;
+}
+
+int cts_verify_mapped(cts_engine* e, const void* dev_buf, uint32_t len, uint32_t expected_offset,
+                      cts_verify_result* out)
+{
+    if (e == nullptr || out == nullptr || (dev_buf == nullptr && len != 0)) return CTS_E_INVALID;
+    if (expected_offset >= CTS_PATTERN_PERIOD) return CTS_E_INVALID;
+    cts_sync_req me{static_cast<const uint8_t*>(dev_buf), len, expected_offset, cts_verify_result{}, CTS_OK, false};
+    std::unique_lock<std::mutex> lk(e->comb_mu);
+    e->comb_q.push_back(&me);
+    while (!me.done) {
+        if (e->comb_busy) {
+            e->comb_cv.wait(lk);
+            continue;
+        }
+        // leader: take everyone queued so far (callers that arrive during this launch form the next one)
+        e->comb_busy = true;
+        std::vector<cts_sync_req*> batch;
+        batch.swap(e->comb_q);
+        lk.unlock();
+        run_sync_group(e, batch);
+        lk.lock();
+        for (cts_sync_req* r : batch) r->done = true;
+        e->comb_busy = false;
+        e->comb_cv.notify_all();
+    }
+    *out = me.out;
+    return me.rc;
 }
 
 }  // extern "C"

@@ -197,6 +197,15 @@ class Engine:
         return {"pass": bool(r.pass_), "first_mismatch": r.first_mismatch, "mismatch_bytes": r.mismatch_bytes,
                 "expected": r.expected, "actual": r.actual, "flags": r.flags}
 
+    def verify_mapped(self, dev_ptr: int, length: int, expected_offset: int) -> dict:
+        """cts_verify_mapped: one GPU-addressable buffer verified in place and waited for; concurrent
+        callers (threads) are combined into one launch by the engine."""
+        r = CtsVerifyResult()
+        check("cts_verify_mapped", lib().cts_verify_mapped(self._h, dev_ptr, length, expected_offset,
+                                                           ctypes.byref(r)))
+        return {"pass": bool(r.pass_), "first_mismatch": r.first_mismatch, "mismatch_bytes": r.mismatch_bytes,
+                "expected": r.expected, "actual": r.actual, "flags": r.flags}
+
     def verify_host_batch(self, bufs: Sequence[np.ndarray], expected: Sequence[int],
                           skip_heads: Optional[Sequence[int]] = None):
         n = len(bufs)

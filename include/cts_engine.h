@@ -134,7 +134,8 @@ typedef enum cts_engine_attr {
     CTS_ATTR_FILL_BLOCKS_PER_CU = 7,  /* grid cap of the fill kernels */
     CTS_ATTR_MS_VARIANT = 8,          /* MediaStream receive kernel (cts_media_stream_verify) */
     CTS_ATTR_SMALL_CHUNK = 9,         /* chunked small-buffer walk: buffers per chunk (0 = contiguous) */
-    CTS_ATTR_FILL_NT = 10             /* cts_fill stores: 0 plain, 1 nontemporal, 2 by path (default) */
+    CTS_ATTR_FILL_NT = 10,            /* cts_fill stores: 0 plain, 1 nontemporal, 2 by path (default) */
+    CTS_ATTR_SYNC_COALESCE = 11       /* 1 = SYNC-mode pattern verifies go through cts_verify_mapped */
 } cts_engine_attr;
 int cts_engine_set_attr(cts_engine* engine, int attr, int value);
 /* A non-blocking HIP stream on the engine's device, whatever device the calling
@@ -193,6 +194,16 @@ int cts_counters_read(cts_engine* engine, const void* dev_counters, cts_counters
  * (RtlCompareMemory semantics, ctsIOPattern.cpp:753-774). Thread-safe. */
 int cts_verify_host(cts_engine* engine, const void* host_buf, uint32_t len,
                     uint32_t expected_offset, cts_verify_result* out);
+
+/* The same one-buffer VerifyBuffer (ctsIOPattern.cpp:745-775) for a buffer the
+ * GPU can already address (a cts_host_alloc dev_view, or HBM), verified in
+ * place and waited for. Thread-safe and coalescing: callers that arrive while
+ * a launch is in flight (concurrent connections' CompleteIo, each serialised
+ * per connection by its ctsSocket lock, ctsSocket.h:189) are verified together
+ * in the next single launch, one launch + synchronize for the whole group.
+ * Each caller receives exactly its own buffer's record. */
+int cts_verify_mapped(cts_engine* engine, const void* dev_buf, uint32_t len,
+                      uint32_t expected_offset, cts_verify_result* out);
 
 /* Pinned host arenas (the recv-buffer container of a GPU-verified
  * ctsIoPattern, ctsIOPattern.cpp:156-175): page-locked and mapped into the

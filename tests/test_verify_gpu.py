@@ -332,6 +332,49 @@ def test_verify_host_single_slice_edges(engine):
                 o["pass"], o["first_mismatch"], o["expected"], o["actual"], o["mismatch_bytes"]), (n, trial)
 
 
+def test_verify_mapped_coalesced_threads(engine):
+    """cts_verify_mapped from 16 threads at once (SYNC verifies of concurrent connections): the engine
+    combines whatever is queued into one launch over buffers in separate pinned arenas; every caller
+    must get exactly the oracle's record for its own buffer (ctsIOPattern.cpp:745-775)."""
+    import threading
+    S = oracle.sender_buffer(140000)
+    T, ITERS, CAP = 16, 40, 70000
+    arenas = [engine.host_alloc(CAP) for _ in range(T)]
+    errors = []
+
+    def worker(t):
+        arr, _, dev = arenas[t]
+        rng = np.random.default_rng(0xC0A1 + t)
+        try:
+            for it in range(ITERS):
+                n = int(rng.choice([0, 1, 1023, 1024, 1025, 4097, 65536, 65537, CAP - 16]))
+                e = int(rng.integers(0, 65536))
+                at = int(rng.integers(0, 16)) if n <= CAP - 16 else 0
+                arr[at:at + n] = S[e:e + n]
+                if n and rng.random() < 0.5:
+                    for k in sorted({int(x) for x in rng.integers(0, n, int(rng.integers(1, 4)))}):
+                        arr[at + k] ^= int(rng.integers(1, 256))
+                r = engine.verify_mapped(dev + at, n, e)
+                o = oracle.verify_buffer(arr[at:at + n].copy(), 0, e, n)
+                got = (r["pass"], r["first_mismatch"], r["expected"], r["actual"], r["mismatch_bytes"])
+                want = (o["pass"], o["first_mismatch"], o["expected"], o["actual"], o["mismatch_bytes"])
+                if got != want:
+                    errors.append((t, it, n, e, got, want))
+        except Exception as ex:  # surfaced below
+            errors.append((t, repr(ex)))
+
+    try:
+        ths = [threading.Thread(target=worker, args=(t,)) for t in range(T)]
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+    finally:
+        for _, h, _ in arenas:
+            engine.host_free(h)
+    assert not errors, errors[:5]
+
+
 def test_verify_host_batch(engine):
     """Repeated calls reuse (and grow) the engine's pinned staging: small, larger, small again."""
     for seed, n, max_len in ((5, 100, 3000), (6, 3000, 70000), (7, 17, 200)):

@@ -4,7 +4,7 @@
 // Variants: the buffer described as S slices (S descriptors of 64 KiB / S, expected offsets advanced,
 // so S workgroups/waves issue their PCIe reads at once) and T threads, each with its own stream,
 // buffer, descriptor and result (T connections completing concurrently). Wait = hipStreamSynchronize
-// or a hipStreamQuery spin. Prints one JSON line per variant: us per verify (per thread).
+// or a hipStreamQuery spin, or cts_verify_mapped (the engine combines concurrent callers into one launch). Prints one JSON line per variant: us per verify (per thread).
 //   build: make tools/sync_probe      run: tools/sync_probe [iters]
 #include <hip/hip_runtime_api.h>
 
@@ -18,7 +18,7 @@
 
 #include "cts_engine.h"
 
-static int run_thread(cts_engine* e, uint32_t slices, bool spin, int iters, double* us_out, int* bad)
+static int run_thread(cts_engine* e, uint32_t slices, bool spin, bool mapped, int iters, double* us_out, int* bad)
 {
     void* stream = nullptr;
     if (cts_engine_stream_create(e, &stream) != CTS_OK) return 1;
@@ -34,6 +34,10 @@ static int run_thread(cts_engine* e, uint32_t slices, bool spin, int iters, doub
     auto* res_d = reinterpret_cast<cts_verify_result*>(static_cast<uint8_t*>(dd) + 2048);
     hipStream_t s = static_cast<hipStream_t>(stream);
     auto once = [&]() {
+        if (mapped) {  // cts_verify_mapped: concurrent threads' verifies coalesce into one launch
+            cts_verify_result r{};
+            return cts_verify_mapped(e, dev, len, 1000, &r) == CTS_OK && r.pass && r.first_mismatch == len;
+        }
         if (cts_verify(e, dev, len, static_cast<cts_buf_desc*>(dd), slices, per, res_d, nullptr, nullptr, 0, stream) !=
             CTS_OK)
             return false;
@@ -65,14 +69,17 @@ int main(int argc, char** argv)
     const int iters = argc > 1 ? std::atoi(argv[1]) : 2000;
     cts_engine* e = nullptr;
     if (cts_engine_create(0, &e) != CTS_OK) return 1;
-    for (int spin = 0; spin < 2; ++spin)
-        for (uint32_t threads : {1u, 8u})
+    // wait: 0 stream_sync, 1 query_spin, 2 cts_verify_mapped (coalescing; slices = its own plan, 64)
+    for (int spin = 0; spin < 3; ++spin)
+        for (uint32_t threads : {1u, 8u, 16u})
             for (uint32_t slices : {1u, 2u, 4u, 8u, 16u, 32u, 64u}) {
+                if ((spin == 2) != (slices == 64) && spin == 2) continue;
+                if (threads == 16 && slices != 64) continue;
                 std::vector<double> us(threads, 0.0);
                 std::vector<int> bad(threads, 0), rc(threads, 0);
                 std::vector<std::thread> th;
                 for (uint32_t t = 0; t < threads; ++t)
-                    th.emplace_back([&, t] { rc[t] = run_thread(e, slices, spin != 0, iters, &us[t], &bad[t]); });
+                    th.emplace_back([&, t] { rc[t] = run_thread(e, slices, spin == 1, spin == 2, iters, &us[t], &bad[t]); });
                 for (auto& x : th) x.join();
                 double mean = 0;
                 int nbad = 0, nrc = 0;
@@ -83,7 +90,7 @@ int main(int argc, char** argv)
                 }
                 std::printf("{\"wait\": \"%s\", \"threads\": %u, \"slices\": %u, \"us_per_verify\": %.2f, "
                             "\"GBps_total\": %.2f, \"bad\": %d, \"rc\": %d}\n",
-                            spin ? "query_spin" : "stream_sync", threads, slices, mean,
+                            spin == 2 ? "mapped_coalesced" : spin ? "query_spin" : "stream_sync", threads, slices, mean,
                             threads * 65536.0 / (mean * 1e3), nbad, nrc);
                 std::fflush(stdout);
             }
