@@ -78,7 +78,7 @@ struct SideResult {
     cts_pattern_stats stats{};
 };
 
-void run_side(int* fdslot, cts_io_pattern* p, bool inject, uint32_t inject_index, SideResult* out)
+void run_side(int* fdslot, cts_io_pattern* p, bool inject, uint32_t inject_index, bool recv_whole, SideResult* out)
 {
     const int fd = *fdslot;
     std::vector<char> scratch;
@@ -105,7 +105,8 @@ void run_side(int* fdslot, cts_io_pattern* p, bool inject, uint32_t inject_index
         }
         case CTS_TASK_RECV: {
             // protocol messages are fixed-size; data recvs complete with whatever arrived
-            const bool whole = t.buffer_type == CTS_BUFFER_TCP_CONNECTION_ID ||
+            // (or, with recv_whole, with the whole posted length: deterministic completions)
+            const bool whole = recv_whole || t.buffer_type == CTS_BUFFER_TCP_CONNECTION_ID ||
                                t.buffer_type == CTS_BUFFER_COMPLETION_MESSAGE;
             status = recv_some(fd, t.buffer + t.buffer_offset, t.buffer_length, &transferred, whole);
             break;
@@ -151,6 +152,7 @@ struct AsyncSide {
     cts_io_pattern* p;
     bool inject;
     uint32_t inject_index;
+    bool recv_whole = false;
     uint32_t data_sends = 0;
     std::mutex mu;  // the ctsSocket lock: every pattern call runs under it (ctsSocket.h:189)
     std::condition_variable cv;
@@ -237,7 +239,7 @@ struct AsyncSide {
                     err = send_all(fd, src, t.buffer_length);
                     transferred = err == 0 ? t.buffer_length : 0;
                 } else {
-                    const bool whole = t.buffer_type == CTS_BUFFER_TCP_CONNECTION_ID ||
+                    const bool whole = recv_whole || t.buffer_type == CTS_BUFFER_TCP_CONNECTION_ID ||
                                        t.buffer_type == CTS_BUFFER_COMPLETION_MESSAGE;
                     err = recv_some(fd, t.buffer + t.buffer_offset, t.buffer_length, &transferred, whole);
                 }
@@ -252,13 +254,15 @@ struct AsyncSide {
     }
 };
 
-void run_side_async(int* fdslot, cts_io_pattern* p, bool inject, uint32_t inject_index, SideResult* out)
+void run_side_async(int* fdslot, cts_io_pattern* p, bool inject, uint32_t inject_index, bool recv_whole,
+                    SideResult* out)
 {
     AsyncSide a;
     a.fd = *fdslot;
     a.p = p;
     a.inject = inject;
     a.inject_index = inject_index;
+    a.recv_whole = recv_whole;
     {
         std::lock_guard<std::mutex> lk(a.mu);
         a.pump();
@@ -289,6 +293,13 @@ extern "C" int cts_loopback_run(const cts_loopback_config* cfg, cts_engine* engi
 
 extern "C" int cts_loopback_run_multi(const cts_loopback_config* cfg, cts_engine* const* engines, uint32_t n_engines,
                                       cts_batch_verifier hook, void* hook_ctx, cts_loopback_result* out)
+{
+    return cts_loopback_run_detailed(cfg, engines, n_engines, hook, hook_ctx, out, nullptr);
+}
+
+extern "C" int cts_loopback_run_detailed(const cts_loopback_config* cfg, cts_engine* const* engines,
+                                         uint32_t n_engines, cts_batch_verifier hook, void* hook_ctx,
+                                         cts_loopback_result* out, cts_loopback_side* sides)
 {
     if (cfg == nullptr || out == nullptr || cfg->connections == 0 || cfg->buffer_size == 0) return CTS_E_INVALID;
     if (n_engines > 0 && engines == nullptr) return CTS_E_INVALID;
@@ -390,7 +401,7 @@ extern "C" int cts_loopback_run_multi(const cts_loopback_config* cfg, cts_engine
         if (fds[i] < 0) continue;
         const bool inject = i % n == cfg->corrupt_connection;  // whichever side(s) send data
         threads.emplace_back(async ? run_side_async : run_side, &fds[i], pats[i], inject, cfg->corrupt_send_index,
-                             &res[i]);
+                             cfg->recv_whole != 0, &res[i]);
     }
     const std::vector<bool>& connected = connected0;
     for (auto& t : threads) t.join();
@@ -414,6 +425,12 @@ extern "C" int cts_loopback_run_multi(const cts_loopback_config* cfg, cts_engine
             ++out->data_errors;
         out->buffers_verified += c.stats.buffers_verified + s.stats.buffers_verified;
     }
+    if (sides != nullptr)
+        for (uint32_t i = 0; i < 2 * n; ++i) {
+            sides[i].stats = res[i].stats;
+            sides[i].status = connected[i] ? (uint32_t)res[i].status : (uint32_t)CTS_IO_FAILED;
+            sides[i].last_error = res[i].last_error;
+        }
     for (auto* p : pats) cts_io_pattern_destroy(p);
     return CTS_OK;
 }

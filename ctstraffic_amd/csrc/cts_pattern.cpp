@@ -83,6 +83,9 @@ public:
         return m_maxTransfer - already;
     }
     uint64_t GetMaxTransfer() const { return m_maxTransfer; }
+    // DEFERRED: completions accepted after a buffer that later failed verification are taken back
+    // (the reference never saw them: it failed the connection at that buffer, ctsIOPattern.cpp:486-489)
+    void RollbackConfirmed(uint64_t bytes) { m_confirmedBytes -= std::min(bytes, m_confirmedBytes); }
     void SetMaxTransfer(uint64_t v) { m_maxTransfer = v; }
     uint32_t GetIdealSendBacklog() const { return m_idealSendBacklog; }
     void SetIdealSendBacklog(uint32_t isb) { m_idealSendBacklog = isb; }  // ctsIOPatternState.hpp:155-158
@@ -272,9 +275,11 @@ struct Pinned {
 };
 
 struct Queued {
-    uint32_t completion;     // recv completion index
+    uint32_t completion;        // recv completion index
     uint32_t transferred;
     uint64_t bytes_recv_after;  // m_bytesRecv after this completion (as the reference would count it)
+    uint64_t bytes_sent_after;  // m_bytesSent at that point (sends completed later are rolled back on failure)
+    uint32_t expected;          // the task's m_expectedPatternOffset
 };
 
 }  // namespace
@@ -601,7 +606,7 @@ struct cts_io_pattern {
             if (rc != CTS_OK) return rc;
             cts_buf_desc* descs = hook ? hdesc.data() : reinterpret_cast<cts_buf_desc*>(stage_desc.host);
             descs[queue.size()] = cts_buf_desc{(uint64_t)(src - ring_base), transferred, t.expected_pattern_offset, 0, 0};
-            queue.push_back(Queued{recv_completions, transferred, recv_after});
+            queue.push_back(Queued{recv_completions, transferred, recv_after, bytes_sent, t.expected_pattern_offset});
             queue_in_ring = true;
             return CTS_OK;
         }
@@ -641,7 +646,7 @@ struct cts_io_pattern {
         if (transferred) std::memcpy(base + stage_used, t.buffer + t.buffer_offset, transferred);
         cts_buf_desc* descs = hook ? hdesc.data() : reinterpret_cast<cts_buf_desc*>(stage_desc.host);
         descs[queue.size()] = cts_buf_desc{stage_used, transferred, t.expected_pattern_offset, 0, 0};
-        queue.push_back(Queued{recv_completions, transferred, recv_after});
+        queue.push_back(Queued{recv_completions, transferred, recv_after, bytes_sent, t.expected_pattern_offset});
         stage_used += slot;
         return CTS_OK;
     }
@@ -669,19 +674,46 @@ struct cts_io_pattern {
             if (hipStreamSynchronize(stream) != hipSuccess) return CTS_E_HIP;
             res = reinterpret_cast<const cts_verify_result*>(stage_res.host);
         }
-        bool failed = false;
-        for (uint32_t i = 0; i < n; ++i) {
+        // The reference stops at the first failing buffer (its CompleteIo fails the connection on that
+        // completion, ctsIOPattern.cpp:486-489, and TCP verify allows one posted recv,
+        // ctsConfig.cpp:3440-3446). Buffers queued after it were never received there: they are neither
+        // counted as verified nor as received, and the sends that completed after it are taken back too,
+        // so every counter equals what the reference reports when it stops at that completion.
+        uint32_t bad = n;
+        for (uint32_t i = 0; i < n; ++i)
+            if (!res[i].pass) {
+                bad = i;
+                break;
+            }
+        const uint32_t counted = bad < n ? bad + 1 : n;
+        for (uint32_t i = 0; i < counted; ++i) {
             ++buffers_verified;
             bytes_verified += queue[i].transferred;
-            if (!res[i].pass) {
-                RecordFailure(queue[i].completion, queue[i].transferred, res[i], queue[i].bytes_recv_after);
-                failed = true;
-            }
+        }
+        if (bad < n) {
+            const Queued& f = queue[bad];
+            RecordFailure(f.completion, f.transferred, res[bad], f.bytes_recv_after);
+            RollbackAfter(f);
         }
         queue.clear();
         stage_used = 0;
-        if (failed) UpdateLastError(CTS_STATUS_ERROR_DATA_DID_NOT_MATCH_BIT_PATTERN);
+        if (bad < n) UpdateLastError(CTS_STATUS_ERROR_DATA_DID_NOT_MATCH_BIT_PATTERN);
         return GetCurrentStatus();
+    }
+
+    // Undo the byte accounting (TcpStatusDetails, ctsStatistics, the pattern state and the recv
+    // pattern offset) of every completion after the failing buffer f (DEFERRED; see Flush).
+    void RollbackAfter(const Queued& f)
+    {
+        const uint64_t recv_undo = bytes_recv - f.bytes_recv_after;
+        const uint64_t send_undo = bytes_sent - f.bytes_sent_after;
+        bytes_recv = f.bytes_recv_after;
+        bytes_sent = f.bytes_sent_after;
+        g_bytesRecv.fetch_sub(recv_undo);
+        g_bytesSent.fetch_sub(send_undo);
+        state.RollbackConfirmed(recv_undo + send_undo);
+        m_recvPatternOffset = (uint32_t)(((uint64_t)f.expected + f.transferred) % kPatternSize);
+        recv_completions = f.completion + 1;
     }
 
     bool Deferred() const { return cfg.verify_mode == CTS_VERIFY_DEFERRED; }
@@ -698,8 +730,12 @@ struct cts_io_pattern {
         bool benign = status == kNoError && (t.io_action == CTS_TASK_SEND || t.io_action == CTS_TASK_RECV) &&
                       state.WouldStayMoreIo(t, transfer) && m_lastError == kStatusIoRunning;
         if (Deferred() && !queue.empty() && !benign) {
+            const bool had_failure = has_failure;
             const int rc = Flush();
             if (rc < 0) return rc;
+            // a queued buffer failed: the reference failed the connection at that completion and never
+            // saw this one, so it is not accounted (ctsIOPattern.cpp:486-489)
+            if (has_failure && !had_failure) return GetCurrentStatus();
         }
         const bool wasIoRequestedFromPattern = state.IsCurrentStateMoreIo();
         if (t.buffer_type == CTS_BUFFER_DYNAMIC && t.io_action == CTS_TASK_RECV)

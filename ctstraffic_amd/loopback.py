@@ -16,7 +16,7 @@ class LoopbackConfig(ctypes.Structure):
                 ("verify_mode", ctypes.c_uint32), ("batch_buffers", ctypes.c_uint32),
                 ("corrupt_connection", ctypes.c_uint32), ("corrupt_send_index", ctypes.c_uint32),
                 ("socket_buffer_bytes", ctypes.c_uint32), ("push_bytes", ctypes.c_uint32),
-                ("pull_bytes", ctypes.c_uint32), ("functor", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+                ("pull_bytes", ctypes.c_uint32), ("functor", ctypes.c_uint32), ("recv_whole", ctypes.c_uint32)]
 
 
 FUNCTOR_AUTO, FUNCTOR_SYNC, FUNCTOR_ASYNC = 0, 1, 2
@@ -34,6 +34,16 @@ class LoopbackResult(ctypes.Structure):
         return d
 
 
+class LoopbackSide(ctypes.Structure):
+    _fields_ = [("stats", A.CtsPatternStats), ("status", ctypes.c_uint32), ("last_error", ctypes.c_uint32)]
+
+    def as_dict(self) -> dict:
+        d = self.stats.as_dict()
+        d["status"] = int(self.status)
+        d["final_error"] = int(self.last_error)
+        return d
+
+
 def declare(L: ctypes.CDLL) -> None:
     fn = L.cts_loopback_run
     fn.argtypes = [ctypes.POINTER(LoopbackConfig), ctypes.c_void_p, A.BATCH_VERIFIER, ctypes.c_void_p,
@@ -43,27 +53,38 @@ def declare(L: ctypes.CDLL) -> None:
     fn.argtypes = [ctypes.POINTER(LoopbackConfig), ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint32,
                    A.BATCH_VERIFIER, ctypes.c_void_p, ctypes.POINTER(LoopbackResult)]
     fn.restype = ctypes.c_int
+    fn = L.cts_loopback_run_detailed
+    fn.argtypes = [ctypes.POINTER(LoopbackConfig), ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint32,
+                   A.BATCH_VERIFIER, ctypes.c_void_p, ctypes.POINTER(LoopbackResult), ctypes.POINTER(LoopbackSide)]
+    fn.restype = ctypes.c_int
 
 
 def run(connections=8, buffer_size=65536, transfer_size=1 << 30, engine=None, verifier=None,
         io_pattern=A.PATTERN_PUSH, verify=True, verify_mode=A.VERIFY_DEFERRED, batch_buffers=0,
         corrupt_connection=None, corrupt_send_index=0, socket_buffer_bytes=0, push_bytes=0, pull_bytes=0,
-        functor=FUNCTOR_AUTO) -> dict:
+        functor=FUNCTOR_AUTO, recv_whole=False, sides=False) -> dict:
     """One loopback run. ``engine`` is one Engine or a list of them (one per GPU: connection i verifies on
     engine[cts_shard_of(i, len)]). ``verifier`` (a cts_batch_verifier or a python fn(arena, descs) -> results)
-    replaces the engines' kernel (test harnesses / the CPU baseline)."""
+    replaces the engines' kernel (test harnesses / the CPU baseline). ``recv_whole``: data recvs complete
+    with the whole posted length (deterministic completions). ``sides``: add every side's pattern statistics,
+    status and last error under "sides" (clients [0, connections), servers [connections, 2 connections))."""
     from .pattern import batch_verifier
 
     cfg = LoopbackConfig(connections, io_pattern, buffer_size, int(verify), transfer_size, verify_mode, batch_buffers,
                          0xFFFFFFFF if corrupt_connection is None else corrupt_connection, corrupt_send_index,
-                         socket_buffer_bytes, push_bytes, pull_bytes, functor, 0)
+                         socket_buffer_bytes, push_bytes, pull_bytes, functor, int(recv_whole))
     hook = None
     if verifier is not None:
         hook = verifier if isinstance(verifier, A.BATCH_VERIFIER) else batch_verifier(verifier)
     res = LoopbackResult()
     engines = engine if isinstance(engine, (list, tuple)) else ([] if engine is None else [engine])
     arr = (ctypes.c_void_p * max(1, len(engines)))(*[e._h.value for e in engines])
-    check("cts_loopback_run_multi",
-          lib().cts_loopback_run_multi(ctypes.byref(cfg), arr if engines else None, len(engines),
-                                       hook if hook is not None else A.BATCH_VERIFIER(), None, ctypes.byref(res)))
-    return res.as_dict()
+    side_arr = (LoopbackSide * (2 * connections))() if sides else None
+    check("cts_loopback_run_detailed",
+          lib().cts_loopback_run_detailed(ctypes.byref(cfg), arr if engines else None, len(engines),
+                                          hook if hook is not None else A.BATCH_VERIFIER(), None, ctypes.byref(res),
+                                          side_arr))
+    out = res.as_dict()
+    if sides:
+        out["sides"] = [s.as_dict() for s in side_arr]
+    return out

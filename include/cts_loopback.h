@@ -37,7 +37,9 @@ typedef struct cts_loopback_config {
     uint32_t push_bytes;            /* -PushBytes (PushPull; 0 = buffer_size) */
     uint32_t pull_bytes;            /* -PullBytes (PushPull; 0 = buffer_size) */
     uint32_t functor;               /* cts_loopback_functor */
-    uint32_t reserved;
+    uint32_t recv_whole;            /* 1 = data recvs complete with the whole posted length (MSG_WAITALL-like):
+                                       deterministic completion sizes, so runs with different verifiers can be
+                                       compared counter for counter; 0 = whatever arrived (partial completions) */
 } cts_loopback_config;
 
 typedef enum cts_loopback_functor {
@@ -69,6 +71,20 @@ int cts_loopback_run(const cts_loopback_config* cfg, cts_engine* engine, cts_bat
  * links with each connection on one GPU. n_engines == 0 runs on the hook alone. */
 int cts_loopback_run_multi(const cts_loopback_config* cfg, cts_engine* const* engines, uint32_t n_engines,
                            cts_batch_verifier hook, void* hook_ctx, cts_loopback_result* out);
+
+/* One connection side's outcome: its pattern's statistics (cts_io_pattern_get_stats), the final
+ * cts_io_status its functor saw, and GetLastPatternError(). */
+typedef struct cts_loopback_side {
+    cts_pattern_stats stats;
+    uint32_t status;
+    uint32_t last_error;
+} cts_loopback_side;
+
+/* cts_loopback_run_multi, plus every side's outcome in sides[2 * connections] when sides != NULL:
+ * sides[i] is connection i's client (connecting) side, sides[connections + i] its server side. */
+int cts_loopback_run_detailed(const cts_loopback_config* cfg, cts_engine* const* engines, uint32_t n_engines,
+                              cts_batch_verifier hook, void* hook_ctx, cts_loopback_result* out,
+                              cts_loopback_side* sides);
 
 #ifdef __cplusplus
 } /* extern "C" */

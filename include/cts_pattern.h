@@ -143,7 +143,7 @@ typedef struct cts_pattern_stats {
     uint64_t bytes_recv;          /* m_statistics.m_bytesRecv */
     uint64_t buffers_verified;    /* VerifyBuffer calls that completed */
     uint64_t bytes_verified;      /* sum of their transferred bytes */
-    uint64_t buffers_failed;      /* verify failures (0 or 1 in SYNC mode: the first fails the connection) */
+    uint64_t buffers_failed;      /* verify failures (0 or 1: the first fails the connection) */
     uint64_t bytes_recv_at_failure; /* DEFERRED: m_bytesRecv as it stood right after the failing completion */
     uint32_t recv_pattern_offset; /* m_recvPatternOffset */
     uint32_t send_pattern_offset; /* m_sendPatternOffset */
@@ -202,12 +202,21 @@ int cts_io_pattern_set_ideal_send_backlog(cts_io_pattern* pattern, uint32_t byte
  * the outcome as the reference would have at the first failing completion:
  * latch CTS_STATUS_ERROR_DATA_DID_NOT_MATCH_BIT_PATTERN and record its offset,
  * expected and actual bytes and the recv byte count at that completion.
+ * Completions accepted after the failing buffer (the reference never saw them:
+ * it failed the connection there, ctsIOPattern.cpp:486-489) are taken back:
+ * they are not counted as verified, and their bytes leave the per-connection
+ * statistics, TcpStatusDetails and the pattern state again, so every counter
+ * equals the reference's after a data error. Sends that completed after the
+ * failing recv are taken back the same way.
  * CompleteIo flushes by itself before any completion that is not a plain
  * in-transfer tracked send/recv (connection id, completion message, FIN,
- * a failed IO, the last bytes of the transfer) and when the batch is full, so
- * the connection's final status is exact; completions between a failing
- * buffer and its flush return CTS_IO_CONTINUE where the reference would have
- * returned CTS_IO_FAILED. Returns the current cts_io_status. */
+ * a failed IO, the last bytes of the transfer) and when the batch is full; when
+ * that flush fails a buffer, the completion that triggered it is not processed.
+ * So the connection's final status and counters are exact; the one remaining
+ * difference is timing: completions between a failing buffer and its flush
+ * return CTS_IO_CONTINUE where the reference would have returned
+ * CTS_IO_FAILED (the feeder keeps the socket open until then). Returns the
+ * current cts_io_status. */
 int cts_io_pattern_flush(cts_io_pattern* pattern);
 int cts_io_pattern_get_stats(const cts_io_pattern* pattern, cts_pattern_stats* out);
 /* The message ctsConfig::PrintErrorInfo receives on a verify failure

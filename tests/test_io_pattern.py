@@ -1150,3 +1150,8 @@ def test_random_push_server_stream(make, seed):
     else:
         # deferred: the failure surfaces at the end of its batch (within its batch of 16) or at the final flush
         assert flushed == FailedIo and fail_at + 1 <= len(statuses) <= fail_at + 16
+    # either way every counter is the reference's, which stopped at the failing completion: the completions
+    # a deferred pattern accepted after it are taken back at the flush
+    assert s["bytes_recv"] == recv_at and s["buffers_verified"] == fail_at + 1 and s["buffers_failed"] == 1
+    assert s["bytes_verified"] == recv_at and s["queued"] == 0
+    assert s["recv_pattern_offset"] == (sum(lens[:fail_at + 1])) % 65536

@@ -150,3 +150,86 @@ def test_loopback_two_engines_gpu(engine, pattern):
                              io_pattern=pattern, verify_mode=A.VERIFY_DEFERRED, corrupt_connection=bad,
                              corrupt_send_index=11)
             assert r["data_errors"] == 1 and r["connections_ok"] == 7
+
+
+# ---- counter parity across verify arrangements (SYNC = the reference's timing; DEFERRED must report the same) -------
+def _side_view(r, connections, corrupt):
+    """Everything a run reports that the reference's own run would report identically. With recv_whole every data
+    completion is a whole buffer, so completion sizes do not depend on the socket's timing. The one quantity the
+    reference itself leaves to timing is left out: how many bytes the corrupted connection's *sender* got out (and
+    the error its send saw) before the receiver's reset reached it."""
+    sides = [dict(s) for s in r["sides"]]
+    if corrupt is not None:
+        for k in ("bytes_sent", "final_error", "last_error"):
+            sides[corrupt].pop(k)
+    totals = {k: r[k] for k in ("bytes_recv", "connections_ok", "connections_failed", "data_errors",
+                                "buffers_verified")}
+    if corrupt is None:
+        totals["bytes_sent"] = r["bytes_sent"]
+    return totals, sides
+
+
+def _three_way(run, connections, transfer, corrupt, send_index, arrangements):
+    views = {}
+    for name, kw in arrangements.items():
+        r = run(connections=connections, buffer_size=65536, transfer_size=transfer, recv_whole=True, sides=True,
+                corrupt_connection=corrupt, corrupt_send_index=send_index, **kw)
+        views[name] = _side_view(r, connections, corrupt)
+    names = list(views)
+    for n in names[1:]:
+        assert views[n][0] == views[names[0]][0], (n, views[n][0], views[names[0]][0])
+        for i, (a, b) in enumerate(zip(views[n][1], views[names[0]][1])):
+            assert a == b, (n, i, a, b)
+    return views[names[0]]
+
+
+@pytest.mark.parametrize("corrupt", [None, 3], ids=["clean", "corrupt"])
+def test_deferred_counters_equal_sync_cpu(corrupt):
+    """A data error in DEFERRED mode is found up to a batch later; the flush takes back every completion after the
+    failing buffer, so TcpStatusDetails, every connection's statistics, its failure record, final status and last
+    error equal SYNC's (the reference's timing: ctsIOPattern.cpp:486-489 fails the connection on that completion)."""
+    shared_buffer_attach(_SENDER)
+    hook = A.BATCH_VERIFIER(oracle.batch_verifier_address())
+    arr = {"sync": dict(verifier=hook, verify_mode=A.VERIFY_SYNC),
+           "deferred": dict(verifier=hook, verify_mode=A.VERIFY_DEFERRED, batch_buffers=64),
+           "deferred_py": dict(verifier=_oracle_verifier, verify_mode=A.VERIFY_DEFERRED, batch_buffers=7)}
+    totals, sides = _three_way(loopback.run, 6, 24 * 1024 * 1024 + 4321, corrupt, 150, arr)
+    if corrupt is None:
+        assert totals["data_errors"] == 0 and totals["connections_ok"] == 6
+    else:
+        assert totals["data_errors"] == 1 and totals["connections_ok"] == 5
+        srv = sides[6 + corrupt]
+        # the 151st data buffer carries the flipped byte at len/2: the server stops right there
+        assert srv["has_failure"] == 1 and srv["fail_completion"] == 150 and srv["fail_offset"] == 32768
+        assert srv["buffers_verified"] == 151 and srv["buffers_failed"] == 1
+        assert srv["bytes_recv"] == 151 * 65536 and srv["bytes_recv_at_failure"] == srv["bytes_recv"]
+        assert srv["final_error"] == 2147483644 and srv["queued"] == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("corrupt", [None, 5], ids=["clean", "corrupt"])
+def test_config1_three_arrangements_gpu(engine, corrupt):
+    """BASELINE configs[0] at full size: loopback TCP push, 8 connections x 1 GiB, 64 KiB IO, -verify:data. The CPU
+    oracle answering VerifyBuffer in each receive thread (the reference's arrangement), the GPU per completion
+    (SYNC) and the GPU in batches (DEFERRED) report identical status details, per-connection statistics, failure
+    records, statuses and last errors, clean and with one corrupted connection."""
+    hook = A.BATCH_VERIFIER(oracle.batch_verifier_address())
+
+    def run(**kw):
+        if "verifier" in kw:
+            shared_buffer_attach(_SENDER)
+        return loopback.run(**kw)
+
+    arr = {"cpu_oracle": dict(verifier=hook, verify_mode=A.VERIFY_SYNC),
+           "gpu_sync": dict(engine=engine, verify_mode=A.VERIFY_SYNC),
+           "gpu_deferred": dict(engine=engine, verify_mode=A.VERIFY_DEFERRED)}
+    totals, sides = _three_way(run, 8, 1 << 30, corrupt, 9000, arr)
+    if corrupt is None:
+        assert totals["connections_ok"] == 8 and totals["data_errors"] == 0
+        assert totals["bytes_recv"] == 8 * ((1 << 30) + 37 + 4)
+        assert all(s["buffers_verified"] == 16384 for s in sides[8:])
+    else:
+        assert totals["connections_ok"] == 7 and totals["data_errors"] == 1
+        srv = sides[8 + corrupt]
+        assert srv["fail_completion"] == 9000 and srv["buffers_verified"] == 9001
+        assert srv["bytes_recv"] == 9001 * 65536 and srv["queued"] == 0
