@@ -38,29 +38,79 @@ METRIC = "GiB/s verified, 64 KiB buffers device-resident; % MI355X HBM roofline"
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=200)
-    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--steps", type=int, default=20,
+                   help="timed steps; a step = one rotation over the R arenas = R config-2 batches (R launches)")
+    p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--arenas", type=int, default=8, help="rotated copies of the batch (defeat the 256 MiB MALL)")
     p.add_argument("--buffers", type=int, default=4096)
-    p.add_argument("--cpu-seconds", type=float, default=8.0, help="budget per CPU-baseline leg")
+    p.add_argument("--cpu-seconds", type=float, default=6.0, help="budget per CPU-baseline leg")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extras", action="store_true", help="skip fill / datagram / host-path extras")
-    p.add_argument("--extras-only", default="", help="comma list: fill,datagram,host")
+    p.add_argument("--extras-only", default="", help="comma list: fill,datagram,host,loopback")
     p.add_argument("--stream", choices=["new", "default"], default="default",
                    help="launch stream: a new HIP stream or the device's default stream")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI)")
+    p.add_argument("--engines", type=int, default=0,
+                   help="single-process multi-GPU leg (the ctsTraffic process model): N engines on GPUs 0..N-1 in "
+                        "this one process, one host thread and stream set per GPU, connections by cts_shard_of, "
+                        "counters folded on the host by cts_counters_read_multi (0 = off)")
     p.add_argument("--graph", action="store_true", help="replay the timed steps from a HIP graph (measured: no gain; "
                    "implies --pipeline-streams 1)")
     p.add_argument("--pipeline-streams", type=int, default=3,
-                   help="headline leg: steps round-robin over S engine streams, so one batch's tail overlaps the "
+                   help="headline leg: launches round-robin over S engine streams, so one batch's tail overlaps the "
                         "next batch's ramp-up (1 = serialized launches; tools/overlap_probe.py)")
     p.add_argument("--verify-variant", type=int, default=-1,
-                   help="CTS_ATTR_VERIFY_VARIANT for both legs (-1 = engine default; tools/tune_verify.py)")
-    p.add_argument("--pipeline-blocks-per-cu", type=int, default=0,
-                   help="verify grid cap (CTS_ATTR_BLOCKS_PER_CU) for the pipelined leg; 0 = engine default (4). "
-                        "In bench.py A/B on one box 4 beat 3 (39.3-40.0 vs 39.8-40.3 us per step) and 2 (42.9-43.5)")
+                   help="CTS_ATTR_VERIFY_VARIANT for both legs (-1 = engine default; tuning builds only)")
     return p.parse_args()
+
+
+class Batch:
+    """One GPU's config-2 work: R rotated arenas of one batch (4096 x 64 KiB received buffers), their descriptors,
+    and the product's outputs per arena: the per-buffer records (cts_verify_result, what CompleteIo reads for the
+    pass bit and the first-mismatch report) and the per-connection first-failure slots (the DataError decision,
+    ctsSocketState.cpp:221-232). Every timed launch writes all three outputs plus the counter block."""
+
+    def __init__(self, torch, engine, W, dev, n_buffers, R, conn_ids):
+        self.engine, self.dev, self.R = engine, dev, R
+        self.w = W.tcp_resident(n_buffers=n_buffers)
+        self.conn_ids = np.asarray(conn_ids)  # the node-wide connection of each buffer (one buffer per connection)
+        assert len(self.conn_ids) == n_buffers
+        self.arenas = []
+        for _ in range(R):
+            a, _d = W.materialize(engine, self.w, device=dev)
+            self.arenas.append(a)
+        # descriptors carry the GPU-local connection slot i (conn_ids[i] on the host), so the first-failure
+        # slots of this GPU's connections are one dense array
+        d = self.w.descs.copy()
+        d["conn_index"] = np.arange(n_buffers, dtype=np.uint32)
+        self.descs = torch.from_numpy(d.view(np.uint8).copy()).to(dev)
+        self.first, self.count, self.exp_ctr, self.exp_cff = W.expected_results(self.w)
+        self.results = [engine.new_results(self.w.n) for _ in range(R)]
+        self.cff = [torch.full((self.w.n,), -1, dtype=torch.int32, device=dev) for _ in range(R)]
+        self.counters = engine.new_counters()
+        self.bytes_per_launch = self.w.verified_bytes()
+
+    def launch(self, i, stream):
+        r = i % self.R
+        self.engine.verify(self.arenas[r], self.descs, max_length_hint=self.w.max_length, results=self.results[r],
+                           counters=self.counters, conn_first_fail=self.cff[r], stream=stream)
+
+    def outputs_ok(self):
+        """Every arena's records and first-failure slots equal the analytic outcome of the corruption plan."""
+        from ctstraffic_amd.engine import results_from_device
+
+        ok = True
+        for r in range(self.R):
+            res = results_from_device(self.results[r])
+            exp_pass = self.first < 0
+            ok &= bool(np.array_equal(res["pass"].astype(bool), exp_pass))
+            fail = ~exp_pass
+            ok &= bool(np.array_equal(res["first_mismatch"][fail].astype(np.int64), self.first[fail]))
+            ok &= bool(np.array_equal(res["mismatch_bytes"][fail].astype(np.int64), self.count[fail]))
+            ok &= bool(np.all(res["first_mismatch"][exp_pass] == 65536))
+            ok &= bool(np.array_equal(self.cff[r].cpu().numpy().view(np.uint32), self.exp_cff))
+        return ok
 
 
 def main():
@@ -76,10 +126,16 @@ def main():
     if not torch.cuda.is_available():
         print("bench.py: no HIP device visible", file=sys.stderr)
         sys.exit(2)
+    if args.engines > 0:
+        if world > 1:
+            print("bench.py: --engines is the single-process leg; do not launch it under torch.distributed.run",
+                  file=sys.stderr)
+            sys.exit(2)
+        return main_engines(args, torch)
     gpu = local % torch.cuda.device_count()  # one rank per GPU; ranks share a GPU only in rehearsals
     torch.cuda.set_device(gpu)
     dev = "cuda:%d" % gpu
-    from ctstraffic_amd import Engine, workload as W
+    from ctstraffic_amd import Engine, _lib, workload as W
     from ctstraffic_amd import distributed as D
 
     if world > 1:
@@ -87,25 +143,18 @@ def main():
 
     engine = Engine(gpu)
     if args.verify_variant >= 0:
-        from ctstraffic_amd import _lib as L
-
-        engine.set_attr(L.ATTR_VERIFY_VARIANT, args.verify_variant)
+        engine.set_attr(_lib.ATTR_VERIFY_VARIANT, args.verify_variant)
     stream = torch.cuda.Stream() if args.stream == "new" else torch.cuda.current_stream()
 
     # ---- workload (per rank: weak scaling) --------------------------------------------------
-    # weak scaling: every rank verifies a config-2 batch of its own connections (rank-disjoint
-    # connection ids, so the per-connection DataError decisions never span GPUs)
-    w = W.tcp_resident(n_buffers=args.buffers, conn_base=rank * args.buffers)
+    # every rank verifies a config-2 batch of its own connections (rank-disjoint connection ids, so the
+    # per-connection DataError decisions never span GPUs)
     R = max(1, args.arenas)
-    arenas = []
-    descs = None
-    for _ in range(R):
-        a, d = W.materialize(engine, w, device=dev)
-        arenas.append(a)
-        descs = d
-    first, count, exp_ctr, _ = W.expected_results(w)
-    bytes_per_step = w.verified_bytes()
-    counters = engine.new_counters()
+    B = Batch(torch, engine, W, dev, args.buffers, R, conn_ids=np.arange(args.buffers) + rank * args.buffers)
+    w, counters = B.w, B.counters
+    exp_ctr = B.exp_ctr
+    bytes_per_launch = B.bytes_per_launch
+    bytes_per_step = bytes_per_launch * R
     torch.cuda.synchronize()
 
     def barrier():
@@ -116,61 +165,52 @@ def main():
     graph = None
     if args.graph:
         for i in range(R):  # first launches outside capture (module load, allocator)
-            engine.verify(arenas[i], descs, max_length_hint=w.max_length, counters=counters, stream=stream)
+            B.launch(i, stream)
         torch.cuda.synchronize()
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph, stream=stream):
             for i in range(R):
-                engine.verify(arenas[i], descs, max_length_hint=w.max_length, counters=counters, stream=stream)
+                B.launch(i, stream)
         torch.cuda.synchronize()
 
-    def run_steps(k0, k):
-        """k verify steps starting at rotation index k0 on `stream` (graph replays for whole rotations)."""
-        done = 0
+    def run_steps(k):
+        """k steps (k rotations = k*R launches) on `stream` (graph: one replay per step)."""
         with torch.cuda.stream(stream):
-            if graph is not None and k0 % R == 0:
-                for _ in range(k // R):
+            if graph is not None:
+                for _ in range(k):
                     graph.replay()
-                done = (k // R) * R
-            for i in range(done, k):
-                engine.verify(arenas[(k0 + i) % R], descs, max_length_hint=w.max_length, counters=counters,
-                              stream=stream)
+                return
+            for i in range(k * R):
+                B.launch(i, stream)
 
-    # pipelined steps: batch i on engine stream i mod S (independent arenas; the counter block takes
+    # pipelined steps: launch i on engine stream i mod S (independent arenas; the counter block takes
     # device atomics from every stream), then `stream` waits for all S before anything reads it
     S = 1 if graph is not None else max(1, args.pipeline_streams)
     pipe = [torch.cuda.ExternalStream(engine.stream_create(), device=dev) for _ in range(S)] if S > 1 else []
 
-    from ctstraffic_amd import _lib
-
-    default_bpc = engine.get_attr(_lib.ATTR_BLOCKS_PER_CU)
-    pipe_bpc = args.pipeline_blocks_per_cu if pipe and args.pipeline_blocks_per_cu > 0 else default_bpc
-
-    def run_pipelined(k0, k):
+    def run_pipelined(k):
         if not pipe:
-            run_steps(k0, k)
+            run_steps(k)
             return
-        engine.set_attr(_lib.ATTR_BLOCKS_PER_CU, pipe_bpc)  # read at launch time; launches below are queued
         start = torch.cuda.Event()
         start.record(stream)
         for ps in pipe:
             ps.wait_event(start)
-        for i in range(k):
-            engine.verify(arenas[(k0 + i) % R], descs, max_length_hint=w.max_length, counters=counters,
-                          stream=pipe[i % S].cuda_stream)
+        for i in range(k * R):
+            B.launch(i, pipe[i % S].cuda_stream)
         for ps in pipe:
             ev = torch.cuda.Event()
             ev.record(ps)
             stream.wait_event(ev)
-        engine.set_attr(_lib.ATTR_BLOCKS_PER_CU, default_bpc)
 
     # ---- warmup -------------------------------------------------------------------------------
-    run_steps(0, max(args.warmup, 1))
-    run_pipelined(0, max(args.warmup, 1))
+    run_steps(max(args.warmup, 1))
+    run_pipelined(max(args.warmup, 1))
     torch.cuda.synchronize()
     K = args.steps
+    launches = K * R
 
-    # ---- roofline leg: serialized launches on one stream, HIP events around exactly the K launches.
+    # ---- roofline leg: serialized launches on one stream, HIP events around exactly the K*R launches.
     # This is the per-kernel duration rocprof reports (run with --pipeline-streams 1 for the trace).
     avg_kernel_s = None
     ser_ok = True
@@ -180,13 +220,17 @@ def main():
         ev_b = torch.cuda.Event(enable_timing=True)
         torch.cuda.synchronize()
         ev_a.record(stream)
-        run_steps(0, K)
+        run_steps(K)
         ev_b.record(stream)
         torch.cuda.synchronize()
-        avg_kernel_s = ev_a.elapsed_time(ev_b) / 1e3 / K
-        ser_ok = engine.read_counters(counters) == {k: v * K for k, v in exp_ctr.items()}
+        avg_kernel_s = ev_a.elapsed_time(ev_b) / 1e3 / launches
+        ser_ok = engine.read_counters(counters) == {k: v * launches for k, v in exp_ctr.items()}
 
     engine.reset_counters(counters, stream=stream)
+    for c in B.cff:
+        c.fill_(-1)
+    for r in B.results:
+        r.zero_()
     if world > 1:
         # the counter all-reduce once before the clock starts (communicator and kernel set-up)
         with torch.cuda.stream(stream):
@@ -201,7 +245,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     ev_a.record(stream)
-    run_pipelined(0, K)
+    run_pipelined(K)
     ev_b.record(stream)
     if world > 1:
         # fold the shards on-device and all-reduce the 5 counters over RCCL/xGMI
@@ -211,18 +255,19 @@ def main():
     barrier()
     t1 = time.perf_counter()
     elapsed = D.max_over_ranks(t1 - t0, device=dev)
-    pipe_step_s = ev_a.elapsed_time(ev_b) / 1e3 / K
+    pipe_launch_s = ev_a.elapsed_time(ev_b) / 1e3 / launches
 
-    # S = 1: the events on the launch stream bracket exactly the K launches of the headline leg, and
-    # the average launch duration includes the (graph) dispatch gaps, so it is an upper bound of the
-    # kernel time rocprof reports
+    # S = 1: the events on the launch stream bracket exactly the K*R launches of the headline leg, and the
+    # average launch duration includes the dispatch gaps, so it is an upper bound of the kernel time rocprof
+    # reports
     if avg_kernel_s is None:
-        avg_kernel_s = pipe_step_s
+        avg_kernel_s = pipe_launch_s
     local_ctr = engine.read_counters(counters)
-    parity_ok = ser_ok and local_ctr == {k: v * K for k, v in exp_ctr.items()}
+    outputs_ok = B.outputs_ok()
+    parity_ok = ser_ok and outputs_ok and local_ctr == {k: v * launches for k, v in exp_ctr.items()}
     if world > 1:
         glob = D.counters_dict(ctr_reduced)
-        exp_glob = {f: exp_ctr[f] * K * world for f in exp_ctr}
+        exp_glob = {f: exp_ctr[f] * launches * world for f in exp_ctr}
         parity_ok = parity_ok and glob == exp_glob
         ok_t = torch.tensor([1 if parity_ok else 0], device=dev)
         dist.all_reduce(ok_t, op=dist.ReduceOp.MIN)
@@ -230,7 +275,7 @@ def main():
 
     total_bytes = bytes_per_step * K * world
     value = total_bytes / elapsed / GIB
-    achieved_gbps = bytes_per_step / avg_kernel_s / 1e9
+    achieved_gbps = bytes_per_launch / avg_kernel_s / 1e9
 
     # allreduce latency (separately, outside the headline)
     allreduce_us = None
@@ -247,15 +292,12 @@ def main():
     if rank == 0 and world == 1:
         want = set(x for x in args.extras_only.split(",") if x) or {"fill", "datagram", "host", "loopback"}
         if not args.no_extras:
-            extras = run_extras(engine, torch, W, w, arenas, descs, dev, want)
+            extras = run_extras(engine, torch, W, w, B.arenas, B.descs, dev, want)
         if not args.no_cpu_baseline:
-            cpu = cpu_baseline(arenas[0], w, args.cpu_seconds)
+            cpu = cpu_baseline(B.arenas[0], w, args.cpu_seconds)
 
     traffic, traffic_src = pmc_traffic(w.name, args.buffers)
-    from ctstraffic_amd import _lib
-
-    variant = engine.get_attr(_lib.ATTR_VERIFY_VARIANT)
-    kernel = VERIFY_KERNELS.get(variant, "variant %d" % variant)
+    kernel = verify_kernel_name(engine)
 
     if rank == 0:
         line = {
@@ -273,9 +315,13 @@ def main():
             "data": "synthetic (seeded pattern fill + 1/1024 one-byte corruptions, seeds 0xC75/0xBAD)",
             "config": {
                 "workload": "config2: %d x 64 KiB received buffers resident in HBM per GPU, cts_verify "
-                            "(RtlCompareMemory semantics), %d rotated arenas" % (args.buffers, R),
+                            "(RtlCompareMemory semantics) writing per-buffer records, per-connection first-failure "
+                            "slots and the counter block; a step = one rotation over %d arenas of that batch "
+                            "(%d launches, %d bytes verified per GPU)" % (args.buffers, R, R, bytes_per_step),
                 "buffers_per_gpu": args.buffers,
                 "buffer_bytes": 65536,
+                "verified_bytes_per_launch_per_gpu": bytes_per_launch,
+                "launches_per_step": R,
                 "verified_bytes_per_step_per_gpu": bytes_per_step,
                 "arenas_rotated": R,
                 "pipeline_streams": S,
@@ -292,23 +338,23 @@ def main():
                 "traffic_source": traffic_src,
                 "kernel": kernel,
                 "avg_kernel_us": round(avg_kernel_s * 1e6, 2),
-                "timing": ("HIP events on the launch stream around the K timed launches (%s), / K"
+                "timing": ("HIP events on the launch stream around the K*R timed launches (%s), / (K*R)"
                            % ("HIP-graph replays" if graph is not None else "host launches")) if not pipe else
-                          ("separate serialized leg of K launches on one stream, HIP events around them, / K "
+                          ("separate serialized leg of K*R launches on one stream, HIP events around them, / (K*R) "
                            "(the per-kernel duration rocprof reports); the headline value is the pipelined leg"),
-                "algorithmic_bytes_per_launch": bytes_per_step,
+                "algorithmic_bytes_per_launch": bytes_per_launch,
                 "pipelined": {
                     "streams": S,
-                    "blocks_per_cu": pipe_bpc,
-                    "us_per_step": round(pipe_step_s * 1e6, 2),
-                    "effective_GBps": round(bytes_per_step / pipe_step_s / 1e9, 1),
-                    "frac": round(bytes_per_step / pipe_step_s / 1e9 / HBM_PEAK_GBPS, 4),
-                    "timing": "HIP events around the headline leg's K steps, / K: batch i on engine stream i mod S, "
-                              "so one launch's tail overlaps the next launch's ramp-up",
+                    "us_per_launch": round(pipe_launch_s * 1e6, 2),
+                    "effective_GBps": round(bytes_per_launch / pipe_launch_s / 1e9, 1),
+                    "frac": round(bytes_per_launch / pipe_launch_s / 1e9 / HBM_PEAK_GBPS, 4),
+                    "timing": "HIP events around the headline leg's K*R launches, / (K*R): launch i on engine "
+                              "stream i mod S, so one launch's tail overlaps the next launch's ramp-up",
                 },
             },
             "cpu_baseline": cpu,
-            "parity": {"counters_match_expected": bool(parity_ok), "counters": local_ctr},
+            "parity": {"counters_match_expected": bool(parity_ok), "records_and_first_fail_match": bool(outputs_ok),
+                       "counters": local_ctr},
         }
         if allreduce_us is not None:
             line["allreduce_counters_us"] = round(allreduce_us, 1)
@@ -321,6 +367,88 @@ def main():
     engine.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def main_engines(args, torch):
+    """The ctsTraffic process model on a node: ONE process, one engine per GPU (cts_engine_create(g)), one host
+    thread and stream set per GPU, connections assigned to GPUs by cts_shard_of, counters folded on the host with
+    cts_counters_read_multi. Each GPU verifies a config-2 batch of its own connections (weak scaling, like the
+    torch.distributed leg); value = all bytes / (wall from the common start to the last GPU's end)."""
+    import threading
+
+    from ctstraffic_amd import Engine, workload as W
+    from ctstraffic_amd.engine import counters_read_multi
+
+    G = args.engines
+    if G > torch.cuda.device_count():
+        print("bench.py: --engines %d but %d GPUs are visible" % (G, torch.cuda.device_count()), file=sys.stderr)
+        sys.exit(2)
+    R, S, K = max(1, args.arenas), max(1, args.pipeline_streams), args.steps
+    # the node's connections (G batches' worth), each on GPU cts_shard_of(conn, G)
+    n_conns = args.buffers * G
+    conns = np.arange(n_conns, dtype=np.uint32)
+    owner = W.shard_of(conns, G)
+    ctx = []
+    for g in range(G):
+        torch.cuda.set_device(g)
+        e = Engine(g)
+        mine = conns[owner == g]
+        B = Batch(torch, e, W, "cuda:%d" % g, len(mine), R, conn_ids=mine)
+        streams = [e.stream_create() for _ in range(S)]
+        ctx.append((e, B, streams, len(mine)))
+    for g in range(G):
+        torch.cuda.synchronize(g)
+
+    def run(g, k, out=None, bar=None):
+        e, B, streams, _ = ctx[g]
+        torch.cuda.set_device(g)
+        if bar is not None:
+            bar.wait()
+        t0 = time.perf_counter()
+        for i in range(k * R):
+            B.launch(i, streams[i % S])
+        for s in streams:
+            e.stream_synchronize(s)
+        if out is not None:
+            out[g] = (t0, time.perf_counter())
+
+    for g in range(G):  # warmup
+        run(g, max(args.warmup, 1))
+        ctx[g][0].reset_counters(ctx[g][1].counters)
+    times = [None] * G
+    bar = threading.Barrier(G + 1)
+    th = [threading.Thread(target=run, args=(g, K, times, bar)) for g in range(G)]
+    for t in th:
+        t.start()
+    bar.wait()
+    t_start = time.perf_counter()
+    for t in th:
+        t.join()
+    t_end = max(t[1] for t in times)
+    elapsed = t_end - min(min(t[0] for t in times), t_start)
+    per_gpu = [ctx[g][1].bytes_per_launch * R * K / (times[g][1] - times[g][0]) / GIB for g in range(G)]
+    folded = counters_read_multi([c[0] for c in ctx], [c[1].counters for c in ctx])
+    per = [c[0].read_counters(c[1].counters) for c in ctx]
+    total = sum(c[1].bytes_per_launch for c in ctx) * R * K
+    exp = {k: sum(c[1].exp_ctr[k] for c in ctx) * K * R for k in ctx[0][1].exp_ctr}
+    line = {
+        "metric": METRIC, "value": round(total / elapsed / GIB, 2), "unit": "GiB/s", "n_gpus": G, "steps": K,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / K * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic (as the default leg)",
+        "config": {"workload": "config2 per GPU, single process: %d engines, one host thread + %d streams each, "
+                               "a step = %d launches per GPU" % (G, S, R),
+                   "process_model": "one process, one engine per GPU (the ctsTraffic host model)",
+                   "connections_per_gpu": [c[3] for c in ctx]},
+        "per_gpu_GiBps": [round(x, 1) for x in per_gpu],
+        "parity": {"folded_counters_match_expected": folded == exp,
+                   "fold_equals_sum_of_reads": folded == {k: sum(p[k] for p in per) for k in exp},
+                   "records_and_first_fail_match": all(c[1].outputs_ok() for c in ctx), "counters": folded},
+    }
+    print(json.dumps(line), flush=True)
+    for e, B, streams, _ in ctx:
+        for s in streams:
+            e.stream_destroy(s)
+        e.close()
 
 
 def _time_kernel(torch, fn, steps):
@@ -337,16 +465,11 @@ def _time_kernel(torch, fn, steps):
     return a.elapsed_time(b) / 1e3 / steps
 
 
-VERIFY_KERNELS = {0: "cts::verify_wg_kernel<8,true>", 1: "cts::verify_wg_kernel<4,true>",
-                  2: "cts::verify_wg_kernel<16,true>", 3: "cts::verify_wave_kernel<8,true>",
-                  4: "cts::verify_wg_nb_kernel<8,true>", 5: "cts::verify_wg_nb_kernel<4,true>",
-                  6: "cts::verify_wg_kernel<8,true,true>", 7: "cts::verify_wg_kernel<4,true,true>",
-                  8: "cts::verify_wg_kernel<8,true,true,true>", 9: "cts::verify_wg_kernel<8,true,true,false,true>",
-                  10: "cts::verify_wg_kernel<4,true,true,false,true>",
-                  11: "cts::verify_wg_kernel<4,true,true,false,true,true>",
-                  12: "cts::verify_wg_kernel<8,true,true,false,true,true>",
-                  13: "cts::verify_wg_kernel<2,true,true,false,true,true>",
-                  14: "cts::verify_wg_kernel<1,true,true,false,true,true>"}
+def verify_kernel_name(engine):
+    """Name of the large-buffer verify kernel the engine launches (as rocprofv3 reports it)."""
+    from ctstraffic_amd import _lib
+
+    return _lib.verify_kernel_name(engine.get_attr(_lib.ATTR_VERIFY_VARIANT))
 
 
 def pmc_traffic(workload, buffers):
@@ -468,9 +591,14 @@ def cpu_baseline(arena, w, seconds):
     import oracle
 
     host = arena.cpu().numpy()
-    nthreads = max(1, min(16, os.cpu_count() or 1))
+    # 1 thread, 16 threads (this pool's CPU share per GPU) and every CPU this process may run on
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except Exception:  # pragma: no cover
+        avail = os.cpu_count() or 1
+    counts = sorted({1, min(16, avail), avail})
     legs = {}
-    for nt in (1, nthreads):
+    for nt in counts:
         reps, t0 = 0, time.perf_counter()
         while True:
             oracle.verify_batch(host, w.descs, nthreads=nt, want_results=False)
@@ -479,6 +607,7 @@ def cpu_baseline(arena, w, seconds):
                 break
         el = time.perf_counter() - t0
         legs[nt] = w.verified_bytes() * reps / el / GIB
+    best = max(legs, key=lambda k: legs[k])
     loop = None
     try:
         # the same config-1 loopback run with the oracle answering VerifyBuffer on the CPU (one
@@ -506,14 +635,24 @@ def cpu_baseline(arena, w, seconds):
                 break
     except Exception:
         pass
+    quota = None
+    try:
+        q = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q[0] != "max":
+            quota = round(int(q[0]) / int(q[1]), 2)
+    except Exception:
+        pass
     return {
-        "value": round(legs[nthreads], 2),
+        "value": round(legs[best], 2),
         "unit": "GiB/s",
-        "cores": nthreads,
+        "cores": best,
         "kind": "port",
-        "sample": "config2 batch (%d x 64 KiB, 256 MiB host copy of the same arena), repeated for ~%.0f s per leg"
-                  % (w.n, seconds),
+        "sample": "config2 batch (%d x 64 KiB, 256 MiB host copy of the same arena), repeated for ~%.0f s per leg; "
+                  "the best of %s threads" % (w.n, seconds, "/".join(str(c) for c in counts)),
+        "threads_GiBps": {str(k): round(v, 2) for k, v in legs.items()},
         "single_thread_value": round(legs[1], 2),
+        "cpus_available": avail,
+        "cgroup_cpu_quota": quota,
         "cpu_model": model,
         "loopback_config1": loop,
     }

@@ -48,6 +48,24 @@ ATTR_FILL_NT = 10
 ATTR_SYNC_COALESCE = 11
 
 
+# large-buffer verify kernels by CTS_ATTR_VERIFY_VARIANT, as rocprofv3 names them (13 = the product default; the
+# others exist only in the tuning build, libcts_engine_tuning.so)
+VERIFY_KERNELS = {0: "cts::verify_wg_kernel<8,true>", 1: "cts::verify_wg_kernel<4,true>",
+                  2: "cts::verify_wg_kernel<16,true>", 3: "cts::verify_wave_kernel<8,true>",
+                  4: "cts::verify_wg_nb_kernel<8,true>", 5: "cts::verify_wg_nb_kernel<4,true>",
+                  6: "cts::verify_wg_kernel<8,true,true>", 7: "cts::verify_wg_kernel<4,true,true>",
+                  8: "cts::verify_wg_kernel<8,true,true,true>", 9: "cts::verify_wg_kernel<8,true,true,false,true>",
+                  10: "cts::verify_wg_kernel<4,true,true,false,true>",
+                  11: "cts::verify_wg_kernel<4,true,true,false,true,true>",
+                  12: "cts::verify_wg_kernel<8,true,true,false,true,true>",
+                  13: "cts::verify_wg_kernel<2,true,true,false,true,true>",
+                  14: "cts::verify_wg_kernel<1,true,true,false,true,true>"}
+
+
+def verify_kernel_name(variant: int) -> str:
+    return VERIFY_KERNELS.get(variant, "variant %d" % variant)
+
+
 class CtsError(RuntimeError):
     def __init__(self, fn: str, status: int):
         super().__init__("%s failed: %s (%d)" % (fn, _status_string(status), status))
@@ -108,6 +126,8 @@ def _declare(L: ctypes.CDLL) -> None:
         "cts_counters_device_bytes": ([], ctypes.c_size_t),
         "cts_counters_reset": ([P, P, P], i32),
         "cts_counters_read": ([P, P, ctypes.POINTER(CtsCounters), P], i32),
+        "cts_counters_read_multi": ([ctypes.POINTER(P), ctypes.POINTER(P), ctypes.POINTER(P), u32,
+                                     ctypes.POINTER(CtsCounters)], i32),
         "cts_verify_host": ([P, P, u32, u32, ctypes.POINTER(CtsVerifyResult)], i32),
         "cts_verify_mapped": ([P, P, u32, u32, ctypes.POINTER(CtsVerifyResult)], i32),
         "cts_verify_host_batch": ([P, P, P, P, P, u32, P, ctypes.POINTER(CtsCounters)], i32),

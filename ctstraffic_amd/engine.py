@@ -81,6 +81,19 @@ def _check_outputs(n: int, results, counters) -> None:
                                                                              int(lib().cts_counters_device_bytes())))
 
 
+def counters_read_multi(engines: Sequence["Engine"], blocks, streams=None) -> dict:
+    """cts_counters_read_multi: the node-wide counters of one process's engines (one per GPU), folded on the host."""
+    n = len(engines)
+    E = (ctypes.c_void_p * max(1, n))(*[e._h.value for e in engines])
+    C = (ctypes.c_void_p * max(1, n))(*[_ptr(b) for b in blocks])
+    S = None
+    if streams is not None:
+        S = (ctypes.c_void_p * max(1, n))(*[_stream(s) for s in streams])
+    out = CtsCounters()
+    check("cts_counters_read_multi", lib().cts_counters_read_multi(E, C, S, n, ctypes.byref(out)))
+    return out.as_dict()
+
+
 class Engine:
     """One engine per GPU (cts_engine_create). Thread-safe across streams."""
 
@@ -126,6 +139,10 @@ class Engine:
 
     def stream_destroy(self, stream: int) -> None:
         check("cts_engine_stream_destroy", lib().cts_engine_stream_destroy(self._h, stream))
+
+    def stream_synchronize(self, stream: int) -> None:
+        """Wait for a stream of this engine (the GIL is released while waiting)."""
+        torch.cuda.ExternalStream(stream, device="cuda:%d" % self.device).synchronize()
 
     # ---- fill ----------------------------------------------------------------
     def sender_buffer(self, max_buffer_size: int, stream=None):

@@ -186,6 +186,12 @@ size_t cts_counters_device_bytes(void);
 int cts_counters_reset(cts_engine* engine, void* dev_counters, void* stream);
 /* Folds the shards into *out. Synchronises `stream`. */
 int cts_counters_read(cts_engine* engine, const void* dev_counters, cts_counters* out, void* stream);
+/* The process-wide counters of a node: one process drives one engine per GPU (the reference is one
+ * process per host), and ctsStatsTracking (ctsStatistics.hpp:87-198) is the sum of every engine's
+ * device block, folded on the host. dev_counters[i] belongs to engines[i]; streams may be NULL
+ * (each engine's legacy stream) or hold one stream per engine (each is synchronised). */
+int cts_counters_read_multi(cts_engine* const* engines, const void* const* dev_counters, void* const* streams,
+                            uint32_t n, cts_counters* out);
 
 /* ---- host-buffer drop-in for ctsIoPattern::VerifyBuffer ---------------------- */
 /* Verifies `len` bytes at host_buf + skip_head against the pattern starting at

@@ -46,4 +46,17 @@ int cts_engine_stream_destroy(cts_engine*, void*) { return CTS_E_NO_DEVICE; }
 
 hipError_t hipStreamSynchronize(hipStream_t) { return hipErrorNoDevice; }
 
+// A "device" counter block here is host memory with the device layout (CTS_COUNTER_SHARDS shards of 8 u64,
+// the first 5 used), so the host-side fold of cts_counters_read_multi can be driven without a GPU.
+int cts_counters_read(cts_engine* e, const void* dev_counters, cts_counters* out, void*)
+{
+    if (e == nullptr || dev_counters == nullptr || out == nullptr) return CTS_E_INVALID;
+    const uint64_t* h = static_cast<const uint64_t*>(dev_counters);
+    uint64_t v[5] = {0, 0, 0, 0, 0};
+    for (uint32_t sh = 0; sh < CTS_COUNTER_SHARDS; ++sh)
+        for (int k = 0; k < 5; ++k) v[k] += h[sh * 8 + k];
+    *out = cts_counters{v[0], v[1], v[2], v[3], v[4]};
+    return CTS_OK;
+}
+
 }  // extern "C"
