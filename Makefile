@@ -1,5 +1,7 @@
 # Build the MI355X engine (gfx950) and the CPU oracle.
-#   make            -> ctstraffic_amd/libcts_engine.so + oracle/libcts_oracle.so + the C++ device sample
+#   make            -> ctstraffic_amd/libcts_engine.so (the product: one kernel per path) + the tuning build
+#                      ctstraffic_amd/libcts_engine_tuning.so (every launch variant, for A/B runs and their
+#                      parity tests) + oracle/libcts_oracle.so + the C++ device sample
 #                      (ctstraffic_amd/build/device_verify) + the ceiling/ablation tools
 #   make asm        -> ctstraffic_amd/build/cts_kernels-gfx950.s (disassembly for inspection)
 HIPCC     ?= /opt/rocm/bin/hipcc
@@ -7,16 +9,26 @@ ARCH      ?= gfx950
 HIPFLAGS  ?= -O3 -std=c++17 -fPIC -Wall -Wno-unused-result --offload-arch=$(ARCH) -Iinclude -Ictstraffic_amd/csrc
 CSRC      := ctstraffic_amd/csrc
 ENGINE_SO := ctstraffic_amd/libcts_engine.so
+TUNING_SO := ctstraffic_amd/libcts_engine_tuning.so
 HDRS      := $(wildcard include/*.h) $(wildcard $(CSRC)/*.hpp)
 SRCS      := $(wildcard $(CSRC)/*.hip) $(wildcard $(CSRC)/*.cpp)
 OBJS      := $(patsubst $(CSRC)/%,ctstraffic_amd/build/%.o,$(SRCS))
+# the tuning build recompiles the two TUs that know about launch variants; the rest is shared
+TUNED     := $(CSRC)/cts_kernels.hip $(CSRC)/cts_engine.cpp
+TUNING_OBJS := $(patsubst $(CSRC)/%,ctstraffic_amd/build/tuning/%.o,$(TUNED)) \
+               $(filter-out $(patsubst $(CSRC)/%,ctstraffic_amd/build/%.o,$(TUNED)),$(OBJS))
+# -Bsymbolic: calls between the library's own cts_* entry points bind inside it, so the product and the
+# tuning library can be loaded into one process side by side
+SOFLAGS   := -shared -Wl,-Bsymbolic -Wl,--version-script=$(CSRC)/exports.map
 
 DEVICE_VERIFY := ctstraffic_amd/build/device_verify
 TOOLS := tools/hbm_read_ceiling tools/verify_ablation
 
 SYNC_PROBE := tools/sync_probe
 
-all: $(ENGINE_SO) oracle $(DEVICE_VERIFY) $(TOOLS) $(SYNC_PROBE)
+all: $(ENGINE_SO) $(TUNING_SO) oracle $(DEVICE_VERIFY) $(TOOLS) $(SYNC_PROBE)
+
+tuning: $(TUNING_SO)
 
 # SYNC-mode (per-completion) verify latency probe against the C ABI
 $(SYNC_PROBE): tools/sync_probe.cpp $(ENGINE_SO) include/cts_engine.h
@@ -35,8 +47,15 @@ ctstraffic_amd/build/%.o: $(CSRC)/% $(HDRS)
 	@mkdir -p ctstraffic_amd/build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+ctstraffic_amd/build/tuning/%.o: $(CSRC)/% $(HDRS)
+	@mkdir -p ctstraffic_amd/build/tuning
+	$(HIPCC) $(HIPFLAGS) -DCTS_TUNING=1 -c $< -o $@
+
 $(ENGINE_SO): $(OBJS) $(CSRC)/exports.map
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJS) -Wl,-soname,libcts_engine.so -Wl,--version-script=$(CSRC)/exports.map
+	$(HIPCC) $(HIPFLAGS) $(SOFLAGS) -o $@ $(OBJS) -Wl,-soname,libcts_engine.so
+
+$(TUNING_SO): $(TUNING_OBJS) $(CSRC)/exports.map
+	$(HIPCC) $(HIPFLAGS) $(SOFLAGS) -o $@ $(TUNING_OBJS) -Wl,-soname,libcts_engine_tuning.so
 
 oracle:
 	$(MAKE) -s -C oracle
@@ -46,7 +65,7 @@ asm: $(CSRC)/cts_kernels.hip $(HDRS)
 	$(HIPCC) $(HIPFLAGS) --cuda-device-only -S $< -o ctstraffic_amd/build/cts_kernels-$(ARCH).s
 
 clean:
-	rm -rf ctstraffic_amd/build $(ENGINE_SO) $(TOOLS) $(SYNC_PROBE)
+	rm -rf ctstraffic_amd/build $(ENGINE_SO) $(TUNING_SO) $(TOOLS) $(SYNC_PROBE)
 	$(MAKE) -s -C oracle clean
 
-.PHONY: all oracle asm clean
+.PHONY: all tuning oracle asm clean

@@ -141,7 +141,8 @@ def main():
     if world > 1:
         D.init(args.dist_backend, device=torch.device(dev) if args.dist_backend == "nccl" else None)
 
-    engine = Engine(gpu)
+    # --verify-variant: A/B runs use the tuning build (every launch variant); the product runs variant 13
+    engine = Engine(gpu, tuning=args.verify_variant >= 0)
     if args.verify_variant >= 0:
         engine.set_attr(_lib.ATTR_VERIFY_VARIANT, args.verify_variant)
     stream = torch.cuda.Stream() if args.stream == "new" else torch.cuda.current_stream()

@@ -24,6 +24,9 @@ except Exception:  # pragma: no cover - torch is part of the image
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # CTS_ENGINE_LIB: an alternative in-tree build of the same library (tools/ A/B runs)
 LIB_PATH = os.environ.get("CTS_ENGINE_LIB") or os.path.join(_HERE, "libcts_engine.so")
+# the tuning build: the same C ABI compiled with every launch variant (CTS_TUNING=1, `make tuning`); only
+# the variant parity tests and the tools/ A/B runs load it, next to the product library
+TUNING_LIB_PATH = os.path.join(_HERE, "libcts_engine_tuning.so")
 
 CTS_OK = 0
 CTS_E_INVALID = -1
@@ -99,6 +102,7 @@ class CtsVerifyResult(ctypes.Structure):
 assert ctypes.sizeof(CtsVerifyResult) == 12
 
 _lib = None
+_tuning_lib = None
 
 
 def _status_string(status: int) -> str:
@@ -164,6 +168,20 @@ def lib() -> ctypes.CDLL:
         _declare(L)
         _lib = L
     return _lib
+
+
+def tuning_lib() -> ctypes.CDLL:
+    """Load the tuning build of the engine (every launch variant). Linked with -Bsymbolic, so it keeps its own
+    entry points even with the product library loaded globally."""
+    global _tuning_lib
+    if _tuning_lib is None:
+        lib()  # the product library first: torch's HIP runtime, then ours
+        if not os.path.exists(TUNING_LIB_PATH):
+            raise ImportError("ctstraffic_amd: %s not built — run `make tuning`" % TUNING_LIB_PATH)
+        L = ctypes.CDLL(TUNING_LIB_PATH, mode=ctypes.RTLD_LOCAL)
+        _declare(L)
+        _tuning_lib = L
+    return _tuning_lib
 
 
 def check(fn: str, status: int) -> None:

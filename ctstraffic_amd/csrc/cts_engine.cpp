@@ -39,7 +39,8 @@ struct cts_engine {
     std::condition_variable comb_cv;
     std::vector<struct cts_sync_req*> comb_q;  // waiting for the next launch
     bool comb_busy = false;
-    int sync_coalesce = 0;                     // CTS_ATTR_SYNC_COALESCE (read by cts_pattern's SYNC verify)                    // a leader owns comb_stream and the comb_* staging
+    int sync_coalesce = 0;  // CTS_ATTR_SYNC_COALESCE (read by cts_pattern's SYNC verify)
+    // a leader owns comb_stream and the comb_* staging
     hipStream_t comb_stream = nullptr;
     void* comb_desc = nullptr;
     size_t comb_desc_cap = 0;
@@ -178,7 +179,13 @@ void run_sync_group(cts_engine* e, const std::vector<cts_sync_req*>& batch)
 
 extern "C" {
 
-const char* cts_version(void) { return "ctstraffic_amd 0.1.0 (gfx950)"; }
+#if CTS_TUNING
+#define cts_variant_count(k) cts::k
+const char* cts_version(void) { return "ctstraffic_amd 0.2.0 (gfx950, tuning build: every launch variant)"; }
+#else
+#define cts_variant_count(k) 0
+const char* cts_version(void) { return "ctstraffic_amd 0.2.0 (gfx950)"; }
+#endif
 
 const char* cts_status_string(int status)
 {
@@ -217,6 +224,13 @@ int cts_engine_create(int device, cts_engine** out)
     e->geo.ms_variant = env_int("CTS_MS_VARIANT", e->geo.ms_variant);
     e->geo.small_chunk = env_int("CTS_SMALL_CHUNK", e->geo.small_chunk);
     e->geo.fill_nt = env_int("CTS_FILL_NT", e->geo.fill_nt);
+    // a variant this build does not compile falls back to the default (the product build has one per path)
+    if (!cts::variant_ok(e->geo.verify_variant, cts::kDefaultVerifyVariant, cts_variant_count(kVerifyVariants)))
+        e->geo.verify_variant = cts::kDefaultVerifyVariant;
+    if (!cts::variant_ok(e->geo.small_variant, cts::kDefaultSmallVariant, cts_variant_count(kSmallVariants)))
+        e->geo.small_variant = cts::kDefaultSmallVariant;
+    if (!cts::variant_ok(e->geo.ms_variant, cts::kDefaultMediaStreamVariant, cts_variant_count(kMediaStreamVariants)))
+        e->geo.ms_variant = cts::kDefaultMediaStreamVariant;
     e->sync_coalesce = env_int("CTS_SYNC_COALESCE", e->sync_coalesce) ? 1 : 0;
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
         delete e;
@@ -297,7 +311,7 @@ int cts_engine_set_attr(cts_engine* e, int attr, int value)
         e->geo.small_threshold = value;
         return CTS_OK;
     case CTS_ATTR_VERIFY_VARIANT:
-        if (value < 0 || value >= cts::kVerifyVariants) return CTS_E_INVALID;
+        if (!cts::variant_ok(value, cts::kDefaultVerifyVariant, cts_variant_count(kVerifyVariants))) return CTS_E_INVALID;
         e->geo.verify_variant = value;
         return CTS_OK;
     case CTS_ATTR_SMALL_BLOCKS_PER_CU:
@@ -305,7 +319,7 @@ int cts_engine_set_attr(cts_engine* e, int attr, int value)
         e->geo.small_blocks_per_cu = value;
         return CTS_OK;
     case CTS_ATTR_SMALL_VARIANT:
-        if (value < 0 || value >= cts::kSmallVariants) return CTS_E_INVALID;
+        if (!cts::variant_ok(value, cts::kDefaultSmallVariant, cts_variant_count(kSmallVariants))) return CTS_E_INVALID;
         e->geo.small_variant = value;
         return CTS_OK;
     case CTS_ATTR_FILL_BLOCKS_PER_CU:
@@ -313,7 +327,8 @@ int cts_engine_set_attr(cts_engine* e, int attr, int value)
         e->geo.fill_blocks_per_cu = value;
         return CTS_OK;
     case CTS_ATTR_MS_VARIANT:
-        if (value < 0 || value >= cts::kMediaStreamVariants) return CTS_E_INVALID;
+        if (!cts::variant_ok(value, cts::kDefaultMediaStreamVariant, cts_variant_count(kMediaStreamVariants)))
+            return CTS_E_INVALID;
         e->geo.ms_variant = value;
         return CTS_OK;
     case CTS_ATTR_SMALL_CHUNK:

@@ -15,9 +15,31 @@ namespace cts {
 constexpr int kCounterSlots = 8;  // 5 used, padded to one 64-byte line
 enum CounterSlot { kBytesChecked = 0, kBytesOk = 1, kBuffersChecked = 2, kBuffersFailed = 3, kMismatchedBytes = 4 };
 
+// The product library compiles one kernel per path, the defaults below. The tuning build
+// (CTS_TUNING=1: libcts_engine_tuning.so, `make tuning`) also compiles every variant measured on the
+// way to them, for A/B runs (tools/tune_verify.py, tools/media_stream_probe.py) and their parity tests.
+#ifndef CTS_TUNING
+#define CTS_TUNING 0
+#endif
+constexpr int kDefaultVerifyVariant = 13;
+constexpr int kDefaultSmallVariant = 9;
+constexpr int kDefaultMediaStreamVariant = 3;
+#if CTS_TUNING
 constexpr int kVerifyVariants = 18;  // workgroup-per-buffer verify variants (launch_verify)
 constexpr int kSmallVariants = 10;   // small-buffer (datagram) verify variants
 constexpr int kMediaStreamVariants = 4;  // MediaStream receive kernels (launch_media_stream_verify)
+#endif
+// A launch-variant attribute value this build can launch.
+inline bool variant_ok(int value, int dflt, int count)
+{
+#if CTS_TUNING
+    (void)dflt;
+    return value >= 0 && value < count;
+#else
+    (void)count;
+    return value == dflt;
+#endif
+}
 
 struct LaunchGeometry {
     int num_cus = 256;        // hipDeviceAttributeMultiprocessorCount
@@ -27,10 +49,10 @@ struct LaunchGeometry {
     int small_blocks_per_cu = 64; // wave-per-buffer grid cap
     int nontemporal = 1;      // nt loads for the once-read verify stream
     int small_threshold = 8192;  // max_length_hint <= this -> small-buffer path
-    int small_variant = 9;       // small-buffer path kernel (launch_verify_nt; 7 = four buffers per wave, line-aligned U6:
+    int small_variant = kDefaultSmallVariant;       // small-buffer path kernel (launch_verify_nt; 7 = four buffers per wave, line-aligned U6:
                                  // config 3 at 5.95 TB/s of payload vs 4.71 for one wave per datagram; 9 = 7 walking
                                  // block-contiguous ranges: 0-5 % faster, results +2 %; tools/media_stream_probe.py)
-    int ms_variant = 3;          // MediaStream receive kernel (launch_media_stream_verify; 3 = four datagrams per wave,
+    int ms_variant = kDefaultMediaStreamVariant;          // MediaStream receive kernel (launch_media_stream_verify; 3 = four datagrams per wave,
                                  // 16-B header chunks + DPP, block-contiguous: with records + results 1.04-1.08 ms per
                                  // 4 M datagrams vs 1.24 ms for variant 1 before output staging)
     int small_chunk = 0;         // chunked walk of small variant 9 / MediaStream variant 3: buffers per chunk (0 = one
@@ -38,7 +60,7 @@ struct LaunchGeometry {
     int fill_nt = 2;             // fill store policy: 0 plain, 1 nontemporal, 2 by path (plain for the workgroup
                                  // path, nontemporal for datagrams; tools/tune_verify.py --op fill)
     int fill_blocks_per_cu = 1;  // fill grid cap (write-bound; plain stores: 1 measured best, 48.7 vs 49.1-49.4 us)
-    int verify_variant = 13;     // see launch_verify (13: variant 11 at U2; 11: variant 10 + in-register exact diff;
+    int verify_variant = kDefaultVerifyVariant;     // see launch_verify (13: variant 11 at U2; 11: variant 10 + in-register exact diff;
                                  // 10: even-phase stream + whole-line spans, U4, measured 1.3-3 % faster than 6,
                                  // which was +0.3-0.7 % over 0)
 };

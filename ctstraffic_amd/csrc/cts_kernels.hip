@@ -1686,6 +1686,7 @@ static inline uint32_t grid_for(uint32_t n, int teams_per_block, const LaunchGeo
     return (uint32_t)(g == 0 ? 1 : g);
 }
 
+#if CTS_TUNING
 // workgroup-per-buffer grid for a WIN-window walk: grid_for's size rounded down to a multiple of
 // WIN (at least WIN), so every window gets gridDim.x / WIN workgroups
 static inline uint32_t grid_win(uint32_t n, uint32_t win, const LaunchGeometry& geo)
@@ -1693,6 +1694,7 @@ static inline uint32_t grid_win(uint32_t n, uint32_t win, const LaunchGeometry& 
     const uint32_t g = grid_for(n, 1, geo);
     return g < win ? win : g - g % win;
 }
+#endif
 
 #define CTS_VERIFY_ARGS arena, arena_bytes, descs, n, results, counters, conn_first_fail, n_conns
 
@@ -1726,6 +1728,7 @@ static void launch_verify_nt(const uint8_t* arena, uint64_t arena_bytes, const c
         // 3 = pipelined across buffers U2, 4 = pipelined U1,
         // 5 = four buffers per wave (16-lane teams) U6, 6 = same, line-aligned rounds U7,
         // 7 = line-aligned U6, 8 = U4, 9 = variant 7 walking block-contiguous buffer ranges
+#if CTS_TUNING
         const uint32_t grid = grid_for(n, kBlock / 64, geo);
         const uint32_t qgrid = grid_for(n, kBlock / kQuadTeam, geo);
         switch (geo.small_variant) {
@@ -1744,6 +1747,10 @@ static void launch_verify_nt(const uint8_t* arena, uint64_t arena_bytes, const c
         case 4: verify_wave_pipe_kernel<1, NT><<<grid, kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         default: verify_wave_kernel<2, NT><<<grid, kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         }
+#else
+        const ContigGrid cg = contig_grid(n, geo);  // small variant 9 (kDefaultSmallVariant)
+        verify_quad_kernel<6, NT, true, true><<<cg.grid, kBlock, 0, stream>>>(CTS_VERIFY_ARGS, cg.per);
+#endif
     } else {
         // variant (large path): 0 = workgroup/buffer U8, 1 = U4, 2 = U16, 3 = wave/buffer U8,
         // 4 = barrier-free workgroup/buffer U8, 5 = barrier-free U4,
@@ -1752,6 +1759,7 @@ static void launch_verify_nt(const uint8_t* arena, uint64_t arena_bytes, const c
         // 9 = variant 6 + whole-line spans streamed without edge/head/tail handling, 10 = same U4,
         // 11 = variant 10 with the exact diff of whole-line spans in registers (no re-read), 12 = same U8,
         // 13 = same U2, 14 = same U1, 15/16/17 = variant 13 walking 2/4/8 windows of the descriptor list
+#if CTS_TUNING
         switch (geo.verify_variant) {
         case 4: verify_wg_nb_kernel<8, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 5: verify_wg_nb_kernel<4, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
@@ -1772,6 +1780,10 @@ static void launch_verify_nt(const uint8_t* arena, uint64_t arena_bytes, const c
         case 3: verify_wave_kernel<8, NT><<<grid_for(n, kBlock / 64, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         default: verify_wg_kernel<8, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         }
+#else
+        // verify variant 13 (kDefaultVerifyVariant)
+        verify_wg_kernel<2, NT, true, false, true, true><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS);
+#endif
     }
 }
 
@@ -1823,6 +1835,7 @@ hipError_t launch_media_stream_verify(const uint8_t* arena, uint64_t arena_bytes
     const uint32_t qgrid = grid_for(n, kBlock / kQuadTeam, geo);
     const uint32_t grid = grid_for(n, kBlock / 64, geo);
     const bool nt = geo.nontemporal != 0;
+#if CTS_TUNING
     switch (geo.ms_variant) {
     case 0:
         if (nt) media_stream_verify_kernel<2, true><<<grid, kBlock, 0, stream>>>(CTS_MS_ARGS);
@@ -1847,6 +1860,15 @@ hipError_t launch_media_stream_verify(const uint8_t* arena, uint64_t arena_bytes
         break;
     }
     }
+#else
+    (void)qgrid;
+    (void)grid;
+    const ContigGrid cg = contig_grid(n, geo);  // MediaStream variant 3 (kDefaultMediaStreamVariant)
+    if (nt)
+        media_stream_verify_quad_kernel<6, true, true, true, true><<<cg.grid, kBlock, 0, stream>>>(CTS_MS_ARGS, cg.per);
+    else
+        media_stream_verify_quad_kernel<6, false, true, true, true><<<cg.grid, kBlock, 0, stream>>>(CTS_MS_ARGS, cg.per);
+#endif
 #undef CTS_MS_ARGS
     return hipGetLastError();
 }

@@ -97,16 +97,20 @@ def counters_read_multi(engines: Sequence["Engine"], blocks, streams=None) -> di
 class Engine:
     """One engine per GPU (cts_engine_create). Thread-safe across streams."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, tuning: bool = False):
+        """``tuning``: an engine of the tuning build (libcts_engine_tuning.so, every launch variant) for A/B runs
+        and variant parity tests; the product library launches one kernel per path."""
+        self._L = _lib.tuning_lib() if tuning else lib()
+        self.tuning = tuning
         h = ctypes.c_void_p()
-        check("cts_engine_create", lib().cts_engine_create(device, ctypes.byref(h)))
+        check("cts_engine_create", self._L.cts_engine_create(device, ctypes.byref(h)))
         self._h = h
         self.device = device
 
     # ---- lifetime ----------------------------------------------------------
     def close(self) -> None:
         if getattr(self, "_h", None) is not None and self._h.value:
-            lib().cts_engine_destroy(self._h)
+            self._L.cts_engine_destroy(self._h)
             self._h = None
 
     def __enter__(self):
@@ -123,22 +127,22 @@ class Engine:
 
     # ---- launch attributes ----------------------------------------------------
     def set_attr(self, attr: int, value: int) -> None:
-        check("cts_engine_set_attr", lib().cts_engine_set_attr(self._h, attr, value))
+        check("cts_engine_set_attr", self._L.cts_engine_set_attr(self._h, attr, value))
 
     def get_attr(self, attr: int) -> int:
         v = ctypes.c_int()
-        check("cts_engine_get_attr", lib().cts_engine_get_attr(self._h, attr, ctypes.byref(v)))
+        check("cts_engine_get_attr", self._L.cts_engine_get_attr(self._h, attr, ctypes.byref(v)))
         return v.value
 
     # ---- streams ---------------------------------------------------------------
     def stream_create(self) -> int:
         """A non-blocking HIP stream on the engine's device (cts_engine_stream_create); raw handle."""
         p = ctypes.c_void_p()
-        check("cts_engine_stream_create", lib().cts_engine_stream_create(self._h, ctypes.byref(p)))
+        check("cts_engine_stream_create", self._L.cts_engine_stream_create(self._h, ctypes.byref(p)))
         return p.value
 
     def stream_destroy(self, stream: int) -> None:
-        check("cts_engine_stream_destroy", lib().cts_engine_stream_destroy(self._h, stream))
+        check("cts_engine_stream_destroy", self._L.cts_engine_stream_destroy(self._h, stream))
 
     def stream_synchronize(self, stream: int) -> None:
         """Wait for a stream of this engine (the GIL is released while waiting)."""
@@ -150,12 +154,12 @@ class Engine:
         n = sender_buffer_size(max_buffer_size)
         out = torch.empty(n + 16, dtype=torch.uint8, device="cuda:%d" % self.device)[:n]
         check("cts_sender_buffer_fill",
-              lib().cts_sender_buffer_fill(self._h, _ptr(out), max_buffer_size, _stream(stream)))
+              self._L.cts_sender_buffer_fill(self._h, _ptr(out), max_buffer_size, _stream(stream)))
         return out
 
     def fill(self, arena, descs, max_length_hint: int = 0, stream=None) -> None:
         n = _nbytes(descs) // DESC_DTYPE.itemsize
-        check("cts_fill", lib().cts_fill(self._h, _ptr(arena), _nbytes(arena), _ptr(descs), n, max_length_hint,
+        check("cts_fill", self._L.cts_fill(self._h, _ptr(arena), _nbytes(arena), _ptr(descs), n, max_length_hint,
                                          _stream(stream)))
 
     # ---- verify --------------------------------------------------------------
@@ -164,7 +168,7 @@ class Engine:
         n = _nbytes(descs) // DESC_DTYPE.itemsize
         n_conns = 0 if conn_first_fail is None else _nbytes(conn_first_fail) // 4
         _check_outputs(n, results, counters)
-        check("cts_verify", lib().cts_verify(self._h, _ptr(arena), _nbytes(arena), _ptr(descs), n, max_length_hint,
+        check("cts_verify", self._L.cts_verify(self._h, _ptr(arena), _nbytes(arena), _ptr(descs), n, max_length_hint,
                                              _ptr(results), _ptr(counters), _ptr(conn_first_fail), n_conns,
                                              _stream(stream)))
 
@@ -173,15 +177,15 @@ class Engine:
 
     # ---- counters --------------------------------------------------------------
     def new_counters(self):
-        nbytes = int(lib().cts_counters_device_bytes())
+        nbytes = int(self._L.cts_counters_device_bytes())
         return torch.zeros(nbytes // 8, dtype=torch.int64, device="cuda:%d" % self.device)
 
     def reset_counters(self, counters, stream=None) -> None:
-        check("cts_counters_reset", lib().cts_counters_reset(self._h, _ptr(counters), _stream(stream)))
+        check("cts_counters_reset", self._L.cts_counters_reset(self._h, _ptr(counters), _stream(stream)))
 
     def read_counters(self, counters, stream=None) -> dict:
         c = CtsCounters()
-        check("cts_counters_read", lib().cts_counters_read(self._h, _ptr(counters), ctypes.byref(c),
+        check("cts_counters_read", self._L.cts_counters_read(self._h, _ptr(counters), ctypes.byref(c),
                                                            _stream(stream)))
         return c.as_dict()
 
@@ -189,19 +193,19 @@ class Engine:
     def host_alloc(self, nbytes: int):
         """Pinned, device-mapped host arena. Returns (numpy uint8 view, host ptr, device-view ptr)."""
         h, d = ctypes.c_void_p(), ctypes.c_void_p()
-        check("cts_host_alloc", lib().cts_host_alloc(self._h, nbytes, ctypes.byref(h), ctypes.byref(d)))
+        check("cts_host_alloc", self._L.cts_host_alloc(self._h, nbytes, ctypes.byref(h), ctypes.byref(d)))
         arr = np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(h.value))
         return arr, h.value, d.value
 
     def host_free(self, host_ptr: int) -> None:
-        check("cts_host_free", lib().cts_host_free(self._h, host_ptr))
+        check("cts_host_free", self._L.cts_host_free(self._h, host_ptr))
 
     def verify_ptr(self, arena_ptr: int, arena_bytes: int, descs, *, max_length_hint: int = 0, results=None,
                    counters=None, stream=None) -> None:
         """cts_verify on a raw device address (e.g. the device view of a pinned host arena)."""
         n = _nbytes(descs) // DESC_DTYPE.itemsize
         _check_outputs(n, results, counters)
-        check("cts_verify", lib().cts_verify(self._h, arena_ptr, arena_bytes, _ptr(descs), n, max_length_hint,
+        check("cts_verify", self._L.cts_verify(self._h, arena_ptr, arena_bytes, _ptr(descs), n, max_length_hint,
                                              _ptr(results), _ptr(counters), None, 0, _stream(stream)))
 
     # ---- host buffers (drop-in VerifyBuffer) ------------------------------------
@@ -209,7 +213,7 @@ class Engine:
         a = np.frombuffer(bytes(buf), dtype=np.uint8) if not isinstance(buf, np.ndarray) else buf
         a = np.ascontiguousarray(a, dtype=np.uint8)
         r = CtsVerifyResult()
-        check("cts_verify_host", lib().cts_verify_host(self._h, a.ctypes.data if a.size else None, a.size,
+        check("cts_verify_host", self._L.cts_verify_host(self._h, a.ctypes.data if a.size else None, a.size,
                                                        expected_offset, ctypes.byref(r)))
         return {"pass": bool(r.pass_), "first_mismatch": r.first_mismatch, "mismatch_bytes": r.mismatch_bytes,
                 "expected": r.expected, "actual": r.actual, "flags": r.flags}
@@ -218,7 +222,7 @@ class Engine:
         """cts_verify_mapped: one GPU-addressable buffer verified in place and waited for; concurrent
         callers (threads) are combined into one launch by the engine."""
         r = CtsVerifyResult()
-        check("cts_verify_mapped", lib().cts_verify_mapped(self._h, dev_ptr, length, expected_offset,
+        check("cts_verify_mapped", self._L.cts_verify_mapped(self._h, dev_ptr, length, expected_offset,
                                                            ctypes.byref(r)))
         return {"pass": bool(r.pass_), "first_mismatch": r.first_mismatch, "mismatch_bytes": r.mismatch_bytes,
                 "expected": r.expected, "actual": r.actual, "flags": r.flags}
@@ -234,7 +238,7 @@ class Engine:
         results = np.zeros(n, dtype=RESULT_DTYPE)
         c = CtsCounters()
         check("cts_verify_host_batch",
-              lib().cts_verify_host_batch(self._h, ptrs, lens.ctypes.data, exp.ctypes.data,
+              self._L.cts_verify_host_batch(self._h, ptrs, lens.ctypes.data, exp.ctypes.data,
                                           None if skips is None else skips.ctypes.data, n, results.ctypes.data,
                                           ctypes.byref(c)))
         return results, c.as_dict()

@@ -78,6 +78,8 @@ def run(connections=8, buffer_size=65536, transfer_size=1 << 30, engine=None, ve
         hook = verifier if isinstance(verifier, A.BATCH_VERIFIER) else batch_verifier(verifier)
     res = LoopbackResult()
     engines = engine if isinstance(engine, (list, tuple)) else ([] if engine is None else [engine])
+    if any(getattr(e, "tuning", False) for e in engines):
+        raise ValueError("the loopback feeder drives product engines only")
     arr = (ctypes.c_void_p * max(1, len(engines)))(*[e._h.value for e in engines])
     side_arr = (LoopbackSide * (2 * connections))() if sides else None
     check("cts_loopback_run_detailed",

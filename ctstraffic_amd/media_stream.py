@@ -85,7 +85,7 @@ def fill(engine, arena, descs, headers, stream=None) -> None:
 
     n = _nbytes(descs) // DESC_DTYPE.itemsize
     assert _nbytes(headers) // DGRAM_HEADER_DTYPE.itemsize == n
-    check("cts_media_stream_fill", lib().cts_media_stream_fill(engine._h, _ptr(arena), _nbytes(arena), _ptr(descs),
+    check("cts_media_stream_fill", engine._L.cts_media_stream_fill(engine._h, _ptr(arena), _nbytes(arena), _ptr(descs),
                                                                _ptr(headers), n, _stream(stream)))
 
 
@@ -98,7 +98,7 @@ def verify(engine, arena, descs, records=None, results=None, counters=None, stre
         raise ValueError("records holds %d bytes, %d datagrams need %d" % (_nbytes(records), n,
                                                                           n * DGRAM_RECORD_DTYPE.itemsize))
     check("cts_media_stream_verify",
-          lib().cts_media_stream_verify(engine._h, _ptr(arena), _nbytes(arena), _ptr(descs), n, _ptr(records),
+          engine._L.cts_media_stream_verify(engine._h, _ptr(arena), _nbytes(arena), _ptr(descs), n, _ptr(records),
                                         _ptr(results), _ptr(counters), _stream(stream)))
 
 

@@ -92,7 +92,7 @@ class IoPattern:
         self._cfg = config.to_c()
         h = ctypes.c_void_p()
         check("cts_io_pattern_create",
-              lib().cts_io_pattern_create(ctypes.byref(self._cfg), None if engine is None else engine._h,
+              lib().cts_io_pattern_create(ctypes.byref(self._cfg), None if engine is None else _product(engine),
                                           ctypes.byref(h)))
         self._h = h
         self._hook = None
@@ -177,7 +177,7 @@ class IoPattern:
 
 
 def shared_buffer_init(engine, max_buffer_size: int) -> None:
-    check("cts_shared_buffer_init", lib().cts_shared_buffer_init(engine._h, max_buffer_size))
+    check("cts_shared_buffer_init", lib().cts_shared_buffer_init(_product(engine), max_buffer_size))
 
 
 def shared_buffer_attach(buf: np.ndarray) -> None:
@@ -197,3 +197,10 @@ def status_details() -> dict:
 
 def status_details_reset() -> None:
     lib().cts_status_details_reset()
+
+
+def _product(engine):
+    """The pattern mirror belongs to the product library: it takes product engines only."""
+    if getattr(engine, "tuning", False):
+        raise ValueError("a tuning-build engine cannot drive the product library's ctsIoPattern mirror")
+    return engine._h

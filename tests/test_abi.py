@@ -236,3 +236,26 @@ def test_python_handle_refuses_short_output_buffers():
     with pytest.raises(ValueError):
         E._check_outputs(1, None, np.zeros(8, np.uint8))
     E._check_outputs(10, np.zeros(10 * RESULT_DTYPE.itemsize, np.uint8), np.zeros(64 * 64, np.uint8))
+
+
+def _kernels(path):
+    import re
+
+    blob = open(path, "rb").read()
+    return set(m.decode() for m in re.findall(rb"_ZN3cts\d+[a-z_]+kernel[A-Za-z0-9_]*\.kd", blob))
+
+
+def test_product_library_carries_only_the_default_kernels():
+    """The product .so compiles one kernel per path (verify variant 13, small variant 9, MediaStream variant 3, the
+    fills), each for nontemporal and plain loads; every measured alternative lives in the tuning build only."""
+    from ctstraffic_amd import _lib
+
+    prod = _kernels(_lib.LIB_PATH)
+    wg = sorted(k for k in prod if "verify_wg_kernel" in k)
+    assert wg == ["_ZN3cts16verify_wg_kernelILi2ELb%dELb1ELb0ELb1ELb1ELi1EEEvPKhmPK12cts_buf_descjP17cts_verify_resultPmPjj"
+                  ".kd" % nt for nt in (0, 1)]
+    assert not any("verify_wave" in k or "_nb_" in k for k in prod)
+    assert len(prod) == 12, sorted(prod)
+    if os.path.exists(_lib.TUNING_LIB_PATH):
+        tun = _kernels(_lib.TUNING_LIB_PATH)
+        assert prod < tun and len(tun) > 40

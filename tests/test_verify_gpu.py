@@ -447,9 +447,10 @@ def test_verify_host_batch(engine):
 # ---- every launch variant / geometry is bit-identical ------------------------------------------
 @pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17])
 @pytest.mark.parametrize("nt", [1, 0])
-def test_launch_variants_parity(engine, variant, nt):
+def test_launch_variants_parity(tuning_engine, variant, nt):
     from ctstraffic_amd import _lib
 
+    engine = tuning_engine
     default_variant = engine.get_attr(_lib.ATTR_VERIFY_VARIANT)
     default_bpc = engine.get_attr(_lib.ATTR_BLOCKS_PER_CU)
     default_small_bpc = engine.get_attr(_lib.ATTR_SMALL_BLOCKS_PER_CU)
@@ -485,13 +486,14 @@ def test_launch_variants_parity(engine, variant, nt):
 
 # ---- every small-buffer (datagram) kernel is bit-identical --------------------------------------
 @pytest.mark.parametrize("small_variant", list(range(10)))
-def test_small_variants_parity(engine, small_variant):
+def test_small_variants_parity(tuning_engine, small_variant):
     """Small-buffer path (max_length_hint <= 8192): one wave per buffer (0-4) and four
     buffers per wave in 16-lane teams (5-8; 9 walking block-contiguous ranges), vs the oracle. Includes spans longer than the
     hint (multi-round teams), empty spans, all start alignments, bad descriptors, a batch
     whose size is not a multiple of the team count, and config-3 datagrams."""
     from ctstraffic_amd import _lib
 
+    engine = tuning_engine
     default_sv = engine.get_attr(_lib.ATTR_SMALL_VARIANT)
     default_sbpc = engine.get_attr(_lib.ATTR_SMALL_BLOCKS_PER_CU)
     default_chunk = engine.get_attr(_lib.ATTR_SMALL_CHUNK)
@@ -533,8 +535,34 @@ def test_small_variants_parity(engine, small_variant):
         engine.set_attr(_lib.ATTR_SMALL_CHUNK, default_chunk)
 
 
+def _pick(attr, variant, product_engine, tuning_engine):
+    from ctstraffic_amd import _lib
+
+    dflt = {_lib.ATTR_VERIFY_VARIANT: 13, _lib.ATTR_SMALL_VARIANT: 9, _lib.ATTR_MS_VARIANT: 3}[attr]
+    return product_engine if variant == dflt else tuning_engine
+
+
+def test_product_build_launches_the_defaults_only(engine, tuning_engine):
+    """The product library compiles one kernel per path (verify variant 13, small variant 9, MediaStream variant 3)
+    and refuses the others; the tuning build accepts every variant."""
+    from ctstraffic_amd import _lib
+    from ctstraffic_amd._lib import CtsError
+
+    assert "tuning" not in _lib.lib().cts_version().decode()
+    assert "tuning" in _lib.tuning_lib().cts_version().decode()
+    for attr, dflt, others in ((_lib.ATTR_VERIFY_VARIANT, 13, (0, 4, 12, 17)), (_lib.ATTR_SMALL_VARIANT, 9, (0, 5)),
+                               (_lib.ATTR_MS_VARIANT, 3, (0, 2))):
+        assert engine.get_attr(attr) == dflt and tuning_engine.get_attr(attr) == dflt
+        engine.set_attr(attr, dflt)
+        for v in others:
+            with pytest.raises(CtsError):
+                engine.set_attr(attr, v)
+            tuning_engine.set_attr(attr, v)
+        tuning_engine.set_attr(attr, dflt)
+
+
 # ---- maximum sizes: one buffer of 2^32 - 1 bytes, buffers past the 4 GiB arena offset -----------------------
-def test_max_length_buffers(engine):
+def test_max_length_buffers(engine, tuning_engine):
     """ctsTask::m_bufferLength is a u32: a single 2^32 - 1-byte buffer (last byte corrupted) and a 2^31 + 77-byte
     buffer starting past 2^32 in the arena at an odd address with the MediaStream skip. Both kernels paths; the fill
     writes them first (its 64-bit offsets are checked at sampled positions against the oracle's pattern). Every
@@ -569,8 +597,11 @@ def test_max_length_buffers(engine):
 
     cases = [(_lib.ATTR_VERIFY_VARIANT, 13, 0), (_lib.ATTR_VERIFY_VARIANT, 4, 0), (_lib.ATTR_VERIFY_VARIANT, 3, 0),
              (_lib.ATTR_SMALL_VARIANT, 9, 1472), (_lib.ATTR_SMALL_VARIANT, 0, 1472), (_lib.ATTR_SMALL_VARIANT, 3, 1472)]
-    defaults = {a: engine.get_attr(a) for a, _, _ in cases}
+    product_engine = engine
+    defaults = {a: tuning_engine.get_attr(a) for a, _, _ in cases}
     for attr, variant, hint in cases:  # workgroup, barrier-free workgroup, wave, four-per-wave, wave, pipelined wave
+        # the defaults run on the product engine, the other families on the tuning build's
+        engine = _pick(attr, variant, product_engine, tuning_engine)
         engine.set_attr(attr, variant)
         res = engine.new_results(2)
         ctr = engine.new_counters()

@@ -27,7 +27,7 @@ def main():
     p.add_argument("--only", default="", help="comma list of case names to run (default: all)")
     args = p.parse_args()
     torch.cuda.set_device(0)
-    eng = Engine(0)
+    eng = Engine(0, tuning=True)  # every launch variant (libcts_engine_tuning.so)
     w = W.udp_datagrams(n_datagrams=args.datagrams)
     arenas = []
     for _ in range(args.arenas):

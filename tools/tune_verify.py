@@ -34,7 +34,7 @@ def main():
                    help="fill: time cts_fill over the same descriptors (write-bound twin)")
     args = p.parse_args()
     torch.cuda.set_device(0)
-    eng = Engine(0)
+    eng = Engine(0, tuning=True)  # every launch variant (libcts_engine_tuning.so)
     if args.workload == "config2":
         w = W.tcp_resident(n_buffers=args.buffers, corrupt_rate=args.corrupt_rate)
     else:
