@@ -20,6 +20,7 @@ STATUS_ERROR_TOO_MUCH_DATA_TRANSFERRED = 2147483645
 STATUS_ERROR_DATA_DID_NOT_MATCH_BIT_PATTERN = 2147483644
 PATTERN_E_FAIL_FAST = 2147483640
 CONNECTION_ID_LENGTH = 37
+RIO_INVALID_BUFFERID = 0xFFFFFFFF
 COMPLETION_MESSAGE_SIZE = 4
 
 
@@ -59,6 +60,8 @@ class CtsPatternConfig(ctypes.Structure):
         ("verify_mode", ctypes.c_uint32),
         ("batch_buffers", ctypes.c_uint32),
         ("batch_bytes", ctypes.c_uint64),
+        ("registered_io", ctypes.c_uint32),
+        ("reserved0", ctypes.c_uint32),
     ]
 
 
@@ -92,12 +95,17 @@ class CtsStatusDetails(ctypes.Structure):
 
 
 assert ctypes.sizeof(CtsTask) == 40
-assert ctypes.sizeof(CtsPatternConfig) == 80
+assert ctypes.sizeof(CtsPatternConfig) == 88
 
 # int (*)(void* ctx, const uint8_t* host_arena, uint64_t arena_bytes, const cts_buf_desc* descs,
 #         uint32_t n, cts_verify_result* results)
 BATCH_VERIFIER = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                                   ctypes.c_uint32, ctypes.POINTER(CtsVerifyResult))
+
+
+# uint64_t (*)(void* ctx, char* buffer, uint32_t length) / void (*)(void* ctx, uint64_t buffer_id)
+RIO_REGISTER = ctypes.CFUNCTYPE(ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32)
+RIO_DEREGISTER = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint64)
 
 
 def declare(L: ctypes.CDLL) -> None:
@@ -115,6 +123,8 @@ def declare(L: ctypes.CDLL) -> None:
         "cts_io_pattern_initiate_io": ([P, ctypes.POINTER(CtsTask)], i32),
         "cts_io_pattern_complete_io": ([P, ctypes.POINTER(CtsTask), u32, u32], i32),
         "cts_io_pattern_last_error": ([P], u32),
+        "cts_io_pattern_rio_buffer_id_count": ([P], u64),
+        "cts_rio_functions_set": ([P, P, P], i32),
         "cts_io_pattern_set_ideal_send_backlog": ([P, u32], i32),
         "cts_io_pattern_flush": ([P], i32),
         "cts_io_pattern_get_stats": ([P, ctypes.POINTER(CtsPatternStats)], i32),

@@ -48,6 +48,19 @@ struct SharedBuffer {
 };
 SharedBuffer g_shared;
 
+// g_configSettings->rioFunctions: RIORegisterBuffer / RIODeregisterBuffer (cts_rio_functions_set)
+struct RioFunctions {
+    std::mutex mu;
+    cts_rio_register_buffer_fn reg = nullptr;
+    cts_rio_deregister_buffer_fn dereg = nullptr;
+    void* ctx = nullptr;
+};
+RioFunctions g_rio;
+constexpr uint64_t kRioInvalid = CTS_RIO_INVALID_BUFFERID;
+constexpr uint64_t kMaxSupportedBytesInFlight = 0x1000000;  // c_maxSupportedBytesInFlight, ctsIOPattern.cpp:49
+
+struct RioRegisterFailed {};
+
 // TcpStatusDetails (ctsConfig.h:415) + a DataError tally
 std::atomic<uint64_t> g_bytesSent{0};
 std::atomic<uint64_t> g_bytesRecv{0};
@@ -293,6 +306,12 @@ struct cts_io_pattern {
     virtual ~cts_io_pattern()
     {
         if (stream) (void)cts_engine_stream_destroy(engine, stream);
+        // ~RioBufferId (ctsIOPattern.h:230-238) for every id this pattern registered
+        if (!rio_owned.empty()) {
+            std::lock_guard<std::mutex> lk(g_rio.mu);
+            if (g_rio.dereg != nullptr)
+                for (const uint64_t id : rio_owned) g_rio.dereg(g_rio.ctx, id);
+        }
     }
 
     cts_pattern_config cfg;
@@ -340,6 +359,34 @@ struct cts_io_pattern {
     uint32_t ring_slots = 0, ring_next = 0;
     char* ring_base = nullptr;
     uint64_t ring_bytes = 0;
+
+    // RIO buffer ids (ctsIOPattern.h:219-269). m_receivingRioBufferIds pairs with
+    // m_recvBufferFreeList entry for entry; in ring mode every ring slot has its own id
+    // (ring_rio_ids) and a recycled slot goes back with its id.
+    std::vector<uint64_t> m_receivingRioBufferIds;
+    std::vector<uint64_t> m_sendingRioBufferIds;
+    std::vector<uint64_t> ring_rio_ids;
+    std::vector<uint64_t> rio_owned;  // every id registered by this pattern (deregistered at destroy)
+    uint64_t m_rioConnectionId = kRioInvalid;
+    uint64_t m_rioCompletionMessage = kRioInvalid;
+
+    bool Rio() const { return cfg.registered_io != 0; }
+    uint64_t RioRegister(char* buffer, uint32_t length)  // RIORegisterBuffer, THROW_WIN32 on failure
+    {
+        uint64_t id = kRioInvalid;
+        {
+            std::lock_guard<std::mutex> lk(g_rio.mu);
+            if (g_rio.reg != nullptr) id = g_rio.reg(g_rio.ctx, buffer, length);
+        }
+        if (id == kRioInvalid) throw RioRegisterFailed{};
+        rio_owned.push_back(id);
+        return id;
+    }
+    uint64_t RioBufferIdCount() const  // ctsIOPattern.h:114-123
+    {
+        if (!Rio()) return 0;
+        return m_receivingRioBufferIds.size() + m_sendingRioBufferIds.size() + 2;
+    }
 
     uint32_t GetBufferSize()  // ctsConfig.cpp:4679-4684
     {
@@ -389,7 +436,26 @@ struct cts_io_pattern {
         return CTS_IO_FAILED;
     }
 
-    int CreateRecvBuffers()  // ctsIOPattern.cpp:133-193 (RIO registration not restated)
+    int CreateRecvBuffers()  // ctsIOPattern.cpp:133-193
+    {
+        const int rc = CreateRecvSlots();
+        if (rc != CTS_OK || !Rio()) return rc;
+        // register the recv slots, then the connection id and the completion message (:141-192)
+        if (ring) {
+            ring_rio_ids.resize(ring_slots);
+            for (uint32_t i = 0; i < ring_slots; ++i)
+                ring_rio_ids[i] = RioRegister(ring_base + (size_t)i * max_buffer_size, max_buffer_size);
+            for (const char* b : m_recvBufferFreeList) m_receivingRioBufferIds.push_back(ring_rio_ids[RingSlot(b)]);
+        } else {
+            const uint32_t len = cfg.use_shared_buffer ? (uint32_t)g_shared.bytes : max_buffer_size;
+            for (char* b : m_recvBufferFreeList) m_receivingRioBufferIds.push_back(RioRegister(b, len));
+        }
+        m_rioConnectionId = RioRegister(connection_id, CTS_CONNECTION_ID_LENGTH);
+        m_rioCompletionMessage = RioRegister(m_completionMessageBuffer.data(), CTS_COMPLETION_MESSAGE_SIZE);
+        return CTS_OK;
+    }
+
+    int CreateRecvSlots()
     {
         m_recvBufferFreeList.assign(recvCount, nullptr);
         if (recvCount == 0) return CTS_OK;
@@ -418,19 +484,32 @@ struct cts_io_pattern {
         return CTS_OK;
     }
 
-    // the buffer to put back on the free list after a completion (ctsIOPattern.cpp:371-376):
-    // the completed one, or in ring mode the next ring slot (the completed one waits for its batch)
-    char* RecycledRecvBuffer(char* completed)
+    uint32_t RingSlot(const char* b) const { return (uint32_t)((size_t)(b - ring_base) / max_buffer_size); }
+
+    // the buffer (and its RIO id) to put back on the free lists after a completion
+    // (ctsIOPattern.cpp:369-386): the completed one, or in ring mode the next ring slot (the
+    // completed one waits for its batch)
+    void RecycleRecvBuffer(const cts_task& t)
     {
-        if (!ring) return completed;
-        char* b = ring_base + (size_t)(ring_next % ring_slots) * max_buffer_size;
-        ++ring_next;
-        return b;
+        char* b = t.buffer;
+        if (ring) {
+            b = ring_base + (size_t)(ring_next % ring_slots) * max_buffer_size;
+            ++ring_next;
+        }
+        m_recvBufferFreeList.push_back(b);
+        if (Rio()) m_receivingRioBufferIds.push_back(ring ? ring_rio_ids[RingSlot(b)] : t.rio_buffer_id);
     }
 
     void CreateSendBuffers()  // ctsIOPattern.cpp:195-217
     {
         std::memcpy(m_completionMessageBuffer.data(), kCompletionMessage, CTS_COMPLETION_MESSAGE_SIZE);
+        if (Rio()) {
+            // g_maxNumberOfRioSendBuffers = c_maxSupportedBytesInFlight / GetMinBufferSize() + 1 (:61)
+            const uint64_t n = kMaxSupportedBytesInFlight / cfg.buffer_size_low + 1;
+            m_sendingRioBufferIds.reserve(n);
+            for (uint64_t i = 0; i < n; ++i)
+                m_sendingRioBufferIds.push_back(RioRegister(g_shared.host, (uint32_t)g_shared.bytes));
+        }
     }
 
     cts_task CreateNewTask(uint8_t action, uint32_t maxTransfer)  // ctsIOPattern.cpp:550-743
@@ -443,6 +522,7 @@ struct cts_io_pattern {
         if (newSize > 0xFFFFFFFFull) throw FailFast{"next buffer size is greater than MAXDWORD"};
         const uint32_t size = (uint32_t)newSize;
         cts_task t{};
+        t.rio_buffer_id = kRioInvalid;
         if (action == CTS_TASK_SEND) {
             t.io_action = CTS_TASK_SEND;
             t.buffer_type = CTS_BUFFER_STATIC;
@@ -450,6 +530,13 @@ struct cts_io_pattern {
             t.buffer_offset = m_sendPatternOffset;
             t.expected_pattern_offset = 0;
             t.buffer = g_shared.host;
+            // every RIOSend needs its own RIO_BUFFERID (ctsIOPattern.cpp:683-692)
+            if (Rio()) {
+                if (m_sendingRioBufferIds.empty()) throw FailFast{"m_sendingRioBufferIds is empty for a new Send task"};
+                t.buffer_type = CTS_BUFFER_DYNAMIC;
+                t.rio_buffer_id = m_sendingRioBufferIds.back();
+                m_sendingRioBufferIds.pop_back();
+            }
             m_sendPatternOffset += size;
             m_sendPatternOffset %= kPatternSize;
             if ((uint64_t)t.buffer_length + t.buffer_offset > g_shared.bytes)
@@ -463,6 +550,11 @@ struct cts_io_pattern {
             if (m_recvBufferFreeList.empty()) throw FailFast{"m_recvBufferFreeList is empty for a new Recv task"};
             t.buffer = m_recvBufferFreeList.back();
             m_recvBufferFreeList.pop_back();
+            if (Rio()) {  // ctsIOPattern.cpp:716-725
+                if (m_receivingRioBufferIds.empty()) throw FailFast{"m_receivingRioBufferIds is empty for a new Recv task"};
+                t.rio_buffer_id = m_receivingRioBufferIds.back();
+                m_receivingRioBufferIds.pop_back();
+            }
             if (m_recvPatternOffset >= kPatternSize) throw FailFast{"recv pattern offset too large"};
         }
         return t;
@@ -477,13 +569,18 @@ struct cts_io_pattern {
     cts_task InitiateIo()  // ctsIOPattern.cpp:251-356
     {
         cts_task t{};
+        t.rio_buffer_id = kRioInvalid;
         switch (state.GetNextPatternType()) {
-        case PatternType::MoreIo: t = GetNextTaskFromPattern(); break;
+        case PatternType::MoreIo:
+            t = GetNextTaskFromPattern();
+            if (t.io_action == CTS_TASK_NONE) t.rio_buffer_id = kRioInvalid;
+            break;
         case PatternType::NoIo: break;
         case PatternType::SendConnectionId:
         case PatternType::RecvConnectionId:
             t.io_action = cfg.listening ? CTS_TASK_SEND : CTS_TASK_RECV;
             t.buffer = connection_id;
+            t.rio_buffer_id = m_rioConnectionId;
             t.buffer_length = CTS_CONNECTION_ID_LENGTH;
             t.buffer_type = CTS_BUFFER_TCP_CONNECTION_ID;
             break;
@@ -491,6 +588,7 @@ struct cts_io_pattern {
         case PatternType::RecvCompletion:
             t.io_action = cfg.listening ? CTS_TASK_SEND : CTS_TASK_RECV;
             t.buffer = m_completionMessageBuffer.data();
+            t.rio_buffer_id = m_rioCompletionMessage;
             t.buffer_length = CTS_COMPLETION_MESSAGE_SIZE;
             t.buffer_type = CTS_BUFFER_COMPLETION_MESSAGE;
             break;
@@ -499,6 +597,7 @@ struct cts_io_pattern {
         case PatternType::RequestFin:
             t.io_action = CTS_TASK_RECV;
             t.buffer = m_completionMessageBuffer.data();
+            t.rio_buffer_id = m_rioCompletionMessage;
             t.buffer_length = CTS_COMPLETION_MESSAGE_SIZE;
             t.buffer_type = CTS_BUFFER_STATIC;
             break;
@@ -738,8 +837,10 @@ struct cts_io_pattern {
             if (has_failure && !had_failure) return GetCurrentStatus();
         }
         const bool wasIoRequestedFromPattern = state.IsCurrentStateMoreIo();
-        if (t.buffer_type == CTS_BUFFER_DYNAMIC && t.io_action == CTS_TASK_RECV)
-            m_recvBufferFreeList.push_back(RecycledRecvBuffer(t.buffer));
+        if (t.buffer_type == CTS_BUFFER_DYNAMIC) {  // ctsIOPattern.cpp:369-386
+            if (t.io_action == CTS_TASK_RECV) RecycleRecvBuffer(t);
+            else if (Rio() && t.io_action == CTS_TASK_SEND) m_sendingRioBufferIds.push_back(t.rio_buffer_id);
+        }
 
         bool verified_now = false, defer_this = false;
         cts_verify_result vr{};
@@ -1058,9 +1159,11 @@ int cts_io_pattern_create(const cts_pattern_config* c, cts_engine* engine, cts_i
     int rc = CTS_OK;
     try {
         rc = p->CreateRecvBuffers();
-        p->CreateSendBuffers();
+        if (rc == CTS_OK) p->CreateSendBuffers();
     } catch (const std::bad_alloc&) {
         rc = CTS_E_NOMEM;
+    } catch (const RioRegisterFailed&) {
+        rc = CTS_E_INVALID;  // THROW_WIN32_MSG(WSAGetLastError(), "RIORegisterBuffer")
     }
     if (rc != CTS_OK) {
         delete p;
@@ -1090,12 +1193,14 @@ int cts_io_pattern_initiate_io(cts_io_pattern* p, cts_task* out)
 {
     if (p == nullptr || out == nullptr) return CTS_E_INVALID;
     *out = cts_task{};
+    out->rio_buffer_id = CTS_RIO_INVALID_BUFFERID;
     if (!p->fail_fast.empty()) return CTS_OK;
     try {
         *out = p->InitiateIo();
     } catch (const FailFast& f) {
         latch_fail_fast(p, f);
         *out = cts_task{};
+        out->rio_buffer_id = CTS_RIO_INVALID_BUFFERID;
     } catch (const std::bad_alloc&) {
         return CTS_E_NOMEM;
     }
@@ -1120,6 +1225,19 @@ int cts_io_pattern_complete_io(cts_io_pattern* p, const cts_task* t, uint32_t cu
 }
 
 uint32_t cts_io_pattern_last_error(const cts_io_pattern* p) { return p ? p->m_lastError : CTS_STATUS_IO_RUNNING; }
+
+uint64_t cts_io_pattern_rio_buffer_id_count(const cts_io_pattern* p) { return p ? p->RioBufferIdCount() : 0; }
+
+int cts_rio_functions_set(cts_rio_register_buffer_fn register_fn, cts_rio_deregister_buffer_fn deregister_fn,
+                          void* ctx)
+{
+    if ((register_fn == nullptr) != (deregister_fn == nullptr)) return CTS_E_INVALID;
+    std::lock_guard<std::mutex> lk(g_rio.mu);
+    g_rio.reg = register_fn;
+    g_rio.dereg = deregister_fn;
+    g_rio.ctx = ctx;
+    return CTS_OK;
+}
 
 int cts_io_pattern_set_ideal_send_backlog(cts_io_pattern* p, uint32_t bytes)
 {

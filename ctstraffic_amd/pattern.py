@@ -41,6 +41,7 @@ class PatternConfig:
     verify_mode: int = A.VERIFY_SYNC
     batch_buffers: int = 0
     batch_bytes: int = 0
+    registered_io: bool = False  # -io:rioiocp (WSA_FLAG_REGISTERED_IO): see rio_functions_set
 
     def to_c(self) -> A.CtsPatternConfig:
         c = A.CtsPatternConfig()
@@ -61,6 +62,7 @@ class PatternConfig:
         c.verify_mode = self.verify_mode
         c.batch_buffers = self.batch_buffers
         c.batch_bytes = self.batch_bytes
+        c.registered_io = int(bool(self.registered_io))
         return c
 
     @property
@@ -128,6 +130,9 @@ class IoPattern:
     def GetLastPatternError(self) -> int:
         return int(lib().cts_io_pattern_last_error(self._h))
 
+    def GetRioBufferIdCount(self) -> int:
+        return int(lib().cts_io_pattern_rio_buffer_id_count(self._h))
+
     def SetIdealSendBacklog(self, isb: int) -> None:
         check("cts_io_pattern_set_ideal_send_backlog", lib().cts_io_pattern_set_ideal_send_backlog(self._h, isb))
 
@@ -187,6 +192,24 @@ def shared_buffer_attach(buf: np.ndarray) -> None:
 
 def shared_buffer_release() -> None:
     lib().cts_shared_buffer_release()
+
+
+def rio_functions_set(register_fn, deregister_fn, ctx=None) -> None:
+    """g_configSettings->rioFunctions: RIORegisterBuffer / RIODeregisterBuffer for patterns created with
+    registered_io. Takes C function pointers (ints) or Python callables (kept alive here); None clears."""
+    global _rio_keepalive
+    if register_fn is None:
+        check("cts_rio_functions_set", lib().cts_rio_functions_set(None, None, None))
+        _rio_keepalive = None
+        return
+    reg = register_fn if isinstance(register_fn, int) else A.RIO_REGISTER(register_fn)
+    dereg = deregister_fn if isinstance(deregister_fn, int) else A.RIO_DEREGISTER(deregister_fn)
+    _rio_keepalive = (reg, dereg)
+    as_ptr = lambda f: f if isinstance(f, int) else ctypes.cast(f, ctypes.c_void_p).value
+    check("cts_rio_functions_set", lib().cts_rio_functions_set(as_ptr(reg), as_ptr(dereg), ctx))
+
+
+_rio_keepalive = None
 
 
 def status_details() -> dict:

@@ -68,7 +68,11 @@ typedef enum cts_buffer_type {
     CTS_BUFFER_DYNAMIC = 5
 } cts_buffer_type;
 
-/* ctsTask (ctsIOTask.hpp:37-60), RIO_BUFFERID as a uint64 (0 = RIO_INVALID_BUFFERID). */
+/* RIO_INVALID_BUFFERID (mswsock.h: (RIO_BUFFERID)(ULONG_PTR)0xFFFFFFFF), the ctsTask default
+ * (ctsIOTask.hpp:40). Every task the pattern hands out carries it unless it carries a registered id. */
+#define CTS_RIO_INVALID_BUFFERID 0xFFFFFFFFull
+
+/* ctsTask (ctsIOTask.hpp:37-60), RIO_BUFFERID as a uint64. */
 typedef struct cts_task {
     int64_t time_offset_ms;           /* m_timeOffsetMilliseconds */
     uint64_t rio_buffer_id;           /* m_rioBufferid */
@@ -134,6 +138,9 @@ typedef struct cts_pattern_config {
     uint32_t verify_mode;       /* cts_verify_mode */
     uint32_t batch_buffers;     /* DEFERRED: max queued buffers per batch (0 = 1024) */
     uint64_t batch_bytes;       /* DEFERRED: staging arena bytes (0 = 64 MiB) */
+    uint32_t registered_io;     /* SocketFlags & WSA_FLAG_REGISTERED_IO (-io:rioiocp): register buffers with
+                                 * the RIO functions of cts_rio_functions_set, hand their ids out in tasks */
+    uint32_t reserved0;
 } cts_pattern_config;
 
 /* Per-connection statistics (ctsTcpStatistics, ctsStatistics.hpp:316-373) and
@@ -168,6 +175,25 @@ typedef int (*cts_batch_verifier)(void* ctx, const uint8_t* host_arena, uint64_t
 
 typedef struct cts_io_pattern cts_io_pattern;
 
+/* ---- RIO buffer registration (g_configSettings->rioFunctions, ctsConfig.h) -------------------
+ * RIORegisterBuffer / RIODeregisterBuffer as the pattern uses them (ctsIOPattern.cpp:133-217,
+ * ctsIOPattern.h:219-269). A register function returns CTS_RIO_INVALID_BUFFERID on failure (the
+ * reference then throws WSAGetLastError() out of the pattern's constructor: cts_io_pattern_create
+ * returns CTS_E_INVALID). With registered_io set, a pattern registers
+ *   - every recv buffer slot (or the shared receiver buffer once per slot with use_shared_buffer),
+ *   - the sender buffer 16 MiB / buffer_size_low + 1 times (one id per concurrent send: RIO cannot
+ *     use one RIO_BUFFERID in two sends at once, ctsIOPattern.cpp:49,61,198-210),
+ *   - the connection id (37 B) and the completion message (4 B) buffers,
+ * hands a recv / send task the id of its buffer (buffer type DYNAMIC, ctsIOPattern.cpp:683-692,
+ * :716-725) and takes it back in CompleteIo (:369-386). The ids of a pattern are deregistered when
+ * it is destroyed, including ids of tasks still in flight (the reference leaks those; its RIO
+ * functor never destroys a pattern with IO outstanding). Process-wide; set before creating
+ * patterns with registered_io. */
+typedef uint64_t (*cts_rio_register_buffer_fn)(void* ctx, char* buffer, uint32_t length);
+typedef void (*cts_rio_deregister_buffer_fn)(void* ctx, uint64_t buffer_id);
+int cts_rio_functions_set(cts_rio_register_buffer_fn register_fn, cts_rio_deregister_buffer_fn deregister_fn,
+                          void* ctx);
+
 /* ---- g_senderSharedBuffer (process-wide, InitOnceIoPatternCallback) ------ */
 /* Materialise the sender buffer (65536 + max_buffer_size bytes) in pinned,
  * device-mapped host memory with the gfx950 fill kernel. Idempotent for a
@@ -194,6 +220,10 @@ int cts_io_pattern_initiate_io(cts_io_pattern* pattern, cts_task* out_task);
 int cts_io_pattern_complete_io(cts_io_pattern* pattern, const cts_task* task, uint32_t current_transfer,
                                uint32_t status_code);
 uint32_t cts_io_pattern_last_error(const cts_io_pattern* pattern);
+/* ctsIoPattern::GetRioBufferIdCount (ctsIOPattern.h:114-123): 0 without registered_io, else the ids
+ * on the pattern's free lists + 2 (connection id, completion message). ctsRioIocp sizes its request
+ * queue and task table with it (ctsRioIocp.cpp:513-530). */
+uint64_t cts_io_pattern_rio_buffer_id_count(const cts_io_pattern* pattern);
 /* ctsIoPattern::SetIdealSendBacklog (ctsIOPattern.h:109-112): the socket's ideal send backlog
  * (SIO_IDEAL_SEND_BACKLOG_QUERY, ctsSocket.cpp:249) bounds the bytes of sends in flight when
  * pre_post_sends == 0. */
