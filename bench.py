@@ -541,15 +541,22 @@ def run_extras(engine, torch, W, w, arenas, descs, dev, want):
         try:
             # config 1 end to end: loopback TCP push, 8 conns, 64 KiB IO, 1 GiB/conn, -verify:data; the
             # sender buffer comes from the fill kernel, every received buffer is verified on the GPU
-            from ctstraffic_amd import _pattern_abi as PA
+            from ctstraffic_amd import _lib, _pattern_abi as PA
             from ctstraffic_amd import loopback as LB
 
-            for name, mode, pat in (("deferred", PA.VERIFY_DEFERRED, PA.PATTERN_PUSH),
-                                    ("sync", PA.VERIFY_SYNC, PA.PATTERN_PUSH),
-                                    ("duplex_deferred", PA.VERIFY_DEFERRED, PA.PATTERN_DUPLEX)):
-                # (duplex: each side sends and receives half of the 1 GiB at once, both directions verified)
-                r = LB.run(connections=8, buffer_size=65536, transfer_size=1 << 30, engine=engine, verify_mode=mode,
-                           io_pattern=pat)
+            for name, mode, pat, mailbox in (("deferred", PA.VERIFY_DEFERRED, PA.PATTERN_PUSH, 1),
+                                             ("sync", PA.VERIFY_SYNC, PA.PATTERN_PUSH, 1),
+                                             ("sync_launch", PA.VERIFY_SYNC, PA.PATTERN_PUSH, 0),
+                                             ("duplex_deferred", PA.VERIFY_DEFERRED, PA.PATTERN_DUPLEX, 1)):
+                # (duplex: each side sends and receives half of the 1 GiB at once, both directions verified;
+                # sync: every completion's VerifyBuffer posted to the resident mailbox grid, the default;
+                # sync_launch: one sliced launch + synchronize per completion instead)
+                engine.set_attr(_lib.ATTR_SYNC_MAILBOX, mailbox)
+                try:
+                    r = LB.run(connections=8, buffer_size=65536, transfer_size=1 << 30, engine=engine,
+                               verify_mode=mode, io_pattern=pat)
+                finally:
+                    engine.set_attr(_lib.ATTR_SYNC_MAILBOX, 1)
                 out["loopback_config1_%s" % name] = {
                     "GBps_recv": round(r["GBps_recv"], 3), "seconds": round(r["seconds"], 3),
                     "connections_ok": r["connections_ok"], "data_errors": r["data_errors"],

@@ -48,7 +48,7 @@ ATTR_FILL_BLOCKS_PER_CU = 7
 ATTR_MS_VARIANT = 8
 ATTR_SMALL_CHUNK = 9
 ATTR_FILL_NT = 10
-ATTR_SYNC_COALESCE = 11
+ATTR_SYNC_MAILBOX = 11
 
 
 # large-buffer verify kernels by CTS_ATTR_VERIFY_VARIANT, as rocprofv3 names them (13 = the product default; the
@@ -134,6 +134,7 @@ def _declare(L: ctypes.CDLL) -> None:
                                      ctypes.POINTER(CtsCounters)], i32),
         "cts_verify_host": ([P, P, u32, u32, ctypes.POINTER(CtsVerifyResult)], i32),
         "cts_verify_mapped": ([P, P, u32, u32, ctypes.POINTER(CtsVerifyResult)], i32),
+        "cts_mailbox_launches": ([P], u64),
         "cts_verify_host_batch": ([P, P, P, P, P, u32, P, ctypes.POINTER(CtsCounters)], i32),
         "cts_host_alloc": ([P, u64, ctypes.POINTER(P), ctypes.POINTER(P)], i32),
         "cts_host_free": ([P, P], i32),

@@ -7,16 +7,21 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "cts_engine.h"
 #include "cts_internal.hpp"
 #include "cts_slices.hpp"
+
+struct Mailbox;
 
 struct cts_engine {
     int device = 0;
@@ -34,28 +39,9 @@ struct cts_engine {
     void* batch_res = nullptr;
     size_t batch_res_cap = 0;
     void* batch_ctr = nullptr;
-    // cts_verify_mapped: concurrent SYNC verifies combined into one launch (flat combining)
-    std::mutex comb_mu;
-    std::condition_variable comb_cv;
-    std::vector<struct cts_sync_req*> comb_q;  // waiting for the next launch
-    bool comb_busy = false;
-    int sync_coalesce = 0;  // CTS_ATTR_SYNC_COALESCE (read by cts_pattern's SYNC verify)
-    // a leader owns comb_stream and the comb_* staging
-    hipStream_t comb_stream = nullptr;
-    void* comb_desc = nullptr;
-    size_t comb_desc_cap = 0;
-    void* comb_res = nullptr;
-    size_t comb_res_cap = 0;
-};
-
-// One caller of cts_verify_mapped: its buffer, and its answer once `done`.
-struct cts_sync_req {
-    const uint8_t* dev;
-    uint32_t len;
-    uint32_t expected;
-    cts_verify_result out;
-    int rc;
-    bool done;
+    int sync_mailbox = 1;  // CTS_ATTR_SYNC_MAILBOX (read by cts_pattern's SYNC verify)
+    std::unique_ptr<Mailbox> mail;  // cts_verify_mapped's resident grid, started on first use
+    std::mutex mail_init_mu;
 };
 
 namespace {
@@ -124,55 +110,219 @@ int ensure_stage(cts_engine* e, size_t bytes)
     return rc;
 }
 
-// The leader's half of cts_verify_mapped: every request of `batch` as slices of one launch.
-// Descriptors address the group relative to its lowest buffer (one flat device address range:
-// mapped pinned host memory and HBM share the GPU's virtual address space; only the described
-// bytes are read). Per-request verdicts fold back with slice_merge, so each caller gets exactly
-// what a launch of its own would have returned (ctsIOPattern.cpp:745-775).
-void run_sync_group(cts_engine* e, const std::vector<cts_sync_req*>& batch)
+}  // namespace
+
+// ---- cts_verify_mapped: the SYNC mailbox -------------------------------------------------------
+// A resident grid (cts::launch_mailbox) answers one-buffer verifies posted through host-coherent
+// pinned slots, so a SYNC completion pays PCIe round trips instead of a launch + synchronize; the
+// caller folds the grid's per-piece part records into the RtlCompareMemory record itself.
+// Tickets are claimed under `mu`; ticket t uses slot t % nslots once its previous user (t - nslots)
+// has read its answer (free_at). The grid is (re)launched by the first post after it stopped, and a
+// watchdog thread stops it with a kMailStop ticket after `idle_ms` without posts, so an idle engine
+// neither holds workgroups nor polls PCIe. The grid's own exit bound (idle_ticks, far longer) is a
+// safety net only: a post racing it would time out (CTS_E_HIP) rather than hang.
+struct Mailbox {
+    cts_engine* e = nullptr;
+    // groups x cts::kMailGroup workgroups: 8 groups measured best for 8-16 concurrent callers (64 KiB:
+    // 18.7 / 25.3 us per verify at 8 / 16 threads against 19.6-32.6 for 1-4 groups; one caller 7.1 us,
+    // 5.8 with one group; tools/sync_probe, profiles/r02/sync_probe_groups.jsonl)
+    uint32_t nslots = 1024, groups = 8;
+    uint64_t idle_ticks = 100000000ull;  // 1 s at 100 MHz
+    int idle_ms = 50;
+    double timeout_s = 2.0;
+    cts::MailSlot* slots = nullptr;      // host view (coherent, pinned)
+    cts::MailSlot* dslots = nullptr;     // device view
+    cts::MailPart* parts = nullptr;      // nslots x kMailGroup part records, host view (coherent, pinned)
+    cts::MailPart* dparts = nullptr;
+    hipStream_t stream = nullptr;
+    std::unique_ptr<std::atomic<uint64_t>[]> free_at;
+    std::mutex mu;
+    bool running = false, broken = false, quit = false;
+    uint64_t next = 0;
+    uint32_t outstanding = 0;
+    std::chrono::steady_clock::time_point last_post;
+    std::condition_variable cv;
+    std::thread watchdog;
+    std::atomic<uint64_t> launches{0};
+
+    ~Mailbox()
+    {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            quit = true;
+        }
+        cv.notify_all();
+        if (watchdog.joinable()) watchdog.join();
+        (void)Stop(false);
+        DeviceGuard g(e->device);
+        if (stream) {
+            (void)hipStreamSynchronize(stream);
+            (void)hipStreamDestroy(stream);
+        }
+        if (parts) (void)hipHostFree(parts);
+        if (slots) (void)hipHostFree(slots);
+    }
+
+    int Init(cts_engine* eng)
+    {
+        e = eng;
+        nslots = (uint32_t)std::max(16, env_int("CTS_MAILBOX_SLOTS", (int)nslots));
+        groups = (uint32_t)std::min(64, std::max(1, env_int("CTS_MAILBOX_GROUPS", (int)groups)));
+        idle_ms = std::max(1, env_int("CTS_MAILBOX_IDLE_MS", idle_ms));
+        DeviceGuard g(e->device);
+        if (!g.ok) return CTS_E_HIP;
+        void* p = nullptr;
+        if (hipHostMalloc(&p, sizeof(cts::MailSlot) * nslots,
+                          hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent) != hipSuccess)
+            return CTS_E_NOMEM;
+        slots = static_cast<cts::MailSlot*>(p);
+        std::memset(slots, 0, sizeof(cts::MailSlot) * nslots);
+        if ((dslots = device_view(slots)) == nullptr) return CTS_E_HIP;
+        nslots = (nslots + groups - 1) / groups * groups;  // slot k always belongs to group k mod G
+        const size_t pbytes = sizeof(cts::MailPart) * nslots * cts::kMailGroup;
+        if (hipHostMalloc(&p, pbytes, hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent) !=
+            hipSuccess)
+            return CTS_E_NOMEM;
+        parts = static_cast<cts::MailPart*>(p);
+        std::memset(parts, 0, pbytes);
+        if ((dparts = device_view(parts)) == nullptr) return CTS_E_HIP;
+        if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) {
+            stream = nullptr;
+            return CTS_E_HIP;
+        }
+        free_at.reset(new (std::nothrow) std::atomic<uint64_t>[nslots]);
+        if (!free_at) return CTS_E_NOMEM;
+        for (uint32_t i = 0; i < nslots; ++i) free_at[i].store(i, std::memory_order_relaxed);
+        last_post = std::chrono::steady_clock::now();
+        watchdog = std::thread([this] { Watch(); });
+        return CTS_OK;
+    }
+
+    // under mu: start the grid at ticket `next` (after any grid still draining, same stream)
+    int LaunchLocked()
+    {
+        DeviceGuard g(e->device);
+        if (!g.ok) return CTS_E_HIP;
+        if (cts::launch_mailbox(dslots, dparts, nslots, next, groups, idle_ticks, stream) != hipSuccess)
+            return CTS_E_HIP;
+        running = true;
+        launches.fetch_add(1, std::memory_order_relaxed);
+        return CTS_OK;
+    }
+
+    // Claim a ticket (launching the grid if needed), write the job, wait for the answer.
+    // Verify [ptr, ptr + len) (len > 0), or stop the grid (len == 0: one stop ticket per group, so
+    // every group leaves; only_if_idle: not while another job is outstanding).
+    int Post(uint64_t ptr, uint32_t len, uint32_t expected, cts_verify_result* out, bool only_if_idle)
+    {
+        uint64_t t;
+        uint32_t n = 1;
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            if (broken) return CTS_E_HIP;
+            if (len == 0) {
+                if (!running || (only_if_idle && outstanding != 0)) return CTS_OK;
+                running = false;
+                n = groups;
+            } else if (!running) {
+                const int rc = LaunchLocked();
+                if (rc != CTS_OK) return rc;
+            }
+            t = next;
+            next += n;
+            ++outstanding;
+            last_post = std::chrono::steady_clock::now();
+        }
+        int rc = CTS_OK;
+        for (uint32_t i = 0; i < n && rc == CTS_OK; ++i) rc = Run(t + i, ptr, len, expected, out);
+        std::lock_guard<std::mutex> lk(mu);
+        if (rc != CTS_OK) {
+            broken = true;  // a straggler may still read or answer the slot: never reuse it
+            running = false;
+        }
+        --outstanding;
+        return rc;
+    }
+
+    // One ticket: wait for its slot, write the job, fold the part records.
+    int Run(uint64_t t, uint64_t ptr, uint32_t len, uint32_t expected, cts_verify_result* out)
+    {
+        const uint32_t k = (uint32_t)(t % nslots);
+        while (free_at[k].load(std::memory_order_acquire) != t) std::this_thread::yield();
+        cts::MailSlot* const s = slots + k;
+        const uint32_t tag = (uint32_t)(t + 1);
+        // the job half first, then the tagged half: the grid's one 16-B read of the slot sees a new tag
+        // only with the new job (x86 keeps the two stores in order)
+        __atomic_store_n(&s->ptr_exp, (ptr & 0xFFFFFFFFFFFFull) | ((uint64_t)expected << 48), __ATOMIC_RELAXED);
+        __atomic_store_n(&s->len_seq, (uint64_t)len | ((uint64_t)tag << 32), __ATOMIC_RELEASE);
+        const uint32_t np = cts::mail_parts(ptr, len);
+        const cts::MailPart* const pr = parts + (size_t)k * cts::kMailGroup;
+        const auto t_start = std::chrono::steady_clock::now();
+        uint32_t first = 0xFFFFFFFFu, actual = 0;
+        uint64_t count = 0;
+        for (uint32_t i = 0; i < np; ++i) {
+            uint64_t g0, g1;
+            for (uint32_t spin = 0;; ++spin) {
+                g0 = __atomic_load_n(&pr[i].g0, __ATOMIC_ACQUIRE);
+                g1 = __atomic_load_n(&pr[i].g1, __ATOMIC_ACQUIRE);
+                if ((uint32_t)(g0 >> 32) == tag && (uint32_t)(g1 >> 40) == (tag & 0xFFFFFFu)) break;
+                if ((spin & 255u) == 255u) {
+                    if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count() > timeout_s)
+                        return CTS_E_HIP;
+                    std::this_thread::yield();
+                }
+            }
+            if ((uint32_t)g0 < first) {
+                first = (uint32_t)g0;
+                actual = (uint32_t)(g1 >> 32) & 0xFFu;
+            }
+            count += (uint32_t)g1;
+        }
+        free_at[k].store(t + nslots, std::memory_order_release);
+        if (out != nullptr && len != 0) {
+            // RtlCompareMemory of the whole buffer (ctsIOPattern.cpp:753-774): the smallest first
+            // difference over the pieces; expected/actual are the two bytes the reference prints
+            const bool pass = first == 0xFFFFFFFFu;
+            out->first_mismatch = pass ? len : first;
+            out->mismatch_bytes = (uint32_t)count;
+            out->expected = pass ? 0 : cts_pattern_byte((uint64_t)expected + first);
+            out->actual = pass ? 0 : (uint8_t)actual;
+            out->pass = pass ? 1 : 0;
+            out->flags = 0;
+        }
+        return CTS_OK;
+    }
+
+    int Stop(bool only_if_idle) { return Post(0, 0, 0, nullptr, only_if_idle); }
+
+    void Watch()
+    {
+        std::unique_lock<std::mutex> lk(mu);
+        while (!quit) {
+            cv.wait_for(lk, std::chrono::milliseconds(std::max(1, idle_ms / 2)));
+            if (quit || !running || outstanding != 0) continue;
+            if (std::chrono::steady_clock::now() - last_post < std::chrono::milliseconds(idle_ms)) continue;
+            lk.unlock();
+            (void)Stop(true);
+            lk.lock();
+        }
+    }
+};
+
+namespace {
+
+int mailbox_of(cts_engine* e, Mailbox** out)
 {
-    int rc = CTS_OK;
-    DeviceGuard g(e->device);
-    if (!g.ok) rc = CTS_E_HIP;
-    if (rc == CTS_OK && e->comb_stream == nullptr &&
-        hipStreamCreateWithFlags(&e->comb_stream, hipStreamNonBlocking) != hipSuccess) {
-        e->comb_stream = nullptr;
-        rc = CTS_E_HIP;
+    std::lock_guard<std::mutex> lk(e->mail_init_mu);
+    if (!e->mail) {
+        std::unique_ptr<Mailbox> m(new (std::nothrow) Mailbox());
+        if (!m) return CTS_E_NOMEM;
+        const int rc = m->Init(e);
+        if (rc != CTS_OK) return rc;
+        e->mail = std::move(m);
     }
-    const size_t maxd = (size_t)cts::kSliceMax * batch.size();
-    if (rc == CTS_OK) rc = ensure_pinned(&e->comb_desc, &e->comb_desc_cap, maxd * sizeof(cts_buf_desc), 4096);
-    if (rc == CTS_OK) rc = ensure_pinned(&e->comb_res, &e->comb_res_cap, maxd * sizeof(cts_verify_result), 4096);
-    std::vector<uint32_t> first(batch.size()), count(batch.size()), slen(batch.size());
-    if (rc == CTS_OK) {
-        const uint8_t* base = batch[0]->dev;
-        const uint8_t* end = batch[0]->dev + batch[0]->len;
-        for (const cts_sync_req* r : batch) {
-            base = std::min(base, r->dev);
-            end = std::max(end, r->dev + r->len);
-        }
-        base -= reinterpret_cast<uintptr_t>(base) & 15u;  // the kernels align loads from a 16-B arena base
-        auto* hd = static_cast<cts_buf_desc*>(e->comb_desc);
-        uint32_t nd = 0, maxsl = 0;
-        for (size_t i = 0; i < batch.size(); ++i) {
-            first[i] = nd;
-            count[i] = cts::slice_plan((uint64_t)(batch[i]->dev - base), batch[i]->len, batch[i]->expected,
-                                       (uint32_t)i, hd + nd, &slen[i]);
-            nd += count[i];
-            maxsl = std::max(maxsl, slen[i]);
-        }
-        const cts_buf_desc* dd = device_view(hd);
-        cts_verify_result* dr = device_view(static_cast<cts_verify_result*>(e->comb_res));
-        hipError_t err = (dd && dr) ? cts::launch_verify(base, (uint64_t)(end - base), dd, nd, maxsl, dr, nullptr,
-                                                         nullptr, 0, e->comb_stream, e->geo)
-                                    : hipErrorInvalidValue;
-        if (err == hipSuccess) err = hipStreamSynchronize(e->comb_stream);
-        if (err != hipSuccess) rc = CTS_E_HIP;
-    }
-    const auto* res = static_cast<const cts_verify_result*>(e->comb_res);
-    for (size_t i = 0; i < batch.size(); ++i) {
-        batch[i]->rc = rc;
-        if (rc == CTS_OK) batch[i]->out = cts::slice_merge(res + first[i], count[i], slen[i], batch[i]->len);
-    }
+    *out = e->mail.get();
+    return CTS_OK;
 }
 
 }  // namespace
@@ -231,7 +381,7 @@ int cts_engine_create(int device, cts_engine** out)
         e->geo.small_variant = cts::kDefaultSmallVariant;
     if (!cts::variant_ok(e->geo.ms_variant, cts::kDefaultMediaStreamVariant, cts_variant_count(kMediaStreamVariants)))
         e->geo.ms_variant = cts::kDefaultMediaStreamVariant;
-    e->sync_coalesce = env_int("CTS_SYNC_COALESCE", e->sync_coalesce) ? 1 : 0;
+    e->sync_mailbox = env_int("CTS_SYNC_MAILBOX", e->sync_mailbox) ? 1 : 0;
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
         delete e;
         return CTS_E_HIP;
@@ -254,6 +404,7 @@ int cts_engine_create(int device, cts_engine** out)
 int cts_engine_destroy(cts_engine* e)
 {
     if (e == nullptr) return CTS_E_INVALID;
+    e->mail.reset();  // stops the resident grid (kMailStop) and joins its watchdog
     {
         DeviceGuard g(e->device);
         if (e->stream) {
@@ -266,12 +417,6 @@ int cts_engine_destroy(cts_engine* e)
         if (e->batch_desc) (void)hipHostFree(e->batch_desc);
         if (e->batch_res) (void)hipHostFree(e->batch_res);
         if (e->batch_ctr) (void)hipHostFree(e->batch_ctr);
-        if (e->comb_stream) {
-            (void)hipStreamSynchronize(e->comb_stream);
-            (void)hipStreamDestroy(e->comb_stream);
-        }
-        if (e->comb_desc) (void)hipHostFree(e->comb_desc);
-        if (e->comb_res) (void)hipHostFree(e->comb_res);
     }
     delete e;
     return CTS_OK;
@@ -335,7 +480,7 @@ int cts_engine_set_attr(cts_engine* e, int attr, int value)
         if (value < 0 || value > (1 << 24)) return CTS_E_INVALID;
         e->geo.small_chunk = value;
         return CTS_OK;
-    case CTS_ATTR_SYNC_COALESCE: e->sync_coalesce = value ? 1 : 0; return CTS_OK;
+    case CTS_ATTR_SYNC_MAILBOX: e->sync_mailbox = value ? 1 : 0; return CTS_OK;
     case CTS_ATTR_FILL_NT:
         if (value < 0 || value > 2) return CTS_E_INVALID;
         e->geo.fill_nt = value;
@@ -358,7 +503,7 @@ int cts_engine_get_attr(const cts_engine* e, int attr, int* value)
     case CTS_ATTR_MS_VARIANT: *value = e->geo.ms_variant; return CTS_OK;
     case CTS_ATTR_SMALL_CHUNK: *value = e->geo.small_chunk; return CTS_OK;
     case CTS_ATTR_FILL_NT: *value = e->geo.fill_nt; return CTS_OK;
-    case CTS_ATTR_SYNC_COALESCE: *value = e->sync_coalesce; return CTS_OK;
+    case CTS_ATTR_SYNC_MAILBOX: *value = e->sync_mailbox; return CTS_OK;
     default: return CTS_E_INVALID;
     }
 }
@@ -584,27 +729,19 @@ int cts_verify_mapped(cts_engine* e, const void* dev_buf, uint32_t len, uint32_t
 {
     if (e == nullptr || out == nullptr || (dev_buf == nullptr && len != 0)) return CTS_E_INVALID;
     if (expected_offset >= CTS_PATTERN_PERIOD) return CTS_E_INVALID;
-    cts_sync_req me{static_cast<const uint8_t*>(dev_buf), len, expected_offset, cts_verify_result{}, CTS_OK, false};
-    std::unique_lock<std::mutex> lk(e->comb_mu);
-    e->comb_q.push_back(&me);
-    while (!me.done) {
-        if (e->comb_busy) {
-            e->comb_cv.wait(lk);
-            continue;
-        }
-        // leader: take everyone queued so far (callers that arrive during this launch form the next one)
-        e->comb_busy = true;
-        std::vector<cts_sync_req*> batch;
-        batch.swap(e->comb_q);
-        lk.unlock();
-        run_sync_group(e, batch);
-        lk.lock();
-        for (cts_sync_req* r : batch) r->done = true;
-        e->comb_busy = false;
-        e->comb_cv.notify_all();
+    if (len == 0) {  // RtlCompareMemory of nothing: a match (no device work)
+        *out = cts_verify_result{0, 0, 0, 0, 1, 0};
+        return CTS_OK;
     }
-    *out = me.out;
-    return me.rc;
+    Mailbox* m = nullptr;
+    const int rc = mailbox_of(e, &m);
+    if (rc != CTS_OK) return rc;
+    return m->Post(reinterpret_cast<uint64_t>(dev_buf), len, expected_offset, out, false);
+}
+
+uint64_t cts_mailbox_launches(const cts_engine* e)
+{
+    return (e != nullptr && e->mail) ? e->mail->launches.load(std::memory_order_relaxed) : 0;
 }
 
 }  // extern "C"

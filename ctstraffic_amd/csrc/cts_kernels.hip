@@ -1787,6 +1787,133 @@ static void launch_verify_nt(const uint8_t* arena, uint64_t arena_bytes, const c
     }
 }
 
+// ---- SYNC mailbox: VerifyBuffer (ctsIOPattern.cpp:745-775) per completion without a launch per call ----
+// A resident grid of G groups x kMailGroup workgroups; ticket t belongs to group t mod G. Lane 0 of
+// each of the group's workgroups polls the ticket's slot with one 16-B system-scope load
+// (+ s_sleep); then the group splits the job's buffer into 4 KiB pieces (one 16-B system-scope load
+// per lane: the host rewrites a reused recv slot between jobs, so nothing may come from a cache) and
+// compares against the pattern regenerated in registers. Each participating workgroup posts one
+// tagged part record to host memory and the caller folds them. No device atomics, fences or
+// inter-workgroup hand-offs sit on the critical path: a job costs the poll's and the data's PCIe
+// round trips (1.2 us each, tools/mailbox_probe) plus one posted write; G jobs run side by side.
+constexpr int kMailAux = 1 | 16;  // sc0 sc1: system scope
+
+__global__ __launch_bounds__(kBlock) void mailbox_kernel(const MailSlot* slots, MailPart* parts, uint32_t nslots,
+                                                         uint64_t t0, uint64_t idle_ticks)
+{
+    __shared__ uint64_t s_job[2];
+    __shared__ uint32_t s_first[kBlock / 64], s_count[kBlock / 64];
+    const uint32_t G = gridDim.x / kMailGroup, g = blockIdx.x / kMailGroup, gi = blockIdx.x % kMailGroup;
+    const uint32_t tid = threadIdx.x;
+    typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+    for (uint64_t t = t0 + (g + G - (uint32_t)(t0 % G)) % G;; t += G) {  // this group's tickets
+        const uint32_t k = (uint32_t)(t % nslots);
+        const uint32_t tag = (uint32_t)(t + 1);
+        if (tid == 0) {
+            const __amdgpu_buffer_rsrc_t r =
+                __builtin_amdgcn_make_buffer_rsrc(const_cast<MailSlot*>(slots + k), (short)0, 16, 0x00020000);
+            const uint64_t start = wall_clock64();
+            u64x2 job = {0, 0};
+            for (;;) {
+                const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, 0u, 0u, kMailAux);
+                job = u64x2{(uint64_t)v[0] | ((uint64_t)v[1] << 32), (uint64_t)v[2] | ((uint64_t)v[3] << 32)};
+                if ((uint32_t)(job[1] >> 32) == tag) break;
+                if (wall_clock64() - start > idle_ticks) {
+                    job[1] = 0;  // no job for this ticket within idle_ticks: leave
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+            s_job[0] = job[0];
+            s_job[1] = job[1];
+        }
+        __syncthreads();
+        const uint64_t ptr_exp = s_job[0], len_seq = s_job[1];
+        __syncthreads();  // s_job is rewritten for the next ticket only after every wave read it
+        if ((uint32_t)(len_seq >> 32) != tag) return;
+        const uint64_t ptr = ptr_exp & 0xFFFFFFFFFFFFull;
+        const uint32_t expected = (uint32_t)(ptr_exp >> 48), len = (uint32_t)len_seq;
+        if (gi >= mail_parts(ptr, len)) continue;
+        MailPart* const out = parts + (size_t)k * kMailGroup + gi;
+        if (len == 0) {  // stop: every workgroup of the group acknowledges, then leaves
+            if (tid == 0) {
+                __hip_atomic_store(&out->g0, 0xFFFFFFFFull | ((uint64_t)tag << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(&out->g1, (uint64_t)(tag & 0xFFFFFFu) << 40, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            return;
+        }
+        const uint32_t d = (uint32_t)ptr & 15u;
+        const uint64_t nchunks = ((uint64_t)d + len + 15u) >> 4;
+        const uint32_t pieces = (uint32_t)((nchunks * 16u + kMailPieceBytes - 1) / kMailPieceBytes);
+        const uint8_t* const base = reinterpret_cast<const uint8_t*>(ptr - d);
+        const uint32_t q_base = (expected + 65536u - d) & 0xFFFFu;  // pattern position of base[0]
+        const uint32_t hi_last = ((d + len - 1u) & 15u) + 1u;
+        uint32_t first = kNone, count = 0;
+        for (uint32_t u0 = gi; u0 < pieces; u0 += 4 * kMailGroup) {
+            u32x4 v[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {  // four pieces' loads in flight before any compare
+                const uint32_t u = u0 + j * kMailGroup;
+                const uint64_t off = (uint64_t)u * kMailPieceBytes;
+                const uint64_t rem = u < pieces ? nchunks * 16u - off : 0u;
+                const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+                    const_cast<uint8_t*>(base + (u < pieces ? off : 0u)), (short)0,
+                    (int)(rem < kMailPieceBytes ? rem : kMailPieceBytes), 0x00020000);
+                v[j] = __builtin_amdgcn_raw_buffer_load_b128(r, tid * 16u, 0u, kMailAux);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint64_t c = (uint64_t)(u0 + j * kMailGroup) * (kMailPieceBytes / 16u) + tid;
+                if (u0 + j * kMailGroup >= pieces || c >= nchunks) continue;
+                const uint32_t q = (uint32_t)((q_base + c * 16u) & 0xFFFFu);
+                u32x4 x = v[j] ^ expected_chunk(q, q & 1u);
+                if (c == 0 || c == nchunks - 1) x &= range_mask(c == 0 ? d : 0u, c == nchunks - 1 ? hi_last : 16u);
+                if (or4(x) == 0u) continue;
+#pragma unroll
+                for (int w = 0; w < 4; ++w) {
+                    const uint32_t nz = nonzero_bytes(x[w]);
+                    if (nz == 0u) continue;
+                    const uint32_t pos = (uint32_t)(c * 16u - d) + 4u * w + ((uint32_t)__builtin_ctz(nz) >> 3);
+                    first = pos < first ? pos : first;
+                    count += (uint32_t)__builtin_popcount(nz);
+                }
+            }
+        }
+        first = wave_min(first);
+        count = wave_sum(count);
+        if ((tid & 63u) == 0) {
+            s_first[tid >> 6] = first;
+            s_count[tid >> 6] = count;
+        }
+        __syncthreads();
+        if (tid == 0) {
+#pragma unroll
+            for (int w = 1; w < kBlock / 64; ++w) {
+                first = s_first[w] < first ? s_first[w] : first;
+                count += s_count[w];
+            }
+            uint32_t actual = 0;
+            if (first != kNone) {  // the received byte there (ctsIOPattern.cpp:761-772 prints it)
+                const __amdgpu_buffer_rsrc_t r =
+                    __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base + d + first), (short)0, 1, 0x00020000);
+                actual = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(r, 0u, 0u, kMailAux);
+            }
+            __hip_atomic_store(&out->g0, (uint64_t)first | ((uint64_t)tag << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&out->g1, (uint64_t)count | ((uint64_t)actual << 32) | ((uint64_t)(tag & 0xFFFFFFu) << 40),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        __syncthreads();  // s_first / s_count are rewritten by the next ticket
+    }
+}
+
+hipError_t launch_mailbox(const MailSlot* slots, MailPart* parts, uint32_t nslots, uint64_t t0, uint32_t groups,
+                          uint64_t idle_ticks, hipStream_t stream)
+{
+    if (slots == nullptr || parts == nullptr || nslots == 0 || groups == 0) return hipErrorInvalidValue;
+    mailbox_kernel<<<groups * kMailGroup, kBlock, 0, stream>>>(slots, parts, nslots, t0, idle_ticks);
+    return hipGetLastError();
+}
+
 hipError_t launch_verify(const uint8_t* arena, uint64_t arena_bytes, const cts_buf_desc* descs, uint32_t n,
                          uint32_t max_length_hint, cts_verify_result* results, uint64_t* counters,
                          uint32_t* conn_first_fail, uint32_t n_conns, hipStream_t stream,

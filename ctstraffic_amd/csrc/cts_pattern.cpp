@@ -643,8 +643,8 @@ struct cts_io_pattern {
         if (recv_pinned.host != nullptr && rp >= recv_pinned.host && rp + transferred <= recv_pinned.host + recv_pinned.bytes) {
             // zero copy: the kernel reads the pinned recv buffer in place over PCIe, as up to
             // cts::kSliceMax slices so the reads go out together (latency-bound; cts_slices.hpp)
-            int coalesce = 0;
-            if (cts_engine_get_attr(engine, CTS_ATTR_SYNC_COALESCE, &coalesce) == CTS_OK && coalesce)
+            int mailbox = 0;
+            if (cts_engine_get_attr(engine, CTS_ATTR_SYNC_MAILBOX, &mailbox) == CTS_OK && mailbox)
                 return cts_verify_mapped(engine, recv_pinned.dev + (rp - recv_pinned.host), transferred,
                                          t.expected_pattern_offset, &r);
             int rc = EnsureStream();

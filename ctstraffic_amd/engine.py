@@ -219,13 +219,17 @@ class Engine:
                 "expected": r.expected, "actual": r.actual, "flags": r.flags}
 
     def verify_mapped(self, dev_ptr: int, length: int, expected_offset: int) -> dict:
-        """cts_verify_mapped: one GPU-addressable buffer verified in place and waited for; concurrent
-        callers (threads) are combined into one launch by the engine."""
+        """cts_verify_mapped: one GPU-addressable buffer verified in place and waited for, through the
+        engine's resident mailbox grid (no launch per call); concurrent callers' jobs run side by side."""
         r = CtsVerifyResult()
         check("cts_verify_mapped", self._L.cts_verify_mapped(self._h, dev_ptr, length, expected_offset,
                                                            ctypes.byref(r)))
         return {"pass": bool(r.pass_), "first_mismatch": r.first_mismatch, "mismatch_bytes": r.mismatch_bytes,
                 "expected": r.expected, "actual": r.actual, "flags": r.flags}
+
+    def mailbox_launches(self) -> int:
+        """How often the mailbox grid behind verify_mapped was (re)started."""
+        return int(self._L.cts_mailbox_launches(self._h))
 
     def verify_host_batch(self, bufs: Sequence[np.ndarray], expected: Sequence[int],
                           skip_heads: Optional[Sequence[int]] = None):

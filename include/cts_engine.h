@@ -135,7 +135,9 @@ typedef enum cts_engine_attr {
     CTS_ATTR_MS_VARIANT = 8,          /* MediaStream receive kernel (cts_media_stream_verify) */
     CTS_ATTR_SMALL_CHUNK = 9,         /* chunked small-buffer walk: buffers per chunk (0 = contiguous) */
     CTS_ATTR_FILL_NT = 10,            /* cts_fill stores: 0 plain, 1 nontemporal, 2 by path (default) */
-    CTS_ATTR_SYNC_COALESCE = 11       /* 1 = SYNC-mode pattern verifies go through cts_verify_mapped */
+    CTS_ATTR_SYNC_MAILBOX = 11        /* 1 (default) = SYNC-mode pattern verifies of pinned recv buffers go
+                                       * through cts_verify_mapped (the resident mailbox grid); 0 = one
+                                       * sliced launch + synchronize per completion */
 } cts_engine_attr;
 int cts_engine_set_attr(cts_engine* engine, int attr, int value);
 /* A non-blocking HIP stream on the engine's device, whatever device the calling
@@ -203,13 +205,20 @@ int cts_verify_host(cts_engine* engine, const void* host_buf, uint32_t len,
 
 /* The same one-buffer VerifyBuffer (ctsIOPattern.cpp:745-775) for a buffer the
  * GPU can already address (a cts_host_alloc dev_view, or HBM), verified in
- * place and waited for. Thread-safe and coalescing: callers that arrive while
- * a launch is in flight (concurrent connections' CompleteIo, each serialised
- * per connection by its ctsSocket lock, ctsSocket.h:189) are verified together
- * in the next single launch, one launch + synchronize for the whole group.
- * Each caller receives exactly its own buffer's record. */
+ * place and waited for, without a kernel launch per call: a resident grid on
+ * the engine's device polls a ring of host-coherent pinned job slots, verifies
+ * each posted buffer as 4 KiB pieces spread over its workgroups and writes the
+ * record back to the slot, which the caller spins on. Thread-safe: concurrent
+ * connections' CompleteIo (each serialised per connection by its ctsSocket
+ * lock, ctsSocket.h:189) post independent tickets whose pieces run side by
+ * side. The grid starts on the first call and stops after
+ * CTS_MAILBOX_IDLE_MS (default 50) ms without calls (env CTS_MAILBOX_GROUPS,
+ * CTS_MAILBOX_SLOTS size it); cts_engine_destroy stops it. */
 int cts_verify_mapped(cts_engine* engine, const void* dev_buf, uint32_t len,
                       uint32_t expected_offset, cts_verify_result* out);
+/* How many times the mailbox grid was launched (0 = never used): each launch serves every
+ * cts_verify_mapped call until the grid goes idle. */
+uint64_t cts_mailbox_launches(const cts_engine* engine);
 
 /* Pinned host arenas (the recv-buffer container of a GPU-verified
  * ctsIoPattern, ctsIOPattern.cpp:156-175): page-locked and mapped into the

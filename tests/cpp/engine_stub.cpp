@@ -39,6 +39,7 @@ int cts_verify(cts_engine*, const void*, uint64_t, const cts_buf_desc*, uint32_t
 
 int cts_verify_host(cts_engine*, const void*, uint32_t, uint32_t, cts_verify_result*) { return CTS_E_NO_DEVICE; }
 int cts_verify_mapped(cts_engine*, const void*, uint32_t, uint32_t, cts_verify_result*) { return CTS_E_NO_DEVICE; }
+uint64_t cts_mailbox_launches(const cts_engine*) { return 0; }
 int cts_engine_get_attr(const cts_engine*, int, int*) { return CTS_E_NO_DEVICE; }
 
 int cts_engine_stream_create(cts_engine*, void**) { return CTS_E_NO_DEVICE; }

@@ -389,10 +389,11 @@ def test_verify_host_single_slice_edges(engine):
                 o["pass"], o["first_mismatch"], o["expected"], o["actual"], o["mismatch_bytes"]), (n, trial)
 
 
-def test_verify_mapped_coalesced_threads(engine):
-    """cts_verify_mapped from 16 threads at once (SYNC verifies of concurrent connections): the engine
-    combines whatever is queued into one launch over buffers in separate pinned arenas; every caller
-    must get exactly the oracle's record for its own buffer (ctsIOPattern.cpp:745-775)."""
+def test_verify_mapped_mailbox_threads(engine):
+    """cts_verify_mapped from 16 threads at once (SYNC verifies of concurrent connections) through the
+    resident mailbox grid, over buffers in separate pinned arenas that every thread rewrites between calls
+    (a reused recv slot: nothing may be answered from a cache); every caller must get exactly the oracle's
+    record for its own buffer (ctsIOPattern.cpp:745-775)."""
     import threading
     S = oracle.sender_buffer(140000)
     T, ITERS, CAP = 16, 40, 70000
@@ -430,6 +431,41 @@ def test_verify_mapped_coalesced_threads(engine):
         for _, h, _ in arenas:
             engine.host_free(h)
     assert not errors, errors[:5]
+
+
+def test_verify_mapped_mailbox_restarts_after_idle(engine):
+    """The mailbox grid stops after CTS_MAILBOX_IDLE_MS (50 ms) without posts and the next post starts it again;
+    answers stay exact across the restart, including an HBM buffer and a buffer larger than the grid's
+    64 x 4 KiB of pieces per round (several rounds per workgroup)."""
+    import time
+
+    import torch
+
+    S = oracle.sender_buffer(3 << 20)
+    arr, h, dev = engine.host_alloc(1 << 20)
+    try:
+        before = engine.mailbox_launches()
+        for rnd in range(3):
+            n = [65536, 1 << 20, 12345][rnd]
+            e = [7, 65535, 0][rnd]
+            arr[:n] = S[e:e + n]
+            arr[n // 3] ^= 0x5A
+            r = engine.verify_mapped(dev, n, e)
+            o = oracle.verify_buffer(arr[:n].copy(), 0, e, n)
+            assert (r["pass"], r["first_mismatch"], r["expected"], r["actual"], r["mismatch_bytes"]) == (
+                o["pass"], o["first_mismatch"], o["expected"], o["actual"], o["mismatch_bytes"])
+            time.sleep(0.3)
+        assert engine.mailbox_launches() - before == 3
+        # an HBM buffer (the ABI takes any GPU-addressable pointer)
+        d = torch.from_numpy(S[100:100 + 300001].copy()).cuda()
+        r = engine.verify_mapped(d.data_ptr(), 300001, 100)
+        assert r["pass"] and r["first_mismatch"] == 300001 and r["mismatch_bytes"] == 0
+        d[299999] ^= 1
+        torch.cuda.synchronize()
+        r = engine.verify_mapped(d.data_ptr(), 300001, 100)
+        assert (r["pass"], r["first_mismatch"], r["mismatch_bytes"]) == (False, 299999, 1)
+    finally:
+        engine.host_free(h)
 
 
 def test_verify_host_batch(engine):

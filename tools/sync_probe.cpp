@@ -4,7 +4,8 @@
 // Variants: the buffer described as S slices (S descriptors of 64 KiB / S, expected offsets advanced,
 // so S workgroups/waves issue their PCIe reads at once) and T threads, each with its own stream,
 // buffer, descriptor and result (T connections completing concurrently). Wait = hipStreamSynchronize
-// or a hipStreamQuery spin, or cts_verify_mapped (the engine combines concurrent callers into one launch). Prints one JSON line per variant: us per verify (per thread).
+// or a hipStreamQuery spin, or cts_verify_mapped (posted to the engine's resident mailbox grid: no launch per
+// verify). Prints one JSON line per variant: us per verify (per thread).
 //   build: make tools/sync_probe      run: tools/sync_probe [iters]
 #include <hip/hip_runtime_api.h>
 
@@ -34,7 +35,7 @@ static int run_thread(cts_engine* e, uint32_t slices, bool spin, bool mapped, in
     auto* res_d = reinterpret_cast<cts_verify_result*>(static_cast<uint8_t*>(dd) + 2048);
     hipStream_t s = static_cast<hipStream_t>(stream);
     auto once = [&]() {
-        if (mapped) {  // cts_verify_mapped: concurrent threads' verifies coalesce into one launch
+        if (mapped) {  // cts_verify_mapped: the mailbox grid
             cts_verify_result r{};
             return cts_verify_mapped(e, dev, len, 1000, &r) == CTS_OK && r.pass && r.first_mismatch == len;
         }
@@ -69,7 +70,7 @@ int main(int argc, char** argv)
     const int iters = argc > 1 ? std::atoi(argv[1]) : 2000;
     cts_engine* e = nullptr;
     if (cts_engine_create(0, &e) != CTS_OK) return 1;
-    // wait: 0 stream_sync, 1 query_spin, 2 cts_verify_mapped (coalescing; slices = its own plan, 64)
+    // wait: 0 stream_sync, 1 query_spin, 2 cts_verify_mapped (mailbox; slices = its 4 KiB pieces, reported as 64)
     for (int spin = 0; spin < 3; ++spin)
         for (uint32_t threads : {1u, 8u, 16u})
             for (uint32_t slices : {1u, 2u, 4u, 8u, 16u, 32u, 64u}) {
@@ -90,7 +91,7 @@ int main(int argc, char** argv)
                 }
                 std::printf("{\"wait\": \"%s\", \"threads\": %u, \"slices\": %u, \"us_per_verify\": %.2f, "
                             "\"GBps_total\": %.2f, \"bad\": %d, \"rc\": %d}\n",
-                            spin == 2 ? "mapped_coalesced" : spin ? "query_spin" : "stream_sync", threads, slices, mean,
+                            spin == 2 ? "mailbox" : spin ? "query_spin" : "stream_sync", threads, slices, mean,
                             threads * 65536.0 / (mean * 1e3), nbad, nrc);
                 std::fflush(stdout);
             }
