@@ -22,7 +22,7 @@ TUNING_OBJS := $(patsubst $(CSRC)/%,ctstraffic_amd/build/tuning/%.o,$(TUNED)) \
 SOFLAGS   := -shared -Wl,-Bsymbolic -Wl,--version-script=$(CSRC)/exports.map
 
 DEVICE_VERIFY := ctstraffic_amd/build/device_verify
-TOOLS := tools/hbm_read_ceiling tools/verify_ablation tools/mailbox_probe
+TOOLS := tools/hbm_read_ceiling tools/verify_ablation tools/mailbox_probe tools/rw_mix_probe
 
 SYNC_PROBE := tools/sync_probe
 

@@ -533,6 +533,12 @@ def run_extras(engine, torch, W, w, arenas, descs, dev, want):
             t = _time_kernel(torch, lambda i: MS.verify(engine, ad, dd, records=recs, results=res), 10)
             out["media_stream_verify_GiBps"] = round(wd.verified_bytes() / t / GIB, 1)
             out["media_stream_verify_Mdgram_per_s"] = round(wd.n / t / 1e6, 1)
+            # the same receive pass over the ring's descriptor-free form (datagram i at i * 1472, lengths only)
+            lens = torch.from_numpy(wd.descs["length"].astype(np.uint32)).to(dev)
+            t = _time_kernel(torch, lambda i: MS.verify_strided(engine, ad, wd.max_length, lens, records=recs,
+                                                                results=res), 10)
+            out["media_stream_strided_verify_GiBps"] = round(wd.verified_bytes() / t / GIB, 1)
+            del lens
             del recs, res
             del ad, dd
         except Exception as e:  # pragma: no cover

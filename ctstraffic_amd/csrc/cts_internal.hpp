@@ -121,6 +121,12 @@ hipError_t launch_media_stream_verify(const uint8_t* arena, uint64_t arena_bytes
                                      cts_datagram_record* records, cts_verify_result* results, uint64_t* counters,
                                      hipStream_t stream, const LaunchGeometry& geo);
 
+// Receive ring: datagram i at arena + i * stride, lengths[i] completed bytes (the windowed kernel).
+hipError_t launch_media_stream_verify_strided(const uint8_t* arena, uint64_t arena_bytes, uint32_t stride,
+                                             const uint32_t* lengths, uint32_t n, cts_datagram_record* records,
+                                             cts_verify_result* results, uint64_t* counters, hipStream_t stream,
+                                             const LaunchGeometry& geo);
+
 hipError_t launch_media_stream_fill(uint8_t* arena, uint64_t arena_bytes, const cts_buf_desc* descs,
                                    const cts_datagram_header* headers, uint32_t n, hipStream_t stream,
                                    const LaunchGeometry& geo);

@@ -1041,7 +1041,9 @@ __device__ __forceinline__ void quad_flush_outputs(const QuadOut& o, uint32_t i,
     if (records != nullptr && l < 32u) {
         const uint32_t t = l >> 3;
         const uint32_t v = o.rec[t][l & 7u];
-        if (i0 + t < n) reinterpret_cast<uint32_t*>(records)[8ull * i0 + l] = v;
+        if (i0 + t < n)
+            __hip_atomic_store(reinterpret_cast<uint32_t*>(records) + 8ull * i0 + l, v, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
     }
     __builtin_amdgcn_wave_barrier();
 }
@@ -1500,13 +1502,34 @@ __device__ __forceinline__ void header_dwords_hdr16(u32x4 own, uint32_t ho, uint
     for (int k = 0; k < 6; ++k) H[k] = __builtin_amdgcn_alignbyte(V[k + 1], V[k], s);
 }
 
+// Where a received datagram sits: a descriptor (cts_media_stream_verify), or slot i of a uniformly
+// strided receive ring with its completed length in lens[i] (STRIDED: cts_media_stream_verify_strided,
+// 4 B of metadata per datagram instead of a 24-B descriptor).
+struct MsSource {
+    const cts_buf_desc* descs;  // !STRIDED
+    const uint32_t* lens;       // STRIDED
+    uint32_t stride;
+};
+
+template <bool STRIDED>
+__device__ __forceinline__ void ms_datagram(const MsSource& src, uint32_t i, uint64_t& off, uint32_t& len)
+{
+    if constexpr (STRIDED) {
+        off = (uint64_t)i * src.stride;
+        len = src.lens[i];
+    } else {
+        const cts_buf_desc d = src.descs[i];
+        off = d.byte_offset;
+        len = d.length;
+    }
+}
+
 // HDR16 = false: header bytes j and j + 16 by byte loads on every team lane, dwords gathered by
 // lane shuffles (ms_variant 1). HDR16 = true: three 16-byte header chunk loads on team lanes
 // 0..2, gathered on lane 0 by DPP row shifts; the DATA verdict is broadcast (ms_variant 2).
-template <int U, bool NT, bool ALIGN, bool HDR16, bool CONTIG = false>
+template <int U, bool NT, bool ALIGN, bool HDR16, bool CONTIG = false, bool STRIDED = false>
 __global__ void __launch_bounds__(kBlock)
-    media_stream_verify_quad_kernel(const uint8_t* __restrict__ arena, uint64_t arena_bytes,
-                                    const cts_buf_desc* __restrict__ descs, uint32_t n,
+    media_stream_verify_quad_kernel(const uint8_t* __restrict__ arena, uint64_t arena_bytes, MsSource src, uint32_t n,
                                     cts_datagram_record* __restrict__ records, cts_verify_result* __restrict__ results,
                                     uint64_t* __restrict__ counters, uint32_t per = 0)
 {
@@ -1515,21 +1538,26 @@ __global__ void __launch_bounds__(kBlock)
     __shared__ QuadOut qout[kBlock / 64];
     const uint32_t lane = threadIdx.x & (kQuadTeam - 1);
     const uint32_t team = threadIdx.x / kQuadTeam;
-    const void* dummy = reinterpret_cast<const void*>(((uintptr_t)descs + 15u) & ~(uintptr_t)15u);
+    // dummy target of an empty span's clamped loads: 16-byte-aligned bytes the launch owns
+    const void* dummy = STRIDED ? reinterpret_cast<const void*>(arena)
+                                : reinterpret_cast<const void*>(((uintptr_t)src.descs + 15u) & ~(uintptr_t)15u);
     const uint8_t* dummy8 = reinterpret_cast<const uint8_t*>(dummy);
     QCounters qc;
     QuadWalk<CONTIG, TEAMS> w(n, per, team);
-    cts_buf_desc dn = descs[w.i < n ? w.i : n - 1u];
+    uint64_t noff;
+    uint32_t nlen;
+    ms_datagram<STRIDED>(src, w.i < n ? w.i : n - 1u, noff, nlen);
     while (__any(w.i < w.end)) {
         const uint32_t i = w.i;
-        const cts_buf_desc d = dn;
+        const uint64_t doff = noff;
+        const uint32_t completed = nlen;
         const uint32_t inext = w.next();
-        dn = descs[inext < n ? inext : n - 1u];
+        ms_datagram<STRIDED>(src, inext < n ? inext : n - 1u, noff, nlen);  // clamped: no load under a branch
         const bool live = i < w.end;
-        const uint32_t completed = d.length;
-        const bool bad = d.byte_offset > arena_bytes || arena_bytes - d.byte_offset < (uint64_t)completed;
+        const bool bad = doff > arena_bytes || arena_bytes - doff < (uint64_t)completed ||
+                         (STRIDED && completed > src.stride);
         const bool in = live && !bad;
-        const uint8_t* dg = arena + d.byte_offset;
+        const uint8_t* dg = arena + (in ? doff : 0u);
         uint32_t hb0 = 0, hb1 = 0;
         bool h0 = false, h1 = false;
         u32x4 hch = u32x4{0u, 0u, 0u, 0u};
@@ -1955,18 +1983,18 @@ hipError_t launch_media_stream_verify(const uint8_t* arena, uint64_t arena_bytes
                                      hipStream_t stream, const LaunchGeometry& geo)
 {
     if (n == 0) return hipSuccess;
-#define CTS_MS_ARGS arena, arena_bytes, descs, n, records, results, counters
+#define CTS_MS_ARGS arena, arena_bytes, MsSource{descs, nullptr, 0u}, n, records, results, counters
     // ms_variant: 0 = one wave per datagram, 1 = four datagrams per wave (header by byte loads),
     // 2 = four per wave, header by three 16-byte chunk loads + DPP, 3 = variant 2 walking
     // block-contiguous datagram ranges (default)
     const uint32_t qgrid = grid_for(n, kBlock / kQuadTeam, geo);
     const uint32_t grid = grid_for(n, kBlock / 64, geo);
-    const bool nt = geo.nontemporal != 0;
 #if CTS_TUNING
+    const bool nt = geo.nontemporal != 0;
     switch (geo.ms_variant) {
     case 0:
-        if (nt) media_stream_verify_kernel<2, true><<<grid, kBlock, 0, stream>>>(CTS_MS_ARGS);
-        else media_stream_verify_kernel<2, false><<<grid, kBlock, 0, stream>>>(CTS_MS_ARGS);
+        if (nt) media_stream_verify_kernel<2, true><<<grid, kBlock, 0, stream>>>(arena, arena_bytes, descs, n, records, results, counters);
+        else media_stream_verify_kernel<2, false><<<grid, kBlock, 0, stream>>>(arena, arena_bytes, descs, n, records, results, counters);
         break;
     case 1:
         if (nt) media_stream_verify_quad_kernel<6, true, true, false><<<qgrid, kBlock, 0, stream>>>(CTS_MS_ARGS);
@@ -1991,12 +2019,30 @@ hipError_t launch_media_stream_verify(const uint8_t* arena, uint64_t arena_bytes
     (void)qgrid;
     (void)grid;
     const ContigGrid cg = contig_grid(n, geo);  // MediaStream variant 3 (kDefaultMediaStreamVariant)
-    if (nt)
+    if (geo.nontemporal)
         media_stream_verify_quad_kernel<6, true, true, true, true><<<cg.grid, kBlock, 0, stream>>>(CTS_MS_ARGS, cg.per);
     else
         media_stream_verify_quad_kernel<6, false, true, true, true><<<cg.grid, kBlock, 0, stream>>>(CTS_MS_ARGS, cg.per);
 #endif
 #undef CTS_MS_ARGS
+    return hipGetLastError();
+}
+
+hipError_t launch_media_stream_verify_strided(const uint8_t* arena, uint64_t arena_bytes, uint32_t stride,
+                                             const uint32_t* lengths, uint32_t n, cts_datagram_record* records,
+                                             cts_verify_result* results, uint64_t* counters, hipStream_t stream,
+                                             const LaunchGeometry& geo)
+{
+    if (n == 0) return hipSuccess;
+    // the variant-3 walk (block-contiguous ranges, four datagrams per wave) over the ring's slots
+    const ContigGrid cg = contig_grid(n, geo);
+    const MsSource src{nullptr, lengths, stride};
+    if (geo.nontemporal)
+        media_stream_verify_quad_kernel<6, true, true, true, true, true><<<cg.grid, kBlock, 0, stream>>>(
+            arena, arena_bytes, src, n, records, results, counters, cg.per);
+    else
+        media_stream_verify_quad_kernel<6, false, true, true, true, true><<<cg.grid, kBlock, 0, stream>>>(
+            arena, arena_bytes, src, n, records, results, counters, cg.per);
     return hipGetLastError();
 }
 

@@ -49,6 +49,7 @@ def declare(L: ctypes.CDLL) -> None:
         "cts_media_stream_split": ([u64, u32, P, u64], u64),
         "cts_media_stream_fill": ([P, P, u64, P, P, u32, P], i32),
         "cts_media_stream_verify": ([P, P, u64, P, u32, P, P, P, P], i32),
+        "cts_media_stream_verify_strided": ([P, P, u64, u32, P, u32, P, P, P, P], i32),
         "cts_media_stream_client_create": ([ctypes.POINTER(Settings), ctypes.POINTER(P)], i32),
         "cts_media_stream_client_destroy": ([P], i32),
         "cts_media_stream_client_complete": ([P, P, P, u32, i64, i64, ctypes.POINTER(u32)], i32),
@@ -100,6 +101,22 @@ def verify(engine, arena, descs, records=None, results=None, counters=None, stre
     check("cts_media_stream_verify",
           engine._L.cts_media_stream_verify(engine._h, _ptr(arena), _nbytes(arena), _ptr(descs), n, _ptr(records),
                                         _ptr(results), _ptr(counters), _stream(stream)))
+
+
+def verify_strided(engine, arena, stride: int, lengths, records=None, results=None, counters=None,
+                   stream=None) -> None:
+    """cts_media_stream_verify_strided: datagram i at arena + i * stride, lengths (uint32 device tensor) its
+    completed bytes."""
+    from .engine import _check_outputs, _nbytes, _stream
+
+    n = _nbytes(lengths) // 4
+    _check_outputs(n, results, counters)
+    if records is not None and _nbytes(records) < n * DGRAM_RECORD_DTYPE.itemsize:
+        raise ValueError("records holds %d bytes, %d datagrams need %d" % (_nbytes(records), n,
+                                                                          n * DGRAM_RECORD_DTYPE.itemsize))
+    check("cts_media_stream_verify_strided",
+          engine._L.cts_media_stream_verify_strided(engine._h, _ptr(arena), _nbytes(arena), stride, _ptr(lengths), n,
+                                                _ptr(records), _ptr(results), _ptr(counters), _stream(stream)))
 
 
 class MediaStreamClient:

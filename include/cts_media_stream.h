@@ -97,6 +97,16 @@ int cts_media_stream_verify(cts_engine* engine, const void* dev_arena, uint64_t 
                             const cts_buf_desc* dev_descs, uint32_t n, cts_datagram_record* dev_records,
                             cts_verify_result* dev_results, void* dev_counters, void* stream);
 
+/* The same receive pass over a uniformly strided receive ring: datagram i occupies
+ * [i * stride, i * stride + dev_lengths[i]) of the arena (the completed byte count of the recv
+ * posted into that slot, ctsMediaStreamClient.cpp:268,404), so the kernel reads 4 bytes of
+ * metadata per datagram instead of a 24-byte descriptor. A length above the stride or past the
+ * arena is CTS_DGRAM_BAD_DESC. Outputs and counters as cts_media_stream_verify. dev_lengths must be
+ * 4-byte aligned, dev_arena 16-byte aligned with arena_bytes >= 16. */
+int cts_media_stream_verify_strided(cts_engine* engine, const void* dev_arena, uint64_t arena_bytes, uint32_t stride,
+                                    const uint32_t* dev_lengths, uint32_t n, cts_datagram_record* dev_records,
+                                    cts_verify_result* dev_results, void* dev_counters, void* stream);
+
 /* ---- client frame accounting (ctsIoPatternMediaStreamClient) ---------------- */
 typedef struct cts_media_stream_settings { /* ctsConfig::MediaStreamSettings */
     uint32_t frame_size_bytes;

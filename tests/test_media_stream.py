@@ -208,19 +208,21 @@ def test_gpu_media_stream_verify_matches_oracle(engine, tuning_engine, ms_varian
     engine.set_attr(_lib.ATTR_MS_VARIANT, ms_variant)
     try:
         # sbpc 1: several rounds per workgroup (5 000+ datagrams over 256 workgroups); chunked walks
-        for sbpc, chunk in ((1, 0), (64, 0), (1, 16), (2, 48)):
-            if chunk and ms_variant != 3:
+        for sbpc, chunk in ((1, 0), (64, 0), (1, 16), (2, 48), (1, 200)):
+            if chunk and ms_variant < 3:
                 continue
             engine.set_attr(_lib.ATTR_SMALL_BLOCKS_PER_CU, sbpc)
             engine.set_attr(_lib.ATTR_SMALL_CHUNK, chunk)
             _media_stream_verify_vs_oracle(engine)
+        if ms_variant == 3:  # outputs at 4-byte-aligned (not 16) addresses
+            _media_stream_verify_vs_oracle(engine, out_shift=4)
     finally:
         engine.set_attr(_lib.ATTR_MS_VARIANT, default)
         engine.set_attr(_lib.ATTR_SMALL_BLOCKS_PER_CU, default_sbpc)
         engine.set_attr(_lib.ATTR_SMALL_CHUNK, default_chunk)
 
 
-def _media_stream_verify_vs_oracle(engine):
+def _media_stream_verify_vs_oracle(engine, out_shift=0):
     import torch
 
     rng = np.random.default_rng(11)
@@ -241,8 +243,8 @@ def _media_stream_verify_vs_oracle(engine):
     er, eres, ectr = oracle.media_stream_verify(arena, descs)
     a = _to_dev(arena, torch)
     d = _to_dev(descs, torch)
-    recs = torch.zeros(len(dgs) * 32, dtype=torch.uint8, device="cuda")
-    res = engine.new_results(len(dgs))
+    recs = torch.zeros(len(dgs) * 32 + out_shift, dtype=torch.uint8, device="cuda")[out_shift:]
+    res = torch.zeros(len(dgs) * 12 + out_shift, dtype=torch.uint8, device="cuda")[out_shift:]
     ctr = engine.new_counters()
     M.verify(engine, a, d, records=recs, results=res, counters=ctr)
     torch.cuda.synchronize()
@@ -310,3 +312,59 @@ def test_gpu_media_stream_end_to_end(engine):
     assert code == 1
     s2 = cm2.stats()
     assert s2["successful_frames"] == n_frames and s2["dropped_frames"] == 0 and s2["last_error"] == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("stride", [1536, 1500, 9017])
+def test_gpu_media_stream_verify_strided_matches_oracle(engine, stride):
+    """cts_media_stream_verify_strided: a receive ring of datagrams at i * stride (16-byte-aligned slots and
+    odd strides) with their completed lengths only; records, results and counters equal the oracle's over the
+    same datagrams described by descriptors. Lengths above the stride are BAD_DESC."""
+    import torch
+
+    rng = np.random.default_rng(stride)
+    S = oracle.sender_buffer(stride + 64)
+    n = 7000
+    ring = np.full(n * stride + 64, 0xEE, dtype=np.uint8)
+    lens = np.zeros(n, dtype=np.uint32)
+    crafted = _crafted()
+    for i in range(n):
+        if i < len(crafted) * 3 and i % 3 == 0:
+            d = crafted[i // 3]
+        else:
+            ln = int(rng.integers(26, stride + 1))
+            d = bytearray(np.array([0], "<u2").tobytes() + np.array([i, rng.integers(0, 1 << 62),
+                                                                     rng.integers(0, 1 << 62)], "<i8").tobytes())
+            d += S[:ln - 26].tobytes()
+            if rng.random() < 0.05:
+                d[int(rng.integers(26, ln))] ^= int(rng.integers(1, 256)) if ln > 26 else 0
+            d = bytes(d)
+        ring[i * stride:i * stride + len(d)] = np.frombuffer(d, dtype=np.uint8)
+        lens[i] = len(d)
+    descs = np.zeros(n, dtype=DESC_DTYPE)
+    descs["byte_offset"] = np.arange(n, dtype=np.uint64) * stride
+    descs["length"] = lens
+    er, eres, ectr = oracle.media_stream_verify(ring, descs)
+    a = _to_dev(ring, torch)
+    ld = _to_dev(lens, torch)
+    recs = torch.zeros(n * 32, dtype=torch.uint8, device="cuda")
+    res = engine.new_results(n)
+    ctr = engine.new_counters()
+    M.verify_strided(engine, a, stride, ld, records=recs, results=res, counters=ctr)
+    torch.cuda.synchronize()
+    gr = recs.cpu().numpy().view(DGRAM_RECORD_DTYPE)
+    gres = res.cpu().numpy().view(RESULT_DTYPE)
+    for f in DGRAM_RECORD_DTYPE.names:
+        assert np.array_equal(gr[f], er[f]), f
+    for f in RESULT_DTYPE.names:
+        assert np.array_equal(gres[f], eres[f]), f
+    assert engine.read_counters(ctr) == ectr
+    # a completion longer than its slot is a bad descriptor, not read
+    lens2 = lens.copy()
+    lens2[5] = stride + 1
+    recs.zero_()
+    M.verify_strided(engine, a, stride, _to_dev(lens2, torch), records=recs, results=res)
+    torch.cuda.synchronize()
+    gr = recs.cpu().numpy().view(DGRAM_RECORD_DTYPE)
+    gres = res.cpu().numpy().view(RESULT_DTYPE)
+    assert gr["kind"][5] == 5 and gres["flags"][5] == 1 and gres["pass"][5] == 0

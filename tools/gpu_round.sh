@@ -20,6 +20,11 @@ if [[ $STEPS == all || $STEPS == *bench* ]]; then
   run bench
   timeout -k 10 400 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
 fi
+if [[ $STEPS == all || $STEPS == *engines* ]]; then
+  # single-process multi-GPU leg (the ctsTraffic process model) at the GPUs this box has
+  run engines
+  timeout -k 10 300 python bench.py --engines 1 --no-cpu-baseline --no-extras > "$OUT/bench_engines1.json" 2> "$OUT/bench_engines1.err"
+fi
 if [[ $STEPS == all || $STEPS == *ceiling* ]]; then
   # plain streaming-read reference on the same box (build: see tools/hbm_read_ceiling.hip)
   run ceiling

@@ -33,6 +33,7 @@ def main():
     for _ in range(args.arenas):
         a, d = W.materialize(eng, w)
         arenas.append(a)
+    lens = torch.from_numpy(w.descs["length"].astype("uint32")).cuda()
     recs = torch.empty(w.n * 32, dtype=torch.uint8, device="cuda")
     res = eng.new_results(w.n)
     ctr = eng.new_counters()
@@ -54,6 +55,9 @@ def main():
                       ("ms+records", ("ms", v, ch), lambda a: MS.verify(eng, a, d, records=recs)),
                       ("ms+records+results", ("ms", v, ch),
                        lambda a: MS.verify(eng, a, d, records=recs, results=res))]
+        # the receive ring's descriptor-free form (datagram i at i * 1472, lengths only; windowed kernel)
+        cases += [("ms_strided+records+results", ("ms", None, ch),
+                   lambda a: MS.verify_strided(eng, a, w.max_length, lens, records=recs, results=res))]
     cases = [c for c in cases if not only or c[0] in only]
     for r in range(args.rounds):
         for name, v, fn in cases:
