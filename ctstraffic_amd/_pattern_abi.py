@@ -14,6 +14,12 @@ PROTOCOL_TCP, PROTOCOL_UDP = 1, 2
 SHUTDOWN_GRACEFUL, SHUTDOWN_HARD = 1, 2
 VERIFY_SYNC, VERIFY_DEFERRED = 0, 1
 
+# ctsIoPatternType / ctsIoPatternError (ctsIOPatternState.hpp:27-48)
+(PT_NO_IO, PT_SEND_CONNECTION_ID, PT_RECV_CONNECTION_ID, PT_MORE_IO, PT_SEND_COMPLETION, PT_RECV_COMPLETION,
+ PT_GRACEFUL_SHUTDOWN, PT_HARD_SHUTDOWN, PT_REQUEST_FIN) = range(9)
+(PE_NO_ERROR, PE_TOO_MANY_BYTES, PE_TOO_FEW_BYTES, PE_CORRUPTED_BYTES, PE_ERROR_IO_FAILED,
+ PE_SUCCESSFULLY_COMPLETED) = range(6)
+
 STATUS_IO_RUNNING = 2147483647
 STATUS_ERROR_NOT_ALL_DATA_TRANSFERRED = 2147483646
 STATUS_ERROR_TOO_MUCH_DATA_TRANSFERRED = 2147483645
@@ -131,6 +137,20 @@ def declare(L: ctypes.CDLL) -> None:
         "cts_io_pattern_failure_message": ([P, ctypes.c_char_p, u32], i32),
         "cts_io_pattern_fail_fast_reason": ([P], ctypes.c_char_p),
         "cts_io_pattern_connection_id": ([P], ctypes.c_char_p),
+        "cts_io_pattern_state_create": ([ctypes.POINTER(CtsPatternConfig), ctypes.POINTER(P)], i32),
+        "cts_io_pattern_state_destroy": ([P], i32),
+        "cts_io_pattern_state_get_remaining_transfer": ([P], u64),
+        "cts_io_pattern_state_get_max_transfer": ([P], u64),
+        "cts_io_pattern_state_set_max_transfer": ([P, u64], i32),
+        "cts_io_pattern_state_get_ideal_send_backlog": ([P], u32),
+        "cts_io_pattern_state_set_ideal_send_backlog": ([P, u32], i32),
+        "cts_io_pattern_state_is_completed": ([P], i32),
+        "cts_io_pattern_state_is_current_state_more_io": ([P], i32),
+        "cts_io_pattern_state_get_next_pattern_type": ([P], i32),
+        "cts_io_pattern_state_notify_next_task": ([P, ctypes.POINTER(CtsTask)], i32),
+        "cts_io_pattern_state_completed_task": ([P, ctypes.POINTER(CtsTask), u32], i32),
+        "cts_io_pattern_state_update_error": ([P, u32], i32),
+        "cts_io_pattern_state_fail_fast_reason": ([P], ctypes.c_char_p),
         "cts_status_details_read": ([ctypes.POINTER(CtsStatusDetails)], i32),
         "cts_status_details_reset": ([], None),
     }

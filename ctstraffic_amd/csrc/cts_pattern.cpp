@@ -81,12 +81,14 @@ public:
                           ClientRecvCompletion, CompletedTransfer, ErrorIoFailed, GracefulShutdown, HardShutdown,
                           RequestFin };
 
-    PatternState(const cts_pattern_config& c, uint32_t max_buffer_size)
+    PatternState(const cts_pattern_config& c, uint32_t max_buffer_size)  // ctsIOPatternState.hpp:108-114
         : m_maxTransfer(c.transfer_size),
           m_idealSendBacklog(c.pre_post_sends == 0 ? max_buffer_size : max_buffer_size * c.pre_post_sends),
           m_listening(c.listening != 0),
-          m_graceful(c.tcp_shutdown != CTS_SHUTDOWN_HARD)
+          m_graceful(c.tcp_shutdown != CTS_SHUTDOWN_HARD),
+          m_udp(c.protocol == CTS_PROTOCOL_UDP)
     {
+        if (m_udp) m_internal = Internal::MoreIo;
     }
 
     uint64_t GetRemainingTransfer() const  // ctsIOPatternState.hpp:123-141
@@ -139,9 +141,16 @@ public:
         if (t.track_io) m_inFlightBytes += t.buffer_length;
     }
 
-    PatternError UpdateError(uint32_t error)  // ctsIOPatternState.hpp:254-293 (TCP branch)
+    PatternError UpdateError(uint32_t error)  // ctsIOPatternState.hpp:254-293
     {
         if (m_internal == Internal::ErrorIoFailed) return PatternError::ErrorIoFailed;
+        if (m_udp) {
+            if (error != 0) {
+                m_internal = Internal::ErrorIoFailed;
+                return PatternError::ErrorIoFailed;
+            }
+            return PatternError::NoError;
+        }
         if (error != 0 && !IsCompleted()) {
             // WSAETIMEDOUT / WSAECONNRESET / WSAECONNABORTED while a server waits for the FIN
             if (m_listening && m_internal == Internal::RequestFin && (error == 10060 || error == 10054 || error == 10053))
@@ -166,7 +175,7 @@ public:
         return false;
     }
 
-    PatternError CompletedTask(const cts_task& t, uint32_t bytes)  // ctsIOPatternState.hpp:295-504 (TCP)
+    PatternError CompletedTask(const cts_task& t, uint32_t bytes)  // ctsIOPatternState.hpp:295-504
     {
         if (m_internal == Internal::ErrorIoFailed) return PatternError::ErrorIoFailed;
         if (m_internal == Internal::ServerSendConnectionId || m_internal == Internal::ClientRecvConnectionId) {
@@ -184,6 +193,7 @@ public:
             m_confirmedBytes += bytes;
         }
         const uint64_t already = m_confirmedBytes + m_inFlightBytes;
+        if (m_udp) return already == m_maxTransfer ? PatternError::SuccessfullyCompleted : PatternError::NoError;
         if (already < m_maxTransfer) {
             if (bytes == 0) {
                 m_internal = Internal::ErrorIoFailed;
@@ -259,6 +269,7 @@ private:
     bool m_pended = false;
     bool m_listening;
     bool m_graceful;
+    bool m_udp;
 };
 
 // ---- pinned host memory helpers -------------------------------------------------------------
@@ -1306,6 +1317,124 @@ const char* cts_io_pattern_fail_fast_reason(const cts_io_pattern* p)
 }
 
 const char* cts_io_pattern_connection_id(cts_io_pattern* p) { return p ? p->connection_id : nullptr; }
+
+}  // extern "C"
+
+// ---- ctsIoPatternState on its own (ctsIOPatternState.hpp:51-504) ----------------------------
+struct cts_io_pattern_state {
+    PatternState st;
+    std::string fail_fast;
+    explicit cts_io_pattern_state(const cts_pattern_config& c)
+        : st(c, c.buffer_size_high ? c.buffer_size_high : c.buffer_size_low)
+    {
+    }
+};
+
+namespace {
+// an internal-consistency FAIL_FAST of the reference: latched, reported as CTS_E_INVALID
+template <typename F>
+int state_call(cts_io_pattern_state* s, F f)
+{
+    if (s == nullptr) return CTS_E_INVALID;
+    if (!s->fail_fast.empty()) return CTS_E_INVALID;
+    try {
+        return f();
+    } catch (const FailFast& e) {
+        s->fail_fast = e.reason;
+        return CTS_E_INVALID;
+    }
+}
+}  // namespace
+
+extern "C" {
+
+int cts_io_pattern_state_create(const cts_pattern_config* c, cts_io_pattern_state** out)
+{
+    if (c == nullptr || out == nullptr) return CTS_E_INVALID;
+    *out = nullptr;
+    if (c->protocol != CTS_PROTOCOL_TCP && c->protocol != CTS_PROTOCOL_UDP) return CTS_E_INVALID;
+    cts_io_pattern_state* s = new (std::nothrow) cts_io_pattern_state(*c);
+    if (s == nullptr) return CTS_E_NOMEM;
+    *out = s;
+    return CTS_OK;
+}
+
+int cts_io_pattern_state_destroy(cts_io_pattern_state* s)
+{
+    if (s == nullptr) return CTS_E_INVALID;
+    delete s;
+    return CTS_OK;
+}
+
+uint64_t cts_io_pattern_state_get_remaining_transfer(cts_io_pattern_state* s)
+{
+    uint64_t v = 0;
+    (void)state_call(s, [&] {
+        v = s->st.GetRemainingTransfer();
+        return CTS_OK;
+    });
+    return v;
+}
+
+uint64_t cts_io_pattern_state_get_max_transfer(const cts_io_pattern_state* s) { return s ? s->st.GetMaxTransfer() : 0; }
+
+int cts_io_pattern_state_set_max_transfer(cts_io_pattern_state* s, uint64_t max_transfer)
+{
+    return state_call(s, [&] {
+        s->st.SetMaxTransfer(max_transfer);
+        return CTS_OK;
+    });
+}
+
+uint32_t cts_io_pattern_state_get_ideal_send_backlog(const cts_io_pattern_state* s)
+{
+    return s ? s->st.GetIdealSendBacklog() : 0;
+}
+
+int cts_io_pattern_state_set_ideal_send_backlog(cts_io_pattern_state* s, uint32_t bytes)
+{
+    return state_call(s, [&] {
+        s->st.SetIdealSendBacklog(bytes);
+        return CTS_OK;
+    });
+}
+
+int cts_io_pattern_state_is_completed(const cts_io_pattern_state* s) { return s ? (s->st.IsCompleted() ? 1 : 0) : CTS_E_INVALID; }
+
+int cts_io_pattern_state_is_current_state_more_io(const cts_io_pattern_state* s)
+{
+    return s ? (s->st.IsCurrentStateMoreIo() ? 1 : 0) : CTS_E_INVALID;
+}
+
+int cts_io_pattern_state_get_next_pattern_type(cts_io_pattern_state* s)
+{
+    return state_call(s, [&] { return (int)s->st.GetNextPatternType(); });
+}
+
+int cts_io_pattern_state_notify_next_task(cts_io_pattern_state* s, const cts_task* t)
+{
+    if (t == nullptr) return CTS_E_INVALID;
+    return state_call(s, [&] {
+        s->st.NotifyNextTask(*t);
+        return CTS_OK;
+    });
+}
+
+int cts_io_pattern_state_completed_task(cts_io_pattern_state* s, const cts_task* t, uint32_t completed_bytes)
+{
+    if (t == nullptr) return CTS_E_INVALID;
+    return state_call(s, [&] { return (int)s->st.CompletedTask(*t, completed_bytes); });
+}
+
+int cts_io_pattern_state_update_error(cts_io_pattern_state* s, uint32_t error)
+{
+    return state_call(s, [&] { return (int)s->st.UpdateError(error); });
+}
+
+const char* cts_io_pattern_state_fail_fast_reason(const cts_io_pattern_state* s)
+{
+    return (s == nullptr || s->fail_fast.empty()) ? nullptr : s->fail_fast.c_str();
+}
 
 int cts_status_details_read(cts_status_details* o)
 {

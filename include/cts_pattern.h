@@ -257,6 +257,53 @@ const char* cts_io_pattern_fail_fast_reason(const cts_io_pattern* pattern);
 /* GetConnectionIdentifier(): the 36-char id + NUL (servers generate it). */
 const char* cts_io_pattern_connection_id(cts_io_pattern* pattern);
 
+/* ---- ctsIoPatternState on its own (ctsIOPatternState.hpp:51-504) ----------------------------
+ * The protocol state machine every pattern above runs on: connection id exchange, in-flight and
+ * confirmed byte tracking against the transfer size, the completion message, the FIN / RST
+ * shutdown, and the TCP error rules (a server waiting for the FIN accepts WSAETIMEDOUT,
+ * WSAECONNRESET, WSAECONNABORTED). UDP (MediaStream) only tracks bytes. Exposed so its own MSTest
+ * project (MSTest/ctsIOPatternStateUnitTest) replays against it; the config fields read are
+ * protocol, listening, tcp_shutdown, transfer_size, pre_post_sends and the buffer size (the ideal
+ * send backlog). A reference FAIL_FAST (an inconsistent completion) latches a reason and every
+ * later call returns CTS_E_INVALID. */
+typedef enum cts_pattern_type { /* ctsIoPatternType */
+    CTS_PT_NO_IO = 0,
+    CTS_PT_SEND_CONNECTION_ID = 1,
+    CTS_PT_RECV_CONNECTION_ID = 2,
+    CTS_PT_MORE_IO = 3,
+    CTS_PT_SEND_COMPLETION = 4,
+    CTS_PT_RECV_COMPLETION = 5,
+    CTS_PT_GRACEFUL_SHUTDOWN = 6,
+    CTS_PT_HARD_SHUTDOWN = 7,
+    CTS_PT_REQUEST_FIN = 8
+} cts_pattern_type;
+
+typedef enum cts_pattern_error { /* ctsIoPatternError */
+    CTS_PE_NO_ERROR = 0,
+    CTS_PE_TOO_MANY_BYTES = 1,
+    CTS_PE_TOO_FEW_BYTES = 2,
+    CTS_PE_CORRUPTED_BYTES = 3,
+    CTS_PE_ERROR_IO_FAILED = 4,
+    CTS_PE_SUCCESSFULLY_COMPLETED = 5
+} cts_pattern_error;
+
+typedef struct cts_io_pattern_state cts_io_pattern_state;
+int cts_io_pattern_state_create(const cts_pattern_config* config, cts_io_pattern_state** out);
+int cts_io_pattern_state_destroy(cts_io_pattern_state* state);
+uint64_t cts_io_pattern_state_get_remaining_transfer(cts_io_pattern_state* state);
+uint64_t cts_io_pattern_state_get_max_transfer(const cts_io_pattern_state* state);
+int cts_io_pattern_state_set_max_transfer(cts_io_pattern_state* state, uint64_t max_transfer);
+uint32_t cts_io_pattern_state_get_ideal_send_backlog(const cts_io_pattern_state* state);
+int cts_io_pattern_state_set_ideal_send_backlog(cts_io_pattern_state* state, uint32_t bytes);
+int cts_io_pattern_state_is_completed(const cts_io_pattern_state* state);           /* 1 / 0 */
+int cts_io_pattern_state_is_current_state_more_io(const cts_io_pattern_state* state); /* 1 / 0 */
+int cts_io_pattern_state_get_next_pattern_type(cts_io_pattern_state* state);         /* cts_pattern_type */
+int cts_io_pattern_state_notify_next_task(cts_io_pattern_state* state, const cts_task* task);
+int cts_io_pattern_state_completed_task(cts_io_pattern_state* state, const cts_task* task,
+                                        uint32_t completed_bytes);                   /* cts_pattern_error */
+int cts_io_pattern_state_update_error(cts_io_pattern_state* state, uint32_t error); /* cts_pattern_error */
+const char* cts_io_pattern_state_fail_fast_reason(const cts_io_pattern_state* state);
+
 /* ---- process-wide status counters (TcpStatusDetails, ctsConfig.h:415-417) ---- */
 typedef struct cts_status_details {
     uint64_t bytes_sent;        /* TcpStatusDetails.m_bytesSent */
