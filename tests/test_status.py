@@ -52,3 +52,67 @@ def test_summary():
     s = S.summary(59, 0, 0, 5194, 67358818304)  # README.md:131-139
     assert "  SuccessfulConnections [59]   NetworkErrors [0]   ProtocolErrors [0]\n" in s
     assert "  Total Bytes Recv : 5194\n  Total Bytes Sent : 67358818304\n" in s
+
+
+# ---- MSTest/ctsPrintStatusUnitTest/ctsPrintStatusUnitTest.cpp, replayed ----------------------------------
+# ConnectionStatusDetails: In-Flight = active connections, Completed = successful, NetError = connection
+# errors, DataError = protocol errors; TcpStatusDetails bytes and times are 0 (TestcaseInit, :24-37).
+def _conn(v):
+    return dict(active_connections=v, successful=v, connection_errors=v, protocol_errors=v)
+
+
+def test_ctsTcpStatusInformationCsvAllZeroTest():  # :39-68
+    assert S.header(S.CSV) == "TimeSlice,SendBps,RecvBps,In-Flight,Completed,NetError,DataError\r\n"
+    assert S.legend(S.CSV) == ""  # nullptr
+    assert S.line(S.CSV, current_time_ms=1000) == "1.000,0,0,0,0,0,0\r\n"
+    assert S.line(S.CSV, current_time_ms=2000, **_conn(1)) == "2.000,0,0,1,1,1,1\r\n"
+
+
+def test_ctsTcpStatusInformationConsoleOutputAllZeroTest():  # :70-96
+    assert S.line(S.CONSOLE, current_time_ms=1000) == \
+        "     1.000            0            0          0          0         0          0\n"
+    assert S.line(S.CONSOLE, current_time_ms=2000, **_conn(1)) == \
+        "     2.000            0            0          1          1         1          1\n"
+
+
+def test_ctsTcpStatusInformationCsvMaxValueTest():  # :98-137
+    assert S.line(S.CSV, current_time_ms=1000) == "1.000,0,0,0,0,0,0\r\n"
+    assert S.line(S.CSV, current_time_ms=2000, **_conn(2**63 - 1)) == \
+        "2.000,0,0,9223372036854775807,9223372036854775807,9223372036854775807,9223372036854775807\r\n"
+    # UINT64_MAX: the CSV form prints the counters unsigned
+    assert S.line(S.CSV, current_time_ms=3000, **_conn(-1)) == \
+        "3.000,0,0,18446744073709551615,18446744073709551615,18446744073709551615,18446744073709551615\r\n"
+
+
+def test_ctsTcpStatusInformationConsoleOutputMaxValueTest():  # :139-176
+    assert S.line(S.CONSOLE, current_time_ms=2000, **_conn(2**63 - 1)) == \
+        "     2.000            0            0      9+++T      9+++T     9+++T      9+++T\n"
+    # "if we go greater than INT64_MAX, we will print -1 to the console. that's fine."
+    assert S.line(S.CONSOLE, current_time_ms=3000, **_conn(-1)) == \
+        "     3.000            0            0         -1         -1        -1         -1\n"
+
+
+def test_ctsTcpStatusInformationConsoleOutputIterativeValuesTest():  # :178-392
+    expect = {
+        9: "          9          9         9          9",
+        99: "         99         99        99         99",
+        999: "        999        999       999        999",
+        9999: "       9999       9999      9999       9999",
+        99999: "      99999      99999     99999      99999",
+        999999: "     999999     999999    999999     999999",
+        9999999: "    9999999    9999999   9999999    9999999",
+        99999999: "     0.1x^9     0.1x^9    0.1x^9     0.1x^9",
+        999999999: "     1.0x^9     1.0x^9    1.0x^9     1.0x^9",
+        9999999999: "    10.0x^9    10.0x^9   10.0x^9    10.0x^9",
+        99999999999: "    0.1x^12    0.1x^12   0.1x^12    0.1x^12",
+        999999999999: "    1.0x^12    1.0x^12   1.0x^12    1.0x^12",
+    }
+    for v in [9999999999999, 99999999999999, 999999999999999, 9999999999999999, 99999999999999999]:
+        expect[v] = "      9+++T      9+++T     9+++T      9+++T"
+    assert S.line(S.CONSOLE, current_time_ms=1000) == \
+        "     1.000            0            0          0          0         0          0\n"
+    t = 2000
+    for v, cols in expect.items():
+        got = S.line(S.CONSOLE, current_time_ms=t, **_conn(v))
+        assert got == "%10.3f            0            0%s\n" % (t / 1000, cols), (v, got)
+        t += 1000
