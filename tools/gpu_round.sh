@@ -55,11 +55,12 @@ fi
 if [[ $STEPS == all || $STEPS == *dgprof* ]]; then
   # config 3 (16 M datagrams): the bench's datagram extras under the same two profilers
   run rocprof-datagram-kernel-trace
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -d "$OUT/prof_dg_kt" -o run --output-format csv \
+  # (no -T: the MediaStream kernel's descriptor and strided-ring forms differ only in a template argument)
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_dg_kt" -o run --output-format csv \
     -- python3 bench.py --no-cpu-baseline --extras-only datagram --steps 5 --warmup 2 > "$OUT/prof_dg_kt_bench.json" 2> "$OUT/prof_dg_kt.err"
   for ctr in FETCH_SIZE WRITE_SIZE; do
     run rocprof-datagram-pmc $ctr
-    timeout -k 10 300 rocprofv3 --pmc $ctr --kernel-trace -T -d "$OUT/prof_dg_pmc_$ctr" -o run --output-format csv \
+    timeout -k 10 300 rocprofv3 --pmc $ctr --kernel-trace -d "$OUT/prof_dg_pmc_$ctr" -o run --output-format csv \
       -- python3 bench.py --no-cpu-baseline --extras-only datagram --steps 5 --warmup 2 > "$OUT/prof_dg_pmc_$ctr.json" 2> "$OUT/prof_dg_pmc_$ctr.err"
   done
 fi

@@ -31,14 +31,22 @@ WORKLOADS = {
     "verify_wave_kernel": "config3 verify: 16M x 1472 B datagrams (%d B payload read)" % (DG * 1446),
     "media_stream_verify_quad_kernel": "config3 MediaStream receive: 16M x 1472 B datagrams (%d B payload read)" % (
         DG * 1446),
+    "media_stream_verify_quad_kernel[strided]": "config3 MediaStream receive, strided ring (lengths only): 16M x "
+                                                "1472 B datagrams (%d B payload read)" % (DG * 1446),
 }
 ALGO_BYTES = {"verify_wg_kernel": 268435456, "fill_kernel": 268435456, "verify_quad_kernel": DG * 1446,
-              "verify_wave_kernel": DG * 1446, "media_stream_verify_quad_kernel": DG * 1446}
+              "verify_wave_kernel": DG * 1446, "media_stream_verify_quad_kernel": DG * 1446,
+              "media_stream_verify_quad_kernel[strided]": DG * 1446}
 RUNS = ("prof", "prof_dg")
 
 
 def _kname(name):
-    return name.split("(")[0].split("<")[0].split("::")[-1].strip()
+    base = name.split("(")[0].split("<")[0].split("::")[-1].strip()
+    if base == "media_stream_verify_quad_kernel" and "<" in name:
+        targs = name.split("(")[0].split("<", 1)[1].rsplit(">", 1)[0].split(",")
+        if len(targs) == 6 and targs[-1].strip() == "true":  # STRIDED: cts_media_stream_verify_strided
+            return base + "[strided]"
+    return base
 
 
 def _grid(r):
