@@ -22,7 +22,7 @@ TUNING_OBJS := $(patsubst $(CSRC)/%,ctstraffic_amd/build/tuning/%.o,$(TUNED)) \
 SOFLAGS   := -shared -Wl,-Bsymbolic -Wl,--version-script=$(CSRC)/exports.map
 
 DEVICE_VERIFY := ctstraffic_amd/build/device_verify
-TOOLS := tools/hbm_read_ceiling tools/verify_ablation tools/mailbox_probe tools/rw_mix_probe
+TOOLS := tools/hbm_read_ceiling tools/verify_ablation tools/mailbox_probe tools/rw_mix_probe tools/write_shape_probe tools/fill_bisect tools/fill_abi_probe
 
 SYNC_PROBE := tools/sync_probe
 
@@ -37,6 +37,14 @@ $(SYNC_PROBE): tools/sync_probe.cpp $(ENGINE_SO) include/cts_engine.h
 # measurement references used by tools/gpu_round.sh (plain streaming read/write ceilings, verify ablation)
 tools/%: tools/%.hip
 	$(HIPCC) --offload-arch=$(ARCH) -O3 $< -o $@
+
+# the product fill kernel included verbatim (diagnostic)
+tools/fill_bisect: tools/fill_bisect.hip $(CSRC)/cts_kernels.hip $(HDRS)
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -Iinclude -I$(CSRC) $< -o $@
+
+# cts_fill through the C ABI without PyTorch (diagnostic)
+tools/fill_abi_probe: tools/fill_abi_probe.cpp $(ENGINE_SO) include/cts_engine.h
+	$(HIPCC) -O2 -std=c++17 -Iinclude $< -o $@ -Lctstraffic_amd -lcts_engine -Wl,-rpath,'$$ORIGIN/../ctstraffic_amd'
 
 # C++ device-resident sample against the C ABI (run on the GPU box by tests/test_cpp_abi.py)
 $(DEVICE_VERIFY): tests/cpp/device_verify.cpp $(ENGINE_SO) include/cts_engine.h

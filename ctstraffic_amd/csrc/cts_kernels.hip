@@ -1294,9 +1294,22 @@ __device__ __forceinline__ void fill_chunk(u32x4* a0, uint32_t c, uint32_t nchun
 template <int TEAM, int U, bool EVEN, bool NTS>
 __device__ __forceinline__ void fill_whole_rounds(u32x4* p, uint32_t nchunks, uint32_t q0, uint32_t lane)
 {
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(p, (short)0, (int)(nchunks * 16u), 0x00020000);
     const uint32_t sh = q0 & 1u;
-    for (uint32_t cb = 0; cb < nchunks; cb += (uint32_t)(TEAM * U)) {
+    typedef u32x4 __attribute__((address_space(1)))* gstore_ptr;
+    uint32_t cb = 0;
+    for (; cb + (uint32_t)(TEAM * U) <= nchunks; cb += (uint32_t)(TEAM * U)) {  // full rounds: global stores
+        const uint32_t k = ((q0 + 16u * (cb + lane)) & 0xFFFFu) >> 1;
+        const uint32_t B = __umul24(k, 0x10001u) + 0x10000u;
+        const gstore_ptr g = (gstore_ptr)(p + cb + lane);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const u32x4 e = expected_step<TEAM, U, EVEN>(B, u, sh);
+            if constexpr (NTS) __builtin_nontemporal_store(e, g + u * TEAM);
+            else g[u * TEAM] = e;
+        }
+    }
+    if (cb < nchunks) {  // tail round: buffer stores past num_records are dropped
+        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(p, (short)0, (int)(nchunks * 16u), 0x00020000);
         const uint32_t k = ((q0 + 16u * (cb + lane)) & 0xFFFFu) >> 1;
         const uint32_t B = __umul24(k, 0x10001u) + 0x10000u;
 #pragma unroll
@@ -1316,8 +1329,15 @@ __global__ void __launch_bounds__(kBlock) fill_kernel(uint8_t* __restrict__ aren
     constexpr int FU = TEAM == kBlock ? 4 : 2;  // stores per lane per whole-span round
     const uint32_t lane = threadIdx.x % TEAM;
     const uint32_t team = (TEAM == kBlock) ? 0u : (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x / TEAM);
-    for (uint32_t i = blockIdx.x * TEAMS + team; i < n; i += gridDim.x * TEAMS) {
-        const cts_buf_desc d = descs[i];
+    const uint32_t step = gridDim.x * TEAMS;
+    uint32_t i = blockIdx.x * TEAMS + team;
+    // the next buffer's descriptor is loaded while this one's stores go out: with one workgroup per CU
+    // nothing else hides a dependent descriptor load per buffer (49.4 -> see DESIGN §3 fill)
+    cts_buf_desc dn;
+    if (i < n) dn = descs[i];
+    for (; i < n; i = (uint64_t)i + step < n ? i + step : n) {
+        const cts_buf_desc d = dn;
+        if ((uint64_t)i + step < n) dn = descs[i + step];
         if (desc_bad(d, arena_bytes)) continue;
         const uint32_t len = d.length - d.skip_head;
         if (len == 0) continue;

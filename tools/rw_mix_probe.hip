@@ -10,7 +10,8 @@
 //   burst     every 8th round, lanes 0..59 store 16 B each (960 B per 32 KiB read)
 //   wt        dword with write-through (sc1) stores
 // Output positions follow the read position (output i belongs to the 4 KiB read as i), as the
-// verify kernels' records follow their datagrams. Prints one JSON line per shape.
+// verify kernels' records follow their datagrams. (The 128 MiB output region is rewritten by every launch and
+// may partly stay in the 256 MB MALL; the 2 GiB read stream cannot.) Prints one JSON line per shape.
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
