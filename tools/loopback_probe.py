@@ -1,0 +1,45 @@
+#!/usr/bin/env python3
+"""Config-1 loopback (8 connections x 1 GiB push, 64 KiB) under different verify arrangements, to see
+what bounds each: no verification (the socket path alone), the C oracle on each receive thread (the
+reference's arrangement), GPU DEFERRED at several batch sizes, GPU SYNC (mailbox). One JSON line per
+(case, round)."""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import oracle  # noqa: E402
+from ctstraffic_amd import Engine, _pattern_abi as PA, loopback as LB  # noqa: E402
+from ctstraffic_amd.pattern import shared_buffer_attach, shared_buffer_init  # noqa: E402
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--rounds", type=int, default=2)
+    p.add_argument("--gib", type=int, default=1)
+    args = p.parse_args()
+    eng = Engine(0)
+    S = oracle.sender_buffer(65536)
+    hook = PA.BATCH_VERIFIER(oracle.batch_verifier_address())
+    cases = [("no_verify", dict(verify=False)),
+             ("cpu_oracle_sync", dict(verifier=hook, verify_mode=PA.VERIFY_SYNC)),
+             ("gpu_deferred_b256", dict(engine=eng, batch_buffers=256)),
+             ("gpu_deferred_b1024", dict(engine=eng, batch_buffers=1024)),
+             ("gpu_deferred_b4096", dict(engine=eng, batch_buffers=4096)),
+             ("gpu_sync_mailbox", dict(engine=eng, verify_mode=PA.VERIFY_SYNC))]
+    for r in range(args.rounds):
+        for name, kw in cases:
+            if "engine" in kw:
+                shared_buffer_init(eng, 65536)
+            else:
+                shared_buffer_attach(S)
+            res = LB.run(connections=8, buffer_size=65536, transfer_size=args.gib << 30, **kw)
+            print(json.dumps({"round": r, "case": name, "GBps_recv": round(res["GBps_recv"], 2),
+                              "connections_ok": res["connections_ok"], "data_errors": res["data_errors"]}),
+                  flush=True)
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()
