@@ -144,6 +144,7 @@ struct Mailbox {
     std::condition_variable cv;
     std::thread watchdog;
     std::atomic<uint64_t> launches{0};
+    std::atomic<bool> broken_flag{false};  // `broken`, readable without mu
 
     ~Mailbox()
     {
@@ -238,6 +239,7 @@ struct Mailbox {
         std::lock_guard<std::mutex> lk(mu);
         if (rc != CTS_OK) {
             broken = true;  // a straggler may still read or answer the slot: never reuse it
+            broken_flag.store(true, std::memory_order_release);
             running = false;
         }
         --outstanding;
@@ -248,7 +250,11 @@ struct Mailbox {
     int Run(uint64_t t, uint64_t ptr, uint32_t len, uint32_t expected, cts_verify_result* out)
     {
         const uint32_t k = (uint32_t)(t % nslots);
-        while (free_at[k].load(std::memory_order_acquire) != t) std::this_thread::yield();
+        while (free_at[k].load(std::memory_order_acquire) != t) {
+            // the slot's previous ticket timed out: it is never freed, and the mailbox is broken
+            if (broken_flag.load(std::memory_order_acquire)) return CTS_E_HIP;
+            std::this_thread::yield();
+        }
         cts::MailSlot* const s = slots + k;
         const uint32_t tag = (uint32_t)(t + 1);
         // the job half first, then the tagged half: the grid's one 16-B read of the slot sees a new tag
