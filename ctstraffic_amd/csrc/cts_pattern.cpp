@@ -316,7 +316,10 @@ struct cts_io_pattern {
     }
     virtual ~cts_io_pattern()
     {
-        if (stream) (void)cts_engine_stream_destroy(engine, stream);
+        if (stream) {
+            if (!inflight.empty()) (void)hipStreamSynchronize(stream);  // the kernel still reads the ring
+            (void)cts_engine_stream_destroy(engine, stream);
+        }
         // ~RioBufferId (ctsIOPattern.h:230-238) for every id this pattern registered
         if (!rio_owned.empty()) {
             std::lock_guard<std::mutex> lk(g_rio.mu);
@@ -363,6 +366,11 @@ struct cts_io_pattern {
     std::vector<cts_verify_result> hres;
     std::vector<Queued> queue;
     uint64_t stage_used = 0;
+    // double buffering (ring mode, device verify): a full batch is launched and left running while
+    // the next one fills in the other half of stage_desc/stage_res; its verdicts are applied before
+    // the next launch, at any non-benign completion and at Flush (Retire)
+    std::vector<Queued> inflight;
+    uint32_t desc_set = 0;  // the half the filling batch uses
     // DEFERRED zero-copy ring: the recv container holds BatchCapacity()+2 buffer slots and a
     // completed buffer's slot is not handed out again before its batch was verified, so a
     // batch is verified in place (no staging copy)
@@ -477,7 +485,8 @@ struct cts_io_pattern {
             return CTS_OK;
         }
         ring = Deferred();
-        ring_slots = ring ? BatchCapacity() + recvCount + 1 : recvCount;
+        // a slot is handed out again only after the (up to two) batches that may hold it were verified
+        ring_slots = ring ? BatchCapacity() * (DoubleBuffered() ? 2u : 1u) + recvCount + 1 : recvCount;
         const uint64_t bytes = (uint64_t)max_buffer_size * ring_slots;
         char* base = nullptr;
         if (engine != nullptr && hook == nullptr) {
@@ -682,6 +691,11 @@ struct cts_io_pattern {
 
     uint64_t StageCapacity() const { return cfg.batch_bytes ? cfg.batch_bytes : (64ull << 20); }
     uint32_t BatchCapacity() const { return cfg.batch_buffers ? cfg.batch_buffers : 1024u; }
+    bool DoubleBuffered() const { return engine != nullptr && hook == nullptr; }
+    cts_buf_desc* StageDescs() const
+    {
+        return reinterpret_cast<cts_buf_desc*>(stage_desc.host) + (size_t)desc_set * BatchCapacity();
+    }
 
     // Queue one buffer for the next batch (DEFERRED). Returns CTS_OK.
     bool InRing(const char* p, uint32_t n) const
@@ -699,12 +713,15 @@ struct cts_io_pattern {
             return CTS_OK;
         }
         if (engine == nullptr) return CTS_E_INVALID;
+        return EnsureStageDescs();
+    }
+
+    int EnsureStageDescs()  // both halves
+    {
+        if (stage_desc.host != nullptr) return CTS_OK;
         int rc;
-        if (stage_desc.host == nullptr) {
-            if ((rc = stage_desc.alloc(engine, sizeof(cts_buf_desc) * (uint64_t)BatchCapacity())) != CTS_OK) return rc;
-            if ((rc = stage_res.alloc(engine, sizeof(cts_verify_result) * (uint64_t)BatchCapacity())) != CTS_OK) return rc;
-        }
-        return CTS_OK;
+        if ((rc = stage_desc.alloc(engine, sizeof(cts_buf_desc) * 2ull * BatchCapacity())) != CTS_OK) return rc;
+        return stage_res.alloc(engine, sizeof(cts_verify_result) * 2ull * BatchCapacity());
     }
 
     int Enqueue(const cts_task& t, uint32_t transferred, uint64_t recv_after)
@@ -714,7 +731,7 @@ struct cts_io_pattern {
             // zero copy: the batch descriptor points at the recv buffer itself
             const int rc = EnsureBatchDescs();
             if (rc != CTS_OK) return rc;
-            cts_buf_desc* descs = hook ? hdesc.data() : reinterpret_cast<cts_buf_desc*>(stage_desc.host);
+            cts_buf_desc* descs = hook ? hdesc.data() : StageDescs();
             descs[queue.size()] = cts_buf_desc{(uint64_t)(src - ring_base), transferred, t.expected_pattern_offset, 0, 0};
             queue.push_back(Queued{recv_completions, transferred, recv_after, bytes_sent, t.expected_pattern_offset});
             queue_in_ring = true;
@@ -746,23 +763,66 @@ struct cts_io_pattern {
                 stage.release();
                 if ((rc = stage.alloc(engine, cap)) != CTS_OK) return rc;
             }
-            if (stage_desc.host == nullptr) {
-                if ((rc = stage_desc.alloc(engine, sizeof(cts_buf_desc) * (uint64_t)BatchCapacity())) != CTS_OK) return rc;
-                if ((rc = stage_res.alloc(engine, sizeof(cts_verify_result) * (uint64_t)BatchCapacity())) != CTS_OK)
-                    return rc;
-            }
+            if ((rc = EnsureStageDescs()) != CTS_OK) return rc;
             base = stage.host;
         }
         if (transferred) std::memcpy(base + stage_used, t.buffer + t.buffer_offset, transferred);
-        cts_buf_desc* descs = hook ? hdesc.data() : reinterpret_cast<cts_buf_desc*>(stage_desc.host);
+        cts_buf_desc* descs = hook ? hdesc.data() : StageDescs();
         descs[queue.size()] = cts_buf_desc{stage_used, transferred, t.expected_pattern_offset, 0, 0};
         queue.push_back(Queued{recv_completions, transferred, recv_after, bytes_sent, t.expected_pattern_offset});
         stage_used += slot;
         return CTS_OK;
     }
 
+    int LaunchBatch()  // verifies `queue` (descriptor half desc_set) on the pattern's stream, async
+    {
+        int rc = EnsureStream();
+        if (rc != CTS_OK) return rc;
+        uint32_t maxlen = 0;
+        for (const auto& q : queue) maxlen = std::max(maxlen, q.transferred);
+        const uint8_t* arena = queue_in_ring ? recv_pinned.dev : stage.dev;
+        const uint64_t bytes = queue_in_ring ? recv_pinned.bytes : stage.bytes;
+        const size_t half = (size_t)desc_set * BatchCapacity();
+        return cts_verify(engine, arena, bytes, reinterpret_cast<cts_buf_desc*>(stage_desc.dev) + half,
+                          (uint32_t)queue.size(), maxlen, reinterpret_cast<cts_verify_result*>(stage_res.dev) + half,
+                          nullptr, nullptr, 0, stream);
+    }
+
+    // Waits for the in-flight batch and applies its verdicts. A failure in it takes back
+    // everything completed after the failing buffer, the filling batch included.
+    int Retire()
+    {
+        if (inflight.empty()) return CTS_OK;
+        if (hipStreamSynchronize(stream) != hipSuccess) return CTS_E_HIP;
+        const size_t half = (size_t)(desc_set ^ 1u) * BatchCapacity();
+        const bool failed = ApplyVerdicts(inflight, reinterpret_cast<const cts_verify_result*>(stage_res.host) + half);
+        inflight.clear();
+        if (failed) {
+            queue.clear();
+            stage_used = 0;
+        }
+        return CTS_OK;
+    }
+
+    // The filling batch is full: retire the in-flight one, launch this one and keep receiving.
+    int Rotate()
+    {
+        if (!DoubleBuffered() || !queue_in_ring) return Flush();
+        const int rc = Retire();
+        if (rc != CTS_OK) return rc;
+        if (queue.empty()) return GetCurrentStatus();  // the in-flight batch failed
+        const int lr = LaunchBatch();
+        if (lr != CTS_OK) return lr;
+        inflight.swap(queue);
+        queue.clear();
+        desc_set ^= 1u;
+        return GetCurrentStatus();
+    }
+
     int Flush()  // cts_io_pattern_flush
     {
+        const int rr = Retire();
+        if (rr != CTS_OK) return rr;
         if (queue.empty()) return GetCurrentStatus();
         const uint32_t n = (uint32_t)queue.size();
         const cts_verify_result* res = nullptr;
@@ -772,23 +832,26 @@ struct cts_io_pattern {
             if (hook(hook_ctx, arena, bytes, hdesc.data(), n, hres.data()) != 0) return CTS_E_INVALID;
             res = hres.data();
         } else {
-            int rc = EnsureStream();
-            if (rc != CTS_OK) return rc;
-            uint32_t maxlen = 0;
-            for (const auto& q : queue) maxlen = std::max(maxlen, q.transferred);
-            const uint8_t* arena = queue_in_ring ? recv_pinned.dev : stage.dev;
-            const uint64_t bytes = queue_in_ring ? recv_pinned.bytes : stage.bytes;
-            rc = cts_verify(engine, arena, bytes, reinterpret_cast<cts_buf_desc*>(stage_desc.dev), n, maxlen,
-                            reinterpret_cast<cts_verify_result*>(stage_res.dev), nullptr, nullptr, 0, stream);
+            const int rc = LaunchBatch();
             if (rc != CTS_OK) return rc;
             if (hipStreamSynchronize(stream) != hipSuccess) return CTS_E_HIP;
-            res = reinterpret_cast<const cts_verify_result*>(stage_res.host);
+            res = reinterpret_cast<const cts_verify_result*>(stage_res.host) + (size_t)desc_set * BatchCapacity();
         }
+        ApplyVerdicts(queue, res);
+        queue.clear();
+        stage_used = 0;
+        return GetCurrentStatus();
+    }
+
+    // Counts the verdicts of batch q; returns true if one of its buffers failed.
         // The reference stops at the first failing buffer (its CompleteIo fails the connection on that
         // completion, ctsIOPattern.cpp:486-489, and TCP verify allows one posted recv,
         // ctsConfig.cpp:3440-3446). Buffers queued after it were never received there: they are neither
         // counted as verified nor as received, and the sends that completed after it are taken back too,
         // so every counter equals what the reference reports when it stops at that completion.
+    bool ApplyVerdicts(const std::vector<Queued>& q, const cts_verify_result* res)
+    {
+        const uint32_t n = (uint32_t)q.size();
         uint32_t bad = n;
         for (uint32_t i = 0; i < n; ++i)
             if (!res[i].pass) {
@@ -798,17 +861,14 @@ struct cts_io_pattern {
         const uint32_t counted = bad < n ? bad + 1 : n;
         for (uint32_t i = 0; i < counted; ++i) {
             ++buffers_verified;
-            bytes_verified += queue[i].transferred;
+            bytes_verified += q[i].transferred;
         }
-        if (bad < n) {
-            const Queued& f = queue[bad];
-            RecordFailure(f.completion, f.transferred, res[bad], f.bytes_recv_after);
-            RollbackAfter(f);
-        }
-        queue.clear();
-        stage_used = 0;
-        if (bad < n) UpdateLastError(CTS_STATUS_ERROR_DATA_DID_NOT_MATCH_BIT_PATTERN);
-        return GetCurrentStatus();
+        if (bad == n) return false;
+        const Queued& f = q[bad];
+        RecordFailure(f.completion, f.transferred, res[bad], f.bytes_recv_after);
+        RollbackAfter(f);
+        UpdateLastError(CTS_STATUS_ERROR_DATA_DID_NOT_MATCH_BIT_PATTERN);
+        return true;
     }
 
     // Undo the byte accounting (TcpStatusDetails, ctsStatistics, the pattern state and the recv
@@ -839,7 +899,7 @@ struct cts_io_pattern {
         // queued verdicts first, so a pending data error latches before it.
         bool benign = status == kNoError && (t.io_action == CTS_TASK_SEND || t.io_action == CTS_TASK_RECV) &&
                       state.WouldStayMoreIo(t, transfer) && m_lastError == kStatusIoRunning;
-        if (Deferred() && !queue.empty() && !benign) {
+        if (Deferred() && (!queue.empty() || !inflight.empty()) && !benign) {
             const bool had_failure = has_failure;
             const int rc = Flush();
             if (rc < 0) return rc;
@@ -915,7 +975,7 @@ struct cts_io_pattern {
             const int rc = Enqueue(t, transfer, bytes_recv);
             if (rc < 0) return rc;
             if (!benign || queue.size() >= BatchCapacity()) {
-                const int fr = Flush();
+                const int fr = benign ? Rotate() : Flush();
                 if (fr < 0) return fr;
             }
         }
@@ -1194,7 +1254,7 @@ int cts_io_pattern_destroy(cts_io_pattern* p)
 int cts_io_pattern_set_verifier(cts_io_pattern* p, cts_batch_verifier fn, void* ctx)
 {
     if (p == nullptr) return CTS_E_INVALID;
-    if (!p->queue.empty()) return CTS_E_INVALID;
+    if (!p->queue.empty() || !p->inflight.empty()) return CTS_E_INVALID;
     p->hook = fn;
     p->hook_ctx = ctx;
     return CTS_OK;
@@ -1281,7 +1341,7 @@ int cts_io_pattern_get_stats(const cts_io_pattern* p, cts_pattern_stats* o)
     o->recv_pattern_offset = p->m_recvPatternOffset;
     o->send_pattern_offset = p->m_sendPatternOffset;
     o->last_error = p->m_lastError;
-    o->queued = (uint32_t)p->queue.size();
+    o->queued = (uint32_t)(p->queue.size() + p->inflight.size());
     o->fail_length = p->fail_length;
     o->fail_offset = p->fail_offset;
     o->fail_expected = p->fail_expected;

@@ -1163,7 +1163,7 @@ def _expected_stream(lens, corrupt):
     return None, recv, None
 
 
-@pytest.mark.parametrize("seed", [1, 2, 3])
+@pytest.mark.parametrize("seed", [1, 2, 3, 4, 5, 6])
 def test_random_push_server_stream(make, seed):
     rng = np.random.default_rng(seed)
     bufsize = int(rng.choice([1000, 4096, 65536]))
@@ -1210,8 +1210,9 @@ def test_random_push_server_stream(make, seed):
     if make.mode == A.VERIFY_SYNC:
         assert statuses[-1] == FailedIo and len(statuses) == fail_at + 1
     else:
-        # deferred: the failure surfaces at the end of its batch (within its batch of 16) or at the final flush
-        assert flushed == FailedIo and fail_at + 1 <= len(statuses) <= fail_at + 16
+        # deferred: the failure surfaces when its batch of 16 is retired -- on the device the batch is
+        # left in flight while the next one fills, so up to two batches later -- or at the final flush
+        assert flushed == FailedIo and fail_at + 1 <= len(statuses) <= fail_at + 32
     # either way every counter is the reference's, which stopped at the failing completion: the completions
     # a deferred pattern accepted after it are taken back at the flush
     assert s["bytes_recv"] == recv_at and s["buffers_verified"] == fail_at + 1 and s["buffers_failed"] == 1

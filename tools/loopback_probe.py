@@ -27,7 +27,10 @@ def main():
              ("gpu_deferred_b256", dict(engine=eng, batch_buffers=256)),
              ("gpu_deferred_b1024", dict(engine=eng, batch_buffers=1024)),
              ("gpu_deferred_b4096", dict(engine=eng, batch_buffers=4096)),
-             ("gpu_sync_mailbox", dict(engine=eng, verify_mode=PA.VERIFY_SYNC))]
+             ("gpu_sync_mailbox", dict(engine=eng, verify_mode=PA.VERIFY_SYNC)),
+             ("duplex_no_verify", dict(verify=False, io_pattern=PA.PATTERN_DUPLEX)),
+             ("duplex_cpu_oracle_sync", dict(verifier=hook, verify_mode=PA.VERIFY_SYNC, io_pattern=PA.PATTERN_DUPLEX)),
+             ("duplex_gpu_deferred_b1024", dict(engine=eng, batch_buffers=1024, io_pattern=PA.PATTERN_DUPLEX))]
     for r in range(args.rounds):
         for name, kw in cases:
             if "engine" in kw:
