@@ -371,9 +371,9 @@ struct cts_io_pattern {
     // the next launch, at any non-benign completion and at Flush (Retire)
     std::vector<Queued> inflight;
     uint32_t desc_set = 0;  // the half the filling batch uses
-    // DEFERRED zero-copy ring: the recv container holds BatchCapacity()+2 buffer slots and a
-    // completed buffer's slot is not handed out again before its batch was verified, so a
-    // batch is verified in place (no staging copy)
+    // DEFERRED zero-copy ring: the recv container holds (1 or 2) x BatchCapacity() + recvCount + 1
+    // buffer slots and a completed buffer's slot is not handed out again before its batch was
+    // verified, so a batch is verified in place (no staging copy)
     bool ring = false, queue_in_ring = false;
     uint32_t ring_slots = 0, ring_next = 0;
     char* ring_base = nullptr;

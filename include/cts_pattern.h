@@ -136,7 +136,9 @@ typedef struct cts_pattern_config {
     uint64_t transfer_size;     /* GetTransferSize() */
     uint64_t random_seed;       /* seed of the -buffer:[lo,hi] draw (reference: random_device) */
     uint32_t verify_mode;       /* cts_verify_mode */
-    uint32_t batch_buffers;     /* DEFERRED: max queued buffers per batch (0 = 1024) */
+    uint32_t batch_buffers;     /* DEFERRED: max queued buffers per batch (0 = 1024); on a device one
+                                   batch verifies while the next fills, so the pinned recv ring holds
+                                   2 x batch_buffers + recvCount + 1 buffers */
     uint64_t batch_bytes;       /* DEFERRED: staging arena bytes (0 = 64 MiB) */
     uint32_t registered_io;     /* SocketFlags & WSA_FLAG_REGISTERED_IO (-io:rioiocp): register buffers with
                                  * the RIO functions of cts_rio_functions_set, hand their ids out in tasks */
