@@ -1846,6 +1846,21 @@ static void launch_verify_nt(const uint8_t* arena, uint64_t arena_bytes, const c
 // round trips (1.2 us each, tools/mailbox_probe) plus one posted write; G jobs run side by side.
 constexpr int kMailAux = 1 | 16;  // sc0 sc1: system scope
 
+#if defined(CTS_MAILBOX_TRACE)
+// diagnostic builds only (tools/mailbox_bisect.hip): per (ticket mod 1024, workgroup) the s_memrealtime
+// stamps of the poll that matched, the data compared, the part record stored, and the poll's start
+__device__ uint64_t* cts_mail_trace;
+#define CTS_MAIL_STAMP(which)                                                                           \
+    do {                                                                                                \
+        if (tid == 0 && cts_mail_trace != nullptr)                                                      \
+            cts_mail_trace[((t % 1024u) * kMailGroup + gi) * 4u + (which)] = wall_clock64();            \
+    } while (0)
+#else
+#define CTS_MAIL_STAMP(which) \
+    do {                      \
+    } while (0)
+#endif
+
 __global__ __launch_bounds__(kBlock) void mailbox_kernel(const MailSlot* slots, MailPart* parts, uint32_t nslots,
                                                          uint64_t t0, uint64_t idle_ticks)
 {
@@ -1861,11 +1876,15 @@ __global__ __launch_bounds__(kBlock) void mailbox_kernel(const MailSlot* slots, 
             const __amdgpu_buffer_rsrc_t r =
                 __builtin_amdgcn_make_buffer_rsrc(const_cast<MailSlot*>(slots + k), (short)0, 16, 0x00020000);
             const uint64_t start = wall_clock64();
+            CTS_MAIL_STAMP(3);
             u64x2 job = {0, 0};
             for (;;) {
                 const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, 0u, 0u, kMailAux);
                 job = u64x2{(uint64_t)v[0] | ((uint64_t)v[1] << 32), (uint64_t)v[2] | ((uint64_t)v[3] << 32)};
-                if ((uint32_t)(job[1] >> 32) == tag) break;
+                if ((uint32_t)(job[1] >> 32) == tag) {
+                    CTS_MAIL_STAMP(0);
+                    break;
+                }
                 if (wall_clock64() - start > idle_ticks) {
                     job[1] = 0;  // no job for this ticket within idle_ticks: leave
                     break;
@@ -1929,6 +1948,7 @@ __global__ __launch_bounds__(kBlock) void mailbox_kernel(const MailSlot* slots, 
         }
         first = wave_min(first);
         count = wave_sum(count);
+        CTS_MAIL_STAMP(1);
         if ((tid & 63u) == 0) {
             s_first[tid >> 6] = first;
             s_count[tid >> 6] = count;
@@ -1949,6 +1969,7 @@ __global__ __launch_bounds__(kBlock) void mailbox_kernel(const MailSlot* slots, 
             __hip_atomic_store(&out->g0, (uint64_t)first | ((uint64_t)tag << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(&out->g1, (uint64_t)count | ((uint64_t)actual << 32) | ((uint64_t)(tag & 0xFFFFFFu) << 40),
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            CTS_MAIL_STAMP(2);
         }
         __syncthreads();  // s_first / s_count are rewritten by the next ticket
     }

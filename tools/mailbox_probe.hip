@@ -41,14 +41,20 @@ __global__ void pingpong_kernel(const uint64_t* seq, uint64_t* ack, const uint8_
         __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(data + (size_t)blockIdx.x * per), (short)0, (int)per, 0x00020000);
     for (int i = 1; i <= iters; ++i) {
         if (threadIdx.x == 0) {
+            const uint64_t start = wall_clock64();
+            go = i;
             for (;;) {
                 const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, 0u, 0u, 1 | 16);
                 if ((int)v[0] >= i) break;
+                if (wall_clock64() - start > 200000000ull) {  // 2 s without the word: give up (every wave exits)
+                    go = 0;
+                    break;
+                }
                 __builtin_amdgcn_s_sleep(2);
             }
-            go = i;
         }
         __syncthreads();
+        if (go == 0) return;
         uint32_t acc = 0;
         for (uint32_t o = threadIdx.x * 16u; o < per; o += blockDim.x * 16u) {
             const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rd, o, 0u, 1 | 16);
@@ -178,5 +184,57 @@ int main()
             std::fflush(stdout);
             if (!ok) return 2;
         }
+    // (4) the same ping-pong with the job word in device memory the host writes through its mapping
+    //     (fine-grained / uncached VRAM behind the BAR): the GPU polls HBM instead of host memory
+    for (const unsigned flag : {(unsigned)hipDeviceMallocUncached, (unsigned)hipDeviceMallocFinegrained}) {
+        const char* fname = flag == hipDeviceMallocUncached ? "uncached" : "finegrained";
+        uint64_t* vseq = nullptr;
+        if (hipExtMallocWithFlags((void**)&vseq, 4096, flag) != hipSuccess) {
+            std::printf("{\"probe\": \"pingpong_vram\", \"alloc\": \"%s\", \"error\": \"alloc\"}\n", fname);
+            continue;
+        }
+        hipPointerAttribute_t at{};
+        const bool attr_ok = hipPointerGetAttributes(&at, vseq) == hipSuccess;
+        std::printf("{\"probe\": \"pingpong_vram\", \"alloc\": \"%s\", \"host_pointer\": \"%p\", \"attr_ok\": %d}\n", fname,
+                    attr_ok ? at.hostPointer : nullptr, attr_ok ? 1 : 0);
+        std::fflush(stdout);
+        uint64_t* hv = attr_ok && at.hostPointer ? static_cast<uint64_t*>(at.hostPointer) : vseq;
+        __atomic_store_n(hv, 0ull, __ATOMIC_SEQ_CST);  // faults here if the BAR is not mapped for the host
+        std::printf("{\"probe\": \"pingpong_vram\", \"alloc\": \"%s\", \"host_write\": \"ok\"}\n", fname);
+        std::fflush(stdout);
+        for (uint32_t bytes : {0u, 65536u})
+            for (uint32_t P : {1u, 16u}) {
+                if (bytes == 0 && P > 1) continue;
+                const int iters = 2000;
+                std::memset(hack, 0, 64 * 16);
+                __atomic_store_n(hv, 0ull, __ATOMIC_SEQ_CST);
+                hipStream_t s;
+                hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+                pingpong_kernel<<<P, 256, 0, s>>>(vseq, dack, ddata, bytes, iters);
+                double t0 = 0;
+                bool ok = true;
+                for (int i = 1; i <= iters && ok; ++i) {
+                    if (i == 101) t0 = now_us();
+                    __atomic_store_n(hv, (uint64_t)i, __ATOMIC_SEQ_CST);
+                    const double ts = now_us();
+                    for (uint32_t b = 0; b < P; ++b)
+                        while ((uint32_t)__atomic_load_n(hack + 2 * b, __ATOMIC_ACQUIRE) != (uint32_t)i)
+                            if (now_us() - ts > 2e6) {
+                                ok = false;
+                                break;
+                            }
+                }
+                const double t1 = now_us();
+                if (!ok) __atomic_store_n(hv, (uint64_t)iters, __ATOMIC_SEQ_CST);
+                hipStreamSynchronize(s);
+                hipStreamDestroy(s);
+                std::printf("{\"probe\": \"pingpong_vram\", \"alloc\": \"%s\", \"bytes\": %u, \"workgroups\": %u, "
+                            "\"us_per_round\": %.3f, \"ok\": %d}\n",
+                            fname, bytes, P, (t1 - t0) / (iters - 100), ok ? 1 : 0);
+                std::fflush(stdout);
+                if (!ok) return 2;
+            }
+        hipFree(vseq);
+    }
     return 0;
 }
