@@ -116,17 +116,19 @@ int ensure_stage(cts_engine* e, size_t bytes)
 // A resident grid (cts::launch_mailbox) answers one-buffer verifies posted through host-coherent
 // pinned slots, so a SYNC completion pays PCIe round trips instead of a launch + synchronize; the
 // caller folds the grid's per-piece part records into the RtlCompareMemory record itself.
-// Tickets are claimed under `mu`; ticket t uses slot t % nslots once its previous user (t - nslots)
-// has read its answer (free_at). The grid is (re)launched by the first post after it stopped, and a
-// watchdog thread stops it with a kMailStop ticket after `idle_ms` without posts, so an idle engine
+// Jobs are claimed under `mu`, in the group with the fewest outstanding; group g's job j uses slot
+// g * per_group + j % per_group once its previous user (j - per_group) has read its answer (free_at).
+// The grid is (re)launched by the first post after it stopped, at every group's next job number, and a
+// watchdog thread stops it with one stop job per group after `idle_ms` without posts, so an idle engine
 // neither holds workgroups nor polls PCIe. The grid's own exit bound (idle_ticks, far longer) is a
 // safety net only: a post racing it would time out (CTS_E_HIP) rather than hang.
 struct Mailbox {
     cts_engine* e = nullptr;
     // groups x cts::kMailGroup workgroups: 8 groups measured best for 8-16 concurrent callers (64 KiB:
-    // 18.7 / 25.3 us per verify at 8 / 16 threads against 19.6-32.6 for 1-4 groups; one caller 7.1 us,
-    // 5.8 with one group; tools/sync_probe, profiles/r02/sync_probe_groups.jsonl)
-    uint32_t nslots = 1024, groups = 8;
+    // 18.7 / 25.3 us per verify at 8 / 16 threads against 19.6-32.6 for 1-4 groups; tools/sync_probe,
+    // profiles/r02/sync_probe_groups.jsonl). A job goes to the group with the fewest outstanding, so
+    // one caller keeps one group hot and the idle ones back off.
+    uint32_t nslots = 1024, groups = 8, per_group = 128;
     uint64_t idle_ticks = 100000000ull;  // 1 s at 100 MHz
     int idle_ms = 50;
     double timeout_s = 2.0;
@@ -138,7 +140,8 @@ struct Mailbox {
     std::unique_ptr<std::atomic<uint64_t>[]> free_at;
     std::mutex mu;
     bool running = false, broken = false, quit = false;
-    uint64_t next = 0;
+    uint64_t next[cts::kMailMaxGroups] = {};       // each group's next job number
+    uint32_t busy[cts::kMailMaxGroups] = {};       // each group's jobs outstanding
     uint32_t outstanding = 0;
     std::chrono::steady_clock::time_point last_post;
     std::condition_variable cv;
@@ -168,18 +171,19 @@ struct Mailbox {
     {
         e = eng;
         nslots = (uint32_t)std::max(16, env_int("CTS_MAILBOX_SLOTS", (int)nslots));
-        groups = (uint32_t)std::min(64, std::max(1, env_int("CTS_MAILBOX_GROUPS", (int)groups)));
+        groups = (uint32_t)std::min((int)cts::kMailMaxGroups, std::max(1, env_int("CTS_MAILBOX_GROUPS", (int)groups)));
         idle_ms = std::max(1, env_int("CTS_MAILBOX_IDLE_MS", idle_ms));
         DeviceGuard g(e->device);
         if (!g.ok) return CTS_E_HIP;
         void* p = nullptr;
+        per_group = (nslots + groups - 1) / groups;
+        nslots = per_group * groups;
         if (hipHostMalloc(&p, sizeof(cts::MailSlot) * nslots,
                           hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent) != hipSuccess)
             return CTS_E_NOMEM;
         slots = static_cast<cts::MailSlot*>(p);
         std::memset(slots, 0, sizeof(cts::MailSlot) * nslots);
         if ((dslots = device_view(slots)) == nullptr) return CTS_E_HIP;
-        nslots = (nslots + groups - 1) / groups * groups;  // slot k always belongs to group k mod G
         const size_t pbytes = sizeof(cts::MailPart) * nslots * cts::kMailGroup;
         if (hipHostMalloc(&p, pbytes, hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent) !=
             hipSuccess)
@@ -193,31 +197,33 @@ struct Mailbox {
         }
         free_at.reset(new (std::nothrow) std::atomic<uint64_t>[nslots]);
         if (!free_at) return CTS_E_NOMEM;
-        for (uint32_t i = 0; i < nslots; ++i) free_at[i].store(i, std::memory_order_relaxed);
+        for (uint32_t i = 0; i < nslots; ++i) free_at[i].store(i % per_group, std::memory_order_relaxed);  // job j of its group
         last_post = std::chrono::steady_clock::now();
         watchdog = std::thread([this] { Watch(); });
         return CTS_OK;
     }
 
-    // under mu: start the grid at ticket `next` (after any grid still draining, same stream)
+    // under mu: start the grid at every group's next job (after any grid still draining, same stream)
     int LaunchLocked()
     {
         DeviceGuard g(e->device);
         if (!g.ok) return CTS_E_HIP;
-        if (cts::launch_mailbox(dslots, dparts, nslots, next, groups, idle_ticks, stream) != hipSuccess)
+        cts::MailStarts starts{};
+        for (uint32_t i = 0; i < groups; ++i) starts.j[i] = next[i];
+        if (cts::launch_mailbox(dslots, dparts, per_group, starts, groups, idle_ticks, stream) != hipSuccess)
             return CTS_E_HIP;
         running = true;
         launches.fetch_add(1, std::memory_order_relaxed);
         return CTS_OK;
     }
 
-    // Claim a ticket (launching the grid if needed), write the job, wait for the answer.
-    // Verify [ptr, ptr + len) (len > 0), or stop the grid (len == 0: one stop ticket per group, so
-    // every group leaves; only_if_idle: not while another job is outstanding).
+    // Claim a job number in the least busy group (launching the grid if needed), write the job, wait
+    // for the answer. Verify [ptr, ptr + len) (len > 0), or stop the grid (len == 0: one stop job per
+    // group, so every group leaves; only_if_idle: not while another job is outstanding).
     int Post(uint64_t ptr, uint32_t len, uint32_t expected, cts_verify_result* out, bool only_if_idle)
     {
-        uint64_t t;
-        uint32_t n = 1;
+        uint64_t js[cts::kMailMaxGroups];
+        uint32_t g0 = 0, n = 1;
         {
             std::lock_guard<std::mutex> lk(mu);
             if (broken) return CTS_E_HIP;
@@ -225,42 +231,48 @@ struct Mailbox {
                 if (!running || (only_if_idle && outstanding != 0)) return CTS_OK;
                 running = false;
                 n = groups;
-            } else if (!running) {
-                const int rc = LaunchLocked();
-                if (rc != CTS_OK) return rc;
+            } else {
+                if (!running) {
+                    const int rc = LaunchLocked();
+                    if (rc != CTS_OK) return rc;
+                }
+                for (uint32_t i = 1; i < groups; ++i)
+                    if (busy[i] < busy[g0]) g0 = i;
             }
-            t = next;
-            next += n;
+            for (uint32_t i = 0; i < n; ++i) {
+                js[i] = next[g0 + i]++;
+                ++busy[g0 + i];
+            }
             ++outstanding;
             last_post = std::chrono::steady_clock::now();
         }
         int rc = CTS_OK;
-        for (uint32_t i = 0; i < n && rc == CTS_OK; ++i) rc = Run(t + i, ptr, len, expected, out);
+        for (uint32_t i = 0; i < n && rc == CTS_OK; ++i) rc = Run(g0 + i, js[i], ptr, len, expected, out);
         std::lock_guard<std::mutex> lk(mu);
         if (rc != CTS_OK) {
             broken = true;  // a straggler may still read or answer the slot: never reuse it
             broken_flag.store(true, std::memory_order_release);
             running = false;
         }
+        for (uint32_t i = 0; i < n; ++i) --busy[g0 + i];
         --outstanding;
         return rc;
     }
 
-    // One ticket: wait for its slot, write the job, fold the part records.
-    int Run(uint64_t t, uint64_t ptr, uint32_t len, uint32_t expected, cts_verify_result* out)
+    // Group g's job j: wait for its slot, write the job, fold the part records.
+    int Run(uint32_t g, uint64_t j, uint64_t ptr, uint32_t len, uint32_t expected, cts_verify_result* out)
     {
-        const uint32_t k = (uint32_t)(t % nslots);
+        const uint32_t k = g * per_group + (uint32_t)(j % per_group);
+        const uint64_t t = j;
         while (free_at[k].load(std::memory_order_acquire) != t) {
             // the slot's previous ticket timed out: it is never freed, and the mailbox is broken
             if (broken_flag.load(std::memory_order_acquire)) return CTS_E_HIP;
             std::this_thread::yield();
         }
-        cts::MailSlot* const s = slots + k;
         const uint32_t tag = (uint32_t)(t + 1);
-        // the job half first, then the tagged half: the grid's one 16-B read of the slot sees a new tag
-        // only with the new job (x86 keeps the two stores in order)
-        __atomic_store_n(&s->ptr_exp, (ptr & 0xFFFFFFFFFFFFull) | ((uint64_t)expected << 48), __ATOMIC_RELAXED);
-        __atomic_store_n(&s->len_seq, (uint64_t)len | ((uint64_t)tag << 32), __ATOMIC_RELEASE);
+        // the job half first, then the tagged half: the grid's one 16-B read of a copy sees a new tag only
+        // with the new job
+        cts::mail_write(slots + k, (ptr & 0xFFFFFFFFFFFFull) | ((uint64_t)expected << 48), (uint64_t)len | ((uint64_t)tag << 32));
         const uint32_t np = cts::mail_parts(ptr, len);
         const cts::MailPart* const pr = parts + (size_t)k * cts::kMailGroup;
         const auto t_start = std::chrono::steady_clock::now();
@@ -284,7 +296,7 @@ struct Mailbox {
             }
             count += (uint32_t)g1;
         }
-        free_at[k].store(t + nslots, std::memory_order_release);
+        free_at[k].store(t + per_group, std::memory_order_release);
         if (out != nullptr && len != 0) {
             // RtlCompareMemory of the whole buffer (ctsIOPattern.cpp:753-774): the smallest first
             // difference over the pieces; expected/actual are the two bytes the reference prints

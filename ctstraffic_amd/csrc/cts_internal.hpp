@@ -66,25 +66,34 @@ struct LaunchGeometry {
 };
 
 // ---- SYNC mailbox (cts_verify_mapped): a resident verify grid fed through pinned host memory ----
-// Host-coherent pinned memory (hipHostMallocCoherent) holds one 64-B slot per ticket mod nslots and
-// one 16-B part record per (slot, piece). The caller writes the job's first 8 bytes, then the 8
+// Host-coherent pinned memory (hipHostMallocCoherent) holds G rings of S 64-B job slots, one ring per
+// group, and one 16-B part record per (slot, piece). Group g's j-th job (j counts per group) uses
+// slot g * S + j mod S and carries the tag j + 1. The caller writes the job's first 8 bytes, then the 8
 // bytes carrying the sequence tag, so the grid's single 16-B read of a slot never sees a new tag
 // with an old job. Every workgroup that verified a piece answers with one 16-B part record whose two
 // 8-byte halves each carry the ticket's tag (each half is one naturally aligned 8-B store, so a
 // half is never torn); the caller folds the parts: min of first differing bytes, sum of counts.
 struct alignas(64) MailSlot {
     uint64_t ptr_exp;  // device address (bits 0-47) | expected pattern offset << 48
-    uint64_t len_seq;  // length (bits 0-31; 0 = stop: the grid exits) | (ticket + 1) << 32
+    uint64_t len_seq;  // length (bits 0-31; 0 = stop: the grid exits) | (j + 1) << 32
     uint64_t pad[6];
 };
 static_assert(sizeof(MailSlot) == 64, "one cache line per slot");
+// Host side: the job half, then the tagged half (x86 keeps the two stores in order), so the grid's one
+// 16-B read of a slot never sees a new tag with an old job.
+inline void mail_write(MailSlot* s, uint64_t ptr_exp, uint64_t len_seq)
+{
+    __atomic_store_n(&s->ptr_exp, ptr_exp, __ATOMIC_RELAXED);
+    __atomic_store_n(&s->len_seq, len_seq, __ATOMIC_RELEASE);
+}
 struct alignas(16) MailPart {
-    uint64_t g0;  // first differing byte of the piece(s), 0xFFFFFFFF = none | (ticket + 1) << 32
-    uint64_t g1;  // differing bytes | received byte at g0's first << 32 | ((ticket + 1) & 0xFFFFFF) << 40
+    uint64_t g0;  // first differing byte of the piece(s), 0xFFFFFFFF = none | (j + 1) << 32
+    uint64_t g1;  // differing bytes | received byte at g0's first << 32 | ((j + 1) & 0xFFFFFF) << 40
 };
 constexpr uint32_t kMailPieceBytes = 4096;  // one 16-B load per lane of a 256-lane workgroup
-// The grid is G groups of kMailGroup workgroups; ticket t belongs to group t mod G, whose workgroups
-// alone poll its slot and verify its pieces (piece u by workgroup u mod kMailGroup of the group).
+// The grid is G groups of kMailGroup workgroups; a group's workgroups alone poll its ring and verify
+// its jobs' pieces (piece u by workgroup u mod kMailGroup of the group). The caller gives each job to
+// the group with the fewest jobs outstanding, so one caller keeps one group busy and the others idle.
 // Sixteen 4-KiB pieces cover a 64 KiB buffer in one PCIe round trip; G jobs run side by side, and
 // no slot is polled by more than kMailGroup readers (64 concurrent pollers of one host line cost
 // 10-13 us per round trip against 4.7 us for 16: tools/mailbox_probe).
@@ -99,11 +108,15 @@ inline uint32_t mail_parts(uint64_t ptr, uint32_t len)
     const uint64_t pieces = (((ptr & 15u) + (uint64_t)len + 15u) / 16u * 16u + kMailPieceBytes - 1) / kMailPieceBytes;
     return pieces < kMailGroup ? (uint32_t)pieces : kMailGroup;
 }
-// Each group polls its tickets from t0 on until a stop job, or until it has waited idle_ticks
-// (s_memrealtime, 100 MHz) for one ticket: every wave reaches one of the two exits. Part records:
-// kMailGroup per slot. groups * kMailGroup workgroups.
-hipError_t launch_mailbox(const MailSlot* slots, MailPart* parts, uint32_t nslots, uint64_t t0, uint32_t groups,
-                          uint64_t idle_ticks, hipStream_t stream);
+constexpr uint32_t kMailMaxGroups = 64;
+struct MailStarts {
+    uint64_t j[kMailMaxGroups];  // each group's first job number (passed by value)
+};
+// Each group polls its jobs from starts.j[g] on until a stop job, or until it has waited idle_ticks
+// (s_memrealtime, 100 MHz) for one job: every wave reaches one of the two exits. per_group = S.
+// groups * kMailGroup workgroups of kMailThreads threads.
+hipError_t launch_mailbox(const MailSlot* slots, MailPart* parts, uint32_t per_group, const MailStarts& starts,
+                          uint32_t groups, uint64_t idle_ticks, hipStream_t stream);
 
 hipError_t launch_verify(const uint8_t* arena, uint64_t arena_bytes, const cts_buf_desc* descs, uint32_t n,
                          uint32_t max_length_hint, cts_verify_result* results, uint64_t* counters,

@@ -1836,24 +1836,35 @@ static void launch_verify_nt(const uint8_t* arena, uint64_t arena_bytes, const c
 }
 
 // ---- SYNC mailbox: VerifyBuffer (ctsIOPattern.cpp:745-775) per completion without a launch per call ----
-// A resident grid of G groups x kMailGroup workgroups; ticket t belongs to group t mod G. Lane 0 of
-// each of the group's workgroups polls the ticket's slot with one 16-B system-scope load
-// (+ s_sleep); then the group splits the job's buffer into 4 KiB pieces (one 16-B system-scope load
-// per lane: the host rewrites a reused recv slot between jobs, so nothing may come from a cache) and
-// compares against the pattern regenerated in registers. Each participating workgroup posts one
-// tagged part record to host memory and the caller folds them. No device atomics, fences or
-// inter-workgroup hand-offs sit on the critical path: a job costs the poll's and the data's PCIe
-// round trips (1.2 us each, tools/mailbox_probe) plus one posted write; G jobs run side by side.
-constexpr int kMailAux = 1 | 16;  // sc0 sc1: system scope
+// A resident grid of G groups x kMailGroup workgroups; group g serves its own ring of S job slots.
+// Every workgroup of the group sees each job itself (no inter-workgroup hand-off on the critical
+// path), splits the job's buffer into 4 KiB pieces (one 16-B system-scope load per lane: the host
+// rewrites a reused recv slot between jobs, so nothing may come from a cache), compares them with the
+// pattern regenerated in registers, and posts one tagged part record to host memory; the caller folds
+// the parts.
+//
+// Each workgroup is four data waves and one polling wave. Lane 0 of the poller reads the next job's
+// slot (one 16-B system-scope load in flight) while the data waves still verify the current one, and
+// publishes the job to them through LDS (job, then tag); the data waves fold their results with LDS
+// atomics and the last one posts the part record. Pollers never join a barrier, and a publication
+// slot is reused (two, by job parity) only after its job was folded. More pollers per workgroup, their
+// phases spread over the PCIe round trip, were slower: 2 or 4 polling waves (each on its own copy of
+// the slot) gave 9.5 us per 64 KiB verify against 6.3 with one, on the same box (tools/sync_probe) --
+// the poll reads compete with the data reads. After kMailHotTicks without a job the poller slows
+// down, which keeps idle groups' PCIe reads low (a caller's job goes to the least busy group).
+constexpr int kMailAux = 1 | 16;                 // sc0 sc1: system scope
+constexpr uint32_t kMailThreads = kBlock + 64;   // four data waves + the polling wave
+constexpr uint64_t kMailHotTicks = 5000;         // 50 us (s_memrealtime, 100 MHz)
 
 #if defined(CTS_MAILBOX_TRACE)
-// diagnostic builds only (tools/mailbox_bisect.hip): per (ticket mod 1024, workgroup) the s_memrealtime
-// stamps of the poll that matched, the data compared, the part record stored, and the poll's start
+// diagnostic builds only (tools/mailbox_bisect.hip): per (job mod 1024, workgroup) the s_memrealtime
+// stamps of the publication, the data compared (wave 0), the part record stored, the poll's start, and
+// each data wave's compare (4 + wave)
 __device__ uint64_t* cts_mail_trace;
-#define CTS_MAIL_STAMP(which)                                                                           \
-    do {                                                                                                \
-        if (tid == 0 && cts_mail_trace != nullptr)                                                      \
-            cts_mail_trace[((t % 1024u) * kMailGroup + gi) * 4u + (which)] = wall_clock64();            \
+#define CTS_MAIL_STAMP(which)                                                                      \
+    do {                                                                                           \
+        if (cts_mail_trace != nullptr)                                                             \
+            cts_mail_trace[((j % 1024u) * kMailGroup + gi) * 8u + (which)] = wall_clock64();       \
     } while (0)
 #else
 #define CTS_MAIL_STAMP(which) \
@@ -1861,125 +1872,161 @@ __device__ uint64_t* cts_mail_trace;
     } while (0)
 #endif
 
-__global__ __launch_bounds__(kBlock) void mailbox_kernel(const MailSlot* slots, MailPart* parts, uint32_t nslots,
-                                                         uint64_t t0, uint64_t idle_ticks)
+__global__ __launch_bounds__(kMailThreads) void mailbox_kernel(const MailSlot* slots, MailPart* parts, uint32_t per_group,
+                                                               MailStarts starts, uint64_t idle_ticks)
 {
-    __shared__ uint64_t s_job[2];
-    __shared__ uint32_t s_first[kBlock / 64], s_count[kBlock / 64];
-    const uint32_t G = gridDim.x / kMailGroup, g = blockIdx.x / kMailGroup, gi = blockIdx.x % kMailGroup;
-    const uint32_t tid = threadIdx.x;
-    typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
-    for (uint64_t t = t0 + (g + G - (uint32_t)(t0 % G)) % G;; t += G) {  // this group's tickets
-        const uint32_t k = (uint32_t)(t % nslots);
-        const uint32_t tag = (uint32_t)(t + 1);
-        if (tid == 0) {
-            const __amdgpu_buffer_rsrc_t r =
-                __builtin_amdgcn_make_buffer_rsrc(const_cast<MailSlot*>(slots + k), (short)0, 16, 0x00020000);
+    __shared__ uint64_t s_job[2][2];              // published job by parity: ptr_exp, len_seq
+    __shared__ uint32_t s_tag[2];                 // its tag, written after the job
+    __shared__ uint32_t s_first[2], s_count[2], s_arrive[2];
+    __shared__ uint32_t s_done;                   // jobs folded
+    const uint32_t g = blockIdx.x / kMailGroup, gi = blockIdx.x % kMailGroup;
+    const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
+    const uint64_t j0 = starts.j[g];
+    const MailSlot* const ring = slots + (size_t)g * per_group;
+    if (tid == 0) {
+        s_tag[0] = s_tag[1] = (uint32_t)j0;  // j0's tag is j0 + 1: neither parity starts published
+        s_first[0] = s_first[1] = kNone;
+        s_count[0] = s_count[1] = s_arrive[0] = s_arrive[1] = 0;
+        s_done = 0;
+    }
+    __syncthreads();  // the kernel's only barrier
+    // LDS words shared with waves that never meet at a barrier: relaxed workgroup-scope atomics (ds_read /
+    // ds_write), ordered by lds_order() -- one wave's LDS operations execute in issue order, so only the
+    // compiler has to be kept from reordering them (no fence: a fence would wait for outstanding loads)
+#define LDS_LD(x) __hip_atomic_load(&(x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
+#define LDS_ST(x, v) __hip_atomic_store(&(x), (v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
+    const auto lds_order = [] { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
+
+    if (wave == kBlock / 64) {  // ---- the poller ----
+        if (lane != 0) return;
+        for (uint32_t i = 0;; ++i) {
+            const uint64_t j = j0 + i;
+            const uint32_t tag = (uint32_t)(j + 1), par = i & 1u;
+            while (LDS_LD(s_done) + 1u < i) __builtin_amdgcn_s_sleep(1);  // job i-2 folded: its parity is free
+            const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<MailSlot*>(ring + (uint32_t)(j % per_group)), (short)0, 16, 0x00020000);
             const uint64_t start = wall_clock64();
             CTS_MAIL_STAMP(3);
-            u64x2 job = {0, 0};
+            u32x4 v;
             for (;;) {
-                const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, 0u, 0u, kMailAux);
-                job = u64x2{(uint64_t)v[0] | ((uint64_t)v[1] << 32), (uint64_t)v[2] | ((uint64_t)v[3] << 32)};
-                if ((uint32_t)(job[1] >> 32) == tag) {
-                    CTS_MAIL_STAMP(0);
+                v = __builtin_amdgcn_raw_buffer_load_b128(r, 0u, 0u, kMailAux);
+                if (v[3] == tag) break;
+                const uint64_t waited = wall_clock64() - start;
+                if (waited > idle_ticks) {  // no job within idle_ticks: publish one whose tag word is not the tag
+                    v = u32x4{0u, 0u, 0u, ~tag};
                     break;
                 }
-                if (wall_clock64() - start > idle_ticks) {
-                    job[1] = 0;  // no job for this ticket within idle_ticks: leave
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(2);
+                if (waited > kMailHotTicks) __builtin_amdgcn_s_sleep(40);
+                else __builtin_amdgcn_s_sleep(2);
             }
-            s_job[0] = job[0];
-            s_job[1] = job[1];
+            LDS_ST(s_job[par][0], (uint64_t)v[0] | ((uint64_t)v[1] << 32));
+            LDS_ST(s_job[par][1], (uint64_t)v[2] | ((uint64_t)v[3] << 32));
+            lds_order();
+            LDS_ST(s_tag[par], tag);
+            CTS_MAIL_STAMP(0);
+            if (v[3] != tag || v[2] == 0u) return;  // idle leave or stop
         }
-        __syncthreads();
-        const uint64_t ptr_exp = s_job[0], len_seq = s_job[1];
-        __syncthreads();  // s_job is rewritten for the next ticket only after every wave read it
-        if ((uint32_t)(len_seq >> 32) != tag) return;
+    }
+
+    // ---- data waves ----
+    for (uint32_t i = 0;; ++i) {
+        const uint64_t j = j0 + i;
+        const uint32_t tag = (uint32_t)(j + 1), par = i & 1u;
+        while (LDS_LD(s_tag[par]) != tag) __builtin_amdgcn_s_sleep(1);
+        lds_order();
+        const uint64_t ptr_exp = LDS_LD(s_job[par][0]), len_seq = LDS_LD(s_job[par][1]);
+        if ((uint32_t)(len_seq >> 32) != tag) return;  // idle leave
         const uint64_t ptr = ptr_exp & 0xFFFFFFFFFFFFull;
         const uint32_t expected = (uint32_t)(ptr_exp >> 48), len = (uint32_t)len_seq;
-        if (gi >= mail_parts(ptr, len)) continue;
-        MailPart* const out = parts + (size_t)k * kMailGroup + gi;
-        if (len == 0) {  // stop: every workgroup of the group acknowledges, then leaves
-            if (tid == 0) {
-                __hip_atomic_store(&out->g0, 0xFFFFFFFFull | ((uint64_t)tag << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                __hip_atomic_store(&out->g1, (uint64_t)(tag & 0xFFFFFFu) << 40, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            }
-            return;
-        }
+        const bool mine = gi < mail_parts(ptr, len);
         const uint32_t d = (uint32_t)ptr & 15u;
-        const uint64_t nchunks = ((uint64_t)d + len + 15u) >> 4;
-        const uint32_t pieces = (uint32_t)((nchunks * 16u + kMailPieceBytes - 1) / kMailPieceBytes);
         const uint8_t* const base = reinterpret_cast<const uint8_t*>(ptr - d);
-        const uint32_t q_base = (expected + 65536u - d) & 0xFFFFu;  // pattern position of base[0]
-        const uint32_t hi_last = ((d + len - 1u) & 15u) + 1u;
         uint32_t first = kNone, count = 0;
-        for (uint32_t u0 = gi; u0 < pieces; u0 += 4 * kMailGroup) {
-            u32x4 v[4];
+        if (mine && len != 0) {
+            const uint64_t nchunks = ((uint64_t)d + len + 15u) >> 4;
+            const uint32_t pieces = (uint32_t)((nchunks * 16u + kMailPieceBytes - 1) / kMailPieceBytes);
+            const uint32_t q_base = (expected + 65536u - d) & 0xFFFFu;  // pattern position of base[0]
+            const uint32_t hi_last = ((d + len - 1u) & 15u) + 1u;
+            for (uint32_t u0 = gi; u0 < pieces; u0 += 4 * kMailGroup) {
+                u32x4 v[4];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {  // four pieces' loads in flight before any compare
-                const uint32_t u = u0 + j * kMailGroup;
-                const uint64_t off = (uint64_t)u * kMailPieceBytes;
-                const uint64_t rem = u < pieces ? nchunks * 16u - off : 0u;
-                const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-                    const_cast<uint8_t*>(base + (u < pieces ? off : 0u)), (short)0,
-                    (int)(rem < kMailPieceBytes ? rem : kMailPieceBytes), 0x00020000);
-                v[j] = __builtin_amdgcn_raw_buffer_load_b128(r, tid * 16u, 0u, kMailAux);
-            }
+                for (int jj = 0; jj < 4; ++jj) {  // four pieces' loads in flight before any compare
+                    const uint32_t u = u0 + jj * kMailGroup;
+                    const uint64_t off = (uint64_t)u * kMailPieceBytes;
+                    const uint64_t rem = u < pieces ? nchunks * 16u - off : 0u;
+                    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+                        const_cast<uint8_t*>(base + (u < pieces ? off : 0u)), (short)0,
+                        (int)(rem < kMailPieceBytes ? rem : kMailPieceBytes), 0x00020000);
+                    v[jj] = __builtin_amdgcn_raw_buffer_load_b128(r, tid * 16u, 0u, kMailAux);
+                }
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const uint64_t c = (uint64_t)(u0 + j * kMailGroup) * (kMailPieceBytes / 16u) + tid;
-                if (u0 + j * kMailGroup >= pieces || c >= nchunks) continue;
-                const uint32_t q = (uint32_t)((q_base + c * 16u) & 0xFFFFu);
-                u32x4 x = v[j] ^ expected_chunk(q, q & 1u);
-                if (c == 0 || c == nchunks - 1) x &= range_mask(c == 0 ? d : 0u, c == nchunks - 1 ? hi_last : 16u);
-                if (or4(x) == 0u) continue;
+                for (int jj = 0; jj < 4; ++jj) {
+                    const uint64_t c = (uint64_t)(u0 + jj * kMailGroup) * (kMailPieceBytes / 16u) + tid;
+                    if (u0 + jj * kMailGroup >= pieces || c >= nchunks) continue;
+                    const uint32_t q = (uint32_t)((q_base + c * 16u) & 0xFFFFu);
+                    u32x4 x = v[jj] ^ expected_chunk(q, q & 1u);
+                    if (c == 0 || c == nchunks - 1) x &= range_mask(c == 0 ? d : 0u, c == nchunks - 1 ? hi_last : 16u);
+                    if (or4(x) == 0u) continue;
 #pragma unroll
-                for (int w = 0; w < 4; ++w) {
-                    const uint32_t nz = nonzero_bytes(x[w]);
-                    if (nz == 0u) continue;
-                    const uint32_t pos = (uint32_t)(c * 16u - d) + 4u * w + ((uint32_t)__builtin_ctz(nz) >> 3);
-                    first = pos < first ? pos : first;
-                    count += (uint32_t)__builtin_popcount(nz);
+                    for (int w = 0; w < 4; ++w) {
+                        const uint32_t nz = nonzero_bytes(x[w]);
+                        if (nz == 0u) continue;
+                        const uint32_t pos = (uint32_t)(c * 16u - d) + 4u * w + ((uint32_t)__builtin_ctz(nz) >> 3);
+                        first = pos < first ? pos : first;
+                        count += (uint32_t)__builtin_popcount(nz);
+                    }
                 }
             }
         }
         first = wave_min(first);
         count = wave_sum(count);
-        CTS_MAIL_STAMP(1);
-        if ((tid & 63u) == 0) {
-            s_first[tid >> 6] = first;
-            s_count[tid >> 6] = count;
-        }
-        __syncthreads();
-        if (tid == 0) {
-#pragma unroll
-            for (int w = 1; w < kBlock / 64; ++w) {
-                first = s_first[w] < first ? s_first[w] : first;
-                count += s_count[w];
+        if (tid == 0) CTS_MAIL_STAMP(1);
+        if (lane == 0) CTS_MAIL_STAMP(4 + wave);
+        if (lane == 0) {
+            __hip_atomic_fetch_min(&s_first[par], first, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_add(&s_count[par], count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            lds_order();
+            if (__hip_atomic_fetch_add(&s_arrive[par], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) ==
+                kBlock / 64 - 1) {  // the last data wave: post the part record, free the parity
+                lds_order();
+                const uint32_t f = LDS_LD(s_first[par]);
+                const uint32_t n = LDS_LD(s_count[par]);
+                if (mine) {
+                    MailPart* const out = parts + ((size_t)g * per_group + (uint32_t)(j % per_group)) * kMailGroup + gi;
+                    uint64_t g0 = 0xFFFFFFFFull | ((uint64_t)tag << 32), g1 = (uint64_t)(tag & 0xFFFFFFu) << 40;
+                    if (len != 0) {
+                        uint32_t actual = 0;
+                        if (f != kNone) {  // the received byte there (ctsIOPattern.cpp:761-772 prints it)
+                            const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+                                const_cast<uint8_t*>(base + d + f), (short)0, 1, 0x00020000);
+                            actual = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(r, 0u, 0u, kMailAux);
+                        }
+                        g0 = (uint64_t)f | ((uint64_t)tag << 32);
+                        g1 |= (uint64_t)n | ((uint64_t)actual << 32);
+                    }
+                    __hip_atomic_store(&out->g0, g0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    __hip_atomic_store(&out->g1, g1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    CTS_MAIL_STAMP(2);
+                }
+                LDS_ST(s_first[par], kNone);
+                LDS_ST(s_count[par], 0u);
+                LDS_ST(s_arrive[par], 0u);
+                lds_order();
+                LDS_ST(s_done, i + 1u);
             }
-            uint32_t actual = 0;
-            if (first != kNone) {  // the received byte there (ctsIOPattern.cpp:761-772 prints it)
-                const __amdgpu_buffer_rsrc_t r =
-                    __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base + d + first), (short)0, 1, 0x00020000);
-                actual = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(r, 0u, 0u, kMailAux);
-            }
-            __hip_atomic_store(&out->g0, (uint64_t)first | ((uint64_t)tag << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(&out->g1, (uint64_t)count | ((uint64_t)actual << 32) | ((uint64_t)(tag & 0xFFFFFFu) << 40),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            CTS_MAIL_STAMP(2);
         }
-        __syncthreads();  // s_first / s_count are rewritten by the next ticket
+        if (len == 0) return;  // stop: acknowledged above
     }
+#undef LDS_LD
+#undef LDS_ST
 }
 
-hipError_t launch_mailbox(const MailSlot* slots, MailPart* parts, uint32_t nslots, uint64_t t0, uint32_t groups,
-                          uint64_t idle_ticks, hipStream_t stream)
+hipError_t launch_mailbox(const MailSlot* slots, MailPart* parts, uint32_t per_group, const MailStarts& starts,
+                          uint32_t groups, uint64_t idle_ticks, hipStream_t stream)
 {
-    if (slots == nullptr || parts == nullptr || nslots == 0 || groups == 0) return hipErrorInvalidValue;
-    mailbox_kernel<<<groups * kMailGroup, kBlock, 0, stream>>>(slots, parts, nslots, t0, idle_ticks);
+    if (slots == nullptr || parts == nullptr || per_group == 0 || groups == 0 || groups > kMailMaxGroups)
+        return hipErrorInvalidValue;
+    mailbox_kernel<<<groups * kMailGroup, kMailThreads, 0, stream>>>(slots, parts, per_group, starts, idle_ticks);
     return hipGetLastError();
 }
 

@@ -206,12 +206,13 @@ int cts_verify_host(cts_engine* engine, const void* host_buf, uint32_t len,
 /* The same one-buffer VerifyBuffer (ctsIOPattern.cpp:745-775) for a buffer the
  * GPU can already address (a cts_host_alloc dev_view, or HBM), verified in
  * place and waited for, without a kernel launch per call: a resident grid on
- * the engine's device polls a ring of host-coherent pinned job slots, verifies
- * each posted buffer as 4 KiB pieces spread over its workgroups and writes the
- * record back to the slot, which the caller spins on. Thread-safe: concurrent
- * connections' CompleteIo (each serialised per connection by its ctsSocket
- * lock, ctsSocket.h:189) post independent tickets whose pieces run side by
- * side. The grid starts on the first call and stops after
+ * the engine's device (groups of workgroups, each group polling its own ring
+ * of host-coherent pinned job slots) verifies each posted buffer as 4 KiB
+ * pieces spread over a group's workgroups, which answer with part records
+ * the caller spins on and folds. Thread-safe: concurrent connections'
+ * CompleteIo (each serialised per connection by its ctsSocket lock,
+ * ctsSocket.h:189) post independent jobs, each to the least busy group, and
+ * those run side by side. The grid starts on the first call and stops after
  * CTS_MAILBOX_IDLE_MS (default 50) ms without calls (env CTS_MAILBOX_GROUPS,
  * CTS_MAILBOX_SLOTS size it); cts_engine_destroy stops it. */
 int cts_verify_mapped(cts_engine* engine, const void* dev_buf, uint32_t len,

@@ -56,13 +56,16 @@ int main(int argc, char** argv)
         if (!slots || !parts) return 1;
         hipStream_t s;
         (void)hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
-        const size_t trace_n = 1024u * cts::kMailGroup * 4u;
+        const size_t trace_n = 1024u * cts::kMailGroup * 8u;
         uint64_t* trace = nullptr;
         if (hipMalloc((void**)&trace, trace_n * 8) != hipSuccess) return 1;
         (void)hipMemset(trace, 0, trace_n * 8);
         if (hipMemcpyToSymbol(HIP_SYMBOL(cts::cts_mail_trace), &trace, sizeof(trace)) != hipSuccess) return 1;
         (void)hipDeviceSynchronize();
-        if (cts::launch_mailbox(dslots, dparts, nslots, 0, G, 100000000ull, s) != hipSuccess) return 1;
+        // every job goes to group 0 (the engine's choice for one caller); the other G - 1 groups idle
+        const uint32_t S = nslots / G;
+        cts::MailStarts starts{};
+        if (cts::launch_mailbox(dslots, dparts, S, starts, G, 100000000ull, s) != hipSuccess) return 1;
         const uint64_t ptr = reinterpret_cast<uint64_t>(dbuf);
         const uint32_t np = cts::mail_parts(ptr, len);
         double sum_first = 0, sum_last = 0, t_begin = 0;
@@ -71,11 +74,9 @@ int main(int argc, char** argv)
         uint64_t t = 0;
         for (int i = 0; i < iters + 100 && ok; ++i, ++t) {
             if (i == 100) t_begin = now_us();
-            const uint32_t k = (uint32_t)(t % nslots), tag = (uint32_t)(t + 1);
-            cts::MailSlot* const sl = slots + k;
+            const uint32_t k = (uint32_t)(t % S), tag = (uint32_t)(t + 1);
             const double t0 = now_us();
-            __atomic_store_n(&sl->ptr_exp, (ptr & 0xFFFFFFFFFFFFull) | ((uint64_t)expected << 48), __ATOMIC_RELAXED);
-            __atomic_store_n(&sl->len_seq, (uint64_t)len | ((uint64_t)tag << 32), __ATOMIC_RELEASE);
+            cts::mail_write(slots + k, (ptr & 0xFFFFFFFFFFFFull) | ((uint64_t)expected << 48), (uint64_t)len | ((uint64_t)tag << 32));
             const cts::MailPart* const pr = parts + (size_t)k * cts::kMailGroup;
             double t_first = 0;
             uint32_t seen = 0, first = 0xFFFFFFFFu;
@@ -103,11 +104,10 @@ int main(int argc, char** argv)
             }
         }
         const double total = now_us() - t_begin;
-        // stop: one stop ticket per group (len 0), then let the grid drain
-        for (uint32_t g = 0; g < G && ok; ++g, ++t) {
-            cts::MailSlot* const sl = slots + (uint32_t)(t % nslots);
-            __atomic_store_n(&sl->ptr_exp, 0ull, __ATOMIC_RELAXED);
-            __atomic_store_n(&sl->len_seq, (uint64_t)(uint32_t)(t + 1) << 32, __ATOMIC_RELEASE);
+        // stop: one stop job per group (len 0; group 0 at job t, the others at job 0), then let the grid drain
+        for (uint32_t g = 0; g < G && ok; ++g) {
+            const uint64_t jg = g == 0 ? t : 0;
+            cts::mail_write(slots + g * S + (uint32_t)(jg % S), 0ull, (uint64_t)(uint32_t)(jg + 1) << 32);
         }
         (void)hipStreamSynchronize(s);
         // GPU-side split of the last 1024 tickets (s_memrealtime: 10 ns ticks): spread of the 16
@@ -115,15 +115,27 @@ int main(int argc, char** argv)
         {
             std::vector<uint64_t> h(trace_n);
             (void)hipMemcpy(h.data(), trace, trace_n * 8, hipMemcpyDeviceToHost);
-            double spread = 0, work = 0, work_max = 0, store = 0, span = 0;
+            double spread = 0, work = 0, work_max = 0, store = 0, span = 0, wave_spread = 0, last_wave = 0, st_after = 0;
+            int nw = 0;
             int n = 0;
-            for (uint64_t tt = t - G - 1024 + 1; tt < t - G; ++tt) {
-                const uint64_t* r = h.data() + (tt % 1024u) * cts::kMailGroup * 4u;
+            for (uint64_t tt = t - 1023; tt < t; ++tt) {
+                const uint64_t* r = h.data() + (tt % 1024u) * cts::kMailGroup * 8u;
                 uint64_t dmin = ~0ull, dmax = 0, smax = 0, wmax = 0;
                 double wsum = 0, ssum = 0;
                 bool okr = true;
                 for (uint32_t w = 0; w < np; ++w) {
-                    const uint64_t d = r[w * 4], c = r[w * 4 + 1], st = r[w * 4 + 2];
+                    const uint64_t d = r[w * 8], c = r[w * 8 + 1], st = r[w * 8 + 2];
+                    uint64_t wlo = ~0ull, whi = 0;
+                    for (int x = 4; x < 8; ++x) {
+                        wlo = std::min(wlo, r[w * 8 + x]);
+                        whi = std::max(whi, r[w * 8 + x]);
+                    }
+                    if (whi >= d && wlo >= d) {
+                        wave_spread += (double)(whi - wlo);
+                        last_wave += (double)(whi - d);
+                        st_after += st >= whi ? (double)(st - whi) : 0.0;
+                        ++nw;
+                    }
                     if (!d || !c || !st || c < d || st < c) okr = false;
                     dmin = std::min(dmin, d);
                     dmax = std::max(dmax, d);
@@ -142,8 +154,10 @@ int main(int argc, char** argv)
             }
             if (n)
                 std::printf("{\"polls\": %u, \"groups\": %u, \"tickets\": %d, \"us_poll_match_spread\": %.3f, \"us_match_to_compared\": %.3f, "
-                            "\"us_match_to_compared_max\": %.3f, \"us_compared_to_stored\": %.3f, \"us_first_match_to_last_store\": %.3f}\n",
-                            polls, G, n, spread / n / 100, work / n / 100, work_max / n / 100, store / n / 100, span / n / 100);
+                            "\"us_match_to_compared_max\": %.3f, \"us_compared_to_stored\": %.3f, \"us_first_match_to_last_store\": %.3f, "
+                            "\"us_data_wave_spread\": %.3f, \"us_match_to_last_wave\": %.3f, \"us_last_wave_to_stored\": %.3f}\n",
+                            polls, G, n, spread / n / 100, work / n / 100, work_max / n / 100, store / n / 100, span / n / 100,
+                            nw ? wave_spread / nw / 100 : 0.0, nw ? last_wave / nw / 100 : 0.0, nw ? st_after / nw / 100 : 0.0);
         }
         (void)hipFree(trace);
         std::printf("{\"polls\": %u, \"groups\": %u, \"iters\": %d, \"us_per_verify\": %.3f, \"us_to_first_part\": %.3f, "

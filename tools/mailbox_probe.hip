@@ -31,11 +31,14 @@ __global__ void chain_kernel(const uint64_t* p, int n, uint64_t* out)
 
 // lane 0 of block 0 polls seq; all blocks read `bytes` of data (bytes / P each) once it appears;
 // every block answers with its own tagged word, the host waits for all P
-__global__ void pingpong_kernel(const uint64_t* seq, uint64_t* ack, const uint8_t* data, uint32_t bytes, int iters)
+// seq_words / ack_words: each block's seq word and ack word sit that many uint64 apart (0: one shared seq)
+__global__ void pingpong_kernel(const uint64_t* seq, uint64_t* ack, const uint8_t* data, uint32_t bytes, int iters,
+                                uint32_t seq_words = 0, uint32_t ack_words = 2)
 {
     __shared__ uint32_t go;
     const uint32_t P = gridDim.x;
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(seq), (short)0, 16, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(seq + blockIdx.x * seq_words), (short)0, 16, 0x00020000);
     const uint32_t per = bytes / P;
     const __amdgpu_buffer_rsrc_t rd =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(data + (size_t)blockIdx.x * per), (short)0, (int)per, 0x00020000);
@@ -62,7 +65,7 @@ __global__ void pingpong_kernel(const uint64_t* seq, uint64_t* ack, const uint8_
         }
         acc = __syncthreads_or(acc != 0x12345678u);
         if (threadIdx.x == 0)
-            __hip_atomic_store(ack + blockIdx.x * 2, (uint64_t)i | ((uint64_t)acc << 32), __ATOMIC_RELAXED,
+            __hip_atomic_store(ack + blockIdx.x * ack_words, (uint64_t)i | ((uint64_t)acc << 32), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_SYSTEM);
         __syncthreads();
     }
@@ -184,6 +187,43 @@ int main()
             std::fflush(stdout);
             if (!ok) return 2;
         }
+    // (5) 16 workgroups, 64 KiB or nothing: one shared seq line vs a line per workgroup (the host writes
+    //     16 copies), and acks 16 B apart (4 per line) vs a line per workgroup
+    for (uint32_t bytes : {0u, 65536u})
+        for (uint32_t seq_words : {0u, 8u})
+            for (uint32_t ack_words : {2u, 8u}) {
+                const uint32_t P = 16;
+                const int iters = 2000;
+                std::memset(hack, 0, 64 * 16);
+                for (uint32_t b = 0; b < P; ++b) __atomic_store_n(hseq + b * seq_words, 0ull, __ATOMIC_SEQ_CST);
+                hipStream_t s;
+                hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+                pingpong_kernel<<<P, 256, 0, s>>>(dseq, dack, ddata, bytes, iters, seq_words, ack_words);
+                double t0 = 0;
+                bool ok = true;
+                for (int i = 1; i <= iters && ok; ++i) {
+                    if (i == 101) t0 = now_us();
+                    for (uint32_t b = 0; b < (seq_words ? P : 1u); ++b)
+                        __atomic_store_n(hseq + b * seq_words, (uint64_t)i, __ATOMIC_RELEASE);
+                    const double ts = now_us();
+                    for (uint32_t b = 0; b < P; ++b)
+                        while ((uint32_t)__atomic_load_n(hack + ack_words * b, __ATOMIC_ACQUIRE) != (uint32_t)i)
+                            if (now_us() - ts > 2e6) {
+                                ok = false;
+                                break;
+                            }
+                }
+                const double t1 = now_us();
+                if (!ok)
+                    for (uint32_t b = 0; b < P; ++b) __atomic_store_n(hseq + b * seq_words, (uint64_t)iters, __ATOMIC_RELEASE);
+                hipStreamSynchronize(s);
+                hipStreamDestroy(s);
+                std::printf("{\"probe\": \"pingpong_lines\", \"bytes\": %u, \"workgroups\": %u, \"seq_line_per_wg\": %d, "
+                            "\"ack_line_per_wg\": %d, \"us_per_round\": %.3f, \"ok\": %d}\n",
+                            bytes, P, seq_words ? 1 : 0, ack_words == 8 ? 1 : 0, (t1 - t0) / (iters - 100), ok ? 1 : 0);
+                std::fflush(stdout);
+                if (!ok) return 2;
+            }
     // (4) the same ping-pong with the job word in device memory the host writes through its mapping
     //     (fine-grained / uncached VRAM behind the BAR): the GPU polls HBM instead of host memory
     for (const unsigned flag : {(unsigned)hipDeviceMallocUncached, (unsigned)hipDeviceMallocFinegrained}) {

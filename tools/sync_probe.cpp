@@ -6,7 +6,7 @@
 // buffer, descriptor and result (T connections completing concurrently). Wait = hipStreamSynchronize
 // or a hipStreamQuery spin, or cts_verify_mapped (posted to the engine's resident mailbox grid: no launch per
 // verify). Prints one JSON line per variant: us per verify (per thread).
-//   build: make tools/sync_probe      run: tools/sync_probe [iters]
+//   build: make tools/sync_probe      run: tools/sync_probe [iters [mailbox]]
 #include <hip/hip_runtime_api.h>
 
 #include <atomic>
@@ -68,10 +68,11 @@ static int run_thread(cts_engine* e, uint32_t slices, bool spin, bool mapped, in
 int main(int argc, char** argv)
 {
     const int iters = argc > 1 ? std::atoi(argv[1]) : 2000;
+    const bool mailbox_only = argc > 2 && std::strcmp(argv[2], "mailbox") == 0;
     cts_engine* e = nullptr;
     if (cts_engine_create(0, &e) != CTS_OK) return 1;
     // wait: 0 stream_sync, 1 query_spin, 2 cts_verify_mapped (mailbox; slices = its 4 KiB pieces, reported as 64)
-    for (int spin = 0; spin < 3; ++spin)
+    for (int spin = mailbox_only ? 2 : 0; spin < 3; ++spin)
         for (uint32_t threads : {1u, 8u, 16u})
             for (uint32_t slices : {1u, 2u, 4u, 8u, 16u, 32u, 64u}) {
                 if ((spin == 2) != (slices == 64) && spin == 2) continue;
