@@ -433,6 +433,56 @@ def test_verify_mapped_mailbox_threads(engine):
     assert not errors, errors[:5]
 
 
+def test_verify_mapped_mailbox_small_rings(monkeypatch):
+    """A fresh engine whose mailbox has 2 groups of 8 job slots (CTS_MAILBOX_GROUPS / CTS_MAILBOX_SLOTS, read when
+    the grid is first set up): 12 threads post at once, so each group's ring wraps many times, posters wait for
+    slots whose previous job is still being answered, and the least-busy assignment keeps both groups busy.
+    Every answer must still be the oracle's record for the caller's own buffer."""
+    import threading
+
+    from ctstraffic_amd import Engine
+
+    monkeypatch.setenv("CTS_MAILBOX_GROUPS", "2")
+    monkeypatch.setenv("CTS_MAILBOX_SLOTS", "16")
+    eng = Engine(0)
+    S = oracle.sender_buffer(70000)
+    T, ITERS, CAP = 12, 60, 4096 + 32
+    arenas = [eng.host_alloc(CAP) for _ in range(T)]
+    errors = []
+
+    def worker(t):
+        arr, _, dev = arenas[t]
+        rng = np.random.default_rng(0x5106 + t)
+        try:
+            for it in range(ITERS):
+                n = int(rng.integers(0, 4097))
+                e = int(rng.integers(0, 65536))
+                at = int(rng.integers(0, 32))
+                arr[at:at + n] = S[e:e + n]
+                if n and rng.random() < 0.3:
+                    arr[at + int(rng.integers(0, n))] ^= int(rng.integers(1, 256))
+                r = eng.verify_mapped(dev + at, n, e)
+                o = oracle.verify_buffer(arr[at:at + n].copy(), 0, e, n)
+                got = (r["pass"], r["first_mismatch"], r["expected"], r["actual"], r["mismatch_bytes"])
+                want = (o["pass"], o["first_mismatch"], o["expected"], o["actual"], o["mismatch_bytes"])
+                if got != want:
+                    errors.append((t, it, n, e, at, got, want))
+        except Exception as ex:  # surfaced below
+            errors.append((t, repr(ex)))
+
+    try:
+        ths = [threading.Thread(target=worker, args=(t,)) for t in range(T)]
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+    finally:
+        for _, h, _ in arenas:
+            eng.host_free(h)
+        eng.close()
+    assert not errors, errors[:5]
+
+
 def test_verify_mapped_mailbox_restarts_after_idle(engine):
     """The mailbox grid stops after CTS_MAILBOX_IDLE_MS (50 ms) without posts and the next post starts it again;
     answers stay exact across the restart, including an HBM buffer and a buffer larger than the grid's
