@@ -543,6 +543,9 @@ struct cts_io_pattern {
         const uint32_t size = (uint32_t)newSize;
         cts_task t{};
         t.rio_buffer_id = kRioInvalid;
+        // with RIO only so many registered send buffers exist: once every one is in flight, no IO yet
+        // (ctsIOPattern.cpp:580-587)
+        if (action == CTS_TASK_SEND && Rio() && m_sendingRioBufferIds.empty()) return t;
         if (action == CTS_TASK_SEND) {
             t.io_action = CTS_TASK_SEND;
             t.buffer_type = CTS_BUFFER_STATIC;

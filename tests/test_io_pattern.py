@@ -1241,6 +1241,29 @@ def test_rio_send_ids_unique_and_recycled(make):
     assert nxt.rio_buffer_id == sends[1].rio_buffer_id
 
 
+def test_rio_send_ids_exhausted_returns_no_io(make):
+    """-io:rioiocp registers the sender buffer 16 MiB / min buffer + 1 times (ctsIOPattern.cpp:61, 195-217). With
+    every one of those ids in flight the next send request is an empty task, not a send (ctsIOPattern.cpp:580-587);
+    a completed send's id makes the next request a send again, and the send offsets stay contiguous."""
+    if not make.rio:
+        pytest.skip("registered IO only")
+    size = 65536
+    p = make(**client_defaults(pre_post_sends=400, buffer_size=size, transfer_size=400 * size))
+    t = p.InitiateIo()
+    assert p.CompleteIo(t, ConnectionIdLength, 0) == ContinueIo
+    ids = (1 << 24) // size + 1
+    sends = [p.InitiateIo() for _ in range(ids)]
+    assert [t.io_action for t in sends] == [Send] * ids
+    assert len({t.rio_buffer_id for t in sends}) == ids
+    assert [t.buffer_offset for t in sends] == [(k * size) % 65536 for k in range(ids)]
+    none = p.InitiateIo()
+    assert none.io_action == A.TASK_NONE and none.rio_buffer_id == A.RIO_INVALID_BUFFERID
+    assert p.CompleteIo(sends[0], size, 0) == ContinueIo
+    nxt = p.InitiateIo()
+    assert nxt.io_action == Send and nxt.rio_buffer_id == sends[0].rio_buffer_id
+    assert nxt.buffer_offset == (ids * size) % 65536
+
+
 def test_rio_without_functions_or_failing_register(rio_fake):
     """RIORegisterBuffer failing anywhere in the constructor (recv slots, connection id, completion message,
     the sender registrations) fails MakeIoPattern and leaves nothing registered."""
