@@ -68,6 +68,10 @@ class CtsPatternConfig(ctypes.Structure):
         ("batch_bytes", ctypes.c_uint64),
         ("registered_io", ctypes.c_uint32),
         ("reserved0", ctypes.c_uint32),
+        ("tcp_bytes_per_second", ctypes.c_int64),
+        ("tcp_bytes_per_second_period", ctypes.c_int64),
+        ("burst_count", ctypes.c_uint32),
+        ("burst_delay", ctypes.c_uint32),
     ]
 
 
@@ -101,7 +105,7 @@ class CtsStatusDetails(ctypes.Structure):
 
 
 assert ctypes.sizeof(CtsTask) == 40
-assert ctypes.sizeof(CtsPatternConfig) == 88
+assert ctypes.sizeof(CtsPatternConfig) == 112
 
 # int (*)(void* ctx, const uint8_t* host_arena, uint64_t arena_bytes, const cts_buf_desc* descs,
 #         uint32_t n, cts_verify_result* results)
@@ -112,6 +116,8 @@ BATCH_VERIFIER = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p
 # uint64_t (*)(void* ctx, char* buffer, uint32_t length) / void (*)(void* ctx, uint64_t buffer_id)
 RIO_REGISTER = ctypes.CFUNCTYPE(ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32)
 RIO_DEREGISTER = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint64)
+# int64_t (*)(void* ctx): the millisecond clock of send pacing (cts_pattern_clock_set)
+CLOCK_MS = ctypes.CFUNCTYPE(ctypes.c_int64, ctypes.c_void_p)
 
 
 def declare(L: ctypes.CDLL) -> None:
@@ -131,6 +137,7 @@ def declare(L: ctypes.CDLL) -> None:
         "cts_io_pattern_last_error": ([P], u32),
         "cts_io_pattern_rio_buffer_id_count": ([P], u64),
         "cts_rio_functions_set": ([P, P, P], i32),
+        "cts_pattern_clock_set": ([P, P], i32),
         "cts_io_pattern_set_ideal_send_backlog": ([P, u32], i32),
         "cts_io_pattern_flush": ([P], i32),
         "cts_io_pattern_get_stats": ([P, ctypes.POINTER(CtsPatternStats)], i32),

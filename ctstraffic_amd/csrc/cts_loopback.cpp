@@ -43,6 +43,13 @@ uint32_t wsa_status(int err)
 }
 
 // returns 0 or a wsa_status
+// A send the pattern deferred (rate limit / burst delay: ctsTask::m_timeOffsetMilliseconds) goes out that
+// many ms later, as ctsSendRecvIocp.cpp:378-383 schedules it on the socket's threadpool timer.
+void pace(const cts_task& t)
+{
+    if (t.time_offset_ms > 0) std::this_thread::sleep_for(std::chrono::milliseconds(t.time_offset_ms));
+}
+
 uint32_t send_all(int fd, const char* p, uint32_t n)
 {
     while (n > 0) {
@@ -93,6 +100,7 @@ void run_side(int* fdslot, cts_io_pattern* p, bool inject, uint32_t inject_index
         uint32_t transferred = 0, status = 0;
         switch (t.io_action) {
         case CTS_TASK_SEND: {
+            pace(t);
             const char* src = t.buffer + t.buffer_offset;
             if (inject && t.track_io && data_sends++ == inject_index && t.buffer_length > 0) {
                 scratch.assign(src, src + t.buffer_length);  // fault injection: one flipped byte on the wire
@@ -230,6 +238,7 @@ struct AsyncSide {
                 const bool inj = sending && inject && t.track_io && data_sends++ == inject_index && t.buffer_length > 0;
                 lk.unlock();
                 if (sending) {
+                    pace(t);
                     const char* src = t.buffer + t.buffer_offset;
                     if (inj) {  // fault injection: one flipped byte on the wire
                         scratch.assign(src, src + t.buffer_length);
@@ -349,6 +358,9 @@ extern "C" int cts_loopback_run_detailed(const cts_loopback_config* cfg, cts_eng
         c.transfer_size = cfg->transfer_size;
         c.verify_mode = cfg->verify_mode;
         c.batch_buffers = cfg->batch_buffers ? cfg->batch_buffers : 256u;
+        c.tcp_bytes_per_second = cfg->tcp_bytes_per_second;  // both sides pace their own sends
+        c.burst_count = cfg->burst_count;
+        c.burst_delay = cfg->burst_delay;
         c.batch_bytes = (uint64_t)c.batch_buffers * cfg->buffer_size;
         return c;
     };

@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <array>
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <memory>
@@ -60,6 +61,23 @@ constexpr uint64_t kRioInvalid = CTS_RIO_INVALID_BUFFERID;
 constexpr uint64_t kMaxSupportedBytesInFlight = 0x1000000;  // c_maxSupportedBytesInFlight, ctsIOPattern.cpp:49
 
 struct RioRegisterFailed {};
+
+// ctTimer::snap_qpc_as_msec, replaceable by cts_pattern_clock_set (the unit-test hook)
+struct Clock {
+    std::mutex mu;
+    cts_clock_ms_fn fn = nullptr;
+    void* ctx = nullptr;
+};
+Clock g_clock;
+int64_t NowMs()
+{
+    {
+        std::lock_guard<std::mutex> lk(g_clock.mu);
+        if (g_clock.fn != nullptr) return g_clock.fn(g_clock.ctx);
+    }
+    return std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
 
 // TcpStatusDetails (ctsConfig.h:415) + a DataError tally
 std::atomic<uint64_t> g_bytesSent{0};
@@ -311,7 +329,11 @@ struct Queued {
 // ---- ctsIoPattern -----------------------------------------------------------------------------
 struct cts_io_pattern {
     explicit cts_io_pattern(const cts_pattern_config& c, uint32_t maxbuf, uint32_t recv_count)
-        : cfg(c), max_buffer_size(maxbuf), state(c, maxbuf), rng(c.random_seed), recvCount(recv_count)
+        : cfg(c), max_buffer_size(maxbuf), state(c, maxbuf), rng(c.random_seed), recvCount(recv_count),
+          m_quantumPeriodMs(c.tcp_bytes_per_second_period > 0 ? c.tcp_bytes_per_second_period : 100),
+          // (bytes/sec) * (1 sec/1000 ms) * (x ms/Quantum) == (bytes/quantum) (ctsIOPattern.cpp:219-224)
+          m_bytesSendingPerQuantum(c.tcp_bytes_per_second * m_quantumPeriodMs / 1000),
+          m_burstCount(c.burst_count), m_quantumStartTimeMs(NowMs())
     {
     }
     virtual ~cts_io_pattern()
@@ -340,6 +362,12 @@ struct cts_io_pattern {
 
     uint32_t m_sendPatternOffset = 0;
     uint32_t m_recvPatternOffset = 0;
+    // send pacing (ctsIOPattern.h:204-205, 273-275); m_burstCount 0 with cfg.burst_count 0 = no burst
+    int64_t m_quantumPeriodMs;
+    int64_t m_bytesSendingPerQuantum;
+    uint32_t m_burstCount;
+    int64_t m_bytesSendingThisQuantum = 0;
+    int64_t m_quantumStartTimeMs;
     uint32_t m_lastError = kStatusIoRunning;
     std::vector<char*> m_recvBufferFreeList;
     Pinned recv_pinned;                 // m_recvBufferContainer when a device verifies in place
@@ -532,6 +560,43 @@ struct cts_io_pattern {
         }
     }
 
+    // When the next send of `size` bytes may go out (ctsIOPattern.cpp:593-674): with a rate limit, the
+    // bytes of each TcpBytesPerSecondPeriod quantum are capped and a send past the cap is deferred to
+    // the quantum it fills; otherwise every BurstCount-th send waits BurstDelay ms.
+    int64_t SendTimeOffset(uint64_t size)
+    {
+        int64_t offset = 0;
+        if (m_bytesSendingPerQuantum > 0) {
+            const int64_t now = NowMs();
+            if (m_bytesSendingThisQuantum < m_bytesSendingPerQuantum) {
+                m_bytesSendingThisQuantum += (int64_t)size;
+                if (now > m_quantumStartTimeMs + m_quantumPeriodMs) {
+                    // now past this quantum: move to the one we are in, and take back the bytes the
+                    // skipped quantums would have carried (never below zero)
+                    const int64_t skipped = (now - m_quantumStartTimeMs) / m_quantumPeriodMs;
+                    m_quantumStartTimeMs += skipped * m_quantumPeriodMs;
+                    const int64_t adjust = m_bytesSendingPerQuantum * skipped;
+                    m_bytesSendingThisQuantum = adjust > m_bytesSendingThisQuantum ? 0 : m_bytesSendingThisQuantum - adjust;
+                }
+            } else {
+                // this quantum (and maybe more) is already full: carry the excess, defer this send to
+                // the end of the quantums it fills
+                const int64_t ahead = m_bytesSendingThisQuantum / m_bytesSendingPerQuantum;
+                const int64_t skip_ms = (ahead - 1) * m_quantumPeriodMs;
+                m_bytesSendingThisQuantum -= m_bytesSendingPerQuantum * ahead;
+                m_bytesSendingThisQuantum += (int64_t)size;
+                if (now < m_quantumStartTimeMs + m_quantumPeriodMs) offset = m_quantumStartTimeMs + m_quantumPeriodMs - now;
+                offset += skip_ms;
+                m_quantumStartTimeMs += skip_ms + m_quantumPeriodMs;
+            }
+        } else if (cfg.burst_count != 0) {
+            if (m_burstCount == 0) m_burstCount = cfg.burst_count;
+            m_burstCount -= 1;
+            if (m_burstCount == 0) offset = (int64_t)cfg.burst_delay;
+        }
+        return offset;
+    }
+
     cts_task CreateNewTask(uint8_t action, uint32_t maxTransfer)  // ctsIOPattern.cpp:550-743
     {
         const uint64_t remaining = state.GetRemainingTransfer();
@@ -547,6 +612,7 @@ struct cts_io_pattern {
         // (ctsIOPattern.cpp:580-587)
         if (action == CTS_TASK_SEND && Rio() && m_sendingRioBufferIds.empty()) return t;
         if (action == CTS_TASK_SEND) {
+            t.time_offset_ms = SendTimeOffset(size);
             t.io_action = CTS_TASK_SEND;
             t.buffer_type = CTS_BUFFER_STATIC;
             t.buffer_length = size;
@@ -1301,6 +1367,14 @@ int cts_io_pattern_complete_io(cts_io_pattern* p, const cts_task* t, uint32_t cu
 uint32_t cts_io_pattern_last_error(const cts_io_pattern* p) { return p ? p->m_lastError : CTS_STATUS_IO_RUNNING; }
 
 uint64_t cts_io_pattern_rio_buffer_id_count(const cts_io_pattern* p) { return p ? p->RioBufferIdCount() : 0; }
+
+int cts_pattern_clock_set(cts_clock_ms_fn fn, void* ctx)
+{
+    std::lock_guard<std::mutex> lk(g_clock.mu);
+    g_clock.fn = fn;
+    g_clock.ctx = fn != nullptr ? ctx : nullptr;
+    return CTS_OK;
+}
 
 int cts_rio_functions_set(cts_rio_register_buffer_fn register_fn, cts_rio_deregister_buffer_fn deregister_fn,
                           void* ctx)

@@ -42,6 +42,10 @@ class PatternConfig:
     batch_buffers: int = 0
     batch_bytes: int = 0
     registered_io: bool = False  # -io:rioiocp (WSA_FLAG_REGISTERED_IO): see rio_functions_set
+    tcp_bytes_per_second: int = 0  # send pacing (ctsIOPattern.cpp:593-655); 0 = no limit
+    tcp_bytes_per_second_period: int = 100  # ms per quantum
+    burst_count: int = 0  # -burstcount (0 = not set); only without a rate limit (:657-674)
+    burst_delay: int = 0  # -burstdelay, ms
 
     def to_c(self) -> A.CtsPatternConfig:
         c = A.CtsPatternConfig()
@@ -63,6 +67,10 @@ class PatternConfig:
         c.batch_buffers = self.batch_buffers
         c.batch_bytes = self.batch_bytes
         c.registered_io = int(bool(self.registered_io))
+        c.tcp_bytes_per_second = self.tcp_bytes_per_second
+        c.tcp_bytes_per_second_period = self.tcp_bytes_per_second_period
+        c.burst_count = self.burst_count
+        c.burst_delay = self.burst_delay
         return c
 
     @property
@@ -210,6 +218,24 @@ def rio_functions_set(register_fn, deregister_fn, ctx=None) -> None:
 
 
 _rio_keepalive = None
+
+
+def clock_set(now_ms) -> None:
+    """The millisecond clock send pacing reads (ctTimer::snap_qpc_as_msec; the reference's unit tests drive
+    ctTimer::g_unitTestQpcTimeMs). A Python callable returning ms, a C function pointer (int), or None for the
+    default monotonic clock."""
+    global _clock_keepalive
+    if now_ms is None:
+        check("cts_pattern_clock_set", lib().cts_pattern_clock_set(None, None))
+        _clock_keepalive = None
+        return
+    fn = now_ms if isinstance(now_ms, int) else A.CLOCK_MS(lambda _ctx: int(now_ms()))
+    _clock_keepalive = fn
+    ptr = fn if isinstance(fn, int) else ctypes.cast(fn, ctypes.c_void_p).value
+    check("cts_pattern_clock_set", lib().cts_pattern_clock_set(ptr, None))
+
+
+_clock_keepalive = None
 
 
 def status_details() -> dict:

@@ -40,6 +40,9 @@ typedef struct cts_loopback_config {
     uint32_t recv_whole;            /* 1 = data recvs complete with the whole posted length (MSG_WAITALL-like):
                                        deterministic completion sizes, so runs with different verifiers can be
                                        compared counter for counter; 0 = whatever arrived (partial completions) */
+    int64_t tcp_bytes_per_second;   /* -RateLimit per connection (0 = none): senders wait the tasks' time offsets */
+    uint32_t burst_count;           /* -BurstCount (0 = not set) */
+    uint32_t burst_delay;           /* -BurstDelay, ms */
 } cts_loopback_config;
 
 typedef enum cts_loopback_functor {

@@ -143,7 +143,17 @@ typedef struct cts_pattern_config {
     uint32_t registered_io;     /* SocketFlags & WSA_FLAG_REGISTERED_IO (-io:rioiocp): register buffers with
                                  * the RIO functions of cts_rio_functions_set, hand their ids out in tasks */
     uint32_t reserved0;
+    /* send pacing (ctsIOPattern.cpp:219-224, 593-674): sets ctsTask::m_timeOffsetMilliseconds of sends */
+    int64_t tcp_bytes_per_second;        /* ctsConfig::GetTcpBytesPerSecond() of this connection (0 = no limit) */
+    int64_t tcp_bytes_per_second_period; /* ->TcpBytesPerSecondPeriod, ms (0 = the reference default, 100) */
+    uint32_t burst_count;                /* ->BurstCount (0 = not set); used only without a rate limit */
+    uint32_t burst_delay;                /* ->BurstDelay, ms: the offset of every burst_count-th send */
 } cts_pattern_config;
+
+/* The millisecond clock send pacing reads (ctTimer::snap_qpc_as_msec). NULL restores the default, a
+ * monotonic clock. Process-wide, like the reference's unit-test hook ctTimer::g_unitTestQpcTimeMs. */
+typedef int64_t (*cts_clock_ms_fn)(void* ctx);
+int cts_pattern_clock_set(cts_clock_ms_fn fn, void* ctx);
 
 /* Per-connection statistics (ctsTcpStatistics, ctsStatistics.hpp:316-373) and
  * the verify bookkeeping of this pattern. */

@@ -1295,3 +1295,131 @@ def test_rio_without_functions_or_failing_register(rio_fake):
     t = p.InitiateIo()
     assert t.rio_buffer_id == A.RIO_INVALID_BUFFERID
     p.close()
+
+
+# ---- send pacing: ctsTask::m_timeOffsetMilliseconds (ctsIOPattern.cpp:219-224, 593-674) ------------------------
+# No MSTest drives the pattern's pacing (ctsIOPatternRateLimitPolicyUnitTest tests a policy class the product does
+# not include), so these tests pin the C++ against a line-by-line Python restatement of CreateNewTask's branch and
+# hand-worked cases: parity with the reference's source, not with a reference fixture.
+class _Pacer:
+    """CreateNewTask's send-time offset (ctsIOPattern.cpp:593-674), restated."""
+
+    def __init__(self, bps, period, burst_count, burst_delay, start_ms):
+        self.period = period
+        self.per = bps * period // 1000
+        self.this = 0
+        self.start = start_ms
+        self.burst_count, self.burst_delay, self.burst = burst_count, burst_delay, burst_count
+
+    def offset(self, now, size):
+        off = 0
+        if self.per > 0:
+            if self.this < self.per:
+                self.this += size
+                if now > self.start + self.period:
+                    skipped = (now - self.start) // self.period
+                    self.start += skipped * self.period
+                    adjust = self.per * skipped
+                    self.this = 0 if adjust > self.this else self.this - adjust
+            else:
+                ahead = self.this // self.per
+                skip = (ahead - 1) * self.period
+                self.this -= self.per * ahead
+                self.this += size
+                if now < self.start + self.period:
+                    off = self.start + self.period - now
+                off += skip
+                self.start += skip + self.period
+        elif self.burst_count:
+            if self.burst == 0:
+                self.burst = self.burst_count
+            self.burst -= 1
+            if self.burst == 0:
+                off = self.burst_delay
+        return off
+
+
+class _FakeClock:
+    def __init__(self, t):
+        self.t = t
+
+    def __call__(self):
+        return self.t
+
+
+def _paced_client(clock, **kw):
+    from ctstraffic_amd.pattern import clock_set
+
+    clock_set(clock)
+    shared_buffer_attach(_SENDER)
+    cfg = PatternConfig(**client_defaults(**kw))
+    p = IoPattern.MakeIoPattern(cfg, None, verifier=_oracle_verifier)
+    t = p.InitiateIo()  # the connection id
+    assert t.io_action == Recv and t.time_offset_ms == 0
+    assert p.CompleteIo(t, ConnectionIdLength, 0) == ContinueIo
+    return p
+
+
+def test_send_pacing_one_buffer_per_quantum():
+    """10 x 64 KiB per second in 100 ms quanta is one buffer per quantum: with the clock standing still the
+    sends are scheduled 0, 100, 200, ... ms ahead; once the clock reaches a send's slot it goes out at once."""
+    from ctstraffic_amd.pattern import clock_set
+
+    clock = _FakeClock(5000)
+    try:
+        p = _paced_client(clock, pre_post_sends=64, buffer_size=65536, transfer_size=1 << 30,
+                          tcp_bytes_per_second=655360, tcp_bytes_per_second_period=100)
+        offs = [p.InitiateIo().time_offset_ms for _ in range(5)]
+        assert offs == [0, 100, 200, 300, 400]
+        clock.t += 450  # the clock passes the five scheduled quanta
+        assert p.InitiateIo().time_offset_ms == 50
+        p.close()
+    finally:
+        clock_set(None)
+
+
+def test_send_burst_delay():
+    """-burstcount:3 -burstdelay:50 without a rate limit: every third send waits 50 ms (:657-674); recvs never."""
+    from ctstraffic_amd.pattern import clock_set
+
+    try:
+        p = _paced_client(None, pre_post_sends=64, transfer_size=1 << 30, burst_count=3, burst_delay=50)
+        ts = [p.InitiateIo() for _ in range(9)]
+        assert [t.io_action for t in ts] == [Send] * 9
+        assert [t.time_offset_ms for t in ts] == [0, 0, 50] * 3
+        p.close()
+        # a rate limit takes precedence over the burst settings
+        p = _paced_client(_FakeClock(0), pre_post_sends=64, transfer_size=1 << 30, burst_count=1, burst_delay=7,
+                          tcp_bytes_per_second=10 ** 9)
+        assert [p.InitiateIo().time_offset_ms for _ in range(4)] == [0, 0, 0, 0]
+        p.close()
+    finally:
+        clock_set(None)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_send_pacing_matches_restatement(seed):
+    """Random rates, quanta, buffer sizes ([lo, hi] draws) and clock steps (standing, within a quantum, skipping
+    several): every send's time offset equals the restated CreateNewTask branch, including carried-over bytes
+    and quantums skipped forward."""
+    from ctstraffic_amd.pattern import clock_set
+
+    rng = np.random.default_rng(seed)
+    bps = int(rng.choice([1, 100_000, 655_360, 3_000_000, 50_000_000]))
+    period = int(rng.choice([1, 10, 100, 250]))
+    lo = int(rng.integers(1000, 30000))
+    clock = _FakeClock(int(rng.integers(0, 10 ** 6)))
+    try:
+        p = _paced_client(clock, pre_post_sends=1 << 20, transfer_size=1 << 40, buffer_size=lo,
+                          buffer_size_high=lo + int(rng.integers(0, 60000)), random_seed=seed,
+                          tcp_bytes_per_second=bps, tcp_bytes_per_second_period=period)
+        model = _Pacer(bps, period, 0, 0, clock.t)
+        for _ in range(400):
+            step = int(rng.choice([0, 0, 1, period // 2, period, 3 * period + 1, 17]))
+            clock.t += step
+            t = p.InitiateIo()
+            assert t.io_action == Send
+            assert t.time_offset_ms == model.offset(clock.t, t.buffer_length), (bps, period, clock.t)
+        p.close()
+    finally:
+        clock_set(None)

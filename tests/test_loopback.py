@@ -233,3 +233,19 @@ def test_config1_three_arrangements_gpu(engine, corrupt):
         srv = sides[8 + corrupt]
         assert srv["fail_completion"] == 9000 and srv["buffers_verified"] == 9001
         assert srv["bytes_recv"] == 9001 * 65536 and srv["queued"] == 0
+
+
+def test_loopback_send_pacing_cpu():
+    """Send pacing end to end: the feeder's senders wait each task's time offset (ctsSendRecvIocp.cpp:378-383).
+    4 Push connections x 40 x 8 KiB at 1 MiB/s each (100 ms quanta of 104 857 B, 13 buffers) are deferred into
+    their third quantum, so the run takes at least 200 ms; -burstcount:4 -burstdelay:30 with 16 sends per
+    connection waits 4 x 30 ms. Data and counters stay exact."""
+    shared_buffer_attach(_SENDER)
+    hook = A.BATCH_VERIFIER(oracle.batch_verifier_address())
+    for kw, n_bufs, floor in [(dict(tcp_bytes_per_second=1 << 20), 40, 0.2),
+                              (dict(burst_count=4, burst_delay=30), 16, 0.12)]:
+        r = loopback.run(connections=4, buffer_size=8192, transfer_size=n_bufs * 8192, verifier=hook,
+                         verify_mode=A.VERIFY_SYNC, functor=loopback.FUNCTOR_SYNC, recv_whole=True, **kw)
+        assert r["connections_ok"] == 4 and r["data_errors"] == 0
+        assert r["bytes_recv"] == 4 * (n_bufs * 8192 + 37 + 4)
+        assert r["seconds"] >= floor, (kw, r["seconds"])
