@@ -57,9 +57,10 @@ def parse():
                         "counters folded on the host by cts_counters_read_multi (0 = off)")
     p.add_argument("--graph", action="store_true", help="replay the timed steps from a HIP graph (measured: no gain; "
                    "implies --pipeline-streams 1)")
-    p.add_argument("--pipeline-streams", type=int, default=3,
+    p.add_argument("--pipeline-streams", type=int, default=2,
                    help="headline leg: launches round-robin over S engine streams, so one batch's tail overlaps the "
-                        "next batch's ramp-up (1 = serialized launches; tools/overlap_probe.py)")
+                        "next batch's ramp-up (1 = serialized launches; 2 measured best at the driver's 20 steps: "
+                        "profiles/r02/pipeline_streams/)")
     p.add_argument("--verify-variant", type=int, default=-1,
                    help="CTS_ATTR_VERIFY_VARIANT for both legs (-1 = engine default; tuning builds only)")
     return p.parse_args()
