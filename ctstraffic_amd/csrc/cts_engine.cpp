@@ -39,7 +39,14 @@ struct cts_engine {
     void* batch_res = nullptr;
     size_t batch_res_cap = 0;
     void* batch_ctr = nullptr;
-    int sync_mailbox = 1;  // CTS_ATTR_SYNC_MAILBOX (read by cts_pattern's SYNC verify)
+    int sync_mailbox = 1;  // CTS_ATTR_SYNC_MAILBOX (read by cts_pattern's SYNC verify and cts_verify_host)
+    // cts_verify_host through the mailbox: pinned, device-mapped staging buffers, one per concurrent caller
+    struct HostStage {
+        void* p = nullptr;
+        size_t cap = 0;
+    };
+    std::mutex stage_pool_mu;
+    std::vector<HostStage> stage_pool;  // idle stages
     std::unique_ptr<Mailbox> mail;  // cts_verify_mapped's resident grid, started on first use
     std::mutex mail_init_mu;
 };
@@ -423,6 +430,8 @@ int cts_engine_destroy(cts_engine* e)
 {
     if (e == nullptr) return CTS_E_INVALID;
     e->mail.reset();  // stops the resident grid (kMailStop) and joins its watchdog
+    for (auto& st : e->stage_pool) (void)hipHostFree(st.p);
+    e->stage_pool.clear();
     {
         DeviceGuard g(e->device);
         if (e->stream) {
@@ -678,6 +687,30 @@ int cts_verify_host(cts_engine* e, const void* host_buf, uint32_t len, uint32_t 
 {
     if (e == nullptr || out == nullptr || (host_buf == nullptr && len != 0)) return CTS_E_INVALID;
     if (expected_offset >= CTS_PATTERN_PERIOD) return CTS_E_INVALID;
+    if (e->sync_mailbox) {
+        // copy into a staging buffer of this call's own (concurrent callers do not wait for each other) and
+        // post it to the resident mailbox grid: no launch or stream synchronize per call
+        cts_engine::HostStage st;
+        {
+            std::lock_guard<std::mutex> lk(e->stage_pool_mu);
+            if (!e->stage_pool.empty()) {
+                st = e->stage_pool.back();
+                e->stage_pool.pop_back();
+            }
+        }
+        int rc = ensure_pinned(&st.p, &st.cap, (size_t)len + 16, 64u << 10);
+        const uint8_t* dev = rc == CTS_OK ? device_view(static_cast<uint8_t*>(st.p)) : nullptr;
+        if (rc == CTS_OK && dev == nullptr) rc = CTS_E_HIP;
+        if (rc == CTS_OK) {
+            if (len) std::memcpy(st.p, host_buf, len);
+            rc = cts_verify_mapped(e, dev, len, expected_offset, out);
+        }
+        if (st.p != nullptr) {
+            std::lock_guard<std::mutex> lk(e->stage_pool_mu);
+            e->stage_pool.push_back(st);
+        }
+        return rc;
+    }
     std::lock_guard<std::mutex> lk(e->host_mu);
     DeviceGuard g(e->device);
     if (!g.ok) return CTS_E_HIP;

@@ -135,9 +135,9 @@ typedef enum cts_engine_attr {
     CTS_ATTR_MS_VARIANT = 8,          /* MediaStream receive kernel (cts_media_stream_verify) */
     CTS_ATTR_SMALL_CHUNK = 9,         /* chunked small-buffer walk: buffers per chunk (0 = contiguous) */
     CTS_ATTR_FILL_NT = 10,            /* cts_fill stores: 0 plain, 1 nontemporal, 2 by path (default) */
-    CTS_ATTR_SYNC_MAILBOX = 11        /* 1 (default) = SYNC-mode pattern verifies of pinned recv buffers go
-                                       * through cts_verify_mapped (the resident mailbox grid); 0 = one
-                                       * sliced launch + synchronize per completion */
+    CTS_ATTR_SYNC_MAILBOX = 11        /* 1 (default) = SYNC-mode pattern verifies of pinned recv buffers and
+                                       * cts_verify_host go through cts_verify_mapped (the resident mailbox
+                                       * grid); 0 = one sliced launch + synchronize per call */
 } cts_engine_attr;
 int cts_engine_set_attr(cts_engine* engine, int attr, int value);
 /* A non-blocking HIP stream on the engine's device, whatever device the calling
@@ -196,10 +196,13 @@ int cts_counters_read_multi(cts_engine* const* engines, const void* const* dev_c
                             uint32_t n, cts_counters* out);
 
 /* ---- host-buffer drop-in for ctsIoPattern::VerifyBuffer ---------------------- */
-/* Verifies `len` bytes at host_buf + skip_head against the pattern starting at
- * expected_offset: stages the bytes into pinned memory, runs the verify kernel
- * on the engine's internal stream and waits. Returns the record in *out
- * (RtlCompareMemory semantics, ctsIOPattern.cpp:753-774). Thread-safe. */
+/* Verifies `len` bytes at host_buf against the pattern starting at
+ * expected_offset and waits. Returns the record in *out (RtlCompareMemory
+ * semantics, ctsIOPattern.cpp:753-774). Thread-safe. With CTS_ATTR_SYNC_MAILBOX
+ * (the default) the bytes are copied into a pinned staging buffer of the
+ * call's own and posted to the resident mailbox grid (cts_verify_mapped), so
+ * concurrent callers run side by side; with it off, they are staged into one
+ * shared buffer and verified by a launch + synchronize on the engine's stream. */
 int cts_verify_host(cts_engine* engine, const void* host_buf, uint32_t len,
                     uint32_t expected_offset, cts_verify_result* out);
 

@@ -352,7 +352,19 @@ def test_config5_full_shard(engine):
 
 
 # ---- host-buffer paths ------------------------------------------------------------------------------
-def test_verify_host_single(engine):
+@pytest.fixture(params=[1, 0], ids=["mailbox", "launch"])
+def host_path(engine, request):
+    """cts_verify_host through the mailbox grid (CTS_ATTR_SYNC_MAILBOX = 1, the default) or one sliced launch +
+    synchronize per call (0)."""
+    from ctstraffic_amd import _lib
+
+    engine.set_attr(_lib.ATTR_SYNC_MAILBOX, request.param)
+    yield engine
+    engine.set_attr(_lib.ATTR_SYNC_MAILBOX, 1)
+
+
+def test_verify_host_single(host_path):
+    engine = host_path
     S = oracle.sender_buffer(70000)
     for e, n in [(0, 10), (0, 0), (4, 6), (65535, 100), (123, 65536), (1, 70000 - 1)]:
         buf = S[e:e + n].copy()
@@ -369,9 +381,11 @@ def test_verify_host_single(engine):
     assert not r["pass"] and r["first_mismatch"] == 2
 
 
-def test_verify_host_single_slice_edges(engine):
-    """cts_verify_host reads one buffer as up to 64 slices (csrc/cts_slices.hpp); corruptions on slice
-    edges, in two slices at once, and ragged last slices fold back to the oracle's whole-buffer result."""
+def test_verify_host_single_slice_edges(host_path):
+    """cts_verify_host reads one buffer as up to 64 slices (csrc/cts_slices.hpp) or as the mailbox's 4 KiB
+    pieces; corruptions on slice edges, in two slices at once, and ragged last slices fold back to the oracle's
+    whole-buffer result."""
+    engine = host_path
     S = oracle.sender_buffer(140000)
     rng = np.random.default_rng(0x51CE)
     for n in (1023, 1024, 1025, 4097, 65536, 65537, 100000, 131072):
@@ -387,6 +401,40 @@ def test_verify_host_single_slice_edges(engine):
             o = oracle.verify_buffer(buf, 0, e, n)
             assert (r["pass"], r["first_mismatch"], r["expected"], r["actual"], r["mismatch_bytes"]) == (
                 o["pass"], o["first_mismatch"], o["expected"], o["actual"], o["mismatch_bytes"]), (n, trial)
+
+
+def test_verify_host_threads(engine):
+    """cts_verify_host from 8 threads at once (a Level-1 VerifyBuffer drop-in called by concurrent IOCP threads):
+    each call stages into a pinned buffer of its own and posts to the mailbox; every answer is the oracle's."""
+    import threading
+
+    S = oracle.sender_buffer(140000)
+    errors = []
+
+    def worker(t):
+        rng = np.random.default_rng(0x4057 + t)
+        try:
+            for it in range(40):
+                n = int(rng.choice([0, 1, 17, 4096, 65536, 70001]))
+                e = int(rng.integers(0, 65536))
+                buf = S[e:e + n].copy()
+                if n and rng.random() < 0.5:
+                    buf[int(rng.integers(0, n))] ^= int(rng.integers(1, 256))
+                r = engine.verify_host(buf, e)
+                o = oracle.verify_buffer(buf, 0, e, n)
+                got = (r["pass"], r["first_mismatch"], r["expected"], r["actual"], r["mismatch_bytes"])
+                want = (o["pass"], o["first_mismatch"], o["expected"], o["actual"], o["mismatch_bytes"])
+                if got != want:
+                    errors.append((t, it, n, e, got, want))
+        except Exception as ex:  # surfaced below
+            errors.append((t, repr(ex)))
+
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    assert not errors, errors[:5]
 
 
 def test_verify_mapped_mailbox_threads(engine):

@@ -6,7 +6,7 @@
 // buffer, descriptor and result (T connections completing concurrently). Wait = hipStreamSynchronize
 // or a hipStreamQuery spin, or cts_verify_mapped (posted to the engine's resident mailbox grid: no launch per
 // verify). Prints one JSON line per variant: us per verify (per thread).
-//   build: make tools/sync_probe      run: tools/sync_probe [iters [mailbox]]
+//   build: make tools/sync_probe      run: tools/sync_probe [iters [mailbox]]  (mailbox: waits 2-4 only)
 #include <hip/hip_runtime_api.h>
 
 #include <atomic>
@@ -19,7 +19,8 @@
 
 #include "cts_engine.h"
 
-static int run_thread(cts_engine* e, uint32_t slices, bool spin, bool mapped, int iters, double* us_out, int* bad)
+static int run_thread(cts_engine* e, uint32_t slices, bool spin, bool mapped, int iters, double* us_out, int* bad,
+                      bool host_copy = false)
 {
     void* stream = nullptr;
     if (cts_engine_stream_create(e, &stream) != CTS_OK) return 1;
@@ -34,7 +35,13 @@ static int run_thread(cts_engine* e, uint32_t slices, bool spin, bool mapped, in
     auto* res_h = reinterpret_cast<cts_verify_result*>(static_cast<uint8_t*>(hd) + 2048);
     auto* res_d = reinterpret_cast<cts_verify_result*>(static_cast<uint8_t*>(dd) + 2048);
     hipStream_t s = static_cast<hipStream_t>(stream);
+    std::vector<uint8_t> pageable;
+    if (host_copy) pageable.assign(static_cast<uint8_t*>(host), static_cast<uint8_t*>(host) + len);
     auto once = [&]() {
+        if (host_copy) {  // cts_verify_host: a pageable buffer (the Level-1 VerifyBuffer drop-in)
+            cts_verify_result r{};
+            return cts_verify_host(e, pageable.data(), len, 1000, &r) == CTS_OK && r.pass && r.first_mismatch == len;
+        }
         if (mapped) {  // cts_verify_mapped: the mailbox grid
             cts_verify_result r{};
             return cts_verify_mapped(e, dev, len, 1000, &r) == CTS_OK && r.pass && r.first_mismatch == len;
@@ -72,16 +79,18 @@ int main(int argc, char** argv)
     cts_engine* e = nullptr;
     if (cts_engine_create(0, &e) != CTS_OK) return 1;
     // wait: 0 stream_sync, 1 query_spin, 2 cts_verify_mapped (mailbox; slices = its 4 KiB pieces, reported as 64)
-    for (int spin = mailbox_only ? 2 : 0; spin < 3; ++spin)
+    // wait 3/4: cts_verify_host (copy of a pageable buffer) through the mailbox / through a launch + sync
+    for (int spin = mailbox_only ? 2 : 0; spin < 5; ++spin)
         for (uint32_t threads : {1u, 8u, 16u})
             for (uint32_t slices : {1u, 2u, 4u, 8u, 16u, 32u, 64u}) {
-                if ((spin == 2) != (slices == 64) && spin == 2) continue;
+                if (spin >= 2 && slices != 64) continue;
                 if (threads == 16 && slices != 64) continue;
                 std::vector<double> us(threads, 0.0);
                 std::vector<int> bad(threads, 0), rc(threads, 0);
                 std::vector<std::thread> th;
+                if (spin >= 3) (void)cts_engine_set_attr(e, CTS_ATTR_SYNC_MAILBOX, spin == 3 ? 1 : 0);
                 for (uint32_t t = 0; t < threads; ++t)
-                    th.emplace_back([&, t] { rc[t] = run_thread(e, slices, spin == 1, spin == 2, iters, &us[t], &bad[t]); });
+                    th.emplace_back([&, t] { rc[t] = run_thread(e, slices, spin == 1, spin == 2, iters, &us[t], &bad[t], spin >= 3); });
                 for (auto& x : th) x.join();
                 double mean = 0;
                 int nbad = 0, nrc = 0;
@@ -92,7 +101,8 @@ int main(int argc, char** argv)
                 }
                 std::printf("{\"wait\": \"%s\", \"threads\": %u, \"slices\": %u, \"us_per_verify\": %.2f, "
                             "\"GBps_total\": %.2f, \"bad\": %d, \"rc\": %d}\n",
-                            spin == 2 ? "mailbox" : spin ? "query_spin" : "stream_sync", threads, slices, mean,
+                            spin == 4 ? "host_launch" : spin == 3 ? "host_mailbox" : spin == 2 ? "mailbox" : spin ? "query_spin" : "stream_sync",
+                            threads, slices, mean,
                             threads * 65536.0 / (mean * 1e3), nbad, nrc);
                 std::fflush(stdout);
             }
