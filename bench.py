@@ -528,6 +528,15 @@ def run_extras(engine, torch, W, w, arenas, descs, dev, want):
             out["datagram_config"] = "config3: 16M x 1472 B (26 B header skipped; payload bytes counted)"
             ok = engine.read_counters(ctr)["buffers_failed"] == 11 * len(np.unique(wd.corrupt_buf))
             out["datagram_parity"] = bool(ok)
+            # the same verify over the ring's descriptor-free form (datagram i at i * 1472, lengths only:
+            # 4 bytes of metadata per datagram instead of a 24-byte descriptor)
+            lens = torch.from_numpy(wd.descs["length"].astype(np.uint32)).to(dev)
+            ctr_s = engine.new_counters()
+            t = _time_kernel(torch, lambda i: engine.verify_strided(ad, wd.max_length, lens, skip_head=26,
+                                                                    expected_offset=0, counters=ctr_s), 10)
+            out["datagram_1472_verify_strided_GiBps"] = round(wd.verified_bytes() / t / GIB, 1)
+            out["datagram_strided_parity"] = bool(
+                engine.read_counters(ctr_s)["buffers_failed"] == 11 * len(np.unique(wd.corrupt_buf)))
             # the MediaStream client path: header parse + validate + payload verify + 32-byte record
             recs = torch.empty(wd.n * 32, dtype=torch.uint8, device=dev)
             res = engine.new_results(wd.n)
@@ -535,7 +544,6 @@ def run_extras(engine, torch, W, w, arenas, descs, dev, want):
             out["media_stream_verify_GiBps"] = round(wd.verified_bytes() / t / GIB, 1)
             out["media_stream_verify_Mdgram_per_s"] = round(wd.n / t / 1e6, 1)
             # the same receive pass over the ring's descriptor-free form (datagram i at i * 1472, lengths only)
-            lens = torch.from_numpy(wd.descs["length"].astype(np.uint32)).to(dev)
             t = _time_kernel(torch, lambda i: MS.verify_strided(engine, ad, wd.max_length, lens, records=recs,
                                                                 results=res), 10)
             out["media_stream_strided_verify_GiBps"] = round(wd.verified_bytes() / t / GIB, 1)

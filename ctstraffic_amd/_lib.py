@@ -127,6 +127,7 @@ def _declare(L: ctypes.CDLL) -> None:
         "cts_sender_buffer_fill": ([P, P, u32, P], i32),
         "cts_fill": ([P, P, u64, P, u32, u32, P], i32),
         "cts_verify": ([P, P, u64, P, u32, u32, P, P, P, u32, P], i32),
+        "cts_verify_strided": ([P, P, u64, u32, P, u32, u32, u32, u32, P, P, P, u32, P], i32),
         "cts_counters_device_bytes": ([], ctypes.c_size_t),
         "cts_counters_reset": ([P, P, P], i32),
         "cts_counters_read": ([P, P, ctypes.POINTER(CtsCounters), P], i32),

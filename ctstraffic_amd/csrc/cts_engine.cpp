@@ -571,6 +571,26 @@ int cts_verify(cts_engine* e, const void* dev_arena, uint64_t arena_bytes, const
                                          dev_conn_first_fail, n_conns, static_cast<hipStream_t>(stream), e->geo));
 }
 
+int cts_verify_strided(cts_engine* e, const void* dev_arena, uint64_t arena_bytes, uint32_t stride,
+                       const uint32_t* dev_lengths, uint32_t n, uint32_t skip_head, uint32_t expected_offset,
+                       uint32_t conn_index, cts_verify_result* dev_results, void* dev_counters,
+                       uint32_t* dev_conn_first_fail, uint32_t n_conns, void* stream)
+{
+    if (e == nullptr) return CTS_E_INVALID;
+    if (n == 0) return CTS_OK;
+    if (dev_arena == nullptr || dev_lengths == nullptr || stride == 0 || arena_bytes < 16 ||
+        ((uintptr_t)dev_arena & 15u) != 0 || ((uintptr_t)dev_lengths & 3u) != 0)
+        return CTS_E_INVALID;
+    if (expected_offset >= CTS_PATTERN_PERIOD) return CTS_E_INVALID;
+    if (dev_conn_first_fail == nullptr && n_conns != 0) return CTS_E_INVALID;
+    DeviceGuard g(e->device);
+    if (!g.ok) return CTS_E_HIP;
+    return hip_status(cts::launch_verify_strided(static_cast<const uint8_t*>(dev_arena), arena_bytes, stride, dev_lengths, n,
+                                                 skip_head, expected_offset, conn_index, dev_results,
+                                                 static_cast<uint64_t*>(dev_counters), dev_conn_first_fail, n_conns,
+                                                 static_cast<hipStream_t>(stream), e->geo));
+}
+
 int cts_media_stream_fill(cts_engine* e, void* dev_arena, uint64_t arena_bytes, const cts_buf_desc* dev_descs,
                           const cts_datagram_header* dev_headers, uint32_t n, void* stream)
 {

@@ -123,6 +123,11 @@ hipError_t launch_verify(const uint8_t* arena, uint64_t arena_bytes, const cts_b
                          uint32_t* conn_first_fail, uint32_t n_conns, hipStream_t stream,
                          const LaunchGeometry& geo);
 
+hipError_t launch_verify_strided(const uint8_t* arena, uint64_t arena_bytes, uint32_t stride, const uint32_t* lens,
+                                 uint32_t n, uint32_t skip_head, uint32_t expected, uint32_t conn_index,
+                                 cts_verify_result* results, uint64_t* counters, uint32_t* conn_first_fail,
+                                 uint32_t n_conns, hipStream_t stream, const LaunchGeometry& geo);
+
 hipError_t launch_fill(uint8_t* arena, uint64_t arena_bytes, const cts_buf_desc* descs, uint32_t n,
                        uint32_t max_length_hint, hipStream_t stream, const LaunchGeometry& geo);
 

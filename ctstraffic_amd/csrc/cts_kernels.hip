@@ -1087,10 +1087,34 @@ struct QuadWalk {
     }
 };
 
-template <int U, bool NT, bool ALIGN, bool CONTIG = false>
+// Where the buffers of a quad-team walk come from: a descriptor array, or (STRIDED) a uniformly strided
+// receive ring -- buffer i at i * stride, completed length lens[i], one skip / expected offset /
+// connection for the whole ring (a UDP socket's datagrams: skip 26, expected 0), read as 4 bytes of
+// metadata per buffer instead of a 24-byte descriptor.
+struct VSource {
+    const cts_buf_desc* descs;  // !STRIDED
+    const uint32_t* lens;       // STRIDED
+    uint32_t stride, skip_head, expected, conn_index;
+};
+
+template <bool STRIDED>
+__device__ __forceinline__ cts_buf_desc vs_desc(const VSource& src, uint32_t i)
+{
+    if constexpr (STRIDED) {
+        const uint32_t len = src.lens[i];
+        // a completion longer than its slot would overlap the next one: flagged (an out-of-range
+        // expected offset makes desc_bad reject it) rather than read
+        return cts_buf_desc{(uint64_t)i * src.stride, len, len <= src.stride ? src.expected : 65536u, src.conn_index,
+                            src.skip_head};
+    } else {
+        return src.descs[i];
+    }
+}
+
+template <int U, bool NT, bool ALIGN, bool CONTIG = false, bool STRIDED = false>
 __global__ void __launch_bounds__(kBlock)
-    verify_quad_kernel(const uint8_t* __restrict__ arena, uint64_t arena_bytes, const cts_buf_desc* __restrict__ descs,
-                       uint32_t n, cts_verify_result* __restrict__ results, uint64_t* __restrict__ counters,
+    verify_quad_kernel(const uint8_t* __restrict__ arena, uint64_t arena_bytes, VSource src, uint32_t n,
+                       cts_verify_result* __restrict__ results, uint64_t* __restrict__ counters,
                        uint32_t* __restrict__ conn_first_fail, uint32_t n_conns, uint32_t per = 0)
 {
     constexpr int TEAMS = kBlock / kQuadTeam;
@@ -1098,17 +1122,18 @@ __global__ void __launch_bounds__(kBlock)
     __shared__ QuadOut qout[kBlock / 64];
     const uint32_t lane = threadIdx.x & (kQuadTeam - 1);
     const uint32_t team = threadIdx.x / kQuadTeam;
-    // the descriptor array holds >= 24 bytes: its first 16-byte-aligned chunk is the
-    // dummy target of an empty span's clamped loads
-    const void* dummy = reinterpret_cast<const void*>(((uintptr_t)descs + 15u) & ~(uintptr_t)15u);
+    // the dummy target of an empty span's clamped loads: the descriptor array (>= 24 bytes) or, for a
+    // strided ring, the arena (>= 16 bytes, 16-aligned), rounded up to 16 bytes
+    const void* dummy = STRIDED ? static_cast<const void*>(arena)
+                                : reinterpret_cast<const void*>(((uintptr_t)src.descs + 15u) & ~(uintptr_t)15u);
     QCounters qc;
     QuadWalk<CONTIG, TEAMS> w(n, per, team);
-    cts_buf_desc dn = descs[w.i < n ? w.i : n - 1u];  // n >= 1 (launch_verify returns early on 0)
+    cts_buf_desc dn = vs_desc<STRIDED>(src, w.i < n ? w.i : n - 1u);  // n >= 1 (launch_verify returns early on 0)
     while (__any(w.i < w.end)) {
         const uint32_t i = w.i;
         const cts_buf_desc d = dn;
         const uint32_t inext = w.next();
-        dn = descs[inext < n ? inext : n - 1u];  // clamped: no load under a branch
+        dn = vs_desc<STRIDED>(src, inext < n ? inext : n - 1u);  // clamped: no load under a branch
         const bool live = i < w.end;
         const bool ok = live && !desc_bad(d, arena_bytes);
         const QSpan q = quad_span<ALIGN>(arena + d.byte_offset + d.skip_head, ok ? d.length - d.skip_head : 0u,
@@ -1745,6 +1770,7 @@ static inline uint32_t grid_win(uint32_t n, uint32_t win, const LaunchGeometry& 
 #endif
 
 #define CTS_VERIFY_ARGS arena, arena_bytes, descs, n, results, counters, conn_first_fail, n_conns
+#define CTS_QUAD_ARGS arena, arena_bytes, VSource{descs, nullptr, 0u, 0u, 0u, 0u}, n, results, counters, conn_first_fail, n_conns
 
 // Chunked launch of a four-buffers-per-wave kernel (QuadWalk<true>): chunk = geo.small_chunk
 // buffers (rounded up to the block's 16 teams); 0 = one block-contiguous range per block, every
@@ -1780,13 +1806,13 @@ static void launch_verify_nt(const uint8_t* arena, uint64_t arena_bytes, const c
         const uint32_t grid = grid_for(n, kBlock / 64, geo);
         const uint32_t qgrid = grid_for(n, kBlock / kQuadTeam, geo);
         switch (geo.small_variant) {
-        case 5: verify_quad_kernel<6, NT, false><<<qgrid, kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
-        case 6: verify_quad_kernel<7, NT, true><<<qgrid, kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
-        case 7: verify_quad_kernel<6, NT, true><<<qgrid, kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
-        case 8: verify_quad_kernel<4, NT, false><<<qgrid, kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
+        case 5: verify_quad_kernel<6, NT, false><<<qgrid, kBlock, 0, stream>>>(CTS_QUAD_ARGS); break;
+        case 6: verify_quad_kernel<7, NT, true><<<qgrid, kBlock, 0, stream>>>(CTS_QUAD_ARGS); break;
+        case 7: verify_quad_kernel<6, NT, true><<<qgrid, kBlock, 0, stream>>>(CTS_QUAD_ARGS); break;
+        case 8: verify_quad_kernel<4, NT, false><<<qgrid, kBlock, 0, stream>>>(CTS_QUAD_ARGS); break;
         case 9: {
             const ContigGrid cg = contig_grid(n, geo);
-            verify_quad_kernel<6, NT, true, true><<<cg.grid, kBlock, 0, stream>>>(CTS_VERIFY_ARGS, cg.per);
+            verify_quad_kernel<6, NT, true, true><<<cg.grid, kBlock, 0, stream>>>(CTS_QUAD_ARGS, cg.per);
             break;
         }
         case 1: verify_wave_kernel<1, NT><<<grid, kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
@@ -1797,7 +1823,7 @@ static void launch_verify_nt(const uint8_t* arena, uint64_t arena_bytes, const c
         }
 #else
         const ContigGrid cg = contig_grid(n, geo);  // small variant 9 (kDefaultSmallVariant)
-        verify_quad_kernel<6, NT, true, true><<<cg.grid, kBlock, 0, stream>>>(CTS_VERIFY_ARGS, cg.per);
+        verify_quad_kernel<6, NT, true, true><<<cg.grid, kBlock, 0, stream>>>(CTS_QUAD_ARGS, cg.per);
 #endif
     } else {
         // variant (large path): 0 = workgroup/buffer U8, 1 = U4, 2 = U16, 3 = wave/buffer U8,
@@ -2044,6 +2070,24 @@ hipError_t launch_verify(const uint8_t* arena, uint64_t arena_bytes, const cts_b
         launch_verify_nt<false>(arena, arena_bytes, descs, n, small, results, counters, conn_first_fail, n_conns,
                                 stream, geo);
     }
+    return hipGetLastError();
+}
+
+// cts_verify_strided: the small-buffer walk (variant 9's kernel) over a uniformly strided ring
+hipError_t launch_verify_strided(const uint8_t* arena, uint64_t arena_bytes, uint32_t stride, const uint32_t* lens,
+                                 uint32_t n, uint32_t skip_head, uint32_t expected, uint32_t conn_index,
+                                 cts_verify_result* results, uint64_t* counters, uint32_t* conn_first_fail,
+                                 uint32_t n_conns, hipStream_t stream, const LaunchGeometry& geo)
+{
+    if (n == 0) return hipSuccess;
+    const VSource src{nullptr, lens, stride, skip_head, expected, conn_index};
+    const ContigGrid cg = contig_grid(n, geo);
+    if (geo.nontemporal)
+        verify_quad_kernel<6, true, true, true, true><<<cg.grid, kBlock, 0, stream>>>(
+            arena, arena_bytes, src, n, results, counters, conn_first_fail, n_conns, cg.per);
+    else
+        verify_quad_kernel<6, false, true, true, true><<<cg.grid, kBlock, 0, stream>>>(
+            arena, arena_bytes, src, n, results, counters, conn_first_fail, n_conns, cg.per);
     return hipGetLastError();
 }
 

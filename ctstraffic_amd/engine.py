@@ -172,6 +172,18 @@ class Engine:
                                              _ptr(results), _ptr(counters), _ptr(conn_first_fail), n_conns,
                                              _stream(stream)))
 
+    def verify_strided(self, arena, stride: int, lengths, *, skip_head: int = 0, expected_offset: int = 0,
+                       conn_index: int = 0, results=None, counters=None, conn_first_fail=None, stream=None) -> None:
+        """cts_verify_strided: buffer i at arena + i * stride, lengths (uint32 device tensor) its completed bytes,
+        one skip / expected offset / connection for the whole ring."""
+        n = _nbytes(lengths) // 4
+        n_conns = 0 if conn_first_fail is None else _nbytes(conn_first_fail) // 4
+        _check_outputs(n, results, counters)
+        check("cts_verify_strided", self._L.cts_verify_strided(self._h, _ptr(arena), _nbytes(arena), stride,
+                                                             _ptr(lengths), n, skip_head, expected_offset, conn_index,
+                                                             _ptr(results), _ptr(counters), _ptr(conn_first_fail),
+                                                             n_conns, _stream(stream)))
+
     def new_results(self, n: int):
         return torch.zeros(n * RESULT_DTYPE.itemsize, dtype=torch.uint8, device="cuda:%d" % self.device)
 

@@ -195,6 +195,18 @@ int cts_counters_read(cts_engine* engine, const void* dev_counters, cts_counters
 int cts_counters_read_multi(cts_engine* const* engines, const void* const* dev_counters, void* const* streams,
                             uint32_t n, cts_counters* out);
 
+/* cts_verify over a uniformly strided receive ring (a UDP socket's datagrams): buffer i occupies
+ * [i * stride, i * stride + dev_lengths[i]) of the arena, its first skip_head bytes are skipped and the rest
+ * is checked against the pattern from expected_offset (MediaStream payloads: skip 26, expected 0,
+ * ctsIOPatternMediaStream.cpp:185-192); every buffer belongs to connection conn_index. The kernel reads 4
+ * bytes of metadata per buffer instead of a 24-byte descriptor. A length above the stride (or one that
+ * leaves the arena) is flagged CTS_RESULT_FLAG_BAD_DESC. Outputs and counters as cts_verify. dev_lengths must
+ * be 4-byte aligned, dev_arena 16-byte aligned with arena_bytes >= 16, stride > 0. */
+int cts_verify_strided(cts_engine* engine, const void* dev_arena, uint64_t arena_bytes, uint32_t stride,
+                       const uint32_t* dev_lengths, uint32_t n, uint32_t skip_head, uint32_t expected_offset,
+                       uint32_t conn_index, cts_verify_result* dev_results, void* dev_counters,
+                       uint32_t* dev_conn_first_fail, uint32_t n_conns, void* stream);
+
 /* ---- host-buffer drop-in for ctsIoPattern::VerifyBuffer ---------------------- */
 /* Verifies `len` bytes at host_buf against the pattern starting at
  * expected_offset and waits. Returns the record in *out (RtlCompareMemory

@@ -770,3 +770,69 @@ def test_engine_stream(engine):
     exp = W.expected_results(w)[2]
     assert engine.read_counters(ctr, stream=s.value) == exp
     assert _lib.lib().cts_engine_stream_destroy(engine._h, s) == 0
+
+
+# ---- strided receive rings (cts_verify_strided) -----------------------------------------------------------------
+@pytest.mark.parametrize("stride,skip,expected", [(1472, 26, 0), (1536, 26, 0), (9017, 0, 777), (64, 3, 65535)])
+def test_verify_strided_matches_oracle(engine, stride, skip, expected):
+    """cts_verify_strided: buffer i of a ring at i * stride (16-byte-aligned slots and odd strides) with only its
+    completed length, one skip / expected offset / connection for the ring (MediaStream payloads: skip 26,
+    expected 0). Results, counters and the connection's first failure equal the oracle's over the same buffers
+    described by descriptors; a length above the stride is BAD_DESC and counts nowhere."""
+    rng = np.random.default_rng(stride)
+    n = 6000
+    S = oracle.sender_buffer(stride + 65536)
+    ring = np.full(n * stride + 64, 0xEE, dtype=np.uint8)
+    lens = rng.integers(0, stride + 1, size=n).astype(np.uint32)
+    lens[:6] = [0, max(0, skip - 1), skip, min(stride, skip + 1), stride, stride]
+    for i in range(n):
+        ln = int(lens[i])
+        if ln > skip:
+            body = S[expected:expected + ln - skip].copy()
+            if rng.random() < 0.05:
+                body[int(rng.integers(0, ln - skip))] ^= int(rng.integers(1, 256))
+            ring[i * stride + skip:i * stride + ln] = body
+    descs = np.zeros(n, dtype=DESC_DTYPE)
+    descs["byte_offset"] = np.arange(n, dtype=np.uint64) * stride
+    descs["length"] = lens
+    descs["expected_pattern_offset"] = expected
+    descs["conn_index"] = 3
+    descs["skip_head"] = skip
+    er, ectr, ecff = oracle.verify_batch(ring, descs, n_conns=5)
+    a = to_dev(ring)
+    res = engine.new_results(n)
+    ctr = engine.new_counters()
+    cff = torch.full((5,), -1, dtype=torch.int32, device=DEV)
+    engine.verify_strided(a, stride, to_dev(lens), skip_head=skip, expected_offset=expected, conn_index=3, results=res,
+                          counters=ctr, conn_first_fail=cff)
+    torch.cuda.synchronize()
+    assert_results_equal(res.cpu().numpy().view(RESULT_DTYPE), er, "stride %d" % stride)
+    assert engine.read_counters(ctr) == ectr
+    assert np.array_equal(cff.cpu().numpy().view(np.uint32), ecff)
+    # a completion longer than its slot is flagged, not read
+    lens2 = lens.copy()
+    lens2[7] = stride + 1
+    res2 = engine.new_results(n)
+    ctr2 = engine.new_counters()
+    engine.verify_strided(a, stride, to_dev(lens2), skip_head=skip, expected_offset=expected, results=res2, counters=ctr2)
+    torch.cuda.synchronize()
+    r2 = res2.cpu().numpy().view(RESULT_DTYPE)
+    assert r2["flags"][7] == 1 and r2["pass"][7] == 0
+    keep = np.arange(n) != 7
+    assert_results_equal(r2[keep], er[keep], "stride %d, one long" % stride)
+    c2 = engine.read_counters(ctr2)
+    assert c2["buffers_checked"] == ectr["buffers_checked"] - 1
+
+
+def test_verify_strided_rejects_bad_arguments(engine):
+    from ctstraffic_amd import CtsError
+
+    a = torch.zeros(4096, dtype=torch.uint8, device=DEV)
+    lens = torch.zeros(4, dtype=torch.int32, device=DEV)
+    for kw in [dict(stride=0), dict(expected_offset=65536)]:
+        args = dict(stride=1024, expected_offset=0)
+        args.update(kw)
+        with pytest.raises(CtsError):
+            engine.verify_strided(a, args["stride"], lens, expected_offset=args["expected_offset"])
+    with pytest.raises(CtsError):
+        engine.verify_strided(a[1:], 1024, lens)  # arena not 16-byte aligned

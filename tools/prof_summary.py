@@ -33,18 +33,21 @@ WORKLOADS = {
         DG * 1446),
     "media_stream_verify_quad_kernel[strided]": "config3 MediaStream receive, strided ring (lengths only): 16M x "
                                                 "1472 B datagrams (%d B payload read)" % (DG * 1446),
+    "verify_quad_kernel[strided]": "config3 verify, strided ring (lengths only): 16M x 1472 B datagrams "
+                                   "(%d B payload read)" % (DG * 1446),
 }
 ALGO_BYTES = {"verify_wg_kernel": 268435456, "fill_kernel": 268435456, "verify_quad_kernel": DG * 1446,
               "verify_wave_kernel": DG * 1446, "media_stream_verify_quad_kernel": DG * 1446,
-              "media_stream_verify_quad_kernel[strided]": DG * 1446}
+              "media_stream_verify_quad_kernel[strided]": DG * 1446, "verify_quad_kernel[strided]": DG * 1446}
 RUNS = ("prof", "prof_dg")
 
 
 def _kname(name):
     base = name.split("(")[0].split("<")[0].split("::")[-1].strip()
-    if base == "media_stream_verify_quad_kernel" and "<" in name:
+    if base in ("media_stream_verify_quad_kernel", "verify_quad_kernel") and "<" in name:
         targs = name.split("(")[0].split("<", 1)[1].rsplit(">", 1)[0].split(",")
-        if len(targs) == 6 and targs[-1].strip() == "true":  # STRIDED: cts_media_stream_verify_strided
+        last = 6 if base == "media_stream_verify_quad_kernel" else 5
+        if len(targs) == last and targs[-1].strip() == "true":  # STRIDED: the *_verify_strided entry points
             return base + "[strided]"
     return base
 
