@@ -17,7 +17,48 @@
 #include <thread>
 #include <vector>
 
+#include <hip/hip_runtime_api.h>
+#include <sched.h>
+
+#include <fstream>
+#include <sstream>
+#include <string>
+
 #include "cts_engine.h"
+
+// CTS_PIN_NEAR_GPU=1: restrict the process to the CPUs of the GPU's NUMA node (PCI device -> numa_node ->
+// cpulist) before any pinned allocation or thread; prints the node and CPU count it used.
+static void pin_near_gpu()
+{
+    const char* v = std::getenv("CTS_PIN_NEAR_GPU");
+    if (v == nullptr || std::atoi(v) == 0) return;
+    char bus[64] = {0};
+    if (hipDeviceGetPCIBusId(bus, sizeof(bus), 0) != hipSuccess) return;
+    std::string id(bus);
+    for (auto& c : id) c = (char)std::tolower((unsigned char)c);
+    int node = -1;
+    std::ifstream(std::string("/sys/bus/pci/devices/") + id + "/numa_node") >> node;
+    if (node < 0) {
+        std::printf("{\"pin\": \"no numa node for %s\"}\n", id.c_str());
+        return;
+    }
+    std::string list;
+    std::ifstream(std::string("/sys/devices/system/node/node") + std::to_string(node) + "/cpulist") >> list;
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    int count = 0;
+    std::stringstream ss(list);
+    std::string part;
+    while (std::getline(ss, part, ',')) {
+        const size_t dash = part.find('-');
+        const int lo = std::atoi(part.substr(0, dash).c_str());
+        const int hi = dash == std::string::npos ? lo : std::atoi(part.substr(dash + 1).c_str());
+        for (int c = lo; c <= hi && c < CPU_SETSIZE; ++c, ++count) CPU_SET(c, &set);
+    }
+    const int rc = sched_setaffinity(0, sizeof(set), &set);
+    std::printf("{\"pin\": \"%s\", \"numa_node\": %d, \"cpus\": %d, \"rc\": %d}\n", id.c_str(), node, count, rc);
+    std::fflush(stdout);
+}
 
 static int run_thread(cts_engine* e, uint32_t slices, bool spin, bool mapped, int iters, double* us_out, int* bad,
                       bool host_copy = false)
@@ -76,6 +117,7 @@ int main(int argc, char** argv)
 {
     const int iters = argc > 1 ? std::atoi(argv[1]) : 2000;
     const bool mailbox_only = argc > 2 && std::strcmp(argv[2], "mailbox") == 0;
+    pin_near_gpu();
     cts_engine* e = nullptr;
     if (cts_engine_create(0, &e) != CTS_OK) return 1;
     // wait: 0 stream_sync, 1 query_spin, 2 cts_verify_mapped (mailbox; slices = its 4 KiB pieces, reported as 64)
