@@ -61,6 +61,10 @@ def parse():
                    help="headline leg: launches round-robin over S engine streams, so one batch's tail overlaps the "
                         "next batch's ramp-up (1 = serialized launches; 2 measured best at the driver's 20 steps: "
                         "profiles/r02/pipeline_streams/)")
+    p.add_argument("--pin-numa", action="store_true",
+                   help="pin the process to the GPU's NUMA node (cts_engine_numa_node): tools/sync_probe's SYNC "
+                        "verifies answer faster there, but whole loopback runs were not faster "
+                        "(profiles/r02/numa/); the device-resident legs do not care")
     p.add_argument("--verify-variant", type=int, default=-1,
                    help="CTS_ATTR_VERIFY_VARIANT for both legs (-1 = engine default; tuning builds only)")
     return p.parse_args()
@@ -146,6 +150,9 @@ def main():
     engine = Engine(gpu, tuning=args.verify_variant >= 0)
     if args.verify_variant >= 0:
         engine.set_attr(_lib.ATTR_VERIFY_VARIANT, args.verify_variant)
+    near = engine.cpus_near() if args.pin_numa else []
+    if near:  # threads started from here on (loopback sides, the mailbox watchdog) inherit it
+        os.sched_setaffinity(0, near)
     stream = torch.cuda.Stream() if args.stream == "new" else torch.cuda.current_stream()
 
     # ---- workload (per rank: weak scaling) --------------------------------------------------
@@ -327,6 +334,8 @@ def main():
                 "verified_bytes_per_step_per_gpu": bytes_per_step,
                 "arenas_rotated": R,
                 "pipeline_streams": S,
+                "host_numa_node": engine.numa_node() if near else None,
+                "host_cpus_pinned": len(near),
                 "parallelism": "%d rank(s), one config-2 batch of its own connections each, no data-path "
                                "collective; RCCL all-reduce of the 5 counters closes the timed region" % world,
             },

@@ -124,6 +124,7 @@ def _declare(L: ctypes.CDLL) -> None:
         "cts_engine_create": ([i32, ctypes.POINTER(P)], i32),
         "cts_engine_destroy": ([P], i32),
         "cts_engine_device": ([P], i32),
+        "cts_engine_numa_node": ([P], i32),
         "cts_sender_buffer_fill": ([P, P, u32, P], i32),
         "cts_fill": ([P, P, u64, P, u32, u32, P], i32),
         "cts_verify": ([P, P, u64, P, u32, u32, P, P, P, u32, P], i32),

@@ -7,13 +7,16 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cctype>
 #include <chrono>
 #include <condition_variable>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
 #include <new>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -450,6 +453,22 @@ int cts_engine_destroy(cts_engine* e)
 }
 
 int cts_engine_device(const cts_engine* e) { return e ? e->device : CTS_E_INVALID; }
+
+int cts_engine_numa_node(const cts_engine* e)
+{
+    if (e == nullptr) return -1;
+    char bus[64] = {0};
+    if (hipDeviceGetPCIBusId(bus, (int)sizeof(bus), e->device) != hipSuccess) return -1;
+    std::string path = "/sys/bus/pci/devices/";
+    for (const char* c = bus; *c; ++c) path += (char)std::tolower((unsigned char)*c);
+    path += "/numa_node";
+    FILE* f = std::fopen(path.c_str(), "r");
+    if (f == nullptr) return -1;
+    int node = -1;
+    if (std::fscanf(f, "%d", &node) != 1) node = -1;
+    std::fclose(f);
+    return node;
+}
 
 int cts_engine_stream_create(cts_engine* e, void** stream)
 {

@@ -157,6 +157,25 @@ class Engine:
               self._L.cts_sender_buffer_fill(self._h, _ptr(out), max_buffer_size, _stream(stream)))
         return out
 
+    def numa_node(self) -> int:
+        """The host NUMA node of the engine's GPU (-1 if unknown): pin SYNC-verify threads there."""
+        return int(self._L.cts_engine_numa_node(self._h))
+
+    def cpus_near(self) -> list:
+        """The CPUs of numa_node() (empty if unknown), for os.sched_setaffinity."""
+        node = self.numa_node()
+        if node < 0:
+            return []
+        try:
+            spec = open("/sys/devices/system/node/node%d/cpulist" % node).read().strip()
+        except OSError:
+            return []
+        cpus = []
+        for part in spec.split(","):
+            lo, _, hi = part.partition("-")
+            cpus.extend(range(int(lo), int(hi or lo) + 1))
+        return cpus
+
     def fill(self, arena, descs, max_length_hint: int = 0, stream=None) -> None:
         n = _nbytes(descs) // DESC_DTYPE.itemsize
         check("cts_fill", self._L.cts_fill(self._h, _ptr(arena), _nbytes(arena), _ptr(descs), n, max_length_hint,

@@ -118,6 +118,11 @@ uint32_t cts_shard_of(uint32_t conn_index, uint32_t n_shards);
 int cts_engine_create(int device, cts_engine** out);
 int cts_engine_destroy(cts_engine* engine);
 int cts_engine_device(const cts_engine* engine);
+/* The host NUMA node the engine's GPU hangs off (its PCI device's numa_node), or -1 if unknown. In
+ * tools/sync_probe, threads posting SYNC verifies (cts_verify_mapped / cts_verify_host) answered faster
+ * pinned there: 6.0-7.5 / 9.9-12.7 / 14.5-15.0 us per 64 KiB at 1 / 8 / 16 callers, against 6.1-9.6 /
+ * 16.1-17.3 / 15.5-24.8 unpinned. Whole loopback runs pinned there were not faster. */
+int cts_engine_numa_node(const cts_engine* engine);
 
 /* Launch-geometry attributes (defaults tuned for MI355X; env overrides
  * CTS_BLOCKS_PER_CU / CTS_NT_LOADS / CTS_SMALL_THRESHOLD / CTS_VERIFY_VARIANT /
