@@ -531,6 +531,57 @@ def test_verify_mapped_mailbox_small_rings(monkeypatch):
     assert not errors, errors[:5]
 
 
+def test_verify_mapped_mailbox_stop_start_races(monkeypatch):
+    """A fresh engine whose watchdog stops the grid after 5 ms without posts (CTS_MAILBOX_IDLE_MS): 6 threads post
+    with random pauses of 0-20 ms, so stops race new posts and relaunches all through the run. Every answer must be
+    the oracle's, the grid must have been relaunched many times, and the engine must close cleanly."""
+    import random
+    import threading
+    import time
+
+    from ctstraffic_amd import Engine
+
+    monkeypatch.setenv("CTS_MAILBOX_IDLE_MS", "5")
+    eng = Engine(0)
+    S = oracle.sender_buffer(70000)
+    arenas = [eng.host_alloc(65536 + 32) for _ in range(6)]
+    errors = []
+
+    def worker(t):
+        arr, _, dev = arenas[t]
+        rng = np.random.default_rng(0x5A0 + t)
+        pause = random.Random(t)
+        try:
+            for it in range(40):
+                n = int(rng.choice([1, 1500, 4096, 65536]))
+                e = int(rng.integers(0, 65536))
+                arr[:n] = S[e:e + n]
+                if rng.random() < 0.3:
+                    arr[int(rng.integers(0, n))] ^= 0x11
+                r = eng.verify_mapped(dev, n, e)
+                o = oracle.verify_buffer(arr[:n].copy(), 0, e, n)
+                if (r["pass"], r["first_mismatch"], r["actual"], r["mismatch_bytes"]) != (
+                        o["pass"], o["first_mismatch"], o["actual"], o["mismatch_bytes"]):
+                    errors.append((t, it, n, e))
+                time.sleep(pause.choice([0, 0, 0.002, 0.006, 0.012, 0.02]))
+        except Exception as ex:  # surfaced below
+            errors.append((t, repr(ex)))
+
+    try:
+        ths = [threading.Thread(target=worker, args=(t,)) for t in range(6)]
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        launches = eng.mailbox_launches()
+    finally:
+        for _, h, _ in arenas:
+            eng.host_free(h)
+        eng.close()
+    assert not errors, errors[:5]
+    assert launches >= 3, launches
+
+
 def test_verify_mapped_mailbox_restarts_after_idle(engine):
     """The mailbox grid stops after CTS_MAILBOX_IDLE_MS (50 ms) without posts and the next post starts it again;
     answers stay exact across the restart, including an HBM buffer and a buffer larger than the grid's
