@@ -130,8 +130,10 @@ int ensure_stage(cts_engine* e, size_t bytes)
 // g * per_group + j % per_group once its previous user (j - per_group) has read its answer (free_at).
 // The grid is (re)launched by the first post after it stopped, at every group's next job number, and a
 // watchdog thread stops it with one stop job per group after `idle_ms` without posts, so an idle engine
-// neither holds workgroups nor polls PCIe. The grid's own exit bound (idle_ticks, far longer) is a
-// safety net only: a post racing it would time out (CTS_E_HIP) rather than hang.
+// neither holds workgroups nor polls PCIe. The grid's own exit bound (a group leaves after exit_ms
+// without a job, far longer) is a safety net: every group gets a job at least every exit_ms / 4 while the
+// grid runs (a caller's job goes to a group that has waited that long, even if another is less busy),
+// and a post after exit_ms / 2 of silence checks whether the grid already left (a starved watchdog).
 struct Mailbox {
     cts_engine* e = nullptr;
     // groups x cts::kMailGroup workgroups: 8 groups measured best for 8-16 concurrent callers (64 KiB:
@@ -139,7 +141,8 @@ struct Mailbox {
     // profiles/r02/sync_probe_groups.jsonl). A job goes to the group with the fewest outstanding, so
     // one caller keeps one group hot and the idle ones back off.
     uint32_t nslots = 1024, groups = 8, per_group = 128;
-    uint64_t idle_ticks = 100000000ull;  // 1 s at 100 MHz
+    int exit_ms = 1000;                  // the grid's own per-group idle exit (CTS_MAILBOX_EXIT_MS)
+    uint64_t idle_ticks = 100000000ull;  // exit_ms at 100 MHz (s_memrealtime)
     int idle_ms = 50;
     double timeout_s = 2.0;
     cts::MailSlot* slots = nullptr;      // host view (coherent, pinned)
@@ -154,6 +157,7 @@ struct Mailbox {
     uint32_t busy[cts::kMailMaxGroups] = {};       // each group's jobs outstanding
     uint32_t outstanding = 0;
     std::chrono::steady_clock::time_point last_post;
+    std::chrono::steady_clock::time_point last_used[cts::kMailMaxGroups];  // each group's latest job
     std::condition_variable cv;
     std::thread watchdog;
     std::atomic<uint64_t> launches{0};
@@ -183,6 +187,8 @@ struct Mailbox {
         nslots = (uint32_t)std::max(16, env_int("CTS_MAILBOX_SLOTS", (int)nslots));
         groups = (uint32_t)std::min((int)cts::kMailMaxGroups, std::max(1, env_int("CTS_MAILBOX_GROUPS", (int)groups)));
         idle_ms = std::max(1, env_int("CTS_MAILBOX_IDLE_MS", idle_ms));
+        exit_ms = std::max(40, env_int("CTS_MAILBOX_EXIT_MS", exit_ms));
+        idle_ticks = (uint64_t)exit_ms * 100000ull;
         DeviceGuard g(e->device);
         if (!g.ok) return CTS_E_HIP;
         void* p = nullptr;
@@ -224,6 +230,8 @@ struct Mailbox {
             return CTS_E_HIP;
         running = true;
         launches.fetch_add(1, std::memory_order_relaxed);
+        const auto now = std::chrono::steady_clock::now();
+        for (uint32_t i = 0; i < groups; ++i) last_used[i] = now;
         return CTS_OK;
     }
 
@@ -242,12 +250,25 @@ struct Mailbox {
                 running = false;
                 n = groups;
             } else {
+                const auto now = std::chrono::steady_clock::now();
+                if (running && now - last_post > std::chrono::milliseconds(exit_ms / 2)) {
+                    // silent long enough that the grid may have left on its own (the watchdog was starved)
+                    DeviceGuard g(e->device);
+                    if (hipStreamQuery(stream) == hipSuccess) running = false;
+                }
                 if (!running) {
                     const int rc = LaunchLocked();
                     if (rc != CTS_OK) return rc;
                 }
                 for (uint32_t i = 1; i < groups; ++i)
                     if (busy[i] < busy[g0]) g0 = i;
+                // keep every group inside its idle exit: one that has waited exit_ms / 4 takes this job
+                for (uint32_t i = 0; i < groups; ++i)
+                    if (busy[i] == 0 && now - last_used[i] > std::chrono::milliseconds(exit_ms / 4)) {
+                        g0 = i;
+                        break;
+                    }
+                last_used[g0] = now;
             }
             for (uint32_t i = 0; i < n; ++i) {
                 js[i] = next[g0 + i]++;

@@ -234,7 +234,9 @@ int cts_verify_host(cts_engine* engine, const void* host_buf, uint32_t len,
  * ctsSocket.h:189) post independent jobs, each to the least busy group, and
  * those run side by side. The grid starts on the first call and stops after
  * CTS_MAILBOX_IDLE_MS (default 50) ms without calls (env CTS_MAILBOX_GROUPS,
- * CTS_MAILBOX_SLOTS size it); cts_engine_destroy stops it. */
+ * CTS_MAILBOX_SLOTS size it); cts_engine_destroy stops it. Each group also
+ * leaves by itself after CTS_MAILBOX_EXIT_MS (default 1000) ms without a job;
+ * posts keep every group inside that bound and relaunch a grid that left. */
 int cts_verify_mapped(cts_engine* engine, const void* dev_buf, uint32_t len,
                       uint32_t expected_offset, cts_verify_result* out);
 /* How many times the mailbox grid was launched (0 = never used): each launch serves every

@@ -582,6 +582,69 @@ def test_verify_mapped_mailbox_stop_start_races(monkeypatch):
     assert launches >= 3, launches
 
 
+def test_verify_mapped_mailbox_group_keepalive(monkeypatch):
+    """A fresh engine whose grid groups leave after 400 ms without a job (CTS_MAILBOX_EXIT_MS) and whose watchdog
+    would wait 5 s (CTS_MAILBOX_IDLE_MS), i.e. a watchdog too slow to stop the grid first. One thread posts for
+    1.2 s (least-busy assignment alone would use one group and let the others leave), then 8 threads post at once
+    (jobs land on every group), then the process is silent for 0.8 s (the whole grid leaves on its own) and posts
+    again (the engine must see the finished grid and relaunch it). Every answer must be the oracle's."""
+    import threading
+    import time
+
+    from ctstraffic_amd import Engine
+
+    monkeypatch.setenv("CTS_MAILBOX_EXIT_MS", "400")
+    monkeypatch.setenv("CTS_MAILBOX_IDLE_MS", "5000")
+    eng = Engine(0)
+    S = oracle.sender_buffer(70000)
+    arenas = [eng.host_alloc(65536 + 32) for _ in range(8)]
+    errors = []
+
+    def one(t, rng):
+        arr, _, dev = arenas[t]
+        n = int(rng.choice([1, 1500, 4096, 65536]))
+        e = int(rng.integers(0, 65536))
+        arr[:n] = S[e:e + n]
+        if rng.random() < 0.3:
+            arr[int(rng.integers(0, n))] ^= 0x24
+        r = eng.verify_mapped(dev, n, e)
+        o = oracle.verify_buffer(arr[:n].copy(), 0, e, n)
+        if (r["pass"], r["first_mismatch"], r["actual"], r["mismatch_bytes"]) != (
+                o["pass"], o["first_mismatch"], o["actual"], o["mismatch_bytes"]):
+            errors.append((t, n, e))
+
+    def burst(t):
+        rng = np.random.default_rng(0x4EE + t)
+        try:
+            for _ in range(200):
+                one(t, rng)
+        except Exception as ex:  # surfaced below
+            errors.append((t, repr(ex)))
+
+    try:
+        rng = np.random.default_rng(0x4EE)
+        t_end = time.monotonic() + 1.2
+        while time.monotonic() < t_end:
+            one(0, rng)
+        ths = [threading.Thread(target=burst, args=(t,)) for t in range(8)]
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        first = eng.mailbox_launches()
+        time.sleep(0.8)
+        for _ in range(50):
+            one(0, rng)
+        launches = eng.mailbox_launches()
+    finally:
+        for _, h, _ in arenas:
+            eng.host_free(h)
+        eng.close()
+    assert not errors, errors[:5]
+    assert first == 1, first
+    assert launches == 2, launches
+
+
 def test_verify_mapped_mailbox_restarts_after_idle(engine):
     """The mailbox grid stops after CTS_MAILBOX_IDLE_MS (50 ms) without posts and the next post starts it again;
     answers stay exact across the restart, including an HBM buffer and a buffer larger than the grid's
