@@ -150,6 +150,8 @@ struct Mailbox {
     cts::MailPart* parts = nullptr;      // nslots x kMailGroup part records, host view (coherent, pinned)
     cts::MailPart* dparts = nullptr;
     hipStream_t stream = nullptr;
+    hipEvent_t grid_done = nullptr;      // recorded after each launch: hipStreamQuery cannot see a kernel end
+                                         // it was not asked about before (no completion signal), an event can
     std::unique_ptr<std::atomic<uint64_t>[]> free_at;
     std::mutex mu;
     bool running = false, broken = false, quit = false;
@@ -177,6 +179,7 @@ struct Mailbox {
             (void)hipStreamSynchronize(stream);
             (void)hipStreamDestroy(stream);
         }
+        if (grid_done) (void)hipEventDestroy(grid_done);
         if (parts) (void)hipHostFree(parts);
         if (slots) (void)hipHostFree(slots);
     }
@@ -211,6 +214,10 @@ struct Mailbox {
             stream = nullptr;
             return CTS_E_HIP;
         }
+        if (hipEventCreateWithFlags(&grid_done, hipEventDisableTiming) != hipSuccess) {
+            grid_done = nullptr;
+            return CTS_E_HIP;
+        }
         free_at.reset(new (std::nothrow) std::atomic<uint64_t>[nslots]);
         if (!free_at) return CTS_E_NOMEM;
         for (uint32_t i = 0; i < nslots; ++i) free_at[i].store(i % per_group, std::memory_order_relaxed);  // job j of its group
@@ -226,7 +233,8 @@ struct Mailbox {
         if (!g.ok) return CTS_E_HIP;
         cts::MailStarts starts{};
         for (uint32_t i = 0; i < groups; ++i) starts.j[i] = next[i];
-        if (cts::launch_mailbox(dslots, dparts, per_group, starts, groups, idle_ticks, stream) != hipSuccess)
+        if (cts::launch_mailbox(dslots, dparts, per_group, starts, groups, idle_ticks, stream) != hipSuccess ||
+            hipEventRecord(grid_done, stream) != hipSuccess)
             return CTS_E_HIP;
         running = true;
         launches.fetch_add(1, std::memory_order_relaxed);
@@ -254,7 +262,7 @@ struct Mailbox {
                 if (running && now - last_post > std::chrono::milliseconds(exit_ms / 2)) {
                     // silent long enough that the grid may have left on its own (the watchdog was starved)
                     DeviceGuard g(e->device);
-                    if (hipStreamQuery(stream) == hipSuccess) running = false;
+                    if (hipEventQuery(grid_done) == hipSuccess) running = false;
                 }
                 if (!running) {
                     const int rc = LaunchLocked();
