@@ -9,6 +9,9 @@
 //   line16    every round, lanes 0..7 store 16 B each (128 B, one line)
 //   burst     every 8th round, lanes 0..59 store 16 B each (960 B per 32 KiB read)
 //   wt        dword with write-through (sc1) stores
+//   phasedP_B the dword outputs of P rounds kept in LDS, then written by every workgroup at once: a
+//             co-resident grid meets at a grid barrier (B = 1: before the write phase; B = 2: before and
+//             after it), so the memory sees read phases and write phases instead of a mix
 // Output positions follow the read position (output i belongs to the 4 KiB read as i), as the
 // verify kernels' records follow their datagrams. (The 128 MiB output region is rewritten by every launch and
 // may partly stay in the 256 MB MALL; the 2 GiB read stream cannot.) Prints one JSON line per shape.
@@ -53,6 +56,108 @@ __global__ void __launch_bounds__(256) rw_kernel(const u32x4* __restrict__ p, ui
     if (acc == 0x12345678u) out[0] = acc;
 }
 
+// Grid barrier for a co-resident grid: workgroup b adds to sub-counter b % nsub (its own 128-B line); the
+// last arriver of a sub-counter adds to the top counter; everyone waits for the top to reach the generation.
+// Counters only grow (generation gen counts from the launch's gen0), so launches need no reset. A barrier
+// that waits past ~200 ms (a grid that is not co-resident) sets *err and lets the waves go.
+template <int SLEEP>
+__device__ __forceinline__ void grid_sync(uint32_t* bar, uint32_t nsub, uint32_t gen, uint32_t* err)
+{
+    // lines: 0 = top arrivals, 1..nsub = sub arrivals, 1+nsub..2*nsub = sub release words
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t s = blockIdx.x % nsub;
+        const uint32_t per = gridDim.x / nsub + (s < gridDim.x % nsub ? 1u : 0u);
+        const uint32_t old = __hip_atomic_fetch_add(bar + 32u * (1u + s), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (old + 1u == gen * per) {
+            const uint32_t top = __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (top + 1u == gen * nsub)
+                for (uint32_t i = 0; i < nsub; ++i)
+                    __hip_atomic_store(bar + 32u * (1u + nsub + i), gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        const uint64_t t0 = wall_clock64();
+        uint32_t* const rel = bar + 32u * (1u + nsub + s);
+        while (__hip_atomic_load(rel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gen) {
+            __builtin_amdgcn_s_sleep(SLEEP);
+            if (wall_clock64() - t0 > 20000000ull) {
+                __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+        }
+    }
+    __syncthreads();
+}
+
+template <int P, int BARS, int SLEEP = 4>
+__global__ void __launch_bounds__(256) phased_kernel(const u32x4* __restrict__ p, uint64_t nchunks, uint32_t* __restrict__ out,
+                                                     uint32_t* bar, uint32_t nsub, uint32_t gen0, uint32_t* err)
+{
+    constexpr int U = 4;
+    __shared__ uint32_t stage[P][4][32];
+    uint32_t acc = 0, gen = gen0;
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint64_t stride = (uint64_t)gridDim.x * 256u * U;
+    uint64_t c = (uint64_t)blockIdx.x * 256u * U + threadIdx.x;
+    uint64_t slot0 = 0;
+    for (uint64_t r = 0; c + 256u * (U - 1) < nchunks; c += stride, ++r) {
+        u32x4 d[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) d[u] = __builtin_nontemporal_load(p + c + u * 256u);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc |= d[u][0] ^ d[u][1] ^ d[u][2] ^ d[u][3];
+        const uint32_t k = (uint32_t)(r % P);
+        if (k == 0) slot0 = ((c - threadIdx.x) / (256u * U)) * 4u;
+        if (lane < 30u) stage[k][wave][lane] = acc | (uint32_t)r;
+        if (k == P - 1) {  // end of a read phase: meet, write the phase's outputs, (meet)
+            grid_sync<SLEEP>(bar, nsub, ++gen, err);
+            for (uint32_t i = threadIdx.x; i < P * 128u; i += 256u) {
+                const uint32_t kk = i / 128u, w = (i / 32u) & 3u, l = i & 31u;
+                if (l < 30u) out[(slot0 + (uint64_t)kk * (gridDim.x * 4u) + w) * 32u + l] = stage[kk][w][l];
+            }
+            if constexpr (BARS == 2) grid_sync<SLEEP>(bar, nsub, ++gen, err);
+        }
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
+template <int P, int BARS, int SLEEP = 4>
+static void run_phased(const char* name, const u32x4* p, uint64_t nchunks, uint32_t* out, uint32_t* bar, uint32_t* err)
+{
+    int dev = 0, cus = 0, per_cu = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, phased_kernel<P, BARS, SLEEP>, 256, 0);
+    int grid = cus * (per_cu < 8 ? per_cu : 8);
+    // every workgroup must run the same number of rounds, a multiple of P (each meets every barrier)
+    while (grid > 0 && (nchunks / (256u * 4u)) % ((uint64_t)grid * P) != 0) grid -= cus;
+    if (grid <= 0) return;
+    const uint32_t nsub = 32;
+    const uint32_t phases = (uint32_t)(nchunks / (256u * 4u) / ((uint64_t)grid * P));
+    const uint32_t per_launch = phases * BARS;
+    (void)hipMemset(bar, 0, 65 * 128);
+    (void)hipMemset(err, 0, 4);
+    uint32_t gen0 = 0;
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+    phased_kernel<P, BARS, SLEEP><<<grid, 256>>>(p, nchunks, out, bar, nsub, gen0, err);
+    gen0 += per_launch;
+    (void)hipEventRecord(a);
+    const int iters = 10;
+    for (int i = 0; i < iters; ++i, gen0 += per_launch) phased_kernel<P, BARS, SLEEP><<<grid, 256>>>(p, nchunks, out, bar, nsub, gen0, err);
+    (void)hipEventRecord(b);
+    (void)hipEventSynchronize(b);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, a, b);
+    uint32_t e = 0;
+    (void)hipMemcpy(&e, err, 4, hipMemcpyDeviceToHost);
+    const double us = ms * 1e3 / iters;
+    std::printf("{\"shape\": \"%s\", \"grid\": %d, \"phases\": %u, \"us\": %.1f, \"read_GBps\": %.1f, \"barrier_timeout\": %u}\n",
+                name, grid, phases, us, nchunks * 16.0 / (us * 1e3), e);
+    std::fflush(stdout);
+}
+
 template <int MODE>
 static void run(const char* name, const u32x4* p, uint64_t nchunks, uint32_t* out, int grid)
 {
@@ -73,12 +178,15 @@ static void run(const char* name, const u32x4* p, uint64_t nchunks, uint32_t* ou
     std::fflush(stdout);
 }
 
-int main()
+int main(int argc, char**)
 {
     const uint64_t bytes = 2ull << 30, nchunks = bytes / 16;
     u32x4* p = nullptr;
     uint32_t* out = nullptr;
-    if (hipMalloc((void**)&p, bytes) != hipSuccess || hipMalloc((void**)&out, bytes / 16) != hipSuccess) return 1;
+    uint32_t *bar = nullptr, *err = nullptr;
+    if (hipMalloc((void**)&p, bytes) != hipSuccess || hipMalloc((void**)&out, bytes / 16) != hipSuccess ||
+        hipMalloc((void**)&bar, 65 * 128) != hipSuccess || hipMalloc((void**)&err, 4) != hipSuccess)
+        return 1;
     (void)hipMemset(p, 1, bytes);
     (void)hipMemset(out, 0, bytes / 16);
     for (int grid : {2048, 4096}) {
@@ -88,6 +196,17 @@ int main()
         run<3>("line16", p, nchunks, out, grid);
         run<4>("burst", p, nchunks, out, grid);
         run<5>("wt_sc1", p, nchunks, out, grid);
+    }
+    if (argc > 1) {
+        run<0>("none", p, nchunks, out, 2048);
+        run<1>("dword", p, nchunks, out, 2048);
+        run_phased<8, 1, 1>("phased8_1_s1", p, nchunks, out, bar, err);
+        run_phased<8, 1, 4>("phased8_1_s4", p, nchunks, out, bar, err);
+        run_phased<8, 1, 16>("phased8_1_s16", p, nchunks, out, bar, err);
+        run_phased<8, 2, 4>("phased8_2_s4", p, nchunks, out, bar, err);
+        run_phased<16, 1, 4>("phased16_1_s4", p, nchunks, out, bar, err);
+        run_phased<32, 1, 4>("phased32_1_s4", p, nchunks, out, bar, err);
+        run_phased<32, 2, 4>("phased32_2_s4", p, nchunks, out, bar, err);
     }
     return 0;
 }
