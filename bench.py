@@ -10,7 +10,7 @@ rotates over R >= 8 identical arenas (2 GiB) so every pass streams from HBM
 rather than the 256 MiB Infinity Cache. The fill kernel (the sender's
 materialisation, InitOnceIoPatternCallback's role) builds the arenas untimed.
 Batches are independent, so the headline leg issues step i on engine stream
-i mod S (S = 3): one launch's tail overlaps the next one's ramp-up, as a receiver
+i mod S (S = 2): one launch's tail overlaps the next one's ramp-up, as a receiver
 verifying a stream of batches would run. roofline.achieved comes from a separate
 serialized leg (one stream, HIP events), the per-kernel time rocprof reports.
 

@@ -136,10 +136,11 @@ int ensure_stage(cts_engine* e, size_t bytes)
 // and a post after exit_ms / 2 of silence checks whether the grid already left (a starved watchdog).
 struct Mailbox {
     cts_engine* e = nullptr;
-    // groups x cts::kMailGroup workgroups: 8 groups measured best for 8-16 concurrent callers (64 KiB:
-    // 18.7 / 25.3 us per verify at 8 / 16 threads against 19.6-32.6 for 1-4 groups; tools/sync_probe,
-    // profiles/r02/sync_probe_groups.jsonl). A job goes to the group with the fewest outstanding, so
-    // one caller keeps one group hot and the idle ones back off.
+    // groups x cts::kMailGroup workgroups: 8 groups measured best for 8-16 concurrent callers (with 16
+    // workgroups per group: 18.7 / 25.3 us per 64 KiB verify at 8 / 16 threads against 19.6-32.6 for 1-4
+    // groups, profiles/r02/sync_probe_groups.jsonl; with 4: 8 and 16 groups alike, mailbox_group_ab.jsonl).
+    // A job goes to the group with the fewest outstanding, so one caller keeps one group hot and the idle
+    // ones back off.
     uint32_t nslots = 1024, groups = 8, per_group = 128;
     int exit_ms = 1000;                  // the grid's own per-group idle exit (CTS_MAILBOX_EXIT_MS)
     uint64_t idle_ticks = 100000000ull;  // exit_ms at 100 MHz (s_memrealtime)

@@ -92,12 +92,17 @@ struct alignas(16) MailPart {
 };
 constexpr uint32_t kMailPieceBytes = 4096;  // one 16-B load per lane of a 256-lane workgroup
 // The grid is G groups of kMailGroup workgroups; a group's workgroups alone poll its ring and verify
-// its jobs' pieces (piece u by workgroup u mod kMailGroup of the group). The caller gives each job to
-// the group with the fewest jobs outstanding, so one caller keeps one group busy and the others idle.
-// Sixteen 4-KiB pieces cover a 64 KiB buffer in one PCIe round trip; G jobs run side by side, and
-// no slot is polled by more than kMailGroup readers (64 concurrent pollers of one host line cost
-// 10-13 us per round trip against 4.7 us for 16: tools/mailbox_probe).
-constexpr uint32_t kMailGroup = 16;
+// its jobs' pieces (piece u by workgroup u mod kMailGroup of the group, up to four pieces per workgroup
+// per round, their loads in flight together). The caller gives each job to the group with the fewest jobs
+// outstanding, so one caller keeps one group busy and the others idle. Four workgroups cover a 64 KiB
+// buffer in one PCIe round trip. Every workgroup polls its group's slot, and the pollers' PCIe reads
+// compete with the data reads: 16 workgroups per group answered a 64 KiB verify in 6.1-6.7 / 26.2-26.3 /
+// 42.3-42.5 us at 1 / 8 / 16 callers, 8 in 5.8-6.7 / 12.8-19.0 / 32.6-36.9, 4 in 5.5 / 11.5-11.8 / 28.1-29.1
+// (tools/sync_probe, tools/mailbox_group_ab.sh, profiles/r02/mailbox_group_ab.jsonl).
+#ifndef CTS_MAIL_GROUP
+#define CTS_MAIL_GROUP 4  // (a -D override builds the A/B libraries of tools/mailbox_group_ab.sh)
+#endif
+constexpr uint32_t kMailGroup = CTS_MAIL_GROUP;
 // Part records a job is answered with (a stop job: one per workgroup of its group).
 #if defined(__HIP__)
 __host__ __device__

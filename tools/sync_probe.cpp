@@ -5,10 +5,12 @@
 // so S workgroups/waves issue their PCIe reads at once) and T threads, each with its own stream,
 // buffer, descriptor and result (T connections completing concurrently). Wait = hipStreamSynchronize
 // or a hipStreamQuery spin, or cts_verify_mapped (posted to the engine's resident mailbox grid: no launch per
-// verify). Prints one JSON line per variant: us per verify (per thread).
+// verify). Prints one JSON line per variant: us per verify (mean, min and max over threads) and GB/s over the
+// wall time from the first thread's start to the last one's end (the timed loops start together).
 //   build: make tools/sync_probe      run: tools/sync_probe [iters [mailbox]]  (mailbox: waits 2-4 only)
 #include <hip/hip_runtime_api.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -60,8 +62,16 @@ static void pin_near_gpu()
     std::fflush(stdout);
 }
 
+// All threads of a variant start their timed loops together (gate) and report their start/end times, so the
+// variant's throughput is all verifies / (last end - first start), fair or not.
+struct Gate {
+    std::atomic<uint32_t> ready{0};
+    uint32_t threads = 1;
+};
+using Clock = std::chrono::steady_clock;
+
 static int run_thread(cts_engine* e, uint32_t slices, bool spin, bool mapped, int iters, double* us_out, int* bad,
-                      bool host_copy = false)
+                      bool host_copy, Gate* gate, Clock::time_point* start, Clock::time_point* end)
 {
     void* stream = nullptr;
     if (cts_engine_stream_create(e, &stream) != CTS_OK) return 1;
@@ -102,10 +112,14 @@ static int run_thread(cts_engine* e, uint32_t slices, bool spin, bool mapped, in
     };
     for (int i = 0; i < 50; ++i)
         if (!once()) ++*bad;
-    const auto t0 = std::chrono::steady_clock::now();
+    gate->ready.fetch_add(1);
+    while (gate->ready.load() < gate->threads) std::this_thread::yield();
+    const auto t0 = Clock::now();
     for (int i = 0; i < iters; ++i)
         if (!once()) ++*bad;
-    const auto t1 = std::chrono::steady_clock::now();
+    const auto t1 = Clock::now();
+    *start = t0;
+    *end = t1;
     *us_out = std::chrono::duration<double, std::micro>(t1 - t0).count() / iters;
     cts_host_free(e, host);
     cts_host_free(e, hd);
@@ -129,23 +143,33 @@ int main(int argc, char** argv)
                 if (threads == 16 && slices != 64) continue;
                 std::vector<double> us(threads, 0.0);
                 std::vector<int> bad(threads, 0), rc(threads, 0);
+                std::vector<Clock::time_point> t_start(threads), t_end(threads);
+                Gate gate;
+                gate.threads = threads;
                 std::vector<std::thread> th;
                 if (spin >= 3) (void)cts_engine_set_attr(e, CTS_ATTR_SYNC_MAILBOX, spin == 3 ? 1 : 0);
                 for (uint32_t t = 0; t < threads; ++t)
-                    th.emplace_back([&, t] { rc[t] = run_thread(e, slices, spin == 1, spin == 2, iters, &us[t], &bad[t], spin >= 3); });
+                    th.emplace_back([&, t] { rc[t] = run_thread(e, slices, spin == 1, spin == 2, iters, &us[t], &bad[t], spin >= 3, &gate,
+                                                            &t_start[t], &t_end[t]); });
                 for (auto& x : th) x.join();
-                double mean = 0;
+                double mean = 0, lo = 1e30, hi = 0;
                 int nbad = 0, nrc = 0;
+                Clock::time_point first = t_start[0], last = t_end[0];
                 for (uint32_t t = 0; t < threads; ++t) {
                     mean += us[t] / threads;
+                    lo = std::min(lo, us[t]);
+                    hi = std::max(hi, us[t]);
                     nbad += bad[t];
                     nrc += rc[t];
+                    first = std::min(first, t_start[t]);
+                    last = std::max(last, t_end[t]);
                 }
+                const double wall_s = std::chrono::duration<double>(last - first).count();
                 std::printf("{\"wait\": \"%s\", \"threads\": %u, \"slices\": %u, \"us_per_verify\": %.2f, "
-                            "\"GBps_total\": %.2f, \"bad\": %d, \"rc\": %d}\n",
+                            "\"us_min_thread\": %.2f, \"us_max_thread\": %.2f, \"GBps_wall\": %.2f, \"bad\": %d, \"rc\": %d}\n",
                             spin == 4 ? "host_launch" : spin == 3 ? "host_mailbox" : spin == 2 ? "mailbox" : spin ? "query_spin" : "stream_sync",
-                            threads, slices, mean,
-                            threads * 65536.0 / (mean * 1e3), nbad, nrc);
+                            threads, slices, mean, lo, hi,
+                            threads * (double)iters * 65536.0 / (wall_s * 1e9), nbad, nrc);
                 std::fflush(stdout);
             }
     cts_engine_destroy(e);
