@@ -150,6 +150,135 @@ __global__ void __launch_bounds__(256) read_ldsdma(const u32x4* __restrict__ p, 
     if (acc == 0x12345678u) out[0] = acc;
 }
 
+// Static slabs, then a dynamically claimed tail: block b reads slabs b, b + G, ... below nstatic * G
+// (the verify's shape), then the remaining slabs as ITEM-chunk work items drawn from 8 per-XCD pools
+// (one head counter per pool, each on its own 128-B line; a block draws from its own XCD's pool and
+// steals from the others once that is dry). The next item is claimed while the current one streams.
+// Heads come in two sets: launch k uses set k & 1 and zeroes the other set for launch k + 1 (launches on
+// one stream only). nread counts the chunks read (checked against the arena by the host).
+template <int U, int ITEM, int STEAL>
+__global__ void __launch_bounds__(256) read_dyntail(const u32x4* __restrict__ p, uint32_t nslabs, uint32_t nstatic,
+                                                    uint32_t* heads, uint32_t set, uint32_t* nread, uint32_t* out)
+{
+    // STEAL 0: a block draws from its own XCD's pool only; 1: then from the others one returning atomic at a
+    // time; 2: then wave 0 probes all 8 heads with one parallel load, claims from the first open pool
+    // (rotated from its own) and leaves after one probe that finds every pool dry.
+    constexpr uint32_t PER = 4096u;  // chunks per 64 KiB slab
+    static_assert(ITEM % (256 * U) == 0 && PER % ITEM == 0, "item shape");
+    if (blockIdx.x == 0 && threadIdx.x < 8)
+        __hip_atomic_store(&heads[((set ^ 1u) * 8u + threadIdx.x) * 32u], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t* h = heads + set * 8u * 32u;
+    uint32_t acc = 0, cnt = 0;
+    const uint32_t G = gridDim.x;
+    const uint32_t dyn0 = nstatic * G < nslabs ? nstatic * G : nslabs;
+    for (uint32_t sl = blockIdx.x; sl < dyn0; sl += G) {
+        const u32x4* q = p + (uint64_t)sl * PER;
+        for (uint32_t c = threadIdx.x; c < PER; c += 256u * U) {
+            u32x4 d[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) d[u] = __builtin_nontemporal_load(q + c + u * 256u);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc |= d[u][0] ^ d[u][1] ^ d[u][2] ^ d[u][3];
+            cnt += U;
+        }
+        acc = __syncthreads_or(acc == 0x12345678u) ? 1u : acc;
+    }
+    const uint32_t items = (nslabs - dyn0) * (PER / ITEM);
+    const uint32_t pool = (items + 7u) / 8u;
+    uint32_t xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    xcc &= 7u;
+    __shared__ uint32_t slot[2];
+    uint32_t dry = 0;  // pools seen empty (wave 0, wave-uniform)
+    const uint32_t lane = threadIdx.x;
+    auto hi_of = [&](uint32_t x) { return x * pool + pool < items ? x * pool + pool : items; };
+    // wave 0 only (all its lanes)
+    auto other = [&]() -> uint32_t {
+        if constexpr (STEAL == 0) {
+            return ~0u;
+        } else if constexpr (STEAL == 1) {
+            uint32_t r = ~0u;
+            if (lane == 0) {
+                for (uint32_t t = 0; t < 8u; ++t) {
+                    const uint32_t x = (xcc + t) & 7u;
+                    if (dry & (1u << x)) continue;
+                    if (x * pool < hi_of(x)) {
+                        const uint32_t v = __hip_atomic_fetch_add(&h[x * 32u], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if (x * pool + v < hi_of(x)) { r = x * pool + v; break; }
+                    }
+                    dry |= 1u << x;
+                }
+            }
+            return __shfl(r, 0);
+        } else {
+            for (;;) {
+                bool open = false;
+                if (lane < 8u && !(dry & (1u << lane)) && lane * pool < hi_of(lane)) {
+                    const uint32_t v = __hip_atomic_load(&h[lane * 32u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    open = lane * pool + v < hi_of(lane);
+                }
+                const uint32_t m = (uint32_t)__ballot(open) & 0xFFu;
+                dry |= ~m & 0xFFu;
+                if (!m) return ~0u;
+                const uint32_t rot = ((m >> xcc) | (m << (8u - xcc))) & 0xFFu;
+                const uint32_t x = (xcc + (uint32_t)__builtin_ctz(rot)) & 7u;
+                uint32_t r = ~0u;
+                if (lane == 0) {
+                    const uint32_t v = __hip_atomic_fetch_add(&h[x * 32u], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (x * pool + v < hi_of(x)) r = x * pool + v;
+                }
+                r = __shfl(r, 0);
+                if (r != ~0u) return r;
+                dry |= 1u << x;
+            }
+        }
+    };
+    if (lane < 64u) {
+        uint32_t r = ~0u;
+        if (items && lane == 0) {
+            const uint32_t v = __hip_atomic_fetch_add(&h[xcc * 32u], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (xcc * pool + v < hi_of(xcc)) r = xcc * pool + v;
+        }
+        r = __shfl(r, 0);
+        if (items && r == ~0u) { dry |= 1u << xcc; r = other(); }
+        if (lane == 0) slot[0] = r;
+    }
+    __syncthreads();
+    uint32_t cur = slot[0], par = 1;
+    while (cur != ~0u) {
+        uint32_t v = 0;
+        const bool own = !(dry & (1u << xcc));
+        if (lane == 0 && own) v = __hip_atomic_fetch_add(&h[xcc * 32u], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t sl = dyn0 + cur / (PER / ITEM), part = cur % (PER / ITEM);
+        const u32x4* q = p + (uint64_t)sl * PER + part * ITEM;
+        for (uint32_t c = threadIdx.x; c < ITEM; c += 256u * U) {
+            u32x4 d[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) d[u] = __builtin_nontemporal_load(q + c + u * 256u);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc |= d[u][0] ^ d[u][1] ^ d[u][2] ^ d[u][3];
+            cnt += U;
+        }
+        if (lane < 64u) {
+            uint32_t r = ~0u;
+            if (lane == 0 && own && xcc * pool + v < hi_of(xcc)) r = xcc * pool + v;
+            r = __shfl(r, 0);
+            if (r == ~0u) {
+                dry |= 1u << xcc;
+                r = other();
+            }
+            if (lane == 0) slot[par] = r;
+        }
+        __syncthreads();
+        cur = slot[par];
+        par ^= 1u;
+    }
+    if (nread && threadIdx.x == 0) atomicAdd(nread, cnt * 256u);  // every lane reads the same chunk count
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
 // write reference for the fill kernel: the same slab shape, 16-byte stores (POL 0 = nontemporal,
 // 1 = plain, 2 = write-through sc1 via an agent-scope relaxed atomic store of each dword)
 template <int U, int POL = 0>
@@ -272,6 +401,49 @@ int main(int argc, char** argv)
                BPC, ms * 1e3, bytes / (ms * 1e-3) / 1e9);                                                       \
     } while (0)
 
+#define RUN_DYN(U, ITEM, NSTATIC, BPC, ST)                                                                            \
+    do {                                                                                                          \
+        const uint32_t nsl = (uint32_t)(arena / 65536);                                                           \
+        const uint32_t grid = (uint32_t)cus * (BPC);                                                              \
+        CHECK(hipMemsetAsync(heads, 0, 2 * 8 * 32 * 4, s));                                                       \
+        CHECK(hipMemsetAsync(nread, 0, 4, s));                                                                    \
+        read_dyntail<U, ITEM, ST><<<grid, 256, 0, s>>>(bufs[0], nsl, NSTATIC, heads, 0u, nread, out);                 \
+        uint32_t got = 0;                                                                                         \
+        CHECK(hipMemcpy(&got, nread, 4, hipMemcpyDeviceToHost));                                                  \
+        CHECK(hipMemsetAsync(heads, 0, 2 * 8 * 32 * 4, s));                                                       \
+        CHECK(hipStreamSynchronize(s));                                                                           \
+        uint32_t k = 0;                                                                                           \
+        float ms = time_ms(                                                                                       \
+            [&](int i) {                                                                                          \
+                read_dyntail<U, ITEM, ST><<<grid, 256, 0, s>>>(bufs[i % R], nsl, NSTATIC, heads, k & 1u, nullptr, out); \
+                ++k;                                                                                              \
+            },                                                                                                    \
+            reps, s);                                                                                             \
+        printf("{\"kind\":\"dyntail\",\"steal\":%d,\"U\":%d,\"item_KiB\":%d,\"nstatic\":%d,\"blocks_per_cu\":%d,\"chunks_ok\":%d,"  \
+               "\"us\":%.2f,\"GBps\":%.1f}\n",                                                                     \
+               ST, U, (ITEM) / 64, NSTATIC, BPC, (int)(got == nchunks), ms * 1e3, arena / (ms * 1e-3) / 1e9);          \
+    } while (0)
+
+    const bool dyn = argc > 8 && atoi(argv[8]) != 0;
+    if (dyn) {
+        uint32_t *heads, *nread;
+        CHECK(hipMalloc(&heads, 2 * 8 * 32 * 4));
+        CHECK(hipMalloc(&nread, 4));
+        for (int pass = 0; pass < 3; ++pass) {
+            RUN_SLABGS(2, true, false, 4);
+            RUN_DYN(2, 2048, 3, 4, 0);
+            RUN_DYN(2, 2048, 3, 4, 1);
+            RUN_DYN(2, 2048, 3, 4, 2);
+            RUN_DYN(2, 1024, 3, 4, 0);
+            RUN_DYN(2, 1024, 3, 4, 2);
+            RUN_DYN(2, 4096, 2, 4, 0);
+            RUN_DYN(2, 4096, 2, 4, 2);
+            RUN_DYN(2, 2048, 2, 4, 2);
+            RUN_DYN(2, 4096, 0, 4, 0);
+            RUN_DYN(2, 4096, 0, 4, 2);
+        }
+        return 0;
+    }
     const bool timeline = argc > 7 && atoi(argv[7]) != 0;
     if (timeline) {
         // one timeline per (U, blocks per CU): 3 launches each, the last one's stamps printed as percentiles

@@ -9,6 +9,10 @@
 //   line16    every round, lanes 0..7 store 16 B each (128 B, one line)
 //   burst     every 8th round, lanes 0..59 store 16 B each (960 B per 32 KiB read)
 //   wt        dword with write-through (sc1) stores
+//   *_deferred the round's outputs stored after the NEXT round's loads are issued (a store counts in
+//             vmcnt, in issue order with the loads: stored before them, its ack joins their wait)
+//   dword_everyK / dword_once_at_end: the dword shape on every K-th round only / once per wave at its end
+//   frac_NB   (argv: any two arguments) dword stores of N bytes per 4 KiB read, N = 4 .. 120
 //   phasedP_B the dword outputs of P rounds kept in LDS, then written by every workgroup at once: a
 //             co-resident grid meets at a grid barrier (B = 1: before the write phase; B = 2: before and
 //             after it), so the memory sees read phases and write phases instead of a mix
@@ -30,11 +34,23 @@ __global__ void __launch_bounds__(256) rw_kernel(const u32x4* __restrict__ p, ui
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     const uint64_t stride = (uint64_t)gridDim.x * 256u * U;
     uint64_t c = (uint64_t)blockIdx.x * 256u * U + threadIdx.x;
+    // MODE 6/7: the previous round's output, stored after this round's loads, by every lane with no branch
+    // (an exec-skip branch around the store makes the compiler's vmcnt at the join count it as if issued:
+    // the loads' wait would then include it). Round 0 stores a placeholder to its own slot, overwritten later.
+    uint32_t pend_v = 0;
+    uint64_t pend_slot = ((c - threadIdx.x) / (256u * U)) * 4u + wave;
     for (uint64_t r = 0; c + 256u * (U - 1) < nchunks; c += stride, ++r) {
         u32x4 d[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) d[u] = __builtin_nontemporal_load(p + c + u * 256u);
         __builtin_amdgcn_sched_barrier(0);
+        if constexpr (MODE == 6) {
+            out[pend_slot * 32u + (lane < 30u ? lane : 29u)] = pend_v;
+            __builtin_amdgcn_sched_barrier(0);
+        } else if constexpr (MODE == 7) {
+            *reinterpret_cast<u32x4*>(out + pend_slot * 32u + 4u * (lane & 7u)) = u32x4{pend_v, pend_v, pend_v, pend_v};
+            __builtin_amdgcn_sched_barrier(0);
+        }
 #pragma unroll
         for (int u = 0; u < U; ++u) acc |= d[u][0] ^ d[u][1] ^ d[u][2] ^ d[u][3];
         // this wave's 4 KiB of the round: output slot = global round-wave index
@@ -51,8 +67,19 @@ __global__ void __launch_bounds__(256) rw_kernel(const u32x4* __restrict__ p, ui
                 *reinterpret_cast<u32x4*>(out + (slot / 8u) * 256u + 4u * lane) = u32x4{v, v, v, v};
         } else if constexpr (MODE == 5) {
             if (lane < 30u) __hip_atomic_store(out + slot * 32u + lane, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else if constexpr (MODE == 9) {
+            if ((r & 15u) == 15u && lane < 30u) out[slot * 32u + lane] = v;
+        } else if constexpr (MODE == 10) {
+            if ((r & 63u) == 63u && lane < 30u) out[slot * 32u + lane] = v;
+        } else if constexpr (MODE == 6 || MODE == 7 || MODE == 8) {
+            pend_v = v;
+            pend_slot = slot;
+        } else if constexpr (MODE > 100) {  // write fraction sweep: lanes 0..MODE-101 store one dword each
+            if (lane < (uint32_t)(MODE - 100)) out[slot * 32u + lane] = v;
         }
     }
+    if constexpr (MODE == 6 || MODE == 7 || MODE == 8)
+        if (lane < 30u) out[pend_slot * 32u + lane] = pend_v;
     if (acc == 0x12345678u) out[0] = acc;
 }
 
@@ -196,6 +223,25 @@ int main(int argc, char**)
         run<3>("line16", p, nchunks, out, grid);
         run<4>("burst", p, nchunks, out, grid);
         run<5>("wt_sc1", p, nchunks, out, grid);
+    }
+    if (argc > 2) {  // how the cost scales with the written fraction (dword shape, bytes per 4 KiB read)
+        for (int pass = 0; pass < 2; ++pass) {
+            run<0>("none", p, nchunks, out, 2048);
+            run<101>("frac_4B", p, nchunks, out, 2048);
+            run<102>("frac_8B", p, nchunks, out, 2048);
+            run<104>("frac_16B", p, nchunks, out, 2048);
+            run<108>("frac_32B", p, nchunks, out, 2048);
+            run<115>("frac_60B", p, nchunks, out, 2048);
+            run<130>("frac_120B", p, nchunks, out, 2048);
+            run<1>("dword", p, nchunks, out, 2048);
+            run<6>("dword_deferred", p, nchunks, out, 2048);
+            run<3>("line16", p, nchunks, out, 2048);
+            run<7>("line16_deferred", p, nchunks, out, 2048);
+            run<9>("dword_every16", p, nchunks, out, 2048);
+            run<10>("dword_every64", p, nchunks, out, 2048);
+            run<8>("dword_once_at_end", p, nchunks, out, 2048);
+        }
+        return 0;
     }
     if (argc > 1) {
         run<0>("none", p, nchunks, out, 2048);
