@@ -556,6 +556,16 @@ def run_extras(engine, torch, W, w, arenas, descs, dev, want):
             t = _time_kernel(torch, lambda i: MS.verify_strided(engine, ad, wd.max_length, lens, records=recs,
                                                                 results=res), 10)
             out["media_stream_strided_verify_GiBps"] = round(wd.verified_bytes() / t / GIB, 1)
+            # the compact receive pass: one 16-byte cts_datagram_status per datagram instead of record + result
+            st = torch.empty(wd.n * 16, dtype=torch.uint8, device=dev)
+            ctr_c = engine.new_counters()
+            t = _time_kernel(torch, lambda i: MS.verify_status(engine, ad, dd, status=st, counters=ctr_c), 10)
+            out["media_stream_status_verify_GiBps"] = round(wd.verified_bytes() / t / GIB, 1)
+            t = _time_kernel(torch, lambda i: MS.verify_strided_status(engine, ad, wd.max_length, lens, status=st), 10)
+            out["media_stream_strided_status_verify_GiBps"] = round(wd.verified_bytes() / t / GIB, 1)
+            out["media_stream_status_parity"] = bool(
+                engine.read_counters(ctr_c)["buffers_failed"] == 11 * len(np.unique(wd.corrupt_buf)))
+            del st
             del lens
             del recs, res
             del ad, dd

@@ -684,6 +684,39 @@ int cts_media_stream_verify_strided(cts_engine* e, const void* dev_arena, uint64
                                                               static_cast<hipStream_t>(stream), e->geo));
 }
 
+int cts_media_stream_verify_status(cts_engine* e, const void* dev_arena, uint64_t arena_bytes,
+                                   const cts_buf_desc* dev_descs, uint32_t n, cts_datagram_status* dev_status,
+                                   void* dev_counters, void* stream)
+{
+    if (e == nullptr) return CTS_E_INVALID;
+    if (n == 0) return CTS_OK;
+    if (dev_arena == nullptr || dev_descs == nullptr || ((uintptr_t)dev_descs & 7u) != 0 || ((uintptr_t)dev_arena & 15u) != 0 ||
+        ((uintptr_t)dev_status & 3u) != 0)
+        return CTS_E_INVALID;
+    DeviceGuard g(e->device);
+    if (!g.ok) return CTS_E_HIP;
+    return hip_status(cts::launch_media_stream_status(static_cast<const uint8_t*>(dev_arena), arena_bytes, dev_descs,
+                                                      nullptr, 0u, n, dev_status, static_cast<uint64_t*>(dev_counters),
+                                                      static_cast<hipStream_t>(stream), e->geo));
+}
+
+int cts_media_stream_verify_strided_status(cts_engine* e, const void* dev_arena, uint64_t arena_bytes, uint32_t stride,
+                                           const uint32_t* dev_lengths, uint32_t n, cts_datagram_status* dev_status,
+                                           void* dev_counters, void* stream)
+{
+    if (e == nullptr) return CTS_E_INVALID;
+    if (n == 0) return CTS_OK;
+    if (dev_arena == nullptr || dev_lengths == nullptr || ((uintptr_t)dev_lengths & 3u) != 0 ||
+        ((uintptr_t)dev_arena & 15u) != 0 || arena_bytes < 16u || stride == 0 || ((uintptr_t)dev_status & 3u) != 0)
+        return CTS_E_INVALID;
+    DeviceGuard g(e->device);
+    if (!g.ok) return CTS_E_HIP;
+    return hip_status(cts::launch_media_stream_status(static_cast<const uint8_t*>(dev_arena), arena_bytes, nullptr,
+                                                      dev_lengths, stride, n, dev_status,
+                                                      static_cast<uint64_t*>(dev_counters),
+                                                      static_cast<hipStream_t>(stream), e->geo));
+}
+
 size_t cts_counters_device_bytes(void) { return (size_t)CTS_COUNTER_SHARDS * cts::kCounterSlots * sizeof(uint64_t); }
 
 int cts_counters_reset(cts_engine* e, void* dev_counters, void* stream)

@@ -25,9 +25,9 @@ constexpr int kDefaultVerifyVariant = 13;
 constexpr int kDefaultSmallVariant = 9;
 constexpr int kDefaultMediaStreamVariant = 3;
 #if CTS_TUNING
-constexpr int kVerifyVariants = 18;  // workgroup-per-buffer verify variants (launch_verify)
+constexpr int kVerifyVariants = 19;  // workgroup-per-buffer verify variants (launch_verify)
 constexpr int kSmallVariants = 10;   // small-buffer (datagram) verify variants
-constexpr int kMediaStreamVariants = 4;  // MediaStream receive kernels (launch_media_stream_verify)
+constexpr int kMediaStreamVariants = 7;  // MediaStream receive kernels (launch_media_stream_verify)
 #endif
 // A launch-variant attribute value this build can launch.
 inline bool variant_ok(int value, int dflt, int count)
@@ -149,6 +149,11 @@ hipError_t launch_media_stream_verify_strided(const uint8_t* arena, uint64_t are
                                              const uint32_t* lengths, uint32_t n, cts_datagram_record* records,
                                              cts_verify_result* results, uint64_t* counters, hipStream_t stream,
                                              const LaunchGeometry& geo);
+
+// The receive pass writing 16-byte statuses (cts_media_stream_verify_status); descs == nullptr: the strided ring.
+hipError_t launch_media_stream_status(const uint8_t* arena, uint64_t arena_bytes, const cts_buf_desc* descs,
+                                     const uint32_t* lengths, uint32_t stride, uint32_t n, cts_datagram_status* status,
+                                     uint64_t* counters, hipStream_t stream, const LaunchGeometry& geo);
 
 hipError_t launch_media_stream_fill(uint8_t* arena, uint64_t arena_bytes, const cts_buf_desc* descs,
                                    const cts_datagram_header* headers, uint32_t n, hipStream_t stream,

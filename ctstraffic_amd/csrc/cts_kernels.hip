@@ -539,12 +539,23 @@ __device__ __forceinline__ void write_bad(cts_verify_result* results, uint32_t i
 }
 
 // Record one verified buffer (called by the team leader).
+// rslot != nullptr: the record goes there (an LDS staging slot) instead of to results[i].
 __device__ __forceinline__ void finish_buffer(const Span& s, const cts_buf_desc& d, uint32_t i, uint32_t first,
                                               uint32_t count, cts_verify_result* results, uint64_t* tc,
-                                              uint32_t* conn_first_fail, uint32_t n_conns)
+                                              uint32_t* conn_first_fail, uint32_t n_conns,
+                                              cts_verify_result* rslot = nullptr)
 {
     const bool pass = (first == kNone);
-    if (results != nullptr) {
+    if (rslot != nullptr) {
+        cts_verify_result r;
+        r.first_mismatch = pass ? s.len : first;
+        r.mismatch_bytes = pass ? 0u : count;
+        r.expected = pass ? 0 : (uint8_t)pattern_byte_dev(s.expected + first);
+        r.actual = pass ? 0 : s.sp[first];
+        r.pass = pass ? 1 : 0;
+        r.flags = 0;
+        *rslot = r;
+    } else if (results != nullptr) {
         cts_verify_result r;
         r.first_mismatch = pass ? s.len : first;
         r.mismatch_bytes = pass ? 0u : count;
@@ -619,6 +630,24 @@ __device__ __forceinline__ void block_reduce_mismatch(uint32_t& first, uint32_t&
     block_reduce_mismatch_with(first, count, red);
 }
 
+// Wave 0 writes the m result records staged in LDS (record j belongs to buffer idx[j]) as dwords, one
+// store instruction for up to 21 records.
+template <int R>
+__device__ __forceinline__ void flush_staged_results(const cts_verify_result* st, const uint32_t* idx, uint32_t m,
+                                                     cts_verify_result* results)
+{
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t l = threadIdx.x;
+#pragma unroll
+    for (uint32_t k = 0; k < (3u * R + 63u) / 64u; ++k) {
+        const uint32_t e = k * 64u + l, j = e / 3u;
+        if (j < m)
+            reinterpret_cast<uint32_t*>(results)[3ull * idx[j] + (e - 3u * j)] =
+                reinterpret_cast<const uint32_t*>(st)[e];
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
 // ---------------------------------------------------------------------------------------------
 // One 256-lane workgroup per buffer (grid-strides over buffers). The next
 // buffer's descriptor is fetched while the current one streams.
@@ -628,14 +657,30 @@ __device__ __forceinline__ void block_reduce_mismatch(uint32_t& first, uint32_t&
 // WIN > 1: the descriptor list is cut into WIN contiguous windows and workgroup b walks window
 // b % WIN with stride gridDim.x / WIN (the launcher makes the grid a multiple of WIN), so WIN
 // far-apart regions of the arena stream at once instead of one 1024-buffer front.
-template <int U, bool NT, bool SPLIT = false, bool SCTR = false, bool WHOLE = false, bool XD = false, int WIN = 1>
+// DEFER = R > 0: per-buffer result records are staged in LDS and written R at a time by wave 0 (and
+// at the end), so the read stream sees a write every R buffers instead of every buffer (a read stream
+// slows with the frequency of the writes mixed into it: tools/rw_mix_probe.hip).
+template <int U, bool NT, bool SPLIT = false, bool SCTR = false, bool WHOLE = false, bool XD = false, int WIN = 1,
+          int DEFER = 0>
 __global__ void __launch_bounds__(kBlock, (U <= 8 ? 8 : 4))
     verify_wg_kernel(const uint8_t* __restrict__ arena, uint64_t arena_bytes, const cts_buf_desc* __restrict__ descs,
                      uint32_t n, cts_verify_result* __restrict__ results, uint64_t* __restrict__ counters,
                      uint32_t* __restrict__ conn_first_fail, uint32_t n_conns)
 {
+    static_assert(!(SCTR && DEFER), "deferred results take the finish_buffer path");
     __shared__ uint64_t ctr[1][5];
+    __shared__ cts_verify_result dres[DEFER ? DEFER : 1];
+    __shared__ uint32_t didx[DEFER ? DEFER : 1];
     const uint32_t lane = threadIdx.x;
+    uint32_t dk = 0;  // DEFER: records staged (uniform)
+    const bool defer = DEFER > 0 && results != nullptr;
+    // DEFER: count the record lane 0 just staged; wave 0 writes a full staging area
+    auto staged = [&]() {
+        if (++dk == (uint32_t)DEFER) {
+            if (lane < 64u) flush_staged_results<DEFER ? DEFER : 1>(dres, didx, dk, results);
+            dk = 0;
+        }
+    };
     zero_counters<1>(ctr);
     uint64_t ok_bytes = 0;     // SCTR: bytes of clean buffers (uniform)
     uint32_t ok_buffers = 0;   // SCTR: clean buffers (uniform)
@@ -655,7 +700,15 @@ __global__ void __launch_bounds__(kBlock, (U <= 8 ? 8 : 4))
         const cts_buf_desc d = dn;
         if ((uint64_t)i + step < end) dn = descs[i + step];
         if (desc_bad(d, arena_bytes)) {
-            if (lane == 0) write_bad(results, i);
+            if (DEFER && defer) {
+                if (lane == 0) {
+                    write_bad(dres + dk, 0);
+                    didx[dk] = i;
+                }
+                staged();
+            } else if (lane == 0) {
+                write_bad(results, i);
+            }
             continue;
         }
         const Span s = make_span(arena, d);
@@ -694,8 +747,18 @@ __global__ void __launch_bounds__(kBlock, (U <= 8 ? 8 : 4))
                 continue;
             }
         }
-        if (lane == 0) finish_buffer(s, d, i, first, count, results, ctr[0], conn_first_fail, n_conns);
+        if (DEFER && defer) {
+            if (lane == 0) {
+                finish_buffer(s, d, i, first, count, results, ctr[0], conn_first_fail, n_conns, dres + dk);
+                didx[dk] = i;
+            }
+            staged();
+        } else if (lane == 0) {
+            finish_buffer(s, d, i, first, count, results, ctr[0], conn_first_fail, n_conns);
+        }
     }
+    if constexpr (DEFER > 0)
+        if (dk && lane < 64u) flush_staged_results<DEFER>(dres, didx, dk, results);
     if constexpr (SCTR) {
         if (lane == 0) {
             ctr[0][kBytesChecked] += ok_bytes;
@@ -1025,9 +1088,11 @@ __device__ __forceinline__ void quad_stage_result(QuadOut& o, uint32_t t, uint32
 }
 
 // All 64 lanes of the wave call this after the leaders staged; i = this lane's buffer index
-// (the wave's four teams hold i0 .. i0 + 3, i0 = lane 0's), n = buffers in the launch.
+// (the wave's four teams hold i0 .. i0 + 3, i0 = lane 0's), n = buffers in the launch. RECDW = dwords per
+// record: 8 (cts_datagram_record) or 4 (cts_datagram_status, staged in rec[t][0..3]).
+template <int RECDW = 8>
 __device__ __forceinline__ void quad_flush_outputs(const QuadOut& o, uint32_t i, uint32_t n,
-                                                   cts_verify_result* results, cts_datagram_record* records)
+                                                   cts_verify_result* results, void* records)
 {
     __builtin_amdgcn_wave_barrier();
     // (64-bit: i0 + t may pass 2^32 on the wave's last round when n is close to it)
@@ -1038,12 +1103,58 @@ __device__ __forceinline__ void quad_flush_outputs(const QuadOut& o, uint32_t i,
         const uint32_t v = o.res[t][l - 3u * t];
         if (i0 + t < n) reinterpret_cast<uint32_t*>(results)[3ull * i0 + l] = v;
     }
-    if (records != nullptr && l < 32u) {
-        const uint32_t t = l >> 3;
-        const uint32_t v = o.rec[t][l & 7u];
+    if (records != nullptr && l < 4u * RECDW) {
+        const uint32_t t = l / RECDW;
+        const uint32_t v = o.rec[t][l % RECDW];
         if (i0 + t < n)
-            __hip_atomic_store(reinterpret_cast<uint32_t*>(records) + 8ull * i0 + l, v, __ATOMIC_RELAXED,
+            __hip_atomic_store(reinterpret_cast<uint32_t*>(records) + (uint64_t)RECDW * i0 + l, v, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
+// Per-wave output ring: the staged outputs of K rounds (QuadOut slots) and each round's first buffer
+// index, written by the wave every K rounds instead of every round. A read stream slows down with the
+// FREQUENCY of the writes mixed into it, not with their bytes (tools/rw_mix_probe.hip: one dword per wave
+// per 4 KiB round costs the read 18 %, the same store on every 16th round 5 %, on every 64th round
+// nothing measurable; 4 to 120 bytes per store cost the same).
+template <int K>
+struct QuadRing {
+    QuadOut slot[K];
+    uint32_t i0[K];
+};
+
+// All 64 lanes: write rounds [0, m) of the ring (round j's four buffers start at i0[j]); n = buffers in
+// the launch. Records go as write-through dwords (as quad_flush_outputs), 32 per round, results as
+// plain dwords, 12 per round.
+template <int K>
+__device__ __forceinline__ void quad_ring_flush(const QuadRing<K>& g, uint32_t m, uint32_t n,
+                                                cts_verify_result* results, void* records)
+{
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t l = threadIdx.x & 63u;
+    if (records != nullptr) {
+#pragma unroll 1  // (unrolled, the LDS reads are hoisted into ~80 VGPRs: occupancy 4 -> 2 waves/SIMD)
+        for (uint32_t k = 0; k < (K * 32u + 63u) / 64u; ++k) {
+            const uint32_t e = k * 64u + l, j = e >> 5, d = e & 31u;
+            if (j < m) {
+                const uint64_t i0 = g.i0[j];
+                if (i0 + (d >> 3) < n)
+                    __hip_atomic_store(reinterpret_cast<uint32_t*>(records) + 8ull * i0 + d, g.slot[j].rec[d >> 3][d & 7u],
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    }
+    if (results != nullptr) {
+#pragma unroll 1
+        for (uint32_t k = 0; k < (K * 12u + 63u) / 64u; ++k) {
+            const uint32_t e = k * 64u + l, j = e / 12u, d = e - 12u * j;
+            if (j < m) {
+                const uint64_t i0 = g.i0[j];
+                const uint32_t t = d / 3u;
+                if (i0 + t < n) reinterpret_cast<uint32_t*>(results)[3ull * i0 + d] = g.slot[j].res[t][d - 3u * t];
+            }
+        }
     }
     __builtin_amdgcn_wave_barrier();
 }
@@ -1572,15 +1683,21 @@ __device__ __forceinline__ void ms_datagram(const MsSource& src, uint32_t i, uin
 // HDR16 = false: header bytes j and j + 16 by byte loads on every team lane, dwords gathered by
 // lane shuffles (ms_variant 1). HDR16 = true: three 16-byte header chunk loads on team lanes
 // 0..2, gathered on lane 0 by DPP row shifts; the DATA verdict is broadcast (ms_variant 2).
-template <int U, bool NT, bool ALIGN, bool HDR16, bool CONTIG = false, bool STRIDED = false>
+// RING > 0: outputs staged in a per-wave ring of RING rounds and written every RING rounds (QuadRing).
+// STATUS: records points at 16-byte cts_datagram_status entries (results unused).
+template <int U, bool NT, bool ALIGN, bool HDR16, bool CONTIG = false, bool STRIDED = false, int RING = 0,
+          bool STATUS = false>
 __global__ void __launch_bounds__(kBlock)
     media_stream_verify_quad_kernel(const uint8_t* __restrict__ arena, uint64_t arena_bytes, MsSource src, uint32_t n,
-                                    cts_datagram_record* __restrict__ records, cts_verify_result* __restrict__ results,
+                                    void* __restrict__ records, cts_verify_result* __restrict__ results,
                                     uint64_t* __restrict__ counters, uint32_t per = 0)
 {
+    static_assert(!(RING && STATUS), "the ring writes full records");
     constexpr int TEAMS = kBlock / kQuadTeam;
     __shared__ uint64_t ctr[TEAMS][5];
-    __shared__ QuadOut qout[kBlock / 64];
+    __shared__ QuadOut qout[RING ? 1 : kBlock / 64];
+    __shared__ QuadRing<RING ? RING : 1> qring[RING ? kBlock / 64 : 1];
+    uint32_t rs = 0;  // RING: this wave's next ring slot (wave-uniform)
     const uint32_t lane = threadIdx.x & (kQuadTeam - 1);
     const uint32_t team = threadIdx.x / kQuadTeam;
     // dummy target of an empty span's clamped loads: 16-byte-aligned bytes the launch owns
@@ -1676,9 +1793,15 @@ __global__ void __launch_bounds__(kBlock)
             quad_team_reduce(first, count);
         }
         if (lane == 0u && live) {
-            QuadOut& o = qout[team >> 2];
+            QuadOut& o = RING ? qring[RING ? team >> 2 : 0].slot[rs] : qout[RING ? 0 : team >> 2];
             const uint32_t t = team & 3u;
-            if (records != nullptr) {
+            if (STATUS && records != nullptr) {
+                // cts_datagram_status as dwords: seq, completed bytes, flag | kind | pass
+                o.rec[t][0] = data ? (H[0] >> 16) | (H[1] << 16) : 0u;
+                o.rec[t][1] = data ? (H[1] >> 16) | (H[2] << 16) : 0u;
+                o.rec[t][2] = completed;
+                o.rec[t][3] = (flag & 0xFFFFu) | (kind << 16) | ((data && first == kNone) ? 1u << 24 : 0u);
+            } else if (records != nullptr) {
                 // cts_datagram_record as dwords: seq = header bytes 2..9 (GetSequenceNumberFromTask);
                 // ctsIOPatternMediaStream.cpp:218-219 read the sender qpc / qpf at bytes 8 and 16
                 o.rec[t][0] = data ? (H[0] >> 16) | (H[1] << 16) : 0u;
@@ -1703,9 +1826,21 @@ __global__ void __launch_bounds__(kBlock)
                 qc.add(q.len, pass, count);
             }
         }
-        quad_flush_outputs(qout[team >> 2], i, w.end, results, records);
+        if constexpr (RING == 0) {
+            quad_flush_outputs<STATUS ? 4 : 8>(qout[team >> 2], i, w.end, STATUS ? nullptr : results, records);
+        } else {
+            QuadRing<RING>& g = qring[team >> 2];
+            const uint32_t i0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)i);
+            if ((threadIdx.x & 63u) == 0u) g.i0[rs] = i0;
+            if (++rs == (uint32_t)RING) {
+                quad_ring_flush<RING>(g, RING, w.end, results, records);
+                rs = 0;
+            }
+        }
         w.i = inext;
     }
+    if constexpr (RING > 0)
+        if (rs) quad_ring_flush<RING>(qring[team >> 2], rs, w.end, results, records);
     qc.flush<TEAMS>(ctr, team, lane, counters);
 }
 
@@ -1832,7 +1967,8 @@ static void launch_verify_nt(const uint8_t* arena, uint64_t arena_bytes, const c
         // 8 = variant 6 with clean-buffer counters in SGPRs,
         // 9 = variant 6 + whole-line spans streamed without edge/head/tail handling, 10 = same U4,
         // 11 = variant 10 with the exact diff of whole-line spans in registers (no re-read), 12 = same U8,
-        // 13 = same U2, 14 = same U1, 15/16/17 = variant 13 walking 2/4/8 windows of the descriptor list
+        // 13 = same U2, 14 = same U1, 15/16/17 = variant 13 walking 2/4/8 windows of the descriptor list,
+        // 18 = variant 13 writing its result records 16 at a time from LDS
 #if CTS_TUNING
         switch (geo.verify_variant) {
         case 4: verify_wg_nb_kernel<8, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
@@ -1848,6 +1984,7 @@ static void launch_verify_nt(const uint8_t* arena, uint64_t arena_bytes, const c
         case 15: verify_wg_kernel<2, NT, true, false, true, true, 2><<<grid_win(n, 2, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 16: verify_wg_kernel<2, NT, true, false, true, true, 4><<<grid_win(n, 4, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 17: verify_wg_kernel<2, NT, true, false, true, true, 8><<<grid_win(n, 8, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
+        case 18: verify_wg_kernel<2, NT, true, false, true, true, 1, 16><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 7: verify_wg_kernel<4, NT, true><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 1: verify_wg_kernel<4, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 2: verify_wg_kernel<16, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
@@ -2118,7 +2255,8 @@ hipError_t launch_media_stream_verify(const uint8_t* arena, uint64_t arena_bytes
 #define CTS_MS_ARGS arena, arena_bytes, MsSource{descs, nullptr, 0u}, n, records, results, counters
     // ms_variant: 0 = one wave per datagram, 1 = four datagrams per wave (header by byte loads),
     // 2 = four per wave, header by three 16-byte chunk loads + DPP, 3 = variant 2 walking
-    // block-contiguous datagram ranges (default)
+    // block-contiguous datagram ranges (default), 4 / 5 / 6 = variant 3 writing its outputs every
+    // 8 / 16 / 32 rounds from a per-wave LDS ring
     const uint32_t qgrid = grid_for(n, kBlock / kQuadTeam, geo);
     const uint32_t grid = grid_for(n, kBlock / 64, geo);
 #if CTS_TUNING
@@ -2136,6 +2274,23 @@ hipError_t launch_media_stream_verify(const uint8_t* arena, uint64_t arena_bytes
         if (nt) media_stream_verify_quad_kernel<6, true, true, true><<<qgrid, kBlock, 0, stream>>>(CTS_MS_ARGS);
         else media_stream_verify_quad_kernel<6, false, true, true><<<qgrid, kBlock, 0, stream>>>(CTS_MS_ARGS);
         break;
+    case 4:
+    case 5:
+    case 6: {  // variant 3 with its outputs written every 8 / 16 / 32 rounds from a per-wave ring
+        const ContigGrid cg = contig_grid(n, geo);
+#define CTS_MS_RING(K)                                                                                              \
+    (nt ? (media_stream_verify_quad_kernel<6, true, true, true, true, false, K><<<cg.grid, kBlock, 0, stream>>>(   \
+               CTS_MS_ARGS, cg.per),                                                                                \
+           0)                                                                                                       \
+        : (media_stream_verify_quad_kernel<6, false, true, true, true, false, K><<<cg.grid, kBlock, 0, stream>>>(  \
+               CTS_MS_ARGS, cg.per),                                                                                \
+           0))
+        if (geo.ms_variant == 4) (void)CTS_MS_RING(8);
+        else if (geo.ms_variant == 5) (void)CTS_MS_RING(16);
+        else (void)CTS_MS_RING(32);
+#undef CTS_MS_RING
+        break;
+    }
     default: {
         const ContigGrid cg = contig_grid(n, geo);
         if (nt)
@@ -2175,6 +2330,28 @@ hipError_t launch_media_stream_verify_strided(const uint8_t* arena, uint64_t are
     else
         media_stream_verify_quad_kernel<6, false, true, true, true, true><<<cg.grid, kBlock, 0, stream>>>(
             arena, arena_bytes, src, n, records, results, counters, cg.per);
+    return hipGetLastError();
+}
+
+hipError_t launch_media_stream_status(const uint8_t* arena, uint64_t arena_bytes, const cts_buf_desc* descs,
+                                     const uint32_t* lengths, uint32_t stride, uint32_t n, cts_datagram_status* status,
+                                     uint64_t* counters, hipStream_t stream, const LaunchGeometry& geo)
+{
+    if (n == 0) return hipSuccess;
+    // the variant-3 walk writing 16-byte statuses; descs == nullptr: the strided-ring form
+    const ContigGrid cg = contig_grid(n, geo);
+    const MsSource src{descs, lengths, stride};
+#define CTS_MS_STATUS(NT, STR)                                                                              \
+    media_stream_verify_quad_kernel<6, NT, true, true, true, STR, 0, true><<<cg.grid, kBlock, 0, stream>>>( \
+        arena, arena_bytes, src, n, status, nullptr, counters, cg.per)
+    if (descs == nullptr) {
+        if (geo.nontemporal) CTS_MS_STATUS(true, true);
+        else CTS_MS_STATUS(false, true);
+    } else {
+        if (geo.nontemporal) CTS_MS_STATUS(true, false);
+        else CTS_MS_STATUS(false, false);
+    }
+#undef CTS_MS_STATUS
     return hipGetLastError();
 }
 

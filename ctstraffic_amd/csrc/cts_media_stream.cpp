@@ -173,16 +173,25 @@ int cts_media_stream_client_destroy(cts_media_stream_client* c)
     return CTS_OK;
 }
 
-int cts_media_stream_client_complete(cts_media_stream_client* c, const cts_datagram_record* recs,
-                                     const cts_verify_result* res, uint32_t n, int64_t receiver_qpc,
-                                     int64_t receiver_qpf, uint32_t* consumed)
+}  // extern "C"
+
+namespace {
+// CompleteTaskBackToPattern (ctsIOPatternMediaStream.cpp:150-272) over n datagrams in completion order; at(j)
+// gives datagram j's {kind, pass, completed bytes, sequence number, sender qpc, sender qpf}.
+struct DgramView {
+    uint32_t kind, pass, completed;
+    int64_t seq, qpc, qpf;
+};
+
+template <typename At>
+int complete_datagrams(cts_media_stream_client* c, uint32_t n, At at, int64_t receiver_qpc, int64_t receiver_qpf,
+                       uint32_t* consumed)
 {
-    if (c == nullptr || (n != 0 && (recs == nullptr || res == nullptr))) return CTS_E_INVALID;
     uint32_t j = 0;
     for (; j < n && c->last_error == CTS_STATUS_IO_RUNNING; ++j) {
-        const cts_datagram_record& r = recs[j];
+        const DgramView r = at(j);
         ++c->datagrams;
-        uint32_t err = 0;  // CompleteTaskBackToPattern (:150-272)
+        uint32_t err = 0;
         switch (r.kind) {
         case CTS_DGRAM_ZERO:
             if (!c->finished) err = CTS_STATUS_ERROR_NOT_ALL_DATA_TRANSFERRED;  // zero-byte datagram: TooFewBytes
@@ -192,23 +201,23 @@ int cts_media_stream_client_complete(cts_media_stream_client* c, const cts_datag
         case CTS_DGRAM_BAD_DESC: err = CTS_STATUS_ERROR_NOT_ALL_DATA_TRANSFERRED; break;  // invalid header
         case CTS_DGRAM_ID: break;  // SetConnectionIdFromTask: see cts_media_stream_client_set_connection_id
         case CTS_DGRAM_DATA: {
-            if (!res[j].pass) {  // VerifyBuffer failed: CorruptedBytes
+            if (!r.pass) {  // VerifyBuffer failed: CorruptedBytes
                 err = CTS_STATUS_ERROR_DATA_DID_NOT_MATCH_BIT_PATTERN;
                 break;
             }
-            c->bits_received += (int64_t)r.completed_bytes * 8;
-            const int64_t seq = r.sequence_number;
+            c->bits_received += (int64_t)r.completed * 8;
+            const int64_t seq = r.seq;
             if (seq > c->final_frame) {
                 ++c->error_frames;  // an unknown seq number past the final frame
             } else {
                 const ptrdiff_t slot = c->find(seq);
                 if (slot >= 0) {
                     Frame& f = c->frames[(size_t)slot];
-                    f.sender_qpc = r.sender_qpc;
-                    f.sender_qpf = r.sender_qpf;
+                    f.sender_qpc = r.qpc;
+                    f.sender_qpf = r.qpf;
                     f.receiver_qpc = receiver_qpc;
                     f.receiver_qpf = receiver_qpf;
-                    f.bytes_received += r.completed_bytes;
+                    f.bytes_received += r.completed;
                 } else {
                     ++c->error_frames;  // a stale or a future seq number
                 }
@@ -226,6 +235,36 @@ int cts_media_stream_client_complete(cts_media_stream_client* c, const cts_datag
     if (consumed != nullptr) *consumed = j;
     if (c->last_error == CTS_STATUS_IO_RUNNING) return CTS_IO_CONTINUE;
     return c->last_error == 0 ? CTS_IO_COMPLETED : CTS_IO_FAILED;
+}
+}  // namespace
+
+extern "C" {
+
+int cts_media_stream_client_complete(cts_media_stream_client* c, const cts_datagram_record* recs,
+                                     const cts_verify_result* res, uint32_t n, int64_t receiver_qpc,
+                                     int64_t receiver_qpf, uint32_t* consumed)
+{
+    if (c == nullptr || (n != 0 && (recs == nullptr || res == nullptr))) return CTS_E_INVALID;
+    return complete_datagrams(
+        c, n,
+        [&](uint32_t j) {
+            const cts_datagram_record& r = recs[j];
+            return DgramView{r.kind, res[j].pass, r.completed_bytes, r.sequence_number, r.sender_qpc, r.sender_qpf};
+        },
+        receiver_qpc, receiver_qpf, consumed);
+}
+
+int cts_media_stream_client_complete_status(cts_media_stream_client* c, const cts_datagram_status* st, uint32_t n,
+                                            int64_t receiver_qpc, int64_t receiver_qpf, uint32_t* consumed)
+{
+    if (c == nullptr || (n != 0 && st == nullptr)) return CTS_E_INVALID;
+    return complete_datagrams(
+        c, n,
+        [&](uint32_t j) {
+            const cts_datagram_status& r = st[j];
+            return DgramView{r.kind, r.pass, r.completed_bytes, r.sequence_number, 0, 0};
+        },
+        receiver_qpc, receiver_qpf, consumed);
 }
 
 int cts_media_stream_client_set_connection_id(cts_media_stream_client* c, const char* dgram, uint32_t len)

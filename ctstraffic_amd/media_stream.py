@@ -15,7 +15,7 @@ import ctypes
 import numpy as np
 
 from ._lib import CtsError, check, lib
-from .types import DESC_DTYPE, DGRAM_HEADER_DTYPE, DGRAM_RECORD_DTYPE, RESULT_DTYPE
+from .types import DESC_DTYPE, DGRAM_HEADER_DTYPE, DGRAM_RECORD_DTYPE, DGRAM_STATUS_DTYPE, RESULT_DTYPE
 
 DGRAM_DATA, DGRAM_ID, DGRAM_ZERO, DGRAM_SHORT, DGRAM_UNKNOWN, DGRAM_BAD_DESC = range(6)
 FLAG_DATA, FLAG_ID = 0x0000, 0x1000
@@ -50,6 +50,9 @@ def declare(L: ctypes.CDLL) -> None:
         "cts_media_stream_fill": ([P, P, u64, P, P, u32, P], i32),
         "cts_media_stream_verify": ([P, P, u64, P, u32, P, P, P, P], i32),
         "cts_media_stream_verify_strided": ([P, P, u64, u32, P, u32, P, P, P, P], i32),
+        "cts_media_stream_verify_status": ([P, P, u64, P, u32, P, P, P], i32),
+        "cts_media_stream_verify_strided_status": ([P, P, u64, u32, P, u32, P, P, P], i32),
+        "cts_media_stream_client_complete_status": ([P, P, u32, i64, i64, ctypes.POINTER(u32)], i32),
         "cts_media_stream_client_create": ([ctypes.POINTER(Settings), ctypes.POINTER(P)], i32),
         "cts_media_stream_client_destroy": ([P], i32),
         "cts_media_stream_client_complete": ([P, P, P, u32, i64, i64, ctypes.POINTER(u32)], i32),
@@ -119,6 +122,39 @@ def verify_strided(engine, arena, stride: int, lengths, records=None, results=No
                                                 _ptr(records), _ptr(results), _ptr(counters), _stream(stream)))
 
 
+def _check_status(n, status):
+    from .engine import _nbytes
+
+    if status is not None and _nbytes(status) < n * DGRAM_STATUS_DTYPE.itemsize:
+        raise ValueError("status holds %d bytes, %d datagrams need %d" % (_nbytes(status), n,
+                                                                         n * DGRAM_STATUS_DTYPE.itemsize))
+
+
+def verify_status(engine, arena, descs, status=None, counters=None, stream=None) -> None:
+    """cts_media_stream_verify_status: the receive pass writing one 16-byte cts_datagram_status per datagram."""
+    from .engine import _check_outputs, _nbytes, _stream
+
+    n = _nbytes(descs) // DESC_DTYPE.itemsize
+    _check_outputs(n, None, counters)
+    _check_status(n, status)
+    check("cts_media_stream_verify_status",
+          engine._L.cts_media_stream_verify_status(engine._h, _ptr(arena), _nbytes(arena), _ptr(descs), n, _ptr(status),
+                                                   _ptr(counters), _stream(stream)))
+
+
+def verify_strided_status(engine, arena, stride: int, lengths, status=None, counters=None, stream=None) -> None:
+    """cts_media_stream_verify_strided_status: the strided receive ring, 16-byte statuses."""
+    from .engine import _check_outputs, _nbytes, _stream
+
+    n = _nbytes(lengths) // 4
+    _check_outputs(n, None, counters)
+    _check_status(n, status)
+    check("cts_media_stream_verify_strided_status",
+          engine._L.cts_media_stream_verify_strided_status(engine._h, _ptr(arena), _nbytes(arena), stride,
+                                                           _ptr(lengths), n, _ptr(status), _ptr(counters),
+                                                           _stream(stream)))
+
+
 class MediaStreamClient:
     """ctsIoPatternMediaStreamClient's frame accounting (ctsIOPatternMediaStream.cpp:46-530)."""
 
@@ -152,6 +188,17 @@ class MediaStreamClient:
                                                     receiver_qpc, receiver_qpf, ctypes.byref(consumed))
         if rc < 0:
             raise CtsError("cts_media_stream_client_complete", rc)
+        return rc, consumed.value
+
+    def complete_status(self, status: np.ndarray, receiver_qpc: int = 0, receiver_qpf: int = 0):
+        """CompleteIo over compact statuses (cts_media_stream_client_complete_status). Returns (cts_io_status,
+        consumed)."""
+        status = np.ascontiguousarray(status, dtype=DGRAM_STATUS_DTYPE)
+        consumed = ctypes.c_uint32()
+        rc = lib().cts_media_stream_client_complete_status(self._h, status.ctypes.data, len(status), receiver_qpc,
+                                                           receiver_qpf, ctypes.byref(consumed))
+        if rc < 0:
+            raise CtsError("cts_media_stream_client_complete_status", rc)
         return rc, consumed.value
 
     def set_connection_id(self, datagram: bytes) -> None:

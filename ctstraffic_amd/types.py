@@ -38,6 +38,17 @@ DGRAM_RECORD_DTYPE = np.dtype(
         ("completed_bytes", "<u4"),
     ]
 )
+# cts_datagram_status (compact receive output)
+DGRAM_STATUS_DTYPE = np.dtype(
+    [
+        ("sequence_number", "<i8"),
+        ("completed_bytes", "<u4"),
+        ("flag", "<u2"),
+        ("kind", "u1"),
+        ("pass", "u1"),
+    ]
+)
+assert DGRAM_STATUS_DTYPE.itemsize == 16
 # cts_datagram_header
 DGRAM_HEADER_DTYPE = np.dtype([("sequence_number", "<i8"), ("qpc", "<i8"), ("qpf", "<i8")])
 RESULT_FLAG_NOT_DATA = 0x2

@@ -107,6 +107,30 @@ int cts_media_stream_verify_strided(cts_engine* engine, const void* dev_arena, u
                                     const uint32_t* dev_lengths, uint32_t n, cts_datagram_record* dev_records,
                                     cts_verify_result* dev_results, void* dev_counters, void* stream);
 
+/* Compact receive output: what the client's frame accounting reads of one datagram when no jitter log is
+ * written. The sender timestamps of cts_datagram_record feed only the jitter log and its time-in-flight
+ * estimate (ctsIOPatternMediaStream.cpp:218-223, 366-393; ctsConfig.cpp:3910-3930), and a failing payload
+ * ends the stream whatever its first mismatch was (:185-190), so 16 bytes per datagram replace the 32-byte
+ * record and the 12-byte result. (Writes mixed into the receive pass cost it about 18 us per output byte per
+ * 16 M datagrams, plus a fixed ~210 us: DESIGN.md section 3.) */
+typedef struct cts_datagram_status {
+    int64_t sequence_number;  /* DATA datagrams: header bytes 2..9 (GetSequenceNumberFromTask); otherwise 0 */
+    uint32_t completed_bytes;
+    uint16_t flag;            /* as cts_datagram_record.flag */
+    uint8_t kind;             /* cts_datagram_kind */
+    uint8_t pass;             /* DATA: 1 = payload verified clean, 0 = corrupt; other kinds: 0 */
+} cts_datagram_status;        /* 16 bytes */
+
+/* The receive pass of cts_media_stream_verify / cts_media_stream_verify_strided writing one
+ * cts_datagram_status per datagram (dev_status may be NULL: counters only). Counters as there; the first
+ * mismatch of a failing datagram is cts_verify of its payload span (skip 26, expected offset 0) when wanted. */
+int cts_media_stream_verify_status(cts_engine* engine, const void* dev_arena, uint64_t arena_bytes,
+                                   const cts_buf_desc* dev_descs, uint32_t n, cts_datagram_status* dev_status,
+                                   void* dev_counters, void* stream);
+int cts_media_stream_verify_strided_status(cts_engine* engine, const void* dev_arena, uint64_t arena_bytes,
+                                           uint32_t stride, const uint32_t* dev_lengths, uint32_t n,
+                                           cts_datagram_status* dev_status, void* dev_counters, void* stream);
+
 /* ---- client frame accounting (ctsIoPatternMediaStreamClient) ---------------- */
 typedef struct cts_media_stream_settings { /* ctsConfig::MediaStreamSettings */
     uint32_t frame_size_bytes;
@@ -145,6 +169,11 @@ int cts_media_stream_client_destroy(cts_media_stream_client* client);
 int cts_media_stream_client_complete(cts_media_stream_client* client, const cts_datagram_record* records,
                                      const cts_verify_result* results, uint32_t n, int64_t receiver_qpc,
                                      int64_t receiver_qpf, uint32_t* consumed);
+/* The same CompleteIo over compact statuses (cts_media_stream_verify_status): frames keep sender
+ * timestamps of 0, everything else (bits, successful / dropped / duplicate / error frames, the failure) is
+ * identical to cts_media_stream_client_complete. */
+int cts_media_stream_client_complete_status(cts_media_stream_client* client, const cts_datagram_status* status,
+                                            uint32_t n, int64_t receiver_qpc, int64_t receiver_qpf, uint32_t* consumed);
 int cts_media_stream_client_set_connection_id(cts_media_stream_client* client, const char* datagram, uint32_t len);
 /* One renderer-timer tick (TimerCallback, ctsIOPatternMediaStream.cpp:470-530,
  * without the wall-clock scheduling): returns 0 = keep rendering, 1 = the stream

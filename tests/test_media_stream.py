@@ -14,7 +14,7 @@ import pytest
 import oracle
 from oracle import media_stream as OM
 from ctstraffic_amd import media_stream as M
-from ctstraffic_amd.types import DESC_DTYPE, DGRAM_HEADER_DTYPE, DGRAM_RECORD_DTYPE, RESULT_DTYPE
+from ctstraffic_amd.types import DESC_DTYPE, DGRAM_HEADER_DTYPE, DGRAM_RECORD_DTYPE, DGRAM_STATUS_DTYPE, RESULT_DTYPE
 
 MAX = 1400  # c_udpDatagramMaximumSizeBytes in the MSTest (ctsMediaStreamProtocolUnitTest.cpp:22)
 
@@ -72,19 +72,33 @@ def _random_stream(rng, frame_size, n_frames, max_dgram, p_drop, p_dup, p_bad, p
     return out
 
 
+def _status_of(recs, res):
+    """The compact statuses (cts_datagram_status) of records + results."""
+    st = np.zeros(len(recs), dtype=DGRAM_STATUS_DTYPE)
+    for f in ("sequence_number", "completed_bytes", "flag", "kind"):
+        st[f] = recs[f]
+    st["pass"] = (recs["kind"] == 0) & (res["pass"] == 1)
+    return st
+
+
 def _run_both(frame_size, buffered, n_frames, stream, renders_between):
+    """The client over records + results, the client over compact statuses and the Python restatement, in
+    lockstep: every render code and the final statistics agree."""
     cm = M.MediaStreamClient(frame_size, buffered, n_frames)
+    cs = M.MediaStreamClient(frame_size, buffered, n_frames)
     om = OM.ClientModel(frame_size, buffered, n_frames)
     recs = np.zeros(len(stream), dtype=DGRAM_RECORD_DTYPE)
     res = np.zeros(len(stream), dtype=RESULT_DTYPE)
     for i, (k, s, ln, ok) in enumerate(stream):
         recs[i] = (s, 0, 0, 0, k, 0, ln if k != 2 else 0)
         res[i]["pass"] = 1 if ok else 0
+    st = _status_of(recs, res)
     i = 0
     status = 0
     while i < len(stream) and status == 0:
         j = min(len(stream), i + renders_between)
         status, consumed = cm.complete(recs[i:j], res[i:j])
+        assert cs.complete_status(st[i:j]) == (status, consumed)
         for q in range(i, i + consumed):
             k, s, ln, ok = stream[q]
             om.complete(k, s, ln if k != 2 else 0, ok)
@@ -92,16 +106,18 @@ def _run_both(frame_size, buffered, n_frames, stream, renders_between):
         i += consumed
         if status == 0:
             code = cm.render()
-            assert code == om.render()
+            assert code == om.render() == cs.render()
             if code != 0:
                 break  # the stream finished (Abort) or aborted: the functor stops receiving
     while cm.stats()["finished"] == 0 and cm.stats()["last_error"] == OM.RUNNING:
-        assert cm.render() == om.render()
+        assert cm.render() == om.render() == cs.render()
     got = cm.stats()
     exp = om.stats()
     for k in exp:
         assert got[k] == exp[k], (k, got, exp)
+    assert cs.stats() == got
     cm.close()
+    cs.close()
     return got
 
 
@@ -192,12 +208,14 @@ def _to_dev(a, torch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("ms_variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("ms_variant", [0, 1, 2, 3, 4, 5, 6])
 def test_gpu_media_stream_verify_matches_oracle(engine, tuning_engine, ms_variant):
     """ms_variant 0: one wave per datagram; 1: four datagrams per wave, header by byte loads;
     2: four per wave, header by 16-byte chunk loads gathered with DPP row shifts; 3: variant 2
     walking block-contiguous datagram ranges (the default, the product library's only one; the others run on
-    the tuning build)."""
+    the tuning build); 4 / 5 / 6: variant 3 writing its outputs every 8 / 16 / 32 rounds from a per-wave
+    LDS ring (partial last rings, chunk ends and the launch end inside a ring are all covered by the
+    block/chunk shapes below)."""
     from ctstraffic_amd import _lib
 
     if ms_variant != 3:
@@ -214,7 +232,7 @@ def test_gpu_media_stream_verify_matches_oracle(engine, tuning_engine, ms_varian
             engine.set_attr(_lib.ATTR_SMALL_BLOCKS_PER_CU, sbpc)
             engine.set_attr(_lib.ATTR_SMALL_CHUNK, chunk)
             _media_stream_verify_vs_oracle(engine)
-        if ms_variant == 3:  # outputs at 4-byte-aligned (not 16) addresses
+        if ms_variant >= 3:  # outputs at 4-byte-aligned (not 16) addresses
             _media_stream_verify_vs_oracle(engine, out_shift=4)
     finally:
         engine.set_attr(_lib.ATTR_MS_VARIANT, default)
@@ -257,6 +275,16 @@ def _media_stream_verify_vs_oracle(engine, out_shift=0):
         assert bad.size == 0, (f, [(int(i), int(descs[i]["byte_offset"]), int(descs[i]["length"]), gres[i].tolist(),
                                     eres[i].tolist()) for i in bad[:6]])
     assert engine.read_counters(ctr) == ectr
+    # the compact form: 16-byte statuses, same counters
+    st = torch.zeros(len(dgs) * 16 + out_shift, dtype=torch.uint8, device="cuda")[out_shift:]
+    ctr2 = engine.new_counters()
+    M.verify_status(engine, a, d, status=st, counters=ctr2)
+    torch.cuda.synchronize()
+    gs = st.cpu().numpy().view(DGRAM_STATUS_DTYPE)
+    es = _status_of(er, eres)
+    for f in DGRAM_STATUS_DTYPE.names:
+        assert np.array_equal(gs[f], es[f]), f
+    assert engine.read_counters(ctr2) == ectr
 
 
 @pytest.mark.gpu
@@ -302,6 +330,14 @@ def test_gpu_media_stream_end_to_end(engine):
     assert status == 2 and consumed == bad + 1  # the corrupt datagram fails the stream (CorruptedBytes)
     s = cm.stats()
     assert s["last_error"] == OM.DATA_MISMATCH and s["fail_datagram"] == bad
+    # the compact receive pass drives the client to the same failure
+    st = torch.zeros(n * 16, dtype=torch.uint8, device="cuda")
+    M.verify_status(engine, a, dd, status=st)
+    torch.cuda.synchronize()
+    gs = st.cpu().numpy().view(DGRAM_STATUS_DTYPE)
+    assert np.array_equal(gs, _status_of(gr, gres))
+    cs = M.MediaStreamClient(frame, buffered, n_frames)
+    assert cs.complete_status(gs) == (2, bad + 1) and cs.stats() == s
     # without the corruption every frame renders successfully
     fixed = gres.copy()
     fixed["pass"][bad] = 1
@@ -359,12 +395,25 @@ def test_gpu_media_stream_verify_strided_matches_oracle(engine, stride):
     for f in RESULT_DTYPE.names:
         assert np.array_equal(gres[f], eres[f]), f
     assert engine.read_counters(ctr) == ectr
+    # the compact form over the same ring
+    st = torch.zeros(n * 16, dtype=torch.uint8, device="cuda")
+    ctr2 = engine.new_counters()
+    M.verify_strided_status(engine, a, stride, ld, status=st, counters=ctr2)
+    torch.cuda.synchronize()
+    gs = st.cpu().numpy().view(DGRAM_STATUS_DTYPE)
+    es = _status_of(er, eres)
+    for f in DGRAM_STATUS_DTYPE.names:
+        assert np.array_equal(gs[f], es[f]), f
+    assert engine.read_counters(ctr2) == ectr
     # a completion longer than its slot is a bad descriptor, not read
     lens2 = lens.copy()
     lens2[5] = stride + 1
     recs.zero_()
     M.verify_strided(engine, a, stride, _to_dev(lens2, torch), records=recs, results=res)
+    M.verify_strided_status(engine, a, stride, _to_dev(lens2, torch), status=st)
     torch.cuda.synchronize()
     gr = recs.cpu().numpy().view(DGRAM_RECORD_DTYPE)
     gres = res.cpu().numpy().view(RESULT_DTYPE)
     assert gr["kind"][5] == 5 and gres["flags"][5] == 1 and gres["pass"][5] == 0
+    gs = st.cpu().numpy().view(DGRAM_STATUS_DTYPE)
+    assert gs["kind"][5] == 5 and gs["pass"][5] == 0 and gs["completed_bytes"][5] == stride + 1

@@ -161,6 +161,40 @@ def test_bad_descriptors(engine):
     assert ctr == ectr and ctr["buffers_checked"] == 1
 
 
+def test_bad_descriptors_staged_results(tuning_engine):
+    """Verify variant 18 stages result records in LDS and writes 16 at a time: bad descriptors interleaved with
+    valid and corrupt buffers across several staging flushes, one and many workgroups, vs the oracle."""
+    from ctstraffic_amd import _lib
+
+    eng = tuning_engine
+    dv, dbpc = eng.get_attr(_lib.ATTR_VERIFY_VARIANT), eng.get_attr(_lib.ATTR_BLOCKS_PER_CU)
+    rng = np.random.default_rng(77)
+    arena = np.zeros(1 << 20, np.uint8)
+    oracle.fill(arena, np.array([(0, 1 << 20, 0, 0, 0)], dtype=oracle.DESC_DTYPE))
+    d = np.zeros(203, dtype=DESC_DTYPE)
+    for k in range(len(d)):
+        if k % 5 == 3:
+            d[k] = ((1 << 20) - 4, 64, 0, k % 7, 0)  # crosses the arena end
+        else:
+            ln = int(rng.integers(9000, 20000))
+            off = int(rng.integers(0, (1 << 20) - ln))
+            d[k] = (off, ln, off % 65536, k % 7, int(rng.integers(0, 30)))
+    for k in rng.choice(len(d), 20, replace=False):  # corrupt some valid buffers
+        if k % 5 != 3:
+            arena[int(d[k]["byte_offset"]) + int(d[k]["length"]) - 1] ^= 0x11
+    try:
+        eng.set_attr(_lib.ATTR_VERIFY_VARIANT, 18)
+        for bpc in (1, 16):
+            eng.set_attr(_lib.ATTR_BLOCKS_PER_CU, bpc)
+            r, ctr, cff = run_verify(eng, arena, d, 0, n_conns=7)
+            er, ectr, ecff = oracle.verify_batch(arena, d, n_conns=7)
+            assert_results_equal(r, er, "bpc %d" % bpc)
+            assert ctr == ectr and np.array_equal(cff, ecff)
+    finally:
+        eng.set_attr(_lib.ATTR_VERIFY_VARIANT, dv)
+        eng.set_attr(_lib.ATTR_BLOCKS_PER_CU, dbpc)
+
+
 def test_misaligned_descriptor_array_is_rejected(engine):
     """The kernels read descriptors as u64 fields: a descriptor array that is not
     8-byte aligned is refused with CTS_E_INVALID, before any launch."""
@@ -693,7 +727,7 @@ def test_verify_host_batch(engine):
 
 
 # ---- every launch variant / geometry is bit-identical ------------------------------------------
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18])
 @pytest.mark.parametrize("nt", [1, 0])
 def test_launch_variants_parity(tuning_engine, variant, nt):
     from ctstraffic_amd import _lib
@@ -844,6 +878,7 @@ def test_max_length_buffers(engine, tuning_engine):
     from ctstraffic_amd import _lib
 
     cases = [(_lib.ATTR_VERIFY_VARIANT, 13, 0), (_lib.ATTR_VERIFY_VARIANT, 4, 0), (_lib.ATTR_VERIFY_VARIANT, 3, 0),
+             (_lib.ATTR_VERIFY_VARIANT, 18, 0),
              (_lib.ATTR_SMALL_VARIANT, 9, 1472), (_lib.ATTR_SMALL_VARIANT, 0, 1472), (_lib.ATTR_SMALL_VARIANT, 3, 1472)]
     product_engine = engine
     defaults = {a: tuning_engine.get_attr(a) for a, _, _ in cases}

@@ -35,6 +35,7 @@ def main():
         arenas.append(a)
     lens = torch.from_numpy(w.descs["length"].astype("uint32")).cuda()
     recs = torch.empty(w.n * 32, dtype=torch.uint8, device="cuda")
+    st = torch.empty(w.n * 16, dtype=torch.uint8, device="cuda")
     res = eng.new_results(w.n)
     ctr = eng.new_counters()
     s = torch.cuda.current_stream()
@@ -58,6 +59,10 @@ def main():
         # the receive ring's descriptor-free form (datagram i at i * 1472, lengths only; windowed kernel)
         cases += [("ms_strided+records+results", ("ms", None, ch),
                    lambda a: MS.verify_strided(eng, a, w.max_length, lens, records=recs, results=res))]
+        # the compact receive pass (16-byte statuses), descriptors and strided ring
+        cases += [("ms+status", ("ms", None, ch), lambda a: MS.verify_status(eng, a, d, status=st)),
+                  ("ms_strided+status", ("ms", None, ch),
+                   lambda a: MS.verify_strided_status(eng, a, w.max_length, lens, status=st))]
     cases = [c for c in cases if not only or c[0] in only]
     for r in range(args.rounds):
         for name, v, fn in cases:
