@@ -1685,8 +1685,10 @@ __device__ __forceinline__ void ms_datagram(const MsSource& src, uint32_t i, uin
 // 0..2, gathered on lane 0 by DPP row shifts; the DATA verdict is broadcast (ms_variant 2).
 // RING > 0: outputs staged in a per-wave ring of RING rounds and written every RING rounds (QuadRing).
 // STATUS: records points at 16-byte cts_datagram_status entries (results unused).
+// FAILMARK: records points at statuses ms_status_gather_kernel already wrote; only a corrupt DATA datagram's
+// pass byte is cleared (a rare byte store: the read stream runs as if it wrote nothing).
 template <int U, bool NT, bool ALIGN, bool HDR16, bool CONTIG = false, bool STRIDED = false, int RING = 0,
-          bool STATUS = false>
+          bool STATUS = false, bool FAILMARK = false>
 __global__ void __launch_bounds__(kBlock)
     media_stream_verify_quad_kernel(const uint8_t* __restrict__ arena, uint64_t arena_bytes, MsSource src, uint32_t n,
                                     void* __restrict__ records, cts_verify_result* __restrict__ results,
@@ -1792,6 +1794,14 @@ __global__ void __launch_bounds__(kBlock)
             if (acc != 0u && data) quad_scan_exact<NT>(q, lane, first, count);
             quad_team_reduce(first, count);
         }
+        if constexpr (FAILMARK) {
+            if (lane == 0u && live && data) {
+                if (records != nullptr && first != kNone) reinterpret_cast<uint8_t*>(records)[16ull * i + 15u] = 0u;
+                qc.add(q.len, first == kNone, count);
+            }
+            w.i = inext;
+            continue;
+        }
         if (lane == 0u && live) {
             QuadOut& o = RING ? qring[RING ? team >> 2 : 0].slot[rs] : qout[RING ? 0 : team >> 2];
             const uint32_t t = team & 3u;
@@ -1842,6 +1852,64 @@ __global__ void __launch_bounds__(kBlock)
     if constexpr (RING > 0)
         if (rs) quad_ring_flush<RING>(qring[team >> 2], rs, w.end, results, records);
     qc.flush<TEAMS>(ctr, team, lane, counters);
+}
+
+// The header half of a two-pass compact receive (tuning build, ms variant 7): one lane per datagram
+// loads the one or two 16-byte chunks holding header bytes [0, min(completed, 10)), classifies the datagram
+// as the receive kernel does (ValidateBufferLengthFromTask, ctsMediaStreamProtocol.hpp:284-329) and writes its
+// 16-byte status with pass = 1 for DATA. The payload pass then runs without outputs and clears pass for
+// corrupt DATA datagrams only (FAILMARK). The idea: take the writes out of the payload pass (writing 16 B per
+// datagram as it reads costs it 11-20 %). Measured slower overall: see launch_media_stream_status.
+template <bool STRIDED>
+__global__ void __launch_bounds__(kBlock)
+    ms_status_gather_kernel(const uint8_t* __restrict__ arena, uint64_t arena_bytes, MsSource src, uint32_t n,
+                            uint32_t* __restrict__ status)
+{
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    uint64_t doff;
+    uint32_t completed;
+    ms_datagram<STRIDED>(src, i, doff, completed);
+    const bool bad = doff > arena_bytes || arena_bytes - doff < (uint64_t)completed || (STRIDED && completed > src.stride);
+    uint32_t kind, flag = 0, s0 = 0, s1 = 0;
+    if (bad) {
+        kind = CTS_DGRAM_BAD_DESC;
+    } else if (completed == 0u) {
+        kind = CTS_DGRAM_ZERO;
+    } else if (completed < CTS_UDP_FLAG_LENGTH) {
+        kind = CTS_DGRAM_SHORT;
+    } else {
+        const uint8_t* dg = arena + doff;
+        const uint32_t ho = (uint32_t)((uintptr_t)dg & 15u);
+        const u32x4* c0 = reinterpret_cast<const u32x4*>(dg - ho);
+        const uint32_t hbytes = completed < 10u ? completed : 10u;  // flag + sequence number
+        const u32x4 a = load_chunk_g<false>(c0);
+        const u32x4 b = ho + hbytes > 16u ? load_chunk_g<false>(c0 + 1) : u32x4{0u, 0u, 0u, 0u};
+        const uint32_t W[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+        const uint32_t j0 = ho >> 2, sh = ho & 3u;
+        uint32_t V[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+            V[m] = j0 == 0u ? W[m] : (j0 == 1u ? W[m + 1] : (j0 == 2u ? W[m + 2] : W[m + 3]));
+        const uint32_t H0 = __builtin_amdgcn_alignbyte(V[1], V[0], sh), H1 = __builtin_amdgcn_alignbyte(V[2], V[1], sh),
+                       H2 = __builtin_amdgcn_alignbyte(V[3], V[2], sh);
+        flag = H0 & 0xFFFFu;
+        if (flag == CTS_UDP_FLAG_DATA)
+            kind = completed < CTS_UDP_DATA_HEADER_LENGTH ? CTS_DGRAM_SHORT : CTS_DGRAM_DATA;
+        else if (flag == CTS_UDP_FLAG_ID)
+            kind = completed < CTS_UDP_CONNECTION_ID_HEADER_LENGTH ? CTS_DGRAM_SHORT : CTS_DGRAM_ID;
+        else
+            kind = CTS_DGRAM_UNKNOWN;
+        if (kind == CTS_DGRAM_DATA) {
+            s0 = (H0 >> 16) | (H1 << 16);
+            s1 = (H1 >> 16) | (H2 << 16);
+        }
+    }
+    uint32_t* o = status + 4ull * i;
+    o[0] = s0;
+    o[1] = s1;
+    o[2] = completed;
+    o[3] = flag | (kind << 16) | (kind == CTS_DGRAM_DATA ? 1u << 24 : 0u);
 }
 
 // Send: header {u16 0, i64 seq, i64 qpc, i64 qpf} + P[0 .. length-26) per datagram
@@ -2256,7 +2324,7 @@ hipError_t launch_media_stream_verify(const uint8_t* arena, uint64_t arena_bytes
     // ms_variant: 0 = one wave per datagram, 1 = four datagrams per wave (header by byte loads),
     // 2 = four per wave, header by three 16-byte chunk loads + DPP, 3 = variant 2 walking
     // block-contiguous datagram ranges (default), 4 / 5 / 6 = variant 3 writing its outputs every
-    // 8 / 16 / 32 rounds from a per-wave LDS ring
+    // 8 / 16 / 32 rounds from a per-wave LDS ring (7: the two-pass form of cts_media_stream_verify_status)
     const uint32_t qgrid = grid_for(n, kBlock / kQuadTeam, geo);
     const uint32_t grid = grid_for(n, kBlock / 64, geo);
 #if CTS_TUNING
@@ -2338,9 +2406,38 @@ hipError_t launch_media_stream_status(const uint8_t* arena, uint64_t arena_bytes
                                      uint64_t* counters, hipStream_t stream, const LaunchGeometry& geo)
 {
     if (n == 0) return hipSuccess;
-    // the variant-3 walk writing 16-byte statuses; descs == nullptr: the strided-ring form
+    // descs == nullptr: the strided-ring form
     const ContigGrid cg = contig_grid(n, geo);
     const MsSource src{descs, lengths, stride};
+#if CTS_TUNING
+    if (geo.ms_variant == 7) {
+        // two passes: headers -> statuses (pass = 1 for DATA), then the payload verify clearing pass on
+        // failures. Measured slower than one pass (4.25 vs 4.08 ms per 16 M datagrams): the header gather's
+        // scattered 16-byte reads cost more than the writes it takes out of the payload pass.
+        const uint32_t ggrid = (n + kBlock - 1) / kBlock;
+        if (status != nullptr) {
+            if (descs == nullptr)
+                ms_status_gather_kernel<true><<<ggrid, kBlock, 0, stream>>>(arena, arena_bytes, src, n,
+                                                                              reinterpret_cast<uint32_t*>(status));
+            else
+                ms_status_gather_kernel<false><<<ggrid, kBlock, 0, stream>>>(arena, arena_bytes, src, n,
+                                                                               reinterpret_cast<uint32_t*>(status));
+        }
+#define CTS_MS_MARK(NT, STR)                                                                                      \
+    media_stream_verify_quad_kernel<6, NT, true, true, true, STR, 0, false, true><<<cg.grid, kBlock, 0, stream>>>( \
+        arena, arena_bytes, src, n, status, nullptr, counters, cg.per)
+        if (descs == nullptr) {
+            if (geo.nontemporal) CTS_MS_MARK(true, true);
+            else CTS_MS_MARK(false, true);
+        } else {
+            if (geo.nontemporal) CTS_MS_MARK(true, false);
+            else CTS_MS_MARK(false, false);
+        }
+#undef CTS_MS_MARK
+        return hipGetLastError();
+    }
+#endif
+    // one pass: the variant-3 walk writing each datagram's status as it verifies
 #define CTS_MS_STATUS(NT, STR)                                                                              \
     media_stream_verify_quad_kernel<6, NT, true, true, true, STR, 0, true><<<cg.grid, kBlock, 0, stream>>>( \
         arena, arena_bytes, src, n, status, nullptr, counters, cg.per)

@@ -248,8 +248,8 @@ def _kernels(path):
 def test_product_library_carries_only_the_default_kernels():
     """The product .so compiles one kernel per path (verify variant 13, small variant 9, MediaStream variant 3, the
     fills), each for nontemporal and plain loads, the small-buffer and MediaStream kernels' strided-ring forms, the
-    MediaStream compact-status forms (descriptors and strided ring), plus the SYNC mailbox grid; every measured
-    alternative lives in the tuning build only."""
+    MediaStream compact-status forms (descriptors and strided ring), plus the
+    SYNC mailbox grid; every measured alternative lives in the tuning build only."""
     from ctstraffic_amd import _lib
 
     prod = _kernels(_lib.LIB_PATH)

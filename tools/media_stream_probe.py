@@ -57,11 +57,12 @@ def main():
                       ("ms+records+results", ("ms", v, ch),
                        lambda a: MS.verify(eng, a, d, records=recs, results=res))]
         # the receive ring's descriptor-free form (datagram i at i * 1472, lengths only; windowed kernel)
-        cases += [("ms_strided+records+results", ("ms", None, ch),
+        cases += [("ms_strided+records+results", ("ms", 3, ch),
                    lambda a: MS.verify_strided(eng, a, w.max_length, lens, records=recs, results=res))]
         # the compact receive pass (16-byte statuses), descriptors and strided ring
-        cases += [("ms+status", ("ms", None, ch), lambda a: MS.verify_status(eng, a, d, status=st)),
-                  ("ms_strided+status", ("ms", None, ch),
+        cases += [("ms+status", ("ms", 3, ch), lambda a: MS.verify_status(eng, a, d, status=st)),
+                  ("ms+status_two_pass", ("ms", 7, ch), lambda a: MS.verify_status(eng, a, d, status=st)),
+                  ("ms_strided+status", ("ms", 3, ch),
                    lambda a: MS.verify_strided_status(eng, a, w.max_length, lens, status=st))]
     cases = [c for c in cases if not only or c[0] in only]
     for r in range(args.rounds):
