@@ -35,20 +35,29 @@ WORKLOADS = {
                                                 "1472 B datagrams (%d B payload read)" % (DG * 1446),
     "verify_quad_kernel[strided]": "config3 verify, strided ring (lengths only): 16M x 1472 B datagrams "
                                    "(%d B payload read)" % (DG * 1446),
+    "media_stream_verify_quad_kernel[status]": "config3 MediaStream compact receive (16-B statuses): 16M x 1472 B "
+                                               "datagrams (%d B payload read)" % (DG * 1446),
+    "media_stream_verify_quad_kernel[strided][status]": "config3 MediaStream compact receive, strided ring: 16M x "
+                                                        "1472 B datagrams (%d B payload read)" % (DG * 1446),
 }
 ALGO_BYTES = {"verify_wg_kernel": 268435456, "fill_kernel": 268435456, "verify_quad_kernel": DG * 1446,
               "verify_wave_kernel": DG * 1446, "media_stream_verify_quad_kernel": DG * 1446,
-              "media_stream_verify_quad_kernel[strided]": DG * 1446, "verify_quad_kernel[strided]": DG * 1446}
+              "media_stream_verify_quad_kernel[strided]": DG * 1446, "verify_quad_kernel[strided]": DG * 1446,
+              "media_stream_verify_quad_kernel[status]": DG * 1446,
+              "media_stream_verify_quad_kernel[strided][status]": DG * 1446}
 RUNS = ("prof", "prof_dg")
 
 
 def _kname(name):
     base = name.split("(")[0].split("<")[0].split("::")[-1].strip()
     if base in ("media_stream_verify_quad_kernel", "verify_quad_kernel") and "<" in name:
-        targs = name.split("(")[0].split("<", 1)[1].rsplit(">", 1)[0].split(",")
-        last = 6 if base == "media_stream_verify_quad_kernel" else 5
-        if len(targs) == last and targs[-1].strip() == "true":  # STRIDED: the *_verify_strided entry points
-            return base + "[strided]"
+        targs = [t.strip() for t in name.split("(")[0].split("<", 1)[1].rsplit(">", 1)[0].split(",")]
+        # template arguments: STRIDED is the 6th (MediaStream) / 5th (verify) one, STATUS the MediaStream's 8th
+        si = 5 if base == "media_stream_verify_quad_kernel" else 4
+        tag = "[strided]" if len(targs) > si and targs[si] == "true" else ""
+        if base == "media_stream_verify_quad_kernel" and len(targs) > 7 and targs[7] == "true":
+            tag += "[status]"
+        return base + tag
     return base
 
 
