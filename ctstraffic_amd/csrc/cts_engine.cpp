@@ -605,6 +605,13 @@ int cts_fill(cts_engine* e, void* dev_arena, uint64_t arena_bytes, const cts_buf
                                        static_cast<hipStream_t>(stream), e->geo));
 }
 
+// The kernels write 12-byte records and DataError slots as dwords and add to the counter block with 64-bit
+// atomics: a misaligned output would fault on the device, so it is refused here.
+static bool outputs_misaligned(const void* results, const void* counters, const void* conn_first_fail = nullptr)
+{
+    return ((uintptr_t)results & 3u) != 0 || ((uintptr_t)counters & 7u) != 0 || ((uintptr_t)conn_first_fail & 3u) != 0;
+}
+
 int cts_verify(cts_engine* e, const void* dev_arena, uint64_t arena_bytes, const cts_buf_desc* dev_descs, uint32_t n,
                uint32_t max_length_hint, cts_verify_result* dev_results, void* dev_counters,
                uint32_t* dev_conn_first_fail, uint32_t n_conns, void* stream)
@@ -613,6 +620,7 @@ int cts_verify(cts_engine* e, const void* dev_arena, uint64_t arena_bytes, const
     if (n == 0) return CTS_OK;
     if (dev_arena == nullptr || dev_descs == nullptr || ((uintptr_t)dev_descs & 7u) != 0 || ((uintptr_t)dev_arena & 15u) != 0) return CTS_E_INVALID;
     if (dev_conn_first_fail == nullptr && n_conns != 0) return CTS_E_INVALID;
+    if (outputs_misaligned(dev_results, dev_counters, dev_conn_first_fail)) return CTS_E_INVALID;
     DeviceGuard g(e->device);
     if (!g.ok) return CTS_E_HIP;
     return hip_status(cts::launch_verify(static_cast<const uint8_t*>(dev_arena), arena_bytes, dev_descs, n,
@@ -632,6 +640,7 @@ int cts_verify_strided(cts_engine* e, const void* dev_arena, uint64_t arena_byte
         return CTS_E_INVALID;
     if (expected_offset >= CTS_PATTERN_PERIOD) return CTS_E_INVALID;
     if (dev_conn_first_fail == nullptr && n_conns != 0) return CTS_E_INVALID;
+    if (outputs_misaligned(dev_results, dev_counters, dev_conn_first_fail)) return CTS_E_INVALID;
     DeviceGuard g(e->device);
     if (!g.ok) return CTS_E_HIP;
     return hip_status(cts::launch_verify_strided(static_cast<const uint8_t*>(dev_arena), arena_bytes, stride, dev_lengths, n,
@@ -659,6 +668,7 @@ int cts_media_stream_verify(cts_engine* e, const void* dev_arena, uint64_t arena
     if (e == nullptr) return CTS_E_INVALID;
     if (n == 0) return CTS_OK;
     if (dev_arena == nullptr || dev_descs == nullptr || ((uintptr_t)dev_descs & 7u) != 0 || ((uintptr_t)dev_arena & 15u) != 0) return CTS_E_INVALID;
+    if (outputs_misaligned(dev_results, dev_counters, dev_records)) return CTS_E_INVALID;
     DeviceGuard g(e->device);
     if (!g.ok) return CTS_E_HIP;
     return hip_status(cts::launch_media_stream_verify(static_cast<const uint8_t*>(dev_arena), arena_bytes, dev_descs,
@@ -676,6 +686,7 @@ int cts_media_stream_verify_strided(cts_engine* e, const void* dev_arena, uint64
     if (dev_arena == nullptr || dev_lengths == nullptr || ((uintptr_t)dev_lengths & 3u) != 0 ||
         ((uintptr_t)dev_arena & 15u) != 0 || arena_bytes < 16u || stride == 0)
         return CTS_E_INVALID;
+    if (outputs_misaligned(dev_results, dev_counters, dev_records)) return CTS_E_INVALID;
     DeviceGuard g(e->device);
     if (!g.ok) return CTS_E_HIP;
     return hip_status(cts::launch_media_stream_verify_strided(static_cast<const uint8_t*>(dev_arena), arena_bytes, stride,
@@ -691,7 +702,7 @@ int cts_media_stream_verify_status(cts_engine* e, const void* dev_arena, uint64_
     if (e == nullptr) return CTS_E_INVALID;
     if (n == 0) return CTS_OK;
     if (dev_arena == nullptr || dev_descs == nullptr || ((uintptr_t)dev_descs & 7u) != 0 || ((uintptr_t)dev_arena & 15u) != 0 ||
-        ((uintptr_t)dev_status & 3u) != 0)
+        outputs_misaligned(dev_status, dev_counters))
         return CTS_E_INVALID;
     DeviceGuard g(e->device);
     if (!g.ok) return CTS_E_HIP;
@@ -707,7 +718,7 @@ int cts_media_stream_verify_strided_status(cts_engine* e, const void* dev_arena,
     if (e == nullptr) return CTS_E_INVALID;
     if (n == 0) return CTS_OK;
     if (dev_arena == nullptr || dev_lengths == nullptr || ((uintptr_t)dev_lengths & 3u) != 0 ||
-        ((uintptr_t)dev_arena & 15u) != 0 || arena_bytes < 16u || stride == 0 || ((uintptr_t)dev_status & 3u) != 0)
+        ((uintptr_t)dev_arena & 15u) != 0 || arena_bytes < 16u || stride == 0 || outputs_misaligned(dev_status, dev_counters))
         return CTS_E_INVALID;
     DeviceGuard g(e->device);
     if (!g.ok) return CTS_E_HIP;

@@ -182,7 +182,9 @@ int cts_fill(cts_engine* engine, void* dev_arena, uint64_t arena_bytes,
  *                           in stream order.
  * dev_arena must be 16-byte aligned and its allocation must extend to a
  * multiple of 16 bytes (every hipMalloc allocation does); dev_descs must be
- * 8-byte aligned (CTS_E_INVALID otherwise). */
+ * 8-byte aligned, dev_results and dev_conn_first_fail 4-byte aligned and
+ * dev_counters 8-byte aligned (CTS_E_INVALID otherwise; the same holds for the
+ * outputs of every verify entry point). */
 int cts_verify(cts_engine* engine, const void* dev_arena, uint64_t arena_bytes,
                const cts_buf_desc* dev_descs, uint32_t n, uint32_t max_length_hint,
                cts_verify_result* dev_results, void* dev_counters,

@@ -197,7 +197,8 @@ def test_bad_descriptors_staged_results(tuning_engine):
 
 def test_misaligned_descriptor_array_is_rejected(engine):
     """The kernels read descriptors as u64 fields: a descriptor array that is not
-    8-byte aligned is refused with CTS_E_INVALID, before any launch."""
+    8-byte aligned is refused with CTS_E_INVALID, before any launch. So are outputs the kernels would write
+    misaligned (dword records and DataError slots, 64-bit counter atomics)."""
     from ctstraffic_amd._lib import CtsError
 
     arena = torch.zeros(256, dtype=torch.uint8, device=DEV)
@@ -206,6 +207,20 @@ def test_misaligned_descriptor_array_is_rejected(engine):
         engine.verify(arena, raw[4:4 + DESC_DTYPE.itemsize], max_length_hint=0)
     with pytest.raises(CtsError):
         engine.fill(arena, raw[4:4 + DESC_DTYPE.itemsize], max_length_hint=0)
+    d = raw[:DESC_DTYPE.itemsize]
+    res = engine.new_results(2)
+    ctr = engine.new_counters()
+    nb = ctr.numel() * ctr.element_size()
+    ctr_raw = torch.zeros(nb + 16, dtype=torch.uint8, device=DEV)
+    cff = torch.full((4,), -1, dtype=torch.int32, device=DEV).view(torch.uint8)
+    with pytest.raises(CtsError):
+        engine.verify(arena, d, max_length_hint=0, results=res.view(torch.uint8)[2:2 + 12])
+    with pytest.raises(CtsError):
+        engine.verify(arena, d, max_length_hint=0, counters=ctr_raw[4:4 + nb])
+    with pytest.raises(CtsError):
+        engine.verify(arena, d, max_length_hint=0, conn_first_fail=cff[2:10])
+    engine.verify(arena, d, max_length_hint=0, results=res, counters=ctr_raw[8:8 + nb], conn_first_fail=cff[4:12])
+    torch.cuda.synchronize()
 
 
 @pytest.mark.parametrize("fill_nt", [0, 1, 2])
