@@ -654,7 +654,9 @@ int cts_media_stream_fill(cts_engine* e, void* dev_arena, uint64_t arena_bytes, 
 {
     if (e == nullptr) return CTS_E_INVALID;
     if (n == 0) return CTS_OK;
-    if (dev_arena == nullptr || dev_descs == nullptr || ((uintptr_t)dev_descs & 7u) != 0 || dev_headers == nullptr) return CTS_E_INVALID;
+    if (dev_arena == nullptr || dev_descs == nullptr || ((uintptr_t)dev_descs & 7u) != 0 || dev_headers == nullptr ||
+        ((uintptr_t)dev_headers & 7u) != 0)
+        return CTS_E_INVALID;
     DeviceGuard g(e->device);
     if (!g.ok) return CTS_E_HIP;
     return hip_status(cts::launch_media_stream_fill(static_cast<uint8_t*>(dev_arena), arena_bytes, dev_descs,

@@ -88,7 +88,9 @@ def fill(engine, arena, descs, headers, stream=None) -> None:
     from .engine import _nbytes, _stream
 
     n = _nbytes(descs) // DESC_DTYPE.itemsize
-    assert _nbytes(headers) // DGRAM_HEADER_DTYPE.itemsize == n
+    if _nbytes(headers) < n * DGRAM_HEADER_DTYPE.itemsize:
+        raise ValueError("headers holds %d bytes, %d datagrams need %d" % (_nbytes(headers), n,
+                                                                          n * DGRAM_HEADER_DTYPE.itemsize))
     check("cts_media_stream_fill", engine._L.cts_media_stream_fill(engine._h, _ptr(arena), _nbytes(arena), _ptr(descs),
                                                                _ptr(headers), n, _stream(stream)))
 
@@ -182,7 +184,8 @@ class MediaStreamClient:
         """Returns (cts_io_status, consumed)."""
         records = np.ascontiguousarray(records, dtype=DGRAM_RECORD_DTYPE)
         results = np.ascontiguousarray(results, dtype=RESULT_DTYPE)
-        assert len(records) == len(results)
+        if len(records) != len(results):
+            raise ValueError("%d records but %d results" % (len(records), len(results)))
         consumed = ctypes.c_uint32()
         rc = lib().cts_media_stream_client_complete(self._h, records.ctypes.data, results.ctypes.data, len(records),
                                                     receiver_qpc, receiver_qpf, ctypes.byref(consumed))

@@ -82,7 +82,8 @@ uint64_t cts_media_stream_split(uint64_t frame_bytes, uint32_t max_datagram, uin
 
 /* Sender: for every descriptor d (one data datagram of d.length bytes at
  * d.byte_offset; skip_head/expected ignored), write the 26-byte header
- * {0, headers[i]} and the payload P[0 .. d.length - 26). */
+ * {0, headers[i]} and the payload P[0 .. d.length - 26). dev_descs and
+ * dev_headers must be 8-byte aligned (CTS_E_INVALID otherwise). */
 int cts_media_stream_fill(cts_engine* engine, void* dev_arena, uint64_t arena_bytes, const cts_buf_desc* dev_descs,
                           const cts_datagram_header* dev_headers, uint32_t n, void* stream);
 
