@@ -255,6 +255,7 @@ def main():
     t0 = time.perf_counter()
     ev_a.record(stream)
     run_pipelined(K)
+    t_enq = time.perf_counter()  # the host has issued every launch (how far ahead of the GPU it ran: below)
     ev_b.record(stream)
     if world > 1:
         # fold the shards on-device and all-reduce the 5 counters over RCCL/xGMI
@@ -361,6 +362,9 @@ def main():
                     "frac": round(bytes_per_launch / pipe_launch_s / 1e9 / HBM_PEAK_GBPS, 4),
                     "timing": "HIP events around the headline leg's K*R launches, / (K*R): launch i on engine "
                               "stream i mod S, so one launch's tail overlaps the next launch's ramp-up",
+                    # where the wall clock of the headline leg goes beyond the GPU's own span of it
+                    "host_enqueue_us": round((t_enq - t0) * 1e6, 1),
+                    "wall_minus_events_us": round((elapsed - pipe_launch_s * launches) * 1e6, 1),
                 },
             },
             "cpu_baseline": cpu,
