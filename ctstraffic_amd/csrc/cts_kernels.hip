@@ -1127,7 +1127,8 @@ struct QuadRing {
 // All 64 lanes: write rounds [0, m) of the ring (round j's four buffers start at i0[j]); n = buffers in
 // the launch. Records go as write-through dwords (as quad_flush_outputs), 32 per round, results as
 // plain dwords, 12 per round.
-template <int K>
+// RECDW = dwords per record: 8 (cts_datagram_record) or 4 (cts_datagram_status, staged in rec[t][0..3]).
+template <int K, int RECDW = 8>
 __device__ __forceinline__ void quad_ring_flush(const QuadRing<K>& g, uint32_t m, uint32_t n,
                                                 cts_verify_result* results, void* records)
 {
@@ -1135,13 +1136,13 @@ __device__ __forceinline__ void quad_ring_flush(const QuadRing<K>& g, uint32_t m
     const uint32_t l = threadIdx.x & 63u;
     if (records != nullptr) {
 #pragma unroll 1  // (unrolled, the LDS reads are hoisted into ~80 VGPRs: occupancy 4 -> 2 waves/SIMD)
-        for (uint32_t k = 0; k < (K * 32u + 63u) / 64u; ++k) {
-            const uint32_t e = k * 64u + l, j = e >> 5, d = e & 31u;
+        for (uint32_t k = 0; k < (K * 4u * RECDW + 63u) / 64u; ++k) {
+            const uint32_t e = k * 64u + l, j = e / (4u * RECDW), d = e % (4u * RECDW);
             if (j < m) {
                 const uint64_t i0 = g.i0[j];
-                if (i0 + (d >> 3) < n)
-                    __hip_atomic_store(reinterpret_cast<uint32_t*>(records) + 8ull * i0 + d, g.slot[j].rec[d >> 3][d & 7u],
-                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (i0 + d / RECDW < n)
+                    __hip_atomic_store(reinterpret_cast<uint32_t*>(records) + (uint64_t)RECDW * i0 + d,
+                                       g.slot[j].rec[d / RECDW][d % RECDW], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
     }
@@ -1694,7 +1695,6 @@ __global__ void __launch_bounds__(kBlock)
                                     void* __restrict__ records, cts_verify_result* __restrict__ results,
                                     uint64_t* __restrict__ counters, uint32_t per = 0)
 {
-    static_assert(!(RING && STATUS), "the ring writes full records");
     constexpr int TEAMS = kBlock / kQuadTeam;
     __shared__ uint64_t ctr[TEAMS][5];
     __shared__ QuadOut qout[RING ? 1 : kBlock / 64];
@@ -1843,14 +1843,14 @@ __global__ void __launch_bounds__(kBlock)
             const uint32_t i0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)i);
             if ((threadIdx.x & 63u) == 0u) g.i0[rs] = i0;
             if (++rs == (uint32_t)RING) {
-                quad_ring_flush<RING>(g, RING, w.end, results, records);
+                quad_ring_flush<RING, STATUS ? 4 : 8>(g, RING, w.end, STATUS ? nullptr : results, records);
                 rs = 0;
             }
         }
         w.i = inext;
     }
     if constexpr (RING > 0)
-        if (rs) quad_ring_flush<RING>(qring[team >> 2], rs, w.end, results, records);
+        if (rs) quad_ring_flush<RING, STATUS ? 4 : 8>(qring[team >> 2], rs, w.end, STATUS ? nullptr : results, records);
     qc.flush<TEAMS>(ctr, team, lane, counters);
 }
 
@@ -2324,7 +2324,9 @@ hipError_t launch_media_stream_verify(const uint8_t* arena, uint64_t arena_bytes
     // ms_variant: 0 = one wave per datagram, 1 = four datagrams per wave (header by byte loads),
     // 2 = four per wave, header by three 16-byte chunk loads + DPP, 3 = variant 2 walking
     // block-contiguous datagram ranges (default), 4 / 5 / 6 = variant 3 writing its outputs every
-    // 8 / 16 / 32 rounds from a per-wave LDS ring (7: the two-pass form of cts_media_stream_verify_status)
+    // 8 / 16 / 32 rounds from a per-wave LDS ring (7: the two-pass form of cts_media_stream_verify_status;
+    // 8 / 9: its one-pass form with the statuses written every round / every 16 rounds; the product writes
+    // them every 32 rounds)
     const uint32_t qgrid = grid_for(n, kBlock / kQuadTeam, geo);
     const uint32_t grid = grid_for(n, kBlock / 64, geo);
 #if CTS_TUNING
@@ -2410,6 +2412,21 @@ hipError_t launch_media_stream_status(const uint8_t* arena, uint64_t arena_bytes
     const ContigGrid cg = contig_grid(n, geo);
     const MsSource src{descs, lengths, stride};
 #if CTS_TUNING
+    if (geo.ms_variant == 8 || geo.ms_variant == 9) {
+        // one pass, statuses written every round (8) or every 16 rounds from the per-wave ring (9)
+#define CTS_MS_STATUS_K(NT, STR, K)                                                                         \
+    media_stream_verify_quad_kernel<6, NT, true, true, true, STR, K, true><<<cg.grid, kBlock, 0, stream>>>( \
+        arena, arena_bytes, src, n, status, nullptr, counters, cg.per)
+        if (geo.ms_variant == 8) {
+            if (descs == nullptr) CTS_MS_STATUS_K(true, true, 0);
+            else CTS_MS_STATUS_K(true, false, 0);
+        } else {
+            if (descs == nullptr) CTS_MS_STATUS_K(true, true, 16);
+            else CTS_MS_STATUS_K(true, false, 16);
+        }
+#undef CTS_MS_STATUS_K
+        return hipGetLastError();
+    }
     if (geo.ms_variant == 7) {
         // two passes: headers -> statuses (pass = 1 for DATA), then the payload verify clearing pass on
         // failures. Measured slower than one pass (4.25 vs 4.08 ms per 16 M datagrams): the header gather's
@@ -2437,9 +2454,11 @@ hipError_t launch_media_stream_status(const uint8_t* arena, uint64_t arena_bytes
         return hipGetLastError();
     }
 #endif
-    // one pass: the variant-3 walk writing each datagram's status as it verifies
-#define CTS_MS_STATUS(NT, STR)                                                                              \
-    media_stream_verify_quad_kernel<6, NT, true, true, true, STR, 0, true><<<cg.grid, kBlock, 0, stream>>>( \
+    // one pass: the variant-3 walk, each wave staging its datagrams' statuses in an LDS ring and writing 32
+    // rounds of them at a time (4.36-4.39 ms per 16 M datagrams against 4.47-4.50 written every round, two
+    // boxes: profiles/r02/ms_status/)
+#define CTS_MS_STATUS(NT, STR)                                                                               \
+    media_stream_verify_quad_kernel<6, NT, true, true, true, STR, 32, true><<<cg.grid, kBlock, 0, stream>>>( \
         arena, arena_bytes, src, n, status, nullptr, counters, cg.per)
     if (descs == nullptr) {
         if (geo.nontemporal) CTS_MS_STATUS(true, true);
