@@ -112,8 +112,8 @@ int cts_media_stream_verify_strided(cts_engine* engine, const void* dev_arena, u
  * written. The sender timestamps of cts_datagram_record feed only the jitter log and its time-in-flight
  * estimate (ctsIOPatternMediaStream.cpp:218-223, 366-393; ctsConfig.cpp:3910-3930), and a failing payload
  * ends the stream whatever its first mismatch was (:185-190), so 16 bytes per datagram replace the 32-byte
- * record and the 12-byte result. (Per 16 M datagrams the receive pass takes 4.08-4.42 ms with statuses against
- * 4.31-4.69 ms with records + results and 3.66 ms with no outputs, by box: DESIGN.md section 3.) */
+ * record and the 12-byte result. (Per 16 M datagrams the receive pass takes 3.99-4.39 ms with statuses against
+ * 4.31-4.89 ms with records + results and 3.67 ms with no outputs, by box: DESIGN.md section 3.) */
 typedef struct cts_datagram_status {
     int64_t sequence_number;  /* DATA datagrams: header bytes 2..9 (GetSequenceNumberFromTask); otherwise 0 */
     uint32_t completed_bytes;
