@@ -26,6 +26,8 @@
 // ("What did not work").
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "cts_internal.hpp"
 
 namespace cts {
@@ -1079,7 +1081,8 @@ __device__ __forceinline__ uint32_t result_dw2(uint32_t expected, uint32_t actua
     return (expected & 0xFFu) | ((actual & 0xFFu) << 8) | (pass << 16) | (flags << 24);  // bytes 8..11
 }
 
-__device__ __forceinline__ void quad_stage_result(QuadOut& o, uint32_t t, uint32_t first_mismatch,
+template <typename O>
+__device__ __forceinline__ void quad_stage_result(O& o, uint32_t t, uint32_t first_mismatch,
                                                   uint32_t mismatch_bytes, uint32_t dw2)
 {
     o.res[t][0] = first_mismatch;
@@ -1118,9 +1121,14 @@ __device__ __forceinline__ void quad_flush_outputs(const QuadOut& o, uint32_t i,
 // FREQUENCY of the writes mixed into it, not with their bytes (tools/rw_mix_probe.hip: one dword per wave
 // per 4 KiB round costs the read 18 %, the same store on every 16th round 5 %, on every 64th round
 // nothing measurable; 4 to 120 bytes per store cost the same).
-template <int K>
+// A ring slot of the compact receive: four cts_datagram_status entries (4 dwords each), no result records.
+struct QuadStatusOut {
+    uint32_t rec[4][4];
+};
+
+template <int K, typename SlotT = QuadOut>
 struct QuadRing {
-    QuadOut slot[K];
+    SlotT slot[K];
     uint32_t i0[K];
 };
 
@@ -1128,8 +1136,8 @@ struct QuadRing {
 // the launch. Records go as write-through dwords (as quad_flush_outputs), 32 per round, results as
 // plain dwords, 12 per round.
 // RECDW = dwords per record: 8 (cts_datagram_record) or 4 (cts_datagram_status, staged in rec[t][0..3]).
-template <int K, int RECDW = 8>
-__device__ __forceinline__ void quad_ring_flush(const QuadRing<K>& g, uint32_t m, uint32_t n,
+template <int K, int RECDW = 8, typename SlotT = QuadOut>
+__device__ __forceinline__ void quad_ring_flush(const QuadRing<K, SlotT>& g, uint32_t m, uint32_t n,
                                                 cts_verify_result* results, void* records)
 {
     __builtin_amdgcn_wave_barrier();
@@ -1146,6 +1154,7 @@ __device__ __forceinline__ void quad_ring_flush(const QuadRing<K>& g, uint32_t m
             }
         }
     }
+    if constexpr (!std::is_same<SlotT, QuadStatusOut>::value)
     if (results != nullptr) {
 #pragma unroll 1
         for (uint32_t k = 0; k < (K * 12u + 63u) / 64u; ++k) {
@@ -1684,6 +1693,46 @@ __device__ __forceinline__ void ms_datagram(const MsSource& src, uint32_t i, uin
 // HDR16 = false: header bytes j and j + 16 by byte loads on every team lane, dwords gathered by
 // lane shuffles (ms_variant 1). HDR16 = true: three 16-byte header chunk loads on team lanes
 // 0..2, gathered on lane 0 by DPP row shifts; the DATA verdict is broadcast (ms_variant 2).
+// The team leader's staging of its datagram's outputs into slot o (a QuadOut, or a ring slot).
+#define CTS_MS_STAGE(o)                                                                                           \
+    do {                                                                                                          \
+            const uint32_t t = team & 3u;                                                                         \
+            if constexpr (STATUS) {                                                                               \
+                if (records != nullptr) {                                                                         \
+                    /* cts_datagram_status as dwords: seq, completed bytes, flag | kind | pass */ \
+                    o.rec[t][0] = data ? (H[0] >> 16) | (H[1] << 16) : 0u;                                        \
+                    o.rec[t][1] = data ? (H[1] >> 16) | (H[2] << 16) : 0u;                                        \
+                    o.rec[t][2] = completed;                                                                      \
+                    o.rec[t][3] = (flag & 0xFFFFu) | (kind << 16) | ((data && first == kNone) ? 1u << 24 : 0u);   \
+                }                                                                                                 \
+            } else if (records != nullptr) {                                                                      \
+                /* cts_datagram_record as dwords: seq = header bytes 2..9 (GetSequenceNumberFromTask); */ \
+                /* ctsIOPatternMediaStream.cpp:218-219 read the sender qpc / qpf at bytes 8 and 16 */ \
+                o.rec[t][0] = data ? (H[0] >> 16) | (H[1] << 16) : 0u;                                            \
+                o.rec[t][1] = data ? (H[1] >> 16) | (H[2] << 16) : 0u;                                            \
+                o.rec[t][2] = data ? H[2] : 0u;                                                                   \
+                o.rec[t][3] = data ? H[3] : 0u;                                                                   \
+                o.rec[t][4] = data ? H[4] : 0u;                                                                   \
+                o.rec[t][5] = data ? H[5] : 0u;                                                                   \
+                o.rec[t][6] = (flag & 0xFFFFu) | (kind << 16);  /* flag, kind, reserved = 0 */ \
+                o.rec[t][7] = completed;                                                                          \
+            }                                                                                                     \
+            if (!data) {                                                                                          \
+                if constexpr (!STATUS)                                                                            \
+                quad_stage_result(o, t, 0u, 0u,                                                                   \
+                                  result_dw2(0u, 0u, 0u, kind == CTS_DGRAM_BAD_DESC ? CTS_RESULT_FLAG_BAD_DESC    \
+                                                                                   : CTS_RESULT_FLAG_NOT_DATA));  \
+            } else {                                                                                              \
+                const bool pass = first == kNone;                                                                 \
+                if constexpr (!STATUS)                                                                            \
+                if (results != nullptr)                                                                           \
+                    quad_stage_result(o, t, pass ? q.len : first, pass ? 0u : count,                              \
+                                      pass ? result_dw2(0u, 0u, 1u, 0u)                                           \
+                                           : result_dw2(pattern_byte_dev(first), q.sp[first], 0u, 0u));           \
+                qc.add(q.len, pass, count);                                                                       \
+            }                                                                                                     \
+    } while (0)
+
 // RING > 0: outputs staged in a per-wave ring of RING rounds and written every RING rounds (QuadRing).
 // STATUS: records points at 16-byte cts_datagram_status entries (results unused).
 // FAILMARK: records points at statuses ms_status_gather_kernel already wrote; only a corrupt DATA datagram's
@@ -1698,7 +1747,8 @@ __global__ void __launch_bounds__(kBlock)
     constexpr int TEAMS = kBlock / kQuadTeam;
     __shared__ uint64_t ctr[TEAMS][5];
     __shared__ QuadOut qout[RING ? 1 : kBlock / 64];
-    __shared__ QuadRing<RING ? RING : 1> qring[RING ? kBlock / 64 : 1];
+    using RingSlot = typename std::conditional<STATUS, QuadStatusOut, QuadOut>::type;
+    __shared__ QuadRing<RING ? RING : 1, RingSlot> qring[RING ? kBlock / 64 : 1];
     uint32_t rs = 0;  // RING: this wave's next ring slot (wave-uniform)
     const uint32_t lane = threadIdx.x & (kQuadTeam - 1);
     const uint32_t team = threadIdx.x / kQuadTeam;
@@ -1803,54 +1853,30 @@ __global__ void __launch_bounds__(kBlock)
             continue;
         }
         if (lane == 0u && live) {
-            QuadOut& o = RING ? qring[RING ? team >> 2 : 0].slot[rs] : qout[RING ? 0 : team >> 2];
-            const uint32_t t = team & 3u;
-            if (STATUS && records != nullptr) {
-                // cts_datagram_status as dwords: seq, completed bytes, flag | kind | pass
-                o.rec[t][0] = data ? (H[0] >> 16) | (H[1] << 16) : 0u;
-                o.rec[t][1] = data ? (H[1] >> 16) | (H[2] << 16) : 0u;
-                o.rec[t][2] = completed;
-                o.rec[t][3] = (flag & 0xFFFFu) | (kind << 16) | ((data && first == kNone) ? 1u << 24 : 0u);
-            } else if (records != nullptr) {
-                // cts_datagram_record as dwords: seq = header bytes 2..9 (GetSequenceNumberFromTask);
-                // ctsIOPatternMediaStream.cpp:218-219 read the sender qpc / qpf at bytes 8 and 16
-                o.rec[t][0] = data ? (H[0] >> 16) | (H[1] << 16) : 0u;
-                o.rec[t][1] = data ? (H[1] >> 16) | (H[2] << 16) : 0u;
-                o.rec[t][2] = data ? H[2] : 0u;
-                o.rec[t][3] = data ? H[3] : 0u;
-                o.rec[t][4] = data ? H[4] : 0u;
-                o.rec[t][5] = data ? H[5] : 0u;
-                o.rec[t][6] = (flag & 0xFFFFu) | (kind << 16);  // flag, kind, reserved = 0
-                o.rec[t][7] = completed;
-            }
-            if (!data) {
-                quad_stage_result(o, t, 0u, 0u,
-                                  result_dw2(0u, 0u, 0u, kind == CTS_DGRAM_BAD_DESC ? CTS_RESULT_FLAG_BAD_DESC
-                                                                                   : CTS_RESULT_FLAG_NOT_DATA));
+            if constexpr (RING > 0) {
+                auto& o_ = qring[team >> 2].slot[rs];
+                CTS_MS_STAGE(o_);
             } else {
-                const bool pass = first == kNone;
-                if (results != nullptr)
-                    quad_stage_result(o, t, pass ? q.len : first, pass ? 0u : count,
-                                      pass ? result_dw2(0u, 0u, 1u, 0u)
-                                           : result_dw2(pattern_byte_dev(first), q.sp[first], 0u, 0u));
-                qc.add(q.len, pass, count);
+                CTS_MS_STAGE(qout[team >> 2]);
             }
         }
         if constexpr (RING == 0) {
             quad_flush_outputs<STATUS ? 4 : 8>(qout[team >> 2], i, w.end, STATUS ? nullptr : results, records);
         } else {
-            QuadRing<RING>& g = qring[team >> 2];
+            auto& g = qring[team >> 2];
             const uint32_t i0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)i);
             if ((threadIdx.x & 63u) == 0u) g.i0[rs] = i0;
             if (++rs == (uint32_t)RING) {
-                quad_ring_flush<RING, STATUS ? 4 : 8>(g, RING, w.end, STATUS ? nullptr : results, records);
+                quad_ring_flush<RING, STATUS ? 4 : 8, RingSlot>(g, RING, w.end, STATUS ? nullptr : results, records);
                 rs = 0;
             }
         }
         w.i = inext;
     }
     if constexpr (RING > 0)
-        if (rs) quad_ring_flush<RING, STATUS ? 4 : 8>(qring[team >> 2], rs, w.end, STATUS ? nullptr : results, records);
+        if (rs)
+            quad_ring_flush<RING, STATUS ? 4 : 8, RingSlot>(qring[team >> 2], rs, w.end, STATUS ? nullptr : results,
+                                                           records);
     qc.flush<TEAMS>(ctr, team, lane, counters);
 }
 
@@ -2325,8 +2351,8 @@ hipError_t launch_media_stream_verify(const uint8_t* arena, uint64_t arena_bytes
     // 2 = four per wave, header by three 16-byte chunk loads + DPP, 3 = variant 2 walking
     // block-contiguous datagram ranges (default), 4 / 5 / 6 = variant 3 writing its outputs every
     // 8 / 16 / 32 rounds from a per-wave LDS ring (7: the two-pass form of cts_media_stream_verify_status;
-    // 8 / 9: its one-pass form with the statuses written every round / every 16 rounds; the product writes
-    // them every 32 rounds)
+    // 8 / 9 / 10: its one-pass form with the statuses written every round / every 16 / 32 rounds; the product
+    // writes them every 64 rounds)
     const uint32_t qgrid = grid_for(n, kBlock / kQuadTeam, geo);
     const uint32_t grid = grid_for(n, kBlock / 64, geo);
 #if CTS_TUNING
@@ -2412,14 +2438,17 @@ hipError_t launch_media_stream_status(const uint8_t* arena, uint64_t arena_bytes
     const ContigGrid cg = contig_grid(n, geo);
     const MsSource src{descs, lengths, stride};
 #if CTS_TUNING
-    if (geo.ms_variant == 8 || geo.ms_variant == 9) {
-        // one pass, statuses written every round (8) or every 16 rounds from the per-wave ring (9)
+    if (geo.ms_variant == 8 || geo.ms_variant == 9 || geo.ms_variant == 10) {
+        // one pass, statuses written every round (8), or every 16 / 32 rounds from the per-wave ring (9 / 10)
 #define CTS_MS_STATUS_K(NT, STR, K)                                                                         \
     media_stream_verify_quad_kernel<6, NT, true, true, true, STR, K, true><<<cg.grid, kBlock, 0, stream>>>( \
         arena, arena_bytes, src, n, status, nullptr, counters, cg.per)
         if (geo.ms_variant == 8) {
             if (descs == nullptr) CTS_MS_STATUS_K(true, true, 0);
             else CTS_MS_STATUS_K(true, false, 0);
+        } else if (geo.ms_variant == 10) {
+            if (descs == nullptr) CTS_MS_STATUS_K(true, true, 32);
+            else CTS_MS_STATUS_K(true, false, 32);
         } else {
             if (descs == nullptr) CTS_MS_STATUS_K(true, true, 16);
             else CTS_MS_STATUS_K(true, false, 16);
@@ -2454,11 +2483,12 @@ hipError_t launch_media_stream_status(const uint8_t* arena, uint64_t arena_bytes
         return hipGetLastError();
     }
 #endif
-    // one pass: the variant-3 walk, each wave staging its datagrams' statuses in an LDS ring and writing 32
-    // rounds of them at a time (4.36-4.39 ms per 16 M datagrams against 4.47-4.50 written every round, two
-    // boxes: profiles/r02/ms_status/)
+    // one pass: the variant-3 walk, each wave staging its datagrams' statuses in an LDS ring and writing 64
+    // rounds of them at a time -- for config 3 (1024 datagrams per workgroup) once, at the workgroup's end.
+    // Per 16 M datagrams 4.30-4.31 ms against 4.44 with 32 rounds and 4.54 written every round, one box
+    // (profiles/r02/ms_status/)
 #define CTS_MS_STATUS(NT, STR)                                                                               \
-    media_stream_verify_quad_kernel<6, NT, true, true, true, STR, 32, true><<<cg.grid, kBlock, 0, stream>>>( \
+    media_stream_verify_quad_kernel<6, NT, true, true, true, STR, 64, true><<<cg.grid, kBlock, 0, stream>>>( \
         arena, arena_bytes, src, n, status, nullptr, counters, cg.per)
     if (descs == nullptr) {
         if (geo.nontemporal) CTS_MS_STATUS(true, true);

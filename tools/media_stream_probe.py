@@ -64,6 +64,7 @@ def main():
                   ("ms+status_two_pass", ("ms", 7, ch), lambda a: MS.verify_status(eng, a, d, status=st)),
                   ("ms+status_every_round", ("ms", 8, ch), lambda a: MS.verify_status(eng, a, d, status=st)),
                   ("ms+status_ring16", ("ms", 9, ch), lambda a: MS.verify_status(eng, a, d, status=st)),
+                  ("ms+status_ring32", ("ms", 10, ch), lambda a: MS.verify_status(eng, a, d, status=st)),
                   ("ms_strided+status", ("ms", 3, ch),
                    lambda a: MS.verify_strided_status(eng, a, w.max_length, lens, status=st))]
     cases = [c for c in cases if not only or c[0] in only]
