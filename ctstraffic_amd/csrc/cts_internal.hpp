@@ -27,7 +27,7 @@ constexpr int kDefaultMediaStreamVariant = 3;
 #if CTS_TUNING
 constexpr int kVerifyVariants = 19;  // workgroup-per-buffer verify variants (launch_verify)
 constexpr int kSmallVariants = 10;   // small-buffer (datagram) verify variants
-constexpr int kMediaStreamVariants = 11;  // MediaStream receive kernels (launch_media_stream_verify)
+constexpr int kMediaStreamVariants = 12;  // MediaStream receive kernels (launch_media_stream_verify)
 #endif
 // A launch-variant attribute value this build can launch.
 inline bool variant_ok(int value, int dflt, int count)

@@ -1116,6 +1116,11 @@ __device__ __forceinline__ void quad_flush_outputs(const QuadOut& o, uint32_t i,
     __builtin_amdgcn_wave_barrier();
 }
 
+// The MediaStream receive writes its records + results every kMsRing rounds from the per-wave ring: for config 3
+// (1 024 datagrams per workgroup, 64 rounds per wave) once, at the workgroup's end. 4.25 vs 4.30 ms per 16 M
+// datagrams written every round (two boxes, profiles/r02/ms_records_ring/); 45 KB of LDS per workgroup.
+constexpr int kMsRing = 64;
+
 // Per-wave output ring: the staged outputs of K rounds (QuadOut slots) and each round's first buffer
 // index, written by the wave every K rounds instead of every round. A read stream slows down with the
 // FREQUENCY of the writes mixed into it, not with their bytes (tools/rw_mix_probe.hip: one dword per wave
@@ -2349,8 +2354,8 @@ hipError_t launch_media_stream_verify(const uint8_t* arena, uint64_t arena_bytes
 #define CTS_MS_ARGS arena, arena_bytes, MsSource{descs, nullptr, 0u}, n, records, results, counters
     // ms_variant: 0 = one wave per datagram, 1 = four datagrams per wave (header by byte loads),
     // 2 = four per wave, header by three 16-byte chunk loads + DPP, 3 = variant 2 walking
-    // block-contiguous datagram ranges (default), 4 / 5 / 6 = variant 3 writing its outputs every
-    // 8 / 16 / 32 rounds from a per-wave LDS ring (7: the two-pass form of cts_media_stream_verify_status;
+    // block-contiguous datagram ranges and writing its outputs every kMsRing = 64 rounds from a per-wave LDS
+    // ring (default), 4 / 5 / 6 = the same every 8 / 16 / 32 rounds, 11 = every round (7: the two-pass form of cts_media_stream_verify_status;
     // 8 / 9 / 10: its one-pass form with the statuses written every round / every 16 / 32 rounds; the product
     // writes them every 64 rounds)
     const uint32_t qgrid = grid_for(n, kBlock / kQuadTeam, geo);
@@ -2372,7 +2377,8 @@ hipError_t launch_media_stream_verify(const uint8_t* arena, uint64_t arena_bytes
         break;
     case 4:
     case 5:
-    case 6: {  // variant 3 with its outputs written every 8 / 16 / 32 rounds from a per-wave ring
+    case 6:
+    case 11: {  // variant 3 with its outputs written every 8 / 16 / 32 rounds from a per-wave ring / every round
         const ContigGrid cg = contig_grid(n, geo);
 #define CTS_MS_RING(K)                                                                                              \
     (nt ? (media_stream_verify_quad_kernel<6, true, true, true, true, false, K><<<cg.grid, kBlock, 0, stream>>>(   \
@@ -2383,18 +2389,19 @@ hipError_t launch_media_stream_verify(const uint8_t* arena, uint64_t arena_bytes
            0))
         if (geo.ms_variant == 4) (void)CTS_MS_RING(8);
         else if (geo.ms_variant == 5) (void)CTS_MS_RING(16);
-        else (void)CTS_MS_RING(32);
+        else if (geo.ms_variant == 6) (void)CTS_MS_RING(32);
+        else (void)CTS_MS_RING(0);
 #undef CTS_MS_RING
         break;
     }
     default: {
         const ContigGrid cg = contig_grid(n, geo);
         if (nt)
-            media_stream_verify_quad_kernel<6, true, true, true, true><<<cg.grid, kBlock, 0, stream>>>(CTS_MS_ARGS,
-                                                                                                     cg.per);
+            media_stream_verify_quad_kernel<6, true, true, true, true, false, kMsRing><<<cg.grid, kBlock, 0, stream>>>(
+                CTS_MS_ARGS, cg.per);
         else
-            media_stream_verify_quad_kernel<6, false, true, true, true><<<cg.grid, kBlock, 0, stream>>>(CTS_MS_ARGS,
-                                                                                                      cg.per);
+            media_stream_verify_quad_kernel<6, false, true, true, true, false, kMsRing><<<cg.grid, kBlock, 0, stream>>>(
+                CTS_MS_ARGS, cg.per);
         break;
     }
     }
@@ -2403,9 +2410,11 @@ hipError_t launch_media_stream_verify(const uint8_t* arena, uint64_t arena_bytes
     (void)grid;
     const ContigGrid cg = contig_grid(n, geo);  // MediaStream variant 3 (kDefaultMediaStreamVariant)
     if (geo.nontemporal)
-        media_stream_verify_quad_kernel<6, true, true, true, true><<<cg.grid, kBlock, 0, stream>>>(CTS_MS_ARGS, cg.per);
+        media_stream_verify_quad_kernel<6, true, true, true, true, false, kMsRing><<<cg.grid, kBlock, 0, stream>>>(
+            CTS_MS_ARGS, cg.per);
     else
-        media_stream_verify_quad_kernel<6, false, true, true, true><<<cg.grid, kBlock, 0, stream>>>(CTS_MS_ARGS, cg.per);
+        media_stream_verify_quad_kernel<6, false, true, true, true, false, kMsRing><<<cg.grid, kBlock, 0, stream>>>(
+            CTS_MS_ARGS, cg.per);
 #endif
 #undef CTS_MS_ARGS
     return hipGetLastError();
@@ -2421,10 +2430,10 @@ hipError_t launch_media_stream_verify_strided(const uint8_t* arena, uint64_t are
     const ContigGrid cg = contig_grid(n, geo);
     const MsSource src{nullptr, lengths, stride};
     if (geo.nontemporal)
-        media_stream_verify_quad_kernel<6, true, true, true, true, true><<<cg.grid, kBlock, 0, stream>>>(
+        media_stream_verify_quad_kernel<6, true, true, true, true, true, kMsRing><<<cg.grid, kBlock, 0, stream>>>(
             arena, arena_bytes, src, n, records, results, counters, cg.per);
     else
-        media_stream_verify_quad_kernel<6, false, true, true, true, true><<<cg.grid, kBlock, 0, stream>>>(
+        media_stream_verify_quad_kernel<6, false, true, true, true, true, kMsRing><<<cg.grid, kBlock, 0, stream>>>(
             arena, arena_bytes, src, n, records, results, counters, cg.per);
     return hipGetLastError();
 }

@@ -208,7 +208,7 @@ def _to_dev(a, torch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("ms_variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10])
+@pytest.mark.parametrize("ms_variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11])
 def test_gpu_media_stream_verify_matches_oracle(engine, tuning_engine, ms_variant):
     """ms_variant 0: one wave per datagram; 1: four datagrams per wave, header by byte loads;
     2: four per wave, header by 16-byte chunk loads gathered with DPP row shifts; 3: variant 2
@@ -218,7 +218,8 @@ def test_gpu_media_stream_verify_matches_oracle(engine, tuning_engine, ms_varian
     block/chunk shapes below); 7: variant 3, with cts_media_stream_verify_status in its two-pass form (header
     gather, then a payload pass that only clears the pass byte of corrupt datagrams); 8 / 9: variant 3 with the
     statuses of cts_media_stream_verify_status written every round / every 16 rounds, 10: every 32 rounds (the
-    product default stages them in the per-wave ring for 64 rounds)."""
+    product default stages them in the per-wave ring for 64 rounds); 11: variant 3 writing records + results every
+    round (the product writes them every 64 rounds from the ring)."""
     from ctstraffic_amd import _lib
 
     if ms_variant != 3:
