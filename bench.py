@@ -15,16 +15,24 @@ verifying a stream of batches would run. roofline.achieved comes from a separate
 serialized leg (one stream, HIP events), the per-kernel time rocprof reports.
 
 Usage:  python bench.py [--gpus N] [--steps K] [--warmup W]
-        N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+        N>1: either form works; with no WORLD_SIZE in the environment, `bench.py --gpus N` starts the N ranks
+        itself as a child `torch.distributed.run` (before anything touches the GPU) and exits with its code:
+          python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+          python bench.py --gpus N
+        A WORLD_SIZE that differs from --gpus is an error (exit 2): the line's n_gpus is what ran.
 Each rank verifies its own shard (no data-path collective: "scaling": "weak");
 one RCCL all-reduce of the 5 ctsStatistics-style counters closes the timed region.
-Rank 0 prints ONE JSON line.
+After it, at every N, rank 0 times the CPU oracle over its own batch (cpu_baseline; the other ranks wait on a
+gloo barrier) and the single-process leg (`--engines N`, one process driving all N GPUs, run as a child
+process) and puts both into the same line. Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -67,7 +75,104 @@ def parse():
                         "(profiles/r02/numa/); the device-resident legs do not care")
     p.add_argument("--verify-variant", type=int, default=-1,
                    help="CTS_ATTR_VERIFY_VARIANT for both legs (-1 = engine default; tuning builds only)")
+    p.add_argument("--no-engines-leg", action="store_true",
+                   help="skip the single-process leg (--engines N as a child process) in the line's extras")
+    p.add_argument("--stub-gpu", action="store_true",
+                   help="launcher test: every rank reports its RANK/WORLD_SIZE over gloo and rank 0 prints one line; "
+                        "nothing touches a GPU (tests/test_bench_launcher.py)")
     return p.parse_args()
+
+
+# environment keys of a torch.distributed.run rank; a child started from a rank (the single-process leg) drops
+# them so it runs as a 1-process job of its own
+_DIST_ENV = ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "GROUP_WORLD_SIZE", "ROLE_RANK",
+             "ROLE_WORLD_SIZE", "ROLE_NAME", "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID",
+             "TORCHELASTIC_RESTART_COUNT", "TORCHELASTIC_MAX_RESTARTS", "TORCHELASTIC_USE_AGENT_STORE",
+             "TORCHELASTIC_ERROR_FILE", "TORCH_NCCL_ASYNC_ERROR_HANDLING")
+
+
+class _StdoutToStderr:
+    """Point fd 1 at fd 2 for a block: gloo's C++ rendezvous prints "[Gloo] Rank r is connected to ..." on stdout,
+    and the driver reads exactly one JSON line from it."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args):
+    """`bench.py --gpus N` without WORLD_SIZE: start the N ranks as ONE child process tree
+    (torch.distributed.run, one rank per GPU, rendezvous on 127.0.0.1) and return its exit code. This process
+    never touches the GPU and never execs; rank 0's JSON line reaches our stdout unchanged."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    sys.stdout.flush()
+    return subprocess.call(cmd, env=env)
+
+
+def stub_main(args):
+    """--stub-gpu: the launcher's CPU test. Each rank joins a gloo group from the torch.distributed.run
+    environment and reports (RANK, WORLD_SIZE, LOCAL_RANK); rank 0 prints one line shaped like the real one."""
+    import torch
+    import torch.distributed as dist
+
+    from ctstraffic_amd import distributed as D
+
+    world, rank, local = D.dist_env()
+    if world > 1:
+        with _StdoutToStderr():
+            D.init("gloo")
+    me = torch.tensor([rank, world, local], dtype=torch.int64)
+    seen = [torch.zeros_like(me) for _ in range(world)]
+    if world > 1:
+        dist.all_gather(seen, me)
+    else:
+        seen = [me]
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": 0.0, "unit": "GiB/s", "n_gpus": world, "stub": True,
+                          "ranks": [[int(x) for x in t.tolist()] for t in seen]}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+def engines_leg(args, world):
+    """The single-process leg at this N (`bench.py --engines N`: one process, one engine per GPU, counters folded
+    on the host), run as a child process with the rank environment removed. Returns a dict for the line's extras."""
+    env = {k: v for k, v in os.environ.items() if k not in _DIST_ENV}
+    cmd = [sys.executable, os.path.abspath(__file__), "--engines", str(world), "--no-cpu-baseline", "--no-extras",
+           "--steps", str(args.steps), "--warmup", str(args.warmup), "--arenas", str(args.arenas),
+           "--buffers", str(args.buffers), "--pipeline-streams", str(args.pipeline_streams)]
+    try:
+        r = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=600)
+    except subprocess.TimeoutExpired:
+        return {"error": "timed out after 600 s"}
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    if r.returncode != 0 or not lines:
+        return {"error": "exit %d: %s" % (r.returncode, r.stderr.strip().splitlines()[-1:] or "")}
+    j = json.loads(lines[-1])
+    return {"value": j["value"], "unit": j["unit"], "n_gpus": j["n_gpus"], "ms_per_step": j["ms_per_step"],
+            "per_gpu_GiBps": j.get("per_gpu_GiBps"), "parity": j.get("parity"),
+            "process_model": "one process, one engine per GPU (cts_engine_create(g)), one host thread + %d streams "
+                             "each, connections by cts_shard_of, counters folded by cts_counters_read_multi"
+                             % args.pipeline_streams}
 
 
 class Batch:
@@ -121,6 +226,14 @@ class Batch:
 def main():
     args = parse()
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1 and args.engines == 0:
+        sys.exit(launch_ranks(args))  # before anything touches the GPU
+    if int(os.environ.get("WORLD_SIZE", "1")) != args.gpus and args.engines == 0:
+        print("bench.py: WORLD_SIZE=%s but --gpus %d: the line's n_gpus must be what ran"
+              % (os.environ.get("WORLD_SIZE", "1"), args.gpus), file=sys.stderr)
+        sys.exit(2)
+    if args.stub_gpu:
+        sys.exit(stub_main(args))
     import torch
 
     from ctstraffic_amd.distributed import dist_env
@@ -143,8 +256,13 @@ def main():
     from ctstraffic_amd import Engine, _lib, workload as W
     from ctstraffic_amd import distributed as D
 
+    cpu_group = None
     if world > 1:
-        D.init(args.dist_backend, device=torch.device(dev) if args.dist_backend == "nccl" else None)
+        with _StdoutToStderr():
+            D.init(args.dist_backend, device=torch.device(dev) if args.dist_backend == "nccl" else None)
+            # host-side waits (while rank 0 runs the CPU baseline and the single-process leg) go over gloo, so
+            # the waiting ranks hold no spinning collective kernel on their GPUs
+            cpu_group = dist.new_group(backend="gloo")
 
     # --verify-variant: A/B runs use the tuning build (every launch variant); the product runs variant 13
     engine = Engine(gpu, tuning=args.verify_variant >= 0)
@@ -265,6 +383,13 @@ def main():
     barrier()
     t1 = time.perf_counter()
     elapsed = D.max_over_ranks(t1 - t0, device=dev)
+    # each rank's own rate over its own bytes and its own clock (the max-over-ranks clock sets `value`)
+    per_rank = [bytes_per_step * K / (t1 - t0) / GIB]
+    if world > 1:
+        mine = torch.tensor([per_rank[0]], dtype=torch.float64)
+        allr = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine, group=cpu_group)
+        per_rank = [float(x.item()) for x in allr]
     pipe_launch_s = ev_a.elapsed_time(ev_b) / 1e3 / launches
 
     # S = 1: the events on the launch stream bracket exactly the K*R launches of the headline leg, and the
@@ -299,12 +424,21 @@ def main():
 
     extras = {}
     cpu = None
-    if rank == 0 and world == 1:
+    if rank == 0:
         want = set(x for x in args.extras_only.split(",") if x) or {"fill", "datagram", "host", "loopback"}
-        if not args.no_extras:
+        if not args.no_extras and world == 1:
             extras = run_extras(engine, torch, W, w, B.arenas, B.descs, dev, want)
         if not args.no_cpu_baseline:
+            # at every N: the reference's CPU verify beside the GPU number (rank 0's host, rank 0's batch)
             cpu = cpu_baseline(B.arenas[0], w, args.cpu_seconds)
+        if not (args.no_engines_leg or args.no_extras or args.extras_only):
+            if world <= torch.cuda.device_count():
+                extras["engines_single_process"] = engines_leg(args, world)
+            else:
+                extras["engines_single_process"] = {"skipped": "%d ranks share %d visible GPU(s)"
+                                                    % (world, torch.cuda.device_count())}
+    if world > 1:
+        dist.barrier(group=cpu_group)
 
     traffic, traffic_src = pmc_traffic(w.name, args.buffers)
     kernel = verify_kernel_name(engine)
@@ -371,6 +505,7 @@ def main():
             "parity": {"counters_match_expected": bool(parity_ok), "records_and_first_fail_match": bool(outputs_ok),
                        "counters": local_ctr},
         }
+        line["per_rank_GiBps"] = [round(x, 1) for x in per_rank]
         if allreduce_us is not None:
             line["allreduce_counters_us"] = round(allreduce_us, 1)
         if extras:

@@ -9,6 +9,7 @@
 //                             threadpool timers, fed with the records and verify
 //                             results cts_media_stream_verify produces on the GPU.
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -36,6 +37,13 @@ uint32_t update_buffer_length(int64_t bytes_to_send, uint32_t max_datagram)
     }
     return total;
 }
+
+// the process-wide UdpStatusDetails (ctsConfig.h:417): every client adds to it exactly where it adds to its own
+// ctsUdpStatistics (ctsIOPatternMediaStream.cpp:195-202, 245-246, 385-386, 405-406, 420-421, 501-502)
+struct UdpStatusDetails {
+    std::atomic<int64_t> bits_received{0}, successful_frames{0}, dropped_frames{0}, duplicate_frames{0},
+        error_frames{0};
+} g_udp;
 
 struct Frame {  // ctsConfig::JitterFrameEntry (ctsConfig.h:188-197)
     int64_t bytes_received = 0;
@@ -104,12 +112,15 @@ struct cts_media_stream_client {
         }
         if (h.bytes_received == (int64_t)cfg.frame_size_bytes) {
             ++successful;
+            g_udp.successful_frames.fetch_add(1, std::memory_order_relaxed);  // :385-386
             if (first_frame.receiver_qpc == 0) first_frame = h;
             previous_frame = h;
         } else if (h.bytes_received < (int64_t)cfg.frame_size_bytes) {
             ++dropped;
+            g_udp.dropped_frames.fetch_add(1, std::memory_order_relaxed);  // :405-406
         } else {
             ++duplicate;
+            g_udp.duplicate_frames.fetch_add(1, std::memory_order_relaxed);  // :420-421
         }
         h.sequence_number += (int64_t)frames.size();
         h.bytes_received = 0;
@@ -206,9 +217,11 @@ int complete_datagrams(cts_media_stream_client* c, uint32_t n, At at, int64_t re
                 break;
             }
             c->bits_received += (int64_t)r.completed * 8;
+            g_udp.bits_received.fetch_add((int64_t)r.completed * 8, std::memory_order_relaxed);  // :195-196
             const int64_t seq = r.seq;
             if (seq > c->final_frame) {
                 ++c->error_frames;  // an unknown seq number past the final frame
+                g_udp.error_frames.fetch_add(1, std::memory_order_relaxed);  // :201-202
             } else {
                 const ptrdiff_t slot = c->find(seq);
                 if (slot >= 0) {
@@ -220,6 +233,7 @@ int complete_datagrams(cts_media_stream_client* c, uint32_t n, At at, int64_t re
                     f.bytes_received += r.completed;
                 } else {
                     ++c->error_frames;  // a stale or a future seq number
+                    g_udp.error_frames.fetch_add(1, std::memory_order_relaxed);  // :245-246
                 }
             }
             break;
@@ -286,6 +300,7 @@ int cts_media_stream_client_render(cts_media_stream_client* c)
         if (!c->received_buffered_frames()) {
             // "have received nothing from the server": every frame counts as dropped, FatalAbort
             c->dropped += c->final_frame;
+            g_udp.dropped_frames.fetch_add(c->final_frame, std::memory_order_relaxed);  // :501-502
             c->finished = true;
             c->finished_code = 2;
             c->latch(CTS_STATUS_ERROR_NOT_ALL_DATA_TRANSFERRED);  // CompleteIo(FatalAbort), ctsIOPattern.cpp:385-388
@@ -321,6 +336,26 @@ int cts_media_stream_client_stats(const cts_media_stream_client* c, cts_media_st
 const char* cts_media_stream_client_connection_id(const cts_media_stream_client* c)
 {
     return c == nullptr ? nullptr : c->connection_id;
+}
+
+int cts_udp_status_details_read(cts_udp_status_details* o)
+{
+    if (o == nullptr) return CTS_E_INVALID;
+    o->bits_received = g_udp.bits_received.load();
+    o->successful_frames = g_udp.successful_frames.load();
+    o->dropped_frames = g_udp.dropped_frames.load();
+    o->duplicate_frames = g_udp.duplicate_frames.load();
+    o->error_frames = g_udp.error_frames.load();
+    return CTS_OK;
+}
+
+void cts_udp_status_details_reset(void)
+{
+    g_udp.bits_received = 0;
+    g_udp.successful_frames = 0;
+    g_udp.dropped_frames = 0;
+    g_udp.duplicate_frames = 0;
+    g_udp.error_frames = 0;
 }
 
 }  // extern "C"

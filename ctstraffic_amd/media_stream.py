@@ -42,6 +42,13 @@ class Stats(ctypes.Structure):
         return {f: int(getattr(self, f)) for f, _ in self._fields_}
 
 
+class UdpStatusDetails(ctypes.Structure):
+    """cts_udp_status_details: the process-wide UdpStatusDetails (ctsConfig.h:417)."""
+
+    _fields_ = [(f, ctypes.c_int64) for f in ("bits_received", "successful_frames", "dropped_frames",
+                                               "duplicate_frames", "error_frames")]
+
+
 def declare(L: ctypes.CDLL) -> None:
     P = ctypes.c_void_p
     u32, u64, i32, i64 = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int, ctypes.c_int64
@@ -60,11 +67,24 @@ def declare(L: ctypes.CDLL) -> None:
         "cts_media_stream_client_render": ([P], i32),
         "cts_media_stream_client_stats": ([P, ctypes.POINTER(Stats)], i32),
         "cts_media_stream_client_connection_id": ([P], ctypes.c_char_p),
+        "cts_udp_status_details_read": ([ctypes.POINTER(UdpStatusDetails)], i32),
+        "cts_udp_status_details_reset": ([], None),
     }
     for name, (argtypes, restype) in sigs.items():
         fn = getattr(L, name)
         fn.argtypes = argtypes
         fn.restype = restype
+
+
+def udp_status_details() -> dict:
+    """The process-wide UDP counters every MediaStreamClient feeds (cts_udp_status_details_read)."""
+    s = UdpStatusDetails()
+    check("cts_udp_status_details_read", lib().cts_udp_status_details_read(ctypes.byref(s)))
+    return {f: int(getattr(s, f)) for f, _ in s._fields_}
+
+
+def udp_status_details_reset() -> None:
+    lib().cts_udp_status_details_reset()
 
 
 def split(frame_bytes: int, max_datagram: int) -> np.ndarray:

@@ -184,6 +184,22 @@ int cts_media_stream_client_stats(const cts_media_stream_client* client, cts_med
 /* The client's connection id (37 bytes incl. NUL) once an ID datagram was applied. */
 const char* cts_media_stream_client_connection_id(const cts_media_stream_client* client);
 
+/* ---- process-wide UDP status counters (UdpStatusDetails, ctsConfig.h:417) ----
+ * Every client adds to these where it adds to its own cts_media_stream_stats, as
+ * ctsIOPatternMediaStream.cpp:195-202, 245-246, 385-386, 405-406, 420-421, 501-502 feed
+ * g_configSettings->UdpStatusDetails; the UDP status line and exit summary (cts_status.h) print them.
+ * A corrupt payload is not an error frame: it fails the stream (CorruptedBytes, :185-190), which the
+ * connection outcome (ProtocolErrors) counts. */
+typedef struct cts_udp_status_details {
+    int64_t bits_received;
+    int64_t successful_frames;
+    int64_t dropped_frames;
+    int64_t duplicate_frames;
+    int64_t error_frames;
+} cts_udp_status_details;
+int cts_udp_status_details_read(cts_udp_status_details* out);
+void cts_udp_status_details_reset(void);
+
 #ifdef __cplusplus
 } /* extern "C" */
 #endif

@@ -1,0 +1,49 @@
+"""CPU: bench.py's multi-rank launcher (VERDICT r02 "Next round" 1).
+
+`python bench.py --gpus N` with no WORLD_SIZE in the environment must start the N ranks itself (a child
+torch.distributed.run, before any GPU call) and pass rank 0's single JSON line through; a WORLD_SIZE that
+differs from --gpus must fail. `--stub-gpu` replaces the GPU work with a gloo all-gather of each rank's
+RANK / WORLD_SIZE / LOCAL_RANK, so this runs here.
+"""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(ROOT, "bench.py")
+_RANK_ENV = ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")
+
+
+def _env(**extra):
+    env = {k: v for k, v in os.environ.items() if k not in _RANK_ENV}
+    env.update(extra)
+    return env
+
+
+def test_gpus2_launches_two_ranks_and_prints_one_line():
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--stub-gpu"], env=_env(), cwd=ROOT,
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [x for x in r.stdout.splitlines() if x.strip()]
+    assert len(lines) == 1, r.stdout
+    j = json.loads(lines[0])
+    assert j["n_gpus"] == 2 and j["stub"] is True
+    # every rank ran with RANK / WORLD_SIZE / LOCAL_RANK set by the launcher
+    assert sorted(tuple(x) for x in j["ranks"]) == [(0, 2, 0), (1, 2, 1)]
+
+
+def test_gpus1_runs_in_process():
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "1", "--stub-gpu"], env=_env(), cwd=ROOT,
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    j = json.loads(r.stdout.strip())
+    assert j["n_gpus"] == 1 and j["ranks"] == [[0, 1, 0]]
+
+
+def test_world_size_must_equal_gpus():
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "1", "--stub-gpu"],
+                       env=_env(WORLD_SIZE="2", RANK="0", LOCAL_RANK="0"), cwd=ROOT,
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=120)
+    assert r.returncode != 0 and r.stdout.strip() == ""
+    assert "WORLD_SIZE=2 but --gpus 1" in r.stderr

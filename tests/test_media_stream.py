@@ -355,6 +355,67 @@ def test_gpu_media_stream_end_to_end(engine):
 
 
 @pytest.mark.gpu
+def test_gpu_media_stream_udp_status_line(engine):
+    """The UDP status output (ctsPrintStatus.hpp:314-446, ctsTraffic.cpp:173-200) over a GPU-verified stream:
+    fill -> one extra datagram with an unknown sequence number -> a corrupt payload in frame 7 -> the compact
+    receive pass -> the client, one frame per render tick. The process-wide counters equal the client's, and
+    the Errors column shows its error frames; the corruption itself fails the stream (CorruptedBytes) and is
+    the connection's ProtocolError, not an error frame (:185-190)."""
+    import torch
+
+    from ctstraffic_amd import status as S
+
+    frame, n_frames, buffered = 52083, 10, 3
+    lens = M.split(frame, 1472)
+    per = len(lens)
+    seqs = np.repeat(np.arange(1, n_frames + 1), per)
+    extra = 2 * per  # after frame 2: a datagram of frame 999 (> the final frame: an error frame, :198-208)
+    seqs = np.insert(seqs, extra, 999)
+    lengths = np.insert(np.tile(lens, n_frames), extra, 1472)
+    n = len(seqs)
+    descs = np.zeros(n, dtype=DESC_DTYPE)
+    descs["length"] = lengths
+    descs["byte_offset"] = np.concatenate([[0], np.cumsum(lengths[:-1].astype(np.uint64))])
+    hdrs = np.zeros(n, dtype=DGRAM_HEADER_DTYPE)
+    hdrs["sequence_number"], hdrs["qpf"] = seqs, 10_000_000
+    arena_bytes = int(lengths.sum())
+    a = torch.zeros(arena_bytes + 64, dtype=torch.uint8, device="cuda")[:arena_bytes]
+    dd = _to_dev(descs, torch)
+    M.fill(engine, a, dd, _to_dev(hdrs, torch))
+    bad = 6 * per + 1 + 2  # the third datagram of frame 7
+    a[int(descs["byte_offset"][bad]) + 26 + 500] ^= 0x81
+    st = torch.zeros(n * 16, dtype=torch.uint8, device="cuda")
+    M.verify_status(engine, a, dd, status=st)
+    torch.cuda.synchronize()
+    gs = st.cpu().numpy().view(DGRAM_STATUS_DTYPE)
+    er, eres, _ = oracle.media_stream_verify(a.cpu().numpy(), descs)
+    assert np.array_equal(gs, _status_of(er, eres))
+    M.udp_status_details_reset()
+    c = M.MediaStreamClient(frame, buffered, n_frames)
+    # the datagrams of frame f + 1, the extra one arriving with frame 2
+    starts = [0] + [f * per + (1 if f >= 2 else 0) for f in range(1, n_frames)] + [n]
+    status = 0
+    for f in range(n_frames):
+        status, consumed = c.complete_status(gs[starts[f]:starts[f + 1]])
+        if status != 0:
+            break
+        c.render()
+    s = c.stats()
+    assert status == 2 and s["last_error"] == OM.DATA_MISMATCH and s["fail_datagram"] == bad
+    assert s["error_frames"] == 1 and s["successful_frames"] == 6
+    udp = M.udp_status_details()
+    assert udp == {f: s[f] for f in udp}
+    line = S.udp_line(S.CONSOLE, current_time_ms=1000, start_time_ms=0, end_time_ms=1000, active_streams=1,
+                      **udp)
+    assert line[79 - 7:79].strip() == str(s["error_frames"]) == "1"
+    assert line[48 - 9:48].strip() == str(s["successful_frames"])
+    summ = S.udp_summary(0, 0, 1, **udp)
+    assert "ProtocolErrors [1]" in summ and "  Total Error Frames : 1 (" in summ
+    assert "  Total Bytes Recv : %d\n" % (udp["bits_received"] // 8) in summ
+    M.udp_status_details_reset()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("stride", [1536, 1500, 9017])
 def test_gpu_media_stream_verify_strided_matches_oracle(engine, stride):
     """cts_media_stream_verify_strided: a receive ring of datagrams at i * stride (16-byte-aligned slots and

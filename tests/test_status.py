@@ -116,3 +116,107 @@ def test_ctsTcpStatusInformationConsoleOutputIterativeValuesTest():  # :178-392
         got = S.line(S.CONSOLE, current_time_ms=t, **_conn(v))
         assert got == "%10.3f            0            0%s\n" % (t / 1000, cols), (v, got)
         t += 1000
+
+
+# ---- UDP (MediaStream) status: ctsUdpStatusInformation (ctsPrintStatus.hpp:314-446) ----------------------
+UDP_HEADER = " TimeSlice       Bits/Sec    Streams   Completed   Dropped   Repeated    Errors \n"
+# (value end column, width) of ctsUdpStatusInformation's c_*Offset / c_*Length (:426-445)
+UDP_COLS = {"time": (10, 10), "bps": (25, 12), "streams": (36, 8), "completed": (48, 9), "dropped": (58, 7),
+            "repeated": (69, 7), "errors": (79, 7)}
+
+
+def test_udp_header_and_legend_are_the_reference_strings():
+    assert S.udp_header(S.CONSOLE) == UDP_HEADER
+    assert S.udp_header(S.CLEAR_TEXT) == UDP_HEADER[:-1] + "\r\n"
+    assert S.udp_header(S.CSV) == "TimeSlice,Bits/Sec,Streams,Completed,Dropped,Repeated,Errors\r\n"
+    leg = S.udp_legend(S.CONSOLE)
+    assert leg == ("Legend:\n"
+                   "* TimeSlice - (seconds) cumulative runtime\n"
+                   "* Streams - count of current number of UDP streams\n"
+                   "* Bits/Sec - bits streamed within the TimeSlice period\n"
+                   "* Completed Frames - count of frames successfully processed within the TimeSlice\n"
+                   "* Dropped Frames - count of frames that were never seen within the TimeSlice\n"
+                   "* Repeated Frames - count of frames received multiple times within the TimeSlice\n"
+                   "* Stream Errors - count of invalid frames or buffers within the TimeSlice\n"
+                   "\n")
+    assert S.udp_legend(S.CLEAR_TEXT) == leg.replace("\n", "\r\n")
+    assert S.udp_legend(S.CSV) == ""
+
+
+def test_udp_line_columns_sit_under_the_header_labels():
+    # README.md:643-716's MediaStream run: 25 Mbps, 60 fps, 1 stream; one 1 s slice
+    got = S.udp_line(S.CONSOLE, current_time_ms=1000, start_time_ms=0, end_time_ms=1000,
+                     bits_received=24999840, active_streams=1, successful_frames=60, dropped_frames=0,
+                     duplicate_frames=0, error_frames=0)
+    assert got == _expect([("1.000", 10), ("24999840", 25), ("1", 36), ("60", 48), ("0", 58), ("0", 69),
+                           ("0", 79)])
+    for label, key in (("Bits/Sec", "bps"), ("Streams", "streams"), ("Completed", "completed"),
+                       ("Dropped", "dropped"), ("Repeated", "repeated"), ("Errors", "errors")):
+        assert UDP_HEADER.index(label) + len(label) == UDP_COLS[key][0], label
+    csv = S.udp_line(S.CSV, current_time_ms=2500, start_time_ms=1000, end_time_ms=2500, bits_received=3000,
+                     active_streams=2, successful_frames=7, dropped_frames=1, duplicate_frames=2, error_frames=3)
+    assert csv == "2.500,2000,2,7,1,2,3\r\n"
+    assert S.udp_line(S.CLEAR_TEXT, current_time_ms=1000) == _expect([("1.000", 10), ("0", 25), ("0", 36),
+                                                                     ("0", 48), ("0", 58), ("0", 69),
+                                                                     ("0", 79)])[:-1] + "\r\n"
+
+
+def test_udp_wide_values_fall_back_to_exponent_notation():
+    got = S.udp_line(S.CONSOLE, current_time_ms=1000, start_time_ms=0, end_time_ms=1000,
+                     bits_received=1234567890123, active_streams=123456789, successful_frames=1234567890,
+                     dropped_frames=12345678, duplicate_frames=10 ** 15, error_frames=2 ** 63 - 1)
+    assert got[25 - 12:25] == "1234567.9x^6"  # 13 digits > 12 columns
+    assert got[36 - 8:36] == "123.5x^6"       # 9 digits > 8 columns
+    assert got[48 - 9:48] == "1234.6x^6"      # Completed is 9 wide
+    assert got[58 - 7:58] == "12.3x^6"
+    assert got[69 - 5:69] == "9+++T"          # 10^15 fits no exponent form in 7 columns
+    assert got[79 - 5:79] == "9+++T"
+    assert len(got) == 80
+
+
+def test_udp_summary():
+    s = S.udp_summary(1, 0, 0, 24999840 * 60, 3590, 6, 3, 1)
+    assert "  SuccessfulConnections [1]   NetworkErrors [0]   ProtocolErrors [0]\n" in s
+    assert s.endswith("\n"
+                      "  Total Bytes Recv : 187498800\n"
+                      "  Total Successful Frames : 3590 (99.722222)\n"
+                      "  Total Dropped Frames : 6 (0.166667)\n"
+                      "  Total Duplicate Frames : 3 (0.083333)\n"
+                      "  Total Error Frames : 1 (0.027778)\n")
+    z = S.udp_summary(0, 0, 0, 0, 0, 0, 0, 0)
+    assert "  Total Successful Frames : 0 (0.000000)\n" in z  # no frames: 0.0, not a division by zero
+
+
+def test_udp_status_details_follow_every_client():
+    """The process-wide UdpStatusDetails is fed where each client's own statistics are
+    (ctsIOPatternMediaStream.cpp:195-202, 245-246, 385-386, 405-406, 420-421, 501-502)."""
+    import numpy as np
+
+    from ctstraffic_amd import media_stream as M
+    from ctstraffic_amd.types import DGRAM_STATUS_DTYPE
+
+    def datagrams(seqs):
+        st = np.zeros(len(seqs), dtype=DGRAM_STATUS_DTYPE)
+        st["kind"], st["pass"], st["completed_bytes"], st["sequence_number"] = 0, 1, 1000, seqs
+        return st
+
+    M.udp_status_details_reset()
+    tot = dict.fromkeys(("bits_received", "successful_frames", "dropped_frames", "duplicate_frames",
+                         "error_frames"), 0)
+    for k in range(2):
+        c = M.MediaStreamClient(3000, 2, 6)  # 3 datagrams of 1000 B per frame
+        for f in range(1, 7):
+            n = 3 if k == 0 or f not in (2, 3) else {2: 2, 3: 4}[f]  # client 1: frame 2 dropped, 3 repeated
+            assert c.complete_status(datagrams([f] * n))[0] == 0
+            c.render()
+            if f == 3:  # past the final frame, then a stale one: two error frames
+                assert c.complete_status(datagrams([99, 1])) == (0, 2)
+        assert c.render() == 1
+        s = c.stats()
+        for f in tot:
+            tot[f] += s[f]
+    assert M.udp_status_details() == tot
+    assert tot["error_frames"] == 4 and tot["dropped_frames"] == 1 and tot["duplicate_frames"] == 1
+    assert tot["successful_frames"] == 10 and tot["bits_received"] == (18 + 18 + 4) * 8000
+    M.udp_status_details_reset()
+    assert all(v == 0 for v in M.udp_status_details().values())
