@@ -97,11 +97,14 @@ T* device_view(T* host)
     return static_cast<T*>(d);
 }
 
+// hipHostFree with the engine's mailbox grid stopped first (defined after Mailbox)
+void pinned_free(cts_engine* e, void* p);
+
 // Grow a pinned, device-mapped staging area to >= bytes (powers of two from `floor`).
-int ensure_pinned(void** p, size_t* cap, size_t bytes, size_t floor)
+int ensure_pinned(cts_engine* e, void** p, size_t* cap, size_t bytes, size_t floor)
 {
     if (*cap >= bytes && *p != nullptr) return CTS_OK;
-    if (*p) (void)hipHostFree(*p);
+    if (*p) pinned_free(e, *p);
     *p = nullptr;
     *cap = 0;
     size_t c = floor;
@@ -115,7 +118,7 @@ int ensure_pinned(void** p, size_t* cap, size_t bytes, size_t floor)
 int ensure_stage(cts_engine* e, size_t bytes)
 {
     void* p = e->stage;
-    const int rc = ensure_pinned(&p, &e->stage_cap, bytes, 1u << 20);
+    const int rc = ensure_pinned(e, &p, &e->stage_cap, bytes, 1u << 20);
     e->stage = static_cast<uint8_t*>(p);
     return rc;
 }
@@ -131,9 +134,16 @@ int ensure_stage(cts_engine* e, size_t bytes)
 // The grid is (re)launched by the first post after it stopped, at every group's next job number, and a
 // watchdog thread stops it with one stop job per group after `idle_ms` without posts, so an idle engine
 // neither holds workgroups nor polls PCIe. The grid's own exit bound (a group leaves after exit_ms
-// without a job, far longer) is a safety net: every group gets a job at least every exit_ms / 4 while the
-// grid runs (a caller's job goes to a group that has waited that long, even if another is less busy),
-// and a post after exit_ms / 2 of silence checks whether the grid already left (a starved watchdog).
+// without a job, far longer) is a safety net: while posts keep coming, the watchdog gives every group
+// that has had no job for exit_ms / 4 a no-op job (kMailSkip: nobody answers it, its slot is free again
+// at once), whatever the post rate and the number of groups; a caller's job also goes to such a group
+// first; and a post after exit_ms / 2 of silence checks whether the grid already left (a starved watchdog).
+// A workgroup that fell a whole ring behind (a late poller) takes the jobs whose slots hold later jobs as
+// no-ops (mailbox_kernel). A job unanswered after timeout_s marks the mailbox broken: callers then verify
+// with a launch per call (cts_verify_mapped), and the first post after the grid has drained resets the
+// rings and starts over. Freeing pinned memory (cts_host_free, a growing staging buffer) first stops the
+// grid (Pause): a free waits for every kernel on the device, and the resident grid would keep it waiting
+// for as long as other threads post.
 struct Mailbox {
     cts_engine* e = nullptr;
     // groups x cts::kMailGroup workgroups: 8 groups measured best for 8-16 concurrent callers (with 16
@@ -145,7 +155,8 @@ struct Mailbox {
     int exit_ms = 1000;                  // the grid's own per-group idle exit (CTS_MAILBOX_EXIT_MS)
     uint64_t idle_ticks = 100000000ull;  // exit_ms at 100 MHz (s_memrealtime)
     int idle_ms = 50;
-    double timeout_s = 2.0;
+    double timeout_s = 2.0;              // CTS_MAILBOX_TIMEOUT_MS
+    uint64_t delay_ticks = 0;            // CTS_MAILBOX_DELAY_MS (test hook: a late poller in the first launch)
     cts::MailSlot* slots = nullptr;      // host view (coherent, pinned)
     cts::MailSlot* dslots = nullptr;     // device view
     cts::MailPart* parts = nullptr;      // nslots x kMailGroup part records, host view (coherent, pinned)
@@ -156,6 +167,7 @@ struct Mailbox {
     std::unique_ptr<std::atomic<uint64_t>[]> free_at;
     std::mutex mu;
     bool running = false, broken = false, quit = false;
+    uint32_t paused = 0;                 // Pause() callers: no (re)launch, posts fall back to a launch
     uint64_t next[cts::kMailMaxGroups] = {};       // each group's next job number
     uint32_t busy[cts::kMailMaxGroups] = {};       // each group's jobs outstanding
     uint32_t outstanding = 0;
@@ -193,6 +205,8 @@ struct Mailbox {
         idle_ms = std::max(1, env_int("CTS_MAILBOX_IDLE_MS", idle_ms));
         exit_ms = std::max(40, env_int("CTS_MAILBOX_EXIT_MS", exit_ms));
         idle_ticks = (uint64_t)exit_ms * 100000ull;
+        timeout_s = std::max(1, env_int("CTS_MAILBOX_TIMEOUT_MS", (int)(timeout_s * 1000))) / 1000.0;
+        delay_ticks = (uint64_t)std::max(0, env_int("CTS_MAILBOX_DELAY_MS", 0)) * 100000ull;
         DeviceGuard g(e->device);
         if (!g.ok) return CTS_E_HIP;
         void* p = nullptr;
@@ -221,10 +235,27 @@ struct Mailbox {
         }
         free_at.reset(new (std::nothrow) std::atomic<uint64_t>[nslots]);
         if (!free_at) return CTS_E_NOMEM;
-        for (uint32_t i = 0; i < nslots; ++i) free_at[i].store(i % per_group, std::memory_order_relaxed);  // job j of its group
+        ResetRings();
         last_post = std::chrono::steady_clock::now();
         watchdog = std::thread([this] { Watch(); });
         return CTS_OK;
+    }
+
+    // no grid runs (or Init): every slot and part record empty, group g's job numbers from 0 again
+    void ResetRings()
+    {
+        std::memset(slots, 0, sizeof(cts::MailSlot) * nslots);
+        std::memset(parts, 0, sizeof(cts::MailPart) * nslots * cts::kMailGroup);
+        for (uint32_t i = 0; i < nslots; ++i) free_at[i].store(i % per_group, std::memory_order_relaxed);  // job j of its group
+        for (uint32_t i = 0; i < cts::kMailMaxGroups; ++i) next[i] = busy[i] = 0;
+    }
+
+    // under mu: the grid's last launch has ended (or there was none)
+    bool DrainedLocked()
+    {
+        if (launches.load(std::memory_order_relaxed) == 0) return true;
+        DeviceGuard g(e->device);
+        return hipEventQuery(grid_done) == hipSuccess;
     }
 
     // under mu: start the grid at every group's next job (after any grid still draining, same stream)
@@ -234,7 +265,8 @@ struct Mailbox {
         if (!g.ok) return CTS_E_HIP;
         cts::MailStarts starts{};
         for (uint32_t i = 0; i < groups; ++i) starts.j[i] = next[i];
-        if (cts::launch_mailbox(dslots, dparts, per_group, starts, groups, idle_ticks, stream) != hipSuccess ||
+        const uint64_t delay = launches.load(std::memory_order_relaxed) == 0 ? delay_ticks : 0;
+        if (cts::launch_mailbox(dslots, dparts, per_group, starts, groups, idle_ticks, stream, delay) != hipSuccess ||
             hipEventRecord(grid_done, stream) != hipSuccess)
             return CTS_E_HIP;
         running = true;
@@ -253,7 +285,14 @@ struct Mailbox {
         uint32_t g0 = 0, n = 1;
         {
             std::lock_guard<std::mutex> lk(mu);
-            if (broken) return CTS_E_HIP;
+            if (broken) {
+                // a job timed out: start over once nothing is outstanding and the grid has ended
+                if (len == 0 || outstanding != 0 || !DrainedLocked()) return CTS_E_HIP;
+                ResetRings();
+                broken = false;
+                broken_flag.store(false, std::memory_order_release);
+            }
+            if (len != 0 && paused != 0) return CTS_E_HIP;  // a free is waiting for the grid to end
             if (len == 0) {
                 if (!running || (only_if_idle && outstanding != 0)) return CTS_OK;
                 running = false;
@@ -353,13 +392,58 @@ struct Mailbox {
 
     int Stop(bool only_if_idle) { return Post(0, 0, 0, nullptr, only_if_idle); }
 
+    // Stop the grid and wait (bounded) until it has ended; posts fall back to a launch until Resume.
+    void Pause()
+    {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            ++paused;
+        }
+        (void)Stop(false);
+        const auto t0 = std::chrono::steady_clock::now();
+        for (;;) {
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                if (DrainedLocked()) return;
+            }
+            if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s) return;
+            std::this_thread::yield();
+        }
+    }
+    void Resume()
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        --paused;
+    }
+
+    // under mu: a no-op job for every group that has had none for exit_ms / 4, so no group reaches its idle exit
+    // while the grid is meant to run. The slot of a no-op is free again at once (no workgroup answers it).
+    void KeepaliveLocked(std::chrono::steady_clock::time_point now)
+    {
+        for (uint32_t g = 0; g < groups; ++g) {
+            if (busy[g] != 0 || now - last_used[g] <= std::chrono::milliseconds(exit_ms / 4)) continue;
+            const uint64_t t = next[g];
+            const uint32_t k = g * per_group + (uint32_t)(t % per_group);
+            if (free_at[k].load(std::memory_order_acquire) != t) continue;  // (busy == 0: always free)
+            ++next[g];
+            cts::mail_write(slots + k, 0, (uint64_t)cts::kMailSkip | ((uint64_t)(uint32_t)(t + 1) << 32));
+            free_at[k].store(t + per_group, std::memory_order_release);
+            last_used[g] = now;
+        }
+    }
+
     void Watch()
     {
         std::unique_lock<std::mutex> lk(mu);
         while (!quit) {
-            cv.wait_for(lk, std::chrono::milliseconds(std::max(1, idle_ms / 2)));
-            if (quit || !running || outstanding != 0) continue;
-            if (std::chrono::steady_clock::now() - last_post < std::chrono::milliseconds(idle_ms)) continue;
+            cv.wait_for(lk, std::chrono::milliseconds(std::max(1, std::min(idle_ms / 2, exit_ms / 8))));
+            if (quit || !running || broken) continue;
+            const auto now = std::chrono::steady_clock::now();
+            // keep the groups alive while posts keep coming; after exit_ms / 2 of silence the grid may leave on
+            // its own (the next post sees it ended and relaunches)
+            if (now - last_post < std::chrono::milliseconds(exit_ms / 2)) KeepaliveLocked(now);
+            if (outstanding != 0) continue;
+            if (now - last_post < std::chrono::milliseconds(idle_ms)) continue;
             lk.unlock();
             (void)Stop(true);
             lk.lock();
@@ -368,6 +452,18 @@ struct Mailbox {
 };
 
 namespace {
+
+void pinned_free(cts_engine* e, void* p)
+{
+    Mailbox* m = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(e->mail_init_mu);
+        m = e->mail.get();
+    }
+    if (m != nullptr) m->Pause();
+    (void)hipHostFree(p);
+    if (m != nullptr) m->Resume();
+}
 
 int mailbox_of(cts_engine* e, Mailbox** out)
 {
@@ -786,7 +882,17 @@ int cts_host_free(cts_engine* e, void* host_ptr)
 {
     if (e == nullptr || host_ptr == nullptr) return CTS_E_INVALID;
     DeviceGuard g(e->device);
-    return hip_status(hipHostFree(host_ptr));
+    // hipHostFree waits for the device's kernels: the resident mailbox grid is stopped first, so a free
+    // returns while other threads keep posting (their verifies take the launch path meanwhile)
+    Mailbox* m = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(e->mail_init_mu);
+        m = e->mail.get();
+    }
+    if (m != nullptr) m->Pause();
+    const int rc = hip_status(hipHostFree(host_ptr));
+    if (m != nullptr) m->Resume();
+    return rc;
 }
 
 int cts_host_device_pointer(void* host_ptr, void** dev_view)
@@ -813,7 +919,7 @@ int cts_verify_host(cts_engine* e, const void* host_buf, uint32_t len, uint32_t 
                 e->stage_pool.pop_back();
             }
         }
-        int rc = ensure_pinned(&st.p, &st.cap, (size_t)len + 16, 64u << 10);
+        int rc = ensure_pinned(e, &st.p, &st.cap, (size_t)len + 16, 64u << 10);
         const uint8_t* dev = rc == CTS_OK ? device_view(static_cast<uint8_t*>(st.p)) : nullptr;
         if (rc == CTS_OK && dev == nullptr) rc = CTS_E_HIP;
         if (rc == CTS_OK) {
@@ -865,8 +971,8 @@ int cts_verify_host_batch(cts_engine* e, const void* const* bufs, const uint32_t
     }
     int rc = ensure_stage(e, (size_t)total + 16);
     if (rc != CTS_OK) return rc;
-    if ((rc = ensure_pinned(&e->batch_desc, &e->batch_desc_cap, sizeof(cts_buf_desc) * n, 4096)) != CTS_OK) return rc;
-    if ((rc = ensure_pinned(&e->batch_res, &e->batch_res_cap, sizeof(cts_verify_result) * n, 4096)) != CTS_OK) return rc;
+    if ((rc = ensure_pinned(e, &e->batch_desc, &e->batch_desc_cap, sizeof(cts_buf_desc) * n, 4096)) != CTS_OK) return rc;
+    if ((rc = ensure_pinned(e, &e->batch_res, &e->batch_res_cap, sizeof(cts_verify_result) * n, 4096)) != CTS_OK) return rc;
     if (counters && e->batch_ctr == nullptr &&
         (rc = host_alloc_mapped(cts_counters_device_bytes(), &e->batch_ctr)) != CTS_OK)
         return rc;
@@ -919,7 +1025,24 @@ int cts_verify_mapped(cts_engine* e, const void* dev_buf, uint32_t len, uint32_t
     Mailbox* m = nullptr;
     const int rc = mailbox_of(e, &m);
     if (rc != CTS_OK) return rc;
-    return m->Post(reinterpret_cast<uint64_t>(dev_buf), len, expected_offset, out, false);
+    if (m->Post(reinterpret_cast<uint64_t>(dev_buf), len, expected_offset, out, false) == CTS_OK) return CTS_OK;
+    // the mailbox is broken (a job timed out; it starts over once its grid has drained) or paused (a free is
+    // waiting for the grid to end): this verify takes one sliced launch + synchronize instead
+    std::lock_guard<std::mutex> lk(e->host_mu);
+    DeviceGuard g(e->device);
+    if (!g.ok) return CTS_E_HIP;
+    const uint64_t d = reinterpret_cast<uintptr_t>(dev_buf) & 15u;  // (the arena base must be 16-byte aligned)
+    uint32_t slice_len = 0;
+    const uint32_t ns = cts::slice_plan(d, len, expected_offset, 0, e->stage_desc, &slice_len);
+    const cts_buf_desc* dd = device_view(e->stage_desc);
+    cts_verify_result* dr = device_view(e->stage_res);
+    if (!dd || !dr) return CTS_E_HIP;
+    hipError_t err = cts::launch_verify(static_cast<const uint8_t*>(dev_buf) - d, d + len, dd, ns, slice_len, dr,
+                                        nullptr, nullptr, 0, e->stream, e->geo);
+    if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
+    if (err != hipSuccess) return CTS_E_HIP;
+    *out = cts::slice_merge(e->stage_res, ns, slice_len, len);
+    return CTS_OK;
 }
 
 uint64_t cts_mailbox_launches(const cts_engine* e)

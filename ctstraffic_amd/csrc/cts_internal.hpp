@@ -26,7 +26,7 @@ constexpr int kDefaultSmallVariant = 9;
 constexpr int kDefaultMediaStreamVariant = 3;
 #if CTS_TUNING
 constexpr int kVerifyVariants = 19;  // workgroup-per-buffer verify variants (launch_verify)
-constexpr int kSmallVariants = 10;   // small-buffer (datagram) verify variants
+constexpr int kSmallVariants = 15;   // small-buffer (datagram) verify variants (10-14: line policies)
 constexpr int kMediaStreamVariants = 12;  // MediaStream receive kernels (launch_media_stream_verify)
 #endif
 // A launch-variant attribute value this build can launch.
@@ -114,14 +114,18 @@ inline uint32_t mail_parts(uint64_t ptr, uint32_t len)
     return pieces < kMailGroup ? (uint32_t)pieces : kMailGroup;
 }
 constexpr uint32_t kMailMaxGroups = 64;
+// Job length of a no-op: the host's keepalive for an idle group (its pollers' idle exit restarts), and what a
+// poller publishes for a job whose slot a later job already holds. No workgroup answers it.
+constexpr uint32_t kMailSkip = 0xFFFFFFFFu;
 struct MailStarts {
     uint64_t j[kMailMaxGroups];  // each group's first job number (passed by value)
 };
 // Each group polls its jobs from starts.j[g] on until a stop job, or until it has waited idle_ticks
 // (s_memrealtime, 100 MHz) for one job: every wave reaches one of the two exits. per_group = S.
 // groups * kMailGroup workgroups of kMailThreads threads.
+// delay_ticks (test hook, 0 in production): group 0's last workgroup starts polling that much later.
 hipError_t launch_mailbox(const MailSlot* slots, MailPart* parts, uint32_t per_group, const MailStarts& starts,
-                          uint32_t groups, uint64_t idle_ticks, hipStream_t stream);
+                          uint32_t groups, uint64_t idle_ticks, hipStream_t stream, uint64_t delay_ticks = 0);
 
 hipError_t launch_verify(const uint8_t* arena, uint64_t arena_bytes, const cts_buf_desc* descs, uint32_t n,
                          uint32_t max_length_hint, cts_verify_result* results, uint64_t* counters,

@@ -977,19 +977,41 @@ __device__ __forceinline__ u32x4 quad_edge_xor(const QSpan& q, uint32_t ce, u32x
 
 // Interior [1, nch-1) in rounds of U loads per lane starting at chunk cs (the wave loops
 // while any of its teams has chunks left); returns the OR of this lane's differences.
-template <int U, bool NT>
+// LP (line policy, tuning): bit 0 clamps out-of-span chunks to the span's first / last 128-B LINE instead of its
+// first / last chunk, so every load instruction requests whole lines; bit 1 loads the span's first and last line
+// with the default (L2-allocating) policy and only the lines in between nontemporal; bit 2 (kQuadEdgesInRound)
+// compares the two partial edge chunks from the round loads (masked) instead of a separate edge load, so no
+// line of the span is requested twice: with nontemporal loads the edge load's line sat at L2's LRU position
+// and was often gone when the round asked for it again (config 3, 4 M datagrams: 8 M extra L2 requests, 0.9 M
+// extra misses, FETCH_SIZE 1.7 % over the arena; profiles/r03/dg_probe/).
+constexpr int kQuadEdgesInRound = 4;
+template <int U, bool NT, int LP = 0>
 __device__ __forceinline__ uint32_t quad_scan_interior(const QSpan& q, uint32_t lane)
 {
     constexpr int ROUND = kQuadTeam * U;
+    constexpr bool EIR = (LP & kQuadEdgesInRound) != 0;
     uint32_t acc = 0;
-    for (int r = 0; __any(q.cs + r * ROUND <= q.c_hi); ++r) {
+    const int lfirst = -(int)(((uintptr_t)q.p >> 4) & 7u);                       // first chunk of chunk 0's line
+    const int llast = q.last + 7 - (int)((((uintptr_t)q.p >> 4) + (uint32_t)q.last) & 7u);  // last of last's line
+    const int lastv = (int)q.nch - 1;  // the last chunk of the span (-1: empty)
+    u32x4 e0 = u32x4{0u, 0u, 0u, 0u}, e1 = e0;  // EIR: this lane's differences in chunk 0 / the last chunk
+    for (int r = 0; __any(q.cs + r * ROUND <= (EIR ? lastv : q.c_hi)); ++r) {
         const int cb = q.cs + r * ROUND + (int)lane;
         u32x4 dd[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             int c = cb + u * kQuadTeam;
-            c = c < 0 ? 0 : (c > q.last ? q.last : c);
-            dd[u] = load_chunk_g<NT>(q.p + c);
+            if constexpr ((LP & 1) != 0) {
+                c = c < lfirst ? lfirst : (c > llast ? llast : c);
+            } else {
+                c = c < 0 ? 0 : (c > q.last ? q.last : c);
+            }
+            if constexpr ((LP & 2) != 0) {
+                if (c < lfirst + 8 || c > llast - 8) dd[u] = load_chunk_g<false>(q.p + c);
+                else dd[u] = load_chunk_g<NT>(q.p + c);
+            } else {
+                dd[u] = load_chunk_g<NT>(q.p + c);
+            }
         }
         __builtin_amdgcn_sched_barrier(0);
         const uint32_t k = ((q.q0 + 16u * (uint32_t)cb) & 0xFFFFu) >> 1;
@@ -997,12 +1019,42 @@ __device__ __forceinline__ uint32_t quad_scan_interior(const QSpan& q, uint32_t 
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int c = cb + u * kQuadTeam;
-            const uint32_t any = or4(dd[u] ^ expected_step<kQuadTeam, U>(B, u, q.sh));
-            acc |= (c >= 1 && c <= q.c_hi) ? any : 0u;
+            if constexpr (EIR) {
+                // interior chunks as always; the two partial edge chunks are kept and masked after the rounds
+                // (chunk 0 is always in round 0's first load: rounds start on its line, cs > -8)
+                const u32x4 x = dd[u] ^ expected_step<kQuadTeam, U>(B, u, q.sh);
+                acc |= (c >= 1 && c < lastv) ? or4(x) : 0u;
+                if (u == 0 && c == 0) e0 = x;
+                if (c == lastv && lastv >= 1) e1 = x;
+            } else {
+                const uint32_t any = or4(dd[u] ^ expected_step<kQuadTeam, U>(B, u, q.sh));
+                acc |= (c >= 1 && c <= q.c_hi) ? any : 0u;
+            }
             __builtin_amdgcn_sched_barrier(0);
         }
     }
+    if constexpr (EIR) {
+        if (lastv >= 0) {
+            acc |= or4(e0 & range_mask(q.lo, lastv == 0 ? q.hi_last : 16u));
+            acc |= or4(e1 & range_mask(0u, q.hi_last));
+        }
+    }
     return acc;
+}
+
+// The exact re-read for kQuadEdgesInRound: the chunks this lane loaded in the rounds (cs + lane mod 16), the
+// edge chunks masked as there.
+template <bool NT>
+__device__ __forceinline__ void quad_scan_exact_eir(const QSpan& q, uint32_t lane, uint32_t& first, uint32_t& count)
+{
+    const int lastv = (int)q.nch - 1;
+    for (int c = q.cs + (int)lane; c <= lastv; c += kQuadTeam) {
+        if (c >= 0) {
+            u32x4 x = load_chunk_g<NT>(q.p + c) ^ expected_chunk((q.q0 + 16u * (uint32_t)c) & 0xFFFFu, q.sh);
+            if (c == 0 || c == lastv) x &= range_mask(c == 0 ? q.lo : 0u, c == lastv ? q.hi_last : 16u);
+            take_diff_at((uint32_t)c, q.lo, x, first, count);
+        }
+    }
 }
 
 // Exact re-read of exactly the chunks this lane owns (interior chunks = cs + lane mod 16,
@@ -1237,12 +1289,13 @@ __device__ __forceinline__ cts_buf_desc vs_desc(const VSource& src, uint32_t i)
     }
 }
 
-template <int U, bool NT, bool ALIGN, bool CONTIG = false, bool STRIDED = false>
+template <int U, bool NT, bool ALIGN, bool CONTIG = false, bool STRIDED = false, int LP = 0>
 __global__ void __launch_bounds__(kBlock)
     verify_quad_kernel(const uint8_t* __restrict__ arena, uint64_t arena_bytes, VSource src, uint32_t n,
                        cts_verify_result* __restrict__ results, uint64_t* __restrict__ counters,
                        uint32_t* __restrict__ conn_first_fail, uint32_t n_conns, uint32_t per = 0)
 {
+    static_assert((LP & kQuadEdgesInRound) == 0 || ALIGN, "edges in round need rounds starting on chunk 0's line");
     constexpr int TEAMS = kBlock / kQuadTeam;
     __shared__ uint64_t ctr[TEAMS][5];
     __shared__ QuadOut qout[kBlock / 64];
@@ -1265,13 +1318,21 @@ __global__ void __launch_bounds__(kBlock)
         const QSpan q = quad_span<ALIGN>(arena + d.byte_offset + d.skip_head, ok ? d.length - d.skip_head : 0u,
                                          d.expected_pattern_offset, dummy);
         // edge chunks first (their latency hides under the interior rounds)
-        const uint32_t ce = quad_edge_chunk(q, lane);
-        const u32x4 edge = load_chunk_g<NT>(q.p + ce);
-        uint32_t acc = quad_scan_interior<U, NT>(q, lane);
-        acc |= quad_edge_used(q, lane) ? or4(quad_edge_xor(q, ce, edge)) : 0u;
+        uint32_t acc;
+        if constexpr ((LP & kQuadEdgesInRound) != 0) {
+            acc = quad_scan_interior<U, NT, LP>(q, lane);
+        } else {
+            const uint32_t ce = quad_edge_chunk(q, lane);
+            const u32x4 edge = load_chunk_g<(LP & 2) ? false : NT>(q.p + ce);
+            acc = quad_scan_interior<U, NT, LP>(q, lane);
+            acc |= quad_edge_used(q, lane) ? or4(quad_edge_xor(q, ce, edge)) : 0u;
+        }
         uint32_t first = kNone, count = 0;
         if (__any(acc != 0u)) {  // rare: exact re-read of the dirty lanes' own chunks
-            if (acc != 0u) quad_scan_exact<NT>(q, lane, first, count);
+            if (acc != 0u) {
+                if constexpr ((LP & kQuadEdgesInRound) != 0) quad_scan_exact_eir<NT>(q, lane, first, count);
+                else quad_scan_exact<NT>(q, lane, first, count);
+            }
             quad_team_reduce(first, count);
         }
         if (lane == 0u && live) {
@@ -2049,6 +2110,23 @@ static void launch_verify_nt(const uint8_t* arena, uint64_t arena_bytes, const c
             verify_quad_kernel<6, NT, true, true><<<cg.grid, kBlock, 0, stream>>>(CTS_QUAD_ARGS, cg.per);
             break;
         }
+        case 10:
+        case 11:
+        case 12:
+        case 13:
+        case 14: {  // variant 9 with line policy LP = 1, 2, 3, 4, 5 (quad_scan_interior)
+            const ContigGrid cg = contig_grid(n, geo);
+#define CTS_QUAD_LP(LP) verify_quad_kernel<6, NT, true, true, false, LP><<<cg.grid, kBlock, 0, stream>>>(CTS_QUAD_ARGS, cg.per)
+            switch (geo.small_variant) {
+            case 10: CTS_QUAD_LP(1); break;
+            case 11: CTS_QUAD_LP(2); break;
+            case 12: CTS_QUAD_LP(3); break;
+            case 13: CTS_QUAD_LP(4); break;
+            default: CTS_QUAD_LP(5); break;
+            }
+#undef CTS_QUAD_LP
+            break;
+        }
         case 1: verify_wave_kernel<1, NT><<<grid, kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 2: verify_wave_kernel<4, NT><<<grid, kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 3: verify_wave_pipe_kernel<2, NT><<<grid, kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
@@ -2135,7 +2213,8 @@ __device__ uint64_t* cts_mail_trace;
 #endif
 
 __global__ __launch_bounds__(kMailThreads) void mailbox_kernel(const MailSlot* slots, MailPart* parts, uint32_t per_group,
-                                                               MailStarts starts, uint64_t idle_ticks)
+                                                               MailStarts starts, uint64_t idle_ticks,
+                                                               uint64_t delay_ticks)
 {
     __shared__ uint64_t s_job[2][2];              // published job by parity: ptr_exp, len_seq
     __shared__ uint32_t s_tag[2];                 // its tag, written after the job
@@ -2161,6 +2240,10 @@ __global__ __launch_bounds__(kMailThreads) void mailbox_kernel(const MailSlot* s
 
     if (wave == kBlock / 64) {  // ---- the poller ----
         if (lane != 0) return;
+        if (delay_ticks != 0 && g == 0 && gi == kMailGroup - 1) {  // test hook (CTS_MAILBOX_DELAY_MS): a late poller
+            const uint64_t t0 = wall_clock64();
+            while (wall_clock64() - t0 < delay_ticks) __builtin_amdgcn_s_sleep(127);
+        }
         for (uint32_t i = 0;; ++i) {
             const uint64_t j = j0 + i;
             const uint32_t tag = (uint32_t)(j + 1), par = i & 1u;
@@ -2173,6 +2256,14 @@ __global__ __launch_bounds__(kMailThreads) void mailbox_kernel(const MailSlot* s
             for (;;) {
                 v = __builtin_amdgcn_raw_buffer_load_b128(r, 0u, 0u, kMailAux);
                 if (v[3] == tag) break;
+                if ((int32_t)(v[3] - tag) > 0) {
+                    // a later job already holds this slot: the host reuses a slot only once every part record of
+                    // its job was folded (or at once for a no-op), so job j needed nothing from this workgroup;
+                    // take it as a no-op and catch up (a workgroup that fell per_group jobs behind would otherwise
+                    // wait for a tag that never comes back)
+                    v = u32x4{0u, 0u, kMailSkip, tag};
+                    break;
+                }
                 const uint64_t waited = wall_clock64() - start;
                 if (waited > idle_ticks) {  // no job within idle_ticks: publish one whose tag word is not the tag
                     v = u32x4{0u, 0u, 0u, ~tag};
@@ -2200,7 +2291,7 @@ __global__ __launch_bounds__(kMailThreads) void mailbox_kernel(const MailSlot* s
         if ((uint32_t)(len_seq >> 32) != tag) return;  // idle leave
         const uint64_t ptr = ptr_exp & 0xFFFFFFFFFFFFull;
         const uint32_t expected = (uint32_t)(ptr_exp >> 48), len = (uint32_t)len_seq;
-        const bool mine = gi < mail_parts(ptr, len);
+        const bool mine = len != kMailSkip && gi < mail_parts(ptr, len);
         const uint32_t d = (uint32_t)ptr & 15u;
         const uint8_t* const base = reinterpret_cast<const uint8_t*>(ptr - d);
         uint32_t first = kNone, count = 0;
@@ -2284,11 +2375,12 @@ __global__ __launch_bounds__(kMailThreads) void mailbox_kernel(const MailSlot* s
 }
 
 hipError_t launch_mailbox(const MailSlot* slots, MailPart* parts, uint32_t per_group, const MailStarts& starts,
-                          uint32_t groups, uint64_t idle_ticks, hipStream_t stream)
+                          uint32_t groups, uint64_t idle_ticks, hipStream_t stream, uint64_t delay_ticks)
 {
     if (slots == nullptr || parts == nullptr || per_group == 0 || groups == 0 || groups > kMailMaxGroups)
         return hipErrorInvalidValue;
-    mailbox_kernel<<<groups * kMailGroup, kMailThreads, 0, stream>>>(slots, parts, per_group, starts, idle_ticks);
+    mailbox_kernel<<<groups * kMailGroup, kMailThreads, 0, stream>>>(slots, parts, per_group, starts, idle_ticks,
+                                                                     delay_ticks);
     return hipGetLastError();
 }
 

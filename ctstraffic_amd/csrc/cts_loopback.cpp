@@ -13,6 +13,7 @@
 #include <arpa/inet.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
+#include <sys/resource.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
@@ -83,10 +84,22 @@ struct SideResult {
     int status = CTS_IO_FAILED;
     uint32_t last_error = 0;
     cts_pattern_stats stats{};
+    double recv_cpu_s = 0;  // CPU time (user + sys) of the thread that ran this side's recvs
+    double send_cpu_s = 0;  // ... and of its send thread (the same thread in the sync functor)
 };
+
+// this thread's CPU seconds so far (user + system)
+double thread_cpu_s()
+{
+    rusage u{};
+    if (::getrusage(RUSAGE_THREAD, &u) != 0) return 0;
+    return (double)u.ru_utime.tv_sec + (double)u.ru_utime.tv_usec * 1e-6 + (double)u.ru_stime.tv_sec +
+           (double)u.ru_stime.tv_usec * 1e-6;
+}
 
 void run_side(int* fdslot, cts_io_pattern* p, bool inject, uint32_t inject_index, bool recv_whole, SideResult* out)
 {
+    const double cpu0 = thread_cpu_s();
     const int fd = *fdslot;
     std::vector<char> scratch;
     uint32_t data_sends = 0;
@@ -152,6 +165,7 @@ void run_side(int* fdslot, cts_io_pattern* p, bool inject, uint32_t inject_index
     out->status = st;
     out->last_error = cts_io_pattern_last_error(p);
     (void)cts_io_pattern_get_stats(p, &out->stats);
+    out->recv_cpu_s = out->send_cpu_s = thread_cpu_s() - cpu0;  // one thread runs both directions
 }
 
 // ---- async functor (Duplex): one send and one recv thread per connection side -----------------
@@ -221,8 +235,16 @@ struct AsyncSide {
         }
         release();
     }
+    double cpu_s[2] = {0, 0};  // CPU seconds of the recv (0) and send (1) worker
     void worker(bool sending)
     {
+        const double cpu0 = thread_cpu_s();
+        struct Done {
+            AsyncSide* a;
+            bool sending;
+            double cpu0;
+            ~Done() { a->cpu_s[sending ? 1 : 0] = thread_cpu_s() - cpu0; }
+        } done{this, sending, cpu0};
         std::deque<cts_task>& q = sending ? sends : recvs;
         std::vector<char> scratch;
         std::unique_lock<std::mutex> lk(mu);
@@ -290,6 +312,8 @@ void run_side_async(int* fdslot, cts_io_pattern* p, bool inject, uint32_t inject
     out->status = st;
     out->last_error = cts_io_pattern_last_error(p);
     (void)cts_io_pattern_get_stats(p, &out->stats);
+    out->recv_cpu_s = a.cpu_s[0];
+    out->send_cpu_s = a.cpu_s[1];
 }
 
 }  // namespace
@@ -357,7 +381,7 @@ extern "C" int cts_loopback_run_detailed(const cts_loopback_config* cfg, cts_eng
         c.tcp_shutdown = CTS_SHUTDOWN_GRACEFUL;
         c.transfer_size = cfg->transfer_size;
         c.verify_mode = cfg->verify_mode;
-        c.batch_buffers = cfg->batch_buffers ? cfg->batch_buffers : 256u;
+        c.batch_buffers = cfg->batch_buffers ? cfg->batch_buffers : 512u;  // (DEFERRED launches halves of 256)
         c.tcp_bytes_per_second = cfg->tcp_bytes_per_second;  // both sides pace their own sends
         c.burst_count = cfg->burst_count;
         c.burst_delay = cfg->burst_delay;
@@ -436,6 +460,17 @@ extern "C" int cts_loopback_run_detailed(const cts_loopback_config* cfg, cts_eng
             s.last_error == CTS_STATUS_ERROR_DATA_DID_NOT_MATCH_BIT_PATTERN)
             ++out->data_errors;
         out->buffers_verified += c.stats.buffers_verified + s.stats.buffers_verified;
+    }
+    for (uint32_t i = 0; i < 2 * n; ++i) {  // the threads that received the data / sent it
+        const cts_pattern_stats& st = res[i].stats;
+        if (async) {  // a recv worker and a send worker per side
+            if (st.bytes_recv != 0) out->recv_cpu_seconds += res[i].recv_cpu_s;
+            if (st.bytes_sent != 0) out->send_cpu_seconds += res[i].send_cpu_s;
+        } else if (st.bytes_recv > st.bytes_sent) {  // one thread per side: by the direction it mostly ran
+            out->recv_cpu_seconds += res[i].recv_cpu_s;
+        } else {
+            out->send_cpu_seconds += res[i].send_cpu_s;
+        }
     }
     if (sides != nullptr)
         for (uint32_t i = 0; i < 2 * n; ++i) {

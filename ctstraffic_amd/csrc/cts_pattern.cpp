@@ -342,6 +342,7 @@ struct cts_io_pattern {
             if (!inflight.empty()) (void)hipStreamSynchronize(stream);  // the kernel still reads the ring
             (void)cts_engine_stream_destroy(engine, stream);
         }
+        if (inflight_done) (void)hipEventDestroy(inflight_done);
         // ~RioBufferId (ctsIOPattern.h:230-238) for every id this pattern registered
         if (!rio_owned.empty()) {
             std::lock_guard<std::mutex> lk(g_rio.mu);
@@ -398,6 +399,7 @@ struct cts_io_pattern {
     // the next one fills in the other half of stage_desc/stage_res; its verdicts are applied before
     // the next launch, at any non-benign completion and at Flush (Retire)
     std::vector<Queued> inflight;
+    hipEvent_t inflight_done = nullptr;  // recorded after the in-flight batch's launch, queried by CompleteIo
     uint32_t desc_set = 0;  // the half the filling batch uses
     // DEFERRED zero-copy ring: the recv container holds (1 or 2) x BatchCapacity() + recvCount + 1
     // buffer slots and a completed buffer's slot is not handed out again before its batch was
@@ -761,6 +763,18 @@ struct cts_io_pattern {
     uint64_t StageCapacity() const { return cfg.batch_bytes ? cfg.batch_bytes : (64ull << 20); }
     uint32_t BatchCapacity() const { return cfg.batch_buffers ? cfg.batch_buffers : 1024u; }
     bool DoubleBuffered() const { return engine != nullptr && hook == nullptr; }
+    // Completions queued before a batch goes to the device. Double-buffered, each half holds half a batch: an
+    // in-flight half is retired at the latest when the next half is full, so every verdict is known within
+    // BatchCapacity() completions of its own (fewer when the in-flight kernel is seen done earlier).
+    uint32_t LaunchAt() const
+    {
+        const uint32_t b = BatchCapacity();
+        return DoubleBuffered() && queue_in_ring ? std::max(1u, b / 2u) : b;
+    }
+
+    // The in-flight batch's kernel has finished (a non-blocking event query; CompleteIo asks every 16th
+    // completion: a query costs about a microsecond, a completion of 64 KiB arrives every ~1.3 us at 50 GB/s).
+    bool InflightDone() const { return !inflight.empty() && inflight_done && hipEventQuery(inflight_done) == hipSuccess; }
     cts_buf_desc* StageDescs() const
     {
         return reinterpret_cast<cts_buf_desc*>(stage_desc.host) + (size_t)desc_set * BatchCapacity();
@@ -882,6 +896,11 @@ struct cts_io_pattern {
         if (queue.empty()) return GetCurrentStatus();  // the in-flight batch failed
         const int lr = LaunchBatch();
         if (lr != CTS_OK) return lr;
+        if (inflight_done == nullptr && hipEventCreateWithFlags(&inflight_done, hipEventDisableTiming) != hipSuccess) {
+            inflight_done = nullptr;
+            return CTS_E_HIP;
+        }
+        if (hipEventRecord(inflight_done, stream) != hipSuccess) return CTS_E_HIP;
         inflight.swap(queue);
         queue.clear();
         desc_set ^= 1u;
@@ -968,6 +987,15 @@ struct cts_io_pattern {
         // queued verdicts first, so a pending data error latches before it.
         bool benign = status == kNoError && (t.io_action == CTS_TASK_SEND || t.io_action == CTS_TASK_RECV) &&
                       state.WouldStayMoreIo(t, transfer) && m_lastError == kStatusIoRunning;
+        if (Deferred() && benign && (queue.size() & 15u) == 0 && InflightDone()) {
+            // the in-flight batch's verdicts are in: apply them now, so a data error fails the connection at
+            // this completion rather than at the next launch (ctsIOPattern.cpp:486-489 fails it at the
+            // failing one; the completions in between are taken back by RollbackAfter)
+            const bool had_failure = has_failure;
+            const int rc = Retire();
+            if (rc < 0) return rc;
+            if (has_failure && !had_failure) return GetCurrentStatus();
+        }
         if (Deferred() && (!queue.empty() || !inflight.empty()) && !benign) {
             const bool had_failure = has_failure;
             const int rc = Flush();
@@ -1043,7 +1071,7 @@ struct cts_io_pattern {
         if (defer_this) {
             const int rc = Enqueue(t, transfer, bytes_recv);
             if (rc < 0) return rc;
-            if (!benign || queue.size() >= BatchCapacity()) {
+            if (!benign || queue.size() >= LaunchAt()) {
                 const int fr = benign ? Rotate() : Flush();
                 if (fr < 0) return fr;
             }

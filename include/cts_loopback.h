@@ -61,6 +61,11 @@ typedef struct cts_loopback_result {
     uint32_t connections_failed;    /* any side FailedIo or a socket error */
     uint32_t data_errors;           /* patterns that latched DATA_DID_NOT_MATCH_BIT_PATTERN (README "DataError") */
     uint32_t reserved;
+    double recv_cpu_seconds;        /* CPU time (user + sys, RUSAGE_THREAD) of the threads that ran the data recvs:
+                                       the sync functor's side threads of the receiving sides (also their sends,
+                                       PushPull), the async functor's recv workers -- recv() copies, CompleteIo
+                                       and VerifyBuffer (ctsSendRecvIocp.cpp:60,97 run it on the IOCP thread) */
+    double send_cpu_seconds;        /* the same for the threads that ran the data sends */
 } cts_loopback_result;
 
 /* Runs cfg->connections loopback connections to completion. engine may be NULL

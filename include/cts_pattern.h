@@ -32,8 +32,10 @@
  * on internal inconsistency. Here every call returns normally; an internal
  * inconsistency latches CTS_PATTERN_E_FAIL_FAST on the pattern (readable with
  * cts_io_pattern_fail_fast_reason) and CompleteIo returns CTS_IO_FAILED.
- * Rate limiting (TcpBytesPerSecond) and burst delays are not part of the
- * data-integrity path and are not restated: time offsets are always 0.
+ * Send pacing is restated: with cts_pattern_config.tcp_bytes_per_second (and
+ * its period) or burst_count / burst_delay set, CreateNewTask gives send tasks
+ * the reference's time_offset_ms (ctsIOPattern.cpp:593-674); with neither set
+ * every time offset is 0.
  */
 #ifndef CTS_PATTERN_H
 #define CTS_PATTERN_H

@@ -46,6 +46,10 @@ int cts_engine_stream_create(cts_engine*, void**) { return CTS_E_NO_DEVICE; }
 int cts_engine_stream_destroy(cts_engine*, void*) { return CTS_E_NO_DEVICE; }
 
 hipError_t hipStreamSynchronize(hipStream_t) { return hipErrorNoDevice; }
+hipError_t hipEventCreateWithFlags(hipEvent_t*, unsigned) { return hipErrorNoDevice; }
+hipError_t hipEventRecord(hipEvent_t, hipStream_t) { return hipErrorNoDevice; }
+hipError_t hipEventQuery(hipEvent_t) { return hipErrorNoDevice; }
+hipError_t hipEventDestroy(hipEvent_t) { return hipErrorNoDevice; }
 
 // A "device" counter block here is host memory with the device layout (CTS_COUNTER_SHARDS shards of 8 u64,
 // the first 5 used), so the host-side fold of cts_counters_read_multi can be driven without a GPU.

@@ -64,6 +64,33 @@ def test_loopback_with_c_oracle_hook():
     assert r["data_errors"] == 1
 
 
+def test_loopback_thread_cpu_accounting():
+    """recv_cpu_seconds / send_cpu_seconds: RUSAGE_THREAD of the threads that ran the data recvs / sends. Verifying
+    on the receive thread (the reference's arrangement) costs that thread CPU that verification off does not;
+    a verifier that burns 2 ms per batch shows up in the receive side only."""
+    import time
+
+    shared_buffer_attach(_SENDER)
+    cfg = dict(connections=2, buffer_size=65536, transfer_size=4 * 1024 * 1024)
+    off = loopback.run(verify=False, **cfg)
+    assert off["connections_ok"] == 2
+    assert 0 < off["recv_cpu_seconds"] and 0 < off["send_cpu_seconds"]
+
+    def slow(arena, descs):  # the oracle after 2 ms of spinning on the calling (receive) thread
+        t_end = time.thread_time() + 0.002
+        while time.thread_time() < t_end:
+            pass
+        return _oracle_verifier(arena, descs)
+
+    r = loopback.run(verifier=slow, verify_mode=A.VERIFY_SYNC, **cfg)
+    assert r["connections_ok"] == 2 and r["data_errors"] == 0
+    calls = r["buffers_verified"]
+    # every VerifyBuffer ran on a receive thread: at least 2 ms of its CPU each
+    assert r["recv_cpu_seconds"] >= 0.002 * calls * 0.9, (r["recv_cpu_seconds"], calls)
+    assert r["send_cpu_seconds"] < 0.002 * calls / 2
+    assert r["recv_cpu_s_per_GiB"] == pytest.approx(r["recv_cpu_seconds"] / (r["bytes_recv"] / (1 << 30)))
+
+
 # ---- PushPull (sync functor) and Duplex (async functor: a send and a recv in flight per side) -----------------
 @pytest.mark.parametrize("mode", [A.VERIFY_SYNC, A.VERIFY_DEFERRED], ids=["sync", "deferred"])
 def test_loopback_pushpull_cpu(mode):

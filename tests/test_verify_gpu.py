@@ -694,6 +694,175 @@ def test_verify_mapped_mailbox_group_keepalive(monkeypatch):
     assert launches == 2, launches
 
 
+def _mapped_check(eng, arr, dev, S, n, e, flip=None):
+    """verify_mapped of arr[:n] (= S[e:e + n], one byte flipped at `flip`) against the oracle's record."""
+    arr[:n] = S[e:e + n]
+    if flip is not None:
+        arr[flip] ^= 0x3C
+    r = eng.verify_mapped(dev, n, e)
+    o = oracle.verify_buffer(arr[:n].copy(), 0, e, n)
+    return (r["pass"], r["first_mismatch"], r["expected"], r["actual"], r["mismatch_bytes"]) == (
+        o["pass"], o["first_mismatch"], o["expected"], o["actual"], o["mismatch_bytes"])
+
+
+def test_verify_mapped_mailbox_late_poller(monkeypatch):
+    """a job slot is reused once the workgroups that answer a job have answered, but every workgroup of
+    the group reads every job. One group of 16 slots whose last workgroup starts polling 300 ms late
+    (CTS_MAILBOX_DELAY_MS): 40 jobs of 1 KiB (one piece: answered by the group's first workgroup alone) wrap the
+    ring twice before it polls, then 64 KiB jobs need all four workgroups. The late poller must take the jobs
+    whose slots hold later jobs as no-ops and catch up, so the big jobs are answered by the grid (one launch, no
+    2 s timeout), exactly."""
+    import time
+
+    from ctstraffic_amd import Engine
+
+    monkeypatch.setenv("CTS_MAILBOX_GROUPS", "1")
+    monkeypatch.setenv("CTS_MAILBOX_SLOTS", "16")
+    monkeypatch.setenv("CTS_MAILBOX_DELAY_MS", "300")
+    eng = Engine(0)
+    S = oracle.sender_buffer(140000)
+    arr, h, dev = eng.host_alloc(65536 + 64)
+    try:
+        t0 = time.monotonic()
+        ok = [_mapped_check(eng, arr, dev, S, 1024, (7 * k) % 65536, flip=(k if k % 5 == 0 else None))
+              for k in range(40)]
+        ok += [_mapped_check(eng, arr, dev, S, 65536, 999 + k, flip=(4096 * k + 3 if k % 2 else None))
+               for k in range(8)]
+        took = time.monotonic() - t0
+        launches = eng.mailbox_launches()
+    finally:
+        eng.host_free(h)
+        eng.close()
+    assert all(ok), ok
+    assert launches == 1 and took < 1.5, (launches, took)
+
+
+def test_verify_mapped_mailbox_timeout_recovers(monkeypatch):
+    """one unanswered job used to break the mailbox for the engine's life. Here the first job times out
+    (group 0's last workgroup starts 1.5 s late, CTS_MAILBOX_TIMEOUT_MS 200): that verify and the ones after it
+    take the launch path and stay exact; once the grid has drained (its groups leave after 300 ms without a job)
+    the next post resets the rings and relaunches, and the mailbox answers again."""
+    import time
+
+    from ctstraffic_amd import Engine
+
+    monkeypatch.setenv("CTS_MAILBOX_GROUPS", "1")
+    monkeypatch.setenv("CTS_MAILBOX_DELAY_MS", "1500")
+    monkeypatch.setenv("CTS_MAILBOX_TIMEOUT_MS", "200")
+    monkeypatch.setenv("CTS_MAILBOX_EXIT_MS", "300")
+    eng = Engine(0)
+    S = oracle.sender_buffer(140000)
+    arr, h, dev = eng.host_alloc(65536 + 64)
+    rng = np.random.default_rng(0x7E0)
+    try:
+        ok, slow = [], 0
+        t_end = time.monotonic() + 2.6
+        while time.monotonic() < t_end:
+            n = int(rng.choice([100, 5000, 65536]))
+            ok.append(_mapped_check(eng, arr, dev, S, n, int(rng.integers(0, 65536)),
+                                    flip=int(rng.integers(0, n)) if rng.random() < 0.3 else None))
+            time.sleep(0.005)
+        launches_before = eng.mailbox_launches()
+        for k in range(20):  # through the relaunched grid
+            t0 = time.monotonic()
+            ok.append(_mapped_check(eng, arr, dev, S, 65536, 17 * k, flip=(k * 1000 if k % 3 == 0 else None)))
+            slow += time.monotonic() - t0 > 0.1
+        launches = eng.mailbox_launches()
+    finally:
+        eng.host_free(h)
+        eng.close()
+    assert all(ok) and len(ok) > 100
+    assert launches_before == 2 and launches == 2 and slow == 0, (launches_before, launches, slow)
+
+
+def test_verify_mapped_mailbox_keepalive_many_groups(monkeypatch):
+    """the keepalive refreshed at most one idle group per post. 32 groups whose workgroups leave after
+    400 ms without a job, a watchdog that never stops the grid (CTS_MAILBOX_IDLE_MS 5 s) and one caller posting
+    every 40 ms for 1.5 s (each post lands on one group): the watchdog's no-op jobs must keep all 32 groups
+    resident, so a burst of 32 threads afterwards (jobs on every group) is answered by the same grid."""
+    import threading
+    import time
+
+    from ctstraffic_amd import Engine
+
+    monkeypatch.setenv("CTS_MAILBOX_GROUPS", "32")
+    monkeypatch.setenv("CTS_MAILBOX_EXIT_MS", "400")
+    monkeypatch.setenv("CTS_MAILBOX_IDLE_MS", "5000")
+    eng = Engine(0)
+    S = oracle.sender_buffer(140000)
+    arenas = [eng.host_alloc(65536 + 64) for _ in range(32)]
+    errors = []
+    try:
+        arr, _, dev = arenas[0]
+        t_end = time.monotonic() + 1.5
+        k = 0
+        while time.monotonic() < t_end:
+            if not _mapped_check(eng, arr, dev, S, 65536, k % 65536, flip=(k if k % 4 == 0 else None)):
+                errors.append(("paced", k))
+            k += 1
+            time.sleep(0.04)
+
+        def burst(t):
+            a, _, d = arenas[t]
+            for j in range(20):
+                t0 = time.monotonic()
+                if not _mapped_check(eng, a, d, S, 65536, (t * 977 + j) % 65536, flip=(j if j % 3 == 0 else None)):
+                    errors.append((t, j))
+                if time.monotonic() - t0 > 0.5:
+                    errors.append((t, j, "slow"))
+
+        ths = [threading.Thread(target=burst, args=(t,)) for t in range(32)]
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        launches = eng.mailbox_launches()
+    finally:
+        for _, h, _ in arenas:
+            eng.host_free(h)
+        eng.close()
+    assert not errors, errors[:5]
+    assert launches == 1, launches
+
+
+def test_host_free_while_posting(engine):
+    """hipHostFree waits for the device's kernels, and the resident mailbox grid never ends while
+    other threads post. cts_host_free stops the grid first: frees return quickly while a thread posts 64 KiB
+    verifies back to back, and every verify stays exact (those posted during a free take the launch path)."""
+    import threading
+    import time
+
+    S = oracle.sender_buffer(140000)
+    arr, h, dev = engine.host_alloc(65536 + 64)
+    stop = threading.Event()
+    errors = []
+
+    def poster():
+        k = 0
+        while not stop.is_set():
+            if not _mapped_check(engine, arr, dev, S, 65536, (31 * k) % 65536, flip=(k if k % 4 == 0 else None)):
+                errors.append(k)
+            k += 1
+
+    th = threading.Thread(target=poster)
+    th.start()
+    frees = []
+    try:
+        time.sleep(0.1)
+        for _ in range(6):
+            _, hh, _ = engine.host_alloc(1 << 20)
+            t0 = time.monotonic()
+            engine.host_free(hh)
+            frees.append(time.monotonic() - t0)
+            time.sleep(0.05)
+    finally:
+        stop.set()
+        th.join()
+        engine.host_free(h)
+    assert not errors, errors[:5]
+    assert max(frees) < 0.5, frees
+
+
 def test_verify_mapped_mailbox_restarts_after_idle(engine):
     """The mailbox grid stops after CTS_MAILBOX_IDLE_MS (50 ms) without posts and the next post starts it again;
     answers stay exact across the restart, including an HBM buffer and a buffer larger than the grid's
@@ -782,7 +951,7 @@ def test_launch_variants_parity(tuning_engine, variant, nt):
 
 
 # ---- every small-buffer (datagram) kernel is bit-identical --------------------------------------
-@pytest.mark.parametrize("small_variant", list(range(10)))
+@pytest.mark.parametrize("small_variant", list(range(15)))
 def test_small_variants_parity(tuning_engine, small_variant):
     """Small-buffer path (max_length_hint <= 8192): one wave per buffer (0-4) and four
     buffers per wave in 16-lane teams (5-8; 9 walking block-contiguous ranges), vs the oracle. Includes spans longer than the
@@ -800,7 +969,7 @@ def test_small_variants_parity(tuning_engine, small_variant):
                                              (33, 120, 20000, 1472, True), (34, 1000, 3000, 8192, False),
                                              (35, 7, 40, 40, True)]:
             for sbpc, chunk in ((1, 0), (64, 0), (1, 16), (2, 48)):
-                if chunk and small_variant != 9:  # (only variant 9 walks chunks)
+                if chunk and small_variant < 9:  # (only variants 9-12 walk chunks)
                     continue
                 engine.set_attr(_lib.ATTR_SMALL_BLOCKS_PER_CU, sbpc)
                 engine.set_attr(_lib.ATTR_SMALL_CHUNK, chunk)
