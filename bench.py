@@ -704,6 +704,20 @@ def run_extras(engine, torch, W, w, arenas, descs, dev, want):
             out["media_stream_strided_status_verify_GiBps"] = round(wd.verified_bytes() / t / GIB, 1)
             out["media_stream_status_parity"] = bool(
                 engine.read_counters(ctr_c)["buffers_failed"] == 11 * len(np.unique(wd.corrupt_buf)))
+            # the receive pass with the client's frame accounting summed on the GPU (no per-datagram output;
+            # a jitter window of 10 frames from sequence number 1: the config-3 datagrams carry seq = i + 1)
+            win = MS.FrameWindow(1, wd.n, 10, 0)
+            sums = MS.FrameSums(win.frames, device=dev)
+            t = _time_kernel(torch, lambda i: MS.verify_frames(engine, ad, dd, win, sums), 10)
+            out["media_stream_frames_verify_GiBps"] = round(wd.verified_bytes() / t / GIB, 1)
+            t = _time_kernel(torch, lambda i: MS.verify_strided_frames(engine, ad, wd.max_length, lens, win, sums), 10)
+            out["media_stream_strided_frames_verify_GiBps"] = round(wd.verified_bytes() / t / GIB, 1)
+            ft, fb = sums.read()
+            bad = np.unique(wd.corrupt_buf)
+            in_win = 10 - int(np.sum(bad < 10))  # clean datagrams of sequence numbers 1..10
+            out["media_stream_frames_parity"] = bool(
+                ft.exceptions == len(bad) and ft.datagrams == wd.n - len(bad) and int(fb.sum()) == 1472 * in_win and
+                ft.error_frames == wd.n - len(bad) - in_win and ft.first_exception == int(bad[0]))
             del st
             del lens
             del recs, res

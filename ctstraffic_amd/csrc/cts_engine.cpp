@@ -826,6 +826,46 @@ int cts_media_stream_verify_strided_status(cts_engine* e, const void* dev_arena,
                                                       static_cast<hipStream_t>(stream), e->geo));
 }
 
+static int media_stream_frames(cts_engine* e, const void* dev_arena, uint64_t arena_bytes, const cts_buf_desc* dev_descs,
+                               uint32_t stride, const uint32_t* dev_lengths, uint32_t n, const cts_frame_window* w,
+                               void* dev_totals, uint64_t* dev_frame_bytes, void* dev_counters, void* stream)
+{
+    if (e == nullptr || w == nullptr || dev_totals == nullptr || ((uintptr_t)dev_totals & 7u) != 0 ||
+        (w->frames != 0 && (dev_frame_bytes == nullptr || ((uintptr_t)dev_frame_bytes & 7u) != 0)))
+        return CTS_E_INVALID;
+    if (n != 0 && (dev_arena == nullptr || ((uintptr_t)dev_arena & 15u) != 0 || outputs_misaligned(nullptr, dev_counters)))
+        return CTS_E_INVALID;
+    if (n != 0 && dev_descs == nullptr &&
+        (dev_lengths == nullptr || ((uintptr_t)dev_lengths & 3u) != 0 || arena_bytes < 16u || stride == 0))
+        return CTS_E_INVALID;
+    if (n != 0 && dev_descs != nullptr && ((uintptr_t)dev_descs & 7u) != 0) return CTS_E_INVALID;
+    DeviceGuard g(e->device);
+    if (!g.ok) return CTS_E_HIP;
+    return hip_status(cts::launch_media_stream_frames(static_cast<const uint8_t*>(dev_arena), arena_bytes, dev_descs,
+                                                      dev_lengths, stride, n, *w, static_cast<uint64_t*>(dev_totals),
+                                                      dev_frame_bytes, static_cast<uint64_t*>(dev_counters),
+                                                      static_cast<hipStream_t>(stream), e->geo));
+}
+
+int cts_media_stream_verify_frames(cts_engine* e, const void* dev_arena, uint64_t arena_bytes,
+                                   const cts_buf_desc* dev_descs, uint32_t n, const cts_frame_window* window,
+                                   void* dev_totals, uint64_t* dev_frame_bytes, void* dev_counters, void* stream)
+{
+    if (n != 0 && dev_descs == nullptr) return CTS_E_INVALID;
+    return media_stream_frames(e, dev_arena, arena_bytes, dev_descs, 0u, nullptr, n, window, dev_totals,
+                               dev_frame_bytes, dev_counters, stream);
+}
+
+int cts_media_stream_verify_strided_frames(cts_engine* e, const void* dev_arena, uint64_t arena_bytes, uint32_t stride,
+                                           const uint32_t* dev_lengths, uint32_t n, const cts_frame_window* window,
+                                           void* dev_totals, uint64_t* dev_frame_bytes, void* dev_counters,
+                                           void* stream)
+{
+    if (n != 0 && dev_lengths == nullptr) return CTS_E_INVALID;
+    return media_stream_frames(e, dev_arena, arena_bytes, nullptr, stride, dev_lengths, n, window, dev_totals,
+                               dev_frame_bytes, dev_counters, stream);
+}
+
 size_t cts_counters_device_bytes(void) { return (size_t)CTS_COUNTER_SHARDS * cts::kCounterSlots * sizeof(uint64_t); }
 
 int cts_counters_reset(cts_engine* e, void* dev_counters, void* stream)

@@ -22,12 +22,12 @@ enum CounterSlot { kBytesChecked = 0, kBytesOk = 1, kBuffersChecked = 2, kBuffer
 #define CTS_TUNING 0
 #endif
 constexpr int kDefaultVerifyVariant = 13;
-constexpr int kDefaultSmallVariant = 9;
+constexpr int kDefaultSmallVariant = 15;  // variant 9 + the edge load L2-allocating (round 3)
 constexpr int kDefaultMediaStreamVariant = 3;
 #if CTS_TUNING
 constexpr int kVerifyVariants = 19;  // workgroup-per-buffer verify variants (launch_verify)
-constexpr int kSmallVariants = 15;   // small-buffer (datagram) verify variants (10-14: line policies)
-constexpr int kMediaStreamVariants = 12;  // MediaStream receive kernels (launch_media_stream_verify)
+constexpr int kSmallVariants = 16;   // small-buffer (datagram) verify variants (10-15: line policies)
+constexpr int kMediaStreamVariants = 13;  // MediaStream receive kernels (launch_media_stream_verify)
 #endif
 // A launch-variant attribute value this build can launch.
 inline bool variant_ok(int value, int dflt, int count)
@@ -158,6 +158,13 @@ hipError_t launch_media_stream_verify_strided(const uint8_t* arena, uint64_t are
 hipError_t launch_media_stream_status(const uint8_t* arena, uint64_t arena_bytes, const cts_buf_desc* descs,
                                      const uint32_t* lengths, uint32_t stride, uint32_t n, cts_datagram_status* status,
                                      uint64_t* counters, hipStream_t stream, const LaunchGeometry& geo);
+
+// The receive pass summing the client's frame accounting (cts_media_stream_verify_frames); descs == nullptr: the
+// strided ring. Zeroes totals (cts_frame_totals_device_bytes()) and frame_bytes[win.frames] first.
+hipError_t launch_media_stream_frames(const uint8_t* arena, uint64_t arena_bytes, const cts_buf_desc* descs,
+                                     const uint32_t* lengths, uint32_t stride, uint32_t n, const cts_frame_window& win,
+                                     uint64_t* totals, uint64_t* frame_bytes, uint64_t* counters, hipStream_t stream,
+                                     const LaunchGeometry& geo);
 
 hipError_t launch_media_stream_fill(uint8_t* arena, uint64_t arena_bytes, const cts_buf_desc* descs,
                                    const cts_datagram_header* headers, uint32_t n, hipStream_t stream,

@@ -985,6 +985,9 @@ __device__ __forceinline__ u32x4 quad_edge_xor(const QSpan& q, uint32_t ce, u32x
 // and was often gone when the round asked for it again (config 3, 4 M datagrams: 8 M extra L2 requests, 0.9 M
 // extra misses, FETCH_SIZE 1.7 % over the arena; profiles/r03/dg_probe/).
 constexpr int kQuadEdgesInRound = 4;
+// LP bit 3: the separate edge-chunk load (issued before the rounds) with the default policy, so the two lines it
+// brings into L2 stay there for the round loads that request them again (nontemporal: inserted at LRU).
+constexpr int kQuadEdgePlain = 8;
 template <int U, bool NT, int LP = 0>
 __device__ __forceinline__ uint32_t quad_scan_interior(const QSpan& q, uint32_t lane)
 {
@@ -1323,7 +1326,7 @@ __global__ void __launch_bounds__(kBlock)
             acc = quad_scan_interior<U, NT, LP>(q, lane);
         } else {
             const uint32_t ce = quad_edge_chunk(q, lane);
-            const u32x4 edge = load_chunk_g<(LP & 2) ? false : NT>(q.p + ce);
+            const u32x4 edge = load_chunk_g<(LP & (2 | kQuadEdgePlain)) ? false : NT>(q.p + ce);
             acc = quad_scan_interior<U, NT, LP>(q, lane);
             acc |= quad_edge_used(q, lane) ? or4(quad_edge_xor(q, ce, edge)) : 0u;
         }
@@ -1803,14 +1806,41 @@ __device__ __forceinline__ void ms_datagram(const MsSource& src, uint32_t i, uin
 // STATUS: records points at 16-byte cts_datagram_status entries (results unused).
 // FAILMARK: records points at statuses ms_status_gather_kernel already wrote; only a corrupt DATA datagram's
 // pass byte is cleared (a rare byte store: the read stream runs as if it wrote nothing).
+// FRAMES (cts_media_stream_verify_frames): the client's accounting of the batch, summed on the GPU. The jitter window
+// does not move between two render ticks, so CompleteTaskBackToPattern (ctsIOPatternMediaStream.cpp:150-272) over a
+// batch is a sum over its clean DATA datagrams: bits received, the bytes of each frame in the window, an error frame
+// for each one outside it. Every other datagram is an exception (its lowest index is kept): the client replays such a
+// batch datagram by datagram.
+constexpr uint32_t kFramesLds = 512;  // window slots summed in LDS per workgroup (larger windows: global atomics)
+struct MsFrames {
+    int64_t head;         // the window's first sequence number (the jitter queue's head)
+    int64_t final_frame;  // m_finalFrame
+    uint32_t frames;      // the window's size
+    uint32_t finished;    // the stream finished: a zero-byte datagram is no exception
+    uint64_t* totals;     // CTS_FRAME_TOTAL_SHARDS x {bits, error frames, datagrams, ~first exception | count << 32}
+    uint64_t* frame_bytes;  // [frames]
+};
+
+// EP: the header chunks and the payload's edge chunks, loaded ahead of the rounds, with the default (L2-allocating)
+// policy (kQuadEdgePlain: nontemporal, their lines were often gone from L2 when the rounds asked again).
 template <int U, bool NT, bool ALIGN, bool HDR16, bool CONTIG = false, bool STRIDED = false, int RING = 0,
-          bool STATUS = false, bool FAILMARK = false>
+          bool STATUS = false, bool FAILMARK = false, bool EP = true, bool FRAMES = false>
 __global__ void __launch_bounds__(kBlock)
     media_stream_verify_quad_kernel(const uint8_t* __restrict__ arena, uint64_t arena_bytes, MsSource src, uint32_t n,
                                     void* __restrict__ records, cts_verify_result* __restrict__ results,
-                                    uint64_t* __restrict__ counters, uint32_t per = 0)
+                                    uint64_t* __restrict__ counters, uint32_t per = 0, MsFrames fr = MsFrames{})
 {
     constexpr int TEAMS = kBlock / kQuadTeam;
+    __shared__ uint64_t s_fbytes[FRAMES ? kFramesLds : 1];  // FRAMES: this workgroup's bytes per window slot
+    __shared__ uint64_t s_ftot[4];                          // FRAMES: bits, error frames, datagrams, exceptions
+    uint64_t f_bits = 0;
+    uint32_t f_err = 0, f_data = 0, f_exc = 0, f_inv_first = 0;
+    const bool f_lds = FRAMES && fr.frames <= kFramesLds;
+    if constexpr (FRAMES) {
+        for (uint32_t k = threadIdx.x; k < kFramesLds; k += kBlock) s_fbytes[k] = 0;
+        if (threadIdx.x < 4) s_ftot[threadIdx.x] = 0;
+        __syncthreads();
+    }
     __shared__ uint64_t ctr[TEAMS][5];
     __shared__ QuadOut qout[RING ? 1 : kBlock / 64];
     using RingSlot = typename std::conditional<STATUS, QuadStatusOut, QuadOut>::type;
@@ -1847,7 +1877,7 @@ __global__ void __launch_bounds__(kBlock)
             // chunk is loaded only if it holds one of those bytes (never past the datagram's page)
             const uint32_t hbytes = completed < CTS_UDP_DATA_HEADER_LENGTH ? completed : CTS_UDP_DATA_HEADER_LENGTH;
             if (in && 16u * lane < ho + hbytes)
-                hch = load_chunk_g<NT>(reinterpret_cast<const u32x4*>(dg - ho) + lane);
+                hch = load_chunk_g<EP ? false : NT>(reinterpret_cast<const u32x4*>(dg - ho) + lane);
         } else {
             // header bytes j and j + 16 of this team's datagram (0 past the completed bytes)
             h0 = in && lane < completed;
@@ -1860,7 +1890,7 @@ __global__ void __launch_bounds__(kBlock)
         const QSpan q = quad_span<ALIGN>(dg + CTS_UDP_DATA_HEADER_LENGTH,
                                          maybe_data ? completed - CTS_UDP_DATA_HEADER_LENGTH : 0u, 0u, dummy);
         const uint32_t ce = quad_edge_chunk(q, lane);
-        const u32x4 edge = load_chunk_g<NT>(q.p + ce);
+        const u32x4 edge = load_chunk_g<EP ? false : NT>(q.p + ce);
         uint32_t acc = quad_scan_interior<U, NT>(q, lane);
         acc |= quad_edge_used(q, lane) ? or4(quad_edge_xor(q, ce, edge)) : 0u;
         uint32_t H[6];
@@ -1918,6 +1948,36 @@ __global__ void __launch_bounds__(kBlock)
             w.i = inext;
             continue;
         }
+        if constexpr (FRAMES) {
+            if (lane == 0u && live) {
+                if (data && first == kNone) {
+                    // GetSequenceNumberFromTask: header bytes 2..9; found in the window -> bytes to its frame
+                    // (ctsIOPatternMediaStream.cpp:195-265)
+                    const int64_t seq = (int64_t)((uint64_t)((H[0] >> 16) | (H[1] << 16)) |
+                                                  ((uint64_t)((H[1] >> 16) | (H[2] << 16)) << 32));
+                    const uint64_t k = (uint64_t)seq - (uint64_t)fr.head;
+                    f_bits += (uint64_t)completed * 8u;
+                    ++f_data;
+                    if (seq > fr.final_frame || seq < fr.head || k >= fr.frames) {
+                        ++f_err;
+                    } else if (f_lds) {
+                        __hip_atomic_fetch_add(&s_fbytes[k], (uint64_t)completed, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP);
+                    } else {
+                        atomicAdd((unsigned long long*)&fr.frame_bytes[k], (unsigned long long)completed);
+                    }
+                    qc.add(q.len, true, 0u);
+                } else {
+                    if (data) qc.add(q.len, false, count);  // a corrupt payload: CorruptedBytes
+                    if (!(kind == CTS_DGRAM_ZERO && fr.finished)) {
+                        ++f_exc;
+                        f_inv_first = f_inv_first > ~i ? f_inv_first : ~i;  // the lowest index: the largest ~i
+                    }
+                }
+            }
+            w.i = inext;
+            continue;
+        }
         if (lane == 0u && live) {
             if constexpr (RING > 0) {
                 auto& o_ = qring[team >> 2].slot[rs];
@@ -1943,6 +2003,26 @@ __global__ void __launch_bounds__(kBlock)
         if (rs)
             quad_ring_flush<RING, STATUS ? 4 : 8, RingSlot>(qring[team >> 2], rs, w.end, STATUS ? nullptr : results,
                                                            records);
+    if constexpr (FRAMES) {
+        // the team leaders' sums -> the workgroup's (LDS) -> one shard of the launch's totals
+        uint64_t* const sh = fr.totals + (size_t)(blockIdx.x % CTS_FRAME_TOTAL_SHARDS) * 4u;
+        if (lane == 0u) {
+            if (f_bits) __hip_atomic_fetch_add(&s_ftot[0], f_bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (f_err) __hip_atomic_fetch_add(&s_ftot[1], (uint64_t)f_err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (f_data) __hip_atomic_fetch_add(&s_ftot[2], (uint64_t)f_data, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (f_exc) {  // rare: straight to the shard (u32 ~first exception, then u32 count)
+                uint32_t* const w3 = reinterpret_cast<uint32_t*>(&sh[3]);
+                atomicMax(&w3[0], f_inv_first);
+                atomicAdd(&w3[1], f_exc);
+            }
+        }
+        __syncthreads();
+        if (f_lds)
+            for (uint32_t k = threadIdx.x; k < fr.frames; k += kBlock)
+                if (s_fbytes[k]) atomicAdd((unsigned long long*)&fr.frame_bytes[k], (unsigned long long)s_fbytes[k]);
+        if (threadIdx.x < 3 && s_ftot[threadIdx.x])
+            atomicAdd((unsigned long long*)&sh[threadIdx.x], (unsigned long long)s_ftot[threadIdx.x]);
+    }
     qc.flush<TEAMS>(ctr, team, lane, counters);
 }
 
@@ -2114,7 +2194,8 @@ static void launch_verify_nt(const uint8_t* arena, uint64_t arena_bytes, const c
         case 11:
         case 12:
         case 13:
-        case 14: {  // variant 9 with line policy LP = 1, 2, 3, 4, 5 (quad_scan_interior)
+        case 14:
+        case 15: {  // variant 9 with line policy LP = 1, 2, 3, 4, 5, 8 (quad_scan_interior)
             const ContigGrid cg = contig_grid(n, geo);
 #define CTS_QUAD_LP(LP) verify_quad_kernel<6, NT, true, true, false, LP><<<cg.grid, kBlock, 0, stream>>>(CTS_QUAD_ARGS, cg.per)
             switch (geo.small_variant) {
@@ -2122,7 +2203,8 @@ static void launch_verify_nt(const uint8_t* arena, uint64_t arena_bytes, const c
             case 11: CTS_QUAD_LP(2); break;
             case 12: CTS_QUAD_LP(3); break;
             case 13: CTS_QUAD_LP(4); break;
-            default: CTS_QUAD_LP(5); break;
+            case 14: CTS_QUAD_LP(5); break;
+            default: CTS_QUAD_LP(8); break;
             }
 #undef CTS_QUAD_LP
             break;
@@ -2134,8 +2216,9 @@ static void launch_verify_nt(const uint8_t* arena, uint64_t arena_bytes, const c
         default: verify_wave_kernel<2, NT><<<grid, kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         }
 #else
-        const ContigGrid cg = contig_grid(n, geo);  // small variant 9 (kDefaultSmallVariant)
-        verify_quad_kernel<6, NT, true, true><<<cg.grid, kBlock, 0, stream>>>(CTS_QUAD_ARGS, cg.per);
+        const ContigGrid cg = contig_grid(n, geo);  // small variant 15 (kDefaultSmallVariant)
+        verify_quad_kernel<6, NT, true, true, false, kQuadEdgePlain><<<cg.grid, kBlock, 0, stream>>>(CTS_QUAD_ARGS,
+                                                                                                     cg.per);
 #endif
     } else {
         // variant (large path): 0 = workgroup/buffer U8, 1 = U4, 2 = U16, 3 = wave/buffer U8,
@@ -2401,7 +2484,7 @@ hipError_t launch_verify(const uint8_t* arena, uint64_t arena_bytes, const cts_b
     return hipGetLastError();
 }
 
-// cts_verify_strided: the small-buffer walk (variant 9's kernel) over a uniformly strided ring
+// cts_verify_strided: the small-buffer walk (variant 15's kernel) over a uniformly strided ring
 hipError_t launch_verify_strided(const uint8_t* arena, uint64_t arena_bytes, uint32_t stride, const uint32_t* lens,
                                  uint32_t n, uint32_t skip_head, uint32_t expected, uint32_t conn_index,
                                  cts_verify_result* results, uint64_t* counters, uint32_t* conn_first_fail,
@@ -2411,10 +2494,10 @@ hipError_t launch_verify_strided(const uint8_t* arena, uint64_t arena_bytes, uin
     const VSource src{nullptr, lens, stride, skip_head, expected, conn_index};
     const ContigGrid cg = contig_grid(n, geo);
     if (geo.nontemporal)
-        verify_quad_kernel<6, true, true, true, true><<<cg.grid, kBlock, 0, stream>>>(
+        verify_quad_kernel<6, true, true, true, true, kQuadEdgePlain><<<cg.grid, kBlock, 0, stream>>>(
             arena, arena_bytes, src, n, results, counters, conn_first_fail, n_conns, cg.per);
     else
-        verify_quad_kernel<6, false, true, true, true><<<cg.grid, kBlock, 0, stream>>>(
+        verify_quad_kernel<6, false, true, true, true, kQuadEdgePlain><<<cg.grid, kBlock, 0, stream>>>(
             arena, arena_bytes, src, n, results, counters, conn_first_fail, n_conns, cg.per);
     return hipGetLastError();
 }
@@ -2484,6 +2567,16 @@ hipError_t launch_media_stream_verify(const uint8_t* arena, uint64_t arena_bytes
         else if (geo.ms_variant == 6) (void)CTS_MS_RING(32);
         else (void)CTS_MS_RING(0);
 #undef CTS_MS_RING
+        break;
+    }
+    case 12: {  // variant 3 with the header / edge loads nontemporal (the round-2 product)
+        const ContigGrid cg = contig_grid(n, geo);
+        if (nt)
+            media_stream_verify_quad_kernel<6, true, true, true, true, false, kMsRing, false, false, false>
+                <<<cg.grid, kBlock, 0, stream>>>(CTS_MS_ARGS, cg.per);
+        else
+            media_stream_verify_quad_kernel<6, false, true, true, true, false, kMsRing, false, false, false>
+                <<<cg.grid, kBlock, 0, stream>>>(CTS_MS_ARGS, cg.per);
         break;
     }
     default: {
@@ -2557,6 +2650,16 @@ hipError_t launch_media_stream_status(const uint8_t* arena, uint64_t arena_bytes
 #undef CTS_MS_STATUS_K
         return hipGetLastError();
     }
+    if (geo.ms_variant == 12) {  // the product form with the header / edge loads nontemporal (round 2)
+#define CTS_MS_STATUS_NTE(STR)                                                                                        \
+    media_stream_verify_quad_kernel<6, true, true, true, true, STR, 64, true, false, false><<<cg.grid, kBlock, 0,   \
+                                                                                           stream>>>(             \
+        arena, arena_bytes, src, n, status, nullptr, counters, cg.per)
+        if (descs == nullptr) CTS_MS_STATUS_NTE(true);
+        else CTS_MS_STATUS_NTE(false);
+#undef CTS_MS_STATUS_NTE
+        return hipGetLastError();
+    }
     if (geo.ms_variant == 7) {
         // two passes: headers -> statuses (pass = 1 for DATA), then the payload verify clearing pass on
         // failures. Measured slower than one pass (4.25 vs 4.08 ms per 16 M datagrams): the header gather's
@@ -2599,6 +2702,33 @@ hipError_t launch_media_stream_status(const uint8_t* arena, uint64_t arena_bytes
         else CTS_MS_STATUS(false, false);
     }
 #undef CTS_MS_STATUS
+    return hipGetLastError();
+}
+
+hipError_t launch_media_stream_frames(const uint8_t* arena, uint64_t arena_bytes, const cts_buf_desc* descs,
+                                     const uint32_t* lengths, uint32_t stride, uint32_t n, const cts_frame_window& win,
+                                     uint64_t* totals, uint64_t* frame_bytes, uint64_t* counters, hipStream_t stream,
+                                     const LaunchGeometry& geo)
+{
+    // the sums start from zero on the launch's stream (a batch's totals, not a running sum)
+    hipError_t err = hipMemsetAsync(totals, 0, (size_t)CTS_FRAME_TOTAL_SHARDS * 4u * sizeof(uint64_t), stream);
+    if (err == hipSuccess && win.frames != 0) err = hipMemsetAsync(frame_bytes, 0, (size_t)win.frames * 8u, stream);
+    if (err != hipSuccess || n == 0) return err;
+    // descs == nullptr: the strided-ring form; the variant-3 walk without per-datagram outputs
+    const ContigGrid cg = contig_grid(n, geo);
+    const MsSource src{descs, lengths, stride};
+    const MsFrames fr{win.head_sequence_number, win.final_frame, win.frames, win.finished, totals, frame_bytes};
+#define CTS_MS_FRAMES(NT, STR)                                                                                      \
+    media_stream_verify_quad_kernel<6, NT, true, true, true, STR, 0, false, false, true, true>                     \
+        <<<cg.grid, kBlock, 0, stream>>>(arena, arena_bytes, src, n, nullptr, nullptr, counters, cg.per, fr)
+    if (descs == nullptr) {
+        if (geo.nontemporal) CTS_MS_FRAMES(true, true);
+        else CTS_MS_FRAMES(false, true);
+    } else {
+        if (geo.nontemporal) CTS_MS_FRAMES(true, false);
+        else CTS_MS_FRAMES(false, false);
+    }
+#undef CTS_MS_FRAMES
     return hipGetLastError();
 }
 

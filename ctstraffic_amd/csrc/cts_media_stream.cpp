@@ -338,6 +338,65 @@ const char* cts_media_stream_client_connection_id(const cts_media_stream_client*
     return c == nullptr ? nullptr : c->connection_id;
 }
 
+size_t cts_frame_totals_device_bytes(void) { return (size_t)CTS_FRAME_TOTAL_SHARDS * 4u * sizeof(uint64_t); }
+
+int cts_frame_totals_fold(const void* host_block, cts_frame_totals* o)
+{
+    if (host_block == nullptr || o == nullptr) return CTS_E_INVALID;
+    // shard: {bits, error frames, datagrams, u32 ~first exception | u32 exceptions << 32} (media_stream_verify_quad_kernel)
+    const uint64_t* b = static_cast<const uint64_t*>(host_block);
+    *o = cts_frame_totals{};
+    uint32_t inv_first = 0;
+    for (uint32_t sh = 0; sh < CTS_FRAME_TOTAL_SHARDS; ++sh, b += 4) {
+        o->bits_received += b[0];
+        o->error_frames += b[1];
+        o->datagrams += b[2];
+        inv_first = std::max(inv_first, (uint32_t)b[3]);
+        o->exceptions += (uint32_t)(b[3] >> 32);
+    }
+    o->first_exception = inv_first != 0 ? ~inv_first : 0xFFFFFFFFu;
+    return CTS_OK;
+}
+
+int cts_media_stream_client_window(const cts_media_stream_client* c, cts_frame_window* o)
+{
+    if (c == nullptr || o == nullptr) return CTS_E_INVALID;
+    *o = cts_frame_window{c->frames[c->head].sequence_number, c->final_frame, (uint32_t)c->frames.size(),
+                          c->finished ? 1u : 0u};
+    return CTS_OK;
+}
+
+int cts_media_stream_client_complete_frames(cts_media_stream_client* c, const cts_frame_window* w,
+                                            const cts_frame_totals* t, const uint64_t* frame_bytes, uint32_t n,
+                                            int64_t receiver_qpc, int64_t receiver_qpf)
+{
+    if (c == nullptr || w == nullptr || t == nullptr || (w->frames != 0 && frame_bytes == nullptr))
+        return CTS_E_INVALID;
+    cts_frame_window now{};
+    (void)cts_media_stream_client_window(c, &now);
+    if (w->head_sequence_number != now.head_sequence_number || w->final_frame != now.final_frame ||
+        w->frames != now.frames || w->finished != now.finished)
+        return CTS_E_INVALID;  // a render tick moved the window since the batch was summed
+    if (c->last_error != CTS_STATUS_IO_RUNNING) return c->last_error == 0 ? CTS_IO_COMPLETED : CTS_IO_FAILED;
+    if (t->first_exception != 0xFFFFFFFFu || t->exceptions != 0) return CTS_MS_FRAMES_REPLAY;
+    // the per-datagram accounting of complete_datagrams, summed (ctsIOPatternMediaStream.cpp:195-265)
+    c->datagrams += n;
+    c->bits_received += (int64_t)t->bits_received;
+    g_udp.bits_received.fetch_add((int64_t)t->bits_received, std::memory_order_relaxed);
+    c->error_frames += (int64_t)t->error_frames;
+    g_udp.error_frames.fetch_add((int64_t)t->error_frames, std::memory_order_relaxed);
+    for (uint32_t k = 0; k < w->frames; ++k) {
+        if (frame_bytes[k] == 0) continue;
+        Frame& f = c->frames[(c->head + k) % c->frames.size()];
+        f.sender_qpc = 0;  // (the sums carry no sender timestamps: no jitter log, as the compact statuses)
+        f.sender_qpf = 0;
+        f.receiver_qpc = receiver_qpc;
+        f.receiver_qpf = receiver_qpf;
+        f.bytes_received += (int64_t)frame_bytes[k];
+    }
+    return CTS_IO_CONTINUE;
+}
+
 int cts_udp_status_details_read(cts_udp_status_details* o)
 {
     if (o == nullptr) return CTS_E_INVALID;

@@ -18,6 +18,7 @@
 #include <atomic>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -400,6 +401,12 @@ struct cts_io_pattern {
     // the next launch, at any non-benign completion and at Flush (Retire)
     std::vector<Queued> inflight;
     hipEvent_t inflight_done = nullptr;  // recorded after the in-flight batch's launch, queried by CompleteIo
+    // Retire waits on inflight_done as a blocking-sync event (the thread sleeps until the kernel's completion
+    // interrupt) instead of spinning in hipStreamSynchronize (CTS_DEFERRED_BLOCKING_SYNC, default 1)
+    bool blocking_retire = [] {
+        const char* v = std::getenv("CTS_DEFERRED_BLOCKING_SYNC");
+        return v == nullptr || *v == 0 || std::atoi(v) != 0;
+    }();
     uint32_t desc_set = 0;  // the half the filling batch uses
     // DEFERRED zero-copy ring: the recv container holds (1 or 2) x BatchCapacity() + recvCount + 1
     // buffer slots and a completed buffer's slot is not handed out again before its batch was
@@ -876,7 +883,9 @@ struct cts_io_pattern {
     int Retire()
     {
         if (inflight.empty()) return CTS_OK;
-        if (hipStreamSynchronize(stream) != hipSuccess) return CTS_E_HIP;
+        if ((blocking_retire && inflight_done ? hipEventSynchronize(inflight_done) : hipStreamSynchronize(stream)) !=
+            hipSuccess)
+            return CTS_E_HIP;
         const size_t half = (size_t)(desc_set ^ 1u) * BatchCapacity();
         const bool failed = ApplyVerdicts(inflight, reinterpret_cast<const cts_verify_result*>(stage_res.host) + half);
         inflight.clear();
@@ -896,7 +905,9 @@ struct cts_io_pattern {
         if (queue.empty()) return GetCurrentStatus();  // the in-flight batch failed
         const int lr = LaunchBatch();
         if (lr != CTS_OK) return lr;
-        if (inflight_done == nullptr && hipEventCreateWithFlags(&inflight_done, hipEventDisableTiming) != hipSuccess) {
+        if (inflight_done == nullptr &&
+            hipEventCreateWithFlags(&inflight_done, hipEventDisableTiming | (blocking_retire ? hipEventBlockingSync : 0u)) !=
+                hipSuccess) {
             inflight_done = nullptr;
             return CTS_E_HIP;
         }

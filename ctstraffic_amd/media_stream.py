@@ -42,6 +42,27 @@ class Stats(ctypes.Structure):
         return {f: int(getattr(self, f)) for f, _ in self._fields_}
 
 
+class FrameWindow(ctypes.Structure):
+    """cts_frame_window: the client's jitter window a batch is summed for."""
+
+    _fields_ = [("head_sequence_number", ctypes.c_int64), ("final_frame", ctypes.c_int64),
+                ("frames", ctypes.c_uint32), ("finished", ctypes.c_uint32)]
+
+
+class FrameTotals(ctypes.Structure):
+    """cts_frame_totals: a batch's sums, folded from the device block."""
+
+    _fields_ = [("bits_received", ctypes.c_uint64), ("error_frames", ctypes.c_uint64), ("datagrams", ctypes.c_uint64),
+                ("first_exception", ctypes.c_uint32), ("exceptions", ctypes.c_uint32)]
+
+    def as_dict(self) -> dict:
+        return {f: int(getattr(self, f)) for f, _ in self._fields_}
+
+
+FRAMES_REPLAY = 16  # CTS_MS_FRAMES_REPLAY
+NO_EXCEPTION = 0xFFFFFFFF
+
+
 class UdpStatusDetails(ctypes.Structure):
     """cts_udp_status_details: the process-wide UdpStatusDetails (ctsConfig.h:417)."""
 
@@ -67,6 +88,14 @@ def declare(L: ctypes.CDLL) -> None:
         "cts_media_stream_client_render": ([P], i32),
         "cts_media_stream_client_stats": ([P, ctypes.POINTER(Stats)], i32),
         "cts_media_stream_client_connection_id": ([P], ctypes.c_char_p),
+        "cts_frame_totals_device_bytes": ([], ctypes.c_size_t),
+        "cts_frame_totals_fold": ([P, ctypes.POINTER(FrameTotals)], i32),
+        "cts_media_stream_verify_frames": ([P, P, u64, P, u32, ctypes.POINTER(FrameWindow), P, P, P, P], i32),
+        "cts_media_stream_verify_strided_frames": ([P, P, u64, u32, P, u32, ctypes.POINTER(FrameWindow), P, P, P, P],
+                                                   i32),
+        "cts_media_stream_client_window": ([P, ctypes.POINTER(FrameWindow)], i32),
+        "cts_media_stream_client_complete_frames": ([P, ctypes.POINTER(FrameWindow), ctypes.POINTER(FrameTotals), P,
+                                                     u32, i64, i64], i32),
         "cts_udp_status_details_read": ([ctypes.POINTER(UdpStatusDetails)], i32),
         "cts_udp_status_details_reset": ([], None),
     }
@@ -177,6 +206,52 @@ def verify_strided_status(engine, arena, stride: int, lengths, status=None, coun
                                                            _stream(stream)))
 
 
+class FrameSums:
+    """Device outputs of one cts_media_stream_verify_frames launch: the totals block and bytes per window slot."""
+
+    def __init__(self, window_frames: int, device="cuda"):
+        import torch
+
+        self.totals = torch.zeros(int(lib().cts_frame_totals_device_bytes()), dtype=torch.uint8, device=device)
+        self.frame_bytes = torch.zeros(max(1, window_frames), dtype=torch.int64, device=device)
+
+    def read(self):
+        """(FrameTotals folded on the host, frame_bytes as uint64 numpy)."""
+        t = FrameTotals()
+        host = np.ascontiguousarray(self.totals.cpu().numpy())
+        check("cts_frame_totals_fold", lib().cts_frame_totals_fold(host.ctypes.data, ctypes.byref(t)))
+        return t, self.frame_bytes.cpu().numpy().view(np.uint64)
+
+
+def verify_frames(engine, arena, descs, window: FrameWindow, sums: FrameSums, counters=None, stream=None) -> None:
+    """cts_media_stream_verify_frames: the receive pass summing the client's frame accounting for `window`."""
+    from .engine import _check_outputs, _nbytes, _stream
+
+    n = _nbytes(descs) // DESC_DTYPE.itemsize
+    _check_outputs(n, None, counters)
+    if sums.frame_bytes.numel() < window.frames:
+        raise ValueError("frame_bytes holds %d slots, the window %d" % (sums.frame_bytes.numel(), window.frames))
+    check("cts_media_stream_verify_frames",
+          engine._L.cts_media_stream_verify_frames(engine._h, _ptr(arena), _nbytes(arena), _ptr(descs), n,
+                                                   ctypes.byref(window), _ptr(sums.totals), _ptr(sums.frame_bytes),
+                                                   _ptr(counters), _stream(stream)))
+
+
+def verify_strided_frames(engine, arena, stride: int, lengths, window: FrameWindow, sums: FrameSums, counters=None,
+                          stream=None) -> None:
+    """cts_media_stream_verify_strided_frames: the same over a strided receive ring."""
+    from .engine import _check_outputs, _nbytes, _stream
+
+    n = _nbytes(lengths) // 4
+    _check_outputs(n, None, counters)
+    if sums.frame_bytes.numel() < window.frames:
+        raise ValueError("frame_bytes holds %d slots, the window %d" % (sums.frame_bytes.numel(), window.frames))
+    check("cts_media_stream_verify_strided_frames",
+          engine._L.cts_media_stream_verify_strided_frames(engine._h, _ptr(arena), _nbytes(arena), stride,
+                                                           _ptr(lengths), n, ctypes.byref(window), _ptr(sums.totals),
+                                                           _ptr(sums.frame_bytes), _ptr(counters), _stream(stream)))
+
+
 class MediaStreamClient:
     """ctsIoPatternMediaStreamClient's frame accounting (ctsIOPatternMediaStream.cpp:46-530)."""
 
@@ -223,6 +298,47 @@ class MediaStreamClient:
         if rc < 0:
             raise CtsError("cts_media_stream_client_complete_status", rc)
         return rc, consumed.value
+
+    def window(self) -> FrameWindow:
+        w = FrameWindow()
+        check("cts_media_stream_client_window", lib().cts_media_stream_client_window(self._h, ctypes.byref(w)))
+        return w
+
+    def complete_frames(self, window: FrameWindow, totals: FrameTotals, frame_bytes: np.ndarray, n: int,
+                        receiver_qpc: int = 0, receiver_qpf: int = 0) -> int:
+        """CompleteIo of a batch of n datagrams from its GPU sums. Returns a cts_io_status, or FRAMES_REPLAY when
+        the batch holds an exception (nothing applied)."""
+        fb = np.ascontiguousarray(frame_bytes, dtype=np.uint64)
+        rc = lib().cts_media_stream_client_complete_frames(self._h, ctypes.byref(window), ctypes.byref(totals),
+                                                           fb.ctypes.data, n, receiver_qpc, receiver_qpf)
+        if rc < 0:
+            raise CtsError("cts_media_stream_client_complete_frames", rc)
+        return rc
+
+    def complete_batch_on_gpu(self, engine, arena, descs, sums: "FrameSums" = None, status=None, receiver_qpc: int = 0,
+                              receiver_qpf: int = 0):
+        """One batch through the GPU sums, replayed datagram by datagram from compact statuses when it holds an
+        exception. Returns (cts_io_status, replayed)."""
+        import torch
+
+        from .engine import _nbytes
+
+        n = _nbytes(descs) // DESC_DTYPE.itemsize
+        w = self.window()
+        sums = sums or FrameSums(w.frames, device=arena.device)
+        verify_frames(engine, arena, descs, w, sums)
+        torch.cuda.synchronize(arena.device)
+        t, fb = sums.read()
+        rc = self.complete_frames(w, t, fb, n, receiver_qpc, receiver_qpf)
+        if rc != FRAMES_REPLAY:
+            return rc, False
+        st = status if status is not None else torch.empty(n * DGRAM_STATUS_DTYPE.itemsize, dtype=torch.uint8,
+                                                           device=arena.device)
+        verify_status(engine, arena, descs, status=st)
+        torch.cuda.synchronize(arena.device)
+        rc, _ = self.complete_status(st[: n * DGRAM_STATUS_DTYPE.itemsize].cpu().numpy().view(DGRAM_STATUS_DTYPE),
+                                     receiver_qpc, receiver_qpf)
+        return rc, True
 
     def set_connection_id(self, datagram: bytes) -> None:
         check("cts_media_stream_client_set_connection_id",

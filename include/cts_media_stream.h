@@ -132,6 +132,50 @@ int cts_media_stream_verify_strided_status(cts_engine* engine, const void* dev_a
                                            uint32_t stride, const uint32_t* dev_lengths, uint32_t n,
                                            cts_datagram_status* dev_status, void* dev_counters, void* stream);
 
+/* ---- the receive pass with the client's frame accounting summed on the GPU -------------------------
+ * Between two render ticks the client's jitter window does not move, so CompleteTaskBackToPattern
+ * (ctsIOPatternMediaStream.cpp:150-272) over a batch of received datagrams is a sum over its DATA datagrams whose
+ * payload verified clean: their bits, the bytes of each frame of the window, and one error frame for each datagram
+ * whose sequence number is past the final frame or outside the window. cts_media_stream_verify_frames verifies the
+ * batch and writes exactly those sums (no per-datagram output). Every other datagram -- an ID datagram, a zero-byte
+ * one (unless the stream finished), a short or unknown one, a corrupt payload -- is an exception: the sums then do not
+ * apply, cts_media_stream_client_complete_frames says so (CTS_MS_FRAMES_REPLAY) and the caller replays the batch datagram
+ * by datagram (cts_media_stream_verify_status + cts_media_stream_client_complete_status). */
+typedef struct cts_frame_window {
+    int64_t head_sequence_number;  /* the jitter queue's head frame */
+    int64_t final_frame;           /* m_finalFrame */
+    uint32_t frames;               /* the queue's size: sequence numbers head .. head + frames - 1 */
+    uint32_t finished;             /* the stream finished: a zero-byte datagram is not an exception */
+} cts_frame_window;
+
+#define CTS_FRAME_TOTAL_SHARDS 64
+/* The batch's sums, folded from the device block (cts_frame_totals_fold). */
+typedef struct cts_frame_totals {
+    uint64_t bits_received;        /* clean DATA datagrams: completed bytes x 8 */
+    uint64_t error_frames;         /* ... of them outside the window or past the final frame */
+    uint64_t datagrams;            /* clean DATA datagrams */
+    uint32_t first_exception;      /* lowest index of an exception (0xFFFFFFFF: none) */
+    uint32_t exceptions;
+} cts_frame_totals;
+
+/* Bytes of the device block of totals: CTS_FRAME_TOTAL_SHARDS shards of 32 bytes (workgroups add into shard
+ * blockIdx mod 64, as the counter block). */
+size_t cts_frame_totals_device_bytes(void);
+/* Fold a host copy of the device block. */
+int cts_frame_totals_fold(const void* host_block, cts_frame_totals* out);
+
+/* The receive pass of cts_media_stream_verify (descriptors) / _strided (a receive ring) summing the batch's frame
+ * accounting for `window` into dev_totals (cts_frame_totals_device_bytes(), 8-byte aligned) and
+ * dev_frame_bytes[window->frames] (bytes of sequence number head + k). Both are zeroed on the stream first. The
+ * counter block (may be NULL) accumulates as in cts_media_stream_verify. */
+int cts_media_stream_verify_frames(cts_engine* engine, const void* dev_arena, uint64_t arena_bytes,
+                                   const cts_buf_desc* dev_descs, uint32_t n, const cts_frame_window* window,
+                                   void* dev_totals, uint64_t* dev_frame_bytes, void* dev_counters, void* stream);
+int cts_media_stream_verify_strided_frames(cts_engine* engine, const void* dev_arena, uint64_t arena_bytes,
+                                           uint32_t stride, const uint32_t* dev_lengths, uint32_t n,
+                                           const cts_frame_window* window, void* dev_totals,
+                                           uint64_t* dev_frame_bytes, void* dev_counters, void* stream);
+
 /* ---- client frame accounting (ctsIoPatternMediaStreamClient) ---------------- */
 typedef struct cts_media_stream_settings { /* ctsConfig::MediaStreamSettings */
     uint32_t frame_size_bytes;
@@ -175,6 +219,16 @@ int cts_media_stream_client_complete(cts_media_stream_client* client, const cts_
  * identical to cts_media_stream_client_complete. */
 int cts_media_stream_client_complete_status(cts_media_stream_client* client, const cts_datagram_status* status,
                                             uint32_t n, int64_t receiver_qpc, int64_t receiver_qpf, uint32_t* consumed);
+/* The client's current window for cts_media_stream_verify_frames (it moves only at a render tick). */
+int cts_media_stream_client_window(const cts_media_stream_client* client, cts_frame_window* out);
+/* CompleteIo of a batch of n datagrams from its GPU sums (cts_media_stream_verify_frames over `window`, folded;
+ * frame_bytes[window->frames] copied to host). Returns a cts_io_status as cts_media_stream_client_complete does
+ * (every datagram consumed), CTS_MS_FRAMES_REPLAY when the batch holds an exception (nothing applied: replay it with
+ * cts_media_stream_client_complete_status), or CTS_E_INVALID when `window` is not the client's current one. */
+#define CTS_MS_FRAMES_REPLAY 16
+int cts_media_stream_client_complete_frames(cts_media_stream_client* client, const cts_frame_window* window,
+                                            const cts_frame_totals* totals, const uint64_t* frame_bytes, uint32_t n,
+                                            int64_t receiver_qpc, int64_t receiver_qpf);
 int cts_media_stream_client_set_connection_id(cts_media_stream_client* client, const char* datagram, uint32_t len);
 /* One renderer-timer tick (TimerCallback, ctsIOPatternMediaStream.cpp:470-530,
  * without the wall-clock scheduling): returns 0 = keep rendering, 1 = the stream

@@ -49,6 +49,7 @@ hipError_t hipStreamSynchronize(hipStream_t) { return hipErrorNoDevice; }
 hipError_t hipEventCreateWithFlags(hipEvent_t*, unsigned) { return hipErrorNoDevice; }
 hipError_t hipEventRecord(hipEvent_t, hipStream_t) { return hipErrorNoDevice; }
 hipError_t hipEventQuery(hipEvent_t) { return hipErrorNoDevice; }
+hipError_t hipEventSynchronize(hipEvent_t) { return hipErrorNoDevice; }
 hipError_t hipEventDestroy(hipEvent_t) { return hipErrorNoDevice; }
 
 // A "device" counter block here is host memory with the device layout (CTS_COUNTER_SHARDS shards of 8 u64,

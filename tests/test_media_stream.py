@@ -81,11 +81,43 @@ def _status_of(recs, res):
     return st
 
 
+def _sums_of(st, w):
+    """What cts_media_stream_verify_frames writes for statuses st under window w (media_stream_verify_quad_kernel,
+    FRAMES): FrameTotals and the bytes per window slot."""
+    t = M.FrameTotals()
+    t.first_exception = M.NO_EXCEPTION
+    fb = np.zeros(w.frames, dtype=np.uint64)
+    for i, d in enumerate(st):
+        if d["kind"] == M.DGRAM_DATA and d["pass"]:
+            seq = int(d["sequence_number"])
+            t.bits_received += 8 * int(d["completed_bytes"])
+            t.datagrams += 1
+            k = seq - w.head_sequence_number
+            if seq > w.final_frame or k < 0 or k >= w.frames:
+                t.error_frames += 1
+            else:
+                fb[k] += int(d["completed_bytes"])
+        elif not (d["kind"] == M.DGRAM_ZERO and w.finished):
+            t.exceptions += 1
+            t.first_exception = min(t.first_exception, i)
+    return t, fb
+
+
+def _complete_by_sums(cf, st):
+    """A batch through the sums path; a batch holding an exception is replayed from its statuses."""
+    w = cf.window()
+    t, fb = _sums_of(st, w)
+    rc = cf.complete_frames(w, t, fb, len(st))
+    return cf.complete_status(st)[0] if rc == M.FRAMES_REPLAY else rc
+
+
 def _run_both(frame_size, buffered, n_frames, stream, renders_between):
-    """The client over records + results, the client over compact statuses and the Python restatement, in
-    lockstep: every render code and the final statistics agree."""
+    """The client over records + results, the client over compact statuses, the client over per-batch sums (the GPU
+    frame accounting, replaying batches with an exception) and the Python restatement, in lockstep: every render
+    code and the final statistics agree."""
     cm = M.MediaStreamClient(frame_size, buffered, n_frames)
     cs = M.MediaStreamClient(frame_size, buffered, n_frames)
+    cf = M.MediaStreamClient(frame_size, buffered, n_frames)
     om = OM.ClientModel(frame_size, buffered, n_frames)
     recs = np.zeros(len(stream), dtype=DGRAM_RECORD_DTYPE)
     res = np.zeros(len(stream), dtype=RESULT_DTYPE)
@@ -99,6 +131,7 @@ def _run_both(frame_size, buffered, n_frames, stream, renders_between):
         j = min(len(stream), i + renders_between)
         status, consumed = cm.complete(recs[i:j], res[i:j])
         assert cs.complete_status(st[i:j]) == (status, consumed)
+        assert _complete_by_sums(cf, st[i:j]) == status
         for q in range(i, i + consumed):
             k, s, ln, ok = stream[q]
             om.complete(k, s, ln if k != 2 else 0, ok)
@@ -106,19 +139,40 @@ def _run_both(frame_size, buffered, n_frames, stream, renders_between):
         i += consumed
         if status == 0:
             code = cm.render()
-            assert code == om.render() == cs.render()
+            assert code == om.render() == cs.render() == cf.render()
             if code != 0:
                 break  # the stream finished (Abort) or aborted: the functor stops receiving
     while cm.stats()["finished"] == 0 and cm.stats()["last_error"] == OM.RUNNING:
-        assert cm.render() == om.render() == cs.render()
+        assert cm.render() == om.render() == cs.render() == cf.render()
     got = cm.stats()
     exp = om.stats()
     for k in exp:
         assert got[k] == exp[k], (k, got, exp)
     assert cs.stats() == got
+    assert cf.stats() == got
     cm.close()
     cs.close()
+    cf.close()
     return got
+
+
+def test_complete_frames_refuses_a_moved_window():
+    """A batch summed for one window cannot be applied after a render tick moved it."""
+    from ctstraffic_amd._lib import CtsError
+
+    c = M.MediaStreamClient(3000, 2, 6)
+    w = c.window()
+    assert (w.head_sequence_number, w.final_frame, w.frames, w.finished) == (1, 6, 4, 0)
+    st = np.zeros(3, dtype=DGRAM_STATUS_DTYPE)  # frame 1 in three clean datagrams
+    st["kind"], st["pass"], st["completed_bytes"], st["sequence_number"] = M.DGRAM_DATA, 1, 1000, 1
+    t, fb = _sums_of(st, w)
+    assert fb.tolist() == [3000, 0, 0, 0] and t.bits_received == 24000
+    assert c.complete_frames(w, t, fb, 3) == 0
+    assert c.render() == 0 and c.stats()["successful_frames"] == 1
+    with pytest.raises(CtsError):
+        c.complete_frames(w, t, fb, 0)
+    t.exceptions, t.first_exception = 1, 0
+    assert c.complete_frames(c.window(), t, fb, 1) == M.FRAMES_REPLAY
 
 
 @pytest.mark.parametrize("seed", range(6))
@@ -208,7 +262,7 @@ def _to_dev(a, torch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("ms_variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11])
+@pytest.mark.parametrize("ms_variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12])
 def test_gpu_media_stream_verify_matches_oracle(engine, tuning_engine, ms_variant):
     """ms_variant 0: one wave per datagram; 1: four datagrams per wave, header by byte loads;
     2: four per wave, header by 16-byte chunk loads gathered with DPP row shifts; 3: variant 2
@@ -219,7 +273,8 @@ def test_gpu_media_stream_verify_matches_oracle(engine, tuning_engine, ms_varian
     gather, then a payload pass that only clears the pass byte of corrupt datagrams); 8 / 9: variant 3 with the
     statuses of cts_media_stream_verify_status written every round / every 16 rounds, 10: every 32 rounds (the
     product default stages them in the per-wave ring for 64 rounds); 11: variant 3 writing records + results every
-    round (the product writes them every 64 rounds from the ring)."""
+    round (the product writes them every 64 rounds from the ring); 12: variant 3 and the compact receive with the
+    header / edge loads nontemporal (round 2's product)."""
     from ctstraffic_amd import _lib
 
     if ms_variant != 3:
@@ -352,6 +407,126 @@ def test_gpu_media_stream_end_to_end(engine):
     assert code == 1
     s2 = cm2.stats()
     assert s2["successful_frames"] == n_frames and s2["dropped_frames"] == 0 and s2["last_error"] == 0
+
+
+def _frames_case(rng, n, head, frames, final, with_exceptions, finished=False):
+    """Random datagrams around a window: clean DATA of random sizes with sequence numbers before, in, after the window
+    and past the final frame; optionally corrupt payloads, zero-byte, short, ID and unknown-flag datagrams."""
+    S = oracle.sender_buffer(4000)
+    dgs = []
+    for _ in range(n):
+        ln = int(rng.integers(26, 3000))
+        seq = int(rng.choice([rng.integers(head - 30, head), rng.integers(head, head + frames),
+                              rng.integers(head, head + frames), rng.integers(head + frames, head + frames + 40),
+                              rng.integers(final + 1, final + 50), -int(rng.integers(1, 1 << 40))]))
+        d = bytearray(np.array([0], "<u2").tobytes() + np.array([seq, 0, 0], "<i8").tobytes()) + S[:ln - 26].tobytes()
+        if with_exceptions and ln > 26 and rng.random() < 0.01:
+            d[int(rng.integers(26, ln))] ^= 0x20
+        dgs.append(bytes(d))
+    if with_exceptions:
+        for c in _crafted()[2:]:
+            dgs.insert(int(rng.integers(0, len(dgs))), c)
+    elif finished:
+        for _ in range(5):
+            dgs.insert(int(rng.integers(0, len(dgs))), b"")  # zero-byte datagrams after the stream finished
+    return dgs
+
+
+@pytest.mark.gpu
+def test_gpu_media_stream_frames_match_statuses(engine):
+    """cts_media_stream_verify_frames / _strided_frames: the GPU sums of the batch's frame accounting equal the sums
+    of the oracle's per-datagram statuses (bits, error frames, clean DATA datagrams, the bytes of every window slot,
+    the first exception and their count), for windows summed in LDS (<= 512 slots) and with global atomics, several
+    walks, both forms; the counter block is the oracle's."""
+    import torch
+
+    from ctstraffic_amd import _lib
+
+    rng = np.random.default_rng(0xF4A)
+    sbpc0, chunk0 = engine.get_attr(_lib.ATTR_SMALL_BLOCKS_PER_CU), engine.get_attr(_lib.ATTR_SMALL_CHUNK)
+    try:
+        for head, frames, final, exc, fin in ((100, 10, 10**6, False, False), (100, 10, 10**6, True, False),
+                                              (5, 2000, 1500, True, False), (40, 512, 45, False, True),
+                                              (7, 513, 10**9, False, False)):
+            dgs = _frames_case(rng, 6000, head, frames, final, exc, fin)
+            arena, descs = _pack(dgs)
+            er, eres, ectr = oracle.media_stream_verify(arena, descs)
+            w = M.FrameWindow(head, final, frames, 1 if fin else 0)
+            et, efb = _sums_of(_status_of(er, eres), w)
+            assert (et.exceptions > 0) == exc and et.error_frames > 0
+            a, d = _to_dev(arena, torch), _to_dev(descs, torch)
+            # the strided form: the same datagrams in a ring of 3072-byte slots (16-byte aligned)
+            ring = np.zeros(len(dgs) * 3072 + 16, dtype=np.uint8)
+            lens = np.array([len(x) for x in dgs], dtype=np.uint32)
+            for i, x in enumerate(dgs):
+                ring[i * 3072:i * 3072 + len(x)] = np.frombuffer(x, dtype=np.uint8)
+            ra, rl = _to_dev(ring, torch), _to_dev(lens, torch)
+            for sbpc, chunk in ((64, 0), (1, 0), (1, 48)):
+                engine.set_attr(_lib.ATTR_SMALL_BLOCKS_PER_CU, sbpc)
+                engine.set_attr(_lib.ATTR_SMALL_CHUNK, chunk)
+                for strided in (False, True):
+                    sums = M.FrameSums(frames)
+                    ctr = engine.new_counters()
+                    if strided:
+                        M.verify_strided_frames(engine, ra, 3072, rl, w, sums, counters=ctr)
+                    else:
+                        M.verify_frames(engine, a, d, w, sums, counters=ctr)
+                    torch.cuda.synchronize()
+                    t, fb = sums.read()
+                    case = (head, frames, final, exc, fin, sbpc, chunk, strided)
+                    assert t.as_dict() == et.as_dict(), (case, t.as_dict(), et.as_dict())
+                    assert np.array_equal(fb[:frames], efb), case
+                    assert engine.read_counters(ctr) == ectr, case
+    finally:
+        engine.set_attr(_lib.ATTR_SMALL_BLOCKS_PER_CU, sbpc0)
+        engine.set_attr(_lib.ATTR_SMALL_CHUNK, chunk0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(3))
+def test_gpu_media_stream_client_by_frames(engine, seed):
+    """A whole MediaStream stream (split frames, drops, duplicates, local reordering, stray sequence numbers, a
+    corrupt payload for seed 2) received in batches between render ticks: the client fed by the GPU sums (replaying
+    batches with an exception from compact statuses) ends with the same statistics as the client fed every
+    datagram's status (ctsIOPatternMediaStream.cpp:150-530)."""
+    import torch
+
+    rng = np.random.default_rng(0xC11 + seed)
+    frame, n_frames, buffered = 52083, 40, 4
+    stream = _random_stream(rng, frame, n_frames, 1472, p_drop=0.03, p_dup=0.03, p_bad=0.0, p_corrupt=0, shuffle=6)
+    stream += [(0, int(s), 700, True) for s in rng.integers(-3, n_frames + 30, size=20)]  # strays
+    if seed == 2:
+        stream.insert(len(stream) // 2, (0, n_frames // 2, 1000, False))
+    S = oracle.sender_buffer(2000)
+    dgs = []
+    for k, sq, ln, ok in stream:
+        d = bytearray(np.array([0], "<u2").tobytes() + np.array([sq, 0, 0], "<i8").tobytes()) + S[:ln - 26].tobytes()
+        if not ok:
+            d[26 + 5] ^= 1
+        dgs.append(bytes(d))
+    arena, descs = _pack(dgs)
+    a = _to_dev(arena, torch)
+    per = max(1, len(dgs) // n_frames)
+    cg = M.MediaStreamClient(frame, buffered, n_frames)
+    cs = M.MediaStreamClient(frame, buffered, n_frames)
+    replays = 0
+    for i in range(0, len(dgs), per):
+        d = _to_dev(descs[i:i + per], torch)
+        rc, replayed = cg.complete_batch_on_gpu(engine, a, d)
+        replays += replayed
+        st = torch.zeros(len(descs[i:i + per]) * 16, dtype=torch.uint8, device="cuda")
+        M.verify_status(engine, a, d, status=st)
+        torch.cuda.synchronize()
+        rs, _ = cs.complete_status(st.cpu().numpy().view(DGRAM_STATUS_DTYPE))
+        assert rc == rs
+        if rc != 0:
+            break
+        assert cg.render() == cs.render()
+    while cs.stats()["finished"] == 0 and cs.stats()["last_error"] == OM.RUNNING:
+        assert cg.render() == cs.render()
+    assert cg.stats() == cs.stats()
+    assert (replays > 0) == (seed == 2)
+    assert cs.stats()["successful_frames"] > 0
 
 
 @pytest.mark.gpu

@@ -389,6 +389,16 @@ def test_config4_ragged_unaligned_vs_oracle(engine):
 def test_config4_full_shard(engine):
     """1 M x 64 KiB hash-sharded over 4 GPUs: this GPU verifies rank 0's shard (~16 GiB)."""
     _check_workload(engine, W.connection_streams(world=4, rank=0), with_oracle=False)
+    torch.cuda.empty_cache()
+
+
+def test_config4_full_shard_two_gpus(engine):
+    """Config 4's first step, 1 M x 64 KiB hash-sharded over 2 GPUs: this GPU verifies rank 0's shard (~32 GiB
+    resident at once), checked against the analytic outcome and, for >= 4 k sampled buffers, the oracle."""
+    w = W.connection_streams(world=2, rank=0)
+    assert w.verified_bytes() > 30 * 2**30
+    _check_workload(engine, w, with_oracle=False)
+    torch.cuda.empty_cache()
 
 
 def test_config5_full_shard(engine):
@@ -951,7 +961,7 @@ def test_launch_variants_parity(tuning_engine, variant, nt):
 
 
 # ---- every small-buffer (datagram) kernel is bit-identical --------------------------------------
-@pytest.mark.parametrize("small_variant", list(range(15)))
+@pytest.mark.parametrize("small_variant", list(range(16)))
 def test_small_variants_parity(tuning_engine, small_variant):
     """Small-buffer path (max_length_hint <= 8192): one wave per buffer (0-4) and four
     buffers per wave in 16-lane teams (5-8; 9 walking block-contiguous ranges), vs the oracle. Includes spans longer than the
@@ -1004,19 +1014,19 @@ def test_small_variants_parity(tuning_engine, small_variant):
 def _pick(attr, variant, product_engine, tuning_engine):
     from ctstraffic_amd import _lib
 
-    dflt = {_lib.ATTR_VERIFY_VARIANT: 13, _lib.ATTR_SMALL_VARIANT: 9, _lib.ATTR_MS_VARIANT: 3}[attr]
+    dflt = {_lib.ATTR_VERIFY_VARIANT: 13, _lib.ATTR_SMALL_VARIANT: 15, _lib.ATTR_MS_VARIANT: 3}[attr]
     return product_engine if variant == dflt else tuning_engine
 
 
 def test_product_build_launches_the_defaults_only(engine, tuning_engine):
-    """The product library compiles one kernel per path (verify variant 13, small variant 9, MediaStream variant 3)
+    """The product library compiles one kernel per path (verify variant 13, small variant 15, MediaStream variant 3)
     and refuses the others; the tuning build accepts every variant."""
     from ctstraffic_amd import _lib
     from ctstraffic_amd._lib import CtsError
 
     assert "tuning" not in _lib.lib().cts_version().decode()
     assert "tuning" in _lib.tuning_lib().cts_version().decode()
-    for attr, dflt, others in ((_lib.ATTR_VERIFY_VARIANT, 13, (0, 4, 12, 17)), (_lib.ATTR_SMALL_VARIANT, 9, (0, 5)),
+    for attr, dflt, others in ((_lib.ATTR_VERIFY_VARIANT, 13, (0, 4, 12, 17)), (_lib.ATTR_SMALL_VARIANT, 15, (0, 5, 9)),
                                (_lib.ATTR_MS_VARIANT, 3, (0, 2))):
         assert engine.get_attr(attr) == dflt and tuning_engine.get_attr(attr) == dflt
         engine.set_attr(attr, dflt)
@@ -1063,7 +1073,8 @@ def test_max_length_buffers(engine, tuning_engine):
 
     cases = [(_lib.ATTR_VERIFY_VARIANT, 13, 0), (_lib.ATTR_VERIFY_VARIANT, 4, 0), (_lib.ATTR_VERIFY_VARIANT, 3, 0),
              (_lib.ATTR_VERIFY_VARIANT, 18, 0),
-             (_lib.ATTR_SMALL_VARIANT, 9, 1472), (_lib.ATTR_SMALL_VARIANT, 0, 1472), (_lib.ATTR_SMALL_VARIANT, 3, 1472)]
+             (_lib.ATTR_SMALL_VARIANT, 15, 1472), (_lib.ATTR_SMALL_VARIANT, 9, 1472), (_lib.ATTR_SMALL_VARIANT, 0, 1472),
+             (_lib.ATTR_SMALL_VARIANT, 3, 1472)]
     product_engine = engine
     defaults = {a: tuning_engine.get_attr(a) for a, _, _ in cases}
     for attr, variant, hint in cases:  # workgroup, barrier-free workgroup, wave, four-per-wave, wave, pipelined wave

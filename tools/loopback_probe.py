@@ -18,11 +18,22 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("--rounds", type=int, default=2)
     p.add_argument("--gib", type=int, default=1)
+    p.add_argument("--cases", default="all", choices=["all", "deferred_sync_ab"])
     args = p.parse_args()
     eng = Engine(0)
     S = oracle.sender_buffer(65536)
     hook = PA.BATCH_VERIFIER(oracle.batch_verifier_address())
-    cases = [("no_verify", dict(verify=False)),
+    if args.cases == "deferred_sync_ab":
+        # round 3: DEFERRED's Retire sleeping on a blocking-sync event vs spinning in hipStreamSynchronize, and
+        # the receive threads' CPU time per GiB next to the socket path alone and the CPU oracle
+        cases = [("no_verify", dict(verify=False)),
+                 ("cpu_oracle_sync", dict(verifier=hook, verify_mode=PA.VERIFY_SYNC)),
+                 ("gpu_deferred_spin", dict(engine=eng, _env={"CTS_DEFERRED_BLOCKING_SYNC": "0"})),
+                 ("gpu_deferred_blocking", dict(engine=eng, _env={"CTS_DEFERRED_BLOCKING_SYNC": "1"})),
+                 ("gpu_sync_mailbox", dict(engine=eng, verify_mode=PA.VERIFY_SYNC))]
+    else:
+        cases = None
+    cases = cases or [("no_verify", dict(verify=False)),
              ("cpu_oracle_sync", dict(verifier=hook, verify_mode=PA.VERIFY_SYNC)),
              ("gpu_deferred_b256", dict(engine=eng, batch_buffers=256)),
              ("gpu_deferred_b1024", dict(engine=eng, batch_buffers=1024)),
@@ -33,12 +44,18 @@ def main():
              ("duplex_gpu_deferred_b1024", dict(engine=eng, batch_buffers=1024, io_pattern=PA.PATTERN_DUPLEX))]
     for r in range(args.rounds):
         for name, kw in cases:
+            kw = dict(kw)
+            env = kw.pop("_env", {})
+            os.environ.update(env)  # read by each pattern at creation
             if "engine" in kw:
                 shared_buffer_init(eng, 65536)
             else:
                 shared_buffer_attach(S)
             res = LB.run(connections=8, buffer_size=65536, transfer_size=args.gib << 30, **kw)
+            for k in env:
+                os.environ.pop(k)
             print(json.dumps({"round": r, "case": name, "GBps_recv": round(res["GBps_recv"], 2),
+                              "recv_cpu_s_per_GiB": round(res["recv_cpu_s_per_GiB"], 4),
                               "connections_ok": res["connections_ok"], "data_errors": res["data_errors"]}),
                   flush=True)
     eng.close()

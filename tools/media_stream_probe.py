@@ -60,6 +60,22 @@ def main():
         cases += [("ms_strided+records+results", ("ms", 3, ch),
                    lambda a: MS.verify_strided(eng, a, w.max_length, lens, records=recs, results=res))]
         # the compact receive pass (16-byte statuses), descriptors and strided ring
+        # the bare datagram verify over the strided ring (the small path's product kernel)
+        cases += [("verify_strided", ("small", None, ch),
+                   lambda a: eng.verify_strided(a, w.max_length, lens, skip_head=26, expected_offset=0,
+                                                counters=ctr))]
+        # the compact receive over the strided ring for every MediaStream variant asked for (3 = product;
+        # 12 = its header / edge loads nontemporal, round 2)
+        for v in msv:
+            if v is not None:
+                cases += [("ms_strided+status_v%d" % v, ("ms", v, ch),
+                           lambda a: MS.verify_strided_status(eng, a, w.max_length, lens, status=st))]
+        # the receive pass with the frame accounting summed on the GPU (a 10-frame window from sequence number 1)
+        win = MS.FrameWindow(1, w.n, 10, 0)
+        sums = MS.FrameSums(win.frames)
+        cases += [("ms+frames", ("ms", 3, ch), lambda a: MS.verify_frames(eng, a, d, win, sums)),
+                  ("ms_strided+frames", ("ms", 3, ch),
+                   lambda a: MS.verify_strided_frames(eng, a, w.max_length, lens, win, sums))]
         cases += [("ms+status", ("ms", 3, ch), lambda a: MS.verify_status(eng, a, d, status=st)),
                   ("ms+status_two_pass", ("ms", 7, ch), lambda a: MS.verify_status(eng, a, d, status=st)),
                   ("ms+status_every_round", ("ms", 8, ch), lambda a: MS.verify_status(eng, a, d, status=st)),

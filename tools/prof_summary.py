@@ -39,12 +39,18 @@ WORKLOADS = {
                                                "datagrams (%d B payload read)" % (DG * 1446),
     "media_stream_verify_quad_kernel[strided][status]": "config3 MediaStream compact receive, strided ring: 16M x "
                                                         "1472 B datagrams (%d B payload read)" % (DG * 1446),
+    "media_stream_verify_quad_kernel[frames]": "config3 MediaStream receive with the frame accounting summed on the "
+                                               "GPU: 16M x 1472 B datagrams (%d B payload read)" % (DG * 1446),
+    "media_stream_verify_quad_kernel[strided][frames]": "config3 MediaStream receive with GPU frame sums, strided "
+                                                        "ring: 16M x 1472 B datagrams (%d B payload read)" % (DG * 1446),
 }
 ALGO_BYTES = {"verify_wg_kernel": 268435456, "fill_kernel": 268435456, "verify_quad_kernel": DG * 1446,
               "verify_wave_kernel": DG * 1446, "media_stream_verify_quad_kernel": DG * 1446,
               "media_stream_verify_quad_kernel[strided]": DG * 1446, "verify_quad_kernel[strided]": DG * 1446,
               "media_stream_verify_quad_kernel[status]": DG * 1446,
-              "media_stream_verify_quad_kernel[strided][status]": DG * 1446}
+              "media_stream_verify_quad_kernel[strided][status]": DG * 1446,
+              "media_stream_verify_quad_kernel[frames]": DG * 1446,
+              "media_stream_verify_quad_kernel[strided][frames]": DG * 1446}
 RUNS = ("prof", "prof_dg")
 
 
@@ -57,6 +63,8 @@ def _kname(name):
         tag = "[strided]" if len(targs) > si and targs[si] == "true" else ""
         if base == "media_stream_verify_quad_kernel" and len(targs) > 7 and targs[7] == "true":
             tag += "[status]"
+        if base == "media_stream_verify_quad_kernel" and len(targs) > 10 and targs[10] == "true":
+            tag += "[frames]"
         return base + tag
     return base
 
@@ -127,6 +135,15 @@ def main(src, dst):
                                  "avg_us": round(float(d.mean()) / 1e3, 2), "median_us": round(float(np.median(d)) / 1e3, 2),
                                  "min_us": round(float(d.min()) / 1e3, 2),
                                  "algorithmic_GBps_at_avg": round(ALGO_BYTES[k] / float(d.mean()), 1)}
+            if k == "fill_kernel":
+                # the profiled runs (--no-extras) launch the fill only in workload.materialize, right after
+                # torch.zeros wrote the same 256 MiB arena: the 256 MB Infinity Cache absorbs most of that re-write,
+                # so this is not an HBM write rate; the bench's extras.fill_GBps (100 launches over 8 rotated
+                # arenas, 2 GiB) is
+                out[WORKLOADS[k]]["note"] = ("MALL-resident re-write of an arena torch.zeros just wrote: not an HBM "
+                                             "rate (see bench.py extras.fill_GBps, 8 rotated arenas)")
+                out[WORKLOADS[k]].pop("algorithmic_GBps_at_avg")
+                out[WORKLOADS[k]]["algorithmic_GBps_at_avg_mall_resident"] = round(ALGO_BYTES[k] / float(d.mean()), 1)
     pipe = _pipelined(os.path.join(src, "prof_pipe_kt", "run_kernel_trace.csv"))
     if pipe:
         out["config2 verify, pipelined headline leg (bench.py default, streams round-robin)"] = pipe
