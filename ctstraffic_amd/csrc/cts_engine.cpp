@@ -157,6 +157,7 @@ struct Mailbox {
     int idle_ms = 50;
     double timeout_s = 2.0;              // CTS_MAILBOX_TIMEOUT_MS
     uint64_t delay_ticks = 0;            // CTS_MAILBOX_DELAY_MS (test hook: a late poller in the first launch)
+    int polls = 1;                       // CTS_MAILBOX_POLLS: slot reads each poller keeps in flight (1 or 2)
     cts::MailSlot* slots = nullptr;      // host view (coherent, pinned)
     cts::MailSlot* dslots = nullptr;     // device view
     cts::MailPart* parts = nullptr;      // nslots x kMailGroup part records, host view (coherent, pinned)
@@ -207,6 +208,7 @@ struct Mailbox {
         idle_ticks = (uint64_t)exit_ms * 100000ull;
         timeout_s = std::max(1, env_int("CTS_MAILBOX_TIMEOUT_MS", (int)(timeout_s * 1000))) / 1000.0;
         delay_ticks = (uint64_t)std::max(0, env_int("CTS_MAILBOX_DELAY_MS", 0)) * 100000ull;
+        polls = env_int("CTS_MAILBOX_POLLS", polls) == 2 ? 2 : 1;
         DeviceGuard g(e->device);
         if (!g.ok) return CTS_E_HIP;
         void* p = nullptr;
@@ -266,7 +268,7 @@ struct Mailbox {
         cts::MailStarts starts{};
         for (uint32_t i = 0; i < groups; ++i) starts.j[i] = next[i];
         const uint64_t delay = launches.load(std::memory_order_relaxed) == 0 ? delay_ticks : 0;
-        if (cts::launch_mailbox(dslots, dparts, per_group, starts, groups, idle_ticks, stream, delay) != hipSuccess ||
+        if (cts::launch_mailbox(dslots, dparts, per_group, starts, groups, idle_ticks, stream, delay, polls) != hipSuccess ||
             hipEventRecord(grid_done, stream) != hipSuccess)
             return CTS_E_HIP;
         running = true;

@@ -124,8 +124,10 @@ struct MailStarts {
 // (s_memrealtime, 100 MHz) for one job: every wave reaches one of the two exits. per_group = S.
 // groups * kMailGroup workgroups of kMailThreads threads.
 // delay_ticks (test hook, 0 in production): group 0's last workgroup starts polling that much later.
+// polls: slot reads each poller keeps in flight (1 or 2).
 hipError_t launch_mailbox(const MailSlot* slots, MailPart* parts, uint32_t per_group, const MailStarts& starts,
-                          uint32_t groups, uint64_t idle_ticks, hipStream_t stream, uint64_t delay_ticks = 0);
+                          uint32_t groups, uint64_t idle_ticks, hipStream_t stream, uint64_t delay_ticks = 0,
+                          int polls = 1);
 
 hipError_t launch_verify(const uint8_t* arena, uint64_t arena_bytes, const cts_buf_desc* descs, uint32_t n,
                          uint32_t max_length_hint, cts_verify_result* results, uint64_t* counters,

@@ -2295,6 +2295,10 @@ __device__ uint64_t* cts_mail_trace;
     } while (0)
 #endif
 
+// POLLS: reads of the job slot the poller keeps in flight (1, or 2 half a round trip apart; CTS_MAILBOX_POLLS)
+constexpr uint32_t kMailPollGap = 18;  // s_sleep units (64 clocks): ~half the 1.2 us PCIe read round trip
+
+template <int POLLS>
 __global__ __launch_bounds__(kMailThreads) void mailbox_kernel(const MailSlot* slots, MailPart* parts, uint32_t per_group,
                                                                MailStarts starts, uint64_t idle_ticks,
                                                                uint64_t delay_ticks)
@@ -2336,24 +2340,57 @@ __global__ __launch_bounds__(kMailThreads) void mailbox_kernel(const MailSlot* s
             const uint64_t start = wall_clock64();
             CTS_MAIL_STAMP(3);
             u32x4 v;
-            for (;;) {
-                v = __builtin_amdgcn_raw_buffer_load_b128(r, 0u, 0u, kMailAux);
-                if (v[3] == tag) break;
-                if ((int32_t)(v[3] - tag) > 0) {
-                    // a later job already holds this slot: the host reuses a slot only once every part record of
-                    // its job was folded (or at once for a no-op), so job j needed nothing from this workgroup;
-                    // take it as a no-op and catch up (a workgroup that fell per_group jobs behind would otherwise
-                    // wait for a tag that never comes back)
-                    v = u32x4{0u, 0u, kMailSkip, tag};
-                    break;
-                }
+            // this slot's job arrived (or a later one holds it); idle: no job within idle_ticks
+            const auto seen = [&](const u32x4& x) { return x[3] == tag || (int32_t)(x[3] - tag) > 0; };
+            const auto idle = [&](bool& leave) {
                 const uint64_t waited = wall_clock64() - start;
-                if (waited > idle_ticks) {  // no job within idle_ticks: publish one whose tag word is not the tag
-                    v = u32x4{0u, 0u, 0u, ~tag};
-                    break;
-                }
+                leave = waited > idle_ticks;
                 if (waited > kMailHotTicks) __builtin_amdgcn_s_sleep(40);
-                else __builtin_amdgcn_s_sleep(2);
+            };
+            bool leave = false;
+            if constexpr (POLLS == 2) {
+                // two reads of the slot in flight, issued half a PCIe round trip apart, so a new job is seen about
+                // a quarter round trip after it lands instead of half a round trip; each check waits for the older
+                // read only (vmcnt(1)), and the loop's two halves keep one read outstanding at the back edge
+                // (the empty asm with a memory clobber after each read keeps LLVM from sinking the read below the
+                // check of the previous one -- it is used on one path only -- which would leave one read in flight)
+                u32x4 x0 = __builtin_amdgcn_raw_buffer_load_b128(r, 0u, 0u, kMailAux);
+                __builtin_amdgcn_s_sleep(kMailPollGap);
+                for (;;) {
+                    const u32x4 x1 = __builtin_amdgcn_raw_buffer_load_b128(r, 0u, 0u, kMailAux);
+                    asm volatile("" ::: "memory");
+                    if (seen(x0)) {
+                        v = x0;
+                        break;
+                    }
+                    idle(leave);
+                    if (leave) break;
+                    x0 = __builtin_amdgcn_raw_buffer_load_b128(r, 0u, 0u, kMailAux);
+                    asm volatile("" ::: "memory");
+                    if (seen(x1)) {
+                        v = x1;
+                        break;
+                    }
+                    idle(leave);
+                    if (leave) break;
+                }
+            } else {
+                for (;;) {
+                    v = __builtin_amdgcn_raw_buffer_load_b128(r, 0u, 0u, kMailAux);
+                    if (seen(v)) break;
+                    idle(leave);
+                    if (leave) break;
+                    __builtin_amdgcn_s_sleep(2);
+                }
+            }
+            if (leave) {
+                v = u32x4{0u, 0u, 0u, ~tag};  // no job within idle_ticks: publish one whose tag word is not the tag
+            } else if (v[3] != tag) {
+                // a later job already holds this slot: the host reuses a slot only once every part record of its
+                // job was folded (or at once for a no-op), so job j needed nothing from this workgroup; take it as a
+                // no-op and catch up (a workgroup that fell per_group jobs behind would otherwise wait for a tag
+                // that never comes back)
+                v = u32x4{0u, 0u, kMailSkip, tag};
             }
             LDS_ST(s_job[par][0], (uint64_t)v[0] | ((uint64_t)v[1] << 32));
             LDS_ST(s_job[par][1], (uint64_t)v[2] | ((uint64_t)v[3] << 32));
@@ -2458,12 +2495,23 @@ __global__ __launch_bounds__(kMailThreads) void mailbox_kernel(const MailSlot* s
 }
 
 hipError_t launch_mailbox(const MailSlot* slots, MailPart* parts, uint32_t per_group, const MailStarts& starts,
-                          uint32_t groups, uint64_t idle_ticks, hipStream_t stream, uint64_t delay_ticks)
+                          uint32_t groups, uint64_t idle_ticks, hipStream_t stream, uint64_t delay_ticks, int polls)
 {
     if (slots == nullptr || parts == nullptr || per_group == 0 || groups == 0 || groups > kMailMaxGroups)
         return hipErrorInvalidValue;
-    mailbox_kernel<<<groups * kMailGroup, kMailThreads, 0, stream>>>(slots, parts, per_group, starts, idle_ticks,
-                                                                     delay_ticks);
+#if CTS_TUNING
+    // two reads in flight: 6.72-6.79 us per 64 KiB at one caller against 6.32-6.51 with one, same box, three
+    // alternating rounds, no gain at 8 / 16 callers (profiles/r03/mailbox_polls_ab/): tuning build only
+    if (polls == 2) {
+        mailbox_kernel<2><<<groups * kMailGroup, kMailThreads, 0, stream>>>(slots, parts, per_group, starts, idle_ticks,
+                                                                            delay_ticks);
+        return hipGetLastError();
+    }
+#else
+    (void)polls;
+#endif
+    mailbox_kernel<1><<<groups * kMailGroup, kMailThreads, 0, stream>>>(slots, parts, per_group, starts, idle_ticks,
+                                                                        delay_ticks);
     return hipGetLastError();
 }
 

@@ -238,7 +238,14 @@ int cts_verify_host(cts_engine* engine, const void* host_buf, uint32_t len,
  * CTS_MAILBOX_IDLE_MS (default 50) ms without calls (env CTS_MAILBOX_GROUPS,
  * CTS_MAILBOX_SLOTS size it); cts_engine_destroy stops it. Each group also
  * leaves by itself after CTS_MAILBOX_EXIT_MS (default 1000) ms without a job;
- * posts keep every group inside that bound and relaunch a grid that left. */
+ * while posts come, the watchdog gives idle groups no-op jobs to keep them
+ * inside that bound, and a post relaunches a grid that left. A job unanswered
+ * after CTS_MAILBOX_TIMEOUT_MS (default 2000) does not fail the call: it and
+ * later calls verify with one sliced launch + synchronize until the grid has
+ * drained, then the mailbox starts over. While the grid is resident a device-
+ * wide wait (hipDeviceSynchronize, torch.cuda.synchronize) waits for it too,
+ * i.e. until CTS_MAILBOX_IDLE_MS after the last call; cts_host_free stops the
+ * grid first, so a free does not wait on other threads' posts. */
 int cts_verify_mapped(cts_engine* engine, const void* dev_buf, uint32_t len,
                       uint32_t expected_offset, cts_verify_result* out);
 /* How many times the mailbox grid was launched (0 = never used): each launch serves every
