@@ -483,6 +483,46 @@ def test_gpu_media_stream_frames_match_statuses(engine):
 
 
 @pytest.mark.gpu
+def test_gpu_media_stream_frames_edges(engine):
+    """cts_media_stream_verify_frames at its edges: an empty batch zeroes the sums, a zero-slot window counts every
+    clean datagram as an error frame without touching frame_bytes, misaligned or missing outputs are refused."""
+    import torch
+
+    rng = np.random.default_rng(0xED6)
+    dgs = _frames_case(rng, 300, 10, 5, 10**6, False)
+    arena, descs = _pack(dgs)
+    a, d = _to_dev(arena, torch), _to_dev(descs, torch)
+    sums = M.FrameSums(5)
+    sums.totals.fill_(0x5A)
+    sums.frame_bytes.fill_(77)
+    M.verify_frames(engine, a, d[:0], M.FrameWindow(10, 10**6, 5, 0), sums)  # n = 0
+    torch.cuda.synchronize()
+    t, fb = sums.read()
+    assert t.as_dict() == {"bits_received": 0, "error_frames": 0, "datagrams": 0,
+                           "first_exception": M.NO_EXCEPTION, "exceptions": 0} and not fb.any()
+    w0 = M.FrameWindow(10, 10**6, 0, 0)  # no window slot: every clean datagram is an error frame
+    M.verify_frames(engine, a, d, w0, sums)
+    torch.cuda.synchronize()
+    t, _ = sums.read()
+    er, eres, _ = oracle.media_stream_verify(arena, descs)
+    et, _ = _sums_of(_status_of(er, eres), w0)
+    assert t.as_dict() == et.as_dict() and t.error_frames == t.datagrams == len(dgs)
+    import ctypes
+
+    def raw(totals_ptr, frame_bytes_ptr, w):
+        return engine._L.cts_media_stream_verify_frames(engine._h, a.data_ptr(), a.numel(), d.data_ptr(), len(dgs),
+                                                        ctypes.byref(w), totals_ptr, frame_bytes_ptr, None, None)
+
+    w5 = M.FrameWindow(10, 10**6, 5, 0)
+    assert raw(sums.totals.data_ptr(), sums.frame_bytes.data_ptr(), w5) == 0
+    assert raw(sums.totals.data_ptr() + 4, sums.frame_bytes.data_ptr(), w5) < 0  # totals not 8-byte aligned
+    assert raw(None, sums.frame_bytes.data_ptr(), w5) < 0                      # no totals
+    assert raw(sums.totals.data_ptr(), None, w5) < 0                           # a window with slots needs frame_bytes
+    assert raw(sums.totals.data_ptr(), None, w0) == 0                          # ... a zero-slot one does not
+    torch.cuda.synchronize()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("seed", range(3))
 def test_gpu_media_stream_client_by_frames(engine, seed):
     """A whole MediaStream stream (split frames, drops, duplicates, local reordering, stray sequence numbers, a
