@@ -425,7 +425,7 @@ def main():
     extras = {}
     cpu = None
     if rank == 0:
-        want = set(x for x in args.extras_only.split(",") if x) or {"fill", "datagram", "host", "loopback"}
+        want = set(x for x in args.extras_only.split(",") if x) or {"fill", "datagram", "host", "loopback", "shards"}
         if not args.no_extras and world == 1:
             extras = run_extras(engine, torch, W, w, B.arenas, B.descs, dev, want)
         if not args.no_cpu_baseline:
@@ -724,6 +724,32 @@ def run_extras(engine, torch, W, w, arenas, descs, dev, want):
             del ad, dd
         except Exception as e:  # pragma: no cover
             out["datagram_error"] = repr(e)
+    if "shards" in want:
+        try:
+            # configs 4 and 5 at full size: rank 0's connection-hash shard of 1 M x 64 KiB over 2 and 4 GPUs
+            # (32 / 16 GiB) and of 8 M x 64 KiB over 8 GPUs (64 GiB), resident at once, verified in one launch each
+            # (per-buffer records, per-connection first-failure slots, counters); per-GPU work of the N-GPU runs
+            for name, kw in (("config4_shard_of_2", dict(world=2, rank=0)), ("config4_shard_of_4", dict(world=4, rank=0)),
+                             ("config5_shard_of_8", dict(n_conns=8192, buffers_per_conn=1024, world=8, rank=0,
+                                                         name="config5"))):
+                ws = W.connection_streams(**kw)
+                a_s, d_s = W.materialize(engine, ws, device=dev)
+                res_s = engine.new_results(ws.n)
+                cff_s = torch.full((ws.n_conns,), -1, dtype=torch.int32, device=dev)
+                ctr_s = engine.new_counters()
+                launches = 5
+                t = _time_kernel(torch, lambda i: engine.verify(a_s, d_s, max_length_hint=ws.max_length, results=res_s,
+                                                                counters=ctr_s, conn_first_fail=cff_s), launches)
+                _, _, exp_c, exp_cff = W.expected_results(ws)
+                ok = engine.read_counters(ctr_s) == {k: v * (launches + 1) for k, v in exp_c.items()}
+                ok = ok and bool(np.array_equal(cff_s.cpu().numpy().view(np.uint32), exp_cff))
+                out[name] = {"GiBps": round(ws.verified_bytes() / t / GIB, 1),
+                             "GBps": round(ws.verified_bytes() / t / 1e9, 1), "ms_per_launch": round(t * 1e3, 3),
+                             "buffers": ws.n, "verified_bytes": ws.verified_bytes(), "parity": ok}
+                del a_s, d_s, res_s, cff_s
+                torch.cuda.empty_cache()
+        except Exception as e:  # pragma: no cover
+            out["shards_error"] = repr(e)
     if "loopback" in want:
         try:
             # config 1 end to end: loopback TCP push, 8 conns, 64 KiB IO, 1 GiB/conn, -verify:data; the

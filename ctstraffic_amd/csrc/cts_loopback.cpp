@@ -334,7 +334,10 @@ extern "C" int cts_loopback_run_detailed(const cts_loopback_config* cfg, cts_eng
                                          uint32_t n_engines, cts_batch_verifier hook, void* hook_ctx,
                                          cts_loopback_result* out, cts_loopback_side* sides)
 {
-    if (cfg == nullptr || out == nullptr || cfg->connections == 0 || cfg->buffer_size == 0) return CTS_E_INVALID;
+    if (cfg == nullptr || out == nullptr || cfg->connections == 0 || cfg->buffer_size == 0 ||
+        (cfg->buffer_size_high != 0 && cfg->buffer_size_high < cfg->buffer_size))
+        return CTS_E_INVALID;
+    const uint32_t max_buffer = cfg->buffer_size_high ? cfg->buffer_size_high : cfg->buffer_size;  // GetMaxBufferSize
     if (n_engines > 0 && engines == nullptr) return CTS_E_INVALID;
     for (uint32_t k = 0; k < n_engines; ++k)
         if (engines[k] == nullptr) return CTS_E_INVALID;
@@ -349,7 +352,7 @@ extern "C" int cts_loopback_run_detailed(const cts_loopback_config* cfg, cts_eng
     if (engine == nullptr && hook == nullptr && cfg->verify_buffers) return CTS_E_INVALID;
     *out = cts_loopback_result{};
     if (engine != nullptr) {
-        const int rc = cts_shared_buffer_init(engine, cfg->buffer_size);
+        const int rc = cts_shared_buffer_init(engine, max_buffer);
         if (rc != CTS_OK) return rc;
     }
     const int lfd = ::socket(AF_INET, SOCK_STREAM, 0);
@@ -367,7 +370,7 @@ extern "C" int cts_loopback_run_detailed(const cts_loopback_config* cfg, cts_eng
         return CTS_E_INVALID;
     }
     const uint32_t n = cfg->connections;
-    auto make_cfg = [&](bool listening) {
+    auto make_cfg = [&](bool listening, uint32_t side) {
         cts_pattern_config c{};
         c.io_pattern = pattern;
         c.push_bytes = cfg->push_bytes ? cfg->push_bytes : cfg->buffer_size;  // PushPull segments
@@ -378,6 +381,8 @@ extern "C" int cts_loopback_run_detailed(const cts_loopback_config* cfg, cts_eng
         c.pre_post_recvs = 1;
         c.pre_post_sends = 1;
         c.buffer_size_low = cfg->buffer_size;
+        c.buffer_size_high = cfg->buffer_size_high;
+        c.random_seed = (uint64_t)cfg->random_seed + side;
         c.tcp_shutdown = CTS_SHUTDOWN_GRACEFUL;
         c.transfer_size = cfg->transfer_size;
         c.verify_mode = cfg->verify_mode;
@@ -385,13 +390,13 @@ extern "C" int cts_loopback_run_detailed(const cts_loopback_config* cfg, cts_eng
         c.tcp_bytes_per_second = cfg->tcp_bytes_per_second;  // both sides pace their own sends
         c.burst_count = cfg->burst_count;
         c.burst_delay = cfg->burst_delay;
-        c.batch_bytes = (uint64_t)c.batch_buffers * cfg->buffer_size;
+        c.batch_bytes = (uint64_t)c.batch_buffers * max_buffer;
         return c;
     };
     std::vector<cts_io_pattern*> pats(2 * n, nullptr);
     int rc = CTS_OK;
     for (uint32_t i = 0; i < 2 * n && rc == CTS_OK; ++i) {
-        const cts_pattern_config c = make_cfg(i >= n);  // [0,n) clients, [n,2n) servers
+        const cts_pattern_config c = make_cfg(i >= n, i);  // [0,n) clients, [n,2n) servers
         cts_engine* const eng = n_engines ? engines[cts_shard_of(i % n, n_engines)] : nullptr;
         rc = cts_io_pattern_create(&c, eng, &pats[i]);
         if (rc == CTS_OK && hook != nullptr) rc = cts_io_pattern_set_verifier(pats[i], hook, hook_ctx);

@@ -43,6 +43,9 @@ typedef struct cts_loopback_config {
     int64_t tcp_bytes_per_second;   /* -RateLimit per connection (0 = none): senders wait the tasks' time offsets */
     uint32_t burst_count;           /* -BurstCount (0 = not set) */
     uint32_t burst_delay;           /* -BurstDelay, ms */
+    uint32_t buffer_size_high;      /* -Buffer:[buffer_size,buffer_size_high]: every IO draws its size uniformly
+                                       (GetBufferSize, ctsConfig.cpp:4679-4684); 0 = fixed buffer_size */
+    uint32_t random_seed;           /* side i draws its sizes from random_seed + i */
 } cts_loopback_config;
 
 typedef enum cts_loopback_functor {
