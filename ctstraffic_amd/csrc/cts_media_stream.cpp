@@ -378,6 +378,7 @@ int cts_media_stream_client_complete_frames(cts_media_stream_client* c, const ct
         w->frames != now.frames || w->finished != now.finished)
         return CTS_E_INVALID;  // a render tick moved the window since the batch was summed
     if (c->last_error != CTS_STATUS_IO_RUNNING) return c->last_error == 0 ? CTS_IO_COMPLETED : CTS_IO_FAILED;
+    if (t->datagrams > n || t->error_frames > t->datagrams) return CTS_E_INVALID;  // not the sums of these n
     if (t->first_exception != 0xFFFFFFFFu || t->exceptions != 0) return CTS_MS_FRAMES_REPLAY;
     // the per-datagram accounting of complete_datagrams, summed (ctsIOPatternMediaStream.cpp:195-265)
     c->datagrams += n;

@@ -172,7 +172,9 @@ def test_complete_frames_refuses_a_moved_window():
     with pytest.raises(CtsError):
         c.complete_frames(w, t, fb, 0)
     t.exceptions, t.first_exception = 1, 0
-    assert c.complete_frames(c.window(), t, fb, 1) == M.FRAMES_REPLAY
+    assert c.complete_frames(c.window(), t, fb, 4) == M.FRAMES_REPLAY
+    with pytest.raises(CtsError):  # sums of 3 clean datagrams cannot be a batch of 1
+        c.complete_frames(c.window(), t, fb, 1)
 
 
 @pytest.mark.parametrize("seed", range(6))
