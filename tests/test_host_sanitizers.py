@@ -4,8 +4,10 @@ The host half of the engine — the ctsIoPattern mirror (cts_pattern.cpp), Media
 client accounting (cts_media_stream.cpp), status output (cts_status.cpp) and the loopback feeder
 with its sync and async functors (cts_loopback.cpp) — is built from source with g++ against
 link-time fakes of the device entry points (tests/cpp/engine_stub.cpp), with the oracle's C
-verifier as every pattern's hook. Two builds run the MSTest replay (tests/cpp/pattern_replay.cpp)
-and whole loopback connections of every TCP pattern (tests/cpp/loopback_stress.cpp):
+verifier as every pattern's hook. Two builds run the MSTest replay (tests/cpp/pattern_replay.cpp),
+whole loopback connections of every TCP pattern (tests/cpp/loopback_stress.cpp) and the MediaStream
+client fed per datagram, by statuses and by GPU-style frame sums over random streams, several clients
+on threads at once feeding the process-wide UDP counters (tests/cpp/media_stream_client.cpp):
 AddressSanitizer + UndefinedBehaviorSanitizer, and ThreadSanitizer (the async functor's send and
 recv threads share one pattern under the connection lock). Any report fails the test.
 """
@@ -47,7 +49,7 @@ def _build(d, san, driver):
 
 @pytest.mark.parametrize("san", sorted(SAN))
 @pytest.mark.parametrize("driver", ["pattern_replay.cpp", "loopback_stress.cpp", "slices_check.cpp",
-                                    "counters_fold.cpp"])
+                                    "counters_fold.cpp", "media_stream_client.cpp"])
 def test_host_code_under_sanitizer(san, driver):
     with tempfile.TemporaryDirectory() as d:
         exe = _build(d, san, driver)
