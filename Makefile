@@ -22,7 +22,7 @@ TUNING_OBJS := $(patsubst $(CSRC)/%,ctstraffic_amd/build/tuning/%.o,$(TUNED)) \
 SOFLAGS   := -shared -Wl,-Bsymbolic -Wl,--version-script=$(CSRC)/exports.map
 
 DEVICE_VERIFY := ctstraffic_amd/build/device_verify
-TOOLS := tools/hbm_read_ceiling tools/verify_ablation tools/mailbox_probe tools/rw_mix_probe tools/write_shape_probe tools/fill_bisect tools/fill_abi_probe tools/mailbox_bisect
+TOOLS := tools/hbm_read_ceiling tools/verify_ablation tools/mailbox_probe tools/rw_mix_probe tools/write_shape_probe tools/fill_bisect tools/fill_abi_probe tools/mailbox_bisect tools/ring_fill_probe
 
 SYNC_PROBE := tools/sync_probe
 
@@ -40,6 +40,10 @@ tools/%: tools/%.hip
 
 # the product fill kernel included verbatim (diagnostic)
 tools/fill_bisect: tools/fill_bisect.hip $(CSRC)/cts_kernels.hip $(HDRS)
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -Iinclude -I$(CSRC) $< -o $@
+
+# the product MediaStream fill beside flat ring walks (diagnostic)
+tools/ring_fill_probe: tools/ring_fill_probe.hip $(CSRC)/cts_kernels.hip $(HDRS)
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -Iinclude -I$(CSRC) $< -o $@
 
 # the product mailbox kernel driven by a bare host loop (diagnostic)

@@ -718,6 +718,25 @@ def run_extras(engine, torch, W, w, arenas, descs, dev, want):
             out["media_stream_frames_parity"] = bool(
                 ft.exceptions == len(bad) and ft.datagrams == wd.n - len(bad) and int(fb.sum()) == 1472 * in_win and
                 ft.error_frames == wd.n - len(bad) - in_win and ft.first_exception == int(bad[0]))
+            # the sender side: whole datagrams (header + payload, as the MediaStream server sends them) written into
+            # the same ring by cts_media_stream_fill (descriptors) and cts_media_stream_fill_strided (the ring);
+            # the corruption plan is overwritten, so the strided receive then finds every datagram clean
+            from ctstraffic_amd.types import DGRAM_HEADER_DTYPE, DGRAM_STATUS_DTYPE
+
+            hdr = np.zeros(wd.n, dtype=DGRAM_HEADER_DTYPE)
+            hdr["sequence_number"] = np.arange(1, wd.n + 1)
+            hd = torch.from_numpy(hdr.view(np.uint8)).to(dev)
+            t = _time_kernel(torch, lambda i: MS.fill(engine, ad, dd, hd), 5)
+            out["media_stream_fill_GBps_written"] = round(wd.arena_bytes / t / 1e9, 1)
+            t = _time_kernel(torch, lambda i: MS.fill_strided(engine, ad, wd.max_length, lens, hd), 5)
+            out["media_stream_fill_strided_GBps_written"] = round(wd.arena_bytes / t / 1e9, 1)
+            ctr_f = engine.new_counters()
+            MS.verify_strided_status(engine, ad, wd.max_length, lens, status=st, counters=ctr_f)
+            cf = engine.read_counters(ctr_f)
+            seq = st.cpu().numpy().view(DGRAM_STATUS_DTYPE)["sequence_number"]
+            out["media_stream_fill_parity"] = bool(cf["buffers_failed"] == 0 and cf["buffers_checked"] == wd.n and
+                                                   np.array_equal(seq, hdr["sequence_number"]))
+            del hd
             del st
             del lens
             del recs, res

@@ -530,6 +530,7 @@ int cts_engine_create(int device, cts_engine** out)
     e->geo.ms_variant = env_int("CTS_MS_VARIANT", e->geo.ms_variant);
     e->geo.small_chunk = env_int("CTS_SMALL_CHUNK", e->geo.small_chunk);
     e->geo.fill_nt = env_int("CTS_FILL_NT", e->geo.fill_nt);
+    e->geo.ring_fill_blocks_per_cu = env_int("CTS_RING_FILL_BLOCKS_PER_CU", e->geo.ring_fill_blocks_per_cu);
     // a variant this build does not compile falls back to the default (the product build has one per path)
     if (!cts::variant_ok(e->geo.verify_variant, cts::kDefaultVerifyVariant, cts_variant_count(kVerifyVariants)))
         e->geo.verify_variant = cts::kDefaultVerifyVariant;
@@ -759,6 +760,23 @@ int cts_media_stream_fill(cts_engine* e, void* dev_arena, uint64_t arena_bytes, 
     if (!g.ok) return CTS_E_HIP;
     return hip_status(cts::launch_media_stream_fill(static_cast<uint8_t*>(dev_arena), arena_bytes, dev_descs,
                                                     dev_headers, n, static_cast<hipStream_t>(stream), e->geo));
+}
+
+int cts_media_stream_fill_strided(cts_engine* e, void* dev_arena, uint64_t arena_bytes, uint32_t stride,
+                                  const uint32_t* dev_lengths, const cts_datagram_header* dev_headers, uint32_t n,
+                                  void* stream)
+{
+    if (e == nullptr) return CTS_E_INVALID;
+    if (n == 0) return CTS_OK;
+    if (dev_arena == nullptr || ((uintptr_t)dev_arena & 15u) != 0 || dev_lengths == nullptr ||
+        ((uintptr_t)dev_lengths & 3u) != 0 || dev_headers == nullptr || ((uintptr_t)dev_headers & 7u) != 0 ||
+        stride < 32u || (stride & 15u) != 0)
+        return CTS_E_INVALID;
+    DeviceGuard g(e->device);
+    if (!g.ok) return CTS_E_HIP;
+    return hip_status(cts::launch_media_stream_fill_strided(static_cast<uint8_t*>(dev_arena), arena_bytes, stride,
+                                                            dev_lengths, dev_headers, n,
+                                                            static_cast<hipStream_t>(stream), e->geo));
 }
 
 int cts_media_stream_verify(cts_engine* e, const void* dev_arena, uint64_t arena_bytes, const cts_buf_desc* dev_descs,

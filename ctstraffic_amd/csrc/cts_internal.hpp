@@ -60,6 +60,8 @@ struct LaunchGeometry {
     int fill_nt = 2;             // fill store policy: 0 plain, 1 nontemporal, 2 by path (plain for the workgroup
                                  // path, nontemporal for datagrams; tools/tune_verify.py --op fill)
     int fill_blocks_per_cu = 1;  // fill grid cap (write-bound; plain stores: 1 measured best, 48.7 vs 49.1-49.4 us)
+    int ring_fill_blocks_per_cu = 4;  // MediaStream ring fill grid cap (16 M x 1472 B: 4.3 ms at 4, 5.0 at 8;
+                                      // CTS_RING_FILL_BLOCKS_PER_CU; tools/ring_fill_probe.hip)
     int verify_variant = kDefaultVerifyVariant;     // see launch_verify (13: variant 11 at U2; 11: variant 10 + in-register exact diff;
                                  // 10: even-phase stream + whole-line spans, U4, measured 1.3-3 % faster than 6,
                                  // which was +0.3-0.7 % over 0)
@@ -171,5 +173,8 @@ hipError_t launch_media_stream_frames(const uint8_t* arena, uint64_t arena_bytes
 hipError_t launch_media_stream_fill(uint8_t* arena, uint64_t arena_bytes, const cts_buf_desc* descs,
                                    const cts_datagram_header* headers, uint32_t n, hipStream_t stream,
                                    const LaunchGeometry& geo);
+hipError_t launch_media_stream_fill_strided(uint8_t* arena, uint64_t arena_bytes, uint32_t stride, const uint32_t* lengths,
+                                           const cts_datagram_header* headers, uint32_t n, hipStream_t stream,
+                                           const LaunchGeometry& geo);
 
 }  // namespace cts

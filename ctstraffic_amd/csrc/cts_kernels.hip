@@ -1483,8 +1483,36 @@ __global__ void __launch_bounds__(kBlock)
 
 // ---------------------------------------------------------------------------------------------
 // fill: the write-bound twin. Interior chunks are 16-byte stores; the (at most
-// two) edge chunks of a span are written bytewise so neighbouring buffers
+// two) edge chunks of a span write only their own bytes, so neighbouring buffers
 // sharing a 16-byte line are never touched.
+
+// Bytes [b0, b1) of the 16-byte chunk e at dst: whole dwords as dword stores, a partial dword as one
+// aligned short and/or one byte store (at most 6 stores; a byte loop took up to 15).
+__device__ __forceinline__ void store_chunk_bytes(uint8_t* dst, const u32x4& e, uint32_t b0, uint32_t b1)
+{
+#pragma unroll
+    for (uint32_t w = 0; w < 4u; ++w) {
+        const uint32_t lo = b0 > 4u * w ? b0 - 4u * w : 0u, hi = b1 < 4u * w + 4u ? (b1 > 4u * w ? b1 - 4u * w : 0u) : 4u;
+        if (lo >= hi) continue;
+        uint8_t* q = dst + 4u * w;
+        const uint32_t v = e[w];
+        if (lo == 0u && hi == 4u) {
+            *reinterpret_cast<uint32_t*>(q) = v;
+            continue;
+        }
+        uint32_t b = lo;
+        if ((b & 1u) && b < hi) {  // odd start: one byte
+            q[b] = (uint8_t)(v >> (8u * b));
+            ++b;
+        }
+        if (b + 2u <= hi) {  // an aligned pair
+            *reinterpret_cast<uint16_t*>(q + b) = (uint16_t)(v >> (8u * b));
+            b += 2u;
+        }
+        if (b < hi) q[b] = (uint8_t)(v >> (8u * b));  // one byte left
+    }
+}
+
 template <bool NTS = false>
 __device__ __forceinline__ void fill_chunk(u32x4* a0, uint32_t c, uint32_t nchunks, uint32_t q0, uint32_t lo,
                                            uint32_t hi_last)
@@ -1498,8 +1526,7 @@ __device__ __forceinline__ void fill_chunk(u32x4* a0, uint32_t c, uint32_t nchun
         if constexpr (NTS) __builtin_nontemporal_store(e, a0 + c);
         else a0[c] = e;
     } else {
-        uint8_t* dst = reinterpret_cast<uint8_t*>(a0 + c);
-        for (uint32_t b = b0; b < b1; ++b) dst[b] = (uint8_t)(e[b >> 2] >> (8 * (b & 3)));
+        store_chunk_bytes(reinterpret_cast<uint8_t*>(a0 + c), e, b0, b1);
     }
 }
 
@@ -2086,6 +2113,15 @@ __global__ void __launch_bounds__(kBlock)
 
 // Send: header {u16 0, i64 seq, i64 qpc, i64 qpf} + P[0 .. length-26) per datagram
 // (ctsMediaStreamSendRequests' WSABUF array, ctsMediaStreamProtocol.hpp:230-243).
+// A datagram starting on a 16-byte boundary (every slot of a receive-ring-shaped arena, 1472 = 92 x 16) is written
+// as whole 16-byte chunks: chunk c holds datagram bytes [16c, 16c + 16), i.e. pattern positions 16c - 26 on, with
+// the header's 26 bytes assembled in registers into chunks 0 and 1. Only a partial last chunk writes bytes. (The
+// header written bytewise by 26 lanes beside nontemporal payload chunks and 6 byte stores for payload bytes 26..31
+// left the first line of every datagram written in pieces: 8.4 -> 7.0 ms for 16 M x 1472 B, tools/media_stream_probe.py.)
+// What still bounds this kernel is latency, not bytes: each datagram's descriptor and header are loaded before its
+// stores, one datagram per wave at a time (a one-datagram prefetch was slower: 9.3 ms, tools/ring_fill_probe.hip).
+// A ring of datagrams goes through media_stream_fill_ring_kernel instead (cts_media_stream_fill_strided: 4.3 ms).
+template <bool NTS>
 __global__ void __launch_bounds__(kBlock)
     media_stream_fill_kernel(uint8_t* __restrict__ arena, uint64_t arena_bytes, const cts_buf_desc* __restrict__ descs,
                              const cts_datagram_header* __restrict__ headers, uint32_t n)
@@ -2095,12 +2131,34 @@ __global__ void __launch_bounds__(kBlock)
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     for (uint32_t i = blockIdx.x * WAVES + wave; i < n; i += gridDim.x * WAVES) {
         const cts_buf_desc d = descs[i];
+        const cts_datagram_header h = headers[i];
         if (d.length < CTS_UDP_DATA_HEADER_LENGTH || d.byte_offset > arena_bytes ||
             arena_bytes - d.byte_offset < (uint64_t)d.length)
             continue;
         uint8_t* dg = arena + d.byte_offset;
+        if (__builtin_amdgcn_readfirstlane(((uintptr_t)dg & 15u) == 0u ? 1u : 0u)) {
+            const uint64_t seq = (uint64_t)h.sequence_number, qpc = (uint64_t)h.qpc, qpf = (uint64_t)h.qpf;
+            const uint32_t nchunks = (d.length + 15u) >> 4;
+            const uint32_t hi_last = d.length - 16u * (nchunks - 1u);
+            u32x4* p = reinterpret_cast<u32x4*>(dg);
+            for (uint32_t c = lane; c < nchunks; c += 64u) {
+                u32x4 e = expected_chunk((16u * c - CTS_UDP_DATA_HEADER_LENGTH) & 0xFFFFu, 0u);
+                if (c == 0u)  // flag 0 | seq | qpc bytes 0..5
+                    e = u32x4{(uint32_t)(seq << 16), (uint32_t)(seq >> 16), (uint32_t)(seq >> 48) | (uint32_t)(qpc << 16),
+                              (uint32_t)(qpc >> 16)};
+                else if (c == 1u)  // qpc bytes 6..7 | qpf | payload bytes 0..5
+                    e = u32x4{(uint32_t)(qpc >> 48) | (uint32_t)(qpf << 16), (uint32_t)(qpf >> 16),
+                              (uint32_t)(qpf >> 48) | (e[2] & 0xFFFF0000u), e[3]};
+                if (c == nchunks - 1u && hi_last != 16u) {
+                    store_chunk_bytes(reinterpret_cast<uint8_t*>(p + c), e, 0u, hi_last);
+                } else {
+                    if constexpr (NTS) __builtin_nontemporal_store(e, p + c);
+                    else p[c] = e;
+                }
+            }
+            continue;
+        }
         if (lane < CTS_UDP_DATA_HEADER_LENGTH) {
-            const cts_datagram_header h = headers[i];
             uint8_t b = 0;
             if (lane >= 2u && lane < 10u) b = (uint8_t)((uint64_t)h.sequence_number >> (8 * (lane - 2u)));
             else if (lane >= 10u && lane < 18u) b = (uint8_t)((uint64_t)h.qpc >> (8 * (lane - 10u)));
@@ -2115,7 +2173,140 @@ __global__ void __launch_bounds__(kBlock)
         const uint32_t hi_last = (uint32_t)((uint64_t)lo + len - 16ull * (nchunks - 1u));
         const uint32_t q0 = (0u - lo) & 0xFFFFu;
         u32x4* p = reinterpret_cast<u32x4*>(sp - lo);
-        for (uint32_t c = lane; c < nchunks; c += 64u) fill_chunk<true>(p, c, nchunks, q0, lo, hi_last);
+        for (uint32_t c = lane; c < nchunks; c += 64u) fill_chunk<NTS>(p, c, nchunks, q0, lo, hi_last);
+    }
+}
+
+// MediaStream sender over a ring (cts_media_stream_fill_strided): datagram i occupies [i * stride, i * stride +
+// lengths[i]) of a 16-byte aligned arena, stride a multiple of 16, so the ring is a flat array of 16-byte chunks and
+// chunk k is chunk c = k mod (stride / 16) of datagram k / (stride / 16). A datagram with a length below the header,
+// above the stride or past the arena is not written; nor are the bytes between a datagram's end and the next slot.
+//
+// Each workgroup walks one contiguous range of datagrams in batches of kRingBatch: the batch's headers and lengths
+// are loaded into LDS (one vector load per thread, then one wait), and its chunks are cut into four contiguous runs,
+// one per wave, written 64 consecutive chunks (1 KiB) per round across datagram boundaries. In the loop nothing is
+// loaded from memory: a store never waits on a load (vmcnt counts loads and stores in issue order, so a vector load
+// in the loop would wait for every store before it; scalar header loads wait for K$ misses at ~1 us each, and every
+// SMEM wait is lgkmcnt(0), so they cannot be prefetched). A round of whole datagrams (the common case) writes its
+// header chunks through two lane selects and checks nothing per lane. Measured on 16 M x 1472 B
+// (tools/ring_fill_probe.hip): scalar per-round header loads 4.4-4.6 ms; the descriptor kernel 7.0 ms; the bare
+// pattern as one span 4.0-4.2 ms.
+constexpr uint32_t kRingBatch = 512;
+
+struct RingHeader {
+    uint64_t seq, qpc, qpf;
+};
+
+__device__ __forceinline__ u32x4 datagram_chunk(uint32_t c, const u32x4& pattern, uint64_t seq, uint64_t qpc,
+                                                uint64_t qpf)
+{
+    if (c == 0u)  // flag 0 | seq | qpc bytes 0..5
+        return u32x4{(uint32_t)(seq << 16), (uint32_t)(seq >> 16), (uint32_t)(seq >> 48) | (uint32_t)(qpc << 16),
+                     (uint32_t)(qpc >> 16)};
+    if (c == 1u)  // qpc bytes 6..7 | qpf | payload bytes 0..5
+        return u32x4{(uint32_t)(qpc >> 48) | (uint32_t)(qpf << 16), (uint32_t)(qpf >> 16),
+                     (uint32_t)(qpf >> 48) | (pattern[2] & 0xFFFF0000u), pattern[3]};
+    return pattern;
+}
+
+// e with header h in lanes l0 (chunk 0) and l0 + 1 (chunk 1, whose bytes 10..15 are payload: the pattern e already
+// holds there). l0 is wave-uniform and may be outside [0, 64) (wrapped), then no lane matches.
+__device__ __forceinline__ u32x4 header_lanes(u32x4 e, uint32_t lane, uint32_t l0, const RingHeader& h)
+{
+    if (lane == l0) {
+        e = u32x4{(uint32_t)(h.seq << 16), (uint32_t)(h.seq >> 16), (uint32_t)(h.seq >> 48) | (uint32_t)(h.qpc << 16),
+                  (uint32_t)(h.qpc >> 16)};
+    } else if (lane == l0 + 1u) {
+        e[0] = (uint32_t)(h.qpc >> 48) | (uint32_t)(h.qpf << 16);
+        e[1] = (uint32_t)(h.qpf >> 16);
+        e[2] = (uint32_t)(h.qpf >> 48) | (e[2] & 0xFFFF0000u);
+    }
+    return e;
+}
+
+// One chunk with every check: chunk c of datagram j (batch slot t) at ring chunk k.
+template <bool NTS>
+__device__ __forceinline__ void ring_chunk_checked(u32x4* ring, uint64_t k, uint64_t j, uint32_t c, uint32_t len,
+                                                   const RingHeader& h, uint32_t stride, uint64_t arena_bytes)
+{
+    if (len < CTS_UDP_DATA_HEADER_LENGTH || len > stride || 16u * c >= len || j * stride + len > arena_bytes) return;
+    const u32x4 e = datagram_chunk(c, expected_chunk((16u * c - CTS_UDP_DATA_HEADER_LENGTH) & 0xFFFFu, 0u), h.seq,
+                                   h.qpc, h.qpf);
+    if (16u * c + 16u > len) {
+        store_chunk_bytes(reinterpret_cast<uint8_t*>(ring + k), e, 0u, len - 16u * c);
+    } else {
+        if constexpr (NTS) __builtin_nontemporal_store(e, ring + k);
+        else ring[k] = e;
+    }
+}
+
+// SCALAR: stride >= 1024, so a round holds at most two datagram starts and the wave tracks its datagram and chunk as
+// wave-uniform values; otherwise each lane finds its own. full_slots: slots wholly inside the arena (clamped to 2^32-1).
+template <bool NTS, bool SCALAR>
+__global__ void __launch_bounds__(kBlock)
+    media_stream_fill_ring_kernel(uint8_t* __restrict__ arena, uint64_t arena_bytes, uint32_t stride,
+                                  const uint32_t* __restrict__ lengths, const cts_datagram_header* __restrict__ headers,
+                                  uint32_t n, uint32_t full_slots)
+{
+    constexpr uint32_t WAVES = kBlock / 64;
+    __shared__ RingHeader hs[kRingBatch];
+    __shared__ uint32_t ls[kRingBatch];
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t cps = stride >> 4;  // chunks per slot
+    const uint32_t per_wg = (uint32_t)(((uint64_t)n + gridDim.x - 1u) / gridDim.x);
+    const uint64_t g0 = (uint64_t)blockIdx.x * per_wg;
+    const uint64_t g1 = g0 + per_wg < n ? g0 + per_wg : n;
+    u32x4* const ring = reinterpret_cast<u32x4*>(arena);
+    for (uint64_t d0 = g0; d0 < g1; d0 += kRingBatch) {
+        const uint32_t nb = (uint32_t)(g1 - d0 < kRingBatch ? g1 - d0 : kRingBatch);
+        __syncthreads();  // every wave is done with the previous batch's LDS
+        for (uint32_t t = threadIdx.x; t < nb; t += kBlock) {
+            const cts_datagram_header h = headers[d0 + t];
+            hs[t] = RingHeader{(uint64_t)h.sequence_number, (uint64_t)h.qpc, (uint64_t)h.qpf};
+            ls[t] = lengths[d0 + t];
+        }
+        __syncthreads();
+        // this wave's run of the batch's chunks, whole 64-chunk rounds (the last run may end inside one)
+        const uint32_t nk = nb * cps;
+        const uint32_t per_w = ((nk + WAVES - 1u) / WAVES + 63u) & ~63u;
+        uint32_t kl = wave * per_w;
+        const uint32_t kl1 = kl + per_w < nk ? kl + per_w : nk;
+        const uint64_t kbase = d0 * cps;  // the batch's first ring chunk
+        if constexpr (SCALAR) {
+            if (kl >= kl1) continue;
+            uint32_t ib = kl / cps, cb = kl - ib * cps;  // lane 0's datagram (in the batch) and chunk
+            for (; kl < kl1; kl += 64u) {
+                const bool crosses = cb + 63u >= cps;
+                const uint32_t i1 = ib + 1u < nb ? ib + 1u : ib;
+                const uint32_t l0 = ls[ib], l1 = ls[i1];
+                const bool whole = kl + 64u <= kl1 && l0 == stride && d0 + ib < full_slots &&
+                                   (!crosses || (ib + 1u < nb && l1 == stride && d0 + ib + 1u < full_slots));
+                uint32_t c = cb + lane;
+                const bool second = c >= cps;
+                if (second) c -= cps;
+                if (__builtin_amdgcn_readfirstlane(whole ? 1 : 0)) {
+                    u32x4 e = expected_chunk((16u * c - CTS_UDP_DATA_HEADER_LENGTH) & 0xFFFFu, 0u);
+                    if (cb < 2u) e = header_lanes(e, lane, 0u - cb, hs[ib]);
+                    if (crosses) e = header_lanes(e, lane, cps - cb, hs[i1]);
+                    if constexpr (NTS) __builtin_nontemporal_store(e, ring + kbase + kl + lane);
+                    else ring[kbase + kl + lane] = e;
+                } else if (kl + lane < kl1) {
+                    const uint32_t t = second ? i1 : ib;
+                    ring_chunk_checked<NTS>(ring, kbase + kl + lane, d0 + t, c, ls[t], hs[t], stride, arena_bytes);
+                }
+                cb += 64u;
+                if (cb >= cps) {
+                    cb -= cps;
+                    ++ib;
+                }
+            }
+        } else {  // stride < 1024: several datagrams per round, each lane finds its own
+            for (uint32_t k = kl + lane; k < kl1; k += 64u) {
+                const uint32_t t = k / cps, c = k - t * cps;
+                ring_chunk_checked<NTS>(ring, kbase + k, d0 + t, c, ls[t], hs[t], stride, arena_bytes);
+            }
+        }
     }
 }
 
@@ -2785,8 +2976,40 @@ hipError_t launch_media_stream_fill(uint8_t* arena, uint64_t arena_bytes, const 
                                    const LaunchGeometry& geo)
 {
     if (n == 0) return hipSuccess;
-    media_stream_fill_kernel<<<grid_for(n, kBlock / 64, geo), kBlock, 0, stream>>>(arena, arena_bytes, descs, headers,
-                                                                                    n);
+    // store policy as cts_fill's datagram path: fill_nt 0 = plain, 1 or 2 (by path) = nontemporal
+    if (geo.fill_nt == 0)
+        media_stream_fill_kernel<false><<<grid_for(n, kBlock / 64, geo), kBlock, 0, stream>>>(arena, arena_bytes, descs,
+                                                                                             headers, n);
+    else
+        media_stream_fill_kernel<true><<<grid_for(n, kBlock / 64, geo), kBlock, 0, stream>>>(arena, arena_bytes, descs,
+                                                                                            headers, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_media_stream_fill_strided(uint8_t* arena, uint64_t arena_bytes, uint32_t stride, const uint32_t* lengths,
+                                           const cts_datagram_header* headers, uint32_t n, hipStream_t stream,
+                                           const LaunchGeometry& geo)
+{
+    if (n == 0) return hipSuccess;
+    if ((stride & 15u) != 0u || stride < 32u || ((uintptr_t)arena & 15u) != 0u) return hipErrorInvalidValue;
+    const uint64_t cap = (uint64_t)geo.num_cus * (uint64_t)(geo.ring_fill_blocks_per_cu > 0 ? geo.ring_fill_blocks_per_cu : 4);
+    // every workgroup gets at least a batch's worth of datagrams, or the whole ring
+    const uint64_t want = ((uint64_t)n + kRingBatch - 1) / kRingBatch;
+    const uint32_t grid = (uint32_t)(want < cap ? want : cap);
+    const uint64_t slots = arena_bytes / stride;
+    const uint32_t full_slots = (uint32_t)(slots < 0xFFFFFFFFull ? slots : 0xFFFFFFFFull);
+    const bool nts = geo.fill_nt != 0;
+#define CTS_RING_FILL(NT_, SC_)                                                                                   \
+    media_stream_fill_ring_kernel<NT_, SC_><<<grid, kBlock, 0, stream>>>(arena, arena_bytes, stride, lengths, headers, n, \
+                                                                         full_slots)
+    if (stride >= 1024u) {
+        if (nts) CTS_RING_FILL(true, true);
+        else CTS_RING_FILL(false, true);
+    } else {
+        if (nts) CTS_RING_FILL(true, false);
+        else CTS_RING_FILL(false, false);
+    }
+#undef CTS_RING_FILL
     return hipGetLastError();
 }
 

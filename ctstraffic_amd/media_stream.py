@@ -76,6 +76,7 @@ def declare(L: ctypes.CDLL) -> None:
     sigs = {
         "cts_media_stream_split": ([u64, u32, P, u64], u64),
         "cts_media_stream_fill": ([P, P, u64, P, P, u32, P], i32),
+        "cts_media_stream_fill_strided": ([P, P, u64, u32, P, P, u32, P], i32),
         "cts_media_stream_verify": ([P, P, u64, P, u32, P, P, P, P], i32),
         "cts_media_stream_verify_strided": ([P, P, u64, u32, P, u32, P, P, P, P], i32),
         "cts_media_stream_verify_status": ([P, P, u64, P, u32, P, P, P], i32),
@@ -142,6 +143,20 @@ def fill(engine, arena, descs, headers, stream=None) -> None:
                                                                           n * DGRAM_HEADER_DTYPE.itemsize))
     check("cts_media_stream_fill", engine._L.cts_media_stream_fill(engine._h, _ptr(arena), _nbytes(arena), _ptr(descs),
                                                                _ptr(headers), n, _stream(stream)))
+
+
+def fill_strided(engine, arena, stride: int, lengths, headers, stream=None) -> None:
+    """cts_media_stream_fill_strided: datagram i at arena + i * stride, lengths (uint32 device tensor) its bytes,
+    headers (uint8 device tensor of DGRAM_HEADER_DTYPE) its header values."""
+    from .engine import _nbytes, _stream
+
+    n = _nbytes(lengths) // 4
+    if _nbytes(headers) < n * DGRAM_HEADER_DTYPE.itemsize:
+        raise ValueError("headers holds %d bytes, %d datagrams need %d" % (_nbytes(headers), n,
+                                                                          n * DGRAM_HEADER_DTYPE.itemsize))
+    check("cts_media_stream_fill_strided",
+          engine._L.cts_media_stream_fill_strided(engine._h, _ptr(arena), _nbytes(arena), stride, _ptr(lengths),
+                                                  _ptr(headers), n, _stream(stream)))
 
 
 def verify(engine, arena, descs, records=None, results=None, counters=None, stream=None) -> None:

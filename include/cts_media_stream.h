@@ -87,6 +87,17 @@ uint64_t cts_media_stream_split(uint64_t frame_bytes, uint32_t max_datagram, uin
 int cts_media_stream_fill(cts_engine* engine, void* dev_arena, uint64_t arena_bytes, const cts_buf_desc* dev_descs,
                           const cts_datagram_header* dev_headers, uint32_t n, void* stream);
 
+/* Sender over a ring (the layout cts_media_stream_verify_strided reads): datagram i occupies
+ * [i * stride, i * stride + dev_lengths[i]) of the arena and gets the header {0, dev_headers[i]} and the payload
+ * P[0 .. dev_lengths[i] - 26), as cts_media_stream_fill writes it. A length below 26, above the stride or past
+ * the arena leaves its slot unwritten; the bytes between a datagram's end and the next slot are never written.
+ * stride must be a multiple of 16 and >= 32, dev_arena 16-byte aligned, dev_lengths 4-byte and dev_headers
+ * 8-byte aligned (CTS_E_INVALID otherwise). The ring is written as whole 16-byte chunks, one contiguous run per
+ * wave (16 M x 1472 B: 4.3 ms against 7.0 ms through descriptors). */
+int cts_media_stream_fill_strided(cts_engine* engine, void* dev_arena, uint64_t arena_bytes, uint32_t stride,
+                                  const uint32_t* dev_lengths, const cts_datagram_header* dev_headers, uint32_t n,
+                                  void* stream);
+
 /* Receiver: d.length = completed bytes of datagram i at d.byte_offset
  * (skip_head/expected ignored). records[i] gets the parsed header; for DATA
  * datagrams results[i] is the payload verify (skip 26, expected offset 0,

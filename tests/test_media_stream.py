@@ -348,6 +348,121 @@ def _media_stream_verify_vs_oracle(engine, out_shift=0):
     assert engine.read_counters(ctr2) == ectr
 
 
+def _media_stream_fill_expected(arena, descs, hdrs):
+    """What cts_media_stream_fill writes (ctsMediaStreamProtocol.hpp:230-243): per datagram the header {u16 0, i64 seq,
+    i64 qpc, i64 qpf} then P[0 .. length - 26) -- the oracle's payload fill (skip 26, pattern offset 0) plus the
+    header bytes; every other byte of the arena untouched."""
+    d = descs.copy()
+    d["skip_head"] = 26
+    d["expected_pattern_offset"] = 0
+    oracle.fill(arena, d)
+    for i in range(len(descs)):
+        o = int(descs["byte_offset"][i])
+        arena[o:o + 26] = np.frombuffer(b"\0\0" + hdrs[i].tobytes(), dtype=np.uint8)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fill_nt", [0, 1])
+def test_gpu_media_stream_fill_matches_oracle(engine, fill_nt):
+    """cts_media_stream_fill byte for byte: datagrams on 16-byte boundaries (the whole-chunk path, header assembled in
+    registers) and off them (the per-byte-edge path), lengths 26 (header only) to 26 + 1446 and past, partial last
+    chunks, sentinel gaps between datagrams that must stay untouched, random 64-bit header values; plain and
+    nontemporal stores."""
+    import torch
+
+    from ctstraffic_amd import _lib
+
+    rng = np.random.default_rng(0x5E4D + fill_nt)
+    lens = [26, 27, 31, 32, 33, 42, 47, 48, 1471, 1472, 1473, 1488, 2048 + 26, 9000, 26 + 65536 - 7]
+    lens += rng.integers(26, 1600, size=300).tolist()
+    n = len(lens)
+    descs = np.zeros(n, dtype=DESC_DTYPE)
+    off = 0
+    for i, ln in enumerate(lens):
+        mis = 0 if i % 3 else int(rng.integers(1, 16))  # two in three on a 16-byte boundary
+        off = ((off + 15) // 16) * 16 + mis + int(rng.integers(0, 3)) * 16
+        descs[i]["byte_offset"] = off
+        descs[i]["length"] = ln
+        off += ln + int(rng.integers(0, 5))
+    hdrs = np.zeros(n, dtype=DGRAM_HEADER_DTYPE)
+    for f in ("sequence_number", "qpc", "qpf"):
+        hdrs[f] = rng.integers(-(1 << 62), 1 << 62, size=n)
+    arena_bytes = off + 64
+    base = rng.integers(0, 256, size=arena_bytes, dtype=np.uint8)
+    expect = base.copy()
+    _media_stream_fill_expected(expect, descs, hdrs)
+    default = engine.get_attr(_lib.ATTR_FILL_NT)
+    engine.set_attr(_lib.ATTR_FILL_NT, fill_nt)
+    try:
+        a = torch.from_numpy(base.copy()).to("cuda")
+        M.fill(engine, a, _to_dev(descs, torch), _to_dev(hdrs, torch))
+        torch.cuda.synchronize()
+    finally:
+        engine.set_attr(_lib.ATTR_FILL_NT, default)
+    got = a.cpu().numpy()
+    bad = np.nonzero(got != expect)[0]
+    assert bad.size == 0, (bad[:8].tolist(), got[bad[:8]].tolist(), expect[bad[:8]].tolist())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fill_nt", [0, 1])
+@pytest.mark.parametrize("stride", [32, 48, 1024, 1472, 1536, 4096])
+def test_gpu_media_stream_fill_strided_matches_oracle(engine, fill_nt, stride):
+    """cts_media_stream_fill_strided byte for byte against the same datagrams through descriptors: full slots, short
+    datagrams (26 bytes, partial last chunks), lengths that must leave their slot unwritten (below 26, above the
+    stride, past the arena's end), the gap after each datagram untouched; strides below 1024 (per-lane loads) and
+    from 1024 (two headers per round as scalar loads); several waves' runs, so run ends fall inside datagrams."""
+    import torch
+
+    from ctstraffic_amd import _lib
+
+    rng = np.random.default_rng(stride * 3 + fill_nt)
+    n = 3000 if stride < 1024 else 700
+    lens = np.full(n, stride, dtype=np.uint32)
+    pick = rng.random(n)
+    lens[pick < 0.3] = rng.integers(26, stride + 1, size=int(np.sum(pick < 0.3)))
+    lens[(pick >= 0.3) & (pick < 0.35)] = 26
+    lens[(pick >= 0.35) & (pick < 0.38)] = rng.integers(0, 26, size=int(np.sum((pick >= 0.35) & (pick < 0.38))))
+    lens[(pick >= 0.38) & (pick < 0.40)] = stride + 1 + rng.integers(0, 64, size=int(np.sum((pick >= 0.38) & (pick < 0.40))))
+    arena_bytes = n * stride - 5  # the last slot ends past the arena: written only if its length still fits
+    lens[-1] = stride
+    hdrs = np.zeros(n, dtype=DGRAM_HEADER_DTYPE)
+    for f in ("sequence_number", "qpc", "qpf"):
+        hdrs[f] = rng.integers(-(1 << 62), 1 << 62, size=n)
+    base = rng.integers(0, 256, size=arena_bytes, dtype=np.uint8)
+    expect = base.copy()
+    ok = (lens >= 26) & (lens <= stride) & (np.arange(n, dtype=np.uint64) * stride + lens <= arena_bytes)
+    descs = np.zeros(int(ok.sum()), dtype=DESC_DTYPE)
+    descs["byte_offset"] = np.nonzero(ok)[0].astype(np.uint64) * stride
+    descs["length"] = lens[ok]
+    _media_stream_fill_expected(expect, descs, hdrs[ok])
+    default = engine.get_attr(_lib.ATTR_FILL_NT)
+    engine.set_attr(_lib.ATTR_FILL_NT, fill_nt)
+    try:
+        a = torch.from_numpy(base.copy()).to("cuda")
+        M.fill_strided(engine, a, stride, torch.from_numpy(lens).to("cuda"), _to_dev(hdrs, torch))
+        torch.cuda.synchronize()
+    finally:
+        engine.set_attr(_lib.ATTR_FILL_NT, default)
+    got = a.cpu().numpy()
+    bad = np.nonzero(got != expect)[0]
+    assert bad.size == 0, (bad[:8].tolist(), got[bad[:8]].tolist(), expect[bad[:8]].tolist())
+
+
+@pytest.mark.gpu
+def test_gpu_media_stream_fill_strided_refuses_bad_shapes(engine):
+    import torch
+
+    a = torch.zeros(4096 + 16, dtype=torch.uint8, device="cuda")
+    lens = torch.full((2,), 64, dtype=torch.int32, device="cuda")
+    hd = torch.zeros(2 * 24 + 8, dtype=torch.uint8, device="cuda")
+    for stride, arena, ln, h in ((40, a[:4096], lens, hd), (16, a[:4096], lens, hd), (64, a[1:4097], lens, hd),
+                                 (64, a[:4096], lens.view(torch.uint8)[1:5], hd),  # lengths not 4-byte aligned
+                                 (64, a[:4096], lens, hd[4:4 + 48])):  # headers not 8-byte aligned
+        with pytest.raises(Exception):
+            M.fill_strided(engine, arena, stride, ln, h)
+
+
 @pytest.mark.gpu
 def test_gpu_media_stream_end_to_end(engine):
     """Server frames -> datagrams (split) -> GPU fill -> GPU verify -> client accounting -> render."""

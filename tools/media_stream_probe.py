@@ -9,10 +9,21 @@ import json
 import os
 import sys
 
+import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from ctstraffic_amd import Engine, _lib, media_stream as MS, workload as W  # noqa: E402
+from ctstraffic_amd.types import DGRAM_HEADER_DTYPE  # noqa: E402
+
+
+def _with_attr(eng, attr, value, fn):
+    old = eng.get_attr(attr)
+    eng.set_attr(attr, value)
+    try:
+        fn()
+    finally:
+        eng.set_attr(attr, old)
 
 
 def main():
@@ -83,6 +94,20 @@ def main():
                   ("ms+status_ring32", ("ms", 10, ch), lambda a: MS.verify_status(eng, a, d, status=st)),
                   ("ms_strided+status", ("ms", 3, ch),
                    lambda a: MS.verify_strided_status(eng, a, w.max_length, lens, status=st))]
+    # the sender side: the payload fill of the same descriptors (skip 26: header bytes untouched) and the whole-
+    # datagram fill (header + payload, cts_media_stream_fill); "GBps_written" counts the bytes each writes
+    hdr = np.zeros(w.n, dtype=DGRAM_HEADER_DTYPE)
+    hdr["sequence_number"] = np.arange(1, w.n + 1)
+    hdr_d = torch.from_numpy(hdr.view(np.uint8)).cuda()
+    cases += [("fill_payload", ("small", None, None), lambda a: eng.fill(a, d, max_length_hint=w.max_length)),
+              ("ms_fill", ("ms", None, None), lambda a: MS.fill(eng, a, d, hdr_d)),
+              ("ms_fill_strided", ("ms", None, None), lambda a: MS.fill_strided(eng, a, w.max_length, lens, hdr_d)),
+              ("ms_fill_plain", ("ms", None, None), lambda a: _with_attr(eng, _lib.ATTR_FILL_NT, 0,
+                                                                         lambda: MS.fill(eng, a, d, hdr_d))),
+              ("fill_payload_plain", ("small", None, None), lambda a: _with_attr(
+                  eng, _lib.ATTR_FILL_NT, 0, lambda: eng.fill(a, d, max_length_hint=w.max_length)))]
+    written = {"fill_payload": w.verified_bytes(), "ms_fill": w.arena_bytes, "ms_fill_strided": w.arena_bytes, "ms_fill_plain": w.arena_bytes,
+               "fill_payload_plain": w.verified_bytes()}
     cases = [c for c in cases if not only or c[0] in only]
     for r in range(args.rounds):
         for name, v, fn in cases:
@@ -101,7 +126,9 @@ def main():
             us = ea.elapsed_time(eb) * 1e3 / args.launches
             print(json.dumps({"round": r, "case": name, "variant": v, "us": round(us, 1),
                               "GBps_payload": round(w.verified_bytes() / us / 1e3, 1),
-                              "Mdgram_per_s": round(w.n / us, 1)}), flush=True)
+                              "Mdgram_per_s": round(w.n / us, 1),
+                              **({"GBps_written": round(written[name] / us / 1e3, 1)} if name in written else {})}),
+                  flush=True)
     eng.close()
 
 

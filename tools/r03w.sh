@@ -1,0 +1,3 @@
+set -euo pipefail
+OUT=gpurun_out/r03w; mkdir -p $OUT
+timeout -k 10 240 tools/ring_fill_probe 16777216 2 > $OUT/ring_fill.jsonl 2> $OUT/ring_fill.err

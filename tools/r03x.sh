@@ -1,0 +1,10 @@
+set -euo pipefail
+OUT=gpurun_out/r03x; mkdir -p $OUT
+echo "[$(date +%T)] tests" >> $OUT/steps.log
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider \
+  tests/test_media_stream.py -m gpu -k "fill" > $OUT/pytest.log 2>&1
+echo "[$(date +%T)] ring probe" >> $OUT/steps.log
+timeout -k 10 240 tools/ring_fill_probe 16777216 2 > $OUT/ring_fill.jsonl 2> $OUT/ring_fill.err
+echo "[$(date +%T)] bench datagram extras" >> $OUT/steps.log
+timeout -k 10 300 python bench.py --no-cpu-baseline --extras-only datagram --steps 5 --warmup 2 > $OUT/bench_dg.json 2> $OUT/bench_dg.err
+echo "[$(date +%T)] done" >> $OUT/steps.log
