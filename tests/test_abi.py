@@ -258,7 +258,7 @@ def test_product_library_carries_only_the_default_kernels():
     assert wg == ["_ZN3cts16verify_wg_kernelILi2ELb%dELb1ELb0ELb1ELb1ELi1ELi0EEEvPKhmPK12cts_buf_descjP17cts_verify_resultPmPjj"
                   ".kd" % nt for nt in (0, 1)]
     assert not any("verify_wave" in k or "_nb_" in k for k in prod)
-    assert len(prod) == 32 and any("mailbox_kernel" in k for k in prod), sorted(prod)
+    assert len(prod) == 30 and any("mailbox_kernel" in k for k in prod), sorted(prod)
     if os.path.exists(_lib.TUNING_LIB_PATH):
         tun = _kernels(_lib.TUNING_LIB_PATH)
         assert prod < tun and len(tun) > 40
