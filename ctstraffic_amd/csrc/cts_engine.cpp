@@ -531,6 +531,7 @@ int cts_engine_create(int device, cts_engine** out)
     e->geo.small_chunk = env_int("CTS_SMALL_CHUNK", e->geo.small_chunk);
     e->geo.fill_nt = env_int("CTS_FILL_NT", e->geo.fill_nt);
     e->geo.ring_fill_blocks_per_cu = env_int("CTS_RING_FILL_BLOCKS_PER_CU", e->geo.ring_fill_blocks_per_cu);
+    e->geo.fill_batched = env_int("CTS_FILL_BATCHED", e->geo.fill_batched);
     // a variant this build does not compile falls back to the default (the product build has one per path)
     if (!cts::variant_ok(e->geo.verify_variant, cts::kDefaultVerifyVariant, cts_variant_count(kVerifyVariants)))
         e->geo.verify_variant = cts::kDefaultVerifyVariant;

@@ -60,6 +60,8 @@ struct LaunchGeometry {
     int fill_nt = 2;             // fill store policy: 0 plain, 1 nontemporal, 2 by path (plain for the workgroup
                                  // path, nontemporal for datagrams; tools/tune_verify.py --op fill)
     int fill_blocks_per_cu = 1;  // fill grid cap (write-bound; plain stores: 1 measured best, 48.7 vs 49.1-49.4 us)
+    int fill_batched = 1;        // MediaStream descriptor fill from LDS-staged batches (tuning build: 0 = the wave-per-
+                                 // datagram kernel, 2 = the small payload fill batched too; CTS_FILL_BATCHED)
     int ring_fill_blocks_per_cu = 4;  // MediaStream ring fill grid cap (16 M x 1472 B: 4.3 ms at 4, 5.0 at 8;
                                       // CTS_RING_FILL_BLOCKS_PER_CU; tools/ring_fill_probe.hip)
     int verify_variant = kDefaultVerifyVariant;     // see launch_verify (13: variant 11 at U2; 11: variant 10 + in-register exact diff;

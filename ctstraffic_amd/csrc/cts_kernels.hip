@@ -1563,6 +1563,29 @@ __device__ __forceinline__ void fill_whole_rounds(u32x4* p, uint32_t nchunks, ui
 
 // NTS: nontemporal stores. Plain stores measured faster for whole 64 KiB buffers (tools/hbm_read_ceiling
 // writes: 5.51-5.60 TB/s plain vs 4.98-5.35 nt on the same slab shape), nontemporal for datagrams.
+// One buffer's payload (descriptor d: bytes [skip_head, length) at pattern offset expected_pattern_offset) by a team of
+// TEAM lanes, FU stores per lane per whole-span round.
+template <int TEAM, int FU, bool NTS>
+__device__ __forceinline__ void fill_one(uint8_t* arena, uint64_t arena_bytes, const cts_buf_desc& d, uint32_t lane)
+{
+    if (desc_bad(d, arena_bytes)) return;
+    const uint32_t len = d.length - d.skip_head;
+    if (len == 0) return;
+    uint8_t* sp = arena + d.byte_offset + d.skip_head;
+    const uint32_t lo = (uint32_t)((uintptr_t)sp & 15u);
+    const uint32_t nchunks = (uint32_t)(((uint64_t)lo + len + 15u) >> 4);
+    const uint32_t hi_last = (uint32_t)((uint64_t)lo + len - 16ull * (nchunks - 1u));
+    const uint32_t q0 = (d.expected_pattern_offset - lo) & 0xFFFFu;
+    u32x4* p = reinterpret_cast<u32x4*>(sp - lo);
+    // (whole-chunk spans stream buffer stores: 32-bit offsets, so spans >= 2 GiB take the pointer loop)
+    if (__builtin_amdgcn_readfirstlane((lo == 0u && hi_last == 16u && nchunks < kGiantChunks) ? 1u : 0u)) {
+        if (__builtin_amdgcn_readfirstlane(q0 & 1u) == 0u) fill_whole_rounds<TEAM, FU, true, NTS>(p, nchunks, q0, lane);
+        else fill_whole_rounds<TEAM, FU, false, NTS>(p, nchunks, q0, lane);
+        return;
+    }
+    for (uint32_t c = lane; c < nchunks; c += TEAM) fill_chunk<NTS>(p, c, nchunks, q0, lo, hi_last);
+}
+
 template <int TEAM, bool NTS = false>
 __global__ void __launch_bounds__(kBlock) fill_kernel(uint8_t* __restrict__ arena, uint64_t arena_bytes,
                                                       const cts_buf_desc* __restrict__ descs, uint32_t n)
@@ -1580,22 +1603,7 @@ __global__ void __launch_bounds__(kBlock) fill_kernel(uint8_t* __restrict__ aren
     for (; i < n; i = (uint64_t)i + step < n ? i + step : n) {
         const cts_buf_desc d = dn;
         if ((uint64_t)i + step < n) dn = descs[i + step];
-        if (desc_bad(d, arena_bytes)) continue;
-        const uint32_t len = d.length - d.skip_head;
-        if (len == 0) continue;
-        uint8_t* sp = arena + d.byte_offset + d.skip_head;
-        const uint32_t lo = (uint32_t)((uintptr_t)sp & 15u);
-        const uint32_t nchunks = (uint32_t)(((uint64_t)lo + len + 15u) >> 4);
-        const uint32_t hi_last = (uint32_t)((uint64_t)lo + len - 16ull * (nchunks - 1u));
-        const uint32_t q0 = (d.expected_pattern_offset - lo) & 0xFFFFu;
-        u32x4* p = reinterpret_cast<u32x4*>(sp - lo);
-        // (whole-chunk spans stream buffer stores: 32-bit offsets, so spans >= 2 GiB take the pointer loop)
-        if (__builtin_amdgcn_readfirstlane((lo == 0u && hi_last == 16u && nchunks < kGiantChunks) ? 1u : 0u)) {
-            if (__builtin_amdgcn_readfirstlane(q0 & 1u) == 0u) fill_whole_rounds<TEAM, FU, true, NTS>(p, nchunks, q0, lane);
-            else fill_whole_rounds<TEAM, FU, false, NTS>(p, nchunks, q0, lane);
-            continue;
-        }
-        for (uint32_t c = lane; c < nchunks; c += TEAM) fill_chunk<NTS>(p, c, nchunks, q0, lo, hi_last);
+        fill_one<TEAM, FU, NTS>(arena, arena_bytes, d, lane);
     }
 }
 
@@ -2121,61 +2129,115 @@ __global__ void __launch_bounds__(kBlock)
 // What still bounds this kernel is latency, not bytes: each datagram's descriptor and header are loaded before its
 // stores, one datagram per wave at a time (a one-datagram prefetch was slower: 9.3 ms, tools/ring_fill_probe.hip).
 // A ring of datagrams goes through media_stream_fill_ring_kernel instead (cts_media_stream_fill_strided: 4.3 ms).
+// One whole datagram (header {0, seq, qpc, qpf} + payload) of descriptor d by one wave.
+template <bool NTS>
+__device__ __forceinline__ void ms_fill_one(uint8_t* arena, uint64_t arena_bytes, const cts_buf_desc& d, uint64_t seq,
+                                            uint64_t qpc, uint64_t qpf, uint32_t lane)
+{
+    if (d.length < CTS_UDP_DATA_HEADER_LENGTH || d.byte_offset > arena_bytes ||
+        arena_bytes - d.byte_offset < (uint64_t)d.length)
+        return;
+    uint8_t* dg = arena + d.byte_offset;
+    if (__builtin_amdgcn_readfirstlane(((uintptr_t)dg & 15u) == 0u ? 1u : 0u)) {
+        const uint32_t nchunks = (d.length + 15u) >> 4;
+        const uint32_t hi_last = d.length - 16u * (nchunks - 1u);
+        u32x4* p = reinterpret_cast<u32x4*>(dg);
+        for (uint32_t c = lane; c < nchunks; c += 64u) {
+            u32x4 e = expected_chunk((16u * c - CTS_UDP_DATA_HEADER_LENGTH) & 0xFFFFu, 0u);
+            if (c == 0u)  // flag 0 | seq | qpc bytes 0..5
+                e = u32x4{(uint32_t)(seq << 16), (uint32_t)(seq >> 16), (uint32_t)(seq >> 48) | (uint32_t)(qpc << 16),
+                          (uint32_t)(qpc >> 16)};
+            else if (c == 1u)  // qpc bytes 6..7 | qpf | payload bytes 0..5
+                e = u32x4{(uint32_t)(qpc >> 48) | (uint32_t)(qpf << 16), (uint32_t)(qpf >> 16),
+                          (uint32_t)(qpf >> 48) | (e[2] & 0xFFFF0000u), e[3]};
+            if (c == nchunks - 1u && hi_last != 16u) {
+                store_chunk_bytes(reinterpret_cast<uint8_t*>(p + c), e, 0u, hi_last);
+            } else {
+                if constexpr (NTS) __builtin_nontemporal_store(e, p + c);
+                else p[c] = e;
+            }
+        }
+        return;
+    }
+    if (lane < CTS_UDP_DATA_HEADER_LENGTH) {
+        uint8_t b = 0;
+        if (lane >= 2u && lane < 10u) b = (uint8_t)(seq >> (8 * (lane - 2u)));
+        else if (lane >= 10u && lane < 18u) b = (uint8_t)(qpc >> (8 * (lane - 10u)));
+        else if (lane >= 18u) b = (uint8_t)(qpf >> (8 * (lane - 18u)));
+        dg[lane] = b;  // flag bytes 0..1 = c_udpDatagramProtocolHeaderFlagData = 0
+    }
+    const uint32_t len = d.length - CTS_UDP_DATA_HEADER_LENGTH;
+    if (len == 0) return;
+    uint8_t* sp = dg + CTS_UDP_DATA_HEADER_LENGTH;
+    const uint32_t lo = (uint32_t)((uintptr_t)sp & 15u);
+    const uint32_t nchunks = (uint32_t)(((uint64_t)lo + len + 15u) >> 4);
+    const uint32_t hi_last = (uint32_t)((uint64_t)lo + len - 16ull * (nchunks - 1u));
+    const uint32_t q0 = (0u - lo) & 0xFFFFu;
+    u32x4* p = reinterpret_cast<u32x4*>(sp - lo);
+    for (uint32_t c = lane; c < nchunks; c += 64u) fill_chunk<NTS>(p, c, nchunks, q0, lo, hi_last);
+}
+
+// Small buffers through descriptors, batched: each workgroup walks one contiguous range of descriptors in batches of
+// kFillBatch, staged in LDS (and, MS, their MediaStream headers), and each wave fills a contiguous quarter of the
+// batch, one buffer at a time. Nothing is loaded inside the per-buffer loop: the wave-per-buffer kernels wait for a
+// descriptor (a scalar load of a far-away line: ~1 us) before every buffer's stores, which bounded them at
+// 3.4-3.9 TB/s on 16 M x 1472 B (tools/media_stream_probe.py). MS: whole MediaStream datagrams
+// (cts_media_stream_fill); otherwise the payload fill of cts_fill's small-buffer path.
+constexpr uint32_t kFillBatch = kBlock;
+
+template <bool NTS, bool MS>
+__global__ void __launch_bounds__(kBlock)
+    fill_batched_kernel(uint8_t* __restrict__ arena, uint64_t arena_bytes, const cts_buf_desc* __restrict__ descs,
+                        const cts_datagram_header* __restrict__ headers, uint32_t n)
+{
+    constexpr uint32_t WAVES = kBlock / 64;
+    __shared__ cts_buf_desc ds[kFillBatch];
+    __shared__ cts_datagram_header hs[MS ? kFillBatch : 1];
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t per_wg = (uint32_t)(((uint64_t)n + gridDim.x - 1u) / gridDim.x);
+    const uint64_t g0 = (uint64_t)blockIdx.x * per_wg;
+    const uint64_t g1 = g0 + per_wg < n ? g0 + per_wg : n;
+    for (uint64_t d0 = g0; d0 < g1; d0 += kFillBatch) {
+        const uint32_t nb = (uint32_t)(g1 - d0 < kFillBatch ? g1 - d0 : kFillBatch);
+        __syncthreads();  // every wave is done with the previous batch
+        if (threadIdx.x < nb) {
+            ds[threadIdx.x] = descs[d0 + threadIdx.x];
+            if constexpr (MS) hs[threadIdx.x] = headers[d0 + threadIdx.x];
+        }
+        __syncthreads();
+        const uint32_t q = (nb + WAVES - 1u) / WAVES;
+        const uint32_t t1 = (wave + 1u) * q < nb ? (wave + 1u) * q : nb;
+        for (uint32_t t = wave * q; t < t1; ++t) {
+            const cts_buf_desc d = ds[t];
+            if constexpr (MS) {
+                const cts_datagram_header h = hs[t];
+                ms_fill_one<NTS>(arena, arena_bytes, d, (uint64_t)h.sequence_number, (uint64_t)h.qpc, (uint64_t)h.qpf,
+                                 lane);
+            } else {
+                fill_one<64, 2, NTS>(arena, arena_bytes, d, lane);
+            }
+        }
+    }
+}
+
+#if CTS_TUNING
+// the round-3 per-descriptor MediaStream fill (one wave per datagram, grid-strided, descriptor and header loaded
+// before each datagram's stores): 6.8-7.0 ms per 16 M x 1472 B; tuning build (CTS_MS_FILL_BATCHED=0)
 template <bool NTS>
 __global__ void __launch_bounds__(kBlock)
     media_stream_fill_kernel(uint8_t* __restrict__ arena, uint64_t arena_bytes, const cts_buf_desc* __restrict__ descs,
                              const cts_datagram_header* __restrict__ headers, uint32_t n)
 {
-    constexpr int WAVES = kBlock / 64;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    for (uint32_t i = blockIdx.x * WAVES + wave; i < n; i += gridDim.x * WAVES) {
-        const cts_buf_desc d = descs[i];
+    for (uint32_t i = blockIdx.x * (kBlock / 64) + wave; i < n; i += gridDim.x * (kBlock / 64)) {
         const cts_datagram_header h = headers[i];
-        if (d.length < CTS_UDP_DATA_HEADER_LENGTH || d.byte_offset > arena_bytes ||
-            arena_bytes - d.byte_offset < (uint64_t)d.length)
-            continue;
-        uint8_t* dg = arena + d.byte_offset;
-        if (__builtin_amdgcn_readfirstlane(((uintptr_t)dg & 15u) == 0u ? 1u : 0u)) {
-            const uint64_t seq = (uint64_t)h.sequence_number, qpc = (uint64_t)h.qpc, qpf = (uint64_t)h.qpf;
-            const uint32_t nchunks = (d.length + 15u) >> 4;
-            const uint32_t hi_last = d.length - 16u * (nchunks - 1u);
-            u32x4* p = reinterpret_cast<u32x4*>(dg);
-            for (uint32_t c = lane; c < nchunks; c += 64u) {
-                u32x4 e = expected_chunk((16u * c - CTS_UDP_DATA_HEADER_LENGTH) & 0xFFFFu, 0u);
-                if (c == 0u)  // flag 0 | seq | qpc bytes 0..5
-                    e = u32x4{(uint32_t)(seq << 16), (uint32_t)(seq >> 16), (uint32_t)(seq >> 48) | (uint32_t)(qpc << 16),
-                              (uint32_t)(qpc >> 16)};
-                else if (c == 1u)  // qpc bytes 6..7 | qpf | payload bytes 0..5
-                    e = u32x4{(uint32_t)(qpc >> 48) | (uint32_t)(qpf << 16), (uint32_t)(qpf >> 16),
-                              (uint32_t)(qpf >> 48) | (e[2] & 0xFFFF0000u), e[3]};
-                if (c == nchunks - 1u && hi_last != 16u) {
-                    store_chunk_bytes(reinterpret_cast<uint8_t*>(p + c), e, 0u, hi_last);
-                } else {
-                    if constexpr (NTS) __builtin_nontemporal_store(e, p + c);
-                    else p[c] = e;
-                }
-            }
-            continue;
-        }
-        if (lane < CTS_UDP_DATA_HEADER_LENGTH) {
-            uint8_t b = 0;
-            if (lane >= 2u && lane < 10u) b = (uint8_t)((uint64_t)h.sequence_number >> (8 * (lane - 2u)));
-            else if (lane >= 10u && lane < 18u) b = (uint8_t)((uint64_t)h.qpc >> (8 * (lane - 10u)));
-            else if (lane >= 18u) b = (uint8_t)((uint64_t)h.qpf >> (8 * (lane - 18u)));
-            dg[lane] = b;  // flag bytes 0..1 = c_udpDatagramProtocolHeaderFlagData = 0
-        }
-        const uint32_t len = d.length - CTS_UDP_DATA_HEADER_LENGTH;
-        if (len == 0) continue;
-        uint8_t* sp = dg + CTS_UDP_DATA_HEADER_LENGTH;
-        const uint32_t lo = (uint32_t)((uintptr_t)sp & 15u);
-        const uint32_t nchunks = (uint32_t)(((uint64_t)lo + len + 15u) >> 4);
-        const uint32_t hi_last = (uint32_t)((uint64_t)lo + len - 16ull * (nchunks - 1u));
-        const uint32_t q0 = (0u - lo) & 0xFFFFu;
-        u32x4* p = reinterpret_cast<u32x4*>(sp - lo);
-        for (uint32_t c = lane; c < nchunks; c += 64u) fill_chunk<NTS>(p, c, nchunks, q0, lo, hi_last);
+        ms_fill_one<NTS>(arena, arena_bytes, descs[i], (uint64_t)h.sequence_number, (uint64_t)h.qpc, (uint64_t)h.qpf,
+                         lane);
     }
 }
+#endif
 
 // MediaStream sender over a ring (cts_media_stream_fill_strided): datagram i occupies [i * stride, i * stride +
 // lengths[i]) of a 16-byte aligned arena, stride a multiple of 16, so the ring is a flat array of 16-byte chunks and
@@ -2189,8 +2251,9 @@ __global__ void __launch_bounds__(kBlock)
 // in the loop would wait for every store before it; scalar header loads wait for K$ misses at ~1 us each, and every
 // SMEM wait is lgkmcnt(0), so they cannot be prefetched). A round of whole datagrams (the common case) writes its
 // header chunks through two lane selects and checks nothing per lane. Measured on 16 M x 1472 B
-// (tools/ring_fill_probe.hip): scalar per-round header loads 4.4-4.6 ms; the descriptor kernel 7.0 ms; the bare
-// pattern as one span 4.0-4.2 ms.
+// (tools/ring_fill_probe.hip, profiles/r03/fill_ring/): 4.6-4.9 ms (5.1-5.4 TB/s) at 4 workgroups per CU; scalar
+// per-round header loads 4.4-5.8 ms by form; the descriptor fill 5.1-5.4 ms batched, 6.8-9.0 ms wave per datagram; the
+// bare pattern as one span 4.0-4.3 ms.
 constexpr uint32_t kRingBatch = 512;
 
 struct RingHeader {
@@ -2741,6 +2804,14 @@ hipError_t launch_verify_strided(const uint8_t* arena, uint64_t arena_bytes, uin
     return hipGetLastError();
 }
 
+// grid of the batched small-buffer fills: whole batches per workgroup, at most ring_fill_blocks_per_cu per CU
+static inline uint32_t batched_fill_grid(uint32_t n, const LaunchGeometry& geo)
+{
+    const uint64_t cap = (uint64_t)geo.num_cus * (uint64_t)(geo.ring_fill_blocks_per_cu > 0 ? geo.ring_fill_blocks_per_cu : 4);
+    const uint64_t want = ((uint64_t)n + kFillBatch - 1) / kFillBatch;
+    return (uint32_t)(want < cap ? want : cap);
+}
+
 hipError_t launch_fill(uint8_t* arena, uint64_t arena_bytes, const cts_buf_desc* descs, uint32_t n,
                        uint32_t max_length_hint, hipStream_t stream, const LaunchGeometry& geo)
 {
@@ -2750,6 +2821,16 @@ hipError_t launch_fill(uint8_t* arena, uint64_t arena_bytes, const cts_buf_desc*
     // config 2 48.7 vs 51.1 us; nontemporal for datagrams: 1.46 vs 1.68 ms per 4 M; tools/tune_verify.py --op fill)
     const bool nts = geo.fill_nt == 2 ? small : geo.fill_nt != 0;
     const uint32_t sgrid = grid_for(n, kBlock / 64, geo), lgrid = grid_for(n, 1, geo, geo.fill_blocks_per_cu);
+    // (the LDS-batched form of the small path measured slower for payload fills of datagrams: 6.9 vs 6.1-6.8 ms per
+    // 16 M x 1446 B, tools/ring_fill_probe.hip: their first chunk is a partial write either way; tuning build only)
+#if CTS_TUNING
+    if (small && geo.fill_batched == 2) {
+        const uint32_t grid = batched_fill_grid(n, geo);
+        if (nts) fill_batched_kernel<true, false><<<grid, kBlock, 0, stream>>>(arena, arena_bytes, descs, nullptr, n);
+        else fill_batched_kernel<false, false><<<grid, kBlock, 0, stream>>>(arena, arena_bytes, descs, nullptr, n);
+        return hipGetLastError();
+    }
+#endif
     if (nts) {
         if (small) fill_kernel<64, true><<<sgrid, kBlock, 0, stream>>>(arena, arena_bytes, descs, n);
         else fill_kernel<kBlock, true><<<lgrid, kBlock, 0, stream>>>(arena, arena_bytes, descs, n);
@@ -2976,13 +3057,19 @@ hipError_t launch_media_stream_fill(uint8_t* arena, uint64_t arena_bytes, const 
                                    const LaunchGeometry& geo)
 {
     if (n == 0) return hipSuccess;
-    // store policy as cts_fill's datagram path: fill_nt 0 = plain, 1 or 2 (by path) = nontemporal
-    if (geo.fill_nt == 0)
-        media_stream_fill_kernel<false><<<grid_for(n, kBlock / 64, geo), kBlock, 0, stream>>>(arena, arena_bytes, descs,
-                                                                                             headers, n);
-    else
-        media_stream_fill_kernel<true><<<grid_for(n, kBlock / 64, geo), kBlock, 0, stream>>>(arena, arena_bytes, descs,
-                                                                                            headers, n);
+    // store policy: fill_nt 0 or 2 (by path) = plain, 1 = nontemporal (batched: 5.08 ms plain vs 5.37 nt per 16 M x
+    // 1472 B, tools/ring_fill_probe.hip)
+    const bool nts = geo.fill_nt == 1;
+#if CTS_TUNING
+    if (!geo.fill_batched) {
+        if (nts) media_stream_fill_kernel<true><<<grid_for(n, kBlock / 64, geo), kBlock, 0, stream>>>(arena, arena_bytes, descs, headers, n);
+        else media_stream_fill_kernel<false><<<grid_for(n, kBlock / 64, geo), kBlock, 0, stream>>>(arena, arena_bytes, descs, headers, n);
+        return hipGetLastError();
+    }
+#endif
+    const uint32_t grid = batched_fill_grid(n, geo);
+    if (nts) fill_batched_kernel<true, true><<<grid, kBlock, 0, stream>>>(arena, arena_bytes, descs, headers, n);
+    else fill_batched_kernel<false, true><<<grid, kBlock, 0, stream>>>(arena, arena_bytes, descs, headers, n);
     return hipGetLastError();
 }
 

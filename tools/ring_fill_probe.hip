@@ -7,6 +7,7 @@
 //   slab     : the pattern over the same bytes as one span (no datagram structure)
 // nontemporal and plain stores. One JSON line per (case, round). Diagnostic only.
 //   build: make tools/ring_fill_probe     run: tools/ring_fill_probe [datagrams] [rounds]
+#define CTS_TUNING 1  // the round-3 wave-per-buffer fills too
 #include "../ctstraffic_amd/csrc/cts_kernels.hip"
 
 #include <cstdio>
@@ -213,6 +214,10 @@ int main(int argc, char** argv)
         return 1;
     (void)hipMemcpy(dd, d.data(), sizeof(cts_buf_desc) * n, hipMemcpyHostToDevice);
     (void)hipMemcpy(hd, h.data(), sizeof(cts_datagram_header) * n, hipMemcpyHostToDevice);
+    cts_buf_desc* dp = nullptr;  // the payload fill's descriptors (26-byte header skipped, pattern offset 0)
+    for (auto& x : d) x.skip_head = CTS_UDP_DATA_HEADER_LENGTH;
+    if (hipMalloc(&dp, sizeof(cts_buf_desc) * n) != hipSuccess) return 1;
+    (void)hipMemcpy(dp, d.data(), sizeof(cts_buf_desc) * n, hipMemcpyHostToDevice);
     cts::LaunchGeometry geo;
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0) == hipSuccess && cus > 0) geo.num_cus = cus;
@@ -225,9 +230,23 @@ int main(int argc, char** argv)
                             nt, us, (double)b / us / 1e3);
                 std::fflush(stdout);
             };
-            line("product", time_us([&](int it) {
-                     (void)cts::launch_media_stream_fill(arena[it & 1], bytes, dd, hd, n, nullptr, geo);
-                 }, 5), bytes);
+            for (int batched : {0, 1}) {
+                for (int bpc : {4, 8}) {
+                    if (!batched && bpc != 4) continue;
+                    cts::LaunchGeometry g2 = geo;
+                    g2.fill_batched = batched;
+                    g2.ring_fill_blocks_per_cu = bpc;
+                    char name[64];
+                    std::snprintf(name, sizeof name, "product%s_bpc%d", batched ? "_batched" : "_wave", bpc);
+                    line(name, time_us([&](int it) {
+                             (void)cts::launch_media_stream_fill(arena[it & 1], bytes, dd, hd, n, nullptr, g2);
+                         }, 5), bytes);
+                    std::snprintf(name, sizeof name, "payload%s_bpc%d", batched ? "_batched" : "_wave", bpc);
+                    line(name, time_us([&](int it) {
+                             (void)cts::launch_fill(arena[it & 1], bytes, dp, n, len, nullptr, g2);
+                         }, 5), (uint64_t)n * (len - 26u));
+                }
+            }
             for (uint32_t bpc : {4u, 8u, 16u}) {
                 const uint32_t g = (uint32_t)geo.num_cus * bpc, stride = g * 256u;
                 char name[64];
