@@ -43,8 +43,13 @@ WORKLOADS = {
                                                "GPU: 16M x 1472 B datagrams (%d B payload read)" % (DG * 1446),
     "media_stream_verify_quad_kernel[strided][frames]": "config3 MediaStream receive with GPU frame sums, strided "
                                                         "ring: 16M x 1472 B datagrams (%d B payload read)" % (DG * 1446),
+    "fill_batched_kernel": "config3 MediaStream fill through descriptors (cts_media_stream_fill, LDS-batched): 16M x "
+                           "1472 B datagrams (%d B written)" % (DG * 1472),
+    "media_stream_fill_ring_kernel": "config3 MediaStream fill of a datagram ring (cts_media_stream_fill_strided): 16M "
+                                     "x 1472 B datagrams (%d B written)" % (DG * 1472),
 }
-ALGO_BYTES = {"verify_wg_kernel": 268435456, "fill_kernel": 268435456, "verify_quad_kernel": DG * 1446,
+ALGO_BYTES = {"fill_batched_kernel": DG * 1472, "media_stream_fill_ring_kernel": DG * 1472,
+              "verify_wg_kernel": 268435456, "fill_kernel": 268435456, "verify_quad_kernel": DG * 1446,
               "verify_wave_kernel": DG * 1446, "media_stream_verify_quad_kernel": DG * 1446,
               "media_stream_verify_quad_kernel[strided]": DG * 1446, "verify_quad_kernel[strided]": DG * 1446,
               "media_stream_verify_quad_kernel[status]": DG * 1446,
@@ -172,7 +177,7 @@ def main(src, dst):
             e["hbm_read_bytes_per_launch_from_rdreq"] = int(128 * e["TCC_EA0_RDREQ_sum_median"])
         if "WRITE_SIZE_median" in e:
             e["hbm_write_bytes_per_launch"] = int(1024 * e["WRITE_SIZE_median"])
-        main_bytes = e.get("hbm_write_bytes_per_launch") if e["kernel"] == "fill_kernel" else e.get(
+        main_bytes = e.get("hbm_write_bytes_per_launch") if "fill" in e["kernel"] else e.get(
             "hbm_read_bytes_per_launch")
         if main_bytes:
             e["traffic_over_algorithmic"] = round(main_bytes / e["algorithmic_bytes"], 4)
