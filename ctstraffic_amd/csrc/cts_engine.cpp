@@ -771,7 +771,7 @@ int cts_media_stream_fill_strided(cts_engine* e, void* dev_arena, uint64_t arena
     if (n == 0) return CTS_OK;
     if (dev_arena == nullptr || ((uintptr_t)dev_arena & 15u) != 0 || dev_lengths == nullptr ||
         ((uintptr_t)dev_lengths & 3u) != 0 || dev_headers == nullptr || ((uintptr_t)dev_headers & 7u) != 0 ||
-        stride < 32u || (stride & 15u) != 0)
+        stride < 32u || (stride & 15u) != 0 || stride > (1u << 20))
         return CTS_E_INVALID;
     DeviceGuard g(e->device);
     if (!g.ok) return CTS_E_HIP;

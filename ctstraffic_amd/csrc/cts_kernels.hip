@@ -3078,7 +3078,9 @@ hipError_t launch_media_stream_fill_strided(uint8_t* arena, uint64_t arena_bytes
                                            const LaunchGeometry& geo)
 {
     if (n == 0) return hipSuccess;
-    if ((stride & 15u) != 0u || stride < 32u || ((uintptr_t)arena & 15u) != 0u) return hipErrorInvalidValue;
+    // (stride <= 1 MiB keeps a batch's chunk count, 512 x stride / 16, in 32 bits; a UDP datagram is < 64 KiB)
+    if ((stride & 15u) != 0u || stride < 32u || stride > (1u << 20) || ((uintptr_t)arena & 15u) != 0u)
+        return hipErrorInvalidValue;
     const uint64_t cap = (uint64_t)geo.num_cus * (uint64_t)(geo.ring_fill_blocks_per_cu > 0 ? geo.ring_fill_blocks_per_cu : 4);
     // every workgroup gets at least a batch's worth of datagrams, or the whole ring
     const uint64_t want = ((uint64_t)n + kRingBatch - 1) / kRingBatch;

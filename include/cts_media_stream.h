@@ -93,7 +93,7 @@ int cts_media_stream_fill(cts_engine* engine, void* dev_arena, uint64_t arena_by
  * [i * stride, i * stride + dev_lengths[i]) of the arena and gets the header {0, dev_headers[i]} and the payload
  * P[0 .. dev_lengths[i] - 26), as cts_media_stream_fill writes it. A length below 26, above the stride or past
  * the arena leaves its slot unwritten; the bytes between a datagram's end and the next slot are never written.
- * stride must be a multiple of 16 and >= 32, dev_arena 16-byte aligned, dev_lengths 4-byte and dev_headers
+ * stride must be a multiple of 16 in [32, 1 MiB], dev_arena 16-byte aligned, dev_lengths 4-byte and dev_headers
  * 8-byte aligned (CTS_E_INVALID otherwise). The ring is written as whole 16-byte chunks, one contiguous run per
  * wave (16 M x 1472 B: 4.6-4.9 ms against 5.1-5.4 ms through descriptors). */
 int cts_media_stream_fill_strided(cts_engine* engine, void* dev_arena, uint64_t arena_bytes, uint32_t stride,

@@ -457,6 +457,7 @@ def test_gpu_media_stream_fill_strided_refuses_bad_shapes(engine):
     lens = torch.full((2,), 64, dtype=torch.int32, device="cuda")
     hd = torch.zeros(2 * 24 + 8, dtype=torch.uint8, device="cuda")
     for stride, arena, ln, h in ((40, a[:4096], lens, hd), (16, a[:4096], lens, hd), (64, a[1:4097], lens, hd),
+                                 ((1 << 20) + 16, a[:4096], lens, hd),  # above 1 MiB
                                  (64, a[:4096], lens.view(torch.uint8)[1:5], hd),  # lengths not 4-byte aligned
                                  (64, a[:4096], lens, hd[4:4 + 48])):  # headers not 8-byte aligned
         with pytest.raises(Exception):
