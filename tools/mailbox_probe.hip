@@ -9,7 +9,17 @@
 #include <atomic>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+
+#define HIP_OK(x)                                                                                        \
+    do {                                                                                                 \
+        const hipError_t e_ = (x);                                                                       \
+        if (e_ != hipSuccess) {                                                                          \
+            std::fprintf(stderr, "%s:%d: %s\n", __FILE__, __LINE__, hipGetErrorString(e_));              \
+            std::exit(1);                                                                                \
+        }                                                                                                \
+    } while (0)
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -88,15 +98,15 @@ template <int AUX>
 static void bw(const char* name, const uint8_t* d, uint64_t bytes, uint32_t* sink)
 {
     hipEvent_t a, b;
-    hipEventCreate(&a);
-    hipEventCreate(&b);
+    HIP_OK(hipEventCreate(&a));
+    HIP_OK(hipEventCreate(&b));
     bw_kernel<AUX><<<1024, 256>>>(d, bytes, sink);
-    hipEventRecord(a);
+    HIP_OK(hipEventRecord(a));
     for (int i = 0; i < 5; ++i) bw_kernel<AUX><<<1024, 256>>>(d, bytes, sink);
-    hipEventRecord(b);
-    hipEventSynchronize(b);
+    HIP_OK(hipEventRecord(b));
+    HIP_OK(hipEventSynchronize(b));
     float ms = 0;
-    hipEventElapsedTime(&ms, a, b);
+    HIP_OK(hipEventElapsedTime(&ms, a, b));
     std::printf("{\"probe\": \"host_read_bw\", \"policy\": \"%s\", \"GBps\": %.2f}\n", name, 5.0 * bytes / (ms * 1e6));
     std::fflush(stdout);
 }
@@ -120,9 +130,9 @@ int main()
     std::memset(hdata, 1, 1 << 20);
     uint64_t *dseq, *dack;
     uint8_t* ddata;
-    hipHostGetDevicePointer((void**)&dseq, hseq, 0);
-    hipHostGetDevicePointer((void**)&dack, hack, 0);
-    hipHostGetDevicePointer((void**)&ddata, hdata, 0);
+    HIP_OK(hipHostGetDevicePointer((void**)&dseq, hseq, 0));
+    HIP_OK(hipHostGetDevicePointer((void**)&dack, hack, 0));
+    HIP_OK(hipHostGetDevicePointer((void**)&ddata, hdata, 0));
     // (0) bandwidth by load policy over 256 MiB of pinned (non-coherent, like a recv container) and coherent memory
     {
         uint8_t *big = nullptr, *dbig = nullptr, *bigc = nullptr, *dbigc = nullptr;
@@ -132,8 +142,8 @@ int main()
             hipHostMalloc((void**)&bigc, B, fl) == hipSuccess && hipMalloc((void**)&sink, 64) == hipSuccess) {
             std::memset(big, 3, B);
             std::memset(bigc, 3, B);
-            hipHostGetDevicePointer((void**)&dbig, big, 0);
-            hipHostGetDevicePointer((void**)&dbigc, bigc, 0);
+            HIP_OK(hipHostGetDevicePointer((void**)&dbig, big, 0));
+            HIP_OK(hipHostGetDevicePointer((void**)&dbigc, bigc, 0));
             bw<0>("default", dbig, B, sink);
             bw<2>("nt", dbig, B, sink);
             bw<16>("sc1", dbig, B, sink);
@@ -141,16 +151,16 @@ int main()
             bw<17>("sc0_sc1", dbig, B, sink);
             bw<0>("coherent_default", dbigc, B, sink);
             bw<17>("coherent_sc0_sc1", dbigc, B, sink);
-            hipHostFree(big);
-            hipHostFree(bigc);
-            hipFree(sink);
+            HIP_OK(hipHostFree(big));
+            HIP_OK(hipHostFree(bigc));
+            HIP_OK(hipFree(sink));
         }
     }
     // (1) dependent load chain
     for (int n : {100, 1000}) {
         chain_kernel<<<1, 64>>>(dseq, n, dout);
         uint64_t h[2];
-        hipMemcpy(h, dout, 16, hipMemcpyDeviceToHost);
+        HIP_OK(hipMemcpy(h, dout, 16, hipMemcpyDeviceToHost));
         std::printf("{\"probe\": \"dependent_16B_sys_load\", \"loads\": %d, \"us_per_load\": %.3f}\n", n, h[0] / 100.0 / n);
     }
     // (2)/(3) ping-pong
@@ -161,7 +171,7 @@ int main()
             std::memset(hack, 0, 64 * 16);
             __atomic_store_n(hseq, 0ull, __ATOMIC_SEQ_CST);
             hipStream_t s;
-            hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+            HIP_OK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
             pingpong_kernel<<<P, 256, 0, s>>>(dseq, dack, ddata, bytes, iters);
             double t0 = 0;
             bool ok = true;
@@ -180,8 +190,8 @@ int main()
             if (!ok) {  // let the grid finish: feed it every remaining ticket
                 __atomic_store_n(hseq, (uint64_t)iters, __ATOMIC_RELEASE);
             }
-            hipStreamSynchronize(s);
-            hipStreamDestroy(s);
+            HIP_OK(hipStreamSynchronize(s));
+            HIP_OK(hipStreamDestroy(s));
             std::printf("{\"probe\": \"pingpong\", \"bytes\": %u, \"workgroups\": %u, \"us_per_round\": %.3f, \"ok\": %d}\n",
                         bytes, P, (t1 - t0) / (iters - 100), ok ? 1 : 0);
             std::fflush(stdout);
@@ -197,7 +207,7 @@ int main()
                 std::memset(hack, 0, 64 * 16);
                 for (uint32_t b = 0; b < P; ++b) __atomic_store_n(hseq + b * seq_words, 0ull, __ATOMIC_SEQ_CST);
                 hipStream_t s;
-                hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+                HIP_OK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
                 pingpong_kernel<<<P, 256, 0, s>>>(dseq, dack, ddata, bytes, iters, seq_words, ack_words);
                 double t0 = 0;
                 bool ok = true;
@@ -216,8 +226,8 @@ int main()
                 const double t1 = now_us();
                 if (!ok)
                     for (uint32_t b = 0; b < P; ++b) __atomic_store_n(hseq + b * seq_words, (uint64_t)iters, __ATOMIC_RELEASE);
-                hipStreamSynchronize(s);
-                hipStreamDestroy(s);
+                HIP_OK(hipStreamSynchronize(s));
+                HIP_OK(hipStreamDestroy(s));
                 std::printf("{\"probe\": \"pingpong_lines\", \"bytes\": %u, \"workgroups\": %u, \"seq_line_per_wg\": %d, "
                             "\"ack_line_per_wg\": %d, \"us_per_round\": %.3f, \"ok\": %d}\n",
                             bytes, P, seq_words ? 1 : 0, ack_words == 8 ? 1 : 0, (t1 - t0) / (iters - 100), ok ? 1 : 0);
@@ -249,7 +259,7 @@ int main()
                 std::memset(hack, 0, 64 * 16);
                 __atomic_store_n(hv, 0ull, __ATOMIC_SEQ_CST);
                 hipStream_t s;
-                hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+                HIP_OK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
                 pingpong_kernel<<<P, 256, 0, s>>>(vseq, dack, ddata, bytes, iters);
                 double t0 = 0;
                 bool ok = true;
@@ -266,15 +276,15 @@ int main()
                 }
                 const double t1 = now_us();
                 if (!ok) __atomic_store_n(hv, (uint64_t)iters, __ATOMIC_SEQ_CST);
-                hipStreamSynchronize(s);
-                hipStreamDestroy(s);
+                HIP_OK(hipStreamSynchronize(s));
+                HIP_OK(hipStreamDestroy(s));
                 std::printf("{\"probe\": \"pingpong_vram\", \"alloc\": \"%s\", \"bytes\": %u, \"workgroups\": %u, "
                             "\"us_per_round\": %.3f, \"ok\": %d}\n",
                             fname, bytes, P, (t1 - t0) / (iters - 100), ok ? 1 : 0);
                 std::fflush(stdout);
                 if (!ok) return 2;
             }
-        hipFree(vseq);
+        HIP_OK(hipFree(vseq));
     }
     return 0;
 }
