@@ -662,8 +662,11 @@ __device__ __forceinline__ void flush_staged_results(const cts_verify_result* st
 // DEFER = R > 0: per-buffer result records are staged in LDS and written R at a time by wave 0 (and
 // at the end), so the read stream sees a write every R buffers instead of every buffer (a read stream
 // slows with the frequency of the writes mixed into it: tools/rw_mix_probe.hip).
+// UT > 0 (tuning): a workgroup's LAST buffer streams with UT loads per lane per round instead of U, so
+// the workgroups still running once others have finished keep more bytes in flight (the launch's
+// finishing window, DESIGN.md §3 "Where a 256 MiB launch's last few percent go").
 template <int U, bool NT, bool SPLIT = false, bool SCTR = false, bool WHOLE = false, bool XD = false, int WIN = 1,
-          int DEFER = 0>
+          int DEFER = 0, int UT = 0>
 __global__ void __launch_bounds__(kBlock, (U <= 8 ? 8 : 4))
     verify_wg_kernel(const uint8_t* __restrict__ arena, uint64_t arena_bytes, const cts_buf_desc* __restrict__ descs,
                      uint32_t n, cts_verify_result* __restrict__ results, uint64_t* __restrict__ counters,
@@ -722,7 +725,10 @@ __global__ void __launch_bounds__(kBlock, (U <= 8 ? 8 : 4))
             if (dirty) block_reduce_mismatch(first, count);
         } else if (XD && __builtin_amdgcn_readfirstlane(span_whole_lines(s) ? 1u : 0u)) {
             // whole-line span, exact diff in registers: only the reduction is left
-            scan_whole_exact<kBlock, U, NT, SPLIT>(s, lane, first, count);
+            if (UT > 0 && (uint64_t)i + step >= end)
+                scan_whole_exact<kBlock, (UT > 0 ? UT : U), NT, SPLIT>(s, lane, first, count);
+            else
+                scan_whole_exact<kBlock, U, NT, SPLIT>(s, lane, first, count);
             dirty = __builtin_amdgcn_readfirstlane(__syncthreads_or(first != kNone)) != 0;
             if (dirty) block_reduce_mismatch(first, count);
         } else {
@@ -2499,6 +2505,8 @@ static void launch_verify_nt(const uint8_t* arena, uint64_t arena_bytes, const c
         case 16: verify_wg_kernel<2, NT, true, false, true, true, 4><<<grid_win(n, 4, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 17: verify_wg_kernel<2, NT, true, false, true, true, 8><<<grid_win(n, 8, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 18: verify_wg_kernel<2, NT, true, false, true, true, 1, 16><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
+        case 19: verify_wg_kernel<2, NT, true, false, true, true, 1, 0, 4><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
+        case 20: verify_wg_kernel<2, NT, true, false, true, true, 1, 0, 8><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 7: verify_wg_kernel<4, NT, true><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 1: verify_wg_kernel<4, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 2: verify_wg_kernel<16, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
