@@ -25,10 +25,15 @@ DEVICE_VERIFY := ctstraffic_amd/build/device_verify
 TOOLS := tools/hbm_read_ceiling tools/verify_ablation tools/mailbox_probe tools/rw_mix_probe tools/write_shape_probe tools/fill_bisect tools/fill_abi_probe tools/mailbox_bisect tools/ring_fill_probe
 
 SYNC_PROBE := tools/sync_probe
+BENCH_MULTI := tools/libcts_bench_multi.so
 
-all: $(ENGINE_SO) $(TUNING_SO) oracle $(DEVICE_VERIFY) $(TOOLS) $(SYNC_PROBE)
+all: $(ENGINE_SO) $(TUNING_SO) oracle $(DEVICE_VERIFY) $(TOOLS) $(SYNC_PROBE) $(BENCH_MULTI)
 
 tuning: $(TUNING_SO)
+
+# bench.py's single-process leg (--engines N): the timed launches from one native thread per GPU
+$(BENCH_MULTI): tools/bench_multi.cpp $(ENGINE_SO) include/cts_engine.h
+	$(HIPCC) -O2 -std=c++17 -fPIC -shared -Iinclude $< -o $@ -Lctstraffic_amd -lcts_engine -Wl,-rpath,'$$ORIGIN/../ctstraffic_amd' -lpthread
 
 # SYNC-mode (per-completion) verify latency probe against the C ABI
 $(SYNC_PROBE): tools/sync_probe.cpp $(ENGINE_SO) include/cts_engine.h

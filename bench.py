@@ -29,6 +29,7 @@ process) and puts both into the same line. Rank 0 prints ONE JSON line.
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import socket
@@ -63,6 +64,13 @@ def parse():
                    help="single-process multi-GPU leg (the ctsTraffic process model): N engines on GPUs 0..N-1 in "
                         "this one process, one host thread and stream set per GPU, connections by cts_shard_of, "
                         "counters folded on the host by cts_counters_read_multi (0 = off)")
+    p.add_argument("--launcher", choices=["native", "python"], default="python",
+                   help="who issues the headline's launches: python = one ctypes cts_verify call per launch; native = "
+                        "cts_verify called from C++ (tools/bench_multi.cpp). Measured the same (the host runs ahead "
+                        "either way: profiles/r03/launcher_ab/); the single-process leg always launches natively")
+    p.add_argument("--engines-same-gpu", action="store_true",
+                   help="--engines N with every engine on GPU 0: a rehearsal of the single-process code path on a "
+                        "one-GPU box (the line then says n_gpus 1)")
     p.add_argument("--graph", action="store_true", help="replay the timed steps from a HIP graph (measured: no gain; "
                    "implies --pipeline-streams 1)")
     p.add_argument("--pipeline-streams", type=int, default=2,
@@ -300,8 +308,30 @@ def main():
                 B.launch(i, stream)
         torch.cuda.synchronize()
 
+    # pipelined steps: launch i on engine stream i mod S (independent arenas; the counter block takes
+    # device atomics from every stream), then `stream` waits for all S before anything reads it
+    S = 1 if graph is not None else max(1, args.pipeline_streams)
+    pipe = [torch.cuda.ExternalStream(engine.stream_create(), device=dev) for _ in range(S)] if S > 1 else []
+
+    # --launcher native: the launches go through cts_verify from native code (tools/bench_multi.cpp, in
+    # this thread), as ctsTraffic's completion threads call VerifyBuffer; python: one ctypes call per launch
+    native = args.launcher == "native" and graph is None
+    if native:
+        NL = _bench_multi_lib()
+        w_ser, keep_ser = _bench_work(B, engine, gpu, [stream.cuda_stream])
+        w_pipe, keep_pipe = _bench_work(B, engine, gpu, [ps.cuda_stream for ps in pipe] or [stream.cuda_stream])
+        nt0, nt1, nts = (ctypes.c_double * 1)(), (ctypes.c_double * 1)(), ctypes.c_double()
+
+        def native_launches(w, k):
+            rc = NL.cts_bench_run_multi(ctypes.byref(w), 1, k * R, nt0, nt1, ctypes.byref(nts), 0)
+            if rc != 0:
+                raise RuntimeError("cts_bench_run_multi failed: %d" % rc)
+
     def run_steps(k):
         """k steps (k rotations = k*R launches) on `stream` (graph: one replay per step)."""
+        if native:
+            native_launches(w_ser, k)
+            return
         with torch.cuda.stream(stream):
             if graph is not None:
                 for _ in range(k):
@@ -309,11 +339,6 @@ def main():
                 return
             for i in range(k * R):
                 B.launch(i, stream)
-
-    # pipelined steps: launch i on engine stream i mod S (independent arenas; the counter block takes
-    # device atomics from every stream), then `stream` waits for all S before anything reads it
-    S = 1 if graph is not None else max(1, args.pipeline_streams)
-    pipe = [torch.cuda.ExternalStream(engine.stream_create(), device=dev) for _ in range(S)] if S > 1 else []
 
     def run_pipelined(k):
         if not pipe:
@@ -323,8 +348,11 @@ def main():
         start.record(stream)
         for ps in pipe:
             ps.wait_event(start)
-        for i in range(k * R):
-            B.launch(i, pipe[i % S].cuda_stream)
+        if native:
+            native_launches(w_pipe, k)
+        else:
+            for i in range(k * R):
+                B.launch(i, pipe[i % S].cuda_stream)
         for ps in pipe:
             ev = torch.cuda.Event()
             ev.record(ps)
@@ -469,6 +497,8 @@ def main():
                 "verified_bytes_per_step_per_gpu": bytes_per_step,
                 "arenas_rotated": R,
                 "pipeline_streams": S,
+                "launcher": ("native (cts_verify called from C++, tools/bench_multi.cpp)" if native else
+                             "python (one ctypes cts_verify call per launch)"),
                 "host_numa_node": engine.numa_node() if near else None,
                 "host_cpus_pinned": len(near),
                 "parallelism": "%d rank(s), one config-2 batch of its own connections each, no data-path "
@@ -519,76 +549,107 @@ def main():
         dist.destroy_process_group()
 
 
-def main_engines(args, torch):
-    """The ctsTraffic process model on a node: ONE process, one engine per GPU (cts_engine_create(g)), one host
-    thread and stream set per GPU, connections assigned to GPUs by cts_shard_of, counters folded on the host with
-    cts_counters_read_multi. Each GPU verifies a config-2 batch of its own connections (weak scaling, like the
-    torch.distributed leg); value = all bytes / (wall from the common start to the last GPU's end)."""
-    import threading
+class _BenchGpu(ctypes.Structure):
+    """tools/bench_multi.cpp's cts_bench_gpu: one GPU's batch, outputs and streams."""
+    _fields_ = [("engine", ctypes.c_void_p), ("device", ctypes.c_int), ("arenas", ctypes.c_uint32),
+                ("arena", ctypes.POINTER(ctypes.c_void_p)), ("arena_bytes", ctypes.c_uint64),
+                ("descs", ctypes.c_void_p), ("n", ctypes.c_uint32), ("max_length_hint", ctypes.c_uint32),
+                ("results", ctypes.POINTER(ctypes.c_void_p)), ("counters", ctypes.c_void_p),
+                ("conn_first_fail", ctypes.POINTER(ctypes.c_void_p)), ("n_conns", ctypes.c_uint32),
+                ("streams", ctypes.POINTER(ctypes.c_void_p)), ("nstreams", ctypes.c_uint32)]
 
+
+def _bench_multi_lib():
+    """tools/libcts_bench_multi.so (make): loaded after libcts_engine.so, so its cts_verify is the engine's."""
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools", "libcts_bench_multi.so")
+    if not os.path.exists(path):
+        raise RuntimeError("%s is missing: run make" % path)
+    L = ctypes.CDLL(path)
+    L.cts_bench_run_multi.restype = ctypes.c_int
+    L.cts_bench_run_multi.argtypes = [ctypes.POINTER(_BenchGpu), ctypes.c_uint32, ctypes.c_uint32,
+                                      ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                      ctypes.POINTER(ctypes.c_double), ctypes.c_int]
+    return L
+
+
+def _bench_work(B, engine, device, streams):
+    """One cts_bench_gpu for Batch B on `streams` (raw HIP stream handles), and the ctypes arrays it points into."""
+    R, S = len(B.arenas), len(streams)
+    arena = (ctypes.c_void_p * R)(*[a.data_ptr() for a in B.arenas])
+    res = (ctypes.c_void_p * R)(*[r.data_ptr() for r in B.results])
+    cff = (ctypes.c_void_p * R)(*[c.data_ptr() for c in B.cff])
+    st = (ctypes.c_void_p * S)(*streams)
+    w = _BenchGpu(engine._h.value, device, R, arena, B.arenas[0].numel(), B.descs.data_ptr(), B.w.n, B.w.max_length,
+                  res, B.counters.data_ptr(), cff, B.w.n, st, S)
+    return w, (arena, res, cff, st)
+
+
+def main_engines(args, torch):
+    """The ctsTraffic process model on a node: ONE process, one engine per GPU (cts_engine_create(g)), one native
+    host thread and stream set per GPU (tools/bench_multi.cpp: the launches go through the C ABI from std::threads,
+    as ctsTraffic's completion threads call VerifyBuffer; Python threads would serialise every launch on the GIL),
+    connections assigned to GPUs by cts_shard_of, counters folded on the host with cts_counters_read_multi. Each GPU
+    verifies a config-2 batch of its own connections (weak scaling, like the torch.distributed leg);
+    value = all bytes / (wall from the common start to the last GPU's end).
+    --engines-same-gpu puts every engine on GPU 0 (a rehearsal of the code path on a one-GPU box)."""
     from ctstraffic_amd import Engine, workload as W
     from ctstraffic_amd.engine import counters_read_multi
 
     G = args.engines
-    if G > torch.cuda.device_count():
+    same = args.engines_same_gpu
+    if G > torch.cuda.device_count() and not same:
         print("bench.py: --engines %d but %d GPUs are visible" % (G, torch.cuda.device_count()), file=sys.stderr)
         sys.exit(2)
+    L = _bench_multi_lib()
     R, S, K = max(1, args.arenas), max(1, args.pipeline_streams), args.steps
     # the node's connections (G batches' worth), each on GPU cts_shard_of(conn, G)
     n_conns = args.buffers * G
     conns = np.arange(n_conns, dtype=np.uint32)
     owner = W.shard_of(conns, G)
     ctx = []
+    keep = []  # ctypes arrays the descriptors point into
+    work = (_BenchGpu * G)()
     for g in range(G):
-        torch.cuda.set_device(g)
-        e = Engine(g)
+        dev = 0 if same else g
+        torch.cuda.set_device(dev)
+        e = Engine(dev)
         mine = conns[owner == g]
-        B = Batch(torch, e, W, "cuda:%d" % g, len(mine), R, conn_ids=mine)
+        B = Batch(torch, e, W, "cuda:%d" % dev, len(mine), R, conn_ids=mine)
         streams = [e.stream_create() for _ in range(S)]
         ctx.append((e, B, streams, len(mine)))
+        work[g], k = _bench_work(B, e, dev, streams)
+        keep.append(k)
     for g in range(G):
-        torch.cuda.synchronize(g)
+        torch.cuda.synchronize(0 if same else g)
+    t0, t1, ts = (ctypes.c_double * G)(), (ctypes.c_double * G)(), ctypes.c_double()
 
-    def run(g, k, out=None, bar=None):
-        e, B, streams, _ = ctx[g]
-        torch.cuda.set_device(g)
-        if bar is not None:
-            bar.wait()
-        t0 = time.perf_counter()
-        for i in range(k * R):
-            B.launch(i, streams[i % S])
-        for s in streams:
-            e.stream_synchronize(s)
-        if out is not None:
-            out[g] = (t0, time.perf_counter())
+    def run(k):
+        rc = L.cts_bench_run_multi(work, G, k * R, t0, t1, ctypes.byref(ts), 1)
+        if rc != 0:
+            raise RuntimeError("cts_bench_run_multi failed: %d" % rc)
 
-    for g in range(G):  # warmup
-        run(g, max(args.warmup, 1))
-        ctx[g][0].reset_counters(ctx[g][1].counters)
-    times = [None] * G
-    bar = threading.Barrier(G + 1)
-    th = [threading.Thread(target=run, args=(g, K, times, bar)) for g in range(G)]
-    for t in th:
-        t.start()
-    bar.wait()
-    t_start = time.perf_counter()
-    for t in th:
-        t.join()
-    t_end = max(t[1] for t in times)
-    elapsed = t_end - min(min(t[0] for t in times), t_start)
-    per_gpu = [ctx[g][1].bytes_per_launch * R * K / (times[g][1] - times[g][0]) / GIB for g in range(G)]
+    run(max(args.warmup, 1))
+    for e, B, _, _ in ctx:
+        e.reset_counters(B.counters)
+    for g in range(G):
+        torch.cuda.synchronize(0 if same else g)
+    run(K)
+    elapsed = max(t1) - min(min(t0), ts.value)
+    per_gpu = [ctx[g][1].bytes_per_launch * R * K / (t1[g] - t0[g]) / GIB for g in range(G)]
     folded = counters_read_multi([c[0] for c in ctx], [c[1].counters for c in ctx])
     per = [c[0].read_counters(c[1].counters) for c in ctx]
     total = sum(c[1].bytes_per_launch for c in ctx) * R * K
     exp = {k: sum(c[1].exp_ctr[k] for c in ctx) * K * R for k in ctx[0][1].exp_ctr}
     line = {
-        "metric": METRIC, "value": round(total / elapsed / GIB, 2), "unit": "GiB/s", "n_gpus": G, "steps": K,
-        "warmup": args.warmup, "ms_per_step": round(elapsed / K * 1e3, 4), "higher_is_better": True,
+        "metric": METRIC, "value": round(total / elapsed / GIB, 2), "unit": "GiB/s", "n_gpus": 1 if same else G,
+        "steps": K, "warmup": args.warmup, "ms_per_step": round(elapsed / K * 1e3, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic (as the default leg)",
-        "config": {"workload": "config2 per GPU, single process: %d engines, one host thread + %d streams each, "
-                               "a step = %d launches per GPU" % (G, S, R),
-                   "process_model": "one process, one engine per GPU (the ctsTraffic host model)",
-                   "connections_per_gpu": [c[3] for c in ctx]},
+        "config": {"workload": "config2 per engine, single process: %d engines%s, one native host thread + %d "
+                               "streams each, a step = %d launches per engine"
+                               % (G, " all on GPU 0 (rehearsal)" if same else "", S, R),
+                   "process_model": "one process, one engine per GPU (the ctsTraffic host model); launches from "
+                                    "std::threads through cts_verify (tools/bench_multi.cpp)",
+                   "engines": G, "connections_per_gpu": [c[3] for c in ctx]},
         "per_gpu_GiBps": [round(x, 1) for x in per_gpu],
         "parity": {"folded_counters_match_expected": folded == exp,
                    "fold_equals_sum_of_reads": folded == {k: sum(p[k] for p in per) for k in exp},
