@@ -9,7 +9,8 @@ TASK_NONE, TASK_SEND, TASK_RECV, TASK_GRACEFUL_SHUTDOWN, TASK_HARD_SHUTDOWN, TAS
 (BUFFER_NULL, BUFFER_TCP_CONNECTION_ID, BUFFER_UDP_CONNECTION_ID, BUFFER_COMPLETION_MESSAGE, BUFFER_STATIC,
  BUFFER_DYNAMIC) = range(6)
 IO_CONTINUE, IO_COMPLETED, IO_FAILED = 0, 1, 2
-PATTERN_PUSH, PATTERN_PULL, PATTERN_PUSHPULL, PATTERN_DUPLEX = 1, 2, 3, 4
+PATTERN_PUSH, PATTERN_PULL, PATTERN_PUSHPULL, PATTERN_DUPLEX, PATTERN_MEDIA_STREAM = 1, 2, 3, 4, 5
+MS_TIMER_START, MS_TIMER_RENDER = 0, 1  # CTS_MS_TIMER_*
 PROTOCOL_TCP, PROTOCOL_UDP = 1, 2
 SHUTDOWN_GRACEFUL, SHUTDOWN_HARD = 1, 2
 VERIFY_SYNC, VERIFY_DEFERRED = 0, 1
@@ -72,6 +73,11 @@ class CtsPatternConfig(ctypes.Structure):
         ("tcp_bytes_per_second_period", ctypes.c_int64),
         ("burst_count", ctypes.c_uint32),
         ("burst_delay", ctypes.c_uint32),
+        ("ms_frames_per_second", ctypes.c_uint32),
+        ("ms_datagram_max_size", ctypes.c_uint32),
+        ("ms_buffered_frames", ctypes.c_uint32),
+        ("ms_manual_timers", ctypes.c_uint32),
+        ("ms_stream_length_frames", ctypes.c_int64),
     ]
 
 
@@ -105,7 +111,7 @@ class CtsStatusDetails(ctypes.Structure):
 
 
 assert ctypes.sizeof(CtsTask) == 40
-assert ctypes.sizeof(CtsPatternConfig) == 112
+assert ctypes.sizeof(CtsPatternConfig) == 136
 
 # int (*)(void* ctx, const uint8_t* host_arena, uint64_t arena_bytes, const cts_buf_desc* descs,
 #         uint32_t n, cts_verify_result* results)
@@ -118,6 +124,8 @@ RIO_REGISTER = ctypes.CFUNCTYPE(ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_
 RIO_DEREGISTER = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint64)
 # int64_t (*)(void* ctx): the millisecond clock of send pacing (cts_pattern_clock_set)
 CLOCK_MS = ctypes.CFUNCTYPE(ctypes.c_int64, ctypes.c_void_p)
+# void (*)(void* ctx, const cts_task* task): RegisterCallback (cts_io_pattern_register_callback)
+TASK_CALLBACK = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.POINTER(CtsTask))
 
 
 def declare(L: ctypes.CDLL) -> None:
@@ -144,6 +152,11 @@ def declare(L: ctypes.CDLL) -> None:
         "cts_io_pattern_failure_message": ([P, ctypes.c_char_p, u32], i32),
         "cts_io_pattern_fail_fast_reason": ([P], ctypes.c_char_p),
         "cts_io_pattern_connection_id": ([P], ctypes.c_char_p),
+        "cts_io_pattern_register_callback": ([P, TASK_CALLBACK, P], i32),
+        "cts_io_pattern_media_stream_fire": ([P, ctypes.c_int], i32),
+        "cts_io_pattern_media_stream_timers": ([P, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)],
+                                               i32),
+        "cts_io_pattern_media_stream_stats": ([P, P], i32),
         "cts_io_pattern_state_create": ([ctypes.POINTER(CtsPatternConfig), ctypes.POINTER(P)], i32),
         "cts_io_pattern_state_destroy": ([P], i32),
         "cts_io_pattern_state_get_remaining_transfer": ([P], u64),

@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "cts_media_stream.h"
+#include "cts_media_stream_client.hpp"
 #include "cts_pattern.h"
 
 namespace {
@@ -211,33 +212,14 @@ int complete_datagrams(cts_media_stream_client* c, uint32_t n, At at, int64_t re
         case CTS_DGRAM_UNKNOWN:
         case CTS_DGRAM_BAD_DESC: err = CTS_STATUS_ERROR_NOT_ALL_DATA_TRANSFERRED; break;  // invalid header
         case CTS_DGRAM_ID: break;  // SetConnectionIdFromTask: see cts_media_stream_client_set_connection_id
-        case CTS_DGRAM_DATA: {
+        case CTS_DGRAM_DATA:
             if (!r.pass) {  // VerifyBuffer failed: CorruptedBytes
                 err = CTS_STATUS_ERROR_DATA_DID_NOT_MATCH_BIT_PATTERN;
                 break;
             }
-            c->bits_received += (int64_t)r.completed * 8;
-            g_udp.bits_received.fetch_add((int64_t)r.completed * 8, std::memory_order_relaxed);  // :195-196
-            const int64_t seq = r.seq;
-            if (seq > c->final_frame) {
-                ++c->error_frames;  // an unknown seq number past the final frame
-                g_udp.error_frames.fetch_add(1, std::memory_order_relaxed);  // :201-202
-            } else {
-                const ptrdiff_t slot = c->find(seq);
-                if (slot >= 0) {
-                    Frame& f = c->frames[(size_t)slot];
-                    f.sender_qpc = r.qpc;
-                    f.sender_qpf = r.qpf;
-                    f.receiver_qpc = receiver_qpc;
-                    f.receiver_qpf = receiver_qpf;
-                    f.bytes_received += r.completed;
-                } else {
-                    ++c->error_frames;  // a stale or a future seq number
-                    g_udp.error_frames.fetch_add(1, std::memory_order_relaxed);  // :245-246
-                }
-            }
+            cts::ms_client_apply_data(c, cts::MsDatagram{r.seq, r.qpc, r.qpf, r.completed}, receiver_qpc,
+                                      receiver_qpf);
             break;
-        }
         default: err = CTS_STATUS_ERROR_NOT_ALL_DATA_TRANSFERRED; break;
         }
         if (err != 0) {
@@ -295,24 +277,10 @@ int cts_media_stream_client_render(cts_media_stream_client* c)
 {
     if (c == nullptr) return CTS_E_INVALID;
     if (c->finished) return (int)c->finished_code;
-    ++c->timer_wheel_offset_frames;  // TimerCallback (:470-530)
-    if (c->timer_wheel_offset_frames >= c->initial_buffer_frames && c->frames[c->head].sequence_number <= c->final_frame) {
-        if (!c->received_buffered_frames()) {
-            // "have received nothing from the server": every frame counts as dropped, FatalAbort
-            c->dropped += c->final_frame;
-            g_udp.dropped_frames.fetch_add(c->final_frame, std::memory_order_relaxed);  // :501-502
-            c->finished = true;
-            c->finished_code = 2;
-            c->latch(CTS_STATUS_ERROR_NOT_ALL_DATA_TRANSFERRED);  // CompleteIo(FatalAbort), ctsIOPattern.cpp:385-388
-            return 2;
-        }
-        c->render_frame();
-    }
-    if (c->frames[c->head].sequence_number <= c->final_frame) return 0;
-    c->finished = true;
-    c->finished_code = 1;
-    c->latch(0);  // CompleteIo(Abort) -> SuccessfullyCompleted (:143-150)
-    return 1;
+    const int code = cts::ms_client_tick(c);
+    if (code == 2) c->latch(CTS_STATUS_ERROR_NOT_ALL_DATA_TRANSFERRED);  // CompleteIo(FatalAbort), ctsIOPattern.cpp:385-388
+    if (code == 1) c->latch(0);  // CompleteIo(Abort) -> SuccessfullyCompleted (:143-150)
+    return code;
 }
 
 int cts_media_stream_client_stats(const cts_media_stream_client* c, cts_media_stream_stats* o)
@@ -419,3 +387,55 @@ void cts_udp_status_details_reset(void)
 }
 
 }  // extern "C"
+
+namespace cts {
+
+void ms_client_apply_data(cts_media_stream_client* c, const MsDatagram& d, int64_t receiver_qpc, int64_t receiver_qpf)
+{
+    c->bits_received += (int64_t)d.completed_bytes * 8;
+    g_udp.bits_received.fetch_add((int64_t)d.completed_bytes * 8, std::memory_order_relaxed);  // :195-196
+    if (d.sequence_number > c->final_frame) {
+        ++c->error_frames;  // an unknown seq number past the final frame
+        g_udp.error_frames.fetch_add(1, std::memory_order_relaxed);  // :201-202
+        return;
+    }
+    const ptrdiff_t slot = c->find(d.sequence_number);
+    if (slot < 0) {
+        ++c->error_frames;  // a stale or a future seq number
+        g_udp.error_frames.fetch_add(1, std::memory_order_relaxed);  // :245-246
+        return;
+    }
+    Frame& f = c->frames[(size_t)slot];
+    f.sender_qpc = d.sender_qpc;
+    f.sender_qpf = d.sender_qpf;
+    f.receiver_qpc = receiver_qpc;
+    f.receiver_qpf = receiver_qpf;
+    f.bytes_received += d.completed_bytes;
+}
+
+int ms_client_tick(cts_media_stream_client* c)
+{
+    ++c->timer_wheel_offset_frames;  // TimerCallback (:470-530)
+    if (c->timer_wheel_offset_frames >= c->initial_buffer_frames && c->frames[c->head].sequence_number <= c->final_frame) {
+        if (!c->received_buffered_frames()) {
+            // "have received nothing from the server": every frame counts as dropped, FatalAbort
+            c->dropped += c->final_frame;
+            g_udp.dropped_frames.fetch_add(c->final_frame, std::memory_order_relaxed);  // :501-502
+            c->finished = true;
+            c->finished_code = 2;
+            return 2;
+        }
+        c->render_frame();
+    }
+    if (c->frames[c->head].sequence_number <= c->final_frame) return 0;
+    c->finished = true;
+    c->finished_code = 1;
+    return 1;
+}
+
+uint32_t ms_client_timer_wheel_offset(const cts_media_stream_client* c) { return c->timer_wheel_offset_frames; }
+bool ms_client_received_buffered_frames(const cts_media_stream_client* c) { return c->received_buffered_frames(); }
+bool ms_client_finished(const cts_media_stream_client* c) { return c->finished; }
+void udp_status_add_bits(int64_t bits) { g_udp.bits_received.fetch_add(bits, std::memory_order_relaxed); }
+
+}  // namespace cts

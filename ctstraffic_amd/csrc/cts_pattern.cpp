@@ -6,6 +6,8 @@
 //   PatternState     ctsTraffic/ctsIOPatternState.hpp:57-504 (ctsIoPatternState)
 //   IoPattern        ctsTraffic/ctsIOPattern.cpp:133-743     (ctsIoPattern base)
 //   Push/Pull/...    ctsTraffic/ctsIOPattern.cpp:796-1031    (concrete TCP patterns)
+//   MediaStream      ctsTraffic/ctsIOPattern.cpp:1100-1175   (UDP server)
+//                    ctsTraffic/ctsIOPatternMediaStream.cpp  (UDP client; frame accounting in cts_media_stream.cpp)
 //
 // The two hot-path pieces go to the GPU: the sender buffer is written by the
 // fill kernel (cts_shared_buffer_init) and VerifyBuffer runs the verify kernel
@@ -17,6 +19,7 @@
 #include <array>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -25,9 +28,11 @@
 #include <new>
 #include <random>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "cts_engine.h"
+#include "cts_media_stream_client.hpp"
 #include "cts_pattern.h"
 #include "cts_slices.hpp"
 
@@ -92,6 +97,9 @@ enum class PatternError { NoError, TooManyBytes, TooFewBytes, CorruptedBytes, Er
 
 struct FailFast {
     std::string reason;
+};
+struct DeviceError {  // a verify call failed (HIP / engine status): CompleteIo returns it
+    int rc;
 };
 
 class PatternState {
@@ -354,6 +362,16 @@ struct cts_io_pattern {
 
     cts_pattern_config cfg;
     uint32_t max_buffer_size;
+    // the pattern's critical section (ctsIoPattern::AcquireIoPatternLock, ctsIOPattern.h:405): every C-ABI call and
+    // the MediaStream client's timer callbacks hold it; recursive, as a Windows critical section is, because a
+    // callback may complete the task it hands out (ctsMediaStreamClient.cpp:317-331)
+    mutable std::recursive_mutex mu;
+    cts_task_callback m_callback = nullptr;  // RegisterCallback (ctsIOPattern.h:94-97)
+    void* m_callback_ctx = nullptr;
+    void SendTaskToCallback(const cts_task& t) const  // ctsIOPattern.h:333-339
+    {
+        if (m_callback != nullptr) m_callback(m_callback_ctx, &t);
+    }
     PatternState state;
     std::mt19937_64 rng;
     uint32_t recvCount;
@@ -454,6 +472,15 @@ struct cts_io_pattern {
     // derived-pattern interface (ctsIOPattern.h:187-188)
     virtual cts_task GetNextTaskFromPattern() = 0;
     virtual PatternError CompleteTaskBackToPattern(const cts_task&, uint32_t) = 0;
+    // a completion of t must be verified (and so needs an engine or a hook)
+    virtual bool NeedsVerifier(const cts_task& t) const
+    {
+        return cfg.verify_buffers && t.io_action == CTS_TASK_RECV && t.track_io;
+    }
+    // MediaStream surface (cts_io_pattern_media_stream_*): CTS_E_INVALID for the TCP patterns
+    virtual int FireTimer(int) { return CTS_E_INVALID; }
+    virtual int Timers(int64_t*, int64_t*) { return CTS_E_INVALID; }
+    virtual int UdpStats(cts_media_stream_stats*) { return CTS_E_INVALID; }
 
     uint64_t GetTotalTransfer() const { return state.GetMaxTransfer(); }
     void SetTotalTransfer(uint64_t v) { state.SetMaxTransfer(v); }
@@ -987,9 +1014,9 @@ struct cts_io_pattern {
 
     bool Deferred() const { return cfg.verify_mode == CTS_VERIFY_DEFERRED; }
 
-    bool VerifyGate(const cts_task& t) const  // ctsIOPattern.cpp:475-479 (TCP checked at create)
+    bool VerifyGate(const cts_task& t) const  // ctsIOPattern.cpp:475-479
     {
-        return cfg.verify_buffers && t.io_action == CTS_TASK_RECV && t.track_io;
+        return cfg.protocol == CTS_PROTOCOL_TCP && cfg.verify_buffers && t.io_action == CTS_TASK_RECV && t.track_io;
     }
 
     int CompleteIo(const cts_task& t, uint32_t transfer, uint32_t status)  // ctsIOPattern.cpp:364-534
@@ -1221,6 +1248,343 @@ struct Duplex : cts_io_pattern {  // :968-1031
     }
 };
 
+// ---- MediaStream (UDP) patterns -----------------------------------------------------------------
+uint16_t load_u16(const char* p)
+{
+    uint16_t v;
+    std::memcpy(&v, p, sizeof v);
+    return v;
+}
+int64_t load_i64(const char* p)
+{
+    int64_t v;
+    std::memcpy(&v, p, sizeof v);
+    return v;
+}
+
+// ctsIoPatternMediaStreamServer (ctsIOPattern.cpp:1100-1175): the connection-id datagram, then one tracked send
+// of one frame per frame, timed to the frame rate.
+struct MediaStreamServer : cts_io_pattern {
+    MediaStreamServer(const cts_pattern_config& c, uint32_t maxbuf)
+        : cts_io_pattern(c, maxbuf, 1),  // one recv buffer: the connection-id datagram is built in it
+          m_frameSizeBytes(c.buffer_size_low), m_frameRateFps(c.ms_frames_per_second)
+    {
+    }
+    enum class ServerState { NotStarted, IdSent, IoStarted } m_state = ServerState::NotStarted;
+    int64_t m_baseTimeMilliseconds = 0;
+    uint32_t m_frameSizeBytes;
+    uint32_t m_currentFrameRequested = 0;
+    uint32_t m_currentFrameCompleted = 0;
+    uint32_t m_frameRateFps;
+    uint32_t m_currentFrame = 1;
+    int64_t m_bitsReceived = 0;  // m_statistics.m_bitsReceived (counts the bits sent)
+
+    cts_task GetNextTaskFromPattern() override  // :1119-1154
+    {
+        cts_task t{};
+        t.rio_buffer_id = kRioInvalid;
+        switch (m_state) {
+        case ServerState::NotStarted: {
+            // ctsMediaStreamMessage::MakeConnectionIdTask (ctsMediaStreamProtocol.hpp:389-405) over a writable
+            // (recv) buffer of c_udpDatagramConnectionIdHeaderLength bytes
+            t = CreateNewTask(CTS_TASK_RECV, CTS_UDP_CONNECTION_ID_HEADER_LENGTH);
+            if (t.buffer_length != CTS_CONNECTION_ID_LENGTH + CTS_UDP_FLAG_LENGTH)
+                throw FailFast{"MakeConnectionIdTask: the task's buffer length is not the connection-id datagram length"};
+            const uint16_t flag = CTS_UDP_FLAG_ID;
+            std::memcpy(t.buffer, &flag, CTS_UDP_FLAG_LENGTH);
+            std::memcpy(t.buffer + CTS_UDP_FLAG_LENGTH, connection_id, CTS_CONNECTION_ID_LENGTH);
+            t.io_action = CTS_TASK_SEND;
+            t.buffer_type = CTS_BUFFER_UDP_CONNECTION_ID;
+            t.track_io = 0;
+            m_state = ServerState::IdSent;
+            break;
+        }
+        case ServerState::IdSent:
+            m_baseTimeMilliseconds = NowMs();
+            m_state = ServerState::IoStarted;
+            [[fallthrough]];
+        case ServerState::IoStarted:
+            if (m_currentFrameRequested < m_frameSizeBytes) {
+                t = CreateTrackedTask(CTS_TASK_SEND, m_frameSizeBytes);
+                // the time of this frame relative to now
+                t.time_offset_ms = m_baseTimeMilliseconds + ((int64_t)m_currentFrame * 1000LL / m_frameRateFps) - NowMs();
+                m_currentFrameRequested += t.buffer_length;
+            }
+            break;
+        }
+        return t;
+    }
+
+    PatternError CompleteTaskBackToPattern(const cts_task& t, uint32_t currentTransfer) override  // :1156-1173
+    {
+        if (t.buffer_type != CTS_BUFFER_UDP_CONNECTION_ID) {
+            const int64_t bits = (int64_t)currentTransfer * 8;
+            cts::udp_status_add_bits(bits);
+            m_bitsReceived += bits;
+            m_currentFrameCompleted += currentTransfer;
+            if (m_currentFrameCompleted == m_frameSizeBytes) {
+                ++m_currentFrame;
+                m_currentFrameRequested = 0;
+                m_currentFrameCompleted = 0;
+            }
+        }
+        return PatternError::NoError;
+    }
+
+    int UdpStats(cts_media_stream_stats* o) override
+    {
+        *o = cts_media_stream_stats{};
+        o->bits_received = m_bitsReceived;
+        o->last_error = m_lastError;
+        return CTS_OK;
+    }
+};
+
+// ctsIoPatternMediaStreamClient (ctsIOPatternMediaStream.cpp:46-530): untracked recvs of one datagram each;
+// every data datagram's payload is verified (on the GPU) and booked to its frame in the jitter queue, which
+// the renderer timer drains at the frame rate. The frame accounting is the one cts_media_stream_client_*
+// exports (cts_media_stream.cpp); the pattern adds the recv tasks, the header checks, the verify and the timers.
+struct MediaStreamClient : cts_io_pattern {
+    MediaStreamClient(const cts_pattern_config& c, uint32_t maxbuf)
+        : cts_io_pattern(c, maxbuf, c.pre_post_recvs),
+          m_frameRateMsPerFrame(1000.0 / (double)c.ms_frames_per_second), m_frameSizeBytes(c.buffer_size_low),
+          m_recvNeeded(c.pre_post_recvs), m_maxDatagramSize(c.ms_datagram_max_size), manual(c.ms_manual_timers != 0)
+    {
+    }
+    ~MediaStreamClient() override
+    {
+        {
+            std::lock_guard<std::recursive_mutex> lk(mu);
+            stop = true;
+            start_due = render_due = -1;
+        }
+        cv.notify_all();
+        if (timer_thread.joinable()) timer_thread.join();
+        if (ms != nullptr) (void)cts_media_stream_client_destroy(ms);
+    }
+
+    cts_media_stream_client* ms = nullptr;  // the jitter queue and frame accounting
+    int64_t m_baseTimeMilliseconds = 0;
+    const double m_frameRateMsPerFrame;
+    const uint32_t m_frameSizeBytes;
+    uint32_t m_recvNeeded;
+    const uint32_t m_maxDatagramSize;
+    uint64_t datagrams = 0;  // recv completions handed to CompleteTaskBackToPattern
+    // the two timers (ctsIOPatternMediaStream.cpp:321-364): when each is due on the pattern clock, -1 = not armed
+    const bool manual;
+    int64_t start_due = -1, render_due = -1;
+    bool stop = false;
+    std::condition_variable_any cv;
+    std::thread timer_thread;
+
+    bool NeedsVerifier(const cts_task& t) const override  // every recv is a datagram to verify
+    {
+        return cfg.verify_buffers && t.io_action == CTS_TASK_RECV;
+    }
+
+    // SetNextTimer (:321-349): the renderer's next tick at base + offset frames; armed when more than 2 ms ahead
+    // (always on the initial call)
+    bool SetNextTimer(bool initial)
+    {
+        const int64_t due = m_baseTimeMilliseconds +
+                            (int64_t)((double)cts::ms_client_timer_wheel_offset(ms) * m_frameRateMsPerFrame);
+        if (!initial && due - NowMs() <= 2) return false;
+        render_due = due;
+        cv.notify_all();
+        return true;
+    }
+    void SetNextStartTimer()  // :351-364
+    {
+        start_due = NowMs() + (int64_t)m_frameRateMsPerFrame + 500;
+        cv.notify_all();
+    }
+
+    // StartCallback (:440-468): re-send START until the first datagram arrived
+    void StartTimer()
+    {
+        static char kStart[] = "START";
+        if (cts::ms_client_finished(ms)) return;
+        if (!cts::ms_client_received_buffered_frames(ms)) {
+            cts_task t{};
+            t.rio_buffer_id = kRioInvalid;
+            t.io_action = CTS_TASK_SEND;
+            t.track_io = 0;
+            t.buffer = kStart;
+            t.buffer_offset = 0;
+            t.buffer_length = sizeof(kStart) - 1;
+            t.buffer_type = CTS_BUFFER_STATIC;
+            SetNextStartTimer();
+            SendTaskToCallback(t);
+        }
+    }
+    // TimerCallback (:470-530): render frames until the next tick lies in the future
+    void RenderTimer()
+    {
+        bool scheduled = false;
+        while (!scheduled) {
+            if (cts::ms_client_finished(ms)) return;
+            const int code = cts::ms_client_tick(ms);
+            if (code != 0) {
+                cts_task t{};
+                t.rio_buffer_id = kRioInvalid;
+                t.io_action = code == 2 ? CTS_TASK_FATAL_ABORT : CTS_TASK_ABORT;
+                SendTaskToCallback(t);
+                return;
+            }
+            scheduled = SetNextTimer(false);
+        }
+    }
+
+    void TimerLoop()  // the threadpool timers: run each callback when it is due
+    {
+        std::unique_lock<std::recursive_mutex> lk(mu);
+        while (!stop) {
+            int64_t due = start_due;
+            if (render_due >= 0 && (due < 0 || render_due < due)) due = render_due;
+            if (due < 0) {
+                cv.wait(lk);
+                continue;
+            }
+            const int64_t now = NowMs();
+            if (due > now) {
+                // a bounded wait on the system clock: libstdc++ turns wait_for into pthread_cond_clockwait, which
+                // ThreadSanitizer does not intercept (it then reports the pattern lock as double-locked); the
+                // bound keeps a wall-clock step from stretching a wait
+                cv.wait_until(lk, std::chrono::system_clock::now() + std::chrono::milliseconds(std::min<int64_t>(due - now, 50)));
+                continue;
+            }
+            if (start_due >= 0 && start_due <= now) {
+                start_due = -1;
+                StartTimer();
+            }
+            if (!stop && render_due >= 0 && render_due <= now) {
+                render_due = -1;
+                RenderTimer();
+            }
+        }
+    }
+
+    int FireTimer(int timer) override
+    {
+        if (timer == CTS_MS_TIMER_START) {
+            start_due = -1;
+            StartTimer();
+        } else if (timer == CTS_MS_TIMER_RENDER) {
+            render_due = -1;
+            RenderTimer();
+        } else {
+            return CTS_E_INVALID;
+        }
+        return CTS_OK;
+    }
+    int Timers(int64_t* s, int64_t* r) override
+    {
+        if (s != nullptr) *s = start_due;
+        if (r != nullptr) *r = render_due;
+        return CTS_OK;
+    }
+
+    cts_task GetNextTaskFromPattern() override  // :115-138
+    {
+        if (m_baseTimeMilliseconds == 0) {
+            // start the timers the first time the pattern is used
+            m_baseTimeMilliseconds = NowMs();
+            SetNextStartTimer();
+            (void)SetNextTimer(true);
+            if (!manual && !timer_thread.joinable()) timer_thread = std::thread([this] { TimerLoop(); });
+        }
+        cts_task t{};
+        t.rio_buffer_id = kRioInvalid;
+        if (m_recvNeeded > 0) {
+            // one datagram per recv; a zero where the header's sequence number goes
+            t = CreateNewTask(CTS_TASK_RECV, std::min(m_frameSizeBytes, m_maxDatagramSize));
+            std::memset(t.buffer, 0, sizeof(int64_t));
+            --m_recvNeeded;
+        }
+        return t;
+    }
+
+    PatternError CompleteTaskBackToPattern(const cts_task& t, uint32_t completedBytes) override  // :140-272
+    {
+        if (t.io_action == CTS_TASK_ABORT) {
+            if (!cts::ms_client_finished(ms)) throw FailFast{"processed an Abort before the stream was finished"};
+            return PatternError::SuccessfullyCompleted;
+        }
+        if (t.io_action != CTS_TASK_RECV) return PatternError::NoError;  // a START send
+        const uint64_t index = datagrams++;
+        if (completedBytes == 0) {
+            // the final recv may complete with zero bytes once the sender closed
+            return cts::ms_client_finished(ms) ? PatternError::NoError : Fail(index, PatternError::TooFewBytes);
+        }
+        // ValidateBufferLengthFromTask (ctsMediaStreamProtocol.hpp:284-329); GetProtocolHeaderFromTask reads the
+        // flag at m_buffer itself (:331-334)
+        if (completedBytes < CTS_UDP_FLAG_LENGTH) return Fail(index, PatternError::TooFewBytes);
+        const uint16_t flag = load_u16(t.buffer);
+        if (flag == CTS_UDP_FLAG_DATA) {
+            if (completedBytes < CTS_UDP_DATA_HEADER_LENGTH) return Fail(index, PatternError::TooFewBytes);
+        } else if (flag == CTS_UDP_FLAG_ID) {
+            if (completedBytes < CTS_UDP_CONNECTION_ID_HEADER_LENGTH) return Fail(index, PatternError::TooFewBytes);
+            // SetConnectionIdFromTask (:336-347)
+            std::memcpy(connection_id, t.buffer + t.buffer_offset + CTS_UDP_FLAG_LENGTH, CTS_CONNECTION_ID_LENGTH);
+            ++m_recvNeeded;
+            return PatternError::NoError;
+        } else {
+            return Fail(index, PatternError::TooFewBytes);
+        }
+        // VerifyBuffer of the payload: skip the data header, pattern offset 0 (:185-192)
+        if (cfg.verify_buffers) {
+            const uint32_t payload = completedBytes - CTS_UDP_DATA_HEADER_LENGTH;
+            cts_verify_result r{};
+            r.first_mismatch = payload;
+            r.pass = 1;
+            if (payload > 0) {
+                cts_task vt = t;
+                vt.buffer_offset = CTS_UDP_DATA_HEADER_LENGTH;
+                vt.buffer_length -= CTS_UDP_DATA_HEADER_LENGTH;
+                const int rc = VerifyNow(vt, payload, r);
+                if (rc != CTS_OK) throw DeviceError{rc};
+            }
+            ++buffers_verified;
+            bytes_verified += payload;
+            if (!r.pass) {
+                RecordFailure((uint32_t)index, payload, r, 0);
+                return Fail(index, PatternError::CorruptedBytes);
+            }
+        }
+        // GetSequenceNumberFromTask (buffer + offset + 2) and the sender's QPC / QPF as the client reads them
+        // (m_buffer + 8, + 16: ctsIOPatternMediaStream.cpp:218-219)
+        const cts::MsDatagram d{load_i64(t.buffer + t.buffer_offset + CTS_UDP_FLAG_LENGTH), load_i64(t.buffer + 8),
+                                load_i64(t.buffer + 16), completedBytes};
+        const int64_t qpc = std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                std::chrono::steady_clock::now().time_since_epoch()).count();
+        cts::ms_client_apply_data(ms, d, qpc, 1000000000LL);
+        ++m_recvNeeded;
+        return PatternError::NoError;
+    }
+
+    PatternError Fail(uint64_t index, PatternError e)
+    {
+        if (!udp_failed) {
+            udp_failed = true;
+            fail_datagram = (uint32_t)index;
+        }
+        return e;
+    }
+    bool udp_failed = false;
+    uint32_t fail_datagram = 0;
+
+    int UdpStats(cts_media_stream_stats* o) override
+    {
+        const int rc = cts_media_stream_client_stats(ms, o);
+        if (rc != CTS_OK) return rc;
+        o->datagrams = datagrams;
+        o->last_error = m_lastError;
+        o->fail_datagram = fail_datagram;
+        o->has_failure = udp_failed ? 1u : 0u;
+        return CTS_OK;
+    }
+};
+
 void make_connection_id(char* out)  // ctsStatistics::GenerateConnectionId: a UUID string
 {
     std::random_device rd;
@@ -1304,11 +1668,24 @@ int cts_io_pattern_create(const cts_pattern_config* c, cts_engine* engine, cts_i
 {
     if (c == nullptr || out == nullptr) return CTS_E_INVALID;
     *out = nullptr;
-    if (c->protocol != CTS_PROTOCOL_TCP) return CTS_E_INVALID;  // MediaStream (UDP) patterns: not restated yet
+    const bool media = c->io_pattern == CTS_PATTERN_MEDIA_STREAM;
+    if (c->protocol != (media ? CTS_PROTOCOL_UDP : CTS_PROTOCOL_TCP)) return CTS_E_INVALID;  // UDP is MediaStream only
     if (c->buffer_size_low == 0 || (c->buffer_size_high != 0 && c->buffer_size_high < c->buffer_size_low))
         return CTS_E_INVALID;
     if (c->pre_post_recvs == 0) return CTS_E_INVALID;                         // ctsConfig.cpp:2169-2171
-    if (c->verify_buffers && c->pre_post_recvs > 1) return CTS_E_INVALID;     // ctsConfig.cpp:3440-3446
+    if (!media && c->verify_buffers && c->pre_post_recvs > 1) return CTS_E_INVALID;  // TCP: ctsConfig.cpp:3440-3446
+    if (media) {
+        // MediaStreamSettings::CalculateTransferSize and the buffer override (ctsConfig.h:297-364,
+        // ctsConfig.cpp:3341-3350): the frame is the buffer, the stream is whole frames
+        if (c->buffer_size_high != 0 || c->buffer_size_low < 40 || c->ms_frames_per_second == 0 ||
+            c->ms_stream_length_frames <= 0 || c->ms_stream_length_frames > (int64_t)UINT32_MAX ||
+            c->transfer_size != (uint64_t)c->buffer_size_low * (uint64_t)c->ms_stream_length_frames)
+            return CTS_E_INVALID;
+        if (!c->listening && (c->ms_buffered_frames == 0 || c->ms_datagram_max_size == 0)) return CTS_E_INVALID;
+        // per-datagram (SYNC) verify only; no RIO and no TCP pacing on the MediaStream path
+        if (c->verify_mode != CTS_VERIFY_SYNC || c->registered_io || c->tcp_bytes_per_second != 0 || c->burst_count != 0)
+            return CTS_E_INVALID;
+    }
     if (c->use_shared_buffer && c->verify_buffers) return CTS_E_INVALID;      // ctsIOPattern.cpp:225-227
     if (c->verify_mode != CTS_VERIFY_SYNC && c->verify_mode != CTS_VERIFY_DEFERRED) return CTS_E_INVALID;
     const uint32_t maxbuf = c->buffer_size_high == 0 ? c->buffer_size_low : c->buffer_size_high;  // GetMaxBufferSize
@@ -1327,6 +1704,21 @@ int cts_io_pattern_create(const cts_pattern_config* c, cts_engine* engine, cts_i
             p = new PushPull(*c, maxbuf);
             break;
         case CTS_PATTERN_DUPLEX: p = new Duplex(*c, maxbuf); break;
+        case CTS_PATTERN_MEDIA_STREAM:
+            if (c->listening) {
+                p = new MediaStreamServer(*c, maxbuf);
+            } else {
+                auto* mc = new MediaStreamClient(*c, maxbuf);
+                p = mc;
+                const cts_media_stream_settings st{c->buffer_size_low, c->ms_datagram_max_size, c->ms_frames_per_second,
+                                                   c->ms_buffered_frames, c->ms_stream_length_frames};
+                const int mrc = cts_media_stream_client_create(&st, &mc->ms);
+                if (mrc != CTS_OK) {
+                    delete p;
+                    return mrc;
+                }
+            }
+            break;
         default: return CTS_E_INVALID;
         }
     } catch (const std::bad_alloc&) {
@@ -1362,6 +1754,7 @@ int cts_io_pattern_destroy(cts_io_pattern* p)
 int cts_io_pattern_set_verifier(cts_io_pattern* p, cts_batch_verifier fn, void* ctx)
 {
     if (p == nullptr) return CTS_E_INVALID;
+    std::lock_guard<std::recursive_mutex> lk(p->mu);
     if (!p->queue.empty() || !p->inflight.empty()) return CTS_E_INVALID;
     p->hook = fn;
     p->hook_ctx = ctx;
@@ -1373,6 +1766,7 @@ int cts_io_pattern_initiate_io(cts_io_pattern* p, cts_task* out)
     if (p == nullptr || out == nullptr) return CTS_E_INVALID;
     *out = cts_task{};
     out->rio_buffer_id = CTS_RIO_INVALID_BUFFERID;
+    std::lock_guard<std::recursive_mutex> lk(p->mu);
     if (!p->fail_fast.empty()) return CTS_OK;
     try {
         *out = p->InitiateIo();
@@ -1389,23 +1783,35 @@ int cts_io_pattern_initiate_io(cts_io_pattern* p, cts_task* out)
 int cts_io_pattern_complete_io(cts_io_pattern* p, const cts_task* t, uint32_t current_transfer, uint32_t status)
 {
     if (p == nullptr || t == nullptr) return CTS_E_INVALID;
+    std::lock_guard<std::recursive_mutex> lk(p->mu);
     if (!p->fail_fast.empty()) return CTS_IO_FAILED;
-    if (p->hook == nullptr && p->engine == nullptr && p->cfg.verify_buffers && t->io_action == CTS_TASK_RECV &&
-        t->track_io)
+    if (p->hook == nullptr && p->engine == nullptr && p->NeedsVerifier(*t))
         return CTS_E_INVALID;  // no verifier: the product has no CPU verify path
     try {
         return p->CompleteIo(*t, current_transfer, status);
     } catch (const FailFast& f) {
         latch_fail_fast(p, f);
         return CTS_IO_FAILED;
+    } catch (const DeviceError& d) {
+        return d.rc;
     } catch (const std::bad_alloc&) {
         return CTS_E_NOMEM;
     }
 }
 
-uint32_t cts_io_pattern_last_error(const cts_io_pattern* p) { return p ? p->m_lastError : CTS_STATUS_IO_RUNNING; }
+uint32_t cts_io_pattern_last_error(const cts_io_pattern* p)
+{
+    if (p == nullptr) return CTS_STATUS_IO_RUNNING;
+    std::lock_guard<std::recursive_mutex> lk(p->mu);  // a MediaStream client's timer thread may be completing a task
+    return p->m_lastError;
+}
 
-uint64_t cts_io_pattern_rio_buffer_id_count(const cts_io_pattern* p) { return p ? p->RioBufferIdCount() : 0; }
+uint64_t cts_io_pattern_rio_buffer_id_count(const cts_io_pattern* p)
+{
+    if (p == nullptr) return 0;
+    std::lock_guard<std::recursive_mutex> lk(p->mu);
+    return p->RioBufferIdCount();
+}
 
 int cts_pattern_clock_set(cts_clock_ms_fn fn, void* ctx)
 {
@@ -1429,6 +1835,7 @@ int cts_rio_functions_set(cts_rio_register_buffer_fn register_fn, cts_rio_deregi
 int cts_io_pattern_set_ideal_send_backlog(cts_io_pattern* p, uint32_t bytes)
 {
     if (p == nullptr) return CTS_E_INVALID;
+    std::lock_guard<std::recursive_mutex> lk(p->mu);
     p->state.SetIdealSendBacklog(bytes);
     return CTS_OK;
 }
@@ -1436,6 +1843,7 @@ int cts_io_pattern_set_ideal_send_backlog(cts_io_pattern* p, uint32_t bytes)
 int cts_io_pattern_flush(cts_io_pattern* p)
 {
     if (p == nullptr) return CTS_E_INVALID;
+    std::lock_guard<std::recursive_mutex> lk(p->mu);
     try {
         return p->Flush();
     } catch (const FailFast& f) {
@@ -1447,6 +1855,7 @@ int cts_io_pattern_flush(cts_io_pattern* p)
 int cts_io_pattern_get_stats(const cts_io_pattern* p, cts_pattern_stats* o)
 {
     if (p == nullptr || o == nullptr) return CTS_E_INVALID;
+    std::lock_guard<std::recursive_mutex> lk(p->mu);
     *o = cts_pattern_stats{};
     o->bytes_sent = p->bytes_sent;
     o->bytes_recv = p->bytes_recv;
@@ -1469,7 +1878,9 @@ int cts_io_pattern_get_stats(const cts_io_pattern* p, cts_pattern_stats* o)
 
 int cts_io_pattern_failure_message(const cts_io_pattern* p, char* buf, uint32_t buf_len)
 {
-    if (p == nullptr || !p->has_failure) return 0;
+    if (p == nullptr) return 0;
+    std::lock_guard<std::recursive_mutex> lk(p->mu);
+    if (!p->has_failure) return 0;
     // ctsIOPattern.cpp:761-772: the bytes are `char`, so values >= 0x80 print sign-extended
     // through %x (MSVC: 32-bit unsigned). Pointers are not part of the parity contract.
     char tmp[512];
@@ -1489,10 +1900,47 @@ int cts_io_pattern_failure_message(const cts_io_pattern* p, char* buf, uint32_t 
 
 const char* cts_io_pattern_fail_fast_reason(const cts_io_pattern* p)
 {
-    return (p == nullptr || p->fail_fast.empty()) ? nullptr : p->fail_fast.c_str();
+    if (p == nullptr) return nullptr;
+    std::lock_guard<std::recursive_mutex> lk(p->mu);  // the reason is written once and never changes after
+    return p->fail_fast.empty() ? nullptr : p->fail_fast.c_str();
 }
 
 const char* cts_io_pattern_connection_id(cts_io_pattern* p) { return p ? p->connection_id : nullptr; }
+
+int cts_io_pattern_register_callback(cts_io_pattern* p, cts_task_callback fn, void* ctx)
+{
+    if (p == nullptr) return CTS_E_INVALID;
+    std::lock_guard<std::recursive_mutex> lk(p->mu);
+    p->m_callback = fn;
+    p->m_callback_ctx = fn != nullptr ? ctx : nullptr;
+    return CTS_OK;
+}
+
+int cts_io_pattern_media_stream_fire(cts_io_pattern* p, int timer)
+{
+    if (p == nullptr) return CTS_E_INVALID;
+    std::lock_guard<std::recursive_mutex> lk(p->mu);
+    try {
+        return p->FireTimer(timer);
+    } catch (const FailFast& f) {
+        latch_fail_fast(p, f);
+        return CTS_OK;
+    }
+}
+
+int cts_io_pattern_media_stream_timers(cts_io_pattern* p, int64_t* start_due_ms, int64_t* render_due_ms)
+{
+    if (p == nullptr) return CTS_E_INVALID;
+    std::lock_guard<std::recursive_mutex> lk(p->mu);
+    return p->Timers(start_due_ms, render_due_ms);
+}
+
+int cts_io_pattern_media_stream_stats(cts_io_pattern* p, cts_media_stream_stats* out)
+{
+    if (p == nullptr || out == nullptr) return CTS_E_INVALID;
+    std::lock_guard<std::recursive_mutex> lk(p->mu);
+    return p->UdpStats(out);
+}
 
 }  // extern "C"
 

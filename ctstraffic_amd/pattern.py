@@ -46,11 +46,31 @@ class PatternConfig:
     tcp_bytes_per_second_period: int = 100  # ms per quantum
     burst_count: int = 0  # -burstcount (0 = not set); only without a rate limit (:657-674)
     burst_delay: int = 0  # -burstdelay, ms
+    # MediaStream (io_pattern PATTERN_MEDIA_STREAM, UDP): buffer_size is the frame size and transfer_size must be
+    # buffer_size * ms_stream_length_frames (MediaStreamSettings::CalculateTransferSize, ctsConfig.h:297-364)
+    ms_frames_per_second: int = 0
+    ms_datagram_max_size: int = 1400  # c_udpDatagramMaximumSizeBytes (ctsConfig.cpp:106)
+    ms_buffered_frames: int = 0
+    ms_stream_length_frames: int = 0
+    ms_manual_timers: bool = False  # the caller fires the client's timers (IoPattern.media_stream_fire)
+
+    @classmethod
+    def media_stream(cls, *, listening: bool, frame_size: int, frames_per_second: int, stream_length_frames: int,
+                     buffered_frames: int = 0, datagram_max_size: int = 1400, pre_post_recvs: int = 1, **kw):
+        """A MediaStream server (listening) or client config as ctsConfig derives it for -Protocol:UDP."""
+        return cls(io_pattern=A.PATTERN_MEDIA_STREAM, listening=listening, buffer_size=frame_size,
+                   transfer_size=frame_size * stream_length_frames, ms_frames_per_second=frames_per_second,
+                   ms_stream_length_frames=stream_length_frames, ms_buffered_frames=buffered_frames,
+                   ms_datagram_max_size=datagram_max_size, pre_post_recvs=pre_post_recvs, **kw)
+
+    @property
+    def protocol(self) -> int:
+        return A.PROTOCOL_UDP if self.io_pattern == A.PATTERN_MEDIA_STREAM else A.PROTOCOL_TCP
 
     def to_c(self) -> A.CtsPatternConfig:
         c = A.CtsPatternConfig()
         c.io_pattern = self.io_pattern
-        c.protocol = A.PROTOCOL_TCP
+        c.protocol = self.protocol
         c.listening = int(bool(self.listening))
         c.verify_buffers = int(bool(self.verify_buffers))
         c.use_shared_buffer = int(bool(self.use_shared_buffer))
@@ -71,6 +91,11 @@ class PatternConfig:
         c.tcp_bytes_per_second_period = self.tcp_bytes_per_second_period
         c.burst_count = self.burst_count
         c.burst_delay = self.burst_delay
+        c.ms_frames_per_second = self.ms_frames_per_second
+        c.ms_datagram_max_size = self.ms_datagram_max_size
+        c.ms_buffered_frames = self.ms_buffered_frames
+        c.ms_manual_timers = int(bool(self.ms_manual_timers))
+        c.ms_stream_length_frames = self.ms_stream_length_frames
         return c
 
     @property
@@ -166,6 +191,35 @@ class IoPattern:
 
     def connection_id(self) -> str:
         return lib().cts_io_pattern_connection_id(self._h).decode()
+
+    # ---- MediaStream (PATTERN_MEDIA_STREAM) ------------------------------------------------
+    def RegisterCallback(self, fn) -> None:
+        """ctsIoPattern::RegisterCallback (ctsIOPattern.h:94-97): fn(task) receives the tasks the client's timers
+        hand out (START sends, Abort, FatalAbort); it runs with the pattern's lock held and may CompleteIo them."""
+        if fn is None:
+            self._callback = None
+            check("cts_io_pattern_register_callback", lib().cts_io_pattern_register_callback(self._h, A.TASK_CALLBACK(), None))
+            return
+        self._callback = A.TASK_CALLBACK(lambda _ctx, t: fn(A.CtsTask.from_buffer_copy(t.contents)))
+        check("cts_io_pattern_register_callback", lib().cts_io_pattern_register_callback(self._h, self._callback, None))
+
+    def media_stream_fire(self, timer: int) -> None:
+        """Run the client's StartCallback (MS_TIMER_START) or TimerCallback (MS_TIMER_RENDER) now."""
+        check("cts_io_pattern_media_stream_fire", lib().cts_io_pattern_media_stream_fire(self._h, timer))
+
+    def media_stream_timers(self) -> tuple:
+        """(start_due_ms, render_due_ms) on the pattern clock; -1 = not armed."""
+        a, b = ctypes.c_int64(), ctypes.c_int64()
+        check("cts_io_pattern_media_stream_timers",
+              lib().cts_io_pattern_media_stream_timers(self._h, ctypes.byref(a), ctypes.byref(b)))
+        return a.value, b.value
+
+    def media_stream_stats(self) -> dict:
+        from .media_stream import Stats
+
+        s = Stats()
+        check("cts_io_pattern_media_stream_stats", lib().cts_io_pattern_media_stream_stats(self._h, ctypes.byref(s)))
+        return s.as_dict()
 
     # ---- helpers the tests use to "simulate the wire" ---------------------------
     @staticmethod

@@ -9,6 +9,8 @@
  *   ctsTask     ctsIoPattern::InitiateIo()                               ctsIOPattern.h:143
  *   ctsIoStatus ctsIoPattern::CompleteIo(task, currentTransfer, status)  ctsIOPattern.h:144
  *
+ * (the MediaStream functors likewise: ctsMediaStreamClient.cpp:136-144,268,404,
+ * ctsMediaStreamServerConnectedSocket.cpp:111-133),
  * plus the factory MakeIoPattern (ctsIOPattern.cpp:97-124), GetLastPatternError
  * (ctsIOPattern.h:126-129) and AccessSharedBuffer (ctsIOPattern.cpp:126-131,
  * which the reference's own tests use to simulate the wire). This header
@@ -44,6 +46,7 @@
 #include <stdint.h>
 
 #include "cts_engine.h"
+#include "cts_media_stream.h"
 
 #ifdef __cplusplus
 extern "C" {
@@ -108,7 +111,10 @@ typedef enum cts_io_pattern_type { /* ctsConfig::IoPatternType */
     CTS_PATTERN_PUSH = 1,
     CTS_PATTERN_PULL = 2,
     CTS_PATTERN_PUSHPULL = 3,
-    CTS_PATTERN_DUPLEX = 4
+    CTS_PATTERN_DUPLEX = 4,
+    /* UDP: listening = ctsIoPatternMediaStreamServer (ctsIOPattern.cpp:1100-1175), else
+     * ctsIoPatternMediaStreamClient (ctsIOPatternMediaStream.cpp:46-530), MakeIoPattern :113-118 */
+    CTS_PATTERN_MEDIA_STREAM = 5
 } cts_io_pattern_type;
 
 typedef enum cts_protocol { CTS_PROTOCOL_TCP = 1, CTS_PROTOCOL_UDP = 2 } cts_protocol;
@@ -150,6 +156,16 @@ typedef struct cts_pattern_config {
     int64_t tcp_bytes_per_second_period; /* ->TcpBytesPerSecondPeriod, ms (0 = the reference default, 100) */
     uint32_t burst_count;                /* ->BurstCount (0 = not set); used only without a rate limit */
     uint32_t burst_delay;                /* ->BurstDelay, ms: the offset of every burst_count-th send */
+    /* MediaStream (CTS_PATTERN_MEDIA_STREAM over CTS_PROTOCOL_UDP): ctsConfig::MediaStreamSettings
+     * (ctsConfig.h:284-364). As CalculateTransferSize and the config parser set them (ctsConfig.cpp:1260,
+     * 3341-3350), the frame size is buffer_size_low (buffer_size_high 0, at least 40 bytes) and transfer_size
+     * must be buffer_size_low x ms_stream_length_frames. */
+    uint32_t ms_frames_per_second;       /* FramesPerSecond */
+    uint32_t ms_datagram_max_size;       /* DatagramMaxSize: the client posts recvs of min(frame, this) bytes */
+    uint32_t ms_buffered_frames;         /* BufferedFrames (client) */
+    uint32_t ms_manual_timers;           /* client: 0 = a timer thread fires the start and renderer timers at the
+                                            reference's times; 1 = the caller fires them (cts_io_pattern_media_stream_fire) */
+    int64_t ms_stream_length_frames;     /* StreamLengthFrames */
 } cts_pattern_config;
 
 /* The millisecond clock send pacing reads (ctTimer::snap_qpc_as_msec). NULL restores the default, a
@@ -270,6 +286,39 @@ int cts_io_pattern_failure_message(const cts_io_pattern* pattern, char* buf, uin
 const char* cts_io_pattern_fail_fast_reason(const cts_io_pattern* pattern);
 /* GetConnectionIdentifier(): the 36-char id + NUL (servers generate it). */
 const char* cts_io_pattern_connection_id(cts_io_pattern* pattern);
+
+/* ---- MediaStream patterns (CTS_PATTERN_MEDIA_STREAM) ---------------------------------------------
+ * The server hands out its connection-id datagram (39 bytes: flag 0x1000 + the id, a UDP_CONNECTION_ID send
+ * task) and then one tracked send task of one frame per frame, each with the time offset of its frame
+ * (base + frame * 1000 / fps - now, ctsIOPattern.cpp:1119-1153); ctsMediaStreamServerConnectedSocket splits a
+ * frame task into datagrams (cts_media_stream_split). The client posts untracked recvs of
+ * min(frame, DatagramMaxSize) bytes, parses each completed datagram (ctsMediaStreamProtocol.hpp:284-366) and
+ * verifies a data datagram's payload (offset 26, expected pattern offset 0) on the GPU, per completion,
+ * before booking it to its frame (ctsIOPatternMediaStream.cpp:140-272). Only CTS_VERIFY_SYNC: the batched form
+ * of the datagram receive is cts_media_stream_verify_* with cts_media_stream_client_*. registered_io is refused
+ * (the MediaStream functors use WSARecvFrom / WSASendTo). Every call on a pattern holds the pattern's own
+ * (recursive) lock, as the reference's functors and timer callbacks hold the pattern's critical section.
+ *
+ * RegisterCallback (ctsIOPattern.h:94-97): the client's timer callbacks hand tasks to the functor through it
+ * (SendTaskToCallback, :333-339): a "START" send (5 bytes, untracked, STATIC) every 500 ms + one frame until
+ * a frame arrived, Abort when the stream rendered its final frame, FatalAbort when nothing ever arrived. The
+ * callback runs with the pattern's lock held and may call cts_io_pattern_complete_io on the task (the
+ * reference functor completes Abort / FatalAbort from inside it, ctsMediaStreamClient.cpp:317-331). */
+typedef void (*cts_task_callback)(void* ctx, const cts_task* task);
+int cts_io_pattern_register_callback(cts_io_pattern* pattern, cts_task_callback fn, void* ctx);
+
+/* The client's two threadpool timers (ctsIOPatternMediaStream.cpp:321-364, 440-530). With ms_manual_timers the
+ * caller runs a timer's callback with cts_io_pattern_media_stream_fire (the renderer callback renders frames until
+ * its next time lies more than 2 ms ahead of the pattern clock, cts_pattern_clock_set); otherwise a thread per
+ * client pattern runs them when due. cts_io_pattern_media_stream_timers reads when each is due, on the pattern
+ * clock (-1: not armed). CTS_E_INVALID on a server pattern or any other pattern. */
+#define CTS_MS_TIMER_START 0
+#define CTS_MS_TIMER_RENDER 1
+int cts_io_pattern_media_stream_fire(cts_io_pattern* pattern, int timer);
+int cts_io_pattern_media_stream_timers(cts_io_pattern* pattern, int64_t* start_due_ms, int64_t* render_due_ms);
+/* ctsUdpStatistics of a MediaStream pattern: the client's frame accounting (as cts_media_stream_client_stats),
+ * or for the server the bits it sent (bits_received, the reference's name, ctsIOPattern.cpp:1156-1172). */
+int cts_io_pattern_media_stream_stats(cts_io_pattern* pattern, cts_media_stream_stats* out);
 
 /* ---- ctsIoPatternState on its own (ctsIOPatternState.hpp:51-504) ----------------------------
  * The protocol state machine every pattern above runs on: connection id exchange, in-flight and

@@ -49,7 +49,8 @@ def _build(d, san, driver):
 
 @pytest.mark.parametrize("san", sorted(SAN))
 @pytest.mark.parametrize("driver", ["pattern_replay.cpp", "loopback_stress.cpp", "slices_check.cpp",
-                                    "counters_fold.cpp", "media_stream_client.cpp"])
+                                    "counters_fold.cpp", "media_stream_client.cpp",
+                                    "media_stream_pattern.cpp"])
 def test_host_code_under_sanitizer(san, driver):
     with tempfile.TemporaryDirectory() as d:
         exe = _build(d, san, driver)
