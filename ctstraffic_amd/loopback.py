@@ -101,3 +101,59 @@ def run(connections=8, buffer_size=65536, transfer_size=1 << 30, engine=None, ve
     if sides:
         out["sides"] = [s.as_dict() for s in side_arr]
     return out
+
+
+# ---- MediaStream over loopback UDP (cts_loopback_media_stream_run) --------------------------------------------
+class MediaStreamLoopbackConfig(ctypes.Structure):
+    _fields_ = [("connections", ctypes.c_uint32), ("frame_size_bytes", ctypes.c_uint32),
+                ("frames_per_second", ctypes.c_uint32), ("stream_length_frames", ctypes.c_uint32),
+                ("buffered_frames", ctypes.c_uint32), ("datagram_max_size", ctypes.c_uint32),
+                ("pre_post_recvs", ctypes.c_uint32), ("verify_buffers", ctypes.c_uint32),
+                ("corrupt_connection", ctypes.c_uint32), ("corrupt_datagram", ctypes.c_uint32),
+                ("socket_buffer_bytes", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+
+
+def _media_stream_result_type():
+    from .media_stream import Stats
+
+    class MediaStreamLoopbackResult(ctypes.Structure):
+        _fields_ = [("seconds", ctypes.c_double), ("connections_ok", ctypes.c_uint32),
+                    ("connections_failed", ctypes.c_uint32), ("data_errors", ctypes.c_uint32),
+                    ("reserved", ctypes.c_uint32), ("datagrams_sent", ctypes.c_uint64),
+                    ("datagrams_received", ctypes.c_uint64), ("clients", Stats),
+                    ("recv_cpu_seconds", ctypes.c_double)]
+
+    return MediaStreamLoopbackResult
+
+
+def media_stream_run(connections=2, frame_size=52083, frames_per_second=60, stream_length_frames=60,
+                     buffered_frames=10, datagram_max_size=1400, pre_post_recvs=2, engine=None, verifier=None,
+                     verify=True, corrupt_connection=None, corrupt_datagram=0, socket_buffer_bytes=0) -> dict:
+    """MediaStream over loopback UDP ("-Protocol:UDP -Pattern:MediaStream", README sizing by default: FrameSize
+    52083 B at 60 frames/s): every connection's server streams its frames at the frame rate and its client verifies
+    every datagram's payload (on ``engine`` or through ``verifier``) and renders the frames."""
+    from .pattern import batch_verifier
+
+    R = _media_stream_result_type()
+    L = lib()
+    fn = L.cts_loopback_media_stream_run
+    fn.argtypes = [ctypes.POINTER(MediaStreamLoopbackConfig), ctypes.c_void_p, A.BATCH_VERIFIER, ctypes.c_void_p,
+                   ctypes.POINTER(R)]
+    fn.restype = ctypes.c_int
+    cfg = MediaStreamLoopbackConfig(connections, frame_size, frames_per_second, stream_length_frames,
+                                    buffered_frames, datagram_max_size, pre_post_recvs, int(verify),
+                                    0xFFFFFFFF if corrupt_connection is None else corrupt_connection,
+                                    corrupt_datagram, socket_buffer_bytes, 0)
+    hook = None
+    if verifier is not None:
+        hook = verifier if isinstance(verifier, A.BATCH_VERIFIER) else batch_verifier(verifier)
+    if engine is not None and getattr(engine, "tuning", False):
+        raise ValueError("the loopback feeder drives product engines only")
+    res = R()
+    check("cts_loopback_media_stream_run",
+          fn(ctypes.byref(cfg), None if engine is None else engine._h.value,
+             hook if hook is not None else A.BATCH_VERIFIER(), None, ctypes.byref(res)))
+    d = {f: getattr(res, f) for f, _ in R._fields_ if f not in ("reserved", "clients")}
+    d["clients"] = res.clients.as_dict()
+    d["payload_MBps"] = (res.clients.bits_received / 8 / 1e6 / res.seconds) if res.seconds > 0 else 0.0
+    return d

@@ -97,6 +97,51 @@ int cts_loopback_run_detailed(const cts_loopback_config* cfg, cts_engine* const*
                               cts_batch_verifier hook, void* hook_ctx, cts_loopback_result* out,
                               cts_loopback_side* sides);
 
+/* ---- MediaStream over loopback UDP -----------------------------------------------------------------
+ * The roles of ctsMediaStreamServer + ctsMediaStreamServerConnectedSocket (ctsMediaStreamServer.cpp:510-600,
+ * ctsMediaStreamServerConnectedSocket.cpp:60-140) and ctsMediaStreamClient (ctsMediaStreamClient.cpp:60-420),
+ * played with blocking POSIX UDP sockets over the MediaStream patterns of cts_pattern.h:
+ *   - the client sends START, then its receive thread completes every datagram into the client pattern
+ *     (header checks, payload verify on the GPU, frame accounting) while the pattern's own timer thread resends
+ *     START until data arrives, renders frames at the frame rate and ends the stream with Abort, which the
+ *     registered callback completes;
+ *   - the server waits for START, sends the connection-id datagram, then sends each frame task when its time
+ *     offset comes: the frame split into datagrams (cts_media_stream_split) of {flag 0, sequence number (one per
+ *     frame, from 1), QPC, QPF} + the first bytes of g_senderSharedBuffer, and completes the task.
+ * "-Protocol:UDP -Pattern:MediaStream -BitsPerSecond:.. -FrameRate:.. -StreamLength:.. -BufferDepth:.." over
+ * loopback, host memory and the kernel's UDP stack included. */
+typedef struct cts_media_stream_loopback_config {
+    uint32_t connections;           /* client/server pairs, each on its own pair of UDP sockets */
+    uint32_t frame_size_bytes;      /* FrameSizeBytes (BitsPerSecond / 8 / FramesPerSecond), >= 40 */
+    uint32_t frames_per_second;     /* -FrameRate */
+    uint32_t stream_length_frames;  /* StreamLengthFrames (-StreamLength seconds x FrameRate) */
+    uint32_t buffered_frames;       /* BufferedFrames (-BufferDepth seconds x FrameRate) */
+    uint32_t datagram_max_size;     /* -DatagramByteSize (0 = 1400, c_udpDatagramMaximumSizeBytes) */
+    uint32_t pre_post_recvs;        /* -PrePostRecvs of the client (0 = 1) */
+    uint32_t verify_buffers;        /* -Verify:data */
+    uint32_t corrupt_connection;    /* fault injection: connection whose server flips one payload byte, or ~0u */
+    uint32_t corrupt_datagram;      /* ... in its n-th data datagram (0-based) */
+    uint32_t socket_buffer_bytes;   /* SO_SNDBUF / SO_RCVBUF (0 = 8 MiB) */
+    uint32_t reserved;
+} cts_media_stream_loopback_config;
+
+typedef struct cts_media_stream_loopback_result {
+    double seconds;                 /* wall time from the first START to the last finished connection */
+    uint32_t connections_ok;        /* the client completed its stream (Abort after the final frame) */
+    uint32_t connections_failed;    /* a client failed (corrupt payload, invalid datagram, FatalAbort) or a socket error */
+    uint32_t data_errors;           /* clients that latched DATA_DID_NOT_MATCH_BIT_PATTERN */
+    uint32_t reserved;
+    uint64_t datagrams_sent;        /* data datagrams the servers sent */
+    uint64_t datagrams_received;    /* datagrams the clients completed */
+    cts_media_stream_stats clients; /* the clients' ctsUdpStatistics, summed (frames, bits) */
+    double recv_cpu_seconds;        /* CPU time of the clients' receive threads (recv, CompleteIo, VerifyBuffer) */
+} cts_media_stream_loopback_result;
+
+/* Runs cfg->connections MediaStream connections to completion. engine may be NULL only when verify_buffers == 0
+ * or hook != NULL. Returns CTS_OK when the run finished (outcomes in *out). */
+int cts_loopback_media_stream_run(const cts_media_stream_loopback_config* cfg, cts_engine* engine,
+                                  cts_batch_verifier hook, void* hook_ctx, cts_media_stream_loopback_result* out);
+
 #ifdef __cplusplus
 } /* extern "C" */
 #endif

@@ -17,6 +17,7 @@
 #include <thread>
 #include <vector>
 
+#include "cts_loopback.h"
 #include "cts_media_stream.h"
 #include "cts_oracle.h"
 #include "cts_pattern.h"
@@ -174,6 +175,22 @@ int main()
     CHECK(completed.load() == 5 && failed.load() == 1);
     cts_udp_status_details u{};
     CHECK(cts_udp_status_details_read(&u) == CTS_OK && u.successful_frames > 0);
+    // the same over loopback UDP sockets (cts_loopback_udp.cpp): server and client threads per connection, the
+    // clients' timer threads, one corrupt datagram
+    cts_media_stream_loopback_config lc{};
+    lc.connections = 3;
+    lc.frame_size_bytes = kFrame;
+    lc.frames_per_second = kFps;
+    lc.stream_length_frames = 20;
+    lc.buffered_frames = 10;
+    lc.pre_post_recvs = 2;
+    lc.verify_buffers = 1;
+    lc.corrupt_connection = 2;
+    lc.corrupt_datagram = 9;
+    cts_media_stream_loopback_result lr{};
+    CHECK(cts_loopback_media_stream_run(&lc, nullptr, reinterpret_cast<cts_batch_verifier>(ora_batch_verifier), nullptr,
+                                        &lr) == CTS_OK);
+    CHECK(lr.connections_ok == 2 && lr.connections_failed == 1 && lr.data_errors == 1);
     cts_shared_buffer_release();
     std::puts("media_stream_pattern: ok");
     return 0;

@@ -18,7 +18,8 @@ import tempfile
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HOST_SRCS = ["cts_pattern.cpp", "cts_media_stream.cpp", "cts_status.cpp", "cts_loopback.cpp", "cts_host_util.cpp"]
+HOST_SRCS = ["cts_pattern.cpp", "cts_media_stream.cpp", "cts_status.cpp", "cts_loopback.cpp", "cts_loopback_udp.cpp",
+             "cts_host_util.cpp"]
 SAN = {
     "asan-ubsan": ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"],
     "tsan": ["-fsanitize=thread"],

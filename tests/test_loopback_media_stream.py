@@ -1,0 +1,83 @@
+"""MediaStream over loopback UDP (cts_loopback_media_stream_run): the reference's -Protocol:UDP -Pattern:MediaStream
+run end to end on Linux sockets. Every connection's server (ctsMediaStreamServer + ConnectedSocket roles) waits for
+START, sends its connection id and then each frame, timed to the frame rate, as datagrams of header + sender-buffer
+bytes; its client (ctsMediaStreamClient role) verifies every datagram's payload and renders the frames with the
+pattern's own timers, ending with Abort.
+
+Buffering is generous (half the stream) so scheduling jitter on a loaded test host cannot drop a frame: a clean run
+must render every frame of every connection.
+"""
+import numpy as np
+import pytest
+
+import oracle
+from ctstraffic_amd import _pattern_abi as A
+from ctstraffic_amd import loopback as LB
+from ctstraffic_amd import media_stream as M
+from ctstraffic_amd.pattern import shared_buffer_attach
+from oracle import media_stream as OM
+
+_SENDER = oracle.sender_buffer(4 * 65536)
+
+
+def _c_hook():
+    return A.BATCH_VERIFIER(oracle.batch_verifier_address())
+
+
+def _run(**kw):
+    kw.setdefault("frames_per_second", 100)
+    kw.setdefault("stream_length_frames", 30)
+    kw.setdefault("buffered_frames", kw["stream_length_frames"] // 2)
+    return LB.media_stream_run(**kw)
+
+
+@pytest.mark.parametrize("frame", [3000, 52083])
+def test_clean_streams_render_every_frame(frame):
+    shared_buffer_attach(_SENDER)
+    M.udp_status_details_reset()
+    n, frames = 3, 30
+    r = _run(connections=n, frame_size=frame, stream_length_frames=frames, verifier=_c_hook())
+    per = len(OM.split(frame, 1400))
+    assert (r["connections_ok"], r["connections_failed"], r["data_errors"]) == (n, 0, 0)
+    assert r["datagrams_sent"] == n * frames * per
+    c = r["clients"]
+    assert c["successful_frames"] == n * frames and c["dropped_frames"] == 0 and c["error_frames"] == 0
+    assert c["bits_received"] == 8 * n * frames * frame
+    assert r["datagrams_received"] == n * (frames * per + 1)  # + the connection-id datagram
+    u = M.udp_status_details()
+    assert u["successful_frames"] == n * frames and u["bits_received"] >= c["bits_received"]
+
+
+def test_corrupt_datagram_fails_its_connection_only():
+    shared_buffer_attach(_SENDER)
+    r = _run(connections=3, frame_size=3000, corrupt_connection=1, corrupt_datagram=20, verifier=_c_hook())
+    assert (r["connections_ok"], r["connections_failed"], r["data_errors"]) == (2, 1, 1)
+
+
+def test_no_verify_needs_no_verifier():
+    shared_buffer_attach(_SENDER)
+    r = _run(connections=2, frame_size=1400, verify=False)
+    assert r["connections_ok"] == 2 and r["clients"]["successful_frames"] == 60
+
+
+def test_refuses_bad_configs():
+    from ctstraffic_amd._lib import CtsError
+
+    shared_buffer_attach(_SENDER)
+    for kw in (dict(frame_size=39), dict(frames_per_second=0), dict(datagram_max_size=26)):
+        with pytest.raises(CtsError):
+            _run(**{**dict(connections=1, frame_size=3000, verifier=_c_hook()), **kw})
+    with pytest.raises(CtsError):  # verify on, no engine, no hook
+        _run(connections=1, frame_size=3000)
+
+
+@pytest.mark.gpu
+def test_gpu_media_stream_loopback(engine):
+    """README MediaStream sizing (52083-byte frames) at 120 frames/s over 4 connections: every datagram's payload is
+    verified on the GPU; clean connections render every frame, a corrupt datagram fails exactly its connection."""
+    r = _run(connections=4, frame_size=52083, frames_per_second=120, stream_length_frames=60, engine=engine)
+    assert (r["connections_ok"], r["connections_failed"], r["data_errors"]) == (4, 0, 0)
+    assert r["clients"]["successful_frames"] == 4 * 60 and r["clients"]["dropped_frames"] == 0
+    r = _run(connections=4, frame_size=52083, frames_per_second=120, stream_length_frames=60, engine=engine,
+             corrupt_connection=2, corrupt_datagram=100)
+    assert (r["connections_ok"], r["connections_failed"], r["data_errors"]) == (3, 1, 1)
