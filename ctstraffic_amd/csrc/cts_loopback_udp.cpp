@@ -208,6 +208,7 @@ extern "C" int cts_loopback_media_stream_run(const cts_media_stream_loopback_con
         cfg->frames_per_second == 0 || cfg->stream_length_frames == 0 || cfg->buffered_frames == 0)
         return CTS_E_INVALID;
     if (engine == nullptr && hook == nullptr && cfg->verify_buffers) return CTS_E_INVALID;
+    if (cfg->verify_mode > CTS_VERIFY_DEFERRED) return CTS_E_INVALID;
     const uint32_t max_dgram = cfg->datagram_max_size ? cfg->datagram_max_size : 1400u;
     if (max_dgram <= CTS_UDP_DATA_HEADER_LENGTH || max_dgram > 65507u) return CTS_E_INVALID;
     *out = cts_media_stream_loopback_result{};
@@ -221,7 +222,7 @@ extern "C" int cts_loopback_media_stream_run(const cts_media_stream_loopback_con
         c.pre_post_recvs = cfg->pre_post_recvs ? cfg->pre_post_recvs : 1u;
         c.buffer_size_low = cfg->frame_size_bytes;
         c.transfer_size = (uint64_t)cfg->frame_size_bytes * cfg->stream_length_frames;
-        c.verify_mode = CTS_VERIFY_SYNC;
+        c.verify_mode = listening ? CTS_VERIFY_SYNC : cfg->verify_mode;
         c.ms_frames_per_second = cfg->frames_per_second;
         c.ms_datagram_max_size = max_dgram;
         c.ms_buffered_frames = cfg->buffered_frames;

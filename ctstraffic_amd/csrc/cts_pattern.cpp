@@ -481,6 +481,8 @@ struct cts_io_pattern {
     virtual int FireTimer(int) { return CTS_E_INVALID; }
     virtual int Timers(int64_t*, int64_t*) { return CTS_E_INVALID; }
     virtual int UdpStats(cts_media_stream_stats*) { return CTS_E_INVALID; }
+    // cts_io_pattern_flush: the DEFERRED queue of this pattern
+    virtual int FlushPending() { return Flush(); }
 
     uint64_t GetTotalTransfer() const { return state.GetMaxTransfer(); }
     void SetTotalTransfer(uint64_t v) { state.SetMaxTransfer(v); }
@@ -1361,6 +1363,9 @@ struct MediaStreamClient : cts_io_pattern {
         cv.notify_all();
         if (timer_thread.joinable()) timer_thread.join();
         if (ms != nullptr) (void)cts_media_stream_client_destroy(ms);
+        if (stream != nullptr) (void)hipStreamSynchronize(stream);
+        if (d_totals != nullptr) (void)hipFree(d_totals);
+        if (d_fbytes != nullptr) (void)hipFree(d_fbytes);
     }
 
     cts_media_stream_client* ms = nullptr;  // the jitter queue and frame accounting
@@ -1380,6 +1385,173 @@ struct MediaStreamClient : cts_io_pattern {
     bool NeedsVerifier(const cts_task& t) const override  // every recv is a datagram to verify
     {
         return cfg.verify_buffers && t.io_action == CTS_TASK_RECV;
+    }
+
+    // ---- DEFERRED: batched datagram verify (round 3) ---------------------------------------------------------
+    // A data datagram whose header the CPU has checked (it is in host memory) stays in its recv-ring slot and is
+    // queued; a batch goes to the GPU's frame-sum receive pass (cts_media_stream_verify_frames), whose sums are
+    // applied as CompleteTaskBackToPattern would have applied each datagram (the jitter window moves only at a
+    // render tick, and every tick flushes first). A batch holding a corrupt payload is replayed datagram by
+    // datagram from the compact statuses (cts_media_stream_verify_status) up to that datagram, which fails the
+    // stream with the first mismatch cts_verify finds in its payload. Anything else that completes (zero-byte,
+    // short, unknown or ID datagram, Abort) flushes first, so the stream's status and counters are the reference's;
+    // only the completion that reports a corrupt datagram comes later (at most one batch).
+    struct MsQueued {
+        uint64_t offset;     // of the datagram in the recv ring
+        uint32_t completed;  // its bytes
+        uint32_t index;      // its completion index
+    };
+    std::vector<MsQueued> msq;
+    Pinned ms_desc, ms_totals, ms_frame_bytes, ms_status, ms_res;
+    // the frame-sum pass adds into its totals and frame bytes with device atomics, which host memory does not
+    // take over PCIe: they live in device memory and are copied into the pinned ms_totals / ms_frame_bytes
+    void* d_totals = nullptr;
+    uint64_t* d_fbytes = nullptr;
+    uint32_t d_fbytes_cap = 0;
+    int DeviceAlloc(void** p, size_t bytes)
+    {
+        int prev = 0;
+        if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(cts_engine_device(engine)) != hipSuccess) return CTS_E_HIP;
+        const hipError_t e = hipMalloc(p, bytes);
+        (void)hipSetDevice(prev);
+        return e == hipSuccess ? CTS_OK : CTS_E_NOMEM;
+    }
+
+    void ApplyClean(const MsQueued& q)
+    {
+        const char* b = ring_base + q.offset;
+        const cts::MsDatagram d{load_i64(b + CTS_UDP_FLAG_LENGTH), load_i64(b + 8), load_i64(b + 16), q.completed};
+        cts::ms_client_apply_data(ms, d, ReceiverQpc(), 1000000000LL);
+        ++buffers_verified;
+        bytes_verified += q.completed - CTS_UDP_DATA_HEADER_LENGTH;
+    }
+    static int64_t ReceiverQpc()
+    {
+        return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+            .count();
+    }
+    void FailQueued(const MsQueued& q, const cts_verify_result& r)
+    {
+        RecordFailure(q.index, q.completed - CTS_UDP_DATA_HEADER_LENGTH, r, 0);
+        ++buffers_verified;
+        bytes_verified += q.completed - CTS_UDP_DATA_HEADER_LENGTH;
+        UpdateLastPatternError(Fail(q.index, PatternError::CorruptedBytes));
+    }
+
+    // Verifies and applies every queued datagram; true when one of them failed the stream.
+    bool FlushMs()
+    {
+        if (msq.empty()) return false;
+        const uint32_t n = (uint32_t)msq.size();
+        std::vector<MsQueued> q;
+        q.swap(msq);
+        if (hook != nullptr) {  // device-less harness: the batch verifier on the payload spans, then one by one
+            std::vector<cts_buf_desc> d(n);
+            std::vector<cts_verify_result> r(n);
+            for (uint32_t i = 0; i < n; ++i)
+                d[i] = cts_buf_desc{q[i].offset, q[i].completed, 0u, 0u, CTS_UDP_DATA_HEADER_LENGTH};
+            if (hook(hook_ctx, reinterpret_cast<const uint8_t*>(ring_base), ring_bytes, d.data(), n, r.data()) != 0)
+                throw DeviceError{CTS_E_INVALID};
+            for (uint32_t i = 0; i < n; ++i) {
+                if (!r[i].pass) {
+                    FailQueued(q[i], r[i]);
+                    return true;
+                }
+                ApplyClean(q[i]);
+            }
+            return false;
+        }
+        int rc = EnsureStream();
+        if (rc == CTS_OK && ms_desc.host == nullptr) {
+            const uint32_t b = BatchCapacity();
+            if ((rc = ms_desc.alloc(engine, sizeof(cts_buf_desc) * (uint64_t)b)) == CTS_OK &&
+                (rc = ms_totals.alloc(engine, cts_frame_totals_device_bytes())) == CTS_OK &&
+                (rc = ms_status.alloc(engine, sizeof(cts_datagram_status) * (uint64_t)b)) == CTS_OK)
+                rc = ms_res.alloc(engine, sizeof(cts_verify_result) + sizeof(cts_buf_desc));
+        }
+        cts_frame_window w{};
+        if (rc == CTS_OK) rc = cts_media_stream_client_window(ms, &w);
+        if (rc == CTS_OK && d_totals == nullptr) rc = DeviceAlloc(&d_totals, cts_frame_totals_device_bytes());
+        if (rc == CTS_OK && d_fbytes_cap < std::max(w.frames, 1u)) {
+            ms_frame_bytes.release();
+            if (d_fbytes != nullptr) (void)hipFree(d_fbytes);
+            d_fbytes = nullptr;
+            d_fbytes_cap = 0;
+            const uint32_t cap = std::max(w.frames, 1u);
+            void* p = nullptr;
+            if ((rc = DeviceAlloc(&p, sizeof(uint64_t) * (uint64_t)cap)) == CTS_OK &&
+                (rc = ms_frame_bytes.alloc(engine, sizeof(uint64_t) * (uint64_t)cap)) == CTS_OK) {
+                d_fbytes = static_cast<uint64_t*>(p);
+                d_fbytes_cap = cap;
+            } else if (p != nullptr) {
+                (void)hipFree(p);
+            }
+        }
+        if (rc != CTS_OK) throw DeviceError{rc};
+        auto* descs = reinterpret_cast<cts_buf_desc*>(ms_desc.host);
+        for (uint32_t i = 0; i < n; ++i) descs[i] = cts_buf_desc{q[i].offset, q[i].completed, 0u, 0u, 0u};
+        rc = cts_media_stream_verify_frames(engine, recv_pinned.dev, recv_pinned.bytes,
+                                            reinterpret_cast<const cts_buf_desc*>(ms_desc.dev), n, &w, d_totals, d_fbytes,
+                                            nullptr, stream);
+        if (rc == CTS_OK &&
+            (hipMemcpyAsync(ms_totals.host, d_totals, cts_frame_totals_device_bytes(), hipMemcpyDeviceToHost, stream) !=
+                 hipSuccess ||
+             hipMemcpyAsync(ms_frame_bytes.host, d_fbytes, sizeof(uint64_t) * (uint64_t)w.frames, hipMemcpyDeviceToHost,
+                            stream) != hipSuccess))
+            rc = CTS_E_HIP;
+        if (rc != CTS_OK || hipStreamSynchronize(stream) != hipSuccess) throw DeviceError{rc != CTS_OK ? rc : CTS_E_HIP};
+        cts_frame_totals t{};
+        (void)cts_frame_totals_fold(ms_totals.host, &t);
+        if (t.exceptions == 0 && t.datagrams == n) {
+            // every datagram clean: the sums are CompleteTaskBackToPattern over the batch (no sender timestamps)
+            const int st = cts_media_stream_client_complete_frames(ms, &w, &t,
+                                                                   reinterpret_cast<const uint64_t*>(ms_frame_bytes.host),
+                                                                   n, ReceiverQpc(), 1000000000LL);
+            if (st < 0) throw DeviceError{st};
+            buffers_verified += n;
+            for (const MsQueued& e : q) bytes_verified += e.completed - CTS_UDP_DATA_HEADER_LENGTH;
+            return false;
+        }
+        // a corrupt payload in the batch: replay from the statuses up to it
+        rc = cts_media_stream_verify_status(engine, recv_pinned.dev, recv_pinned.bytes,
+                                            reinterpret_cast<const cts_buf_desc*>(ms_desc.dev), n,
+                                            reinterpret_cast<cts_datagram_status*>(ms_status.dev), nullptr, stream);
+        if (rc != CTS_OK || hipStreamSynchronize(stream) != hipSuccess) throw DeviceError{rc != CTS_OK ? rc : CTS_E_HIP};
+        const auto* st = reinterpret_cast<const cts_datagram_status*>(ms_status.host);
+        for (uint32_t i = 0; i < n; ++i) {
+            if (st[i].pass) {
+                ApplyClean(q[i]);
+                continue;
+            }
+            // the first mismatch of its payload (the reference prints it, ctsIOPattern.cpp:761-772)
+            // (the descriptor first: the C ABI wants it 8-byte aligned, the result 4-byte aligned)
+            *reinterpret_cast<cts_buf_desc*>(ms_res.host) =
+                cts_buf_desc{q[i].offset, q[i].completed, 0u, 0u, CTS_UDP_DATA_HEADER_LENGTH};
+            rc = cts_verify(engine, recv_pinned.dev, recv_pinned.bytes, reinterpret_cast<const cts_buf_desc*>(ms_res.dev),
+                            1, q[i].completed, reinterpret_cast<cts_verify_result*>(ms_res.dev + sizeof(cts_buf_desc)),
+                            nullptr, nullptr, 0, stream);
+            if (rc != CTS_OK || hipStreamSynchronize(stream) != hipSuccess) throw DeviceError{rc != CTS_OK ? rc : CTS_E_HIP};
+            FailQueued(q[i], *reinterpret_cast<const cts_verify_result*>(ms_res.host + sizeof(cts_buf_desc)));
+            return true;
+        }
+        return false;
+    }
+    int FlushPending() override
+    {
+        (void)FlushMs();
+        return GetCurrentStatus();
+    }
+    // FlushMs from a timer callback, which has no caller to return a device error to: the error fails the
+    // pattern (a latched FAIL_FAST, as an inconsistency would)
+    void TimerFlush()
+    {
+        try {
+            (void)FlushMs();
+        } catch (const DeviceError& d) {
+            if (fail_fast.empty()) fail_fast = "the batched datagram verify failed in a timer callback (status " +
+                                               std::to_string(d.rc) + ")";
+            m_lastError = CTS_PATTERN_E_FAIL_FAST;
+        }
     }
 
     // SetNextTimer (:321-349): the renderer's next tick at base + offset frames; armed when more than 2 ms ahead
@@ -1404,6 +1576,7 @@ struct MediaStreamClient : cts_io_pattern {
     {
         static char kStart[] = "START";
         if (cts::ms_client_finished(ms)) return;
+        TimerFlush();  // DEFERRED: the datagrams that arrived count
         if (!cts::ms_client_received_buffered_frames(ms)) {
             cts_task t{};
             t.rio_buffer_id = kRioInvalid;
@@ -1423,6 +1596,7 @@ struct MediaStreamClient : cts_io_pattern {
         bool scheduled = false;
         while (!scheduled) {
             if (cts::ms_client_finished(ms)) return;
+            TimerFlush();  // DEFERRED: a tick renders what arrived before it
             const int code = cts::ms_client_tick(ms);
             if (code != 0) {
                 cts_task t{};
@@ -1453,13 +1627,18 @@ struct MediaStreamClient : cts_io_pattern {
                 cv.wait_until(lk, std::chrono::system_clock::now() + std::chrono::milliseconds(std::min<int64_t>(due - now, 50)));
                 continue;
             }
-            if (start_due >= 0 && start_due <= now) {
-                start_due = -1;
-                StartTimer();
-            }
-            if (!stop && render_due >= 0 && render_due <= now) {
-                render_due = -1;
-                RenderTimer();
+            try {
+                if (start_due >= 0 && start_due <= now) {
+                    start_due = -1;
+                    StartTimer();
+                }
+                if (!stop && render_due >= 0 && render_due <= now) {
+                    render_due = -1;
+                    RenderTimer();
+                }
+            } catch (const FailFast& f) {  // nothing may leave the timer thread
+                if (fail_fast.empty()) fail_fast = f.reason;
+                m_lastError = CTS_PATTERN_E_FAIL_FAST;
             }
         }
     }
@@ -1508,10 +1687,21 @@ struct MediaStreamClient : cts_io_pattern {
     {
         if (t.io_action == CTS_TASK_ABORT) {
             if (!cts::ms_client_finished(ms)) throw FailFast{"processed an Abort before the stream was finished"};
+            if (FlushMs()) return PatternError::NoError;  // DEFERRED: a queued datagram failed the stream first
             return PatternError::SuccessfullyCompleted;
         }
         if (t.io_action != CTS_TASK_RECV) return PatternError::NoError;  // a START send
         const uint64_t index = datagrams++;
+        const bool queue_data = Deferred() && cfg.verify_buffers && completedBytes >= CTS_UDP_DATA_HEADER_LENGTH &&
+                                load_u16(t.buffer) == CTS_UDP_FLAG_DATA && InRing(t.buffer, completedBytes);
+        if (queue_data) {
+            // DEFERRED: verified and applied with its batch (FlushMs)
+            msq.push_back(MsQueued{(uint64_t)(t.buffer - ring_base), completedBytes, (uint32_t)index});
+            ++m_recvNeeded;
+            if (msq.size() >= BatchCapacity()) (void)FlushMs();
+            return PatternError::NoError;
+        }
+        if (FlushMs()) return PatternError::NoError;  // the datagrams before this one first
         if (completedBytes == 0) {
             // the final recv may complete with zero bytes once the sender closed
             return cts::ms_client_finished(ms) ? PatternError::NoError : Fail(index, PatternError::TooFewBytes);
@@ -1682,8 +1872,8 @@ int cts_io_pattern_create(const cts_pattern_config* c, cts_engine* engine, cts_i
             c->transfer_size != (uint64_t)c->buffer_size_low * (uint64_t)c->ms_stream_length_frames)
             return CTS_E_INVALID;
         if (!c->listening && (c->ms_buffered_frames == 0 || c->ms_datagram_max_size == 0)) return CTS_E_INVALID;
-        // per-datagram (SYNC) verify only; no RIO and no TCP pacing on the MediaStream path
-        if (c->verify_mode != CTS_VERIFY_SYNC || c->registered_io || c->tcp_bytes_per_second != 0 || c->burst_count != 0)
+        // no RIO and no TCP pacing on the MediaStream path
+        if (c->verify_mode > CTS_VERIFY_DEFERRED || c->registered_io || c->tcp_bytes_per_second != 0 || c->burst_count != 0)
             return CTS_E_INVALID;
     }
     if (c->use_shared_buffer && c->verify_buffers) return CTS_E_INVALID;      // ctsIOPattern.cpp:225-227
@@ -1845,10 +2035,12 @@ int cts_io_pattern_flush(cts_io_pattern* p)
     if (p == nullptr) return CTS_E_INVALID;
     std::lock_guard<std::recursive_mutex> lk(p->mu);
     try {
-        return p->Flush();
+        return p->FlushPending();
     } catch (const FailFast& f) {
         latch_fail_fast(p, f);
         return CTS_IO_FAILED;
+    } catch (const DeviceError& d) {
+        return d.rc;
     }
 }
 

@@ -122,7 +122,8 @@ typedef struct cts_media_stream_loopback_config {
     uint32_t corrupt_connection;    /* fault injection: connection whose server flips one payload byte, or ~0u */
     uint32_t corrupt_datagram;      /* ... in its n-th data datagram (0-based) */
     uint32_t socket_buffer_bytes;   /* SO_SNDBUF / SO_RCVBUF (0 = 8 MiB) */
-    uint32_t reserved;
+    uint32_t verify_mode;           /* the client's CTS_VERIFY_SYNC (per datagram) or CTS_VERIFY_DEFERRED (batches
+                                       through the frame-sum receive pass, flushed at every render tick) */
 } cts_media_stream_loopback_config;
 
 typedef struct cts_media_stream_loopback_result {

@@ -294,8 +294,12 @@ const char* cts_io_pattern_connection_id(cts_io_pattern* pattern);
  * frame task into datagrams (cts_media_stream_split). The client posts untracked recvs of
  * min(frame, DatagramMaxSize) bytes, parses each completed datagram (ctsMediaStreamProtocol.hpp:284-366) and
  * verifies a data datagram's payload (offset 26, expected pattern offset 0) on the GPU, per completion,
- * before booking it to its frame (ctsIOPatternMediaStream.cpp:140-272). Only CTS_VERIFY_SYNC: the batched form
- * of the datagram receive is cts_media_stream_verify_* with cts_media_stream_client_*. registered_io is refused
+ * before booking it to its frame (ctsIOPatternMediaStream.cpp:140-272). CTS_VERIFY_SYNC verifies each data
+ * datagram in its CompleteIo (the reference's timing); CTS_VERIFY_DEFERRED queues data datagrams in the recv ring
+ * (their headers checked on the CPU) and verifies batches of batch_buffers with the GPU frame-sum receive pass
+ * (cts_media_stream_verify_frames), flushing before every render tick, every other completion and Abort, so the
+ * frames, bits and the stream's status are the reference's; a corrupt payload fails the stream when its batch is
+ * verified (at most one batch later), with the first mismatch cts_verify finds in it. registered_io is refused
  * (the MediaStream functors use WSARecvFrom / WSASendTo). Every call on a pattern holds the pattern's own
  * (recursive) lock, as the reference's functors and timer callbacks hold the pattern's critical section.
  *

@@ -10,6 +10,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include "cts_engine.h"
+#include "cts_media_stream.h"
 
 extern "C" {
 
@@ -37,15 +38,32 @@ int cts_verify(cts_engine*, const void*, uint64_t, const cts_buf_desc*, uint32_t
     return CTS_E_NO_DEVICE;
 }
 
+int cts_media_stream_verify_frames(cts_engine*, const void*, uint64_t, const cts_buf_desc*, uint32_t,
+                                   const cts_frame_window*, void*, uint64_t*, void*, void*)
+{
+    return CTS_E_NO_DEVICE;
+}
+int cts_media_stream_verify_status(cts_engine*, const void*, uint64_t, const cts_buf_desc*, uint32_t,
+                                   cts_datagram_status*, void*, void*)
+{
+    return CTS_E_NO_DEVICE;
+}
+
 int cts_verify_host(cts_engine*, const void*, uint32_t, uint32_t, cts_verify_result*) { return CTS_E_NO_DEVICE; }
 int cts_verify_mapped(cts_engine*, const void*, uint32_t, uint32_t, cts_verify_result*) { return CTS_E_NO_DEVICE; }
 uint64_t cts_mailbox_launches(const cts_engine*) { return 0; }
 int cts_engine_get_attr(const cts_engine*, int, int*) { return CTS_E_NO_DEVICE; }
+int cts_engine_device(const cts_engine*) { return CTS_E_NO_DEVICE; }
 
 int cts_engine_stream_create(cts_engine*, void**) { return CTS_E_NO_DEVICE; }
 int cts_engine_stream_destroy(cts_engine*, void*) { return CTS_E_NO_DEVICE; }
 
 hipError_t hipStreamSynchronize(hipStream_t) { return hipErrorNoDevice; }
+hipError_t hipGetDevice(int*) { return hipErrorNoDevice; }
+hipError_t hipSetDevice(int) { return hipErrorNoDevice; }
+hipError_t hipMalloc(void**, size_t) { return hipErrorNoDevice; }
+hipError_t hipFree(void*) { return hipErrorNoDevice; }
+hipError_t hipMemcpyAsync(void*, const void*, size_t, hipMemcpyKind, hipStream_t) { return hipErrorNoDevice; }
 hipError_t hipEventCreateWithFlags(hipEvent_t*, unsigned) { return hipErrorNoDevice; }
 hipError_t hipEventRecord(hipEvent_t, hipStream_t) { return hipErrorNoDevice; }
 hipError_t hipEventQuery(hipEvent_t) { return hipErrorNoDevice; }

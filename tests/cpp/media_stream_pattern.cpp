@@ -34,7 +34,7 @@ namespace {
 
 constexpr uint32_t kFrame = 3000, kMaxDgram = 1400, kFps = 200, kFrames = 12;
 
-cts_pattern_config config(bool listening)
+cts_pattern_config config(bool listening, uint32_t mode = CTS_VERIFY_SYNC)
 {
     cts_pattern_config c{};
     c.io_pattern = CTS_PATTERN_MEDIA_STREAM;
@@ -44,7 +44,8 @@ cts_pattern_config config(bool listening)
     c.pre_post_recvs = 2;
     c.buffer_size_low = kFrame;
     c.transfer_size = (uint64_t)kFrame * kFrames;
-    c.verify_mode = CTS_VERIFY_SYNC;
+    c.verify_mode = mode;
+    c.batch_buffers = 5;  // DEFERRED: small batches, so batches fill between ticks as well as at them
     c.ms_frames_per_second = kFps;
     c.ms_datagram_max_size = kMaxDgram;
     c.ms_buffered_frames = kFrames;  // the whole stream fits the jitter window
@@ -70,10 +71,10 @@ void on_task(void* ctx, const cts_task* t)
 }
 
 // one connection: returns the client's final cts_io_status; `corrupt` flips one payload byte of one datagram
-int run_connection(uint64_t seed, bool corrupt)
+int run_connection(uint64_t seed, bool corrupt, uint32_t mode)
 {
     std::mt19937_64 rng(seed);
-    cts_pattern_config sc = config(true), cc = config(false);
+    cts_pattern_config sc = config(true), cc = config(false, mode);
     cts_io_pattern *server = nullptr, *client = nullptr;
     CHECK(cts_io_pattern_create(&sc, nullptr, &server) == CTS_OK);
     CHECK(cts_io_pattern_set_verifier(server, reinterpret_cast<cts_batch_verifier>(ora_batch_verifier), nullptr) == CTS_OK);
@@ -168,11 +169,13 @@ int main()
     std::atomic<int> completed{0}, failed{0};
     for (int c = 0; c < 6; ++c)
         conns.emplace_back([&, c] {
-            const int st = run_connection(0xC0FFEEull + (uint64_t)c, c == 5);
+            // connections alternate per-datagram (SYNC) and batched (DEFERRED) verify
+            const int st = run_connection(0xC0FFEEull + (uint64_t)c, c >= 4,
+                                          c % 2 ? (uint32_t)CTS_VERIFY_DEFERRED : (uint32_t)CTS_VERIFY_SYNC);
             (st == CTS_IO_COMPLETED ? completed : failed).fetch_add(1);
         });
     for (auto& th : conns) th.join();
-    CHECK(completed.load() == 5 && failed.load() == 1);
+    CHECK(completed.load() == 4 && failed.load() == 2);
     cts_udp_status_details u{};
     CHECK(cts_udp_status_details_read(&u) == CTS_OK && u.successful_frames > 0);
     // the same over loopback UDP sockets (cts_loopback_udp.cpp): server and client threads per connection, the
@@ -187,10 +190,13 @@ int main()
     lc.verify_buffers = 1;
     lc.corrupt_connection = 2;
     lc.corrupt_datagram = 9;
-    cts_media_stream_loopback_result lr{};
-    CHECK(cts_loopback_media_stream_run(&lc, nullptr, reinterpret_cast<cts_batch_verifier>(ora_batch_verifier), nullptr,
-                                        &lr) == CTS_OK);
-    CHECK(lr.connections_ok == 2 && lr.connections_failed == 1 && lr.data_errors == 1);
+    for (const uint32_t mode : {(uint32_t)CTS_VERIFY_SYNC, (uint32_t)CTS_VERIFY_DEFERRED}) {
+        lc.verify_mode = mode;
+        cts_media_stream_loopback_result lr{};
+        CHECK(cts_loopback_media_stream_run(&lc, nullptr, reinterpret_cast<cts_batch_verifier>(ora_batch_verifier),
+                                            nullptr, &lr) == CTS_OK);
+        CHECK(lr.connections_ok == 2 && lr.connections_failed == 1 && lr.data_errors == 1);
+    }
     cts_shared_buffer_release();
     std::puts("media_stream_pattern: ok");
     return 0;

@@ -31,12 +31,16 @@ def _run(**kw):
     return LB.media_stream_run(**kw)
 
 
+MODES = [pytest.param(A.VERIFY_SYNC, id="sync"), pytest.param(A.VERIFY_DEFERRED, id="deferred")]
+
+
+@pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("frame", [3000, 52083])
-def test_clean_streams_render_every_frame(frame):
+def test_clean_streams_render_every_frame(frame, mode):
     shared_buffer_attach(_SENDER)
     M.udp_status_details_reset()
     n, frames = 3, 30
-    r = _run(connections=n, frame_size=frame, stream_length_frames=frames, verifier=_c_hook())
+    r = _run(connections=n, frame_size=frame, stream_length_frames=frames, verifier=_c_hook(), verify_mode=mode)
     per = len(OM.split(frame, 1400))
     assert (r["connections_ok"], r["connections_failed"], r["data_errors"]) == (n, 0, 0)
     assert r["datagrams_sent"] == n * frames * per
@@ -48,9 +52,11 @@ def test_clean_streams_render_every_frame(frame):
     assert u["successful_frames"] == n * frames and u["bits_received"] >= c["bits_received"]
 
 
-def test_corrupt_datagram_fails_its_connection_only():
+@pytest.mark.parametrize("mode", MODES)
+def test_corrupt_datagram_fails_its_connection_only(mode):
     shared_buffer_attach(_SENDER)
-    r = _run(connections=3, frame_size=3000, corrupt_connection=1, corrupt_datagram=20, verifier=_c_hook())
+    r = _run(connections=3, frame_size=3000, corrupt_connection=1, corrupt_datagram=20, verifier=_c_hook(),
+             verify_mode=mode)
     assert (r["connections_ok"], r["connections_failed"], r["data_errors"]) == (2, 1, 1)
 
 
@@ -72,12 +78,15 @@ def test_refuses_bad_configs():
 
 
 @pytest.mark.gpu
-def test_gpu_media_stream_loopback(engine):
+@pytest.mark.parametrize("mode", MODES)
+def test_gpu_media_stream_loopback(engine, mode):
     """README MediaStream sizing (52083-byte frames) at 120 frames/s over 4 connections: every datagram's payload is
-    verified on the GPU; clean connections render every frame, a corrupt datagram fails exactly its connection."""
-    r = _run(connections=4, frame_size=52083, frames_per_second=120, stream_length_frames=60, engine=engine)
+    verified on the GPU (per datagram, or in batches through the frame-sum receive pass); clean connections render
+    every frame, a corrupt datagram fails exactly its connection."""
+    r = _run(connections=4, frame_size=52083, frames_per_second=120, stream_length_frames=60, engine=engine,
+             verify_mode=mode)
     assert (r["connections_ok"], r["connections_failed"], r["data_errors"]) == (4, 0, 0)
     assert r["clients"]["successful_frames"] == 4 * 60 and r["clients"]["dropped_frames"] == 0
     r = _run(connections=4, frame_size=52083, frames_per_second=120, stream_length_frames=60, engine=engine,
-             corrupt_connection=2, corrupt_datagram=100)
+             corrupt_connection=2, corrupt_datagram=100, verify_mode=mode)
     assert (r["connections_ok"], r["connections_failed"], r["data_errors"]) == (3, 1, 1)

@@ -109,11 +109,12 @@ class ClientRun:
     the Python restatement of the client (oracle ClientModel) fed the same datagrams and render ticks."""
 
     def __init__(self, clock, frame, buffered, frames, fps=100, max_dgram=1400, recvs=3, engine=None,
-                 complete_in_callback=False):
+                 complete_in_callback=False, mode=A.VERIFY_SYNC, batch=0):
         self.clock, self.frame, self.fps = clock, frame, fps
         cfg = PatternConfig.media_stream(listening=False, frame_size=frame, frames_per_second=fps,
                                          stream_length_frames=frames, buffered_frames=buffered,
-                                         datagram_max_size=max_dgram, pre_post_recvs=recvs, ms_manual_timers=True)
+                                         datagram_max_size=max_dgram, pre_post_recvs=recvs, ms_manual_timers=True,
+                                         verify_mode=mode, batch_buffers=batch)
         self.p = _make(cfg, engine)
         self.model = OM.ClientModel(frame, buffered, frames)
         self.tasks = []  # tasks handed to the callback
@@ -183,11 +184,17 @@ def test_client_timers_armed_at_first_initiate(clock):
     r.p.close()
 
 
+MODES = [pytest.param((A.VERIFY_SYNC, 0), id="sync"), pytest.param((A.VERIFY_DEFERRED, 0), id="deferred"),
+         pytest.param((A.VERIFY_DEFERRED, 5), id="deferred-batch5")]
+
+
+@pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("complete_in_callback", [False, True])
-def test_client_clean_stream_in_lockstep_with_model(clock, complete_in_callback):
+def test_client_clean_stream_in_lockstep_with_model(clock, complete_in_callback, mode):
     M.udp_status_details_reset()
     frame, frames = 3000, 8
-    r = ClientRun(clock, frame=frame, buffered=2, frames=frames, complete_in_callback=complete_in_callback)
+    r = ClientRun(clock, frame=frame, buffered=2, frames=frames, complete_in_callback=complete_in_callback,
+                  mode=mode[0], batch=mode[1])
     cid = b"0123456789abcdef0123456789abcdef0123"
     assert r.deliver(b"\x00\x10" + cid + b"\x00", model_kind=1) == A.IO_CONTINUE
     assert r.p.connection_id() == cid.decode()
@@ -215,13 +222,15 @@ def test_client_clean_stream_in_lockstep_with_model(clock, complete_in_callback)
     r.p.close()
 
 
+@pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("seed", range(4))
-def test_client_random_stream_matches_model(clock, seed):
+def test_client_random_stream_matches_model(clock, seed, mode):
     rng = np.random.default_rng(seed)
     frame = int(rng.choice([1400, 3000, 5000]))
     frames = int(rng.integers(6, 20))
     buffered = int(rng.integers(1, 5))
-    r = ClientRun(clock, frame=frame, buffered=buffered, frames=frames, recvs=int(rng.integers(1, 4)))
+    r = ClientRun(clock, frame=frame, buffered=buffered, frames=frames, recvs=int(rng.integers(1, 4)), mode=mode[0],
+                  batch=mode[1])
     st = A.IO_CONTINUE
     for f in range(1, frames + 1):
         lens = OM.split(frame, 1400)
@@ -246,11 +255,36 @@ def test_client_corrupt_payload_fails_the_stream(clock):
     r = ClientRun(clock, frame=3000, buffered=2, frames=5)
     assert r.deliver(_datagram(1, 1400), seq=1) == A.IO_CONTINUE
     assert r.deliver(_datagram(1, 1400, corrupt_at=700), seq=1, ok=False) == A.IO_FAILED
+    _check_corrupt_failure(r)
+    r.p.close()
+
+
+def _check_corrupt_failure(r):
     assert r.p.GetLastPatternError() == A.STATUS_ERROR_DATA_DID_NOT_MATCH_BIT_PATTERN
     s = r.p.media_stream_stats()
     assert s["has_failure"] == 1 and s["fail_datagram"] == 1 and s["bits_received"] == 8 * 1400
     ps = r.p.stats()
     assert (ps["buffers_failed"], ps["fail_offset"], ps["fail_length"]) == (1, 700, 1374)
+
+
+@pytest.mark.parametrize("batch", [0, 4])
+def test_client_deferred_corrupt_payload(clock, batch):
+    """DEFERRED: the corrupt datagram fails the stream when its batch is verified (a full batch, a render tick or
+    any completion that is not a queued data datagram), with the same failure record and counters as SYNC; the
+    datagrams queued after it are not applied."""
+    r = ClientRun(clock, frame=3000, buffered=2, frames=5, mode=A.VERIFY_DEFERRED, batch=batch)
+    assert r.deliver(_datagram(1, 1400), seq=1) == A.IO_CONTINUE
+    assert r.deliver(_datagram(1, 1400, corrupt_at=700), seq=1, ok=False) == A.IO_CONTINUE  # queued
+    st = r.deliver(_datagram(2, 1400), seq=2)  # the model stops at the corrupt one
+    if batch == 4:
+        assert st == A.IO_CONTINUE
+        st = r.p.CompleteIo(r.posted.pop(0), 0)  # a zero-byte datagram: not queued, flushes first
+    else:
+        assert st == A.IO_CONTINUE
+        assert r.p.Flush() == A.IO_FAILED
+        st = A.IO_FAILED
+    assert st == A.IO_FAILED
+    _check_corrupt_failure(r)
     r.p.close()
 
 
@@ -349,7 +383,7 @@ def test_media_stream_config_is_checked(clock):
     ok = dict(listening=False, frame_size=3000, frames_per_second=100, stream_length_frames=5, buffered_frames=2)
     bad = [
         PatternConfig(**{**PatternConfig.media_stream(**ok).__dict__, "transfer_size": 3000 * 5 + 1}),
-        PatternConfig(**{**PatternConfig.media_stream(**ok).__dict__, "verify_mode": A.VERIFY_DEFERRED}),
+        PatternConfig(**{**PatternConfig.media_stream(**ok).__dict__, "verify_mode": 7}),
         PatternConfig(**{**PatternConfig.media_stream(**ok).__dict__, "ms_buffered_frames": 0}),
         PatternConfig.media_stream(**{**ok, "frame_size": 39, "stream_length_frames": 5}),
         PatternConfig(**{**PatternConfig.media_stream(**ok).__dict__, "registered_io": True}),
@@ -375,12 +409,13 @@ def test_tcp_patterns_refuse_the_media_stream_calls():
 
 # ---- GPU: the payload verify on the gfx950 kernel ----------------------------------------------------
 @pytest.mark.gpu
-def test_gpu_client_stream_with_corruption(engine, clock):
+@pytest.mark.parametrize("mode", MODES)
+def test_gpu_client_stream_with_corruption(engine, clock, mode):
     """The client pattern on a device engine: every data datagram's payload is verified on the GPU (the SYNC
     mailbox over the pattern's pinned recv buffers); a clean stream renders every frame, and a corrupted
     payload fails the stream at that datagram with the first mismatch the kernel found."""
     frame, frames = 5000, 6
-    r = ClientRun(clock, frame=frame, buffered=2, frames=frames, engine=engine)
+    r = ClientRun(clock, frame=frame, buffered=2, frames=frames, engine=engine, mode=mode[0], batch=mode[1])
     for f in range(1, frames + 1):
         for ln in OM.split(frame, 1400):
             assert r.deliver(_datagram(f, ln), seq=f) == A.IO_CONTINUE
@@ -394,9 +429,13 @@ def test_gpu_client_stream_with_corruption(engine, clock):
     assert r.p.stats()["buffers_verified"] == frames * len(OM.split(frame, 1400))
     r.p.close()
 
-    r = ClientRun(clock, frame=frame, buffered=2, frames=frames, engine=engine)
+    r = ClientRun(clock, frame=frame, buffered=2, frames=frames, engine=engine, mode=mode[0], batch=mode[1])
     assert r.deliver(_datagram(1, 1400), seq=1) == A.IO_CONTINUE
-    assert r.deliver(_datagram(1, 1400, corrupt_at=1001), seq=1, ok=False) == A.IO_FAILED
+    st = r.deliver(_datagram(1, 1400, corrupt_at=1001), seq=1, ok=False)
+    if mode[0] == A.VERIFY_DEFERRED:
+        assert st == A.IO_CONTINUE and r.p.Flush() == A.IO_FAILED  # the batch's verdict
+    else:
+        assert st == A.IO_FAILED
     ps = r.p.stats()
     assert (ps["buffers_failed"], ps["fail_offset"], ps["fail_length"]) == (1, 1001, 1374)
     assert ps["fail_expected"] == int(_SENDER[1001]) and ps["fail_actual"] == int(_SENDER[1001]) ^ 0x5A
