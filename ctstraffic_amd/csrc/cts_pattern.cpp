@@ -1403,8 +1403,8 @@ struct MediaStreamClient : cts_io_pattern {
     };
     std::vector<MsQueued> msq;
     Pinned ms_desc, ms_totals, ms_frame_bytes, ms_status, ms_res;
-    // the frame-sum pass adds into its totals and frame bytes with device atomics, which host memory does not
-    // take over PCIe: they live in device memory and are copied into the pinned ms_totals / ms_frame_bytes
+    // the frame-sum pass adds into its totals and frame bytes with device-scope atomics: they live in device memory
+    // (as cts_media_stream_verify_frames documents them) and are copied into the pinned ms_totals / ms_frame_bytes
     void* d_totals = nullptr;
     uint64_t* d_fbytes = nullptr;
     uint32_t d_fbytes_cap = 0;
