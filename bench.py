@@ -860,6 +860,19 @@ def run_extras(engine, torch, W, w, arenas, descs, dev, want):
             out["loopback_config1_verify_off"] = {
                 "GBps_recv": round(r["GBps_recv"], 3), "seconds": round(r["seconds"], 3),
                 "connections_ok": r["connections_ok"], "recv_cpu_s_per_GiB": round(r["recv_cpu_s_per_GiB"], 4)}
+            # MediaStream over loopback UDP (README sizing, 52083-byte frames at 240 frames/s, 16 connections, ~1.3 s):
+            # the client patterns verify every datagram per completion (SYNC) or in batches through the frame-sum
+            # receive pass (DEFERRED); the stream is rate-paced, so the number is the receive threads' CPU per datagram
+            for name, mode in (("sync", PA.VERIFY_SYNC), ("deferred", PA.VERIFY_DEFERRED)):
+                r = LB.media_stream_run(connections=16, frame_size=52083, frames_per_second=240,
+                                        stream_length_frames=240, buffered_frames=60, engine=engine, verify_mode=mode)
+                c = r["clients"]
+                out["loopback_media_stream_%s" % name] = {
+                    "connections_ok": r["connections_ok"], "data_errors": r["data_errors"],
+                    "datagrams_received": r["datagrams_received"], "successful_frames": c["successful_frames"],
+                    "dropped_frames": c["dropped_frames"], "payload_MBps": round(r["payload_MBps"], 1),
+                    "recv_cpu_us_per_datagram": round(1e6 * r["recv_cpu_seconds"] / max(1, r["datagrams_received"]),
+                                                      3)}
         except Exception as e:  # pragma: no cover
             out["loopback_error"] = repr(e)
     if "host" in want:
