@@ -1363,9 +1363,9 @@ struct MediaStreamClient : cts_io_pattern {
         cv.notify_all();
         if (timer_thread.joinable()) timer_thread.join();
         if (ms != nullptr) (void)cts_media_stream_client_destroy(ms);
+        if (d_totals != nullptr) (void)hipFreeAsync(d_totals, stream);
+        if (d_fbytes != nullptr) (void)hipFreeAsync(d_fbytes, stream);
         if (stream != nullptr) (void)hipStreamSynchronize(stream);
-        if (d_totals != nullptr) (void)hipFree(d_totals);
-        if (d_fbytes != nullptr) (void)hipFree(d_fbytes);
     }
 
     cts_media_stream_client* ms = nullptr;  // the jitter queue and frame accounting
@@ -1408,13 +1408,11 @@ struct MediaStreamClient : cts_io_pattern {
     void* d_totals = nullptr;
     uint64_t* d_fbytes = nullptr;
     uint32_t d_fbytes_cap = 0;
+    // stream-ordered (hipMallocAsync / hipFreeAsync on the pattern's stream): a plain hipFree waits for the whole
+    // device, and with other connections posting to the engine's resident SYNC mailbox grid that can be a long time
     int DeviceAlloc(void** p, size_t bytes)
     {
-        int prev = 0;
-        if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(cts_engine_device(engine)) != hipSuccess) return CTS_E_HIP;
-        const hipError_t e = hipMalloc(p, bytes);
-        (void)hipSetDevice(prev);
-        return e == hipSuccess ? CTS_OK : CTS_E_NOMEM;
+        return hipMallocAsync(p, bytes, stream) == hipSuccess ? CTS_OK : CTS_E_NOMEM;
     }
 
     void ApplyClean(const MsQueued& q)
@@ -1474,7 +1472,7 @@ struct MediaStreamClient : cts_io_pattern {
         if (rc == CTS_OK && d_totals == nullptr) rc = DeviceAlloc(&d_totals, cts_frame_totals_device_bytes());
         if (rc == CTS_OK && d_fbytes_cap < std::max(w.frames, 1u)) {
             ms_frame_bytes.release();
-            if (d_fbytes != nullptr) (void)hipFree(d_fbytes);
+            if (d_fbytes != nullptr) (void)hipFreeAsync(d_fbytes, stream);
             d_fbytes = nullptr;
             d_fbytes_cap = 0;
             const uint32_t cap = std::max(w.frames, 1u);
@@ -1484,7 +1482,7 @@ struct MediaStreamClient : cts_io_pattern {
                 d_fbytes = static_cast<uint64_t*>(p);
                 d_fbytes_cap = cap;
             } else if (p != nullptr) {
-                (void)hipFree(p);
+                (void)hipFreeAsync(p, stream);
             }
         }
         if (rc != CTS_OK) throw DeviceError{rc};

@@ -53,16 +53,13 @@ int cts_verify_host(cts_engine*, const void*, uint32_t, uint32_t, cts_verify_res
 int cts_verify_mapped(cts_engine*, const void*, uint32_t, uint32_t, cts_verify_result*) { return CTS_E_NO_DEVICE; }
 uint64_t cts_mailbox_launches(const cts_engine*) { return 0; }
 int cts_engine_get_attr(const cts_engine*, int, int*) { return CTS_E_NO_DEVICE; }
-int cts_engine_device(const cts_engine*) { return CTS_E_NO_DEVICE; }
 
 int cts_engine_stream_create(cts_engine*, void**) { return CTS_E_NO_DEVICE; }
 int cts_engine_stream_destroy(cts_engine*, void*) { return CTS_E_NO_DEVICE; }
 
 hipError_t hipStreamSynchronize(hipStream_t) { return hipErrorNoDevice; }
-hipError_t hipGetDevice(int*) { return hipErrorNoDevice; }
-hipError_t hipSetDevice(int) { return hipErrorNoDevice; }
-hipError_t hipMalloc(void**, size_t) { return hipErrorNoDevice; }
-hipError_t hipFree(void*) { return hipErrorNoDevice; }
+hipError_t hipMallocAsync(void**, size_t, hipStream_t) { return hipErrorNoDevice; }
+hipError_t hipFreeAsync(void*, hipStream_t) { return hipErrorNoDevice; }
 hipError_t hipMemcpyAsync(void*, const void*, size_t, hipMemcpyKind, hipStream_t) { return hipErrorNoDevice; }
 hipError_t hipEventCreateWithFlags(hipEvent_t*, unsigned) { return hipErrorNoDevice; }
 hipError_t hipEventRecord(hipEvent_t, hipStream_t) { return hipErrorNoDevice; }
