@@ -51,6 +51,11 @@ def test_loopback_gpu(engine, mode):
     r = loopback.run(connections=4, buffer_size=65536, transfer_size=8 * 1024 * 1024, engine=engine, verify_mode=mode,
                      corrupt_connection=2, corrupt_send_index=40)
     assert r["data_errors"] == 1 and r["connections_ok"] == 3
+    # small batches: DEFERRED's zero-copy recv ring (2 x 8 + 2 slots) has wrapped several times before send 100, so
+    # the kernel must see the slot's new bytes, not a line cached from an earlier batch
+    r = loopback.run(connections=4, buffer_size=65536, transfer_size=8 * 1024 * 1024, engine=engine, verify_mode=mode,
+                     batch_buffers=8, corrupt_connection=1, corrupt_send_index=100)
+    assert r["data_errors"] == 1 and r["connections_ok"] == 3
 
 
 def test_loopback_with_c_oracle_hook():

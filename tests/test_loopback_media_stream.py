@@ -87,6 +87,9 @@ def test_gpu_media_stream_loopback(engine, mode):
              verify_mode=mode)
     assert (r["connections_ok"], r["connections_failed"], r["data_errors"]) == (4, 0, 0)
     assert r["clients"]["successful_frames"] == 4 * 60 and r["clients"]["dropped_frames"] == 0
-    r = _run(connections=4, frame_size=52083, frames_per_second=120, stream_length_frames=60, engine=engine,
-             corrupt_connection=2, corrupt_datagram=100, verify_mode=mode)
-    assert (r["connections_ok"], r["connections_failed"], r["data_errors"]) == (3, 1, 1)
+    # a corrupt datagram early, and one after the client's recv ring has wrapped (60 frames x 38 datagrams = 2280
+    # per connection against 2 x 1024 + 3 ring slots in DEFERRED): the GPU must read the slot's new bytes
+    for at in (100, 2200):
+        r = _run(connections=4, frame_size=52083, frames_per_second=120, stream_length_frames=60, engine=engine,
+                 corrupt_connection=2, corrupt_datagram=at, verify_mode=mode)
+        assert (r["connections_ok"], r["connections_failed"], r["data_errors"]) == (3, 1, 1), at
