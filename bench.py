@@ -386,7 +386,8 @@ def main():
             gs = torch.cuda.Stream()
             try:
                 sg = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(sg, stream=gs):
+                # thread_local: other threads' HIP calls (RCCL's watchdog at N > 1) stay legal during the capture
+                with torch.cuda.graph(sg, stream=gs, capture_error_mode="thread_local"):
                     for i in range(R):
                         B.launch(i, gs)
             except Exception as e:  # pragma: no cover - keep the host-launch leg
