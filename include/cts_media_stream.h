@@ -17,6 +17,9 @@
  * datagram and verifies the data payloads in one pass.
  * Host side: cts_media_stream_split (frame -> datagram sizes) and the client's
  * frame accounting (cts_media_stream_client_*), fed with the GPU's records.
+ * The ctsIoPattern form of both MediaStream roles (connection-id and START
+ * datagrams, timed frame sends, the client's timers on a pattern thread) is
+ * CTS_PATTERN_MEDIA_STREAM in cts_pattern.h, built on these calls.
  */
 #ifndef CTS_MEDIA_STREAM_H
 #define CTS_MEDIA_STREAM_H
@@ -244,7 +247,7 @@ int cts_media_stream_client_complete_frames(cts_media_stream_client* client, con
                                             int64_t receiver_qpc, int64_t receiver_qpf);
 int cts_media_stream_client_set_connection_id(cts_media_stream_client* client, const char* datagram, uint32_t len);
 /* One renderer-timer tick (TimerCallback, ctsIOPatternMediaStream.cpp:470-530,
- * without the wall-clock scheduling): returns 0 = keep rendering, 1 = the stream
+ * without the wall-clock scheduling, which CTS_PATTERN_MEDIA_STREAM adds): returns 0 = keep rendering, 1 = the stream
  * finished (Abort), 2 = nothing was ever received (FatalAbort). */
 int cts_media_stream_client_render(cts_media_stream_client* client);
 int cts_media_stream_client_stats(const cts_media_stream_client* client, cts_media_stream_stats* out);
