@@ -24,7 +24,7 @@ SOFLAGS   := -shared -Wl,-Bsymbolic -Wl,--version-script=$(CSRC)/exports.map
 DEVICE_VERIFY := ctstraffic_amd/build/device_verify
 TOOLS := tools/hbm_read_ceiling tools/verify_ablation tools/mailbox_probe tools/rw_mix_probe tools/write_shape_probe tools/fill_bisect tools/fill_abi_probe tools/mailbox_bisect tools/ring_fill_probe
 
-SYNC_PROBE := tools/sync_probe
+SYNC_PROBE := tools/sync_probe tools/pattern_cpu_probe
 BENCH_MULTI := tools/libcts_bench_multi.so
 
 all: $(ENGINE_SO) $(TUNING_SO) oracle $(DEVICE_VERIFY) $(TOOLS) $(SYNC_PROBE) $(BENCH_MULTI)
@@ -36,7 +36,11 @@ $(BENCH_MULTI): tools/bench_multi.cpp $(ENGINE_SO) include/cts_engine.h
 	$(HIPCC) -O2 -std=c++17 -fPIC -shared -Iinclude $< -o $@ -Lctstraffic_amd -lcts_engine -Wl,-rpath,'$$ORIGIN/../ctstraffic_amd' -lpthread
 
 # SYNC-mode (per-completion) verify latency probe against the C ABI
-$(SYNC_PROBE): tools/sync_probe.cpp $(ENGINE_SO) include/cts_engine.h
+tools/sync_probe: tools/sync_probe.cpp $(ENGINE_SO) include/cts_engine.h
+	$(HIPCC) -O2 -std=c++17 -Iinclude $< -o $@ -Lctstraffic_amd -lcts_engine -Wl,-rpath,'$$ORIGIN/../ctstraffic_amd' -lpthread
+
+# receive-thread CPU inside the ctsIoPattern calls (no sockets)
+tools/pattern_cpu_probe: tools/pattern_cpu_probe.cpp $(ENGINE_SO) include/cts_pattern.h
 	$(HIPCC) -O2 -std=c++17 -Iinclude $< -o $@ -Lctstraffic_amd -lcts_engine -Wl,-rpath,'$$ORIGIN/../ctstraffic_amd' -lpthread
 
 # measurement references used by tools/gpu_round.sh (plain streaming read/write ceilings, verify ablation)

@@ -885,12 +885,14 @@ def run_extras(engine, torch, W, w, arenas, descs, dev, want):
                     "GBps_recv": round(r["GBps_recv"], 3), "seconds": round(r["seconds"], 3),
                     "connections_ok": r["connections_ok"], "data_errors": r["data_errors"],
                     "buffers_verified": r["buffers_verified"],
-                    "recv_cpu_s_per_GiB": round(r["recv_cpu_s_per_GiB"], 4)}
+                    "recv_cpu_s_per_GiB": round(r["recv_cpu_s_per_GiB"], 4),
+                    "recv_pattern_cpu_s_per_GiB": round(r["recv_pattern_cpu_s_per_GiB"], 4)}
             # the socket path alone (-verify:connection): what the receive threads spend without any VerifyBuffer
             r = LB.run(connections=8, buffer_size=65536, transfer_size=1 << 30, verify=False)
             out["loopback_config1_verify_off"] = {
                 "GBps_recv": round(r["GBps_recv"], 3), "seconds": round(r["seconds"], 3),
-                "connections_ok": r["connections_ok"], "recv_cpu_s_per_GiB": round(r["recv_cpu_s_per_GiB"], 4)}
+                "connections_ok": r["connections_ok"], "recv_cpu_s_per_GiB": round(r["recv_cpu_s_per_GiB"], 4),
+                "recv_pattern_cpu_s_per_GiB": round(r["recv_pattern_cpu_s_per_GiB"], 4)}
             # MediaStream over loopback UDP (README sizing, 52083-byte frames at 240 frames/s, 16 connections, ~1.3 s):
             # the client patterns verify every datagram per completion (SYNC) or in batches through the frame-sum
             # receive pass (DEFERRED); the stream is rate-paced, so the number is the receive threads' CPU per datagram
@@ -974,6 +976,7 @@ def cpu_baseline(arena, w, seconds):
                    verify_mode=PA.VERIFY_SYNC)
         loop = {"GBps_recv": round(r["GBps_recv"], 3), "connections_ok": r["connections_ok"],
                 "seconds": round(r["seconds"], 3), "recv_cpu_s_per_GiB": round(r["recv_cpu_s_per_GiB"], 4),
+                "recv_pattern_cpu_s_per_GiB": round(r["recv_pattern_cpu_s_per_GiB"], 4),
                 "sample": "config 1: 8 conns x 1 GiB loopback push, 64 KiB, oracle VerifyBuffer (C) per completion "
                           "on each connection's receive thread"}
     except Exception as e:  # pragma: no cover

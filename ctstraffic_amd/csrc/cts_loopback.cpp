@@ -22,6 +22,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstring>
+#include <ctime>
 #include <deque>
 #include <mutex>
 #include <thread>
@@ -86,6 +87,7 @@ struct SideResult {
     cts_pattern_stats stats{};
     double recv_cpu_s = 0;  // CPU time (user + sys) of the thread that ran this side's recvs
     double send_cpu_s = 0;  // ... and of its send thread (the same thread in the sync functor)
+    double recv_io_cpu_s = 0;  // the part of recv_cpu_s spent inside the socket calls (send/recv syscalls)
 };
 
 // this thread's CPU seconds so far (user + system)
@@ -97,6 +99,14 @@ double thread_cpu_s()
            (double)u.ru_stime.tv_usec * 1e-6;
 }
 
+// the same at nanosecond resolution, cheap enough to bracket every socket call (one clock_gettime)
+double thread_cpu_ns_s()
+{
+    timespec ts{};
+    if (::clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts) != 0) return 0;
+    return (double)ts.tv_sec + (double)ts.tv_nsec * 1e-9;
+}
+
 void run_side(int* fdslot, cts_io_pattern* p, bool inject, uint32_t inject_index, bool recv_whole, SideResult* out)
 {
     const double cpu0 = thread_cpu_s();
@@ -104,6 +114,7 @@ void run_side(int* fdslot, cts_io_pattern* p, bool inject, uint32_t inject_index
     std::vector<char> scratch;
     uint32_t data_sends = 0;
     int st = CTS_IO_CONTINUE;
+    double io_cpu = 0;  // CPU inside the socket calls; the rest of the thread's time is the pattern's
     for (;;) {
         cts_task t{};
         if (cts_io_pattern_initiate_io(p, &t) != CTS_OK) {
@@ -120,7 +131,9 @@ void run_side(int* fdslot, cts_io_pattern* p, bool inject, uint32_t inject_index
                 scratch[t.buffer_length / 2] ^= 0x5A;
                 src = scratch.data();
             }
+            const double c0 = thread_cpu_ns_s();
             status = send_all(fd, src, t.buffer_length);
+            io_cpu += thread_cpu_ns_s() - c0;
             transferred = status == 0 ? t.buffer_length : 0;
             break;
         }
@@ -129,7 +142,9 @@ void run_side(int* fdslot, cts_io_pattern* p, bool inject, uint32_t inject_index
             // (or, with recv_whole, with the whole posted length: deterministic completions)
             const bool whole = recv_whole || t.buffer_type == CTS_BUFFER_TCP_CONNECTION_ID ||
                                t.buffer_type == CTS_BUFFER_COMPLETION_MESSAGE;
+            const double c0 = thread_cpu_ns_s();
             status = recv_some(fd, t.buffer + t.buffer_offset, t.buffer_length, &transferred, whole);
+            io_cpu += thread_cpu_ns_s() - c0;
             break;
         }
         case CTS_TASK_GRACEFUL_SHUTDOWN:
@@ -166,6 +181,7 @@ void run_side(int* fdslot, cts_io_pattern* p, bool inject, uint32_t inject_index
     out->last_error = cts_io_pattern_last_error(p);
     (void)cts_io_pattern_get_stats(p, &out->stats);
     out->recv_cpu_s = out->send_cpu_s = thread_cpu_s() - cpu0;  // one thread runs both directions
+    out->recv_io_cpu_s = io_cpu;
 }
 
 // ---- async functor (Duplex): one send and one recv thread per connection side -----------------
@@ -236,6 +252,7 @@ struct AsyncSide {
         release();
     }
     double cpu_s[2] = {0, 0};  // CPU seconds of the recv (0) and send (1) worker
+    double recv_io_cpu_s = 0;  // the recv worker's CPU inside recv()
     void worker(bool sending)
     {
         const double cpu0 = thread_cpu_s();
@@ -272,7 +289,9 @@ struct AsyncSide {
                 } else {
                     const bool whole = recv_whole || t.buffer_type == CTS_BUFFER_TCP_CONNECTION_ID ||
                                        t.buffer_type == CTS_BUFFER_COMPLETION_MESSAGE;
+                    const double c0 = thread_cpu_ns_s();
                     err = recv_some(fd, t.buffer + t.buffer_offset, t.buffer_length, &transferred, whole);
+                    recv_io_cpu_s += thread_cpu_ns_s() - c0;
                 }
                 lk.lock();
             }
@@ -314,6 +333,7 @@ void run_side_async(int* fdslot, cts_io_pattern* p, bool inject, uint32_t inject
     (void)cts_io_pattern_get_stats(p, &out->stats);
     out->recv_cpu_s = a.cpu_s[0];
     out->send_cpu_s = a.cpu_s[1];
+    out->recv_io_cpu_s = a.recv_io_cpu_s;
 }
 
 }  // namespace
@@ -469,10 +489,14 @@ extern "C" int cts_loopback_run_detailed(const cts_loopback_config* cfg, cts_eng
     for (uint32_t i = 0; i < 2 * n; ++i) {  // the threads that received the data / sent it
         const cts_pattern_stats& st = res[i].stats;
         if (async) {  // a recv worker and a send worker per side
-            if (st.bytes_recv != 0) out->recv_cpu_seconds += res[i].recv_cpu_s;
+            if (st.bytes_recv != 0) {
+                out->recv_cpu_seconds += res[i].recv_cpu_s;
+                out->recv_io_cpu_seconds += res[i].recv_io_cpu_s;
+            }
             if (st.bytes_sent != 0) out->send_cpu_seconds += res[i].send_cpu_s;
         } else if (st.bytes_recv > st.bytes_sent) {  // one thread per side: by the direction it mostly ran
             out->recv_cpu_seconds += res[i].recv_cpu_s;
+            out->recv_io_cpu_seconds += res[i].recv_io_cpu_s;
         } else {
             out->send_cpu_seconds += res[i].send_cpu_s;
         }

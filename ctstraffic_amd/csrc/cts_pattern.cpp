@@ -419,11 +419,27 @@ struct cts_io_pattern {
     // the next launch, at any non-benign completion and at Flush (Retire)
     std::vector<Queued> inflight;
     hipEvent_t inflight_done = nullptr;  // recorded after the in-flight batch's launch, queried by CompleteIo
-    // Retire waits on inflight_done as a blocking-sync event (the thread sleeps until the kernel's completion
-    // interrupt) instead of spinning in hipStreamSynchronize (CTS_DEFERRED_BLOCKING_SYNC, default 1)
-    bool blocking_retire = [] {
+    // How Retire waits for the in-flight batch (CTS_DEFERRED_BLOCKING_SYNC): 0 = spin in hipStreamSynchronize,
+    // 1 = hipEventSynchronize on a blocking-sync event, 2 (default) = sleep in 50 us steps between non-blocking
+    // queries of the event. With 8 connections sharing the PCIe link, the first two burned ~2 ms of receive-thread
+    // CPU per wait, 1 as much as 0 (tools/pattern_cpu_probe, profiles/r03/pattern_cpu/): the runtime's blocking wait
+    // spins before it sleeps
+    int retire_wait = [] {
         const char* v = std::getenv("CTS_DEFERRED_BLOCKING_SYNC");
-        return v == nullptr || *v == 0 || std::atoi(v) != 0;
+        if (v == nullptr || *v == 0) return 2;
+        const int n = std::atoi(v);
+        return n < 0 || n > 2 ? 2 : n;
+    }();
+    // CompleteIo asks whether the in-flight batch is done every query_period-th completion (a power of two;
+    // CTS_DEFERRED_QUERY_PERIOD, default 16; 0 = never: verdicts land at the next Rotate / Flush only)
+    uint32_t query_period = [] {
+        const char* v = std::getenv("CTS_DEFERRED_QUERY_PERIOD");
+        if (v == nullptr || *v == 0) return 16u;
+        const long n = std::atol(v);
+        if (n <= 0) return 0u;
+        uint32_t p = 1;
+        while (p < (uint32_t)std::min<long>(n, 1L << 20)) p <<= 1;
+        return p;
     }();
     uint32_t desc_set = 0;  // the half the filling batch uses
     // DEFERRED zero-copy ring: the recv container holds (1 or 2) x BatchCapacity() + recvCount + 1
@@ -907,14 +923,23 @@ struct cts_io_pattern {
                           nullptr, nullptr, 0, stream);
     }
 
+    hipError_t WaitInflight()
+    {
+        if (inflight_done == nullptr || retire_wait == 0) return hipStreamSynchronize(stream);
+        if (retire_wait == 1) return hipEventSynchronize(inflight_done);
+        for (;;) {
+            const hipError_t q = hipEventQuery(inflight_done);
+            if (q != hipErrorNotReady) return q;
+            std::this_thread::sleep_for(std::chrono::microseconds(50));
+        }
+    }
+
     // Waits for the in-flight batch and applies its verdicts. A failure in it takes back
     // everything completed after the failing buffer, the filling batch included.
     int Retire()
     {
         if (inflight.empty()) return CTS_OK;
-        if ((blocking_retire && inflight_done ? hipEventSynchronize(inflight_done) : hipStreamSynchronize(stream)) !=
-            hipSuccess)
-            return CTS_E_HIP;
+        if (WaitInflight() != hipSuccess) return CTS_E_HIP;
         const size_t half = (size_t)(desc_set ^ 1u) * BatchCapacity();
         const bool failed = ApplyVerdicts(inflight, reinterpret_cast<const cts_verify_result*>(stage_res.host) + half);
         inflight.clear();
@@ -935,7 +960,7 @@ struct cts_io_pattern {
         const int lr = LaunchBatch();
         if (lr != CTS_OK) return lr;
         if (inflight_done == nullptr &&
-            hipEventCreateWithFlags(&inflight_done, hipEventDisableTiming | (blocking_retire ? hipEventBlockingSync : 0u)) !=
+            hipEventCreateWithFlags(&inflight_done, hipEventDisableTiming | (retire_wait == 1 ? hipEventBlockingSync : 0u)) !=
                 hipSuccess) {
             inflight_done = nullptr;
             return CTS_E_HIP;
@@ -1027,7 +1052,7 @@ struct cts_io_pattern {
         // queued verdicts first, so a pending data error latches before it.
         bool benign = status == kNoError && (t.io_action == CTS_TASK_SEND || t.io_action == CTS_TASK_RECV) &&
                       state.WouldStayMoreIo(t, transfer) && m_lastError == kStatusIoRunning;
-        if (Deferred() && benign && (queue.size() & 15u) == 0 && InflightDone()) {
+        if (Deferred() && benign && query_period != 0 && (queue.size() & (query_period - 1u)) == 0 && InflightDone()) {
             // the in-flight batch's verdicts are in: apply them now, so a data error fails the connection at
             // this completion rather than at the next launch (ctsIOPattern.cpp:486-489 fails it at the
             // failing one; the completions in between are taken back by RollbackAfter)

@@ -30,13 +30,17 @@ class LoopbackResult(ctypes.Structure):
                 ("buffers_verified", ctypes.c_uint64), ("connections_ok", ctypes.c_uint32),
                 ("connections_failed", ctypes.c_uint32), ("data_errors", ctypes.c_uint32),
                 ("reserved", ctypes.c_uint32), ("recv_cpu_seconds", ctypes.c_double),
-                ("send_cpu_seconds", ctypes.c_double)]
+                ("send_cpu_seconds", ctypes.c_double), ("recv_io_cpu_seconds", ctypes.c_double)]
 
     def as_dict(self) -> dict:
         d = {f: getattr(self, f) for f, _ in self._fields_ if f != "reserved"}
         d["GBps_recv"] = self.bytes_recv / self.seconds / 1e9 if self.seconds > 0 else 0.0
         # receive-thread CPU per GiB received: what verifying on the GPU saves (or costs) the host
-        d["recv_cpu_s_per_GiB"] = self.recv_cpu_seconds / (self.bytes_recv / (1 << 30)) if self.bytes_recv else 0.0
+        gib = self.bytes_recv / (1 << 30)
+        d["recv_cpu_s_per_GiB"] = self.recv_cpu_seconds / gib if self.bytes_recv else 0.0
+        # ... split into the socket calls and the rest (the pattern: CompleteIo, verify, batch bookkeeping)
+        d["recv_io_cpu_s_per_GiB"] = self.recv_io_cpu_seconds / gib if self.bytes_recv else 0.0
+        d["recv_pattern_cpu_s_per_GiB"] = d["recv_cpu_s_per_GiB"] - d["recv_io_cpu_s_per_GiB"]
         return d
 
 

@@ -69,6 +69,9 @@ typedef struct cts_loopback_result {
                                        PushPull), the async functor's recv workers -- recv() copies, CompleteIo
                                        and VerifyBuffer (ctsSendRecvIocp.cpp:60,97 run it on the IOCP thread) */
     double send_cpu_seconds;        /* the same for the threads that ran the data sends */
+    double recv_io_cpu_seconds;     /* the part of recv_cpu_seconds spent inside the socket calls (recv() and, on a
+                                       sync side thread, send()); the rest ran in the pattern: InitiateIo,
+                                       CompleteIo, VerifyBuffer / the DEFERRED batch bookkeeping and launches */
 } cts_loopback_result;
 
 /* Runs cfg->connections loopback connections to completion. engine may be NULL

@@ -58,6 +58,21 @@ def test_loopback_gpu(engine, mode):
     assert r["data_errors"] == 1 and r["connections_ok"] == 3
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("wait", ["0", "1", "2"], ids=["spin", "event", "sleep_poll"])
+def test_loopback_deferred_retire_waits_gpu(engine, wait, monkeypatch):
+    """Every way DEFERRED's Retire can wait for the in-flight batch (CTS_DEFERRED_BLOCKING_SYNC, read when a pattern is
+    created; 2 = sleep between event queries, the default) gives the same outcome: clean connections complete, the
+    corrupt one fails with exactly one DataError, and every buffer of the clean ones was verified."""
+    monkeypatch.setenv("CTS_DEFERRED_BLOCKING_SYNC", wait)
+    n, total = 4, 8 * 1024 * 1024
+    r = loopback.run(connections=n, buffer_size=65536, transfer_size=total, engine=engine,
+                     verify_mode=A.VERIFY_DEFERRED, batch_buffers=16, recv_whole=True,
+                     corrupt_connection=3, corrupt_send_index=50)
+    assert (r["connections_ok"], r["connections_failed"], r["data_errors"]) == (n - 1, 1, 1)
+    assert r["buffers_verified"] >= (n - 1) * total // 65536
+
+
 def test_loopback_with_c_oracle_hook():
     """The CPU baseline's arrangement: the oracle's C entry point as the pattern's verifier."""
     shared_buffer_attach(_SENDER)
@@ -95,6 +110,11 @@ def test_loopback_thread_cpu_accounting():
     assert r["recv_cpu_seconds"] >= 0.002 * calls * 0.9, (r["recv_cpu_seconds"], calls)
     assert r["send_cpu_seconds"] < 0.002 * calls / 2
     assert r["recv_cpu_s_per_GiB"] == pytest.approx(r["recv_cpu_seconds"] / (r["bytes_recv"] / (1 << 30)))
+    # the split: the socket calls' share, and the rest (here the spinning verifier) in the pattern's share
+    for x in (off, r):
+        assert 0 < x["recv_io_cpu_seconds"] <= x["recv_cpu_seconds"] * 1.01
+    assert r["recv_pattern_cpu_s_per_GiB"] * r["bytes_recv"] / (1 << 30) >= 0.002 * calls * 0.9
+    assert r["recv_io_cpu_seconds"] < r["recv_cpu_seconds"] - 0.002 * calls * 0.9
 
 
 # ---- PushPull (sync functor) and Duplex (async functor: a send and a recv in flight per side) -----------------

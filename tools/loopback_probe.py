@@ -18,7 +18,7 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("--rounds", type=int, default=2)
     p.add_argument("--gib", type=int, default=1)
-    p.add_argument("--cases", default="all", choices=["all", "deferred_sync_ab"])
+    p.add_argument("--cases", default="all", choices=["all", "deferred_sync_ab", "cpu_split", "query_period"])
     args = p.parse_args()
     eng = Engine(0)
     S = oracle.sender_buffer(65536)
@@ -30,7 +30,23 @@ def main():
                  ("cpu_oracle_sync", dict(verifier=hook, verify_mode=PA.VERIFY_SYNC)),
                  ("gpu_deferred_spin", dict(engine=eng, _env={"CTS_DEFERRED_BLOCKING_SYNC": "0"})),
                  ("gpu_deferred_blocking", dict(engine=eng, _env={"CTS_DEFERRED_BLOCKING_SYNC": "1"})),
+                 ("gpu_deferred_sleep_poll", dict(engine=eng, _env={"CTS_DEFERRED_BLOCKING_SYNC": "2"})),
                  ("gpu_sync_mailbox", dict(engine=eng, verify_mode=PA.VERIFY_SYNC))]
+    elif args.cases == "cpu_split":
+        # where a receive thread's CPU goes (socket calls vs the pattern), per arrangement
+        cases = [("no_verify", dict(verify=False)),
+                 ("cpu_oracle_sync", dict(verifier=hook, verify_mode=PA.VERIFY_SYNC)),
+                 ("cpu_oracle_deferred_b1024", dict(verifier=hook, verify_mode=PA.VERIFY_DEFERRED, batch_buffers=1024)),
+                 ("gpu_deferred_b1024", dict(engine=eng, batch_buffers=1024)),
+                 ("gpu_deferred_b4096", dict(engine=eng, batch_buffers=4096)),
+                 ("gpu_sync_mailbox", dict(engine=eng, verify_mode=PA.VERIFY_SYNC))]
+    elif args.cases == "query_period":
+        # the DEFERRED early retire's hipEventQuery: how much receive-thread CPU it costs per GiB
+        cases = [("no_verify", dict(verify=False)),
+                 ("cpu_oracle_sync", dict(verifier=hook, verify_mode=PA.VERIFY_SYNC))]
+        cases += [("gpu_deferred_b1024_q%s" % q, dict(engine=eng, batch_buffers=1024,
+                                                     _env={"CTS_DEFERRED_QUERY_PERIOD": q}))
+                  for q in ("16", "0", "256")]
     else:
         cases = None
     cases = cases or [("no_verify", dict(verify=False)),
@@ -56,6 +72,7 @@ def main():
                 os.environ.pop(k)
             print(json.dumps({"round": r, "case": name, "GBps_recv": round(res["GBps_recv"], 2),
                               "recv_cpu_s_per_GiB": round(res["recv_cpu_s_per_GiB"], 4),
+                              "recv_pattern_cpu_s_per_GiB": round(res["recv_pattern_cpu_s_per_GiB"], 4),
                               "connections_ok": res["connections_ok"], "data_errors": res["data_errors"]}),
                   flush=True)
     eng.close()
