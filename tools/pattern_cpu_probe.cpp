@@ -1,6 +1,6 @@
 // pattern_cpu_probe.cpp — receive-thread CPU inside the ctsIoPattern calls, without sockets: a Push server
 // pattern (ctsIOPattern.cpp:796-886) receives `gib` GiB in 64 KiB completions whose bytes are copied from the
-// shared sender buffer (the copy stands in for recv() and is not timed). Every cts_io_pattern_initiate_io and
+// shared sender buffer (the copy stands in for recv(); it is timed on its own: copy_cpu_s_per_GiB). Every cts_io_pattern_initiate_io and
 // cts_io_pattern_complete_io call is bracketed with CLOCK_THREAD_CPUTIME_ID; completions that took more than
 // 20 us are tallied apart (the DEFERRED batch rotations: retire + launch). One JSON line per run.
 //   build: make tools/pattern_cpu_probe
@@ -32,7 +32,7 @@ static double wall_now()
 }
 
 struct Run {
-    double t_init = 0, t_complete = 0, t_slow = 0;
+    double t_init = 0, t_complete = 0, t_slow = 0, t_copy = 0;
     uint64_t n_complete = 0, n_slow = 0, recvs = 0, bytes = 0, verified = 0;
     int st = CTS_IO_CONTINUE;
     uint32_t last_error = 0;
@@ -73,7 +73,9 @@ static void run_one(cts_engine* e, const char* mode, uint64_t gib, uint32_t batc
             if (r.bytes >= c.transfer_size) {
                 done = 0;  // the transfer is in: the client's FIN after the server's DONE
             } else {
+                const double m0 = cpu_now();
                 std::memcpy(t.buffer + t.buffer_offset, sender + t.expected_pattern_offset, t.buffer_length);
+                r.t_copy += cpu_now() - m0;
                 ++r.recvs;
                 r.bytes += t.buffer_length;
             }
@@ -128,6 +130,7 @@ int main(int argc, char** argv)
         r.t_init += x.t_init;
         r.t_complete += x.t_complete;
         r.t_slow += x.t_slow;
+        r.t_copy += x.t_copy;
         r.n_complete += x.n_complete;
         r.n_slow += x.n_slow;
         r.recvs += x.recvs;
@@ -140,11 +143,11 @@ int main(int argc, char** argv)
     std::printf("{\"mode\": \"%s\", \"batch_buffers\": %u, \"threads\": %u, \"status\": %d, \"last_error\": %u, "
                 "\"recvs\": %llu, \"buffers_verified\": %llu, \"wall_s\": %.4f, \"initiate_cpu_s_per_GiB\": %.5f, "
                 "\"complete_cpu_s_per_GiB\": %.5f, \"complete_us_mean\": %.3f, \"slow_completes\": %llu, "
-                "\"slow_cpu_s_per_GiB\": %.5f, \"complete_us_mean_fast\": %.3f}\n",
+                "\"slow_cpu_s_per_GiB\": %.5f, \"complete_us_mean_fast\": %.3f, \"copy_cpu_s_per_GiB\": %.5f}\n",
                 mode, batch, threads, st, r.last_error, (unsigned long long)r.recvs, (unsigned long long)r.verified,
                 wall, r.t_init / g, r.t_complete / g, 1e6 * r.t_complete / (double)r.n_complete,
                 (unsigned long long)r.n_slow, r.t_slow / g,
-                1e6 * (r.t_complete - r.t_slow) / (double)(r.n_complete - r.n_slow));
+                1e6 * (r.t_complete - r.t_slow) / (double)(r.n_complete - r.n_slow), r.t_copy / g);
     cts_shared_buffer_release();
     cts_engine_destroy(e);
     return st == CTS_IO_COMPLETED ? 0 : 2;
