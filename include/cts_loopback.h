@@ -71,7 +71,9 @@ typedef struct cts_loopback_result {
     double send_cpu_seconds;        /* the same for the threads that ran the data sends */
     double recv_io_cpu_seconds;     /* the part of recv_cpu_seconds spent inside the socket calls (recv() and, on a
                                        sync side thread, send()); the rest ran in the pattern: InitiateIo,
-                                       CompleteIo, VerifyBuffer / the DEFERRED batch bookkeeping and launches */
+                                       CompleteIo, VerifyBuffer / the DEFERRED batch bookkeeping and launches
+                                       (each socket call is bracketed by two CLOCK_THREAD_CPUTIME_ID reads, a few
+                                       hundred ns that land in both shares alike in every arrangement) */
 } cts_loopback_result;
 
 /* Runs cfg->connections loopback connections to completion. engine may be NULL
