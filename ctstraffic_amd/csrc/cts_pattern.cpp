@@ -352,6 +352,7 @@ struct cts_io_pattern {
             (void)cts_engine_stream_destroy(engine, stream);
         }
         if (inflight_done) (void)hipEventDestroy(inflight_done);
+        if (sync_done) (void)hipEventDestroy(sync_done);
         // ~RioBufferId (ctsIOPattern.h:230-238) for every id this pattern registered
         if (!rio_owned.empty()) {
             std::lock_guard<std::mutex> lk(g_rio.mu);
@@ -921,6 +922,25 @@ struct cts_io_pattern {
         return cts_verify(engine, arena, bytes, reinterpret_cast<cts_buf_desc*>(stage_desc.dev) + half,
                           (uint32_t)queue.size(), maxlen, reinterpret_cast<cts_verify_result*>(stage_res.dev) + half,
                           nullptr, nullptr, 0, stream);
+    }
+
+    // Waits for everything enqueued on the pattern's stream. With retire_wait 2 it sleeps in `step_us` steps between
+    // non-blocking queries of an event recorded behind the work (the runtime's own waits spin first).
+    hipEvent_t sync_done = nullptr;
+    hipError_t SleepSync(uint32_t step_us)
+    {
+        if (retire_wait != 2) return hipStreamSynchronize(stream);
+        if (sync_done == nullptr && hipEventCreateWithFlags(&sync_done, hipEventDisableTiming) != hipSuccess) {
+            sync_done = nullptr;
+            return hipStreamSynchronize(stream);
+        }
+        hipError_t rc = hipEventRecord(sync_done, stream);
+        if (rc != hipSuccess) return rc;
+        for (;;) {
+            rc = hipEventQuery(sync_done);
+            if (rc != hipErrorNotReady) return rc;
+            std::this_thread::sleep_for(std::chrono::microseconds(step_us));
+        }
     }
 
     hipError_t WaitInflight()
@@ -1522,7 +1542,8 @@ struct MediaStreamClient : cts_io_pattern {
              hipMemcpyAsync(ms_frame_bytes.host, d_fbytes, sizeof(uint64_t) * (uint64_t)w.frames, hipMemcpyDeviceToHost,
                             stream) != hipSuccess))
             rc = CTS_E_HIP;
-        if (rc != CTS_OK || hipStreamSynchronize(stream) != hipSuccess) throw DeviceError{rc != CTS_OK ? rc : CTS_E_HIP};
+        // a short kernel (one render tick's datagrams) behind a launch: sleep rather than spin while it runs
+        if (rc != CTS_OK || SleepSync(20) != hipSuccess) throw DeviceError{rc != CTS_OK ? rc : CTS_E_HIP};
         cts_frame_totals t{};
         (void)cts_frame_totals_fold(ms_totals.host, &t);
         if (t.exceptions == 0 && t.datagrams == n) {
