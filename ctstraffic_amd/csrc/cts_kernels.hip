@@ -632,6 +632,33 @@ __device__ __forceinline__ void block_reduce_mismatch(uint32_t& first, uint32_t&
     block_reduce_mismatch_with(first, count, red);
 }
 
+// the same for a BS-thread workgroup (tuning: verify_wg_kernel with BS != kBlock)
+template <int BS>
+__device__ __forceinline__ void block_reduce_mismatch_bs(uint32_t& first, uint32_t& count)
+{
+    if constexpr (BS == kBlock) {
+        block_reduce_mismatch(first, count);
+    } else {
+        __shared__ uint32_t red[2 * (BS / 64)];
+        const uint32_t wave = threadIdx.x / 64;
+        first = wave_min(first);
+        count = wave_sum(count);
+        if ((threadIdx.x & 63) == 0) {
+            red[wave] = first;
+            red[BS / 64 + wave] = count;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+#pragma unroll
+            for (int w = 1; w < BS / 64; ++w) {
+                first = red[w] < first ? red[w] : first;
+                count += red[BS / 64 + w];
+            }
+        }
+        __syncthreads();
+    }
+}
+
 // Wave 0 writes the m result records staged in LDS (record j belongs to buffer idx[j]) as dwords, one
 // store instruction for up to 21 records.
 template <int R>
@@ -666,8 +693,8 @@ __device__ __forceinline__ void flush_staged_results(const cts_verify_result* st
 // the workgroups still running once others have finished keep more bytes in flight (the launch's
 // finishing window, DESIGN.md §3 "Where a 256 MiB launch's last few percent go").
 template <int U, bool NT, bool SPLIT = false, bool SCTR = false, bool WHOLE = false, bool XD = false, int WIN = 1,
-          int DEFER = 0, int UT = 0>
-__global__ void __launch_bounds__(kBlock, (U <= 8 ? 8 : 4))
+          int DEFER = 0, int UT = 0, int BS = kBlock>
+__global__ void __launch_bounds__(BS, (BS == kBlock ? (U <= 8 ? 8 : 4) : 2048 / BS))
     verify_wg_kernel(const uint8_t* __restrict__ arena, uint64_t arena_bytes, const cts_buf_desc* __restrict__ descs,
                      uint32_t n, cts_verify_result* __restrict__ results, uint64_t* __restrict__ counters,
                      uint32_t* __restrict__ conn_first_fail, uint32_t n_conns)
@@ -720,26 +747,26 @@ __global__ void __launch_bounds__(kBlock, (U <= 8 ? 8 : 4))
         uint32_t first = kNone, count = 0;
         bool dirty;
         if (span_giant(s)) {  // >= 2 GiB: 64-bit exact pass
-            scan_giant_exact<kBlock, NT>(s, lane, first, count);
+            scan_giant_exact<BS, NT>(s, lane, first, count);
             dirty = __builtin_amdgcn_readfirstlane(__syncthreads_or(first != kNone)) != 0;
-            if (dirty) block_reduce_mismatch(first, count);
+            if (dirty) block_reduce_mismatch_bs<BS>(first, count);
         } else if (XD && __builtin_amdgcn_readfirstlane(span_whole_lines(s) ? 1u : 0u)) {
             // whole-line span, exact diff in registers: only the reduction is left
             if (UT > 0 && (uint64_t)i + step >= end)
-                scan_whole_exact<kBlock, (UT > 0 ? UT : U), NT, SPLIT>(s, lane, first, count);
+                scan_whole_exact<BS, (UT > 0 ? UT : U), NT, SPLIT>(s, lane, first, count);
             else
-                scan_whole_exact<kBlock, U, NT, SPLIT>(s, lane, first, count);
+                scan_whole_exact<BS, U, NT, SPLIT>(s, lane, first, count);
             dirty = __builtin_amdgcn_readfirstlane(__syncthreads_or(first != kNone)) != 0;
-            if (dirty) block_reduce_mismatch(first, count);
+            if (dirty) block_reduce_mismatch_bs<BS>(first, count);
         } else {
-            const uint32_t acc = scan_buffer<kBlock, U, NT, SPLIT, WHOLE>(s, lane);
+            const uint32_t acc = scan_buffer<BS, U, NT, SPLIT, WHOLE>(s, lane);
             dirty = __builtin_amdgcn_readfirstlane(__syncthreads_or(acc != 0u)) != 0;
             if (dirty) {  // rare: exact re-scan by the dirty lanes + reduction
                 if (acc != 0u) {
-                    if (WHOLE && span_whole_lines(s)) scan_exact_whole<kBlock, 2, NT>(s, lane, first, count);
-                    else scan_exact_owned<kBlock, 2, NT>(s, lane, first, count);
+                    if (WHOLE && span_whole_lines(s)) scan_exact_whole<BS, 2, NT>(s, lane, first, count);
+                    else scan_exact_owned<BS, 2, NT>(s, lane, first, count);
                 }
-                block_reduce_mismatch(first, count);
+                block_reduce_mismatch_bs<BS>(first, count);
             }
         }
         if constexpr (SCTR) {
@@ -2507,6 +2534,11 @@ static void launch_verify_nt(const uint8_t* arena, uint64_t arena_bytes, const c
         case 18: verify_wg_kernel<2, NT, true, false, true, true, 1, 16><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 19: verify_wg_kernel<2, NT, true, false, true, true, 1, 0, 4><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 20: verify_wg_kernel<2, NT, true, false, true, true, 1, 0, 8><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
+        // 21: variant 13 with 512-thread workgroups (each 64 KiB buffer streams in half the time, so the launch's
+        // finishing window is cut in whole buffers half as long); the grid cap is blocks_per_cu / 2 workgroups per CU
+        case 21: verify_wg_kernel<2, NT, true, false, true, true, 1, 0, 0, 2 * kBlock>
+                     <<<grid_for(n, 1, geo, std::max(1, geo.blocks_per_cu / 2)), 2 * kBlock, 0, stream>>>(CTS_VERIFY_ARGS);
+                 break;
         case 7: verify_wg_kernel<4, NT, true><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 1: verify_wg_kernel<4, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 2: verify_wg_kernel<16, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
