@@ -17,6 +17,7 @@
 #include <mutex>
 #include <new>
 #include <string>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -239,7 +240,11 @@ struct Mailbox {
         if (!free_at) return CTS_E_NOMEM;
         ResetRings();
         last_post = std::chrono::steady_clock::now();
-        watchdog = std::thread([this] { Watch(); });
+        try {  // nothing may cross the C ABI: a thread that cannot start leaves the engine on the launch path
+            watchdog = std::thread([this] { Watch(); });
+        } catch (const std::system_error&) {
+            return CTS_E_NOMEM;
+        }
         return CTS_OK;
     }
 
@@ -902,9 +907,9 @@ int cts_counters_read(cts_engine* e, const void* dev_counters, cts_counters* out
     if (e == nullptr || dev_counters == nullptr || out == nullptr) return CTS_E_INVALID;
     DeviceGuard g(e->device);
     if (!g.ok) return CTS_E_HIP;
-    std::vector<uint64_t> h(CTS_COUNTER_SHARDS * cts::kCounterSlots);
+    uint64_t h[CTS_COUNTER_SHARDS * cts::kCounterSlots];  // 4 KiB: no allocation on the ABI path
     hipStream_t s = static_cast<hipStream_t>(stream);
-    if (hipMemcpyAsync(h.data(), dev_counters, cts_counters_device_bytes(), hipMemcpyDeviceToHost, s) != hipSuccess)
+    if (hipMemcpyAsync(h, dev_counters, cts_counters_device_bytes(), hipMemcpyDeviceToHost, s) != hipSuccess)
         return CTS_E_HIP;
     if (hipStreamSynchronize(s) != hipSuccess) return CTS_E_HIP;
     uint64_t v[5] = {0, 0, 0, 0, 0};
@@ -988,8 +993,16 @@ int cts_verify_host(cts_engine* e, const void* host_buf, uint32_t len, uint32_t 
             rc = cts_verify_mapped(e, dev, len, expected_offset, out);
         }
         if (st.p != nullptr) {
-            std::lock_guard<std::mutex> lk(e->stage_pool_mu);
-            e->stage_pool.push_back(st);
+            bool pooled = false;
+            {
+                std::lock_guard<std::mutex> lk(e->stage_pool_mu);
+                try {
+                    e->stage_pool.push_back(st);
+                    pooled = true;
+                } catch (const std::bad_alloc&) {  // nothing may cross the C ABI: the stage is freed instead
+                }
+            }
+            if (!pooled) pinned_free(e, st.p);
         }
         return rc;
     }

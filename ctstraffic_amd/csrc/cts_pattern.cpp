@@ -23,6 +23,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <memory>
 #include <mutex>
 #include <new>
@@ -1683,6 +1684,12 @@ struct MediaStreamClient : cts_io_pattern {
             } catch (const FailFast& f) {  // nothing may leave the timer thread
                 if (fail_fast.empty()) fail_fast = f.reason;
                 m_lastError = CTS_PATTERN_E_FAIL_FAST;
+            } catch (const DeviceError& d) {
+                if (fail_fast.empty()) fail_fast = "a timer callback failed (status " + std::to_string(d.rc) + ")";
+                m_lastError = CTS_PATTERN_E_FAIL_FAST;
+            } catch (const std::exception& e) {  // e.g. bad_alloc growing a queue: latched, never std::terminate
+                if (fail_fast.empty()) fail_fast = std::string("a timer callback threw: ") + e.what();
+                m_lastError = CTS_PATTERN_E_FAIL_FAST;
             }
         }
     }
@@ -2085,6 +2092,8 @@ int cts_io_pattern_flush(cts_io_pattern* p)
         return CTS_IO_FAILED;
     } catch (const DeviceError& d) {
         return d.rc;
+    } catch (const std::bad_alloc&) {
+        return CTS_E_NOMEM;
     }
 }
 
@@ -2161,6 +2170,10 @@ int cts_io_pattern_media_stream_fire(cts_io_pattern* p, int timer)
     } catch (const FailFast& f) {
         latch_fail_fast(p, f);
         return CTS_OK;
+    } catch (const DeviceError& d) {
+        return d.rc;
+    } catch (const std::bad_alloc&) {  // nothing may cross the C ABI
+        return CTS_E_NOMEM;
     }
 }
 
