@@ -25,6 +25,7 @@
 #include <ctime>
 #include <deque>
 #include <mutex>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -458,11 +459,18 @@ extern "C" int cts_loopback_run_detailed(const cts_loopback_config* cfg, cts_eng
     }
     std::vector<bool> connected0(2 * n);
     for (uint32_t i = 0; i < 2 * n; ++i) connected0[i] = fds[i] >= 0;
+    threads.reserve(2 * n);
     for (uint32_t i = 0; i < 2 * n; ++i) {
         if (fds[i] < 0) continue;
         const bool inject = i % n == cfg->corrupt_connection;  // whichever side(s) send data
-        threads.emplace_back(async ? run_side_async : run_side, &fds[i], pats[i], inject, cfg->corrupt_send_index,
-                             cfg->recv_whole != 0, &res[i]);
+        try {
+            threads.emplace_back(async ? run_side_async : run_side, &fds[i], pats[i], inject, cfg->corrupt_send_index,
+                                 cfg->recv_whole != 0, &res[i]);
+        } catch (const std::system_error&) {
+            // no thread for this side: its connection fails (the peer sees the reset), the others run on
+            ::shutdown(fds[i], SHUT_RDWR);
+            connected0[i] = false;
+        }
     }
     const std::vector<bool>& connected = connected0;
     for (auto& t : threads) t.join();
