@@ -21,6 +21,7 @@
 #include <chrono>
 #include <cstring>
 #include <deque>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -264,10 +265,23 @@ extern "C" int cts_loopback_media_stream_run(const cts_media_stream_loopback_con
         (void)cts_udp_status_details_read(&before);
         std::vector<std::thread> threads;
         const auto t0 = Clock::now();
+        threads.reserve(2 * n);
         for (uint32_t i = 0; i < n; ++i) {
-            threads.emplace_back(run_server, &conns[i], cfg->frame_size_bytes, max_dgram, i == cfg->corrupt_connection,
-                                 cfg->corrupt_datagram);
-            threads.emplace_back(run_client, &conns[i]);
+            // a side whose thread cannot start fails its connection, never std::terminate: a server without its
+            // client gives up on START after 5 s; a client without its server drops every frame and finishes
+            try {
+                threads.emplace_back(run_server, &conns[i], cfg->frame_size_bytes, max_dgram,
+                                     i == cfg->corrupt_connection, cfg->corrupt_datagram);
+            } catch (const std::system_error&) {
+                conns[i].socket_error = true;
+                conns[i].server_status = CTS_IO_FAILED;
+            }
+            try {
+                threads.emplace_back(run_client, &conns[i]);
+            } catch (const std::system_error&) {
+                // (the server thread may be running: nothing is written here; client_status never reaches
+                // CTS_IO_COMPLETED, so the connection counts as failed)
+            }
         }
         for (auto& t : threads) t.join();
         auto t1 = t0;
