@@ -532,7 +532,9 @@ def main():
                 "host_numa_node": engine.numa_node() if near else None,
                 "host_cpus_pinned": len(near),
                 "parallelism": "%d rank(s), one config-2 batch of its own connections each, no data-path "
-                               "collective; RCCL all-reduce of the 5 counters closes the timed region" % world,
+                               "collective; %s" % (world, "one rank: no collective" if world == 1 else
+                                                   "%s all-reduce of the 5 counters closes the timed region"
+                                                   % ("RCCL" if args.dist_backend == "nccl" else args.dist_backend)),
             },
             "roofline": {
                 "bound": "hbm",
