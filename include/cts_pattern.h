@@ -307,7 +307,9 @@ const char* cts_io_pattern_connection_id(cts_io_pattern* pattern);
  * (SendTaskToCallback, :333-339): a "START" send (5 bytes, untracked, STATIC) every 500 ms + one frame until
  * a frame arrived, Abort when the stream rendered its final frame, FatalAbort when nothing ever arrived. The
  * callback runs with the pattern's lock held and may call cts_io_pattern_complete_io on the task (the
- * reference functor completes Abort / FatalAbort from inside it, ctsMediaStreamClient.cpp:317-331). */
+ * reference functor completes Abort / FatalAbort from inside it, ctsMediaStreamClient.cpp:317-331). It must
+ * not call cts_io_pattern_destroy: destroy joins the timer thread the callback runs on (as the reference's
+ * destructor waits for its threadpool timer callbacks); destroy from another thread once it has returned. */
 typedef void (*cts_task_callback)(void* ctx, const cts_task* task);
 int cts_io_pattern_register_callback(cts_io_pattern* pattern, cts_task_callback fn, void* ctx);
 
