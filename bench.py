@@ -39,6 +39,7 @@ import time
 
 import numpy as np
 
+ENGINES_LEG_CAP_S = 300  # the single-process leg (a child process) normally takes ~20 s
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 GIB = float(1 << 30)
 METRIC = "GiB/s verified, 64 KiB buffers device-resident; % MI355X HBM roofline"
@@ -90,6 +91,15 @@ def parse():
     p.add_argument("--stub-gpu", action="store_true",
                    help="launcher test: every rank reports its RANK/WORLD_SIZE over gloo and rank 0 prints one line; "
                         "nothing touches a GPU (tests/test_bench_launcher.py)")
+    p.add_argument("--dist-timeout", type=float, default=600.0,
+                   help="seconds any collective or barrier may wait at N > 1 (process-group timeout). Above rank 0's "
+                        "work after the timed region, which the other ranks wait out at a barrier: the CPU baseline "
+                        "(~1 min) and the single-process leg (capped at %d s). A rank that stalls longer or dies makes "
+                        "the others raise; a rank that raises exits non-zero, and the launcher with it" % ENGINES_LEG_CAP_S)
+    p.add_argument("--stub-fail-rank", type=int, default=-1,
+                   help="with --stub-gpu: this rank fails (tests/test_bench_launcher.py)")
+    p.add_argument("--stub-fail-mode", choices=["raise", "stall"], default="raise",
+                   help="with --stub-fail-rank: raise before the all-gather, or sleep past --dist-timeout")
     return p.parse_args()
 
 
@@ -147,7 +157,11 @@ def stub_main(args):
     world, rank, local = D.dist_env()
     if world > 1:
         with _StdoutToStderr():
-            D.init("gloo")
+            D.init("gloo", timeout_s=args.dist_timeout)
+    if rank == args.stub_fail_rank:
+        if args.stub_fail_mode == "raise":
+            raise RuntimeError("bench.py --stub-fail-rank %d: this rank fails" % rank)
+        time.sleep(args.dist_timeout * 20)  # stall: the others time out at the all-gather
     me = torch.tensor([rank, world, local], dtype=torch.int64)
     seen = [torch.zeros_like(me) for _ in range(world)]
     if world > 1:
@@ -171,9 +185,10 @@ def engines_leg(args, world):
            "--steps", str(args.steps), "--warmup", str(args.warmup), "--arenas", str(args.arenas),
            "--buffers", str(args.buffers), "--pipeline-streams", str(args.pipeline_streams)]
     try:
-        r = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=600)
+        r = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                           timeout=ENGINES_LEG_CAP_S)
     except subprocess.TimeoutExpired:
-        return {"error": "timed out after 600 s"}
+        return {"error": "timed out after %d s" % ENGINES_LEG_CAP_S}
     lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
     if r.returncode != 0 or not lines:
         return {"error": "exit %d: %s" % (r.returncode, r.stderr.strip().splitlines()[-1:] or "")}
@@ -269,10 +284,11 @@ def main():
     cpu_group = None
     if world > 1:
         with _StdoutToStderr():
-            D.init(args.dist_backend, device=torch.device(dev) if args.dist_backend == "nccl" else None)
+            D.init(args.dist_backend, device=torch.device(dev) if args.dist_backend == "nccl" else None,
+                   timeout_s=args.dist_timeout)
             # host-side waits (while rank 0 runs the CPU baseline and the single-process leg) go over gloo, so
             # the waiting ranks hold no spinning collective kernel on their GPUs
-            cpu_group = dist.new_group(backend="gloo")
+            cpu_group = D.new_cpu_group(timeout_s=args.dist_timeout)
 
     # --verify-variant: A/B runs use the tuning build (every launch variant); the product runs variant 13
     engine = Engine(gpu, tuning=args.verify_variant >= 0)
@@ -489,6 +505,9 @@ def main():
         if not args.no_cpu_baseline:
             # at every N: the reference's CPU verify beside the GPU number (rank 0's host, rank 0's batch)
             cpu = cpu_baseline(B.arenas[0], w, args.cpu_seconds)
+            # config 3 and the MediaStream receive on the CPU, beside the datagram extras' GPU numbers
+            cpu["config3"] = cpu_baseline_config3(W, max(1.0, args.cpu_seconds / 2))
+            cpu["loopback_media_stream_oracle"] = loopback_media_stream_oracle()
         if not (args.no_engines_leg or args.no_extras or args.extras_only):
             if world <= torch.cuda.device_count():
                 extras["engines_single_process"] = engines_leg(args, world)
@@ -940,6 +959,80 @@ def run_extras(engine, torch, W, w, arenas, descs, dev, want):
     return out
 
 
+def _cpu_threads():
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except Exception:  # pragma: no cover
+        avail = os.cpu_count() or 1
+    return avail, sorted({1, min(16, avail)})
+
+
+def cpu_baseline_config3(W, seconds, n_datagrams=1 << 20, ring=16 * 1024 * 1024):
+    """Config 3 on the CPU: the oracle's VerifyBuffer with the MediaStream client's arguments (skip the 26-byte
+    header, expected pattern offset 0: ctsIOPatternMediaStream.cpp:185-192) over the first `n_datagrams` of the
+    16 M x 1472 B ring in host memory (the datagram extras' ring: same layout, headers and corruption plan, restricted
+    to the slice), on 1 and 16 threads, ~`seconds` per leg. GiB/s of payload, as the GPU's datagram numbers."""
+    import oracle
+
+    full = W.udp_datagrams(n_datagrams=ring)  # the ring's descriptors and corruption plan (host arrays only)
+    keep = full.corrupt_buf < n_datagrams
+    ws = W.Workload("config3_slice", full.descs[:n_datagrams].copy(), n_datagrams * int(full.max_length),
+                    full.max_length, full.corrupt_buf[keep], full.corrupt_pos[keep], full.corrupt_xor[keep],
+                    n_conns=1, datagram_headers=True)
+    del full
+    # the bytes as received: payloads from the sender's pattern, {flag 0, seq i + 1, 0, 0} headers, the corruptions
+    host = np.zeros(ws.arena_bytes, dtype=np.uint8)
+    oracle.fill(host, ws.descs)
+    host.reshape(n_datagrams, -1)[:, :W.UDP_DATA_HEADER_LENGTH] = W.header_bytes(np.arange(1, n_datagrams + 1))
+    host[ws.corrupt_abs_offsets()] ^= ws.corrupt_xor
+    _, _, exp_ctr, _ = W.expected_results(ws)
+    avail, counts = _cpu_threads()
+    legs, parity = {}, True
+    for nt in counts:
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            _, c, _ = oracle.verify_batch(host, ws.descs, nthreads=nt, want_results=False)
+            parity &= c == exp_ctr
+            reps += 1
+            if time.perf_counter() - t0 >= seconds:
+                break
+        legs[nt] = ws.verified_bytes() * reps / (time.perf_counter() - t0) / GIB
+    best = max(legs, key=lambda k: legs[k])
+    return {"value": round(legs[best], 2), "unit": "GiB/s of payload", "cores": best, "kind": "port",
+            "sample": "config3 slice: the first %d of the 16 M x 1472 B datagrams (%d MiB host copy), oracle "
+                      "VerifyBuffer skip 26 / expected 0 per datagram, ~%.1f s per leg" %
+                      (n_datagrams, ws.arena_bytes >> 20, seconds),
+            "threads_GiBps": {str(k): round(v, 2) for k, v in legs.items()},
+            "single_thread_value": round(legs[1], 2), "counters_match_expected": bool(parity)}
+
+
+def loopback_media_stream_oracle():
+    """The MediaStream loopback run of the extras (16 UDP connections, README frame size 52083 B at 240 frames/s)
+    with the oracle as every client pattern's VerifyBuffer, per datagram on the receive thread: the reference's own
+    arrangement (ctsIOPatternMediaStream.cpp:185-192 on the IOCP thread). Receive-thread CPU per datagram beside the
+    GPU SYNC / DEFERRED legs (extras.loopback_media_stream_*)."""
+    import oracle
+    from ctstraffic_amd import _pattern_abi as PA
+    from ctstraffic_amd import loopback as LB
+    from ctstraffic_amd.pattern import shared_buffer_attach
+
+    try:
+        S = oracle.sender_buffer(65536)  # attached by pointer: kept alive for the run
+        shared_buffer_attach(S)
+        hook = PA.BATCH_VERIFIER(oracle.batch_verifier_address())
+        r = LB.media_stream_run(connections=16, frame_size=52083, frames_per_second=240, stream_length_frames=240,
+                                buffered_frames=60, verifier=hook, verify_mode=PA.VERIFY_SYNC)
+        c = r["clients"]
+        return {"connections_ok": r["connections_ok"], "data_errors": r["data_errors"],
+                "datagrams_received": r["datagrams_received"], "successful_frames": c["successful_frames"],
+                "dropped_frames": c["dropped_frames"], "payload_MBps": round(r["payload_MBps"], 1),
+                "recv_cpu_us_per_datagram": round(1e6 * r["recv_cpu_seconds"] / max(1, r["datagrams_received"]), 3),
+                "sample": "16 conns x 240 frames of 52083 B at 240 frames/s over loopback UDP, oracle VerifyBuffer "
+                          "(C) per datagram on each client's receive thread", "sender_buffer_bytes": int(S.size)}
+    except Exception as e:  # pragma: no cover
+        return {"error": repr(e)}
+
+
 def cpu_baseline(arena, w, seconds):
     """The oracle (g++/gcc restatement of VerifyBuffer, RtlCompareMemory semantics) on this host's
     cores over a host copy of the same batch. Bounded: ~`seconds` per leg."""
@@ -947,11 +1040,8 @@ def cpu_baseline(arena, w, seconds):
 
     host = arena.cpu().numpy()
     # 1 thread, 16 threads (this pool's CPU share per GPU) and every CPU this process may run on
-    try:
-        avail = len(os.sched_getaffinity(0))
-    except Exception:  # pragma: no cover
-        avail = os.cpu_count() or 1
-    counts = sorted({1, min(16, avail), avail})
+    avail, counts = _cpu_threads()
+    counts = sorted(set(counts) | {avail})
     legs = {}
     for nt in counts:
         reps, t0 = 0, time.perf_counter()

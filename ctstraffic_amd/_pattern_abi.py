@@ -100,6 +100,8 @@ class CtsPatternStats(ctypes.Structure):
         ("has_failure", ctypes.c_uint8),
         ("reserved", ctypes.c_uint8),
         ("fail_completion", ctypes.c_uint32),
+        ("bytes_sent_held", ctypes.c_uint64),
+        ("bytes_recv_held", ctypes.c_uint64),
     ]
 
     def as_dict(self) -> dict:

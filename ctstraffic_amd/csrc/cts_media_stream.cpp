@@ -104,7 +104,8 @@ struct cts_media_stream_client {
     void render_frame()
     {
         Frame& h = frames[head];
-        if (h.receiver_qpf != 0 && first_frame.receiver_qpf != 0) {
+        // frames booked from GPU batch sums (statuses, frame sums) carry no sender timestamps (qpf 0): no estimate
+        if (h.receiver_qpf != 0 && first_frame.receiver_qpf != 0 && h.sender_qpf != 0 && first_frame.sender_qpf != 0) {
             const double ms_since_first_receive = (double)h.receiver_qpc * 1000.0 / (double)h.receiver_qpf -
                                                   (double)first_frame.receiver_qpc * 1000.0 / (double)first_frame.receiver_qpf;
             const double ms_since_first_send = (double)h.sender_qpc * 1000.0 / (double)h.sender_qpf -

@@ -29,6 +29,7 @@
 #include <new>
 #include <random>
 #include <string>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -332,6 +333,8 @@ struct Queued {
     uint64_t bytes_recv_after;  // m_bytesRecv after this completion (as the reference would count it)
     uint64_t bytes_sent_after;  // m_bytesSent at that point (sends completed later are rolled back on failure)
     uint32_t expected;          // the task's m_expectedPatternOffset
+    uint64_t status_recv_after; // this pattern's TcpStatusDetails.m_bytesRecv contribution after this completion
+    uint64_t status_sent_after; // ... and its m_bytesSent contribution at that point
 };
 
 }  // namespace
@@ -400,6 +403,34 @@ struct cts_io_pattern {
 
     // statistics + verify bookkeeping
     uint64_t bytes_sent = 0, bytes_recv = 0;
+    // The reference's byte counters only ever Add (ctsStatistics.hpp:153-186; ctsIOPattern.cpp:505-521), and its
+    // status timer prints their SnapValueDifference (ctsStatistics.hpp:363). A DEFERRED pattern therefore holds back
+    // the bytes of every completion behind a recv whose verdict is not in yet: status_* is this pattern's running
+    // contribution to TcpStatusDetails, published_* what it has added to g_bytesSent/g_bytesRecv so far. A batch that
+    // verifies publishes up to its last buffer; a failing buffer publishes up to and including itself, and everything
+    // after it is dropped unpublished (the reference never saw it). Nothing published is ever taken back.
+    uint64_t status_sent = 0, status_recv = 0;
+    uint64_t published_sent = 0, published_recv = 0;
+    void Publish(uint64_t recv_to, uint64_t sent_to)
+    {
+        if (recv_to > published_recv) {
+            g_bytesRecv.fetch_add(recv_to - published_recv);
+            published_recv = recv_to;
+        }
+        if (sent_to > published_sent) {
+            g_bytesSent.fetch_add(sent_to - published_sent);
+            published_sent = sent_to;
+        }
+    }
+    // held back: completed, counted by the pattern, not yet published (only while a DEFERRED verdict is pending; every
+    // completion accepted meanwhile is a pattern-requested send/recv, so the per-connection counters hold back the same)
+    uint64_t HeldRecv() const { return status_recv - published_recv; }
+    uint64_t HeldSent() const { return status_sent - published_sent; }
+    bool VerdictsPending() const { return !queue.empty() || !inflight.empty(); }
+    void PublishIfSettled()
+    {
+        if (!VerdictsPending()) Publish(status_recv, status_sent);
+    }
     uint64_t buffers_verified = 0, bytes_verified = 0, buffers_failed = 0;
     uint64_t bytes_recv_at_failure = 0;
     uint32_t recv_completions = 0;
@@ -449,6 +480,7 @@ struct cts_io_pattern {
     // verified, so a batch is verified in place (no staging copy)
     bool ring = false, queue_in_ring = false;
     uint32_t ring_slots = 0, ring_next = 0;
+    uint32_t slot_bytes = 0;  // one recv buffer (RecvSlotBytes)
     char* ring_base = nullptr;
     uint64_t ring_bytes = 0;
 
@@ -495,6 +527,11 @@ struct cts_io_pattern {
     {
         return cfg.verify_buffers && t.io_action == CTS_TASK_RECV && t.track_io;
     }
+    // The bytes of one recv buffer (m_recvBufferContainer holds GetMaxBufferSize() per recv, ctsIOPattern.cpp:156-175).
+    // The MediaStream patterns never post a recv that large: their slots are sized to what they post.
+    virtual uint32_t RecvSlotBytes() const { return max_buffer_size; }
+    // Whether its recvs carry data to verify (a DEFERRED pattern that does gets the zero-copy recv ring)
+    virtual bool VerifiesRecvs() const { return cfg.verify_buffers != 0; }
     // MediaStream surface (cts_io_pattern_media_stream_*): CTS_E_INVALID for the TCP patterns
     virtual int FireTimer(int) { return CTS_E_INVALID; }
     virtual int Timers(int64_t*, int64_t*) { return CTS_E_INVALID; }
@@ -547,10 +584,10 @@ struct cts_io_pattern {
         if (ring) {
             ring_rio_ids.resize(ring_slots);
             for (uint32_t i = 0; i < ring_slots; ++i)
-                ring_rio_ids[i] = RioRegister(ring_base + (size_t)i * max_buffer_size, max_buffer_size);
+                ring_rio_ids[i] = RioRegister(ring_base + (size_t)i * slot_bytes, slot_bytes);
             for (const char* b : m_recvBufferFreeList) m_receivingRioBufferIds.push_back(ring_rio_ids[RingSlot(b)]);
         } else {
-            const uint32_t len = cfg.use_shared_buffer ? (uint32_t)g_shared.bytes : max_buffer_size;
+            const uint32_t len = cfg.use_shared_buffer ? (uint32_t)g_shared.bytes : slot_bytes;
             for (char* b : m_recvBufferFreeList) m_receivingRioBufferIds.push_back(RioRegister(b, len));
         }
         m_rioConnectionId = RioRegister(connection_id, CTS_CONNECTION_ID_LENGTH);
@@ -568,10 +605,11 @@ struct cts_io_pattern {
             for (auto& b : m_recvBufferFreeList) b = g_shared.receiver.data();
             return CTS_OK;
         }
-        ring = Deferred();
+        ring = Deferred() && VerifiesRecvs();
+        slot_bytes = RecvSlotBytes();
         // a slot is handed out again only after the (up to two) batches that may hold it were verified
         ring_slots = ring ? BatchCapacity() * (DoubleBuffered() ? 2u : 1u) + recvCount + 1 : recvCount;
-        const uint64_t bytes = (uint64_t)max_buffer_size * ring_slots;
+        const uint64_t bytes = (uint64_t)slot_bytes * ring_slots;
         char* base = nullptr;
         if (engine != nullptr && hook == nullptr) {
             const int rc = recv_pinned.alloc(engine, bytes ? bytes : 16);
@@ -581,14 +619,14 @@ struct cts_io_pattern {
             recv_plain.assign(bytes, 0);
             base = recv_plain.data();
         }
-        for (uint32_t i = 0; i < recvCount; ++i) m_recvBufferFreeList[i] = base + (size_t)i * max_buffer_size;
+        for (uint32_t i = 0; i < recvCount; ++i) m_recvBufferFreeList[i] = base + (size_t)i * slot_bytes;
         ring_base = base;
         ring_bytes = bytes;
         ring_next = recvCount;
         return CTS_OK;
     }
 
-    uint32_t RingSlot(const char* b) const { return (uint32_t)((size_t)(b - ring_base) / max_buffer_size); }
+    uint32_t RingSlot(const char* b) const { return (uint32_t)((size_t)(b - ring_base) / slot_bytes); }
 
     // the buffer (and its RIO id) to put back on the free lists after a completion
     // (ctsIOPattern.cpp:369-386): the completed one, or in ring mode the next ring slot (the
@@ -597,7 +635,7 @@ struct cts_io_pattern {
     {
         char* b = t.buffer;
         if (ring) {
-            b = ring_base + (size_t)(ring_next % ring_slots) * max_buffer_size;
+            b = ring_base + (size_t)(ring_next % ring_slots) * slot_bytes;
             ++ring_next;
         }
         m_recvBufferFreeList.push_back(b);
@@ -870,7 +908,8 @@ struct cts_io_pattern {
             if (rc != CTS_OK) return rc;
             cts_buf_desc* descs = hook ? hdesc.data() : StageDescs();
             descs[queue.size()] = cts_buf_desc{(uint64_t)(src - ring_base), transferred, t.expected_pattern_offset, 0, 0};
-            queue.push_back(Queued{recv_completions, transferred, recv_after, bytes_sent, t.expected_pattern_offset});
+            queue.push_back(Queued{recv_completions, transferred, recv_after, bytes_sent, t.expected_pattern_offset,
+                                status_recv, status_sent});
             queue_in_ring = true;
             return CTS_OK;
         }
@@ -906,7 +945,8 @@ struct cts_io_pattern {
         if (transferred) std::memcpy(base + stage_used, t.buffer + t.buffer_offset, transferred);
         cts_buf_desc* descs = hook ? hdesc.data() : StageDescs();
         descs[queue.size()] = cts_buf_desc{stage_used, transferred, t.expected_pattern_offset, 0, 0};
-        queue.push_back(Queued{recv_completions, transferred, recv_after, bytes_sent, t.expected_pattern_offset});
+        queue.push_back(Queued{recv_completions, transferred, recv_after, bytes_sent, t.expected_pattern_offset,
+                                status_recv, status_sent});
         stage_used += slot;
         return CTS_OK;
     }
@@ -968,6 +1008,7 @@ struct cts_io_pattern {
             queue.clear();
             stage_used = 0;
         }
+        PublishIfSettled();
         return CTS_OK;
     }
 
@@ -1014,15 +1055,16 @@ struct cts_io_pattern {
         ApplyVerdicts(queue, res);
         queue.clear();
         stage_used = 0;
+        PublishIfSettled();
         return GetCurrentStatus();
     }
 
     // Counts the verdicts of batch q; returns true if one of its buffers failed.
-        // The reference stops at the first failing buffer (its CompleteIo fails the connection on that
-        // completion, ctsIOPattern.cpp:486-489, and TCP verify allows one posted recv,
-        // ctsConfig.cpp:3440-3446). Buffers queued after it were never received there: they are neither
-        // counted as verified nor as received, and the sends that completed after it are taken back too,
-        // so every counter equals what the reference reports when it stops at that completion.
+    // The reference stops at the first failing buffer (its CompleteIo fails the connection on that
+    // completion, ctsIOPattern.cpp:486-489, and TCP verify allows one posted recv,
+    // ctsConfig.cpp:3440-3446). Buffers queued after it were never received there: they are neither
+    // counted as verified nor as received, and the sends that completed after it are dropped too,
+    // so every counter equals what the reference reports when it stops at that completion.
     bool ApplyVerdicts(const std::vector<Queued>& q, const cts_verify_result* res)
     {
         const uint32_t n = (uint32_t)q.size();
@@ -1037,24 +1079,33 @@ struct cts_io_pattern {
             ++buffers_verified;
             bytes_verified += q[i].transferred;
         }
-        if (bad == n) return false;
+        if (n == 0) return false;
+        if (bad == n) {
+            // every buffer of the batch verified: the bytes up to its last completion are the reference's
+            Publish(q[n - 1].status_recv_after, q[n - 1].status_sent_after);
+            return false;
+        }
         const Queued& f = q[bad];
         RecordFailure(f.completion, f.transferred, res[bad], f.bytes_recv_after);
+        // the failing completion's own bytes are counted (the reference adds them after VerifyBuffer failed,
+        // ctsIOPattern.cpp:505-516); nothing after it is
+        Publish(f.status_recv_after, f.status_sent_after);
         RollbackAfter(f);
         UpdateLastError(CTS_STATUS_ERROR_DATA_DID_NOT_MATCH_BIT_PATTERN);
         return true;
     }
 
-    // Undo the byte accounting (TcpStatusDetails, ctsStatistics, the pattern state and the recv
-    // pattern offset) of every completion after the failing buffer f (DEFERRED; see Flush).
+    // Drop the byte accounting (ctsStatistics, the pattern state and the recv pattern offset) of every
+    // completion after the failing buffer f (DEFERRED; see Flush). Those bytes were held back, never
+    // published to TcpStatusDetails, so the process-wide counters are not touched.
     void RollbackAfter(const Queued& f)
     {
         const uint64_t recv_undo = bytes_recv - f.bytes_recv_after;
         const uint64_t send_undo = bytes_sent - f.bytes_sent_after;
         bytes_recv = f.bytes_recv_after;
         bytes_sent = f.bytes_sent_after;
-        g_bytesRecv.fetch_sub(recv_undo);
-        g_bytesSent.fetch_sub(send_undo);
+        status_recv = f.status_recv_after;
+        status_sent = f.status_sent_after;
         state.RollbackConfirmed(recv_undo + send_undo);
         m_recvPatternOffset = (uint32_t)(((uint64_t)f.expected + f.transferred) % kPatternSize);
         recv_completions = f.completion + 1;
@@ -1142,8 +1193,9 @@ struct cts_io_pattern {
         }
 
         if (t.io_action != CTS_TASK_NONE && status == kNoError) {
-            if (t.io_action == CTS_TASK_SEND) g_bytesSent.fetch_add(transfer);
-            else if (t.io_action == CTS_TASK_RECV) g_bytesRecv.fetch_add(transfer);
+            // TcpStatusDetails (ctsIOPattern.cpp:505-516): published below, or held back while a verdict is pending
+            if (t.io_action == CTS_TASK_SEND) status_sent += transfer;
+            else if (t.io_action == CTS_TASK_RECV) status_recv += transfer;
             if (wasIoRequestedFromPattern) UpdateLastPatternError(CompleteTaskBackToPattern(t, transfer));
         }
         if (verified_now) {
@@ -1163,6 +1215,7 @@ struct cts_io_pattern {
             }
         }
         if (t.io_action == CTS_TASK_RECV && t.track_io) ++recv_completions;
+        PublishIfSettled();
         if (state.IsCompleted()) UpdateLastError(kNoError);
         return GetCurrentStatus();
     }
@@ -1319,6 +1372,9 @@ struct MediaStreamServer : cts_io_pattern {
     {
     }
     enum class ServerState { NotStarted, IdSent, IoStarted } m_state = ServerState::NotStarted;
+    // its one recv buffer only ever holds the connection-id datagram, and it receives nothing to verify (no ring)
+    uint32_t RecvSlotBytes() const override { return (CTS_UDP_CONNECTION_ID_HEADER_LENGTH + 15u) & ~15u; }
+    bool VerifiesRecvs() const override { return false; }
     int64_t m_baseTimeMilliseconds = 0;
     uint32_t m_frameSizeBytes;
     uint32_t m_currentFrameRequested = 0;
@@ -1431,6 +1487,12 @@ struct MediaStreamClient : cts_io_pattern {
     bool NeedsVerifier(const cts_task& t) const override  // every recv is a datagram to verify
     {
         return cfg.verify_buffers && t.io_action == CTS_TASK_RECV;
+    }
+    // every recv is one datagram of min(frame, DatagramMaxSize) bytes (GetNextTaskFromPattern): a slot of a frame's
+    // size would leave 97 % of a README-sized (52083-B) slot unused, per slot of the DEFERRED ring
+    uint32_t RecvSlotBytes() const override
+    {
+        return (std::max(std::min(m_frameSizeBytes, m_maxDatagramSize), 16u) + 15u) & ~15u;
     }
 
     // ---- DEFERRED: batched datagram verify (round 3) ---------------------------------------------------------
@@ -1599,6 +1661,8 @@ struct MediaStreamClient : cts_io_pattern {
         }
     }
 
+    bool FlushFailed() const { return m_lastError == CTS_PATTERN_E_FAIL_FAST; }
+
     // SetNextTimer (:321-349): the renderer's next tick at base + offset frames; armed when more than 2 ms ahead
     // (always on the initial call)
     bool SetNextTimer(bool initial)
@@ -1622,6 +1686,7 @@ struct MediaStreamClient : cts_io_pattern {
         static char kStart[] = "START";
         if (cts::ms_client_finished(ms)) return;
         TimerFlush();  // DEFERRED: the datagrams that arrived count
+        if (FlushFailed()) return;
         if (!cts::ms_client_received_buffered_frames(ms)) {
             cts_task t{};
             t.rio_buffer_id = kRioInvalid;
@@ -1642,6 +1707,15 @@ struct MediaStreamClient : cts_io_pattern {
         while (!scheduled) {
             if (cts::ms_client_finished(ms)) return;
             TimerFlush();  // DEFERRED: a tick renders what arrived before it
+            if (FlushFailed()) {
+                // the batched verify failed on the device: the stream cannot be rendered further, so it ends here
+                // as a stream that cannot continue does (ctsIOPatternMediaStream.cpp:490-508: a FatalAbort task)
+                cts_task t{};
+                t.rio_buffer_id = kRioInvalid;
+                t.io_action = CTS_TASK_FATAL_ABORT;
+                SendTaskToCallback(t);
+                return;
+            }
             const int code = cts::ms_client_tick(ms);
             if (code != 0) {
                 cts_task t{};
@@ -1717,11 +1791,18 @@ struct MediaStreamClient : cts_io_pattern {
     cts_task GetNextTaskFromPattern() override  // :115-138
     {
         if (m_baseTimeMilliseconds == 0) {
-            // start the timers the first time the pattern is used
+            // start the timers the first time the pattern is used: the thread first, so a thread that cannot start
+            // leaves no armed timer behind and fails the pattern (a latched FAIL_FAST; nothing crosses the C ABI)
+            if (!manual && !timer_thread.joinable()) {
+                try {
+                    timer_thread = std::thread([this] { TimerLoop(); });
+                } catch (const std::system_error& e) {
+                    throw FailFast{std::string("the MediaStream client's timer thread could not start: ") + e.what()};
+                }
+            }
             m_baseTimeMilliseconds = NowMs();
             SetNextStartTimer();
             (void)SetNextTimer(true);
-            if (!manual && !timer_thread.joinable()) timer_thread = std::thread([this] { TimerLoop(); });
         }
         cts_task t{};
         t.rio_buffer_id = kRioInvalid;
@@ -2017,6 +2098,10 @@ int cts_io_pattern_initiate_io(cts_io_pattern* p, cts_task* out)
         out->rio_buffer_id = CTS_RIO_INVALID_BUFFERID;
     } catch (const std::bad_alloc&) {
         return CTS_E_NOMEM;
+    } catch (const std::exception& e) {  // nothing may cross the C ABI
+        latch_fail_fast(p, FailFast{std::string("InitiateIo threw: ") + e.what()});
+        *out = cts_task{};
+        out->rio_buffer_id = CTS_RIO_INVALID_BUFFERID;
     }
     return CTS_OK;
 }
@@ -2037,6 +2122,9 @@ int cts_io_pattern_complete_io(cts_io_pattern* p, const cts_task* t, uint32_t cu
         return d.rc;
     } catch (const std::bad_alloc&) {
         return CTS_E_NOMEM;
+    } catch (const std::exception& e) {  // nothing may cross the C ABI
+        latch_fail_fast(p, FailFast{std::string("CompleteIo threw: ") + e.what()});
+        return CTS_IO_FAILED;
     }
 }
 
@@ -2094,6 +2182,9 @@ int cts_io_pattern_flush(cts_io_pattern* p)
         return d.rc;
     } catch (const std::bad_alloc&) {
         return CTS_E_NOMEM;
+    } catch (const std::exception& e) {  // nothing may cross the C ABI
+        latch_fail_fast(p, FailFast{std::string("Flush threw: ") + e.what()});
+        return CTS_IO_FAILED;
     }
 }
 
@@ -2102,12 +2193,15 @@ int cts_io_pattern_get_stats(const cts_io_pattern* p, cts_pattern_stats* o)
     if (p == nullptr || o == nullptr) return CTS_E_INVALID;
     std::lock_guard<std::recursive_mutex> lk(p->mu);
     *o = cts_pattern_stats{};
-    o->bytes_sent = p->bytes_sent;
-    o->bytes_recv = p->bytes_recv;
+    // m_statistics as published: a DEFERRED pattern's bytes behind a pending verdict are reported apart
+    o->bytes_sent_held = std::min(p->HeldSent(), p->bytes_sent);
+    o->bytes_recv_held = std::min(p->HeldRecv(), p->bytes_recv);
+    o->bytes_sent = p->bytes_sent - o->bytes_sent_held;
+    o->bytes_recv = p->bytes_recv - o->bytes_recv_held;
     o->buffers_verified = p->buffers_verified;
     o->bytes_verified = p->bytes_verified;
     o->buffers_failed = p->buffers_failed;
-    o->bytes_recv_at_failure = p->has_failure ? p->bytes_recv_at_failure : p->bytes_recv;
+    o->bytes_recv_at_failure = p->has_failure ? p->bytes_recv_at_failure : o->bytes_recv;
     o->recv_pattern_offset = p->m_recvPatternOffset;
     o->send_pattern_offset = p->m_sendPatternOffset;
     o->last_error = p->m_lastError;
@@ -2174,6 +2268,9 @@ int cts_io_pattern_media_stream_fire(cts_io_pattern* p, int timer)
         return d.rc;
     } catch (const std::bad_alloc&) {  // nothing may cross the C ABI
         return CTS_E_NOMEM;
+    } catch (const std::exception& e) {
+        latch_fail_fast(p, FailFast{std::string("a timer callback threw: ") + e.what()});
+        return CTS_OK;
     }
 }
 

@@ -24,8 +24,17 @@ def dist_env():
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
-def init(backend: str, device=None):
-    """init_process_group from the env; MASTER_ADDR defaults to 127.0.0.1."""
+DEFAULT_TIMEOUT_S = 600.0
+
+
+def init(backend: str, device=None, timeout_s: Optional[float] = DEFAULT_TIMEOUT_S):
+    """init_process_group from the env; MASTER_ADDR defaults to 127.0.0.1.
+
+    ``timeout_s`` bounds every collective and barrier of the group (the library default is 10 to 30 min): a rank
+    that dies or stalls makes the others raise after that long instead of holding the whole job, and a rank that
+    raises exits non-zero, so torch.distributed.run stops the group and returns non-zero."""
+    import datetime
+
     import torch.distributed as dist
 
     world, rank, _ = dist_env()
@@ -33,8 +42,20 @@ def init(backend: str, device=None):
     kw = {}
     if device is not None:
         kw["device_id"] = device
+    if timeout_s is not None:
+        kw["timeout"] = datetime.timedelta(seconds=float(timeout_s))
     dist.init_process_group(backend, rank=rank, world_size=world, **kw)
     return world, rank
+
+
+def new_cpu_group(timeout_s: Optional[float] = DEFAULT_TIMEOUT_S):
+    """A gloo group over all ranks for host-side waits, with the same bound."""
+    import datetime
+
+    import torch.distributed as dist
+
+    kw = {} if timeout_s is None else {"timeout": datetime.timedelta(seconds=float(timeout_s))}
+    return dist.new_group(backend="gloo", **kw)
 
 
 def fold_counters(counter_block):
@@ -81,5 +102,5 @@ def data_error_count(conn_first_fail, group=None) -> int:
     return int(n.item())
 
 
-__all__ = ["dist_env", "init", "fold_counters", "allreduce_counters", "counters_dict", "max_over_ranks",
+__all__ = ["dist_env", "init", "new_cpu_group", "DEFAULT_TIMEOUT_S", "fold_counters", "allreduce_counters", "counters_dict", "max_over_ranks",
            "data_error_count"]

@@ -247,13 +247,21 @@ def shared_buffer_init(engine, max_buffer_size: int) -> None:
     check("cts_shared_buffer_init", lib().cts_shared_buffer_init(_product(engine), max_buffer_size))
 
 
+_shared_keepalive = None
+
+
 def shared_buffer_attach(buf: np.ndarray) -> None:
-    """Harnesses without a device: use caller-owned bytes as g_senderSharedBuffer (keep buf alive)."""
+    """Harnesses without a device: use caller-owned bytes as g_senderSharedBuffer. The library keeps only the
+    pointer, so the array is held here until the next attach or release."""
+    global _shared_keepalive
     check("cts_shared_buffer_attach", lib().cts_shared_buffer_attach(buf.ctypes.data, buf.nbytes))
+    _shared_keepalive = buf
 
 
 def shared_buffer_release() -> None:
+    global _shared_keepalive
     lib().cts_shared_buffer_release()
+    _shared_keepalive = None
 
 
 def rio_functions_set(register_fn, deregister_fn, ctx=None) -> None:

@@ -176,8 +176,8 @@ int cts_pattern_clock_set(cts_clock_ms_fn fn, void* ctx);
 /* Per-connection statistics (ctsTcpStatistics, ctsStatistics.hpp:316-373) and
  * the verify bookkeeping of this pattern. */
 typedef struct cts_pattern_stats {
-    uint64_t bytes_sent;          /* m_statistics.m_bytesSent */
-    uint64_t bytes_recv;          /* m_statistics.m_bytesRecv */
+    uint64_t bytes_sent;          /* m_statistics.m_bytesSent (published: see bytes_sent_held) */
+    uint64_t bytes_recv;          /* m_statistics.m_bytesRecv (published: see bytes_recv_held) */
     uint64_t buffers_verified;    /* VerifyBuffer calls that completed */
     uint64_t bytes_verified;      /* sum of their transferred bytes */
     uint64_t buffers_failed;      /* verify failures (0 or 1: the first fails the connection) */
@@ -194,6 +194,12 @@ typedef struct cts_pattern_stats {
     uint8_t has_failure;
     uint8_t reserved;
     uint32_t fail_completion;     /* index of the failing recv completion (0-based) */
+    /* DEFERRED: bytes completed behind a recv whose batch verdict is still pending. They are held back from
+     * bytes_sent / bytes_recv above and from the process-wide cts_status_details until that batch verifies, so
+     * every counter only grows, as the reference's do (ctsStatistics.hpp:153-186). Bytes after a failing buffer
+     * are dropped without ever being published. 0 in SYNC mode. */
+    uint64_t bytes_sent_held;
+    uint64_t bytes_recv_held;
 } cts_pattern_stats;
 
 /* Batch verifier hook: verify n buffers of a host arena (results[i] per

@@ -47,3 +47,31 @@ def test_world_size_must_equal_gpus():
                        stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=120)
     assert r.returncode != 0 and r.stdout.strip() == ""
     assert "WORLD_SIZE=2 but --gpus 1" in r.stderr
+
+
+def _run_failing(mode, timeout_s):
+    import time
+
+    t0 = time.monotonic()
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--stub-gpu", "--stub-fail-rank", "1",
+                        "--stub-fail-mode", mode, "--dist-timeout", str(timeout_s)], env=_env(), cwd=ROOT,
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=240)
+    return r, time.monotonic() - t0
+
+
+def test_a_failing_rank_fails_the_run_promptly():
+    """A rank that raises ends the whole run with a non-zero exit and no JSON line: torch.distributed.run stops the
+    other rank, which would otherwise wait in its collective (the driver's 8-GPU run must not hang on one rank)."""
+    r, took = _run_failing("raise", 30)
+    assert r.returncode != 0 and r.stdout.strip() == "", (r.returncode, r.stdout)
+    assert "this rank fails" in r.stderr
+    assert took < 120, took
+
+
+def test_a_stalled_rank_times_out_the_run():
+    """A rank that stalls (sleeps far past the process-group timeout before its collective): the other rank's
+    collective raises after --dist-timeout seconds, its non-zero exit stops the group, and the launcher returns
+    non-zero with no JSON line, in about that long rather than the library's default of 10-30 minutes."""
+    r, took = _run_failing("stall", 8)
+    assert r.returncode != 0 and r.stdout.strip() == "", (r.returncode, r.stdout)
+    assert took < 120, took

@@ -21,6 +21,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HOST_SRCS = ["cts_pattern.cpp", "cts_media_stream.cpp", "cts_status.cpp", "cts_loopback.cpp", "cts_loopback_udp.cpp",
              "cts_host_util.cpp"]
 SAN = {
+    "plain": [],
     "asan-ubsan": ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"],
     "tsan": ["-fsanitize=thread"],
 }
@@ -29,7 +30,7 @@ ENV = {"ASAN_OPTIONS": "detect_leaks=1:abort_on_error=0:exitcode=23",
        "TSAN_OPTIONS": "halt_on_error=1:exitcode=25"}
 
 
-def _build(d, san, driver):
+def _build(d, san, driver, extra_link=()):
     flags = ["-g", "-O1", "-fno-omit-frame-pointer", "-pthread"] + SAN[san]
     inc = ["-I", os.path.join(ROOT, "include"), "-I", os.path.join(ROOT, "ctstraffic_amd", "csrc"),
            "-I", os.path.join(ROOT, "oracle"), "-I", "/opt/rocm/include", "-D__HIP_PLATFORM_AMD__"]
@@ -44,11 +45,11 @@ def _build(d, san, driver):
                     os.path.join(ROOT, "oracle", "cts_oracle.c"), "-o", o], check=True)
     objs.append(o)
     exe = os.path.join(d, driver[:-4])
-    subprocess.run(["g++", *flags, *objs, "-o", exe], check=True)
+    subprocess.run(["g++", *flags, *objs, "-o", exe, *extra_link], check=True)
     return exe
 
 
-@pytest.mark.parametrize("san", sorted(SAN))
+@pytest.mark.parametrize("san", sorted(set(SAN) - {"plain"}))
 @pytest.mark.parametrize("driver", ["pattern_replay.cpp", "loopback_stress.cpp", "slices_check.cpp",
                                     "counters_fold.cpp", "media_stream_client.cpp",
                                     "media_stream_pattern.cpp"])
@@ -59,3 +60,15 @@ def test_host_code_under_sanitizer(san, driver):
         assert out.returncode == 0, (out.returncode, out.stderr[-4000:])
         assert ": ok" in out.stdout
         assert "runtime error" not in out.stderr and "WARNING: ThreadSanitizer" not in out.stderr, out.stderr[-4000:]
+
+
+def test_thread_start_failure_never_crosses_the_abi():
+    """Every host thread start (the MediaStream client's timer thread, the TCP and UDP feeders' side threads) fails
+    on demand through a pthread_create interposer (tests/cpp/thread_start_failure.cpp): the client latches a
+    FAIL_FAST with no timer left armed, the feeders fail those connections and return, and no std::system_error
+    reaches std::terminate. Built without a sanitizer (they intercept pthread_create themselves)."""
+    with tempfile.TemporaryDirectory() as d:
+        exe = _build(d, "plain", "thread_start_failure.cpp", extra_link=("-rdynamic", "-ldl"))
+        out = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+        assert out.returncode == 0, (out.returncode, out.stderr[-4000:])
+        assert ": ok" in out.stdout

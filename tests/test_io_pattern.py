@@ -1223,6 +1223,81 @@ def test_random_push_server_stream(make, seed):
     assert s["recv_pattern_offset"] == (sum(lens[:fail_at + 1])) % 65536
 
 
+@pytest.mark.parametrize("seed,corrupt", [(11, False), (12, True), (13, True), (14, True)])
+def test_deferred_counters_never_decrease(make, seed, corrupt):
+    """TcpStatusDetails and the per-connection byte counters only ever grow. The reference only Adds to them
+    (ctsIOPattern.cpp:505-516, ctsStatistics.hpp:153-186) and its status timer prints their SnapValueDifference
+    (ctsStatistics.hpp:363), so a slice can never be negative. A DEFERRED pattern holds back the bytes of every
+    completion behind a pending batch verdict and publishes them when the batch verifies. Here a paced Duplex client
+    completes its sends and recvs in random order, with a corrupt recv in the middle of a batch. Both counters are
+    read after every completion; the end totals must be the reference's: everything up to and including the failing
+    recv, nothing after it, in every verify mode."""
+    from ctstraffic_amd.pattern import status_details, status_details_reset
+
+    rng = np.random.default_rng(seed)
+    size, n_each = 1024, 200
+    p = make(**duplex_defaults(False, buffer_size=size, transfer_size=2 * n_each * size, pre_post_sends=2,
+                               batch_buffers=16, tcp_bytes_per_second=40 * size, tcp_bytes_per_second_period=100))
+    status_details_reset()
+    _complete_connection_id(p, False)
+    bad_recv = int(rng.integers(20, n_each - 20)) if corrupt else None
+    pending, log = [], []  # data completions in order: (action, bytes)
+    recvs = 0
+    prev = (status_details(), p.stats())
+    st = ContinueIo
+    while st == ContinueIo:
+        while True:
+            t = p.InitiateIo()
+            if t.io_action == NoneAction:
+                break
+            pending.append(t)
+        assert pending, "the pattern stalled"
+        t = pending.pop(int(rng.integers(0, len(pending))))
+        if t.io_action == Recv and t.buffer_type == A.BUFFER_DYNAMIC:
+            n = int(t.buffer_length)
+            IoPattern.recv_from_wire(t, n)
+            if recvs == bad_recv:
+                pos = int(rng.integers(0, n))
+                IoPattern.write_task_buffer(t, bytes([IoPattern.read_task_buffer(t, 1, pos)[0] ^ 0x5A]), pos)
+            recvs += 1
+            log.append((Recv, n))
+        elif t.io_action == Send and t.buffer_type != A.BUFFER_COMPLETION_MESSAGE:
+            n = int(t.buffer_length)
+            log.append((Send, n))
+        elif t.buffer_type == A.BUFFER_COMPLETION_MESSAGE:
+            n = 4  # "DONE": the client's completion buffer already holds it
+        else:
+            n = 0  # graceful shutdown, then the FIN
+        st = p.CompleteIo(t, n, 0)
+        cur = (status_details(), p.stats())
+        for k in ("bytes_sent", "bytes_recv"):
+            assert cur[0][k] >= prev[0][k], ("TcpStatusDetails", k, prev[0], cur[0])
+            assert cur[1][k] >= prev[1][k], ("per-connection", k, prev[1], cur[1])
+        if make.mode == A.VERIFY_SYNC:
+            assert cur[1]["bytes_recv_held"] == 0 and cur[1]["bytes_sent_held"] == 0
+        prev = cur
+    p.Flush()
+    s, g = p.stats(), status_details()
+    # the reference's totals: it fails the connection at the corrupt recv's completion
+    upto = log
+    if corrupt:
+        k = [i for i, (a, _) in enumerate(log) if a == Recv][bad_recv]
+        upto = log[:k + 1]
+    want_recv = sum(n for a, n in upto if a == Recv)
+    want_sent = sum(n for a, n in upto if a == Send)
+    assert (s["bytes_recv"], s["bytes_sent"]) == (want_recv, want_sent)
+    assert s["bytes_recv_held"] == 0 and s["bytes_sent_held"] == 0 and s["queued"] == 0
+    if corrupt:
+        assert st == FailedIo and p.GetLastPatternError() == A.STATUS_ERROR_DATA_DID_NOT_MATCH_BIT_PATTERN
+        assert s["fail_completion"] == bad_recv and s["bytes_recv_at_failure"] == want_recv
+        assert (g["bytes_recv"], g["bytes_sent"]) == (ConnectionIdLength + want_recv, want_sent)
+        assert g["data_errors"] == 1
+    else:
+        assert st == CompletedIo and p.GetLastPatternError() == 0
+        assert (g["bytes_recv"], g["bytes_sent"]) == (ConnectionIdLength + want_recv + 4, want_sent)
+        assert want_recv == want_sent == n_each * size
+
+
 # ---- RIO buffer ids (ctsIOPattern.cpp:133-217, :369-386, :683-692, :716-725) ------------------------
 def test_rio_send_ids_unique_and_recycled(make):
     """A Push client under -io:rioiocp: concurrent sends carry distinct ids of the sender buffer's

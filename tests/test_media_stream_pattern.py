@@ -457,3 +457,62 @@ def test_gpu_server_sends_frames(engine, clock):
         p.CompleteIo(t, 52083)
     assert p.GetLastPatternError() == 0
     p.close()
+
+
+@pytest.mark.parametrize("backend", ["cpu", pytest.param("gpu", marks=pytest.mark.gpu)])
+@pytest.mark.parametrize("mode", [A.VERIFY_SYNC, A.VERIFY_DEFERRED], ids=["sync", "deferred"])
+@pytest.mark.parametrize("frame,max_dgram,slot", [(52083, 1400, 1408), (1000, 1400, 1008), (3000, 1472, 1472),
+                                                  (64, 30, 32)])
+def test_client_recv_slots_sized_to_one_datagram(request, clock, backend, mode, frame, max_dgram, slot):
+    """A client recv is one datagram of min(frame, DatagramMaxSize) bytes (ctsIOPatternMediaStream.cpp:115-138), so
+    its recv slots (and every slot of the DEFERRED recv ring) are that many bytes rounded up to 16, not a frame's:
+    at the README frame size (52083 B) a frame-sized slot left 97 % of the pinned ring unused. The posted recvs sit
+    `slot` bytes apart, the ring hands its slots out in order and wraps after 2 x batch + PrePostRecvs + 1 slots on a
+    device (batch + PrePostRecvs + 1 with a CPU hook), and the stream still verifies."""
+    engine = request.getfixturevalue("engine") if backend == "gpu" else None
+    recvs, batch = 3, 4
+    cfg = PatternConfig.media_stream(listening=False, frame_size=frame, frames_per_second=100, stream_length_frames=50,
+                                     buffered_frames=50, datagram_max_size=max_dgram, pre_post_recvs=recvs,
+                                     ms_manual_timers=True, verify_mode=mode, batch_buffers=batch)
+    p = _make(cfg, engine)
+    posted = [p.InitiateIo() for _ in range(recvs)]
+    post_len = min(frame, max_dgram)
+    assert all(t.buffer_length == post_len for t in posted)
+    base = posted[0].buffer
+    # the free list hands out its back first (ctsIOPattern.cpp:708-715)
+    assert sorted(t.buffer - base for t in posted) == [-slot * k for k in range(recvs)][::-1]
+    base = min(t.buffer for t in posted)
+    ring = mode == A.VERIFY_DEFERRED
+    slots = (batch * (2 if engine is not None else 1) + recvs + 1) if ring else recvs
+    n = 3 * slots
+    length = post_len
+    seen = []
+    for i in range(n):
+        t = posted.pop(0)
+        IoPattern.write_task_buffer(t, _datagram(1 + i // 40, length))
+        assert p.CompleteIo(t, length) == A.IO_CONTINUE
+        nxt = p.InitiateIo()
+        assert nxt.io_action == Recv
+        off = nxt.buffer - base
+        assert off % slot == 0 and 0 <= off < slots * slot
+        seen.append(off // slot)
+        posted.append(nxt)
+    if ring:  # recycled in ring order: slot recvs, recvs + 1, ... wrapping at `slots`
+        assert seen == [(recvs + i) % slots for i in range(n)]
+    assert p.Flush() == A.IO_CONTINUE
+    s = p.media_stream_stats()
+    assert s["datagrams"] == n and s["has_failure"] == 0
+    p.close()
+
+
+@pytest.mark.parametrize("mode", [A.VERIFY_SYNC, A.VERIFY_DEFERRED], ids=["sync", "deferred"])
+def test_server_keeps_no_recv_ring(clock, mode):
+    """The server receives nothing to verify: its one recv buffer only ever holds the 39-byte connection-id datagram
+    (ctsIOPattern.cpp:1119-1128), whatever the frame size and verify mode, and it builds that datagram correctly."""
+    p = _make(PatternConfig.media_stream(listening=True, frame_size=60000, frames_per_second=10,
+                                         stream_length_frames=2, verify_mode=mode))
+    t = p.InitiateIo()
+    assert (t.io_action, t.buffer_type, t.buffer_length) == (Send, A.BUFFER_UDP_CONNECTION_ID, 39)
+    assert IoPattern.read_task_buffer(t, 39) == b"\x00\x10" + p.connection_id().encode() + b"\x00"
+    assert p.CompleteIo(t, 39) == A.IO_CONTINUE
+    p.close()
