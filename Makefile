@@ -22,9 +22,10 @@ TUNING_OBJS := $(patsubst $(CSRC)/%,ctstraffic_amd/build/tuning/%.o,$(TUNED)) \
 SOFLAGS   := -shared -Wl,-Bsymbolic -Wl,--version-script=$(CSRC)/exports.map
 
 DEVICE_VERIFY := ctstraffic_amd/build/device_verify
-TOOLS := tools/hbm_read_ceiling tools/verify_ablation tools/mailbox_probe tools/rw_mix_probe tools/write_shape_probe tools/fill_bisect tools/fill_abi_probe tools/mailbox_bisect tools/ring_fill_probe
+TOOLS := tools/hbm_read_ceiling tools/verify_ablation tools/mailbox_probe tools/rw_mix_probe tools/write_shape_probe tools/fill_bisect tools/fill_abi_probe tools/mailbox_bisect tools/ring_fill_probe \
+         tools/verify_timeline tools/verify_timeline_kp
 
-SYNC_PROBE := tools/sync_probe tools/pattern_cpu_probe
+SYNC_PROBE := tools/sync_probe tools/pattern_cpu_probe tools/deferred_ab
 BENCH_MULTI := tools/libcts_bench_multi.so
 
 all: $(ENGINE_SO) $(TUNING_SO) oracle $(DEVICE_VERIFY) $(TOOLS) $(SYNC_PROBE) $(BENCH_MULTI)
@@ -39,6 +40,10 @@ $(BENCH_MULTI): tools/bench_multi.cpp $(ENGINE_SO) include/cts_engine.h
 tools/sync_probe: tools/sync_probe.cpp $(ENGINE_SO) include/cts_engine.h
 	$(HIPCC) -O2 -std=c++17 -Iinclude $< -o $@ -Lctstraffic_amd -lcts_engine -Wl,-rpath,'$$ORIGIN/../ctstraffic_amd' -lpthread
 
+# config-1 DEFERRED vs verify-off A/B: background PCIe reads, recv-ring footprint (diagnostic)
+tools/deferred_ab: tools/deferred_ab.cpp $(ENGINE_SO) include/cts_engine.h include/cts_loopback.h
+	$(HIPCC) -O2 -std=c++17 -Iinclude $< -o $@ -Lctstraffic_amd -lcts_engine -Wl,-rpath,'$$ORIGIN/../ctstraffic_amd' -lpthread
+
 # receive-thread CPU inside the ctsIoPattern calls (no sockets)
 tools/pattern_cpu_probe: tools/pattern_cpu_probe.cpp $(ENGINE_SO) include/cts_pattern.h
 	$(HIPCC) -O2 -std=c++17 -Iinclude $< -o $@ -Lctstraffic_amd -lcts_engine -Wl,-rpath,'$$ORIGIN/../ctstraffic_amd' -lpthread
@@ -50,6 +55,14 @@ tools/%: tools/%.hip
 # the product fill kernel included verbatim (diagnostic)
 tools/fill_bisect: tools/fill_bisect.hip $(CSRC)/cts_kernels.hip $(HDRS)
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -Iinclude -I$(CSRC) $< -o $@
+
+# the product verify kernel beside a plain read of the same shape: times and per-workgroup timelines (diagnostic);
+# the _kp build preloads the kernel arguments into SGPRs
+tools/verify_timeline: tools/verify_timeline.hip $(CSRC)/cts_kernels.hip $(HDRS)
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -Iinclude -I$(CSRC) $< -o $@
+tools/verify_timeline_kp: tools/verify_timeline.hip $(CSRC)/cts_kernels.hip $(HDRS)
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -Iinclude -I$(CSRC) -DCTS_TOOL_KERNARG_PRELOAD=1 \
+	  -mllvm -amdgpu-kernarg-preload-count=16 $< -o $@
 
 # the product MediaStream fill beside flat ring walks (diagnostic)
 tools/ring_fill_probe: tools/ring_fill_probe.hip $(CSRC)/cts_kernels.hip $(HDRS)

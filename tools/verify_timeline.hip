@@ -1,0 +1,310 @@
+// verify_timeline.hip — where does a config-2 verify launch spend the time a plain streaming read of the same
+// bytes does not? (DESIGN.md §3 "Where a 256 MiB launch's last few percent go"; VERDICT r03 "Next round" 3.)
+//
+// The product kernel (cts_kernels.hip, included verbatim) against the plain read of the same shape, in one process on
+// one box, 8 rotated 256 MiB arenas (4096 x 64 KiB buffers each; 75 % phase-0 / 25 % random expected offsets, one
+// corrupt byte per 1024 buffers, as bench.py's config 2):
+//   time    : HIP events around R launches, per launch: the product verify_wg_kernel (variant 13, the default), a
+//             replica of it built from the same device helpers with the stamps compiled out (must equal the product),
+//             and the plain read (grid = 4 x CUs, workgroup b reads 64-KiB slabs b, b + grid, ..., U = 2, the
+//             verify's per-buffer barrier);
+//   timeline: per-workgroup s_memrealtime stamps (100 MHz) of the stamped replica and of the plain read:
+//             entry, first data issue (after the first descriptor arrived), the end of every buffer, the end
+//             after the counter flush; printed as percentiles over the 1024 workgroups and by XCC.
+// Built twice by the Makefile: tools/verify_timeline and tools/verify_timeline_kp (kernel arguments preloaded into
+// SGPRs: -mllvm -amdgpu-kernarg-preload-count=16), so one call compares both prologues. Diagnostic only.
+#include "../ctstraffic_amd/csrc/cts_kernels.hip"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CHECK(x)                                                                              \
+    do {                                                                                      \
+        hipError_t e_ = (x);                                                                  \
+        if (e_ != hipSuccess) {                                                               \
+            fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+            exit(1);                                                                          \
+        }                                                                                     \
+    } while (0)
+
+namespace {
+using cts::u32x4;
+constexpr int kSt = 16;  // stamp slots per workgroup
+
+__device__ __forceinline__ uint64_t stamp() { return __builtin_amdgcn_s_memrealtime(); }
+// a stamp taken once `dep` is available (the asm's input makes the compiler wait for it first)
+__device__ __forceinline__ uint64_t stamp_after(uint32_t dep)
+{
+    uint64_t t;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : "s"(dep));
+    return t;
+}
+__device__ __forceinline__ uint32_t xcc_id()
+{
+    uint32_t x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+    return x & 0xFu;
+}
+
+// the test arena: buffer i = the pattern from its expected offset, written 16 bytes at a time
+__global__ void fill_arena(u32x4* a, const cts_buf_desc* d, uint32_t n)
+{
+    for (uint64_t c = (uint64_t)blockIdx.x * 256 + threadIdx.x; c < (uint64_t)n * 4096; c += (uint64_t)gridDim.x * 256) {
+        const uint32_t q = (d[c / 4096].expected_pattern_offset + 16u * (uint32_t)(c % 4096)) & 0xFFFFu;
+        a[c] = cts::expected_chunk(q, q & 1u);
+    }
+}
+
+// verify_wg_kernel<2, true, true, false, true, true> (the product's variant 13) on the whole-line path every config-2
+// buffer takes, built from the same helpers; STAMP adds the timeline stores (lane 0, one 8-byte store per event)
+template <bool STAMP>
+__global__ void __launch_bounds__(256, 8)
+    verify_replica(const uint8_t* __restrict__ arena, uint64_t arena_bytes, const cts_buf_desc* __restrict__ descs,
+                   uint32_t n, cts_verify_result* __restrict__ results, uint64_t* __restrict__ counters,
+                   uint32_t* __restrict__ conn_first_fail, uint32_t n_conns, uint64_t* __restrict__ st)
+{
+    const uint64_t t_entry = STAMP ? stamp() : 0;
+    __shared__ uint64_t ctr[1][5];
+    const uint32_t lane = threadIdx.x;
+    cts::zero_counters<1>(ctr);
+    uint32_t i = blockIdx.x, k = 0;
+    const uint32_t step = gridDim.x;
+    cts_buf_desc dn;
+    if (i < n) dn = descs[i];
+    uint64_t* my = st + (uint64_t)blockIdx.x * kSt;
+    for (; i < n; i = i + step < n ? i + step : n, ++k) {
+        const cts_buf_desc d = dn;
+        if (i + step < n) dn = descs[i + step];
+        if (cts::desc_bad(d, arena_bytes)) continue;
+        const cts::Span s = cts::make_span(arena, d);
+        if (STAMP && k == 0 && lane == 0) my[1] = stamp_after((uint32_t)d.byte_offset);
+        uint32_t first = cts::kNone, count = 0;
+        cts::scan_whole_exact<256, 2, true, true>(s, lane, first, count);
+        const bool dirty = __builtin_amdgcn_readfirstlane(__syncthreads_or(first != cts::kNone)) != 0;
+        if (dirty) cts::block_reduce_mismatch(first, count);
+        if (lane == 0) cts::finish_buffer(s, d, i, first, count, results, ctr[0], conn_first_fail, n_conns);
+        if (STAMP && lane == 0 && k < 8) my[2 + k] = stamp();
+    }
+    cts::flush_counters<1>(counters, ctr);
+    if (STAMP && lane == 0) {
+        my[0] = t_entry;
+        my[10] = stamp();
+        my[11] = (uint64_t)xcc_id() | ((uint64_t)k << 8);
+    }
+}
+
+// the plain read of the same shape (hbm_read_ceiling.hip read_slab_timeline): no descriptor, no compare, no output
+template <bool STAMP>
+__global__ void __launch_bounds__(256) plain_read(const u32x4* __restrict__ p, uint32_t nslabs, uint64_t* st,
+                                                  uint32_t* out)
+{
+    const uint64_t t_entry = STAMP ? stamp() : 0;
+    uint32_t acc = 0, k = 0;
+    uint64_t* my = st + (uint64_t)blockIdx.x * kSt;
+    for (uint32_t sl = blockIdx.x; sl < nslabs; sl += gridDim.x, ++k) {
+        const u32x4* q = p + (uint64_t)sl * 4096u;
+        if (STAMP && k == 0 && threadIdx.x == 0) my[1] = stamp();
+        for (uint32_t r = 0; r < 8; ++r) {
+            const uint32_t c = r * 512u + threadIdx.x;
+            u32x4 d[2];
+            d[0] = __builtin_nontemporal_load(q + c);
+            d[1] = __builtin_nontemporal_load(q + c + 256u);
+            __builtin_amdgcn_sched_barrier(0);
+            acc |= d[0][0] ^ d[0][1] ^ d[0][2] ^ d[0][3] ^ d[1][0] ^ d[1][1] ^ d[1][2] ^ d[1][3];
+        }
+        acc = __syncthreads_or(acc == 0x12345678u) ? 1u : acc;
+        if (STAMP && threadIdx.x == 0 && k < 8) my[2 + k] = stamp();
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+    if (STAMP && threadIdx.x == 0) {
+        my[0] = t_entry;
+        my[10] = stamp();
+        my[11] = (uint64_t)xcc_id() | ((uint64_t)k << 8);
+    }
+}
+
+template <typename F>
+double time_us(F launch, int reps, hipStream_t s)
+{
+    launch(0);
+    hipEvent_t a, b;
+    CHECK(hipEventCreate(&a));
+    CHECK(hipEventCreate(&b));
+    CHECK(hipEventRecord(a, s));
+    for (int i = 0; i < reps; ++i) launch(i);
+    CHECK(hipEventRecord(b, s));
+    CHECK(hipEventSynchronize(b));
+    float ms = 0;
+    CHECK(hipEventElapsedTime(&ms, a, b));
+    CHECK(hipEventDestroy(a));
+    CHECK(hipEventDestroy(b));
+    return ms * 1e3 / reps;
+}
+
+double pct(std::vector<double> v, double q)
+{
+    if (v.empty()) return -1;
+    std::sort(v.begin(), v.end());
+    return v[(size_t)(q * (double)(v.size() - 1))];
+}
+
+void print_timeline(const char* kind, const std::vector<uint64_t>& h, uint32_t grid, bool kp)
+{
+    uint64_t t0 = ~0ull;
+    for (uint32_t b = 0; b < grid; ++b) t0 = std::min(t0, h[(size_t)b * kSt]);
+    std::vector<double> entry, first_issue, first_buf, per_buf, last_buf, tail, end;
+    for (uint32_t b = 0; b < grid; ++b) {
+        const uint64_t* m = &h[(size_t)b * kSt];
+        const uint32_t k = (uint32_t)(m[11] >> 8);
+        if (k == 0) continue;
+        const uint32_t kk = std::min<uint32_t>(k, 8);
+        entry.push_back((m[0] - t0) * 0.01);
+        first_issue.push_back((m[1] - m[0]) * 0.01);
+        first_buf.push_back((m[2] - m[1]) * 0.01);
+        for (uint32_t j = 1; j < kk; ++j) per_buf.push_back((m[2 + j] - m[1 + j]) * 0.01);
+        last_buf.push_back((m[1 + kk] - t0) * 0.01);
+        tail.push_back((m[10] - m[1 + kk]) * 0.01);
+        end.push_back((m[10] - t0) * 0.01);
+    }
+    auto p3 = [&](const std::vector<double>& v) {
+        static char buf[8][96];
+        static int slot = 0;
+        char* o = buf[slot++ & 7];
+        std::snprintf(o, 96, "[%.2f,%.2f,%.2f,%.2f,%.2f]", pct(v, 0), pct(v, 0.1), pct(v, 0.5), pct(v, 0.9), pct(v, 1));
+        return o;
+    };
+    std::printf("{\"kind\":\"timeline\",\"kernel\":\"%s\",\"kernarg_preload\":%d,\"workgroups\":%u,"
+                "\"pcts\":\"p0,p10,p50,p90,p100 in us\",\"entry_us\":%s,\"entry_to_first_issue_us\":%s,"
+                "\"first_buffer_us\":%s,\"later_buffer_us\":%s,\"last_buffer_end_us\":%s,\"flush_after_last_us\":%s,"
+                "\"end_us\":%s,\"end_by_xcc\":[",
+                kind, kp ? 1 : 0, grid, p3(entry), p3(first_issue), p3(first_buf), p3(per_buf), p3(last_buf), p3(tail),
+                p3(end));
+    for (uint32_t x = 0, first = 1; x < 8; ++x) {
+        std::vector<double> ex;
+        for (uint32_t b = 0; b < grid; ++b) {
+            const uint64_t* m = &h[(size_t)b * kSt];
+            if ((m[11] >> 8) != 0 && (m[11] & 0xFu) == x) ex.push_back((m[10] - t0) * 0.01);
+        }
+        if (ex.empty()) continue;
+        std::printf("%s[%u,%.2f,%.2f,%.2f]", first ? "" : ",", x, pct(ex, 0), pct(ex, 0.5), pct(ex, 1));
+        first = 0;
+    }
+    std::printf("]}\n");
+    std::fflush(stdout);
+}
+
+}  // namespace
+
+int main(int argc, char** argv)
+{
+#ifdef CTS_TOOL_KERNARG_PRELOAD
+    const bool kp = true;
+#else
+    const bool kp = false;
+#endif
+    const int passes = argc > 1 ? atoi(argv[1]) : 3;
+    const int reps = argc > 2 ? atoi(argv[2]) : 64;
+    int cus = 0;
+    CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+    const uint32_t n = 4096, grid = (uint32_t)cus * 4u;  // the engine's grid for 4096 x 64 KiB: 4 buffers per workgroup
+    const uint64_t bytes = (uint64_t)n << 16;
+    constexpr int R = 8;
+    std::vector<cts_buf_desc> hd(n);
+    uint64_t x = 0xC75;
+    auto rnd = [&] {
+        x ^= x << 13;
+        x ^= x >> 7;
+        x ^= x << 17;
+        return x;
+    };
+    for (uint32_t i = 0; i < n; ++i) {
+        const bool random_phase = rnd() % 4 == 0;
+        hd[i] = cts_buf_desc{(uint64_t)i << 16, 65536u, random_phase ? (uint32_t)(rnd() & 0xFFFFu) : 0u, i, 0u};
+    }
+    cts_buf_desc* d = nullptr;
+    CHECK(hipMalloc((void**)&d, n * sizeof(cts_buf_desc)));
+    CHECK(hipMemcpy(d, hd.data(), n * sizeof(cts_buf_desc), hipMemcpyHostToDevice));
+    std::vector<uint8_t*> arena(R);
+    for (auto& a : arena) {
+        CHECK(hipMalloc((void**)&a, bytes));
+        fill_arena<<<4096, 256>>>(reinterpret_cast<u32x4*>(a), d, n);
+        // one corrupt byte per 1024 buffers
+        for (uint32_t b = 0; b < n; b += 1024) {
+            const uint64_t off = ((uint64_t)b << 16) + 12345u;
+            uint8_t v = 0;
+            CHECK(hipMemcpy(&v, a + off, 1, hipMemcpyDeviceToHost));
+            v ^= 0x5A;
+            CHECK(hipMemcpy(a + off, &v, 1, hipMemcpyHostToDevice));
+        }
+    }
+    cts_verify_result* res = nullptr;
+    uint64_t* ctr = nullptr;
+    uint32_t *cff = nullptr, *out = nullptr;
+    uint64_t* st = nullptr;
+    CHECK(hipMalloc((void**)&res, n * sizeof(cts_verify_result)));
+    CHECK(hipMalloc((void**)&ctr, CTS_COUNTER_SHARDS * 64));
+    CHECK(hipMalloc((void**)&cff, n * 4));
+    CHECK(hipMalloc((void**)&out, 64));
+    CHECK(hipMalloc((void**)&st, (size_t)grid * kSt * 8));
+    CHECK(hipMemset(ctr, 0, CTS_COUNTER_SHARDS * 64));
+    CHECK(hipMemset(cff, 0xFF, n * 4));
+    hipStream_t s;
+    CHECK(hipStreamCreate(&s));
+    CHECK(hipDeviceSynchronize());
+
+    // parity of the replica against the product on arena 0 (the tool measures the product's code path)
+    {
+        std::vector<cts_verify_result> a(n), b(n);
+        cts::verify_wg_kernel<2, true, true, false, true, true><<<grid, 256, 0, s>>>(arena[0], bytes, d, n, res, ctr, cff, n);
+        CHECK(hipMemcpy(a.data(), res, n * sizeof(cts_verify_result), hipMemcpyDeviceToHost));
+        CHECK(hipMemset(res, 0, n * sizeof(cts_verify_result)));
+        verify_replica<true><<<grid, 256, 0, s>>>(arena[0], bytes, d, n, res, ctr, cff, n, st);
+        CHECK(hipMemcpy(b.data(), res, n * sizeof(cts_verify_result), hipMemcpyDeviceToHost));
+        uint32_t failed = 0;
+        for (uint32_t i = 0; i < n; ++i) failed += a[i].pass ? 0u : 1u;
+        const bool same = std::equal(a.begin(), a.end(), b.begin(), [](const cts_verify_result& p, const cts_verify_result& q) {
+            return p.first_mismatch == q.first_mismatch && p.mismatch_bytes == q.mismatch_bytes && p.pass == q.pass &&
+                   p.expected == q.expected && p.actual == q.actual;
+        });
+        std::printf("{\"kind\":\"parity\",\"kernarg_preload\":%d,\"replica_equals_product\":%d,\"failed_buffers\":%u}\n",
+                    kp ? 1 : 0, same ? 1 : 0, failed);
+    }
+
+    for (int pass = 0; pass < passes; ++pass) {
+        const double t_prod = time_us([&](int i) {
+            cts::verify_wg_kernel<2, true, true, false, true, true><<<grid, 256, 0, s>>>(arena[i % R], bytes, d, n, res,
+                                                                                        ctr, cff, n);
+        }, reps, s);
+        const double t_rep = time_us([&](int i) {
+            verify_replica<false><<<grid, 256, 0, s>>>(arena[i % R], bytes, d, n, res, ctr, cff, n, st);
+        }, reps, s);
+        const double t_plain = time_us([&](int i) {
+            plain_read<false><<<grid, 256, 0, s>>>(reinterpret_cast<const u32x4*>(arena[i % R]), n, st, out);
+        }, reps, s);
+        std::printf("{\"kind\":\"time\",\"kernarg_preload\":%d,\"pass\":%d,\"launches\":%d,\"product_verify_us\":%.2f,"
+                    "\"replica_verify_us\":%.2f,\"plain_read_us\":%.2f,\"product_GBps\":%.1f,\"plain_GBps\":%.1f,"
+                    "\"product_over_plain\":%.4f}\n",
+                    kp ? 1 : 0, pass, reps, t_prod, t_rep, t_plain, bytes / t_prod / 1e3, bytes / t_plain / 1e3,
+                    t_prod / t_plain);
+        std::fflush(stdout);
+    }
+    // timelines: the last of 3 launches of each (rotating arenas), alternating
+    std::vector<uint64_t> h((size_t)grid * kSt);
+    for (int pass = 0; pass < passes; ++pass) {
+        for (int which = 0; which < 2; ++which) {
+            for (int rep = 0; rep < 3; ++rep) {
+                CHECK(hipMemsetAsync(st, 0, (size_t)grid * kSt * 8, s));
+                if (which == 0)
+                    verify_replica<true><<<grid, 256, 0, s>>>(arena[rep % R], bytes, d, n, res, ctr, cff, n, st);
+                else
+                    plain_read<true><<<grid, 256, 0, s>>>(reinterpret_cast<const u32x4*>(arena[rep % R]), n, st, out);
+                CHECK(hipStreamSynchronize(s));
+            }
+            CHECK(hipMemcpy(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost));
+            print_timeline(which == 0 ? "verify_replica" : "plain_read", h, grid, kp);
+        }
+    }
+    return 0;
+}
