@@ -12,7 +12,8 @@ STEPS=${STEPS:-all}
 run() { echo "[$(date +%T)] $*" | tee -a "$OUT/steps.log"; }
 if [[ $STEPS == all || $STEPS == *tests* ]]; then
   run pytest-gpu
-  timeout -k 10 400 python -m pytest tests -m gpu -x -q -p no:cacheprovider > "$OUT/pytest_gpu.log" 2>&1
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread \
+    > "$OUT/pytest_gpu.log" 2>&1
   run smoke
   timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
 fi
@@ -63,5 +64,18 @@ if [[ $STEPS == all || $STEPS == *dgprof* ]]; then
     timeout -k 10 300 rocprofv3 --pmc $ctr --kernel-trace -d "$OUT/prof_dg_pmc_$ctr" -o run --output-format csv \
       -- python3 bench.py --no-cpu-baseline --extras-only datagram --steps 5 --warmup 2 > "$OUT/prof_dg_pmc_$ctr.json" 2> "$OUT/prof_dg_pmc_$ctr.err"
   done
+fi
+if [[ $STEPS == *timeline* ]]; then
+  # the product verify kernel beside a plain read of the same shape: times and per-workgroup timelines,
+  # without and with the kernel arguments preloaded into SGPRs (tools/verify_timeline.hip)
+  run verify-timeline
+  timeout -k 10 120 tools/verify_timeline 3 64 > "$OUT/verify_timeline.jsonl" 2> "$OUT/verify_timeline.err"
+  run verify-timeline-kp
+  timeout -k 10 120 tools/verify_timeline_kp 3 64 > "$OUT/verify_timeline_kp.jsonl" 2> "$OUT/verify_timeline_kp.err"
+fi
+if [[ $STEPS == *deferred_ab* ]]; then
+  # config-1 DEFERRED vs verify off: background PCIe reads, recv-ring footprint (tools/deferred_ab.cpp)
+  run deferred-ab
+  timeout -k 10 600 tools/deferred_ab 3 > "$OUT/deferred_ab.jsonl" 2> "$OUT/deferred_ab.err"
 fi
 run done
