@@ -13,10 +13,22 @@
  * (:360-530).
  *
  * GPU side (batched, device-resident): cts_media_stream_fill writes whole data
- * datagrams; cts_media_stream_verify parses + validates every received
- * datagram and verifies the data payloads in one pass.
+ * datagrams; the receive pass parses + validates every received datagram and
+ * verifies the data payloads in one pass. It comes in three output forms:
+ *   - frame sums (cts_media_stream_verify_frames / _strided_frames): the product
+ *     receive path (the DEFERRED MediaStream client pattern uses it); 2-3 % over
+ *     the bare payload verify per 16 M datagrams;
+ *   - compact statuses, 16 B per datagram (cts_media_stream_verify_status /
+ *     _strided_status): per-datagram replay of a batch the sums cannot account
+ *     for; 5-13 % over the bare verify;
+ *   - records + results, 44 B per datagram (cts_media_stream_verify / _strided):
+ *     DIAGNOSTIC, for a caller that keeps the jitter log's sender timestamps or
+ *     wants every datagram's first mismatch. 16-24 % over the bare verify: a
+ *     write stream of 3 % of the bytes read costs an HBM read stream that much
+ *     whatever its shape ("Why the outputs cost 20 %").
+ *     Not a throughput path; use the frame sums or the statuses.
  * Host side: cts_media_stream_split (frame -> datagram sizes) and the client's
- * frame accounting (cts_media_stream_client_*), fed with the GPU's records.
+ * frame accounting (cts_media_stream_client_*), fed with any of the three.
  * The ctsIoPattern form of both MediaStream roles (connection-id and START
  * datagrams, timed frame sends, the client's timers on a pattern thread) is
  * CTS_PATTERN_MEDIA_STREAM in cts_pattern.h, built on these calls.
@@ -103,7 +115,9 @@ int cts_media_stream_fill_strided(cts_engine* engine, void* dev_arena, uint64_t 
                                   const uint32_t* dev_lengths, const cts_datagram_header* dev_headers, uint32_t n,
                                   void* stream);
 
-/* Receiver: d.length = completed bytes of datagram i at d.byte_offset
+/* Receiver, records + results form (DIAGNOSTIC: see the top of this header; the throughput paths are
+ * cts_media_stream_verify_frames and cts_media_stream_verify_status).
+ * d.length = completed bytes of datagram i at d.byte_offset
  * (skip_head/expected ignored). records[i] gets the parsed header; for DATA
  * datagrams results[i] is the payload verify (skip 26, expected offset 0,
  * RtlCompareMemory semantics, ctsIOPatternMediaStream.cpp:185-192) and the
@@ -114,7 +128,7 @@ int cts_media_stream_verify(cts_engine* engine, const void* dev_arena, uint64_t 
                             const cts_buf_desc* dev_descs, uint32_t n, cts_datagram_record* dev_records,
                             cts_verify_result* dev_results, void* dev_counters, void* stream);
 
-/* The same receive pass over a uniformly strided receive ring: datagram i occupies
+/* The same receive pass (records + results: DIAGNOSTIC) over a uniformly strided receive ring: datagram i occupies
  * [i * stride, i * stride + dev_lengths[i]) of the arena (the completed byte count of the recv
  * posted into that slot, ctsMediaStreamClient.cpp:268,404), so the kernel reads 4 bytes of
  * metadata per datagram instead of a 24-byte descriptor. A length above the stride or past the
@@ -240,7 +254,10 @@ int cts_media_stream_client_window(const cts_media_stream_client* client, cts_fr
 /* CompleteIo of a batch of n datagrams from its GPU sums (cts_media_stream_verify_frames over `window`, folded;
  * frame_bytes[window->frames] copied to host). Returns a cts_io_status as cts_media_stream_client_complete does
  * (every datagram consumed), CTS_MS_FRAMES_REPLAY when the batch holds an exception (nothing applied: replay it with
- * cts_media_stream_client_complete_status), or CTS_E_INVALID when `window` is not the client's current one. */
+ * cts_media_stream_client_complete_status), or CTS_E_INVALID when `window` is not the client's current one.
+ * Frames booked from sums (as from statuses) carry no sender timestamps (0): the jitter log's time-in-flight estimate
+ * (ctsIOPatternMediaStream.cpp:366-393) is left at 0 for them rather than computed from a zero frequency; a caller
+ * that logs jitter uses the records form. */
 #define CTS_MS_FRAMES_REPLAY 16
 int cts_media_stream_client_complete_frames(cts_media_stream_client* client, const cts_frame_window* window,
                                             const cts_frame_totals* totals, const uint64_t* frame_bytes, uint32_t n,
