@@ -102,6 +102,7 @@ class CtsPatternStats(ctypes.Structure):
         ("fail_completion", ctypes.c_uint32),
         ("bytes_sent_held", ctypes.c_uint64),
         ("bytes_recv_held", ctypes.c_uint64),
+        ("verify_wait_ns", ctypes.c_uint64),
     ]
 
     def as_dict(self) -> dict:

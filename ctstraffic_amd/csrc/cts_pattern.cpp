@@ -475,6 +475,13 @@ struct cts_io_pattern {
         return p;
     }();
     uint32_t desc_set = 0;  // the half the filling batch uses
+    // time the calls spent waiting for a DEFERRED batch's device verdicts (cts_pattern_stats.verify_wait_ns)
+    uint64_t verify_wait_ns = 0;
+    void AddVerifyWait(std::chrono::steady_clock::time_point t0)
+    {
+        verify_wait_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                              std::chrono::steady_clock::now() - t0).count();
+    }
     // DEFERRED zero-copy ring: the recv container holds (1 or 2) x BatchCapacity() + recvCount + 1
     // buffer slots and a completed buffer's slot is not handed out again before its batch was
     // verified, so a batch is verified in place (no staging copy)
@@ -970,6 +977,13 @@ struct cts_io_pattern {
     hipEvent_t sync_done = nullptr;
     hipError_t SleepSync(uint32_t step_us)
     {
+        const auto w0 = std::chrono::steady_clock::now();
+        const hipError_t rc = SleepSyncImpl(step_us);
+        AddVerifyWait(w0);
+        return rc;
+    }
+    hipError_t SleepSyncImpl(uint32_t step_us)
+    {
         if (retire_wait != 2) return hipStreamSynchronize(stream);
         if (sync_done == nullptr && hipEventCreateWithFlags(&sync_done, hipEventDisableTiming) != hipSuccess) {
             sync_done = nullptr;
@@ -1000,7 +1014,10 @@ struct cts_io_pattern {
     int Retire()
     {
         if (inflight.empty()) return CTS_OK;
-        if (WaitInflight() != hipSuccess) return CTS_E_HIP;
+        const auto w0 = std::chrono::steady_clock::now();
+        const hipError_t wr = WaitInflight();
+        AddVerifyWait(w0);
+        if (wr != hipSuccess) return CTS_E_HIP;
         const size_t half = (size_t)(desc_set ^ 1u) * BatchCapacity();
         const bool failed = ApplyVerdicts(inflight, reinterpret_cast<const cts_verify_result*>(stage_res.host) + half);
         inflight.clear();
@@ -1049,7 +1066,10 @@ struct cts_io_pattern {
         } else {
             const int rc = LaunchBatch();
             if (rc != CTS_OK) return rc;
-            if (hipStreamSynchronize(stream) != hipSuccess) return CTS_E_HIP;
+            const auto w0 = std::chrono::steady_clock::now();
+            const hipError_t wr = hipStreamSynchronize(stream);
+            AddVerifyWait(w0);
+            if (wr != hipSuccess) return CTS_E_HIP;
             res = reinterpret_cast<const cts_verify_result*>(stage_res.host) + (size_t)desc_set * BatchCapacity();
         }
         ApplyVerdicts(queue, res);
@@ -2212,6 +2232,7 @@ int cts_io_pattern_get_stats(const cts_io_pattern* p, cts_pattern_stats* o)
     o->fail_actual = p->fail_actual;
     o->has_failure = p->has_failure ? 1 : 0;
     o->fail_completion = p->fail_completion;
+    o->verify_wait_ns = p->verify_wait_ns;
     return CTS_OK;
 }
 

@@ -200,6 +200,9 @@ typedef struct cts_pattern_stats {
      * are dropped without ever being published. 0 in SYNC mode. */
     uint64_t bytes_sent_held;
     uint64_t bytes_recv_held;
+    /* DEFERRED: wall time this pattern's calls spent waiting for batch verdicts from the device (retiring the in-flight
+     * half, a flush's synchronize, a MediaStream client's batch): the receive thread is idle on the GPU meanwhile. */
+    uint64_t verify_wait_ns;
 } cts_pattern_stats;
 
 /* Batch verifier hook: verify n buffers of a host arena (results[i] per

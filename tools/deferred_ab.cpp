@@ -20,6 +20,7 @@
 
 #include "cts_engine.h"
 #include "cts_loopback.h"
+#include "cts_pattern.h"
 
 namespace {
 
@@ -85,9 +86,12 @@ void leg(const char* name, int round, cts_engine* e, uint32_t verify, uint32_t m
     c.batch_buffers = batch;
     c.corrupt_connection = ~0u;
     cts_loopback_result r{};
+    std::vector<cts_loopback_side> sides(2 * c.connections);
     if (bg != nullptr) bg->start();
     const auto t0 = std::chrono::steady_clock::now();
-    const int rc = cts_loopback_run(&c, verify ? e : nullptr, nullptr, nullptr, &r);
+    cts_engine* engines[1] = {e};
+    const int rc = cts_loopback_run_detailed(&c, verify ? engines : nullptr, verify ? 1u : 0u, nullptr, nullptr, &r,
+                                             sides.data());
     const double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     double bg_gbps = 0;
     if (bg != nullptr) {
@@ -95,11 +99,18 @@ void leg(const char* name, int round, cts_engine* e, uint32_t verify, uint32_t m
         bg_gbps = (double)bg->bytes.load() / wall / 1e9;
     }
     const double gib = (double)r.bytes_recv / (double)(1ull << 30);
-    std::printf("{\"leg\":\"%s\",\"round\":%d,\"rc\":%d,\"connections_ok\":%u,\"GBps_recv\":%.3f,"
+    double wait_s = 0;  // the receiving (server) sides' waits for device verdicts
+    for (uint32_t i = c.connections; i < 2 * c.connections; ++i) wait_s += (double)sides[i].stats.verify_wait_ns * 1e-9;
+    const double thread_s = r.seconds * c.connections;  // wall time of the receive threads
+    std::printf("{\"leg\":\"%s\",\"round\":%d,\"rc\":%d,\"hw_queues\":\"%s\",\"connections_ok\":%u,"
+                "\"GBps_recv\":%.3f,\"recv_busy_frac\":%.3f,\"send_busy_frac\":%.3f,\"recv_verify_wait_frac\":%.3f,"
+                "\"recv_verify_wait_s_per_GiB\":%.4f,"
                 "\"recv_cpu_s_per_GiB\":%.4f,\"recv_socket_cpu_s_per_GiB\":%.4f,\"recv_pattern_cpu_s_per_GiB\":%.4f,"
                 "\"send_cpu_s_per_GiB\":%.4f,\"batch_buffers\":%u,\"ring_MiB_per_connection\":%.2f,"
                 "\"background_pcie_read_GBps\":%.1f}\n",
-                name, round, rc, r.connections_ok, (double)r.bytes_recv / r.seconds / 1e9, r.recv_cpu_seconds / gib,
+                name, round, rc, std::getenv("GPU_MAX_HW_QUEUES") ? std::getenv("GPU_MAX_HW_QUEUES") : "default",
+                r.connections_ok, (double)r.bytes_recv / r.seconds / 1e9, r.recv_cpu_seconds / thread_s,
+                r.send_cpu_seconds / thread_s, wait_s / thread_s, wait_s / gib, r.recv_cpu_seconds / gib,
                 r.recv_io_cpu_seconds / gib, (r.recv_cpu_seconds - r.recv_io_cpu_seconds) / gib, r.send_cpu_seconds / gib,
                 batch, mode == CTS_VERIFY_DEFERRED && verify ? (2.0 * batch + 2.0) * 65536.0 / (1 << 20) : 0.0, bg_gbps);
     std::fflush(stdout);
@@ -112,13 +123,21 @@ int main(int argc, char** argv)
     const int rounds = argc > 1 ? std::atoi(argv[1]) : 3;
     cts_engine* e = nullptr;
     if (cts_engine_create(0, &e) != CTS_OK) return 1;
+    // g_senderSharedBuffer from the fill kernel before any leg (the verify-off legs create patterns without an engine)
+    if (cts_shared_buffer_init(e, 65536) != CTS_OK) return 2;
     Background bg;
     if (!bg.init(e)) return 2;
     for (int r = 0; r < rounds; ++r) {
-        leg("verify_off", r, e, 0, CTS_VERIFY_SYNC, 0, nullptr);
-        leg("verify_off_plus_pcie_reads", r, e, 0, CTS_VERIFY_SYNC, 0, &bg);
-        leg("gpu_deferred_batch512", r, e, 1, CTS_VERIFY_DEFERRED, 512, nullptr);
-        leg("gpu_deferred_batch16", r, e, 1, CTS_VERIFY_DEFERRED, 16, nullptr);
+        // the legs in a rotated order each round, so no leg always follows the same one
+        for (int k = 0; k < 5; ++k) {
+            switch ((k + r) % 5) {
+            case 0: leg("verify_off", r, e, 0, CTS_VERIFY_SYNC, 0, nullptr); break;
+            case 1: leg("verify_off_plus_pcie_reads", r, e, 0, CTS_VERIFY_SYNC, 0, &bg); break;
+            case 2: leg("gpu_deferred_batch512", r, e, 1, CTS_VERIFY_DEFERRED, 512, nullptr); break;
+            case 3: leg("gpu_deferred_batch2048", r, e, 1, CTS_VERIFY_DEFERRED, 2048, nullptr); break;
+            case 4: leg("gpu_deferred_batch64", r, e, 1, CTS_VERIFY_DEFERRED, 64, nullptr); break;
+            }
+        }
     }
     (void)cts_engine_destroy(e);
     return 0;

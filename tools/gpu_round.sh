@@ -68,14 +68,19 @@ fi
 if [[ $STEPS == *timeline* ]]; then
   # the product verify kernel beside a plain read of the same shape: times and per-workgroup timelines,
   # without and with the kernel arguments preloaded into SGPRs (tools/verify_timeline.hip)
-  run verify-timeline
-  timeout -k 10 120 tools/verify_timeline 3 64 > "$OUT/verify_timeline.jsonl" 2> "$OUT/verify_timeline.err"
-  run verify-timeline-kp
-  timeout -k 10 120 tools/verify_timeline_kp 3 64 > "$OUT/verify_timeline_kp.jsonl" 2> "$OUT/verify_timeline_kp.err"
+  for rep in 1 2; do  # the two builds alternated
+    run verify-timeline $rep
+    timeout -k 10 120 tools/verify_timeline 3 64 >> "$OUT/verify_timeline.jsonl" 2>> "$OUT/verify_timeline.err"
+    run verify-timeline-kp $rep
+    timeout -k 10 120 tools/verify_timeline_kp 3 64 >> "$OUT/verify_timeline_kp.jsonl" 2>> "$OUT/verify_timeline_kp.err"
+  done
 fi
 if [[ $STEPS == *deferred_ab* ]]; then
   # config-1 DEFERRED vs verify off: background PCIe reads, recv-ring footprint (tools/deferred_ab.cpp)
   run deferred-ab
-  timeout -k 10 600 tools/deferred_ab 3 > "$OUT/deferred_ab.jsonl" 2> "$OUT/deferred_ab.err"
+  timeout -k 10 300 tools/deferred_ab 5 > "$OUT/deferred_ab.jsonl" 2> "$OUT/deferred_ab.err"
+  # the same with as many HIP hardware queues as connections (one connection's verify never queues behind another's)
+  run deferred-ab-8q
+  GPU_MAX_HW_QUEUES=8 timeout -k 10 300 tools/deferred_ab 5 > "$OUT/deferred_ab_8q.jsonl" 2> "$OUT/deferred_ab_8q.err"
 fi
 run done
