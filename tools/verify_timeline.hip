@@ -57,8 +57,25 @@ __global__ void fill_arena(u32x4* a, const cts_buf_desc* d, uint32_t n)
     }
 }
 
-// scan_whole_exact_impl (cts_kernels.hip) with the first round's two loads already issued (SPEC below)
-template <bool EVEN>
+// Expected chunk u of a round (cts::expected_step<256, 2, PH == 1> for PH 0 / 1). PH 2: the span starts on a
+// 16-aligned pattern position, so a chunk's eight u16 values k..k+7 (k % 8 == 0) never cross the 32768 wrap: only
+// the round's base needs the per-half mask, and the four words are that base plus constants (5 VALU, not 8).
+template <int PH>
+__device__ __forceinline__ u32x4 expected_local(uint32_t B, int u, uint32_t sh)
+{
+    if constexpr (PH == 2) {
+        uint32_t bb = B;
+        asm volatile("" : "+v"(bb));
+        const uint32_t b = (bb + (uint32_t)u * 2048u * 0x10001u) & 0x7FFF7FFFu;
+        return u32x4{b, b + 0x20002u, b + 0x40004u, b + 0x60006u};
+    } else {
+        return cts::expected_step<256, 2, PH == 1>(B, u, sh);
+    }
+}
+
+// scan_whole_exact_impl (cts_kernels.hip) for whole-round spans, optionally with the first round's two loads already
+// issued (PRE: SPEC below), with the PH expected-word forms
+template <int PH, bool PRE>
 __device__ __forceinline__ void scan_whole_exact_pre(const cts::Span& s, __amdgpu_buffer_rsrc_t r, uint32_t lane,
                                                      u32x4 p0, u32x4 p1, uint32_t& first, uint32_t& count)
 {
@@ -66,7 +83,7 @@ __device__ __forceinline__ void scan_whole_exact_pre(const cts::Span& s, __amdgp
     const uint32_t voff = lane * 16u;
     for (uint32_t cb = 0; cb + (uint32_t)(TEAM * U) <= s.nchunks; cb += (uint32_t)(TEAM * U)) {
         u32x4 d[U];
-        if (cb == 0) {
+        if (PRE && cb == 0) {
             d[0] = p0;
             d[1] = p1;
         } else {
@@ -78,7 +95,7 @@ __device__ __forceinline__ void scan_whole_exact_pre(const cts::Span& s, __amdgp
         uint32_t any = 0;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            d[u] ^= cts::expected_step<TEAM, U, EVEN>(B, u, s.sh);
+            d[u] ^= expected_local<PH>(B, u, s.sh);
             any |= cts::or4(d[u]);
             __builtin_amdgcn_sched_barrier(0);
         }
@@ -89,12 +106,26 @@ __device__ __forceinline__ void scan_whole_exact_pre(const cts::Span& s, __amdgp
     }
 }
 
+template <bool PRE, bool A16>
+__device__ __forceinline__ void scan_local(const cts::Span& s, uint32_t lane, u32x4 p0, u32x4 p1, uint32_t& first,
+                                           uint32_t& count)
+{
+    const __amdgpu_buffer_rsrc_t r = cts::span_rsrc(s);
+    if (A16 && __builtin_amdgcn_readfirstlane(s.q0 & 15u) == 0u)
+        scan_whole_exact_pre<2, PRE>(s, r, lane, p0, p1, first, count);
+    else if (__builtin_amdgcn_readfirstlane(s.sh) == 0u)
+        scan_whole_exact_pre<1, PRE>(s, r, lane, p0, p1, first, count);
+    else
+        scan_whole_exact_pre<0, PRE>(s, r, lane, p0, p1, first, count);
+}
+
 // verify_wg_kernel<2, true, true, false, true, true> (the product's variant 13) on the whole-line path every config-2
 // buffer takes, built from the same helpers; STAMP adds the timeline stores (lane 0, one 8-byte store per event).
 // SPEC: the first buffer's first round is loaded before its descriptor arrives, from the slot a uniformly strided
 // arena would give it (byte offset i * arena_bytes / n, that many bytes), and used if the descriptor says so (a
 // whole-line span of exactly that slot); otherwise it is dropped and the buffer streams as usual.
-template <bool STAMP, bool SPEC = false>
+// A16: spans on a 16-aligned pattern position take expected_local<2> (the other spans as the product)
+template <bool STAMP, bool SPEC = false, bool A16 = false>
 __global__ void __launch_bounds__(256, 8)
     verify_replica(const uint8_t* __restrict__ arena, uint64_t arena_bytes, const cts_buf_desc* __restrict__ descs,
                    uint32_t n, cts_verify_result* __restrict__ results, uint64_t* __restrict__ counters,
@@ -133,9 +164,9 @@ __global__ void __launch_bounds__(256, 8)
         if (SPEC && k == 0 &&
             __builtin_amdgcn_readfirstlane((d.byte_offset == g_off && d.length == g_len && d.skip_head == 0u &&
                                             cts::span_whole_lines(s)) ? 1u : 0u)) {
-            const __amdgpu_buffer_rsrc_t r = cts::span_rsrc(s);
-            if (__builtin_amdgcn_readfirstlane(s.sh) == 0u) scan_whole_exact_pre<true>(s, r, lane, p0, p1, first, count);
-            else scan_whole_exact_pre<false>(s, r, lane, p0, p1, first, count);
+            scan_local<true, A16>(s, lane, p0, p1, first, count);
+        } else if (A16 && __builtin_amdgcn_readfirstlane((cts::span_whole_lines(s) && s.nchunks % 512u == 0u) ? 1u : 0u)) {
+            scan_local<false, A16>(s, lane, p0, p1, first, count);
         } else {
             cts::scan_whole_exact<256, 2, true, true>(s, lane, first, count);
         }
@@ -287,9 +318,9 @@ int main(int argc, char** argv)
     for (auto& a : arena) {
         CHECK(hipMalloc((void**)&a, bytes));
         fill_arena<<<4096, 256>>>(reinterpret_cast<u32x4*>(a), d, n);
-        // one corrupt byte per 1024 buffers
-        for (uint32_t b = 0; b < n; b += 1024) {
-            const uint64_t off = ((uint64_t)b << 16) + 12345u;
+        // one corrupt byte per 1024 buffers (in the second round), and two in a first round (the SPEC round)
+        for (uint32_t b : {0u, 1024u, 2048u, 3072u, 5u, 1029u}) {
+            const uint64_t off = ((uint64_t)b << 16) + (b % 1024u ? 77u : 12345u);
             uint8_t v = 0;
             CHECK(hipMemcpy(&v, a + off, 1, hipMemcpyDeviceToHost));
             v ^= 0x5A;
@@ -334,9 +365,18 @@ int main(int argc, char** argv)
         verify_replica<false, true><<<grid, 256, 0, s>>>(arena[0], bytes, d, n, res, ctr, cff, n, st);
         CHECK(hipMemcpy(c.data(), res, n * sizeof(cts_verify_result), hipMemcpyDeviceToHost));
         const bool spec_same = eq(a, c);
+        CHECK(hipMemset(res, 0, n * sizeof(cts_verify_result)));
+        verify_replica<false, true, true><<<grid, 256, 0, s>>>(arena[0], bytes, d, n, res, ctr, cff, n, st);
+        CHECK(hipMemcpy(c.data(), res, n * sizeof(cts_verify_result), hipMemcpyDeviceToHost));
+        const bool both_same = eq(a, c);
+        CHECK(hipMemset(res, 0, n * sizeof(cts_verify_result)));
+        verify_replica<false, false, true><<<grid, 256, 0, s>>>(arena[0], bytes, d, n, res, ctr, cff, n, st);
+        CHECK(hipMemcpy(c.data(), res, n * sizeof(cts_verify_result), hipMemcpyDeviceToHost));
+        const bool a16_same = eq(a, c);
         std::printf("{\"kind\":\"parity\",\"kernarg_preload\":%d,\"replica_equals_product\":%d,"
-                    "\"spec_equals_product\":%d,\"failed_buffers\":%u}\n",
-                    kp ? 1 : 0, same ? 1 : 0, spec_same ? 1 : 0, failed);
+                    "\"spec_equals_product\":%d,\"a16_equals_product\":%d,\"spec_a16_equals_product\":%d,"
+                    "\"failed_buffers\":%u}\n",
+                    kp ? 1 : 0, same ? 1 : 0, spec_same ? 1 : 0, a16_same ? 1 : 0, both_same ? 1 : 0, failed);
     }
 
     for (int pass = 0; pass < passes; ++pass) {
@@ -353,11 +393,19 @@ int main(int argc, char** argv)
         const double t_spec = time_us([&](int i) {
             verify_replica<false, true><<<grid, 256, 0, s>>>(arena[i % R], bytes, d, n, res, ctr, cff, n, st);
         }, reps, s);
+        const double t_a16 = time_us([&](int i) {
+            verify_replica<false, false, true><<<grid, 256, 0, s>>>(arena[i % R], bytes, d, n, res, ctr, cff, n, st);
+        }, reps, s);
+        const double t_both = time_us([&](int i) {
+            verify_replica<false, true, true><<<grid, 256, 0, s>>>(arena[i % R], bytes, d, n, res, ctr, cff, n, st);
+        }, reps, s);
         std::printf("{\"kind\":\"time\",\"kernarg_preload\":%d,\"pass\":%d,\"launches\":%d,\"product_verify_us\":%.2f,"
-                    "\"replica_verify_us\":%.2f,\"spec_verify_us\":%.2f,\"plain_read_us\":%.2f,\"product_GBps\":%.1f,"
-                    "\"plain_GBps\":%.1f,\"product_over_plain\":%.4f,\"spec_over_plain\":%.4f}\n",
-                    kp ? 1 : 0, pass, reps, t_prod, t_rep, t_spec, t_plain, bytes / t_prod / 1e3, bytes / t_plain / 1e3,
-                    t_prod / t_plain, t_spec / t_plain);
+                    "\"replica_verify_us\":%.2f,\"spec_verify_us\":%.2f,\"a16_verify_us\":%.2f,\"spec_a16_verify_us\":%.2f,"
+                    "\"plain_read_us\":%.2f,\"product_GBps\":%.1f,"
+                    "\"plain_GBps\":%.1f,\"product_over_plain\":%.4f,\"spec_over_plain\":%.4f,\"a16_over_plain\":%.4f,"
+                    "\"spec_a16_over_plain\":%.4f}\n",
+                    kp ? 1 : 0, pass, reps, t_prod, t_rep, t_spec, t_a16, t_both, t_plain, bytes / t_prod / 1e3,
+                    bytes / t_plain / 1e3, t_prod / t_plain, t_spec / t_plain, t_a16 / t_plain, t_both / t_plain);
         std::fflush(stdout);
     }
     // timelines: the last of 3 launches of each (rotating arenas), alternating
