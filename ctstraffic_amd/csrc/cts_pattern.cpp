@@ -2089,6 +2089,17 @@ int cts_io_pattern_create(const cts_pattern_config* c, cts_engine* engine, cts_i
 int cts_io_pattern_destroy(cts_io_pattern* p)
 {
     if (p == nullptr) return CTS_E_INVALID;
+    {
+        // DEFERRED: completions still waiting for a verdict are verified now, so their bytes reach TcpStatusDetails
+        // as the reference's (verified at completion) did; best effort, nothing may leave the ABI
+        std::lock_guard<std::recursive_mutex> lk(p->mu);
+        if (p->fail_fast.empty() && p->VerdictsPending()) {
+            try {
+                (void)p->FlushPending();
+            } catch (...) {
+            }
+        }
+    }
     delete p;
     return CTS_OK;
 }

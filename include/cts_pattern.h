@@ -249,6 +249,8 @@ void cts_shared_buffer_release(void);
 /* engine may be NULL only when verify_buffers == 0 or a batch verifier is set
  * with cts_io_pattern_set_verifier before the first CompleteIo. */
 int cts_io_pattern_create(const cts_pattern_config* config, cts_engine* engine, cts_io_pattern** out);
+/* A DEFERRED pattern destroyed with completions still waiting for their batch verdict verifies them first, so their
+ * bytes are published (cts_pattern_stats.bytes_*_held) as the reference counted them at completion. */
 int cts_io_pattern_destroy(cts_io_pattern* pattern);
 int cts_io_pattern_set_verifier(cts_io_pattern* pattern, cts_batch_verifier fn, void* ctx);
 

@@ -1501,3 +1501,27 @@ def test_send_pacing_matches_restatement(seed):
         p.close()
     finally:
         clock_set(None)
+
+
+def test_deferred_destroy_publishes_held_bytes(make):
+    """A DEFERRED pattern destroyed while completions wait for their batch verdict verifies them first, so their bytes
+    reach TcpStatusDetails: the reference verified and counted every completion inside its CompleteIo
+    (ctsIOPattern.cpp:461-521) whenever the connection was torn down."""
+    from ctstraffic_amd.pattern import status_details, status_details_reset
+
+    p = make(**server_defaults(buffer_size=4096, transfer_size=100 * 4096, batch_buffers=64))
+    status_details_reset()
+    t = p.InitiateIo()
+    assert p.CompleteIo(t, ConnectionIdLength, 0) == ContinueIo
+    for _ in range(5):
+        t = p.InitiateIo()
+        assert _complete_data_recv(p, t, 4096) == ContinueIo
+    s = p.stats()
+    held = s["bytes_recv_held"]
+    if make.mode == A.VERIFY_SYNC:
+        assert held == 0 and s["bytes_recv"] == 5 * 4096
+    else:
+        assert held == 5 * 4096 and s["bytes_recv"] == 0 and s["queued"] == 5
+    assert status_details()["bytes_recv"] == 5 * 4096 - held
+    p.close()
+    assert status_details()["bytes_recv"] == 5 * 4096
