@@ -62,7 +62,10 @@ VERIFY_KERNELS = {0: "cts::verify_wg_kernel<8,true>", 1: "cts::verify_wg_kernel<
                   11: "cts::verify_wg_kernel<4,true,true,false,true,true>",
                   12: "cts::verify_wg_kernel<8,true,true,false,true,true>",
                   13: "cts::verify_wg_kernel<2,true,true,false,true,true>",
-                  14: "cts::verify_wg_kernel<1,true,true,false,true,true>"}
+                  14: "cts::verify_wg_kernel<1,true,true,false,true,true>",
+                  22: "cts::verify_wg_kernel<2,true,true,false,true,true,1,0,0,256,true>",
+                  23: "cts::verify_wg_kernel<2,true,true,false,true,true,1,0,0,256,false,true>",
+                  24: "cts::verify_wg_kernel<2,true,true,false,true,true,1,0,0,256,true,true>"}
 
 
 def verify_kernel_name(variant: int) -> str:

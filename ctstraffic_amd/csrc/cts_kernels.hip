@@ -215,6 +215,19 @@ __device__ __forceinline__ u32x4 expected_step(uint32_t B, int u, uint32_t sh)
     }
 }
 
+// expected_step for a span on a 16-aligned pattern position (q0 % 16 == 0): every chunk's eight u16 values
+// k..k+7 have k % 8 == 0, so none crosses the 32768 wrap inside the chunk; only the packed base needs the per-half
+// mask, and the four words are that base plus constants (5 VALU per chunk instead of 8).
+template <int TEAM, int U>
+__device__ __forceinline__ u32x4 expected_step_a16(uint32_t B, int u)
+{
+    static_assert(32767 + 8 * TEAM * (U - 1) + 8 < 65536, "packed k must not carry");
+    uint32_t bb = B;
+    asm volatile("" : "+v"(bb));
+    const uint32_t b = (bb + (uint32_t)u * (uint32_t)(8 * TEAM) * 0x10001u) & 0x7FFF7FFFu;
+    return u32x4{b, b + 0x20002u, b + 0x40004u, b + 0x60006u};
+}
+
 // packed base (k*0x10001 + 0x10000) of the chunk at index c
 __device__ __forceinline__ uint32_t chunk_base(const Span& s, uint32_t c)
 {
@@ -415,7 +428,8 @@ __device__ __forceinline__ void scan_exact_whole(const Span& s, uint32_t lane, u
 // during which the workgroup's next buffer waits, and with one corrupt buffer in a
 // thousand that workgroup is the launch's last to finish.) The clean-path cost is
 // one compare and branch per round.
-template <int TEAM, int U, bool NT, bool EVEN>
+// A16: the span starts on a 16-aligned pattern position (expected_step_a16).
+template <int TEAM, int U, bool NT, bool EVEN, bool A16 = false>
 __device__ __forceinline__ void scan_whole_exact_impl(const Span& s, __amdgpu_buffer_rsrc_t r, uint32_t lane,
                                                       uint32_t& first, uint32_t& count)
 {
@@ -431,7 +445,8 @@ __device__ __forceinline__ void scan_whole_exact_impl(const Span& s, __amdgpu_bu
         uint32_t any = 0;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            d[u] ^= expected_step<TEAM, U, EVEN>(B, u, s.sh);
+            if constexpr (A16) d[u] ^= expected_step_a16<TEAM, U>(B, u);
+            else d[u] ^= expected_step<TEAM, U, EVEN>(B, u, s.sh);
             any |= or4(d[u]);
             __builtin_amdgcn_sched_barrier(0);
         }
@@ -450,7 +465,10 @@ __device__ __forceinline__ void scan_whole_exact_impl(const Span& s, __amdgpu_bu
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const bool in = cb + (uint32_t)(u * TEAM) + lane < c_end;
-            d[u] = in ? (d[u] ^ expected_step<TEAM, U, EVEN>(B, u, s.sh)) : u32x4{0u, 0u, 0u, 0u};
+            u32x4 e;
+            if constexpr (A16) e = expected_step_a16<TEAM, U>(B, u);
+            else e = expected_step<TEAM, U, EVEN>(B, u, s.sh);
+            d[u] = in ? (d[u] ^ e) : u32x4{0u, 0u, 0u, 0u};
             any |= or4(d[u]);
             __builtin_amdgcn_sched_barrier(0);
         }
@@ -461,10 +479,16 @@ __device__ __forceinline__ void scan_whole_exact_impl(const Span& s, __amdgpu_bu
     }
 }
 
-template <int TEAM, int U, bool NT, bool SPLIT>
+template <int TEAM, int U, bool NT, bool SPLIT, bool A16 = false>
 __device__ __forceinline__ void scan_whole_exact(const Span& s, uint32_t lane, uint32_t& first, uint32_t& count)
 {
     const __amdgpu_buffer_rsrc_t r = span_rsrc(s);
+    if constexpr (A16) {
+        if (__builtin_amdgcn_readfirstlane(s.q0 & 15u) == 0u) {
+            scan_whole_exact_impl<TEAM, U, NT, true, true>(s, r, lane, first, count);
+            return;
+        }
+    }
     if constexpr (SPLIT) {
         if (__builtin_amdgcn_readfirstlane(s.sh) == 0u) {
             scan_whole_exact_impl<TEAM, U, NT, true>(s, r, lane, first, count);
@@ -692,14 +716,21 @@ __device__ __forceinline__ void flush_staged_results(const cts_verify_result* st
 // UT > 0 (tuning): a workgroup's LAST buffer streams with UT loads per lane per round instead of U, so
 // the workgroups still running once others have finished keep more bytes in flight (the launch's
 // finishing window, DESIGN.md §3 "Where a 256 MiB launch's last few percent go").
+// A16 (XD): whole-line spans on a 16-aligned pattern position build their expected words with expected_step_a16.
+// SPEC: while the workgroup's first descriptor is on its way, the first round of the slot a uniformly strided arena
+// gives buffer i (byte offset i * arena_bytes / n) is read into L2 and dropped; when the descriptor names that slot,
+// its first round then comes from L2 instead of HBM, so the descriptor's latency overlaps the first data fetch
+// instead of preceding it (tools/verify_timeline: 0.56-0.60 against 0.28-0.32 us from entry to the first data
+// load for a plain read). A wrong guess costs one round of reads.
 template <int U, bool NT, bool SPLIT = false, bool SCTR = false, bool WHOLE = false, bool XD = false, int WIN = 1,
-          int DEFER = 0, int UT = 0, int BS = kBlock>
+          int DEFER = 0, int UT = 0, int BS = kBlock, bool A16 = false, bool SPEC = false>
 __global__ void __launch_bounds__(BS, (BS == kBlock ? (U <= 8 ? 8 : 4) : 2048 / BS))
     verify_wg_kernel(const uint8_t* __restrict__ arena, uint64_t arena_bytes, const cts_buf_desc* __restrict__ descs,
                      uint32_t n, cts_verify_result* __restrict__ results, uint64_t* __restrict__ counters,
                      uint32_t* __restrict__ conn_first_fail, uint32_t n_conns)
 {
     static_assert(!(SCTR && DEFER), "deferred results take the finish_buffer path");
+    static_assert(!SPEC || WIN == 1, "the guessed slot is the grid-stride walk's first buffer");
     __shared__ uint64_t ctr[1][5];
     __shared__ cts_verify_result dres[DEFER ? DEFER : 1];
     __shared__ uint32_t didx[DEFER ? DEFER : 1];
@@ -728,6 +759,23 @@ __global__ void __launch_bounds__(BS, (BS == kBlock ? (U <= 8 ? 8 : 4) : 2048 / 
     }
     cts_buf_desc dn;
     if (i < end) dn = descs[i];
+    if constexpr (SPEC) {
+        // the guessed slot's first round, L2-allocating (the default policy), beside the descriptor's load; the data
+        // is dropped once it arrived (the asm keeps the loads), the round's own loads then hit L2
+        if (i < end) {
+            const uint64_t per = arena_bytes / n;
+            if (per >= 16u) {
+                const uint32_t g_len = (uint32_t)(per < (uint64_t)BS * U * 16u ? per : (uint64_t)BS * U * 16u);
+                const __amdgpu_buffer_rsrc_t gr = __builtin_amdgcn_make_buffer_rsrc(
+                    const_cast<uint8_t*>(arena) + (uint64_t)i * per, (short)0, (int)g_len, 0x00020000);
+                u32x4 p[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) p[u] = buf_load<false>(gr, lane * 16u, (uint32_t)(u * BS) * 16u);
+#pragma unroll
+                for (int u = 0; u < U; ++u) asm volatile("" ::"v"(p[u]));
+            }
+        }
+    }
     for (; i < end; i = (uint64_t)i + step < end ? i + step : end) {
         const cts_buf_desc d = dn;
         if ((uint64_t)i + step < end) dn = descs[i + step];
@@ -753,9 +801,9 @@ __global__ void __launch_bounds__(BS, (BS == kBlock ? (U <= 8 ? 8 : 4) : 2048 / 
         } else if (XD && __builtin_amdgcn_readfirstlane(span_whole_lines(s) ? 1u : 0u)) {
             // whole-line span, exact diff in registers: only the reduction is left
             if (UT > 0 && (uint64_t)i + step >= end)
-                scan_whole_exact<BS, (UT > 0 ? UT : U), NT, SPLIT>(s, lane, first, count);
+                scan_whole_exact<BS, (UT > 0 ? UT : U), NT, SPLIT, A16>(s, lane, first, count);
             else
-                scan_whole_exact<BS, U, NT, SPLIT>(s, lane, first, count);
+                scan_whole_exact<BS, U, NT, SPLIT, A16>(s, lane, first, count);
             dirty = __builtin_amdgcn_readfirstlane(__syncthreads_or(first != kNone)) != 0;
             if (dirty) block_reduce_mismatch_bs<BS>(first, count);
         } else {
@@ -2538,6 +2586,17 @@ static void launch_verify_nt(const uint8_t* arena, uint64_t arena_bytes, const c
         // finishing window is cut in whole buffers half as long); the grid cap is blocks_per_cu / 2 workgroups per CU
         case 21: verify_wg_kernel<2, NT, true, false, true, true, 1, 0, 0, 2 * kBlock>
                      <<<grid_for(n, 1, geo, std::max(1, geo.blocks_per_cu / 2)), 2 * kBlock, 0, stream>>>(CTS_VERIFY_ARGS);
+                 break;
+        // 22: variant 13 + 16-aligned spans with the 5-VALU expected words; 23: variant 13 + the first round of the
+        // guessed first slot read into L2 beside the first descriptor; 24: both (round 4, tools/verify_timeline)
+        case 22: verify_wg_kernel<2, NT, true, false, true, true, 1, 0, 0, kBlock, true>
+                     <<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS);
+                 break;
+        case 23: verify_wg_kernel<2, NT, true, false, true, true, 1, 0, 0, kBlock, false, true>
+                     <<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS);
+                 break;
+        case 24: verify_wg_kernel<2, NT, true, false, true, true, 1, 0, 0, kBlock, true, true>
+                     <<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS);
                  break;
         case 7: verify_wg_kernel<4, NT, true><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 1: verify_wg_kernel<4, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;

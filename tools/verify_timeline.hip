@@ -4,7 +4,8 @@
 // The product kernel (cts_kernels.hip, included verbatim) against the plain read of the same shape, in one process on
 // one box, 8 rotated 256 MiB arenas (4096 x 64 KiB buffers each; 75 % phase-0 / 25 % random expected offsets, one
 // corrupt byte per 1024 buffers, as bench.py's config 2):
-//   time    : HIP events around R launches, per launch: the product verify_wg_kernel (variant 13, the default), a
+//   time    : HIP events around R launches, per launch: the product verify_wg_kernel (variant 13, the default; and
+//             the tuning variants 22 = A16, 23 = SPEC, 24 = both, launched directly), a
 //             replica of it built from the same device helpers with the stamps compiled out (must equal the product),
 //             and the plain read (grid = 4 x CUs, workgroup b reads 64-KiB slabs b, b + grid, ..., U = 2, the
 //             verify's per-buffer barrier);
@@ -57,75 +58,9 @@ __global__ void fill_arena(u32x4* a, const cts_buf_desc* d, uint32_t n)
     }
 }
 
-// Expected chunk u of a round (cts::expected_step<256, 2, PH == 1> for PH 0 / 1). PH 2: the span starts on a
-// 16-aligned pattern position, so a chunk's eight u16 values k..k+7 (k % 8 == 0) never cross the 32768 wrap: only
-// the round's base needs the per-half mask, and the four words are that base plus constants (5 VALU, not 8).
-template <int PH>
-__device__ __forceinline__ u32x4 expected_local(uint32_t B, int u, uint32_t sh)
-{
-    if constexpr (PH == 2) {
-        uint32_t bb = B;
-        asm volatile("" : "+v"(bb));
-        const uint32_t b = (bb + (uint32_t)u * 2048u * 0x10001u) & 0x7FFF7FFFu;
-        return u32x4{b, b + 0x20002u, b + 0x40004u, b + 0x60006u};
-    } else {
-        return cts::expected_step<256, 2, PH == 1>(B, u, sh);
-    }
-}
-
-// scan_whole_exact_impl (cts_kernels.hip) for whole-round spans, optionally with the first round's two loads already
-// issued (PRE: SPEC below), with the PH expected-word forms
-template <int PH, bool PRE>
-__device__ __forceinline__ void scan_whole_exact_pre(const cts::Span& s, __amdgpu_buffer_rsrc_t r, uint32_t lane,
-                                                     u32x4 p0, u32x4 p1, uint32_t& first, uint32_t& count)
-{
-    constexpr int TEAM = 256, U = 2;
-    const uint32_t voff = lane * 16u;
-    for (uint32_t cb = 0; cb + (uint32_t)(TEAM * U) <= s.nchunks; cb += (uint32_t)(TEAM * U)) {
-        u32x4 d[U];
-        if (PRE && cb == 0) {
-            d[0] = p0;
-            d[1] = p1;
-        } else {
-#pragma unroll
-            for (int u = 0; u < U; ++u) d[u] = cts::buf_load<true>(r, voff, (cb + (uint32_t)(u * TEAM)) * 16u);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        const uint32_t B = cts::chunk_base(s, cb + lane);
-        uint32_t any = 0;
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            d[u] ^= expected_local<PH>(B, u, s.sh);
-            any |= cts::or4(d[u]);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        if (any != 0u) {
-#pragma unroll
-            for (int u = 0; u < U; ++u) cts::take_diff(s, cb + (uint32_t)(u * TEAM) + lane, d[u], first, count);
-        }
-    }
-}
-
-template <bool PRE, bool A16>
-__device__ __forceinline__ void scan_local(const cts::Span& s, uint32_t lane, u32x4 p0, u32x4 p1, uint32_t& first,
-                                           uint32_t& count)
-{
-    const __amdgpu_buffer_rsrc_t r = cts::span_rsrc(s);
-    if (A16 && __builtin_amdgcn_readfirstlane(s.q0 & 15u) == 0u)
-        scan_whole_exact_pre<2, PRE>(s, r, lane, p0, p1, first, count);
-    else if (__builtin_amdgcn_readfirstlane(s.sh) == 0u)
-        scan_whole_exact_pre<1, PRE>(s, r, lane, p0, p1, first, count);
-    else
-        scan_whole_exact_pre<0, PRE>(s, r, lane, p0, p1, first, count);
-}
-
 // verify_wg_kernel<2, true, true, false, true, true> (the product's variant 13) on the whole-line path every config-2
 // buffer takes, built from the same helpers; STAMP adds the timeline stores (lane 0, one 8-byte store per event).
-// SPEC: the first buffer's first round is loaded before its descriptor arrives, from the slot a uniformly strided
-// arena would give it (byte offset i * arena_bytes / n, that many bytes), and used if the descriptor says so (a
-// whole-line span of exactly that slot); otherwise it is dropped and the buffer streams as usual.
-// A16: spans on a 16-aligned pattern position take expected_local<2> (the other spans as the product)
-template <bool STAMP, bool SPEC = false, bool A16 = false>
+template <bool STAMP>
 __global__ void __launch_bounds__(256, 8)
     verify_replica(const uint8_t* __restrict__ arena, uint64_t arena_bytes, const cts_buf_desc* __restrict__ descs,
                    uint32_t n, cts_verify_result* __restrict__ results, uint64_t* __restrict__ counters,
@@ -138,20 +73,6 @@ __global__ void __launch_bounds__(256, 8)
     const uint32_t step = gridDim.x;
     cts_buf_desc dn;
     if (i < n) dn = descs[i];
-    u32x4 p0 = {0u, 0u, 0u, 0u}, p1 = {0u, 0u, 0u, 0u};
-    uint64_t g_off = ~0ull;
-    uint32_t g_len = 0;
-    if (SPEC && i < n) {
-        const uint64_t per = arena_bytes / n;
-        if (per >= 8192u && per <= 0x7FFFFFF0u && per % 8192u == 0u) {  // whole rounds of 256 lanes x 2 chunks
-            g_len = (uint32_t)per;
-            g_off = (uint64_t)i * per;
-            const __amdgpu_buffer_rsrc_t gr =
-                __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(arena) + g_off, (short)0, (int)g_len, 0x00020000);
-            p0 = cts::buf_load<true>(gr, lane * 16u, 0u);
-            p1 = cts::buf_load<true>(gr, lane * 16u, 256u * 16u);
-        }
-    }
     cts::zero_counters<1>(ctr);
     uint64_t* my = st + (uint64_t)blockIdx.x * kSt;
     for (; i < n; i = i + step < n ? i + step : n, ++k) {
@@ -161,15 +82,7 @@ __global__ void __launch_bounds__(256, 8)
         const cts::Span s = cts::make_span(arena, d);
         if (STAMP && k == 0 && lane == 0) my[1] = stamp_after((uint32_t)d.byte_offset);
         uint32_t first = cts::kNone, count = 0;
-        if (SPEC && k == 0 &&
-            __builtin_amdgcn_readfirstlane((d.byte_offset == g_off && d.length == g_len && d.skip_head == 0u &&
-                                            cts::span_whole_lines(s)) ? 1u : 0u)) {
-            scan_local<true, A16>(s, lane, p0, p1, first, count);
-        } else if (A16 && __builtin_amdgcn_readfirstlane((cts::span_whole_lines(s) && s.nchunks % 512u == 0u) ? 1u : 0u)) {
-            scan_local<false, A16>(s, lane, p0, p1, first, count);
-        } else {
-            cts::scan_whole_exact<256, 2, true, true>(s, lane, first, count);
-        }
+        cts::scan_whole_exact<256, 2, true, true>(s, lane, first, count);
         const bool dirty = __builtin_amdgcn_readfirstlane(__syncthreads_or(first != cts::kNone)) != 0;
         if (dirty) cts::block_reduce_mismatch(first, count);
         if (lane == 0) cts::finish_buffer(s, d, i, first, count, results, ctr[0], conn_first_fail, n_conns);
@@ -212,6 +125,9 @@ __global__ void __launch_bounds__(256) plain_read(const u32x4* __restrict__ p, u
         my[11] = (uint64_t)xcc_id() | ((uint64_t)k << 8);
     }
 }
+
+// the product kernel's tuning variants 22 (A16), 23 (SPEC), 24 (both) beside the default 13
+#define PRODUCT_VARIANT(A16, SPEC) cts::verify_wg_kernel<2, true, true, false, true, true, 1, 0, 0, 256, A16, SPEC>
 
 template <typename F>
 double time_us(F launch, int reps, hipStream_t s)
@@ -362,15 +278,15 @@ int main(int argc, char** argv)
         // the speculative form, on the same arena and on one whose first buffers hold a corrupt byte in round 0
         std::vector<cts_verify_result> c(n);
         CHECK(hipMemset(res, 0, n * sizeof(cts_verify_result)));
-        verify_replica<false, true><<<grid, 256, 0, s>>>(arena[0], bytes, d, n, res, ctr, cff, n, st);
+        PRODUCT_VARIANT(false, true)<<<grid, 256, 0, s>>>(arena[0], bytes, d, n, res, ctr, cff, n);
         CHECK(hipMemcpy(c.data(), res, n * sizeof(cts_verify_result), hipMemcpyDeviceToHost));
         const bool spec_same = eq(a, c);
         CHECK(hipMemset(res, 0, n * sizeof(cts_verify_result)));
-        verify_replica<false, true, true><<<grid, 256, 0, s>>>(arena[0], bytes, d, n, res, ctr, cff, n, st);
+        PRODUCT_VARIANT(true, true)<<<grid, 256, 0, s>>>(arena[0], bytes, d, n, res, ctr, cff, n);
         CHECK(hipMemcpy(c.data(), res, n * sizeof(cts_verify_result), hipMemcpyDeviceToHost));
         const bool both_same = eq(a, c);
         CHECK(hipMemset(res, 0, n * sizeof(cts_verify_result)));
-        verify_replica<false, false, true><<<grid, 256, 0, s>>>(arena[0], bytes, d, n, res, ctr, cff, n, st);
+        PRODUCT_VARIANT(true, false)<<<grid, 256, 0, s>>>(arena[0], bytes, d, n, res, ctr, cff, n);
         CHECK(hipMemcpy(c.data(), res, n * sizeof(cts_verify_result), hipMemcpyDeviceToHost));
         const bool a16_same = eq(a, c);
         std::printf("{\"kind\":\"parity\",\"kernarg_preload\":%d,\"replica_equals_product\":%d,"
@@ -391,16 +307,16 @@ int main(int argc, char** argv)
             plain_read<false><<<grid, 256, 0, s>>>(reinterpret_cast<const u32x4*>(arena[i % R]), n, st, out);
         }, reps, s);
         const double t_spec = time_us([&](int i) {
-            verify_replica<false, true><<<grid, 256, 0, s>>>(arena[i % R], bytes, d, n, res, ctr, cff, n, st);
+            PRODUCT_VARIANT(false, true)<<<grid, 256, 0, s>>>(arena[i % R], bytes, d, n, res, ctr, cff, n);
         }, reps, s);
         const double t_a16 = time_us([&](int i) {
-            verify_replica<false, false, true><<<grid, 256, 0, s>>>(arena[i % R], bytes, d, n, res, ctr, cff, n, st);
+            PRODUCT_VARIANT(true, false)<<<grid, 256, 0, s>>>(arena[i % R], bytes, d, n, res, ctr, cff, n);
         }, reps, s);
         const double t_both = time_us([&](int i) {
-            verify_replica<false, true, true><<<grid, 256, 0, s>>>(arena[i % R], bytes, d, n, res, ctr, cff, n, st);
+            PRODUCT_VARIANT(true, true)<<<grid, 256, 0, s>>>(arena[i % R], bytes, d, n, res, ctr, cff, n);
         }, reps, s);
         std::printf("{\"kind\":\"time\",\"kernarg_preload\":%d,\"pass\":%d,\"launches\":%d,\"product_verify_us\":%.2f,"
-                    "\"replica_verify_us\":%.2f,\"spec_verify_us\":%.2f,\"a16_verify_us\":%.2f,\"spec_a16_verify_us\":%.2f,"
+                    "\"replica_verify_us\":%.2f,\"v23_spec_us\":%.2f,\"v22_a16_us\":%.2f,\"v24_both_us\":%.2f,"
                     "\"plain_read_us\":%.2f,\"product_GBps\":%.1f,"
                     "\"plain_GBps\":%.1f,\"product_over_plain\":%.4f,\"spec_over_plain\":%.4f,\"a16_over_plain\":%.4f,"
                     "\"spec_a16_over_plain\":%.4f}\n",
