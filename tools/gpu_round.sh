@@ -17,6 +17,12 @@ if [[ $STEPS == all || $STEPS == *tests* ]]; then
   run smoke
   timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
 fi
+if [[ $STEPS == *variants* ]]; then
+  # every tuning launch variant bit-exact against the oracle (tests/test_verify_gpu.py::test_launch_variants_parity)
+  run variants-parity
+  timeout -k 10 300 python -u -m pytest tests/test_verify_gpu.py -m gpu -x -q -p no:cacheprovider --timeout 120 \
+    --timeout-method thread -k "launch_variants_parity" > "$OUT/pytest_variants.log" 2>&1
+fi
 if [[ $STEPS == all || $STEPS == *bench* ]]; then
   run bench
   timeout -k 10 400 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
