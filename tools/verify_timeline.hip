@@ -58,6 +58,59 @@ __global__ void fill_arena(u32x4* a, const cts_buf_desc* d, uint32_t n)
     }
 }
 
+// A whole-line span streamed one chunk per lane per step with the next two steps' loads in flight (a pipeline of depth
+// 2 at U = 1): at most 2 KiB in flight per wave, as the product's U = 2 rounds, but never none while the wave compares.
+template <bool EVEN>
+__device__ __forceinline__ void scan_pipe2(const cts::Span& s, uint32_t lane, uint32_t& first, uint32_t& count)
+{
+    const __amdgpu_buffer_rsrc_t r = cts::span_rsrc(s);
+    const uint32_t steps = s.nchunks / 256u;
+    const uint32_t voff = lane * 16u;
+    u32x4 a = cts::buf_load<true>(r, voff, 0u);
+    u32x4 b = cts::buf_load<true>(r, voff, 256u * 16u);  // past the span: reads 0, no request
+    for (uint32_t j = 0; j < steps; ++j) {
+        const u32x4 nxt = cts::buf_load<true>(r, voff, (j + 2u) * 256u * 16u);
+        __builtin_amdgcn_sched_barrier(0);
+        const uint32_t B = cts::chunk_base(s, j * 256u + lane);
+        const u32x4 x = a ^ cts::expected_step<256, 1, EVEN>(B, 0, s.sh);
+        if (cts::or4(x) != 0u) cts::take_diff(s, j * 256u + lane, x, first, count);
+        a = b;
+        b = nxt;
+    }
+}
+
+template <bool STAMP>
+__global__ void __launch_bounds__(256, 8)
+    verify_pipe(const uint8_t* __restrict__ arena, uint64_t arena_bytes, const cts_buf_desc* __restrict__ descs,
+                uint32_t n, cts_verify_result* __restrict__ results, uint64_t* __restrict__ counters,
+                uint32_t* __restrict__ conn_first_fail, uint32_t n_conns)
+{
+    __shared__ uint64_t ctr[1][5];
+    const uint32_t lane = threadIdx.x;
+    uint32_t i = blockIdx.x;
+    const uint32_t step = gridDim.x;
+    cts_buf_desc dn;
+    if (i < n) dn = descs[i];
+    cts::zero_counters<1>(ctr);
+    for (; i < n; i = i + step < n ? i + step : n) {
+        const cts_buf_desc d = dn;
+        if (i + step < n) dn = descs[i + step];
+        if (cts::desc_bad(d, arena_bytes)) continue;
+        const cts::Span s = cts::make_span(arena, d);
+        uint32_t first = cts::kNone, count = 0;
+        if (__builtin_amdgcn_readfirstlane((cts::span_whole_lines(s) && s.nchunks % 256u == 0u) ? 1u : 0u)) {
+            if (__builtin_amdgcn_readfirstlane(s.sh) == 0u) scan_pipe2<true>(s, lane, first, count);
+            else scan_pipe2<false>(s, lane, first, count);
+        } else {
+            cts::scan_whole_exact<256, 2, true, true>(s, lane, first, count);
+        }
+        const bool dirty = __builtin_amdgcn_readfirstlane(__syncthreads_or(first != cts::kNone)) != 0;
+        if (dirty) cts::block_reduce_mismatch(first, count);
+        if (lane == 0) cts::finish_buffer(s, d, i, first, count, results, ctr[0], conn_first_fail, n_conns);
+    }
+    cts::flush_counters<1>(counters, ctr);
+}
+
 // verify_wg_kernel<2, true, true, false, true, true> (the product's variant 13) on the whole-line path every config-2
 // buffer takes, built from the same helpers; STAMP adds the timeline stores (lane 0, one 8-byte store per event).
 template <bool STAMP>
@@ -289,6 +342,10 @@ int main(int argc, char** argv)
         PRODUCT_VARIANT(true, false)<<<grid, 256, 0, s>>>(arena[0], bytes, d, n, res, ctr, cff, n);
         CHECK(hipMemcpy(c.data(), res, n * sizeof(cts_verify_result), hipMemcpyDeviceToHost));
         const bool a16_same = eq(a, c);
+        CHECK(hipMemset(res, 0, n * sizeof(cts_verify_result)));
+        verify_pipe<false><<<grid, 256, 0, s>>>(arena[0], bytes, d, n, res, ctr, cff, n);
+        CHECK(hipMemcpy(c.data(), res, n * sizeof(cts_verify_result), hipMemcpyDeviceToHost));
+        std::printf("{\"kind\":\"parity\",\"pipe2_equals_product\":%d}\n", eq(a, c) ? 1 : 0);
         std::printf("{\"kind\":\"parity\",\"kernarg_preload\":%d,\"replica_equals_product\":%d,"
                     "\"spec_equals_product\":%d,\"a16_equals_product\":%d,\"spec_a16_equals_product\":%d,"
                     "\"failed_buffers\":%u}\n",
@@ -312,15 +369,18 @@ int main(int argc, char** argv)
         const double t_a16 = time_us([&](int i) {
             PRODUCT_VARIANT(true, false)<<<grid, 256, 0, s>>>(arena[i % R], bytes, d, n, res, ctr, cff, n);
         }, reps, s);
+        const double t_pipe = time_us([&](int i) {
+            verify_pipe<false><<<grid, 256, 0, s>>>(arena[i % R], bytes, d, n, res, ctr, cff, n);
+        }, reps, s);
         const double t_both = time_us([&](int i) {
             PRODUCT_VARIANT(true, true)<<<grid, 256, 0, s>>>(arena[i % R], bytes, d, n, res, ctr, cff, n);
         }, reps, s);
         std::printf("{\"kind\":\"time\",\"kernarg_preload\":%d,\"pass\":%d,\"launches\":%d,\"product_verify_us\":%.2f,"
-                    "\"replica_verify_us\":%.2f,\"v23_spec_us\":%.2f,\"v22_a16_us\":%.2f,\"v24_both_us\":%.2f,"
+                    "\"replica_verify_us\":%.2f,\"v23_spec_us\":%.2f,\"v22_a16_us\":%.2f,\"v24_both_us\":%.2f,\"pipe2_us\":%.2f,"
                     "\"plain_read_us\":%.2f,\"product_GBps\":%.1f,"
                     "\"plain_GBps\":%.1f,\"product_over_plain\":%.4f,\"spec_over_plain\":%.4f,\"a16_over_plain\":%.4f,"
                     "\"spec_a16_over_plain\":%.4f}\n",
-                    kp ? 1 : 0, pass, reps, t_prod, t_rep, t_spec, t_a16, t_both, t_plain, bytes / t_prod / 1e3,
+                    kp ? 1 : 0, pass, reps, t_prod, t_rep, t_spec, t_a16, t_both, t_pipe, t_plain, bytes / t_prod / 1e3,
                     bytes / t_plain / 1e3, t_prod / t_plain, t_spec / t_plain, t_a16 / t_plain, t_both / t_plain);
         std::fflush(stdout);
     }
