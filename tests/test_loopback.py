@@ -248,6 +248,8 @@ def _side_view(r, connections, corrupt):
     reference itself leaves to timing is left out: how many bytes the corrupted connection's *sender* got out (and
     the error its send saw) before the receiver's reset reached it."""
     sides = [dict(s) for s in r["sides"]]
+    for s in sides:  # wall time spent waiting for device verdicts: a timing, not a count (0 without a device)
+        s.pop("verify_wait_ns", None)
     if corrupt is not None:
         for k in ("bytes_sent", "final_error", "last_error"):
             sides[corrupt].pop(k)
