@@ -70,7 +70,10 @@ def parse():
                         "cts_verify called from C++ (tools/bench_multi.cpp). Measured the same (the host runs ahead "
                         "either way: profiles/r03/launcher_ab/); the single-process leg always launches natively")
     p.add_argument("--no-serial-graph", action="store_true",
-                   help="roofline leg from K*R host launches instead of K replays of a HIP graph of one rotation")
+                   help="roofline leg from K*R host launches instead of replays of a HIP graph")
+    p.add_argument("--serial-graph-rotations", type=int, default=0,
+                   help="roofline leg: rotations (R launches each) per captured graph; 0 = all K in one graph, replayed "
+                        "once after an untimed upload replay; 1 = round 3's K replays of one rotation")
     p.add_argument("--engines-same-gpu", action="store_true",
                    help="--engines N with every engine on GPU 0: a rehearsal of the single-process code path on a "
                         "one-GPU box (the line then says n_gpus 1)")
@@ -394,18 +397,25 @@ def main():
         ev_b = torch.cuda.Event(enable_timing=True)
         torch.cuda.synchronize()
         sg = None
+        # rotations per captured graph: all K by default (one replay of K*R launches), so no replay boundary and no
+        # first-replay upload sits inside the timed interval
+        G = K if args.serial_graph_rotations <= 0 else max(1, min(K, args.serial_graph_rotations))
+        while K % G:
+            G -= 1
         if not args.no_serial_graph:
-            # one rotation (R launches) captured on its own stream and replayed K times: the host's dispatch gaps
-            # between back-to-back kernels leave the measured interval, so it is the kernels' own time, as rocprof
-            # reports it (host launches: 41.74-42.41 us, graph: 41.56-41.79 us, alternating on one box,
+            # launches captured on their own stream and replayed: the host's dispatch gaps between back-to-back
+            # kernels leave the measured interval, so it is the kernels' own time, as rocprof reports it (host
+            # launches: 41.74-42.41 us, graph of one rotation: 41.56-41.79 us, alternating on one box,
             # profiles/r03/serial_graph/)
             gs = torch.cuda.Stream()
             try:
                 sg = torch.cuda.CUDAGraph()
                 # thread_local: other threads' HIP calls (RCCL's watchdog at N > 1) stay legal during the capture
                 with torch.cuda.graph(sg, stream=gs, capture_error_mode="thread_local"):
-                    for i in range(R):
+                    for i in range(G * R):
                         B.launch(i, gs)
+                with torch.cuda.stream(gs):
+                    sg.replay()  # untimed: the graph's first replay uploads it
             except Exception as e:  # pragma: no cover - keep the host-launch leg
                 print("bench.py: graph capture failed (%r); roofline leg from host launches" % e, file=sys.stderr)
                 sg = None
@@ -415,7 +425,7 @@ def main():
         if sg is not None:
             with torch.cuda.stream(gs):  # replay() launches on the current stream
                 ev_a.record(gs)
-                for _ in range(K):
+                for _ in range(K // G):
                     sg.replay()
                 ev_b.record(gs)
         else:
@@ -569,7 +579,8 @@ def main():
                            % ("HIP-graph replays" if graph is not None else "host launches")) if not pipe else
                           ("separate serialized leg of K*R launches on one stream (%s), HIP events around them, "
                            "/ (K*R) (the per-kernel duration rocprof reports); the headline value is the pipelined leg"
-                           % ("K replays of a HIP graph of one rotation" if serial_graph else "host launches")),
+                           % (("%d replay(s) of a HIP graph of %d rotation(s), after an untimed upload replay"
+                               % (K // G, G)) if serial_graph else "host launches")),
                 "algorithmic_bytes_per_launch": bytes_per_launch,
                 "pipelined": {
                     "streams": S,

@@ -89,4 +89,14 @@ if [[ $STEPS == *deferred_ab* ]]; then
   run deferred-ab-8q
   GPU_MAX_HW_QUEUES=8 timeout -k 10 300 tools/deferred_ab 5 > "$OUT/deferred_ab_8q.jsonl" 2> "$OUT/deferred_ab_8q.err"
 fi
+if [[ $STEPS == *serial_ab* ]]; then
+  # roofline leg: one graph of all K rotations (default) against K replays of a one-rotation graph, alternated
+  for rep in 1 2 3; do
+    for g in 0 1; do
+      run serial-ab $rep $g
+      timeout -k 10 200 python bench.py --no-extras --no-cpu-baseline --serial-graph-rotations $g \
+        >> "$OUT/serial_ab.jsonl" 2>> "$OUT/serial_ab.err"
+    done
+  done
+fi
 run done
