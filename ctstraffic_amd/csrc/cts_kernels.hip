@@ -3129,9 +3129,13 @@ hipError_t launch_media_stream_frames(const uint8_t* arena, uint64_t arena_bytes
                                      uint64_t* totals, uint64_t* frame_bytes, uint64_t* counters, hipStream_t stream,
                                      const LaunchGeometry& geo)
 {
-    // the sums start from zero on the launch's stream (a batch's totals, not a running sum)
-    hipError_t err = hipMemsetAsync(totals, 0, (size_t)CTS_FRAME_TOTAL_SHARDS * 4u * sizeof(uint64_t), stream);
-    if (err == hipSuccess && win.frames != 0) err = hipMemsetAsync(frame_bytes, 0, (size_t)win.frames * 8u, stream);
+    // the sums start from zero on the launch's stream (a batch's totals, not a running sum); frame bytes placed right
+    // after the totals (the pattern's layout) are cleared with them in one call
+    const size_t tb = (size_t)CTS_FRAME_TOTAL_SHARDS * 4u * sizeof(uint64_t);
+    const bool adjacent = frame_bytes == totals + CTS_FRAME_TOTAL_SHARDS * 4u;
+    hipError_t err = hipMemsetAsync(totals, 0, tb + (adjacent ? (size_t)win.frames * 8u : 0u), stream);
+    if (err == hipSuccess && win.frames != 0 && !adjacent)
+        err = hipMemsetAsync(frame_bytes, 0, (size_t)win.frames * 8u, stream);
     if (err != hipSuccess || n == 0) return err;
     // descs == nullptr: the strided-ring form; the variant-3 walk without per-datagram outputs
     const ContigGrid cg = contig_grid(n, geo);

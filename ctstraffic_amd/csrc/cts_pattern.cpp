@@ -1485,8 +1485,7 @@ struct MediaStreamClient : cts_io_pattern {
         cv.notify_all();
         if (timer_thread.joinable()) timer_thread.join();
         if (ms != nullptr) (void)cts_media_stream_client_destroy(ms);
-        if (d_totals != nullptr) (void)hipFreeAsync(d_totals, stream);
-        if (d_fbytes != nullptr) (void)hipFreeAsync(d_fbytes, stream);
+        if (d_sums != nullptr) (void)hipFreeAsync(d_sums, stream);
         if (stream != nullptr) (void)hipStreamSynchronize(stream);
     }
 
@@ -1529,13 +1528,15 @@ struct MediaStreamClient : cts_io_pattern {
         uint32_t completed;  // its bytes
         uint32_t index;      // its completion index
     };
-    std::vector<MsQueued> msq;
-    Pinned ms_desc, ms_totals, ms_frame_bytes, ms_status, ms_res;
+    std::vector<MsQueued> msq, msq_spare;
+    Pinned ms_desc, ms_sums, ms_status, ms_res;
     // the frame-sum pass adds into its totals and frame bytes with device-scope atomics: they live in device memory
-    // (as cts_media_stream_verify_frames documents them) and are copied into the pinned ms_totals / ms_frame_bytes
-    void* d_totals = nullptr;
-    uint64_t* d_fbytes = nullptr;
-    uint32_t d_fbytes_cap = 0;
+    // (as cts_media_stream_verify_frames documents them), back to back in one allocation (the totals' shards, then one
+    // u64 per window slot), so one memset clears them and one copy brings them to the pinned ms_sums: per render tick
+    // a connection pays one launch, one memset and one copy (round 4; two of each before)
+    static constexpr size_t kTotalsWords = CTS_FRAME_TOTAL_SHARDS * 4u;
+    uint64_t* d_sums = nullptr;
+    uint32_t d_sums_cap = 0;  // window slots
     // stream-ordered (hipMallocAsync / hipFreeAsync on the pattern's stream): a plain hipFree waits for the whole
     // device, and with other connections posting to the engine's resident SYNC mailbox grid that can be a long time
     int DeviceAlloc(void** p, size_t bytes)
@@ -1569,7 +1570,9 @@ struct MediaStreamClient : cts_io_pattern {
     {
         if (msq.empty()) return false;
         const uint32_t n = (uint32_t)msq.size();
-        std::vector<MsQueued> q;
+        // the batch moves to msq_spare and msq takes msq_spare's storage: both keep their capacity across ticks
+        std::vector<MsQueued>& q = msq_spare;
+        q.clear();
         q.swap(msq);
         if (hook != nullptr) {  // device-less harness: the batch verifier on the payload spans, then one by one
             std::vector<cts_buf_desc> d(n);
@@ -1591,24 +1594,23 @@ struct MediaStreamClient : cts_io_pattern {
         if (rc == CTS_OK && ms_desc.host == nullptr) {
             const uint32_t b = BatchCapacity();
             if ((rc = ms_desc.alloc(engine, sizeof(cts_buf_desc) * (uint64_t)b)) == CTS_OK &&
-                (rc = ms_totals.alloc(engine, cts_frame_totals_device_bytes())) == CTS_OK &&
                 (rc = ms_status.alloc(engine, sizeof(cts_datagram_status) * (uint64_t)b)) == CTS_OK)
                 rc = ms_res.alloc(engine, sizeof(cts_verify_result) + sizeof(cts_buf_desc));
         }
+        static_assert(kTotalsWords * sizeof(uint64_t) == (size_t)CTS_FRAME_TOTAL_SHARDS * 32u, "the totals block");
         cts_frame_window w{};
         if (rc == CTS_OK) rc = cts_media_stream_client_window(ms, &w);
-        if (rc == CTS_OK && d_totals == nullptr) rc = DeviceAlloc(&d_totals, cts_frame_totals_device_bytes());
-        if (rc == CTS_OK && d_fbytes_cap < std::max(w.frames, 1u)) {
-            ms_frame_bytes.release();
-            if (d_fbytes != nullptr) (void)hipFreeAsync(d_fbytes, stream);
-            d_fbytes = nullptr;
-            d_fbytes_cap = 0;
+        if (rc == CTS_OK && (d_sums == nullptr || d_sums_cap < std::max(w.frames, 1u))) {
+            ms_sums.release();
+            if (d_sums != nullptr) (void)hipFreeAsync(d_sums, stream);
+            d_sums = nullptr;
+            d_sums_cap = 0;
             const uint32_t cap = std::max(w.frames, 1u);
+            const uint64_t bytes = sizeof(uint64_t) * (kTotalsWords + (uint64_t)cap);
             void* p = nullptr;
-            if ((rc = DeviceAlloc(&p, sizeof(uint64_t) * (uint64_t)cap)) == CTS_OK &&
-                (rc = ms_frame_bytes.alloc(engine, sizeof(uint64_t) * (uint64_t)cap)) == CTS_OK) {
-                d_fbytes = static_cast<uint64_t*>(p);
-                d_fbytes_cap = cap;
+            if ((rc = DeviceAlloc(&p, bytes)) == CTS_OK && (rc = ms_sums.alloc(engine, bytes)) == CTS_OK) {
+                d_sums = static_cast<uint64_t*>(p);
+                d_sums_cap = cap;
             } else if (p != nullptr) {
                 (void)hipFreeAsync(p, stream);
             }
@@ -1617,22 +1619,20 @@ struct MediaStreamClient : cts_io_pattern {
         auto* descs = reinterpret_cast<cts_buf_desc*>(ms_desc.host);
         for (uint32_t i = 0; i < n; ++i) descs[i] = cts_buf_desc{q[i].offset, q[i].completed, 0u, 0u, 0u};
         rc = cts_media_stream_verify_frames(engine, recv_pinned.dev, recv_pinned.bytes,
-                                            reinterpret_cast<const cts_buf_desc*>(ms_desc.dev), n, &w, d_totals, d_fbytes,
-                                            nullptr, stream);
-        if (rc == CTS_OK &&
-            (hipMemcpyAsync(ms_totals.host, d_totals, cts_frame_totals_device_bytes(), hipMemcpyDeviceToHost, stream) !=
-                 hipSuccess ||
-             hipMemcpyAsync(ms_frame_bytes.host, d_fbytes, sizeof(uint64_t) * (uint64_t)w.frames, hipMemcpyDeviceToHost,
-                            stream) != hipSuccess))
+                                            reinterpret_cast<const cts_buf_desc*>(ms_desc.dev), n, &w, d_sums,
+                                            d_sums + kTotalsWords, nullptr, stream);
+        if (rc == CTS_OK && hipMemcpyAsync(ms_sums.host, d_sums, sizeof(uint64_t) * (kTotalsWords + (uint64_t)w.frames),
+                                           hipMemcpyDeviceToHost, stream) != hipSuccess)
             rc = CTS_E_HIP;
         // a short kernel (one render tick's datagrams) behind a launch: sleep rather than spin while it runs
         if (rc != CTS_OK || SleepSync(20) != hipSuccess) throw DeviceError{rc != CTS_OK ? rc : CTS_E_HIP};
         cts_frame_totals t{};
-        (void)cts_frame_totals_fold(ms_totals.host, &t);
+        (void)cts_frame_totals_fold(ms_sums.host, &t);
         if (t.exceptions == 0 && t.datagrams == n) {
             // every datagram clean: the sums are CompleteTaskBackToPattern over the batch (no sender timestamps)
             const int st = cts_media_stream_client_complete_frames(ms, &w, &t,
-                                                                   reinterpret_cast<const uint64_t*>(ms_frame_bytes.host),
+                                                                   reinterpret_cast<const uint64_t*>(ms_sums.host) +
+                                                                       kTotalsWords,
                                                                    n, ReceiverQpc(), 1000000000LL);
             if (st < 0) throw DeviceError{st};
             buffers_verified += n;
