@@ -910,15 +910,19 @@ def run_extras(engine, torch, W, w, arenas, descs, dev, want):
                 engine.set_attr(_lib.ATTR_SYNC_MAILBOX, mailbox)
                 try:
                     r = LB.run(connections=8, buffer_size=65536, transfer_size=1 << 30, engine=engine,
-                               verify_mode=mode, io_pattern=pat)
+                               verify_mode=mode, io_pattern=pat, sides=True)
                 finally:
                     engine.set_attr(_lib.ATTR_SYNC_MAILBOX, 1)
+                # the patterns' waits for DEFERRED batch verdicts (cts_pattern_stats.verify_wait_ns), as a share of
+                # the 2 x 8 sides' wall time (every side of a Duplex run receives)
+                wait_s = sum(sd["verify_wait_ns"] for sd in r["sides"]) * 1e-9
                 out["loopback_config1_%s" % name] = {
                     "GBps_recv": round(r["GBps_recv"], 3), "seconds": round(r["seconds"], 3),
                     "connections_ok": r["connections_ok"], "data_errors": r["data_errors"],
                     "buffers_verified": r["buffers_verified"],
                     "recv_cpu_s_per_GiB": round(r["recv_cpu_s_per_GiB"], 4),
-                    "recv_pattern_cpu_s_per_GiB": round(r["recv_pattern_cpu_s_per_GiB"], 4)}
+                    "recv_pattern_cpu_s_per_GiB": round(r["recv_pattern_cpu_s_per_GiB"], 4),
+                    "verdict_wait_s_per_GiB": round(wait_s / max(r["bytes_recv"] / GIB, 1e-9), 4)}
             # the socket path alone (-verify:connection): what the receive threads spend without any VerifyBuffer
             r = LB.run(connections=8, buffer_size=65536, transfer_size=1 << 30, verify=False)
             out["loopback_config1_verify_off"] = {
