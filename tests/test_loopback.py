@@ -26,8 +26,10 @@ def _oracle_verifier(arena, descs):
 def test_loopback_clean_cpu(mode, pattern):
     shared_buffer_attach(_SENDER)
     r = loopback.run(connections=4, buffer_size=65536, transfer_size=3 * 1024 * 1024 + 12345, verifier=_oracle_verifier,
-                     io_pattern=pattern, verify_mode=mode, batch_buffers=16)
+                     io_pattern=pattern, verify_mode=mode, batch_buffers=16, sides=True)
     assert r["connections_ok"] == 4 and r["connections_failed"] == 0 and r["data_errors"] == 0
+    # a CPU hook answers synchronously: no device verdict is ever waited for, nothing stays held after the run
+    assert all(sd["verify_wait_ns"] == 0 and sd["bytes_recv_held"] == 0 for sd in r["sides"])
     # every data byte crosses once; connection ids (37 B) and DONE (4 B) are counted too (ctsIOPattern.cpp:505-516)
     data = 4 * (3 * 1024 * 1024 + 12345)
     assert r["bytes_recv"] == data + 4 * (37 + 4)
@@ -46,8 +48,13 @@ def test_loopback_detects_wire_corruption_cpu(mode):
 @pytest.mark.parametrize("mode", [A.VERIFY_SYNC, A.VERIFY_DEFERRED], ids=["sync", "deferred"])
 def test_loopback_gpu(engine, mode):
     r = loopback.run(connections=4, buffer_size=65536, transfer_size=16 * 1024 * 1024 + 7, engine=engine,
-                     verify_mode=mode)
+                     verify_mode=mode, sides=True)
     assert r["connections_ok"] == 4 and r["data_errors"] == 0
+    # cts_pattern_stats.verify_wait_ns: the receiving sides of a DEFERRED run waited for device verdicts (at least the
+    # final flush's synchronize); SYNC has no batch to wait for
+    waits = [sd["verify_wait_ns"] for sd in r["sides"][4:]]
+    assert all(w > 0 for w in waits) if mode == A.VERIFY_DEFERRED else all(w == 0 for w in waits), waits
+    assert all(sd["bytes_recv_held"] == 0 and sd["bytes_sent_held"] == 0 for sd in r["sides"])
     r = loopback.run(connections=4, buffer_size=65536, transfer_size=8 * 1024 * 1024, engine=engine, verify_mode=mode,
                      corrupt_connection=2, corrupt_send_index=40)
     assert r["data_errors"] == 1 and r["connections_ok"] == 3
