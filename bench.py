@@ -293,7 +293,7 @@ def main():
             # the waiting ranks hold no spinning collective kernel on their GPUs
             cpu_group = D.new_cpu_group(timeout_s=args.dist_timeout)
 
-    # --verify-variant: A/B runs use the tuning build (every launch variant); the product runs variant 13
+    # --verify-variant: A/B runs use the tuning build (every launch variant); the product runs variant 25
     engine = Engine(gpu, tuning=args.verify_variant >= 0)
     if args.verify_variant >= 0:
         engine.set_attr(_lib.ATTR_VERIFY_VARIANT, args.verify_variant)

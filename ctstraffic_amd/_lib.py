@@ -51,7 +51,7 @@ ATTR_FILL_NT = 10
 ATTR_SYNC_MAILBOX = 11
 
 
-# large-buffer verify kernels by CTS_ATTR_VERIFY_VARIANT, as rocprofv3 names them (13 = the product default; the
+# large-buffer verify kernels by CTS_ATTR_VERIFY_VARIANT, as rocprofv3 names them (25 = the product default; the
 # others exist only in the tuning build, libcts_engine_tuning.so)
 VERIFY_KERNELS = {0: "cts::verify_wg_kernel<8,true>", 1: "cts::verify_wg_kernel<4,true>",
                   2: "cts::verify_wg_kernel<16,true>", 3: "cts::verify_wave_kernel<8,true>",
@@ -65,7 +65,8 @@ VERIFY_KERNELS = {0: "cts::verify_wg_kernel<8,true>", 1: "cts::verify_wg_kernel<
                   14: "cts::verify_wg_kernel<1,true,true,false,true,true>",
                   22: "cts::verify_wg_kernel<2,true,true,false,true,true,1,0,0,256,true>",
                   23: "cts::verify_wg_kernel<2,true,true,false,true,true,1,0,0,256,false,true>",
-                  24: "cts::verify_wg_kernel<2,true,true,false,true,true,1,0,0,256,true,true>"}
+                  24: "cts::verify_wg_kernel<2,true,true,false,true,true,1,0,0,256,true,true>",
+                  25: "cts::verify_wg_kernel<2,true,true,false,true,true,1,0,0,256,false,false,4>"}
 
 
 def verify_kernel_name(variant: int) -> str:

@@ -21,11 +21,11 @@ enum CounterSlot { kBytesChecked = 0, kBytesOk = 1, kBuffersChecked = 2, kBuffer
 #ifndef CTS_TUNING
 #define CTS_TUNING 0
 #endif
-constexpr int kDefaultVerifyVariant = 13;
+constexpr int kDefaultVerifyVariant = 25;  // variant 13 with registers for 4 waves per SIMD (round 4)
 constexpr int kDefaultSmallVariant = 15;  // variant 9 + the edge load L2-allocating (round 3)
 constexpr int kDefaultMediaStreamVariant = 3;
 #if CTS_TUNING
-constexpr int kVerifyVariants = 25;  // workgroup-per-buffer verify variants (launch_verify)
+constexpr int kVerifyVariants = 26;  // workgroup-per-buffer verify variants (launch_verify)
 constexpr int kSmallVariants = 16;   // small-buffer (datagram) verify variants (10-15: line policies)
 constexpr int kMediaStreamVariants = 13;  // MediaStream receive kernels (launch_media_stream_verify)
 #endif
@@ -64,7 +64,7 @@ struct LaunchGeometry {
                                  // datagram kernel, 2 = the small payload fill batched too; CTS_FILL_BATCHED)
     int ring_fill_blocks_per_cu = 4;  // MediaStream ring fill grid cap (16 M x 1472 B: 4.3 ms at 4, 5.0 at 8;
                                       // CTS_RING_FILL_BLOCKS_PER_CU; tools/ring_fill_probe.hip)
-    int verify_variant = kDefaultVerifyVariant;     // see launch_verify (13: variant 11 at U2; 11: variant 10 + in-register exact diff;
+    int verify_variant = kDefaultVerifyVariant;     // see launch_verify (25: 13 for 4 waves/SIMD; 13: variant 11 at U2; 11: variant 10 + in-register exact diff;
                                  // 10: even-phase stream + whole-line spans, U4, measured 1.3-3 % faster than 6,
                                  // which was +0.3-0.7 % over 0)
 };

@@ -717,14 +717,15 @@ __device__ __forceinline__ void flush_staged_results(const cts_verify_result* st
 // the workgroups still running once others have finished keep more bytes in flight (the launch's
 // finishing window, DESIGN.md §3 "Where a 256 MiB launch's last few percent go").
 // A16 (XD): whole-line spans on a 16-aligned pattern position build their expected words with expected_step_a16.
+// WPE > 0: the waves per SIMD the register allocation targets (otherwise 8 for a 256-lane workgroup up to U 8).
 // SPEC: while the workgroup's first descriptor is on its way, the first round of the slot a uniformly strided arena
 // gives buffer i (byte offset i * arena_bytes / n) is read into L2 and dropped; when the descriptor names that slot,
 // its first round then comes from L2 instead of HBM, so the descriptor's latency overlaps the first data fetch
 // instead of preceding it (tools/verify_timeline: 0.56-0.60 against 0.28-0.32 us from entry to the first data
 // load for a plain read). A wrong guess costs one round of reads.
 template <int U, bool NT, bool SPLIT = false, bool SCTR = false, bool WHOLE = false, bool XD = false, int WIN = 1,
-          int DEFER = 0, int UT = 0, int BS = kBlock, bool A16 = false, bool SPEC = false>
-__global__ void __launch_bounds__(BS, (BS == kBlock ? (U <= 8 ? 8 : 4) : 2048 / BS))
+          int DEFER = 0, int UT = 0, int BS = kBlock, bool A16 = false, bool SPEC = false, int WPE = 0>
+__global__ void __launch_bounds__(BS, (WPE > 0 ? WPE : (BS == kBlock ? (U <= 8 ? 8 : 4) : 2048 / BS)))
     verify_wg_kernel(const uint8_t* __restrict__ arena, uint64_t arena_bytes, const cts_buf_desc* __restrict__ descs,
                      uint32_t n, cts_verify_result* __restrict__ results, uint64_t* __restrict__ counters,
                      uint32_t* __restrict__ conn_first_fail, uint32_t n_conns)
@@ -2598,6 +2599,12 @@ static void launch_verify_nt(const uint8_t* arena, uint64_t arena_bytes, const c
         case 24: verify_wg_kernel<2, NT, true, false, true, true, 1, 0, 0, kBlock, true, true>
                      <<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS);
                  break;
+        // 25: variant 13 with its registers allocated for 4 waves per SIMD (the 4 workgroups per CU it runs at)
+        // instead of 8: no SGPR spills in the per-buffer set-up (the default since round 4: 41.18-41.27 against
+        // 41.42-41.45 us per serialized config-2 launch, alternated on one box, profiles/r04/h/wpe.jsonl)
+        case 25: verify_wg_kernel<2, NT, true, false, true, true, 1, 0, 0, kBlock, false, false, 4>
+                     <<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS);
+                 break;
         case 7: verify_wg_kernel<4, NT, true><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 1: verify_wg_kernel<4, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 2: verify_wg_kernel<16, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
@@ -2605,8 +2612,9 @@ static void launch_verify_nt(const uint8_t* arena, uint64_t arena_bytes, const c
         default: verify_wg_kernel<8, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         }
 #else
-        // verify variant 13 (kDefaultVerifyVariant)
-        verify_wg_kernel<2, NT, true, false, true, true><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS);
+        // verify variant 25 (kDefaultVerifyVariant): variant 13 with registers allocated for 4 waves per SIMD
+        verify_wg_kernel<2, NT, true, false, true, true, 1, 0, 0, kBlock, false, false, 4>
+            <<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS);
 #endif
     }
 }

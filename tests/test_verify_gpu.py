@@ -921,7 +921,7 @@ def test_verify_host_batch(engine):
 
 
 # ---- every launch variant / geometry is bit-identical ------------------------------------------
-@pytest.mark.parametrize("variant", list(range(25)))
+@pytest.mark.parametrize("variant", list(range(26)))
 @pytest.mark.parametrize("nt", [1, 0])
 def test_launch_variants_parity(tuning_engine, variant, nt):
     from ctstraffic_amd import _lib
@@ -1014,19 +1014,19 @@ def test_small_variants_parity(tuning_engine, small_variant):
 def _pick(attr, variant, product_engine, tuning_engine):
     from ctstraffic_amd import _lib
 
-    dflt = {_lib.ATTR_VERIFY_VARIANT: 13, _lib.ATTR_SMALL_VARIANT: 15, _lib.ATTR_MS_VARIANT: 3}[attr]
+    dflt = {_lib.ATTR_VERIFY_VARIANT: 25, _lib.ATTR_SMALL_VARIANT: 15, _lib.ATTR_MS_VARIANT: 3}[attr]
     return product_engine if variant == dflt else tuning_engine
 
 
 def test_product_build_launches_the_defaults_only(engine, tuning_engine):
-    """The product library compiles one kernel per path (verify variant 13, small variant 15, MediaStream variant 3)
+    """The product library compiles one kernel per path (verify variant 25, small variant 15, MediaStream variant 3)
     and refuses the others; the tuning build accepts every variant."""
     from ctstraffic_amd import _lib
     from ctstraffic_amd._lib import CtsError
 
     assert "tuning" not in _lib.lib().cts_version().decode()
     assert "tuning" in _lib.tuning_lib().cts_version().decode()
-    for attr, dflt, others in ((_lib.ATTR_VERIFY_VARIANT, 13, (0, 4, 12, 17)), (_lib.ATTR_SMALL_VARIANT, 15, (0, 5, 9)),
+    for attr, dflt, others in ((_lib.ATTR_VERIFY_VARIANT, 25, (0, 4, 12, 13, 17)), (_lib.ATTR_SMALL_VARIANT, 15, (0, 5, 9)),
                                (_lib.ATTR_MS_VARIANT, 3, (0, 2))):
         assert engine.get_attr(attr) == dflt and tuning_engine.get_attr(attr) == dflt
         engine.set_attr(attr, dflt)
@@ -1071,7 +1071,7 @@ def test_max_length_buffers(engine, tuning_engine):
     act_bytes = [exp_bytes[0] ^ 0x5A, exp_bytes[1] ^ 0xFF]
     from ctstraffic_amd import _lib
 
-    cases = [(_lib.ATTR_VERIFY_VARIANT, 13, 0), (_lib.ATTR_VERIFY_VARIANT, 4, 0), (_lib.ATTR_VERIFY_VARIANT, 3, 0),
+    cases = [(_lib.ATTR_VERIFY_VARIANT, 25, 0), (_lib.ATTR_VERIFY_VARIANT, 13, 0), (_lib.ATTR_VERIFY_VARIANT, 4, 0), (_lib.ATTR_VERIFY_VARIANT, 3, 0),
              (_lib.ATTR_VERIFY_VARIANT, 18, 0),
              (_lib.ATTR_SMALL_VARIANT, 15, 1472), (_lib.ATTR_SMALL_VARIANT, 9, 1472), (_lib.ATTR_SMALL_VARIANT, 0, 1472),
              (_lib.ATTR_SMALL_VARIANT, 3, 1472)]

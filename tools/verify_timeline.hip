@@ -4,8 +4,9 @@
 // The product kernel (cts_kernels.hip, included verbatim) against the plain read of the same shape, in one process on
 // one box, 8 rotated 256 MiB arenas (4096 x 64 KiB buffers each; 75 % phase-0 / 25 % random expected offsets, one
 // corrupt byte per 1024 buffers, as bench.py's config 2):
-//   time    : HIP events around R launches, per launch: the product verify_wg_kernel (variant 13, the default; and
-//             the tuning variants 22 = A16, 23 = SPEC, 24 = both, launched directly), a
+//   time    : HIP events around R launches, per launch: verify_wg_kernel variant 13 ("product_verify_us": the
+//             default until late in round 4; the replica mirrors it), variant 25 (the same code with registers for 4
+//             waves per SIMD, the default since), the tuning variants 22 = A16, 23 = SPEC, 24 = both, a
 //             replica of it built from the same device helpers with the stamps compiled out (must equal the product),
 //             and the plain read (grid = 4 x CUs, workgroup b reads 64-KiB slabs b, b + grid, ..., U = 2, the
 //             verify's per-buffer barrier);
@@ -181,6 +182,8 @@ __global__ void __launch_bounds__(256) plain_read(const u32x4* __restrict__ p, u
 
 // the product kernel's tuning variants 22 (A16), 23 (SPEC), 24 (both) beside the default 13
 #define PRODUCT_VARIANT(A16, SPEC) cts::verify_wg_kernel<2, true, true, false, true, true, 1, 0, 0, 256, A16, SPEC>
+// variant 25: variant 13 with its registers allocated for 4 waves per SIMD (no SGPR spills)
+#define VARIANT_25 cts::verify_wg_kernel<2, true, true, false, true, true, 1, 0, 0, 256, false, false, 4>
 
 template <typename F>
 double time_us(F launch, int reps, hipStream_t s)
@@ -346,6 +349,10 @@ int main(int argc, char** argv)
         verify_pipe<false><<<grid, 256, 0, s>>>(arena[0], bytes, d, n, res, ctr, cff, n);
         CHECK(hipMemcpy(c.data(), res, n * sizeof(cts_verify_result), hipMemcpyDeviceToHost));
         std::printf("{\"kind\":\"parity\",\"pipe2_equals_product\":%d}\n", eq(a, c) ? 1 : 0);
+        CHECK(hipMemset(res, 0, n * sizeof(cts_verify_result)));
+        VARIANT_25<<<grid, 256, 0, s>>>(arena[0], bytes, d, n, res, ctr, cff, n);
+        CHECK(hipMemcpy(c.data(), res, n * sizeof(cts_verify_result), hipMemcpyDeviceToHost));
+        std::printf("{\"kind\":\"parity\",\"v25_equals_product\":%d}\n", eq(a, c) ? 1 : 0);
         std::printf("{\"kind\":\"parity\",\"kernarg_preload\":%d,\"replica_equals_product\":%d,"
                     "\"spec_equals_product\":%d,\"a16_equals_product\":%d,\"spec_a16_equals_product\":%d,"
                     "\"failed_buffers\":%u}\n",
@@ -375,12 +382,16 @@ int main(int argc, char** argv)
         const double t_both = time_us([&](int i) {
             PRODUCT_VARIANT(true, true)<<<grid, 256, 0, s>>>(arena[i % R], bytes, d, n, res, ctr, cff, n);
         }, reps, s);
+        const double t_v25 = time_us([&](int i) {
+            VARIANT_25<<<grid, 256, 0, s>>>(arena[i % R], bytes, d, n, res, ctr, cff, n);
+        }, reps, s);
         std::printf("{\"kind\":\"time\",\"kernarg_preload\":%d,\"pass\":%d,\"launches\":%d,\"product_verify_us\":%.2f,"
+                    "\"v25_wpe4_us\":%.2f,\"v25_over_plain\":%.4f,"
                     "\"replica_verify_us\":%.2f,\"v23_spec_us\":%.2f,\"v22_a16_us\":%.2f,\"v24_both_us\":%.2f,\"pipe2_us\":%.2f,"
                     "\"plain_read_us\":%.2f,\"product_GBps\":%.1f,"
                     "\"plain_GBps\":%.1f,\"product_over_plain\":%.4f,\"spec_over_plain\":%.4f,\"a16_over_plain\":%.4f,"
                     "\"spec_a16_over_plain\":%.4f}\n",
-                    kp ? 1 : 0, pass, reps, t_prod, t_rep, t_spec, t_a16, t_both, t_pipe, t_plain, bytes / t_prod / 1e3,
+                    kp ? 1 : 0, pass, reps, t_prod, t_v25, t_v25 / t_plain, t_rep, t_spec, t_a16, t_both, t_pipe, t_plain, bytes / t_prod / 1e3,
                     bytes / t_plain / 1e3, t_prod / t_plain, t_spec / t_plain, t_a16 / t_plain, t_both / t_plain);
         std::fflush(stdout);
     }
