@@ -2605,6 +2605,10 @@ static void launch_verify_nt(const uint8_t* arena, uint64_t arena_bytes, const c
         case 25: verify_wg_kernel<2, NT, true, false, true, true, 1, 0, 0, kBlock, false, false, 4>
                      <<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS);
                  break;
+        // 26: variant 25 at U = 4 (4 loads per lane per round)
+        case 26: verify_wg_kernel<4, NT, true, false, true, true, 1, 0, 0, kBlock, false, false, 4>
+                     <<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS);
+                 break;
         case 7: verify_wg_kernel<4, NT, true><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 1: verify_wg_kernel<4, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
         case 2: verify_wg_kernel<16, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
