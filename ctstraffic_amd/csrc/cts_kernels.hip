@@ -429,31 +429,47 @@ __device__ __forceinline__ void scan_exact_whole(const Span& s, uint32_t lane, u
 // thousand that workgroup is the launch's last to finish.) The clean-path cost is
 // one compare and branch per round.
 // A16: the span starts on a 16-aligned pattern position (expected_step_a16).
-template <int TEAM, int U, bool NT, bool EVEN, bool A16 = false>
+// PRE: the first round's U chunks per lane were loaded by the caller (pre[u] = chunk u * TEAM + lane); the span holds
+// at least one whole round.
+template <int TEAM, int U, bool EVEN, bool A16>
+__device__ __forceinline__ void whole_exact_round(const Span& s, u32x4 (&d)[U], uint32_t cb, uint32_t lane,
+                                                  uint32_t& first, uint32_t& count)
+{
+    const uint32_t B = chunk_base(s, cb + lane);
+    uint32_t any = 0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        if constexpr (A16) d[u] ^= expected_step_a16<TEAM, U>(B, u);
+        else d[u] ^= expected_step<TEAM, U, EVEN>(B, u, s.sh);
+        any |= or4(d[u]);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    if (any != 0u) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) take_diff(s, cb + (uint32_t)(u * TEAM) + lane, d[u], first, count);
+    }
+}
+
+template <int TEAM, int U, bool NT, bool EVEN, bool A16 = false, bool PRE = false>
 __device__ __forceinline__ void scan_whole_exact_impl(const Span& s, __amdgpu_buffer_rsrc_t r, uint32_t lane,
-                                                      uint32_t& first, uint32_t& count)
+                                                      uint32_t& first, uint32_t& count, const u32x4* pre = nullptr)
 {
     const uint32_t voff = lane * 16u;
     uint32_t cb = 0;
     const uint32_t c_end = s.nchunks;
+    if constexpr (PRE) {
+        u32x4 d[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) d[u] = pre[u];
+        whole_exact_round<TEAM, U, EVEN, A16>(s, d, 0u, lane, first, count);
+        cb = (uint32_t)(TEAM * U);
+    }
     for (; cb + (uint32_t)(TEAM * U) <= c_end; cb += (uint32_t)(TEAM * U)) {
         u32x4 d[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) d[u] = buf_load<NT>(r, voff, (cb + (uint32_t)(u * TEAM)) * 16u);
         __builtin_amdgcn_sched_barrier(0);
-        const uint32_t B = chunk_base(s, cb + lane);
-        uint32_t any = 0;
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            if constexpr (A16) d[u] ^= expected_step_a16<TEAM, U>(B, u);
-            else d[u] ^= expected_step<TEAM, U, EVEN>(B, u, s.sh);
-            any |= or4(d[u]);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        if (any != 0u) {
-#pragma unroll
-            for (int u = 0; u < U; ++u) take_diff(s, cb + (uint32_t)(u * TEAM) + lane, d[u], first, count);
-        }
+        whole_exact_round<TEAM, U, EVEN, A16>(s, d, cb, lane, first, count);
     }
     if (cb < c_end) {
         u32x4 d[U];
@@ -479,23 +495,24 @@ __device__ __forceinline__ void scan_whole_exact_impl(const Span& s, __amdgpu_bu
     }
 }
 
-template <int TEAM, int U, bool NT, bool SPLIT, bool A16 = false>
-__device__ __forceinline__ void scan_whole_exact(const Span& s, uint32_t lane, uint32_t& first, uint32_t& count)
+template <int TEAM, int U, bool NT, bool SPLIT, bool A16 = false, bool PRE = false>
+__device__ __forceinline__ void scan_whole_exact(const Span& s, uint32_t lane, uint32_t& first, uint32_t& count,
+                                                 const u32x4* pre = nullptr)
 {
     const __amdgpu_buffer_rsrc_t r = span_rsrc(s);
     if constexpr (A16) {
         if (__builtin_amdgcn_readfirstlane(s.q0 & 15u) == 0u) {
-            scan_whole_exact_impl<TEAM, U, NT, true, true>(s, r, lane, first, count);
+            scan_whole_exact_impl<TEAM, U, NT, true, true, PRE>(s, r, lane, first, count, pre);
             return;
         }
     }
     if constexpr (SPLIT) {
         if (__builtin_amdgcn_readfirstlane(s.sh) == 0u) {
-            scan_whole_exact_impl<TEAM, U, NT, true>(s, r, lane, first, count);
+            scan_whole_exact_impl<TEAM, U, NT, true, false, PRE>(s, r, lane, first, count, pre);
             return;
         }
     }
-    scan_whole_exact_impl<TEAM, U, NT, false>(s, r, lane, first, count);
+    scan_whole_exact_impl<TEAM, U, NT, false, false, PRE>(s, r, lane, first, count, pre);
 }
 
 // Spans of 2 GiB or more (a u32 ctsTask length allows 4 GiB - 1). The buffer-resource streams above
@@ -718,13 +735,16 @@ __device__ __forceinline__ void flush_staged_results(const cts_verify_result* st
 // finishing window, DESIGN.md §3 "Where a 256 MiB launch's last few percent go").
 // A16 (XD): whole-line spans on a 16-aligned pattern position build their expected words with expected_step_a16.
 // WPE > 0: the waves per SIMD the register allocation targets (otherwise 8 for a 256-lane workgroup up to U 8).
+// SPECR: the SPEC guess loaded into registers instead of L2: the first round of the slot a uniformly strided arena
+// gives the workgroup's first buffer is read beside its descriptor, and used as that buffer's first round when the
+// descriptor names exactly that slot (a whole-line span of at least one round); otherwise it is dropped.
 // SPEC: while the workgroup's first descriptor is on its way, the first round of the slot a uniformly strided arena
 // gives buffer i (byte offset i * arena_bytes / n) is read into L2 and dropped; when the descriptor names that slot,
 // its first round then comes from L2 instead of HBM, so the descriptor's latency overlaps the first data fetch
 // instead of preceding it (tools/verify_timeline: 0.56-0.60 against 0.28-0.32 us from entry to the first data
 // load for a plain read). A wrong guess costs one round of reads.
 template <int U, bool NT, bool SPLIT = false, bool SCTR = false, bool WHOLE = false, bool XD = false, int WIN = 1,
-          int DEFER = 0, int UT = 0, int BS = kBlock, bool A16 = false, bool SPEC = false, int WPE = 0>
+          int DEFER = 0, int UT = 0, int BS = kBlock, bool A16 = false, bool SPEC = false, int WPE = 0, bool SPECR = false>
 __global__ void __launch_bounds__(BS, (WPE > 0 ? WPE : (BS == kBlock ? (U <= 8 ? 8 : 4) : 2048 / BS)))
     verify_wg_kernel(const uint8_t* __restrict__ arena, uint64_t arena_bytes, const cts_buf_desc* __restrict__ descs,
                      uint32_t n, cts_verify_result* __restrict__ results, uint64_t* __restrict__ counters,
@@ -732,6 +752,7 @@ __global__ void __launch_bounds__(BS, (WPE > 0 ? WPE : (BS == kBlock ? (U <= 8 ?
 {
     static_assert(!(SCTR && DEFER), "deferred results take the finish_buffer path");
     static_assert(!SPEC || WIN == 1, "the guessed slot is the grid-stride walk's first buffer");
+    static_assert(!SPECR || (WIN == 1 && XD && !SPEC && UT == 0), "SPECR: the whole-line exact stream's first round");
     __shared__ uint64_t ctr[1][5];
     __shared__ cts_verify_result dres[DEFER ? DEFER : 1];
     __shared__ uint32_t didx[DEFER ? DEFER : 1];
@@ -777,9 +798,25 @@ __global__ void __launch_bounds__(BS, (WPE > 0 ? WPE : (BS == kBlock ? (U <= 8 ?
             }
         }
     }
+    u32x4 pre[SPECR ? U : 1];
+    const uint8_t* pre_p = nullptr;  // SPECR: the guessed slot (uniform; null = no guess pending)
+    if constexpr (SPECR) {
+        if (i < end) {
+            const uint64_t per = arena_bytes / n;
+            if (per >= (uint64_t)BS * U * 16u) {
+                pre_p = arena + (uint64_t)i * per;
+                const __amdgpu_buffer_rsrc_t gr = __builtin_amdgcn_make_buffer_rsrc(
+                    const_cast<uint8_t*>(pre_p), (short)0, (int)(BS * U * 16), 0x00020000);
+#pragma unroll
+                for (int u = 0; u < U; ++u) pre[u] = buf_load<NT>(gr, lane * 16u, (uint32_t)(u * BS) * 16u);
+            }
+        }
+    }
     for (; i < end; i = (uint64_t)i + step < end ? i + step : end) {
         const cts_buf_desc d = dn;
         if ((uint64_t)i + step < end) dn = descs[i + step];
+        const uint8_t* guess = pre_p;
+        if constexpr (SPECR) pre_p = nullptr;
         if (desc_bad(d, arena_bytes)) {
             if (DEFER && defer) {
                 if (lane == 0) {
@@ -803,6 +840,9 @@ __global__ void __launch_bounds__(BS, (WPE > 0 ? WPE : (BS == kBlock ? (U <= 8 ?
             // whole-line span, exact diff in registers: only the reduction is left
             if (UT > 0 && (uint64_t)i + step >= end)
                 scan_whole_exact<BS, (UT > 0 ? UT : U), NT, SPLIT, A16>(s, lane, first, count);
+            else if (SPECR && guess != nullptr && reinterpret_cast<const uint8_t*>(s.p) == guess &&
+                     s.nchunks >= (uint32_t)(BS * U))
+                scan_whole_exact<BS, U, NT, SPLIT, A16, true>(s, lane, first, count, pre);
             else
                 scan_whole_exact<BS, U, NT, SPLIT, A16>(s, lane, first, count);
             dirty = __builtin_amdgcn_readfirstlane(__syncthreads_or(first != kNone)) != 0;
@@ -2607,6 +2647,10 @@ static void launch_verify_nt(const uint8_t* arena, uint64_t arena_bytes, const c
                  break;
         // 26: variant 25 at U = 4 (4 loads per lane per round)
         case 26: verify_wg_kernel<4, NT, true, false, true, true, 1, 0, 0, kBlock, false, false, 4>
+                     <<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS);
+                 break;
+        // 27: variant 25 + the guessed first slot's first round loaded into registers beside the first descriptor
+        case 27: verify_wg_kernel<2, NT, true, false, true, true, 1, 0, 0, kBlock, false, false, 4, true>
                      <<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS);
                  break;
         case 7: verify_wg_kernel<4, NT, true><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
