@@ -66,9 +66,10 @@ VERIFY_KERNELS = {0: "cts::verify_wg_kernel<8,true>", 1: "cts::verify_wg_kernel<
                   22: "cts::verify_wg_kernel<2,true,true,false,true,true,1,0,0,256,true>",
                   23: "cts::verify_wg_kernel<2,true,true,false,true,true,1,0,0,256,false,true>",
                   24: "cts::verify_wg_kernel<2,true,true,false,true,true,1,0,0,256,true,true>",
-                  25: "cts::verify_wg_kernel<2,true,true,false,true,true,1,0,0,256,false,false,4,false>",
-                  26: "cts::verify_wg_kernel<4,true,true,false,true,true,1,0,0,256,false,false,4,false>",
-                  27: "cts::verify_wg_kernel<2,true,true,false,true,true,1,0,0,256,false,false,4,true>"}
+                  25: "cts::verify_wg_kernel<2,true,true,false,true,true,1,0,0,256,false,false,4,false,false>",
+                  26: "cts::verify_wg_kernel<4,true,true,false,true,true,1,0,0,256,false,false,4,false,false>",
+                  27: "cts::verify_wg_kernel<2,true,true,false,true,true,1,0,0,256,false,false,4,true,false>",
+                  28: "cts::verify_wg_kernel<2,true,true,false,true,true,1,0,0,256,false,false,4,false,true>"}
 
 
 def verify_kernel_name(variant: int) -> str:

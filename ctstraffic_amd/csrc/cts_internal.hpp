@@ -25,7 +25,7 @@ constexpr int kDefaultVerifyVariant = 25;  // variant 13 with registers for 4 wa
 constexpr int kDefaultSmallVariant = 15;  // variant 9 + the edge load L2-allocating (round 3)
 constexpr int kDefaultMediaStreamVariant = 3;
 #if CTS_TUNING
-constexpr int kVerifyVariants = 28;  // workgroup-per-buffer verify variants (launch_verify)
+constexpr int kVerifyVariants = 29;  // workgroup-per-buffer verify variants (launch_verify)
 constexpr int kSmallVariants = 16;   // small-buffer (datagram) verify variants (10-15: line policies)
 constexpr int kMediaStreamVariants = 13;  // MediaStream receive kernels (launch_media_stream_verify)
 #endif

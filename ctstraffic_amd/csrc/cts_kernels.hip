@@ -744,7 +744,8 @@ __device__ __forceinline__ void flush_staged_results(const cts_verify_result* st
 // instead of preceding it (tools/verify_timeline: 0.56-0.60 against 0.28-0.32 us from entry to the first data
 // load for a plain read). A wrong guess costs one round of reads.
 template <int U, bool NT, bool SPLIT = false, bool SCTR = false, bool WHOLE = false, bool XD = false, int WIN = 1,
-          int DEFER = 0, int UT = 0, int BS = kBlock, bool A16 = false, bool SPEC = false, int WPE = 0, bool SPECR = false>
+          int DEFER = 0, int UT = 0, int BS = kBlock, bool A16 = false, bool SPEC = false, int WPE = 0, bool SPECR = false,
+          bool ROT = false>
 __global__ void __launch_bounds__(BS, (WPE > 0 ? WPE : (BS == kBlock ? (U <= 8 ? 8 : 4) : 2048 / BS)))
     verify_wg_kernel(const uint8_t* __restrict__ arena, uint64_t arena_bytes, const cts_buf_desc* __restrict__ descs,
                      uint32_t n, cts_verify_result* __restrict__ results, uint64_t* __restrict__ counters,
@@ -753,6 +754,7 @@ __global__ void __launch_bounds__(BS, (WPE > 0 ? WPE : (BS == kBlock ? (U <= 8 ?
     static_assert(!(SCTR && DEFER), "deferred results take the finish_buffer path");
     static_assert(!SPEC || WIN == 1, "the guessed slot is the grid-stride walk's first buffer");
     static_assert(!SPECR || (WIN == 1 && XD && !SPEC && UT == 0), "SPECR: the whole-line exact stream's first round");
+    static_assert(!ROT || (WIN == 1 && !SPEC && !SPECR), "ROT permutes the plain grid-stride walk");
     __shared__ uint64_t ctr[1][5];
     __shared__ cts_verify_result dres[DEFER ? DEFER : 1];
     __shared__ uint32_t didx[DEFER ? DEFER : 1];
@@ -779,8 +781,17 @@ __global__ void __launch_bounds__(BS, (WPE > 0 ? WPE : (BS == kBlock ? (U <= 8 ?
         i = s0 < end ? (uint32_t)s0 : end;
         step = gridDim.x / WIN;
     }
+    // ROT: in every full round k of the walk (k * step + step <= end) workgroup b takes descriptor
+    // k * step + (b + k) mod step instead of k * step + b (a partial last round keeps b), so the buffers one
+    // workgroup (and one XCD) reads are not all congruent modulo the grid
+    uint32_t rr = blockIdx.x;  // ROT: (b + k) mod step
+    auto walk = [&](uint32_t slot, uint32_t r) -> uint32_t {
+        if constexpr (!ROT) return slot;
+        const uint32_t kbase = slot - blockIdx.x;
+        return (uint64_t)kbase + step <= end ? kbase + r : slot;
+    };
     cts_buf_desc dn;
-    if (i < end) dn = descs[i];
+    if (i < end) dn = descs[walk(i, rr)];
     if constexpr (SPEC) {
         // the guessed slot's first round, L2-allocating (the default policy), beside the descriptor's load; the data
         // is dropped once it arrived (the asm keeps the loads), the round's own loads then hit L2
@@ -814,18 +825,20 @@ __global__ void __launch_bounds__(BS, (WPE > 0 ? WPE : (BS == kBlock ? (U <= 8 ?
     }
     for (; i < end; i = (uint64_t)i + step < end ? i + step : end) {
         const cts_buf_desc d = dn;
-        if ((uint64_t)i + step < end) dn = descs[i + step];
+        const uint32_t di = walk(i, rr);  // the descriptor (and result record) this step verifies
+        if constexpr (ROT) rr = rr + 1u == step ? 0u : rr + 1u;
+        if ((uint64_t)i + step < end) dn = descs[walk(i + step, rr)];
         const uint8_t* guess = pre_p;
         if constexpr (SPECR) pre_p = nullptr;
         if (desc_bad(d, arena_bytes)) {
             if (DEFER && defer) {
                 if (lane == 0) {
                     write_bad(dres + dk, 0);
-                    didx[dk] = i;
+                    didx[dk] = di;
                 }
                 staged();
             } else if (lane == 0) {
-                write_bad(results, i);
+                write_bad(results, di);
             }
             continue;
         }
@@ -866,19 +879,19 @@ __global__ void __launch_bounds__(BS, (WPE > 0 ? WPE : (BS == kBlock ? (U <= 8 ?
                     cts_verify_result r{};
                     r.first_mismatch = s.len;
                     r.pass = 1;
-                    results[i] = r;
+                    results[di] = r;
                 }
                 continue;
             }
         }
         if (DEFER && defer) {
             if (lane == 0) {
-                finish_buffer(s, d, i, first, count, results, ctr[0], conn_first_fail, n_conns, dres + dk);
-                didx[dk] = i;
+                finish_buffer(s, d, di, first, count, results, ctr[0], conn_first_fail, n_conns, dres + dk);
+                didx[dk] = di;
             }
             staged();
         } else if (lane == 0) {
-            finish_buffer(s, d, i, first, count, results, ctr[0], conn_first_fail, n_conns);
+            finish_buffer(s, d, di, first, count, results, ctr[0], conn_first_fail, n_conns);
         }
     }
     if constexpr (DEFER > 0)
@@ -2651,6 +2664,10 @@ static void launch_verify_nt(const uint8_t* arena, uint64_t arena_bytes, const c
                  break;
         // 27: variant 25 + the guessed first slot's first round loaded into registers beside the first descriptor
         case 27: verify_wg_kernel<2, NT, true, false, true, true, 1, 0, 0, kBlock, false, false, 4, true>
+                     <<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS);
+                 break;
+        // 28: variant 25 walking the descriptors rotated by one per round (ROT)
+        case 28: verify_wg_kernel<2, NT, true, false, true, true, 1, 0, 0, kBlock, false, false, 4, false, true>
                      <<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS);
                  break;
         case 7: verify_wg_kernel<4, NT, true><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;

@@ -257,7 +257,7 @@ def test_product_library_carries_only_the_default_kernels():
 
     prod = _kernels(_lib.LIB_PATH)
     wg = sorted(k for k in prod if "verify_wg_kernel" in k)
-    assert wg == ["_ZN3cts16verify_wg_kernelILi2ELb%dELb1ELb0ELb1ELb1ELi1ELi0ELi0ELi256ELb0ELb0ELi4ELb0EEEvPKhmPK12cts_buf_descjP17cts_verify_resultPmPjj"
+    assert wg == ["_ZN3cts16verify_wg_kernelILi2ELb%dELb1ELb0ELb1ELb1ELi1ELi0ELi0ELi256ELb0ELb0ELi4ELb0ELb0EEEvPKhmPK12cts_buf_descjP17cts_verify_resultPmPjj"
                   ".kd" % nt for nt in (0, 1)]
     assert not any("verify_wave" in k or "_nb_" in k for k in prod)
     assert len(prod) == 30 and any("mailbox_kernel" in k for k in prod), sorted(prod)

@@ -921,7 +921,7 @@ def test_verify_host_batch(engine):
 
 
 # ---- every launch variant / geometry is bit-identical ------------------------------------------
-@pytest.mark.parametrize("variant", list(range(28)))
+@pytest.mark.parametrize("variant", list(range(29)))
 @pytest.mark.parametrize("nt", [1, 0])
 def test_launch_variants_parity(tuning_engine, variant, nt):
     from ctstraffic_amd import _lib

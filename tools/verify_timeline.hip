@@ -20,6 +20,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #define CHECK(x)                                                                              \
@@ -150,15 +151,20 @@ __global__ void __launch_bounds__(256, 8)
     }
 }
 
-// the plain read of the same shape (hbm_read_ceiling.hip read_slab_timeline): no descriptor, no compare, no output
-template <bool STAMP>
+// the plain read of the same shape (hbm_read_ceiling.hip read_slab_timeline): no descriptor, no compare, no output.
+// MAP (the "map" mode): which slab workgroup b reads in its k-th step: 0 = b + k G (the verify's walk), 1 = (b ^ 1) + k G
+// (each XCC reads the other parity of 64 KiB slots), 2 = ((b + k) mod G) + k G (each XCC's slots alternate in parity)
+template <bool STAMP, int MAP = 0>
 __global__ void __launch_bounds__(256) plain_read(const u32x4* __restrict__ p, uint32_t nslabs, uint64_t* st,
                                                   uint32_t* out)
 {
     const uint64_t t_entry = STAMP ? stamp() : 0;
     uint32_t acc = 0, k = 0;
     uint64_t* my = st + (uint64_t)blockIdx.x * kSt;
-    for (uint32_t sl = blockIdx.x; sl < nslabs; sl += gridDim.x, ++k) {
+    for (uint32_t sl0 = blockIdx.x; sl0 < nslabs; sl0 += gridDim.x, ++k) {
+        uint32_t sl = sl0;
+        if constexpr (MAP == 1) sl = sl0 ^ 1u;
+        if constexpr (MAP == 2) sl = sl0 - blockIdx.x + (blockIdx.x + k) % gridDim.x;
         const u32x4* q = p + (uint64_t)sl * 4096u;
         if (STAMP && k == 0 && threadIdx.x == 0) my[1] = stamp();
         for (uint32_t r = 0; r < 8; ++r) {
@@ -265,6 +271,7 @@ int main(int argc, char** argv)
     const bool kp = false;
 #endif
     const int passes = argc > 1 ? atoi(argv[1]) : 3;
+    const bool map_mode = argc > 3 && std::string(argv[3]) == "map";
     const int reps = argc > 2 ? atoi(argv[2]) : 64;
     int cus = 0;
     CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
@@ -314,6 +321,54 @@ int main(int argc, char** argv)
     CHECK(hipStreamCreate(&s));
     CHECK(hipDeviceSynchronize());
 
+    if (map_mode) {
+        // does a late XCC follow the XCC or the addresses it reads? the plain read under three slab maps, and the
+        // product verify with its descriptors permuted the way map 2 permutes the slabs (workgroup b's k-th buffer at
+        // slot ((b + k) mod G) + k G)
+        std::vector<cts_buf_desc> pd(n);
+        for (uint32_t j = 0; j < n; ++j) {
+            const uint32_t b = j % grid, k = j / grid;
+            pd[j] = hd[k * grid + (b + k) % grid];
+        }
+        cts_buf_desc* dp = nullptr;
+        CHECK(hipMalloc((void**)&dp, n * sizeof(cts_buf_desc)));
+        CHECK(hipMemcpy(dp, pd.data(), n * sizeof(cts_buf_desc), hipMemcpyHostToDevice));
+        std::vector<uint64_t> h((size_t)grid * kSt);
+        for (int pass = 0; pass < passes; ++pass) {
+            const double t0 = time_us([&](int i) {
+                plain_read<false, 0><<<grid, 256, 0, s>>>(reinterpret_cast<const u32x4*>(arena[i % R]), n, st, out);
+            }, reps, s);
+            const double t1 = time_us([&](int i) {
+                plain_read<false, 1><<<grid, 256, 0, s>>>(reinterpret_cast<const u32x4*>(arena[i % R]), n, st, out);
+            }, reps, s);
+            const double t2 = time_us([&](int i) {
+                plain_read<false, 2><<<grid, 256, 0, s>>>(reinterpret_cast<const u32x4*>(arena[i % R]), n, st, out);
+            }, reps, s);
+            const double v0 = time_us([&](int i) {
+                VARIANT_25<<<grid, 256, 0, s>>>(arena[i % R], bytes, d, n, res, ctr, cff, n);
+            }, reps, s);
+            const double v2 = time_us([&](int i) {
+                VARIANT_25<<<grid, 256, 0, s>>>(arena[i % R], bytes, dp, n, res, ctr, cff, n);
+            }, reps, s);
+            std::printf("{\"kind\":\"map_time\",\"pass\":%d,\"launches\":%d,\"plain_map0_us\":%.2f,\"plain_map1_us\":%.2f,"
+                        "\"plain_map2_us\":%.2f,\"verify_descs_in_order_us\":%.2f,\"verify_descs_map2_us\":%.2f}\n",
+                        pass, reps, t0, t1, t2, v0, v2);
+            std::fflush(stdout);
+            for (int m = 0; m < 3; ++m) {
+                for (int rep = 0; rep < 3; ++rep) {
+                    CHECK(hipMemsetAsync(st, 0, (size_t)grid * kSt * 8, s));
+                    const u32x4* a = reinterpret_cast<const u32x4*>(arena[rep % R]);
+                    if (m == 0) plain_read<true, 0><<<grid, 256, 0, s>>>(a, n, st, out);
+                    if (m == 1) plain_read<true, 1><<<grid, 256, 0, s>>>(a, n, st, out);
+                    if (m == 2) plain_read<true, 2><<<grid, 256, 0, s>>>(a, n, st, out);
+                    CHECK(hipStreamSynchronize(s));
+                }
+                CHECK(hipMemcpy(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost));
+                print_timeline(m == 0 ? "plain_map0" : m == 1 ? "plain_map1" : "plain_map2", h, grid, kp);
+            }
+        }
+        return 0;
+    }
     // parity of the replica against the product on arena 0 (the tool measures the product's code path)
     {
         std::vector<cts_verify_result> a(n), b(n);
