@@ -191,6 +191,51 @@ __global__ void __launch_bounds__(256) plain_read(const u32x4* __restrict__ p, u
 // variant 25: variant 13 with its registers allocated for 4 waves per SIMD (no SGPR spills)
 #define VARIANT_25 cts::verify_wg_kernel<2, true, true, false, true, true, 1, 0, 0, 256, false, false, 4>
 
+// XCD-skewed plain read ("skew" mode): the grid has S = gridDim.x / 8 slots per XCD (workgroup b runs on XCD b mod 8,
+// the dispatcher's round robin); on the odd XCDs only S - 2 dd of them work, dd = S * SKEW / (64 + SKEW), so the even
+// XCDs read (S) / (S - 2 dd) times as many slabs. The active workgroups are ranked even XCDs first and walk slabs
+// rank, rank + A, ... (A = active count): every slab is read once whatever the placement.
+template <bool STAMP, int SKEW>
+__global__ void __launch_bounds__(256) plain_read_skew(const u32x4* __restrict__ p, uint32_t nslabs, uint64_t* st,
+                                                       uint32_t* out)
+{
+    const uint64_t t_entry = STAMP ? stamp() : 0;
+    const uint32_t S = gridDim.x / 8u, dd = S * (uint32_t)SKEW / (64u + (uint32_t)SKEW), So = S - 2u * dd;
+    const uint32_t x = blockIdx.x & 7u, q = blockIdx.x >> 3;
+    if ((x & 1u) && q >= So) return;
+    const uint32_t rank = (x & 1u) ? 4u * S + (x >> 1) * So + q : (x >> 1) * S + q;
+    const uint32_t A = 4u * S + 4u * So;
+    uint32_t acc = 0, k = 0;
+    uint64_t* my = st + (uint64_t)rank * kSt;
+    for (uint32_t sl = rank; sl < nslabs; sl += A, ++k) {
+        const u32x4* qq = p + (uint64_t)sl * 4096u;
+        if (STAMP && k == 0 && threadIdx.x == 0) my[1] = stamp();
+        for (uint32_t r = 0; r < 8; ++r) {
+            const uint32_t c = r * 512u + threadIdx.x;
+            u32x4 d[2];
+            d[0] = __builtin_nontemporal_load(qq + c);
+            d[1] = __builtin_nontemporal_load(qq + c + 256u);
+            __builtin_amdgcn_sched_barrier(0);
+            acc |= d[0][0] ^ d[0][1] ^ d[0][2] ^ d[0][3] ^ d[1][0] ^ d[1][1] ^ d[1][2] ^ d[1][3];
+        }
+        acc = __syncthreads_or(acc == 0x12345678u) ? 1u : acc;
+        if (STAMP && threadIdx.x == 0 && k < 8) my[2 + k] = stamp();
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+    if (STAMP && threadIdx.x == 0) {
+        my[0] = t_entry;
+        my[10] = stamp();
+        my[11] = (uint64_t)xcc_id() | ((uint64_t)k << 8);
+    }
+}
+
+// the grid plain_read_skew<SKEW> needs for about `active` working workgroups
+inline uint32_t skew_grid(uint32_t active, int skew)
+{
+    const uint32_t P = active / 8u;
+    return 8u * (P + (P * (uint32_t)skew + 63u) / 64u);
+}
+
 template <typename F>
 double time_us(F launch, int reps, hipStream_t s)
 {
@@ -272,6 +317,7 @@ int main(int argc, char** argv)
 #endif
     const int passes = argc > 1 ? atoi(argv[1]) : 3;
     const bool map_mode = argc > 3 && std::string(argv[3]) == "map";
+    const bool skew_mode = argc > 3 && std::string(argv[3]) == "skew";
     const int reps = argc > 2 ? atoi(argv[2]) : 64;
     int cus = 0;
     CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
@@ -321,6 +367,49 @@ int main(int argc, char** argv)
     CHECK(hipStreamCreate(&s));
     CHECK(hipDeviceSynchronize());
 
+    if (skew_mode) {
+        // does reading fewer slabs on the late (odd) XCDs shorten the launch? active workgroups stay ~1024
+        std::vector<uint64_t> h((size_t)grid * 2 * kSt);
+        uint64_t* st2 = nullptr;
+        CHECK(hipMalloc((void**)&st2, h.size() * 8));
+        for (int pass = 0; pass < passes; ++pass) {
+            double t[5];
+            const int sk[5] = {0, 2, 4, 6, 8};
+            for (int v = 0; v < 5; ++v) {
+                const uint32_t g = skew_grid(grid, sk[v]);
+                t[v] = time_us([&](int i) {
+                    const u32x4* a = reinterpret_cast<const u32x4*>(arena[i % R]);
+                    switch (sk[v]) {
+                    case 0: plain_read_skew<false, 0><<<g, 256, 0, s>>>(a, n, st2, out); break;
+                    case 2: plain_read_skew<false, 2><<<g, 256, 0, s>>>(a, n, st2, out); break;
+                    case 4: plain_read_skew<false, 4><<<g, 256, 0, s>>>(a, n, st2, out); break;
+                    case 6: plain_read_skew<false, 6><<<g, 256, 0, s>>>(a, n, st2, out); break;
+                    default: plain_read_skew<false, 8><<<g, 256, 0, s>>>(a, n, st2, out); break;
+                    }
+                }, reps, s);
+            }
+            const double t_plain = time_us([&](int i) {
+                plain_read<false><<<grid, 256, 0, s>>>(reinterpret_cast<const u32x4*>(arena[i % R]), n, st, out);
+            }, reps, s);
+            std::printf("{\"kind\":\"skew_time\",\"pass\":%d,\"launches\":%d,\"plain_us\":%.2f,\"skew0_us\":%.2f,"
+                        "\"skew2_us\":%.2f,\"skew4_us\":%.2f,\"skew6_us\":%.2f,\"skew8_us\":%.2f}\n",
+                        pass, reps, t_plain, t[0], t[1], t[2], t[3], t[4]);
+            std::fflush(stdout);
+            for (int v : {0, 4}) {
+                const uint32_t g = skew_grid(grid, v);
+                for (int rep = 0; rep < 3; ++rep) {
+                    CHECK(hipMemsetAsync(st2, 0, h.size() * 8, s));
+                    const u32x4* a = reinterpret_cast<const u32x4*>(arena[rep % R]);
+                    if (v == 0) plain_read_skew<true, 0><<<g, 256, 0, s>>>(a, n, st2, out);
+                    else plain_read_skew<true, 4><<<g, 256, 0, s>>>(a, n, st2, out);
+                    CHECK(hipStreamSynchronize(s));
+                }
+                CHECK(hipMemcpy(h.data(), st2, h.size() * 8, hipMemcpyDeviceToHost));
+                print_timeline(v == 0 ? "plain_skew0" : "plain_skew4", h, grid, kp);  // ranks 0..1023 (A = 1024 at 0 and 4)
+            }
+        }
+        return 0;
+    }
     if (map_mode) {
         // does a late XCC follow the XCC or the addresses it reads? the plain read under three slab maps, and the
         // product verify with its descriptors permuted the way map 2 permutes the slabs (workgroup b's k-th buffer at
