@@ -191,4 +191,6 @@ def main(src, dst):
 
 
 if __name__ == "__main__":
+    if len(sys.argv) != 3:
+        sys.exit("usage: python tools/prof_summary.py gpurun_out/<tag> profiles/<round>/<dir>")
     main(sys.argv[1], sys.argv[2])
