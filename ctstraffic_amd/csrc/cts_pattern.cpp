@@ -26,6 +26,7 @@
 #include <exception>
 #include <memory>
 #include <mutex>
+#include <deque>
 #include <new>
 #include <random>
 #include <string>
@@ -352,10 +353,12 @@ struct cts_io_pattern {
     virtual ~cts_io_pattern()
     {
         if (stream) {
-            if (!inflight.empty()) (void)hipStreamSynchronize(stream);  // the kernel still reads the ring
+            (void)hipStreamSynchronize(stream);  // kernels may still read the ring (cheap when idle)
             (void)cts_engine_stream_destroy(engine, stream);
         }
-        if (inflight_done) (void)hipEventDestroy(inflight_done);
+        for (Flight& f : flights) spare_events.push_back(f.done);
+        for (hipEvent_t e : spare_events)
+            if (e) (void)hipEventDestroy(e);
         if (sync_done) (void)hipEventDestroy(sync_done);
         // ~RioBufferId (ctsIOPattern.h:230-238) for every id this pattern registered
         if (!rio_owned.empty()) {
@@ -426,7 +429,13 @@ struct cts_io_pattern {
     // completion accepted meanwhile is a pattern-requested send/recv, so the per-connection counters hold back the same)
     uint64_t HeldRecv() const { return status_recv - published_recv; }
     uint64_t HeldSent() const { return status_sent - published_sent; }
-    bool VerdictsPending() const { return !queue.empty() || !inflight.empty(); }
+    bool VerdictsPending() const { return !queue.empty() || !flights.empty(); }
+    uint32_t InFlightCount() const
+    {
+        uint32_t n = 0;
+        for (const Flight& f : flights) n += (uint32_t)f.q.size();
+        return n;
+    }
     void PublishIfSettled()
     {
         if (!VerdictsPending()) Publish(status_recv, status_sent);
@@ -447,11 +456,26 @@ struct cts_io_pattern {
     std::vector<cts_verify_result> hres;
     std::vector<Queued> queue;
     uint64_t stage_used = 0;
-    // double buffering (ring mode, device verify): a full batch is launched and left running while
-    // the next one fills in the other half of stage_desc/stage_res; its verdicts are applied before
-    // the next launch, at any non-benign completion and at Flush (Retire)
-    std::vector<Queued> inflight;
-    hipEvent_t inflight_done = nullptr;  // recorded after the in-flight batch's launch, queried by CompleteIo
+    // pipelined batches (ring mode, device verify): a full batch is launched and left running while the next one
+    // fills in another set of stage_desc/stage_res; up to Depth() batches run at once. The oldest one's verdicts are
+    // applied when a launch would exceed Depth(), as soon as CompleteIo sees its kernel done, at any non-benign
+    // completion and at Flush. A failing batch discards the ones launched after it.
+    struct Flight {
+        std::vector<Queued> q;
+        hipEvent_t done = nullptr;  // recorded after the batch's launch, queried by CompleteIo
+        uint32_t set = 0;           // its descriptor / result set
+    };
+    std::deque<Flight> flights;              // oldest first
+    std::vector<hipEvent_t> spare_events;    // events of retired flights, for reuse
+    std::vector<std::vector<Queued>> spare_queues;  // their entry vectors (capacity kept across batches)
+    // Batches in flight per connection (CTS_DEFERRED_DEPTH, 1-4; default 1). Each launch holds
+    // BatchCapacity() / (Depth() + 1) buffers, so a verdict is still known within BatchCapacity() completions.
+    uint32_t depth_env = [] {
+        const char* v = std::getenv("CTS_DEFERRED_DEPTH");
+        if (v == nullptr || *v == 0) return 1u;
+        const long n = std::atol(v);
+        return n < 1 ? 1u : (n > 4 ? 4u : (uint32_t)n);
+    }();
     // How Retire waits for the in-flight batch (CTS_DEFERRED_BLOCKING_SYNC): 0 = spin in hipStreamSynchronize,
     // 1 = hipEventSynchronize on a blocking-sync event, 2 (default) = sleep in 50 us steps between non-blocking
     // queries of the event. With 8 connections sharing the PCIe link, the first two burned ~2 ms of receive-thread
@@ -474,7 +498,7 @@ struct cts_io_pattern {
         while (p < (uint32_t)std::min<long>(n, 1L << 20)) p <<= 1;
         return p;
     }();
-    uint32_t desc_set = 0;  // the half the filling batch uses
+    uint32_t desc_set = 0;  // the set the filling batch uses
     // time the calls spent waiting for a DEFERRED batch's device verdicts (cts_pattern_stats.verify_wait_ns)
     uint64_t verify_wait_ns = 0;
     void AddVerifyWait(std::chrono::steady_clock::time_point t0)
@@ -862,18 +886,29 @@ struct cts_io_pattern {
     uint64_t StageCapacity() const { return cfg.batch_bytes ? cfg.batch_bytes : (64ull << 20); }
     uint32_t BatchCapacity() const { return cfg.batch_buffers ? cfg.batch_buffers : 1024u; }
     bool DoubleBuffered() const { return engine != nullptr && hook == nullptr; }
-    // Completions queued before a batch goes to the device. Double-buffered, each half holds half a batch: an
-    // in-flight half is retired at the latest when the next half is full, so every verdict is known within
-    // BatchCapacity() completions of its own (fewer when the in-flight kernel is seen done earlier).
+    // Batches in flight at once (pipelined: at least 1, and at most BatchCapacity() - 1 so that a launch holds a
+    // buffer or more)
+    uint32_t Depth() const
+    {
+        const uint32_t b = BatchCapacity();
+        return b < 3u ? 1u : std::min(depth_env, b - 1u);
+    }
+    uint32_t Sets() const { return Depth() + 1u; }  // descriptor / result sets: the filling batch + those in flight
+    // Completions queued before a batch goes to the device. Pipelined, each launch holds BatchCapacity() / Sets():
+    // the oldest launch is retired at the latest when the filling one is full and Depth() are in flight, so every
+    // verdict is known within BatchCapacity() completions of its own (fewer when a kernel is seen done earlier).
     uint32_t LaunchAt() const
     {
         const uint32_t b = BatchCapacity();
-        return DoubleBuffered() && queue_in_ring ? std::max(1u, b / 2u) : b;
+        return DoubleBuffered() && queue_in_ring ? std::max(1u, b / Sets()) : b;
     }
 
-    // The in-flight batch's kernel has finished (a non-blocking event query; CompleteIo asks every 16th
+    // The oldest in-flight batch's kernel has finished (a non-blocking event query; CompleteIo asks every 16th
     // completion: a query costs about a microsecond, a completion of 64 KiB arrives every ~1.3 us at 50 GB/s).
-    bool InflightDone() const { return !inflight.empty() && inflight_done && hipEventQuery(inflight_done) == hipSuccess; }
+    bool InflightDone() const
+    {
+        return !flights.empty() && flights.front().done && hipEventQuery(flights.front().done) == hipSuccess;
+    }
     cts_buf_desc* StageDescs() const
     {
         return reinterpret_cast<cts_buf_desc*>(stage_desc.host) + (size_t)desc_set * BatchCapacity();
@@ -898,12 +933,13 @@ struct cts_io_pattern {
         return EnsureStageDescs();
     }
 
-    int EnsureStageDescs()  // both halves
+    int EnsureStageDescs()  // every set
     {
         if (stage_desc.host != nullptr) return CTS_OK;
         int rc;
-        if ((rc = stage_desc.alloc(engine, sizeof(cts_buf_desc) * 2ull * BatchCapacity())) != CTS_OK) return rc;
-        return stage_res.alloc(engine, sizeof(cts_verify_result) * 2ull * BatchCapacity());
+        const uint64_t n = (uint64_t)Sets() * BatchCapacity();
+        if ((rc = stage_desc.alloc(engine, sizeof(cts_buf_desc) * n)) != CTS_OK) return rc;
+        return stage_res.alloc(engine, sizeof(cts_verify_result) * n);
     }
 
     int Enqueue(const cts_task& t, uint32_t transferred, uint64_t recv_after)
@@ -958,7 +994,7 @@ struct cts_io_pattern {
         return CTS_OK;
     }
 
-    int LaunchBatch()  // verifies `queue` (descriptor half desc_set) on the pattern's stream, async
+    int LaunchBatch()  // verifies `queue` (descriptor set desc_set) on the pattern's stream, async
     {
         int rc = EnsureStream();
         if (rc != CTS_OK) return rc;
@@ -998,56 +1034,99 @@ struct cts_io_pattern {
         }
     }
 
-    hipError_t WaitInflight()
+    hipError_t WaitInflight(hipEvent_t done)  // the kernel behind `done`
     {
-        if (inflight_done == nullptr || retire_wait == 0) return hipStreamSynchronize(stream);
-        if (retire_wait == 1) return hipEventSynchronize(inflight_done);
+        if (done == nullptr || retire_wait == 0) return hipStreamSynchronize(stream);
+        if (retire_wait == 1) return hipEventSynchronize(done);
         for (;;) {
-            const hipError_t q = hipEventQuery(inflight_done);
+            const hipError_t q = hipEventQuery(done);
             if (q != hipErrorNotReady) return q;
             std::this_thread::sleep_for(std::chrono::microseconds(50));
         }
     }
 
-    // Waits for the in-flight batch and applies its verdicts. A failure in it takes back
-    // everything completed after the failing buffer, the filling batch included.
-    int Retire()
+    // Waits for the oldest in-flight batch and applies its verdicts. A failure in it takes back everything completed
+    // after the failing buffer: the batches launched after it and the filling batch are dropped.
+    int RetireOldest()
     {
-        if (inflight.empty()) return CTS_OK;
+        if (flights.empty()) return CTS_OK;
+        Flight& f = flights.front();
         const auto w0 = std::chrono::steady_clock::now();
-        const hipError_t wr = WaitInflight();
+        const hipError_t wr = WaitInflight(f.done);
         AddVerifyWait(w0);
         if (wr != hipSuccess) return CTS_E_HIP;
-        const size_t half = (size_t)(desc_set ^ 1u) * BatchCapacity();
-        const bool failed = ApplyVerdicts(inflight, reinterpret_cast<const cts_verify_result*>(stage_res.host) + half);
-        inflight.clear();
+        const bool failed = ApplyVerdicts(
+            f.q, reinterpret_cast<const cts_verify_result*>(stage_res.host) + (size_t)f.set * BatchCapacity());
+        spare_events.push_back(f.done);
+        f.q.clear();
+        spare_queues.push_back(std::move(f.q));
+        flights.pop_front();
         if (failed) {
+            // the later kernels' verdicts are never applied; they finish before their sets are written again
+            if (!flights.empty() && hipStreamSynchronize(stream) != hipSuccess) return CTS_E_HIP;
+            for (Flight& g : flights) spare_events.push_back(g.done);
+            flights.clear();
             queue.clear();
             stage_used = 0;
         }
         PublishIfSettled();
         return CTS_OK;
     }
+    int Retire()  // every in-flight batch, oldest first, up to a failing one
+    {
+        const bool had_failure = has_failure;
+        while (!flights.empty()) {
+            const int rc = RetireOldest();
+            if (rc != CTS_OK) return rc;
+            if (has_failure && !had_failure) break;
+        }
+        return CTS_OK;
+    }
+    int RetireDone()  // the in-flight batches whose kernels have finished, oldest first
+    {
+        const bool had_failure = has_failure;
+        while (InflightDone()) {
+            const int rc = RetireOldest();
+            if (rc != CTS_OK) return rc;
+            if (has_failure && !had_failure) break;
+        }
+        return CTS_OK;
+    }
 
-    // The filling batch is full: retire the in-flight one, launch this one and keep receiving.
+    // The filling batch is full: retire the oldest in-flight one if Depth() are running, launch this one and keep
+    // receiving.
     int Rotate()
     {
         if (!DoubleBuffered() || !queue_in_ring) return Flush();
-        const int rc = Retire();
-        if (rc != CTS_OK) return rc;
-        if (queue.empty()) return GetCurrentStatus();  // the in-flight batch failed
+        const bool had_failure = has_failure;
+        while (flights.size() >= Depth()) {
+            const int rc = RetireOldest();
+            if (rc != CTS_OK) return rc;
+            if (has_failure && !had_failure) return GetCurrentStatus();  // an in-flight batch failed
+        }
+        if (queue.empty()) return GetCurrentStatus();
         const int lr = LaunchBatch();
         if (lr != CTS_OK) return lr;
-        if (inflight_done == nullptr &&
-            hipEventCreateWithFlags(&inflight_done, hipEventDisableTiming | (retire_wait == 1 ? hipEventBlockingSync : 0u)) !=
-                hipSuccess) {
-            inflight_done = nullptr;
+        hipEvent_t e = nullptr;
+        if (!spare_events.empty()) {
+            e = spare_events.back();
+            spare_events.pop_back();
+        } else if (hipEventCreateWithFlags(&e, hipEventDisableTiming | (retire_wait == 1 ? hipEventBlockingSync : 0u)) !=
+                   hipSuccess) {
             return CTS_E_HIP;
         }
-        if (hipEventRecord(inflight_done, stream) != hipSuccess) return CTS_E_HIP;
-        inflight.swap(queue);
+        if (hipEventRecord(e, stream) != hipSuccess) {
+            spare_events.push_back(e);
+            return CTS_E_HIP;
+        }
+        flights.push_back(Flight{{}, e, desc_set});
+        flights.back().q.swap(queue);
+        if (!spare_queues.empty()) {
+            queue.swap(spare_queues.back());
+            spare_queues.pop_back();
+        }
         queue.clear();
-        desc_set ^= 1u;
+        desc_set = (desc_set + 1u) % Sets();
         return GetCurrentStatus();
     }
 
@@ -1149,11 +1228,11 @@ struct cts_io_pattern {
             // this completion rather than at the next launch (ctsIOPattern.cpp:486-489 fails it at the
             // failing one; the completions in between are taken back by RollbackAfter)
             const bool had_failure = has_failure;
-            const int rc = Retire();
+            const int rc = RetireDone();
             if (rc < 0) return rc;
             if (has_failure && !had_failure) return GetCurrentStatus();
         }
-        if (Deferred() && (!queue.empty() || !inflight.empty()) && !benign) {
+        if (Deferred() && (!queue.empty() || !flights.empty()) && !benign) {
             const bool had_failure = has_failure;
             const int rc = Flush();
             if (rc < 0) return rc;
@@ -2108,7 +2187,7 @@ int cts_io_pattern_set_verifier(cts_io_pattern* p, cts_batch_verifier fn, void* 
 {
     if (p == nullptr) return CTS_E_INVALID;
     std::lock_guard<std::recursive_mutex> lk(p->mu);
-    if (!p->queue.empty() || !p->inflight.empty()) return CTS_E_INVALID;
+    if (!p->queue.empty() || !p->flights.empty()) return CTS_E_INVALID;
     p->hook = fn;
     p->hook_ctx = ctx;
     return CTS_OK;
@@ -2236,7 +2315,7 @@ int cts_io_pattern_get_stats(const cts_io_pattern* p, cts_pattern_stats* o)
     o->recv_pattern_offset = p->m_recvPatternOffset;
     o->send_pattern_offset = p->m_sendPatternOffset;
     o->last_error = p->m_lastError;
-    o->queued = (uint32_t)(p->queue.size() + p->inflight.size());
+    o->queued = (uint32_t)p->queue.size() + p->InFlightCount();
     o->fail_length = p->fail_length;
     o->fail_offset = p->fail_offset;
     o->fail_expected = p->fail_expected;
