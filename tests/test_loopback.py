@@ -333,6 +333,41 @@ def test_config1_three_arrangements_gpu(engine, corrupt):
         assert srv["bytes_recv"] == 9001 * 65536 and srv["queued"] == 0
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch", [0, 16])
+@pytest.mark.parametrize("depth", [2, 3])
+@pytest.mark.parametrize("corrupt", [None, 5], ids=["clean", "corrupt"])
+def test_config1_deferred_depths_gpu(engine, monkeypatch, depth, corrupt, batch):
+    """Config 1 at full size with 2 and 3 DEFERRED batches in flight per connection (CTS_DEFERRED_DEPTH): the same
+    status details, per-connection statistics, failure records and statuses as the CPU oracle in each receive
+    thread, clean and with one corrupted connection (a failing batch drops the ones launched after it); at the
+    feeder's batch and at 16 buffers (launches of 5 or 4 buffers, thousands per connection)."""
+    hook = A.BATCH_VERIFIER(oracle.batch_verifier_address())
+
+    def run(**kw):
+        if "verifier" in kw:
+            shared_buffer_attach(_SENDER)
+            monkeypatch.delenv("CTS_DEFERRED_DEPTH", raising=False)
+        else:
+            monkeypatch.setenv("CTS_DEFERRED_DEPTH", str(depth))
+        try:
+            return loopback.run(**kw)
+        finally:
+            monkeypatch.delenv("CTS_DEFERRED_DEPTH", raising=False)
+
+    arr = {"cpu_oracle": dict(verifier=hook, verify_mode=A.VERIFY_SYNC),
+           "gpu_deferred": dict(engine=engine, verify_mode=A.VERIFY_DEFERRED, batch_buffers=batch)}
+    totals, sides = _three_way(run, 8, 1 << 30, corrupt, 9000, arr)
+    if corrupt is None:
+        assert totals["connections_ok"] == 8 and totals["data_errors"] == 0
+        assert all(s["buffers_verified"] == 16384 for s in sides[8:])
+    else:
+        assert totals["connections_ok"] == 7 and totals["data_errors"] == 1
+        srv = sides[8 + corrupt]
+        assert srv["fail_completion"] == 9000 and srv["buffers_verified"] == 9001
+        assert srv["bytes_recv"] == 9001 * 65536 and srv["queued"] == 0
+
+
 def test_loopback_send_pacing_cpu():
     """Send pacing end to end: the feeder's senders wait each task's time offset (ctsSendRecvIocp.cpp:378-383).
     4 Push connections x 40 x 8 KiB at 1 MiB/s each (100 ms quanta of 104 857 B, 13 buffers) are deferred into
