@@ -228,6 +228,7 @@ extern "C" int cts_loopback_media_stream_run(const cts_media_stream_loopback_con
         c.ms_datagram_max_size = max_dgram;
         c.ms_buffered_frames = cfg->buffered_frames;
         c.ms_stream_length_frames = cfg->stream_length_frames;
+        c.batch_buffers = listening ? 0u : cfg->batch_buffers;
         return c;
     };
     std::vector<Conn> conns(n);

@@ -114,7 +114,8 @@ class MediaStreamLoopbackConfig(ctypes.Structure):
                 ("buffered_frames", ctypes.c_uint32), ("datagram_max_size", ctypes.c_uint32),
                 ("pre_post_recvs", ctypes.c_uint32), ("verify_buffers", ctypes.c_uint32),
                 ("corrupt_connection", ctypes.c_uint32), ("corrupt_datagram", ctypes.c_uint32),
-                ("socket_buffer_bytes", ctypes.c_uint32), ("verify_mode", ctypes.c_uint32)]
+                ("socket_buffer_bytes", ctypes.c_uint32), ("verify_mode", ctypes.c_uint32),
+                ("batch_buffers", ctypes.c_uint32)]
 
 
 def _media_stream_result_type():
@@ -133,7 +134,7 @@ def _media_stream_result_type():
 def media_stream_run(connections=2, frame_size=52083, frames_per_second=60, stream_length_frames=60,
                      buffered_frames=10, datagram_max_size=1400, pre_post_recvs=2, engine=None, verifier=None,
                      verify=True, corrupt_connection=None, corrupt_datagram=0, socket_buffer_bytes=0,
-                     verify_mode=A.VERIFY_SYNC) -> dict:
+                     verify_mode=A.VERIFY_SYNC, batch_buffers=0) -> dict:
     """MediaStream over loopback UDP ("-Protocol:UDP -Pattern:MediaStream", README sizing by default: FrameSize
     52083 B at 60 frames/s): every connection's server streams its frames at the frame rate and its client verifies
     every datagram's payload (on ``engine`` or through ``verifier``) and renders the frames."""
@@ -148,7 +149,7 @@ def media_stream_run(connections=2, frame_size=52083, frames_per_second=60, stre
     cfg = MediaStreamLoopbackConfig(connections, frame_size, frames_per_second, stream_length_frames,
                                     buffered_frames, datagram_max_size, pre_post_recvs, int(verify),
                                     0xFFFFFFFF if corrupt_connection is None else corrupt_connection,
-                                    corrupt_datagram, socket_buffer_bytes, verify_mode)
+                                    corrupt_datagram, socket_buffer_bytes, verify_mode, batch_buffers)
     hook = None
     if verifier is not None:
         hook = verifier if isinstance(verifier, A.BATCH_VERIFIER) else batch_verifier(verifier)

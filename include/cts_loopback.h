@@ -129,6 +129,8 @@ typedef struct cts_media_stream_loopback_config {
     uint32_t socket_buffer_bytes;   /* SO_SNDBUF / SO_RCVBUF (0 = 8 MiB) */
     uint32_t verify_mode;           /* the client's CTS_VERIFY_SYNC (per datagram) or CTS_VERIFY_DEFERRED (batches
                                        through the frame-sum receive pass, flushed at every render tick) */
+    uint32_t batch_buffers;         /* the client's DEFERRED batch: datagrams queued before a flush between ticks,
+                                       and half its recv ring (0 = the pattern's default, 1024) */
 } cts_media_stream_loopback_config;
 
 typedef struct cts_media_stream_loopback_result {
