@@ -200,10 +200,13 @@ __global__ void __launch_bounds__(256) plain_read_skew(const u32x4* __restrict__
                                                        uint32_t* out)
 {
     const uint64_t t_entry = STAMP ? stamp() : 0;
-    const uint32_t S = gridDim.x / 8u, dd = S * (uint32_t)SKEW / (64u + (uint32_t)SKEW), So = S - 2u * dd;
+    // SKEW < 0: the even XCDs get the fewer workgroups instead
+    constexpr uint32_t AS = (uint32_t)(SKEW < 0 ? -SKEW : SKEW);
+    const uint32_t S = gridDim.x / 8u, dd = S * AS / (64u + AS), So = S - 2u * dd;
     const uint32_t x = blockIdx.x & 7u, q = blockIdx.x >> 3;
-    if ((x & 1u) && q >= So) return;
-    const uint32_t rank = (x & 1u) ? 4u * S + (x >> 1) * So + q : (x >> 1) * S + q;
+    const uint32_t few = (x & 1u) ^ (SKEW < 0 ? 1u : 0u);  // this XCD runs So workgroups
+    if (few && q >= So) return;
+    const uint32_t rank = few ? 4u * S + (x >> 1) * So + q : (x >> 1) * S + q;
     const uint32_t A = 4u * S + 4u * So;
     uint32_t acc = 0, k = 0;
     uint64_t* my = st + (uint64_t)rank * kSt;
@@ -232,8 +235,41 @@ __global__ void __launch_bounds__(256) plain_read_skew(const u32x4* __restrict__
 // the grid plain_read_skew<SKEW> needs for about `active` working workgroups
 inline uint32_t skew_grid(uint32_t active, int skew)
 {
-    const uint32_t P = active / 8u;
-    return 8u * (P + (P * (uint32_t)skew + 63u) / 64u);
+    const uint32_t P = active / 8u, a = (uint32_t)(skew < 0 ? -skew : skew);
+    return 8u * (P + (P * a + 63u) / 64u);
+}
+
+// The plain read with UO loads per lane per round on the odd XCDs (by HW_REG_XCC_ID) and 2 on the even ones ("xu"
+// mode): do the late XCDs want more bytes in flight?
+template <int UO>
+__global__ void __launch_bounds__(256) plain_read_xu(const u32x4* __restrict__ p, uint32_t nslabs, uint32_t* out)
+{
+    uint32_t acc = 0;
+    const bool odd = (xcc_id() & 1u) != 0u;
+    for (uint32_t sl = blockIdx.x; sl < nslabs; sl += gridDim.x) {
+        const u32x4* q = p + (uint64_t)sl * 4096u;
+        if (odd) {
+            for (uint32_t r = 0; r < 16u / UO; ++r) {
+                u32x4 d[UO];
+#pragma unroll
+                for (int u = 0; u < UO; ++u) d[u] = __builtin_nontemporal_load(q + r * 256u * UO + u * 256u + threadIdx.x);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int u = 0; u < UO; ++u) acc |= d[u][0] ^ d[u][1] ^ d[u][2] ^ d[u][3];
+            }
+        } else {
+            for (uint32_t r = 0; r < 8; ++r) {
+                const uint32_t c = r * 512u + threadIdx.x;
+                u32x4 d[2];
+                d[0] = __builtin_nontemporal_load(q + c);
+                d[1] = __builtin_nontemporal_load(q + c + 256u);
+                __builtin_amdgcn_sched_barrier(0);
+                acc |= d[0][0] ^ d[0][1] ^ d[0][2] ^ d[0][3] ^ d[1][0] ^ d[1][1] ^ d[1][2] ^ d[1][3];
+            }
+        }
+        acc = __syncthreads_or(acc == 0x12345678u) ? 1u : acc;
+    }
+    if (acc == 0x12345678u) out[0] = acc;
 }
 
 template <typename F>
@@ -318,6 +354,7 @@ int main(int argc, char** argv)
     const int passes = argc > 1 ? atoi(argv[1]) : 3;
     const bool map_mode = argc > 3 && std::string(argv[3]) == "map";
     const bool skew_mode = argc > 3 && std::string(argv[3]) == "skew";
+    const bool xu_mode = argc > 3 && std::string(argv[3]) == "xu";
     const int reps = argc > 2 ? atoi(argv[2]) : 64;
     int cus = 0;
     CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
@@ -367,6 +404,27 @@ int main(int argc, char** argv)
     CHECK(hipStreamCreate(&s));
     CHECK(hipDeviceSynchronize());
 
+    if (xu_mode) {
+        // more bytes in flight on the late XCDs (U 4 / 8 on the odd ones), or more workgroups there (skew -4 / -8)
+        for (int pass = 0; pass < passes; ++pass) {
+            auto a = [&](int i) { return reinterpret_cast<const u32x4*>(arena[i % R]); };
+            const double t2 = time_us([&](int i) { plain_read_xu<2><<<grid, 256, 0, s>>>(a(i), n, out); }, reps, s);
+            const double t4 = time_us([&](int i) { plain_read_xu<4><<<grid, 256, 0, s>>>(a(i), n, out); }, reps, s);
+            const double t8 = time_us([&](int i) { plain_read_xu<8><<<grid, 256, 0, s>>>(a(i), n, out); }, reps, s);
+            const double m4 = time_us([&](int i) {
+                plain_read_skew<false, -4><<<skew_grid(grid, -4), 256, 0, s>>>(a(i), n, st, out);
+            }, reps, s);
+            const double m8 = time_us([&](int i) {
+                plain_read_skew<false, -8><<<skew_grid(grid, -8), 256, 0, s>>>(a(i), n, st, out);
+            }, reps, s);
+            const double p0 = time_us([&](int i) { plain_read<false><<<grid, 256, 0, s>>>(a(i), n, st, out); }, reps, s);
+            std::printf("{\"kind\":\"xu_time\",\"pass\":%d,\"launches\":%d,\"plain_us\":%.2f,\"odd_u2_us\":%.2f,"
+                        "\"odd_u4_us\":%.2f,\"odd_u8_us\":%.2f,\"more_wg_on_odd_skew4_us\":%.2f,"
+                        "\"more_wg_on_odd_skew8_us\":%.2f}\n", pass, reps, p0, t2, t4, t8, m4, m8);
+            std::fflush(stdout);
+        }
+        return 0;
+    }
     if (skew_mode) {
         // does reading fewer slabs on the late (odd) XCDs shorten the launch? active workgroups stay ~1024
         std::vector<uint64_t> h((size_t)grid * 2 * kSt);
