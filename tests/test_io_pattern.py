@@ -83,6 +83,9 @@ class RioCheckedPattern(IoPattern):
         return super().CompleteIo(task, current_transfer, status_code)
 
 
+RIO_BACKENDS = [b for b in BACKENDS if b.values[0][2]]  # the registered-IO backends (tests of RIO ids only)
+
+
 @pytest.fixture(params=BACKENDS)
 def make(request):
     kind, mode, rio = request.param
@@ -1299,12 +1302,11 @@ def test_deferred_counters_never_decrease(make, seed, corrupt):
 
 
 # ---- RIO buffer ids (ctsIOPattern.cpp:133-217, :369-386, :683-692, :716-725) ------------------------
+@pytest.mark.parametrize("make", RIO_BACKENDS, indirect=True)
 def test_rio_send_ids_unique_and_recycled(make):
     """A Push client under -io:rioiocp: concurrent sends carry distinct ids of the sender buffer's
     registrations; a completed send's id goes back on the list and is the next one handed out (the
     reference pops and pushes at the back)."""
-    if not make.rio:
-        pytest.skip("registered IO only")
     p = make(**client_defaults(pre_post_sends=3, transfer_size=100000))
     t = p.InitiateIo()
     assert p.CompleteIo(t, ConnectionIdLength, 0) == ContinueIo
@@ -1319,12 +1321,11 @@ def test_rio_send_ids_unique_and_recycled(make):
     assert nxt.rio_buffer_id == sends[1].rio_buffer_id
 
 
+@pytest.mark.parametrize("make", RIO_BACKENDS, indirect=True)
 def test_rio_send_ids_exhausted_returns_no_io(make):
     """-io:rioiocp registers the sender buffer 16 MiB / min buffer + 1 times (ctsIOPattern.cpp:61, 195-217). With
     every one of those ids in flight the next send request is an empty task, not a send (ctsIOPattern.cpp:580-587);
     a completed send's id makes the next request a send again, and the send offsets stay contiguous."""
-    if not make.rio:
-        pytest.skip("registered IO only")
     size = 65536
     p = make(**client_defaults(pre_post_sends=400, buffer_size=size, transfer_size=400 * size))
     t = p.InitiateIo()
