@@ -338,6 +338,25 @@ void print_timeline(const char* kind, const std::vector<uint64_t>& h, uint32_t g
         std::printf("%s[%u,%.2f,%.2f,%.2f]", first ? "" : ",", x, pct(ex, 0), pct(ex, 0.5), pct(ex, 1));
         first = 0;
     }
+    // per XCC: medians of entry, entry to first issue, first buffer, later buffers
+    std::printf("],\"phases_by_xcc\":[");
+    for (uint32_t x = 0, first = 1; x < 8; ++x) {
+        std::vector<double> en, fi, fb, lb;
+        for (uint32_t b = 0; b < grid; ++b) {
+            const uint64_t* m = &h[(size_t)b * kSt];
+            const uint32_t k = (uint32_t)(m[11] >> 8);
+            if (k == 0 || (m[11] & 0xFu) != x) continue;
+            const uint32_t kk = std::min<uint32_t>(k, 8);
+            en.push_back((m[0] - t0) * 0.01);
+            fi.push_back((m[1] - m[0]) * 0.01);
+            fb.push_back((m[2] - m[1]) * 0.01);
+            for (uint32_t j = 1; j < kk; ++j) lb.push_back((m[2 + j] - m[1 + j]) * 0.01);
+        }
+        if (en.empty()) continue;
+        std::printf("%s[%u,%.2f,%.2f,%.2f,%.2f]", first ? "" : ",", x, pct(en, 0.5), pct(fi, 0.5), pct(fb, 0.5),
+                    pct(lb, 0.5));
+        first = 0;
+    }
     std::printf("]}\n");
     std::fflush(stdout);
 }
