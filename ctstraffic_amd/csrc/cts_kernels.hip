@@ -429,8 +429,7 @@ __device__ __forceinline__ void scan_exact_whole(const Span& s, uint32_t lane, u
 // thousand that workgroup is the launch's last to finish.) The clean-path cost is
 // one compare and branch per round.
 // A16: the span starts on a 16-aligned pattern position (expected_step_a16).
-// PRE: the first round's U chunks per lane were loaded by the caller (pre[u] = chunk u * TEAM + lane); the span holds
-// at least one whole round.
+// One whole round: XOR the U loaded chunks with the expected words, then the exact diff of a round that differs.
 template <int TEAM, int U, bool EVEN, bool A16>
 __device__ __forceinline__ void whole_exact_round(const Span& s, u32x4 (&d)[U], uint32_t cb, uint32_t lane,
                                                   uint32_t& first, uint32_t& count)
@@ -450,6 +449,8 @@ __device__ __forceinline__ void whole_exact_round(const Span& s, u32x4 (&d)[U], 
     }
 }
 
+// PRE: the first round's U chunks per lane were loaded by the caller (pre[u] = chunk u * TEAM + lane); the span holds
+// at least one whole round.
 template <int TEAM, int U, bool NT, bool EVEN, bool A16 = false, bool PRE = false>
 __device__ __forceinline__ void scan_whole_exact_impl(const Span& s, __amdgpu_buffer_rsrc_t r, uint32_t lane,
                                                       uint32_t& first, uint32_t& count, const u32x4* pre = nullptr)
