@@ -1226,6 +1226,19 @@ def test_random_push_server_stream(make, seed):
     assert s["recv_pattern_offset"] == (sum(lens[:fail_at + 1])) % 65536
 
 
+GPU_DEFERRED_BACKENDS = [b for b in BACKENDS if b.values[0][0] == "gpu" and b.values[0][1] == A.VERIFY_DEFERRED]
+
+
+@pytest.mark.parametrize("depth", [2, 3])
+@pytest.mark.parametrize("seed,corrupt", [(21, False), (22, True), (23, True)])
+@pytest.mark.parametrize("make", GPU_DEFERRED_BACKENDS, indirect=True)
+def test_deferred_counters_never_decrease_pipelined(make, seed, corrupt, depth, monkeypatch):
+    """The same with 2 and 3 DEFERRED batches in flight (CTS_DEFERRED_DEPTH, read when the pattern is made): a batch
+    that fails drops the ones launched after it, and nothing published is taken back."""
+    monkeypatch.setenv("CTS_DEFERRED_DEPTH", str(depth))
+    _check_counters_never_decrease(make, seed, corrupt)
+
+
 @pytest.mark.parametrize("seed,corrupt", [(11, False), (12, True), (13, True), (14, True)])
 def test_deferred_counters_never_decrease(make, seed, corrupt):
     """TcpStatusDetails and the per-connection byte counters only ever grow. The reference only Adds to them
@@ -1235,6 +1248,11 @@ def test_deferred_counters_never_decrease(make, seed, corrupt):
     completes its sends and recvs in random order, with a corrupt recv in the middle of a batch. Both counters are
     read after every completion; the end totals must be the reference's: everything up to and including the failing
     recv, nothing after it, in every verify mode."""
+    _check_counters_never_decrease(make, seed, corrupt)
+
+
+def _check_counters_never_decrease(make, seed, corrupt):
+    """The body of test_deferred_counters_never_decrease (and of its pipelined form)."""
     from ctstraffic_amd.pattern import status_details, status_details_reset
 
     rng = np.random.default_rng(seed)
