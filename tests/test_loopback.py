@@ -335,13 +335,14 @@ def test_config1_three_arrangements_gpu(engine, corrupt):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("batch", [0, 16])
-@pytest.mark.parametrize("depth", [2, 3])
+@pytest.mark.parametrize("depth", [1, 3])
 @pytest.mark.parametrize("corrupt", [None, 5], ids=["clean", "corrupt"])
 def test_config1_deferred_depths_gpu(engine, monkeypatch, depth, corrupt, batch):
-    """Config 1 at full size with 2 and 3 DEFERRED batches in flight per connection (CTS_DEFERRED_DEPTH): the same
+    """Config 1 at full size with 1 and 3 DEFERRED batches in flight per connection (CTS_DEFERRED_DEPTH; the default,
+    2, runs in test_config1_three_arrangements_gpu): the same
     status details, per-connection statistics, failure records and statuses as the CPU oracle in each receive
     thread, clean and with one corrupted connection (a failing batch drops the ones launched after it); at the
-    feeder's batch and at 16 buffers (launches of 5 or 4 buffers, thousands per connection)."""
+    feeder's batch and at 16 buffers (launches of 8 or 4 buffers, thousands per connection)."""
     hook = A.BATCH_VERIFIER(oracle.batch_verifier_address())
 
     def run(**kw):
