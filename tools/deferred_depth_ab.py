@@ -4,7 +4,8 @@ flight per connection (CTS_DEFERRED_DEPTH, read when a pattern is made), beside 
 one process. Each launch holds batch / (depth + 1) buffers, so the ring and the verdict bound stay the
 same. One JSON line per leg and round: GB/s received, receive-thread CPU per GiB, and the verdict waits
 (cts_pattern_stats.verify_wait_ns summed over the receiving sides) per GiB.
-usage: python tools/deferred_depth_ab.py [rounds] [batch_buffers] [legs, e.g. off,1,2]"""
+usage: python tools/deferred_depth_ab.py [rounds] [batch_buffers] [legs, e.g. off,1,2 or 2@512,2@1024]
+(a leg "d@b" runs depth d at batch b)"""
 import json
 import os
 import sys
@@ -28,15 +29,16 @@ def main():
                 res = LB.run(connections=8, buffer_size=65536, transfer_size=1 << 30, verify=False)
                 wait = 0.0
             else:
-                os.environ["CTS_DEFERRED_DEPTH"] = leg
+                depth, _, b = leg.partition("@")
+                os.environ["CTS_DEFERRED_DEPTH"] = depth
                 try:
                     res = LB.run(connections=8, buffer_size=65536, transfer_size=1 << 30, engine=eng,
-                                 verify_mode=PA.VERIFY_DEFERRED, batch_buffers=batch, sides=True)
+                                 verify_mode=PA.VERIFY_DEFERRED, batch_buffers=int(b) if b else batch, sides=True)
                 finally:
                     os.environ.pop("CTS_DEFERRED_DEPTH", None)
                 wait = sum(sd["verify_wait_ns"] for sd in res["sides"]) * 1e-9
             print(json.dumps({"round": r, "leg": "verify_off" if leg == "off" else "deferred_depth_" + leg,
-                              "batch_buffers": batch, "GBps_recv": round(res["GBps_recv"], 3),
+                              "batch_buffers": batch if "@" not in leg else int(leg.partition("@")[2]), "GBps_recv": round(res["GBps_recv"], 3),
                               "connections_ok": res["connections_ok"], "data_errors": res.get("data_errors", 0),
                               "recv_cpu_s_per_GiB": round(res["recv_cpu_s_per_GiB"], 4),
                               "verdict_wait_s_per_GiB": round(wait / max(res["bytes_recv"] / GIB, 1e-9), 4)}),
