@@ -144,9 +144,10 @@ typedef struct cts_pattern_config {
     uint64_t transfer_size;     /* GetTransferSize() */
     uint64_t random_seed;       /* seed of the -buffer:[lo,hi] draw (reference: random_device) */
     uint32_t verify_mode;       /* cts_verify_mode */
-    uint32_t batch_buffers;     /* DEFERRED: max queued buffers per batch (0 = 1024); on a device one
-                                   batch verifies while the next fills, so the pinned recv ring holds
-                                   2 x batch_buffers + recvCount + 1 buffers */
+    uint32_t batch_buffers;     /* DEFERRED: completions within which every verdict is known (0 = 1024); on a
+                                   device the batch is launched in parts of batch_buffers / (depth + 1) with
+                                   up to depth running while the next fills (CTS_DEFERRED_DEPTH, default 2), and
+                                   the pinned recv ring holds 2 x batch_buffers + recvCount + 1 buffers */
     uint64_t batch_bytes;       /* DEFERRED: staging arena bytes (0 = 64 MiB) */
     uint32_t registered_io;     /* SocketFlags & WSA_FLAG_REGISTERED_IO (-io:rioiocp): register buffers with
                                  * the RIO functions of cts_rio_functions_set, hand their ids out in tasks */
@@ -200,8 +201,9 @@ typedef struct cts_pattern_stats {
      * are dropped without ever being published. 0 in SYNC mode. */
     uint64_t bytes_sent_held;
     uint64_t bytes_recv_held;
-    /* DEFERRED: wall time this pattern's calls spent waiting for batch verdicts from the device (retiring the in-flight
-     * half, a flush's synchronize, a MediaStream client's batch): the receive thread is idle on the GPU meanwhile. */
+    /* DEFERRED: wall time this pattern's calls spent waiting for batch verdicts from the device (retiring the oldest
+     * in-flight launch, a flush's synchronize, a MediaStream client's batch): the receive thread is idle on the GPU
+     * meanwhile. */
     uint64_t verify_wait_ns;
 } cts_pattern_stats;
 
