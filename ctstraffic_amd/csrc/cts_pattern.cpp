@@ -886,7 +886,7 @@ struct cts_io_pattern {
 
     uint64_t StageCapacity() const { return cfg.batch_bytes ? cfg.batch_bytes : (64ull << 20); }
     uint32_t BatchCapacity() const { return cfg.batch_buffers ? cfg.batch_buffers : 1024u; }
-    bool DoubleBuffered() const { return engine != nullptr && hook == nullptr; }
+    bool DoubleBuffered() const { return engine != nullptr && hook == nullptr; }  // launches pipelined (Depth())
     // Batches in flight at once (pipelined: at least 1, and at most BatchCapacity() - 1 so that a launch holds a
     // buffer or more)
     uint32_t Depth() const
@@ -1003,9 +1003,9 @@ struct cts_io_pattern {
         for (const auto& q : queue) maxlen = std::max(maxlen, q.transferred);
         const uint8_t* arena = queue_in_ring ? recv_pinned.dev : stage.dev;
         const uint64_t bytes = queue_in_ring ? recv_pinned.bytes : stage.bytes;
-        const size_t half = (size_t)desc_set * BatchCapacity();
-        return cts_verify(engine, arena, bytes, reinterpret_cast<cts_buf_desc*>(stage_desc.dev) + half,
-                          (uint32_t)queue.size(), maxlen, reinterpret_cast<cts_verify_result*>(stage_res.dev) + half,
+        const size_t set = (size_t)desc_set * BatchCapacity();
+        return cts_verify(engine, arena, bytes, reinterpret_cast<cts_buf_desc*>(stage_desc.dev) + set,
+                          (uint32_t)queue.size(), maxlen, reinterpret_cast<cts_verify_result*>(stage_res.dev) + set,
                           nullptr, nullptr, 0, stream);
     }
 
