@@ -108,7 +108,15 @@ double thread_cpu_ns_s()
     return (double)ts.tv_sec + (double)ts.tv_nsec * 1e-9;
 }
 
-void run_side(int* fdslot, cts_io_pattern* p, bool inject, uint32_t inject_index, bool recv_whole, SideResult* out)
+// The diagnostic recv ring (cts_loopback_config.recv_ring_buffers): data recvs land in its slots round robin.
+struct RecvRing {
+    char* base = nullptr;
+    uint32_t slots = 0, slot_bytes = 0, next = 0;
+    char* take() { return base + (size_t)(next++ % slots) * slot_bytes; }
+};
+
+void run_side(int* fdslot, cts_io_pattern* p, bool inject, uint32_t inject_index, bool recv_whole, SideResult* out,
+              RecvRing ring = {})
 {
     const double cpu0 = thread_cpu_s();
     const int fd = *fdslot;
@@ -143,8 +151,12 @@ void run_side(int* fdslot, cts_io_pattern* p, bool inject, uint32_t inject_index
             // (or, with recv_whole, with the whole posted length: deterministic completions)
             const bool whole = recv_whole || t.buffer_type == CTS_BUFFER_TCP_CONNECTION_ID ||
                                t.buffer_type == CTS_BUFFER_COMPLETION_MESSAGE;
+            char* dst = t.buffer + t.buffer_offset;
+            if (ring.base != nullptr && t.buffer_type == CTS_BUFFER_DYNAMIC && t.track_io &&
+                t.buffer_length <= ring.slot_bytes)
+                dst = ring.take();  // verify is off: the pattern never reads the bytes
             const double c0 = thread_cpu_ns_s();
-            status = recv_some(fd, t.buffer + t.buffer_offset, t.buffer_length, &transferred, whole);
+            status = recv_some(fd, dst, t.buffer_length, &transferred, whole);
             io_cpu += thread_cpu_ns_s() - c0;
             break;
         }
@@ -428,6 +440,44 @@ extern "C" int cts_loopback_run_detailed(const cts_loopback_config* cfg, cts_eng
         ::close(lfd);
         return rc;
     }
+    // the diagnostic recv ring: one per side that receives data, verify off and the sync functor only
+    std::vector<RecvRing> rings(2 * n);
+    std::vector<std::vector<char>> ring_pageable;
+    std::vector<void*> ring_pinned;
+    auto free_rings = [&] {
+        for (void* q : ring_pinned) (void)cts_host_free(engine, q);
+        ring_pinned.clear();
+    };
+    if (cfg->recv_ring_buffers) {
+        if (cfg->verify_buffers || async || (cfg->recv_ring_pinned && engine == nullptr)) {
+            for (auto* p : pats) cts_io_pattern_destroy(p);
+            ::close(lfd);
+            return CTS_E_INVALID;
+        }
+        const uint64_t bytes = (uint64_t)cfg->recv_ring_buffers * max_buffer;
+        for (uint32_t i = 0; i < 2 * n && rc == CTS_OK; ++i) {
+            const bool receives = pattern == CTS_PATTERN_PUSH ? i >= n : (pattern == CTS_PATTERN_PULL ? i < n : true);
+            if (!receives) continue;
+            char* base = nullptr;
+            if (cfg->recv_ring_pinned) {
+                void* h = nullptr;
+                void* d = nullptr;
+                rc = cts_host_alloc(engine, bytes, &h, &d);
+                if (rc == CTS_OK) ring_pinned.push_back(h);
+                base = static_cast<char*>(h);
+            } else {
+                ring_pageable.emplace_back(bytes);
+                base = ring_pageable.back().data();
+            }
+            rings[i] = RecvRing{base, cfg->recv_ring_buffers, max_buffer, 0};
+        }
+        if (rc != CTS_OK) {
+            free_rings();
+            for (auto* p : pats) cts_io_pattern_destroy(p);
+            ::close(lfd);
+            return rc;
+        }
+    }
     cts_status_details before{};
     (void)cts_status_details_read(&before);
     std::vector<SideResult> res(2 * n);
@@ -464,8 +514,12 @@ extern "C" int cts_loopback_run_detailed(const cts_loopback_config* cfg, cts_eng
         if (fds[i] < 0) continue;
         const bool inject = i % n == cfg->corrupt_connection;  // whichever side(s) send data
         try {
-            threads.emplace_back(async ? run_side_async : run_side, &fds[i], pats[i], inject, cfg->corrupt_send_index,
-                                 cfg->recv_whole != 0, &res[i]);
+            if (async)
+                threads.emplace_back(run_side_async, &fds[i], pats[i], inject, cfg->corrupt_send_index,
+                                     cfg->recv_whole != 0, &res[i]);
+            else
+                threads.emplace_back(run_side, &fds[i], pats[i], inject, cfg->corrupt_send_index, cfg->recv_whole != 0,
+                                     &res[i], rings[i]);
         } catch (const std::system_error&) {
             // no thread for this side: its connection fails (the peer sees the reset), the others run on
             ::shutdown(fds[i], SHUT_RDWR);
@@ -516,5 +570,6 @@ extern "C" int cts_loopback_run_detailed(const cts_loopback_config* cfg, cts_eng
             sides[i].last_error = res[i].last_error;
         }
     for (auto* p : pats) cts_io_pattern_destroy(p);
+    free_rings();
     return CTS_OK;
 }

@@ -19,7 +19,8 @@ class LoopbackConfig(ctypes.Structure):
                 ("pull_bytes", ctypes.c_uint32), ("functor", ctypes.c_uint32), ("recv_whole", ctypes.c_uint32),
                 ("tcp_bytes_per_second", ctypes.c_int64), ("burst_count", ctypes.c_uint32),
                 ("burst_delay", ctypes.c_uint32), ("buffer_size_high", ctypes.c_uint32),
-                ("random_seed", ctypes.c_uint32)]
+                ("random_seed", ctypes.c_uint32), ("recv_ring_buffers", ctypes.c_uint32),
+                ("recv_ring_pinned", ctypes.c_uint32)]
 
 
 FUNCTOR_AUTO, FUNCTOR_SYNC, FUNCTOR_ASYNC = 0, 1, 2
@@ -73,7 +74,7 @@ def run(connections=8, buffer_size=65536, transfer_size=1 << 30, engine=None, ve
         io_pattern=A.PATTERN_PUSH, verify=True, verify_mode=A.VERIFY_DEFERRED, batch_buffers=0,
         corrupt_connection=None, corrupt_send_index=0, socket_buffer_bytes=0, push_bytes=0, pull_bytes=0,
         functor=FUNCTOR_AUTO, recv_whole=False, sides=False, tcp_bytes_per_second=0, burst_count=0,
-        burst_delay=0, buffer_size_high=0, random_seed=0) -> dict:
+        burst_delay=0, buffer_size_high=0, random_seed=0, recv_ring_buffers=0, recv_ring_pinned=False) -> dict:
     """One loopback run. ``engine`` is one Engine or a list of them (one per GPU: connection i verifies on
     engine[cts_shard_of(i, len)]). ``verifier`` (a cts_batch_verifier or a python fn(arena, descs) -> results)
     replaces the engines' kernel (test harnesses / the CPU baseline). ``recv_whole``: data recvs complete
@@ -81,13 +82,16 @@ def run(connections=8, buffer_size=65536, transfer_size=1 << 30, engine=None, ve
     status and last error under "sides" (clients [0, connections), servers [connections, 2 connections)).
     ``tcp_bytes_per_second`` / ``burst_count`` / ``burst_delay``: send pacing of every side (the senders wait the
     tasks' time offsets). ``buffer_size_high``: -Buffer:[buffer_size, buffer_size_high], every IO's size drawn
-    uniformly (side i seeded with ``random_seed`` + i)."""
+    uniformly (side i seeded with ``random_seed`` + i). ``recv_ring_buffers`` (diagnostic, ``verify=False``, sync
+    functor): data recvs land round robin in a ring of that many buffers (pinned with ``recv_ring_pinned``, on the
+    first engine), as a DEFERRED pattern's do."""
     from .pattern import batch_verifier
 
     cfg = LoopbackConfig(connections, io_pattern, buffer_size, int(verify), transfer_size, verify_mode, batch_buffers,
                          0xFFFFFFFF if corrupt_connection is None else corrupt_connection, corrupt_send_index,
                          socket_buffer_bytes, push_bytes, pull_bytes, functor, int(recv_whole), tcp_bytes_per_second,
-                         burst_count, burst_delay, buffer_size_high, random_seed)
+                         burst_count, burst_delay, buffer_size_high, random_seed, recv_ring_buffers,
+                         int(recv_ring_pinned))
     hook = None
     if verifier is not None:
         hook = verifier if isinstance(verifier, A.BATCH_VERIFIER) else batch_verifier(verifier)

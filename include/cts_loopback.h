@@ -46,6 +46,11 @@ typedef struct cts_loopback_config {
     uint32_t buffer_size_high;      /* -Buffer:[buffer_size,buffer_size_high]: every IO draws its size uniformly
                                        (GetBufferSize, ctsConfig.cpp:4679-4684); 0 = fixed buffer_size */
     uint32_t random_seed;           /* side i draws its sizes from random_seed + i */
+    uint32_t recv_ring_buffers;     /* diagnostic, verify off and the sync functor only: every data recv lands in the
+                                       next slot of a ring of this many max-buffer-size slots (round robin), as a
+                                       DEFERRED pattern's recvs do, instead of the pattern's buffer (0 = off) */
+    uint32_t recv_ring_pinned;      /* 1 = that ring in pinned host memory (cts_host_alloc on the first engine, as
+                                       the DEFERRED ring), 0 = pageable */
 } cts_loopback_config;
 
 typedef enum cts_loopback_functor {

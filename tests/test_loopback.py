@@ -369,6 +369,30 @@ def test_config1_deferred_depths_gpu(engine, monkeypatch, depth, corrupt, batch)
         assert srv["bytes_recv"] == 9001 * 65536 and srv["queued"] == 0
 
 
+def test_loopback_diagnostic_recv_ring_cpu():
+    """The feeder's diagnostic recv ring (verify off, sync functor): data recvs land round robin in a ring of
+    buffers, as a DEFERRED pattern's do; counters and statuses are the plain verify-off run's. It refuses to run
+    with verification on, with the async functor, or pinned without an engine."""
+    shared_buffer_attach(_SENDER)
+    base = loopback.run(connections=3, buffer_size=65536, transfer_size=40 * 65536 + 123, verify=False,
+                        recv_whole=True, sides=True)
+    ring = loopback.run(connections=3, buffer_size=65536, transfer_size=40 * 65536 + 123, verify=False,
+                        recv_whole=True, sides=True, recv_ring_buffers=7)
+    for r in (base, ring):
+        assert r["connections_ok"] == 3 and r["data_errors"] == 0
+        assert r["bytes_recv"] == 3 * (40 * 65536 + 123 + 37 + 4)
+    assert [s["bytes_recv"] for s in ring["sides"]] == [s["bytes_recv"] for s in base["sides"]]
+    with pytest.raises(Exception):
+        loopback.run(connections=1, buffer_size=4096, transfer_size=8192, verifier=_oracle_verifier,
+                     verify_mode=A.VERIFY_SYNC, recv_ring_buffers=4)
+    with pytest.raises(Exception):
+        loopback.run(connections=1, buffer_size=4096, transfer_size=8192, verify=False, recv_ring_buffers=4,
+                     io_pattern=A.PATTERN_DUPLEX)
+    with pytest.raises(Exception):
+        loopback.run(connections=1, buffer_size=4096, transfer_size=8192, verify=False, recv_ring_buffers=4,
+                     recv_ring_pinned=True)
+
+
 def test_loopback_send_pacing_cpu():
     """Send pacing end to end: the feeder's senders wait each task's time offset (ctsSendRecvIocp.cpp:378-383).
     4 Push connections x 40 x 8 KiB at 1 MiB/s each (100 ms quanta of 104 857 B, 13 buffers) are deferred into

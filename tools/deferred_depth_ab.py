@@ -5,7 +5,9 @@ one process. Each launch holds batch / (depth + 1) buffers, so
 same. One JSON line per leg and round: GB/s received, receive-thread CPU per GiB, and the verdict waits
 (cts_pattern_stats.verify_wait_ns summed over the receiving sides) per GiB.
 usage: python tools/deferred_depth_ab.py [rounds] [batch_buffers] [legs, e.g. off,1,2 or 2@512,2@1024]
-(a leg "d@b" runs depth d at batch b)"""
+(a leg "d@b" runs depth d at batch b; "ring" / "ringpinned" run verify off with every data recv landing round robin in
+a ring the size of a DEFERRED pattern's at that batch, 2 x batch + 2 buffers, pageable / pinned: the feeder's
+diagnostic recv ring)"""
 import json
 import os
 import sys
@@ -28,6 +30,11 @@ def main():
             if leg == "off":
                 res = LB.run(connections=8, buffer_size=65536, transfer_size=1 << 30, verify=False)
                 wait = 0.0
+            elif leg in ("ring", "ringpinned"):
+                slots = 2 * (batch or 512) + 2  # the DEFERRED ring: 2 x batch + PrePostRecvs + 1
+                res = LB.run(connections=8, buffer_size=65536, transfer_size=1 << 30, verify=False, engine=eng,
+                             recv_ring_buffers=slots, recv_ring_pinned=leg == "ringpinned")
+                wait = 0.0
             else:
                 depth, _, b = leg.partition("@")
                 os.environ["CTS_DEFERRED_DEPTH"] = depth
@@ -37,7 +44,9 @@ def main():
                 finally:
                     os.environ.pop("CTS_DEFERRED_DEPTH", None)
                 wait = sum(sd["verify_wait_ns"] for sd in res["sides"]) * 1e-9
-            print(json.dumps({"round": r, "leg": "verify_off" if leg == "off" else "deferred_depth_" + leg,
+            name = {"off": "verify_off", "ring": "verify_off_ring", "ringpinned": "verify_off_pinned_ring"}.get(
+                leg, "deferred_depth_" + leg)
+            print(json.dumps({"round": r, "leg": name,
                               "batch_buffers": batch if "@" not in leg else int(leg.partition("@")[2]), "GBps_recv": round(res["GBps_recv"], 3),
                               "connections_ok": res["connections_ok"], "data_errors": res.get("data_errors", 0),
                               "recv_cpu_s_per_GiB": round(res["recv_cpu_s_per_GiB"], 4),
