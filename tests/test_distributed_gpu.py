@@ -68,10 +68,15 @@ def test_rccl_world1_collectives_of_the_multi_gpu_path():
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    p = ctx.Process(target=_rank_main, args=(_free_port(), q))
+    p = ctx.Process(target=_rank_main, args=(_free_port(), q), daemon=True)
     p.start()
-    r = q.get(timeout=110)
-    p.join(60)
+    try:
+        r = q.get(timeout=100)
+        p.join(15)
+    finally:
+        if p.is_alive():  # a hung rank must not outlive the test
+            p.kill()
+            p.join(5)
     assert r[0] != "error", r[1]
     glob, local, exp, ok, t, gathered, backend = r
     assert backend == "nccl"
