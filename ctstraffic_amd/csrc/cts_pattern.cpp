@@ -26,7 +26,6 @@
 #include <exception>
 #include <memory>
 #include <mutex>
-#include <cstdint>
 #include <deque>
 #include <new>
 #include <random>
@@ -478,15 +477,6 @@ struct cts_io_pattern {
         const long n = std::atol(v);
         return n < 1 ? 1u : (n > 4 ? 4u : (uint32_t)n);
     }();
-    // Launch lag in parts (CTS_DEFERRED_LAG, 0-2; default 0): a full part is launched only once `lag` more parts have
-    // been received behind it, so the GPU reads buffers at least that many completions after the socket wrote them
-    // (its reads of freshly written lines slow the receive path). Parts shrink to keep the bound.
-    uint32_t lag_env = [] {
-        const char* v = std::getenv("CTS_DEFERRED_LAG");
-        if (v == nullptr || *v == 0) return 0u;
-        const long n = std::atol(v);
-        return n < 0 ? 0u : (n > 2 ? 2u : (uint32_t)n);
-    }();
     // How Retire waits for the in-flight batch (CTS_DEFERRED_BLOCKING_SYNC): 0 = spin in hipStreamSynchronize,
     // 1 = hipEventSynchronize on a blocking-sync event, 2 (default) = sleep in 50 us steps between non-blocking
     // queries of the event. With 8 connections sharing the PCIe link, the first two burned ~2 ms of receive-thread
@@ -905,25 +895,13 @@ struct cts_io_pattern {
         return b < 3u ? 1u : std::min(depth_env, b - 1u);
     }
     uint32_t Sets() const { return Depth() + 1u; }  // descriptor / result sets: the filling batch + those in flight
-    // parts received behind a full part before it is launched (pipelined ring mode only; the parts must still hold a
-    // buffer each)
-    uint32_t Lag() const
-    {
-        if (!DoubleBuffered() || !queue_in_ring) return 0u;
-        const uint32_t b = BatchCapacity();
-        uint32_t l = lag_env;
-        while (l > 0 && Depth() + 1u + l > b) --l;
-        return l;
-    }
-    // queued completions at which Rotate launches the oldest part
-    uint32_t RotateAt() const { return LaunchAt() * (1u + Lag()); }
     // Completions queued before a batch goes to the device. Pipelined, each launch holds BatchCapacity() / Sets():
     // the oldest launch is retired at the latest when the filling one is full and Depth() are in flight, so every
     // verdict is known within BatchCapacity() completions of its own (fewer when a kernel is seen done earlier).
     uint32_t LaunchAt() const
     {
         const uint32_t b = BatchCapacity();
-        return DoubleBuffered() && queue_in_ring ? std::max(1u, b / (Sets() + Lag())) : b;
+        return DoubleBuffered() && queue_in_ring ? std::max(1u, b / Sets()) : b;
     }
 
     // The oldest in-flight batch's kernel has finished (a non-blocking event query; CompleteIo asks every 16th
@@ -1017,18 +995,17 @@ struct cts_io_pattern {
         return CTS_OK;
     }
 
-    int LaunchBatch(size_t count = SIZE_MAX)  // verifies the first `count` of `queue` (set desc_set), async
+    int LaunchBatch()  // verifies `queue` (descriptor set desc_set) on the pattern's stream, async
     {
         int rc = EnsureStream();
         if (rc != CTS_OK) return rc;
-        count = std::min(count, queue.size());
         uint32_t maxlen = 0;
-        for (size_t k = 0; k < count; ++k) maxlen = std::max(maxlen, queue[k].transferred);
+        for (const auto& q : queue) maxlen = std::max(maxlen, q.transferred);
         const uint8_t* arena = queue_in_ring ? recv_pinned.dev : stage.dev;
         const uint64_t bytes = queue_in_ring ? recv_pinned.bytes : stage.bytes;
         const size_t set = (size_t)desc_set * BatchCapacity();
         return cts_verify(engine, arena, bytes, reinterpret_cast<cts_buf_desc*>(stage_desc.dev) + set,
-                          (uint32_t)count, maxlen, reinterpret_cast<cts_verify_result*>(stage_res.dev) + set,
+                          (uint32_t)queue.size(), maxlen, reinterpret_cast<cts_verify_result*>(stage_res.dev) + set,
                           nullptr, nullptr, 0, stream);
     }
 
@@ -1129,10 +1106,7 @@ struct cts_io_pattern {
             if (has_failure && !had_failure) return GetCurrentStatus();  // an in-flight batch failed
         }
         if (queue.empty()) return GetCurrentStatus();
-        // the newest Lag() parts stay queued: they move to the next set and launch with the part after them
-        const size_t keep = std::min(queue.size() - 1u, (size_t)Lag() * LaunchAt());
-        const size_t n_launch = queue.size() - keep;
-        const int lr = LaunchBatch(n_launch);
+        const int lr = LaunchBatch();
         if (lr != CTS_OK) return lr;
         hipEvent_t e = nullptr;
         if (!spare_events.empty()) {
@@ -1147,22 +1121,13 @@ struct cts_io_pattern {
             return CTS_E_HIP;
         }
         flights.push_back(Flight{{}, e, desc_set});
-        std::vector<Queued>& launched = flights.back().q;
-        launched.swap(queue);
+        flights.back().q.swap(queue);
         if (!spare_queues.empty()) {
             queue.swap(spare_queues.back());
             spare_queues.pop_back();
         }
         queue.clear();
-        const uint32_t next = (desc_set + 1u) % Sets();
-        if (keep > 0) {
-            auto* base = reinterpret_cast<cts_buf_desc*>(stage_desc.host);
-            std::memcpy(base + (size_t)next * BatchCapacity(), base + (size_t)desc_set * BatchCapacity() + n_launch,
-                        keep * sizeof(cts_buf_desc));
-            queue.assign(launched.begin() + (std::ptrdiff_t)n_launch, launched.end());
-            launched.resize(n_launch);
-        }
-        desc_set = next;
+        desc_set = (desc_set + 1u) % Sets();
         return GetCurrentStatus();
     }
 
@@ -1344,7 +1309,7 @@ struct cts_io_pattern {
         if (defer_this) {
             const int rc = Enqueue(t, transfer, bytes_recv);
             if (rc < 0) return rc;
-            if (!benign || queue.size() >= RotateAt()) {
+            if (!benign || queue.size() >= LaunchAt()) {
                 const int fr = benign ? Rotate() : Flush();
                 if (fr < 0) return fr;
             }

@@ -5,7 +5,7 @@ one process. Each launch holds batch / (depth + 1) buffers, so
 same. One JSON line per leg and round: GB/s received, receive-thread CPU per GiB, and the verdict waits
 (cts_pattern_stats.verify_wait_ns summed over the receiving sides) per GiB.
 usage: python tools/deferred_depth_ab.py [rounds] [batch_buffers] [legs, e.g. off,1,2 or 2@512,2@1024]
-(a leg "d@b" runs depth d at batch b, "dLl" depth d with a launch lag of l parts; "ring" / "ringpinned" run verify off with every data recv landing round robin in
+(a leg "d@b" runs depth d at batch b; "ring" / "ringpinned" run verify off with every data recv landing round robin in
 a ring the size of a DEFERRED pattern's at that batch, 2 x batch + 2 buffers, pageable / pinned: the feeder's
 diagnostic recv ring)"""
 import json
@@ -36,16 +36,13 @@ def main():
                              recv_ring_buffers=slots, recv_ring_pinned=leg == "ringpinned")
                 wait = 0.0
             else:
-                spec, _, b = leg.partition("@")
-                depth, _, lag = spec.partition("L")  # "2L1": depth 2, launch lag 1 part (CTS_DEFERRED_LAG)
+                depth, _, b = leg.partition("@")
                 os.environ["CTS_DEFERRED_DEPTH"] = depth
-                os.environ["CTS_DEFERRED_LAG"] = lag or "0"
                 try:
                     res = LB.run(connections=8, buffer_size=65536, transfer_size=1 << 30, engine=eng,
                                  verify_mode=PA.VERIFY_DEFERRED, batch_buffers=int(b) if b else batch, sides=True)
                 finally:
                     os.environ.pop("CTS_DEFERRED_DEPTH", None)
-                    os.environ.pop("CTS_DEFERRED_LAG", None)
                 wait = sum(sd["verify_wait_ns"] for sd in res["sides"]) * 1e-9
             name = {"off": "verify_off", "ring": "verify_off_ring", "ringpinned": "verify_off_pinned_ring"}.get(
                 leg, "deferred_depth_" + leg)
