@@ -393,6 +393,21 @@ def test_loopback_diagnostic_recv_ring_cpu():
                      recv_ring_pinned=True)
 
 
+@pytest.mark.gpu
+def test_loopback_diagnostic_recv_ring_pinned_gpu(engine):
+    """The diagnostic recv ring in pinned host memory (cts_host_alloc on the engine, as a DEFERRED pattern's ring):
+    a verify-off run's counters and statuses are the plain run's."""
+    base = loopback.run(connections=4, buffer_size=65536, transfer_size=300 * 65536 + 77, verify=False,
+                        recv_whole=True, sides=True, engine=engine)
+    ring = loopback.run(connections=4, buffer_size=65536, transfer_size=300 * 65536 + 77, verify=False,
+                        recv_whole=True, sides=True, engine=engine, recv_ring_buffers=2 * 512 + 2,
+                        recv_ring_pinned=True)
+    for r in (base, ring):
+        assert r["connections_ok"] == 4 and r["data_errors"] == 0
+        assert r["bytes_recv"] == 4 * (300 * 65536 + 77 + 37 + 4)
+    assert [s["bytes_recv"] for s in ring["sides"]] == [s["bytes_recv"] for s in base["sides"]]
+
+
 def test_loopback_send_pacing_cpu():
     """Send pacing end to end: the feeder's senders wait each task's time offset (ctsSendRecvIocp.cpp:378-383).
     4 Push connections x 40 x 8 KiB at 1 MiB/s each (100 ms quanta of 104 857 B, 13 buffers) are deferred into
