@@ -470,7 +470,7 @@ struct cts_io_pattern {
     std::vector<std::vector<Queued>> spare_queues;  // their entry vectors (capacity kept across batches)
     // Batches in flight per connection (CTS_DEFERRED_DEPTH, 1-4; default 2). Each launch holds
     // BatchCapacity() / (Depth() + 1) buffers, so a verdict is still known within BatchCapacity() completions.
-    // Config 1 over loopback, three boxes, 28 alternated rounds: 2 beat 1 in 20.
+    // Config 1 over loopback, four boxes, 40 alternated rounds: 2 beat 1 in 29.
     uint32_t depth_env = [] {
         const char* v = std::getenv("CTS_DEFERRED_DEPTH");
         if (v == nullptr || *v == 0) return 2u;
