@@ -1,36 +1,30 @@
 # Build the MI355X engine (gfx950) and the CPU oracle.
-#   make            -> ctstraffic_amd/libcts_engine.so (the product: one kernel per path) + the tuning build
-#                      ctstraffic_amd/libcts_engine_tuning.so (every launch variant, for A/B runs and their
-#                      parity tests) + oracle/libcts_oracle.so + the C++ device sample
-#                      (ctstraffic_amd/build/device_verify) + the ceiling/ablation tools
+#   make            -> ctstraffic_amd/libcts_engine.so (the product: one kernel per path) + oracle/libcts_oracle.so +
+#                      the C++ device sample (ctstraffic_amd/build/device_verify) + what bench.py and the tests run
+#                      (tools/libcts_bench_multi.so, tools/pattern_cpu_probe)
+#   make probes     -> the measurement probes of tools/ (ceilings, timelines, ablations; built before an A/B call)
 #   make asm        -> ctstraffic_amd/build/cts_kernels-gfx950.s (disassembly for inspection)
 HIPCC     ?= /opt/rocm/bin/hipcc
 ARCH      ?= gfx950
 HIPFLAGS  ?= -O3 -std=c++17 -fPIC -Wall -Wno-unused-result --offload-arch=$(ARCH) -Iinclude -Ictstraffic_amd/csrc
 CSRC      := ctstraffic_amd/csrc
 ENGINE_SO := ctstraffic_amd/libcts_engine.so
-TUNING_SO := ctstraffic_amd/libcts_engine_tuning.so
 HDRS      := $(wildcard include/*.h) $(wildcard $(CSRC)/*.hpp)
 SRCS      := $(wildcard $(CSRC)/*.hip) $(wildcard $(CSRC)/*.cpp)
 OBJS      := $(patsubst $(CSRC)/%,ctstraffic_amd/build/%.o,$(SRCS))
-# the tuning build recompiles the two TUs that know about launch variants; the rest is shared
-TUNED     := $(CSRC)/cts_kernels.hip $(CSRC)/cts_engine.cpp
-TUNING_OBJS := $(patsubst $(CSRC)/%,ctstraffic_amd/build/tuning/%.o,$(TUNED)) \
-               $(filter-out $(patsubst $(CSRC)/%,ctstraffic_amd/build/%.o,$(TUNED)),$(OBJS))
-# -Bsymbolic: calls between the library's own cts_* entry points bind inside it, so the product and the
-# tuning library can be loaded into one process side by side
+# -Bsymbolic: calls between the library's own cts_* entry points bind inside it (an A/B build of the same ABI can
+# be loaded beside it)
 SOFLAGS   := -shared -Wl,-Bsymbolic -Wl,--version-script=$(CSRC)/exports.map
 
 DEVICE_VERIFY := ctstraffic_amd/build/device_verify
-TOOLS := tools/hbm_read_ceiling tools/verify_ablation tools/mailbox_probe tools/rw_mix_probe tools/write_shape_probe tools/fill_bisect tools/fill_abi_probe tools/mailbox_bisect tools/ring_fill_probe \
-         tools/verify_timeline tools/verify_timeline_kp
-
-SYNC_PROBE := tools/sync_probe tools/pattern_cpu_probe tools/deferred_ab
+PROBES := tools/hbm_read_ceiling tools/verify_ablation tools/mailbox_probe tools/rw_mix_probe tools/write_shape_probe \
+          tools/fill_bisect tools/fill_abi_probe tools/mailbox_bisect tools/ring_fill_probe tools/verify_timeline \
+          tools/verify_timeline_kp tools/sync_probe tools/deferred_ab
 BENCH_MULTI := tools/libcts_bench_multi.so
 
-all: $(ENGINE_SO) $(TUNING_SO) oracle $(DEVICE_VERIFY) $(TOOLS) $(SYNC_PROBE) $(BENCH_MULTI)
+all: $(ENGINE_SO) oracle $(DEVICE_VERIFY) $(BENCH_MULTI) tools/pattern_cpu_probe
 
-tuning: $(TUNING_SO)
+probes: $(PROBES)
 
 # bench.py's single-process leg (--engines N): the timed launches from one native thread per GPU
 $(BENCH_MULTI): tools/bench_multi.cpp $(ENGINE_SO) include/cts_engine.h
@@ -86,21 +80,14 @@ $(DEVICE_VERIFY): tests/cpp/device_verify.cpp $(ENGINE_SO) include/cts_engine.h
 # tools/verify_timeline vs verify_timeline_kp alternated on one box, profiles/r04/b/); firmware without the feature
 # runs the compiler's fallback prologue, which loads them as before
 KERNARG_PRELOAD := -mllvm -amdgpu-kernarg-preload-count=16
-ctstraffic_amd/build/cts_kernels.hip.o ctstraffic_amd/build/tuning/cts_kernels.hip.o: HIPFLAGS += $(KERNARG_PRELOAD)
+ctstraffic_amd/build/cts_kernels.hip.o: HIPFLAGS += $(KERNARG_PRELOAD)
 
 ctstraffic_amd/build/%.o: $(CSRC)/% $(HDRS)
 	@mkdir -p ctstraffic_amd/build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-ctstraffic_amd/build/tuning/%.o: $(CSRC)/% $(HDRS)
-	@mkdir -p ctstraffic_amd/build/tuning
-	$(HIPCC) $(HIPFLAGS) -DCTS_TUNING=1 -c $< -o $@
-
 $(ENGINE_SO): $(OBJS) $(CSRC)/exports.map
 	$(HIPCC) $(HIPFLAGS) $(SOFLAGS) -o $@ $(OBJS) -Wl,-soname,libcts_engine.so
-
-$(TUNING_SO): $(TUNING_OBJS) $(CSRC)/exports.map
-	$(HIPCC) $(HIPFLAGS) $(SOFLAGS) -o $@ $(TUNING_OBJS) -Wl,-soname,libcts_engine_tuning.so
 
 oracle:
 	$(MAKE) -s -C oracle
@@ -110,7 +97,7 @@ asm: $(CSRC)/cts_kernels.hip $(HDRS)
 	$(HIPCC) $(HIPFLAGS) $(KERNARG_PRELOAD) --cuda-device-only -S $< -o ctstraffic_amd/build/cts_kernels-$(ARCH).s
 
 clean:
-	rm -rf ctstraffic_amd/build $(ENGINE_SO) $(TUNING_SO) $(TOOLS) $(SYNC_PROBE)
+	rm -rf ctstraffic_amd/build $(ENGINE_SO) $(PROBES) $(BENCH_MULTI) tools/pattern_cpu_probe
 	$(MAKE) -s -C oracle clean
 
-.PHONY: all tuning oracle asm clean
+.PHONY: all probes oracle asm clean

@@ -87,8 +87,6 @@ def parse():
                    help="pin the process to the GPU's NUMA node (cts_engine_numa_node): tools/sync_probe's SYNC "
                         "verifies answer faster there, but whole loopback runs were not faster "
                         "(profiles/r02/numa/); the device-resident legs do not care")
-    p.add_argument("--verify-variant", type=int, default=-1,
-                   help="CTS_ATTR_VERIFY_VARIANT for both legs (-1 = engine default; tuning builds only)")
     p.add_argument("--no-engines-leg", action="store_true",
                    help="skip the single-process leg (--engines N as a child process) in the line's extras")
     p.add_argument("--stub-gpu", action="store_true",
@@ -149,6 +147,31 @@ def launch_ranks(args):
     return subprocess.call(cmd, env=env)
 
 
+def rank_diagnostics(rows) -> dict:
+    """The per-rank rows of gather_rank_rows([avg_kernel_us, engine device, torch device, placement ok, local rank])
+    as the line's keys: one slow GPU or one misplaced rank in the driver's N-GPU run then shows by name."""
+    return {"per_rank_avg_kernel_us": [round(r[0], 2) for r in rows],
+            "per_rank_device": [int(r[1]) for r in rows],
+            "per_rank_torch_device": [int(r[2]) for r in rows],
+            "per_rank_local_rank": [int(r[4]) for r in rows],
+            "placement_ok": all(r[3] == 1.0 for r in rows)}
+
+
+def check_placement(torch, engine, B, gpu, local):
+    """Before the timed region: this rank's engine, its current torch device and every buffer it launches over (arenas,
+    descriptors, records, first-failure slots, counter block) sit on GPU `gpu` = LOCAL_RANK mod the visible GPUs.
+    Raises otherwise (torch.distributed.run then stops the other ranks)."""
+    where = {("arena", t.device.index) for t in B.arenas} | {("results", t.device.index) for t in B.results} | \
+            {("first_fail", t.device.index) for t in B.cff} | {("descs", B.descs.device.index),
+                                                              ("counters", B.counters.device.index)}
+    bad = sorted(x for x in where if x[1] != gpu)
+    eng_dev, cur = engine.device_ordinal(), torch.cuda.current_device()
+    if bad or eng_dev != gpu or cur != gpu or gpu != local % torch.cuda.device_count():
+        raise RuntimeError("bench.py: rank placement (LOCAL_RANK %d, GPU %d): engine on %d, torch current device %d, "
+                           "buffers off the GPU: %s" % (local, gpu, eng_dev, cur, bad))
+    return eng_dev, cur
+
+
 def stub_main(args):
     """--stub-gpu: the launcher's CPU test. Each rank joins a gloo group from the torch.distributed.run
     environment and reports (RANK, WORLD_SIZE, LOCAL_RANK); rank 0 prints one line shaped like the real one."""
@@ -171,9 +194,13 @@ def stub_main(args):
         dist.all_gather(seen, me)
     else:
         seen = [me]
+    # the per-rank diagnostics of the real line, with stand-in values (kernel time 40 + rank, device = LOCAL_RANK)
+    diag = rank_diagnostics(D.gather_rank_rows([40.0 + rank, local, local, 1, local]))
     if rank == 0:
         print(json.dumps({"metric": METRIC, "value": 0.0, "unit": "GiB/s", "n_gpus": world, "stub": True,
-                          "ranks": [[int(x) for x in t.tolist()] for t in seen]}), flush=True)
+                          "ranks": [[int(x) for x in t.tolist()] for t in seen],
+                          "roofline": {k: v for k, v in diag.items() if k == "per_rank_avg_kernel_us"},
+                          **{k: v for k, v in diag.items() if k != "per_rank_avg_kernel_us"}}), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
@@ -293,10 +320,7 @@ def main():
             # the waiting ranks hold no spinning collective kernel on their GPUs
             cpu_group = D.new_cpu_group(timeout_s=args.dist_timeout)
 
-    # --verify-variant: A/B runs use the tuning build (every launch variant); the product runs variant 25
-    engine = Engine(gpu, tuning=args.verify_variant >= 0)
-    if args.verify_variant >= 0:
-        engine.set_attr(_lib.ATTR_VERIFY_VARIANT, args.verify_variant)
+    engine = Engine(gpu)
     near = engine.cpus_near() if args.pin_numa else []
     if near:  # threads started from here on (loopback sides, the mailbox watchdog) inherit it
         os.sched_setaffinity(0, near)
@@ -437,6 +461,7 @@ def main():
         ser_ok = engine.read_counters(counters) == {k: v * launches for k, v in exp_ctr.items()}
         serial_graph = sg is not None
 
+    eng_dev, torch_dev = check_placement(torch, engine, B, gpu, local)
     engine.reset_counters(counters, stream=stream)
     for c in B.cff:
         c.fill_(-1)
@@ -529,6 +554,8 @@ def main():
 
     traffic, traffic_src = pmc_traffic(w.name, args.buffers)
     kernel = verify_kernel_name(engine)
+    # every rank's serialized-leg kernel time and placement, beside per_rank_GiBps
+    diag = rank_diagnostics(D.gather_rank_rows([avg_kernel_s * 1e6, eng_dev, torch_dev, 1, local], group=cpu_group))
 
     if rank == 0:
         line = {
@@ -575,6 +602,7 @@ def main():
                 "traffic_source": traffic_src,
                 "kernel": kernel,
                 "avg_kernel_us": round(avg_kernel_s * 1e6, 2),
+                "per_rank_avg_kernel_us": diag["per_rank_avg_kernel_us"],
                 "timing": ("HIP events on the launch stream around the K*R timed launches (%s), / (K*R)"
                            % ("HIP-graph replays" if graph is not None else "host launches")) if not pipe else
                           ("separate serialized leg of K*R launches on one stream (%s), HIP events around them, "
@@ -599,6 +627,7 @@ def main():
                        "counters": local_ctr},
         }
         line["per_rank_GiBps"] = [round(x, 1) for x in per_rank]
+        line.update({k: v for k, v in diag.items() if k != "per_rank_avg_kernel_us"})
         if allreduce_us is not None:
             line["allreduce_counters_us"] = round(allreduce_us, 1)
         if extras:
@@ -647,6 +676,16 @@ def _bench_work(B, engine, device, streams):
     return w, (arena, res, cff, st)
 
 
+def _median_us(fn, reps: int) -> float:
+    """Median wall time of fn() in microseconds over reps calls (host-synchronous calls)."""
+    ts = []
+    for _ in range(reps):
+        t = time.perf_counter()
+        fn()
+        ts.append((time.perf_counter() - t) * 1e6)
+    return float(np.median(ts))
+
+
 def main_engines(args, torch):
     """The ctsTraffic process model on a node: ONE process, one engine per GPU (cts_engine_create(g)), one native
     host thread and stream set per GPU (tools/bench_multi.cpp: the launches go through the C ABI from std::threads,
@@ -656,7 +695,7 @@ def main_engines(args, torch):
     value = all bytes / (wall from the common start to the last GPU's end).
     --engines-same-gpu puts every engine on GPU 0 (a rehearsal of the code path on a one-GPU box)."""
     from ctstraffic_amd import Engine, workload as W
-    from ctstraffic_amd.engine import counters_read_multi
+    from ctstraffic_amd.engine import counters_allreduce, counters_allreduce_release, counters_read_multi
 
     G = args.engines
     same = args.engines_same_gpu
@@ -678,6 +717,7 @@ def main_engines(args, torch):
         e = Engine(dev)
         mine = conns[owner == g]
         B = Batch(torch, e, W, "cuda:%d" % dev, len(mine), R, conn_ids=mine)
+        check_placement(torch, e, B, dev, dev)  # engine g, its buffers and outputs on GPU g (0 in the rehearsal)
         streams = [e.stream_create() for _ in range(S)]
         ctx.append((e, B, streams, len(mine)))
         work[g], k = _bench_work(B, e, dev, streams)
@@ -699,8 +739,21 @@ def main_engines(args, torch):
     run(K)
     elapsed = max(t1) - min(min(t0), ts.value)
     per_gpu = [ctx[g][1].bytes_per_launch * R * K / (t1[g] - t0[g]) / GIB for g in range(G)]
-    folded = counters_read_multi([c[0] for c in ctx], [c[1].counters for c in ctx])
+    engs, blocks = [c[0] for c in ctx], [c[1].counters for c in ctx]
+    folded = counters_read_multi(engs, blocks)
     per = [c[0].read_counters(c[1].counters) for c in ctx]
+    # after the timed region: the node-wide counters both ways, the host fold and the RCCL all-reduce issued from
+    # the C ABI (cts_counters_allreduce: per-device fold + ncclAllReduce sum u64 x 5 per device), each timed
+    reduced, red = None, {}
+    fold_us = _median_us(lambda: counters_read_multi(engs, blocks), 20)
+    try:
+        t = time.perf_counter()
+        reduced = counters_allreduce(engs, blocks)  # the first call creates the communicators
+        red["allreduce_first_call_ms"] = round((time.perf_counter() - t) * 1e3, 2)
+        red["allreduce_counters_us"] = round(_median_us(lambda: counters_allreduce(engs, blocks), 20), 1)
+        counters_allreduce_release()
+    except Exception as ex:  # reported, not fatal: the verify leg above is the measurement
+        red["allreduce_error"] = repr(ex)
     total = sum(c[1].bytes_per_launch for c in ctx) * R * K
     exp = {k: sum(c[1].exp_ctr[k] for c in ctx) * K * R for k in ctx[0][1].exp_ctr}
     line = {
@@ -716,7 +769,10 @@ def main_engines(args, torch):
         "per_gpu_GiBps": [round(x, 1) for x in per_gpu],
         "parity": {"folded_counters_match_expected": folded == exp,
                    "fold_equals_sum_of_reads": folded == {k: sum(p[k] for p in per) for k in exp},
-                   "records_and_first_fail_match": all(c[1].outputs_ok() for c in ctx), "counters": folded},
+                   "records_and_first_fail_match": all(c[1].outputs_ok() for c in ctx), "counters": folded,
+                   "allreduce_equals_fold": reduced == folded},
+        "node_counters": {"fold_counters_us": round(fold_us, 1), **red,
+                          "devices": [c[0].device_ordinal() for c in ctx]},
     }
     print(json.dumps(line), flush=True)
     for e, B, streams, _ in ctx:
@@ -740,10 +796,10 @@ def _time_kernel(torch, fn, steps):
 
 
 def verify_kernel_name(engine):
-    """Name of the large-buffer verify kernel the engine launches (as rocprofv3 reports it)."""
+    """The large-buffer verify kernel the engine launches, demangled as rocprofv3 reports it."""
     from ctstraffic_amd import _lib
 
-    return _lib.verify_kernel_name(engine.get_attr(_lib.ATTR_VERIFY_VARIANT))
+    return _lib.verify_kernel_name(bool(engine.get_attr(_lib.ATTR_NT_LOADS)))
 
 
 def pmc_traffic(workload, buffers):

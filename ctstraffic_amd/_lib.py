@@ -24,15 +24,13 @@ except Exception:  # pragma: no cover - torch is part of the image
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # CTS_ENGINE_LIB: an alternative in-tree build of the same library (tools/ A/B runs)
 LIB_PATH = os.environ.get("CTS_ENGINE_LIB") or os.path.join(_HERE, "libcts_engine.so")
-# the tuning build: the same C ABI compiled with every launch variant (CTS_TUNING=1, `make tuning`); only
-# the variant parity tests and the tools/ A/B runs load it, next to the product library
-TUNING_LIB_PATH = os.path.join(_HERE, "libcts_engine_tuning.so")
 
 CTS_OK = 0
 CTS_E_INVALID = -1
 CTS_E_HIP = -2
 CTS_E_NOMEM = -3
 CTS_E_NO_DEVICE = -4
+CTS_E_UNAVAILABLE = -5
 
 PATTERN_PERIOD = 65536
 UDP_DATA_HEADER_LENGTH = 26
@@ -51,29 +49,14 @@ ATTR_FILL_NT = 10
 ATTR_SYNC_MAILBOX = 11
 
 
-# large-buffer verify kernels by CTS_ATTR_VERIFY_VARIANT, as rocprofv3 names them (25 = the product default; the
-# others exist only in the tuning build, libcts_engine_tuning.so)
-VERIFY_KERNELS = {0: "cts::verify_wg_kernel<8,true>", 1: "cts::verify_wg_kernel<4,true>",
-                  2: "cts::verify_wg_kernel<16,true>", 3: "cts::verify_wave_kernel<8,true>",
-                  4: "cts::verify_wg_nb_kernel<8,true>", 5: "cts::verify_wg_nb_kernel<4,true>",
-                  6: "cts::verify_wg_kernel<8,true,true>", 7: "cts::verify_wg_kernel<4,true,true>",
-                  8: "cts::verify_wg_kernel<8,true,true,true>", 9: "cts::verify_wg_kernel<8,true,true,false,true>",
-                  10: "cts::verify_wg_kernel<4,true,true,false,true>",
-                  11: "cts::verify_wg_kernel<4,true,true,false,true,true>",
-                  12: "cts::verify_wg_kernel<8,true,true,false,true,true>",
-                  13: "cts::verify_wg_kernel<2,true,true,false,true,true>",
-                  14: "cts::verify_wg_kernel<1,true,true,false,true,true>",
-                  22: "cts::verify_wg_kernel<2,true,true,false,true,true,1,0,0,256,true>",
-                  23: "cts::verify_wg_kernel<2,true,true,false,true,true,1,0,0,256,false,true>",
-                  24: "cts::verify_wg_kernel<2,true,true,false,true,true,1,0,0,256,true,true>",
-                  25: "cts::verify_wg_kernel<2,true,true,false,true,true,1,0,0,256,false,false,4,false,false>",
-                  26: "cts::verify_wg_kernel<4,true,true,false,true,true,1,0,0,256,false,false,4,false,false>",
-                  27: "cts::verify_wg_kernel<2,true,true,false,true,true,1,0,0,256,false,false,4,true,false>",
-                  28: "cts::verify_wg_kernel<2,true,true,false,true,true,1,0,0,256,false,false,4,false,true>"}
+# the large-buffer verify kernel (CTS_ATTR_VERIFY_VARIANT reports its id, 25), demangled as rocprofv3 prints it;
+# the nontemporal-load form is the default (CTS_ATTR_NT_LOADS)
+VERIFY_KERNEL_ID = 25
 
 
-def verify_kernel_name(variant: int) -> str:
-    return VERIFY_KERNELS.get(variant, "variant %d" % variant)
+def verify_kernel_name(nontemporal: bool = True) -> str:
+    return ("void cts::verify_wg_kernel<%s>(unsigned char const*, unsigned long, cts_buf_desc const*, unsigned int, "
+            "cts_verify_result*, unsigned long*, unsigned int*, unsigned int)" % ("true" if nontemporal else "false"))
 
 
 class CtsError(RuntimeError):
@@ -109,7 +92,6 @@ class CtsVerifyResult(ctypes.Structure):
 assert ctypes.sizeof(CtsVerifyResult) == 12
 
 _lib = None
-_tuning_lib = None
 
 
 def _status_string(status: int) -> str:
@@ -141,6 +123,9 @@ def _declare(L: ctypes.CDLL) -> None:
         "cts_counters_read": ([P, P, ctypes.POINTER(CtsCounters), P], i32),
         "cts_counters_read_multi": ([ctypes.POINTER(P), ctypes.POINTER(P), ctypes.POINTER(P), u32,
                                      ctypes.POINTER(CtsCounters)], i32),
+        "cts_counters_allreduce": ([ctypes.POINTER(P), ctypes.POINTER(P), ctypes.POINTER(P), u32,
+                                    ctypes.POINTER(CtsCounters)], i32),
+        "cts_counters_allreduce_release": ([], i32),
         "cts_verify_host": ([P, P, u32, u32, ctypes.POINTER(CtsVerifyResult)], i32),
         "cts_verify_mapped": ([P, P, u32, u32, ctypes.POINTER(CtsVerifyResult)], i32),
         "cts_mailbox_launches": ([P], u64),
@@ -178,20 +163,6 @@ def lib() -> ctypes.CDLL:
         _declare(L)
         _lib = L
     return _lib
-
-
-def tuning_lib() -> ctypes.CDLL:
-    """Load the tuning build of the engine (every launch variant). Linked with -Bsymbolic, so it keeps its own
-    entry points even with the product library loaded globally."""
-    global _tuning_lib
-    if _tuning_lib is None:
-        lib()  # the product library first: torch's HIP runtime, then ours
-        if not os.path.exists(TUNING_LIB_PATH):
-            raise ImportError("ctstraffic_amd: %s not built — run `make tuning`" % TUNING_LIB_PATH)
-        L = ctypes.CDLL(TUNING_LIB_PATH, mode=ctypes.RTLD_LOCAL)
-        _declare(L)
-        _tuning_lib = L
-    return _tuning_lib
 
 
 def check(fn: str, status: int) -> None:

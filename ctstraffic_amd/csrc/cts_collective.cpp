@@ -1,0 +1,230 @@
+// cts_collective.cpp — cts_counters_allreduce (include/cts_engine.h): the node-wide ctsStatsTracking counters
+// (ctsStatistics.hpp:87-198) of ONE process that drives one engine per GPU, reduced over RCCL on the GPUs.
+//
+// ctsTraffic is one process per host with many IO threads; its byte/error statistics are process-global atomics
+// (ctsStatistics.hpp:87-198, read by ctsConfig::TcpStatusDetails, ctsConfig.h:415-417). With the verify on N GPUs
+// each engine's counters live in its own device block. This entry point folds every block on its own device (one
+// 64-thread launch, counters_fold_kernel), reduces the five sums across the devices with one ncclAllReduce (sum,
+// ncclUint64, count 5) per device inside ncclGroupStart/End over the xGMI links, and
+// reads the result back. Every device's copy is read and compared: a reduction that disagrees is an error.
+//
+// RCCL is loaded on first use (dlopen of librccl.so.1, or $CTS_RCCL_LIBRARY), so the engine library itself does
+// not pull the 570 MB RCCL image into every process that only verifies; inside a PyTorch process the soname
+// resolves to the RCCL torch already loaded. One communicator clique (ncclCommInitAll) is kept per set of
+// devices and reused until cts_counters_allreduce_release. Calls are serialised by one lock (a counter read
+// happens once per status interval, not per IO).
+#include <dlfcn.h>
+#include <hip/hip_runtime_api.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "cts_engine.h"
+#include "cts_internal.hpp"
+
+namespace {
+
+struct Rccl {
+    void* handle = nullptr;
+    ncclResult_t (*comm_init_all)(ncclComm_t*, int, const int*) = nullptr;
+    ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*all_reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
+                               hipStream_t) = nullptr;
+    ncclResult_t (*group_start)() = nullptr;
+    ncclResult_t (*group_end)() = nullptr;
+};
+
+// One communicator per device of a device set, plus a 5 x u64 device slot each (the fold's output and the
+// all-reduce's in-place buffer).
+struct Clique {
+    std::vector<int> devices;
+    std::vector<ncclComm_t> comms;
+    std::vector<uint64_t*> sums;
+};
+
+std::mutex g_mu;  // guards everything below
+Rccl g_rccl;
+std::vector<std::unique_ptr<Clique>> g_cliques;
+
+struct DeviceGuard {
+    int prev = -1;
+    bool ok = false;
+    explicit DeviceGuard(int dev)
+    {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        ok = (prev == dev) || (hipSetDevice(dev) == hipSuccess);
+    }
+    ~DeviceGuard()
+    {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+// Resolves the RCCL entry points once; a failed load is retried on the next call.
+bool load_rccl()
+{
+    if (g_rccl.handle != nullptr) return true;
+    const char* env = std::getenv("CTS_RCCL_LIBRARY");
+    void* h = nullptr;
+    if (env != nullptr && *env != 0) {
+        h = dlopen(env, RTLD_NOW | RTLD_LOCAL);
+    } else {
+        h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (h == nullptr) h = dlopen("librccl.so", RTLD_NOW | RTLD_LOCAL);
+    }
+    if (h == nullptr) return false;
+    Rccl r;
+    r.handle = h;
+    r.comm_init_all = reinterpret_cast<decltype(r.comm_init_all)>(dlsym(h, "ncclCommInitAll"));
+    r.comm_destroy = reinterpret_cast<decltype(r.comm_destroy)>(dlsym(h, "ncclCommDestroy"));
+    r.all_reduce = reinterpret_cast<decltype(r.all_reduce)>(dlsym(h, "ncclAllReduce"));
+    r.group_start = reinterpret_cast<decltype(r.group_start)>(dlsym(h, "ncclGroupStart"));
+    r.group_end = reinterpret_cast<decltype(r.group_end)>(dlsym(h, "ncclGroupEnd"));
+    if (!r.comm_init_all || !r.comm_destroy || !r.all_reduce || !r.group_start || !r.group_end) {
+        dlclose(h);
+        return false;
+    }
+    g_rccl = r;
+    return true;
+}
+
+void destroy_clique(Clique& c)
+{
+    for (size_t k = 0; k < c.comms.size(); ++k) {
+        if (c.comms[k] != nullptr) (void)g_rccl.comm_destroy(c.comms[k]);
+        if (c.sums[k] != nullptr) {
+            DeviceGuard g(c.devices[k]);
+            (void)hipFree(c.sums[k]);
+        }
+    }
+    c.comms.clear();
+    c.sums.clear();
+}
+
+// The clique of exactly these devices (in this order), created on first use.
+int clique_for(const std::vector<int>& devices, Clique** out)
+{
+    for (auto& c : g_cliques)
+        if (c->devices == devices) {
+            *out = c.get();
+            return CTS_OK;
+        }
+    std::unique_ptr<Clique> c(new (std::nothrow) Clique());
+    if (!c) return CTS_E_NOMEM;
+    c->devices = devices;
+    c->comms.assign(devices.size(), nullptr);
+    c->sums.assign(devices.size(), nullptr);
+    for (size_t k = 0; k < devices.size(); ++k) {
+        DeviceGuard g(devices[k]);
+        void* p = nullptr;
+        if (!g.ok || hipMalloc(&p, 5 * sizeof(uint64_t)) != hipSuccess) {
+            destroy_clique(*c);
+            return g.ok ? CTS_E_NOMEM : CTS_E_HIP;
+        }
+        c->sums[k] = static_cast<uint64_t*>(p);
+    }
+    int prev = -1;
+    (void)hipGetDevice(&prev);
+    const ncclResult_t r = g_rccl.comm_init_all(c->comms.data(), (int)devices.size(), devices.data());
+    if (prev >= 0) (void)hipSetDevice(prev);
+    if (r != ncclSuccess) {
+        std::fill(c->comms.begin(), c->comms.end(), nullptr);
+        destroy_clique(*c);
+        return CTS_E_HIP;
+    }
+    *out = c.get();
+    g_cliques.push_back(std::move(c));
+    return CTS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int cts_counters_allreduce(cts_engine* const* engines, const void* const* dev_counters, void* const* streams,
+                           uint32_t n, cts_counters* out)
+{
+    if (out == nullptr || (n > 0 && (engines == nullptr || dev_counters == nullptr))) return CTS_E_INVALID;
+    if (n == 0) {
+        *out = cts_counters{0, 0, 0, 0, 0};
+        return CTS_OK;
+    }
+    // engines grouped by device: the first engine of a device leads (its stream carries the device's folds and
+    // its all-reduce); the others' blocks are folded into the same slot
+    std::vector<int> dev_of(n);
+    std::vector<int> devices;
+    std::vector<uint32_t> leader;  // per device: index of its first engine
+    for (uint32_t i = 0; i < n; ++i) {
+        if (engines[i] == nullptr || dev_counters[i] == nullptr) return CTS_E_INVALID;
+        const int d = cts_engine_device(engines[i]);
+        if (d < 0) return CTS_E_INVALID;
+        dev_of[i] = d;
+        if (std::find(devices.begin(), devices.end(), d) == devices.end()) {
+            devices.push_back(d);
+            leader.push_back(i);
+        }
+    }
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!load_rccl()) return CTS_E_UNAVAILABLE;
+    Clique* c = nullptr;
+    int rc = clique_for(devices, &c);
+    if (rc != CTS_OK) return rc;
+    const size_t D = devices.size();
+    std::vector<hipStream_t> lead_stream(D);
+    for (size_t k = 0; k < D; ++k) lead_stream[k] = streams ? static_cast<hipStream_t>(streams[leader[k]]) : nullptr;
+    // 1. fold every engine's shard block into its device's slot, on the device's leading stream
+    for (size_t k = 0; k < D; ++k) {
+        DeviceGuard g(devices[k]);
+        if (!g.ok) return CTS_E_HIP;
+        bool first = true;
+        for (uint32_t i = 0; i < n; ++i) {
+            if (dev_of[i] != devices[k]) continue;
+            const hipStream_t s = streams ? static_cast<hipStream_t>(streams[i]) : nullptr;
+            // another stream's verifies must be complete before the leading stream reads this block
+            if (s != lead_stream[k] && hipStreamSynchronize(s) != hipSuccess) return CTS_E_HIP;
+            if (cts::launch_counters_fold(dev_counters[i], c->sums[k], !first, lead_stream[k]) != hipSuccess)
+                return CTS_E_HIP;
+            first = false;
+        }
+    }
+    // 2. one all-reduce per device, grouped (one thread drives every rank of the clique)
+    if (g_rccl.group_start() != ncclSuccess) return CTS_E_HIP;
+    ncclResult_t r = ncclSuccess;
+    for (size_t k = 0; k < D && r == ncclSuccess; ++k)
+        r = g_rccl.all_reduce(c->sums[k], c->sums[k], 5, ncclUint64, ncclSum, c->comms[k], lead_stream[k]);
+    const ncclResult_t re = g_rccl.group_end();
+    if (r != ncclSuccess || re != ncclSuccess) return CTS_E_HIP;
+    // 3. every device's copy back; they must agree
+    uint64_t first_copy[5] = {0, 0, 0, 0, 0};
+    for (size_t k = 0; k < D; ++k) {
+        DeviceGuard g(devices[k]);
+        uint64_t h[5];
+        if (!g.ok || hipMemcpyAsync(h, c->sums[k], sizeof(h), hipMemcpyDeviceToHost, lead_stream[k]) != hipSuccess ||
+            hipStreamSynchronize(lead_stream[k]) != hipSuccess)
+            return CTS_E_HIP;
+        if (k == 0) std::memcpy(first_copy, h, sizeof(h));
+        else if (std::memcmp(first_copy, h, sizeof(h)) != 0) return CTS_E_HIP;
+    }
+    out->bytes_checked = first_copy[cts::kBytesChecked];
+    out->bytes_ok = first_copy[cts::kBytesOk];
+    out->buffers_checked = first_copy[cts::kBuffersChecked];
+    out->buffers_failed = first_copy[cts::kBuffersFailed];
+    out->mismatched_bytes = first_copy[cts::kMismatchedBytes];
+    return CTS_OK;
+}
+
+int cts_counters_allreduce_release(void)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    for (auto& c : g_cliques) destroy_clique(*c);
+    g_cliques.clear();
+    return CTS_OK;
+}
+
+}  // extern "C"

@@ -158,7 +158,6 @@ struct Mailbox {
     int idle_ms = 50;
     double timeout_s = 2.0;              // CTS_MAILBOX_TIMEOUT_MS
     uint64_t delay_ticks = 0;            // CTS_MAILBOX_DELAY_MS (test hook: a late poller in the first launch)
-    int polls = 1;                       // CTS_MAILBOX_POLLS: slot reads each poller keeps in flight (1 or 2)
     cts::MailSlot* slots = nullptr;      // host view (coherent, pinned)
     cts::MailSlot* dslots = nullptr;     // device view
     cts::MailPart* parts = nullptr;      // nslots x kMailGroup part records, host view (coherent, pinned)
@@ -209,7 +208,6 @@ struct Mailbox {
         idle_ticks = (uint64_t)exit_ms * 100000ull;
         timeout_s = std::max(1, env_int("CTS_MAILBOX_TIMEOUT_MS", (int)(timeout_s * 1000))) / 1000.0;
         delay_ticks = (uint64_t)std::max(0, env_int("CTS_MAILBOX_DELAY_MS", 0)) * 100000ull;
-        polls = env_int("CTS_MAILBOX_POLLS", polls) == 2 ? 2 : 1;
         DeviceGuard g(e->device);
         if (!g.ok) return CTS_E_HIP;
         void* p = nullptr;
@@ -273,7 +271,7 @@ struct Mailbox {
         cts::MailStarts starts{};
         for (uint32_t i = 0; i < groups; ++i) starts.j[i] = next[i];
         const uint64_t delay = launches.load(std::memory_order_relaxed) == 0 ? delay_ticks : 0;
-        if (cts::launch_mailbox(dslots, dparts, per_group, starts, groups, idle_ticks, stream, delay, polls) != hipSuccess ||
+        if (cts::launch_mailbox(dslots, dparts, per_group, starts, groups, idle_ticks, stream, delay) != hipSuccess ||
             hipEventRecord(grid_done, stream) != hipSuccess)
             return CTS_E_HIP;
         running = true;
@@ -490,13 +488,7 @@ int mailbox_of(cts_engine* e, Mailbox** out)
 
 extern "C" {
 
-#if CTS_TUNING
-#define cts_variant_count(k) cts::k
-const char* cts_version(void) { return "ctstraffic_amd 0.2.0 (gfx950, tuning build: every launch variant)"; }
-#else
-#define cts_variant_count(k) 0
-const char* cts_version(void) { return "ctstraffic_amd 0.2.0 (gfx950)"; }
-#endif
+const char* cts_version(void) { return "ctstraffic_amd 0.3.0 (gfx950)"; }
 
 const char* cts_status_string(int status)
 {
@@ -506,6 +498,7 @@ const char* cts_status_string(int status)
     case CTS_E_HIP: return "HIP runtime error";
     case CTS_E_NOMEM: return "out of memory";
     case CTS_E_NO_DEVICE: return "no such HIP device";
+    case CTS_E_UNAVAILABLE: return "runtime library unavailable (RCCL)";
     default: return "unknown status";
     }
 }
@@ -528,22 +521,11 @@ int cts_engine_create(int device, cts_engine** out)
     e->geo.blocks_per_cu = env_int("CTS_BLOCKS_PER_CU", e->geo.blocks_per_cu);
     e->geo.nontemporal = env_int("CTS_NT_LOADS", e->geo.nontemporal);
     e->geo.small_threshold = env_int("CTS_SMALL_THRESHOLD", e->geo.small_threshold);
-    e->geo.verify_variant = env_int("CTS_VERIFY_VARIANT", e->geo.verify_variant);
     e->geo.small_blocks_per_cu = env_int("CTS_SMALL_BLOCKS_PER_CU", e->geo.small_blocks_per_cu);
-    e->geo.small_variant = env_int("CTS_SMALL_VARIANT", e->geo.small_variant);
     e->geo.fill_blocks_per_cu = env_int("CTS_FILL_BLOCKS_PER_CU", e->geo.fill_blocks_per_cu);
-    e->geo.ms_variant = env_int("CTS_MS_VARIANT", e->geo.ms_variant);
     e->geo.small_chunk = env_int("CTS_SMALL_CHUNK", e->geo.small_chunk);
     e->geo.fill_nt = env_int("CTS_FILL_NT", e->geo.fill_nt);
     e->geo.ring_fill_blocks_per_cu = env_int("CTS_RING_FILL_BLOCKS_PER_CU", e->geo.ring_fill_blocks_per_cu);
-    e->geo.fill_batched = env_int("CTS_FILL_BATCHED", e->geo.fill_batched);
-    // a variant this build does not compile falls back to the default (the product build has one per path)
-    if (!cts::variant_ok(e->geo.verify_variant, cts::kDefaultVerifyVariant, cts_variant_count(kVerifyVariants)))
-        e->geo.verify_variant = cts::kDefaultVerifyVariant;
-    if (!cts::variant_ok(e->geo.small_variant, cts::kDefaultSmallVariant, cts_variant_count(kSmallVariants)))
-        e->geo.small_variant = cts::kDefaultSmallVariant;
-    if (!cts::variant_ok(e->geo.ms_variant, cts::kDefaultMediaStreamVariant, cts_variant_count(kMediaStreamVariants)))
-        e->geo.ms_variant = cts::kDefaultMediaStreamVariant;
     e->sync_mailbox = env_int("CTS_SYNC_MAILBOX", e->sync_mailbox) ? 1 : 0;
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
         delete e;
@@ -636,26 +618,17 @@ int cts_engine_set_attr(cts_engine* e, int attr, int value)
         if (value < 0) return CTS_E_INVALID;
         e->geo.small_threshold = value;
         return CTS_OK;
-    case CTS_ATTR_VERIFY_VARIANT:
-        if (!cts::variant_ok(value, cts::kDefaultVerifyVariant, cts_variant_count(kVerifyVariants))) return CTS_E_INVALID;
-        e->geo.verify_variant = value;
-        return CTS_OK;
+    // the kernel of each path is fixed: its id is accepted, nothing else
+    case CTS_ATTR_VERIFY_VARIANT: return value == cts::kVerifyKernelId ? CTS_OK : CTS_E_INVALID;
+    case CTS_ATTR_SMALL_VARIANT: return value == cts::kSmallKernelId ? CTS_OK : CTS_E_INVALID;
+    case CTS_ATTR_MS_VARIANT: return value == cts::kMediaStreamKernelId ? CTS_OK : CTS_E_INVALID;
     case CTS_ATTR_SMALL_BLOCKS_PER_CU:
         if (value < 1 || value > 256) return CTS_E_INVALID;
         e->geo.small_blocks_per_cu = value;
         return CTS_OK;
-    case CTS_ATTR_SMALL_VARIANT:
-        if (!cts::variant_ok(value, cts::kDefaultSmallVariant, cts_variant_count(kSmallVariants))) return CTS_E_INVALID;
-        e->geo.small_variant = value;
-        return CTS_OK;
     case CTS_ATTR_FILL_BLOCKS_PER_CU:
         if (value < 1 || value > 64) return CTS_E_INVALID;
         e->geo.fill_blocks_per_cu = value;
-        return CTS_OK;
-    case CTS_ATTR_MS_VARIANT:
-        if (!cts::variant_ok(value, cts::kDefaultMediaStreamVariant, cts_variant_count(kMediaStreamVariants)))
-            return CTS_E_INVALID;
-        e->geo.ms_variant = value;
         return CTS_OK;
     case CTS_ATTR_SMALL_CHUNK:
         if (value < 0 || value > (1 << 24)) return CTS_E_INVALID;
@@ -677,11 +650,11 @@ int cts_engine_get_attr(const cts_engine* e, int attr, int* value)
     case CTS_ATTR_BLOCKS_PER_CU: *value = e->geo.blocks_per_cu; return CTS_OK;
     case CTS_ATTR_NT_LOADS: *value = e->geo.nontemporal; return CTS_OK;
     case CTS_ATTR_SMALL_THRESHOLD: *value = e->geo.small_threshold; return CTS_OK;
-    case CTS_ATTR_VERIFY_VARIANT: *value = e->geo.verify_variant; return CTS_OK;
+    case CTS_ATTR_VERIFY_VARIANT: *value = cts::kVerifyKernelId; return CTS_OK;
     case CTS_ATTR_SMALL_BLOCKS_PER_CU: *value = e->geo.small_blocks_per_cu; return CTS_OK;
-    case CTS_ATTR_SMALL_VARIANT: *value = e->geo.small_variant; return CTS_OK;
+    case CTS_ATTR_SMALL_VARIANT: *value = cts::kSmallKernelId; return CTS_OK;
     case CTS_ATTR_FILL_BLOCKS_PER_CU: *value = e->geo.fill_blocks_per_cu; return CTS_OK;
-    case CTS_ATTR_MS_VARIANT: *value = e->geo.ms_variant; return CTS_OK;
+    case CTS_ATTR_MS_VARIANT: *value = cts::kMediaStreamKernelId; return CTS_OK;
     case CTS_ATTR_SMALL_CHUNK: *value = e->geo.small_chunk; return CTS_OK;
     case CTS_ATTR_FILL_NT: *value = e->geo.fill_nt; return CTS_OK;
     case CTS_ATTR_SYNC_MAILBOX: *value = e->sync_mailbox; return CTS_OK;

@@ -15,58 +15,27 @@ namespace cts {
 constexpr int kCounterSlots = 8;  // 5 used, padded to one 64-byte line
 enum CounterSlot { kBytesChecked = 0, kBytesOk = 1, kBuffersChecked = 2, kBuffersFailed = 3, kMismatchedBytes = 4 };
 
-// The product library compiles one kernel per path, the defaults below. The tuning build
-// (CTS_TUNING=1: libcts_engine_tuning.so, `make tuning`) also compiles every variant measured on the
-// way to them, for A/B runs (tools/tune_verify.py, tools/media_stream_probe.py) and their parity tests.
-#ifndef CTS_TUNING
-#define CTS_TUNING 0
-#endif
-constexpr int kDefaultVerifyVariant = 25;  // variant 13 with registers for 4 waves per SIMD (round 4)
-constexpr int kDefaultSmallVariant = 15;  // variant 9 + the edge load L2-allocating (round 3)
-constexpr int kDefaultMediaStreamVariant = 3;
-#if CTS_TUNING
-constexpr int kVerifyVariants = 29;  // workgroup-per-buffer verify variants (launch_verify)
-constexpr int kSmallVariants = 16;   // small-buffer (datagram) verify variants (10-15: line policies)
-constexpr int kMediaStreamVariants = 13;  // MediaStream receive kernels (launch_media_stream_verify)
-#endif
-// A launch-variant attribute value this build can launch.
-inline bool variant_ok(int value, int dflt, int count)
-{
-#if CTS_TUNING
-    (void)dflt;
-    return value >= 0 && value < count;
-#else
-    (void)count;
-    return value == dflt;
-#endif
-}
+// One kernel per path. CTS_ATTR_VERIFY_VARIANT / SMALL_VARIANT / MS_VARIANT report which one, by the number it
+// had among the alternatives measured in rounds 1-4; setting any other value is CTS_E_INVALID.
+constexpr int kVerifyKernelId = 25;       // verify_wg_kernel: U2 whole-line exact stream, 4 waves per SIMD (round 4)
+constexpr int kSmallKernelId = 15;        // verify_quad_kernel: block-contiguous, edge loads L2-allocating (round 3)
+constexpr int kMediaStreamKernelId = 3;   // media_stream_verify_quad_kernel: DPP header, per-wave output ring
 
 struct LaunchGeometry {
     int num_cus = 256;        // hipDeviceAttributeMultiprocessorCount
     int blocks_per_cu = 4;        // workgroup-per-buffer grid cap = num_cus * this (grid-stride beyond);
                                   // 4 x 4 waves x U2 = 32 KiB of loads in flight per CU measured best
                                   // (config 2: 41.0-41.2 us vs 42.6-43.9 at 8; tools/tune_verify.py)
-    int small_blocks_per_cu = 64; // wave-per-buffer grid cap
+    int small_blocks_per_cu = 64; // small-buffer (quad) path grid cap
     int nontemporal = 1;      // nt loads for the once-read verify stream
     int small_threshold = 8192;  // max_length_hint <= this -> small-buffer path
-    int small_variant = kDefaultSmallVariant;       // small-buffer path kernel (launch_verify_nt; 7 = four buffers per wave, line-aligned U6:
-                                 // config 3 at 5.95 TB/s of payload vs 4.71 for one wave per datagram; 9 = 7 walking
-                                 // block-contiguous ranges: 0-5 % faster, results +2 %; tools/media_stream_probe.py)
-    int ms_variant = kDefaultMediaStreamVariant;          // MediaStream receive kernel (launch_media_stream_verify; 3 = four datagrams per wave,
-                                 // 16-B header chunks + DPP, block-contiguous: with records + results 1.04-1.08 ms per
-                                 // 4 M datagrams vs 1.24 ms for variant 1 before output staging)
-    int small_chunk = 0;         // chunked walk of small variant 9 / MediaStream variant 3: buffers per chunk (0 = one
-                                 // contiguous range per workgroup)
+    int small_chunk = 0;         // chunked walk of the quad kernels: buffers per chunk (0 = one contiguous range per
+                                 // workgroup)
     int fill_nt = 2;             // fill store policy: 0 plain, 1 nontemporal, 2 by path (plain for the workgroup
                                  // path, nontemporal for datagrams; tools/tune_verify.py --op fill)
     int fill_blocks_per_cu = 1;  // fill grid cap (write-bound; plain stores: 1 measured best, 48.7 vs 49.1-49.4 us)
-    int fill_batched = 1;        // MediaStream descriptor fill from LDS-staged batches (tuning build: 0 = the wave-per-
-                                 // datagram kernel, 2 = the small payload fill batched too; CTS_FILL_BATCHED)
     int ring_fill_blocks_per_cu = 4;  // MediaStream ring fill grid cap (16 M x 1472 B: 4.3 ms at 4, 5.0 at 8;
                                       // CTS_RING_FILL_BLOCKS_PER_CU; tools/ring_fill_probe.hip)
-    int verify_variant = kDefaultVerifyVariant;     // see launch_verify (25: 13 for 4 waves/SIMD; 13: variant 11 at U2; 11: variant 10 + in-register exact diff;
-                                 // 10: even-phase stream + whole-line spans, U4, measured 1.3-3 % faster than 6,
-                                 // which was +0.3-0.7 % over 0)
 };
 
 // ---- SYNC mailbox (cts_verify_mapped): a resident verify grid fed through pinned host memory ----
@@ -128,10 +97,12 @@ struct MailStarts {
 // (s_memrealtime, 100 MHz) for one job: every wave reaches one of the two exits. per_group = S.
 // groups * kMailGroup workgroups of kMailThreads threads.
 // delay_ticks (test hook, 0 in production): group 0's last workgroup starts polling that much later.
-// polls: slot reads each poller keeps in flight (1 or 2).
 hipError_t launch_mailbox(const MailSlot* slots, MailPart* parts, uint32_t per_group, const MailStarts& starts,
-                          uint32_t groups, uint64_t idle_ticks, hipStream_t stream, uint64_t delay_ticks = 0,
-                          int polls = 1);
+                          uint32_t groups, uint64_t idle_ticks, hipStream_t stream, uint64_t delay_ticks = 0);
+
+// out[0..5) = (accumulate ? out : 0) + the five counters of a device counter block, summed over its
+// CTS_COUNTER_SHARDS shards (one 64-thread workgroup; cts_counters_allreduce folds on the device with it).
+hipError_t launch_counters_fold(const void* block, uint64_t* out, bool accumulate, hipStream_t stream);
 
 hipError_t launch_verify(const uint8_t* arena, uint64_t arena_bytes, const cts_buf_desc* descs, uint32_t n,
                          uint32_t max_length_hint, cts_verify_result* results, uint64_t* counters,

@@ -18,12 +18,16 @@
 // the byte phase. Only when a team's OR is nonzero (rare) does an exact re-scan
 // compute the first differing byte and the differing-byte count.
 //
-// Paths:
-//   verify_wg_kernel    one 256-lane workgroup per buffer (64 KiB TCP buffers)
-//   verify_wave_kernel  one wave per buffer (1472-byte MediaStream datagrams)
-// An LDS-DMA (global_load_lds_dwordx4) variant of the workgroup path measured
-// 2.9 TB/s against 5.7 TB/s for register loads on this stream and was dropped
-// ("What did not work").
+// Paths (one kernel per path; nontemporal and plain-load forms of each):
+//   verify_wg_kernel                  one 256-lane workgroup per buffer (64 KiB TCP buffers)
+//   verify_quad_kernel                four buffers per wave (datagram-sized buffers; descriptors or a strided ring)
+//   media_stream_verify_quad_kernel   MediaStream receive: header + payload, four datagrams per wave
+//   fill_kernel / fill_span_kernel / fill_batched_kernel / media_stream_fill_ring_kernel   the sender side
+//   mailbox_kernel                    SYNC-mode VerifyBuffer without a launch per call (resident grid)
+// Every alternative measured on the way to these (other unroll depths, barrier-free and wave-per-buffer
+// workgroups, windowed and rotated walks, staged records, speculative first loads, LDS-DMA, line policies,
+// two-pass MediaStream receives) was removed from the source once it lost; DESIGN.md §10 lists them with
+// their numbers, and git history (up to round 4, commit fe0efda) holds their code.
 #include <hip/hip_runtime.h>
 
 #include <type_traits>
@@ -215,19 +219,6 @@ __device__ __forceinline__ u32x4 expected_step(uint32_t B, int u, uint32_t sh)
     }
 }
 
-// expected_step for a span on a 16-aligned pattern position (q0 % 16 == 0): every chunk's eight u16 values
-// k..k+7 have k % 8 == 0, so none crosses the 32768 wrap inside the chunk; only the packed base needs the per-half
-// mask, and the four words are that base plus constants (5 VALU per chunk instead of 8).
-template <int TEAM, int U>
-__device__ __forceinline__ u32x4 expected_step_a16(uint32_t B, int u)
-{
-    static_assert(32767 + 8 * TEAM * (U - 1) + 8 < 65536, "packed k must not carry");
-    uint32_t bb = B;
-    asm volatile("" : "+v"(bb));
-    const uint32_t b = (bb + (uint32_t)u * (uint32_t)(8 * TEAM) * 0x10001u) & 0x7FFF7FFFu;
-    return u32x4{b, b + 0x20002u, b + 0x40004u, b + 0x60006u};
-}
-
 // packed base (k*0x10001 + 0x10000) of the chunk at index c
 __device__ __forceinline__ uint32_t chunk_base(const Span& s, uint32_t c)
 {
@@ -302,19 +293,10 @@ __device__ __forceinline__ uint32_t scan_interior(const Span& s, __amdgpu_buffer
 // chunk 0 line-aligned: every buffer of a 64 KiB-strided arena or recv ring
 // whose completion is a multiple of 16 bytes) has no partial chunk to mask: all
 // of [0, nchunks) streams in rounds, with no edge/head load and, for 64 KiB, no
-// tail round (4096 chunks = 2 full rounds of 256 lanes x U8).
+// tail round (4096 chunks = 8 full rounds of 256 lanes x U2; scan_whole_exact).
 __device__ __forceinline__ bool span_whole_lines(const Span& s)
 {
     return s.lo == 0u && s.hi_last == 16u && s.cb0 == 8u;
-}
-
-template <int TEAM, int U, bool NT, bool SPLIT>
-__device__ __forceinline__ uint32_t scan_whole(const Span& s, __amdgpu_buffer_rsrc_t r, uint32_t lane)
-{
-    if constexpr (SPLIT) {
-        if (__builtin_amdgcn_readfirstlane(s.sh) == 0u) return scan_rounds<TEAM, U, NT, true>(s, r, lane, 0u, s.nchunks);
-    }
-    return scan_rounds<TEAM, U, NT, false>(s, r, lane, 0u, s.nchunks);
 }
 
 // Fast pass over a whole span: OR of (received ^ expected) over this lane's
@@ -340,13 +322,10 @@ __device__ __forceinline__ bool edge_chunk_used(const Span& s, uint32_t lane)
     return lane >= 2u && lane <= 8u && lane - 1u < h;
 }
 
-template <int TEAM, int U, bool NT, bool SPLIT = false, bool WHOLE = false>
+template <int TEAM, int U, bool NT, bool SPLIT = false>
 __device__ __forceinline__ uint32_t scan_buffer(const Span& s, uint32_t lane)
 {
     const __amdgpu_buffer_rsrc_t r = span_rsrc(s);
-    if constexpr (WHOLE) {
-        if (__builtin_amdgcn_readfirstlane(span_whole_lines(s) ? 1u : 0u)) return scan_whole<TEAM, U, NT, SPLIT>(s, r, lane);
-    }
     const uint32_t ce = edge_chunk_of(s, lane);
     // lanes without an edge/head chunk address past the resource: the range check
     // returns 0 without a memory request (waves 1..3 of a workgroup fetch nothing)
@@ -404,33 +383,15 @@ __device__ __forceinline__ void scan_exact_owned(const Span& s, uint32_t lane, u
     }
 }
 
-// scan_exact_owned for a span scan_whole streamed: chunk c -> lane c % TEAM, no edges
-template <int TEAM, int U, bool NT>
-__device__ __forceinline__ void scan_exact_whole(const Span& s, uint32_t lane, uint32_t& first, uint32_t& count)
-{
-    const __amdgpu_buffer_rsrc_t r = span_rsrc(s);
-    for (uint32_t cb = 0; cb < s.nchunks; cb += (uint32_t)(TEAM * U)) {
-        u32x4 d[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) d[u] = buf_load<NT>(r, (cb + (uint32_t)(u * TEAM) + lane) * 16u, 0u);
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t c = cb + (uint32_t)(u * TEAM) + lane;
-            if (c < s.nchunks) take_diff(s, c, chunk_xor(s, c, d[u]), first, count);
-        }
-    }
-}
-
 // The whole-span stream with the exact diff done in registers: a lane whose round
 // saw a difference computes its first differing byte and differing-byte count from
-// the XORs it still holds, so a corrupt buffer costs no re-read. (The re-read of
-// scan_exact_whole is 8 dependent rounds for a 64 KiB buffer: several microseconds
-// during which the workgroup's next buffer waits, and with one corrupt buffer in a
-// thousand that workgroup is the launch's last to finish.) The clean-path cost is
-// one compare and branch per round.
-// A16: the span starts on a 16-aligned pattern position (expected_step_a16).
+// the XORs it still holds, so a corrupt buffer costs no re-read. (A re-read is 8
+// dependent rounds for a 64 KiB buffer: several microseconds during which the
+// workgroup's next buffer waits, and with one corrupt buffer in a thousand that
+// workgroup is the launch's last to finish.) The clean-path cost is one compare and
+// branch per round.
 // One whole round: XOR the U loaded chunks with the expected words, then the exact diff of a round that differs.
-template <int TEAM, int U, bool EVEN, bool A16>
+template <int TEAM, int U, bool EVEN>
 __device__ __forceinline__ void whole_exact_round(const Span& s, u32x4 (&d)[U], uint32_t cb, uint32_t lane,
                                                   uint32_t& first, uint32_t& count)
 {
@@ -438,8 +399,7 @@ __device__ __forceinline__ void whole_exact_round(const Span& s, u32x4 (&d)[U], 
     uint32_t any = 0;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-        if constexpr (A16) d[u] ^= expected_step_a16<TEAM, U>(B, u);
-        else d[u] ^= expected_step<TEAM, U, EVEN>(B, u, s.sh);
+        d[u] ^= expected_step<TEAM, U, EVEN>(B, u, s.sh);
         any |= or4(d[u]);
         __builtin_amdgcn_sched_barrier(0);
     }
@@ -449,28 +409,19 @@ __device__ __forceinline__ void whole_exact_round(const Span& s, u32x4 (&d)[U], 
     }
 }
 
-// PRE: the first round's U chunks per lane were loaded by the caller (pre[u] = chunk u * TEAM + lane); the span holds
-// at least one whole round.
-template <int TEAM, int U, bool NT, bool EVEN, bool A16 = false, bool PRE = false>
+template <int TEAM, int U, bool NT, bool EVEN>
 __device__ __forceinline__ void scan_whole_exact_impl(const Span& s, __amdgpu_buffer_rsrc_t r, uint32_t lane,
-                                                      uint32_t& first, uint32_t& count, const u32x4* pre = nullptr)
+                                                      uint32_t& first, uint32_t& count)
 {
     const uint32_t voff = lane * 16u;
     uint32_t cb = 0;
     const uint32_t c_end = s.nchunks;
-    if constexpr (PRE) {
-        u32x4 d[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) d[u] = pre[u];
-        whole_exact_round<TEAM, U, EVEN, A16>(s, d, 0u, lane, first, count);
-        cb = (uint32_t)(TEAM * U);
-    }
     for (; cb + (uint32_t)(TEAM * U) <= c_end; cb += (uint32_t)(TEAM * U)) {
         u32x4 d[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) d[u] = buf_load<NT>(r, voff, (cb + (uint32_t)(u * TEAM)) * 16u);
         __builtin_amdgcn_sched_barrier(0);
-        whole_exact_round<TEAM, U, EVEN, A16>(s, d, cb, lane, first, count);
+        whole_exact_round<TEAM, U, EVEN>(s, d, cb, lane, first, count);
     }
     if (cb < c_end) {
         u32x4 d[U];
@@ -482,10 +433,7 @@ __device__ __forceinline__ void scan_whole_exact_impl(const Span& s, __amdgpu_bu
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const bool in = cb + (uint32_t)(u * TEAM) + lane < c_end;
-            u32x4 e;
-            if constexpr (A16) e = expected_step_a16<TEAM, U>(B, u);
-            else e = expected_step<TEAM, U, EVEN>(B, u, s.sh);
-            d[u] = in ? (d[u] ^ e) : u32x4{0u, 0u, 0u, 0u};
+            d[u] = in ? (d[u] ^ expected_step<TEAM, U, EVEN>(B, u, s.sh)) : u32x4{0u, 0u, 0u, 0u};
             any |= or4(d[u]);
             __builtin_amdgcn_sched_barrier(0);
         }
@@ -496,24 +444,18 @@ __device__ __forceinline__ void scan_whole_exact_impl(const Span& s, __amdgpu_bu
     }
 }
 
-template <int TEAM, int U, bool NT, bool SPLIT, bool A16 = false, bool PRE = false>
-__device__ __forceinline__ void scan_whole_exact(const Span& s, uint32_t lane, uint32_t& first, uint32_t& count,
-                                                 const u32x4* pre = nullptr)
+// SPLIT: a span-uniform branch on the byte phase selects the funnel-shift-free even-phase stream
+template <int TEAM, int U, bool NT, bool SPLIT>
+__device__ __forceinline__ void scan_whole_exact(const Span& s, uint32_t lane, uint32_t& first, uint32_t& count)
 {
     const __amdgpu_buffer_rsrc_t r = span_rsrc(s);
-    if constexpr (A16) {
-        if (__builtin_amdgcn_readfirstlane(s.q0 & 15u) == 0u) {
-            scan_whole_exact_impl<TEAM, U, NT, true, true, PRE>(s, r, lane, first, count, pre);
-            return;
-        }
-    }
     if constexpr (SPLIT) {
         if (__builtin_amdgcn_readfirstlane(s.sh) == 0u) {
-            scan_whole_exact_impl<TEAM, U, NT, true, false, PRE>(s, r, lane, first, count, pre);
+            scan_whole_exact_impl<TEAM, U, NT, true>(s, r, lane, first, count);
             return;
         }
     }
-    scan_whole_exact_impl<TEAM, U, NT, false, false, PRE>(s, r, lane, first, count, pre);
+    scan_whole_exact_impl<TEAM, U, NT, false>(s, r, lane, first, count);
 }
 
 // Spans of 2 GiB or more (a u32 ctsTask length allows 4 GiB - 1). The buffer-resource streams above
@@ -674,383 +616,76 @@ __device__ __forceinline__ void block_reduce_mismatch(uint32_t& first, uint32_t&
     block_reduce_mismatch_with(first, count, red);
 }
 
-// the same for a BS-thread workgroup (tuning: verify_wg_kernel with BS != kBlock)
-template <int BS>
-__device__ __forceinline__ void block_reduce_mismatch_bs(uint32_t& first, uint32_t& count)
-{
-    if constexpr (BS == kBlock) {
-        block_reduce_mismatch(first, count);
-    } else {
-        __shared__ uint32_t red[2 * (BS / 64)];
-        const uint32_t wave = threadIdx.x / 64;
-        first = wave_min(first);
-        count = wave_sum(count);
-        if ((threadIdx.x & 63) == 0) {
-            red[wave] = first;
-            red[BS / 64 + wave] = count;
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-#pragma unroll
-            for (int w = 1; w < BS / 64; ++w) {
-                first = red[w] < first ? red[w] : first;
-                count += red[BS / 64 + w];
-            }
-        }
-        __syncthreads();
-    }
-}
-
-// Wave 0 writes the m result records staged in LDS (record j belongs to buffer idx[j]) as dwords, one
-// store instruction for up to 21 records.
-template <int R>
-__device__ __forceinline__ void flush_staged_results(const cts_verify_result* st, const uint32_t* idx, uint32_t m,
-                                                     cts_verify_result* results)
-{
-    __builtin_amdgcn_wave_barrier();
-    const uint32_t l = threadIdx.x;
-#pragma unroll
-    for (uint32_t k = 0; k < (3u * R + 63u) / 64u; ++k) {
-        const uint32_t e = k * 64u + l, j = e / 3u;
-        if (j < m)
-            reinterpret_cast<uint32_t*>(results)[3ull * idx[j] + (e - 3u * j)] =
-                reinterpret_cast<const uint32_t*>(st)[e];
-    }
-    __builtin_amdgcn_wave_barrier();
-}
-
 // ---------------------------------------------------------------------------------------------
-// One 256-lane workgroup per buffer (grid-strides over buffers). The next
-// buffer's descriptor is fetched while the current one streams.
-// SCTR: the per-buffer verdict is workgroup-uniform (__syncthreads_or), so the
-// counters of clean buffers are kept in SGPRs by every wave (scalar adds, no LDS
-// round trip per buffer); only a corrupt buffer goes through lane 0 + LDS.
-// WIN > 1: the descriptor list is cut into WIN contiguous windows and workgroup b walks window
-// b % WIN with stride gridDim.x / WIN (the launcher makes the grid a multiple of WIN), so WIN
-// far-apart regions of the arena stream at once instead of one 1024-buffer front.
-// DEFER = R > 0: per-buffer result records are staged in LDS and written R at a time by wave 0 (and
-// at the end), so the read stream sees a write every R buffers instead of every buffer (a read stream
-// slows with the frequency of the writes mixed into it: tools/rw_mix_probe.hip).
-// UT > 0 (tuning): a workgroup's LAST buffer streams with UT loads per lane per round instead of U, so
-// the workgroups still running once others have finished keep more bytes in flight (the launch's
-// finishing window, DESIGN.md §3 "Where a 256 MiB launch's last few percent go").
-// A16 (XD): whole-line spans on a 16-aligned pattern position build their expected words with expected_step_a16.
-// WPE > 0: the waves per SIMD the register allocation targets (otherwise 8 for a 256-lane workgroup up to U 8).
-// SPECR: the SPEC guess loaded into registers instead of L2: the first round of the slot a uniformly strided arena
-// gives the workgroup's first buffer is read beside its descriptor, and used as that buffer's first round when the
-// descriptor names exactly that slot (a whole-line span of at least one round); otherwise it is dropped.
-// SPEC: while the workgroup's first descriptor is on its way, the first round of the slot a uniformly strided arena
-// gives buffer i (byte offset i * arena_bytes / n) is read into L2 and dropped; when the descriptor names that slot,
-// its first round then comes from L2 instead of HBM, so the descriptor's latency overlaps the first data fetch
-// instead of preceding it (tools/verify_timeline: 0.56-0.60 against 0.28-0.32 us from entry to the first data
-// load for a plain read). A wrong guess costs one round of reads.
-template <int U, bool NT, bool SPLIT = false, bool SCTR = false, bool WHOLE = false, bool XD = false, int WIN = 1,
-          int DEFER = 0, int UT = 0, int BS = kBlock, bool A16 = false, bool SPEC = false, int WPE = 0, bool SPECR = false,
-          bool ROT = false>
-__global__ void __launch_bounds__(BS, (WPE > 0 ? WPE : (BS == kBlock ? (U <= 8 ? 8 : 4) : 2048 / BS)))
+// One 256-lane workgroup per buffer (64 KiB TCP buffers; grid-strides over the descriptors). The next
+// buffer's descriptor is fetched while the current one streams. A whole-line span (every buffer of a
+// 64 KiB-strided arena whose completion is a multiple of 16 bytes) streams in rounds of kWgLoads 16-byte
+// buffer loads per lane with the exact diff in registers (scan_whole_exact); any other span takes the
+// edge-first fast pass (scan_buffer) and, when it differs, an exact re-read by the lanes that saw it. The
+// per-buffer verdict is workgroup-uniform (__syncthreads_or); only a corrupt buffer reduces (first, count)
+// over the workgroup. Registers are allocated for 4 waves per SIMD, the 4 workgroups per CU the launch runs
+// at (LaunchGeometry::blocks_per_cu): no SGPR spills in the per-buffer set-up (41.18-41.27 against 41.42-41.45
+// us per config-2 launch for the 8-wave allocation, profiles/r04/h/wpe.jsonl).
+constexpr int kWgLoads = 2;  // loads per lane per round: 4 workgroups x 4 waves x 2 = 32 KiB in flight per CU
+
+template <bool NT>
+__global__ void __launch_bounds__(kBlock, 4)
     verify_wg_kernel(const uint8_t* __restrict__ arena, uint64_t arena_bytes, const cts_buf_desc* __restrict__ descs,
                      uint32_t n, cts_verify_result* __restrict__ results, uint64_t* __restrict__ counters,
                      uint32_t* __restrict__ conn_first_fail, uint32_t n_conns)
 {
-    static_assert(!(SCTR && DEFER), "deferred results take the finish_buffer path");
-    static_assert(!SPEC || WIN == 1, "the guessed slot is the grid-stride walk's first buffer");
-    static_assert(!SPECR || (WIN == 1 && XD && !SPEC && UT == 0), "SPECR: the whole-line exact stream's first round");
-    static_assert(!ROT || (WIN == 1 && !SPEC && !SPECR), "ROT permutes the plain grid-stride walk");
     __shared__ uint64_t ctr[1][5];
-    __shared__ cts_verify_result dres[DEFER ? DEFER : 1];
-    __shared__ uint32_t didx[DEFER ? DEFER : 1];
     const uint32_t lane = threadIdx.x;
-    uint32_t dk = 0;  // DEFER: records staged (uniform)
-    const bool defer = DEFER > 0 && results != nullptr;
-    // DEFER: count the record lane 0 just staged; wave 0 writes a full staging area
-    auto staged = [&]() {
-        if (++dk == (uint32_t)DEFER) {
-            if (lane < 64u) flush_staged_results<DEFER ? DEFER : 1>(dres, didx, dk, results);
-            dk = 0;
-        }
-    };
     zero_counters<1>(ctr);
-    uint64_t ok_bytes = 0;     // SCTR: bytes of clean buffers (uniform)
-    uint32_t ok_buffers = 0;   // SCTR: clean buffers (uniform)
-    uint32_t i = blockIdx.x, end = n, step = gridDim.x;
-    if constexpr (WIN > 1) {
-        const uint32_t per = (uint32_t)(((uint64_t)n + WIN - 1) / WIN);
-        const uint32_t g = blockIdx.x % WIN;
-        const uint64_t e = (uint64_t)(g + 1) * per;
-        end = e < n ? (uint32_t)e : n;
-        const uint64_t s0 = (uint64_t)g * per + blockIdx.x / WIN;
-        i = s0 < end ? (uint32_t)s0 : end;
-        step = gridDim.x / WIN;
-    }
-    // ROT: in every full round k of the walk (k * step + step <= end) workgroup b takes descriptor
-    // k * step + (b + k) mod step instead of k * step + b (a partial last round keeps b), so the buffers one
-    // workgroup (and one XCD) reads are not all congruent modulo the grid
-    uint32_t rr = blockIdx.x;  // ROT: (b + k) mod step
-    auto walk = [&](uint32_t slot, uint32_t r) -> uint32_t {
-        if constexpr (!ROT) return slot;
-        const uint32_t kbase = slot - blockIdx.x;
-        return (uint64_t)kbase + step <= end ? kbase + r : slot;
-    };
+    const uint32_t step = gridDim.x;
+    uint32_t i = blockIdx.x;
     cts_buf_desc dn;
-    if (i < end) dn = descs[walk(i, rr)];
-    if constexpr (SPEC) {
-        // the guessed slot's first round, L2-allocating (the default policy), beside the descriptor's load; the data
-        // is dropped once it arrived (the asm keeps the loads), the round's own loads then hit L2
-        if (i < end) {
-            const uint64_t per = arena_bytes / n;
-            if (per >= 16u) {
-                const uint32_t g_len = (uint32_t)(per < (uint64_t)BS * U * 16u ? per : (uint64_t)BS * U * 16u);
-                const __amdgpu_buffer_rsrc_t gr = __builtin_amdgcn_make_buffer_rsrc(
-                    const_cast<uint8_t*>(arena) + (uint64_t)i * per, (short)0, (int)g_len, 0x00020000);
-                u32x4 p[U];
-#pragma unroll
-                for (int u = 0; u < U; ++u) p[u] = buf_load<false>(gr, lane * 16u, (uint32_t)(u * BS) * 16u);
-#pragma unroll
-                for (int u = 0; u < U; ++u) asm volatile("" ::"v"(p[u]));
-            }
-        }
-    }
-    u32x4 pre[SPECR ? U : 1];
-    const uint8_t* pre_p = nullptr;  // SPECR: the guessed slot (uniform; null = no guess pending)
-    if constexpr (SPECR) {
-        if (i < end) {
-            const uint64_t per = arena_bytes / n;
-            if (per >= (uint64_t)BS * U * 16u) {
-                pre_p = arena + (uint64_t)i * per;
-                const __amdgpu_buffer_rsrc_t gr = __builtin_amdgcn_make_buffer_rsrc(
-                    const_cast<uint8_t*>(pre_p), (short)0, (int)(BS * U * 16), 0x00020000);
-#pragma unroll
-                for (int u = 0; u < U; ++u) pre[u] = buf_load<NT>(gr, lane * 16u, (uint32_t)(u * BS) * 16u);
-            }
-        }
-    }
-    for (; i < end; i = (uint64_t)i + step < end ? i + step : end) {
+    if (i < n) dn = descs[i];
+    for (; i < n; i = (uint64_t)i + step < n ? i + step : n) {
         const cts_buf_desc d = dn;
-        const uint32_t di = walk(i, rr);  // the descriptor (and result record) this step verifies
-        if constexpr (ROT) rr = rr + 1u == step ? 0u : rr + 1u;
-        if ((uint64_t)i + step < end) dn = descs[walk(i + step, rr)];
-        const uint8_t* guess = pre_p;
-        if constexpr (SPECR) pre_p = nullptr;
+        if ((uint64_t)i + step < n) dn = descs[i + step];
         if (desc_bad(d, arena_bytes)) {
-            if (DEFER && defer) {
-                if (lane == 0) {
-                    write_bad(dres + dk, 0);
-                    didx[dk] = di;
-                }
-                staged();
-            } else if (lane == 0) {
-                write_bad(results, di);
-            }
+            if (lane == 0) write_bad(results, i);
             continue;
         }
         const Span s = make_span(arena, d);
         uint32_t first = kNone, count = 0;
         bool dirty;
         if (span_giant(s)) {  // >= 2 GiB: 64-bit exact pass
-            scan_giant_exact<BS, NT>(s, lane, first, count);
+            scan_giant_exact<kBlock, NT>(s, lane, first, count);
             dirty = __builtin_amdgcn_readfirstlane(__syncthreads_or(first != kNone)) != 0;
-            if (dirty) block_reduce_mismatch_bs<BS>(first, count);
-        } else if (XD && __builtin_amdgcn_readfirstlane(span_whole_lines(s) ? 1u : 0u)) {
+            if (dirty) block_reduce_mismatch(first, count);
+        } else if (__builtin_amdgcn_readfirstlane(span_whole_lines(s) ? 1u : 0u)) {
             // whole-line span, exact diff in registers: only the reduction is left
-            if (UT > 0 && (uint64_t)i + step >= end)
-                scan_whole_exact<BS, (UT > 0 ? UT : U), NT, SPLIT, A16>(s, lane, first, count);
-            else if (SPECR && guess != nullptr && reinterpret_cast<const uint8_t*>(s.p) == guess &&
-                     s.nchunks >= (uint32_t)(BS * U))
-                scan_whole_exact<BS, U, NT, SPLIT, A16, true>(s, lane, first, count, pre);
-            else
-                scan_whole_exact<BS, U, NT, SPLIT, A16>(s, lane, first, count);
+            scan_whole_exact<kBlock, kWgLoads, NT, true>(s, lane, first, count);
             dirty = __builtin_amdgcn_readfirstlane(__syncthreads_or(first != kNone)) != 0;
-            if (dirty) block_reduce_mismatch_bs<BS>(first, count);
+            if (dirty) block_reduce_mismatch(first, count);
         } else {
-            const uint32_t acc = scan_buffer<BS, U, NT, SPLIT, WHOLE>(s, lane);
+            const uint32_t acc = scan_buffer<kBlock, kWgLoads, NT, true>(s, lane);
             dirty = __builtin_amdgcn_readfirstlane(__syncthreads_or(acc != 0u)) != 0;
             if (dirty) {  // rare: exact re-scan by the dirty lanes + reduction
-                if (acc != 0u) {
-                    if (WHOLE && span_whole_lines(s)) scan_exact_whole<BS, 2, NT>(s, lane, first, count);
-                    else scan_exact_owned<BS, 2, NT>(s, lane, first, count);
-                }
-                block_reduce_mismatch_bs<BS>(first, count);
+                if (acc != 0u) scan_exact_owned<kBlock, 2, NT>(s, lane, first, count);
+                block_reduce_mismatch(first, count);
             }
         }
-        if constexpr (SCTR) {
-            if (!dirty) {
-                ok_bytes += s.len;
-                ok_buffers += 1;
-                if (results != nullptr && lane == 0) {
-                    cts_verify_result r{};
-                    r.first_mismatch = s.len;
-                    r.pass = 1;
-                    results[di] = r;
-                }
-                continue;
-            }
-        }
-        if (DEFER && defer) {
-            if (lane == 0) {
-                finish_buffer(s, d, di, first, count, results, ctr[0], conn_first_fail, n_conns, dres + dk);
-                didx[dk] = di;
-            }
-            staged();
-        } else if (lane == 0) {
-            finish_buffer(s, d, di, first, count, results, ctr[0], conn_first_fail, n_conns);
-        }
-    }
-    if constexpr (DEFER > 0)
-        if (dk && lane < 64u) flush_staged_results<DEFER>(dres, didx, dk, results);
-    if constexpr (SCTR) {
-        if (lane == 0) {
-            ctr[0][kBytesChecked] += ok_bytes;
-            ctr[0][kBytesOk] += ok_bytes;
-            ctr[0][kBuffersChecked] += ok_buffers;
-        }
+        if (lane == 0) finish_buffer(s, d, i, first, count, results, ctr[0], conn_first_fail, n_conns);
     }
     flush_counters<1>(counters, ctr);
 }
 
 // ---------------------------------------------------------------------------------------------
-// Barrier-free workgroup-per-buffer verify. verify_wg_kernel ends every buffer
-// with __syncthreads_or: each wave drains its loads (vmcnt(0)) and then waits
-// for the slowest wave before the next buffer's loads go out — one HBM latency
-// of dead time per buffer per workgroup. Here the four waves of a workgroup
-// only meet through an LDS arrival word per buffer: a wave that saw a mismatch
-// in its own chunks computes its exact (first, count) share first and merges it
-// with LDS atomics, then every wave adds one arrival (count | flag << 8); the
-// wave that arrives last writes the record and resets the slot. Waves run
-// ahead into the next buffer immediately. Slots form a ring of kRing; a
-// barrier every kRing buffers bounds the skew between waves so a slot is
-// never reused while a slower wave still owns it.
-constexpr uint32_t kRing = 16;
-
-struct ArriveSlot {
-    uint32_t arrive;  // arrivals (low 8 bits) | flagged waves << 8
-    uint32_t first;   // min first-mismatch over flagged waves
-    uint32_t count;   // sum of differing bytes over flagged waves
-};
-
-template <int U, bool NT>
-__global__ void __launch_bounds__(kBlock, (U <= 8 ? 8 : 4))
-    verify_wg_nb_kernel(const uint8_t* __restrict__ arena, uint64_t arena_bytes, const cts_buf_desc* __restrict__ descs,
-                        uint32_t n, cts_verify_result* __restrict__ results, uint64_t* __restrict__ counters,
-                        uint32_t* __restrict__ conn_first_fail, uint32_t n_conns)
-{
-    constexpr int WAVES = kBlock / 64;
-    __shared__ uint64_t ctr[WAVES][5];
-    __shared__ ArriveSlot slots[kRing];
-    const uint32_t lane = threadIdx.x;
-    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (threadIdx.x < kRing) slots[threadIdx.x] = ArriveSlot{0u, kNone, 0u};
-    zero_counters<WAVES>(ctr);  // ends with __syncthreads
-    uint32_t i = blockIdx.x;
-    uint32_t j = 0;
-    cts_buf_desc dn;
-    if (i < n) dn = descs[i];
-    for (; i < n; i += gridDim.x, ++j) {
-        const cts_buf_desc d = dn;
-        if (i + gridDim.x < n) dn = descs[i + gridDim.x];
-        if (j != 0 && (j % kRing) == 0) __syncthreads();  // bound inter-wave skew (slot reuse)
-        if (desc_bad(d, arena_bytes)) {
-            if (lane == 0) write_bad(results, i);
-            continue;
-        }
-        const Span s = make_span(arena, d);
-        const bool giant = span_giant(s);
-        uint32_t gfirst = kNone, gcount = 0;
-        if (giant) scan_giant_exact<kBlock, NT>(s, lane, gfirst, gcount);  // >= 2 GiB: 64-bit exact pass
-        const uint32_t acc = giant ? (gfirst != kNone ? 1u : 0u) : scan_buffer<kBlock, U, NT>(s, lane);
-        ArriveSlot* slot = &slots[j % kRing];
-        uint32_t flag = 0;
-        if (__any(acc != 0u)) {  // rare: exact share of this wave's chunks
-            uint32_t first = gfirst, count = gcount;
-            if (acc != 0u && !giant) scan_exact_owned<kBlock, 2, NT>(s, lane, first, count);
-            first = wave_min(first);
-            count = wave_sum(count);
-            if ((lane & 63u) == 0) {
-                atomicMin(&slot->first, first);
-                atomicAdd(&slot->count, count);
-            }
-            flag = 0x100u;
-        }
-        uint32_t old = 0;
-        if ((lane & 63u) == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            old = atomicAdd(&slot->arrive, 1u | flag);
-        }
-        old = (uint32_t)__builtin_amdgcn_readfirstlane((int)__shfl((int)old, 0, 64));
-        if ((old & 0xFFu) == (uint32_t)(WAVES - 1) && (lane & 63u) == 0) {  // last arrival finishes the buffer
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            const bool any = ((old >> 8) + (flag >> 8)) != 0u;
-            uint32_t first = kNone, count = 0;
-            if (any) {
-                first = __hip_atomic_load(&slot->first, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                count = __hip_atomic_load(&slot->count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
-            slot->first = kNone;
-            slot->count = 0;
-            slot->arrive = 0;
-            finish_buffer(s, d, i, first, count, results, ctr[wave], conn_first_fail, n_conns);
-        }
-    }
-    flush_counters<WAVES>(counters, ctr);
-}
-
-// ---------------------------------------------------------------------------------------------
-// One wave per buffer (datagram-sized buffers; also any buffer when there are
-// enough of them to fill the chip one wave each). Waves grid-stride over the
-// descriptors, fetching the next descriptor while the current buffer streams.
-template <int U, bool NT>
-__global__ void __launch_bounds__(kBlock)
-    verify_wave_kernel(const uint8_t* __restrict__ arena, uint64_t arena_bytes, const cts_buf_desc* __restrict__ descs,
-                       uint32_t n, cts_verify_result* __restrict__ results, uint64_t* __restrict__ counters,
-                       uint32_t* __restrict__ conn_first_fail, uint32_t n_conns)
-{
-    constexpr int WAVES = kBlock / 64;
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t nw = gridDim.x * WAVES;
-    __shared__ uint64_t ctr[WAVES][5];
-    zero_counters<WAVES>(ctr);
-    uint32_t i = blockIdx.x * WAVES + wave;
-    cts_buf_desc dn;
-    if (i < n) dn = descs[i];
-    for (; i < n; i += nw) {
-        const cts_buf_desc d = dn;
-        if (i + nw < n) dn = descs[i + nw];
-        if (desc_bad(d, arena_bytes)) {
-            if (lane == 0) write_bad(results, i);
-            continue;
-        }
-        const Span s = make_span(arena, d);
-        uint32_t first = kNone, count = 0;
-        if (span_giant(s)) {  // >= 2 GiB: 64-bit exact pass
-            scan_giant_exact<64, NT>(s, lane, first, count);
-            first = wave_min(first);
-            count = wave_sum(count);
-        } else {
-            const uint32_t acc = scan_buffer<64, U, NT>(s, lane);
-            if (__any(acc != 0u)) {
-                if (acc != 0u) scan_exact_owned<64, 2, NT>(s, lane, first, count);
-                first = wave_min(first);
-                count = wave_sum(count);
-            }
-        }
-        if (lane == 0) finish_buffer(s, d, i, first, count, results, ctr[wave], conn_first_fail, n_conns);
-    }
-    flush_counters<WAVES>(counters, ctr);
-}
-
-// ---------------------------------------------------------------------------------------------
 // Four buffers per wave: 16-lane teams, one buffer each (datagram-sized spans).
-// verify_wave_kernel spends a whole wave per 1472-byte datagram: its per-buffer
-// scalar work (descriptor, span set-up, edge lanes, record, counters) is issued once
-// per datagram and a third of its lanes' loads fall past the span. Here a wave's
-// instructions serve four datagrams at once: the span fields live in VGPRs (one
+// A whole wave per 1472-byte datagram issues its per-buffer scalar work (descriptor,
+// span set-up, edge lanes, record, counters) once per datagram, and a third of its
+// lanes' loads fall past the span (4.71 against 5.95 TB/s of payload for this form on
+// config 3, tools/media_stream_probe.py). Here a wave's instructions serve four datagrams at once: the span fields live in VGPRs (one
 // descriptor per team), each load instruction fetches four 256-byte runs, and
 // U loads per lane cover 16*U chunks per round (U = 6: 1536 B, one round for a
 // 1446-byte payload at any alignment). Loads are global (per-lane 64-bit
 // addresses: a buffer resource must be wave-uniform); addresses of chunks outside
 // a span are clamped into it (same lines, no extra traffic) and their compare is
-// discarded. ALIGN starts the rounds on the 128-byte line of chunk 0 (the
-// line-aligned interior of scan_buffer), so a team's run covers 2 lines, not 3.
+// discarded. The rounds start on the 128-byte line of chunk 0 (the line-aligned
+// interior of scan_buffer), so a team's run covers 2 lines, not 3.
 // A team whose OR is nonzero (rare; the verdict is a wave ballot) re-reads its own
 // chunks exactly and reduces (first, count) over its 16 lanes.
 __device__ __forceinline__ void take_diff_at(uint32_t c, uint32_t lo, u32x4 x, uint32_t& first, uint32_t& count)
@@ -1074,14 +709,13 @@ struct QSpan {
     const uint8_t* sp;  // first verified byte
     uint32_t len, nch, hi_last, lo, q0, sh;
     int last;  // address clamp: the last chunk (0 for an empty span)
-    int cs;    // first chunk of round 0 (line-aligned with ALIGN, else 1)
+    int cs;    // first chunk of round 0: the first chunk of chunk 0's 128-byte line (-7..0)
     int c_hi;  // last interior chunk (nch - 2)
 };
 
 // Span of [sp, sp + len) at pattern offset `expected`; an empty span (len 0: an idle
 // team, a bad descriptor, a non-DATA datagram) points at `dummy`, 16-byte-aligned
 // memory the clamped loads may read (every compare of an empty span is discarded).
-template <bool ALIGN>
 __device__ __forceinline__ QSpan quad_span(const uint8_t* sp, uint32_t len, uint32_t expected, const void* dummy)
 {
     QSpan q;
@@ -1094,7 +728,7 @@ __device__ __forceinline__ QSpan quad_span(const uint8_t* sp, uint32_t len, uint
     q.sh = q.q0 & 1u;
     q.p = reinterpret_cast<const u32x4*>(q.sp - q.lo);
     q.last = q.nch == 0u ? 0 : (int)q.nch - 1;
-    q.cs = ALIGN ? -(int)(((uintptr_t)q.p >> 4) & 7u) : 1;
+    q.cs = -(int)(((uintptr_t)q.p >> 4) & 7u);
     q.c_hi = (int)q.nch - 2;
     return q;
 }
@@ -1113,44 +747,20 @@ __device__ __forceinline__ u32x4 quad_edge_xor(const QSpan& q, uint32_t ce, u32x
 
 // Interior [1, nch-1) in rounds of U loads per lane starting at chunk cs (the wave loops
 // while any of its teams has chunks left); returns the OR of this lane's differences.
-// LP (line policy, tuning): bit 0 clamps out-of-span chunks to the span's first / last 128-B LINE instead of its
-// first / last chunk, so every load instruction requests whole lines; bit 1 loads the span's first and last line
-// with the default (L2-allocating) policy and only the lines in between nontemporal; bit 2 (kQuadEdgesInRound)
-// compares the two partial edge chunks from the round loads (masked) instead of a separate edge load, so no
-// line of the span is requested twice: with nontemporal loads the edge load's line sat at L2's LRU position
-// and was often gone when the round asked for it again (config 3, 4 M datagrams: 8 M extra L2 requests, 0.9 M
-// extra misses, FETCH_SIZE 1.7 % over the arena; profiles/r03/dg_probe/).
-constexpr int kQuadEdgesInRound = 4;
-// LP bit 3: the separate edge-chunk load (issued before the rounds) with the default policy, so the two lines it
-// brings into L2 stay there for the round loads that request them again (nontemporal: inserted at LRU).
-constexpr int kQuadEdgePlain = 8;
-template <int U, bool NT, int LP = 0>
+// Chunks outside the span are clamped to its first / last chunk.
+template <int U, bool NT>
 __device__ __forceinline__ uint32_t quad_scan_interior(const QSpan& q, uint32_t lane)
 {
     constexpr int ROUND = kQuadTeam * U;
-    constexpr bool EIR = (LP & kQuadEdgesInRound) != 0;
     uint32_t acc = 0;
-    const int lfirst = -(int)(((uintptr_t)q.p >> 4) & 7u);                       // first chunk of chunk 0's line
-    const int llast = q.last + 7 - (int)((((uintptr_t)q.p >> 4) + (uint32_t)q.last) & 7u);  // last of last's line
-    const int lastv = (int)q.nch - 1;  // the last chunk of the span (-1: empty)
-    u32x4 e0 = u32x4{0u, 0u, 0u, 0u}, e1 = e0;  // EIR: this lane's differences in chunk 0 / the last chunk
-    for (int r = 0; __any(q.cs + r * ROUND <= (EIR ? lastv : q.c_hi)); ++r) {
+    for (int r = 0; __any(q.cs + r * ROUND <= q.c_hi); ++r) {
         const int cb = q.cs + r * ROUND + (int)lane;
         u32x4 dd[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             int c = cb + u * kQuadTeam;
-            if constexpr ((LP & 1) != 0) {
-                c = c < lfirst ? lfirst : (c > llast ? llast : c);
-            } else {
-                c = c < 0 ? 0 : (c > q.last ? q.last : c);
-            }
-            if constexpr ((LP & 2) != 0) {
-                if (c < lfirst + 8 || c > llast - 8) dd[u] = load_chunk_g<false>(q.p + c);
-                else dd[u] = load_chunk_g<NT>(q.p + c);
-            } else {
-                dd[u] = load_chunk_g<NT>(q.p + c);
-            }
+            c = c < 0 ? 0 : (c > q.last ? q.last : c);
+            dd[u] = load_chunk_g<NT>(q.p + c);
         }
         __builtin_amdgcn_sched_barrier(0);
         const uint32_t k = ((q.q0 + 16u * (uint32_t)cb) & 0xFFFFu) >> 1;
@@ -1158,42 +768,12 @@ __device__ __forceinline__ uint32_t quad_scan_interior(const QSpan& q, uint32_t 
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int c = cb + u * kQuadTeam;
-            if constexpr (EIR) {
-                // interior chunks as always; the two partial edge chunks are kept and masked after the rounds
-                // (chunk 0 is always in round 0's first load: rounds start on its line, cs > -8)
-                const u32x4 x = dd[u] ^ expected_step<kQuadTeam, U>(B, u, q.sh);
-                acc |= (c >= 1 && c < lastv) ? or4(x) : 0u;
-                if (u == 0 && c == 0) e0 = x;
-                if (c == lastv && lastv >= 1) e1 = x;
-            } else {
-                const uint32_t any = or4(dd[u] ^ expected_step<kQuadTeam, U>(B, u, q.sh));
-                acc |= (c >= 1 && c <= q.c_hi) ? any : 0u;
-            }
+            const uint32_t any = or4(dd[u] ^ expected_step<kQuadTeam, U>(B, u, q.sh));
+            acc |= (c >= 1 && c <= q.c_hi) ? any : 0u;
             __builtin_amdgcn_sched_barrier(0);
         }
     }
-    if constexpr (EIR) {
-        if (lastv >= 0) {
-            acc |= or4(e0 & range_mask(q.lo, lastv == 0 ? q.hi_last : 16u));
-            acc |= or4(e1 & range_mask(0u, q.hi_last));
-        }
-    }
     return acc;
-}
-
-// The exact re-read for kQuadEdgesInRound: the chunks this lane loaded in the rounds (cs + lane mod 16), the
-// edge chunks masked as there.
-template <bool NT>
-__device__ __forceinline__ void quad_scan_exact_eir(const QSpan& q, uint32_t lane, uint32_t& first, uint32_t& count)
-{
-    const int lastv = (int)q.nch - 1;
-    for (int c = q.cs + (int)lane; c <= lastv; c += kQuadTeam) {
-        if (c >= 0) {
-            u32x4 x = load_chunk_g<NT>(q.p + c) ^ expected_chunk((q.q0 + 16u * (uint32_t)c) & 0xFFFFu, q.sh);
-            if (c == 0 || c == lastv) x &= range_mask(c == 0 ? q.lo : 0u, c == lastv ? q.hi_last : 16u);
-            take_diff_at((uint32_t)c, q.lo, x, first, count);
-        }
-    }
 }
 
 // Exact re-read of exactly the chunks this lane owns (interior chunks = cs + lane mod 16,
@@ -1281,12 +861,9 @@ __device__ __forceinline__ void quad_stage_result(O& o, uint32_t t, uint32_t fir
     o.res[t][2] = dw2;
 }
 
-// All 64 lanes of the wave call this after the leaders staged; i = this lane's buffer index
-// (the wave's four teams hold i0 .. i0 + 3, i0 = lane 0's), n = buffers in the launch. RECDW = dwords per
-// record: 8 (cts_datagram_record) or 4 (cts_datagram_status, staged in rec[t][0..3]).
-template <int RECDW = 8>
-__device__ __forceinline__ void quad_flush_outputs(const QuadOut& o, uint32_t i, uint32_t n,
-                                                   cts_verify_result* results, void* records)
+// All 64 lanes of the wave call this after the leaders staged their results; i = this lane's buffer index
+// (the wave's four teams hold i0 .. i0 + 3, i0 = lane 0's), n = buffers in the launch.
+__device__ __forceinline__ void quad_flush_results(const QuadOut& o, uint32_t i, uint32_t n, cts_verify_result* results)
 {
     __builtin_amdgcn_wave_barrier();
     // (64-bit: i0 + t may pass 2^32 on the wave's last round when n is close to it)
@@ -1296,13 +873,6 @@ __device__ __forceinline__ void quad_flush_outputs(const QuadOut& o, uint32_t i,
         const uint32_t t = l / 3u;
         const uint32_t v = o.res[t][l - 3u * t];
         if (i0 + t < n) reinterpret_cast<uint32_t*>(results)[3ull * i0 + l] = v;
-    }
-    if (records != nullptr && l < 4u * RECDW) {
-        const uint32_t t = l / RECDW;
-        const uint32_t v = o.rec[t][l % RECDW];
-        if (i0 + t < n)
-            __hip_atomic_store(reinterpret_cast<uint32_t*>(records) + (uint64_t)RECDW * i0 + l, v, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
     }
     __builtin_amdgcn_wave_barrier();
 }
@@ -1329,8 +899,8 @@ struct QuadRing {
 };
 
 // All 64 lanes: write rounds [0, m) of the ring (round j's four buffers start at i0[j]); n = buffers in
-// the launch. Records go as write-through dwords (as quad_flush_outputs), 32 per round, results as
-// plain dwords, 12 per round.
+// the launch. Records go as agent-scope relaxed atomic dwords, RECDW x 4 per round, results as plain dwords,
+// 12 per round.
 // RECDW = dwords per record: 8 (cts_datagram_record) or 4 (cts_datagram_status, staged in rec[t][0..3]).
 template <int K, int RECDW = 8, typename SlotT = QuadOut>
 __device__ __forceinline__ void quad_ring_flush(const QuadRing<K, SlotT>& g, uint32_t m, uint32_t n,
@@ -1365,40 +935,28 @@ __device__ __forceinline__ void quad_ring_flush(const QuadRing<K, SlotT>& g, uin
     __builtin_amdgcn_wave_barrier();
 }
 
-// Which buffers a team visits. Grid-stride (CONTIG = false): team k of block b takes
-// b * TEAMS + k, then steps by the grid's team count. Chunked (CONTIG = true): the buffers are cut
-// into chunks of `per` consecutive buffers (a multiple of TEAMS); block b walks chunks b, b + grid,
-// ... TEAMS buffers at a time, so the rounds of a wave write adjacent outputs and a 128-byte line
-// of 12-byte results fills up in ONE CU's L2 (grid-stride spreads a line over workgroups on
-// different XCDs: partial-line writes). per = TEAMS is the grid-stride walk; one chunk per block
-// is a fully block-contiguous walk.
-template <bool CONTIG, int TEAMS>
+// Which buffers a team visits: the buffers are cut into chunks of `per` consecutive buffers (a multiple of
+// TEAMS); block b walks chunks b, b + grid, ... TEAMS buffers at a time, so the rounds of a wave write adjacent
+// outputs and a 128-byte line of 12-byte results fills up in ONE CU's L2 (a grid-stride walk spreads a line over
+// workgroups on different XCDs: partial-line writes, 0-5 % slower, tools/media_stream_probe.py). One chunk per
+// block (contig_grid's default) is a fully block-contiguous walk.
+template <int TEAMS>
 struct QuadWalk {
     uint32_t i, end;
-    uint64_t cbase;  // first buffer of the current chunk (CONTIG)
+    uint64_t cbase;  // first buffer of the current chunk
     uint32_t per, team;
     __device__ __forceinline__ QuadWalk(uint32_t n, uint32_t per_, uint32_t team_) : end(n), per(per_), team(team_)
     {
-        if constexpr (CONTIG) {
-            cbase = (uint64_t)blockIdx.x * per;
-            i = cbase + team < (uint64_t)n ? (uint32_t)(cbase + team) : n;
-        } else {
-            cbase = 0;
-            i = blockIdx.x * TEAMS + team;
-        }
+        cbase = (uint64_t)blockIdx.x * per;
+        i = cbase + team < (uint64_t)n ? (uint32_t)(cbase + team) : n;
     }
     // the buffer after i (end when none); moves to the block's next chunk at a chunk's end
     __device__ __forceinline__ uint32_t next()
     {
-        uint64_t nx;
-        if constexpr (CONTIG) {
-            nx = (uint64_t)i + TEAMS;
-            if (nx - cbase >= per) {
-                cbase += (uint64_t)gridDim.x * per;
-                nx = cbase + team;
-            }
-        } else {
-            nx = (uint64_t)i + (uint64_t)gridDim.x * TEAMS;
+        uint64_t nx = (uint64_t)i + TEAMS;
+        if (nx - cbase >= per) {
+            cbase += (uint64_t)gridDim.x * per;
+            nx = cbase + team;
         }
         return nx < (uint64_t)end ? (uint32_t)nx : end;
     }
@@ -1428,13 +986,19 @@ __device__ __forceinline__ cts_buf_desc vs_desc(const VSource& src, uint32_t i)
     }
 }
 
-template <int U, bool NT, bool ALIGN, bool CONTIG = false, bool STRIDED = false, int LP = 0>
+// U = 6 loads per lane per round: 1536 B per team, one round for a 1446-byte payload at any alignment.
+// The two edge chunks are loaded first with the default (L2-allocating) policy, so the lines they bring into L2
+// stay there for the round loads that request them again (nontemporal, they sat at L2's LRU position and were
+// often gone: config 3, 4 M datagrams, 8 M extra L2 requests and FETCH_SIZE 1.7 % over the arena,
+// profiles/r03/dg_probe/).
+constexpr int kQuadLoads = 6;
+
+template <bool NT, bool STRIDED>
 __global__ void __launch_bounds__(kBlock)
     verify_quad_kernel(const uint8_t* __restrict__ arena, uint64_t arena_bytes, VSource src, uint32_t n,
                        cts_verify_result* __restrict__ results, uint64_t* __restrict__ counters,
-                       uint32_t* __restrict__ conn_first_fail, uint32_t n_conns, uint32_t per = 0)
+                       uint32_t* __restrict__ conn_first_fail, uint32_t n_conns, uint32_t per)
 {
-    static_assert((LP & kQuadEdgesInRound) == 0 || ALIGN, "edges in round need rounds starting on chunk 0's line");
     constexpr int TEAMS = kBlock / kQuadTeam;
     __shared__ uint64_t ctr[TEAMS][5];
     __shared__ QuadOut qout[kBlock / 64];
@@ -1445,7 +1009,7 @@ __global__ void __launch_bounds__(kBlock)
     const void* dummy = STRIDED ? static_cast<const void*>(arena)
                                 : reinterpret_cast<const void*>(((uintptr_t)src.descs + 15u) & ~(uintptr_t)15u);
     QCounters qc;
-    QuadWalk<CONTIG, TEAMS> w(n, per, team);
+    QuadWalk<TEAMS> w(n, per, team);
     cts_buf_desc dn = vs_desc<STRIDED>(src, w.i < n ? w.i : n - 1u);  // n >= 1 (launch_verify returns early on 0)
     while (__any(w.i < w.end)) {
         const uint32_t i = w.i;
@@ -1454,24 +1018,16 @@ __global__ void __launch_bounds__(kBlock)
         dn = vs_desc<STRIDED>(src, inext < n ? inext : n - 1u);  // clamped: no load under a branch
         const bool live = i < w.end;
         const bool ok = live && !desc_bad(d, arena_bytes);
-        const QSpan q = quad_span<ALIGN>(arena + d.byte_offset + d.skip_head, ok ? d.length - d.skip_head : 0u,
-                                         d.expected_pattern_offset, dummy);
+        const QSpan q = quad_span(arena + d.byte_offset + d.skip_head, ok ? d.length - d.skip_head : 0u,
+                                  d.expected_pattern_offset, dummy);
         // edge chunks first (their latency hides under the interior rounds)
-        uint32_t acc;
-        if constexpr ((LP & kQuadEdgesInRound) != 0) {
-            acc = quad_scan_interior<U, NT, LP>(q, lane);
-        } else {
-            const uint32_t ce = quad_edge_chunk(q, lane);
-            const u32x4 edge = load_chunk_g<(LP & (2 | kQuadEdgePlain)) ? false : NT>(q.p + ce);
-            acc = quad_scan_interior<U, NT, LP>(q, lane);
-            acc |= quad_edge_used(q, lane) ? or4(quad_edge_xor(q, ce, edge)) : 0u;
-        }
+        const uint32_t ce = quad_edge_chunk(q, lane);
+        const u32x4 edge = load_chunk_g<false>(q.p + ce);
+        uint32_t acc = quad_scan_interior<kQuadLoads, NT>(q, lane);
+        acc |= quad_edge_used(q, lane) ? or4(quad_edge_xor(q, ce, edge)) : 0u;
         uint32_t first = kNone, count = 0;
         if (__any(acc != 0u)) {  // rare: exact re-read of the dirty lanes' own chunks
-            if (acc != 0u) {
-                if constexpr ((LP & kQuadEdgesInRound) != 0) quad_scan_exact_eir<NT>(q, lane, first, count);
-                else quad_scan_exact<NT>(q, lane, first, count);
-            }
+            if (acc != 0u) quad_scan_exact<NT>(q, lane, first, count);
             quad_team_reduce(first, count);
         }
         if (lane == 0u && live) {
@@ -1490,131 +1046,10 @@ __global__ void __launch_bounds__(kBlock)
                     atomicMin(&conn_first_fail[d.conn_index], i);
             }
         }
-        quad_flush_outputs(qout[team >> 2], i, w.end, results, nullptr);
+        quad_flush_results(qout[team >> 2], i, w.end, results);
         w.i = inext;
     }
     qc.flush<TEAMS>(ctr, team, lane, counters);
-}
-
-// ---------------------------------------------------------------------------------------------
-// One wave per buffer, software-pipelined across buffers (datagram-sized spans):
-// the loads of the next buffer (edge/head chunks + one interior round of U
-// chunks per lane) are in flight while the current buffer is compared, so a wave
-// keeps two buffers' bytes in the memory system instead of one. A span whose
-// interior does not fit one round finishes its remaining rounds synchronously.
-template <int U, bool NT>
-struct Pending {
-    Span s;
-    u32x4 edge;
-    u32x4 d[U];
-    bool one_round;
-};
-
-template <int U, bool NT>
-__device__ __forceinline__ void pipe_issue(const Span& s, uint32_t lane, Pending<U, NT>& p)
-{
-    p.s = s;
-    const __amdgpu_buffer_rsrc_t r = span_rsrc(s);
-    const uint32_t ce = edge_chunk_of(s, lane);
-    p.edge = buf_load<NT>(r, edge_chunk_used(s, lane) ? ce * 16u : 0x7FFFFFF0u, 0u);
-    const uint32_t c_end = s.nchunks > 0u ? s.nchunks - 1u : 0u;
-    p.one_round = s.nchunks < 3u || c_end <= s.cb0 + (uint32_t)(64 * U);
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        // interior chunk cb0 + u*64 + lane; past the span -> out of range -> 0, no request
-        const uint32_t c = s.cb0 + (uint32_t)(u * 64) + lane;
-        p.d[u] = buf_load<NT>(r, (s.nchunks >= 3u && c < c_end) ? c * 16u : 0x7FFFFFF0u, 0u);
-    }
-}
-
-template <int U, bool NT>
-__device__ __forceinline__ uint32_t pipe_consume(const Pending<U, NT>& p, uint32_t lane)
-{
-    const Span& s = p.s;
-    uint32_t acc = 0;
-    if (s.nchunks >= 3u) {
-        const uint32_t c_end = s.nchunks - 1u;
-        const uint32_t B = chunk_base(s, s.cb0 + lane);
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t c = s.cb0 + (uint32_t)(u * 64) + lane;
-            const uint32_t any = or4(p.d[u] ^ expected_step<64, U>(B, u, s.sh));
-            acc |= c < c_end ? any : 0u;
-        }
-        if (!p.one_round) {  // rare for datagrams: the rest of the interior, round by round
-            Span t = s;
-            t.cb0 = s.cb0 + (uint32_t)(64 * U);
-            acc |= scan_interior<64, U, NT, false>(t, span_rsrc(s), lane);
-        }
-    }
-    const uint32_t ce = edge_chunk_of(s, lane);
-    const u32x4 x = chunk_xor(s, ce, p.edge) & range_mask(ce == 0u ? s.lo : 0u, ce == s.nchunks - 1u ? s.hi_last : 16u);
-    acc |= edge_chunk_used(s, lane) ? or4(x) : 0u;
-    return acc;
-}
-
-template <int U, bool NT>
-__global__ void __launch_bounds__(kBlock)
-    verify_wave_pipe_kernel(const uint8_t* __restrict__ arena, uint64_t arena_bytes,
-                            const cts_buf_desc* __restrict__ descs, uint32_t n, cts_verify_result* __restrict__ results,
-                            uint64_t* __restrict__ counters, uint32_t* __restrict__ conn_first_fail, uint32_t n_conns)
-{
-    constexpr int WAVES = kBlock / 64;
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t nw = gridDim.x * WAVES;
-    __shared__ uint64_t ctr[WAVES][5];
-    zero_counters<WAVES>(ctr);
-    uint32_t i = blockIdx.x * WAVES + wave;
-    if (i < n) {
-        // a bad descriptor becomes an empty span (no loads); its record is written at consume time
-        auto span_of = [&](const cts_buf_desc& d, bool& bad) {
-            bad = desc_bad(d, arena_bytes);
-            cts_buf_desc e = d;
-            if (bad) {
-                e.byte_offset = 0;
-                e.length = 0;
-                e.skip_head = 0;
-            }
-            return make_span(arena, e);
-        };
-        cts_buf_desc dc = descs[i];
-        bool bad_c;
-        Pending<U, NT> cur;
-        pipe_issue<U, NT>(span_of(dc, bad_c), lane, cur);
-        cts_buf_desc dn;
-        if (i + nw < n) dn = descs[i + nw];
-        for (; i < n; i += nw) {
-            Pending<U, NT> nxt;
-            bool bad_n = true;
-            const cts_buf_desc dnn = dn;
-            if (i + nw < n) {
-                pipe_issue<U, NT>(span_of(dnn, bad_n), lane, nxt);
-                if (i + 2 * nw < n) dn = descs[i + 2 * nw];
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            if (bad_c) {
-                if (lane == 0) write_bad(results, i);
-            } else {
-                const uint32_t acc = pipe_consume<U, NT>(cur, lane);
-                uint32_t first = kNone, count = 0;
-                if (span_giant(cur.s)) {  // >= 2 GiB: the prefetched round is discarded, 64-bit exact pass
-                    scan_giant_exact<64, NT>(cur.s, lane, first, count);
-                    first = wave_min(first);
-                    count = wave_sum(count);
-                } else if (__any(acc != 0u)) {
-                    if (acc != 0u) scan_exact_owned<64, 2, NT>(cur.s, lane, first, count);
-                    first = wave_min(first);
-                    count = wave_sum(count);
-                }
-                if (lane == 0) finish_buffer(cur.s, dc, i, first, count, results, ctr[wave], conn_first_fail, n_conns);
-            }
-            cur = nxt;
-            dc = dnn;
-            bad_c = bad_n;
-        }
-    }
-    flush_counters<WAVES>(counters, ctr);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1756,127 +1191,13 @@ __global__ void __launch_bounds__(kBlock) fill_span_kernel(uint8_t* __restrict__
 }
 
 // ---------------------------------------------------------------------------------------------
-// MediaStream (UDP) datagrams: one wave per datagram, like verify_wave_kernel.
-// Receive: parse + validate the header (ctsMediaStreamProtocol.hpp:284-329), then
-// verify the payload of DATA datagrams at pattern offset 0 after the 26-byte
-// header (ctsIOPatternMediaStream.cpp:185-192).
-__device__ __forceinline__ int64_t load_i64_unaligned(const uint8_t* p)
-{
-    uint64_t v = 0;
-#pragma unroll
-    for (int b = 0; b < 8; ++b) v |= (uint64_t)p[b] << (8 * b);
-    return (int64_t)v;
-}
-
-// Lane l (< 26) holds header byte l (0 past the completed bytes); returns the
-// little-endian i64 at byte offset `at` via v_readlane (wave-uniform, no memory).
-__device__ __forceinline__ int64_t header_i64(uint32_t hb, int at)
-{
-    uint64_t v = 0;
-#pragma unroll
-    for (int b = 0; b < 8; ++b) v |= (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hb, at + b) << (8 * b);
-    return (int64_t)v;
-}
-
-template <int U, bool NT>
-__global__ void __launch_bounds__(kBlock)
-    media_stream_verify_kernel(const uint8_t* __restrict__ arena, uint64_t arena_bytes,
-                               const cts_buf_desc* __restrict__ descs, uint32_t n,
-                               cts_datagram_record* __restrict__ records, cts_verify_result* __restrict__ results,
-                               uint64_t* __restrict__ counters)
-{
-    constexpr int WAVES = kBlock / 64;
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t nw = gridDim.x * WAVES;
-    __shared__ uint64_t ctr[WAVES][5];
-    zero_counters<WAVES>(ctr);
-    uint32_t i = blockIdx.x * WAVES + wave;
-    cts_buf_desc dn;
-    if (i < n) dn = descs[i];
-    for (; i < n; i += nw) {
-        cts_buf_desc d = dn;
-        if (i + nw < n) dn = descs[i + nw];
-        const uint32_t completed = d.length;
-        const bool bad = d.byte_offset > arena_bytes || arena_bytes - d.byte_offset < (uint64_t)completed;
-        // The header bytes and the payload stream are loaded together: the payload is
-        // verified speculatively (as a DATA datagram) while the header is in flight, and
-        // discarded if the header says otherwise — no dependent round trip per datagram.
-        // Lane l < 26 loads header byte l through a resource covering only the completed
-        // bytes (out of range -> 0, no request).
-        const __amdgpu_buffer_rsrc_t hr = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<uint8_t*>(arena + (bad ? 0 : d.byte_offset)), (short)0, (int)(bad ? 0u : completed), 0x00020000);
-        const uint32_t hb = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(hr, lane < CTS_UDP_DATA_HEADER_LENGTH ? lane : 0x7FFFFFF0u, 0u, 0);
-        const bool maybe_data = !bad && completed >= CTS_UDP_DATA_HEADER_LENGTH;
-        d.skip_head = CTS_UDP_DATA_HEADER_LENGTH;
-        d.expected_pattern_offset = 0;
-        if (!maybe_data) {
-            d.byte_offset = 0;  // an empty span: scan_buffer issues no in-range loads
-            d.length = CTS_UDP_DATA_HEADER_LENGTH;
-        }
-        const Span s = make_span(arena, d);
-        const bool giant = span_giant(s);  // >= 2 GiB: 64-bit exact pass (below)
-        const uint32_t acc = giant ? 0u : scan_buffer<64, U, NT>(s, lane);
-        // header: ctsMediaStreamMessage::ValidateBufferLengthFromTask (ctsMediaStreamProtocol.hpp:284-329)
-        uint32_t flag = 0, kind;
-        if (bad) {
-            kind = CTS_DGRAM_BAD_DESC;
-        } else if (completed == 0u) {
-            kind = CTS_DGRAM_ZERO;
-        } else if (completed < CTS_UDP_FLAG_LENGTH) {
-            kind = CTS_DGRAM_SHORT;
-        } else {
-            flag = (uint32_t)__builtin_amdgcn_readlane((int)hb, 0) | ((uint32_t)__builtin_amdgcn_readlane((int)hb, 1) << 8);
-            if (flag == CTS_UDP_FLAG_DATA)
-                kind = completed < CTS_UDP_DATA_HEADER_LENGTH ? CTS_DGRAM_SHORT : CTS_DGRAM_DATA;
-            else if (flag == CTS_UDP_FLAG_ID)
-                kind = completed < CTS_UDP_CONNECTION_ID_HEADER_LENGTH ? CTS_DGRAM_SHORT : CTS_DGRAM_ID;
-            else
-                kind = CTS_DGRAM_UNKNOWN;
-        }
-        const bool data = kind == CTS_DGRAM_DATA;
-        if (records != nullptr && lane == 0) {
-            cts_datagram_record rec;
-            rec.sequence_number = data ? header_i64(hb, 2) : 0;   // GetSequenceNumberFromTask
-            rec.sender_qpc = data ? header_i64(hb, 8) : 0;        // ctsIOPatternMediaStream.cpp:218
-            rec.sender_qpf = data ? header_i64(hb, 16) : 0;       // :219
-            rec.flag = (uint16_t)flag;
-            rec.kind = (uint8_t)kind;
-            rec.reserved = 0;
-            rec.completed_bytes = completed;
-            records[i] = rec;
-        }
-        if (!data) {
-            if (results != nullptr && lane == 0) {
-                cts_verify_result r{};
-                r.flags = kind == CTS_DGRAM_BAD_DESC ? CTS_RESULT_FLAG_BAD_DESC : CTS_RESULT_FLAG_NOT_DATA;
-                results[i] = r;
-            }
-            continue;
-        }
-        uint32_t first = kNone, count = 0;
-        if (giant) {
-            scan_giant_exact<64, NT>(s, lane, first, count);
-            first = wave_min(first);
-            count = wave_sum(count);
-        } else if (__any(acc != 0u)) {
-            if (acc != 0u) scan_exact_owned<64, 2, NT>(s, lane, first, count);
-            first = wave_min(first);
-            count = wave_sum(count);
-        }
-        if (lane == 0) finish_buffer(s, d, i, first, count, results, ctr[wave], nullptr, 0);
-    }
-    flush_counters<WAVES>(counters, ctr);
-}
-
-// MediaStream receive, four datagrams per wave (16-lane teams; see verify_quad_kernel).
-// Team lane j loads header bytes j and j + 16 (bytes past the completed length read as 0,
-// from the dummy address) alongside the speculative DATA payload stream; the header dwords
-// reach the team leader through lane shuffles, with no dependent memory round trip.
-__device__ __forceinline__ uint8_t load_byte_g(const uint8_t* p)
-{
-    return *(const uint8_t __attribute__((address_space(1)))*)p;
-}
+// MediaStream (UDP) datagrams, four per wave (16-lane teams; see verify_quad_kernel).
+// Receive: parse + validate the header (ctsMediaStreamProtocol.hpp:284-329), then verify the payload of
+// DATA datagrams at pattern offset 0 after the 26-byte header (ctsIOPatternMediaStream.cpp:185-192).
+// Team lanes 0..2 load the 16-byte chunks holding the header alongside the speculative DATA payload
+// stream; the header dwords reach the team leader through DPP row shifts, with no dependent memory round
+// trip (header bytes by byte loads and lane shuffles, and one wave per datagram, measured slower:
+// tools/media_stream_probe.py).
 
 // Team lane 0 receives dword c of lane `from`'s u32x4 (from = 1, 2) within its 16-lane DPP
 // row (row_shl:from; a VALU move, no LDS round trip).
@@ -1886,7 +1207,7 @@ __device__ __forceinline__ uint32_t row_shl(uint32_t v)
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x100 | FROM, 0xF, 0xF, true);
 }
 
-// Header dwords of the 16-B-chunk form (HDR16): team lanes 0..2 each hold one 16-byte chunk of
+// Header dwords: team lanes 0..2 each hold one 16-byte chunk of
 // the 48-byte window starting at the datagram's 16-byte-aligned base; header byte b sits at
 // window byte ho + b. Returns dwords H[0..5] = header bytes 0..23 on team lane 0.
 __device__ __forceinline__ void header_dwords_hdr16(u32x4 own, uint32_t ho, uint32_t (&H)[6])
@@ -1930,9 +1251,6 @@ __device__ __forceinline__ void ms_datagram(const MsSource& src, uint32_t i, uin
     }
 }
 
-// HDR16 = false: header bytes j and j + 16 by byte loads on every team lane, dwords gathered by
-// lane shuffles (ms_variant 1). HDR16 = true: three 16-byte header chunk loads on team lanes
-// 0..2, gathered on lane 0 by DPP row shifts; the DATA verdict is broadcast (ms_variant 2).
 // The team leader's staging of its datagram's outputs into slot o (a QuadOut, or a ring slot).
 #define CTS_MS_STAGE(o)                                                                                           \
     do {                                                                                                          \
@@ -1973,10 +1291,9 @@ __device__ __forceinline__ void ms_datagram(const MsSource& src, uint32_t i, uin
             }                                                                                                     \
     } while (0)
 
-// RING > 0: outputs staged in a per-wave ring of RING rounds and written every RING rounds (QuadRing).
+// RING: outputs staged in a per-wave ring of RING rounds and written every RING rounds (QuadRing); 0 only with
+// FRAMES, which writes no per-datagram outputs.
 // STATUS: records points at 16-byte cts_datagram_status entries (results unused).
-// FAILMARK: records points at statuses ms_status_gather_kernel already wrote; only a corrupt DATA datagram's
-// pass byte is cleared (a rare byte store: the read stream runs as if it wrote nothing).
 // FRAMES (cts_media_stream_verify_frames): the client's accounting of the batch, summed on the GPU. The jitter window
 // does not move between two render ticks, so CompleteTaskBackToPattern (ctsIOPatternMediaStream.cpp:150-272) over a
 // batch is a sum over its clean DATA datagrams: bits received, the bytes of each frame in the window, an error frame
@@ -1992,15 +1309,16 @@ struct MsFrames {
     uint64_t* frame_bytes;  // [frames]
 };
 
-// EP: the header chunks and the payload's edge chunks, loaded ahead of the rounds, with the default (L2-allocating)
-// policy (kQuadEdgePlain: nontemporal, their lines were often gone from L2 when the rounds asked again).
-template <int U, bool NT, bool ALIGN, bool HDR16, bool CONTIG = false, bool STRIDED = false, int RING = 0,
-          bool STATUS = false, bool FAILMARK = false, bool EP = true, bool FRAMES = false>
+// The header chunks and the payload's edge chunks are loaded ahead of the rounds with the default (L2-allocating)
+// policy, as verify_quad_kernel's edges (nontemporal, their lines were often gone from L2 when the rounds asked again).
+template <bool NT, bool STRIDED, int RING, bool STATUS = false, bool FRAMES = false>
 __global__ void __launch_bounds__(kBlock)
     media_stream_verify_quad_kernel(const uint8_t* __restrict__ arena, uint64_t arena_bytes, MsSource src, uint32_t n,
                                     void* __restrict__ records, cts_verify_result* __restrict__ results,
-                                    uint64_t* __restrict__ counters, uint32_t per = 0, MsFrames fr = MsFrames{})
+                                    uint64_t* __restrict__ counters, uint32_t per, MsFrames fr = MsFrames{})
 {
+    static_assert(RING > 0 || FRAMES, "per-datagram outputs go through the per-wave ring");
+    constexpr int U = kQuadLoads;
     constexpr int TEAMS = kBlock / kQuadTeam;
     __shared__ uint64_t s_fbytes[FRAMES ? kFramesLds : 1];  // FRAMES: this workgroup's bytes per window slot
     __shared__ uint64_t s_ftot[4];                          // FRAMES: bits, error frames, datagrams, exceptions
@@ -2013,7 +1331,6 @@ __global__ void __launch_bounds__(kBlock)
         __syncthreads();
     }
     __shared__ uint64_t ctr[TEAMS][5];
-    __shared__ QuadOut qout[RING ? 1 : kBlock / 64];
     using RingSlot = typename std::conditional<STATUS, QuadStatusOut, QuadOut>::type;
     __shared__ QuadRing<RING ? RING : 1, RingSlot> qring[RING ? kBlock / 64 : 1];
     uint32_t rs = 0;  // RING: this wave's next ring slot (wave-uniform)
@@ -2022,9 +1339,8 @@ __global__ void __launch_bounds__(kBlock)
     // dummy target of an empty span's clamped loads: 16-byte-aligned bytes the launch owns
     const void* dummy = STRIDED ? reinterpret_cast<const void*>(arena)
                                 : reinterpret_cast<const void*>(((uintptr_t)src.descs + 15u) & ~(uintptr_t)15u);
-    const uint8_t* dummy8 = reinterpret_cast<const uint8_t*>(dummy);
     QCounters qc;
-    QuadWalk<CONTIG, TEAMS> w(n, per, team);
+    QuadWalk<TEAMS> w(n, per, team);
     uint64_t noff;
     uint32_t nlen;
     ms_datagram<STRIDED>(src, w.i < n ? w.i : n - 1u, noff, nlen);
@@ -2039,54 +1355,24 @@ __global__ void __launch_bounds__(kBlock)
                          (STRIDED && completed > src.stride);
         const bool in = live && !bad;
         const uint8_t* dg = arena + (in ? doff : 0u);
-        uint32_t hb0 = 0, hb1 = 0;
-        bool h0 = false, h1 = false;
         u32x4 hch = u32x4{0u, 0u, 0u, 0u};
         const uint32_t ho = (uint32_t)((uintptr_t)dg & 15u);
-        if constexpr (HDR16) {
-            // header chunks: the 16-byte-aligned chunks holding bytes [0, min(completed, 26)); a
-            // chunk is loaded only if it holds one of those bytes (never past the datagram's page)
-            const uint32_t hbytes = completed < CTS_UDP_DATA_HEADER_LENGTH ? completed : CTS_UDP_DATA_HEADER_LENGTH;
-            if (in && 16u * lane < ho + hbytes)
-                hch = load_chunk_g<EP ? false : NT>(reinterpret_cast<const u32x4*>(dg - ho) + lane);
-        } else {
-            // header bytes j and j + 16 of this team's datagram (0 past the completed bytes)
-            h0 = in && lane < completed;
-            h1 = in && lane + 16u < CTS_UDP_DATA_HEADER_LENGTH && lane + 16u < completed;
-            hb0 = load_byte_g(h0 ? dg + lane : dummy8);
-            hb1 = load_byte_g(h1 ? dg + lane + 16u : dummy8);
-        }
+        // header chunks: the 16-byte-aligned chunks holding bytes [0, min(completed, 26)); a
+        // chunk is loaded only if it holds one of those bytes (never past the datagram's page)
+        const uint32_t hbytes = completed < CTS_UDP_DATA_HEADER_LENGTH ? completed : CTS_UDP_DATA_HEADER_LENGTH;
+        if (in && 16u * lane < ho + hbytes) hch = load_chunk_g<false>(reinterpret_cast<const u32x4*>(dg - ho) + lane);
         // speculative DATA payload: [26, completed) at pattern offset 0
         const bool maybe_data = in && completed >= CTS_UDP_DATA_HEADER_LENGTH;
-        const QSpan q = quad_span<ALIGN>(dg + CTS_UDP_DATA_HEADER_LENGTH,
-                                         maybe_data ? completed - CTS_UDP_DATA_HEADER_LENGTH : 0u, 0u, dummy);
+        const QSpan q = quad_span(dg + CTS_UDP_DATA_HEADER_LENGTH, maybe_data ? completed - CTS_UDP_DATA_HEADER_LENGTH : 0u,
+                                  0u, dummy);
         const uint32_t ce = quad_edge_chunk(q, lane);
-        const u32x4 edge = load_chunk_g<EP ? false : NT>(q.p + ce);
+        const u32x4 edge = load_chunk_g<false>(q.p + ce);
         uint32_t acc = quad_scan_interior<U, NT>(q, lane);
         acc |= quad_edge_used(q, lane) ? or4(quad_edge_xor(q, ce, edge)) : 0u;
+        // header dwords, valid on team lane 0; bytes past the completed length are never read (the flag needs
+        // completed >= 2, the DATA fields completed >= 26)
         uint32_t H[6];
-        if constexpr (HDR16) {
-            // valid on team lane 0; bytes past the completed length are never read (the flag needs
-            // completed >= 2, the DATA fields completed >= 26)
-            header_dwords_hdr16(hch, ho, H);
-        } else {
-            // header dwords: lane 4k packs bytes 4k..4k+3 of each half; every lane gathers
-            hb0 = h0 ? hb0 : 0u;
-            hb1 = h1 ? hb1 : 0u;
-            uint32_t w0 = hb0, w1 = hb1;
-#pragma unroll
-            for (int b = 1; b < 4; ++b) {
-                w0 |= (uint32_t)__shfl_down((int)hb0, b, kQuadTeam) << (8 * b);
-                w1 |= (uint32_t)__shfl_down((int)hb1, b, kQuadTeam) << (8 * b);
-            }
-            // (every lane needs them: the DATA verdict gates each lane's differences)
-            H[0] = (uint32_t)__shfl((int)w0, 0, kQuadTeam);     // bytes 0..3
-            H[1] = (uint32_t)__shfl((int)w0, 4, kQuadTeam);     // 4..7
-            H[2] = (uint32_t)__shfl((int)w0, 8, kQuadTeam);     // 8..11
-            H[3] = (uint32_t)__shfl((int)w0, 12, kQuadTeam);    // 12..15
-            H[4] = (uint32_t)__shfl((int)w1, 0, kQuadTeam);     // 16..19
-            H[5] = (uint32_t)__shfl((int)w1, 4, kQuadTeam);     // 20..23
-        }
+        header_dwords_hdr16(hch, ho, H);
         // header: ctsMediaStreamMessage::ValidateBufferLengthFromTask (ctsMediaStreamProtocol.hpp:284-329)
         uint32_t flag = 0, kind;
         if (bad) {
@@ -2104,20 +1390,12 @@ __global__ void __launch_bounds__(kBlock)
             else
                 kind = CTS_DGRAM_UNKNOWN;
         }
-        if constexpr (HDR16) kind = (uint32_t)__shfl((int)kind, 0, kQuadTeam);  // lane 0's verdict
+        kind = (uint32_t)__shfl((int)kind, 0, kQuadTeam);  // lane 0's verdict, for every lane
         const bool data = kind == CTS_DGRAM_DATA;
         uint32_t first = kNone, count = 0;
         if (__any(acc != 0u && data)) {  // rare: exact re-read (non-DATA teams' differences are discarded)
             if (acc != 0u && data) quad_scan_exact<NT>(q, lane, first, count);
             quad_team_reduce(first, count);
-        }
-        if constexpr (FAILMARK) {
-            if (lane == 0u && live && data) {
-                if (records != nullptr && first != kNone) reinterpret_cast<uint8_t*>(records)[16ull * i + 15u] = 0u;
-                qc.add(q.len, first == kNone, count);
-            }
-            w.i = inext;
-            continue;
         }
         if constexpr (FRAMES) {
             if (lane == 0u && live) {
@@ -2149,17 +1427,11 @@ __global__ void __launch_bounds__(kBlock)
             w.i = inext;
             continue;
         }
-        if (lane == 0u && live) {
-            if constexpr (RING > 0) {
+        if constexpr (RING > 0) {
+            if (lane == 0u && live) {
                 auto& o_ = qring[team >> 2].slot[rs];
                 CTS_MS_STAGE(o_);
-            } else {
-                CTS_MS_STAGE(qout[team >> 2]);
             }
-        }
-        if constexpr (RING == 0) {
-            quad_flush_outputs<STATUS ? 4 : 8>(qout[team >> 2], i, w.end, STATUS ? nullptr : results, records);
-        } else {
             auto& g = qring[team >> 2];
             const uint32_t i0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)i);
             if ((threadIdx.x & 63u) == 0u) g.i0[rs] = i0;
@@ -2195,64 +1467,6 @@ __global__ void __launch_bounds__(kBlock)
             atomicAdd((unsigned long long*)&sh[threadIdx.x], (unsigned long long)s_ftot[threadIdx.x]);
     }
     qc.flush<TEAMS>(ctr, team, lane, counters);
-}
-
-// The header half of a two-pass compact receive (tuning build, ms variant 7): one lane per datagram
-// loads the one or two 16-byte chunks holding header bytes [0, min(completed, 10)), classifies the datagram
-// as the receive kernel does (ValidateBufferLengthFromTask, ctsMediaStreamProtocol.hpp:284-329) and writes its
-// 16-byte status with pass = 1 for DATA. The payload pass then runs without outputs and clears pass for
-// corrupt DATA datagrams only (FAILMARK). The idea: take the writes out of the payload pass (writing 16 B per
-// datagram as it reads costs it 11-20 %). Measured slower overall: see launch_media_stream_status.
-template <bool STRIDED>
-__global__ void __launch_bounds__(kBlock)
-    ms_status_gather_kernel(const uint8_t* __restrict__ arena, uint64_t arena_bytes, MsSource src, uint32_t n,
-                            uint32_t* __restrict__ status)
-{
-    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
-    uint64_t doff;
-    uint32_t completed;
-    ms_datagram<STRIDED>(src, i, doff, completed);
-    const bool bad = doff > arena_bytes || arena_bytes - doff < (uint64_t)completed || (STRIDED && completed > src.stride);
-    uint32_t kind, flag = 0, s0 = 0, s1 = 0;
-    if (bad) {
-        kind = CTS_DGRAM_BAD_DESC;
-    } else if (completed == 0u) {
-        kind = CTS_DGRAM_ZERO;
-    } else if (completed < CTS_UDP_FLAG_LENGTH) {
-        kind = CTS_DGRAM_SHORT;
-    } else {
-        const uint8_t* dg = arena + doff;
-        const uint32_t ho = (uint32_t)((uintptr_t)dg & 15u);
-        const u32x4* c0 = reinterpret_cast<const u32x4*>(dg - ho);
-        const uint32_t hbytes = completed < 10u ? completed : 10u;  // flag + sequence number
-        const u32x4 a = load_chunk_g<false>(c0);
-        const u32x4 b = ho + hbytes > 16u ? load_chunk_g<false>(c0 + 1) : u32x4{0u, 0u, 0u, 0u};
-        const uint32_t W[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
-        const uint32_t j0 = ho >> 2, sh = ho & 3u;
-        uint32_t V[4];
-#pragma unroll
-        for (int m = 0; m < 4; ++m)
-            V[m] = j0 == 0u ? W[m] : (j0 == 1u ? W[m + 1] : (j0 == 2u ? W[m + 2] : W[m + 3]));
-        const uint32_t H0 = __builtin_amdgcn_alignbyte(V[1], V[0], sh), H1 = __builtin_amdgcn_alignbyte(V[2], V[1], sh),
-                       H2 = __builtin_amdgcn_alignbyte(V[3], V[2], sh);
-        flag = H0 & 0xFFFFu;
-        if (flag == CTS_UDP_FLAG_DATA)
-            kind = completed < CTS_UDP_DATA_HEADER_LENGTH ? CTS_DGRAM_SHORT : CTS_DGRAM_DATA;
-        else if (flag == CTS_UDP_FLAG_ID)
-            kind = completed < CTS_UDP_CONNECTION_ID_HEADER_LENGTH ? CTS_DGRAM_SHORT : CTS_DGRAM_ID;
-        else
-            kind = CTS_DGRAM_UNKNOWN;
-        if (kind == CTS_DGRAM_DATA) {
-            s0 = (H0 >> 16) | (H1 << 16);
-            s1 = (H1 >> 16) | (H2 << 16);
-        }
-    }
-    uint32_t* o = status + 4ull * i;
-    o[0] = s0;
-    o[1] = s1;
-    o[2] = completed;
-    o[3] = flag | (kind << 16) | (kind == CTS_DGRAM_DATA ? 1u << 24 : 0u);
 }
 
 // Send: header {u16 0, i64 seq, i64 qpc, i64 qpf} + P[0 .. length-26) per datagram
@@ -2313,22 +1527,23 @@ __device__ __forceinline__ void ms_fill_one(uint8_t* arena, uint64_t arena_bytes
     for (uint32_t c = lane; c < nchunks; c += 64u) fill_chunk<NTS>(p, c, nchunks, q0, lo, hi_last);
 }
 
-// Small buffers through descriptors, batched: each workgroup walks one contiguous range of descriptors in batches of
-// kFillBatch, staged in LDS (and, MS, their MediaStream headers), and each wave fills a contiguous quarter of the
-// batch, one buffer at a time. Nothing is loaded inside the per-buffer loop: the wave-per-buffer kernels wait for a
-// descriptor (a scalar load of a far-away line: ~1 us) before every buffer's stores, which bounded them at
-// 3.4-3.9 TB/s on 16 M x 1472 B (tools/media_stream_probe.py). MS: whole MediaStream datagrams
-// (cts_media_stream_fill); otherwise the payload fill of cts_fill's small-buffer path.
+// Whole MediaStream datagrams through descriptors (cts_media_stream_fill), batched: each workgroup walks one
+// contiguous range of descriptors in batches of kFillBatch, staged in LDS with their headers, and each wave fills a
+// contiguous quarter of the batch, one datagram at a time. Nothing is loaded inside the per-datagram loop: the
+// wave-per-datagram form waits for a descriptor (a scalar load of a far-away line: ~1 us) before every datagram's
+// stores, which bounded it at 3.4-3.9 TB/s on 16 M x 1472 B (6.8-7.0 ms, tools/media_stream_probe.py). (The same
+// batching measured slower for cts_fill's payload-only small buffers, whose first chunk is a partial write either
+// way: 6.9 against 6.1-6.8 ms per 16 M x 1446 B, tools/ring_fill_probe.hip.)
 constexpr uint32_t kFillBatch = kBlock;
 
-template <bool NTS, bool MS>
+template <bool NTS>
 __global__ void __launch_bounds__(kBlock)
     fill_batched_kernel(uint8_t* __restrict__ arena, uint64_t arena_bytes, const cts_buf_desc* __restrict__ descs,
                         const cts_datagram_header* __restrict__ headers, uint32_t n)
 {
     constexpr uint32_t WAVES = kBlock / 64;
     __shared__ cts_buf_desc ds[kFillBatch];
-    __shared__ cts_datagram_header hs[MS ? kFillBatch : 1];
+    __shared__ cts_datagram_header hs[kFillBatch];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t per_wg = (uint32_t)(((uint64_t)n + gridDim.x - 1u) / gridDim.x);
@@ -2339,41 +1554,19 @@ __global__ void __launch_bounds__(kBlock)
         __syncthreads();  // every wave is done with the previous batch
         if (threadIdx.x < nb) {
             ds[threadIdx.x] = descs[d0 + threadIdx.x];
-            if constexpr (MS) hs[threadIdx.x] = headers[d0 + threadIdx.x];
+            hs[threadIdx.x] = headers[d0 + threadIdx.x];
         }
         __syncthreads();
         const uint32_t q = (nb + WAVES - 1u) / WAVES;
         const uint32_t t1 = (wave + 1u) * q < nb ? (wave + 1u) * q : nb;
         for (uint32_t t = wave * q; t < t1; ++t) {
-            const cts_buf_desc d = ds[t];
-            if constexpr (MS) {
-                const cts_datagram_header h = hs[t];
-                ms_fill_one<NTS>(arena, arena_bytes, d, (uint64_t)h.sequence_number, (uint64_t)h.qpc, (uint64_t)h.qpf,
-                                 lane);
-            } else {
-                fill_one<64, 2, NTS>(arena, arena_bytes, d, lane);
-            }
+            const cts_datagram_header h = hs[t];
+            ms_fill_one<NTS>(arena, arena_bytes, ds[t], (uint64_t)h.sequence_number, (uint64_t)h.qpc, (uint64_t)h.qpf,
+                             lane);
         }
     }
 }
 
-#if CTS_TUNING
-// the round-3 per-descriptor MediaStream fill (one wave per datagram, grid-strided, descriptor and header loaded
-// before each datagram's stores): 6.8-7.0 ms per 16 M x 1472 B; tuning build (CTS_MS_FILL_BATCHED=0)
-template <bool NTS>
-__global__ void __launch_bounds__(kBlock)
-    media_stream_fill_kernel(uint8_t* __restrict__ arena, uint64_t arena_bytes, const cts_buf_desc* __restrict__ descs,
-                             const cts_datagram_header* __restrict__ headers, uint32_t n)
-{
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    for (uint32_t i = blockIdx.x * (kBlock / 64) + wave; i < n; i += gridDim.x * (kBlock / 64)) {
-        const cts_datagram_header h = headers[i];
-        ms_fill_one<NTS>(arena, arena_bytes, descs[i], (uint64_t)h.sequence_number, (uint64_t)h.qpc, (uint64_t)h.qpf,
-                         lane);
-    }
-}
-#endif
 
 // MediaStream sender over a ring (cts_media_stream_fill_strided): datagram i occupies [i * stride, i * stride +
 // lengths[i]) of a 16-byte aligned arena, stride a multiple of 16, so the ring is a flat array of 16-byte chunks and
@@ -2524,20 +1717,9 @@ static inline uint32_t grid_for(uint32_t n, int teams_per_block, const LaunchGeo
     return (uint32_t)(g == 0 ? 1 : g);
 }
 
-#if CTS_TUNING
-// workgroup-per-buffer grid for a WIN-window walk: grid_for's size rounded down to a multiple of
-// WIN (at least WIN), so every window gets gridDim.x / WIN workgroups
-static inline uint32_t grid_win(uint32_t n, uint32_t win, const LaunchGeometry& geo)
-{
-    const uint32_t g = grid_for(n, 1, geo);
-    return g < win ? win : g - g % win;
-}
-#endif
 
-#define CTS_VERIFY_ARGS arena, arena_bytes, descs, n, results, counters, conn_first_fail, n_conns
-#define CTS_QUAD_ARGS arena, arena_bytes, VSource{descs, nullptr, 0u, 0u, 0u, 0u}, n, results, counters, conn_first_fail, n_conns
 
-// Chunked launch of a four-buffers-per-wave kernel (QuadWalk<true>): chunk = geo.small_chunk
+// Chunked launch of a four-buffers-per-wave kernel (QuadWalk): chunk = geo.small_chunk
 // buffers (rounded up to the block's 16 teams); 0 = one block-contiguous range per block, every
 // block but the last with the same count.
 struct ContigGrid {
@@ -2563,125 +1745,13 @@ static void launch_verify_nt(const uint8_t* arena, uint64_t arena_bytes, const c
                              uint32_t n_conns, hipStream_t stream, const LaunchGeometry& geo)
 {
     if (small) {
-        // small_variant: 0 = one wave per buffer U2, 1 = U1, 2 = U4 (chunks per lane per round),
-        // 3 = pipelined across buffers U2, 4 = pipelined U1,
-        // 5 = four buffers per wave (16-lane teams) U6, 6 = same, line-aligned rounds U7,
-        // 7 = line-aligned U6, 8 = U4, 9 = variant 7 walking block-contiguous buffer ranges
-#if CTS_TUNING
-        const uint32_t grid = grid_for(n, kBlock / 64, geo);
-        const uint32_t qgrid = grid_for(n, kBlock / kQuadTeam, geo);
-        switch (geo.small_variant) {
-        case 5: verify_quad_kernel<6, NT, false><<<qgrid, kBlock, 0, stream>>>(CTS_QUAD_ARGS); break;
-        case 6: verify_quad_kernel<7, NT, true><<<qgrid, kBlock, 0, stream>>>(CTS_QUAD_ARGS); break;
-        case 7: verify_quad_kernel<6, NT, true><<<qgrid, kBlock, 0, stream>>>(CTS_QUAD_ARGS); break;
-        case 8: verify_quad_kernel<4, NT, false><<<qgrid, kBlock, 0, stream>>>(CTS_QUAD_ARGS); break;
-        case 9: {
-            const ContigGrid cg = contig_grid(n, geo);
-            verify_quad_kernel<6, NT, true, true><<<cg.grid, kBlock, 0, stream>>>(CTS_QUAD_ARGS, cg.per);
-            break;
-        }
-        case 10:
-        case 11:
-        case 12:
-        case 13:
-        case 14:
-        case 15: {  // variant 9 with line policy LP = 1, 2, 3, 4, 5, 8 (quad_scan_interior)
-            const ContigGrid cg = contig_grid(n, geo);
-#define CTS_QUAD_LP(LP) verify_quad_kernel<6, NT, true, true, false, LP><<<cg.grid, kBlock, 0, stream>>>(CTS_QUAD_ARGS, cg.per)
-            switch (geo.small_variant) {
-            case 10: CTS_QUAD_LP(1); break;
-            case 11: CTS_QUAD_LP(2); break;
-            case 12: CTS_QUAD_LP(3); break;
-            case 13: CTS_QUAD_LP(4); break;
-            case 14: CTS_QUAD_LP(5); break;
-            default: CTS_QUAD_LP(8); break;
-            }
-#undef CTS_QUAD_LP
-            break;
-        }
-        case 1: verify_wave_kernel<1, NT><<<grid, kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
-        case 2: verify_wave_kernel<4, NT><<<grid, kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
-        case 3: verify_wave_pipe_kernel<2, NT><<<grid, kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
-        case 4: verify_wave_pipe_kernel<1, NT><<<grid, kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
-        default: verify_wave_kernel<2, NT><<<grid, kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
-        }
-#else
-        const ContigGrid cg = contig_grid(n, geo);  // small variant 15 (kDefaultSmallVariant)
-        verify_quad_kernel<6, NT, true, true, false, kQuadEdgePlain><<<cg.grid, kBlock, 0, stream>>>(CTS_QUAD_ARGS,
-                                                                                                     cg.per);
-#endif
+        const ContigGrid cg = contig_grid(n, geo);
+        verify_quad_kernel<NT, false><<<cg.grid, kBlock, 0, stream>>>(
+            arena, arena_bytes, VSource{descs, nullptr, 0u, 0u, 0u, 0u}, n, results, counters, conn_first_fail, n_conns,
+            cg.per);
     } else {
-        // variant (large path): 0 = workgroup/buffer U8, 1 = U4, 2 = U16, 3 = wave/buffer U8,
-        // 4 = barrier-free workgroup/buffer U8, 5 = barrier-free U4,
-        // 6 = workgroup/buffer U8 with an even-phase fast stream, 7 = same U4,
-        // 8 = variant 6 with clean-buffer counters in SGPRs,
-        // 9 = variant 6 + whole-line spans streamed without edge/head/tail handling, 10 = same U4,
-        // 11 = variant 10 with the exact diff of whole-line spans in registers (no re-read), 12 = same U8,
-        // 13 = same U2, 14 = same U1, 15/16/17 = variant 13 walking 2/4/8 windows of the descriptor list,
-        // 18 = variant 13 writing its result records 16 at a time from LDS
-#if CTS_TUNING
-        switch (geo.verify_variant) {
-        case 4: verify_wg_nb_kernel<8, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
-        case 5: verify_wg_nb_kernel<4, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
-        case 6: verify_wg_kernel<8, NT, true><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
-        case 8: verify_wg_kernel<8, NT, true, true><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
-        case 9: verify_wg_kernel<8, NT, true, false, true><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
-        case 10: verify_wg_kernel<4, NT, true, false, true><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
-        case 11: verify_wg_kernel<4, NT, true, false, true, true><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
-        case 12: verify_wg_kernel<8, NT, true, false, true, true><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
-        case 13: verify_wg_kernel<2, NT, true, false, true, true><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
-        case 14: verify_wg_kernel<1, NT, true, false, true, true><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
-        case 15: verify_wg_kernel<2, NT, true, false, true, true, 2><<<grid_win(n, 2, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
-        case 16: verify_wg_kernel<2, NT, true, false, true, true, 4><<<grid_win(n, 4, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
-        case 17: verify_wg_kernel<2, NT, true, false, true, true, 8><<<grid_win(n, 8, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
-        case 18: verify_wg_kernel<2, NT, true, false, true, true, 1, 16><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
-        case 19: verify_wg_kernel<2, NT, true, false, true, true, 1, 0, 4><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
-        case 20: verify_wg_kernel<2, NT, true, false, true, true, 1, 0, 8><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
-        // 21: variant 13 with 512-thread workgroups (each 64 KiB buffer streams in half the time, so the launch's
-        // finishing window is cut in whole buffers half as long); the grid cap is blocks_per_cu / 2 workgroups per CU
-        case 21: verify_wg_kernel<2, NT, true, false, true, true, 1, 0, 0, 2 * kBlock>
-                     <<<grid_for(n, 1, geo, std::max(1, geo.blocks_per_cu / 2)), 2 * kBlock, 0, stream>>>(CTS_VERIFY_ARGS);
-                 break;
-        // 22: variant 13 + 16-aligned spans with the 5-VALU expected words; 23: variant 13 + the first round of the
-        // guessed first slot read into L2 beside the first descriptor; 24: both (round 4, tools/verify_timeline)
-        case 22: verify_wg_kernel<2, NT, true, false, true, true, 1, 0, 0, kBlock, true>
-                     <<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS);
-                 break;
-        case 23: verify_wg_kernel<2, NT, true, false, true, true, 1, 0, 0, kBlock, false, true>
-                     <<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS);
-                 break;
-        case 24: verify_wg_kernel<2, NT, true, false, true, true, 1, 0, 0, kBlock, true, true>
-                     <<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS);
-                 break;
-        // 25: variant 13 with its registers allocated for 4 waves per SIMD (the 4 workgroups per CU it runs at)
-        // instead of 8: no SGPR spills in the per-buffer set-up (the default since round 4: 41.18-41.27 against
-        // 41.42-41.45 us per serialized config-2 launch, alternated on one box, profiles/r04/h/wpe.jsonl)
-        case 25: verify_wg_kernel<2, NT, true, false, true, true, 1, 0, 0, kBlock, false, false, 4>
-                     <<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS);
-                 break;
-        // 26: variant 25 at U = 4 (4 loads per lane per round)
-        case 26: verify_wg_kernel<4, NT, true, false, true, true, 1, 0, 0, kBlock, false, false, 4>
-                     <<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS);
-                 break;
-        // 27: variant 25 + the guessed first slot's first round loaded into registers beside the first descriptor
-        case 27: verify_wg_kernel<2, NT, true, false, true, true, 1, 0, 0, kBlock, false, false, 4, true>
-                     <<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS);
-                 break;
-        // 28: variant 25 walking the descriptors rotated by one per round (ROT)
-        case 28: verify_wg_kernel<2, NT, true, false, true, true, 1, 0, 0, kBlock, false, false, 4, false, true>
-                     <<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS);
-                 break;
-        case 7: verify_wg_kernel<4, NT, true><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
-        case 1: verify_wg_kernel<4, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
-        case 2: verify_wg_kernel<16, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
-        case 3: verify_wave_kernel<8, NT><<<grid_for(n, kBlock / 64, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
-        default: verify_wg_kernel<8, NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS); break;
-        }
-#else
-        // verify variant 25 (kDefaultVerifyVariant): variant 13 with registers allocated for 4 waves per SIMD
-        verify_wg_kernel<2, NT, true, false, true, true, 1, 0, 0, kBlock, false, false, 4>
-            <<<grid_for(n, 1, geo), kBlock, 0, stream>>>(CTS_VERIFY_ARGS);
-#endif
+        verify_wg_kernel<NT><<<grid_for(n, 1, geo), kBlock, 0, stream>>>(arena, arena_bytes, descs, n, results,
+                                                                         counters, conn_first_fail, n_conns);
     }
 }
 
@@ -2722,10 +1792,8 @@ __device__ uint64_t* cts_mail_trace;
     } while (0)
 #endif
 
-// POLLS: reads of the job slot the poller keeps in flight (1, or 2 half a round trip apart; CTS_MAILBOX_POLLS)
-constexpr uint32_t kMailPollGap = 18;  // s_sleep units (64 clocks): ~half the 1.2 us PCIe read round trip
-
-template <int POLLS>
+// The poller keeps one read of the job slot in flight (two reads half a PCIe round trip apart measured 6.72-6.79 us
+// per 64 KiB at one caller against 6.32-6.51 with one, and no gain at 8 / 16 callers: profiles/r03/mailbox_polls_ab/).
 __global__ __launch_bounds__(kMailThreads) void mailbox_kernel(const MailSlot* slots, MailPart* parts, uint32_t per_group,
                                                                MailStarts starts, uint64_t idle_ticks,
                                                                uint64_t delay_ticks)
@@ -2775,40 +1843,12 @@ __global__ __launch_bounds__(kMailThreads) void mailbox_kernel(const MailSlot* s
                 if (waited > kMailHotTicks) __builtin_amdgcn_s_sleep(40);
             };
             bool leave = false;
-            if constexpr (POLLS == 2) {
-                // two reads of the slot in flight, issued half a PCIe round trip apart, so a new job is seen about
-                // a quarter round trip after it lands instead of half a round trip; each check waits for the older
-                // read only (vmcnt(1)), and the loop's two halves keep one read outstanding at the back edge
-                // (the empty asm with a memory clobber after each read keeps LLVM from sinking the read below the
-                // check of the previous one -- it is used on one path only -- which would leave one read in flight)
-                u32x4 x0 = __builtin_amdgcn_raw_buffer_load_b128(r, 0u, 0u, kMailAux);
-                __builtin_amdgcn_s_sleep(kMailPollGap);
-                for (;;) {
-                    const u32x4 x1 = __builtin_amdgcn_raw_buffer_load_b128(r, 0u, 0u, kMailAux);
-                    asm volatile("" ::: "memory");
-                    if (seen(x0)) {
-                        v = x0;
-                        break;
-                    }
-                    idle(leave);
-                    if (leave) break;
-                    x0 = __builtin_amdgcn_raw_buffer_load_b128(r, 0u, 0u, kMailAux);
-                    asm volatile("" ::: "memory");
-                    if (seen(x1)) {
-                        v = x1;
-                        break;
-                    }
-                    idle(leave);
-                    if (leave) break;
-                }
-            } else {
-                for (;;) {
-                    v = __builtin_amdgcn_raw_buffer_load_b128(r, 0u, 0u, kMailAux);
-                    if (seen(v)) break;
-                    idle(leave);
-                    if (leave) break;
-                    __builtin_amdgcn_s_sleep(2);
-                }
+            for (;;) {
+                v = __builtin_amdgcn_raw_buffer_load_b128(r, 0u, 0u, kMailAux);
+                if (seen(v)) break;
+                idle(leave);
+                if (leave) break;
+                __builtin_amdgcn_s_sleep(2);
             }
             if (leave) {
                 v = u32x4{0u, 0u, 0u, ~tag};  // no job within idle_ticks: publish one whose tag word is not the tag
@@ -2922,23 +1962,36 @@ __global__ __launch_bounds__(kMailThreads) void mailbox_kernel(const MailSlot* s
 }
 
 hipError_t launch_mailbox(const MailSlot* slots, MailPart* parts, uint32_t per_group, const MailStarts& starts,
-                          uint32_t groups, uint64_t idle_ticks, hipStream_t stream, uint64_t delay_ticks, int polls)
+                          uint32_t groups, uint64_t idle_ticks, hipStream_t stream, uint64_t delay_ticks)
 {
     if (slots == nullptr || parts == nullptr || per_group == 0 || groups == 0 || groups > kMailMaxGroups)
         return hipErrorInvalidValue;
-#if CTS_TUNING
-    // two reads in flight: 6.72-6.79 us per 64 KiB at one caller against 6.32-6.51 with one, same box, three
-    // alternating rounds, no gain at 8 / 16 callers (profiles/r03/mailbox_polls_ab/): tuning build only
-    if (polls == 2) {
-        mailbox_kernel<2><<<groups * kMailGroup, kMailThreads, 0, stream>>>(slots, parts, per_group, starts, idle_ticks,
-                                                                            delay_ticks);
-        return hipGetLastError();
+    mailbox_kernel<<<groups * kMailGroup, kMailThreads, 0, stream>>>(slots, parts, per_group, starts, idle_ticks,
+                                                                     delay_ticks);
+    return hipGetLastError();
+}
+
+// ---- counter fold (cts_counters_allreduce): one lane per shard, the five sums by lanes 0..4 ----
+static_assert(CTS_COUNTER_SHARDS == 64, "one lane per counter shard");
+__global__ void __launch_bounds__(64) counters_fold_kernel(const uint64_t* __restrict__ block, uint64_t* __restrict__ out,
+                                                           int accumulate)
+{
+    __shared__ uint64_t part[CTS_COUNTER_SHARDS][5];
+    const uint32_t t = threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) part[t][k] = block[t * kCounterSlots + k];
+    __syncthreads();
+    if (t < 5u) {
+        uint64_t s = accumulate ? out[t] : 0u;
+        for (uint32_t sh = 0; sh < CTS_COUNTER_SHARDS; ++sh) s += part[sh][t];
+        out[t] = s;
     }
-#else
-    (void)polls;
-#endif
-    mailbox_kernel<1><<<groups * kMailGroup, kMailThreads, 0, stream>>>(slots, parts, per_group, starts, idle_ticks,
-                                                                        delay_ticks);
+}
+
+hipError_t launch_counters_fold(const void* block, uint64_t* out, bool accumulate, hipStream_t stream)
+{
+    if (block == nullptr || out == nullptr) return hipErrorInvalidValue;
+    counters_fold_kernel<<<1, 64, 0, stream>>>(static_cast<const uint64_t*>(block), out, accumulate ? 1 : 0);
     return hipGetLastError();
 }
 
@@ -2959,7 +2012,7 @@ hipError_t launch_verify(const uint8_t* arena, uint64_t arena_bytes, const cts_b
     return hipGetLastError();
 }
 
-// cts_verify_strided: the small-buffer walk (variant 15's kernel) over a uniformly strided ring
+// cts_verify_strided: the small-buffer walk (verify_quad_kernel) over a uniformly strided ring
 hipError_t launch_verify_strided(const uint8_t* arena, uint64_t arena_bytes, uint32_t stride, const uint32_t* lens,
                                  uint32_t n, uint32_t skip_head, uint32_t expected, uint32_t conn_index,
                                  cts_verify_result* results, uint64_t* counters, uint32_t* conn_first_fail,
@@ -2969,15 +2022,15 @@ hipError_t launch_verify_strided(const uint8_t* arena, uint64_t arena_bytes, uin
     const VSource src{nullptr, lens, stride, skip_head, expected, conn_index};
     const ContigGrid cg = contig_grid(n, geo);
     if (geo.nontemporal)
-        verify_quad_kernel<6, true, true, true, true, kQuadEdgePlain><<<cg.grid, kBlock, 0, stream>>>(
-            arena, arena_bytes, src, n, results, counters, conn_first_fail, n_conns, cg.per);
+        verify_quad_kernel<true, true><<<cg.grid, kBlock, 0, stream>>>(arena, arena_bytes, src, n, results, counters,
+                                                                       conn_first_fail, n_conns, cg.per);
     else
-        verify_quad_kernel<6, false, true, true, true, kQuadEdgePlain><<<cg.grid, kBlock, 0, stream>>>(
-            arena, arena_bytes, src, n, results, counters, conn_first_fail, n_conns, cg.per);
+        verify_quad_kernel<false, true><<<cg.grid, kBlock, 0, stream>>>(arena, arena_bytes, src, n, results, counters,
+                                                                        conn_first_fail, n_conns, cg.per);
     return hipGetLastError();
 }
 
-// grid of the batched small-buffer fills: whole batches per workgroup, at most ring_fill_blocks_per_cu per CU
+// grid of the batched datagram fills: whole batches per workgroup, at most ring_fill_blocks_per_cu per CU
 static inline uint32_t batched_fill_grid(uint32_t n, const LaunchGeometry& geo)
 {
     const uint64_t cap = (uint64_t)geo.num_cus * (uint64_t)(geo.ring_fill_blocks_per_cu > 0 ? geo.ring_fill_blocks_per_cu : 4);
@@ -2994,16 +2047,6 @@ hipError_t launch_fill(uint8_t* arena, uint64_t arena_bytes, const cts_buf_desc*
     // config 2 48.7 vs 51.1 us; nontemporal for datagrams: 1.46 vs 1.68 ms per 4 M; tools/tune_verify.py --op fill)
     const bool nts = geo.fill_nt == 2 ? small : geo.fill_nt != 0;
     const uint32_t sgrid = grid_for(n, kBlock / 64, geo), lgrid = grid_for(n, 1, geo, geo.fill_blocks_per_cu);
-    // (the LDS-batched form of the small path measured slower for payload fills of datagrams: 6.9 vs 6.1-6.8 ms per
-    // 16 M x 1446 B, tools/ring_fill_probe.hip: their first chunk is a partial write either way; tuning build only)
-#if CTS_TUNING
-    if (small && geo.fill_batched == 2) {
-        const uint32_t grid = batched_fill_grid(n, geo);
-        if (nts) fill_batched_kernel<true, false><<<grid, kBlock, 0, stream>>>(arena, arena_bytes, descs, nullptr, n);
-        else fill_batched_kernel<false, false><<<grid, kBlock, 0, stream>>>(arena, arena_bytes, descs, nullptr, n);
-        return hipGetLastError();
-    }
-#endif
     if (nts) {
         if (small) fill_kernel<64, true><<<sgrid, kBlock, 0, stream>>>(arena, arena_bytes, descs, n);
         else fill_kernel<kBlock, true><<<lgrid, kBlock, 0, stream>>>(arena, arena_bytes, descs, n);
@@ -3014,87 +2057,21 @@ hipError_t launch_fill(uint8_t* arena, uint64_t arena_bytes, const cts_buf_desc*
     return hipGetLastError();
 }
 
+// The MediaStream receive: four datagrams per wave walking block-contiguous ranges (contig_grid), records + results
+// staged in a per-wave LDS ring and written every kMsRing rounds (for config 3 once, at the workgroup's end).
 hipError_t launch_media_stream_verify(const uint8_t* arena, uint64_t arena_bytes, const cts_buf_desc* descs, uint32_t n,
                                      cts_datagram_record* records, cts_verify_result* results, uint64_t* counters,
                                      hipStream_t stream, const LaunchGeometry& geo)
 {
     if (n == 0) return hipSuccess;
-#define CTS_MS_ARGS arena, arena_bytes, MsSource{descs, nullptr, 0u}, n, records, results, counters
-    // ms_variant: 0 = one wave per datagram, 1 = four datagrams per wave (header by byte loads),
-    // 2 = four per wave, header by three 16-byte chunk loads + DPP, 3 = variant 2 walking
-    // block-contiguous datagram ranges and writing its outputs every kMsRing = 64 rounds from a per-wave LDS
-    // ring (default), 4 / 5 / 6 = the same every 8 / 16 / 32 rounds, 11 = every round (7: the two-pass form of cts_media_stream_verify_status;
-    // 8 / 9 / 10: its one-pass form with the statuses written every round / every 16 / 32 rounds; the product
-    // writes them every 64 rounds)
-    const uint32_t qgrid = grid_for(n, kBlock / kQuadTeam, geo);
-    const uint32_t grid = grid_for(n, kBlock / 64, geo);
-#if CTS_TUNING
-    const bool nt = geo.nontemporal != 0;
-    switch (geo.ms_variant) {
-    case 0:
-        if (nt) media_stream_verify_kernel<2, true><<<grid, kBlock, 0, stream>>>(arena, arena_bytes, descs, n, records, results, counters);
-        else media_stream_verify_kernel<2, false><<<grid, kBlock, 0, stream>>>(arena, arena_bytes, descs, n, records, results, counters);
-        break;
-    case 1:
-        if (nt) media_stream_verify_quad_kernel<6, true, true, false><<<qgrid, kBlock, 0, stream>>>(CTS_MS_ARGS);
-        else media_stream_verify_quad_kernel<6, false, true, false><<<qgrid, kBlock, 0, stream>>>(CTS_MS_ARGS);
-        break;
-    case 2:
-        if (nt) media_stream_verify_quad_kernel<6, true, true, true><<<qgrid, kBlock, 0, stream>>>(CTS_MS_ARGS);
-        else media_stream_verify_quad_kernel<6, false, true, true><<<qgrid, kBlock, 0, stream>>>(CTS_MS_ARGS);
-        break;
-    case 4:
-    case 5:
-    case 6:
-    case 11: {  // variant 3 with its outputs written every 8 / 16 / 32 rounds from a per-wave ring / every round
-        const ContigGrid cg = contig_grid(n, geo);
-#define CTS_MS_RING(K)                                                                                              \
-    (nt ? (media_stream_verify_quad_kernel<6, true, true, true, true, false, K><<<cg.grid, kBlock, 0, stream>>>(   \
-               CTS_MS_ARGS, cg.per),                                                                                \
-           0)                                                                                                       \
-        : (media_stream_verify_quad_kernel<6, false, true, true, true, false, K><<<cg.grid, kBlock, 0, stream>>>(  \
-               CTS_MS_ARGS, cg.per),                                                                                \
-           0))
-        if (geo.ms_variant == 4) (void)CTS_MS_RING(8);
-        else if (geo.ms_variant == 5) (void)CTS_MS_RING(16);
-        else if (geo.ms_variant == 6) (void)CTS_MS_RING(32);
-        else (void)CTS_MS_RING(0);
-#undef CTS_MS_RING
-        break;
-    }
-    case 12: {  // variant 3 with the header / edge loads nontemporal (the round-2 product)
-        const ContigGrid cg = contig_grid(n, geo);
-        if (nt)
-            media_stream_verify_quad_kernel<6, true, true, true, true, false, kMsRing, false, false, false>
-                <<<cg.grid, kBlock, 0, stream>>>(CTS_MS_ARGS, cg.per);
-        else
-            media_stream_verify_quad_kernel<6, false, true, true, true, false, kMsRing, false, false, false>
-                <<<cg.grid, kBlock, 0, stream>>>(CTS_MS_ARGS, cg.per);
-        break;
-    }
-    default: {
-        const ContigGrid cg = contig_grid(n, geo);
-        if (nt)
-            media_stream_verify_quad_kernel<6, true, true, true, true, false, kMsRing><<<cg.grid, kBlock, 0, stream>>>(
-                CTS_MS_ARGS, cg.per);
-        else
-            media_stream_verify_quad_kernel<6, false, true, true, true, false, kMsRing><<<cg.grid, kBlock, 0, stream>>>(
-                CTS_MS_ARGS, cg.per);
-        break;
-    }
-    }
-#else
-    (void)qgrid;
-    (void)grid;
-    const ContigGrid cg = contig_grid(n, geo);  // MediaStream variant 3 (kDefaultMediaStreamVariant)
+    const ContigGrid cg = contig_grid(n, geo);
+    const MsSource src{descs, nullptr, 0u};
     if (geo.nontemporal)
-        media_stream_verify_quad_kernel<6, true, true, true, true, false, kMsRing><<<cg.grid, kBlock, 0, stream>>>(
-            CTS_MS_ARGS, cg.per);
+        media_stream_verify_quad_kernel<true, false, kMsRing><<<cg.grid, kBlock, 0, stream>>>(
+            arena, arena_bytes, src, n, records, results, counters, cg.per);
     else
-        media_stream_verify_quad_kernel<6, false, true, true, true, false, kMsRing><<<cg.grid, kBlock, 0, stream>>>(
-            CTS_MS_ARGS, cg.per);
-#endif
-#undef CTS_MS_ARGS
+        media_stream_verify_quad_kernel<false, false, kMsRing><<<cg.grid, kBlock, 0, stream>>>(
+            arena, arena_bytes, src, n, records, results, counters, cg.per);
     return hipGetLastError();
 }
 
@@ -3104,14 +2081,14 @@ hipError_t launch_media_stream_verify_strided(const uint8_t* arena, uint64_t are
                                              const LaunchGeometry& geo)
 {
     if (n == 0) return hipSuccess;
-    // the variant-3 walk (block-contiguous ranges, four datagrams per wave) over the ring's slots
+    // the same walk over the ring's slots
     const ContigGrid cg = contig_grid(n, geo);
     const MsSource src{nullptr, lengths, stride};
     if (geo.nontemporal)
-        media_stream_verify_quad_kernel<6, true, true, true, true, true, kMsRing><<<cg.grid, kBlock, 0, stream>>>(
+        media_stream_verify_quad_kernel<true, true, kMsRing><<<cg.grid, kBlock, 0, stream>>>(
             arena, arena_bytes, src, n, records, results, counters, cg.per);
     else
-        media_stream_verify_quad_kernel<6, false, true, true, true, true, kMsRing><<<cg.grid, kBlock, 0, stream>>>(
+        media_stream_verify_quad_kernel<false, true, kMsRing><<<cg.grid, kBlock, 0, stream>>>(
             arena, arena_bytes, src, n, records, results, counters, cg.per);
     return hipGetLastError();
 }
@@ -3121,72 +2098,18 @@ hipError_t launch_media_stream_status(const uint8_t* arena, uint64_t arena_bytes
                                      uint64_t* counters, hipStream_t stream, const LaunchGeometry& geo)
 {
     if (n == 0) return hipSuccess;
-    // descs == nullptr: the strided-ring form
+    // one pass over descriptors, or (descs == nullptr) the strided ring: the receive walk, each wave staging its
+    // datagrams' 16-byte statuses in an LDS ring and writing 64 rounds of them at a time -- for config 3 (1024
+    // datagrams per workgroup) once, at the workgroup's end. Per 16 M datagrams 4.30-4.31 ms against 4.44 with 32
+    // rounds and 4.54 written every round, one box (profiles/r02/ms_status/); a two-pass form (headers -> statuses,
+    // then the payload clearing pass on failures) measured 4.25 against 4.08 ms (the header gather's scattered
+    // 16-byte reads cost more than the writes it takes out of the payload pass)
     const ContigGrid cg = contig_grid(n, geo);
     const MsSource src{descs, lengths, stride};
-#if CTS_TUNING
-    if (geo.ms_variant == 8 || geo.ms_variant == 9 || geo.ms_variant == 10) {
-        // one pass, statuses written every round (8), or every 16 / 32 rounds from the per-wave ring (9 / 10)
-#define CTS_MS_STATUS_K(NT, STR, K)                                                                         \
-    media_stream_verify_quad_kernel<6, NT, true, true, true, STR, K, true><<<cg.grid, kBlock, 0, stream>>>( \
-        arena, arena_bytes, src, n, status, nullptr, counters, cg.per)
-        if (geo.ms_variant == 8) {
-            if (descs == nullptr) CTS_MS_STATUS_K(true, true, 0);
-            else CTS_MS_STATUS_K(true, false, 0);
-        } else if (geo.ms_variant == 10) {
-            if (descs == nullptr) CTS_MS_STATUS_K(true, true, 32);
-            else CTS_MS_STATUS_K(true, false, 32);
-        } else {
-            if (descs == nullptr) CTS_MS_STATUS_K(true, true, 16);
-            else CTS_MS_STATUS_K(true, false, 16);
-        }
-#undef CTS_MS_STATUS_K
-        return hipGetLastError();
-    }
-    if (geo.ms_variant == 12) {  // the product form with the header / edge loads nontemporal (round 2)
-#define CTS_MS_STATUS_NTE(STR)                                                                                        \
-    media_stream_verify_quad_kernel<6, true, true, true, true, STR, 64, true, false, false><<<cg.grid, kBlock, 0,   \
-                                                                                           stream>>>(             \
-        arena, arena_bytes, src, n, status, nullptr, counters, cg.per)
-        if (descs == nullptr) CTS_MS_STATUS_NTE(true);
-        else CTS_MS_STATUS_NTE(false);
-#undef CTS_MS_STATUS_NTE
-        return hipGetLastError();
-    }
-    if (geo.ms_variant == 7) {
-        // two passes: headers -> statuses (pass = 1 for DATA), then the payload verify clearing pass on
-        // failures. Measured slower than one pass (4.25 vs 4.08 ms per 16 M datagrams): the header gather's
-        // scattered 16-byte reads cost more than the writes it takes out of the payload pass.
-        const uint32_t ggrid = (n + kBlock - 1) / kBlock;
-        if (status != nullptr) {
-            if (descs == nullptr)
-                ms_status_gather_kernel<true><<<ggrid, kBlock, 0, stream>>>(arena, arena_bytes, src, n,
-                                                                              reinterpret_cast<uint32_t*>(status));
-            else
-                ms_status_gather_kernel<false><<<ggrid, kBlock, 0, stream>>>(arena, arena_bytes, src, n,
-                                                                               reinterpret_cast<uint32_t*>(status));
-        }
-#define CTS_MS_MARK(NT, STR)                                                                                      \
-    media_stream_verify_quad_kernel<6, NT, true, true, true, STR, 0, false, true><<<cg.grid, kBlock, 0, stream>>>( \
-        arena, arena_bytes, src, n, status, nullptr, counters, cg.per)
-        if (descs == nullptr) {
-            if (geo.nontemporal) CTS_MS_MARK(true, true);
-            else CTS_MS_MARK(false, true);
-        } else {
-            if (geo.nontemporal) CTS_MS_MARK(true, false);
-            else CTS_MS_MARK(false, false);
-        }
-#undef CTS_MS_MARK
-        return hipGetLastError();
-    }
-#endif
-    // one pass: the variant-3 walk, each wave staging its datagrams' statuses in an LDS ring and writing 64
-    // rounds of them at a time -- for config 3 (1024 datagrams per workgroup) once, at the workgroup's end.
-    // Per 16 M datagrams 4.30-4.31 ms against 4.44 with 32 rounds and 4.54 written every round, one box
-    // (profiles/r02/ms_status/)
-#define CTS_MS_STATUS(NT, STR)                                                                               \
-    media_stream_verify_quad_kernel<6, NT, true, true, true, STR, 64, true><<<cg.grid, kBlock, 0, stream>>>( \
-        arena, arena_bytes, src, n, status, nullptr, counters, cg.per)
+#define CTS_MS_STATUS(NT, STR)                                                                                \
+    media_stream_verify_quad_kernel<NT, STR, 64, true><<<cg.grid, kBlock, 0, stream>>>(arena, arena_bytes, src, n, \
+                                                                                       status, nullptr, counters, \
+                                                                                       cg.per)
     if (descs == nullptr) {
         if (geo.nontemporal) CTS_MS_STATUS(true, true);
         else CTS_MS_STATUS(false, true);
@@ -3215,9 +2138,9 @@ hipError_t launch_media_stream_frames(const uint8_t* arena, uint64_t arena_bytes
     const ContigGrid cg = contig_grid(n, geo);
     const MsSource src{descs, lengths, stride};
     const MsFrames fr{win.head_sequence_number, win.final_frame, win.frames, win.finished, totals, frame_bytes};
-#define CTS_MS_FRAMES(NT, STR)                                                                                      \
-    media_stream_verify_quad_kernel<6, NT, true, true, true, STR, 0, false, false, true, true>                     \
-        <<<cg.grid, kBlock, 0, stream>>>(arena, arena_bytes, src, n, nullptr, nullptr, counters, cg.per, fr)
+#define CTS_MS_FRAMES(NT, STR)                                                                        \
+    media_stream_verify_quad_kernel<NT, STR, 0, false, true><<<cg.grid, kBlock, 0, stream>>>(           \
+        arena, arena_bytes, src, n, nullptr, nullptr, counters, cg.per, fr)
     if (descs == nullptr) {
         if (geo.nontemporal) CTS_MS_FRAMES(true, true);
         else CTS_MS_FRAMES(false, true);
@@ -3237,16 +2160,9 @@ hipError_t launch_media_stream_fill(uint8_t* arena, uint64_t arena_bytes, const 
     // store policy: fill_nt 0 or 2 (by path) = plain, 1 = nontemporal (batched: 5.08 ms plain vs 5.37 nt per 16 M x
     // 1472 B, tools/ring_fill_probe.hip)
     const bool nts = geo.fill_nt == 1;
-#if CTS_TUNING
-    if (!geo.fill_batched) {
-        if (nts) media_stream_fill_kernel<true><<<grid_for(n, kBlock / 64, geo), kBlock, 0, stream>>>(arena, arena_bytes, descs, headers, n);
-        else media_stream_fill_kernel<false><<<grid_for(n, kBlock / 64, geo), kBlock, 0, stream>>>(arena, arena_bytes, descs, headers, n);
-        return hipGetLastError();
-    }
-#endif
     const uint32_t grid = batched_fill_grid(n, geo);
-    if (nts) fill_batched_kernel<true, true><<<grid, kBlock, 0, stream>>>(arena, arena_bytes, descs, headers, n);
-    else fill_batched_kernel<false, true><<<grid, kBlock, 0, stream>>>(arena, arena_bytes, descs, headers, n);
+    if (nts) fill_batched_kernel<true><<<grid, kBlock, 0, stream>>>(arena, arena_bytes, descs, headers, n);
+    else fill_batched_kernel<false><<<grid, kBlock, 0, stream>>>(arena, arena_bytes, descs, headers, n);
     return hipGetLastError();
 }
 

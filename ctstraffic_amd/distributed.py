@@ -102,5 +102,19 @@ def data_error_count(conn_first_fail, group=None) -> int:
     return int(n.item())
 
 
+def gather_rank_rows(row, group=None) -> list:
+    """Every rank's row of floats, in rank order (an all-gather over `group`, the gloo group in bench.py); at world
+    size 1, [row]. bench.py's per-rank diagnostics: kernel time, engine device, torch device, placement check."""
+    import torch
+    import torch.distributed as dist
+
+    mine = torch.tensor([float(x) for x in row], dtype=torch.float64)
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        return [mine.tolist()]
+    rows = [torch.zeros_like(mine) for _ in range(dist.get_world_size(group))]
+    dist.all_gather(rows, mine, group=group)
+    return [r.tolist() for r in rows]
+
+
 __all__ = ["dist_env", "init", "new_cpu_group", "DEFAULT_TIMEOUT_S", "fold_counters", "allreduce_counters", "counters_dict", "max_over_ranks",
-           "data_error_count"]
+           "data_error_count", "gather_rank_rows"]

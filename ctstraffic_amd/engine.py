@@ -94,20 +94,40 @@ def counters_read_multi(engines: Sequence["Engine"], blocks, streams=None) -> di
     return out.as_dict()
 
 
+def counters_allreduce(engines: Sequence["Engine"], blocks, streams=None) -> dict:
+    """cts_counters_allreduce: the same node-wide counters reduced on the GPUs: each block folded on its engine's
+    device, then one RCCL all-reduce (sum, u64 x 5) per device over xGMI (one process drives every GPU)."""
+    n = len(engines)
+    E = (ctypes.c_void_p * max(1, n))(*[e._h.value for e in engines])
+    C = (ctypes.c_void_p * max(1, n))(*[_ptr(b) for b in blocks])
+    S = None
+    if streams is not None:
+        S = (ctypes.c_void_p * max(1, n))(*[_stream(s) for s in streams])
+    out = CtsCounters()
+    check("cts_counters_allreduce", lib().cts_counters_allreduce(E, C, S, n, ctypes.byref(out)))
+    return out.as_dict()
+
+
+def counters_allreduce_release() -> None:
+    """cts_counters_allreduce_release: destroy the cached RCCL communicators (before the devices go away)."""
+    check("cts_counters_allreduce_release", lib().cts_counters_allreduce_release())
+
+
 class Engine:
     """One engine per GPU (cts_engine_create). Thread-safe across streams."""
 
-    def __init__(self, device: int = 0, tuning: bool = False):
-        """``tuning``: an engine of the tuning build (libcts_engine_tuning.so, every launch variant) for A/B runs
-        and variant parity tests; the product library launches one kernel per path."""
-        self._L = _lib.tuning_lib() if tuning else lib()
-        self.tuning = tuning
+    def __init__(self, device: int = 0):
+        self._L = lib()
         h = ctypes.c_void_p()
         check("cts_engine_create", self._L.cts_engine_create(device, ctypes.byref(h)))
         self._h = h
         self.device = device
 
     # ---- lifetime ----------------------------------------------------------
+    def device_ordinal(self) -> int:
+        """cts_engine_device: the GPU this engine launches on (as the library sees it)."""
+        return int(self._L.cts_engine_device(self._h))
+
     def close(self) -> None:
         if getattr(self, "_h", None) is not None and self._h.value:
             self._L.cts_engine_destroy(self._h)

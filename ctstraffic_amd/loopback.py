@@ -97,8 +97,6 @@ def run(connections=8, buffer_size=65536, transfer_size=1 << 30, engine=None, ve
         hook = verifier if isinstance(verifier, A.BATCH_VERIFIER) else batch_verifier(verifier)
     res = LoopbackResult()
     engines = engine if isinstance(engine, (list, tuple)) else ([] if engine is None else [engine])
-    if any(getattr(e, "tuning", False) for e in engines):
-        raise ValueError("the loopback feeder drives product engines only")
     arr = (ctypes.c_void_p * max(1, len(engines)))(*[e._h.value for e in engines])
     side_arr = (LoopbackSide * (2 * connections))() if sides else None
     check("cts_loopback_run_detailed",
@@ -157,8 +155,6 @@ def media_stream_run(connections=2, frame_size=52083, frames_per_second=60, stre
     hook = None
     if verifier is not None:
         hook = verifier if isinstance(verifier, A.BATCH_VERIFIER) else batch_verifier(verifier)
-    if engine is not None and getattr(engine, "tuning", False):
-        raise ValueError("the loopback feeder drives product engines only")
     res = R()
     check("cts_loopback_media_stream_run",
           fn(ctypes.byref(cfg), None if engine is None else engine._h.value,

@@ -311,7 +311,5 @@ def status_details_reset() -> None:
 
 
 def _product(engine):
-    """The pattern mirror belongs to the product library: it takes product engines only."""
-    if getattr(engine, "tuning", False):
-        raise ValueError("a tuning-build engine cannot drive the product library's ctsIoPattern mirror")
+    """The engine handle the pattern mirror passes to the C ABI."""
     return engine._h

@@ -53,7 +53,8 @@ typedef enum cts_status {
     CTS_E_INVALID = -1,   /* bad argument (null, misaligned, out of range) */
     CTS_E_HIP = -2,       /* a HIP runtime call or kernel launch failed */
     CTS_E_NOMEM = -3,     /* allocation failed */
-    CTS_E_NO_DEVICE = -4  /* no HIP device / device index out of range */
+    CTS_E_NO_DEVICE = -4, /* no HIP device / device index out of range */
+    CTS_E_UNAVAILABLE = -5 /* an optional runtime library (RCCL) could not be loaded */
 } cts_status;
 
 /* One received (verify) or outgoing (fill) buffer inside a device arena.
@@ -125,19 +126,18 @@ int cts_engine_device(const cts_engine* engine);
 int cts_engine_numa_node(const cts_engine* engine);
 
 /* Launch-geometry attributes (defaults tuned for MI355X; env overrides
- * CTS_BLOCKS_PER_CU / CTS_NT_LOADS / CTS_SMALL_THRESHOLD / CTS_VERIFY_VARIANT /
- * CTS_SMALL_BLOCKS_PER_CU / CTS_SMALL_VARIANT / CTS_FILL_BLOCKS_PER_CU / CTS_MS_VARIANT /
- * CTS_SMALL_CHUNK / CTS_FILL_NT
+ * CTS_BLOCKS_PER_CU / CTS_NT_LOADS / CTS_SMALL_THRESHOLD / CTS_SMALL_BLOCKS_PER_CU /
+ * CTS_FILL_BLOCKS_PER_CU / CTS_SMALL_CHUNK / CTS_FILL_NT / CTS_RING_FILL_BLOCKS_PER_CU
  * are read at create time). */
 typedef enum cts_engine_attr {
     CTS_ATTR_BLOCKS_PER_CU = 1,   /* grid cap = CUs x this (grid-strides beyond) */
     CTS_ATTR_NT_LOADS = 2,        /* 1 = nontemporal loads on the verify stream */
     CTS_ATTR_SMALL_THRESHOLD = 3, /* max_length_hint <= this -> one wave per buffer */
-    CTS_ATTR_VERIFY_VARIANT = 4,  /* kernel variant (see cts_kernels.hip launch_verify) */
+    CTS_ATTR_VERIFY_VARIANT = 4,  /* read-only id of the workgroup-per-buffer kernel (25); set: that id only */
     CTS_ATTR_SMALL_BLOCKS_PER_CU = 5, /* grid cap of the small-buffer path */
-    CTS_ATTR_SMALL_VARIANT = 6,       /* small-buffer (datagram) kernel variant */
+    CTS_ATTR_SMALL_VARIANT = 6,       /* read-only id of the small-buffer (datagram) kernel (15) */
     CTS_ATTR_FILL_BLOCKS_PER_CU = 7,  /* grid cap of the fill kernels */
-    CTS_ATTR_MS_VARIANT = 8,          /* MediaStream receive kernel (cts_media_stream_verify) */
+    CTS_ATTR_MS_VARIANT = 8,          /* read-only id of the MediaStream receive kernel (3) */
     CTS_ATTR_SMALL_CHUNK = 9,         /* chunked small-buffer walk: buffers per chunk (0 = contiguous) */
     CTS_ATTR_FILL_NT = 10,            /* cts_fill stores: 0 plain, 1 nontemporal, 2 by path (default) */
     CTS_ATTR_SYNC_MAILBOX = 11        /* 1 (default) = SYNC-mode pattern verifies of pinned recv buffers and
@@ -201,6 +201,21 @@ int cts_counters_read(cts_engine* engine, const void* dev_counters, cts_counters
  * (each engine's legacy stream) or hold one stream per engine (each is synchronised). */
 int cts_counters_read_multi(cts_engine* const* engines, const void* const* dev_counters, void* const* streams,
                             uint32_t n, cts_counters* out);
+/* The same node-wide counters reduced on the GPUs over RCCL (ncclAllReduce, sum,
+ * ncclUint64, count 5, over xGMI), for ctsTraffic's one-process host: each engine's block is folded on its own
+ * device (engines sharing a device fold into one slot), then one ncclAllReduce per device runs inside
+ * ncclGroupStart/End on that device's stream (the stream of its first engine in the list; streams may be NULL =
+ * each engine's legacy stream; another engine's stream on the same device is synchronised first). Every device's
+ * result is read back and must agree. The communicators (ncclCommInitAll over the distinct devices, in list
+ * order) are created on the first call for a device set and reused. RCCL is loaded on first use (librccl.so.1,
+ * or the path in $CTS_RCCL_LIBRARY): CTS_E_UNAVAILABLE when it cannot be; CTS_E_HIP when an RCCL or HIP call
+ * fails or the devices' results disagree. Thread-safe (calls are serialised). Replaces the reads behind
+ * ctsConfig::TcpStatusDetails / ctsStatsTracking (ctsConfig.h:415-417, ctsStatistics.hpp:87-198). */
+int cts_counters_allreduce(cts_engine* const* engines, const void* const* dev_counters, void* const* streams,
+                           uint32_t n, cts_counters* out);
+/* Destroys the communicators and device slots cts_counters_allreduce keeps (call before the engines' devices go
+ * away, e.g. at shutdown); the next all-reduce creates them again. */
+int cts_counters_allreduce_release(void);
 
 /* cts_verify over a uniformly strided receive ring (a UDP socket's datagrams): buffer i occupies
  * [i * stride, i * stride + dev_lengths[i]) of the arena, its first skip_head bytes are skipped and the rest

@@ -47,19 +47,6 @@ def engine():
     e.close()
 
 
-@pytest.fixture(scope="session")
-def tuning_engine():
-    """An engine of the tuning build (libcts_engine_tuning.so: every launch variant) for the variant parity tests;
-    the product library compiles one kernel per path."""
-    if not _gpu_available():
-        pytest.fail("gpu test selected but no HIP device is visible (the engine has no CPU fallback)")
-    from ctstraffic_amd import Engine
-
-    e = Engine(0, tuning=True)
-    yield e
-    e.close()
-
-
 class RioFake:
     """tests/cpp/rio_fake.c loaded with ctypes: the RIORegisterBuffer/RIODeregisterBuffer fakes and their
     bookkeeping queries."""

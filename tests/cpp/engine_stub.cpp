@@ -10,6 +10,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include "cts_engine.h"
+#include "cts_internal.hpp"
 #include "cts_media_stream.h"
 
 extern "C" {
@@ -57,15 +58,23 @@ int cts_engine_get_attr(const cts_engine*, int, int*) { return CTS_E_NO_DEVICE; 
 int cts_engine_stream_create(cts_engine*, void**) { return CTS_E_NO_DEVICE; }
 int cts_engine_stream_destroy(cts_engine*, void*) { return CTS_E_NO_DEVICE; }
 
-hipError_t hipStreamSynchronize(hipStream_t) { return hipErrorNoDevice; }
-hipError_t hipMallocAsync(void**, size_t, hipStream_t) { return hipErrorNoDevice; }
-hipError_t hipFreeAsync(void*, hipStream_t) { return hipErrorNoDevice; }
-hipError_t hipMemcpyAsync(void*, const void*, size_t, hipMemcpyKind, hipStream_t) { return hipErrorNoDevice; }
-hipError_t hipEventCreateWithFlags(hipEvent_t*, unsigned) { return hipErrorNoDevice; }
-hipError_t hipEventRecord(hipEvent_t, hipStream_t) { return hipErrorNoDevice; }
-hipError_t hipEventQuery(hipEvent_t) { return hipErrorNoDevice; }
-hipError_t hipEventSynchronize(hipEvent_t) { return hipErrorNoDevice; }
-hipError_t hipEventDestroy(hipEvent_t) { return hipErrorNoDevice; }
+// The HIP runtime calls the host code makes, all failing. Weak: a driver that needs a working fake device
+// (counters_fold.cpp: host memory standing in for device memory) defines its own.
+#define CTS_STUB __attribute__((weak))
+CTS_STUB hipError_t hipStreamSynchronize(hipStream_t) { return hipErrorNoDevice; }
+CTS_STUB hipError_t hipMallocAsync(void**, size_t, hipStream_t) { return hipErrorNoDevice; }
+CTS_STUB hipError_t hipFreeAsync(void*, hipStream_t) { return hipErrorNoDevice; }
+CTS_STUB hipError_t hipMemcpyAsync(void*, const void*, size_t, hipMemcpyKind, hipStream_t) { return hipErrorNoDevice; }
+CTS_STUB hipError_t hipEventCreateWithFlags(hipEvent_t*, unsigned) { return hipErrorNoDevice; }
+CTS_STUB hipError_t hipEventRecord(hipEvent_t, hipStream_t) { return hipErrorNoDevice; }
+CTS_STUB hipError_t hipEventQuery(hipEvent_t) { return hipErrorNoDevice; }
+CTS_STUB hipError_t hipEventSynchronize(hipEvent_t) { return hipErrorNoDevice; }
+CTS_STUB hipError_t hipEventDestroy(hipEvent_t) { return hipErrorNoDevice; }
+CTS_STUB hipError_t hipMalloc(void**, size_t) { return hipErrorNoDevice; }
+CTS_STUB hipError_t hipFree(void*) { return hipErrorNoDevice; }
+CTS_STUB hipError_t hipGetDevice(int*) { return hipErrorNoDevice; }
+CTS_STUB hipError_t hipSetDevice(int) { return hipErrorNoDevice; }
+CTS_STUB int cts_engine_device(const cts_engine*) { return CTS_E_NO_DEVICE; }
 
 // A "device" counter block here is host memory with the device layout (CTS_COUNTER_SHARDS shards of 8 u64,
 // the first 5 used), so the host-side fold of cts_counters_read_multi can be driven without a GPU.
@@ -81,3 +90,8 @@ int cts_counters_read(cts_engine* e, const void* dev_counters, cts_counters* out
 }
 
 }  // extern "C"
+
+namespace cts {
+// the device fold of cts_counters_allreduce (cts_collective.cpp); counters_fold.cpp defines a host one
+CTS_STUB hipError_t launch_counters_fold(const void*, uint64_t*, bool, hipStream_t) { return hipErrorNoDevice; }
+}  // namespace cts

@@ -31,6 +31,10 @@ def test_gpus2_launches_two_ranks_and_prints_one_line():
     assert j["n_gpus"] == 2 and j["stub"] is True
     # every rank ran with RANK / WORLD_SIZE / LOCAL_RANK set by the launcher
     assert sorted(tuple(x) for x in j["ranks"]) == [(0, 2, 0), (1, 2, 1)]
+    # the per-rank diagnostics of the real line (stand-in values): kernel time and placement of every rank
+    assert j["roofline"]["per_rank_avg_kernel_us"] == [40.0, 41.0]
+    assert j["per_rank_device"] == [0, 1] and j["per_rank_torch_device"] == [0, 1]
+    assert j["per_rank_local_rank"] == [0, 1] and j["placement_ok"] is True
 
 
 def test_gpus1_runs_in_process():
@@ -39,6 +43,7 @@ def test_gpus1_runs_in_process():
     assert r.returncode == 0, r.stderr[-2000:]
     j = json.loads(r.stdout.strip())
     assert j["n_gpus"] == 1 and j["ranks"] == [[0, 1, 0]]
+    assert j["roofline"]["per_rank_avg_kernel_us"] == [40.0] and j["per_rank_device"] == [0]
 
 
 def test_world_size_must_equal_gpus():

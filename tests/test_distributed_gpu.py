@@ -83,3 +83,66 @@ def test_rccl_world1_collectives_of_the_multi_gpu_path():
     assert glob == local == exp and exp["buffers_failed"] > 0
     assert ok == 1 and t == 1.25 and gathered == 2.5
     assert p.exitcode == 0
+
+
+def _allreduce_main(q):
+    """cts_counters_allreduce through the C ABI: one engine (a one-rank RCCL clique), then two engines on this GPU
+    (folded into one device slot; each on its own stream), against cts_counters_read_multi and the oracle."""
+    try:
+        import torch
+
+        import oracle
+        from ctstraffic_amd import Engine
+        from ctstraffic_amd import workload as W
+        from ctstraffic_amd.engine import counters_allreduce, counters_allreduce_release, counters_read_multi
+
+        torch.cuda.set_device(0)
+        out = {}
+        with Engine(0) as e0, Engine(0) as e1:
+            blocks, exps = [], []
+            for k, eng in enumerate((e0, e1)):
+                w = W.connection_streams(world=2, rank=k, n_conns=64, buffers_per_conn=8, length=65536,
+                                         corrupt_rate=7 + k)
+                arena, descs = W.materialize(eng, w, device="cuda:0")
+                ctr = eng.new_counters()
+                eng.verify(arena, descs, max_length_hint=65536, counters=ctr)
+                torch.cuda.synchronize()
+                blocks.append(ctr)
+                exps.append(oracle.verify_batch(arena.cpu().numpy(), w.descs)[1])
+            out["one"] = (counters_allreduce([e0], blocks[:1]), counters_read_multi([e0], blocks[:1]), exps[0])
+            s0, s1 = e0.stream_create(), e1.stream_create()
+            out["two"] = (counters_allreduce([e0, e1], blocks, [s0, s1]), counters_read_multi([e0, e1], blocks),
+                          {k: exps[0][k] + exps[1][k] for k in exps[0]})
+            counters_allreduce_release()
+            out["again"] = counters_allreduce([e0, e1], blocks)
+            counters_allreduce_release()
+            e0.stream_destroy(s0)
+            e1.stream_destroy(s1)
+        q.put(out)
+    except Exception as e:  # pragma: no cover
+        q.put(("error", repr(e)))
+
+
+def test_counters_allreduce_c_abi_over_rccl():
+    """north_star / config 5: the RCCL all-reduce of the ctsStatistics counters, issued from the C ABI (ctsTraffic's
+    one-process C++ host cannot call torch.distributed). Run in a child so RCCL's threads end with it."""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_allreduce_main, args=(q,), daemon=True)
+    p.start()
+    try:
+        r = q.get(timeout=100)
+        p.join(15)
+    finally:
+        if p.is_alive():
+            p.kill()
+            p.join(5)
+    assert not (isinstance(r, tuple) and r[0] == "error"), r[1]
+    red, fold, exp = r["one"]
+    assert red == fold == exp and exp["buffers_failed"] > 0
+    red, fold, exp = r["two"]
+    assert red == fold == exp
+    assert r["again"] == exp
+    assert p.exitcode == 0

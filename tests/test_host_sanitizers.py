@@ -19,7 +19,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HOST_SRCS = ["cts_pattern.cpp", "cts_media_stream.cpp", "cts_status.cpp", "cts_loopback.cpp", "cts_loopback_udp.cpp",
-             "cts_host_util.cpp"]
+             "cts_host_util.cpp", "cts_collective.cpp"]
 SAN = {
     "plain": [],
     "asan-ubsan": ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"],
@@ -45,8 +45,16 @@ def _build(d, san, driver, extra_link=()):
                     os.path.join(ROOT, "oracle", "cts_oracle.c"), "-o", o], check=True)
     objs.append(o)
     exe = os.path.join(d, driver[:-4])
-    subprocess.run(["g++", *flags, *objs, "-o", exe, *extra_link], check=True)
+    subprocess.run(["g++", *flags, *objs, "-o", exe, *extra_link, "-ldl"], check=True)
     return exe
+
+
+def _build_rccl_stub(d, san):
+    """tests/cpp/rccl_stub.cpp as the shared library cts_counters_allreduce loads ($CTS_RCCL_LIBRARY)."""
+    so = os.path.join(d, "librccl_stub.so")
+    subprocess.run(["g++", "-std=c++17", "-g", "-O1", "-fPIC", "-shared", "-pthread", *SAN[san], "-I", "/opt/rocm/include",
+                    "-D__HIP_PLATFORM_AMD__", os.path.join(ROOT, "tests", "cpp", "rccl_stub.cpp"), "-o", so], check=True)
+    return so
 
 
 @pytest.mark.parametrize("san", sorted(set(SAN) - {"plain"}))
@@ -56,7 +64,9 @@ def _build(d, san, driver, extra_link=()):
 def test_host_code_under_sanitizer(san, driver):
     with tempfile.TemporaryDirectory() as d:
         exe = _build(d, san, driver)
-        out = subprocess.run([exe], capture_output=True, text=True, timeout=300, env={**os.environ, **ENV})
+        # counters_fold also drives cts_counters_allreduce against a stub RCCL (tests/cpp/rccl_stub.cpp)
+        args = [_build_rccl_stub(d, san)] if driver == "counters_fold.cpp" else []
+        out = subprocess.run([exe, *args], capture_output=True, text=True, timeout=300, env={**os.environ, **ENV})
         assert out.returncode == 0, (out.returncode, out.stderr[-4000:])
         assert ": ok" in out.stdout
         assert "runtime error" not in out.stderr and "WARNING: ThreadSanitizer" not in out.stderr, out.stderr[-4000:]

@@ -264,39 +264,23 @@ def _to_dev(a, torch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("ms_variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12])
-def test_gpu_media_stream_verify_matches_oracle(engine, tuning_engine, ms_variant):
-    """ms_variant 0: one wave per datagram; 1: four datagrams per wave, header by byte loads;
-    2: four per wave, header by 16-byte chunk loads gathered with DPP row shifts; 3: variant 2
-    walking block-contiguous datagram ranges (the default, the product library's only one; the others run on
-    the tuning build); 4 / 5 / 6: variant 3 writing its outputs every 8 / 16 / 32 rounds from a per-wave
-    LDS ring (partial last rings, chunk ends and the launch end inside a ring are all covered by the
-    block/chunk shapes below); 7: variant 3, with cts_media_stream_verify_status in its two-pass form (header
-    gather, then a payload pass that only clears the pass byte of corrupt datagrams); 8 / 9: variant 3 with the
-    statuses of cts_media_stream_verify_status written every round / every 16 rounds, 10: every 32 rounds (the
-    product default stages them in the per-wave ring for 64 rounds); 11: variant 3 writing records + results every
-    round (the product writes them every 64 rounds from the ring); 12: variant 3 and the compact receive with the
-    header / edge loads nontemporal (round 2's product)."""
+def test_gpu_media_stream_verify_matches_oracle(engine):
+    """The MediaStream receive (four datagrams per wave, header by 16-byte chunk loads gathered with DPP row shifts,
+    block-contiguous datagram ranges, outputs written every 64 rounds from a per-wave LDS ring) vs the oracle under
+    several walks: several rounds per workgroup, chunked walks (partial last rings, chunk ends and the launch end
+    inside a ring), and outputs at 4-byte-aligned (not 16) addresses."""
     from ctstraffic_amd import _lib
 
-    if ms_variant != 3:
-        engine = tuning_engine
-    default = engine.get_attr(_lib.ATTR_MS_VARIANT)
     default_sbpc = engine.get_attr(_lib.ATTR_SMALL_BLOCKS_PER_CU)
     default_chunk = engine.get_attr(_lib.ATTR_SMALL_CHUNK)
-    engine.set_attr(_lib.ATTR_MS_VARIANT, ms_variant)
     try:
         # sbpc 1: several rounds per workgroup (5 000+ datagrams over 256 workgroups); chunked walks
         for sbpc, chunk in ((1, 0), (64, 0), (1, 16), (2, 48), (1, 200)):
-            if chunk and ms_variant < 3:
-                continue
             engine.set_attr(_lib.ATTR_SMALL_BLOCKS_PER_CU, sbpc)
             engine.set_attr(_lib.ATTR_SMALL_CHUNK, chunk)
             _media_stream_verify_vs_oracle(engine)
-        if ms_variant >= 3:  # outputs at 4-byte-aligned (not 16) addresses
-            _media_stream_verify_vs_oracle(engine, out_shift=4)
+        _media_stream_verify_vs_oracle(engine, out_shift=4)
     finally:
-        engine.set_attr(_lib.ATTR_MS_VARIANT, default)
         engine.set_attr(_lib.ATTR_SMALL_BLOCKS_PER_CU, default_sbpc)
         engine.set_attr(_lib.ATTR_SMALL_CHUNK, default_chunk)
 

@@ -161,13 +161,13 @@ def test_bad_descriptors(engine):
     assert ctr == ectr and ctr["buffers_checked"] == 1
 
 
-def test_bad_descriptors_staged_results(tuning_engine):
-    """Verify variant 18 stages result records in LDS and writes 16 at a time: bad descriptors interleaved with
-    valid and corrupt buffers across several staging flushes, one and many workgroups, vs the oracle."""
+def test_bad_descriptors_interleaved(engine):
+    """Bad descriptors interleaved with valid and corrupt buffers, one and many workgroups (each workgroup then walks
+    bad, clean and corrupt buffers in turn), vs the oracle."""
     from ctstraffic_amd import _lib
 
-    eng = tuning_engine
-    dv, dbpc = eng.get_attr(_lib.ATTR_VERIFY_VARIANT), eng.get_attr(_lib.ATTR_BLOCKS_PER_CU)
+    eng = engine
+    dbpc = eng.get_attr(_lib.ATTR_BLOCKS_PER_CU)
     rng = np.random.default_rng(77)
     arena = np.zeros(1 << 20, np.uint8)
     oracle.fill(arena, np.array([(0, 1 << 20, 0, 0, 0)], dtype=oracle.DESC_DTYPE))
@@ -183,7 +183,6 @@ def test_bad_descriptors_staged_results(tuning_engine):
         if k % 5 != 3:
             arena[int(d[k]["byte_offset"]) + int(d[k]["length"]) - 1] ^= 0x11
     try:
-        eng.set_attr(_lib.ATTR_VERIFY_VARIANT, 18)
         for bpc in (1, 16):
             eng.set_attr(_lib.ATTR_BLOCKS_PER_CU, bpc)
             r, ctr, cff = run_verify(eng, arena, d, 0, n_conns=7)
@@ -191,7 +190,6 @@ def test_bad_descriptors_staged_results(tuning_engine):
             assert_results_equal(r, er, "bpc %d" % bpc)
             assert ctr == ectr and np.array_equal(cff, ecff)
     finally:
-        eng.set_attr(_lib.ATTR_VERIFY_VARIANT, dv)
         eng.set_attr(_lib.ATTR_BLOCKS_PER_CU, dbpc)
 
 
@@ -920,25 +918,24 @@ def test_verify_host_batch(engine):
         assert c == ec
 
 
-# ---- every launch variant / geometry is bit-identical ------------------------------------------
-@pytest.mark.parametrize("variant", list(range(29)))
+# ---- every launch geometry and load policy is bit-identical ----------------------------------------
 @pytest.mark.parametrize("nt", [1, 0])
-def test_launch_variants_parity(tuning_engine, variant, nt):
+def test_launch_geometry_parity(engine, nt):
+    """The workgroup-per-buffer kernel and the small-buffer kernel under nontemporal and plain loads, 1 and 16
+    workgroups per CU: random lengths, alignments, phases and skips, spans longer than the small-path hint, whole-line
+    arenas, fewer buffers than workgroups, more than 1024 buffers per workgroup, vs the oracle."""
     from ctstraffic_amd import _lib
 
-    engine = tuning_engine
-    default_variant = engine.get_attr(_lib.ATTR_VERIFY_VARIANT)
     default_bpc = engine.get_attr(_lib.ATTR_BLOCKS_PER_CU)
     default_small_bpc = engine.get_attr(_lib.ATTR_SMALL_BLOCKS_PER_CU)
     try:
-        engine.set_attr(_lib.ATTR_VERIFY_VARIANT, variant)
         engine.set_attr(_lib.ATTR_NT_LOADS, nt)
         for seed, n, max_len, hint, skip, whole in [
                 (21, 200, 3000, 1472, True, False), (22, 64, 140000, 0, False, False),
                 (23, 300, 1472, 1472, True, False), (24, 100, 70000, 0, True, False),
-                (25, 6000, 9000, 0, False, False),  # > kRing buffers per workgroup
+                (25, 6000, 9000, 0, False, False),
                 (26, 400, 140000, 0, False, True), (27, 300, 2000, 1472, False, True),
-                (28, 3, 70000, 0, False, False)]:  # fewer buffers than windows (variants 15-17)
+                (28, 3, 70000, 0, False, False)]:
             for bpc in (1, 16):
                 engine.set_attr(_lib.ATTR_BLOCKS_PER_CU, bpc)
                 engine.set_attr(_lib.ATTR_SMALL_BLOCKS_PER_CU, bpc)
@@ -946,7 +943,7 @@ def test_launch_variants_parity(tuning_engine, variant, nt):
                 arena, descs = _random_case(rng, n, max_len, skip=skip, whole=whole)
                 r, ctr, cff = run_verify(engine, arena, descs, hint, n_conns=7)
                 er, ectr, ecff = oracle.verify_batch(arena, descs, n_conns=7)
-                assert_results_equal(r, er, "variant %d nt %d seed %d bpc %d" % (variant, nt, seed, bpc))
+                assert_results_equal(r, er, "nt %d seed %d bpc %d" % (nt, seed, bpc))
                 assert ctr == ectr
                 assert np.array_equal(cff, ecff)
         w = W.udp_datagrams(n_datagrams=4099, corrupt_rate=7)
@@ -954,41 +951,33 @@ def test_launch_variants_parity(tuning_engine, variant, nt):
         w = W.tcp_resident(n_buffers=300, corrupt_rate=5)
         _check_workload(engine, w, with_oracle=True)
     finally:
-        engine.set_attr(_lib.ATTR_VERIFY_VARIANT, default_variant)
         engine.set_attr(_lib.ATTR_NT_LOADS, 1)
         engine.set_attr(_lib.ATTR_BLOCKS_PER_CU, default_bpc)
         engine.set_attr(_lib.ATTR_SMALL_BLOCKS_PER_CU, default_small_bpc)
 
 
-# ---- every small-buffer (datagram) kernel is bit-identical --------------------------------------
-@pytest.mark.parametrize("small_variant", list(range(16)))
-def test_small_variants_parity(tuning_engine, small_variant):
-    """Small-buffer path (max_length_hint <= 8192): one wave per buffer (0-4) and four
-    buffers per wave in 16-lane teams (5-8; 9 walking block-contiguous ranges), vs the oracle. Includes spans longer than the
-    hint (multi-round teams), empty spans, all start alignments, bad descriptors, a batch
-    whose size is not a multiple of the team count, and config-3 datagrams."""
+# ---- the small-buffer (datagram) kernel under every walk ------------------------------------------------
+def test_small_path_parity(engine):
+    """Small-buffer path (max_length_hint <= 8192, four buffers per wave in 16-lane teams) under block-contiguous and
+    chunked walks and 1 / 2 / 64 workgroups per CU, vs the oracle. Includes spans longer than the hint (multi-round
+    teams), empty spans, all start alignments, bad descriptors, a batch whose size is not a multiple of the team count,
+    and config-3 datagrams."""
     from ctstraffic_amd import _lib
 
-    engine = tuning_engine
-    default_sv = engine.get_attr(_lib.ATTR_SMALL_VARIANT)
     default_sbpc = engine.get_attr(_lib.ATTR_SMALL_BLOCKS_PER_CU)
     default_chunk = engine.get_attr(_lib.ATTR_SMALL_CHUNK)
     try:
-        engine.set_attr(_lib.ATTR_SMALL_VARIANT, small_variant)
         for seed, n, max_len, hint, skip in [(31, 301, 1500, 1472, True), (32, 257, 200, 64, False),
                                              (33, 120, 20000, 1472, True), (34, 1000, 3000, 8192, False),
                                              (35, 7, 40, 40, True)]:
             for sbpc, chunk in ((1, 0), (64, 0), (1, 16), (2, 48)):
-                if chunk and small_variant < 9:  # (only variants 9-12 walk chunks)
-                    continue
                 engine.set_attr(_lib.ATTR_SMALL_BLOCKS_PER_CU, sbpc)
                 engine.set_attr(_lib.ATTR_SMALL_CHUNK, chunk)
                 rng = np.random.default_rng(seed)
                 arena, descs = _random_case(rng, n, max_len, skip=skip)
                 r, ctr, cff = run_verify(engine, arena, descs, hint, n_conns=7)
                 er, ectr, ecff = oracle.verify_batch(arena, descs, n_conns=7)
-                assert_results_equal(r, er, "small variant %d seed %d sbpc %d chunk %d" % (small_variant, seed, sbpc,
-                                                                                           chunk))
+                assert_results_equal(r, er, "seed %d sbpc %d chunk %d" % (seed, sbpc, chunk))
                 assert ctr == ectr
                 assert np.array_equal(cff, ecff)
         arena = np.zeros(256, np.uint8)
@@ -1006,43 +995,32 @@ def test_small_variants_parity(tuning_engine, small_variant):
         w = W.udp_datagrams(n_datagrams=4099, corrupt_rate=7)
         _check_workload(engine, w, with_oracle=True)
     finally:
-        engine.set_attr(_lib.ATTR_SMALL_VARIANT, default_sv)
         engine.set_attr(_lib.ATTR_SMALL_BLOCKS_PER_CU, default_sbpc)
         engine.set_attr(_lib.ATTR_SMALL_CHUNK, default_chunk)
 
 
-def _pick(attr, variant, product_engine, tuning_engine):
-    from ctstraffic_amd import _lib
-
-    dflt = {_lib.ATTR_VERIFY_VARIANT: 25, _lib.ATTR_SMALL_VARIANT: 15, _lib.ATTR_MS_VARIANT: 3}[attr]
-    return product_engine if variant == dflt else tuning_engine
-
-
-def test_product_build_launches_the_defaults_only(engine, tuning_engine):
-    """The product library compiles one kernel per path (verify variant 25, small variant 15, MediaStream variant 3)
-    and refuses the others; the tuning build accepts every variant."""
+def test_kernel_ids_are_fixed(engine):
+    """One kernel per path: the variant attributes report its id (verify 25, small 15, MediaStream 3) and refuse any
+    other value."""
     from ctstraffic_amd import _lib
     from ctstraffic_amd._lib import CtsError
 
-    assert "tuning" not in _lib.lib().cts_version().decode()
-    assert "tuning" in _lib.tuning_lib().cts_version().decode()
     for attr, dflt, others in ((_lib.ATTR_VERIFY_VARIANT, 25, (0, 4, 12, 13, 17)), (_lib.ATTR_SMALL_VARIANT, 15, (0, 5, 9)),
                                (_lib.ATTR_MS_VARIANT, 3, (0, 2))):
-        assert engine.get_attr(attr) == dflt and tuning_engine.get_attr(attr) == dflt
+        assert engine.get_attr(attr) == dflt
         engine.set_attr(attr, dflt)
         for v in others:
             with pytest.raises(CtsError):
                 engine.set_attr(attr, v)
-            tuning_engine.set_attr(attr, v)
-        tuning_engine.set_attr(attr, dflt)
+        assert engine.get_attr(attr) == dflt
 
 
 # ---- maximum sizes: one buffer of 2^32 - 1 bytes, buffers past the 4 GiB arena offset -----------------------
-def test_max_length_buffers(engine, tuning_engine):
+def test_max_length_buffers(engine):
     """ctsTask::m_bufferLength is a u32: a single 2^32 - 1-byte buffer (last byte corrupted) and a 2^31 + 77-byte
-    buffer starting past 2^32 in the arena at an odd address with the MediaStream skip. Both kernels paths; the fill
-    writes them first (its 64-bit offsets are checked at sampled positions against the oracle's pattern). Every
-    kernel family: workgroup, barrier-free workgroup, wave, pipelined wave, four-per-wave."""
+    buffer starting past 2^32 in the arena at an odd address with the MediaStream skip. Both kernel paths (workgroup
+    per buffer, four buffers per wave); the fill writes them first (its 64-bit offsets are checked at sampled positions
+    against the oracle's pattern)."""
     L0, L1 = 2**32 - 1, 2**31 + 77
     off1 = 2**32 + 3
     total = off1 + L1 + 64
@@ -1069,18 +1047,7 @@ def test_max_length_buffers(engine, tuning_engine):
     exp_first = [c0, c1]
     exp_bytes = [int(pat[(12345 + c0) % 65536]), int(pat[(65535 + c1) % 65536])]
     act_bytes = [exp_bytes[0] ^ 0x5A, exp_bytes[1] ^ 0xFF]
-    from ctstraffic_amd import _lib
-
-    cases = [(_lib.ATTR_VERIFY_VARIANT, 25, 0), (_lib.ATTR_VERIFY_VARIANT, 13, 0), (_lib.ATTR_VERIFY_VARIANT, 4, 0), (_lib.ATTR_VERIFY_VARIANT, 3, 0),
-             (_lib.ATTR_VERIFY_VARIANT, 18, 0),
-             (_lib.ATTR_SMALL_VARIANT, 15, 1472), (_lib.ATTR_SMALL_VARIANT, 9, 1472), (_lib.ATTR_SMALL_VARIANT, 0, 1472),
-             (_lib.ATTR_SMALL_VARIANT, 3, 1472)]
-    product_engine = engine
-    defaults = {a: tuning_engine.get_attr(a) for a, _, _ in cases}
-    for attr, variant, hint in cases:  # workgroup, barrier-free workgroup, wave, four-per-wave, wave, pipelined wave
-        # the defaults run on the product engine, the other families on the tuning build's
-        engine = _pick(attr, variant, product_engine, tuning_engine)
-        engine.set_attr(attr, variant)
+    for hint in (0, 1472):  # workgroup per buffer, four buffers per wave
         res = engine.new_results(2)
         ctr = engine.new_counters()
         engine.verify(arena, d, max_length_hint=hint, results=res, counters=ctr)
@@ -1089,11 +1056,10 @@ def test_max_length_buffers(engine, tuning_engine):
         for b in range(2):
             assert (int(r[b]["first_mismatch"]), int(r[b]["mismatch_bytes"]), int(r[b]["expected"]),
                     int(r[b]["actual"]), int(r[b]["pass"])) == (exp_first[b], 1, exp_bytes[b], act_bytes[b], 0), (
-                        attr, variant, b)
+                        hint, b)
         c = engine.read_counters(ctr)
         assert c == {"bytes_checked": L0 + L1 - 26, "bytes_ok": 0, "buffers_checked": 2, "buffers_failed": 2,
                      "mismatched_bytes": 2}
-        engine.set_attr(attr, defaults[attr])
     del arena
     torch.cuda.empty_cache()
 

@@ -2,7 +2,8 @@
 # One gpurun call: GPU parity tests, smoke, bench, rocprofv3 kernel-trace stats and
 # PMC HBM-traffic passes. Every GPU step has its own time limit; steps chain with &&
 # semantics (set -e), so nothing more runs on the GPU after a failure.
-#   usage (from this container):  gpurun --timeout 1100 -- bash tools/gpu_round.sh TAG
+#   usage (from this container):  make probes && gpurun --timeout 1100 -- bash tools/gpu_round.sh TAG
+#   (the ceiling / timeline steps run the probes of `make probes`)
 set -euo pipefail
 TAG=${1:-r01}
 OUT=gpurun_out/$TAG
@@ -16,12 +17,6 @@ if [[ $STEPS == all || $STEPS == *tests* ]]; then
     > "$OUT/pytest_gpu.log" 2>&1
   run smoke
   timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
-fi
-if [[ $STEPS == *variants* ]]; then
-  # every tuning launch variant bit-exact against the oracle (tests/test_verify_gpu.py::test_launch_variants_parity)
-  run variants-parity
-  timeout -k 10 300 python -u -m pytest tests/test_verify_gpu.py -m gpu -x -q -p no:cacheprovider --timeout 120 \
-    --timeout-method thread -k "launch_variants_parity" > "$OUT/pytest_variants.log" 2>&1
 fi
 if [[ $STEPS == all || $STEPS == *bench* ]]; then
   run bench

@@ -65,7 +65,7 @@ int main(int argc, char** argv)
         // every job goes to group 0 (the engine's choice for one caller); the other G - 1 groups idle
         const uint32_t S = nslots / G;
         cts::MailStarts starts{};
-        if (cts::launch_mailbox(dslots, dparts, S, starts, G, 100000000ull, s, 0, 1) != hipSuccess) return 1;
+        if (cts::launch_mailbox(dslots, dparts, S, starts, G, 100000000ull, s, 0) != hipSuccess) return 1;
         const uint64_t ptr = reinterpret_cast<uint64_t>(dbuf);
         const uint32_t np = cts::mail_parts(ptr, len);
         double sum_first = 0, sum_last = 0, t_begin = 0;

@@ -28,7 +28,6 @@ WORKLOADS = {
     "verify_wg_kernel": "config2 verify: 4096 x 64 KiB (268435456 B read)",
     "fill_kernel": "config2 fill: 4096 x 64 KiB (268435456 B written)",
     "verify_quad_kernel": "config3 verify: 16M x 1472 B datagrams (%d B payload read)" % (DG * 1446),
-    "verify_wave_kernel": "config3 verify: 16M x 1472 B datagrams (%d B payload read)" % (DG * 1446),
     "media_stream_verify_quad_kernel": "config3 MediaStream receive: 16M x 1472 B datagrams (%d B payload read)" % (
         DG * 1446),
     "media_stream_verify_quad_kernel[strided]": "config3 MediaStream receive, strided ring (lengths only): 16M x "
@@ -50,7 +49,7 @@ WORKLOADS = {
 }
 ALGO_BYTES = {"fill_batched_kernel": DG * 1472, "media_stream_fill_ring_kernel": DG * 1472,
               "verify_wg_kernel": 268435456, "fill_kernel": 268435456, "verify_quad_kernel": DG * 1446,
-              "verify_wave_kernel": DG * 1446, "media_stream_verify_quad_kernel": DG * 1446,
+              "media_stream_verify_quad_kernel": DG * 1446,
               "media_stream_verify_quad_kernel[strided]": DG * 1446, "verify_quad_kernel[strided]": DG * 1446,
               "media_stream_verify_quad_kernel[status]": DG * 1446,
               "media_stream_verify_quad_kernel[strided][status]": DG * 1446,
@@ -63,12 +62,11 @@ def _kname(name):
     base = name.split("(")[0].split("<")[0].split("::")[-1].strip()
     if base in ("media_stream_verify_quad_kernel", "verify_quad_kernel") and "<" in name:
         targs = [t.strip() for t in name.split("(")[0].split("<", 1)[1].rsplit(">", 1)[0].split(",")]
-        # template arguments: STRIDED is the 6th (MediaStream) / 5th (verify) one, STATUS the MediaStream's 8th
-        si = 5 if base == "media_stream_verify_quad_kernel" else 4
-        tag = "[strided]" if len(targs) > si and targs[si] == "true" else ""
-        if base == "media_stream_verify_quad_kernel" and len(targs) > 7 and targs[7] == "true":
+        # template arguments <NT, STRIDED[, RING, STATUS, FRAMES]> (cts_kernels.hip)
+        tag = "[strided]" if len(targs) > 1 and targs[1] == "true" else ""
+        if base == "media_stream_verify_quad_kernel" and len(targs) > 3 and targs[3] == "true":
             tag += "[status]"
-        if base == "media_stream_verify_quad_kernel" and len(targs) > 10 and targs[10] == "true":
+        if base == "media_stream_verify_quad_kernel" and len(targs) > 4 and targs[4] == "true":
             tag += "[frames]"
         return base + tag
     return base

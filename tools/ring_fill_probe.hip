@@ -230,22 +230,18 @@ int main(int argc, char** argv)
                             nt, us, (double)b / us / 1e3);
                 std::fflush(stdout);
             };
-            for (int batched : {0, 1}) {
-                for (int bpc : {4, 8}) {
-                    if (!batched && bpc != 4) continue;
-                    cts::LaunchGeometry g2 = geo;
-                    g2.fill_batched = batched;
-                    g2.ring_fill_blocks_per_cu = bpc;
-                    char name[64];
-                    std::snprintf(name, sizeof name, "product%s_bpc%d", batched ? "_batched" : "_wave", bpc);
-                    line(name, time_us([&](int it) {
-                             (void)cts::launch_media_stream_fill(arena[it & 1], bytes, dd, hd, n, nullptr, g2);
-                         }, 5), bytes);
-                    std::snprintf(name, sizeof name, "payload%s_bpc%d", batched ? "_batched" : "_wave", bpc);
-                    line(name, time_us([&](int it) {
-                             (void)cts::launch_fill(arena[it & 1], bytes, dp, n, len, nullptr, g2);
-                         }, 5), (uint64_t)n * (len - 26u));
-                }
+            for (int bpc : {4, 8}) {
+                cts::LaunchGeometry g2 = geo;
+                g2.ring_fill_blocks_per_cu = bpc;
+                char name[64];
+                std::snprintf(name, sizeof name, "product_batched_bpc%d", bpc);
+                line(name, time_us([&](int it) {
+                         (void)cts::launch_media_stream_fill(arena[it & 1], bytes, dd, hd, n, nullptr, g2);
+                     }, 5), bytes);
+                std::snprintf(name, sizeof name, "payload_wave_bpc%d", bpc);
+                line(name, time_us([&](int it) {
+                         (void)cts::launch_fill(arena[it & 1], bytes, dp, n, len, nullptr, g2);
+                     }, 5), (uint64_t)n * (len - 26u));
             }
             for (uint32_t bpc : {4u, 8u, 16u}) {
                 const uint32_t g = (uint32_t)geo.num_cus * bpc, stride = g * 256u;

@@ -4,12 +4,10 @@
 // The product kernel (cts_kernels.hip, included verbatim) against the plain read of the same shape, in one process on
 // one box, 8 rotated 256 MiB arenas (4096 x 64 KiB buffers each; 75 % phase-0 / 25 % random expected offsets, one
 // corrupt byte per 1024 buffers, as bench.py's config 2):
-//   time    : HIP events around R launches, per launch: verify_wg_kernel variant 13 ("product_verify_us": the
-//             default until late in round 4; the replica mirrors it), variant 25 (the same code with registers for 4
-//             waves per SIMD, the default since), the tuning variants 22 = A16, 23 = SPEC, 24 = both, a
-//             replica of it built from the same device helpers with the stamps compiled out (must equal the product),
-//             and the plain read (grid = 4 x CUs, workgroup b reads 64-KiB slabs b, b + grid, ..., U = 2, the
-//             verify's per-buffer barrier);
+//   time    : HIP events around R launches, per launch: the product verify_wg_kernel ("product_verify_us"), a
+//             replica of its whole-line path built from the same device helpers with the stamps compiled out (must
+//             equal the product), a depth-2 pipelined form (pipe2), and the plain read (grid = 4 x CUs, workgroup b
+//             reads 64-KiB slabs b, b + grid, ..., U = 2, the verify's per-buffer barrier);
 //   timeline: per-workgroup s_memrealtime stamps (100 MHz) of the stamped replica and of the plain read:
 //             entry, first data issue (after the first descriptor arrived), the end of every buffer, the end
 //             after the counter flush; printed as percentiles over the 1024 workgroups and by XCC.
@@ -113,10 +111,10 @@ __global__ void __launch_bounds__(256, 8)
     cts::flush_counters<1>(counters, ctr);
 }
 
-// verify_wg_kernel<2, true, true, false, true, true> (the product's variant 13) on the whole-line path every config-2
-// buffer takes, built from the same helpers; STAMP adds the timeline stores (lane 0, one 8-byte store per event).
+// verify_wg_kernel<true> on the whole-line path every config-2 buffer takes, built from the same helpers; STAMP adds the
+// timeline stores (lane 0, one 8-byte store per event).
 template <bool STAMP>
-__global__ void __launch_bounds__(256, 8)
+__global__ void __launch_bounds__(256, 4)
     verify_replica(const uint8_t* __restrict__ arena, uint64_t arena_bytes, const cts_buf_desc* __restrict__ descs,
                    uint32_t n, cts_verify_result* __restrict__ results, uint64_t* __restrict__ counters,
                    uint32_t* __restrict__ conn_first_fail, uint32_t n_conns, uint64_t* __restrict__ st)
@@ -186,10 +184,7 @@ __global__ void __launch_bounds__(256) plain_read(const u32x4* __restrict__ p, u
     }
 }
 
-// the product kernel's tuning variants 22 (A16), 23 (SPEC), 24 (both) beside the default 13
-#define PRODUCT_VARIANT(A16, SPEC) cts::verify_wg_kernel<2, true, true, false, true, true, 1, 0, 0, 256, A16, SPEC>
-// variant 25: variant 13 with its registers allocated for 4 waves per SIMD (no SGPR spills)
-#define VARIANT_25 cts::verify_wg_kernel<2, true, true, false, true, true, 1, 0, 0, 256, false, false, 4>
+#define PRODUCT cts::verify_wg_kernel<true>
 
 // XCD-skewed plain read ("skew" mode): the grid has S = gridDim.x / 8 slots per XCD (workgroup b runs on XCD b mod 8,
 // the dispatcher's round robin); on the odd XCDs only S - 2 dd of them work, dd = S * SKEW / (64 + SKEW), so the even
@@ -511,10 +506,10 @@ int main(int argc, char** argv)
                 plain_read<false, 2><<<grid, 256, 0, s>>>(reinterpret_cast<const u32x4*>(arena[i % R]), n, st, out);
             }, reps, s);
             const double v0 = time_us([&](int i) {
-                VARIANT_25<<<grid, 256, 0, s>>>(arena[i % R], bytes, d, n, res, ctr, cff, n);
+                PRODUCT<<<grid, 256, 0, s>>>(arena[i % R], bytes, d, n, res, ctr, cff, n);
             }, reps, s);
             const double v2 = time_us([&](int i) {
-                VARIANT_25<<<grid, 256, 0, s>>>(arena[i % R], bytes, dp, n, res, ctr, cff, n);
+                PRODUCT<<<grid, 256, 0, s>>>(arena[i % R], bytes, dp, n, res, ctr, cff, n);
             }, reps, s);
             std::printf("{\"kind\":\"map_time\",\"pass\":%d,\"launches\":%d,\"plain_map0_us\":%.2f,\"plain_map1_us\":%.2f,"
                         "\"plain_map2_us\":%.2f,\"verify_descs_in_order_us\":%.2f,\"verify_descs_map2_us\":%.2f}\n",
@@ -535,10 +530,10 @@ int main(int argc, char** argv)
         }
         return 0;
     }
-    // parity of the replica against the product on arena 0 (the tool measures the product's code path)
+    // parity of the replica and the pipelined form against the product on arena 0
     {
         std::vector<cts_verify_result> a(n), b(n);
-        cts::verify_wg_kernel<2, true, true, false, true, true><<<grid, 256, 0, s>>>(arena[0], bytes, d, n, res, ctr, cff, n);
+        PRODUCT<<<grid, 256, 0, s>>>(arena[0], bytes, d, n, res, ctr, cff, n);
         CHECK(hipMemcpy(a.data(), res, n * sizeof(cts_verify_result), hipMemcpyDeviceToHost));
         CHECK(hipMemset(res, 0, n * sizeof(cts_verify_result)));
         verify_replica<true><<<grid, 256, 0, s>>>(arena[0], bytes, d, n, res, ctr, cff, n, st);
@@ -552,38 +547,17 @@ int main(int argc, char** argv)
             });
         };
         const bool same = eq(a, b);
-        // the speculative form, on the same arena and on one whose first buffers hold a corrupt byte in round 0
-        std::vector<cts_verify_result> c(n);
-        CHECK(hipMemset(res, 0, n * sizeof(cts_verify_result)));
-        PRODUCT_VARIANT(false, true)<<<grid, 256, 0, s>>>(arena[0], bytes, d, n, res, ctr, cff, n);
-        CHECK(hipMemcpy(c.data(), res, n * sizeof(cts_verify_result), hipMemcpyDeviceToHost));
-        const bool spec_same = eq(a, c);
-        CHECK(hipMemset(res, 0, n * sizeof(cts_verify_result)));
-        PRODUCT_VARIANT(true, true)<<<grid, 256, 0, s>>>(arena[0], bytes, d, n, res, ctr, cff, n);
-        CHECK(hipMemcpy(c.data(), res, n * sizeof(cts_verify_result), hipMemcpyDeviceToHost));
-        const bool both_same = eq(a, c);
-        CHECK(hipMemset(res, 0, n * sizeof(cts_verify_result)));
-        PRODUCT_VARIANT(true, false)<<<grid, 256, 0, s>>>(arena[0], bytes, d, n, res, ctr, cff, n);
-        CHECK(hipMemcpy(c.data(), res, n * sizeof(cts_verify_result), hipMemcpyDeviceToHost));
-        const bool a16_same = eq(a, c);
         CHECK(hipMemset(res, 0, n * sizeof(cts_verify_result)));
         verify_pipe<false><<<grid, 256, 0, s>>>(arena[0], bytes, d, n, res, ctr, cff, n);
-        CHECK(hipMemcpy(c.data(), res, n * sizeof(cts_verify_result), hipMemcpyDeviceToHost));
-        std::printf("{\"kind\":\"parity\",\"pipe2_equals_product\":%d}\n", eq(a, c) ? 1 : 0);
-        CHECK(hipMemset(res, 0, n * sizeof(cts_verify_result)));
-        VARIANT_25<<<grid, 256, 0, s>>>(arena[0], bytes, d, n, res, ctr, cff, n);
-        CHECK(hipMemcpy(c.data(), res, n * sizeof(cts_verify_result), hipMemcpyDeviceToHost));
-        std::printf("{\"kind\":\"parity\",\"v25_equals_product\":%d}\n", eq(a, c) ? 1 : 0);
+        CHECK(hipMemcpy(b.data(), res, n * sizeof(cts_verify_result), hipMemcpyDeviceToHost));
         std::printf("{\"kind\":\"parity\",\"kernarg_preload\":%d,\"replica_equals_product\":%d,"
-                    "\"spec_equals_product\":%d,\"a16_equals_product\":%d,\"spec_a16_equals_product\":%d,"
-                    "\"failed_buffers\":%u}\n",
-                    kp ? 1 : 0, same ? 1 : 0, spec_same ? 1 : 0, a16_same ? 1 : 0, both_same ? 1 : 0, failed);
+                    "\"pipe2_equals_product\":%d,\"failed_buffers\":%u}\n",
+                    kp ? 1 : 0, same ? 1 : 0, eq(a, b) ? 1 : 0, failed);
     }
 
     for (int pass = 0; pass < passes; ++pass) {
         const double t_prod = time_us([&](int i) {
-            cts::verify_wg_kernel<2, true, true, false, true, true><<<grid, 256, 0, s>>>(arena[i % R], bytes, d, n, res,
-                                                                                        ctr, cff, n);
+            PRODUCT<<<grid, 256, 0, s>>>(arena[i % R], bytes, d, n, res, ctr, cff, n);
         }, reps, s);
         const double t_rep = time_us([&](int i) {
             verify_replica<false><<<grid, 256, 0, s>>>(arena[i % R], bytes, d, n, res, ctr, cff, n, st);
@@ -591,29 +565,14 @@ int main(int argc, char** argv)
         const double t_plain = time_us([&](int i) {
             plain_read<false><<<grid, 256, 0, s>>>(reinterpret_cast<const u32x4*>(arena[i % R]), n, st, out);
         }, reps, s);
-        const double t_spec = time_us([&](int i) {
-            PRODUCT_VARIANT(false, true)<<<grid, 256, 0, s>>>(arena[i % R], bytes, d, n, res, ctr, cff, n);
-        }, reps, s);
-        const double t_a16 = time_us([&](int i) {
-            PRODUCT_VARIANT(true, false)<<<grid, 256, 0, s>>>(arena[i % R], bytes, d, n, res, ctr, cff, n);
-        }, reps, s);
         const double t_pipe = time_us([&](int i) {
             verify_pipe<false><<<grid, 256, 0, s>>>(arena[i % R], bytes, d, n, res, ctr, cff, n);
         }, reps, s);
-        const double t_both = time_us([&](int i) {
-            PRODUCT_VARIANT(true, true)<<<grid, 256, 0, s>>>(arena[i % R], bytes, d, n, res, ctr, cff, n);
-        }, reps, s);
-        const double t_v25 = time_us([&](int i) {
-            VARIANT_25<<<grid, 256, 0, s>>>(arena[i % R], bytes, d, n, res, ctr, cff, n);
-        }, reps, s);
         std::printf("{\"kind\":\"time\",\"kernarg_preload\":%d,\"pass\":%d,\"launches\":%d,\"product_verify_us\":%.2f,"
-                    "\"v25_wpe4_us\":%.2f,\"v25_over_plain\":%.4f,"
-                    "\"replica_verify_us\":%.2f,\"v23_spec_us\":%.2f,\"v22_a16_us\":%.2f,\"v24_both_us\":%.2f,\"pipe2_us\":%.2f,"
-                    "\"plain_read_us\":%.2f,\"product_GBps\":%.1f,"
-                    "\"plain_GBps\":%.1f,\"product_over_plain\":%.4f,\"spec_over_plain\":%.4f,\"a16_over_plain\":%.4f,"
-                    "\"spec_a16_over_plain\":%.4f}\n",
-                    kp ? 1 : 0, pass, reps, t_prod, t_v25, t_v25 / t_plain, t_rep, t_spec, t_a16, t_both, t_pipe, t_plain, bytes / t_prod / 1e3,
-                    bytes / t_plain / 1e3, t_prod / t_plain, t_spec / t_plain, t_a16 / t_plain, t_both / t_plain);
+                    "\"replica_verify_us\":%.2f,\"pipe2_us\":%.2f,\"plain_read_us\":%.2f,\"product_GBps\":%.1f,"
+                    "\"plain_GBps\":%.1f,\"product_over_plain\":%.4f}\n",
+                    kp ? 1 : 0, pass, reps, t_prod, t_rep, t_pipe, t_plain, bytes / t_prod / 1e3, bytes / t_plain / 1e3,
+                    t_prod / t_plain);
         std::fflush(stdout);
     }
     // timelines: the last of 3 launches of each (rotating arenas), alternating
