@@ -980,9 +980,9 @@ def run_extras(engine, torch, W, w, arenas, descs, dev, want):
                     "recv_pattern_cpu_s_per_GiB": round(r["recv_pattern_cpu_s_per_GiB"], 4),
                     "verdict_wait_s_per_GiB": round(wait_s / max(r["bytes_recv"] / GIB, 1e-9), 4)}
                 if mode == PA.VERIFY_DEFERRED:
-                    # launches in flight per connection (cts_pattern.cpp Depth(): CTS_DEFERRED_DEPTH, default 2)
-                    out["loopback_config1_%s" % name]["launches_in_flight"] = \
-                        min(4, max(1, int(os.environ.get("CTS_DEFERRED_DEPTH") or 2)))
+                    # launches in flight per connection, as the patterns ran them (cts_pattern_stats.deferred_depth)
+                    out["loopback_config1_%s" % name]["launches_in_flight"] = max(sd["deferred_depth"]
+                                                                                  for sd in r["sides"])
             # the socket path alone (-verify:connection): what the receive threads spend without any VerifyBuffer
             r = LB.run(connections=8, buffer_size=65536, transfer_size=1 << 30, verify=False)
             out["loopback_config1_verify_off"] = {

@@ -103,10 +103,12 @@ class CtsPatternStats(ctypes.Structure):
         ("bytes_sent_held", ctypes.c_uint64),
         ("bytes_recv_held", ctypes.c_uint64),
         ("verify_wait_ns", ctypes.c_uint64),
+        ("deferred_depth", ctypes.c_uint32),
+        ("reserved2", ctypes.c_uint32),
     ]
 
     def as_dict(self) -> dict:
-        return {f: int(getattr(self, f)) for f, _ in self._fields_ if f != "reserved"}
+        return {f: int(getattr(self, f)) for f, _ in self._fields_ if f not in ("reserved", "reserved2")}
 
 
 class CtsStatusDetails(ctypes.Structure):

@@ -639,7 +639,11 @@ struct cts_io_pattern {
         }
         ring = Deferred() && VerifiesRecvs();
         slot_bytes = RecvSlotBytes();
-        // a slot is handed out again only after the (up to two) batches that may hold it were verified
+        // a slot is handed out again only after every batch that may hold it was verified: the filling batch and the
+        // up to Depth() launches in flight hold (Depth() + 1) x BatchCapacity() / (Depth() + 1) = BatchCapacity()
+        // unverified slots, and recvCount more are posted. The pipelined ring keeps a second BatchCapacity() of slots
+        // beyond that bound (the depth-1 layout of round 3; config-1 throughput did not move with the ring's size
+        // within the run-to-run spread)
         ring_slots = ring ? BatchCapacity() * (DoubleBuffered() ? 2u : 1u) + recvCount + 1 : recvCount;
         const uint64_t bytes = (uint64_t)slot_bytes * ring_slots;
         char* base = nullptr;
@@ -1009,8 +1013,23 @@ struct cts_io_pattern {
                           nullptr, nullptr, 0, stream);
     }
 
-    // Waits for everything enqueued on the pattern's stream. With retire_wait 2 it sleeps in `step_us` steps between
-    // non-blocking queries of an event recorded behind the work (the runtime's own waits spin first).
+    // cts_io_pattern_destroy bounds its waits (a hung kernel must not hang teardown): while set, every wait below
+    // polls its event and gives up with hipErrorNotReady once wait_deadline has passed.
+    bool bounded_wait = false;
+    std::chrono::steady_clock::time_point wait_deadline{};
+    hipError_t PollEvent(hipEvent_t e, uint32_t step_us)
+    {
+        for (;;) {
+            const hipError_t q = hipEventQuery(e);
+            if (q != hipErrorNotReady) return q;
+            if (bounded_wait && std::chrono::steady_clock::now() > wait_deadline) return hipErrorNotReady;
+            std::this_thread::sleep_for(std::chrono::microseconds(step_us));
+        }
+    }
+
+    // Waits for everything enqueued on the pattern's stream. With retire_wait 2 (or a bounded wait) it sleeps in
+    // `step_us` steps between non-blocking queries of an event recorded behind the work (the runtime's own waits
+    // spin first).
     hipEvent_t sync_done = nullptr;
     hipError_t SleepSync(uint32_t step_us)
     {
@@ -1021,29 +1040,22 @@ struct cts_io_pattern {
     }
     hipError_t SleepSyncImpl(uint32_t step_us)
     {
-        if (retire_wait != 2) return hipStreamSynchronize(stream);
+        if (retire_wait != 2 && !bounded_wait) return hipStreamSynchronize(stream);
         if (sync_done == nullptr && hipEventCreateWithFlags(&sync_done, hipEventDisableTiming) != hipSuccess) {
             sync_done = nullptr;
-            return hipStreamSynchronize(stream);
+            return bounded_wait ? hipErrorNotReady : hipStreamSynchronize(stream);
         }
-        hipError_t rc = hipEventRecord(sync_done, stream);
+        const hipError_t rc = hipEventRecord(sync_done, stream);
         if (rc != hipSuccess) return rc;
-        for (;;) {
-            rc = hipEventQuery(sync_done);
-            if (rc != hipErrorNotReady) return rc;
-            std::this_thread::sleep_for(std::chrono::microseconds(step_us));
-        }
+        return PollEvent(sync_done, step_us);
     }
 
     hipError_t WaitInflight(hipEvent_t done)  // the kernel behind `done`
     {
+        if (bounded_wait) return done != nullptr ? PollEvent(done, 50) : SleepSyncImpl(50);
         if (done == nullptr || retire_wait == 0) return hipStreamSynchronize(stream);
         if (retire_wait == 1) return hipEventSynchronize(done);
-        for (;;) {
-            const hipError_t q = hipEventQuery(done);
-            if (q != hipErrorNotReady) return q;
-            std::this_thread::sleep_for(std::chrono::microseconds(50));
-        }
+        return PollEvent(done, 50);
     }
 
     // Waits for the oldest in-flight batch and applies its verdicts. A failure in it takes back everything completed
@@ -1064,7 +1076,7 @@ struct cts_io_pattern {
         flights.pop_front();
         if (failed) {
             // the later kernels' verdicts are never applied; they finish before their sets are written again
-            if (!flights.empty() && hipStreamSynchronize(stream) != hipSuccess) return CTS_E_HIP;
+            if (!flights.empty() && SleepSyncImpl(50) != hipSuccess) return CTS_E_HIP;
             for (Flight& g : flights) spare_events.push_back(g.done);
             flights.clear();
             queue.clear();
@@ -1763,6 +1775,20 @@ struct MediaStreamClient : cts_io_pattern {
 
     bool FlushFailed() const { return m_lastError == CTS_PATTERN_E_FAIL_FAST; }
 
+    // The batched verify failed on the device: the stream cannot be rendered further, so it ends here as a stream
+    // that cannot continue does (ctsIOPatternMediaStream.cpp:490-508: a FatalAbort task). Sent once, by whichever
+    // timer saw the failure first (the START timer can run before the renderer has been armed).
+    bool device_abort_sent = false;
+    void SendDeviceAbort()
+    {
+        if (device_abort_sent) return;
+        device_abort_sent = true;
+        cts_task t{};
+        t.rio_buffer_id = kRioInvalid;
+        t.io_action = CTS_TASK_FATAL_ABORT;
+        SendTaskToCallback(t);
+    }
+
     // SetNextTimer (:321-349): the renderer's next tick at base + offset frames; armed when more than 2 ms ahead
     // (always on the initial call)
     bool SetNextTimer(bool initial)
@@ -1786,7 +1812,10 @@ struct MediaStreamClient : cts_io_pattern {
         static char kStart[] = "START";
         if (cts::ms_client_finished(ms)) return;
         TimerFlush();  // DEFERRED: the datagrams that arrived count
-        if (FlushFailed()) return;
+        if (FlushFailed()) {
+            SendDeviceAbort();
+            return;
+        }
         if (!cts::ms_client_received_buffered_frames(ms)) {
             cts_task t{};
             t.rio_buffer_id = kRioInvalid;
@@ -1808,12 +1837,7 @@ struct MediaStreamClient : cts_io_pattern {
             if (cts::ms_client_finished(ms)) return;
             TimerFlush();  // DEFERRED: a tick renders what arrived before it
             if (FlushFailed()) {
-                // the batched verify failed on the device: the stream cannot be rendered further, so it ends here
-                // as a stream that cannot continue does (ctsIOPatternMediaStream.cpp:490-508: a FatalAbort task)
-                cts_task t{};
-                t.rio_buffer_id = kRioInvalid;
-                t.io_action = CTS_TASK_FATAL_ABORT;
-                SendTaskToCallback(t);
+                SendDeviceAbort();
                 return;
             }
             const int code = cts::ms_client_tick(ms);
@@ -2169,19 +2193,29 @@ int cts_io_pattern_create(const cts_pattern_config* c, cts_engine* engine, cts_i
 int cts_io_pattern_destroy(cts_io_pattern* p)
 {
     if (p == nullptr) return CTS_E_INVALID;
+    int rc = CTS_OK;
     {
         // DEFERRED: completions still waiting for a verdict are verified now, so their bytes reach TcpStatusDetails
-        // as the reference's (verified at completion) did; best effort, nothing may leave the ABI
+        // as the reference's (verified at completion) did. Every wait is bounded (CTS_PATTERN_DESTROY_WAIT_MS,
+        // default 2000); nothing may leave the ABI.
         std::lock_guard<std::recursive_mutex> lk(p->mu);
+        const char* env = std::getenv("CTS_PATTERN_DESTROY_WAIT_MS");
+        const long ms = env != nullptr && *env != 0 ? std::atol(env) : 2000;
+        p->bounded_wait = true;
+        p->wait_deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(ms > 0 ? ms : 2000);
         if (p->fail_fast.empty() && p->VerdictsPending()) {
             try {
                 (void)p->FlushPending();
             } catch (...) {
+                rc = CTS_E_HIP;
             }
         }
+        // the pattern's buffers go with it: a kernel still reading them (it did not finish within the bound) keeps
+        // them, and the pattern is left allocated rather than freed under the GPU's reads
+        if (p->stream != nullptr && p->SleepSyncImpl(50) != hipSuccess) return CTS_E_HIP;
     }
     delete p;
-    return CTS_OK;
+    return rc;
 }
 
 int cts_io_pattern_set_verifier(cts_io_pattern* p, cts_batch_verifier fn, void* ctx)
@@ -2324,6 +2358,7 @@ int cts_io_pattern_get_stats(const cts_io_pattern* p, cts_pattern_stats* o)
     o->has_failure = p->has_failure ? 1 : 0;
     o->fail_completion = p->fail_completion;
     o->verify_wait_ns = p->verify_wait_ns;
+    o->deferred_depth = p->Deferred() && p->DoubleBuffered() ? p->Depth() : 0u;
     return CTS_OK;
 }
 

@@ -205,6 +205,10 @@ typedef struct cts_pattern_stats {
      * in-flight launch, a flush's synchronize, a MediaStream client's batch): the receive thread is idle on the GPU
      * meanwhile. */
     uint64_t verify_wait_ns;
+    /* DEFERRED: device launches this pattern keeps in flight at once (CTS_DEFERRED_DEPTH as clamped to the batch:
+     * 1-4), 0 in SYNC mode or with a host batch verifier. */
+    uint32_t deferred_depth;
+    uint32_t reserved2;
 } cts_pattern_stats;
 
 /* Batch verifier hook: verify n buffers of a host arena (results[i] per
@@ -252,7 +256,11 @@ void cts_shared_buffer_release(void);
  * with cts_io_pattern_set_verifier before the first CompleteIo. */
 int cts_io_pattern_create(const cts_pattern_config* config, cts_engine* engine, cts_io_pattern** out);
 /* A DEFERRED pattern destroyed with completions still waiting for their batch verdict verifies them first, so their
- * bytes are published (cts_pattern_stats.bytes_*_held) as the reference counted them at completion. */
+ * bytes are published (cts_pattern_stats.bytes_*_held) as the reference counted them at completion. A data mismatch
+ * found by that final verify reaches only the process-wide counters (cts_status_details_*): the caller has read this
+ * pattern's stats before destroying it. Every wait of destroy is bounded (env CTS_PATTERN_DESTROY_WAIT_MS, default
+ * 2000): CTS_OK, or CTS_E_HIP when the final verify failed (the pattern is freed) or the pattern's stream did not go
+ * idle within the bound (a kernel still reads its buffers: the pattern is left allocated, not freed under it). */
 int cts_io_pattern_destroy(cts_io_pattern* pattern);
 int cts_io_pattern_set_verifier(cts_io_pattern* pattern, cts_batch_verifier fn, void* ctx);
 

@@ -142,7 +142,7 @@ int main(void){
  O(cts_pattern_config,transfer_size); O(cts_pattern_config,random_seed); O(cts_pattern_config,verify_mode);
  O(cts_pattern_config,batch_bytes);
  O(cts_pattern_stats,recv_pattern_offset); O(cts_pattern_stats,fail_expected); O(cts_pattern_stats,fail_completion);
- O(cts_pattern_stats,bytes_recv_held); O(cts_pattern_stats,verify_wait_ns);
+ O(cts_pattern_stats,bytes_recv_held); O(cts_pattern_stats,verify_wait_ns); O(cts_pattern_stats,deferred_depth);
  return 0; }
 """
     with tempfile.TemporaryDirectory() as d:
@@ -159,7 +159,8 @@ int main(void){
                "random_seed": A.CtsPatternConfig, "verify_mode": A.CtsPatternConfig,
                "batch_bytes": A.CtsPatternConfig, "recv_pattern_offset": A.CtsPatternStats,
                "fail_expected": A.CtsPatternStats, "fail_completion": A.CtsPatternStats,
-               "bytes_recv_held": A.CtsPatternStats, "verify_wait_ns": A.CtsPatternStats}
+               "bytes_recv_held": A.CtsPatternStats, "verify_wait_ns": A.CtsPatternStats,
+               "deferred_depth": A.CtsPatternStats}
     for line in lines[1:]:
         if not line.strip():
             continue

@@ -257,6 +257,7 @@ def _side_view(r, connections, corrupt):
     sides = [dict(s) for s in r["sides"]]
     for s in sides:  # wall time spent waiting for device verdicts: a timing, not a count (0 without a device)
         s.pop("verify_wait_ns", None)
+        s.pop("deferred_depth", None)  # how the arrangement verifies, not what it reports
     if corrupt is not None:
         for k in ("bytes_sent", "final_error", "last_error"):
             sides[corrupt].pop(k)
@@ -267,11 +268,15 @@ def _side_view(r, connections, corrupt):
     return totals, sides
 
 
-def _three_way(run, connections, transfer, corrupt, send_index, arrangements):
+def _three_way(run, connections, transfer, corrupt, send_index, arrangements, depths=None):
+    """Runs every arrangement and checks that each reports what the first does; `depths` (a dict), when given, gets
+    each arrangement's DEFERRED launches in flight per connection (cts_pattern_stats.deferred_depth, max over sides)."""
     views = {}
     for name, kw in arrangements.items():
         r = run(connections=connections, buffer_size=65536, transfer_size=transfer, recv_whole=True, sides=True,
                 corrupt_connection=corrupt, corrupt_send_index=send_index, **kw)
+        if depths is not None:
+            depths[name] = max(s["deferred_depth"] for s in r["sides"])
         views[name] = _side_view(r, connections, corrupt)
     names = list(views)
     for n in names[1:]:
@@ -358,7 +363,10 @@ def test_config1_deferred_depths_gpu(engine, monkeypatch, depth, corrupt, batch)
 
     arr = {"cpu_oracle": dict(verifier=hook, verify_mode=A.VERIFY_SYNC),
            "gpu_deferred": dict(engine=engine, verify_mode=A.VERIFY_DEFERRED, batch_buffers=batch)}
-    totals, sides = _three_way(run, 8, 1 << 30, corrupt, 9000, arr)
+    depths = {}
+    totals, sides = _three_way(run, 8, 1 << 30, corrupt, 9000, arr, depths)
+    # the patterns ran the depth asked for (clamped to batch - 1: 3 at batch 16 and at the feeder's batch)
+    assert depths == {"cpu_oracle": 0, "gpu_deferred": depth}
     if corrupt is None:
         assert totals["connections_ok"] == 8 and totals["data_errors"] == 0
         assert all(s["buffers_verified"] == 16384 for s in sides[8:])

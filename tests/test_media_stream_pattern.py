@@ -288,6 +288,39 @@ def test_client_deferred_corrupt_payload(clock, batch):
     r.p.close()
 
 
+def _failing_verifier(arena, descs):
+    raise RuntimeError("the batched verify fails (a device error stand-in)")
+
+
+@pytest.mark.parametrize("first_timer", ["start", "render"])
+def test_client_deferred_device_failure_on_the_first_tick(clock, first_timer):
+    """DEFERRED: the batched verify of the datagrams queued before the first timer fails (the hook returns an error,
+    as a failed kernel launch would). Whichever timer flushes first, START (before the renderer ever ran) or the
+    renderer, hands exactly one FatalAbort task to the callback (ctsIOPatternMediaStream.cpp:490-508), and the
+    pattern reports the latched failure; the other timer sends nothing more."""
+    cfg = PatternConfig.media_stream(listening=False, frame_size=3000, frames_per_second=100, stream_length_frames=5,
+                                     buffered_frames=2, datagram_max_size=1400, pre_post_recvs=2,
+                                     ms_manual_timers=True, verify_mode=A.VERIFY_DEFERRED, batch_buffers=4)
+    shared_buffer_attach(_SENDER)
+    p = IoPattern.MakeIoPattern(cfg, None, verifier=_failing_verifier)
+    tasks = []
+    p.RegisterCallback(tasks.append)
+    posted = [p.InitiateIo() for _ in range(2)]
+    t = posted.pop(0)
+    IoPattern.write_task_buffer(t, _datagram(1, 1400))
+    assert p.CompleteIo(t, 1400) == A.IO_CONTINUE  # queued for the batch
+    start, render = p.media_stream_timers()
+    first, second = (A.MS_TIMER_START, A.MS_TIMER_RENDER) if first_timer == "start" else (A.MS_TIMER_RENDER,
+                                                                                          A.MS_TIMER_START)
+    clock.t = max(start, render)
+    p.media_stream_fire(first)
+    assert [x.io_action for x in tasks] == [A.TASK_FATAL_ABORT]
+    assert p.GetLastPatternError() != 0
+    p.media_stream_fire(second)
+    assert [x.io_action for x in tasks] == [A.TASK_FATAL_ABORT]
+    p.close()
+
+
 @pytest.mark.parametrize("payload,why", [
     (b"", "zero-byte datagram before the stream finished"),
     (b"\x00", "shorter than the flag"),
