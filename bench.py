@@ -40,6 +40,7 @@ import time
 import numpy as np
 
 ENGINES_LEG_CAP_S = 300  # the single-process leg (a child process) normally takes ~20 s
+ALLREDUCE_CAP_S = 120    # cts_counters_allreduce timing in that leg: a first 8-GPU communicator set-up takes seconds
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 GIB = float(1 << 30)
 METRIC = "GiB/s verified, 64 KiB buffers device-resident; % MI355X HBM roofline"
@@ -224,10 +225,10 @@ def engines_leg(args, world):
         return {"error": "exit %d: %s" % (r.returncode, r.stderr.strip().splitlines()[-1:] or "")}
     j = json.loads(lines[-1])
     return {"value": j["value"], "unit": j["unit"], "n_gpus": j["n_gpus"], "ms_per_step": j["ms_per_step"],
-            "per_gpu_GiBps": j.get("per_gpu_GiBps"), "parity": j.get("parity"),
+            "per_gpu_GiBps": j.get("per_gpu_GiBps"), "parity": j.get("parity"), "node_counters": j.get("node_counters"),
             "process_model": "one process, one engine per GPU (cts_engine_create(g)), one host thread + %d streams "
-                             "each, connections by cts_shard_of, counters folded by cts_counters_read_multi"
-                             % args.pipeline_streams}
+                             "each, connections by cts_shard_of, counters folded by cts_counters_read_multi and "
+                             "all-reduced over RCCL by cts_counters_allreduce" % args.pipeline_streams}
 
 
 class Batch:
@@ -744,16 +745,29 @@ def main_engines(args, torch):
     per = [c[0].read_counters(c[1].counters) for c in ctx]
     # after the timed region: the node-wide counters both ways, the host fold and the RCCL all-reduce issued from
     # the C ABI (cts_counters_allreduce: per-device fold + ncclAllReduce sum u64 x 5 per device), each timed
-    reduced, red = None, {}
     fold_us = _median_us(lambda: counters_read_multi(engs, blocks), 20)
-    try:
-        t = time.perf_counter()
-        reduced = counters_allreduce(engs, blocks)  # the first call creates the communicators
-        red["allreduce_first_call_ms"] = round((time.perf_counter() - t) * 1e3, 2)
-        red["allreduce_counters_us"] = round(_median_us(lambda: counters_allreduce(engs, blocks), 20), 1)
-        counters_allreduce_release()
-    except Exception as ex:  # reported, not fatal: the verify leg above is the measurement
-        red["allreduce_error"] = repr(ex)
+    red = {}
+
+    def allreduce_timing():
+        try:
+            t = time.perf_counter()
+            red["reduced"] = counters_allreduce(engs, blocks)  # the first call creates the communicators
+            red["allreduce_first_call_ms"] = round((time.perf_counter() - t) * 1e3, 2)
+            red["allreduce_counters_us"] = round(_median_us(lambda: counters_allreduce(engs, blocks), 20), 1)
+            counters_allreduce_release()
+        except Exception as ex:  # reported, not fatal: the verify leg above is the measurement
+            red["allreduce_error"] = repr(ex)
+
+    # on its own thread with a bound: a collective that never returns must not cost the leg's line
+    import threading
+
+    th = threading.Thread(target=allreduce_timing, daemon=True)
+    th.start()
+    th.join(ALLREDUCE_CAP_S)
+    hung = th.is_alive()
+    if hung:
+        red["allreduce_error"] = "cts_counters_allreduce did not return within %d s" % ALLREDUCE_CAP_S
+    reduced = red.pop("reduced", None)
     total = sum(c[1].bytes_per_launch for c in ctx) * R * K
     exp = {k: sum(c[1].exp_ctr[k] for c in ctx) * K * R for k in ctx[0][1].exp_ctr}
     line = {
@@ -775,6 +789,9 @@ def main_engines(args, torch):
                           "devices": [c[0].device_ordinal() for c in ctx]},
     }
     print(json.dumps(line), flush=True)
+    if hung:  # the RCCL call still holds the devices: leave without tearing down under it
+        sys.stderr.flush()
+        os._exit(0)
     for e, B, streams, _ in ctx:
         for s in streams:
             e.stream_destroy(s)

@@ -25,14 +25,14 @@ struct LaunchGeometry {
     int num_cus = 256;        // hipDeviceAttributeMultiprocessorCount
     int blocks_per_cu = 4;        // workgroup-per-buffer grid cap = num_cus * this (grid-stride beyond);
                                   // 4 x 4 waves x U2 = 32 KiB of loads in flight per CU measured best
-                                  // (config 2: 41.0-41.2 us vs 42.6-43.9 at 8; tools/tune_verify.py)
+                                  // (config 2: 41.0-41.2 us vs 42.6-43.9 at 8; tools/rounds/r04/tune_verify.py)
     int small_blocks_per_cu = 64; // small-buffer (quad) path grid cap
     int nontemporal = 1;      // nt loads for the once-read verify stream
     int small_threshold = 8192;  // max_length_hint <= this -> small-buffer path
     int small_chunk = 0;         // chunked walk of the quad kernels: buffers per chunk (0 = one contiguous range per
                                  // workgroup)
     int fill_nt = 2;             // fill store policy: 0 plain, 1 nontemporal, 2 by path (plain for the workgroup
-                                 // path, nontemporal for datagrams; tools/tune_verify.py --op fill)
+                                 // path, nontemporal for datagrams; tools/rounds/r04/tune_verify.py --op fill)
     int fill_blocks_per_cu = 1;  // fill grid cap (write-bound; plain stores: 1 measured best, 48.7 vs 49.1-49.4 us)
     int ring_fill_blocks_per_cu = 4;  // MediaStream ring fill grid cap (16 M x 1472 B: 4.3 ms at 4, 5.0 at 8;
                                       // CTS_RING_FILL_BLOCKS_PER_CU; tools/ring_fill_probe.hip)

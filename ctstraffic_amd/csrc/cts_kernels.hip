@@ -678,7 +678,7 @@ __global__ void __launch_bounds__(kBlock, 4)
 // A whole wave per 1472-byte datagram issues its per-buffer scalar work (descriptor,
 // span set-up, edge lanes, record, counters) once per datagram, and a third of its
 // lanes' loads fall past the span (4.71 against 5.95 TB/s of payload for this form on
-// config 3, tools/media_stream_probe.py). Here a wave's instructions serve four datagrams at once: the span fields live in VGPRs (one
+// config 3, tools/rounds/r04/media_stream_probe.py). Here a wave's instructions serve four datagrams at once: the span fields live in VGPRs (one
 // descriptor per team), each load instruction fetches four 256-byte runs, and
 // U loads per lane cover 16*U chunks per round (U = 6: 1536 B, one round for a
 // 1446-byte payload at any alignment). Loads are global (per-lane 64-bit
@@ -839,7 +839,7 @@ struct QCounters {
 // 4 x 12 = 48 contiguous result bytes, one covers 4 x 32 = 128 record bytes. Written directly,
 // each leader's struct became 4-lane sub-dword and unaligned stores (global_store_short/byte,
 // dword at +7): on 4 M datagrams the records alone added 265 us to a 920 us launch
-// (tools/media_stream_probe.py). Nontemporal stores here measured 2-4 % slower; write-through
+// (tools/rounds/r04/media_stream_probe.py). Nontemporal stores here measured 2-4 % slower; write-through
 // (sc1) stores helped the records and hurt the results, and deferring the stores until the next
 // buffer's loads were in flight changed nothing (+-0.5 %).
 struct QuadOut {
@@ -938,7 +938,7 @@ __device__ __forceinline__ void quad_ring_flush(const QuadRing<K, SlotT>& g, uin
 // Which buffers a team visits: the buffers are cut into chunks of `per` consecutive buffers (a multiple of
 // TEAMS); block b walks chunks b, b + grid, ... TEAMS buffers at a time, so the rounds of a wave write adjacent
 // outputs and a 128-byte line of 12-byte results fills up in ONE CU's L2 (a grid-stride walk spreads a line over
-// workgroups on different XCDs: partial-line writes, 0-5 % slower, tools/media_stream_probe.py). One chunk per
+// workgroups on different XCDs: partial-line writes, 0-5 % slower, tools/rounds/r04/media_stream_probe.py). One chunk per
 // block (contig_grid's default) is a fully block-contiguous walk.
 template <int TEAMS>
 struct QuadWalk {
@@ -1197,7 +1197,7 @@ __global__ void __launch_bounds__(kBlock) fill_span_kernel(uint8_t* __restrict__
 // Team lanes 0..2 load the 16-byte chunks holding the header alongside the speculative DATA payload
 // stream; the header dwords reach the team leader through DPP row shifts, with no dependent memory round
 // trip (header bytes by byte loads and lane shuffles, and one wave per datagram, measured slower:
-// tools/media_stream_probe.py).
+// tools/rounds/r04/media_stream_probe.py).
 
 // Team lane 0 receives dword c of lane `from`'s u32x4 (from = 1, 2) within its 16-lane DPP
 // row (row_shl:from; a VALU move, no LDS round trip).
@@ -1475,7 +1475,7 @@ __global__ void __launch_bounds__(kBlock)
 // as whole 16-byte chunks: chunk c holds datagram bytes [16c, 16c + 16), i.e. pattern positions 16c - 26 on, with
 // the header's 26 bytes assembled in registers into chunks 0 and 1. Only a partial last chunk writes bytes. (The
 // header written bytewise by 26 lanes beside nontemporal payload chunks and 6 byte stores for payload bytes 26..31
-// left the first line of every datagram written in pieces: 8.4 -> 7.0 ms for 16 M x 1472 B, tools/media_stream_probe.py.)
+// left the first line of every datagram written in pieces: 8.4 -> 7.0 ms for 16 M x 1472 B, tools/rounds/r04/media_stream_probe.py.)
 // What still bounds this kernel is latency, not bytes: each datagram's descriptor and header are loaded before its
 // stores, one datagram per wave at a time (a one-datagram prefetch was slower: 9.3 ms, tools/ring_fill_probe.hip).
 // A ring of datagrams goes through media_stream_fill_ring_kernel instead (cts_media_stream_fill_strided: 4.3 ms).
@@ -1531,7 +1531,7 @@ __device__ __forceinline__ void ms_fill_one(uint8_t* arena, uint64_t arena_bytes
 // contiguous range of descriptors in batches of kFillBatch, staged in LDS with their headers, and each wave fills a
 // contiguous quarter of the batch, one datagram at a time. Nothing is loaded inside the per-datagram loop: the
 // wave-per-datagram form waits for a descriptor (a scalar load of a far-away line: ~1 us) before every datagram's
-// stores, which bounded it at 3.4-3.9 TB/s on 16 M x 1472 B (6.8-7.0 ms, tools/media_stream_probe.py). (The same
+// stores, which bounded it at 3.4-3.9 TB/s on 16 M x 1472 B (6.8-7.0 ms, tools/rounds/r04/media_stream_probe.py). (The same
 // batching measured slower for cts_fill's payload-only small buffers, whose first chunk is a partial write either
 // way: 6.9 against 6.1-6.8 ms per 16 M x 1446 B, tools/ring_fill_probe.hip.)
 constexpr uint32_t kFillBatch = kBlock;
@@ -2044,7 +2044,7 @@ hipError_t launch_fill(uint8_t* arena, uint64_t arena_bytes, const cts_buf_desc*
     if (n == 0) return hipSuccess;
     const bool small = max_length_hint != 0 && max_length_hint <= (uint32_t)geo.small_threshold;
     // store policy: fill_nt 0 = plain, 1 = nontemporal, 2 = by path (plain for the workgroup path:
-    // config 2 48.7 vs 51.1 us; nontemporal for datagrams: 1.46 vs 1.68 ms per 4 M; tools/tune_verify.py --op fill)
+    // config 2 48.7 vs 51.1 us; nontemporal for datagrams: 1.46 vs 1.68 ms per 4 M; tools/rounds/r04/tune_verify.py --op fill)
     const bool nts = geo.fill_nt == 2 ? small : geo.fill_nt != 0;
     const uint32_t sgrid = grid_for(n, kBlock / 64, geo), lgrid = grid_for(n, 1, geo, geo.fill_blocks_per_cu);
     if (nts) {

@@ -55,6 +55,10 @@ def test_engines_leg_native_threads(engines):
     assert sum(j["config"]["connections_per_gpu"]) == 512 * engines
     assert p["counters"]["buffers_checked"] == 512 * engines * 3 * 2
     assert j["value"] > 0
+    # the node's counters over RCCL from the C ABI (every engine on this GPU: one device, one rank) = the host fold
+    nc = j["node_counters"]
+    assert "allreduce_error" not in nc, nc
+    assert p["allreduce_equals_fold"] and nc["allreduce_counters_us"] > 0 and nc["devices"] == [0] * engines
 
 
 @pytest.mark.gpu

@@ -7,6 +7,8 @@ for i in 1 2 3; do
   timeout -k 10 90 tools/ab/verify_timeline_r04 2 64 > $O/tl_r04_$i.jsonl 2>&1
   timeout -k 10 90 tools/verify_timeline 2 64 > $O/tl_r05_$i.jsonl 2>&1
 done
+echo "[$(date +%T)] tail"
+timeout -k 10 150 tools/verify_timeline 3 64 tail > $O/tail.jsonl 2>&1
 echo "[$(date +%T)] bench"
 timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err
 echo "[$(date +%T)] engines"

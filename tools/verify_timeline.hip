@@ -18,6 +18,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <string>
 #include <vector>
 
@@ -267,6 +268,111 @@ __global__ void __launch_bounds__(256) plain_read_xu(const u32x4* __restrict__ p
     if (acc == 0x12345678u) out[0] = acc;
 }
 
+// ---- "tail" mode (VERDICT r04 "Next round" 6): the last round's buffers cut into PARTS sub-buffers, one per extra
+// workgroup. The first main_grid workgroups run the product's grid-stride walk over the first full_rounds rounds; the
+// PARTS x (n - full_rounds x main_grid) tail workgroups come after them in the grid, so the dispatcher hands them out
+// as main workgroups retire and the faster CUs take more of the tail. The parts of a buffer merge their verdicts
+// through a per-buffer global slot {~first (atomicMax), count (atomicAdd), arrivals}; the last to arrive writes the
+// record and counts the buffer, and resets the slot (the slots start zeroed and stay so between launches).
+struct TailSlot {
+    uint32_t first, count, arrive, pad;
+};
+
+__device__ __forceinline__ void verify_one_product(const cts::Span& s, uint32_t lane, uint32_t& first, uint32_t& count)
+{
+    if (cts::span_giant(s)) {
+        cts::scan_giant_exact<256, true>(s, lane, first, count);
+    } else if (__builtin_amdgcn_readfirstlane(cts::span_whole_lines(s) ? 1u : 0u)) {
+        cts::scan_whole_exact<256, 2, true, true>(s, lane, first, count);
+        return;
+    } else {
+        const uint32_t acc = cts::scan_buffer<256, 2, true, true>(s, lane);
+        if (__builtin_amdgcn_readfirstlane(__syncthreads_or(acc != 0u)) != 0 && acc != 0u)
+            cts::scan_exact_owned<256, 2, true>(s, lane, first, count);
+    }
+}
+
+template <int PARTS>
+__global__ void __launch_bounds__(256, 4)
+    verify_tail(const uint8_t* __restrict__ arena, uint64_t arena_bytes, const cts_buf_desc* __restrict__ descs, uint32_t n,
+                cts_verify_result* __restrict__ results, uint64_t* __restrict__ counters,
+                uint32_t* __restrict__ conn_first_fail, uint32_t n_conns, uint32_t main_grid, uint32_t full_rounds,
+                TailSlot* __restrict__ slots)
+{
+    __shared__ uint64_t ctr[1][5];
+    const uint32_t lane = threadIdx.x;
+    cts::zero_counters<1>(ctr);
+    if (blockIdx.x < main_grid) {
+        const uint32_t end = full_rounds * main_grid < n ? full_rounds * main_grid : n;
+        uint32_t i = blockIdx.x;
+        cts_buf_desc dn;
+        if (i < end) dn = descs[i];
+        for (; i < end; i += main_grid) {
+            const cts_buf_desc d = dn;
+            if (i + main_grid < end) dn = descs[i + main_grid];
+            if (cts::desc_bad(d, arena_bytes)) {
+                if (lane == 0) cts::write_bad(results, i);
+                continue;
+            }
+            const cts::Span s = cts::make_span(arena, d);
+            uint32_t first = cts::kNone, count = 0;
+            verify_one_product(s, lane, first, count);
+            if (__builtin_amdgcn_readfirstlane(__syncthreads_or(first != cts::kNone)) != 0)
+                cts::block_reduce_mismatch(first, count);
+            if (lane == 0) cts::finish_buffer(s, d, i, first, count, results, ctr[0], conn_first_fail, n_conns);
+        }
+    } else {
+        const uint32_t t = blockIdx.x - main_grid;
+        const uint32_t i = full_rounds * main_grid + t / PARTS, part = t % PARTS;
+        if (i < n) {
+            const cts_buf_desc d = descs[i];
+            if (cts::desc_bad(d, arena_bytes)) {
+                if (lane == 0 && part == 0) cts::write_bad(results, i);
+            } else {
+                const cts::Span s = cts::make_span(arena, d);
+                uint32_t first = cts::kNone, count = 0;
+                const uint32_t per = s.nchunks / PARTS;
+                if (__builtin_amdgcn_readfirstlane((cts::span_whole_lines(s) && !cts::span_giant(s) &&
+                                                    s.nchunks % (PARTS * 512u) == 0u) ? 1u : 0u)) {
+                    // this part's whole-line sub-span [part x per, (part + 1) x per) chunks
+                    cts::Span q = s;
+                    const uint32_t c0 = part * per;
+                    q.p = s.p + c0;
+                    q.sp = s.sp + 16u * c0;
+                    q.nchunks = per;
+                    q.len = 16u * per;
+                    q.q0 = (s.q0 + 16u * c0) & 0xFFFFu;
+                    q.expected = q.q0;
+                    cts::scan_whole_exact<256, 2, true, true>(q, lane, first, count);
+                    if (first != cts::kNone) first += 16u * c0;
+                } else if (part == 0) {
+                    verify_one_product(s, lane, first, count);  // any other span: part 0 takes it whole
+                }
+                if (__builtin_amdgcn_readfirstlane(__syncthreads_or(first != cts::kNone)) != 0)
+                    cts::block_reduce_mismatch(first, count);
+                if (lane == 0) {
+                    TailSlot* sl = slots + i;
+                    if (first != cts::kNone) {  // stored as ~first (0 = none: the slots start zeroed)
+                        atomicMax(&sl->first, ~first);
+                        atomicAdd(&sl->count, count);
+                    }
+                    __threadfence();
+                    if (atomicAdd(&sl->arrive, 1u) == (uint32_t)PARTS - 1u) {  // the last part finishes the buffer
+                        __threadfence();
+                        const uint32_t f = atomicAdd(&sl->first, 0u), c = atomicAdd(&sl->count, 0u);
+                        cts::finish_buffer(s, d, i, f == 0u ? cts::kNone : ~f, c, results, ctr[0], conn_first_fail,
+                                           n_conns);
+                        sl->first = 0u;
+                        sl->count = 0u;
+                        sl->arrive = 0u;
+                    }
+                }
+            }
+        }
+    }
+    cts::flush_counters<1>(counters, ctr);
+}
+
 template <typename F>
 double time_us(F launch, int reps, hipStream_t s)
 {
@@ -369,6 +475,7 @@ int main(int argc, char** argv)
     const bool map_mode = argc > 3 && std::string(argv[3]) == "map";
     const bool skew_mode = argc > 3 && std::string(argv[3]) == "skew";
     const bool xu_mode = argc > 3 && std::string(argv[3]) == "xu";
+    const bool tail_mode = argc > 3 && std::string(argv[3]) == "tail";
     const int reps = argc > 2 ? atoi(argv[2]) : 64;
     int cus = 0;
     CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
@@ -479,6 +586,70 @@ int main(int argc, char** argv)
                 CHECK(hipMemcpy(h.data(), st2, h.size() * 8, hipMemcpyDeviceToHost));
                 print_timeline(v == 0 ? "plain_skew0" : "plain_skew4", h, grid, kp);  // ranks 0..1023 (A = 1024 at 0 and 4)
             }
+        }
+        return 0;
+    }
+    if (tail_mode) {
+        // the last round(s) split into sub-buffers handed out by the dispatcher, against the product
+        TailSlot* slots = nullptr;
+        CHECK(hipMalloc((void**)&slots, n * sizeof(TailSlot)));
+        CHECK(hipMemset(slots, 0, n * sizeof(TailSlot)));
+        auto read_ctr = [&] {
+            std::vector<uint64_t> h(CTS_COUNTER_SHARDS * 8);
+            CHECK(hipMemcpy(h.data(), ctr, h.size() * 8, hipMemcpyDeviceToHost));
+            std::vector<uint64_t> v(5, 0);
+            for (uint32_t sh = 0; sh < CTS_COUNTER_SHARDS; ++sh)
+                for (int k = 0; k < 5; ++k) v[k] += h[sh * 8 + k];
+            return v;
+        };
+        auto run = [&](int form, int i, uint32_t fr) {
+            const uint32_t tail = n - fr * grid;
+            switch (form) {
+            case 0: PRODUCT<<<grid, 256, 0, s>>>(arena[i % R], bytes, d, n, res, ctr, cff, n); break;
+            case 2: verify_tail<2><<<grid + 2 * tail, 256, 0, s>>>(arena[i % R], bytes, d, n, res, ctr, cff, n, grid, fr, slots); break;
+            case 4: verify_tail<4><<<grid + 4 * tail, 256, 0, s>>>(arena[i % R], bytes, d, n, res, ctr, cff, n, grid, fr, slots); break;
+            default: verify_tail<8><<<grid + 8 * tail, 256, 0, s>>>(arena[i % R], bytes, d, n, res, ctr, cff, n, grid, fr, slots); break;
+            }
+        };
+        // parity on arena 0: records, first-failure slots and counters against the product's
+        std::vector<cts_verify_result> a(n), b(n);
+        std::vector<uint32_t> ca(n), cb(n);
+        CHECK(hipMemset(ctr, 0, CTS_COUNTER_SHARDS * 64));
+        CHECK(hipMemset(cff, 0xFF, n * 4));
+        run(0, 0, 3);
+        CHECK(hipMemcpy(a.data(), res, n * sizeof(cts_verify_result), hipMemcpyDeviceToHost));
+        CHECK(hipMemcpy(ca.data(), cff, n * 4, hipMemcpyDeviceToHost));
+        const std::vector<uint64_t> c0 = read_ctr();
+        int ok = 1;
+        for (int form : {2, 4, 8})
+            for (uint32_t fr : {3u, 2u}) {
+                CHECK(hipMemset(res, 0, n * sizeof(cts_verify_result)));
+                CHECK(hipMemset(ctr, 0, CTS_COUNTER_SHARDS * 64));
+                CHECK(hipMemset(cff, 0xFF, n * 4));
+                run(form, 0, fr);
+                CHECK(hipMemcpy(b.data(), res, n * sizeof(cts_verify_result), hipMemcpyDeviceToHost));
+                CHECK(hipMemcpy(cb.data(), cff, n * 4, hipMemcpyDeviceToHost));
+                const bool same = std::memcmp(a.data(), b.data(), n * sizeof(cts_verify_result)) == 0 && ca == cb &&
+                                  read_ctr() == c0;
+                std::printf("{\"kind\":\"tail_parity\",\"parts\":%d,\"full_rounds\":%u,\"equals_product\":%d}\n", form,
+                            fr, same ? 1 : 0);
+                ok &= same ? 1 : 0;
+            }
+        std::fflush(stdout);
+        if (!ok) return 3;
+        for (int pass = 0; pass < passes; ++pass) {
+            double t[7];
+            int k = 0;
+            t[k++] = time_us([&](int i) { run(0, i, 3); }, reps, s);
+            for (int form : {2, 4, 8})
+                for (uint32_t fr : {3u, 2u}) t[k++] = time_us([&](int i) { run(form, i, fr); }, reps, s);
+            const double tp = time_us([&](int i) {
+                plain_read<false><<<grid, 256, 0, s>>>(reinterpret_cast<const u32x4*>(arena[i % R]), n, st, out);
+            }, reps, s);
+            std::printf("{\"kind\":\"tail_time\",\"pass\":%d,\"launches\":%d,\"product_us\":%.2f,\"p2_r3_us\":%.2f,"
+                        "\"p2_r2_us\":%.2f,\"p4_r3_us\":%.2f,\"p4_r2_us\":%.2f,\"p8_r3_us\":%.2f,\"p8_r2_us\":%.2f,"
+                        "\"plain_read_us\":%.2f}\n", pass, reps, t[0], t[1], t[2], t[3], t[4], t[5], t[6], tp);
+            std::fflush(stdout);
         }
         return 0;
     }
