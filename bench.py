@@ -113,6 +113,24 @@ _DIST_ENV = ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK
              "TORCHELASTIC_ERROR_FILE", "TORCH_NCCL_ASYNC_ERROR_HANDLING")
 
 
+_LINE_OUT = None  # this process's real stdout, kept for the one JSON line once fd 1 points at stderr
+
+
+def _claim_stdout():
+    """From here on fd 1 is stderr: whatever a library prints (RCCL's version banner when it creates a communicator,
+    gloo's rendezvous) stays off stdout, where the driver reads exactly one JSON line (written by emit())."""
+    global _LINE_OUT
+    sys.stdout.flush()
+    _LINE_OUT = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+
+
+def emit(line: dict) -> None:
+    out = _LINE_OUT if _LINE_OUT is not None else sys.stdout
+    out.write(json.dumps(line) + "\n")
+    out.flush()
+
+
 class _StdoutToStderr:
     """Point fd 1 at fd 2 for a block: gloo's C++ rendezvous prints "[Gloo] Rank r is connected to ..." on stdout,
     and the driver reads exactly one JSON line from it."""
@@ -195,13 +213,16 @@ def stub_main(args):
         dist.all_gather(seen, me)
     else:
         seen = [me]
+    # a library printing on fd 1 (as RCCL prints its version banner when it creates a communicator) must not reach
+    # the driver's stdout
+    os.write(1, b"RCCL version : stand-in banner of bench.py --stub-gpu\n")
     # the per-rank diagnostics of the real line, with stand-in values (kernel time 40 + rank, device = LOCAL_RANK)
     diag = rank_diagnostics(D.gather_rank_rows([40.0 + rank, local, local, 1, local]))
     if rank == 0:
-        print(json.dumps({"metric": METRIC, "value": 0.0, "unit": "GiB/s", "n_gpus": world, "stub": True,
-                          "ranks": [[int(x) for x in t.tolist()] for t in seen],
-                          "roofline": {k: v for k, v in diag.items() if k == "per_rank_avg_kernel_us"},
-                          **{k: v for k, v in diag.items() if k != "per_rank_avg_kernel_us"}}), flush=True)
+        emit({"metric": METRIC, "value": 0.0, "unit": "GiB/s", "n_gpus": world, "stub": True,
+              "ranks": [[int(x) for x in t.tolist()] for t in seen],
+              "roofline": {k: v for k, v in diag.items() if k == "per_rank_avg_kernel_us"},
+              **{k: v for k, v in diag.items() if k != "per_rank_avg_kernel_us"}})
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
@@ -288,6 +309,7 @@ def main():
         print("bench.py: WORLD_SIZE=%s but --gpus %d: the line's n_gpus must be what ran"
               % (os.environ.get("WORLD_SIZE", "1"), args.gpus), file=sys.stderr)
         sys.exit(2)
+    _claim_stdout()
     if args.stub_gpu:
         sys.exit(stub_main(args))
     import torch
@@ -633,7 +655,7 @@ def main():
             line["allreduce_counters_us"] = round(allreduce_us, 1)
         if extras:
             line["extras"] = extras
-        print(json.dumps(line), flush=True)
+        emit(line)
     torch.cuda.synchronize()
     for ps in pipe:
         engine.stream_destroy(ps.cuda_stream)
@@ -788,7 +810,7 @@ def main_engines(args, torch):
         "node_counters": {"fold_counters_us": round(fold_us, 1), **red,
                           "devices": [c[0].device_ordinal() for c in ctx]},
     }
-    print(json.dumps(line), flush=True)
+    emit(line)
     if hung:  # the RCCL call still holds the devices: leave without tearing down under it
         sys.stderr.flush()
         os._exit(0)

@@ -101,6 +101,18 @@ int main()
     CHECK(c.bytes_checked == total && c.buffers_checked == n && c.buffers_failed == bad_buffers);
     CHECK(c.bytes_ok == total - bad_bytes && c.mismatched_bytes == bad_buffers);
 
+    // the node's counters as ctsTraffic's one-process host reads them (ctsConfig.h:415-417): the host fold and the
+    // RCCL all-reduce over every engine's device (one here), both through the C ABI
+    cts_engine* const engines[1] = {e};
+    const void* const blocks[1] = {ctr};
+    void* const streams[1] = {stream};
+    cts_counters folded{}, reduced{};
+    CHECK(cts_counters_read_multi(engines, blocks, streams, 1, &folded) == CTS_OK);
+    const int ar = cts_counters_allreduce(engines, blocks, streams, 1, &reduced);
+    CHECK(ar == CTS_OK);
+    CHECK(std::memcmp(&folded, &c, sizeof(c)) == 0 && std::memcmp(&reduced, &c, sizeof(c)) == 0);
+    CHECK(cts_counters_allreduce_release() == CTS_OK);
+
     CHECK(hipFree(arena) == hipSuccess && hipFree(descs) == hipSuccess && hipFree(results) == hipSuccess);
     CHECK(hipFree(ctr) == hipSuccess && hipFree(cff) == hipSuccess);
     CHECK(cts_engine_stream_destroy(e, stream) == CTS_OK);

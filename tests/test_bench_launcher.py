@@ -26,7 +26,8 @@ def test_gpus2_launches_two_ranks_and_prints_one_line():
                        stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [x for x in r.stdout.splitlines() if x.strip()]
-    assert len(lines) == 1, r.stdout
+    assert len(lines) == 1, r.stdout  # the ranks' fd-1 banners went to stderr
+    assert "stand-in banner" in r.stderr
     j = json.loads(lines[0])
     assert j["n_gpus"] == 2 and j["stub"] is True
     # every rank ran with RANK / WORLD_SIZE / LOCAL_RANK set by the launcher
@@ -41,7 +42,7 @@ def test_gpus1_runs_in_process():
     r = subprocess.run([sys.executable, BENCH, "--gpus", "1", "--stub-gpu"], env=_env(), cwd=ROOT,
                        stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
-    j = json.loads(r.stdout.strip())
+    j = json.loads(r.stdout.strip())  # exactly one line: the banner printed on fd 1 went to stderr
     assert j["n_gpus"] == 1 and j["ranks"] == [[0, 1, 0]]
     assert j["roofline"]["per_rank_avg_kernel_us"] == [40.0] and j["per_rank_device"] == [0]
 

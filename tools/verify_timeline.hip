@@ -352,19 +352,20 @@ __global__ void __launch_bounds__(256, 4)
                     cts::block_reduce_mismatch(first, count);
                 if (lane == 0) {
                     TailSlot* sl = slots + i;
+                    // device-scope atomics only, no fences: an agent-scope fence on gfx950 writes back / invalidates
+                    // the XCD's L2 (~70-100 ns each, serialised: the first form of this tool ran 139-1095 us)
                     if (first != cts::kNone) {  // stored as ~first (0 = none: the slots start zeroed)
                         atomicMax(&sl->first, ~first);
                         atomicAdd(&sl->count, count);
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // both done before the arrival
                     }
-                    __threadfence();
                     if (atomicAdd(&sl->arrive, 1u) == (uint32_t)PARTS - 1u) {  // the last part finishes the buffer
-                        __threadfence();
                         const uint32_t f = atomicAdd(&sl->first, 0u), c = atomicAdd(&sl->count, 0u);
                         cts::finish_buffer(s, d, i, f == 0u ? cts::kNone : ~f, c, results, ctr[0], conn_first_fail,
                                            n_conns);
-                        sl->first = 0u;
-                        sl->count = 0u;
-                        sl->arrive = 0u;
+                        atomicExch(&sl->first, 0u);
+                        atomicExch(&sl->count, 0u);
+                        atomicExch(&sl->arrive, 0u);
                     }
                 }
             }
@@ -606,6 +607,7 @@ int main(int argc, char** argv)
             const uint32_t tail = n - fr * grid;
             switch (form) {
             case 0: PRODUCT<<<grid, 256, 0, s>>>(arena[i % R], bytes, d, n, res, ctr, cff, n); break;
+            case 1: verify_tail<1><<<grid + tail, 256, 0, s>>>(arena[i % R], bytes, d, n, res, ctr, cff, n, grid, fr, slots); break;
             case 2: verify_tail<2><<<grid + 2 * tail, 256, 0, s>>>(arena[i % R], bytes, d, n, res, ctr, cff, n, grid, fr, slots); break;
             case 4: verify_tail<4><<<grid + 4 * tail, 256, 0, s>>>(arena[i % R], bytes, d, n, res, ctr, cff, n, grid, fr, slots); break;
             default: verify_tail<8><<<grid + 8 * tail, 256, 0, s>>>(arena[i % R], bytes, d, n, res, ctr, cff, n, grid, fr, slots); break;
@@ -621,7 +623,7 @@ int main(int argc, char** argv)
         CHECK(hipMemcpy(ca.data(), cff, n * 4, hipMemcpyDeviceToHost));
         const std::vector<uint64_t> c0 = read_ctr();
         int ok = 1;
-        for (int form : {2, 4, 8})
+        for (int form : {1, 2, 4, 8})
             for (uint32_t fr : {3u, 2u}) {
                 CHECK(hipMemset(res, 0, n * sizeof(cts_verify_result)));
                 CHECK(hipMemset(ctr, 0, CTS_COUNTER_SHARDS * 64));
@@ -638,17 +640,18 @@ int main(int argc, char** argv)
         std::fflush(stdout);
         if (!ok) return 3;
         for (int pass = 0; pass < passes; ++pass) {
-            double t[7];
+            double t[9];
             int k = 0;
             t[k++] = time_us([&](int i) { run(0, i, 3); }, reps, s);
-            for (int form : {2, 4, 8})
+            for (int form : {1, 2, 4, 8})
                 for (uint32_t fr : {3u, 2u}) t[k++] = time_us([&](int i) { run(form, i, fr); }, reps, s);
             const double tp = time_us([&](int i) {
                 plain_read<false><<<grid, 256, 0, s>>>(reinterpret_cast<const u32x4*>(arena[i % R]), n, st, out);
             }, reps, s);
-            std::printf("{\"kind\":\"tail_time\",\"pass\":%d,\"launches\":%d,\"product_us\":%.2f,\"p2_r3_us\":%.2f,"
-                        "\"p2_r2_us\":%.2f,\"p4_r3_us\":%.2f,\"p4_r2_us\":%.2f,\"p8_r3_us\":%.2f,\"p8_r2_us\":%.2f,"
-                        "\"plain_read_us\":%.2f}\n", pass, reps, t[0], t[1], t[2], t[3], t[4], t[5], t[6], tp);
+            std::printf("{\"kind\":\"tail_time\",\"pass\":%d,\"launches\":%d,\"product_us\":%.2f,\"p1_r3_us\":%.2f,"
+                        "\"p1_r2_us\":%.2f,\"p2_r3_us\":%.2f,\"p2_r2_us\":%.2f,\"p4_r3_us\":%.2f,\"p4_r2_us\":%.2f,"
+                        "\"p8_r3_us\":%.2f,\"p8_r2_us\":%.2f,\"plain_read_us\":%.2f}\n", pass, reps, t[0], t[1], t[2], t[3],
+                        t[4], t[5], t[6], t[7], t[8], tp);
             std::fflush(stdout);
         }
         return 0;
