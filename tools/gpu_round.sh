@@ -26,6 +26,9 @@ if [[ $STEPS == all || $STEPS == *engines* ]]; then
   # single-process multi-GPU leg (the ctsTraffic process model) at the GPUs this box has
   run engines
   timeout -k 10 300 python bench.py --engines 1 --no-cpu-baseline --no-extras > "$OUT/bench_engines1.json" 2> "$OUT/bench_engines1.err"
+  # two engines sharing this GPU: the node-wide fold and RCCL all-reduce over two blocks (one device, one rank)
+  timeout -k 10 300 python bench.py --engines 2 --engines-same-gpu --no-cpu-baseline --no-extras \
+    > "$OUT/bench_engines2same.json" 2> "$OUT/bench_engines2same.err"
 fi
 if [[ $STEPS == all || $STEPS == *ceiling* ]]; then
   # plain streaming-read reference on the same box (build: see tools/hbm_read_ceiling.hip)
