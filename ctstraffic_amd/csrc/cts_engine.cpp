@@ -142,9 +142,9 @@ int ensure_stage(cts_engine* e, size_t bytes)
 // A workgroup that fell a whole ring behind (a late poller) takes the jobs whose slots hold later jobs as
 // no-ops (mailbox_kernel). A job unanswered after timeout_s marks the mailbox broken: callers then verify
 // with a launch per call (cts_verify_mapped), and the first post after the grid has drained resets the
-// rings and starts over. Freeing pinned memory (cts_host_free, a growing staging buffer) first stops the
-// grid (Pause): a free waits for every kernel on the device, and the resident grid would keep it waiting
-// for as long as other threads post.
+// rings and starts over. Freeing pinned memory (cts_host_free, a growing staging buffer, teardown) first makes
+// the engine's device current and stops every engine's grid on it (DeviceQuiesce, Pause): a free waits for
+// every kernel on the current device, and a resident grid would keep it waiting for as long as threads post.
 struct Mailbox {
     cts_engine* e = nullptr;
     // groups x cts::kMailGroup workgroups: 8 groups measured best for 8-16 concurrent callers (with 16
@@ -179,24 +179,7 @@ struct Mailbox {
     std::atomic<uint64_t> launches{0};
     std::atomic<bool> broken_flag{false};  // `broken`, readable without mu
 
-    ~Mailbox()
-    {
-        {
-            std::lock_guard<std::mutex> lk(mu);
-            quit = true;
-        }
-        cv.notify_all();
-        if (watchdog.joinable()) watchdog.join();
-        (void)Stop(false);
-        DeviceGuard g(e->device);
-        if (stream) {
-            (void)hipStreamSynchronize(stream);
-            (void)hipStreamDestroy(stream);
-        }
-        if (grid_done) (void)hipEventDestroy(grid_done);
-        if (parts) (void)hipHostFree(parts);
-        if (slots) (void)hipHostFree(slots);
-    }
+    ~Mailbox();  // (after DeviceQuiesce)
 
     int Init(cts_engine* eng)
     {
@@ -458,17 +441,41 @@ struct Mailbox {
 
 namespace {
 
-void pinned_free(cts_engine* e, void* p)
-{
-    Mailbox* m = nullptr;
+// Every engine's mailbox, whatever its device. hipHostFree is an implicit hipDeviceSynchronize of the current
+// device: a resident grid on that device, any engine's, would hold a free up for as long as its callers keep
+// posting. A pinned free therefore makes its engine's device current and stops every grid on it first
+// (DeviceQuiesce); the grids relaunch on their next post.
+std::mutex g_mail_reg_mu;  // guards g_mail_reg; held while a free pauses grids (lock order: before any Mailbox::mu)
+std::vector<Mailbox*> g_mail_reg;
+
+class DeviceQuiesce {
+public:
+    explicit DeviceQuiesce(int device) : dev_(device), guard_(device), lk_(g_mail_reg_mu)
     {
-        std::lock_guard<std::mutex> lk(e->mail_init_mu);
-        m = e->mail.get();
+        for (Mailbox* m : g_mail_reg)
+            if (m->e->device == dev_) m->Pause();
     }
-    if (m != nullptr) m->Pause();
-    (void)hipHostFree(p);
-    if (m != nullptr) m->Resume();
+    ~DeviceQuiesce()
+    {
+        for (Mailbox* m : g_mail_reg)
+            if (m->e->device == dev_) m->Resume();
+    }
+    DeviceQuiesce(const DeviceQuiesce&) = delete;
+    DeviceQuiesce& operator=(const DeviceQuiesce&) = delete;
+
+private:
+    int dev_;
+    DeviceGuard guard_;
+    std::unique_lock<std::mutex> lk_;
+};
+
+int pinned_free_on(int device, void* p)
+{
+    DeviceQuiesce q(device);
+    return hip_status(hipHostFree(p));
 }
+
+void pinned_free(cts_engine* e, void* p) { (void)pinned_free_on(e->device, p); }
 
 int mailbox_of(cts_engine* e, Mailbox** out)
 {
@@ -478,6 +485,14 @@ int mailbox_of(cts_engine* e, Mailbox** out)
         if (!m) return CTS_E_NOMEM;
         const int rc = m->Init(e);
         if (rc != CTS_OK) return rc;
+        {
+            std::lock_guard<std::mutex> lk(g_mail_reg_mu);
+            try {
+                g_mail_reg.push_back(m.get());
+            } catch (const std::bad_alloc&) {  // nothing may cross the C ABI
+                return CTS_E_NOMEM;
+            }
+        }
         e->mail = std::move(m);
     }
     *out = e->mail.get();
@@ -485,6 +500,34 @@ int mailbox_of(cts_engine* e, Mailbox** out)
 }
 
 }  // namespace
+
+Mailbox::~Mailbox()
+{
+    if (e == nullptr) return;
+    {
+        std::lock_guard<std::mutex> lk(g_mail_reg_mu);  // no free pauses this mailbox from here on
+        g_mail_reg.erase(std::remove(g_mail_reg.begin(), g_mail_reg.end(), this), g_mail_reg.end());
+    }
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        quit = true;
+    }
+    cv.notify_all();
+    if (watchdog.joinable()) watchdog.join();
+    (void)Stop(false);
+    {
+        DeviceGuard g(e->device);
+        if (stream) {
+            (void)hipStreamSynchronize(stream);
+            (void)hipStreamDestroy(stream);
+        }
+        if (grid_done) (void)hipEventDestroy(grid_done);
+    }
+    if (parts == nullptr && slots == nullptr) return;
+    DeviceQuiesce q(e->device);  // the other engines' grids on this device
+    if (parts) (void)hipHostFree(parts);
+    if (slots) (void)hipHostFree(slots);
+}
 
 extern "C" {
 
@@ -550,14 +593,17 @@ int cts_engine_destroy(cts_engine* e)
 {
     if (e == nullptr) return CTS_E_INVALID;
     e->mail.reset();  // stops the resident grid (kMailStop) and joins its watchdog
-    for (auto& st : e->stage_pool) (void)hipHostFree(st.p);
-    e->stage_pool.clear();
     {
         DeviceGuard g(e->device);
         if (e->stream) {
             (void)hipStreamSynchronize(e->stream);
             (void)hipStreamDestroy(e->stream);
         }
+    }
+    {
+        DeviceQuiesce q(e->device);  // the other engines' grids on this device
+        for (auto& st : e->stage_pool) (void)hipHostFree(st.p);
+        e->stage_pool.clear();
         if (e->stage) (void)hipHostFree(e->stage);
         if (e->stage_desc) (void)hipHostFree(e->stage_desc);
         if (e->stage_res) (void)hipHostFree(e->stage_res);
@@ -908,7 +954,7 @@ int cts_host_alloc(cts_engine* e, uint64_t bytes, void** host_ptr, void** dev_vi
     if (dev_view != nullptr) {
         void* d = nullptr;
         if (hipHostGetDevicePointer(&d, p, 0) != hipSuccess) {
-            (void)hipHostFree(p);
+            (void)pinned_free_on(e->device, p);
             *host_ptr = nullptr;
             return CTS_E_HIP;
         }
@@ -920,18 +966,9 @@ int cts_host_alloc(cts_engine* e, uint64_t bytes, void** host_ptr, void** dev_vi
 int cts_host_free(cts_engine* e, void* host_ptr)
 {
     if (e == nullptr || host_ptr == nullptr) return CTS_E_INVALID;
-    DeviceGuard g(e->device);
-    // hipHostFree waits for the device's kernels: the resident mailbox grid is stopped first, so a free
-    // returns while other threads keep posting (their verifies take the launch path meanwhile)
-    Mailbox* m = nullptr;
-    {
-        std::lock_guard<std::mutex> lk(e->mail_init_mu);
-        m = e->mail.get();
-    }
-    if (m != nullptr) m->Pause();
-    const int rc = hip_status(hipHostFree(host_ptr));
-    if (m != nullptr) m->Resume();
-    return rc;
+    // hipHostFree waits for the device's kernels: every resident mailbox grid on the device is stopped first, so a
+    // free returns while other threads keep posting (their verifies take the launch path meanwhile)
+    return pinned_free_on(e->device, host_ptr);
 }
 
 int cts_host_device_pointer(void* host_ptr, void** dev_view)

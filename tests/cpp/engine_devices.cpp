@@ -1,0 +1,610 @@
+// engine_devices.cpp — the engine's C ABI (cts_engine.cpp) on a fake eight-device HIP runtime, built with g++ under
+// the host sanitizers (tests/test_host_sanitizers.py). The test box has one GPU, so every engine on device g > 0
+// runs only here: each entry point must make the engine's device current for every HIP call and launch it makes
+// (DeviceGuard) and give the caller its own device back, on the caller's thread, the watchdog thread and
+// concurrent callers alike.
+//
+// The fake runtime keeps a current device per thread, gives every stream and event the device current at its
+// creation, and counts a violation whenever a stream-ordered call (launch, memset, copy, event record, stream
+// synchronize or destroy) runs with another device current. The SYNC mailbox's resident grid
+// (cts::launch_mailbox) is emulated by a host thread that polls the slot rings exactly as mailbox_kernel does
+// (tags, no-op jobs, stop jobs, the idle exit) and answers every piece with a clean part record; the event
+// recorded after it completes when that thread has left, and hipHostFree counts a violation when it would wait
+// on a running grid (the reason Pause exists). Verify launches record their device and write clean records.
+#include <hip/hip_runtime_api.h>
+#include <pthread.h>
+#include <time.h>
+
+#include <atomic>
+#include <chrono>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <set>
+#include <thread>
+#include <vector>
+
+#include "cts_engine.h"
+#include "cts_internal.hpp"
+#include "cts_media_stream.h"
+
+namespace {
+
+constexpr int kDevices = 8;
+thread_local int t_cur = 0;
+
+std::atomic<int> g_violations{0};
+std::atomic<int> g_launches[kDevices];
+std::atomic<int> g_grids{0};  // emulated mailbox grids started
+std::mutex g_grid_mu;
+std::vector<std::shared_ptr<std::atomic<bool>>> g_grid_done;  // every grid's done flag, in launch order
+
+void violation(const char* what, int want, int have)
+{
+    std::fprintf(stderr, "violation: %s on device %d with device %d current\n", what, want, have);
+    g_violations.fetch_add(1);
+}
+
+}  // namespace
+
+// The runtime's opaque handles, defined by the fake.
+struct ihipStream_t {
+    int device;
+    std::mutex mu;
+    std::vector<std::shared_ptr<std::atomic<bool>>> work;  // emulated grids launched on it (done flags)
+    std::vector<std::thread> threads;
+};
+struct ihipEvent_t {
+    int device;
+    std::mutex mu;
+    std::vector<std::shared_ptr<std::atomic<bool>>> waits;  // the stream's work when recorded
+};
+
+namespace {
+
+std::mutex g_mu;                 // guards g_streams, g_pinned and every null stream
+std::set<ihipStream_t*> g_streams;
+std::set<void*> g_pinned;
+ihipStream_t g_null[kDevices];   // the null stream of each device
+const bool g_null_init = [] {
+    for (int d = 0; d < kDevices; ++d) g_null[d].device = d;
+    return true;
+}();
+
+ihipStream_t* stream_of(hipStream_t s) { return s ? s : &g_null[t_cur]; }
+
+void check_stream(const char* what, hipStream_t s)
+{
+    const ihipStream_t* st = stream_of(s);
+    if (st->device != t_cur) violation(what, st->device, t_cur);
+}
+
+// an emulated grid still running on a stream of `dev` (what hipDeviceSynchronize of `dev` would wait for); -1: any
+bool grid_running(int dev)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto busy = [](ihipStream_t* st) {
+        std::lock_guard<std::mutex> l2(st->mu);
+        for (auto& w : st->work)
+            if (!w->load(std::memory_order_acquire)) return true;
+        return false;
+    };
+    for (ihipStream_t* st : g_streams)
+        if ((dev < 0 || st->device == dev) && busy(st)) return true;
+    for (int d = 0; d < kDevices; ++d)
+        if ((dev < 0 || d == dev) && busy(&g_null[d])) return true;
+    return false;
+}
+
+void join_stream(ihipStream_t* st)
+{
+    std::vector<std::thread> ts;
+    {
+        std::lock_guard<std::mutex> lk(st->mu);
+        ts.swap(st->threads);
+        st->work.clear();
+    }
+    for (auto& t : ts) t.join();
+}
+
+}  // namespace
+
+extern "C" {
+
+hipError_t hipGetDeviceCount(int* count)
+{
+    *count = kDevices;
+    return hipSuccess;
+}
+hipError_t hipGetDevice(int* d)
+{
+    *d = t_cur;
+    return hipSuccess;
+}
+hipError_t hipSetDevice(int d)
+{
+    if (d < 0 || d >= kDevices) return hipErrorInvalidDevice;
+    t_cur = d;
+    return hipSuccess;
+}
+hipError_t hipDeviceGetAttribute(int* v, hipDeviceAttribute_t attr, int dev)
+{
+    if (dev < 0 || dev >= kDevices) return hipErrorInvalidDevice;
+    *v = attr == hipDeviceAttributeMultiprocessorCount ? 256 : 0;
+    return hipSuccess;
+}
+hipError_t hipDeviceGetPCIBusId(char* bus, int len, int dev)
+{
+    if (dev < 0 || dev >= kDevices) return hipErrorInvalidDevice;
+    std::snprintf(bus, (size_t)len, "0000:FF:%02X.0", dev);  // no such PCI device: numa node -1
+    return hipSuccess;
+}
+hipError_t hipStreamCreateWithFlags(hipStream_t* s, unsigned int)
+{
+    ihipStream_t* st = new ihipStream_t();
+    st->device = t_cur;
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_streams.insert(st);
+    *s = st;
+    return hipSuccess;
+}
+hipError_t hipStreamDestroy(hipStream_t s)
+{
+    if (s == nullptr) return hipErrorInvalidHandle;
+    check_stream("hipStreamDestroy", s);
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        if (g_streams.erase(s) == 0) return hipErrorInvalidHandle;
+    }
+    join_stream(s);
+    delete s;
+    return hipSuccess;
+}
+hipError_t hipStreamSynchronize(hipStream_t s)
+{
+    check_stream("hipStreamSynchronize", s);
+    join_stream(stream_of(s));
+    return hipSuccess;
+}
+hipError_t hipEventCreateWithFlags(hipEvent_t* e, unsigned)
+{
+    ihipEvent_t* ev = new ihipEvent_t();
+    ev->device = t_cur;
+    *e = ev;
+    return hipSuccess;
+}
+hipError_t hipEventRecord(hipEvent_t e, hipStream_t s)
+{
+    check_stream("hipEventRecord", s);
+    ihipStream_t* st = stream_of(s);
+    if (st->device != e->device) violation("hipEventRecord (event of another device)", e->device, st->device);
+    std::vector<std::shared_ptr<std::atomic<bool>>> w;
+    {
+        std::lock_guard<std::mutex> lk(st->mu);
+        w = st->work;
+    }
+    std::lock_guard<std::mutex> lk(e->mu);
+    e->waits.swap(w);
+    return hipSuccess;
+}
+hipError_t hipEventQuery(hipEvent_t e)
+{
+    std::lock_guard<std::mutex> lk(e->mu);
+    for (auto& w : e->waits)
+        if (!w->load(std::memory_order_acquire)) return hipErrorNotReady;
+    return hipSuccess;
+}
+hipError_t hipEventDestroy(hipEvent_t e)
+{
+    delete e;
+    return hipSuccess;
+}
+hipError_t hipHostMalloc(void** p, size_t bytes, unsigned int)
+{
+    *p = std::aligned_alloc(64, (bytes + 63) & ~(size_t)63);
+    if (*p == nullptr) return hipErrorOutOfMemory;
+    std::memset(*p, 0, bytes);
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_pinned.insert(*p);
+    return hipSuccess;
+}
+hipError_t hipHostFree(void* p)
+{
+    // the runtime's free is an implicit hipDeviceSynchronize of the current device: a resident grid still polling
+    // there would hold it up for as long as that grid's callers keep posting
+    if (grid_running(t_cur)) violation("hipHostFree while a mailbox grid runs on the current device", t_cur, t_cur);
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        if (g_pinned.erase(p) == 0) return hipErrorInvalidValue;
+    }
+    std::free(p);
+    return hipSuccess;
+}
+hipError_t hipHostGetDevicePointer(void** d, void* h, unsigned int)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    for (void* b : g_pinned)  // (a handful of allocations: a scan is fine)
+        if (b == h) {
+            *d = h;  // portable mapped memory: the same address on every device
+            return hipSuccess;
+        }
+    return hipErrorInvalidValue;
+}
+hipError_t hipMemsetAsync(void* dst, int v, size_t bytes, hipStream_t s)
+{
+    check_stream("hipMemsetAsync", s);
+    std::memset(dst, v, bytes);
+    return hipSuccess;
+}
+hipError_t hipMemcpyAsync(void* dst, const void* src, size_t bytes, hipMemcpyKind, hipStream_t s)
+{
+    check_stream("hipMemcpyAsync", s);
+    std::memcpy(dst, src, bytes);
+    return hipSuccess;
+}
+
+// std::condition_variable::wait_for (the mailbox watchdog) waits in pthread_cond_clockwait, which this
+// toolchain's ThreadSanitizer does not intercept: it would miss the wait's unlock and report a double lock. The
+// driver routes it to pthread_cond_timedwait (intercepted) with the same deadline.
+int pthread_cond_clockwait(pthread_cond_t* c, pthread_mutex_t* m, clockid_t clk, const struct timespec* abs)
+{
+    struct timespec now_c, now_r;
+    clock_gettime(clk, &now_c);
+    clock_gettime(CLOCK_REALTIME, &now_r);
+    int64_t left = (int64_t)(abs->tv_sec - now_c.tv_sec) * 1000000000 + (abs->tv_nsec - now_c.tv_nsec);
+    if (left < 0) left = 0;
+    const int64_t t = (int64_t)now_r.tv_sec * 1000000000 + now_r.tv_nsec + left;
+    struct timespec dl;
+    dl.tv_sec = t / 1000000000;
+    dl.tv_nsec = t % 1000000000;
+    return pthread_cond_timedwait(c, m, &dl);
+}
+
+}  // extern "C"
+
+// ---- the launchers: record the device, write clean records ---------------------------------------------------
+namespace cts {
+namespace {
+
+void launched(const char* what, hipStream_t s)
+{
+    check_stream(what, s);
+    g_launches[stream_of(s)->device].fetch_add(1);
+}
+
+void clean(cts_verify_result* r, const cts_buf_desc* d, uint32_t n)
+{
+    if (r == nullptr) return;
+    for (uint32_t i = 0; i < n; ++i) r[i] = cts_verify_result{d[i].length, 0, 0, 0, 1, 0};
+}
+
+}  // namespace
+
+hipError_t launch_fill(uint8_t*, uint64_t, const cts_buf_desc*, uint32_t, uint32_t, hipStream_t s, const LaunchGeometry&)
+{
+    launched("launch_fill", s);
+    return hipSuccess;
+}
+hipError_t launch_fill_span(uint8_t*, uint64_t, uint32_t, hipStream_t s, const LaunchGeometry&)
+{
+    launched("launch_fill_span", s);
+    return hipSuccess;
+}
+hipError_t launch_verify(const uint8_t*, uint64_t, const cts_buf_desc* d, uint32_t n, uint32_t, cts_verify_result* r,
+                         uint64_t*, uint32_t*, uint32_t, hipStream_t s, const LaunchGeometry&)
+{
+    launched("launch_verify", s);
+    clean(r, d, n);
+    return hipSuccess;
+}
+hipError_t launch_verify_strided(const uint8_t*, uint64_t, uint32_t, const uint32_t*, uint32_t, uint32_t, uint32_t,
+                                 uint32_t, cts_verify_result*, uint64_t*, uint32_t*, uint32_t, hipStream_t s,
+                                 const LaunchGeometry&)
+{
+    launched("launch_verify_strided", s);
+    return hipSuccess;
+}
+hipError_t launch_media_stream_fill(uint8_t*, uint64_t, const cts_buf_desc*, const cts_datagram_header*, uint32_t,
+                                    hipStream_t s, const LaunchGeometry&)
+{
+    launched("launch_media_stream_fill", s);
+    return hipSuccess;
+}
+hipError_t launch_media_stream_fill_strided(uint8_t*, uint64_t, uint32_t, const uint32_t*, const cts_datagram_header*,
+                                            uint32_t, hipStream_t s, const LaunchGeometry&)
+{
+    launched("launch_media_stream_fill_strided", s);
+    return hipSuccess;
+}
+hipError_t launch_media_stream_verify(const uint8_t*, uint64_t, const cts_buf_desc*, uint32_t, cts_datagram_record*,
+                                      cts_verify_result*, uint64_t*, hipStream_t s, const LaunchGeometry&)
+{
+    launched("launch_media_stream_verify", s);
+    return hipSuccess;
+}
+hipError_t launch_media_stream_verify_strided(const uint8_t*, uint64_t, uint32_t, const uint32_t*, uint32_t,
+                                              cts_datagram_record*, cts_verify_result*, uint64_t*, hipStream_t s,
+                                              const LaunchGeometry&)
+{
+    launched("launch_media_stream_verify_strided", s);
+    return hipSuccess;
+}
+hipError_t launch_media_stream_status(const uint8_t*, uint64_t, const cts_buf_desc*, const uint32_t*, uint32_t,
+                                      uint32_t, cts_datagram_status*, uint64_t*, hipStream_t s, const LaunchGeometry&)
+{
+    launched("launch_media_stream_status", s);
+    return hipSuccess;
+}
+hipError_t launch_media_stream_frames(const uint8_t*, uint64_t, const cts_buf_desc*, const uint32_t*, uint32_t,
+                                      uint32_t, const cts_frame_window&, uint64_t*, uint64_t*, uint64_t*,
+                                      hipStream_t s, const LaunchGeometry&)
+{
+    launched("launch_media_stream_frames", s);
+    return hipSuccess;
+}
+
+// The resident grid, emulated: group g polls slot g * per_group + j % per_group for the tag j + 1 from
+// starts.j[g] on, as mailbox_kernel does; every piece of a job is answered clean; a stop job (len 0) is answered
+// by every workgroup of the group and ends it; a group that waits idle_ticks (100 MHz) for a job leaves.
+hipError_t launch_mailbox(const MailSlot* slots, MailPart* parts, uint32_t per_group, const MailStarts& starts,
+                          uint32_t groups, uint64_t idle_ticks, hipStream_t s, uint64_t)
+{
+    launched("launch_mailbox", s);
+    ihipStream_t* st = stream_of(s);
+    auto done = std::make_shared<std::atomic<bool>>(false);
+    const MailStarts js = starts;
+    MailSlot* ring = const_cast<MailSlot*>(slots);
+    std::thread t([=] {
+        using clock = std::chrono::steady_clock;
+        const auto idle = std::chrono::nanoseconds(idle_ticks * 10);
+        std::vector<uint64_t> j(js.j, js.j + groups);
+        std::vector<bool> live(groups, true);
+        std::vector<clock::time_point> since(groups, clock::now());
+        uint32_t nlive = groups;
+        while (nlive != 0) {
+            bool progress = false;
+            for (uint32_t g = 0; g < groups; ++g) {
+                if (!live[g]) continue;
+                const uint32_t k = g * per_group + (uint32_t)(j[g] % per_group);
+                const uint32_t tag = (uint32_t)(j[g] + 1);
+                const uint64_t ls = __atomic_load_n(&ring[k].len_seq, __ATOMIC_ACQUIRE);
+                const uint32_t have = (uint32_t)(ls >> 32);
+                if (have == tag) {
+                    const uint64_t pe = __atomic_load_n(&ring[k].ptr_exp, __ATOMIC_RELAXED);
+                    const uint32_t len = (uint32_t)ls;
+                    ++j[g];
+                    progress = true;
+                    since[g] = clock::now();
+                    if (len == kMailSkip) continue;
+                    const uint32_t np = mail_parts(pe & 0xFFFFFFFFFFFFull, len);
+                    for (uint32_t i = 0; i < np; ++i) {
+                        MailPart* p = parts + (size_t)k * kMailGroup + i;
+                        __atomic_store_n(&p->g0, 0xFFFFFFFFull | ((uint64_t)tag << 32), __ATOMIC_RELEASE);
+                        __atomic_store_n(&p->g1, (uint64_t)(tag & 0xFFFFFFu) << 40, __ATOMIC_RELEASE);
+                    }
+                    if (len == 0) {
+                        live[g] = false;
+                        --nlive;
+                    }
+                } else if ((int32_t)(have - tag) > 0) {  // a later job holds the slot: this one is a no-op
+                    ++j[g];
+                    progress = true;
+                } else if (clock::now() - since[g] > idle) {
+                    live[g] = false;
+                    --nlive;
+                }
+            }
+            if (!progress) std::this_thread::sleep_for(std::chrono::microseconds(20));
+        }
+        done->store(true, std::memory_order_release);
+    });
+    {
+        std::lock_guard<std::mutex> lk(g_grid_mu);
+        g_grid_done.push_back(done);
+    }
+    std::lock_guard<std::mutex> lk(st->mu);
+    st->work.push_back(done);
+    st->threads.push_back(std::move(t));
+    g_grids.fetch_add(1);
+    return hipSuccess;
+}
+
+}  // namespace cts
+
+// ---- the driver --------------------------------------------------------------------------------------------
+namespace {
+
+int g_fail = 0;
+#define CHECK(c)                                                               \
+    do {                                                                       \
+        if (!(c)) {                                                            \
+            std::fprintf(stderr, "%s:%d: check failed: %s\n", __FILE__, __LINE__, #c); \
+            ++g_fail;                                                          \
+        }                                                                      \
+    } while (0)
+
+// One engine's every device entry point from a thread whose own device is `home`; the launches counted on the
+// engine's device must grow by exactly the entry points that launch, and `home` must be current afterwards.
+void drive(cts_engine* e, int dev, int home, int rounds)
+{
+    CHECK(hipSetDevice(home) == hipSuccess);
+    alignas(64) static thread_local uint8_t arena[1 << 16];
+    alignas(64) static thread_local uint64_t block[CTS_COUNTER_SHARDS * 8];
+    alignas(64) static thread_local uint8_t host[70000];
+    cts_buf_desc d[2] = {{0, 4096, 0, 0, 0}, {4096, 1472, 7, 1, 0}};
+    cts_verify_result r[2];
+    uint32_t lens[2] = {1472, 1472}, first_fail[2] = {0, 0};
+    cts_datagram_header hd[2] = {{1, 2, 3}, {2, 2, 3}};
+    cts_datagram_record rec[2];
+    cts_datagram_status sts[2];
+    cts_frame_window w{0, 100, 4, 0};
+    alignas(8) static thread_local uint8_t totals[4096];
+    uint64_t frame_bytes[4];
+    cts_counters c{};
+    void* s = nullptr;
+    int cur = -1;
+    auto here = [&](const char* what) {
+        (void)hipGetDevice(&cur);
+        if (cur != home) {
+            std::fprintf(stderr, "%s left device %d current (caller's %d, engine's %d)\n", what, cur, home, dev);
+            ++g_fail;
+            (void)hipSetDevice(home);
+        }
+    };
+    CHECK(cts_engine_stream_create(e, &s) == CTS_OK);
+    here("stream_create");
+    CHECK(s != nullptr && static_cast<ihipStream_t*>(s)->device == dev);
+    for (int it = 0; it < rounds; ++it) {
+        const int before = g_launches[dev].load();
+        CHECK(cts_counters_reset(e, block, s) == CTS_OK);
+        here("counters_reset");
+        CHECK(cts_fill(e, arena, sizeof(arena), d, 2, 4096, s) == CTS_OK);
+        here("fill");
+        CHECK(cts_sender_buffer_fill(e, arena, 1024, s) == CTS_OK);
+        here("sender_buffer_fill");
+        CHECK(cts_verify(e, arena, sizeof(arena), d, 2, 4096, r, block, first_fail, 2, s) == CTS_OK);
+        here("verify");
+        CHECK(cts_verify(e, arena, sizeof(arena), d, 2, 4096, r, block, first_fail, 2, nullptr) == CTS_OK);  // null stream
+        here("verify (null stream)");
+        CHECK(cts_verify_strided(e, arena, sizeof(arena), 2048, lens, 2, 0, 0, 0, r, block, first_fail, 2, s) == CTS_OK);
+        here("verify_strided");
+        CHECK(cts_media_stream_fill(e, arena, sizeof(arena), d, hd, 2, s) == CTS_OK);
+        here("media_stream_fill");
+        CHECK(cts_media_stream_fill_strided(e, arena, sizeof(arena), 2048, lens, hd, 2, s) == CTS_OK);
+        here("media_stream_fill_strided");
+        CHECK(cts_media_stream_verify(e, arena, sizeof(arena), d, 2, rec, r, block, s) == CTS_OK);
+        here("media_stream_verify");
+        CHECK(cts_media_stream_verify_strided(e, arena, sizeof(arena), 2048, lens, 2, rec, r, block, s) == CTS_OK);
+        here("media_stream_verify_strided");
+        CHECK(cts_media_stream_verify_status(e, arena, sizeof(arena), d, 2, sts, block, s) == CTS_OK);
+        here("media_stream_verify_status");
+        CHECK(cts_media_stream_verify_strided_status(e, arena, sizeof(arena), 2048, lens, 2, sts, block, s) == CTS_OK);
+        here("media_stream_verify_strided_status");
+        CHECK(cts_media_stream_verify_frames(e, arena, sizeof(arena), d, 2, &w, totals, frame_bytes, block, s) == CTS_OK);
+        here("media_stream_verify_frames");
+        CHECK(cts_media_stream_verify_strided_frames(e, arena, sizeof(arena), 2048, lens, 2, &w, totals, frame_bytes,
+                                                     block, s) == CTS_OK);
+        here("media_stream_verify_strided_frames");
+        CHECK(g_launches[dev].load() - before >= 13);
+        CHECK(cts_counters_read(e, block, &c, s) == CTS_OK);
+        here("counters_read");
+        // the host paths: one-buffer verifies (the mailbox, and the launch path), a batch, pinned memory
+        for (int k = 0; k < 4; ++k) {
+            cts_verify_result hr{};
+            const uint32_t len = k == 3 ? 70000u : 1024u << k;
+            CHECK(cts_verify_host(e, host, len, (uint32_t)k, &hr) == CTS_OK);
+            here("verify_host");
+            CHECK(hr.pass == 1 && hr.first_mismatch == len);
+        }
+        void* hp = nullptr;
+        void* dv = nullptr;
+        CHECK(cts_host_alloc(e, 4096, &hp, &dv) == CTS_OK);
+        here("host_alloc");
+        cts_verify_result mr{};
+        CHECK(cts_verify_mapped(e, dv, 4000, 5, &mr) == CTS_OK && mr.pass == 1);
+        here("verify_mapped");
+        CHECK(cts_host_free(e, hp) == CTS_OK);  // stops this engine's grid first
+        here("host_free");
+        const void* bufs[2] = {host, host + 100};
+        const uint32_t blens[2] = {100, 3000}, exp[2] = {0, 100};
+        cts_verify_result br[2];
+        cts_counters bc{};
+        CHECK(cts_verify_host_batch(e, bufs, blens, exp, nullptr, 2, br, &bc) == CTS_OK);
+        here("verify_host_batch");
+        int prev = cts_engine_set_attr(e, CTS_ATTR_SYNC_MAILBOX, 0);
+        CHECK(prev == CTS_OK);
+        cts_verify_result lr{};
+        CHECK(cts_verify_host(e, host, 9000, 3, &lr) == CTS_OK);
+        here("verify_host (launch path)");
+        CHECK(cts_engine_set_attr(e, CTS_ATTR_SYNC_MAILBOX, 1) == CTS_OK);
+    }
+    CHECK(cts_engine_numa_node(e) == -1);
+    here("numa_node");
+    CHECK(cts_engine_stream_destroy(e, s) == CTS_OK);
+    here("stream_destroy");
+}
+
+}  // namespace
+
+int main()
+{
+    std::setvbuf(stdout, nullptr, _IONBF, 0);
+    // grids stay up between posts (no watchdog stop for 10 s): every pinned free below meets running grids
+    setenv("CTS_MAILBOX_IDLE_MS", "10000", 1);
+    // engines on every device, created from a thread whose device is 3
+    CHECK(hipSetDevice(3) == hipSuccess);
+    cts_engine* eng[kDevices + 1] = {};
+    for (int g = 0; g < kDevices; ++g) {
+        CHECK(cts_engine_create(g, &eng[g]) == CTS_OK);
+        CHECK(eng[g] != nullptr && cts_engine_device(eng[g]) == g);
+    }
+    CHECK(cts_engine_create(5, &eng[kDevices]) == CTS_OK);  // a second engine on one device
+    cts_engine* bad = nullptr;
+    CHECK(cts_engine_create(kDevices, &bad) == CTS_E_NO_DEVICE && bad == nullptr);
+    int cur = -1;
+    (void)hipGetDevice(&cur);
+    CHECK(cur == 3);
+
+    // every engine from the main thread (device 3 current), one after the other
+    for (int g = 0; g <= kDevices; ++g) drive(eng[g], cts_engine_device(eng[g]), 3, 2);
+    std::printf("sequential: %d grids, violations %d\n", g_grids.load(), g_violations.load());
+
+    // a staging buffer that grows on engine 2 from a thread whose device (1) runs engine 1's grid: the old
+    // buffer's free must happen on device 2, with device 2's grids stopped, not on the caller's device
+    {
+        static uint8_t big[1 << 20];
+        cts_verify_result r{};
+        CHECK(cts_verify_mapped(eng[1], eng[1] ? (const void*)big : nullptr, 4096, 0, &r) == CTS_OK);  // device 1 busy
+        CHECK(hipSetDevice(1) == hipSuccess);
+        CHECK(cts_verify_host(eng[2], big, sizeof(big) - 64, 9, &r) == CTS_OK && r.pass == 1);
+        (void)hipGetDevice(&cur);
+        CHECK(cur == 1);
+        CHECK(hipSetDevice(3) == hipSuccess);
+    }
+    std::printf("growth: violations %d\n", g_violations.load());
+
+    // one thread per engine at once, each starting from another device than its engine's
+    std::vector<std::thread> ts;
+    for (int g = 0; g <= kDevices; ++g)
+        ts.emplace_back([&, g] { drive(eng[g], cts_engine_device(eng[g]), (g + 1) % kDevices, 3); });
+    for (auto& t : ts) t.join();
+    std::printf("threads: %d grids, violations %d\n", g_grids.load(), g_violations.load());
+
+    // an idle engine's watchdog stops its grid from its own thread (no device current there but its own guard)
+    setenv("CTS_MAILBOX_IDLE_MS", "20", 1);
+    cts_engine* idle = nullptr;
+    CHECK(cts_engine_create(6, &idle) == CTS_OK);
+    {
+        static uint8_t buf[8192];
+        cts_verify_result r{};
+        CHECK(cts_verify_mapped(idle, idle ? (const void*)buf : nullptr, 8192, 1, &r) == CTS_OK && r.pass == 1);
+        std::shared_ptr<std::atomic<bool>> last;
+        {
+            std::lock_guard<std::mutex> lk(g_grid_mu);
+            last = g_grid_done.back();
+        }
+        for (int i = 0; i < 200 && !last->load(); ++i) std::this_thread::sleep_for(std::chrono::milliseconds(10));
+        CHECK(last->load());
+        CHECK(cts_mailbox_launches(idle) == 1);
+    }
+    CHECK(cts_engine_destroy(idle) == CTS_OK);
+
+    for (int g = 0; g <= kDevices; ++g) CHECK(cts_engine_destroy(eng[g]) == CTS_OK);
+    (void)hipGetDevice(&cur);
+    CHECK(cur == 3);
+    for (int g = 0; g < kDevices; ++g) CHECK(g_launches[g].load() > 0);
+    CHECK(g_grids.load() >= kDevices + 1);
+    CHECK(g_violations.load() == 0);
+    CHECK(!grid_running(-1));
+    for (int g = 0; g < kDevices; ++g) join_stream(&g_null[g]);
+    if (g_fail != 0) {
+        std::fprintf(stderr, "engine_devices: %d failures\n", g_fail);
+        return 1;
+    }
+    std::printf("engine_devices: ok (%d engines on %d devices, %d mailbox grids)\n", kDevices + 2, kDevices,
+                g_grids.load());
+    return 0;
+}

@@ -72,6 +72,33 @@ def test_host_code_under_sanitizer(san, driver):
         assert "runtime error" not in out.stderr and "WARNING: ThreadSanitizer" not in out.stderr, out.stderr[-4000:]
 
 
+@pytest.mark.parametrize("san", sorted(set(SAN) - {"plain"}))
+def test_engine_abi_on_eight_fake_devices(san):
+    """The engine's C ABI (cts_engine.cpp) on a fake eight-device HIP runtime (tests/cpp/engine_devices.cpp): engines
+    on devices 0-7 plus a second one on device 5, driven from threads whose own device differs, one after the other and
+    all at once. Every stream-ordered HIP call and launch must run with the engine's device current, the caller's
+    device must be current again afterwards, and no pinned free may run while a SYNC mailbox grid (emulated by a host
+    thread that polls the slot rings as mailbox_kernel does) is resident on the current device: hipHostFree is an
+    implicit hipDeviceSynchronize. The one-GPU test box never runs an engine on a device other than 0."""
+    flags = ["-g", "-O1", "-fno-omit-frame-pointer", "-pthread"] + SAN[san]
+    inc = ["-I", os.path.join(ROOT, "include"), "-I", os.path.join(ROOT, "ctstraffic_amd", "csrc"),
+           "-I", "/opt/rocm/include", "-D__HIP_PLATFORM_AMD__"]
+    with tempfile.TemporaryDirectory() as d:
+        objs = []
+        for src in [os.path.join(ROOT, "ctstraffic_amd", "csrc", "cts_engine.cpp"),
+                    os.path.join(ROOT, "ctstraffic_amd", "csrc", "cts_host_util.cpp"),
+                    os.path.join(ROOT, "tests", "cpp", "engine_devices.cpp")]:
+            o = os.path.join(d, os.path.basename(src) + ".o")
+            subprocess.run(["g++", "-std=c++17", *flags, *inc, "-c", src, "-o", o], check=True)
+            objs.append(o)
+        exe = os.path.join(d, "engine_devices")
+        subprocess.run(["g++", *flags, *objs, "-o", exe, "-ldl"], check=True)
+        out = subprocess.run([exe], capture_output=True, text=True, timeout=300, env={**os.environ, **ENV})
+        assert out.returncode == 0, (out.returncode, out.stdout[-2000:], out.stderr[-4000:])
+        assert "engine_devices: ok" in out.stdout and "violation" not in out.stderr
+        assert "runtime error" not in out.stderr and "WARNING: ThreadSanitizer" not in out.stderr, out.stderr[-4000:]
+
+
 def test_thread_start_failure_never_crosses_the_abi():
     """Every host thread start (the MediaStream client's timer thread, the TCP and UDP feeders' side threads) fails
     on demand through a pthread_create interposer (tests/cpp/thread_start_failure.cpp): the client latches a
