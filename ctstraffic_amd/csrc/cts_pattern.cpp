@@ -101,6 +101,26 @@ enum class PatternError { NoError, TooManyBytes, TooFewBytes, CorruptedBytes, Er
 struct FailFast {
     std::string reason;
 };
+// Makes an engine's device current for the HIP calls a pattern makes itself (events, waits, copies, stream-ordered
+// allocations) and gives the thread its own device back. IO threads and the MediaStream timer thread may have any
+// device current, and an event must be created on the device of the stream it is recorded on.
+struct EngineDevice {
+    int prev = -1;
+    bool switched = false;
+    explicit EngineDevice(const cts_engine* e)
+    {
+        const int d = e != nullptr ? cts_engine_device(e) : -1;
+        if (d < 0 || hipGetDevice(&prev) != hipSuccess) return;
+        switched = prev != d && hipSetDevice(d) == hipSuccess;
+    }
+    ~EngineDevice()
+    {
+        if (switched) (void)hipSetDevice(prev);
+    }
+    EngineDevice(const EngineDevice&) = delete;
+    EngineDevice& operator=(const EngineDevice&) = delete;
+};
+
 struct DeviceError {  // a verify call failed (HIP / engine status): CompleteIo returns it
     int rc;
 };
@@ -352,6 +372,7 @@ struct cts_io_pattern {
     }
     virtual ~cts_io_pattern()
     {
+        EngineDevice on(engine);
         if (stream) {
             (void)hipStreamSynchronize(stream);  // kernels may still read the ring (cheap when idle)
             (void)cts_engine_stream_destroy(engine, stream);
@@ -880,6 +901,7 @@ struct cts_io_pattern {
                             slice_len, reinterpret_cast<cts_verify_result*>(one.dev + kResAt), nullptr, nullptr, 0,
                             stream);
             if (rc != CTS_OK) return rc;
+            EngineDevice on(engine);
             if (hipStreamSynchronize(stream) != hipSuccess) return CTS_E_HIP;
             r = cts::slice_merge(reinterpret_cast<const cts_verify_result*>(one.host + kResAt), ns, slice_len,
                                  transferred);
@@ -1040,6 +1062,7 @@ struct cts_io_pattern {
     }
     hipError_t SleepSyncImpl(uint32_t step_us)
     {
+        EngineDevice on(engine);
         if (retire_wait != 2 && !bounded_wait) return hipStreamSynchronize(stream);
         if (sync_done == nullptr && hipEventCreateWithFlags(&sync_done, hipEventDisableTiming) != hipSuccess) {
             sync_done = nullptr;
@@ -1052,6 +1075,7 @@ struct cts_io_pattern {
 
     hipError_t WaitInflight(hipEvent_t done)  // the kernel behind `done`
     {
+        EngineDevice on(engine);
         if (bounded_wait) return done != nullptr ? PollEvent(done, 50) : SleepSyncImpl(50);
         if (done == nullptr || retire_wait == 0) return hipStreamSynchronize(stream);
         if (retire_wait == 1) return hipEventSynchronize(done);
@@ -1120,6 +1144,7 @@ struct cts_io_pattern {
         if (queue.empty()) return GetCurrentStatus();
         const int lr = LaunchBatch();
         if (lr != CTS_OK) return lr;
+        EngineDevice on(engine);
         hipEvent_t e = nullptr;
         if (!spare_events.empty()) {
             e = spare_events.back();
@@ -1159,7 +1184,11 @@ struct cts_io_pattern {
             const int rc = LaunchBatch();
             if (rc != CTS_OK) return rc;
             const auto w0 = std::chrono::steady_clock::now();
-            const hipError_t wr = hipStreamSynchronize(stream);
+            hipError_t wr;
+            {
+                EngineDevice on(engine);
+                wr = hipStreamSynchronize(stream);
+            }
             AddVerifyWait(w0);
             if (wr != hipSuccess) return CTS_E_HIP;
             res = reinterpret_cast<const cts_verify_result*>(stage_res.host) + (size_t)desc_set * BatchCapacity();
@@ -1577,6 +1606,7 @@ struct MediaStreamClient : cts_io_pattern {
         cv.notify_all();
         if (timer_thread.joinable()) timer_thread.join();
         if (ms != nullptr) (void)cts_media_stream_client_destroy(ms);
+        EngineDevice on(engine);
         if (d_sums != nullptr) (void)hipFreeAsync(d_sums, stream);
         if (stream != nullptr) (void)hipStreamSynchronize(stream);
     }
@@ -1682,6 +1712,7 @@ struct MediaStreamClient : cts_io_pattern {
             }
             return false;
         }
+        EngineDevice on(engine);
         int rc = EnsureStream();
         if (rc == CTS_OK && ms_desc.host == nullptr) {
             const uint32_t b = BatchCapacity();
@@ -2071,7 +2102,10 @@ int cts_shared_buffer_init(cts_engine* engine, uint32_t max_buffer_size)
         return rc;
     }
     rc = cts_sender_buffer_fill(engine, d, max_buffer_size, s);
-    if (rc == CTS_OK && hipStreamSynchronize(static_cast<hipStream_t>(s)) != hipSuccess) rc = CTS_E_HIP;
+    if (rc == CTS_OK) {
+        EngineDevice on(engine);
+        if (hipStreamSynchronize(static_cast<hipStream_t>(s)) != hipSuccess) rc = CTS_E_HIP;
+    }
     (void)cts_engine_stream_destroy(engine, s);
     if (rc != CTS_OK) {
         (void)cts_host_free(engine, h);

@@ -29,10 +29,14 @@ uint64_t ora_sender_buffer_size(uint32_t max_buffer_size)
 /* ctsIOPattern.cpp:72-80: copy at most c_bufferPatternSize bytes of
  * g_bufferPattern per iteration until g_maximumBufferSize bytes are written.
  * Only the first 65536 bytes of the 131072-byte table are ever used. */
+static uint8_t g_table[ORA_PATTERN_SIZE * 2]; /* g_bufferPattern, built once (callers may run on many threads) */
+static pthread_once_t g_table_once = PTHREAD_ONCE_INIT;
+static void build_table(void) { ora_build_pattern_table(g_table); }
+
 void ora_build_sender_buffer(uint8_t* dst, uint32_t max_buffer_size)
 {
-    static uint8_t table[ORA_PATTERN_SIZE * 2];
-    ora_build_pattern_table(table);
+    pthread_once(&g_table_once, build_table);
+    const uint8_t* const table = g_table;
     uint8_t* protectedDestination = dst;
     uint64_t writeSizeRemaining = ora_sender_buffer_size(max_buffer_size);
     while (writeSizeRemaining > 0) {

@@ -10,7 +10,10 @@
 // (cts::launch_mailbox) is emulated by a host thread that polls the slot rings exactly as mailbox_kernel does
 // (tags, no-op jobs, stop jobs, the idle exit) and answers every piece with a clean part record; the event
 // recorded after it completes when that thread has left, and hipHostFree counts a violation when it would wait
-// on a running grid (the reason Pause exists). Verify launches record their device and write clean records.
+// on a running grid (the reason Pause exists). The verify and fill launches compute what the kernels do with the
+// oracle (oracle/cts_oracle.c), and the emulated grid verifies each job, so whole loopback TCP connections
+// (cts_loopback_run_multi, SYNC and DEFERRED patterns, clean and corrupt) run over eight engines: their IO threads
+// start on device 0, as new threads do, and drive patterns on every device. MediaStream patterns are not run here.
 #include <hip/hip_runtime_api.h>
 #include <pthread.h>
 #include <time.h>
@@ -29,7 +32,9 @@
 
 #include "cts_engine.h"
 #include "cts_internal.hpp"
+#include "cts_loopback.h"
 #include "cts_media_stream.h"
+#include "cts_oracle.h"
 
 namespace {
 
@@ -245,6 +250,23 @@ hipError_t hipMemcpyAsync(void* dst, const void* src, size_t bytes, hipMemcpyKin
     std::memcpy(dst, src, bytes);
     return hipSuccess;
 }
+hipError_t hipMallocAsync(void** p, size_t bytes, hipStream_t s)
+{
+    check_stream("hipMallocAsync", s);
+    *p = std::calloc(1, bytes);
+    return *p ? hipSuccess : hipErrorOutOfMemory;
+}
+hipError_t hipFreeAsync(void* p, hipStream_t s)
+{
+    check_stream("hipFreeAsync", s);
+    std::free(p);
+    return hipSuccess;
+}
+hipError_t hipEventSynchronize(hipEvent_t e)
+{
+    while (hipEventQuery(e) == hipErrorNotReady) std::this_thread::sleep_for(std::chrono::microseconds(20));
+    return hipSuccess;
+}
 
 // std::condition_variable::wait_for (the mailbox watchdog) waits in pthread_cond_clockwait, which this
 // toolchain's ThreadSanitizer does not intercept: it would miss the wait's unlock and report a double lock. The
@@ -275,29 +297,40 @@ void launched(const char* what, hipStream_t s)
     g_launches[stream_of(s)->device].fetch_add(1);
 }
 
-void clean(cts_verify_result* r, const cts_buf_desc* d, uint32_t n)
-{
-    if (r == nullptr) return;
-    for (uint32_t i = 0; i < n; ++i) r[i] = cts_verify_result{d[i].length, 0, 0, 0, 1, 0};
-}
+static_assert(sizeof(ora_desc) == sizeof(cts_buf_desc) && sizeof(ora_result) == sizeof(cts_verify_result),
+              "the oracle's records are the ABI's");
 
 }  // namespace
 
-hipError_t launch_fill(uint8_t*, uint64_t, const cts_buf_desc*, uint32_t, uint32_t, hipStream_t s, const LaunchGeometry&)
+hipError_t launch_fill(uint8_t* arena, uint64_t bytes, const cts_buf_desc* d, uint32_t n, uint32_t, hipStream_t s,
+                       const LaunchGeometry&)
 {
     launched("launch_fill", s);
+    ora_fill(arena, bytes, reinterpret_cast<const ora_desc*>(d), n);
     return hipSuccess;
 }
-hipError_t launch_fill_span(uint8_t*, uint64_t, uint32_t, hipStream_t s, const LaunchGeometry&)
+hipError_t launch_fill_span(uint8_t* dst, uint64_t bytes, uint32_t pattern_offset, hipStream_t s, const LaunchGeometry&)
 {
     launched("launch_fill_span", s);
+    for (uint64_t i = 0; i < bytes; ++i) dst[i] = ora_pattern_byte(pattern_offset + i);
     return hipSuccess;
 }
-hipError_t launch_verify(const uint8_t*, uint64_t, const cts_buf_desc* d, uint32_t n, uint32_t, cts_verify_result* r,
-                         uint64_t*, uint32_t*, uint32_t, hipStream_t s, const LaunchGeometry&)
+hipError_t launch_verify(const uint8_t* arena, uint64_t bytes, const cts_buf_desc* d, uint32_t n, uint32_t,
+                         cts_verify_result* r, uint64_t* counters, uint32_t* first_fail, uint32_t n_conns,
+                         hipStream_t s, const LaunchGeometry&)
 {
     launched("launch_verify", s);
-    clean(r, d, n);
+    ora_counters c{};
+    if (ora_verify_batch(arena, bytes, reinterpret_cast<const ora_desc*>(d), n, reinterpret_cast<ora_result*>(r), &c,
+                         first_fail, n_conns, 1) != 0)
+        return hipErrorInvalidValue;
+    if (counters != nullptr) {  // (shard 0 of the device block)
+        counters[kBytesChecked] += c.bytes_checked;
+        counters[kBytesOk] += c.bytes_ok;
+        counters[kBuffersChecked] += c.buffers_checked;
+        counters[kBuffersFailed] += c.buffers_failed;
+        counters[kMismatchedBytes] += c.mismatched_bytes;
+    }
     return hipSuccess;
 }
 hipError_t launch_verify_strided(const uint8_t*, uint64_t, uint32_t, const uint32_t*, uint32_t, uint32_t, uint32_t,
@@ -379,11 +412,28 @@ hipError_t launch_mailbox(const MailSlot* slots, MailPart* parts, uint32_t per_g
                     progress = true;
                     since[g] = clock::now();
                     if (len == kMailSkip) continue;
-                    const uint32_t np = mail_parts(pe & 0xFFFFFFFFFFFFull, len);
+                    const uint64_t ptr = pe & 0xFFFFFFFFFFFFull;
+                    const uint32_t np = mail_parts(ptr, len);
+                    // the job verified whole; part 0 carries its first mismatch and count, the others answer clean
+                    uint32_t first = 0xFFFFFFFFu, count = 0, actual = 0;
+                    const uint8_t* b = reinterpret_cast<const uint8_t*>(ptr);
+                    for (uint32_t x = 0; len != 0 && x < len; ++x)
+                        if (b[x] != ora_pattern_byte((pe >> 48) + x)) {
+                            if (first == 0xFFFFFFFFu) {
+                                first = x;
+                                actual = b[x];
+                            }
+                            ++count;
+                        }
                     for (uint32_t i = 0; i < np; ++i) {
                         MailPart* p = parts + (size_t)k * kMailGroup + i;
-                        __atomic_store_n(&p->g0, 0xFFFFFFFFull | ((uint64_t)tag << 32), __ATOMIC_RELEASE);
-                        __atomic_store_n(&p->g1, (uint64_t)(tag & 0xFFFFFFu) << 40, __ATOMIC_RELEASE);
+                        const bool mine = i == 0 && count != 0;
+                        __atomic_store_n(&p->g0, (mine ? first : 0xFFFFFFFFull) | ((uint64_t)tag << 32),
+                                         __ATOMIC_RELEASE);
+                        __atomic_store_n(&p->g1,
+                                         (mine ? (uint64_t)count | ((uint64_t)actual << 32) : 0) |
+                                             ((uint64_t)(tag & 0xFFFFFFu) << 40),
+                                         __ATOMIC_RELEASE);
                     }
                     if (len == 0) {
                         live[g] = false;
@@ -418,6 +468,7 @@ hipError_t launch_mailbox(const MailSlot* slots, MailPart* parts, uint32_t per_g
 namespace {
 
 int g_fail = 0;
+std::vector<uint8_t> g_S;  // g_senderSharedBuffer for 1 MiB buffers: S[k + b] is the pattern byte at offset k + b
 #define CHECK(c)                                                               \
     do {                                                                       \
         if (!(c)) {                                                            \
@@ -431,9 +482,10 @@ int g_fail = 0;
 void drive(cts_engine* e, int dev, int home, int rounds)
 {
     CHECK(hipSetDevice(home) == hipSuccess);
-    alignas(64) static thread_local uint8_t arena[1 << 16];
+    alignas(64) static thread_local uint8_t arena[1 << 18];
     alignas(64) static thread_local uint64_t block[CTS_COUNTER_SHARDS * 8];
-    alignas(64) static thread_local uint8_t host[70000];
+    alignas(64) static thread_local uint8_t bad[70000];
+    const uint8_t* const S = g_S.data();
     cts_buf_desc d[2] = {{0, 4096, 0, 0, 0}, {4096, 1472, 7, 1, 0}};
     cts_verify_result r[2];
     uint32_t lens[2] = {1472, 1472}, first_fail[2] = {0, 0};
@@ -463,12 +515,16 @@ void drive(cts_engine* e, int dev, int home, int rounds)
         here("counters_reset");
         CHECK(cts_fill(e, arena, sizeof(arena), d, 2, 4096, s) == CTS_OK);
         here("fill");
-        CHECK(cts_sender_buffer_fill(e, arena, 1024, s) == CTS_OK);
+        CHECK(cts_sender_buffer_fill(e, arena + (1 << 17), 1024, s) == CTS_OK);
         here("sender_buffer_fill");
+        CHECK(std::memcmp(arena + (1 << 17), S, 65536 + 1024) == 0);
         CHECK(cts_verify(e, arena, sizeof(arena), d, 2, 4096, r, block, first_fail, 2, s) == CTS_OK);
         here("verify");
+        CHECK(r[0].pass == 1 && r[1].pass == 1 && r[1].first_mismatch == 1472);
+        arena[4096 + 1000] ^= 0x40;
         CHECK(cts_verify(e, arena, sizeof(arena), d, 2, 4096, r, block, first_fail, 2, nullptr) == CTS_OK);  // null stream
         here("verify (null stream)");
+        CHECK(r[0].pass == 1 && r[1].pass == 0 && r[1].first_mismatch == 1000 && r[1].mismatch_bytes == 1);
         CHECK(cts_verify_strided(e, arena, sizeof(arena), 2048, lens, 2, 0, 0, 0, r, block, first_fail, 2, s) == CTS_OK);
         here("verify_strided");
         CHECK(cts_media_stream_fill(e, arena, sizeof(arena), d, hd, 2, s) == CTS_OK);
@@ -491,34 +547,44 @@ void drive(cts_engine* e, int dev, int home, int rounds)
         CHECK(g_launches[dev].load() - before >= 13);
         CHECK(cts_counters_read(e, block, &c, s) == CTS_OK);
         here("counters_read");
+        CHECK(c.buffers_checked == 4 && c.buffers_failed == 1 && c.mismatched_bytes == 1);
         // the host paths: one-buffer verifies (the mailbox, and the launch path), a batch, pinned memory
         for (int k = 0; k < 4; ++k) {
             cts_verify_result hr{};
             const uint32_t len = k == 3 ? 70000u : 1024u << k;
-            CHECK(cts_verify_host(e, host, len, (uint32_t)k, &hr) == CTS_OK);
+            CHECK(cts_verify_host(e, S + k, len, (uint32_t)k, &hr) == CTS_OK);
             here("verify_host");
             CHECK(hr.pass == 1 && hr.first_mismatch == len);
+            std::memcpy(bad, S + k, len);
+            bad[len - 1 - (uint32_t)it] ^= 0x01;
+            CHECK(cts_verify_host(e, bad, len, (uint32_t)k, &hr) == CTS_OK);
+            here("verify_host (corrupt)");
+            CHECK(hr.pass == 0 && hr.first_mismatch == len - 1 - (uint32_t)it && hr.mismatch_bytes == 1 &&
+                  hr.actual == (S[k + len - 1 - it] ^ 0x01) && hr.expected == S[k + len - 1 - it]);
         }
         void* hp = nullptr;
         void* dv = nullptr;
         CHECK(cts_host_alloc(e, 4096, &hp, &dv) == CTS_OK);
         here("host_alloc");
+        if (hp != nullptr) std::memcpy(hp, S + 5, 4000);
         cts_verify_result mr{};
         CHECK(cts_verify_mapped(e, dv, 4000, 5, &mr) == CTS_OK && mr.pass == 1);
         here("verify_mapped");
         CHECK(cts_host_free(e, hp) == CTS_OK);  // stops this engine's grid first
         here("host_free");
-        const void* bufs[2] = {host, host + 100};
+        const void* bufs[2] = {S, S + 100};
         const uint32_t blens[2] = {100, 3000}, exp[2] = {0, 100};
         cts_verify_result br[2];
         cts_counters bc{};
         CHECK(cts_verify_host_batch(e, bufs, blens, exp, nullptr, 2, br, &bc) == CTS_OK);
         here("verify_host_batch");
+        CHECK(br[0].pass == 1 && br[1].pass == 1 && bc.buffers_checked == 2 && bc.bytes_ok == 3100);
         int prev = cts_engine_set_attr(e, CTS_ATTR_SYNC_MAILBOX, 0);
         CHECK(prev == CTS_OK);
         cts_verify_result lr{};
-        CHECK(cts_verify_host(e, host, 9000, 3, &lr) == CTS_OK);
+        CHECK(cts_verify_host(e, S + 3, 9000, 3, &lr) == CTS_OK);
         here("verify_host (launch path)");
+        CHECK(lr.pass == 1 && lr.first_mismatch == 9000);
         CHECK(cts_engine_set_attr(e, CTS_ATTR_SYNC_MAILBOX, 1) == CTS_OK);
     }
     CHECK(cts_engine_numa_node(e) == -1);
@@ -532,6 +598,8 @@ void drive(cts_engine* e, int dev, int home, int rounds)
 int main()
 {
     std::setvbuf(stdout, nullptr, _IONBF, 0);
+    g_S.resize(ora_sender_buffer_size(1u << 20));
+    ora_build_sender_buffer(g_S.data(), 1u << 20);
     // grids stay up between posts (no watchdog stop for 10 s): every pinned free below meets running grids
     setenv("CTS_MAILBOX_IDLE_MS", "10000", 1);
     // engines on every device, created from a thread whose device is 3
@@ -555,11 +623,10 @@ int main()
     // a staging buffer that grows on engine 2 from a thread whose device (1) runs engine 1's grid: the old
     // buffer's free must happen on device 2, with device 2's grids stopped, not on the caller's device
     {
-        static uint8_t big[1 << 20];
         cts_verify_result r{};
-        CHECK(cts_verify_mapped(eng[1], eng[1] ? (const void*)big : nullptr, 4096, 0, &r) == CTS_OK);  // device 1 busy
+        CHECK(cts_verify_mapped(eng[1], eng[1] ? (const void*)g_S.data() : nullptr, 4096, 0, &r) == CTS_OK);  // device 1 busy
         CHECK(hipSetDevice(1) == hipSuccess);
-        CHECK(cts_verify_host(eng[2], big, sizeof(big) - 64, 9, &r) == CTS_OK && r.pass == 1);
+        CHECK(cts_verify_host(eng[2], g_S.data() + 9, (1u << 20) - 64, 9, &r) == CTS_OK && r.pass == 1);
         (void)hipGetDevice(&cur);
         CHECK(cur == 1);
         CHECK(hipSetDevice(3) == hipSuccess);
@@ -573,14 +640,49 @@ int main()
     for (auto& t : ts) t.join();
     std::printf("threads: %d grids, violations %d\n", g_grids.load(), g_violations.load());
 
+    // whole loopback TCP connections over the eight engines (connection i on engine cts_shard_of(i, 8)): the feeder's
+    // side threads start on device 0 and drive SYNC (the mailbox) and DEFERRED (batches, events) patterns on every
+    // device; the wire corruption of one connection must fail exactly that connection
+    struct Run {
+        uint32_t pattern, mode, corrupt;
+    };
+    for (const Run& run : {Run{CTS_PATTERN_PUSH, CTS_VERIFY_DEFERRED, 0}, Run{CTS_PATTERN_PULL, CTS_VERIFY_SYNC, 0},
+                           Run{CTS_PATTERN_PUSH, CTS_VERIFY_SYNC, 1}, Run{CTS_PATTERN_PULL, CTS_VERIFY_DEFERRED, 1}}) {
+        cts_loopback_config cfg{};
+        cfg.connections = 16;
+        cfg.io_pattern = run.pattern;
+        cfg.buffer_size = 65536;
+        cfg.verify_buffers = 1;
+        cfg.transfer_size = (2u << 20) + 12345;
+        cfg.verify_mode = run.mode;
+        cfg.batch_buffers = 8;
+        cfg.corrupt_connection = run.corrupt ? 5u : ~0u;
+        cfg.corrupt_send_index = 11;
+        cfg.recv_whole = 1;
+        cts_loopback_result out{};
+        CHECK(cts_loopback_run_multi(&cfg, eng, kDevices, nullptr, nullptr, &out) == CTS_OK);
+        (void)hipGetDevice(&cur);
+        CHECK(cur == 3);
+        if (run.corrupt)
+            CHECK(out.connections_ok == 15 && out.connections_failed == 1 && out.data_errors == 1);
+        else
+            CHECK(out.connections_ok == 16 && out.connections_failed == 0 && out.data_errors == 0 &&
+                  out.buffers_verified == 16 * 33);
+        std::printf("loopback pattern %u mode %u corrupt %u: ok %u failed %u data errors %u verified %llu\n",
+                    run.pattern, run.mode, run.corrupt, out.connections_ok, out.connections_failed, out.data_errors,
+                    (unsigned long long)out.buffers_verified);
+    }
+    cts_shared_buffer_release();
+    std::printf("loopback: %d grids, violations %d\n", g_grids.load(), g_violations.load());
+
     // an idle engine's watchdog stops its grid from its own thread (no device current there but its own guard)
     setenv("CTS_MAILBOX_IDLE_MS", "20", 1);
     cts_engine* idle = nullptr;
     CHECK(cts_engine_create(6, &idle) == CTS_OK);
     {
-        static uint8_t buf[8192];
         cts_verify_result r{};
-        CHECK(cts_verify_mapped(idle, idle ? (const void*)buf : nullptr, 8192, 1, &r) == CTS_OK && r.pass == 1);
+        CHECK(cts_verify_mapped(idle, idle ? (const void*)(g_S.data() + 1) : nullptr, 8192, 1, &r) == CTS_OK &&
+              r.pass == 1);
         std::shared_ptr<std::atomic<bool>> last;
         {
             std::lock_guard<std::mutex> lk(g_grid_mu);

@@ -11,6 +11,7 @@ on threads at once feeding the process-wide UDP counters (tests/cpp/media_stream
 AddressSanitizer + UndefinedBehaviorSanitizer, and ThreadSanitizer (the async functor's send and
 recv threads share one pattern under the connection lock). Any report fails the test.
 """
+import concurrent.futures
 import os
 import subprocess
 import tempfile
@@ -74,23 +75,31 @@ def test_host_code_under_sanitizer(san, driver):
 
 @pytest.mark.parametrize("san", sorted(set(SAN) - {"plain"}))
 def test_engine_abi_on_eight_fake_devices(san):
-    """The engine's C ABI (cts_engine.cpp) on a fake eight-device HIP runtime (tests/cpp/engine_devices.cpp): engines
-    on devices 0-7 plus a second one on device 5, driven from threads whose own device differs, one after the other and
-    all at once. Every stream-ordered HIP call and launch must run with the engine's device current, the caller's
-    device must be current again afterwards, and no pinned free may run while a SYNC mailbox grid (emulated by a host
-    thread that polls the slot rings as mailbox_kernel does) is resident on the current device: hipHostFree is an
-    implicit hipDeviceSynchronize. The one-GPU test box never runs an engine on a device other than 0."""
+    """The engine's C ABI (cts_engine.cpp) and the host half above it on a fake eight-device HIP runtime
+    (tests/cpp/engine_devices.cpp): engines on devices 0-7 plus a second one on device 5, driven from threads whose own
+    device differs, one after the other and all at once, then whole loopback TCP connections (Push/Pull, SYNC/DEFERRED,
+    clean and corrupt) spread over the eight engines from feeder threads that start on device 0. Every stream-ordered
+    HIP call and launch must run with its engine's device current, every event must be recorded on a stream of its own
+    device, the caller's device must be current again afterwards, and no pinned free may run while a SYNC mailbox grid
+    (emulated by a host thread that polls the slot rings as mailbox_kernel does) is resident on the current device:
+    hipHostFree is an implicit hipDeviceSynchronize. Launches compute with the oracle, so verdicts are checked too.
+    The one-GPU test box never runs an engine on a device other than 0."""
     flags = ["-g", "-O1", "-fno-omit-frame-pointer", "-pthread"] + SAN[san]
     inc = ["-I", os.path.join(ROOT, "include"), "-I", os.path.join(ROOT, "ctstraffic_amd", "csrc"),
-           "-I", "/opt/rocm/include", "-D__HIP_PLATFORM_AMD__"]
+           "-I", os.path.join(ROOT, "oracle"), "-I", "/opt/rocm/include", "-D__HIP_PLATFORM_AMD__"]
+    srcs = [os.path.join(ROOT, "ctstraffic_amd", "csrc", x) for x in (
+        "cts_engine.cpp", "cts_host_util.cpp", "cts_pattern.cpp", "cts_media_stream.cpp", "cts_status.cpp",
+        "cts_loopback.cpp", "cts_loopback_udp.cpp")] + [os.path.join(ROOT, "tests", "cpp", "engine_devices.cpp")]
     with tempfile.TemporaryDirectory() as d:
-        objs = []
-        for src in [os.path.join(ROOT, "ctstraffic_amd", "csrc", "cts_engine.cpp"),
-                    os.path.join(ROOT, "ctstraffic_amd", "csrc", "cts_host_util.cpp"),
-                    os.path.join(ROOT, "tests", "cpp", "engine_devices.cpp")]:
-            o = os.path.join(d, os.path.basename(src) + ".o")
-            subprocess.run(["g++", "-std=c++17", *flags, *inc, "-c", src, "-o", o], check=True)
-            objs.append(o)
+        objs = [os.path.join(d, os.path.basename(src) + ".o") for src in srcs]
+        with concurrent.futures.ThreadPoolExecutor(4) as pool:  # (the pattern mirror alone takes ~30 s under a sanitizer)
+            for f in [pool.submit(subprocess.run, ["g++", "-std=c++17", *flags, *inc, "-c", src, "-o", o], check=True)
+                      for src, o in zip(srcs, objs)]:
+                f.result()
+        o = os.path.join(d, "cts_oracle.o")
+        subprocess.run(["gcc", "-std=c11", *flags, "-I", os.path.join(ROOT, "oracle"), "-c",
+                        os.path.join(ROOT, "oracle", "cts_oracle.c"), "-o", o], check=True)
+        objs.append(o)
         exe = os.path.join(d, "engine_devices")
         subprocess.run(["g++", *flags, *objs, "-o", exe, "-ldl"], check=True)
         out = subprocess.run([exe], capture_output=True, text=True, timeout=300, env={**os.environ, **ENV})

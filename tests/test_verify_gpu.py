@@ -871,6 +871,55 @@ def test_host_free_while_posting(engine):
     assert max(frees) < 0.5, frees
 
 
+def test_host_free_while_another_engine_posts(engine):
+    """hipHostFree is an implicit hipDeviceSynchronize: a second engine's resident grid on the same GPU, kept alive by
+    a thread posting to it back to back, would hold a free on the first engine up for as long as the posts go on
+    (round 4 paused only the freeing engine's own grid). A free now stops every engine's grid on the device, so each
+    returns quickly, and both engines' verifies (the posting one's and a growing staging buffer's) stay exact."""
+    import threading
+    import time
+
+    from ctstraffic_amd import Engine
+
+    S = oracle.sender_buffer(300000)
+    other = Engine(0)
+    arr, h, dev = other.host_alloc(65536 + 64)
+    stop = threading.Event()
+    errors = []
+
+    def poster():
+        k = 0
+        while not stop.is_set():
+            if not _mapped_check(other, arr, dev, S, 65536, (17 * k) % 65536, flip=(k if k % 5 == 0 else None)):
+                errors.append(k)
+            k += 1
+
+    th = threading.Thread(target=poster)
+    th.start()
+    frees = []
+    try:
+        time.sleep(0.1)
+        for i in range(6):
+            _, hh, _ = engine.host_alloc(1 << 20)
+            t0 = time.monotonic()
+            engine.host_free(hh)
+            frees.append(time.monotonic() - t0)
+            # the first engine's own staging buffer grows (its old one is freed the same way)
+            n = 70000 + 40000 * i
+            buf = S[3:3 + n].copy()
+            buf[n // 2] ^= 0x11
+            r = engine.verify_host(buf, 3)
+            assert (r["pass"], r["first_mismatch"], r["mismatch_bytes"]) == (False, n // 2, 1)
+            time.sleep(0.05)
+    finally:
+        stop.set()
+        th.join()
+        other.host_free(h)
+        other.close()
+    assert not errors, errors[:5]
+    assert max(frees) < 0.5, frees
+
+
 def test_verify_mapped_mailbox_restarts_after_idle(engine):
     """The mailbox grid stops after CTS_MAILBOX_IDLE_MS (50 ms) without posts and the next post starts it again;
     answers stay exact across the restart, including an HBM buffer and a buffer larger than the grid's
