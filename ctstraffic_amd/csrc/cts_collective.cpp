@@ -100,7 +100,7 @@ void destroy_clique(Clique& c)
         if (c.comms[k] != nullptr) (void)g_rccl.comm_destroy(c.comms[k]);
         if (c.sums[k] != nullptr) {
             DeviceGuard g(c.devices[k]);
-            (void)hipFree(c.sums[k]);
+            (void)hipFreeAsync(c.sums[k], nullptr);  // stream-ordered: hipFree would wait for every kernel on the device
         }
     }
     c.comms.clear();
@@ -123,11 +123,17 @@ int clique_for(const std::vector<int>& devices, Clique** out)
     for (size_t k = 0; k < devices.size(); ++k) {
         DeviceGuard g(devices[k]);
         void* p = nullptr;
-        if (!g.ok || hipMalloc(&p, 5 * sizeof(uint64_t)) != hipSuccess) {
+        // on the device's null stream, which the engines' non-blocking streams never wait for; the caller's
+        // leading stream uses the slot only after the synchronize below
+        if (!g.ok || hipMallocAsync(&p, 5 * sizeof(uint64_t), nullptr) != hipSuccess) {
             destroy_clique(*c);
             return g.ok ? CTS_E_NOMEM : CTS_E_HIP;
         }
         c->sums[k] = static_cast<uint64_t*>(p);
+        if (hipStreamSynchronize(nullptr) != hipSuccess) {
+            destroy_clique(*c);
+            return CTS_E_HIP;
+        }
     }
     int prev = -1;
     (void)hipGetDevice(&prev);

@@ -51,15 +51,18 @@ hipError_t hipSetDevice(int d)
     t_cur = d;
     return hipSuccess;
 }
-hipError_t hipMalloc(void** p, size_t bytes)
+// the clique's slots are stream-ordered on the device's null stream (a plain hipFree would synchronize the device)
+hipError_t hipMallocAsync(void** p, size_t bytes, hipStream_t s)
 {
+    if (s != nullptr) return hipErrorInvalidValue;
     *p = std::calloc(1, bytes);
     std::lock_guard<std::mutex> lk(g_mu);
     g_alloc_dev[*p] = t_cur;
     return *p ? hipSuccess : hipErrorOutOfMemory;
 }
-hipError_t hipFree(void* p)
+hipError_t hipFreeAsync(void* p, hipStream_t s)
 {
+    if (s != nullptr) return hipErrorInvalidValue;
     {
         std::lock_guard<std::mutex> lk(g_mu);
         auto it = g_alloc_dev.find(p);
