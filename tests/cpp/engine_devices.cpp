@@ -13,7 +13,8 @@
 // on a running grid (the reason Pause exists). The verify and fill launches compute what the kernels do with the
 // oracle (oracle/cts_oracle.c), and the emulated grid verifies each job, so whole loopback TCP connections
 // (cts_loopback_run_multi, SYNC and DEFERRED patterns, clean and corrupt) run over eight engines: their IO threads
-// start on device 0, as new threads do, and drive patterns on every device. MediaStream patterns are not run here.
+// start on device 0, as new threads do, and drive patterns on every device, and MediaStream connections in SYNC mode
+// (DEFERRED's frame-sum receive pass is not emulated).
 #include <hip/hip_runtime_api.h>
 #include <pthread.h>
 #include <time.h>
@@ -671,6 +672,31 @@ int main()
         std::printf("loopback pattern %u mode %u corrupt %u: ok %u failed %u data errors %u verified %llu\n",
                     run.pattern, run.mode, run.corrupt, out.connections_ok, out.connections_failed, out.data_errors,
                     (unsigned long long)out.buffers_verified);
+    }
+    // MediaStream over loopback UDP on engine 6, SYNC (one verify per datagram; the client's timer thread starts on
+    // device 0 and renders frames and flushes through the pattern). DEFERRED's frame-sum pass is not emulated.
+    for (uint32_t corrupt = 0; corrupt < 2; ++corrupt) {
+        cts_media_stream_loopback_config mc{};
+        mc.connections = 2;
+        mc.frame_size_bytes = 3000;
+        mc.frames_per_second = 100;
+        mc.stream_length_frames = 30;
+        mc.buffered_frames = 15;
+        mc.verify_buffers = 1;
+        mc.corrupt_connection = corrupt ? 1u : ~0u;
+        mc.corrupt_datagram = 20;
+        mc.verify_mode = CTS_VERIFY_SYNC;
+        cts_media_stream_loopback_result mo{};
+        CHECK(cts_loopback_media_stream_run(&mc, eng[6], nullptr, nullptr, &mo) == CTS_OK);
+        (void)hipGetDevice(&cur);
+        CHECK(cur == 3);
+        if (corrupt)
+            CHECK(mo.connections_ok == 1 && mo.connections_failed == 1 && mo.data_errors == 1);
+        else
+            CHECK(mo.connections_ok == 2 && mo.connections_failed == 0 && mo.data_errors == 0);
+        std::printf("media stream corrupt %u: ok %u failed %u data errors %u datagrams %llu\n", corrupt,
+                    mo.connections_ok, mo.connections_failed, mo.data_errors,
+                    (unsigned long long)mo.datagrams_received);
     }
     cts_shared_buffer_release();
     std::printf("loopback: %d grids, violations %d\n", g_grids.load(), g_violations.load());
