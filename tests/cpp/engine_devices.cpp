@@ -13,12 +13,13 @@
 // on a running grid (the reason Pause exists). The verify and fill launches compute what the kernels do with the
 // oracle (oracle/cts_oracle.c), and the emulated grid verifies each job, so whole loopback TCP connections
 // (cts_loopback_run_multi, SYNC and DEFERRED patterns, clean and corrupt) run over eight engines: their IO threads
-// start on device 0, as new threads do, and drive patterns on every device, and MediaStream connections in SYNC mode
-// (DEFERRED's frame-sum receive pass is not emulated).
+// start on device 0, as new threads do, and drive patterns on every device, and MediaStream connections (SYNC, and
+// DEFERRED through an emulated frame-sum pass) with their client timer threads on device 0.
 #include <hip/hip_runtime_api.h>
 #include <pthread.h>
 #include <time.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cstdint>
@@ -366,17 +367,80 @@ hipError_t launch_media_stream_verify_strided(const uint8_t*, uint64_t, uint32_t
     launched("launch_media_stream_verify_strided", s);
     return hipSuccess;
 }
-hipError_t launch_media_stream_status(const uint8_t*, uint64_t, const cts_buf_desc*, const uint32_t*, uint32_t,
-                                      uint32_t, cts_datagram_status*, uint64_t*, hipStream_t s, const LaunchGeometry&)
+// One received datagram as media_stream_verify_quad_kernel reads it (ValidateBufferLengthFromTask, the payload
+// verify after the 26-byte header at pattern offset 0).
+struct MsDatagram {
+    uint32_t kind = CTS_DGRAM_BAD_DESC, completed = 0;
+    uint16_t flag = 0;
+    int64_t seq = 0;
+    bool clean = false;
+};
+MsDatagram ms_read(const uint8_t* arena, uint64_t bytes, const cts_buf_desc* descs, const uint32_t* lengths,
+                   uint32_t stride, uint32_t i)
+{
+    MsDatagram m;
+    const uint64_t off = descs ? descs[i].byte_offset : (uint64_t)i * stride;
+    m.completed = descs ? descs[i].length : lengths[i];
+    if (off > bytes || bytes - off < m.completed || (!descs && m.completed > stride)) return m;
+    const uint8_t* b = arena + off;
+    if (m.completed == 0) {
+        m.kind = CTS_DGRAM_ZERO;
+    } else if (m.completed < CTS_UDP_FLAG_LENGTH) {
+        m.kind = CTS_DGRAM_SHORT;
+    } else {
+        std::memcpy(&m.flag, b, 2);
+        if (m.flag == CTS_UDP_FLAG_DATA)
+            m.kind = m.completed < CTS_UDP_DATA_HEADER_LENGTH ? CTS_DGRAM_SHORT : CTS_DGRAM_DATA;
+        else if (m.flag == CTS_UDP_FLAG_ID)
+            m.kind = m.completed < CTS_UDP_CONNECTION_ID_HEADER_LENGTH ? CTS_DGRAM_SHORT : CTS_DGRAM_ID;
+        else
+            m.kind = CTS_DGRAM_UNKNOWN;
+    }
+    if (m.kind == CTS_DGRAM_DATA) {
+        std::memcpy(&m.seq, b + 2, 8);
+        m.clean = true;
+        for (uint32_t x = CTS_UDP_DATA_HEADER_LENGTH; x < m.completed && m.clean; ++x)
+            m.clean = b[x] == ora_pattern_byte(x - CTS_UDP_DATA_HEADER_LENGTH);
+    }
+    return m;
+}
+
+hipError_t launch_media_stream_status(const uint8_t* arena, uint64_t bytes, const cts_buf_desc* descs,
+                                      const uint32_t* lengths, uint32_t stride, uint32_t n, cts_datagram_status* st,
+                                      uint64_t*, hipStream_t s, const LaunchGeometry&)
 {
     launched("launch_media_stream_status", s);
+    for (uint32_t i = 0; st != nullptr && i < n; ++i) {
+        const MsDatagram m = ms_read(arena, bytes, descs, lengths, stride, i);
+        st[i] = cts_datagram_status{m.kind == CTS_DGRAM_DATA ? m.seq : 0, m.completed, m.flag, (uint8_t)m.kind,
+                                    (uint8_t)(m.clean ? 1 : 0)};
+    }
     return hipSuccess;
 }
-hipError_t launch_media_stream_frames(const uint8_t*, uint64_t, const cts_buf_desc*, const uint32_t*, uint32_t,
-                                      uint32_t, const cts_frame_window&, uint64_t*, uint64_t*, uint64_t*,
-                                      hipStream_t s, const LaunchGeometry&)
+// the frame sums of media_stream_verify_quad_kernel<FRAMES>, all in shard 0
+hipError_t launch_media_stream_frames(const uint8_t* arena, uint64_t bytes, const cts_buf_desc* descs,
+                                      const uint32_t* lengths, uint32_t stride, uint32_t n, const cts_frame_window& w,
+                                      uint64_t* totals, uint64_t* frame_bytes, uint64_t*, hipStream_t s,
+                                      const LaunchGeometry&)
 {
     launched("launch_media_stream_frames", s);
+    std::memset(totals, 0, cts_frame_totals_device_bytes());
+    if (w.frames) std::memset(frame_bytes, 0, sizeof(uint64_t) * w.frames);
+    uint32_t inv_first = 0, exc = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const MsDatagram m = ms_read(arena, bytes, descs, lengths, stride, i);
+        if (m.kind == CTS_DGRAM_DATA && m.clean) {
+            totals[0] += (uint64_t)m.completed * 8u;
+            totals[2] += 1;
+            const uint64_t k = (uint64_t)m.seq - (uint64_t)w.head_sequence_number;
+            if (m.seq > w.final_frame || m.seq < w.head_sequence_number || k >= w.frames) totals[1] += 1;
+            else frame_bytes[k] += m.completed;
+        } else if (!(m.kind == CTS_DGRAM_ZERO && w.finished)) {
+            ++exc;
+            inv_first = std::max(inv_first, ~i);
+        }
+    }
+    totals[3] = (uint64_t)inv_first | ((uint64_t)exc << 32);
     return hipSuccess;
 }
 
@@ -673,9 +737,10 @@ int main()
                     run.pattern, run.mode, run.corrupt, out.connections_ok, out.connections_failed, out.data_errors,
                     (unsigned long long)out.buffers_verified);
     }
-    // MediaStream over loopback UDP on engine 6, SYNC (one verify per datagram; the client's timer thread starts on
-    // device 0 and renders frames and flushes through the pattern). DEFERRED's frame-sum pass is not emulated.
-    for (uint32_t corrupt = 0; corrupt < 2; ++corrupt) {
+    // MediaStream over loopback UDP on engine 6, SYNC (one verify per datagram) and DEFERRED (the frame-sum pass
+    // flushed at every render tick): the client's timer thread starts on device 0 and flushes through the pattern
+    for (uint32_t run = 0; run < 4; ++run) {
+        const uint32_t corrupt = run & 1u, mode = run < 2 ? CTS_VERIFY_SYNC : CTS_VERIFY_DEFERRED;
         cts_media_stream_loopback_config mc{};
         mc.connections = 2;
         mc.frame_size_bytes = 3000;
@@ -685,7 +750,8 @@ int main()
         mc.verify_buffers = 1;
         mc.corrupt_connection = corrupt ? 1u : ~0u;
         mc.corrupt_datagram = 20;
-        mc.verify_mode = CTS_VERIFY_SYNC;
+        mc.verify_mode = mode;
+        mc.batch_buffers = 16;
         cts_media_stream_loopback_result mo{};
         CHECK(cts_loopback_media_stream_run(&mc, eng[6], nullptr, nullptr, &mo) == CTS_OK);
         (void)hipGetDevice(&cur);
@@ -694,7 +760,7 @@ int main()
             CHECK(mo.connections_ok == 1 && mo.connections_failed == 1 && mo.data_errors == 1);
         else
             CHECK(mo.connections_ok == 2 && mo.connections_failed == 0 && mo.data_errors == 0);
-        std::printf("media stream corrupt %u: ok %u failed %u data errors %u datagrams %llu\n", corrupt,
+        std::printf("media stream mode %u corrupt %u: ok %u failed %u data errors %u datagrams %llu\n", mode, corrupt,
                     mo.connections_ok, mo.connections_failed, mo.data_errors,
                     (unsigned long long)mo.datagrams_received);
     }
