@@ -78,11 +78,11 @@ def test_engine_abi_on_eight_fake_devices(san):
     """The engine's C ABI (cts_engine.cpp) and the host half above it on a fake eight-device HIP runtime
     (tests/cpp/engine_devices.cpp): engines on devices 0-7 plus a second one on device 5, driven from threads whose own
     device differs, one after the other and all at once, then whole loopback TCP connections (Push/Pull, SYNC/DEFERRED,
-    clean and corrupt) spread over the eight engines from feeder threads that start on device 0, and MediaStream
+    clean and corrupt; PushPull; Duplex on the async functor) spread over the eight engines from feeder threads that start on device 0, and MediaStream
     connections (SYNC, and DEFERRED through an emulated frame-sum pass) on device 6 with the client timer thread on
     device 0. Every stream-ordered
     HIP call and launch must run with its engine's device current, every event must be recorded on a stream of its own
-    device, the caller's device must be current again afterwards, and no pinned free may run while a SYNC mailbox grid
+    device, the caller's device must be current again afterwards (PushPull and Duplex on the async functor too), and no pinned free may run while a SYNC mailbox grid
     (emulated by a host thread that polls the slot rings as mailbox_kernel does) is resident on the current device:
     hipHostFree is an implicit hipDeviceSynchronize. Launches compute with the oracle, so verdicts are checked too.
     The one-GPU test box never runs an engine on a device other than 0."""
