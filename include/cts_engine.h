@@ -260,7 +260,8 @@ int cts_verify_host(cts_engine* engine, const void* host_buf, uint32_t len,
  * drained, then the mailbox starts over. While the grid is resident a device-
  * wide wait (hipDeviceSynchronize, torch.cuda.synchronize) waits for it too,
  * i.e. until CTS_MAILBOX_IDLE_MS after the last call; cts_host_free stops the
- * grid first, so a free does not wait on other threads' posts. */
+ * grids of every engine on its device first (with that device current), so a
+ * free does not wait on other threads' posts. */
 int cts_verify_mapped(cts_engine* engine, const void* dev_buf, uint32_t len,
                       uint32_t expected_offset, cts_verify_result* out);
 /* How many times the mailbox grid was launched (0 = never used): each launch serves every
@@ -273,6 +274,9 @@ uint64_t cts_mailbox_launches(const cts_engine* engine);
  * (zero-copy) or hipMemcpyAsync can DMA them. *dev_view receives the device
  * address to pass as dev_arena. */
 int cts_host_alloc(cts_engine* engine, uint64_t bytes, void** host_ptr, void** dev_view);
+/* Frees cts_host_alloc memory. hipHostFree synchronizes the current device, so the
+ * engine's device is made current and every engine's resident mailbox grid on it is
+ * stopped first (they relaunch on their next cts_verify_mapped). */
 int cts_host_free(cts_engine* engine, void* host_ptr);
 /* Device address of pinned+mapped host memory (hipHostGetDevicePointer);
  * CTS_E_INVALID if host_ptr is not device-accessible pinned memory. */
