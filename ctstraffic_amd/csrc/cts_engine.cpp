@@ -284,6 +284,8 @@ struct Mailbox {
             if (len == 0) {
                 if (!running || (only_if_idle && outstanding != 0)) return CTS_OK;
                 running = false;
+                // a grid that already left on its own (idle exit) answers no stop job
+                if (outstanding == 0 && DrainedLocked()) return CTS_OK;
                 n = groups;
             } else {
                 const auto now = std::chrono::steady_clock::now();

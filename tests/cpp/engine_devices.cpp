@@ -788,6 +788,38 @@ int main()
     }
     CHECK(cts_engine_destroy(idle) == CTS_OK);
 
+    // a grid that left on its own (its idle exit, CTS_MAILBOX_EXIT_MS, before the watchdog's stop): a free stops
+    // nothing and does not wait for stop jobs no workgroup will answer (CTS_MAILBOX_TIMEOUT_MS), and the next post
+    // relaunches
+    setenv("CTS_MAILBOX_IDLE_MS", "10000", 1);
+    setenv("CTS_MAILBOX_EXIT_MS", "40", 1);
+    cts_engine* lone = nullptr;
+    CHECK(cts_engine_create(2, &lone) == CTS_OK);
+    {
+        cts_verify_result r{};
+        CHECK(cts_verify_mapped(lone, lone ? (const void*)(g_S.data() + 7) : nullptr, 5000, 7, &r) == CTS_OK &&
+              r.pass == 1);
+        std::shared_ptr<std::atomic<bool>> last;
+        {
+            std::lock_guard<std::mutex> lk(g_grid_mu);
+            last = g_grid_done.back();
+        }
+        for (int i = 0; i < 200 && !last->load(); ++i) std::this_thread::sleep_for(std::chrono::milliseconds(10));
+        CHECK(last->load());
+        void *hp = nullptr, *dv = nullptr;
+        CHECK(cts_host_alloc(lone, 4096, &hp, &dv) == CTS_OK);
+        const auto t0 = std::chrono::steady_clock::now();
+        CHECK(cts_host_free(lone, hp) == CTS_OK);
+        const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        CHECK(s < 0.5);
+        CHECK(cts_verify_mapped(lone, lone ? (const void*)(g_S.data() + 7) : nullptr, 5000, 7, &r) == CTS_OK &&
+              r.pass == 1);
+        CHECK(cts_mailbox_launches(lone) == 2);
+        std::printf("grid gone on its own: free %.3f s\n", s);
+    }
+    CHECK(cts_engine_destroy(lone) == CTS_OK);
+    unsetenv("CTS_MAILBOX_EXIT_MS");
+
     for (int g = 0; g <= kDevices; ++g) CHECK(cts_engine_destroy(eng[g]) == CTS_OK);
     (void)hipGetDevice(&cur);
     CHECK(cur == 3);

@@ -702,6 +702,38 @@ def test_verify_mapped_mailbox_group_keepalive(monkeypatch):
     assert launches == 2, launches
 
 
+def test_host_free_after_the_grid_left_on_its_own(monkeypatch):
+    """The grid leaves on its own (CTS_MAILBOX_EXIT_MS 40) long before the watchdog would stop it (10 s): a free then
+    stops nothing and must not wait CTS_MAILBOX_TIMEOUT_MS for stop jobs no workgroup will answer (round 4 did), and
+    the next post relaunches the grid with exact answers."""
+    import time
+
+    from ctstraffic_amd import Engine
+
+    monkeypatch.setenv("CTS_MAILBOX_EXIT_MS", "40")
+    monkeypatch.setenv("CTS_MAILBOX_IDLE_MS", "10000")
+    eng = Engine(0)
+    S = oracle.sender_buffer(70000)
+    arr, h, dev = eng.host_alloc(65536 + 32)
+    try:
+        arr[:65536] = S[9:9 + 65536]
+        assert eng.verify_mapped(dev, 65536, 9)["pass"]
+        time.sleep(0.3)  # every group's idle exit has passed
+        _, hh, _ = eng.host_alloc(1 << 20)
+        t0 = time.monotonic()
+        eng.host_free(hh)
+        took = time.monotonic() - t0
+        arr[777] ^= 0x08
+        r = eng.verify_mapped(dev, 65536, 9)
+        assert (r["pass"], r["first_mismatch"], r["mismatch_bytes"]) == (False, 777, 1)
+        launches = eng.mailbox_launches()
+    finally:
+        eng.host_free(h)
+        eng.close()
+    assert took < 0.5, took
+    assert launches == 2, launches
+
+
 def _mapped_check(eng, arr, dev, S, n, e, flip=None):
     """verify_mapped of arr[:n] (= S[e:e + n], one byte flipped at `flip`) against the oracle's record."""
     arr[:n] = S[e:e + n]
