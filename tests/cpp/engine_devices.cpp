@@ -8,10 +8,10 @@
 // creation, and counts a violation whenever a stream-ordered call (launch, memset, copy, event record, stream
 // synchronize or destroy) runs with another device current. The SYNC mailbox's resident grid
 // (cts::launch_mailbox) is emulated by a host thread that polls the slot rings exactly as mailbox_kernel does
-// (tags, no-op jobs, stop jobs, the idle exit) and answers every piece with a clean part record; the event
+// (tags, no-op jobs, stop jobs, the idle exit; on demand a job left unanswered) and verifies each job; the event
 // recorded after it completes when that thread has left, and hipHostFree counts a violation when it would wait
 // on a running grid (the reason Pause exists). The verify and fill launches compute what the kernels do with the
-// oracle (oracle/cts_oracle.c), and the emulated grid verifies each job, so whole loopback TCP connections
+// oracle (oracle/cts_oracle.c), so verdicts are checked as well as devices, and whole loopback TCP connections
 // (cts_loopback_run_multi, SYNC and DEFERRED patterns, clean and corrupt) run over eight engines: their IO threads
 // start on device 0, as new threads do, and drive patterns on every device, and MediaStream connections (SYNC, and
 // DEFERRED through an emulated frame-sum pass) with their client timer threads on device 0.
@@ -46,6 +46,7 @@ thread_local int t_cur = 0;
 std::atomic<int> g_violations{0};
 std::atomic<int> g_launches[kDevices];
 std::atomic<int> g_grids{0};  // emulated mailbox grids started
+std::atomic<int> g_drop_jobs{0};  // the emulated grids leave this many verify jobs unanswered (a lost job)
 std::mutex g_grid_mu;
 std::vector<std::shared_ptr<std::atomic<bool>>> g_grid_done;  // every grid's done flag, in launch order
 
@@ -477,6 +478,10 @@ hipError_t launch_mailbox(const MailSlot* slots, MailPart* parts, uint32_t per_g
                     progress = true;
                     since[g] = clock::now();
                     if (len == kMailSkip) continue;
+                    if (len != 0) {
+                        int d = g_drop_jobs.load();
+                        if (d > 0 && g_drop_jobs.compare_exchange_strong(d, d - 1)) continue;  // never answered
+                    }
                     const uint64_t ptr = pe & 0xFFFFFFFFFFFFull;
                     const uint32_t np = mail_parts(ptr, len);
                     // the job verified whole; part 0 carries its first mismatch and count, the others answer clean
@@ -818,6 +823,37 @@ int main()
         std::printf("grid gone on its own: free %.3f s\n", s);
     }
     CHECK(cts_engine_destroy(lone) == CTS_OK);
+
+    // a job the grid never answers: the caller gives up after CTS_MAILBOX_TIMEOUT_MS and verifies with a launch (the
+    // answer stays exact), the mailbox is broken until its grid has drained (the idle exit), then starts over
+    setenv("CTS_MAILBOX_TIMEOUT_MS", "200", 1);
+    cts_engine* flaky = nullptr;
+    CHECK(cts_engine_create(4, &flaky) == CTS_OK);
+    {
+        static uint8_t buf[20000];
+        std::memcpy(buf, g_S.data() + 11, sizeof(buf));
+        buf[12345] ^= 0x80;
+        cts_verify_result r{};
+        CHECK(cts_verify_mapped(flaky, flaky ? (const void*)buf : nullptr, sizeof(buf), 11, &r) == CTS_OK &&
+              r.pass == 0 && r.first_mismatch == 12345);
+        g_drop_jobs.store(1);
+        const auto t0 = std::chrono::steady_clock::now();
+        r = cts_verify_result{};
+        CHECK(cts_verify_mapped(flaky, flaky ? (const void*)buf : nullptr, sizeof(buf), 11, &r) == CTS_OK &&
+              r.pass == 0 && r.first_mismatch == 12345 && r.mismatch_bytes == 1);
+        const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        CHECK(s >= 0.2 && g_drop_jobs.load() == 0);
+        std::this_thread::sleep_for(std::chrono::milliseconds(300));  // the grid's idle exit (40 ms)
+        for (int k = 0; k < 3; ++k) {
+            r = cts_verify_result{};
+            CHECK(cts_verify_mapped(flaky, flaky ? (const void*)buf : nullptr, sizeof(buf), 11, &r) == CTS_OK &&
+                  r.pass == 0 && r.first_mismatch == 12345);
+        }
+        CHECK(cts_mailbox_launches(flaky) == 2);
+        std::printf("lost job: answered by a launch after %.3f s, mailbox relaunched\n", s);
+    }
+    CHECK(cts_engine_destroy(flaky) == CTS_OK);
+    unsetenv("CTS_MAILBOX_TIMEOUT_MS");
     unsetenv("CTS_MAILBOX_EXIT_MS");
 
     for (int g = 0; g <= kDevices; ++g) CHECK(cts_engine_destroy(eng[g]) == CTS_OK);
