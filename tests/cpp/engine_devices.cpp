@@ -47,6 +47,8 @@ std::atomic<int> g_violations{0};
 std::atomic<int> g_launches[kDevices];
 std::atomic<int> g_grids{0};  // emulated mailbox grids started
 std::atomic<int> g_drop_jobs{0};  // the emulated grids leave this many verify jobs unanswered (a lost job)
+std::atomic<int> g_async_us{0};
+std::atomic<int> g_not_ready{0};  // event queries that found work still in flight   // > 0: a verify launch completes this long after it was enqueued, on its own thread
 std::mutex g_grid_mu;
 std::vector<std::shared_ptr<std::atomic<bool>>> g_grid_done;  // every grid's done flag, in launch order
 
@@ -58,17 +60,19 @@ void violation(const char* what, int want, int have)
 
 }  // namespace
 
-// The runtime's opaque handles, defined by the fake.
+// The runtime's opaque handles, defined by the fake. A stream runs its asynchronous work (an emulated mailbox grid,
+// a verify launch while g_async_us > 0) each on a thread of its own that first waits for every earlier item of the
+// stream, so the stream stays in order; its synchronous operations wait for the items before them.
+using Done = std::shared_ptr<std::atomic<bool>>;
 struct ihipStream_t {
     int device;
     std::mutex mu;
-    std::vector<std::shared_ptr<std::atomic<bool>>> work;  // emulated grids launched on it (done flags)
-    std::vector<std::thread> threads;
+    std::vector<std::pair<Done, std::thread>> items;  // enqueued work, oldest first (finished ones reaped)
 };
 struct ihipEvent_t {
     int device;
     std::mutex mu;
-    std::vector<std::shared_ptr<std::atomic<bool>>> waits;  // the stream's work when recorded
+    std::vector<Done> waits;  // the stream's work when recorded
 };
 
 namespace {
@@ -96,8 +100,8 @@ bool grid_running(int dev)
     std::lock_guard<std::mutex> lk(g_mu);
     auto busy = [](ihipStream_t* st) {
         std::lock_guard<std::mutex> l2(st->mu);
-        for (auto& w : st->work)
-            if (!w->load(std::memory_order_acquire)) return true;
+        for (auto& w : st->items)
+            if (!w.first->load(std::memory_order_acquire)) return true;
         return false;
     };
     for (ihipStream_t* st : g_streams)
@@ -109,13 +113,55 @@ bool grid_running(int dev)
 
 void join_stream(ihipStream_t* st)
 {
-    std::vector<std::thread> ts;
+    std::vector<std::pair<Done, std::thread>> items;
     {
         std::lock_guard<std::mutex> lk(st->mu);
-        ts.swap(st->threads);
-        st->work.clear();
+        items.swap(st->items);
     }
-    for (auto& t : ts) t.join();
+    for (auto& w : items) w.second.join();
+}
+
+std::vector<Done> pending(ihipStream_t* st)
+{
+    std::vector<Done> w;
+    std::lock_guard<std::mutex> lk(st->mu);
+    for (auto& x : st->items)
+        if (!x.first->load(std::memory_order_acquire)) w.push_back(x.first);
+    return w;
+}
+
+void wait_for(const std::vector<Done>& w)
+{
+    for (auto& d : w)
+        while (!d->load(std::memory_order_acquire)) std::this_thread::sleep_for(std::chrono::microseconds(10));
+}
+
+// a synchronous operation on a stream: after everything enqueued before it
+void in_order(hipStream_t s) { wait_for(pending(stream_of(s))); }
+
+// asynchronous work on a stream: runs after everything enqueued before it
+template <typename F>
+Done enqueue(ihipStream_t* st, F body)
+{
+    auto done = std::make_shared<std::atomic<bool>>(false);
+    std::lock_guard<std::mutex> lk(st->mu);
+    std::vector<Done> before;
+    for (auto it = st->items.begin(); it != st->items.end();) {
+        if (it->first->load(std::memory_order_acquire)) {  // finished: reap
+            it->second.join();
+            it = st->items.erase(it);
+        } else {
+            before.push_back(it->first);
+            ++it;
+        }
+    }
+    std::thread t([before, body, done]() mutable {
+        wait_for(before);
+        body();
+        done->store(true, std::memory_order_release);
+    });
+    st->items.emplace_back(done, std::move(t));
+    return done;
 }
 
 }  // namespace
@@ -189,11 +235,7 @@ hipError_t hipEventRecord(hipEvent_t e, hipStream_t s)
     check_stream("hipEventRecord", s);
     ihipStream_t* st = stream_of(s);
     if (st->device != e->device) violation("hipEventRecord (event of another device)", e->device, st->device);
-    std::vector<std::shared_ptr<std::atomic<bool>>> w;
-    {
-        std::lock_guard<std::mutex> lk(st->mu);
-        w = st->work;
-    }
+    std::vector<Done> w = pending(st);
     std::lock_guard<std::mutex> lk(e->mu);
     e->waits.swap(w);
     return hipSuccess;
@@ -202,7 +244,10 @@ hipError_t hipEventQuery(hipEvent_t e)
 {
     std::lock_guard<std::mutex> lk(e->mu);
     for (auto& w : e->waits)
-        if (!w->load(std::memory_order_acquire)) return hipErrorNotReady;
+        if (!w->load(std::memory_order_acquire)) {
+            g_not_ready.fetch_add(1);
+            return hipErrorNotReady;
+        }
     return hipSuccess;
 }
 hipError_t hipEventDestroy(hipEvent_t e)
@@ -244,12 +289,14 @@ hipError_t hipHostGetDevicePointer(void** d, void* h, unsigned int)
 hipError_t hipMemsetAsync(void* dst, int v, size_t bytes, hipStream_t s)
 {
     check_stream("hipMemsetAsync", s);
+    in_order(s);
     std::memset(dst, v, bytes);
     return hipSuccess;
 }
 hipError_t hipMemcpyAsync(void* dst, const void* src, size_t bytes, hipMemcpyKind, hipStream_t s)
 {
     check_stream("hipMemcpyAsync", s);
+    in_order(s);
     std::memcpy(dst, src, bytes);
     return hipSuccess;
 }
@@ -262,6 +309,7 @@ hipError_t hipMallocAsync(void** p, size_t bytes, hipStream_t s)
 hipError_t hipFreeAsync(void* p, hipStream_t s)
 {
     check_stream("hipFreeAsync", s);
+    in_order(s);
     std::free(p);
     return hipSuccess;
 }
@@ -294,10 +342,12 @@ int pthread_cond_clockwait(pthread_cond_t* c, pthread_mutex_t* m, clockid_t clk,
 namespace cts {
 namespace {
 
-void launched(const char* what, hipStream_t s)
+// a launch: counted on its stream's device; the synchronous fakes run after the stream's earlier work
+void launched(const char* what, hipStream_t s, bool sync = true)
 {
     check_stream(what, s);
     g_launches[stream_of(s)->device].fetch_add(1);
+    if (sync) in_order(s);
 }
 
 static_assert(sizeof(ora_desc) == sizeof(cts_buf_desc) && sizeof(ora_result) == sizeof(cts_verify_result),
@@ -322,18 +372,24 @@ hipError_t launch_verify(const uint8_t* arena, uint64_t bytes, const cts_buf_des
                          cts_verify_result* r, uint64_t* counters, uint32_t* first_fail, uint32_t n_conns,
                          hipStream_t s, const LaunchGeometry&)
 {
-    launched("launch_verify", s);
-    ora_counters c{};
-    if (ora_verify_batch(arena, bytes, reinterpret_cast<const ora_desc*>(d), n, reinterpret_cast<ora_result*>(r), &c,
-                         first_fail, n_conns, 1) != 0)
-        return hipErrorInvalidValue;
-    if (counters != nullptr) {  // (shard 0 of the device block)
-        counters[kBytesChecked] += c.bytes_checked;
-        counters[kBytesOk] += c.bytes_ok;
-        counters[kBuffersChecked] += c.buffers_checked;
-        counters[kBuffersFailed] += c.buffers_failed;
-        counters[kMismatchedBytes] += c.mismatched_bytes;
-    }
+    const int async_us = g_async_us.load();
+    launched("launch_verify", s, async_us == 0);
+    auto body = [=] {
+        if (async_us > 0) std::this_thread::sleep_for(std::chrono::microseconds(async_us));
+        ora_counters c{};
+        (void)ora_verify_batch(arena, bytes, reinterpret_cast<const ora_desc*>(d), n, reinterpret_cast<ora_result*>(r),
+                               &c, first_fail, n_conns, 1);
+        if (counters != nullptr) {  // (shard 0 of the device block)
+            counters[kBytesChecked] += c.bytes_checked;
+            counters[kBytesOk] += c.bytes_ok;
+            counters[kBuffersChecked] += c.buffers_checked;
+            counters[kBuffersFailed] += c.buffers_failed;
+            counters[kMismatchedBytes] += c.mismatched_bytes;
+        }
+    };
+    if (d == nullptr && n != 0) return hipErrorInvalidValue;
+    if (async_us > 0) enqueue(stream_of(s), body);  // done later, behind the stream's earlier work
+    else body();
     return hipSuccess;
 }
 hipError_t launch_verify_strided(const uint8_t*, uint64_t, uint32_t, const uint32_t*, uint32_t, uint32_t, uint32_t,
@@ -451,12 +507,11 @@ hipError_t launch_media_stream_frames(const uint8_t* arena, uint64_t bytes, cons
 hipError_t launch_mailbox(const MailSlot* slots, MailPart* parts, uint32_t per_group, const MailStarts& starts,
                           uint32_t groups, uint64_t idle_ticks, hipStream_t s, uint64_t)
 {
-    launched("launch_mailbox", s);
+    launched("launch_mailbox", s, false);
     ihipStream_t* st = stream_of(s);
-    auto done = std::make_shared<std::atomic<bool>>(false);
     const MailStarts js = starts;
     MailSlot* ring = const_cast<MailSlot*>(slots);
-    std::thread t([=] {
+    const Done done = enqueue(st, [=] {
         using clock = std::chrono::steady_clock;
         const auto idle = std::chrono::nanoseconds(idle_ticks * 10);
         std::vector<uint64_t> j(js.j, js.j + groups);
@@ -519,15 +574,11 @@ hipError_t launch_mailbox(const MailSlot* slots, MailPart* parts, uint32_t per_g
             }
             if (!progress) std::this_thread::sleep_for(std::chrono::microseconds(20));
         }
-        done->store(true, std::memory_order_release);
     });
     {
         std::lock_guard<std::mutex> lk(g_grid_mu);
         g_grid_done.push_back(done);
     }
-    std::lock_guard<std::mutex> lk(st->mu);
-    st->work.push_back(done);
-    st->threads.push_back(std::move(t));
     g_grids.fetch_add(1);
     return hipSuccess;
 }
@@ -712,7 +763,9 @@ int main()
 
     // whole loopback TCP connections over the eight engines (connection i on engine cts_shard_of(i, 8)): the feeder's
     // side threads start on device 0 and drive SYNC (the mailbox) and DEFERRED (batches, events) patterns on every
-    // device; the wire corruption of one connection must fail exactly that connection
+    // device; the wire corruption of one connection must fail exactly that connection. Verify launches complete
+    // 300 us after they are enqueued, so DEFERRED batches are really in flight when the pattern polls their events.
+    g_async_us.store(300);
     struct Run {
         uint32_t pattern, mode, corrupt;
     };
@@ -772,7 +825,10 @@ int main()
                     (unsigned long long)mo.datagrams_received);
     }
     cts_shared_buffer_release();
-    std::printf("loopback: %d grids, violations %d\n", g_grids.load(), g_violations.load());
+    g_async_us.store(0);
+    CHECK(g_not_ready.load() > 0);  // DEFERRED polled batches still in flight
+    std::printf("loopback: %d grids, %d event queries in flight, violations %d\n", g_grids.load(), g_not_ready.load(),
+                g_violations.load());
 
     // an idle engine's watchdog stops its grid from its own thread (no device current there but its own guard)
     setenv("CTS_MAILBOX_IDLE_MS", "20", 1);
