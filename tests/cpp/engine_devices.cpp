@@ -768,22 +768,39 @@ int main()
     g_async_us.store(300);
     struct Run {
         uint32_t pattern, mode, corrupt;
+        uint32_t buffer_high = 0, recv_whole = 1, depth = 2, batch = 8;  // -Buffer:[64 KiB, high], partial recvs, DEFERRED
     };
-    for (const Run& run : {Run{CTS_PATTERN_PUSH, CTS_VERIFY_DEFERRED, 0}, Run{CTS_PATTERN_PULL, CTS_VERIFY_SYNC, 0},
-                           Run{CTS_PATTERN_PUSH, CTS_VERIFY_SYNC, 1}, Run{CTS_PATTERN_PULL, CTS_VERIFY_DEFERRED, 1},
-                           Run{CTS_PATTERN_PUSHPULL, CTS_VERIFY_DEFERRED, 0}, Run{CTS_PATTERN_DUPLEX, CTS_VERIFY_DEFERRED, 0},
-                           Run{CTS_PATTERN_DUPLEX, CTS_VERIFY_SYNC, 1}}) {
+    const Run runs[] = {
+        {CTS_PATTERN_PUSH, CTS_VERIFY_DEFERRED, 0},
+        {CTS_PATTERN_PULL, CTS_VERIFY_SYNC, 0},
+        {CTS_PATTERN_PUSH, CTS_VERIFY_SYNC, 1},
+        {CTS_PATTERN_PULL, CTS_VERIFY_DEFERRED, 1},
+        {CTS_PATTERN_PUSHPULL, CTS_VERIFY_DEFERRED, 0},
+        {CTS_PATTERN_DUPLEX, CTS_VERIFY_DEFERRED, 0},
+        {CTS_PATTERN_DUPLEX, CTS_VERIFY_SYNC, 1},
+        // random buffer sizes, partial completions, other DEFERRED depths and batches
+        {CTS_PATTERN_PUSH, CTS_VERIFY_DEFERRED, 0, 200000u, 0u, 3u, 16u},
+        {CTS_PATTERN_PULL, CTS_VERIFY_DEFERRED, 1, 0u, 0u, 1u, 8u},
+        {CTS_PATTERN_PUSHPULL, CTS_VERIFY_SYNC, 0, 150000u, 0u, 2u, 8u},
+        {CTS_PATTERN_DUPLEX, CTS_VERIFY_DEFERRED, 1, 100000u, 0u, 2u, 12u},
+    };
+    for (const Run& run : runs) {
+        char depth[8];
+        std::snprintf(depth, sizeof(depth), "%u", run.depth);
+        setenv("CTS_DEFERRED_DEPTH", depth, 1);
         cts_loopback_config cfg{};
         cfg.connections = 16;
         cfg.io_pattern = run.pattern;
         cfg.buffer_size = 65536;
+        cfg.buffer_size_high = run.buffer_high;
+        cfg.random_seed = 7;
         cfg.verify_buffers = 1;
         cfg.transfer_size = (2u << 20) + 12345;
         cfg.verify_mode = run.mode;
-        cfg.batch_buffers = 8;
+        cfg.batch_buffers = run.batch;
         cfg.corrupt_connection = run.corrupt ? 5u : ~0u;
         cfg.corrupt_send_index = 11;
-        cfg.recv_whole = 1;
+        cfg.recv_whole = run.recv_whole;
         cts_loopback_result out{};
         CHECK(cts_loopback_run_multi(&cfg, eng, kDevices, nullptr, nullptr, &out) == CTS_OK);
         (void)hipGetDevice(&cur);
@@ -792,11 +809,14 @@ int main()
             CHECK(out.connections_ok == 15 && out.connections_failed == 1 && out.data_errors == 1);
         else
             CHECK(out.connections_ok == 16 && out.connections_failed == 0 && out.data_errors == 0 &&
-                  out.buffers_verified >= 16 * 33);
-        std::printf("loopback pattern %u mode %u corrupt %u: ok %u failed %u data errors %u verified %llu\n",
-                    run.pattern, run.mode, run.corrupt, out.connections_ok, out.connections_failed, out.data_errors,
+                  out.buffers_verified >= (run.recv_whole && !run.buffer_high ? 16u * 33u : 16u));
+        std::printf("loopback pattern %u mode %u corrupt %u buffers [65536, %u] whole %u depth %u batch %u: ok %u "
+                    "failed %u data errors %u verified %llu\n",
+                    run.pattern, run.mode, run.corrupt, run.buffer_high, run.recv_whole, run.depth, run.batch,
+                    out.connections_ok, out.connections_failed, out.data_errors,
                     (unsigned long long)out.buffers_verified);
     }
+    unsetenv("CTS_DEFERRED_DEPTH");
     // MediaStream over loopback UDP on engine 6, SYNC (one verify per datagram) and DEFERRED (the frame-sum pass
     // flushed at every render tick): the client's timer thread starts on device 0 and flushes through the pattern
     for (uint32_t run = 0; run < 4; ++run) {
