@@ -375,7 +375,13 @@ hipError_t launch_verify(const uint8_t* arena, uint64_t bytes, const cts_buf_des
     const int async_us = g_async_us.load();
     launched("launch_verify", s, async_us == 0);
     auto body = [=] {
-        if (async_us > 0) std::this_thread::sleep_for(std::chrono::microseconds(async_us));
+        if (async_us > 0) {  // 0.5-1.5 x async_us: launches on different streams finish in any order
+            thread_local uint32_t x = 0x9E3779B9u ^ (uint32_t)(uintptr_t)&x;
+            x ^= x << 13;
+            x ^= x >> 17;
+            x ^= x << 5;
+            std::this_thread::sleep_for(std::chrono::microseconds(async_us / 2 + x % (uint32_t)(async_us + 1)));
+        }
         ora_counters c{};
         (void)ora_verify_batch(arena, bytes, reinterpret_cast<const ora_desc*>(d), n, reinterpret_cast<ora_result*>(r),
                                &c, first_fail, n_conns, 1);
@@ -764,7 +770,7 @@ int main()
     // whole loopback TCP connections over the eight engines (connection i on engine cts_shard_of(i, 8)): the feeder's
     // side threads start on device 0 and drive SYNC (the mailbox) and DEFERRED (batches, events) patterns on every
     // device; the wire corruption of one connection must fail exactly that connection. Verify launches complete
-    // 300 us after they are enqueued, so DEFERRED batches are really in flight when the pattern polls their events.
+    // 150-450 us after they are enqueued, so DEFERRED batches are really in flight when the pattern polls their events.
     g_async_us.store(300);
     struct Run {
         uint32_t pattern, mode, corrupt;
