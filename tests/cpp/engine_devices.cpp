@@ -14,7 +14,8 @@
 // oracle (oracle/cts_oracle.c), so verdicts are checked as well as devices, and whole loopback TCP connections
 // (cts_loopback_run_multi, SYNC and DEFERRED patterns, clean and corrupt) run over eight engines: their IO threads
 // start on device 0, as new threads do, and drive patterns on every device, and MediaStream connections (SYNC, and
-// DEFERRED through an emulated frame-sum pass) with their client timer threads on device 0.
+// DEFERRED through an emulated frame-sum pass) with their client timer threads on device 0. cts_counters_allreduce
+// (cts_collective.cpp) then reduces nine engines' counter blocks over a stub RCCL (argv[1]).
 #include <hip/hip_runtime_api.h>
 #include <pthread.h>
 #include <time.h>
@@ -507,6 +508,19 @@ hipError_t launch_media_stream_frames(const uint8_t* arena, uint64_t bytes, cons
     return hipSuccess;
 }
 
+// counters_fold_kernel: the 64 shards' five sums into out (accumulating), after the stream's earlier work
+hipError_t launch_counters_fold(const void* block, uint64_t* out, bool accumulate, hipStream_t s)
+{
+    launched("launch_counters_fold", s);
+    const uint64_t* h = static_cast<const uint64_t*>(block);
+    for (int k = 0; k < 5; ++k) {
+        uint64_t v = accumulate ? out[k] : 0;
+        for (uint32_t sh = 0; sh < CTS_COUNTER_SHARDS; ++sh) v += h[sh * kCounterSlots + k];
+        out[k] = v;
+    }
+    return hipSuccess;
+}
+
 // The resident grid, emulated: group g polls slot g * per_group + j % per_group for the tag j + 1 from
 // starts.j[g] on, as mailbox_kernel does; every piece of a job is answered clean; a stop job (len 0) is answered
 // by every workgroup of the group and ends it; a group that waits idle_ticks (100 MHz) for a job leaves.
@@ -722,8 +736,10 @@ void drive(cts_engine* e, int dev, int home, int rounds)
 
 }  // namespace
 
-int main()
+int main(int argc, char** argv)
 {
+    // argv[1]: the stub RCCL (tests/cpp/rccl_stub.cpp) for cts_counters_allreduce; without it that phase is skipped
+    if (argc > 1) setenv("CTS_RCCL_LIBRARY", argv[1], 1);
     std::setvbuf(stdout, nullptr, _IONBF, 0);
     g_S.resize(ora_sender_buffer_size(1u << 20));
     ora_build_sender_buffer(g_S.data(), 1u << 20);
@@ -855,6 +871,61 @@ int main()
     CHECK(g_not_ready.load() > 0);  // DEFERRED polled batches still in flight
     std::printf("loopback: %d grids, %d event queries in flight, violations %d\n", g_grids.load(), g_not_ready.load(),
                 g_violations.load());
+
+    // the node's counters: every engine verifies a batch with a few corrupt buffers on a stream of its own (launches
+    // still in flight), then cts_counters_allreduce (each block folded on its device, one all-reduce per device over
+    // the stub RCCL; engines 5 and 5b share device 5) from a thread on device 3 must equal cts_counters_read_multi
+    // and the oracle's sums, with device 3 current afterwards
+    if (argc > 1) {
+        g_async_us.store(300);
+        constexpr uint32_t kN = kDevices + 1, kBufs = 32;
+        std::vector<std::vector<uint8_t>> arenas(kN, std::vector<uint8_t>((size_t)kBufs * 4096 + 64));
+        std::vector<std::vector<uint64_t>> blocks(kN, std::vector<uint64_t>(CTS_COUNTER_SHARDS * 8));
+        std::vector<std::vector<cts_buf_desc>> descs(kN);
+        std::vector<std::vector<cts_verify_result>> res(kN, std::vector<cts_verify_result>(kBufs));
+        std::vector<void*> streams(kN);
+        std::vector<const void*> bptr(kN);
+        uint64_t want[5] = {0, 0, 0, 0, 0};
+        for (uint32_t g = 0; g < kN; ++g) {
+            uint8_t* a = reinterpret_cast<uint8_t*>(((uintptr_t)arenas[g].data() + 15u) & ~(uintptr_t)15u);
+            for (uint32_t b = 0; b < kBufs; ++b) {
+                const uint32_t len = 1000u + 97u * b + g, e = (7919u * b + 31u * g) & 0xFFFFu;
+                descs[g].push_back(cts_buf_desc{(uint64_t)b * 4096u, len, e, b % 5u, 0u});
+                for (uint32_t k = 0; k < len; ++k) a[(size_t)b * 4096u + k] = ora_pattern_byte(e + k);
+                want[cts::kBytesChecked] += len;
+                want[cts::kBuffersChecked] += 1;
+                if ((b + g) % 7u == 3u) {  // one corrupt byte
+                    a[(size_t)b * 4096u + len / 2] ^= 0x10;
+                    want[cts::kBuffersFailed] += 1;
+                    want[cts::kMismatchedBytes] += 1;
+                } else {
+                    want[cts::kBytesOk] += len;
+                }
+            }
+            CHECK(cts_engine_stream_create(eng[g], &streams[g]) == CTS_OK);
+            CHECK(cts_counters_reset(eng[g], blocks[g].data(), streams[g]) == CTS_OK);
+            CHECK(cts_verify(eng[g], a, (uint64_t)kBufs * 4096u, descs[g].data(), kBufs, 4096u, res[g].data(),
+                             blocks[g].data(), nullptr, 0, streams[g]) == CTS_OK);
+            bptr[g] = blocks[g].data();
+        }
+        cts_counters all{}, fold{};
+        CHECK(cts_counters_allreduce(eng, bptr.data(), streams.data(), kN, &all) == CTS_OK);
+        CHECK(cts_counters_read_multi(eng, bptr.data(), streams.data(), kN, &fold) == CTS_OK);
+        (void)hipGetDevice(&cur);
+        CHECK(cur == 3);
+        const uint64_t got[5] = {all.bytes_checked, all.bytes_ok, all.buffers_checked, all.buffers_failed,
+                                 all.mismatched_bytes};
+        const uint64_t gotf[5] = {fold.bytes_checked, fold.bytes_ok, fold.buffers_checked, fold.buffers_failed,
+                                  fold.mismatched_bytes};
+        for (int k = 0; k < 5; ++k) CHECK(got[k] == want[k] && gotf[k] == want[k]);
+        for (uint32_t g = 0; g < kN; ++g) CHECK(cts_engine_stream_destroy(eng[g], streams[g]) == CTS_OK);
+        CHECK(cts_counters_allreduce_release() == CTS_OK);
+        g_async_us.store(0);
+        std::printf("allreduce: %llu buffers, %llu failed, equal to the host fold and the oracle\n",
+                    (unsigned long long)all.buffers_checked, (unsigned long long)all.buffers_failed);
+    } else {
+        std::printf("allreduce: skipped (no stub RCCL)\n");
+    }
 
     // an idle engine's watchdog stops its grid from its own thread (no device current there but its own guard)
     setenv("CTS_MAILBOX_IDLE_MS", "20", 1);

@@ -80,7 +80,8 @@ def test_engine_abi_on_eight_fake_devices(san):
     device differs, one after the other and all at once; then whole loopback TCP connections (Push, Pull, PushPull,
     Duplex on the async functor; SYNC and DEFERRED; clean and corrupt) spread over the eight engines from feeder
     threads that start on device 0; then MediaStream connections (SYNC, and DEFERRED through an emulated frame-sum
-    pass) on device 6 with the client timer thread on device 0. Every stream-ordered HIP call and launch must run with
+    pass) on device 6 with the client timer thread on device 0; then cts_counters_allreduce over the nine engines
+    (a stub RCCL, tests/cpp/rccl_stub.cpp) against the host fold and the oracle's sums. Every stream-ordered HIP call and launch must run with
     its engine's device current, every event must be recorded on a stream of its own device, the caller's device must
     be current again afterwards, and no pinned free may run while a SYNC mailbox grid (emulated by a host thread that
     polls the slot rings as mailbox_kernel does) is resident on the current device: hipHostFree is an implicit
@@ -145,7 +146,8 @@ def test_engine_abi_on_eight_fake_devices(san):
            "-I", os.path.join(ROOT, "oracle"), "-I", "/opt/rocm/include", "-D__HIP_PLATFORM_AMD__"]
     srcs = [os.path.join(ROOT, "ctstraffic_amd", "csrc", x) for x in (
         "cts_engine.cpp", "cts_host_util.cpp", "cts_pattern.cpp", "cts_media_stream.cpp", "cts_status.cpp",
-        "cts_loopback.cpp", "cts_loopback_udp.cpp")] + [os.path.join(ROOT, "tests", "cpp", "engine_devices.cpp")]
+        "cts_loopback.cpp", "cts_loopback_udp.cpp", "cts_collective.cpp")] + [
+        os.path.join(ROOT, "tests", "cpp", "engine_devices.cpp")]
     with tempfile.TemporaryDirectory() as d:
         objs = [os.path.join(d, os.path.basename(src) + ".o") for src in srcs]
         with concurrent.futures.ThreadPoolExecutor(4) as pool:  # (the pattern mirror alone takes ~30 s under a sanitizer)
@@ -158,9 +160,11 @@ def test_engine_abi_on_eight_fake_devices(san):
         objs.append(o)
         exe = os.path.join(d, "engine_devices")
         subprocess.run(["g++", *flags, *objs, "-o", exe, "-ldl"], check=True)
-        out = subprocess.run([exe], capture_output=True, text=True, timeout=300, env={**os.environ, **ENV})
+        out = subprocess.run([exe, _build_rccl_stub(d, san)], capture_output=True, text=True, timeout=300,
+                             env={**os.environ, **ENV})
         assert out.returncode == 0, (out.returncode, out.stdout[-2000:], out.stderr[-4000:])
         assert "engine_devices: ok" in out.stdout and "violation" not in out.stderr
+        assert "equal to the host fold and the oracle" in out.stdout
         assert "runtime error" not in out.stderr and "WARNING: ThreadSanitizer" not in out.stderr, out.stderr[-4000:]
 
 
