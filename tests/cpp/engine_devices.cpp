@@ -15,7 +15,8 @@
 // (cts_loopback_run_multi, SYNC and DEFERRED patterns, clean and corrupt) run over eight engines: their IO threads
 // start on device 0, as new threads do, and drive patterns on every device, and MediaStream connections (SYNC, and
 // DEFERRED through an emulated frame-sum pass) with their client timer threads on device 0. cts_counters_allreduce
-// (cts_collective.cpp) then reduces nine engines' counter blocks over a stub RCCL (argv[1]).
+// (cts_collective.cpp) then reduces nine engines' counter blocks over a stub RCCL (argv[1]), and bench.py's
+// single-process leg (tools/bench_multi.cpp) runs one native launch thread per engine on eight devices.
 #include <hip/hip_runtime_api.h>
 #include <pthread.h>
 #include <time.h>
@@ -386,12 +387,12 @@ hipError_t launch_verify(const uint8_t* arena, uint64_t bytes, const cts_buf_des
         ora_counters c{};
         (void)ora_verify_batch(arena, bytes, reinterpret_cast<const ora_desc*>(d), n, reinterpret_cast<ora_result*>(r),
                                &c, first_fail, n_conns, 1);
-        if (counters != nullptr) {  // (shard 0 of the device block)
-            counters[kBytesChecked] += c.bytes_checked;
-            counters[kBytesOk] += c.bytes_ok;
-            counters[kBuffersChecked] += c.buffers_checked;
-            counters[kBuffersFailed] += c.buffers_failed;
-            counters[kMismatchedBytes] += c.mismatched_bytes;
+        if (counters != nullptr) {  // (shard 0 of the device block; atomics, as the kernels': streams run at once)
+            __atomic_fetch_add(&counters[kBytesChecked], c.bytes_checked, __ATOMIC_RELAXED);
+            __atomic_fetch_add(&counters[kBytesOk], c.bytes_ok, __ATOMIC_RELAXED);
+            __atomic_fetch_add(&counters[kBuffersChecked], c.buffers_checked, __ATOMIC_RELAXED);
+            __atomic_fetch_add(&counters[kBuffersFailed], c.buffers_failed, __ATOMIC_RELAXED);
+            __atomic_fetch_add(&counters[kMismatchedBytes], c.mismatched_bytes, __ATOMIC_RELAXED);
         }
     };
     if (d == nullptr && n != 0) return hipErrorInvalidValue;
@@ -606,6 +607,28 @@ hipError_t launch_mailbox(const MailSlot* slots, MailPart* parts, uint32_t per_g
 }  // namespace cts
 
 // ---- the driver --------------------------------------------------------------------------------------------
+// tools/bench_multi.cpp (bench.py's single-process leg): one native launch thread per GPU
+extern "C" {
+struct cts_bench_gpu {  // as declared in tools/bench_multi.cpp (and bench.py's _BenchGpu)
+    cts_engine* engine;
+    int device;
+    uint32_t arenas;
+    const void* const* arena;
+    uint64_t arena_bytes;
+    const cts_buf_desc* descs;
+    uint32_t n;
+    uint32_t max_length_hint;
+    cts_verify_result* const* results;
+    void* counters;
+    uint32_t* const* conn_first_fail;
+    uint32_t n_conns;
+    void* const* streams;
+    uint32_t nstreams;
+};
+int cts_bench_run_multi(const cts_bench_gpu* gpus, uint32_t G, uint32_t launches, double* t0, double* t1,
+                        double* t_start, int sync);
+}
+
 namespace {
 
 int g_fail = 0;
@@ -925,6 +948,66 @@ int main(int argc, char** argv)
                     (unsigned long long)all.buffers_checked, (unsigned long long)all.buffers_failed);
     } else {
         std::printf("allreduce: skipped (no stub RCCL)\n");
+    }
+
+    // bench.py's single-process leg at eight GPUs: one native thread per engine sets its device and issues its
+    // launches round robin over 2 arenas and 2 streams (launches in flight), then synchronises its streams
+    {
+        g_async_us.store(200);
+        constexpr uint32_t kG = kDevices, kR = 2, kS = 2, kBufs = 16, kLaunches = 6;
+        struct Gpu {
+            std::vector<uint8_t> mem[kR];
+            const void* arena[kR];
+            std::vector<cts_verify_result> res[kR];
+            cts_verify_result* resp[kR];
+            std::vector<uint32_t> cff[kR];
+            uint32_t* cffp[kR];
+            std::vector<uint64_t> block;
+            void* streams[kS];
+        };
+        std::vector<Gpu> gp(kG);
+        std::vector<cts_buf_desc> dd;
+        for (uint32_t b = 0; b < kBufs; ++b) dd.push_back(cts_buf_desc{(uint64_t)b * 4096u, 4096u, (1237u * b) & 0xFFFFu, b % 4u, 0u});
+        std::vector<cts_bench_gpu> work(kG);
+        for (uint32_t g = 0; g < kG; ++g) {
+            Gpu& G = gp[g];
+            for (uint32_t a = 0; a < kR; ++a) {
+                G.mem[a].assign((size_t)kBufs * 4096u + 16, 0);
+                uint8_t* base = reinterpret_cast<uint8_t*>(((uintptr_t)G.mem[a].data() + 15u) & ~(uintptr_t)15u);
+                for (uint32_t b = 0; b < kBufs; ++b)
+                    for (uint32_t k = 0; k < 4096u; ++k) base[(size_t)b * 4096u + k] = ora_pattern_byte(dd[b].expected_pattern_offset + k);
+                if (a == 1) base[(size_t)(g % kBufs) * 4096u + 100u] ^= 0x01;  // arena 1: buffer g % 16 corrupt
+                G.arena[a] = base;
+                G.res[a].assign(kBufs, cts_verify_result{});
+                G.resp[a] = G.res[a].data();
+                G.cff[a].assign(4, 0xFFFFFFFFu);
+                G.cffp[a] = G.cff[a].data();
+            }
+            G.block.assign(CTS_COUNTER_SHARDS * 8, 0);
+            for (uint32_t k = 0; k < kS; ++k) CHECK(cts_engine_stream_create(eng[g], &G.streams[k]) == CTS_OK);
+            work[g] = cts_bench_gpu{eng[g], (int)g, kR, G.arena, (uint64_t)kBufs * 4096u, dd.data(), kBufs, 4096u,
+                                    G.resp, G.block.data(), G.cffp, 4u, G.streams, kS};
+        }
+        double t0[kG], t1[kG], ts = 0;
+        CHECK(cts_bench_run_multi(work.data(), kG, kLaunches, t0, t1, &ts, 1) == CTS_OK);
+        (void)hipGetDevice(&cur);
+        CHECK(cur == 3);
+        for (uint32_t g = 0; g < kG; ++g) {
+            cts_counters c{};
+            CHECK(cts_counters_read(eng[g], gp[g].block.data(), &c, gp[g].streams[0]) == CTS_OK);
+            CHECK(c.buffers_checked == (uint64_t)kLaunches * kBufs && c.buffers_failed == kLaunches / kR &&
+                  c.mismatched_bytes == kLaunches / kR);
+            for (uint32_t b = 0; b < kBufs; ++b) {
+                CHECK(gp[g].res[0][b].pass == 1);
+                CHECK(gp[g].res[1][b].pass == (b == g % kBufs ? 0 : 1));
+            }
+            CHECK(gp[g].res[1][g % kBufs].first_mismatch == 100u);
+            CHECK(gp[g].cff[1][(g % kBufs) % 4u] == g % kBufs && gp[g].cff[0][0] == 0xFFFFFFFFu);
+            for (uint32_t k = 0; k < kS; ++k) CHECK(cts_engine_stream_destroy(eng[g], gp[g].streams[k]) == CTS_OK);
+        }
+        g_async_us.store(0);
+        std::printf("bench_multi: %u GPUs x %u launches, records, first failures and counters as planned\n", kG,
+                    kLaunches);
     }
 
     // an idle engine's watchdog stops its grid from its own thread (no device current there but its own guard)

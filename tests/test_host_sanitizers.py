@@ -81,7 +81,8 @@ def test_engine_abi_on_eight_fake_devices(san):
     Duplex on the async functor; SYNC and DEFERRED; clean and corrupt) spread over the eight engines from feeder
     threads that start on device 0; then MediaStream connections (SYNC, and DEFERRED through an emulated frame-sum
     pass) on device 6 with the client timer thread on device 0; then cts_counters_allreduce over the nine engines
-    (a stub RCCL, tests/cpp/rccl_stub.cpp) against the host fold and the oracle's sums. Every stream-ordered HIP call and launch must run with
+    (a stub RCCL, tests/cpp/rccl_stub.cpp) against the host fold and the oracle's sums; then bench.py's
+    single-process leg at eight GPUs (tools/bench_multi.cpp: one native launch thread per engine). Every stream-ordered HIP call and launch must run with
     its engine's device current, every event must be recorded on a stream of its own device, the caller's device must
     be current again afterwards, and no pinned free may run while a SYNC mailbox grid (emulated by a host thread that
     polls the slot rings as mailbox_kernel does) is resident on the current device: hipHostFree is an implicit
@@ -147,7 +148,7 @@ def test_engine_abi_on_eight_fake_devices(san):
     srcs = [os.path.join(ROOT, "ctstraffic_amd", "csrc", x) for x in (
         "cts_engine.cpp", "cts_host_util.cpp", "cts_pattern.cpp", "cts_media_stream.cpp", "cts_status.cpp",
         "cts_loopback.cpp", "cts_loopback_udp.cpp", "cts_collective.cpp")] + [
-        os.path.join(ROOT, "tests", "cpp", "engine_devices.cpp")]
+        os.path.join(ROOT, "tests", "cpp", "engine_devices.cpp"), os.path.join(ROOT, "tools", "bench_multi.cpp")]
     with tempfile.TemporaryDirectory() as d:
         objs = [os.path.join(d, os.path.basename(src) + ".o") for src in srcs]
         with concurrent.futures.ThreadPoolExecutor(4) as pool:  # (the pattern mirror alone takes ~30 s under a sanitizer)
@@ -164,7 +165,7 @@ def test_engine_abi_on_eight_fake_devices(san):
                              env={**os.environ, **ENV})
         assert out.returncode == 0, (out.returncode, out.stdout[-2000:], out.stderr[-4000:])
         assert "engine_devices: ok" in out.stdout and "violation" not in out.stderr
-        assert "equal to the host fold and the oracle" in out.stdout
+        assert "equal to the host fold and the oracle" in out.stdout and "bench_multi: 8 GPUs" in out.stdout
         assert "runtime error" not in out.stderr and "WARNING: ThreadSanitizer" not in out.stderr, out.stderr[-4000:]
 
 
