@@ -39,6 +39,7 @@
 #include "cts_loopback.h"
 #include "cts_media_stream.h"
 #include "cts_oracle.h"
+#include "cts_pattern.h"
 
 namespace {
 
@@ -1008,6 +1009,54 @@ int main(int argc, char** argv)
         g_async_us.store(0);
         std::printf("bench_multi: %u GPUs x %u launches, records, first failures and counters as planned\n", kG,
                     kLaunches);
+    }
+
+    // a DEFERRED pattern on engine 7 whose batch launch does not finish in time (a hung kernel, emulated: it completes
+    // late, 0.5-1.5 s): cts_io_pattern_destroy gives up within its bound (CTS_PATTERN_DESTROY_WAIT_MS) with CTS_E_HIP and
+    // leaves the pattern allocated under the running launch; once the launch has finished a second destroy succeeds
+    {
+        std::vector<uint8_t> sender(ora_sender_buffer_size(4096));
+        ora_build_sender_buffer(sender.data(), 4096);
+        CHECK(cts_shared_buffer_attach(sender.data(), sender.size()) == CTS_OK);
+        setenv("CTS_PATTERN_DESTROY_WAIT_MS", "300", 1);
+        cts_pattern_config pc{};
+        pc.io_pattern = CTS_PATTERN_PUSH;
+        pc.protocol = CTS_PROTOCOL_TCP;
+        pc.listening = 1;
+        pc.verify_buffers = 1;
+        pc.pre_post_recvs = 1;
+        pc.pre_post_sends = 1;
+        pc.buffer_size_low = 4096;
+        pc.tcp_shutdown = CTS_SHUTDOWN_GRACEFUL;
+        pc.transfer_size = 64u * 4096u;
+        pc.verify_mode = CTS_VERIFY_DEFERRED;
+        pc.batch_buffers = 12;  // launches of 4 (depth 2)
+        cts_io_pattern* pat = nullptr;
+        CHECK(cts_io_pattern_create(&pc, eng[7], &pat) == CTS_OK);
+        if (pat != nullptr) {
+            cts_task t{};
+            CHECK(cts_io_pattern_initiate_io(pat, &t) == CTS_OK && t.io_action == CTS_TASK_SEND);
+            CHECK(cts_io_pattern_complete_io(pat, &t, t.buffer_length, 0) == CTS_IO_CONTINUE);
+            g_async_us.store(1000000);  // 0.5-1.5 s (the fake's jitter is 0.5-1.5 x): past the 0.3 s bound
+            for (int k = 0; k < 6; ++k) {  // one launch of 4 in flight, 2 completions queued
+                CHECK(cts_io_pattern_initiate_io(pat, &t) == CTS_OK && t.io_action == CTS_TASK_RECV);
+                std::memcpy(t.buffer + t.buffer_offset, cts_shared_buffer() + t.expected_pattern_offset, t.buffer_length);
+                CHECK(cts_io_pattern_complete_io(pat, &t, t.buffer_length, 0) == CTS_IO_CONTINUE);
+            }
+            const auto t0 = std::chrono::steady_clock::now();
+            const int rc1 = cts_io_pattern_destroy(pat);
+            const double s1 = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+            CHECK(rc1 == CTS_E_HIP && s1 < 0.9);
+            (void)hipGetDevice(&cur);
+            CHECK(cur == 3);
+            g_async_us.store(0);
+            std::this_thread::sleep_for(std::chrono::milliseconds(1700));  // the hung launch ends
+            const int rc2 = cts_io_pattern_destroy(pat);
+            CHECK(rc2 == CTS_OK);
+            std::printf("destroy under a hung launch: CTS_E_HIP after %.3f s, then ok\n", s1);
+        }
+        unsetenv("CTS_PATTERN_DESTROY_WAIT_MS");
+        cts_shared_buffer_release();
     }
 
     // an idle engine's watchdog stops its grid from its own thread (no device current there but its own guard)

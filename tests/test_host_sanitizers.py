@@ -82,7 +82,9 @@ def test_engine_abi_on_eight_fake_devices(san):
     threads that start on device 0; then MediaStream connections (SYNC, and DEFERRED through an emulated frame-sum
     pass) on device 6 with the client timer thread on device 0; then cts_counters_allreduce over the nine engines
     (a stub RCCL, tests/cpp/rccl_stub.cpp) against the host fold and the oracle's sums; then bench.py's
-    single-process leg at eight GPUs (tools/bench_multi.cpp: one native launch thread per engine). Every stream-ordered HIP call and launch must run with
+    single-process leg at eight GPUs (tools/bench_multi.cpp: one native launch thread per engine); then a DEFERRED
+    pattern destroyed under a launch that has not finished (bounded: CTS_E_HIP, the pattern kept until a second
+    destroy). Every stream-ordered HIP call and launch must run with
     its engine's device current, every event must be recorded on a stream of its own device, the caller's device must
     be current again afterwards, and no pinned free may run while a SYNC mailbox grid (emulated by a host thread that
     polls the slot rings as mailbox_kernel does) is resident on the current device: hipHostFree is an implicit
@@ -166,6 +168,7 @@ def test_engine_abi_on_eight_fake_devices(san):
         assert out.returncode == 0, (out.returncode, out.stdout[-2000:], out.stderr[-4000:])
         assert "engine_devices: ok" in out.stdout and "violation" not in out.stderr
         assert "equal to the host fold and the oracle" in out.stdout and "bench_multi: 8 GPUs" in out.stdout
+        assert "destroy under a hung launch: CTS_E_HIP" in out.stdout
         assert "runtime error" not in out.stderr and "WARNING: ThreadSanitizer" not in out.stderr, out.stderr[-4000:]
 
 
