@@ -1,11 +1,13 @@
-"""INTEGRATION.md's reference-side bindings compile against the real headers.
+"""INTEGRATION.md's reference-side bindings and call sequences compile against the real headers.
 
 The C++ blocks of INTEGRATION.md that a ctsTraffic maintainer would paste (Level 1's InitOnceIoPatternCallback and
 VerifyBuffer, the zero-copy VerifyBuffer, Level 2's ctsIoPatternGpu adapter) are extracted from the document and
 compiled with g++ -fsyntax-only against include/, each in its own translation unit. The reference's own types and
 macros they use are declared by a small prelude written here from their documented shapes (ctsIOTask.hpp:37-60,
-ctsIOPattern.h:38-43 and :329, the Windows typedefs): it declares names, it compiles nothing of the reference. A
-renamed entry point or a changed argument list in the ABI fails this test before it strands the document.
+ctsIOPattern.h:38-43 and :329, the Windows typedefs): it declares names, it compiles nothing of the reference. The
+statement fragments (the device-resident sequence, the node counters, the MediaStream receive forms) are compiled as
+the body of a function whose parameters declare their free variables. A renamed entry point or a changed argument
+list in the ABI fails this test before it strands the document.
 """
 import os
 import re
@@ -85,5 +87,60 @@ def test_integration_snippet_compiles(name):
         with open(src, "w", encoding="utf-8") as f:
             f.write(PRELUDE + "\n" + code)
         r = subprocess.run(["g++", "-std=c++17", "-fsyntax-only", "-Wall", "-Wno-unused-function",
+                            "-I", os.path.join(ROOT, "include"), src], capture_output=True, text=True)
+        assert r.returncode == 0, r.stderr[-3000:]
+
+
+# statement fragments: first line -> the parameters that declare their free variables
+FRAGMENTS = {
+    "device_resident": ("cts_engine* e;  cts_engine_create(dev, &e);",
+                        "int dev, const void* arena, uint64_t arena_bytes, const cts_buf_desc* descs, uint32_t n, "
+                        "cts_verify_result* results, uint32_t* conn_first_fail, uint32_t n_conns, hipStream_t stream"),
+    "node_counters": ("// ctsConfig.cpp, where the status line reads g_configSettings->TcpStatusDetails",
+                      "cts_engine* const* engines, const void* const* blocks, void* const* streams, uint32_t gpu_count"),
+    "media_stream_records": ("// descs[i] = {byte_offset of datagram i in the recv arena, completed bytes, 0, 0, 0}",
+                             "const void* arena, uint64_t arena_bytes, const cts_buf_desc* descs, uint32_t n, "
+                             "cts_datagram_record* records, cts_verify_result* results, void* counters, "
+                             "hipStream_t stream, cts_media_stream_client* client, int64_t qpc_now, int64_t qpf"),
+    "media_stream_statuses": ("// receive ring of n datagram slots of `stride` bytes",
+                              "const void* dev_ring, uint64_t ring_bytes, uint32_t stride, const uint32_t* dev_lengths, "
+                              "uint32_t n, cts_datagram_status* dev_status, void* dev_counters, hipStream_t stream, "
+                              "cts_datagram_status* host_status, cts_media_stream_client* client, LARGE_INTEGER qpc, "
+                              "int64_t qpf"),
+    "media_stream_frames": ("cts_frame_window w;",
+                            "const void* dev_ring, uint64_t ring_bytes, uint32_t stride, const uint32_t* dev_lengths, "
+                            "uint32_t n, void* dev_totals, uint64_t* dev_frame_bytes, void* dev_counters, "
+                            "hipStream_t stream, void* host_totals, uint64_t* host_frame_bytes, "
+                            "cts_datagram_status* dev_status, cts_datagram_status* host_status, "
+                            "cts_media_stream_client* client, LARGE_INTEGER qpc, int64_t qpf, uint32_t consumed"),
+}
+
+FRAGMENT_PRELUDE = r"""
+#include <hip/hip_runtime_api.h>
+#include "cts_engine.h"
+#include "cts_media_stream.h"
+typedef struct { int64_t QuadPart; } LARGE_INTEGER;
+struct ctsStatsCounter { void SetValue(uint64_t) {} };
+struct { ctsStatsCounter m_bytesRecv; } TcpStatusDetails;
+extern cts_engine* g_ctsEngine;
+"""
+
+
+def _all_blocks():
+    text = open(os.path.join(ROOT, "INTEGRATION.md"), encoding="utf-8").read()
+    return [code for lang, code in re.findall(r"```(\w*)\n(.*?)```", text, re.S) if lang in ("c", "cpp")]
+
+
+@pytest.mark.parametrize("name", sorted(FRAGMENTS))
+def test_integration_fragment_compiles(name):
+    first, params = FRAGMENTS[name]
+    found = [c for c in _all_blocks() if c.startswith(first)]
+    assert len(found) == 1, "INTEGRATION.md lost the %s block" % name
+    body = "\n".join(l for l in found[0].splitlines() if l.strip() != "...")  # an elision line, not code
+    with tempfile.TemporaryDirectory() as d:
+        src = os.path.join(d, name + ".cpp")
+        with open(src, "w", encoding="utf-8") as f:
+            f.write(FRAGMENT_PRELUDE + "\nvoid snippet(" + params + ")\n{\n" + body + "\n}\n")
+        r = subprocess.run(["g++", "-std=c++17", "-fsyntax-only", "-D__HIP_PLATFORM_AMD__", "-I", "/opt/rocm/include",
                             "-I", os.path.join(ROOT, "include"), src], capture_output=True, text=True)
         assert r.returncode == 0, r.stderr[-3000:]
