@@ -242,14 +242,19 @@ def engines_leg(args, world):
     except subprocess.TimeoutExpired:
         return {"error": "timed out after %d s" % ENGINES_LEG_CAP_S}
     lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
-    if r.returncode != 0 or not lines:
-        return {"error": "exit %d: %s" % (r.returncode, r.stderr.strip().splitlines()[-1:] or "")}
+    err = "exit %d: %s" % (r.returncode, r.stderr.strip().splitlines()[-1:] or "")
+    if not lines:
+        return {"error": err}
     j = json.loads(lines[-1])
-    return {"value": j["value"], "unit": j["unit"], "n_gpus": j["n_gpus"], "ms_per_step": j["ms_per_step"],
-            "per_gpu_GiBps": j.get("per_gpu_GiBps"), "parity": j.get("parity"), "node_counters": j.get("node_counters"),
-            "process_model": "one process, one engine per GPU (cts_engine_create(g)), one host thread + %d streams "
-                             "each, connections by cts_shard_of, counters folded by cts_counters_read_multi and "
-                             "all-reduced over RCCL by cts_counters_allreduce" % args.pipeline_streams}
+    out = {"value": j["value"], "unit": j["unit"], "n_gpus": j["n_gpus"], "ms_per_step": j["ms_per_step"],
+           "per_gpu_GiBps": j.get("per_gpu_GiBps"), "parity": j.get("parity"), "node_counters": j.get("node_counters"),
+           "process_model": "one process, one engine per GPU (cts_engine_create(g)), one host thread + %d streams "
+                            "each, connections by cts_shard_of, counters folded by cts_counters_read_multi_ex and "
+                            "all-reduced over RCCL by cts_counters_allreduce_ex after cts_counters_allreduce_prepare "
+                            "at start-up" % args.pipeline_streams}
+    if r.returncode != 0:  # e.g. an RCCL call that never returned: the line was emitted, the leg still failed
+        out["error"] = err
+    return out
 
 
 class Batch:
@@ -333,6 +338,7 @@ def main():
     dev = "cuda:%d" % gpu
     from ctstraffic_amd import Engine, _lib, workload as W
     from ctstraffic_amd import distributed as D
+    from ctstraffic_amd.types import COUNTER_FIELDS_EX
 
     cpu_group = None
     if world > 1:
@@ -493,7 +499,7 @@ def main():
     if world > 1:
         # the counter all-reduce once before the clock starts (communicator and kernel set-up)
         with torch.cuda.stream(stream):
-            D.allreduce_counters(D.fold_counters(counters))
+            D.allreduce_counters(D.fold_counters(counters, COUNTER_FIELDS_EX))
     torch.cuda.synchronize()
 
     # ---- timed region (headline) --------------------------------------------------------------
@@ -508,9 +514,10 @@ def main():
     t_enq = time.perf_counter()  # the host has issued every launch (how far ahead of the GPU it ran: below)
     ev_b.record(stream)
     if world > 1:
-        # fold the shards on-device and all-reduce the 5 counters over RCCL/xGMI
+        # fold the shards on-device and all-reduce the 6 counters (bytes, buffers, DataError connections) over
+        # RCCL/xGMI
         with torch.cuda.stream(stream):
-            ctr_reduced = D.allreduce_counters(D.fold_counters(counters))
+            ctr_reduced = D.allreduce_counters(D.fold_counters(counters, COUNTER_FIELDS_EX))
     torch.cuda.synchronize()
     barrier()
     t1 = time.perf_counter()
@@ -530,11 +537,18 @@ def main():
     if avg_kernel_s is None:
         avg_kernel_s = pipe_launch_s
     local_ctr = engine.read_counters(counters)
+    # the DataError count: every arena's slots were emptied before the timed region, so its first launch claims
+    # the batch's failed connections and the later rotations find them claimed (one per connection,
+    # ctsSocketState.cpp:221-228)
+    conns_failed = engine.read_counters_ex(counters)["connections_failed"]
+    exp_conns = int((B.exp_cff != 0xFFFFFFFF).sum()) * R
     outputs_ok = B.outputs_ok()
-    parity_ok = ser_ok and outputs_ok and local_ctr == {k: v * launches for k, v in exp_ctr.items()}
+    parity_ok = (ser_ok and outputs_ok and local_ctr == {k: v * launches for k, v in exp_ctr.items()} and
+                 conns_failed == exp_conns)
     if world > 1:
         glob = D.counters_dict(ctr_reduced)
         exp_glob = {f: exp_ctr[f] * launches * world for f in exp_ctr}
+        exp_glob["connections_failed"] = exp_conns * world
         parity_ok = parity_ok and glob == exp_glob
         ok_t = torch.tensor([1 if parity_ok else 0], device=dev)
         dist.all_reduce(ok_t, op=dist.ReduceOp.MIN)
@@ -612,7 +626,8 @@ def main():
                 "host_cpus_pinned": len(near),
                 "parallelism": "%d rank(s), one config-2 batch of its own connections each, no data-path "
                                "collective; %s" % (world, "one rank: no collective" if world == 1 else
-                                                   "%s all-reduce of the 5 counters closes the timed region"
+                                                   "%s all-reduce of the 6 counters (bytes, buffers, DataError connections) closes the timed "
+                                                   "region"
                                                    % ("RCCL" if args.dist_backend == "nccl" else args.dist_backend)),
             },
             "roofline": {
@@ -647,7 +662,8 @@ def main():
             },
             "cpu_baseline": cpu,
             "parity": {"counters_match_expected": bool(parity_ok), "records_and_first_fail_match": bool(outputs_ok),
-                       "counters": local_ctr},
+                       "counters": {**local_ctr, "connections_failed": conns_failed},
+                       "connections_failed_expected": exp_conns},
         }
         line["per_rank_GiBps"] = [round(x, 1) for x in per_rank]
         line.update({k: v for k, v in diag.items() if k != "per_rank_avg_kernel_us"})
@@ -717,8 +733,11 @@ def main_engines(args, torch):
     verifies a config-2 batch of its own connections (weak scaling, like the torch.distributed leg);
     value = all bytes / (wall from the common start to the last GPU's end).
     --engines-same-gpu puts every engine on GPU 0 (a rehearsal of the code path on a one-GPU box)."""
+    import threading
+
     from ctstraffic_amd import Engine, workload as W
-    from ctstraffic_amd.engine import counters_allreduce, counters_allreduce_release, counters_read_multi
+    from ctstraffic_amd.engine import (counters_allreduce_ex, counters_allreduce_prepare, counters_allreduce_release,
+                                       counters_allreduce_setup_times, counters_read_multi, counters_read_multi_ex)
 
     G = args.engines
     same = args.engines_same_gpu
@@ -747,6 +766,32 @@ def main_engines(args, torch):
         keep.append(k)
     for g in range(G):
         torch.cuda.synchronize(0 if same else g)
+    engs, blocks = [c[0] for c in ctx], [c[1].counters for c in ctx]
+    red = {}
+
+    def bounded(fn):
+        """fn() on its own thread, joined for at most ALLREDUCE_CAP_S: a collective that never returns must not
+        cost the leg's line. True when it returned."""
+        th = threading.Thread(target=fn, daemon=True)
+        th.start()
+        th.join(ALLREDUCE_CAP_S)
+        return not th.is_alive()
+
+    def prepare():
+        # the node's RCCL clique built next to cts_engine_create, as the status timer's first tick (t = 0,
+        # ctsTraffic.cpp:107-113) reads the counters: not inside the first counter read
+        try:
+            t = time.perf_counter()
+            counters_allreduce_prepare(engs)
+            red["prepare_ms"] = round((time.perf_counter() - t) * 1e3, 2)
+            red["allreduce_setup_breakdown_ms"] = {k: (round(v, 3) if isinstance(v, float) else v)
+                                                   for k, v in counters_allreduce_setup_times().items()}
+        except Exception as ex:  # reported, not fatal: the verify leg is the measurement
+            red["allreduce_error"] = repr(ex)
+
+    hung = not bounded(prepare)
+    if hung:
+        red["allreduce_error"] = "cts_counters_allreduce_prepare did not return within %d s" % ALLREDUCE_CAP_S
     t0, t1, ts = (ctypes.c_double * G)(), (ctypes.c_double * G)(), ctypes.c_double()
 
     def run(k):
@@ -757,41 +802,39 @@ def main_engines(args, torch):
     run(max(args.warmup, 1))
     for e, B, _, _ in ctx:
         e.reset_counters(B.counters)
+        for c in B.cff:  # empty slots: the timed launches claim every failed connection again
+            c.fill_(-1)
     for g in range(G):
         torch.cuda.synchronize(0 if same else g)
     run(K)
     elapsed = max(t1) - min(min(t0), ts.value)
     per_gpu = [ctx[g][1].bytes_per_launch * R * K / (t1[g] - t0[g]) / GIB for g in range(G)]
-    engs, blocks = [c[0] for c in ctx], [c[1].counters for c in ctx]
-    folded = counters_read_multi(engs, blocks)
-    per = [c[0].read_counters(c[1].counters) for c in ctx]
+    folded = counters_read_multi_ex(engs, blocks)
+    per = [c[0].read_counters_ex(c[1].counters) for c in ctx]
     # after the timed region: the node-wide counters both ways, the host fold and the RCCL all-reduce issued from
-    # the C ABI (cts_counters_allreduce: per-device fold + ncclAllReduce sum u64 x 5 per device), each timed
+    # the C ABI (cts_counters_allreduce_ex: per-device fold + ncclAllReduce sum u64 x 6 per device), each timed
     fold_us = _median_us(lambda: counters_read_multi(engs, blocks), 20)
-    red = {}
 
     def allreduce_timing():
         try:
             t = time.perf_counter()
-            red["reduced"] = counters_allreduce(engs, blocks)  # the first call creates the communicators
-            red["allreduce_first_call_ms"] = round((time.perf_counter() - t) * 1e3, 2)
-            red["allreduce_counters_us"] = round(_median_us(lambda: counters_allreduce(engs, blocks), 20), 1)
+            red["reduced"] = counters_allreduce_ex(engs, blocks)  # the first read: the prepared clique's
+            red["allreduce_first_call_us"] = round((time.perf_counter() - t) * 1e6, 1)
+            red["allreduce_counters_us"] = round(_median_us(lambda: counters_allreduce_ex(engs, blocks), 20), 1)
             counters_allreduce_release()
         except Exception as ex:  # reported, not fatal: the verify leg above is the measurement
             red["allreduce_error"] = repr(ex)
 
-    # on its own thread with a bound: a collective that never returns must not cost the leg's line
-    import threading
-
-    th = threading.Thread(target=allreduce_timing, daemon=True)
-    th.start()
-    th.join(ALLREDUCE_CAP_S)
-    hung = th.is_alive()
-    if hung:
-        red["allreduce_error"] = "cts_counters_allreduce did not return within %d s" % ALLREDUCE_CAP_S
+    if not hung and "allreduce_error" not in red:
+        hung = not bounded(allreduce_timing)
+        if hung:
+            red["allreduce_error"] = "cts_counters_allreduce_ex did not return within %d s" % ALLREDUCE_CAP_S
     reduced = red.pop("reduced", None)
     total = sum(c[1].bytes_per_launch for c in ctx) * R * K
     exp = {k: sum(c[1].exp_ctr[k] for c in ctx) * K * R for k in ctx[0][1].exp_ctr}
+    # each arena's slots were emptied before the timed region: its first launch claims the batch's failed
+    # connections, the later rotations find them claimed (ctsSocketState.cpp:221-228 counts a connection once)
+    exp["connections_failed"] = sum(int((c[1].exp_cff != 0xFFFFFFFF).sum()) for c in ctx) * R
     line = {
         "metric": METRIC, "value": round(total / elapsed / GIB, 2), "unit": "GiB/s", "n_gpus": 1 if same else G,
         "steps": K, "warmup": args.warmup, "ms_per_step": round(elapsed / K * 1e3, 4), "higher_is_better": True,
@@ -811,9 +854,10 @@ def main_engines(args, torch):
                           "devices": [c[0].device_ordinal() for c in ctx]},
     }
     emit(line)
-    if hung:  # the RCCL call still holds the devices: leave without tearing down under it
+    if hung:  # the RCCL call still holds the devices: leave without tearing down under it, and say it failed
+        sys.stdout.flush()
         sys.stderr.flush()
-        os._exit(0)
+        os._exit(3)
     for e, B, streams, _ in ctx:
         for s in streams:
             e.stream_destroy(s)
@@ -868,15 +912,31 @@ def run_extras(engine, torch, W, w, arenas, descs, dev, want):
         t = _time_kernel(torch, lambda i: engine.fill(arenas[i % R], descs, max_length_hint=w.max_length), 100)
         out["fill_GiBps"] = round(nbytes / t / GIB, 1)
         out["fill_GBps"] = round(nbytes / t / 1e9, 1)
-        # fused view: fill + verify of the same batch back to back
+        # config 2's "fill+verify" as HBM traffic: fill arena i, then verify arena i + R/2, which was filled R/2
+        # launch pairs earlier (R/2 x 256 MiB written and as much read since: its lines have left the 256 MB
+        # Infinity Cache). Beside it the series bound of the two kernels' own rotated rates, and the same-arena
+        # pair, whose verify reads what the fill just left in the Infinity Cache (labelled _mall).
         ctr = engine.new_counters()
+        t_ver = _time_kernel(torch, lambda i: engine.verify(arenas[i % R], descs, max_length_hint=w.max_length,
+                                                           counters=ctr), 100)
 
         def fv(i):
             engine.fill(arenas[i % R], descs, max_length_hint=w.max_length)
+            engine.verify(arenas[(i + R // 2) % R], descs, max_length_hint=w.max_length, counters=ctr)
+
+        def fv_same(i):
+            engine.fill(arenas[i % R], descs, max_length_hint=w.max_length)
             engine.verify(arenas[i % R], descs, max_length_hint=w.max_length, counters=ctr)
 
-        t = _time_kernel(torch, fv, 50)
-        out["fill_then_verify_GiBps_verified"] = round(nbytes / t / GIB, 1)
+        t_fv = _time_kernel(torch, fv, 50)
+        t_same = _time_kernel(torch, fv_same, 50)
+        out["verify_GBps_rotated"] = round(nbytes / t_ver / 1e9, 1)
+        out["fill_then_verify_GiBps_verified"] = round(nbytes / t_fv / GIB, 1)
+        out["fill_then_verify_series_bound_GiBps"] = round(nbytes / (t + t_ver) / GIB, 1)
+        out["fill_then_verify_pair"] = ("fill arena i, verify arena i+%d of %d (filled %d pairs earlier: HBM); "
+                                        "series bound = verified bytes / (fill time + verify time), each rotated"
+                                        % (R // 2, R, R // 2))
+        out["fill_then_verify_mall_GiBps_verified"] = round(nbytes / t_same / GIB, 1)
         for a in arenas:  # restore the corruption plan
             pos = torch.from_numpy(w.corrupt_abs_offsets()).to(dev)
             a[pos] = a[pos] ^ torch.from_numpy(w.corrupt_xor).to(dev)
@@ -1147,9 +1207,17 @@ def loopback_media_stream_oracle():
         return {"error": repr(e)}
 
 
-def cpu_baseline(arena, w, seconds):
+# the BASELINE configs the CPU baseline times (BASELINE.md promises the full set or a labelled subset)
+CPU_CONFIGS_TIMED = ["config1-loopback", "config2", "config3-slice(1/16)"]
+CPU_CONFIGS_NOTE = ("configs 4 and 5 are not timed on the CPU: their buffers are 64 KiB completions of per-connection "
+                    "streams, the per-byte work of config 2 (the same VerifyBuffer over 64 KiB at a prefix-sum offset), "
+                    "so config 2's GiB/s per core stands for them; config 3 is timed on its first 1 M of 16 M datagrams")
+
+
+def cpu_baseline(arena, w, seconds, loopback=True):
     """The oracle (g++/gcc restatement of VerifyBuffer, RtlCompareMemory semantics) on this host's
-    cores over a host copy of the same batch. Bounded: ~`seconds` per leg."""
+    cores over a host copy of the same batch. Bounded: ~`seconds` per leg. loopback=False skips the config-1
+    loopback leg (the CPU tests)."""
     import oracle
 
     host = arena.cpu().numpy()
@@ -1169,6 +1237,8 @@ def cpu_baseline(arena, w, seconds):
     best = max(legs, key=lambda k: legs[k])
     loop = None
     try:
+        if not loopback:
+            raise RuntimeError("skipped (loopback=False)")
         # the same config-1 loopback run with the oracle answering VerifyBuffer on the CPU (one
         # verifying thread per connection), i.e. the reference's own arrangement
         from ctstraffic_amd import _pattern_abi as PA
@@ -1215,6 +1285,8 @@ def cpu_baseline(arena, w, seconds):
         "cgroup_cpu_quota": quota,
         "cpu_model": model,
         "loopback_config1": loop,
+        "configs_timed": list(CPU_CONFIGS_TIMED),
+        "configs_note": CPU_CONFIGS_NOTE,
     }
 
 

@@ -31,6 +31,7 @@ CTS_E_HIP = -2
 CTS_E_NOMEM = -3
 CTS_E_NO_DEVICE = -4
 CTS_E_UNAVAILABLE = -5
+CTS_E_TIMEOUT = -6
 
 PATTERN_PERIOD = 65536
 UDP_DATA_HEADER_LENGTH = 26
@@ -76,6 +77,29 @@ class CtsCounters(ctypes.Structure):
 
     def as_dict(self) -> dict:
         return {f: int(getattr(self, f)) for f, _ in self._fields_}
+
+
+class CtsCountersEx(ctypes.Structure):
+    """cts_counters_ex: cts_counters plus the DataError count (connections with a failing buffer)."""
+    _fields_ = CtsCounters._fields_ + [("connections_failed", ctypes.c_uint64)]
+
+    def as_dict(self) -> dict:
+        return {f: int(getattr(self, f)) for f, _ in self._fields_}
+
+
+class CtsAllreduceSetup(ctypes.Structure):
+    """cts_allreduce_setup: where the newest RCCL clique's set-up time went (ms)."""
+    _fields_ = [
+        ("rccl_load_ms", ctypes.c_double),
+        ("slots_ms", ctypes.c_double),
+        ("comm_init_ms", ctypes.c_double),
+        ("first_allreduce_ms", ctypes.c_double),
+        ("devices", ctypes.c_uint32),
+        ("prepared", ctypes.c_uint32),
+    ]
+
+    def as_dict(self) -> dict:
+        return {f: (float if t is ctypes.c_double else int)(getattr(self, f)) for f, t in self._fields_}
 
 
 class CtsVerifyResult(ctypes.Structure):
@@ -126,6 +150,13 @@ def _declare(L: ctypes.CDLL) -> None:
         "cts_counters_allreduce": ([ctypes.POINTER(P), ctypes.POINTER(P), ctypes.POINTER(P), u32,
                                     ctypes.POINTER(CtsCounters)], i32),
         "cts_counters_allreduce_release": ([], i32),
+        "cts_counters_read_ex": ([P, P, ctypes.POINTER(CtsCountersEx), P], i32),
+        "cts_counters_read_multi_ex": ([ctypes.POINTER(P), ctypes.POINTER(P), ctypes.POINTER(P), u32,
+                                        ctypes.POINTER(CtsCountersEx)], i32),
+        "cts_counters_allreduce_ex": ([ctypes.POINTER(P), ctypes.POINTER(P), ctypes.POINTER(P), u32,
+                                       ctypes.POINTER(CtsCountersEx)], i32),
+        "cts_counters_allreduce_prepare": ([ctypes.POINTER(P), u32], i32),
+        "cts_counters_allreduce_setup_times": ([ctypes.POINTER(CtsAllreduceSetup)], i32),
         "cts_verify_host": ([P, P, u32, u32, ctypes.POINTER(CtsVerifyResult)], i32),
         "cts_verify_mapped": ([P, P, u32, u32, ctypes.POINTER(CtsVerifyResult)], i32),
         "cts_mailbox_launches": ([P], u64),

@@ -4,20 +4,23 @@
 // ctsTraffic is one process per host with many IO threads; its byte/error statistics are process-global atomics
 // (ctsStatistics.hpp:87-198, read by ctsConfig::TcpStatusDetails, ctsConfig.h:415-417). With the verify on N GPUs
 // each engine's counters live in its own device block. This entry point folds every block on its own device (one
-// 64-thread launch, counters_fold_kernel), reduces the five sums across the devices with one ncclAllReduce (sum,
-// ncclUint64, count 5) per device inside ncclGroupStart/End over the xGMI links, and
+// 64-thread launch, counters_fold_kernel), reduces the six sums (ctsStatsTracking's bytes and buffers, and the
+// DataError count of ConnectionStatusDetails, ctsSocketState.cpp:221-228) across the devices with one ncclAllReduce
+// (sum, ncclUint64, count 6) per device inside ncclGroupStart/End over the xGMI links, and
 // reads the result back. Every device's copy is read and compared: a reduction that disagrees is an error.
 //
 // RCCL is loaded on first use (dlopen of librccl.so.1, or $CTS_RCCL_LIBRARY), so the engine library itself does
 // not pull the 570 MB RCCL image into every process that only verifies; inside a PyTorch process the soname
 // resolves to the RCCL torch already loaded. One communicator clique (ncclCommInitAll) is kept per set of
-// devices and reused until cts_counters_allreduce_release. Calls are serialised by one lock (a counter read
-// happens once per status interval, not per IO).
+// devices and reused until cts_counters_allreduce_release; cts_counters_allreduce_prepare builds it (and runs its
+// first all-reduce, which carries RCCL's own first-collective set-up) before the status timer's first tick. Calls
+// are serialised by one lock (a counter read happens once per status interval, not per IO).
 #include <dlfcn.h>
 #include <hip/hip_runtime_api.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -40,8 +43,8 @@ struct Rccl {
     ncclResult_t (*group_end)() = nullptr;
 };
 
-// One communicator per device of a device set, plus a 5 x u64 device slot each (the fold's output and the
-// all-reduce's in-place buffer).
+// One communicator per device of a device set, plus a device slot each: kCounterSlots u64 (the fold's output and the
+// all-reduce's in-place buffer), then a zeroed counter block of the device layout that the set-up's dry run folds.
 struct Clique {
     std::vector<int> devices;
     std::vector<ncclComm_t> comms;
@@ -51,6 +54,12 @@ struct Clique {
 std::mutex g_mu;  // guards everything below
 Rccl g_rccl;
 std::vector<std::unique_ptr<Clique>> g_cliques;
+cts_allreduce_setup g_setup{0.0, 0.0, 0.0, 0.0, 0u, 0u};  // the newest clique's set-up times
+
+double ms_since(std::chrono::steady_clock::time_point t0)
+{
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
 
 struct DeviceGuard {
     int prev = -1;
@@ -66,10 +75,13 @@ struct DeviceGuard {
     }
 };
 
-// Resolves the RCCL entry points once; a failed load is retried on the next call.
-bool load_rccl()
+// Resolves the RCCL entry points once; a failed load is retried on the next call. *load_ms: the time this call
+// spent loading (0 when RCCL was already loaded).
+bool load_rccl(double* load_ms)
 {
+    *load_ms = 0.0;
     if (g_rccl.handle != nullptr) return true;
+    const auto t0 = std::chrono::steady_clock::now();
     const char* env = std::getenv("CTS_RCCL_LIBRARY");
     void* h = nullptr;
     if (env != nullptr && *env != 0) {
@@ -91,6 +103,7 @@ bool load_rccl()
         return false;
     }
     g_rccl = r;
+    *load_ms = ms_since(t0);
     return true;
 }
 
@@ -107,67 +120,102 @@ void destroy_clique(Clique& c)
     c.sums.clear();
 }
 
-// The clique of exactly these devices (in this order), created on first use.
-int clique_for(const std::vector<int>& devices, Clique** out)
+// One grouped all-reduce (sum, u64 x kCounterCount, in place on every device's slot), each device's op on
+// streams[k]. One thread drives every rank of the clique, so a multi-rank clique must be grouped.
+int grouped_allreduce(Clique& c, const std::vector<hipStream_t>& streams)
+{
+    if (g_rccl.group_start() != ncclSuccess) return CTS_E_HIP;
+    ncclResult_t r = ncclSuccess;
+    for (size_t k = 0; k < c.devices.size() && r == ncclSuccess; ++k)
+        r = g_rccl.all_reduce(c.sums[k], c.sums[k], cts::kCounterCount, ncclUint64, ncclSum, c.comms[k], streams[k]);
+    const ncclResult_t re = g_rccl.group_end();
+    return (r != ncclSuccess || re != ncclSuccess) ? CTS_E_HIP : CTS_OK;
+}
+
+constexpr size_t kSlotWords = cts::kCounterSlots + (size_t)CTS_COUNTER_SHARDS * cts::kCounterSlots;
+
+// The clique of exactly these devices (in this order), created on first use: slots, communicators, and one dry run
+// of a counter read on each device's null stream (the fold of a zeroed block, the grouped all-reduce, the copy back):
+// RCCL sets up its first collective's channels and kernels in it, and the fold kernel and the device-to-host copy
+// have run once, so the first real read costs what every later one does. Each step is timed into g_setup. load_ms:
+// what this call spent loading RCCL.
+int clique_for(const std::vector<int>& devices, double load_ms, bool prepared, Clique** out)
 {
     for (auto& c : g_cliques)
         if (c->devices == devices) {
             *out = c.get();
             return CTS_OK;
         }
+    cts_allreduce_setup t{load_ms, 0.0, 0.0, 0.0, (uint32_t)devices.size(), prepared ? 1u : 0u};
     std::unique_ptr<Clique> c(new (std::nothrow) Clique());
     if (!c) return CTS_E_NOMEM;
     c->devices = devices;
     c->comms.assign(devices.size(), nullptr);
     c->sums.assign(devices.size(), nullptr);
+    auto t0 = std::chrono::steady_clock::now();
     for (size_t k = 0; k < devices.size(); ++k) {
         DeviceGuard g(devices[k]);
         void* p = nullptr;
         // on the device's null stream, which the engines' non-blocking streams never wait for; the caller's
         // leading stream uses the slot only after the synchronize below
-        if (!g.ok || hipMallocAsync(&p, 5 * sizeof(uint64_t), nullptr) != hipSuccess) {
+        if (!g.ok || hipMallocAsync(&p, kSlotWords * sizeof(uint64_t), nullptr) != hipSuccess) {
             destroy_clique(*c);
             return g.ok ? CTS_E_NOMEM : CTS_E_HIP;
         }
         c->sums[k] = static_cast<uint64_t*>(p);
-        if (hipStreamSynchronize(nullptr) != hipSuccess) {
+        if (hipMemsetAsync(p, 0, kSlotWords * sizeof(uint64_t), nullptr) != hipSuccess ||
+            hipStreamSynchronize(nullptr) != hipSuccess) {
             destroy_clique(*c);
             return CTS_E_HIP;
         }
     }
+    t.slots_ms = ms_since(t0);
     int prev = -1;
     (void)hipGetDevice(&prev);
+    t0 = std::chrono::steady_clock::now();
     const ncclResult_t r = g_rccl.comm_init_all(c->comms.data(), (int)devices.size(), devices.data());
+    t.comm_init_ms = ms_since(t0);
     if (prev >= 0) (void)hipSetDevice(prev);
     if (r != ncclSuccess) {
         std::fill(c->comms.begin(), c->comms.end(), nullptr);
         destroy_clique(*c);
         return CTS_E_HIP;
     }
+    t0 = std::chrono::steady_clock::now();
+    int rc = CTS_OK;
+    for (size_t k = 0; k < devices.size() && rc == CTS_OK; ++k) {
+        DeviceGuard g(devices[k]);
+        if (!g.ok || cts::launch_counters_fold(c->sums[k] + cts::kCounterSlots, c->sums[k], false, nullptr) != hipSuccess)
+            rc = CTS_E_HIP;
+    }
+    if (rc == CTS_OK) rc = grouped_allreduce(*c, std::vector<hipStream_t>(devices.size(), nullptr));
+    for (size_t k = 0; k < devices.size() && rc == CTS_OK; ++k) {
+        DeviceGuard g(devices[k]);
+        uint64_t h[cts::kCounterCount];
+        if (!g.ok || hipMemcpyAsync(h, c->sums[k], sizeof(h), hipMemcpyDeviceToHost, nullptr) != hipSuccess ||
+            hipStreamSynchronize(nullptr) != hipSuccess)
+            rc = CTS_E_HIP;
+        for (int j = 0; j < cts::kCounterCount && rc == CTS_OK; ++j)
+            if (h[j] != 0) rc = CTS_E_HIP;  // zeros folded and summed must stay zeros
+    }
+    t.first_allreduce_ms = ms_since(t0);
+    if (rc != CTS_OK) {
+        destroy_clique(*c);
+        return rc;
+    }
+    g_setup = t;
     *out = c.get();
     g_cliques.push_back(std::move(c));
     return CTS_OK;
 }
 
-}  // namespace
-
-extern "C" {
-
-int cts_counters_allreduce(cts_engine* const* engines, const void* const* dev_counters, void* const* streams,
-                           uint32_t n, cts_counters* out)
+// engines grouped by device: devices in first-appearance order, leader[k] = index of device k's first engine
+int group_by_device(cts_engine* const* engines, uint32_t n, std::vector<int>& dev_of, std::vector<int>& devices,
+                    std::vector<uint32_t>& leader)
 {
-    if (out == nullptr || (n > 0 && (engines == nullptr || dev_counters == nullptr))) return CTS_E_INVALID;
-    if (n == 0) {
-        *out = cts_counters{0, 0, 0, 0, 0};
-        return CTS_OK;
-    }
-    // engines grouped by device: the first engine of a device leads (its stream carries the device's folds and
-    // its all-reduce); the others' blocks are folded into the same slot
-    std::vector<int> dev_of(n);
-    std::vector<int> devices;
-    std::vector<uint32_t> leader;  // per device: index of its first engine
+    dev_of.assign(n, -1);
     for (uint32_t i = 0; i < n; ++i) {
-        if (engines[i] == nullptr || dev_counters[i] == nullptr) return CTS_E_INVALID;
+        if (engines[i] == nullptr) return CTS_E_INVALID;
         const int d = cts_engine_device(engines[i]);
         if (d < 0) return CTS_E_INVALID;
         dev_of[i] = d;
@@ -176,11 +224,34 @@ int cts_counters_allreduce(cts_engine* const* engines, const void* const* dev_co
             leader.push_back(i);
         }
     }
-    std::lock_guard<std::mutex> lk(g_mu);
-    if (!load_rccl()) return CTS_E_UNAVAILABLE;
-    Clique* c = nullptr;
-    int rc = clique_for(devices, &c);
+    return CTS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int cts_counters_allreduce_ex(cts_engine* const* engines, const void* const* dev_counters, void* const* streams,
+                              uint32_t n, cts_counters_ex* out)
+{
+    if (out == nullptr || (n > 0 && (engines == nullptr || dev_counters == nullptr))) return CTS_E_INVALID;
+    if (n == 0) {
+        *out = cts_counters_ex{0, 0, 0, 0, 0, 0};
+        return CTS_OK;
+    }
+    // the first engine of a device leads (its stream carries the device's folds and its all-reduce); the others'
+    // blocks are folded into the same slot
+    std::vector<int> dev_of, devices;
+    std::vector<uint32_t> leader;
+    for (uint32_t i = 0; i < n; ++i)
+        if (dev_counters[i] == nullptr) return CTS_E_INVALID;
+    int rc = group_by_device(engines, n, dev_of, devices, leader);
     if (rc != CTS_OK) return rc;
+    std::lock_guard<std::mutex> lk(g_mu);
+    double load_ms = 0.0;
+    if (!load_rccl(&load_ms)) return CTS_E_UNAVAILABLE;
+    Clique* c = nullptr;
+    if ((rc = clique_for(devices, load_ms, false, &c)) != CTS_OK) return rc;
     const size_t D = devices.size();
     std::vector<hipStream_t> lead_stream(D);
     for (size_t k = 0; k < D; ++k) lead_stream[k] = streams ? static_cast<hipStream_t>(streams[leader[k]]) : nullptr;
@@ -199,29 +270,53 @@ int cts_counters_allreduce(cts_engine* const* engines, const void* const* dev_co
             first = false;
         }
     }
-    // 2. one all-reduce per device, grouped (one thread drives every rank of the clique)
-    if (g_rccl.group_start() != ncclSuccess) return CTS_E_HIP;
-    ncclResult_t r = ncclSuccess;
-    for (size_t k = 0; k < D && r == ncclSuccess; ++k)
-        r = g_rccl.all_reduce(c->sums[k], c->sums[k], 5, ncclUint64, ncclSum, c->comms[k], lead_stream[k]);
-    const ncclResult_t re = g_rccl.group_end();
-    if (r != ncclSuccess || re != ncclSuccess) return CTS_E_HIP;
+    // 2. one all-reduce per device, grouped
+    if ((rc = grouped_allreduce(*c, lead_stream)) != CTS_OK) return rc;
     // 3. every device's copy back; they must agree
-    uint64_t first_copy[5] = {0, 0, 0, 0, 0};
+    uint64_t first_copy[cts::kCounterCount] = {};
     for (size_t k = 0; k < D; ++k) {
         DeviceGuard g(devices[k]);
-        uint64_t h[5];
+        uint64_t h[cts::kCounterCount];
         if (!g.ok || hipMemcpyAsync(h, c->sums[k], sizeof(h), hipMemcpyDeviceToHost, lead_stream[k]) != hipSuccess ||
             hipStreamSynchronize(lead_stream[k]) != hipSuccess)
             return CTS_E_HIP;
         if (k == 0) std::memcpy(first_copy, h, sizeof(h));
         else if (std::memcmp(first_copy, h, sizeof(h)) != 0) return CTS_E_HIP;
     }
-    out->bytes_checked = first_copy[cts::kBytesChecked];
-    out->bytes_ok = first_copy[cts::kBytesOk];
-    out->buffers_checked = first_copy[cts::kBuffersChecked];
-    out->buffers_failed = first_copy[cts::kBuffersFailed];
-    out->mismatched_bytes = first_copy[cts::kMismatchedBytes];
+    *out = cts::counters_ex_of(first_copy);
+    return CTS_OK;
+}
+
+int cts_counters_allreduce(cts_engine* const* engines, const void* const* dev_counters, void* const* streams,
+                           uint32_t n, cts_counters* out)
+{
+    if (out == nullptr) return CTS_E_INVALID;
+    cts_counters_ex x{};
+    const int rc = cts_counters_allreduce_ex(engines, dev_counters, streams, n, &x);
+    if (rc == CTS_OK) *out = cts::counters_of(x);
+    return rc;
+}
+
+int cts_counters_allreduce_prepare(cts_engine* const* engines, uint32_t n)
+{
+    if (n > 0 && engines == nullptr) return CTS_E_INVALID;
+    if (n == 0) return CTS_OK;
+    std::vector<int> dev_of, devices;
+    std::vector<uint32_t> leader;
+    int rc = group_by_device(engines, n, dev_of, devices, leader);
+    if (rc != CTS_OK) return rc;
+    std::lock_guard<std::mutex> lk(g_mu);
+    double load_ms = 0.0;
+    if (!load_rccl(&load_ms)) return CTS_E_UNAVAILABLE;
+    Clique* c = nullptr;
+    return clique_for(devices, load_ms, true, &c);
+}
+
+int cts_counters_allreduce_setup_times(cts_allreduce_setup* out)
+{
+    if (out == nullptr) return CTS_E_INVALID;
+    std::lock_guard<std::mutex> lk(g_mu);
+    *out = g_setup;
     return CTS_OK;
 }
 

@@ -544,6 +544,7 @@ const char* cts_status_string(int status)
     case CTS_E_NOMEM: return "out of memory";
     case CTS_E_NO_DEVICE: return "no such HIP device";
     case CTS_E_UNAVAILABLE: return "runtime library unavailable (RCCL)";
+    case CTS_E_TIMEOUT: return "timed out (nothing freed; retry)";
     default: return "unknown status";
     }
 }
@@ -923,7 +924,7 @@ int cts_counters_reset(cts_engine* e, void* dev_counters, void* stream)
     return hip_status(hipMemsetAsync(dev_counters, 0, cts_counters_device_bytes(), static_cast<hipStream_t>(stream)));
 }
 
-int cts_counters_read(cts_engine* e, const void* dev_counters, cts_counters* out, void* stream)
+int cts_counters_read_ex(cts_engine* e, const void* dev_counters, cts_counters_ex* out, void* stream)
 {
     if (e == nullptr || dev_counters == nullptr || out == nullptr) return CTS_E_INVALID;
     DeviceGuard g(e->device);
@@ -933,15 +934,20 @@ int cts_counters_read(cts_engine* e, const void* dev_counters, cts_counters* out
     if (hipMemcpyAsync(h, dev_counters, cts_counters_device_bytes(), hipMemcpyDeviceToHost, s) != hipSuccess)
         return CTS_E_HIP;
     if (hipStreamSynchronize(s) != hipSuccess) return CTS_E_HIP;
-    uint64_t v[5] = {0, 0, 0, 0, 0};
+    uint64_t v[cts::kCounterCount] = {};
     for (uint32_t sh = 0; sh < CTS_COUNTER_SHARDS; ++sh)
-        for (int k = 0; k < 5; ++k) v[k] += h[sh * cts::kCounterSlots + k];
-    out->bytes_checked = v[cts::kBytesChecked];
-    out->bytes_ok = v[cts::kBytesOk];
-    out->buffers_checked = v[cts::kBuffersChecked];
-    out->buffers_failed = v[cts::kBuffersFailed];
-    out->mismatched_bytes = v[cts::kMismatchedBytes];
+        for (int k = 0; k < cts::kCounterCount; ++k) v[k] += h[sh * cts::kCounterSlots + k];
+    *out = cts::counters_ex_of(v);
     return CTS_OK;
+}
+
+int cts_counters_read(cts_engine* e, const void* dev_counters, cts_counters* out, void* stream)
+{
+    if (out == nullptr) return CTS_E_INVALID;
+    cts_counters_ex x{};
+    const int rc = cts_counters_read_ex(e, dev_counters, &x, stream);
+    if (rc == CTS_OK) *out = cts::counters_of(x);
+    return rc;
 }
 
 int cts_host_alloc(cts_engine* e, uint64_t bytes, void** host_ptr, void** dev_view)

@@ -12,8 +12,31 @@ namespace cts {
 // Device counter block: CTS_COUNTER_SHARDS rows of 8 u64 (64 B each); a
 // workgroup adds its totals to row (blockIdx.x % CTS_COUNTER_SHARDS) so the
 // adds of a 2048-block grid spread over 64 lines instead of one.
-constexpr int kCounterSlots = 8;  // 5 used, padded to one 64-byte line
-enum CounterSlot { kBytesChecked = 0, kBytesOk = 1, kBuffersChecked = 2, kBuffersFailed = 3, kMismatchedBytes = 4 };
+constexpr int kCounterSlots = 8;  // kCounterCount used, padded to one 64-byte line
+enum CounterSlot {
+    kBytesChecked = 0,
+    kBytesOk = 1,
+    kBuffersChecked = 2,
+    kBuffersFailed = 3,
+    kMismatchedBytes = 4,
+    // conn_first_fail slots a launch moved off 0xFFFFFFFF: the atomicMin that returned the empty value is the
+    // connection's first recorded failure, so each failed connection counts once however many of its buffers fail
+    // and however many launches share the slot array (ctsSocketState.cpp:221-228, m_protocolErrorCount)
+    kConnectionsFailed = 5
+};
+constexpr int kCounterCount = 6;
+static_assert(kCounterCount <= kCounterSlots, "counters fit a shard line");
+
+// The folded sums v[kCounterCount] as the ABI's structs.
+inline cts_counters_ex counters_ex_of(const uint64_t* v)
+{
+    return cts_counters_ex{v[kBytesChecked],  v[kBytesOk],         v[kBuffersChecked],
+                           v[kBuffersFailed], v[kMismatchedBytes], v[kConnectionsFailed]};
+}
+inline cts_counters counters_of(const cts_counters_ex& x)
+{
+    return cts_counters{x.bytes_checked, x.bytes_ok, x.buffers_checked, x.buffers_failed, x.mismatched_bytes};
+}
 
 // One kernel per path. CTS_ATTR_VERIFY_VARIANT / SMALL_VARIANT / MS_VARIANT report which one, by the number it
 // had among the alternatives measured in rounds 1-4; setting any other value is CTS_E_INVALID.
@@ -100,7 +123,7 @@ struct MailStarts {
 hipError_t launch_mailbox(const MailSlot* slots, MailPart* parts, uint32_t per_group, const MailStarts& starts,
                           uint32_t groups, uint64_t idle_ticks, hipStream_t stream, uint64_t delay_ticks = 0);
 
-// out[0..5) = (accumulate ? out : 0) + the five counters of a device counter block, summed over its
+// out[0..kCounterCount) = (accumulate ? out : 0) + the counters of a device counter block, summed over its
 // CTS_COUNTER_SHARDS shards (one 64-thread workgroup; cts_counters_allreduce folds on the device with it).
 hipError_t launch_counters_fold(const void* block, uint64_t* out, bool accumulate, hipStream_t stream);
 

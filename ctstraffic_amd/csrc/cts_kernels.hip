@@ -551,7 +551,7 @@ __device__ __forceinline__ void finish_buffer(const Span& s, const cts_buf_desc&
         r.flags = 0;
         results[i] = r;
     }
-    // the team's running counters live in LDS (tc[5]), not in 10 VGPRs across the stream loop
+    // the team's running counters live in LDS (tc[kCounterCount]), not in 12 VGPRs across the stream loop
     tc[kBytesChecked] += s.len;
     tc[kBuffersChecked] += 1;
     if (pass) {
@@ -559,26 +559,28 @@ __device__ __forceinline__ void finish_buffer(const Span& s, const cts_buf_desc&
     } else {
         tc[kBuffersFailed] += 1;
         tc[kMismatchedBytes] += count;
-        if (conn_first_fail != nullptr && d.conn_index < n_conns) atomicMin(&conn_first_fail[d.conn_index], i);
+        if (conn_first_fail != nullptr && d.conn_index < n_conns &&
+            atomicMin(&conn_first_fail[d.conn_index], i) == 0xFFFFFFFFu)
+            tc[kConnectionsFailed] += 1;
     }
 }
 
-// Per-team running counters in LDS: ctr[team][5], zeroed at kernel start.
+// Per-team running counters in LDS: ctr[team][kCounterCount], zeroed at kernel start.
 template <int TEAMS>
-__device__ __forceinline__ void zero_counters(uint64_t (*ctr)[5])
+__device__ __forceinline__ void zero_counters(uint64_t (*ctr)[kCounterCount])
 {
-    if (threadIdx.x < (unsigned)(TEAMS * 5)) ctr[threadIdx.x / 5][threadIdx.x % 5] = 0;
+    if (threadIdx.x < (unsigned)(TEAMS * kCounterCount)) ctr[threadIdx.x / kCounterCount][threadIdx.x % kCounterCount] = 0;
     __syncthreads();
 }
 
 // Fold the per-team counters of a workgroup and add them to the counter shard
 // of this workgroup (one 64-byte line per shard, CTS_COUNTER_SHARDS shards).
 template <int TEAMS>
-__device__ __forceinline__ void flush_counters(uint64_t* counters, uint64_t (*ctr)[5])
+__device__ __forceinline__ void flush_counters(uint64_t* counters, uint64_t (*ctr)[kCounterCount])
 {
     __syncthreads();
     if (counters == nullptr) return;
-    if (threadIdx.x < 5) {
+    if (threadIdx.x < (unsigned)kCounterCount) {
         uint64_t sum = 0;
 #pragma unroll
         for (int t = 0; t < TEAMS; ++t) sum += ctr[t][threadIdx.x];
@@ -634,7 +636,7 @@ __global__ void __launch_bounds__(kBlock, 4)
                      uint32_t n, cts_verify_result* __restrict__ results, uint64_t* __restrict__ counters,
                      uint32_t* __restrict__ conn_first_fail, uint32_t n_conns)
 {
-    __shared__ uint64_t ctr[1][5];
+    __shared__ uint64_t ctr[1][kCounterCount];
     const uint32_t lane = threadIdx.x;
     zero_counters<1>(ctr);
     const uint32_t step = gridDim.x;
@@ -807,7 +809,7 @@ __device__ __forceinline__ void quad_team_reduce(uint32_t& first, uint32_t& coun
 // Team-leader running counters (registers), written to LDS once at the end.
 struct QCounters {
     uint64_t bytes = 0, ok = 0, mism = 0;
-    uint32_t bufs = 0, fail = 0;
+    uint32_t bufs = 0, fail = 0, conns = 0;
     __device__ __forceinline__ void add(uint32_t len, bool pass, uint32_t count)
     {
         bytes += len;
@@ -820,7 +822,8 @@ struct QCounters {
         }
     }
     template <int TEAMS>
-    __device__ __forceinline__ void flush(uint64_t (*ctr)[5], uint32_t team, uint32_t lane, uint64_t* counters) const
+    __device__ __forceinline__ void flush(uint64_t (*ctr)[kCounterCount], uint32_t team, uint32_t lane,
+                                          uint64_t* counters) const
     {
         if (lane == 0u) {
             ctr[team][kBytesChecked] = bytes;
@@ -828,6 +831,7 @@ struct QCounters {
             ctr[team][kBuffersChecked] = bufs;
             ctr[team][kBuffersFailed] = fail;
             ctr[team][kMismatchedBytes] = mism;
+            ctr[team][kConnectionsFailed] = conns;
         }
         flush_counters<TEAMS>(counters, ctr);
     }
@@ -1000,7 +1004,7 @@ __global__ void __launch_bounds__(kBlock)
                        uint32_t* __restrict__ conn_first_fail, uint32_t n_conns, uint32_t per)
 {
     constexpr int TEAMS = kBlock / kQuadTeam;
-    __shared__ uint64_t ctr[TEAMS][5];
+    __shared__ uint64_t ctr[TEAMS][kCounterCount];
     __shared__ QuadOut qout[kBlock / 64];
     const uint32_t lane = threadIdx.x & (kQuadTeam - 1);
     const uint32_t team = threadIdx.x / kQuadTeam;
@@ -1042,8 +1046,9 @@ __global__ void __launch_bounds__(kBlock)
                                            : result_dw2(pattern_byte_dev(d.expected_pattern_offset + first),
                                                         q.sp[first], 0u, 0u));
                 qc.add(q.len, pass, count);
-                if (!pass && conn_first_fail != nullptr && d.conn_index < n_conns)
-                    atomicMin(&conn_first_fail[d.conn_index], i);
+                if (!pass && conn_first_fail != nullptr && d.conn_index < n_conns &&
+                    atomicMin(&conn_first_fail[d.conn_index], i) == 0xFFFFFFFFu)
+                    qc.conns += 1u;  // this connection's first recorded failure (kConnectionsFailed)
             }
         }
         quad_flush_results(qout[team >> 2], i, w.end, results);
@@ -1330,7 +1335,7 @@ __global__ void __launch_bounds__(kBlock)
         if (threadIdx.x < 4) s_ftot[threadIdx.x] = 0;
         __syncthreads();
     }
-    __shared__ uint64_t ctr[TEAMS][5];
+    __shared__ uint64_t ctr[TEAMS][kCounterCount];
     using RingSlot = typename std::conditional<STATUS, QuadStatusOut, QuadOut>::type;
     __shared__ QuadRing<RING ? RING : 1, RingSlot> qring[RING ? kBlock / 64 : 1];
     uint32_t rs = 0;  // RING: this wave's next ring slot (wave-uniform)
@@ -1971,17 +1976,17 @@ hipError_t launch_mailbox(const MailSlot* slots, MailPart* parts, uint32_t per_g
     return hipGetLastError();
 }
 
-// ---- counter fold (cts_counters_allreduce): one lane per shard, the five sums by lanes 0..4 ----
+// ---- counter fold (cts_counters_allreduce): one lane per shard, the kCounterCount sums by lanes 0.. ----
 static_assert(CTS_COUNTER_SHARDS == 64, "one lane per counter shard");
 __global__ void __launch_bounds__(64) counters_fold_kernel(const uint64_t* __restrict__ block, uint64_t* __restrict__ out,
                                                            int accumulate)
 {
-    __shared__ uint64_t part[CTS_COUNTER_SHARDS][5];
+    __shared__ uint64_t part[CTS_COUNTER_SHARDS][kCounterCount];
     const uint32_t t = threadIdx.x;
 #pragma unroll
-    for (int k = 0; k < 5; ++k) part[t][k] = block[t * kCounterSlots + k];
+    for (int k = 0; k < kCounterCount; ++k) part[t][k] = block[t * kCounterSlots + k];
     __syncthreads();
-    if (t < 5u) {
+    if (t < (uint32_t)kCounterCount) {
         uint64_t s = accumulate ? out[t] : 0u;
         for (uint32_t sh = 0; sh < CTS_COUNTER_SHARDS; ++sh) s += part[sh][t];
         out[t] = s;

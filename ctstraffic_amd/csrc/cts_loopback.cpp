@@ -30,6 +30,7 @@
 #include <vector>
 
 #include "cts_loopback.h"
+#include "cts_teardown.hpp"
 
 namespace {
 
@@ -435,8 +436,7 @@ extern "C" int cts_loopback_run_detailed(const cts_loopback_config* cfg, cts_eng
         if (rc == CTS_OK && hook != nullptr) rc = cts_io_pattern_set_verifier(pats[i], hook, hook_ctx);
     }
     if (rc != CTS_OK) {
-        for (auto* p : pats)
-            if (p) cts_io_pattern_destroy(p);
+        (void)cts::destroy_patterns(pats);  // (the creation error is the one reported)
         ::close(lfd);
         return rc;
     }
@@ -450,7 +450,7 @@ extern "C" int cts_loopback_run_detailed(const cts_loopback_config* cfg, cts_eng
     };
     if (cfg->recv_ring_buffers) {
         if (cfg->verify_buffers || async || (cfg->recv_ring_pinned && engine == nullptr)) {
-            for (auto* p : pats) cts_io_pattern_destroy(p);
+            (void)cts::destroy_patterns(pats);
             ::close(lfd);
             return CTS_E_INVALID;
         }
@@ -473,7 +473,7 @@ extern "C" int cts_loopback_run_detailed(const cts_loopback_config* cfg, cts_eng
         }
         if (rc != CTS_OK) {
             free_rings();
-            for (auto* p : pats) cts_io_pattern_destroy(p);
+            (void)cts::destroy_patterns(pats);
             ::close(lfd);
             return rc;
         }
@@ -569,7 +569,8 @@ extern "C" int cts_loopback_run_detailed(const cts_loopback_config* cfg, cts_eng
             sides[i].status = connected[i] ? (uint32_t)res[i].status : (uint32_t)CTS_IO_FAILED;
             sides[i].last_error = res[i].last_error;
         }
-    for (auto* p : pats) cts_io_pattern_destroy(p);
+    // a pattern whose final verify failed or whose kernels outlived every bounded wait is a failed run
+    const int drc = cts::destroy_patterns(pats);
     free_rings();
-    return CTS_OK;
+    return drc;
 }

@@ -27,6 +27,7 @@
 
 #include "cts_loopback.h"
 #include "cts_media_stream.h"
+#include "cts_teardown.hpp"
 
 namespace {
 
@@ -309,8 +310,10 @@ extern "C" int cts_loopback_media_stream_run(const cts_media_stream_loopback_con
         }
     }
     for (Conn& c : conns) {
-        if (c.client) cts_io_pattern_destroy(c.client);  // stops its timer thread
-        if (c.server) cts_io_pattern_destroy(c.server);
+        // (the client's timer thread is stopped by its first destroy call); a teardown failure fails a run that
+        // had not failed already
+        const int dc = cts::destroy_pattern(c.client), ds = cts::destroy_pattern(c.server);
+        if (rc == CTS_OK) rc = dc != CTS_OK ? dc : ds;
         if (c.sfd >= 0) ::close(c.sfd);
         if (c.cfd >= 0) ::close(c.cfd);
     }

@@ -591,6 +591,8 @@ struct cts_io_pattern {
     virtual int UdpStats(cts_media_stream_stats*) { return CTS_E_INVALID; }
     // cts_io_pattern_flush: the DEFERRED queue of this pattern
     virtual int FlushPending() { return Flush(); }
+    // Stops and joins any thread of the pattern's own that calls into it (the MediaStream client's timers).
+    virtual void StopTimers() {}
 
     uint64_t GetTotalTransfer() const { return state.GetMaxTransfer(); }
     void SetTotalTransfer(uint64_t v) { state.SetMaxTransfer(v); }
@@ -1073,6 +1075,14 @@ struct cts_io_pattern {
         return PollEvent(sync_done, step_us);
     }
 
+    // A plain wait for the pattern's stream, bounded like the others while cts_io_pattern_destroy runs.
+    hipError_t StreamWait(uint32_t step_us)
+    {
+        if (bounded_wait) return SleepSyncImpl(step_us);
+        EngineDevice on(engine);
+        return hipStreamSynchronize(stream);
+    }
+
     hipError_t WaitInflight(hipEvent_t done)  // the kernel behind `done`
     {
         EngineDevice on(engine);
@@ -1184,11 +1194,7 @@ struct cts_io_pattern {
             const int rc = LaunchBatch();
             if (rc != CTS_OK) return rc;
             const auto w0 = std::chrono::steady_clock::now();
-            hipError_t wr;
-            {
-                EngineDevice on(engine);
-                wr = hipStreamSynchronize(stream);
-            }
+            const hipError_t wr = StreamWait(50);  // (destroy's flush of the filling batch: up to the deadline)
             AddVerifyWait(w0);
             if (wr != hipSuccess) return CTS_E_HIP;
             res = reinterpret_cast<const cts_verify_result*>(stage_res.host) + (size_t)desc_set * BatchCapacity();
@@ -1596,7 +1602,7 @@ struct MediaStreamClient : cts_io_pattern {
           m_recvNeeded(c.pre_post_recvs), m_maxDatagramSize(c.ms_datagram_max_size), manual(c.ms_manual_timers != 0)
     {
     }
-    ~MediaStreamClient() override
+    void StopTimers() override
     {
         {
             std::lock_guard<std::recursive_mutex> lk(mu);
@@ -1605,6 +1611,10 @@ struct MediaStreamClient : cts_io_pattern {
         }
         cv.notify_all();
         if (timer_thread.joinable()) timer_thread.join();
+    }
+    ~MediaStreamClient() override
+    {
+        StopTimers();
         if (ms != nullptr) (void)cts_media_stream_client_destroy(ms);
         EngineDevice on(engine);
         if (d_sums != nullptr) (void)hipFreeAsync(d_sums, stream);
@@ -1766,7 +1776,7 @@ struct MediaStreamClient : cts_io_pattern {
         rc = cts_media_stream_verify_status(engine, recv_pinned.dev, recv_pinned.bytes,
                                             reinterpret_cast<const cts_buf_desc*>(ms_desc.dev), n,
                                             reinterpret_cast<cts_datagram_status*>(ms_status.dev), nullptr, stream);
-        if (rc != CTS_OK || hipStreamSynchronize(stream) != hipSuccess) throw DeviceError{rc != CTS_OK ? rc : CTS_E_HIP};
+        if (rc != CTS_OK || StreamWait(20) != hipSuccess) throw DeviceError{rc != CTS_OK ? rc : CTS_E_HIP};
         const auto* st = reinterpret_cast<const cts_datagram_status*>(ms_status.host);
         for (uint32_t i = 0; i < n; ++i) {
             if (st[i].pass) {
@@ -1780,7 +1790,7 @@ struct MediaStreamClient : cts_io_pattern {
             rc = cts_verify(engine, recv_pinned.dev, recv_pinned.bytes, reinterpret_cast<const cts_buf_desc*>(ms_res.dev),
                             1, q[i].completed, reinterpret_cast<cts_verify_result*>(ms_res.dev + sizeof(cts_buf_desc)),
                             nullptr, nullptr, 0, stream);
-            if (rc != CTS_OK || hipStreamSynchronize(stream) != hipSuccess) throw DeviceError{rc != CTS_OK ? rc : CTS_E_HIP};
+            if (rc != CTS_OK || StreamWait(20) != hipSuccess) throw DeviceError{rc != CTS_OK ? rc : CTS_E_HIP};
             FailQueued(q[i], *reinterpret_cast<const cts_verify_result*>(ms_res.host + sizeof(cts_buf_desc)));
             return true;
         }
@@ -2227,6 +2237,9 @@ int cts_io_pattern_create(const cts_pattern_config* c, cts_engine* engine, cts_i
 int cts_io_pattern_destroy(cts_io_pattern* p)
 {
     if (p == nullptr) return CTS_E_INVALID;
+    // a MediaStream client's timer thread is stopped and joined first (not under the pattern lock, which its
+    // callbacks take): nothing calls into the engine from it once destroy has begun, whatever destroy returns
+    p->StopTimers();
     int rc = CTS_OK;
     {
         // DEFERRED: completions still waiting for a verdict are verified now, so their bytes reach TcpStatusDetails
@@ -2239,14 +2252,24 @@ int cts_io_pattern_destroy(cts_io_pattern* p)
         p->wait_deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(ms > 0 ? ms : 2000);
         if (p->fail_fast.empty() && p->VerdictsPending()) {
             try {
-                (void)p->FlushPending();
+                const int fr = p->FlushPending();  // an io status (>= 0), or a negative CTS_E_* of the final verify
+                if (fr < 0) rc = fr;
+            } catch (const DeviceError& d) {
+                rc = d.rc < 0 ? d.rc : CTS_E_HIP;
             } catch (...) {
                 rc = CTS_E_HIP;
             }
         }
         // the pattern's buffers go with it: a kernel still reading them (it did not finish within the bound) keeps
-        // them, and the pattern is left allocated rather than freed under the GPU's reads
-        if (p->stream != nullptr && p->SleepSyncImpl(50) != hipSuccess) return CTS_E_HIP;
+        // them, and the pattern is left allocated rather than freed under the GPU's reads (CTS_E_TIMEOUT: call
+        // destroy again later). Any other failure of that wait is the device's own (a sticky error): no kernel of
+        // the pattern runs any more and a later call could not do better, so the pattern is freed (CTS_E_HIP).
+        const hipError_t w = p->stream != nullptr ? p->SleepSyncImpl(50) : hipSuccess;
+        if (w == hipErrorNotReady) {
+            p->bounded_wait = false;
+            return CTS_E_TIMEOUT;
+        }
+        if (w != hipSuccess) rc = CTS_E_HIP;
     }
     delete p;
     return rc;

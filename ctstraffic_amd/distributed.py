@@ -5,15 +5,16 @@ offset, and connections are assigned to ranks by ``fmix32(conn_index) mod G``
 (:func:`ctstraffic_amd.workload.shard_of`), so a connection's first failing
 buffer and its DataError decision (ctsSocketState.cpp:221-232) stay on one
 rank. The only collective is an optional all-reduce (sum) of the five
-ctsStatistics-style counters (ctsStatistics.hpp:87-198) — 40 bytes over
-RCCL/xGMI (backend "nccl") or gloo on CPU.
+ctsStatistics-style counters (ctsStatistics.hpp:87-198) and the DataError
+count (ctsSocketState.cpp:221-228) — 48 bytes over RCCL/xGMI (backend
+"nccl") or gloo on CPU.
 """
 from __future__ import annotations
 
 import os
 from typing import Optional
 
-from .types import COUNTER_FIELDS
+from .types import COUNTER_FIELDS, COUNTER_FIELDS_EX
 
 COUNTER_SLOTS = 8  # u64 per 64-byte counter shard (cts_internal.hpp kCounterSlots)
 
@@ -58,24 +59,27 @@ def new_cpu_group(timeout_s: Optional[float] = DEFAULT_TIMEOUT_S):
     return dist.new_group(backend="gloo", **kw)
 
 
-def fold_counters(counter_block):
-    """Device counter block (CTS_COUNTER_SHARDS x 8 int64, cts_counters_device_bytes) -> int64[5],
-    on the block's own device (no host round trip)."""
-    return counter_block.view(-1, COUNTER_SLOTS)[:, : len(COUNTER_FIELDS)].sum(0)
+def fold_counters(counter_block, fields=COUNTER_FIELDS):
+    """Device counter block (CTS_COUNTER_SHARDS x 8 int64, cts_counters_device_bytes) -> int64[len(fields)], on the
+    block's own device (no host round trip). fields=COUNTER_FIELDS_EX adds the DataError count (connections_failed,
+    counted by the verifies given a conn_first_fail array)."""
+    assert tuple(fields) == COUNTER_FIELDS_EX[: len(fields)], fields
+    return counter_block.view(-1, COUNTER_SLOTS)[:, : len(fields)].sum(0)
 
 
-def allreduce_counters(counters5, group=None):
-    """In-place sum of the five counters over all ranks (ctsStatsTracking::Add across GPUs)."""
+def allreduce_counters(counters, group=None):
+    """In-place sum of the folded counters over all ranks (ctsStatsTracking::Add across GPUs)."""
     import torch.distributed as dist
 
     if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
-        dist.all_reduce(counters5, op=dist.ReduceOp.SUM, group=group)
-    return counters5
+        dist.all_reduce(counters, op=dist.ReduceOp.SUM, group=group)
+    return counters
 
 
-def counters_dict(counters5) -> dict:
-    vals = [int(x) for x in counters5.tolist()]
-    return dict(zip(COUNTER_FIELDS, vals))
+def counters_dict(counters) -> dict:
+    """Folded counters (5, or 6 with connections_failed) -> {field: value}."""
+    vals = [int(x) for x in counters.tolist()]
+    return dict(zip(COUNTER_FIELDS_EX, vals))
 
 
 def max_over_ranks(value: float, device=None, group=None) -> float:

@@ -12,7 +12,7 @@ from typing import Optional, Sequence
 import numpy as np
 
 from . import _lib
-from ._lib import CtsCounters, CtsVerifyResult, check, lib
+from ._lib import CtsAllreduceSetup, CtsCounters, CtsCountersEx, CtsVerifyResult, check, lib
 from .types import DESC_DTYPE, RESULT_DTYPE
 
 try:
@@ -81,30 +81,61 @@ def _check_outputs(n: int, results, counters) -> None:
                                                                              int(lib().cts_counters_device_bytes())))
 
 
-def counters_read_multi(engines: Sequence["Engine"], blocks, streams=None) -> dict:
-    """cts_counters_read_multi: the node-wide counters of one process's engines (one per GPU), folded on the host."""
+def _multi_args(engines, blocks, streams):
     n = len(engines)
     E = (ctypes.c_void_p * max(1, n))(*[e._h.value for e in engines])
     C = (ctypes.c_void_p * max(1, n))(*[_ptr(b) for b in blocks])
     S = None
     if streams is not None:
         S = (ctypes.c_void_p * max(1, n))(*[_stream(s) for s in streams])
+    return E, C, S, n
+
+
+def counters_read_multi(engines: Sequence["Engine"], blocks, streams=None) -> dict:
+    """cts_counters_read_multi: the node-wide counters of one process's engines (one per GPU), folded on the host."""
+    E, C, S, n = _multi_args(engines, blocks, streams)
     out = CtsCounters()
     check("cts_counters_read_multi", lib().cts_counters_read_multi(E, C, S, n, ctypes.byref(out)))
     return out.as_dict()
 
 
+def counters_read_multi_ex(engines: Sequence["Engine"], blocks, streams=None) -> dict:
+    """cts_counters_read_multi_ex: counters_read_multi plus connections_failed (the node's DataError count)."""
+    E, C, S, n = _multi_args(engines, blocks, streams)
+    out = CtsCountersEx()
+    check("cts_counters_read_multi_ex", lib().cts_counters_read_multi_ex(E, C, S, n, ctypes.byref(out)))
+    return out.as_dict()
+
+
 def counters_allreduce(engines: Sequence["Engine"], blocks, streams=None) -> dict:
     """cts_counters_allreduce: the same node-wide counters reduced on the GPUs: each block folded on its engine's
-    device, then one RCCL all-reduce (sum, u64 x 5) per device over xGMI (one process drives every GPU)."""
-    n = len(engines)
-    E = (ctypes.c_void_p * max(1, n))(*[e._h.value for e in engines])
-    C = (ctypes.c_void_p * max(1, n))(*[_ptr(b) for b in blocks])
-    S = None
-    if streams is not None:
-        S = (ctypes.c_void_p * max(1, n))(*[_stream(s) for s in streams])
+    device, then one RCCL all-reduce (sum, u64) per device over xGMI (one process drives every GPU)."""
+    E, C, S, n = _multi_args(engines, blocks, streams)
     out = CtsCounters()
     check("cts_counters_allreduce", lib().cts_counters_allreduce(E, C, S, n, ctypes.byref(out)))
+    return out.as_dict()
+
+
+def counters_allreduce_ex(engines: Sequence["Engine"], blocks, streams=None) -> dict:
+    """cts_counters_allreduce_ex: counters_allreduce plus connections_failed (u64 x 6 over RCCL)."""
+    E, C, S, n = _multi_args(engines, blocks, streams)
+    out = CtsCountersEx()
+    check("cts_counters_allreduce_ex", lib().cts_counters_allreduce_ex(E, C, S, n, ctypes.byref(out)))
+    return out.as_dict()
+
+
+def counters_allreduce_prepare(engines: Sequence["Engine"]) -> None:
+    """cts_counters_allreduce_prepare: build the RCCL clique of these engines' devices (and run its first
+    all-reduce) now, so the status timer's first counter read (t = 0, ctsTraffic.cpp:107-113) does not pay it."""
+    n = len(engines)
+    E = (ctypes.c_void_p * max(1, n))(*[e._h.value for e in engines])
+    check("cts_counters_allreduce_prepare", lib().cts_counters_allreduce_prepare(E, n))
+
+
+def counters_allreduce_setup_times() -> dict:
+    """cts_counters_allreduce_setup_times: the newest clique's set-up breakdown (ms)."""
+    out = CtsAllreduceSetup()
+    check("cts_counters_allreduce_setup_times", lib().cts_counters_allreduce_setup_times(ctypes.byref(out)))
     return out.as_dict()
 
 
@@ -238,6 +269,14 @@ class Engine:
         c = CtsCounters()
         check("cts_counters_read", self._L.cts_counters_read(self._h, _ptr(counters), ctypes.byref(c),
                                                            _stream(stream)))
+        return c.as_dict()
+
+    def read_counters_ex(self, counters, stream=None) -> dict:
+        """cts_counters_read_ex: read_counters plus connections_failed (the DataError count, ctsSocketState.cpp:
+        221-228), counted by the verifies given a conn_first_fail array."""
+        c = CtsCountersEx()
+        check("cts_counters_read_ex", self._L.cts_counters_read_ex(self._h, _ptr(counters), ctypes.byref(c),
+                                                                 _stream(stream)))
         return c.as_dict()
 
     # ---- pinned host arenas ---------------------------------------------------------

@@ -15,6 +15,7 @@ from typing import Callable, Optional
 import numpy as np
 
 from . import _pattern_abi as A
+from . import _lib
 from ._lib import CtsError, check, lib
 from .types import DESC_DTYPE, RESULT_DTYPE
 
@@ -138,9 +139,13 @@ class IoPattern:
     MakeIoPattern = classmethod(lambda cls, config, engine=None, verifier=None: cls(config, engine, verifier))
 
     def close(self) -> None:
+        """cts_io_pattern_destroy. On CTS_E_TIMEOUT (a kernel still reads the pattern's buffers) the handle is kept
+        and CtsError raised: call close() again. Any other failure frees the pattern and raises."""
         if getattr(self, "_h", None) is not None and self._h.value:
-            lib().cts_io_pattern_destroy(self._h)
-            self._h = None
+            rc = lib().cts_io_pattern_destroy(self._h)
+            if rc != _lib.CTS_E_TIMEOUT:
+                self._h = None
+            check("cts_io_pattern_destroy", rc)
 
     def __del__(self):  # pragma: no cover
         try:

@@ -23,6 +23,8 @@ RESULT_DTYPE = np.dtype(
     ]
 )
 COUNTER_FIELDS = ("bytes_checked", "bytes_ok", "buffers_checked", "buffers_failed", "mismatched_bytes")
+# cts_counters_ex: plus the DataError count (ctsSocketState.cpp:221-228), slot 5 of a device counter shard
+COUNTER_FIELDS_EX = COUNTER_FIELDS + ("connections_failed",)
 RESULT_FLAG_BAD_DESC = 0x1
 
 assert DESC_DTYPE.itemsize == 24 and RESULT_DTYPE.itemsize == 12

@@ -54,7 +54,9 @@ typedef enum cts_status {
     CTS_E_HIP = -2,       /* a HIP runtime call or kernel launch failed */
     CTS_E_NOMEM = -3,     /* allocation failed */
     CTS_E_NO_DEVICE = -4, /* no HIP device / device index out of range */
-    CTS_E_UNAVAILABLE = -5 /* an optional runtime library (RCCL) could not be loaded */
+    CTS_E_UNAVAILABLE = -5, /* an optional runtime library (RCCL) could not be loaded */
+    CTS_E_TIMEOUT = -6      /* a bounded wait ran out; nothing was freed, the call may be repeated
+                             * (cts_io_pattern_destroy while a kernel still reads the pattern's buffers) */
 } cts_status;
 
 /* One received (verify) or outgoing (fill) buffer inside a device arena.
@@ -98,6 +100,21 @@ typedef struct cts_counters {
     uint64_t buffers_failed;
     uint64_t mismatched_bytes;
 } cts_counters;
+
+/* cts_counters plus the DataError count, read by the *_ex entry points (cts_counters keeps its size and meaning).
+ * connections_failed: # connections with a failing buffer, i.e. the ConnectionStatusDetails.m_protocolErrorCount
+ * increments of ctsSocketState.cpp:221-228 (one per connection whose verify failed, however many of its buffers
+ * did). Counted on the device when a verify's atomicMin on dev_conn_first_fail[c] finds the slot still
+ * 0xFFFFFFFF, so it counts only in launches given a dev_conn_first_fail array, once per slot over the life of
+ * that array (re-initialise the slots when the counter block is reset). */
+typedef struct cts_counters_ex {
+    uint64_t bytes_checked;
+    uint64_t bytes_ok;
+    uint64_t buffers_checked;
+    uint64_t buffers_failed;
+    uint64_t mismatched_bytes;
+    uint64_t connections_failed;
+} cts_counters_ex;
 
 typedef struct cts_engine cts_engine;
 
@@ -179,7 +196,9 @@ int cts_fill(cts_engine* engine, void* dev_arena, uint64_t arena_bytes,
  *                           Initialise to 0xFFFFFFFF. The DataError count
  *                           (ctsSocketState.cpp:221-232) is the number of slots
  *                           != 0xFFFFFFFF when descriptors of one connection are
- *                           in stream order.
+ *                           in stream order; with dev_counters given it is also
+ *                           accumulated on the device (connections_failed,
+ *                           cts_counters_read_ex).
  * dev_arena must be 16-byte aligned and its allocation must extend to a
  * multiple of 16 bytes (every hipMalloc allocation does); dev_descs must be
  * 8-byte aligned, dev_results and dev_conn_first_fail 4-byte aligned and
@@ -216,6 +235,33 @@ int cts_counters_allreduce(cts_engine* const* engines, const void* const* dev_co
 /* Destroys the communicators and device slots cts_counters_allreduce keeps (call before the engines' devices go
  * away, e.g. at shutdown); the next all-reduce creates them again. */
 int cts_counters_allreduce_release(void);
+
+/* The same three reads with the DataError count (cts_counters_ex.connections_failed): the all-reduce is one
+ * ncclAllReduce of count 6. cts_counters_read / _read_multi / _allreduce return the first five fields of these. */
+int cts_counters_read_ex(cts_engine* engine, const void* dev_counters, cts_counters_ex* out, void* stream);
+int cts_counters_read_multi_ex(cts_engine* const* engines, const void* const* dev_counters, void* const* streams,
+                               uint32_t n, cts_counters_ex* out);
+int cts_counters_allreduce_ex(cts_engine* const* engines, const void* const* dev_counters, void* const* streams,
+                              uint32_t n, cts_counters_ex* out);
+
+/* Everything the first cts_counters_allreduce of a device set would set up, done now: RCCL loaded, the device
+ * slots allocated, ncclCommInitAll over the engines' distinct devices (in list order, as the all-reduce groups
+ * them) and one dry run of a counter read per device (a zeroed block folded, all-reduced and copied back), so
+ * RCCL's first-collective set-up and the fold's first launch are paid here too. Call it next
+ * to cts_engine_create, before the status timer's first tick (ctsTraffic.cpp:107-113 prints at t = 0); later
+ * all-reduces over the same device set reuse the clique. Idempotent. Errors as cts_counters_allreduce. */
+int cts_counters_allreduce_prepare(cts_engine* const* engines, uint32_t n);
+
+/* Where the set-up time of the newest clique went (ms, host wall clock); all zero before one was built. */
+typedef struct cts_allreduce_setup {
+    double rccl_load_ms;       /* dlopen of librccl + dlsym (0 when RCCL was already loaded by an earlier clique) */
+    double slots_ms;           /* the per-device result slots: hipMallocAsync + synchronize */
+    double comm_init_ms;       /* ncclCommInitAll */
+    double first_allreduce_ms; /* the dry run: fold of a zeroed block, the first grouped ncclAllReduce, copy back */
+    uint32_t devices;          /* ranks in that clique */
+    uint32_t prepared;         /* 1 = built by cts_counters_allreduce_prepare, 0 = by a first all-reduce */
+} cts_allreduce_setup;
+int cts_counters_allreduce_setup_times(cts_allreduce_setup* out);
 
 /* cts_verify over a uniformly strided receive ring (a UDP socket's datagrams): buffer i occupies
  * [i * stride, i * stride + dev_lengths[i]) of the arena, its first skip_head bytes are skipped and the rest

@@ -258,9 +258,14 @@ int cts_io_pattern_create(const cts_pattern_config* config, cts_engine* engine, 
 /* A DEFERRED pattern destroyed with completions still waiting for their batch verdict verifies them first, so their
  * bytes are published (cts_pattern_stats.bytes_*_held) as the reference counted them at completion. A data mismatch
  * found by that final verify reaches only the process-wide counters (cts_status_details_*): the caller has read this
- * pattern's stats before destroying it. Every wait of destroy is bounded (env CTS_PATTERN_DESTROY_WAIT_MS, default
- * 2000): CTS_OK, or CTS_E_HIP when the final verify failed (the pattern is freed) or the pattern's stream did not go
- * idle within the bound (a kernel still reads its buffers: the pattern is left allocated, not freed under it). */
+ * pattern's stats before destroying it. A MediaStream client's timer thread is stopped and joined first, whatever
+ * destroy then returns. Every wait of destroy is bounded (env CTS_PATTERN_DESTROY_WAIT_MS, default 2000), the flush
+ * of the batch destroy itself launches included. Returns:
+ *   CTS_OK        the pattern is freed;
+ *   CTS_E_TIMEOUT a kernel still reads the pattern's buffers after the bound: nothing was freed, the handle stays
+ *                 valid, and destroy should be called again (it flushes nothing more, only waits again);
+ *   CTS_E_HIP / another negative status: the final verify failed, or the device reported an error (sticky: no later
+ *                 call could wait better); the pattern is freed. */
 int cts_io_pattern_destroy(cts_io_pattern* pattern);
 int cts_io_pattern_set_verifier(cts_io_pattern* pattern, cts_batch_verifier fn, void* ctx);
 

@@ -72,6 +72,11 @@ hipError_t hipFreeAsync(void* p, hipStream_t s)
     std::free(p);
     return hipSuccess;
 }
+hipError_t hipMemsetAsync(void* dst, int v, size_t bytes, hipStream_t)
+{
+    std::memset(dst, v, bytes);
+    return hipSuccess;
+}
 hipError_t hipMemcpyAsync(void* dst, const void* src, size_t bytes, hipMemcpyKind, hipStream_t)
 {
     std::memcpy(dst, src, bytes);
@@ -101,7 +106,7 @@ hipError_t launch_counters_fold(const void* block, uint64_t* out, bool accumulat
         ++g_folds;
     }
     const uint64_t* h = static_cast<const uint64_t*>(block);
-    for (int k = 0; k < 5; ++k) {
+    for (int k = 0; k < kCounterCount; ++k) {
         uint64_t s = accumulate ? out[k] : 0;
         for (uint32_t sh = 0; sh < CTS_COUNTER_SHARDS; ++sh) s += h[sh * kCounterSlots + k];
         out[k] = s;
@@ -115,7 +120,7 @@ struct Node {
     std::vector<std::vector<uint64_t>> blocks;
     std::vector<cts_engine*> eng;
     std::vector<const void*> ptrs;
-    uint64_t want[5] = {0, 0, 0, 0, 0};
+    uint64_t want[cts::kCounterCount] = {};
 };
 
 // n engines, engine g on device dev(g); block values distinct per engine, shard and slot
@@ -130,10 +135,10 @@ Node make_node(uint32_t n, DevOf dev)
         x.ptrs.push_back(x.blocks[g].data());
         for (uint32_t sh = 0; sh < CTS_COUNTER_SHARDS; ++sh)
             for (int k = 0; k < 8; ++k) {
-                // slots 5..7 of a shard are not counters and must not be folded in
+                // slots kCounterCount..7 of a shard are not counters and must not be folded in
                 const uint64_t v = (uint64_t)(g + 1) * 1000003ull * (sh + 1) + (uint64_t)k * 7919ull;
                 x.blocks[g][sh * 8 + k] = v;
-                if (k < 5) x.want[k] += v;
+                if (k < cts::kCounterCount) x.want[k] += v;
             }
     }
     return x;
@@ -143,6 +148,11 @@ bool equal(const cts_counters& c, const uint64_t* w)
 {
     return c.bytes_checked == w[0] && c.bytes_ok == w[1] && c.buffers_checked == w[2] && c.buffers_failed == w[3] &&
            c.mismatched_bytes == w[4];
+}
+bool equal(const cts_counters_ex& c, const uint64_t* w)
+{
+    return c.bytes_checked == w[0] && c.bytes_ok == w[1] && c.buffers_checked == w[2] && c.buffers_failed == w[3] &&
+           c.mismatched_bytes == w[4] && c.connections_failed == w[5];
 }
 
 int main(int argc, char** argv)
@@ -203,12 +213,13 @@ int main(int argc, char** argv)
         const int ndev = (int)((k.n + k.per_dev - 1) / k.per_dev);
         for (int rep = 0; rep < 2; ++rep) {
             t_cur = 3;
-            const int folds0 = g_folds;
+            const int folds0 = g_folds, live0 = live();
             cts_counters a{};
             CHECK(cts_counters_allreduce(x.eng.data(), x.ptrs.data(), nullptr, k.n, &a) == CTS_OK);
             CHECK(equal(a, x.want));
             CHECK(t_cur == 3);                          // the caller's current device is restored
-            CHECK(g_folds - folds0 == (int)k.n);        // every block folded once, on its own device
+            // every block folded once, on its own device, plus one dry-run fold per device of a new clique
+            CHECK(g_folds - folds0 == (int)k.n + (live() - live0));
             cts_counters h{};
             CHECK(cts_counters_read_multi(x.eng.data(), x.ptrs.data(), nullptr, k.n, &h) == CTS_OK);
             CHECK(std::memcmp(&a, &h, sizeof(a)) == 0);  // the two ways agree
@@ -262,6 +273,76 @@ int main(int argc, char** argv)
         CHECK(live() == 2);
     }
     CHECK(cts_counters_allreduce_release() == CTS_OK && live() == 0);
+
+    // 3. the DataError count (slot kConnectionsFailed) through the _ex reads, both ways
+    for (uint32_t n : {1u, 3u, 8u}) {
+        Node x = make_node(n, [](uint32_t g) { return (int)g; });
+        cts_counters_ex a{}, h{};
+        CHECK(cts_counters_read_multi_ex(x.eng.data(), x.ptrs.data(), nullptr, n, &h) == CTS_OK && equal(h, x.want));
+        CHECK(cts_counters_allreduce_ex(x.eng.data(), x.ptrs.data(), nullptr, n, &a) == CTS_OK && equal(a, x.want));
+        CHECK(std::memcmp(&a, &h, sizeof(a)) == 0);
+        cts_counters five{};  // the five-field reads are the _ex reads' first five fields
+        CHECK(cts_counters_allreduce(x.eng.data(), x.ptrs.data(), nullptr, n, &five) == CTS_OK && equal(five, x.want));
+    }
+    CHECK(cts_counters_read_multi_ex(nullptr, nullptr, nullptr, 1, nullptr) == CTS_E_INVALID);
+    CHECK(cts_counters_allreduce_ex(nullptr, nullptr, nullptr, 1, nullptr) == CTS_E_INVALID);
+    CHECK(cts_counters_allreduce_release() == CTS_OK && live() == 0);
+
+    // 4. prepare: the clique (slots, communicators, a first all-reduce) is built before any counter read, once
+    CHECK(cts_counters_allreduce_prepare(nullptr, 0) == CTS_OK);
+    CHECK(cts_counters_allreduce_prepare(nullptr, 2) == CTS_E_INVALID);
+    CHECK(cts_counters_allreduce_prepare(bogus, 1) == CTS_E_INVALID);
+    CHECK(cts_counters_allreduce_setup_times(nullptr) == CTS_E_INVALID);
+    {
+        Node x = make_node(6, [](uint32_t g) { return (int)(g / 2); });  // devices 0, 1, 2: two engines each
+        t_cur = 5;
+        const int folds_before = g_folds;
+        CHECK(cts_counters_allreduce_prepare(x.eng.data(), 6) == CTS_OK);
+        CHECK(t_cur == 5 && live() == 3);
+        CHECK(g_folds - folds_before == 3);  // the dry run: one fold of a zeroed block per device
+        {
+            std::lock_guard<std::mutex> lk(g_mu);
+            CHECK(g_alloc_dev.size() == 3);  // one slot per device
+        }
+        cts_allreduce_setup st{};
+        CHECK(cts_counters_allreduce_setup_times(&st) == CTS_OK);
+        CHECK(st.devices == 3 && st.prepared == 1 && st.slots_ms >= 0.0 && st.comm_init_ms >= 0.0 &&
+              st.first_allreduce_ms >= 0.0 && st.rccl_load_ms == 0.0);  // RCCL was loaded by an earlier call
+        CHECK(cts_counters_allreduce_prepare(x.eng.data(), 6) == CTS_OK && live() == 3);  // idempotent
+        const int folds0 = g_folds;
+        cts_counters_ex a{};
+        CHECK(cts_counters_allreduce_ex(x.eng.data(), x.ptrs.data(), nullptr, 6, &a) == CTS_OK && equal(a, x.want));
+        CHECK(live() == 3 && g_folds - folds0 == 6);  // the prepared clique is the one used: no dry run again
+        cts_allreduce_setup st2{};
+        CHECK(cts_counters_allreduce_setup_times(&st2) == CTS_OK && std::memcmp(&st, &st2, sizeof(st)) == 0);
+    }
+    // a clique built lazily by a first all-reduce says so
+    {
+        Node x = make_node(2, [](uint32_t g) { return (int)g + 4; });
+        cts_counters_ex a{};
+        CHECK(cts_counters_allreduce_ex(x.eng.data(), x.ptrs.data(), nullptr, 2, &a) == CTS_OK && equal(a, x.want));
+        cts_allreduce_setup st{};
+        CHECK(cts_counters_allreduce_setup_times(&st) == CTS_OK && st.devices == 2 && st.prepared == 0);
+    }
+    // communicator creation failing in prepare: an error, nothing kept, a later prepare succeeds
+    CHECK(cts_counters_allreduce_release() == CTS_OK && live() == 0);
+    setenv("STUB_RCCL_FAIL_INIT", "1", 1);
+    {
+        Node x = make_node(2, [](uint32_t g) { return (int)g; });
+        CHECK(cts_counters_allreduce_prepare(x.eng.data(), 2) == CTS_E_HIP && live() == 0);
+        std::lock_guard<std::mutex> lk(g_mu);
+        CHECK(g_alloc_dev.empty());
+    }
+    unsetenv("STUB_RCCL_FAIL_INIT");
+    {
+        Node x = make_node(2, [](uint32_t g) { return (int)g; });
+        CHECK(cts_counters_allreduce_prepare(x.eng.data(), 2) == CTS_OK && live() == 2);
+    }
+    CHECK(cts_counters_allreduce_release() == CTS_OK && live() == 0);
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        CHECK(g_alloc_dev.empty());
+    }
     dlclose(stub);
     std::printf("counters_fold: ok\n");
     return 0;

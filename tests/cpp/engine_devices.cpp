@@ -386,14 +386,28 @@ hipError_t launch_verify(const uint8_t* arena, uint64_t bytes, const cts_buf_des
             std::this_thread::sleep_for(std::chrono::microseconds(async_us / 2 + x % (uint32_t)(async_us + 1)));
         }
         ora_counters c{};
+        // the launch's own first failures, then merged into the caller's slots by an atomic min per connection as
+        // the kernels do: a min that found the slot empty is the connection's first failure (kConnectionsFailed)
+        std::vector<uint32_t> own(first_fail != nullptr ? n_conns : 0u, 0xFFFFFFFFu);
         (void)ora_verify_batch(arena, bytes, reinterpret_cast<const ora_desc*>(d), n, reinterpret_cast<ora_result*>(r),
-                               &c, first_fail, n_conns, 1);
+                               &c, own.empty() ? nullptr : own.data(), (uint32_t)own.size(), 1);
+        uint64_t conns = 0;
+        for (uint32_t k = 0; k < own.size(); ++k) {
+            if (own[k] == 0xFFFFFFFFu) continue;
+            uint32_t cur = __atomic_load_n(&first_fail[k], __ATOMIC_RELAXED);
+            const uint32_t old = cur;
+            while (own[k] < cur &&
+                   !__atomic_compare_exchange_n(&first_fail[k], &cur, own[k], false, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) {
+            }
+            if (old == 0xFFFFFFFFu && cur == 0xFFFFFFFFu) ++conns;  // (cur holds the value the exchange replaced)
+        }
         if (counters != nullptr) {  // (shard 0 of the device block; atomics, as the kernels': streams run at once)
             __atomic_fetch_add(&counters[kBytesChecked], c.bytes_checked, __ATOMIC_RELAXED);
             __atomic_fetch_add(&counters[kBytesOk], c.bytes_ok, __ATOMIC_RELAXED);
             __atomic_fetch_add(&counters[kBuffersChecked], c.buffers_checked, __ATOMIC_RELAXED);
             __atomic_fetch_add(&counters[kBuffersFailed], c.buffers_failed, __ATOMIC_RELAXED);
             __atomic_fetch_add(&counters[kMismatchedBytes], c.mismatched_bytes, __ATOMIC_RELAXED);
+            __atomic_fetch_add(&counters[kConnectionsFailed], conns, __ATOMIC_RELAXED);
         }
     };
     if (d == nullptr && n != 0) return hipErrorInvalidValue;
@@ -510,12 +524,12 @@ hipError_t launch_media_stream_frames(const uint8_t* arena, uint64_t bytes, cons
     return hipSuccess;
 }
 
-// counters_fold_kernel: the 64 shards' five sums into out (accumulating), after the stream's earlier work
+// counters_fold_kernel: the 64 shards' kCounterCount sums into out (accumulating), after the stream's earlier work
 hipError_t launch_counters_fold(const void* block, uint64_t* out, bool accumulate, hipStream_t s)
 {
     launched("launch_counters_fold", s);
     const uint64_t* h = static_cast<const uint64_t*>(block);
-    for (int k = 0; k < 5; ++k) {
+    for (int k = 0; k < kCounterCount; ++k) {
         uint64_t v = accumulate ? out[k] : 0;
         for (uint32_t sh = 0; sh < CTS_COUNTER_SHARDS; ++sh) v += h[sh * kCounterSlots + k];
         out[k] = v;
@@ -909,7 +923,9 @@ int main(int argc, char** argv)
         std::vector<std::vector<cts_verify_result>> res(kN, std::vector<cts_verify_result>(kBufs));
         std::vector<void*> streams(kN);
         std::vector<const void*> bptr(kN);
-        uint64_t want[5] = {0, 0, 0, 0, 0};
+        std::vector<std::vector<uint32_t>> first_fail(kN, std::vector<uint32_t>(5, 0xFFFFFFFFu));  // the live slots
+        std::vector<std::vector<uint32_t>> want_ff(kN, std::vector<uint32_t>(5, 0xFFFFFFFFu));
+        uint64_t want[cts::kCounterCount] = {};
         for (uint32_t g = 0; g < kN; ++g) {
             uint8_t* a = reinterpret_cast<uint8_t*>(((uintptr_t)arenas[g].data() + 15u) & ~(uintptr_t)15u);
             for (uint32_t b = 0; b < kBufs; ++b) {
@@ -922,6 +938,8 @@ int main(int argc, char** argv)
                     a[(size_t)b * 4096u + len / 2] ^= 0x10;
                     want[cts::kBuffersFailed] += 1;
                     want[cts::kMismatchedBytes] += 1;
+                    if (want_ff[g][b % 5u] == 0xFFFFFFFFu) want[cts::kConnectionsFailed] += 1;
+                    want_ff[g][b % 5u] = std::min(want_ff[g][b % 5u], b);
                 } else {
                     want[cts::kBytesOk] += len;
                 }
@@ -929,24 +947,34 @@ int main(int argc, char** argv)
             CHECK(cts_engine_stream_create(eng[g], &streams[g]) == CTS_OK);
             CHECK(cts_counters_reset(eng[g], blocks[g].data(), streams[g]) == CTS_OK);
             CHECK(cts_verify(eng[g], a, (uint64_t)kBufs * 4096u, descs[g].data(), kBufs, 4096u, res[g].data(),
-                             blocks[g].data(), nullptr, 0, streams[g]) == CTS_OK);
+                             blocks[g].data(), first_fail[g].data(), 5, streams[g]) == CTS_OK);
             bptr[g] = blocks[g].data();
         }
-        cts_counters all{}, fold{};
-        CHECK(cts_counters_allreduce(eng, bptr.data(), streams.data(), kN, &all) == CTS_OK);
-        CHECK(cts_counters_read_multi(eng, bptr.data(), streams.data(), kN, &fold) == CTS_OK);
+        // the clique set up before the status timer's first read (from the same thread, device 3 current)
+        CHECK(cts_counters_allreduce_prepare(eng, kN) == CTS_OK);
         (void)hipGetDevice(&cur);
         CHECK(cur == 3);
-        const uint64_t got[5] = {all.bytes_checked, all.bytes_ok, all.buffers_checked, all.buffers_failed,
-                                 all.mismatched_bytes};
-        const uint64_t gotf[5] = {fold.bytes_checked, fold.bytes_ok, fold.buffers_checked, fold.buffers_failed,
-                                  fold.mismatched_bytes};
-        for (int k = 0; k < 5; ++k) CHECK(got[k] == want[k] && gotf[k] == want[k]);
+        cts_allreduce_setup st{};
+        CHECK(cts_counters_allreduce_setup_times(&st) == CTS_OK && st.prepared == 1 && st.devices == kDevices);
+        cts_counters_ex all{}, fold{};
+        CHECK(cts_counters_allreduce_ex(eng, bptr.data(), streams.data(), kN, &all) == CTS_OK);
+        CHECK(cts_counters_read_multi_ex(eng, bptr.data(), streams.data(), kN, &fold) == CTS_OK);
+        (void)hipGetDevice(&cur);
+        CHECK(cur == 3);
+        const uint64_t got[cts::kCounterCount] = {all.bytes_checked, all.bytes_ok, all.buffers_checked, all.buffers_failed,
+                                             all.mismatched_bytes, all.connections_failed};
+        const uint64_t gotf[cts::kCounterCount] = {fold.bytes_checked, fold.bytes_ok, fold.buffers_checked,
+                                              fold.buffers_failed, fold.mismatched_bytes, fold.connections_failed};
+        for (int k = 0; k < cts::kCounterCount; ++k) CHECK(got[k] == want[k] && gotf[k] == want[k]);
+        CHECK(want[cts::kConnectionsFailed] > 0);
+        for (uint32_t g = 0; g < kN; ++g) CHECK(first_fail[g] == want_ff[g]);  // (the reads synchronised the streams)
         for (uint32_t g = 0; g < kN; ++g) CHECK(cts_engine_stream_destroy(eng[g], streams[g]) == CTS_OK);
         CHECK(cts_counters_allreduce_release() == CTS_OK);
         g_async_us.store(0);
-        std::printf("allreduce: %llu buffers, %llu failed, equal to the host fold and the oracle\n",
-                    (unsigned long long)all.buffers_checked, (unsigned long long)all.buffers_failed);
+        std::printf("allreduce: %llu buffers, %llu failed, %llu connections failed, equal to the host fold and the "
+                    "oracle\n",
+                    (unsigned long long)all.buffers_checked, (unsigned long long)all.buffers_failed,
+                    (unsigned long long)all.connections_failed);
     } else {
         std::printf("allreduce: skipped (no stub RCCL)\n");
     }
@@ -1012,8 +1040,10 @@ int main(int argc, char** argv)
     }
 
     // a DEFERRED pattern on engine 7 whose batch launch does not finish in time (a hung kernel, emulated: it completes
-    // late, 0.5-1.5 s): cts_io_pattern_destroy gives up within its bound (CTS_PATTERN_DESTROY_WAIT_MS) with CTS_E_HIP and
-    // leaves the pattern allocated under the running launch; once the launch has finished a second destroy succeeds
+    // late, 0.5-1.5 s): cts_io_pattern_destroy gives up within its bound (CTS_PATTERN_DESTROY_WAIT_MS) with
+    // CTS_E_TIMEOUT and leaves the pattern allocated under the running launch; once the launch has finished a second
+    // destroy succeeds. Then the same with nothing in flight when destroy starts: the late kernel is the filling
+    // batch destroy launches itself (its flush waits are bounded too)
     {
         std::vector<uint8_t> sender(ora_sender_buffer_size(4096));
         ora_build_sender_buffer(sender.data(), 4096);
@@ -1046,14 +1076,35 @@ int main(int argc, char** argv)
             const auto t0 = std::chrono::steady_clock::now();
             const int rc1 = cts_io_pattern_destroy(pat);
             const double s1 = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-            CHECK(rc1 == CTS_E_HIP && s1 < 0.9);
+            CHECK(rc1 == CTS_E_TIMEOUT && s1 < 0.9);
             (void)hipGetDevice(&cur);
             CHECK(cur == 3);
             g_async_us.store(0);
             std::this_thread::sleep_for(std::chrono::milliseconds(1700));  // the hung launch ends
             const int rc2 = cts_io_pattern_destroy(pat);
             CHECK(rc2 == CTS_OK);
-            std::printf("destroy under a hung launch: CTS_E_HIP after %.3f s, then ok\n", s1);
+            std::printf("destroy under a hung launch: CTS_E_TIMEOUT after %.3f s, then ok\n", s1);
+        }
+        pat = nullptr;
+        CHECK(cts_io_pattern_create(&pc, eng[7], &pat) == CTS_OK);
+        if (pat != nullptr) {
+            cts_task t{};
+            CHECK(cts_io_pattern_initiate_io(pat, &t) == CTS_OK && t.io_action == CTS_TASK_SEND);
+            CHECK(cts_io_pattern_complete_io(pat, &t, t.buffer_length, 0) == CTS_IO_CONTINUE);
+            for (int k = 0; k < 2; ++k) {  // two completions queued, fewer than a launch: nothing in flight
+                CHECK(cts_io_pattern_initiate_io(pat, &t) == CTS_OK && t.io_action == CTS_TASK_RECV);
+                std::memcpy(t.buffer + t.buffer_offset, cts_shared_buffer() + t.expected_pattern_offset, t.buffer_length);
+                CHECK(cts_io_pattern_complete_io(pat, &t, t.buffer_length, 0) == CTS_IO_CONTINUE);
+            }
+            g_async_us.store(1000000);  // the batch destroy launches finishes late
+            const auto t0 = std::chrono::steady_clock::now();
+            const int rc1 = cts_io_pattern_destroy(pat);
+            const double s1 = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+            CHECK(rc1 == CTS_E_TIMEOUT && s1 < 0.9);
+            g_async_us.store(0);
+            std::this_thread::sleep_for(std::chrono::milliseconds(1700));
+            CHECK(cts_io_pattern_destroy(pat) == CTS_OK);
+            std::printf("destroy whose own flush is late: CTS_E_TIMEOUT after %.3f s, then ok\n", s1);
         }
         unsetenv("CTS_PATTERN_DESTROY_WAIT_MS");
         cts_shared_buffer_release();

@@ -63,6 +63,7 @@ int cts_engine_stream_destroy(cts_engine*, void*) { return CTS_E_NO_DEVICE; }
 #define CTS_STUB __attribute__((weak))
 CTS_STUB hipError_t hipStreamSynchronize(hipStream_t) { return hipErrorNoDevice; }
 CTS_STUB hipError_t hipMallocAsync(void**, size_t, hipStream_t) { return hipErrorNoDevice; }
+CTS_STUB hipError_t hipMemsetAsync(void*, int, size_t, hipStream_t) { return hipErrorNoDevice; }
 CTS_STUB hipError_t hipFreeAsync(void*, hipStream_t) { return hipErrorNoDevice; }
 CTS_STUB hipError_t hipMemcpyAsync(void*, const void*, size_t, hipMemcpyKind, hipStream_t) { return hipErrorNoDevice; }
 CTS_STUB hipError_t hipEventCreateWithFlags(hipEvent_t*, unsigned) { return hipErrorNoDevice; }
@@ -77,16 +78,24 @@ CTS_STUB hipError_t hipSetDevice(int) { return hipErrorNoDevice; }
 CTS_STUB int cts_engine_device(const cts_engine*) { return CTS_E_NO_DEVICE; }
 
 // A "device" counter block here is host memory with the device layout (CTS_COUNTER_SHARDS shards of 8 u64,
-// the first 5 used), so the host-side fold of cts_counters_read_multi can be driven without a GPU.
-int cts_counters_read(cts_engine* e, const void* dev_counters, cts_counters* out, void*)
+// the first kCounterCount used), so the host-side fold of cts_counters_read_multi can be driven without a GPU.
+int cts_counters_read_ex(cts_engine* e, const void* dev_counters, cts_counters_ex* out, void*)
 {
     if (e == nullptr || dev_counters == nullptr || out == nullptr) return CTS_E_INVALID;
     const uint64_t* h = static_cast<const uint64_t*>(dev_counters);
-    uint64_t v[5] = {0, 0, 0, 0, 0};
+    uint64_t v[cts::kCounterCount] = {};
     for (uint32_t sh = 0; sh < CTS_COUNTER_SHARDS; ++sh)
-        for (int k = 0; k < 5; ++k) v[k] += h[sh * 8 + k];
-    *out = cts_counters{v[0], v[1], v[2], v[3], v[4]};
+        for (int k = 0; k < cts::kCounterCount; ++k) v[k] += h[sh * 8 + k];
+    *out = cts::counters_ex_of(v);
     return CTS_OK;
+}
+int cts_counters_read(cts_engine* e, const void* dev_counters, cts_counters* out, void* s)
+{
+    if (out == nullptr) return CTS_E_INVALID;
+    cts_counters_ex x{};
+    const int rc = cts_counters_read_ex(e, dev_counters, &x, s);
+    if (rc == CTS_OK) *out = cts::counters_of(x);
+    return rc;
 }
 
 }  // extern "C"

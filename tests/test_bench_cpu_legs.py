@@ -26,3 +26,15 @@ def test_loopback_media_stream_oracle_leg():
     assert r["connections_ok"] == 16 and r["data_errors"] == 0
     assert r["successful_frames"] + r["dropped_frames"] == 16 * 240
     assert r["recv_cpu_us_per_datagram"] > 0
+
+
+def test_cpu_baseline_labels_the_configs_it_times():
+    """BASELINE.md promises the full config set or a labelled subset: the line names what the CPU legs time."""
+    import torch
+
+    w = W.tcp_resident(n_buffers=64)
+    arena = torch.zeros(w.arena_bytes, dtype=torch.uint8)
+    r = bench.cpu_baseline(arena, w, 0.02, loopback=False)
+    assert r["configs_timed"] == ["config1-loopback", "config2", "config3-slice(1/16)"]
+    assert "configs 4 and 5" in r["configs_note"]
+    assert r["kind"] == "port" and r["value"] > 0

@@ -45,27 +45,35 @@ def _run(*argv):
 @pytest.mark.gpu
 @pytest.mark.parametrize("engines", [1, 2, 4])
 def test_engines_leg_native_threads(engines):
-    argv = ["--engines", str(engines), "--steps", "3", "--warmup", "1", "--arenas", "2", "--buffers", "512"]
+    # 2048 buffers: two corrupt ones per batch (1/1024), so DataErrors are counted
+    argv = ["--engines", str(engines), "--steps", "3", "--warmup", "1", "--arenas", "2", "--buffers", "2048"]
     if engines > 1:
         argv.append("--engines-same-gpu")
     j = _run(*argv)
     p = j["parity"]
     assert p["folded_counters_match_expected"] and p["fold_equals_sum_of_reads"] and p["records_and_first_fail_match"]
     assert j["config"]["engines"] == engines and len(j["per_gpu_GiBps"]) == engines
-    assert sum(j["config"]["connections_per_gpu"]) == 512 * engines
-    assert p["counters"]["buffers_checked"] == 512 * engines * 3 * 2
+    assert sum(j["config"]["connections_per_gpu"]) == 2048 * engines
+    assert p["counters"]["buffers_checked"] == 2048 * engines * 3 * 2
     assert j["value"] > 0
     # the node's counters over RCCL from the C ABI (every engine on this GPU: one device, one rank) = the host fold
     nc = j["node_counters"]
     assert "allreduce_error" not in nc, nc
     assert p["allreduce_equals_fold"] and nc["allreduce_counters_us"] > 0 and nc["devices"] == [0] * engines
+    # the DataError count: the timed launches claim each failed connection once per arena (slots emptied before)
+    assert p["counters"]["connections_failed"] > 0
+    # the clique was built by cts_counters_allreduce_prepare at start-up, so the first counter read pays no set-up
+    st = nc["allreduce_setup_breakdown_ms"]
+    assert st["prepared"] == 1 and st["devices"] == 1 and nc["prepare_ms"] > 0
+    assert nc["allreduce_first_call_us"] < 50e3, nc
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("launcher", ["native", "python"])
 def test_headline_launchers(launcher):
-    j = _run("--launcher", launcher, "--steps", "3", "--warmup", "1", "--arenas", "2", "--buffers", "512",
+    j = _run("--launcher", launcher, "--steps", "3", "--warmup", "1", "--arenas", "2", "--buffers", "2048",
              "--no-cpu-baseline", "--no-extras", "--no-engines-leg")
     assert j["parity"]["counters_match_expected"] and j["parity"]["records_and_first_fail_match"]
     assert j["config"]["launcher"].startswith(launcher)
-    assert j["parity"]["counters"]["buffers_checked"] == 512 * 3 * 2
+    assert j["parity"]["counters"]["buffers_checked"] == 2048 * 3 * 2
+    assert j["parity"]["counters"]["connections_failed"] == j["parity"]["connections_failed_expected"] > 0

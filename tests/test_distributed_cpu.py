@@ -20,7 +20,7 @@ import torch.multiprocessing as mp
 import oracle
 from ctstraffic_amd import distributed as D
 from ctstraffic_amd import workload as W
-from ctstraffic_amd.types import COUNTER_FIELDS
+from ctstraffic_amd.types import COUNTER_FIELDS, COUNTER_FIELDS_EX
 
 KW = dict(n_conns=48, buffers_per_conn=6, length=4096, ragged=True, corrupt_rate=7, align=1)
 
@@ -54,6 +54,13 @@ def _rank_main(rank, world, port, q):
         assert D.counters_dict(c5) == ctr
         D.allreduce_counters(c5)
         derr = D.data_error_count(torch.from_numpy(cff.view(np.int32).copy()))
+        # the same block with its DataError slot (what the kernels count): six counters in one all-reduce
+        block[5] = int((cff != 0xFFFFFFFF).sum())
+        c6 = D.fold_counters(block, COUNTER_FIELDS_EX)
+        assert D.counters_dict(c6) == {**ctr, "connections_failed": int(block[5])}
+        D.allreduce_counters(c6)
+        assert D.counters_dict(c6)["connections_failed"] == derr
+        assert {f: v for f, v in D.counters_dict(c6).items() if f in COUNTER_FIELDS} == D.counters_dict(c5)
         wall = D.max_over_ranks(float(rank + 1))
         q.put((rank, sorted(set(w.descs["conn_index"].tolist())), D.counters_dict(c5), derr, wall, ctr))
         dist.barrier()

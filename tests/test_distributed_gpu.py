@@ -146,3 +146,82 @@ def test_counters_allreduce_c_abi_over_rccl():
     assert red == fold == exp
     assert r["again"] == exp
     assert p.exitcode == 0
+
+
+def _allreduce_ex_main(q):
+    """cts_counters_allreduce_prepare, then cts_counters_allreduce_ex with the DataError count: one engine, then two
+    engines on this GPU, each block carrying the connections_failed its verify counted on its slot array."""
+    try:
+        import time
+
+        import numpy as np
+        import torch
+
+        import oracle
+        from ctstraffic_amd import Engine
+        from ctstraffic_amd import workload as W
+        from ctstraffic_amd.engine import (counters_allreduce_ex, counters_allreduce_prepare,
+                                           counters_allreduce_release, counters_allreduce_setup_times,
+                                           counters_read_multi_ex)
+
+        torch.cuda.set_device(0)
+        out = {}
+        with Engine(0) as e0, Engine(0) as e1:
+            t = time.perf_counter()
+            counters_allreduce_prepare([e0, e1])  # before any verify: the status timer's t = 0
+            out["prepare_ms"] = (time.perf_counter() - t) * 1e3
+            out["setup"] = counters_allreduce_setup_times()
+            blocks, exps = [], []
+            for k, eng in enumerate((e0, e1)):
+                w = W.connection_streams(world=2, rank=k, n_conns=64, buffers_per_conn=8, length=65536,
+                                         corrupt_rate=5 + k)
+                arena, descs = W.materialize(eng, w, device="cuda:0")
+                ctr = eng.new_counters()
+                cff = torch.full((w.n_conns,), -1, dtype=torch.int32, device="cuda:0")
+                eng.verify(arena, descs, max_length_hint=65536, counters=ctr, conn_first_fail=cff)
+                torch.cuda.synchronize()
+                blocks.append(ctr)
+                _, c, ocff = oracle.verify_batch(arena.cpu().numpy(), w.descs, n_conns=w.n_conns)
+                c["connections_failed"] = int((ocff != 0xFFFFFFFF).sum())
+                exps.append(c)
+            t = time.perf_counter()
+            red2 = counters_allreduce_ex([e0, e1], blocks)  # the prepared clique: no set-up inside
+            out["first_ex_us"] = (time.perf_counter() - t) * 1e6
+            out["two"] = (red2, counters_read_multi_ex([e0, e1], blocks),
+                          {k: exps[0][k] + exps[1][k] for k in exps[0]})
+            out["setup_after"] = counters_allreduce_setup_times()
+            out["one"] = (counters_allreduce_ex([e0], blocks[:1]), counters_read_multi_ex([e0], blocks[:1]), exps[0])
+            counters_allreduce_release()
+        q.put(out)
+    except Exception as e:  # pragma: no cover
+        q.put(("error", repr(e)))
+
+
+def test_counters_allreduce_ex_prepared_carries_data_errors():
+    """The node's DataError count through RCCL from the C ABI, after cts_counters_allreduce_prepare built the
+    clique at start-up: the first all-reduce then pays no communicator set-up (< 100 ms here; the bench reports
+    its microseconds), and the set-up breakdown names the prepared clique."""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_allreduce_ex_main, args=(q,), daemon=True)
+    p.start()
+    try:
+        r = q.get(timeout=100)
+        p.join(15)
+    finally:
+        if p.is_alive():
+            p.kill()
+            p.join(5)
+    assert not (isinstance(r, tuple) and r[0] == "error"), r[1]
+    st = r["setup"]
+    assert st["devices"] == 1 and st["prepared"] == 1  # two engines on one GPU: one rank
+    assert st["comm_init_ms"] > 0 and st["first_allreduce_ms"] > 0
+    assert r["setup_after"] == st  # the all-reduce reused the prepared clique
+    assert r["first_ex_us"] < 100e3, r["first_ex_us"]
+    red, fold, exp = r["two"]
+    assert red == fold == exp and exp["connections_failed"] > 0
+    red, fold, exp = r["one"]
+    assert red == fold == exp and exp["connections_failed"] > 0
+    assert p.exitcode == 0

@@ -96,8 +96,11 @@ FRAGMENTS = {
     "device_resident": ("cts_engine* e;  cts_engine_create(dev, &e);",
                         "int dev, const void* arena, uint64_t arena_bytes, const cts_buf_desc* descs, uint32_t n, "
                         "cts_verify_result* results, uint32_t* conn_first_fail, uint32_t n_conns, hipStream_t stream"),
+    "node_counters_prepare": ("// ctsTraffic.cpp, after the engines are created (one per GPU)",
+                              "cts_engine** engines, uint32_t gpu_count"),
     "node_counters": ("// ctsConfig.cpp, where the status line reads g_configSettings->TcpStatusDetails",
-                      "cts_engine* const* engines, const void* const* blocks, void* const* streams, uint32_t gpu_count"),
+                      "cts_engine* const* engines, const void* const* blocks, void* const* streams, uint32_t gpu_count, "
+                      "bool rccl"),
     "media_stream_records": ("// descs[i] = {byte_offset of datagram i in the recv arena, completed bytes, 0, 0, 0}",
                              "const void* arena, uint64_t arena_bytes, const cts_buf_desc* descs, uint32_t n, "
                              "cts_datagram_record* records, cts_verify_result* results, void* counters, "
@@ -120,8 +123,15 @@ FRAGMENT_PRELUDE = r"""
 #include "cts_engine.h"
 #include "cts_media_stream.h"
 typedef struct { int64_t QuadPart; } LARGE_INTEGER;
-struct ctsStatsCounter { void SetValue(uint64_t) {} };
-struct { ctsStatsCounter m_bytesRecv; } TcpStatusDetails;
+// ctsStatsTracking (ctsStatistics.hpp:87-198), ctsTcpStatistics / ctsConnectionStatistics and the two members of
+// ctsConfigSettings the status line reads (ctsConfig.h:415-416): declared by shape only
+struct ctsStatsTracking { void Add(int64_t) noexcept; void Increment() noexcept; int64_t GetValue() const noexcept; };
+struct ctsTcpStatistics { ctsStatsTracking m_bytesSent, m_bytesRecv; };
+struct ctsConnectionStatistics {
+    ctsStatsTracking m_activeConnectionCount, m_successfulCompletionCount, m_connectionErrorCount, m_protocolErrorCount;
+};
+struct ctsConfigSettings { ctsConnectionStatistics ConnectionStatusDetails; ctsTcpStatistics TcpStatusDetails; };
+extern ctsConfigSettings* g_configSettings;
 extern cts_engine* g_ctsEngine;
 """
 

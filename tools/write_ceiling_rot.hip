@@ -1,0 +1,148 @@
+// write_ceiling_rot.hip — the HBM write ceiling on a rotated footprint, beside the product fill kernel.
+//
+// Every launch writes a different 256 MiB arena of a 4 GiB set (16 arenas, far past the 256 MB Infinity
+// Cache, so no launch rewrites lines the MALL still holds), with the ctsTraffic pattern's u16 ramp as data.
+// Shapes (all plain stores):
+//   dword_slab   : the guide's store shape (MI355X_MICROARCH.md, "plain stores of the same shape": one dword per
+//                  lane, 256 B per wave-instruction), each workgroup writing whole contiguous 64 KiB slabs;
+//                  8 waves per CU = 2 workgroups of 256 per CU; also at 4 and 16 waves per CU
+//   dword_flat   : the same stores, grid-strided over the arena (consecutive waves on adjacent 256 B)
+//   b16_slab     : 16 B per lane (1 KiB per wave-instruction), whole 64 KiB slabs, 4/8/16 waves per CU
+//   product_fill : cts::fill_kernel<256> (cts_kernels.hip, included verbatim) on config 2's 4096 descriptors, at
+//                  the product's grid (1 workgroup of 4 waves per CU) and at 2 and 4 per CU
+// Each (shape, waves) is timed over 32 launches (HIP events), the whole sweep three times, interleaved; one JSON
+// line per measurement. Diagnostic only (profiles/r06/write_ceiling_rotated.jsonl).
+#include "../ctstraffic_amd/csrc/cts_kernels.hip"
+
+#include <cstdio>
+#include <vector>
+
+namespace {
+
+using cts::u32x4;
+constexpr uint64_t kArena = 256ull << 20;
+constexpr int kArenas = 16;
+constexpr int kIters = 32;
+
+// u16 ramp of the pattern: dword w of a 64 KiB slab holds u16 values 2w, 2w+1 (mod 32768, as the sender buffer)
+__device__ __forceinline__ uint32_t ramp_dword(uint32_t w)
+{
+    const uint32_t k = (2u * w) & 0x7FFFu;
+    return k | ((k + 1u) << 16);
+}
+
+template <int U>
+__global__ void __launch_bounds__(256) dword_slab_kernel(uint32_t* __restrict__ p, uint64_t bytes)
+{
+    typedef uint32_t __attribute__((address_space(1)))* gptr;
+    const uint64_t nslabs = bytes >> 16;
+    for (uint64_t sl = blockIdx.x; sl < nslabs; sl += gridDim.x) {
+        const gptr q = (gptr)(p + (sl << 14));
+        for (uint32_t r = 0; r < 16384u; r += 256u * U) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t w = r + (uint32_t)u * 256u + threadIdx.x;
+                q[w] = ramp_dword(w);
+            }
+        }
+    }
+}
+
+template <int U>
+__global__ void __launch_bounds__(256) dword_flat_kernel(uint32_t* __restrict__ p, uint64_t bytes)
+{
+    typedef uint32_t __attribute__((address_space(1)))* gptr;
+    const uint64_t words = bytes >> 2;
+    const uint64_t per_round = (uint64_t)gridDim.x * 256u * U;
+    for (uint64_t base = (uint64_t)blockIdx.x * 256u * U; base < words; base += per_round) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t w = base + (uint64_t)u * 256u + threadIdx.x;
+            ((gptr)p)[w] = ramp_dword((uint32_t)w);
+        }
+    }
+}
+
+template <int U>
+__global__ void __launch_bounds__(256) b16_slab_kernel(u32x4* __restrict__ p, uint64_t bytes)
+{
+    typedef u32x4 __attribute__((address_space(1)))* gptr;
+    const uint64_t nslabs = bytes >> 16;
+    for (uint64_t sl = blockIdx.x; sl < nslabs; sl += gridDim.x) {
+        const gptr q = (gptr)(p + (sl << 12));
+        for (uint32_t r = 0; r < 4096u; r += 256u * U) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t c = r + (uint32_t)u * 256u + threadIdx.x;
+                q[c] = u32x4{ramp_dword(4u * c), ramp_dword(4u * c + 1u), ramp_dword(4u * c + 2u),
+                             ramp_dword(4u * c + 3u)};
+            }
+        }
+    }
+}
+
+template <typename F>
+double time_rot_us(F launch)
+{
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+    for (int i = 0; i < kArenas; ++i) launch(i);  // untimed: every arena touched once
+    (void)hipEventRecord(a);
+    for (int i = 0; i < kIters; ++i) launch(i % kArenas);
+    (void)hipEventRecord(b);
+    (void)hipEventSynchronize(b);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, a, b);
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    return ms * 1e3 / kIters;
+}
+
+void emit(const char* shape, int waves_per_cu, int grid, int rep, double us)
+{
+    std::printf("{\"shape\": \"%s\", \"waves_per_cu\": %d, \"grid\": %d, \"rep\": %d, \"bytes\": %llu, "
+                "\"footprint_bytes\": %llu, \"us\": %.2f, \"GBps\": %.1f}\n",
+                shape, waves_per_cu, grid, rep, (unsigned long long)kArena, (unsigned long long)(kArena * kArenas), us,
+                (double)kArena / (us * 1e3));
+    std::fflush(stdout);
+}
+
+}  // namespace
+
+int main()
+{
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess || cus <= 0) return 1;
+    uint8_t* big = nullptr;
+    if (hipMalloc((void**)&big, kArena * kArenas) != hipSuccess) return 1;
+    const uint32_t n = (uint32_t)(kArena >> 16);
+    std::vector<cts_buf_desc> h(n);
+    for (uint32_t i = 0; i < n; ++i) h[i] = cts_buf_desc{(uint64_t)i << 16, 65536u, 0u, i, 0u};
+    cts_buf_desc* d = nullptr;
+    if (hipMalloc((void**)&d, n * sizeof(cts_buf_desc)) != hipSuccess ||
+        hipMemcpy(d, h.data(), n * sizeof(cts_buf_desc), hipMemcpyHostToDevice) != hipSuccess)
+        return 1;
+    auto arena = [&](int i) { return big + (uint64_t)i * kArena; };
+    for (int rep = 0; rep < 3; ++rep) {
+        for (int wpc : {4, 8, 16}) {  // waves per CU: workgroups of 4 waves, wpc / 4 per CU
+            const int grid = cus * wpc / 4;
+            emit("dword_slab_u8", wpc, grid, rep, time_rot_us([&](int i) {
+                     dword_slab_kernel<8><<<grid, 256>>>(reinterpret_cast<uint32_t*>(arena(i)), kArena);
+                 }));
+            emit("dword_flat_u8", wpc, grid, rep, time_rot_us([&](int i) {
+                     dword_flat_kernel<8><<<grid, 256>>>(reinterpret_cast<uint32_t*>(arena(i)), kArena);
+                 }));
+            emit("b16_slab_u4", wpc, grid, rep, time_rot_us([&](int i) {
+                     b16_slab_kernel<4><<<grid, 256>>>(reinterpret_cast<u32x4*>(arena(i)), kArena);
+                 }));
+            emit("product_fill_kernel", wpc, grid, rep, time_rot_us([&](int i) {
+                     cts::fill_kernel<256, false><<<grid, 256>>>(arena(i), kArena, d, n);
+                 }));
+        }
+    }
+    const hipError_t e = hipDeviceSynchronize();
+    (void)hipFree(d);
+    (void)hipFree(big);
+    return e == hipSuccess ? 0 : 1;
+}
