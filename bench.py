@@ -817,10 +817,31 @@ def main_engines(args, torch):
 
     def allreduce_timing():
         try:
+            # this thread's first HIP call (the runtime's per-thread set-up), apart from the first counter read: a
+            # status timer thread pays it once in its life, whatever it calls first
+            t = time.perf_counter()
+            torch.cuda.synchronize()
+            red["thread_first_hip_call_us"] = round((time.perf_counter() - t) * 1e6, 1)
             t = time.perf_counter()
             red["reduced"] = counters_allreduce_ex(engs, blocks)  # the first read: the prepared clique's
             red["allreduce_first_call_us"] = round((time.perf_counter() - t) * 1e6, 1)
             red["allreduce_counters_us"] = round(_median_us(lambda: counters_allreduce_ex(engs, blocks), 20), 1)
+            # where a new thread's first read goes: its first HIP call, a host fold (device-to-host copies and
+            # synchronizes only), then the all-reduce (fold kernel, RCCL group, copy back)
+            first = {}
+
+            def other_thread():
+                for k, fn in (("hip", torch.cuda.synchronize), ("host_fold", lambda: counters_read_multi_ex(engs, blocks)),
+                              ("allreduce", lambda: counters_allreduce_ex(engs, blocks)),
+                              ("allreduce_again", lambda: counters_allreduce_ex(engs, blocks))):
+                    t = time.perf_counter()
+                    fn()
+                    first[k] = round((time.perf_counter() - t) * 1e6, 1)
+
+            th2 = threading.Thread(target=other_thread)
+            th2.start()
+            th2.join()
+            red["new_thread_first_calls_us"] = first
             counters_allreduce_release()
         except Exception as ex:  # reported, not fatal: the verify leg above is the measurement
             red["allreduce_error"] = repr(ex)

@@ -1183,6 +1183,79 @@ __global__ void __launch_bounds__(kBlock) fill_kernel(uint8_t* __restrict__ aren
     }
 }
 
+// The workgroup path's fill in piece order. Every buffer is cut into ppb pieces of kFillPiece bytes (the last
+// piece of a buffer also takes whatever lies past ppb pieces, so any length is filled whatever the hint said);
+// pieces are numbered buffer-major and dealt to the workgroups round robin, so at any moment the grid's stores
+// cover adjacent pieces -- adjacent buffers of an arena that holds them in order -- rather than one 64 KiB slab per
+// workgroup spread over the arena. Rotated over 4 GiB of arenas, one workgroup per CU: 6.31 TB/s in this order
+// against 5.50 for the slab order at the same store width and occupancy (tools/write_ceiling_rot.hip,
+// profiles/r06/c/). The descriptors of kPieceBatch pieces come in one round trip (lane m loads piece m's, the next
+// batch's loads issued before this batch's stores) and reach the wave by readlane, so no piece waits on a
+// dependent descriptor load (each piece fetching its own: 3.8-4.1 TB/s at one workgroup per CU).
+constexpr uint32_t kFillPiece = 8192;
+constexpr int kPieceBatch = 16;
+
+template <bool NTS>
+__global__ void __launch_bounds__(kBlock) fill_pieces_kernel(uint8_t* __restrict__ arena, uint64_t arena_bytes,
+                                                             const cts_buf_desc* __restrict__ descs, uint32_t n,
+                                                             uint32_t ppb)
+{
+    typedef u32x4 __attribute__((address_space(1)))* gstore_ptr;
+    constexpr uint32_t kChunks = kFillPiece / 16;
+    const uint64_t total = (uint64_t)n * ppb;
+    const uint32_t lane = threadIdx.x;
+    const uint64_t G = gridDim.x;
+    // lane m (< kPieceBatch) holds the descriptor of piece v0 + m * G
+    auto fetch = [&](uint64_t v0) {
+        cts_buf_desc d{};
+        const uint64_t v = v0 + (uint64_t)lane * G;
+        if (lane < (uint32_t)kPieceBatch && v < total) d = descs[(uint32_t)(v / ppb)];
+        return d;
+    };
+    cts_buf_desc cur = fetch(blockIdx.x);
+    for (uint64_t v0 = blockIdx.x; v0 < total; v0 += (uint64_t)kPieceBatch * G) {
+        const cts_buf_desc nxt = fetch(v0 + (uint64_t)kPieceBatch * G);
+#pragma unroll 1
+        for (int m = 0; m < kPieceBatch; ++m) {
+            const uint64_t v = v0 + (uint64_t)m * G;
+            if (v >= total) break;
+            cts_buf_desc d;
+            d.byte_offset = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(cur.byte_offset >> 32), m)
+                             << 32) |
+                            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)cur.byte_offset, m);
+            d.length = (uint32_t)__builtin_amdgcn_readlane((int)cur.length, m);
+            d.expected_pattern_offset = (uint32_t)__builtin_amdgcn_readlane((int)cur.expected_pattern_offset, m);
+            d.conn_index = 0u;
+            d.skip_head = (uint32_t)__builtin_amdgcn_readlane((int)cur.skip_head, m);
+            if (desc_bad(d, arena_bytes)) continue;
+            const uint32_t len = d.length - d.skip_head;
+            if (len == 0u) continue;
+            const uint32_t pc = (uint32_t)(v % ppb);
+            uint8_t* sp = arena + d.byte_offset + d.skip_head;
+            const uint32_t lo = (uint32_t)((uintptr_t)sp & 15u);
+            const uint32_t nchunks = (uint32_t)(((uint64_t)lo + len + 15u) >> 4);
+            const uint32_t hi_last = (uint32_t)((uint64_t)lo + len - 16ull * (nchunks - 1u));
+            const uint32_t q0 = (d.expected_pattern_offset - lo) & 0xFFFFu;
+            u32x4* p = reinterpret_cast<u32x4*>(sp - lo);
+            const uint64_t cb = (uint64_t)pc * kChunks;
+            if (cb >= nchunks) continue;
+            const uint32_t ce = pc + 1u == ppb ? nchunks : (uint32_t)(cb + kChunks < nchunks ? cb + kChunks : nchunks);
+            if (lo == 0u && hi_last == 16u) {  // whole 16-byte chunks: straight stores
+                const gstore_ptr g = (gstore_ptr)p;
+                const uint32_t sh = q0 & 1u;
+                for (uint32_t c = (uint32_t)cb + lane; c < ce; c += kBlock) {
+                    const u32x4 e = expected_chunk((q0 + 16u * c) & 0xFFFFu, sh);
+                    if constexpr (NTS) __builtin_nontemporal_store(e, g + c);
+                    else g[c] = e;
+                }
+            } else {  // the edge chunks write only their own bytes
+                for (uint32_t c = (uint32_t)cb + lane; c < ce; c += kBlock) fill_chunk<NTS>(p, c, nchunks, q0, lo, hi_last);
+            }
+        }
+        cur = nxt;
+    }
+}
+
 // One long span, all workgroups cooperating (sender buffer materialisation).
 __global__ void __launch_bounds__(kBlock) fill_span_kernel(uint8_t* __restrict__ dst, uint64_t bytes, uint32_t e)
 {
@@ -2052,6 +2125,15 @@ hipError_t launch_fill(uint8_t* arena, uint64_t arena_bytes, const cts_buf_desc*
     // config 2 48.7 vs 51.1 us; nontemporal for datagrams: 1.46 vs 1.68 ms per 4 M; tools/rounds/r04/tune_verify.py --op fill)
     const bool nts = geo.fill_nt == 2 ? small : geo.fill_nt != 0;
     const uint32_t sgrid = grid_for(n, kBlock / 64, geo), lgrid = grid_for(n, 1, geo, geo.fill_blocks_per_cu);
+    if (!small && max_length_hint != 0) {  // the workgroup path in piece order (fill_pieces_kernel)
+        const uint32_t ppb = (uint32_t)(((uint64_t)max_length_hint + kFillPiece - 1) / kFillPiece);
+        const uint64_t total = (uint64_t)n * ppb;
+        const uint64_t cap = (uint64_t)geo.num_cus * (uint64_t)(geo.fill_blocks_per_cu > 0 ? geo.fill_blocks_per_cu : 1);
+        const uint32_t pgrid = (uint32_t)(total < cap ? total : cap);
+        if (nts) fill_pieces_kernel<true><<<pgrid, kBlock, 0, stream>>>(arena, arena_bytes, descs, n, ppb);
+        else fill_pieces_kernel<false><<<pgrid, kBlock, 0, stream>>>(arena, arena_bytes, descs, n, ppb);
+        return hipGetLastError();
+    }
     if (nts) {
         if (small) fill_kernel<64, true><<<sgrid, kBlock, 0, stream>>>(arena, arena_bytes, descs, n);
         else fill_kernel<kBlock, true><<<lgrid, kBlock, 0, stream>>>(arena, arena_bytes, descs, n);

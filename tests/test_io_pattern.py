@@ -1545,3 +1545,33 @@ def test_deferred_destroy_publishes_held_bytes(make):
     assert status_details()["bytes_recv"] == 5 * 4096 - held
     p.close()
     assert status_details()["bytes_recv"] == 5 * 4096
+
+
+def test_deferred_destroy_reports_a_failed_final_verify():
+    """cts_io_pattern_destroy returns the final flush's error (here the verifier hook failing on the batch destroy
+    verifies) instead of CTS_OK, the pattern is freed all the same, and IoPattern.close() raises it once: a second
+    close is a no-op (a CTS_E_TIMEOUT, by contrast, keeps the handle for another close: tests/cpp/engine_devices.cpp)."""
+    from ctstraffic_amd._lib import CTS_E_INVALID, CtsError
+
+    fail = [False]
+
+    def verifier(arena, descs):
+        if fail[0]:
+            raise RuntimeError("the final verify fails")
+        return _oracle_verifier(arena, descs)
+
+    shared_buffer_attach(_SENDER)
+    p = IoPattern(PatternConfig(**server_defaults(buffer_size=4096, transfer_size=100 * 4096, batch_buffers=64,
+                                                  verify_mode=A.VERIFY_DEFERRED)), verifier=verifier)
+    t = p.InitiateIo()
+    assert p.CompleteIo(t, ConnectionIdLength, 0) == ContinueIo
+    for _ in range(3):
+        t = p.InitiateIo()
+        assert _complete_data_recv(p, t, 4096) == ContinueIo
+    assert p.stats()["queued"] == 3
+    fail[0] = True
+    with pytest.raises(CtsError) as e:
+        p.close()
+    assert e.value.status == CTS_E_INVALID
+    assert p._h is None
+    p.close()

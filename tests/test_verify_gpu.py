@@ -237,18 +237,22 @@ def _fill_vs_oracle(engine):
     rng = np.random.default_rng(11)
     # aligned: 16-byte-aligned spans of whole chunks (the fill's straight-line store rounds;
     # a third are 64 KiB, phases odd and even), with 16-byte gaps that must stay untouched
-    for hint, aligned in ((0, False), (1472, False), (0, True), (1472, True)):
+    # hints: 0 (unknown: one workgroup per buffer), 1472 (the datagram path), 65536 and 70000 (the piece order,
+    # fill_pieces_kernel: 8 and 9 pieces per buffer) and 9000 (under the true maximum: the last piece of a buffer
+    # takes the rest)
+    for hint, aligned in ((0, False), (1472, False), (0, True), (1472, True), (65536, False), (65536, True),
+                          (70000, False), (9000, False), (9000, True)):
         n = 400
         descs = np.zeros(n, dtype=DESC_DTYPE)
         off = 0
         for i in range(n):
             if aligned:
                 off += 16 * int(rng.integers(0, 3))
-                ln = 65536 if rng.random() < 0.33 else 16 * int(rng.integers(0, (3000 if hint else 70000) // 16))
+                ln = 65536 if rng.random() < 0.33 else 16 * int(rng.integers(0, (3000 if hint == 1472 else 70000) // 16))
                 descs[i] = (off, ln, int(rng.integers(0, 65536)), 0, 0)
             else:
                 off += int(rng.integers(0, 9))
-                ln = int(rng.integers(0, 3000 if hint else 70000))
+                ln = int(rng.integers(0, 3000 if hint == 1472 else 70000))
                 descs[i] = (off, ln, int(rng.integers(0, 65536)), 0, int(rng.integers(0, min(ln, 30) + 1)))
             off += ln
         init = rng.integers(0, 256, size=off + 32, dtype=np.uint8)

@@ -16,8 +16,9 @@ if [[ $STEPS == *tests* ]]; then
   timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1
 fi
 if [[ $STEPS == *ceiling* ]]; then
+  # SWEEP=0: slab vs grid-strided stores at 4/8/16 waves per CU; SWEEP=1: store width and the piece-order fill
   run write-ceiling-rotated
-  timeout -k 10 180 tools/write_ceiling_rot > "$O/write_ceiling_rotated.jsonl" 2> "$O/write_ceiling_rotated.err"
+  SWEEP=${SWEEP:-1} timeout -k 10 240 tools/write_ceiling_rot > "$O/write_ceiling_rotated.jsonl" 2> "$O/write_ceiling_rotated.err"
 fi
 if [[ $STEPS == *pairs* ]]; then
   run fill-verify-pairs
@@ -33,6 +34,12 @@ if [[ $STEPS == *engines* ]]; then
   timeout -k 10 300 python bench.py --engines 1 --no-cpu-baseline --no-extras > "$O/bench_engines1.json" 2> "$O/bench_engines1.err"
   timeout -k 10 300 python bench.py --engines 2 --engines-same-gpu --no-cpu-baseline --no-extras \
     > "$O/bench_engines2same.json" 2> "$O/bench_engines2same.err"
+fi
+if [[ $STEPS == *fillx* ]]; then
+  # the fill extras alone (fill_GBps, the fill+verify pairs) through the C ABI
+  run bench-fill-extras
+  timeout -k 10 300 python bench.py --no-cpu-baseline --extras-only fill --no-engines-leg --steps 5 --warmup 2 \
+    > "$O/bench_fill.json" 2> "$O/bench_fill.err"
 fi
 if [[ $STEPS == *bench* ]]; then
   run bench

@@ -10,11 +10,14 @@
 //   b16_slab     : 16 B per lane (1 KiB per wave-instruction), whole 64 KiB slabs, 4/8/16 waves per CU
 //   product_fill : cts::fill_kernel<256> (cts_kernels.hip, included verbatim) on config 2's 4096 descriptors, at
 //                  the product's grid (1 workgroup of 4 waves per CU) and at 2 and 4 per CU
+//   b16_flat     : 16-B stores grid-strided (second pass)
+//   fill_pieces  : the candidate fill order, buffers cut in 4/8/16 KiB pieces dealt round robin (second pass)
 // Each (shape, waves) is timed over 32 launches (HIP events), the whole sweep three times, interleaved; one JSON
-// line per measurement. Diagnostic only (profiles/r06/write_ceiling_rotated.jsonl).
+// line per measurement. Diagnostic only (profiles/r06/a/write_ceiling_rotated.jsonl: SWEEP=0; SWEEP=1 the second).
 #include "../ctstraffic_amd/csrc/cts_kernels.hip"
 
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 namespace {
@@ -81,6 +84,88 @@ __global__ void __launch_bounds__(256) b16_slab_kernel(u32x4* __restrict__ p, ui
     }
 }
 
+template <int U>
+__global__ void __launch_bounds__(256) b16_flat_kernel(u32x4* __restrict__ p, uint64_t bytes)
+{
+    typedef u32x4 __attribute__((address_space(1)))* gptr;
+    const uint64_t chunks = bytes >> 4;
+    const uint64_t per_round = (uint64_t)gridDim.x * 256u * U;
+    for (uint64_t base = (uint64_t)blockIdx.x * 256u * U; base < chunks; base += per_round) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t c = base + (uint64_t)u * 256u + threadIdx.x;
+            const uint32_t w = 4u * (uint32_t)c;
+            ((gptr)p)[c] = u32x4{ramp_dword(w), ramp_dword(w + 1u), ramp_dword(w + 2u), ramp_dword(w + 3u)};
+        }
+    }
+}
+
+// The candidate product order: every buffer cut into pieces of PIECE bytes, pieces numbered buffer-major and dealt
+// to the workgroups round robin, so the grid's concurrent stores cover adjacent pieces (of adjacent buffers, when
+// the arena holds them in order) instead of one 64 KiB slab per workgroup. 16-B stores of the product's pattern
+// words (cts::expected_chunk); whole-line spans only (config 2), ppb = pieces per buffer.
+template <int PIECE>
+__global__ void __launch_bounds__(256) fill_pieces_kernel(uint8_t* __restrict__ arena, const cts_buf_desc* __restrict__ d,
+                                                          uint32_t n, uint32_t ppb)
+{
+    typedef u32x4 __attribute__((address_space(1)))* gptr;
+    constexpr uint32_t kChunks = PIECE / 16, kU = kChunks / 256;
+    const uint64_t total = (uint64_t)n * ppb;
+    for (uint64_t v = blockIdx.x; v < total; v += gridDim.x) {
+        const uint32_t i = (uint32_t)(v / ppb), pc = (uint32_t)(v % ppb);
+        const cts_buf_desc dd = d[i];
+        const uint32_t nchunks = dd.length >> 4;
+        const gptr q = (gptr)(arena + dd.byte_offset);
+        const uint32_t q0 = dd.expected_pattern_offset, sh = q0 & 1u;
+#pragma unroll
+        for (uint32_t u = 0; u < kU; ++u) {
+            const uint32_t c = pc * kChunks + u * 256u + threadIdx.x;
+            if (c < nchunks) q[c] = cts::expected_chunk((q0 + 16u * c) & 0xFFFFu, sh);
+        }
+    }
+}
+
+// fill_pieces with the descriptors of M pieces fetched per batch (lane m loads piece m's, one round trip per batch,
+// the next batch's fetched before this batch's stores) and broadcast by readlane: the per-piece dependent
+// descriptor load that starved fill_pieces at one workgroup per CU is gone.
+template <int PIECE, int M>
+__global__ void __launch_bounds__(256) fill_pieces_batched_kernel(uint8_t* __restrict__ arena,
+                                                                  const cts_buf_desc* __restrict__ d, uint32_t n,
+                                                                  uint32_t ppb)
+{
+    typedef u32x4 __attribute__((address_space(1)))* gptr;
+    constexpr uint32_t kChunks = PIECE / 16, kU = kChunks / 256;
+    const uint64_t total = (uint64_t)n * ppb;
+    const uint32_t lane = threadIdx.x;
+    const uint64_t G = gridDim.x;
+    auto fetch = [&](uint64_t v0) {
+        const uint64_t v = v0 + (uint64_t)(lane & (M - 1)) * G;
+        return d[(uint32_t)((v < total ? v : total - 1) / ppb)];
+    };
+    cts_buf_desc cur = fetch(blockIdx.x);
+    for (uint64_t v0 = blockIdx.x; v0 < total; v0 += (uint64_t)M * G) {
+        const cts_buf_desc nxt = fetch(v0 + (uint64_t)M * G < total ? v0 + (uint64_t)M * G : v0);
+#pragma unroll 1
+        for (int m = 0; m < M; ++m) {
+            const uint64_t v = v0 + (uint64_t)m * G;
+            if (v >= total) break;
+            const uint32_t off_lo = __builtin_amdgcn_readlane((int)(uint32_t)cur.byte_offset, m);
+            const uint32_t off_hi = __builtin_amdgcn_readlane((int)(uint32_t)(cur.byte_offset >> 32), m);
+            const uint32_t len = __builtin_amdgcn_readlane((int)cur.length, m);
+            const uint32_t q0 = __builtin_amdgcn_readlane((int)cur.expected_pattern_offset, m);
+            const uint32_t pc = (uint32_t)(v % ppb);
+            const gptr q = (gptr)(arena + (((uint64_t)off_hi << 32) | off_lo));
+            const uint32_t nchunks = len >> 4, sh = q0 & 1u;
+#pragma unroll
+            for (uint32_t u = 0; u < kU; ++u) {
+                const uint32_t c = pc * kChunks + u * 256u + lane;
+                if (c < nchunks) q[c] = cts::expected_chunk((q0 + 16u * c) & 0xFFFFu, sh);
+            }
+        }
+        cur = nxt;
+    }
+}
+
 template <typename F>
 double time_rot_us(F launch)
 {
@@ -124,22 +209,79 @@ int main()
         hipMemcpy(d, h.data(), n * sizeof(cts_buf_desc), hipMemcpyHostToDevice) != hipSuccess)
         return 1;
     auto arena = [&](int i) { return big + (uint64_t)i * kArena; };
+    // SWEEP=1 (default): the round-6 second pass (store width and order at 8 waves per CU, and the piece order of
+    // the candidate fill); SWEEP=0: the first pass (slab vs grid-strided at 4/8/16 waves per CU)
+    const char* sw = std::getenv("SWEEP");
+    const int sweep = sw != nullptr ? std::atoi(sw) : 1;
     for (int rep = 0; rep < 3; ++rep) {
-        for (int wpc : {4, 8, 16}) {  // waves per CU: workgroups of 4 waves, wpc / 4 per CU
-            const int grid = cus * wpc / 4;
-            emit("dword_slab_u8", wpc, grid, rep, time_rot_us([&](int i) {
-                     dword_slab_kernel<8><<<grid, 256>>>(reinterpret_cast<uint32_t*>(arena(i)), kArena);
+        if (sweep == 0) {
+            for (int wpc : {4, 8, 16}) {  // waves per CU: workgroups of 4 waves, wpc / 4 per CU
+                const int grid = cus * wpc / 4;
+                emit("dword_slab_u8", wpc, grid, rep, time_rot_us([&](int i) {
+                         dword_slab_kernel<8><<<grid, 256>>>(reinterpret_cast<uint32_t*>(arena(i)), kArena);
+                     }));
+                emit("dword_flat_u8", wpc, grid, rep, time_rot_us([&](int i) {
+                         dword_flat_kernel<8><<<grid, 256>>>(reinterpret_cast<uint32_t*>(arena(i)), kArena);
+                     }));
+                emit("b16_slab_u4", wpc, grid, rep, time_rot_us([&](int i) {
+                         b16_slab_kernel<4><<<grid, 256>>>(reinterpret_cast<u32x4*>(arena(i)), kArena);
+                     }));
+                emit("product_fill_kernel", wpc, grid, rep, time_rot_us([&](int i) {
+                         cts::fill_kernel<256, false><<<grid, 256>>>(arena(i), kArena, d, n);
+                     }));
+            }
+            continue;
+        }
+        const int g4 = cus, g8 = cus * 2, g16 = cus * 4;
+        emit("product_fill_kernel", 4, g4, rep, time_rot_us([&](int i) {
+                 cts::fill_kernel<256, false><<<g4, 256>>>(arena(i), kArena, d, n);
+             }));
+        emit("dword_flat_u8", 8, g8, rep, time_rot_us([&](int i) {
+                 dword_flat_kernel<8><<<g8, 256>>>(reinterpret_cast<uint32_t*>(arena(i)), kArena);
+             }));
+        emit("dword_flat_u2", 8, g8, rep, time_rot_us([&](int i) {
+                 dword_flat_kernel<2><<<g8, 256>>>(reinterpret_cast<uint32_t*>(arena(i)), kArena);
+             }));
+        if (sweep == 2) {  // the batched-descriptor piece order beside the flat stores it imitates
+            for (int wpc : {4, 8}) {
+                const int g = cus * wpc / 4;
+                emit("b16_flat_u1", wpc, g, rep, time_rot_us([&](int i) {
+                         b16_flat_kernel<1><<<g, 256>>>(reinterpret_cast<u32x4*>(arena(i)), kArena);
+                     }));
+                emit("fill_pieces_batched_4k_m16", wpc, g, rep, time_rot_us([&](int i) {
+                         fill_pieces_batched_kernel<4096, 16><<<g, 256>>>(arena(i), d, n, 16u);
+                     }));
+                emit("fill_pieces_batched_4k_m32", wpc, g, rep, time_rot_us([&](int i) {
+                         fill_pieces_batched_kernel<4096, 32><<<g, 256>>>(arena(i), d, n, 16u);
+                     }));
+                emit("fill_pieces_batched_8k_m16", wpc, g, rep, time_rot_us([&](int i) {
+                         fill_pieces_batched_kernel<8192, 16><<<g, 256>>>(arena(i), d, n, 8u);
+                     }));
+                emit("product_fill_pieces_kernel", wpc, g, rep, time_rot_us([&](int i) {
+                         cts::fill_pieces_kernel<false><<<g, 256>>>(arena(i), kArena, d, n, 8u);
+                     }));
+            }
+            continue;
+        }
+        for (int wpc : {4, 8, 16}) {
+            const int g = cus * wpc / 4;
+            emit("b16_flat_u1", wpc, g, rep, time_rot_us([&](int i) {
+                     b16_flat_kernel<1><<<g, 256>>>(reinterpret_cast<u32x4*>(arena(i)), kArena);
                  }));
-            emit("dword_flat_u8", wpc, grid, rep, time_rot_us([&](int i) {
-                     dword_flat_kernel<8><<<grid, 256>>>(reinterpret_cast<uint32_t*>(arena(i)), kArena);
+            emit("b16_flat_u2", wpc, g, rep, time_rot_us([&](int i) {
+                     b16_flat_kernel<2><<<g, 256>>>(reinterpret_cast<u32x4*>(arena(i)), kArena);
                  }));
-            emit("b16_slab_u4", wpc, grid, rep, time_rot_us([&](int i) {
-                     b16_slab_kernel<4><<<grid, 256>>>(reinterpret_cast<u32x4*>(arena(i)), kArena);
+            emit("fill_pieces_4k", wpc, g, rep, time_rot_us([&](int i) {
+                     fill_pieces_kernel<4096><<<g, 256>>>(arena(i), d, n, 16u);
                  }));
-            emit("product_fill_kernel", wpc, grid, rep, time_rot_us([&](int i) {
-                     cts::fill_kernel<256, false><<<grid, 256>>>(arena(i), kArena, d, n);
+            emit("fill_pieces_8k", wpc, g, rep, time_rot_us([&](int i) {
+                     fill_pieces_kernel<8192><<<g, 256>>>(arena(i), d, n, 8u);
+                 }));
+            emit("fill_pieces_16k", wpc, g, rep, time_rot_us([&](int i) {
+                     fill_pieces_kernel<16384><<<g, 256>>>(arena(i), d, n, 4u);
                  }));
         }
+        (void)g16;
     }
     const hipError_t e = hipDeviceSynchronize();
     (void)hipFree(d);
