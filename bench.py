@@ -736,8 +736,9 @@ def main_engines(args, torch):
     import threading
 
     from ctstraffic_amd import Engine, workload as W
-    from ctstraffic_amd.engine import (counters_allreduce_ex, counters_allreduce_prepare, counters_allreduce_release,
-                                       counters_allreduce_setup_times, counters_read_multi, counters_read_multi_ex)
+    from ctstraffic_amd.engine import (_multi_args, counters_allreduce_ex, counters_allreduce_prepare,
+                                       counters_allreduce_release, counters_allreduce_setup_times, counters_read_multi,
+                                       counters_read_multi_ex)
 
     G = args.engines
     same = args.engines_same_gpu
@@ -769,27 +770,59 @@ def main_engines(args, torch):
     engs, blocks = [c[0] for c in ctx], [c[1].counters for c in ctx]
     red = {}
 
-    def bounded(fn):
-        """fn() on its own thread, joined for at most ALLREDUCE_CAP_S: a collective that never returns must not
-        cost the leg's line. True when it returned."""
-        th = threading.Thread(target=fn, daemon=True)
-        th.start()
-        th.join(ALLREDUCE_CAP_S)
-        return not th.is_alive()
+    # the status thread: it builds the node's RCCL clique at start-up (cts_counters_allreduce_prepare, next to
+    # cts_engine_create, before the status timer's first tick at t = 0, ctsTraffic.cpp:107-113), waits for the
+    # timed region to end, then makes its counter reads (the first one timed apart); a collective that never returns
+    # costs the leg only its own numbers (the waits on this thread are bounded)
+    prepared, go = threading.Event(), threading.Event()
 
-    def prepare():
-        # the node's RCCL clique built next to cts_engine_create, as the status timer's first tick (t = 0,
-        # ctsTraffic.cpp:107-113) reads the counters: not inside the first counter read
+    def status_thread():
         try:
             t = time.perf_counter()
             counters_allreduce_prepare(engs)
             red["prepare_ms"] = round((time.perf_counter() - t) * 1e3, 2)
             red["allreduce_setup_breakdown_ms"] = {k: (round(v, 3) if isinstance(v, float) else v)
-                                                   for k, v in counters_allreduce_setup_times().items()}
+                                                   for k, v in counters_allreduce_setup_times().items()
+                                                   if not k.startswith("last_")}
         except Exception as ex:  # reported, not fatal: the verify leg is the measurement
             red["allreduce_error"] = repr(ex)
+        prepared.set()
+        if "allreduce_error" in red or not go.wait(ALLREDUCE_CAP_S * 4):
+            return
+        try:
+            _multi_args(engs, blocks, None)  # the ctypes array types of the binding, made once (not the C ABI's time)
+            t = time.perf_counter()
+            red["reduced"] = counters_allreduce_ex(engs, blocks)  # the first read: the prepared clique's
+            red["allreduce_first_call_us"] = round((time.perf_counter() - t) * 1e6, 1)
+            ph = counters_allreduce_setup_times()
+            red["allreduce_first_call_phases_us"] = {k[5:]: round(ph[k], 1) for k in ph if k.startswith("last_")}
+            red["allreduce_counters_us"] = round(_median_us(lambda: counters_allreduce_ex(engs, blocks), 20), 1)
+            ph = counters_allreduce_setup_times()
+            red["allreduce_last_call_phases_us"] = {k[5:]: round(ph[k], 1) for k in ph if k.startswith("last_")}
+            # a thread that never called HIP before (a timer callback landing on a new pool thread): its first HIP
+            # call, a host fold (device-to-host copies and synchronizes only), then the all-reduce, then again
+            first = {}
 
-    hung = not bounded(prepare)
+            def other_thread():
+                for k, fn in (("hip", torch.cuda.synchronize),
+                              ("host_fold", lambda: counters_read_multi_ex(engs, blocks)),
+                              ("allreduce", lambda: counters_allreduce_ex(engs, blocks)),
+                              ("allreduce_again", lambda: counters_allreduce_ex(engs, blocks))):
+                    t = time.perf_counter()
+                    fn()
+                    first[k] = round((time.perf_counter() - t) * 1e6, 1)
+
+            th2 = threading.Thread(target=other_thread)
+            th2.start()
+            th2.join()
+            red["new_thread_first_calls_us"] = first
+            counters_allreduce_release()
+        except Exception as ex:  # reported, not fatal: the verify leg above is the measurement
+            red["allreduce_error"] = repr(ex)
+
+    st = threading.Thread(target=status_thread, daemon=True)
+    st.start()
+    hung = not prepared.wait(ALLREDUCE_CAP_S)
     if hung:
         red["allreduce_error"] = "cts_counters_allreduce_prepare did not return within %d s" % ALLREDUCE_CAP_S
     t0, t1, ts = (ctypes.c_double * G)(), (ctypes.c_double * G)(), ctypes.c_double()
@@ -815,39 +848,10 @@ def main_engines(args, torch):
     # the C ABI (cts_counters_allreduce_ex: per-device fold + ncclAllReduce sum u64 x 6 per device), each timed
     fold_us = _median_us(lambda: counters_read_multi(engs, blocks), 20)
 
-    def allreduce_timing():
-        try:
-            # this thread's first HIP call (the runtime's per-thread set-up), apart from the first counter read: a
-            # status timer thread pays it once in its life, whatever it calls first
-            t = time.perf_counter()
-            torch.cuda.synchronize()
-            red["thread_first_hip_call_us"] = round((time.perf_counter() - t) * 1e6, 1)
-            t = time.perf_counter()
-            red["reduced"] = counters_allreduce_ex(engs, blocks)  # the first read: the prepared clique's
-            red["allreduce_first_call_us"] = round((time.perf_counter() - t) * 1e6, 1)
-            red["allreduce_counters_us"] = round(_median_us(lambda: counters_allreduce_ex(engs, blocks), 20), 1)
-            # where a new thread's first read goes: its first HIP call, a host fold (device-to-host copies and
-            # synchronizes only), then the all-reduce (fold kernel, RCCL group, copy back)
-            first = {}
-
-            def other_thread():
-                for k, fn in (("hip", torch.cuda.synchronize), ("host_fold", lambda: counters_read_multi_ex(engs, blocks)),
-                              ("allreduce", lambda: counters_allreduce_ex(engs, blocks)),
-                              ("allreduce_again", lambda: counters_allreduce_ex(engs, blocks))):
-                    t = time.perf_counter()
-                    fn()
-                    first[k] = round((time.perf_counter() - t) * 1e6, 1)
-
-            th2 = threading.Thread(target=other_thread)
-            th2.start()
-            th2.join()
-            red["new_thread_first_calls_us"] = first
-            counters_allreduce_release()
-        except Exception as ex:  # reported, not fatal: the verify leg above is the measurement
-            red["allreduce_error"] = repr(ex)
-
-    if not hung and "allreduce_error" not in red:
-        hung = not bounded(allreduce_timing)
+    if not hung:
+        go.set()
+        st.join(ALLREDUCE_CAP_S)
+        hung = st.is_alive()
         if hung:
             red["allreduce_error"] = "cts_counters_allreduce_ex did not return within %d s" % ALLREDUCE_CAP_S
     reduced = red.pop("reduced", None)

@@ -96,6 +96,9 @@ class CtsAllreduceSetup(ctypes.Structure):
         ("first_allreduce_ms", ctypes.c_double),
         ("devices", ctypes.c_uint32),
         ("prepared", ctypes.c_uint32),
+        ("last_fold_us", ctypes.c_double),
+        ("last_allreduce_us", ctypes.c_double),
+        ("last_readback_us", ctypes.c_double),
     ]
 
     def as_dict(self) -> dict:

@@ -54,7 +54,7 @@ struct Clique {
 std::mutex g_mu;  // guards everything below
 Rccl g_rccl;
 std::vector<std::unique_ptr<Clique>> g_cliques;
-cts_allreduce_setup g_setup{0.0, 0.0, 0.0, 0.0, 0u, 0u};  // the newest clique's set-up times
+cts_allreduce_setup g_setup{0.0, 0.0, 0.0, 0.0, 0u, 0u, 0.0, 0.0, 0.0};  // the newest clique's set-up, the last call
 
 double ms_since(std::chrono::steady_clock::time_point t0)
 {
@@ -146,7 +146,7 @@ int clique_for(const std::vector<int>& devices, double load_ms, bool prepared, C
             *out = c.get();
             return CTS_OK;
         }
-    cts_allreduce_setup t{load_ms, 0.0, 0.0, 0.0, (uint32_t)devices.size(), prepared ? 1u : 0u};
+    cts_allreduce_setup t{load_ms, 0.0, 0.0, 0.0, (uint32_t)devices.size(), prepared ? 1u : 0u, 0.0, 0.0, 0.0};
     std::unique_ptr<Clique> c(new (std::nothrow) Clique());
     if (!c) return CTS_E_NOMEM;
     c->devices = devices;
@@ -256,6 +256,7 @@ int cts_counters_allreduce_ex(cts_engine* const* engines, const void* const* dev
     std::vector<hipStream_t> lead_stream(D);
     for (size_t k = 0; k < D; ++k) lead_stream[k] = streams ? static_cast<hipStream_t>(streams[leader[k]]) : nullptr;
     // 1. fold every engine's shard block into its device's slot, on the device's leading stream
+    auto t0 = std::chrono::steady_clock::now();
     for (size_t k = 0; k < D; ++k) {
         DeviceGuard g(devices[k]);
         if (!g.ok) return CTS_E_HIP;
@@ -270,9 +271,13 @@ int cts_counters_allreduce_ex(cts_engine* const* engines, const void* const* dev
             first = false;
         }
     }
+    const double fold_us = ms_since(t0) * 1e3;
     // 2. one all-reduce per device, grouped
+    t0 = std::chrono::steady_clock::now();
     if ((rc = grouped_allreduce(*c, lead_stream)) != CTS_OK) return rc;
+    const double allreduce_us = ms_since(t0) * 1e3;
     // 3. every device's copy back; they must agree
+    t0 = std::chrono::steady_clock::now();
     uint64_t first_copy[cts::kCounterCount] = {};
     for (size_t k = 0; k < D; ++k) {
         DeviceGuard g(devices[k]);
@@ -283,6 +288,9 @@ int cts_counters_allreduce_ex(cts_engine* const* engines, const void* const* dev
         if (k == 0) std::memcpy(first_copy, h, sizeof(h));
         else if (std::memcmp(first_copy, h, sizeof(h)) != 0) return CTS_E_HIP;
     }
+    g_setup.last_fold_us = fold_us;
+    g_setup.last_allreduce_us = allreduce_us;
+    g_setup.last_readback_us = ms_since(t0) * 1e3;
     *out = cts::counters_ex_of(first_copy);
     return CTS_OK;
 }

@@ -1187,69 +1187,100 @@ __global__ void __launch_bounds__(kBlock) fill_kernel(uint8_t* __restrict__ aren
 // piece of a buffer also takes whatever lies past ppb pieces, so any length is filled whatever the hint said);
 // pieces are numbered buffer-major and dealt to the workgroups round robin, so at any moment the grid's stores
 // cover adjacent pieces -- adjacent buffers of an arena that holds them in order -- rather than one 64 KiB slab per
-// workgroup spread over the arena. Rotated over 4 GiB of arenas, one workgroup per CU: 6.31 TB/s in this order
-// against 5.50 for the slab order at the same store width and occupancy (tools/write_ceiling_rot.hip,
-// profiles/r06/c/). The descriptors of kPieceBatch pieces come in one round trip (lane m loads piece m's, the next
-// batch's loads issued before this batch's stores) and reach the wave by readlane, so no piece waits on a
-// dependent descriptor load (each piece fetching its own: 3.8-4.1 TB/s at one workgroup per CU).
+// workgroup spread over the arena. Rotated over 4 GiB of arenas at one workgroup per CU, plain 16-B stores of the
+// pattern write 6.4-6.5 TB/s in this order against 5.5-5.6 in the slab order (tools/write_ceiling_rot.hip,
+// profiles/r06/). One workgroup per CU leaves nothing to hide a wave's scalar work between its stores, so the
+// pieces of a batch are decoded together: lane m of every wave loads piece m's descriptor and works out its span
+// (checks, alignment, chunk range, pattern phase) in vector registers, the next batch's load is issued before this
+// batch's stores, and each piece then costs a few readlanes and its stores. (Decoded piece by piece on the scalar
+// unit, the same order wrote 3.9 TB/s at one workgroup per CU.)
 constexpr uint32_t kFillPiece = 8192;
 constexpr int kPieceBatch = 16;
 
-template <bool NTS>
+struct PieceJob {   // one piece, decoded by its lane of the batch
+    uint64_t base;  // 16-B-aligned address of the span's chunk 0
+    uint32_t q0;    // pattern position of chunk 0's first byte
+    uint32_t cb, ce;  // chunk range of the piece
+    uint32_t nchunks, lo, hi_last;
+    uint32_t kind;  // 0 nothing to write, 1 whole 16-B chunks, 2 edge chunks in the range
+};
+
+template <uint32_t PIECE>
+__device__ __forceinline__ PieceJob decode_piece(uint8_t* arena, uint64_t arena_bytes, const cts_buf_desc* descs,
+                                                 uint64_t v, uint64_t total, uint32_t ppb, bool mine)
+{
+    constexpr uint32_t kChunks = PIECE / 16;
+    PieceJob j{};
+    if (!mine || v >= total) return j;
+    const uint32_t i = (uint32_t)(v / ppb), pc = (uint32_t)(v - (uint64_t)i * ppb);
+    const cts_buf_desc d = descs[i];
+    if (desc_bad(d, arena_bytes) || d.length == d.skip_head) return j;
+    const uint32_t len = d.length - d.skip_head;
+    const uint64_t sp = (uint64_t)(uintptr_t)arena + d.byte_offset + d.skip_head;
+    j.lo = (uint32_t)(sp & 15u);
+    j.nchunks = (uint32_t)(((uint64_t)j.lo + len + 15u) >> 4);
+    j.hi_last = (uint32_t)((uint64_t)j.lo + len - 16ull * (j.nchunks - 1u));
+    j.q0 = (d.expected_pattern_offset - j.lo) & 0xFFFFu;
+    j.base = sp - j.lo;
+    const uint64_t cb = (uint64_t)pc * kChunks;
+    if (cb >= j.nchunks) return j;
+    j.cb = (uint32_t)cb;
+    j.ce = pc + 1u == ppb ? j.nchunks : (uint32_t)(cb + kChunks < j.nchunks ? cb + kChunks : j.nchunks);
+    j.kind = (j.lo == 0u && j.hi_last == 16u) ? 1u : 2u;
+    return j;
+}
+
+__device__ __forceinline__ uint32_t lane_u32(uint32_t x, int m) { return (uint32_t)__builtin_amdgcn_readlane((int)x, m); }
+
+// (PIECE and BATCH other than the defaults: tools/write_ceiling_rot.hip's sweep only)
+template <bool NTS, uint32_t PIECE = kFillPiece, int BATCH = kPieceBatch>
 __global__ void __launch_bounds__(kBlock) fill_pieces_kernel(uint8_t* __restrict__ arena, uint64_t arena_bytes,
                                                              const cts_buf_desc* __restrict__ descs, uint32_t n,
                                                              uint32_t ppb)
 {
     typedef u32x4 __attribute__((address_space(1)))* gstore_ptr;
-    constexpr uint32_t kChunks = kFillPiece / 16;
+    constexpr uint32_t kChunks = PIECE / 16;
+    static_assert(PIECE % (16 * kBlock) == 0 && BATCH <= 64, "whole rounds per piece; one lane per piece");
     const uint64_t total = (uint64_t)n * ppb;
     const uint32_t lane = threadIdx.x;
+    const uint32_t m_own = lane & 63u;  // every wave decodes the batch for itself (readlane reads the own wave)
     const uint64_t G = gridDim.x;
-    // lane m (< kPieceBatch) holds the descriptor of piece v0 + m * G
-    auto fetch = [&](uint64_t v0) {
-        cts_buf_desc d{};
-        const uint64_t v = v0 + (uint64_t)lane * G;
-        if (lane < (uint32_t)kPieceBatch && v < total) d = descs[(uint32_t)(v / ppb)];
-        return d;
-    };
-    cts_buf_desc cur = fetch(blockIdx.x);
-    for (uint64_t v0 = blockIdx.x; v0 < total; v0 += (uint64_t)kPieceBatch * G) {
-        const cts_buf_desc nxt = fetch(v0 + (uint64_t)kPieceBatch * G);
+    PieceJob cur = decode_piece<PIECE>(arena, arena_bytes, descs, blockIdx.x + (uint64_t)m_own * G, total, ppb,
+                                       m_own < (uint32_t)BATCH);
+    for (uint64_t v0 = blockIdx.x; v0 < total; v0 += (uint64_t)BATCH * G) {
+        const PieceJob nxt = decode_piece<PIECE>(arena, arena_bytes, descs, v0 + (uint64_t)(BATCH + m_own) * G, total,
+                                                 ppb, m_own < (uint32_t)BATCH);
 #pragma unroll 1
-        for (int m = 0; m < kPieceBatch; ++m) {
-            const uint64_t v = v0 + (uint64_t)m * G;
-            if (v >= total) break;
-            cts_buf_desc d;
-            d.byte_offset = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(cur.byte_offset >> 32), m)
-                             << 32) |
-                            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)cur.byte_offset, m);
-            d.length = (uint32_t)__builtin_amdgcn_readlane((int)cur.length, m);
-            d.expected_pattern_offset = (uint32_t)__builtin_amdgcn_readlane((int)cur.expected_pattern_offset, m);
-            d.conn_index = 0u;
-            d.skip_head = (uint32_t)__builtin_amdgcn_readlane((int)cur.skip_head, m);
-            if (desc_bad(d, arena_bytes)) continue;
-            const uint32_t len = d.length - d.skip_head;
-            if (len == 0u) continue;
-            const uint32_t pc = (uint32_t)(v % ppb);
-            uint8_t* sp = arena + d.byte_offset + d.skip_head;
-            const uint32_t lo = (uint32_t)((uintptr_t)sp & 15u);
-            const uint32_t nchunks = (uint32_t)(((uint64_t)lo + len + 15u) >> 4);
-            const uint32_t hi_last = (uint32_t)((uint64_t)lo + len - 16ull * (nchunks - 1u));
-            const uint32_t q0 = (d.expected_pattern_offset - lo) & 0xFFFFu;
-            u32x4* p = reinterpret_cast<u32x4*>(sp - lo);
-            const uint64_t cb = (uint64_t)pc * kChunks;
-            if (cb >= nchunks) continue;
-            const uint32_t ce = pc + 1u == ppb ? nchunks : (uint32_t)(cb + kChunks < nchunks ? cb + kChunks : nchunks);
-            if (lo == 0u && hi_last == 16u) {  // whole 16-byte chunks: straight stores
-                const gstore_ptr g = (gstore_ptr)p;
+        for (int m = 0; m < BATCH; ++m) {
+            const uint32_t kind = lane_u32(cur.kind, m);
+            if (kind == 0u) continue;
+            const uint64_t base = ((uint64_t)lane_u32((uint32_t)(cur.base >> 32), m) << 32) | lane_u32((uint32_t)cur.base, m);
+            const uint32_t q0 = lane_u32(cur.q0, m), cb = lane_u32(cur.cb, m), ce = lane_u32(cur.ce, m);
+            if (kind == 1u) {  // whole 16-byte chunks: straight stores
+                const gstore_ptr g = (gstore_ptr)base;
                 const uint32_t sh = q0 & 1u;
-                for (uint32_t c = (uint32_t)cb + lane; c < ce; c += kBlock) {
-                    const u32x4 e = expected_chunk((q0 + 16u * c) & 0xFFFFu, sh);
-                    if constexpr (NTS) __builtin_nontemporal_store(e, g + c);
-                    else g[c] = e;
+                if (ce <= cb + kChunks) {  // one piece: kChunks / kBlock stores per lane, unrolled
+#pragma unroll
+                    for (uint32_t u = 0; u < kChunks / kBlock; ++u) {
+                        const uint32_t c = cb + u * kBlock + lane;
+                        if (c < ce) {
+                            const u32x4 e = expected_chunk((q0 + 16u * c) & 0xFFFFu, sh);
+                            if constexpr (NTS) __builtin_nontemporal_store(e, g + c);
+                            else g[c] = e;
+                        }
+                    }
+                } else {  // the last piece of a buffer longer than the hint said
+                    for (uint32_t c = cb + lane; c < ce; c += kBlock) {
+                        const u32x4 e = expected_chunk((q0 + 16u * c) & 0xFFFFu, sh);
+                        if constexpr (NTS) __builtin_nontemporal_store(e, g + c);
+                        else g[c] = e;
+                    }
                 }
             } else {  // the edge chunks write only their own bytes
-                for (uint32_t c = (uint32_t)cb + lane; c < ce; c += kBlock) fill_chunk<NTS>(p, c, nchunks, q0, lo, hi_last);
+                const uint32_t nchunks = lane_u32(cur.nchunks, m), lo = lane_u32(cur.lo, m),
+                               hi_last = lane_u32(cur.hi_last, m);
+                u32x4* p = reinterpret_cast<u32x4*>((uintptr_t)base);
+                for (uint32_t c = cb + lane; c < ce; c += kBlock) fill_chunk<NTS>(p, c, nchunks, q0, lo, hi_last);
             }
         }
         cur = nxt;

@@ -260,6 +260,11 @@ typedef struct cts_allreduce_setup {
     double first_allreduce_ms; /* the dry run: fold of a zeroed block, the first grouped ncclAllReduce, copy back */
     uint32_t devices;          /* ranks in that clique */
     uint32_t prepared;         /* 1 = built by cts_counters_allreduce_prepare, 0 = by a first all-reduce */
+    /* the newest completed cts_counters_allreduce(_ex) call, in us: the folds launched (and other streams'
+     * synchronised), the grouped all-reduce enqueued, the copies back and their synchronisation */
+    double last_fold_us;
+    double last_allreduce_us;
+    double last_readback_us;
 } cts_allreduce_setup;
 int cts_counters_allreduce_setup_times(cts_allreduce_setup* out);
 

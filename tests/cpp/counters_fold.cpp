@@ -314,7 +314,11 @@ int main(int argc, char** argv)
         CHECK(cts_counters_allreduce_ex(x.eng.data(), x.ptrs.data(), nullptr, 6, &a) == CTS_OK && equal(a, x.want));
         CHECK(live() == 3 && g_folds - folds0 == 6);  // the prepared clique is the one used: no dry run again
         cts_allreduce_setup st2{};
-        CHECK(cts_counters_allreduce_setup_times(&st2) == CTS_OK && std::memcmp(&st, &st2, sizeof(st)) == 0);
+        CHECK(cts_counters_allreduce_setup_times(&st2) == CTS_OK);
+        // the set-up part unchanged; the last call's phases are the all-reduce's own
+        CHECK(st2.rccl_load_ms == st.rccl_load_ms && st2.slots_ms == st.slots_ms && st2.comm_init_ms == st.comm_init_ms &&
+              st2.first_allreduce_ms == st.first_allreduce_ms && st2.devices == st.devices && st2.prepared == 1);
+        CHECK(st2.last_fold_us >= 0.0 && st2.last_allreduce_us >= 0.0 && st2.last_readback_us >= 0.0);
     }
     // a clique built lazily by a first all-reduce says so
     {

@@ -41,6 +41,12 @@ if [[ $STEPS == *fillx* ]]; then
   timeout -k 10 300 python bench.py --no-cpu-baseline --extras-only fill --no-engines-leg --steps 5 --warmup 2 \
     > "$O/bench_fill.json" 2> "$O/bench_fill.err"
 fi
+if [[ $STEPS == *dgx* ]]; then
+  # the datagram extras alone (config-3 verify, MediaStream receive forms and fills)
+  run bench-datagram-extras
+  timeout -k 10 300 python bench.py --no-cpu-baseline --extras-only datagram --no-engines-leg --steps 5 --warmup 2 \
+    > "$O/bench_datagram.json" 2> "$O/bench_datagram.err"
+fi
 if [[ $STEPS == *bench* ]]; then
   run bench
   timeout -k 10 500 python bench.py > "$O/bench.json" 2> "$O/bench.err"

@@ -138,8 +138,8 @@ __global__ void __launch_bounds__(256) fill_pieces_batched_kernel(uint8_t* __res
     const uint64_t total = (uint64_t)n * ppb;
     const uint32_t lane = threadIdx.x;
     const uint64_t G = gridDim.x;
-    auto fetch = [&](uint64_t v0) {
-        const uint64_t v = v0 + (uint64_t)(lane & (M - 1)) * G;
+    auto fetch = [&](uint64_t v0) {  // (every wave its own copy: readlane reads the own wave's lanes)
+        const uint64_t v = v0 + (uint64_t)(lane & 63u & (M - 1)) * G;
         return d[(uint32_t)((v < total ? v : total - 1) / ppb)];
     };
     cts_buf_desc cur = fetch(blockIdx.x);
@@ -166,9 +166,23 @@ __global__ void __launch_bounds__(256) fill_pieces_batched_kernel(uint8_t* __res
     }
 }
 
+// bytes of p[0, bytes) that differ from the ctsTraffic pattern P(j mod 65536) (every shape writes it)
+__global__ void __launch_bounds__(256) count_bad_kernel(const uint8_t* __restrict__ p, uint64_t bytes,
+                                                        unsigned long long* bad)
+{
+    uint32_t c = 0;
+    for (uint64_t j = (uint64_t)blockIdx.x * 256u + threadIdx.x; j < bytes; j += (uint64_t)gridDim.x * 256u)
+        c += p[j] != (uint8_t)cts::pattern_byte_dev((uint32_t)j);
+    if (c) atomicAdd(bad, (unsigned long long)c);
+}
+
+unsigned long long* g_bad = nullptr;
+uint8_t* g_check = nullptr;  // the arena the last timed launch writes
+
 template <typename F>
 double time_rot_us(F launch)
 {
+    (void)hipMemset(g_check, 0xA5, kArena);  // not the pattern: a shape that skips bytes leaves them
     hipEvent_t a, b;
     (void)hipEventCreate(&a);
     (void)hipEventCreate(&b);
@@ -186,10 +200,15 @@ double time_rot_us(F launch)
 
 void emit(const char* shape, int waves_per_cu, int grid, int rep, double us)
 {
+    unsigned long long bad = ~0ull;
+    if (hipMemset(g_bad, 0, sizeof(*g_bad)) == hipSuccess) {
+        count_bad_kernel<<<1024, 256>>>(g_check, kArena, g_bad);
+        (void)hipMemcpy(&bad, g_bad, sizeof(bad), hipMemcpyDeviceToHost);
+    }
     std::printf("{\"shape\": \"%s\", \"waves_per_cu\": %d, \"grid\": %d, \"rep\": %d, \"bytes\": %llu, "
-                "\"footprint_bytes\": %llu, \"us\": %.2f, \"GBps\": %.1f}\n",
+                "\"footprint_bytes\": %llu, \"us\": %.2f, \"GBps\": %.1f, \"bad_bytes\": %llu}\n",
                 shape, waves_per_cu, grid, rep, (unsigned long long)kArena, (unsigned long long)(kArena * kArenas), us,
-                (double)kArena / (us * 1e3));
+                (double)kArena / (us * 1e3), bad);
     std::fflush(stdout);
 }
 
@@ -201,6 +220,8 @@ int main()
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess || cus <= 0) return 1;
     uint8_t* big = nullptr;
     if (hipMalloc((void**)&big, kArena * kArenas) != hipSuccess) return 1;
+    if (hipMalloc((void**)&g_bad, sizeof(*g_bad)) != hipSuccess) return 1;
+    g_check = big + (uint64_t)((kIters - 1) % kArenas) * kArena;
     const uint32_t n = (uint32_t)(kArena >> 16);
     std::vector<cts_buf_desc> h(n);
     for (uint32_t i = 0; i < n; ++i) h[i] = cts_buf_desc{(uint64_t)i << 16, 65536u, 0u, i, 0u};
@@ -248,17 +269,23 @@ int main()
                 emit("b16_flat_u1", wpc, g, rep, time_rot_us([&](int i) {
                          b16_flat_kernel<1><<<g, 256>>>(reinterpret_cast<u32x4*>(arena(i)), kArena);
                      }));
-                emit("fill_pieces_batched_4k_m16", wpc, g, rep, time_rot_us([&](int i) {
-                         fill_pieces_batched_kernel<4096, 16><<<g, 256>>>(arena(i), d, n, 16u);
-                     }));
-                emit("fill_pieces_batched_4k_m32", wpc, g, rep, time_rot_us([&](int i) {
-                         fill_pieces_batched_kernel<4096, 32><<<g, 256>>>(arena(i), d, n, 16u);
-                     }));
                 emit("fill_pieces_batched_8k_m16", wpc, g, rep, time_rot_us([&](int i) {
                          fill_pieces_batched_kernel<8192, 16><<<g, 256>>>(arena(i), d, n, 8u);
                      }));
                 emit("product_fill_pieces_kernel", wpc, g, rep, time_rot_us([&](int i) {
                          cts::fill_pieces_kernel<false><<<g, 256>>>(arena(i), kArena, d, n, 8u);
+                     }));
+                emit("product_pieces_16k_b16", wpc, g, rep, time_rot_us([&](int i) {
+                         cts::fill_pieces_kernel<false, 16384, 16><<<g, 256>>>(arena(i), kArena, d, n, 4u);
+                     }));
+                emit("product_pieces_8k_b32", wpc, g, rep, time_rot_us([&](int i) {
+                         cts::fill_pieces_kernel<false, 8192, 32><<<g, 256>>>(arena(i), kArena, d, n, 8u);
+                     }));
+                emit("product_pieces_16k_b32", wpc, g, rep, time_rot_us([&](int i) {
+                         cts::fill_pieces_kernel<false, 16384, 32><<<g, 256>>>(arena(i), kArena, d, n, 4u);
+                     }));
+                emit("product_pieces_4k_b32", wpc, g, rep, time_rot_us([&](int i) {
+                         cts::fill_pieces_kernel<false, 4096, 32><<<g, 256>>>(arena(i), kArena, d, n, 16u);
                      }));
             }
             continue;
