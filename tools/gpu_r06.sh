@@ -29,6 +29,12 @@ if [[ $STEPS == *pairs* ]]; then
       -- python3 tools/fill_verify_pairs.py > "$O/pairs_pmc_$ctr.json" 2> "$O/pairs_pmc_$ctr.err"
   done
 fi
+if [[ $STEPS == *pairsprof* ]]; then
+  # the fill+verify pairs under the kernel trace: per-launch durations of the rotated fill and verify
+  run fill-verify-pairs-kernel-trace
+  timeout -k 10 120 rocprofv3 --kernel-trace --stats -d "$O/pairs_kt" -o run --output-format csv \
+    -- python3 tools/fill_verify_pairs.py > "$O/pairs_kt.json" 2> "$O/pairs_kt.err"
+fi
 if [[ $STEPS == *engines* ]]; then
   run engines
   timeout -k 10 300 python bench.py --engines 1 --no-cpu-baseline --no-extras > "$O/bench_engines1.json" 2> "$O/bench_engines1.err"

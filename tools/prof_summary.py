@@ -27,6 +27,7 @@ DG = 16 * 1024 * 1024
 WORKLOADS = {
     "verify_wg_kernel": "config2 verify: 4096 x 64 KiB (268435456 B read)",
     "fill_kernel": "config2 fill: 4096 x 64 KiB (268435456 B written)",
+    "fill_pieces_kernel": "config2 fill in piece order (round 6): 4096 x 64 KiB (268435456 B written)",
     "verify_quad_kernel": "config3 verify: 16M x 1472 B datagrams (%d B payload read)" % (DG * 1446),
     "media_stream_verify_quad_kernel": "config3 MediaStream receive: 16M x 1472 B datagrams (%d B payload read)" % (
         DG * 1446),
@@ -48,7 +49,8 @@ WORKLOADS = {
                                      "x 1472 B datagrams (%d B written)" % (DG * 1472),
 }
 ALGO_BYTES = {"fill_batched_kernel": DG * 1472, "media_stream_fill_ring_kernel": DG * 1472,
-              "verify_wg_kernel": 268435456, "fill_kernel": 268435456, "verify_quad_kernel": DG * 1446,
+              "verify_wg_kernel": 268435456, "fill_kernel": 268435456, "fill_pieces_kernel": 268435456,
+              "verify_quad_kernel": DG * 1446,
               "media_stream_verify_quad_kernel": DG * 1446,
               "media_stream_verify_quad_kernel[strided]": DG * 1446, "verify_quad_kernel[strided]": DG * 1446,
               "media_stream_verify_quad_kernel[status]": DG * 1446,
@@ -56,6 +58,14 @@ ALGO_BYTES = {"fill_batched_kernel": DG * 1472, "media_stream_fill_ring_kernel":
               "media_stream_verify_quad_kernel[frames]": DG * 1446,
               "media_stream_verify_quad_kernel[strided][frames]": DG * 1446}
 RUNS = ("prof", "prof_dg")
+# since round 6 the config-2 run launches fill_pieces_kernel; fill_kernel is then the datagram run's payload fill
+# (cts_fill with a 1472-B hint: one wave per datagram, 26-B header skipped)
+RUN_WORKLOADS = {("fill_kernel", "prof_dg"): ("config3 datagram payload fill (cts_fill, wave per datagram): 16M x 1472 B "
+                                              "datagrams (%d B payload written)" % (DG * 1446), DG * 1446)}
+
+
+def _label(k, run):
+    return RUN_WORKLOADS.get((k, run), (WORKLOADS[k], ALGO_BYTES[k]))
 
 
 def _kname(name):
@@ -131,22 +141,23 @@ def main(src, dst):
             continue
         best = _by_kernel(csv.DictReader(open(tr)), lambda r: int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
         for k, (g, d) in best.items():
-            if WORKLOADS[k] in out:
+            label, algo = _label(k, run)
+            if label in out:
                 continue
             d = np.array(d)
-            out[WORKLOADS[k]] = {"kernel": k, "grid": int(g), "launches": int(d.size), "run": run,
-                                 "avg_us": round(float(d.mean()) / 1e3, 2), "median_us": round(float(np.median(d)) / 1e3, 2),
-                                 "min_us": round(float(d.min()) / 1e3, 2),
-                                 "algorithmic_GBps_at_avg": round(ALGO_BYTES[k] / float(d.mean()), 1)}
-            if k == "fill_kernel":
+            out[label] = {"kernel": k, "grid": int(g), "launches": int(d.size), "run": run,
+                          "avg_us": round(float(d.mean()) / 1e3, 2), "median_us": round(float(np.median(d)) / 1e3, 2),
+                          "min_us": round(float(d.min()) / 1e3, 2),
+                          "algorithmic_GBps_at_avg": round(algo / float(d.mean()), 1)}
+            if k in ("fill_kernel", "fill_pieces_kernel") and run == "prof":
                 # the profiled runs (--no-extras) launch the fill only in workload.materialize, right after
                 # torch.zeros wrote the same 256 MiB arena: the 256 MB Infinity Cache absorbs most of that re-write,
                 # so this is not an HBM write rate; the bench's extras.fill_GBps (100 launches over 8 rotated
                 # arenas, 2 GiB) is
-                out[WORKLOADS[k]]["note"] = ("MALL-resident re-write of an arena torch.zeros just wrote: not an HBM "
-                                             "rate (see bench.py extras.fill_GBps, 8 rotated arenas)")
-                out[WORKLOADS[k]].pop("algorithmic_GBps_at_avg")
-                out[WORKLOADS[k]]["algorithmic_GBps_at_avg_mall_resident"] = round(ALGO_BYTES[k] / float(d.mean()), 1)
+                out[label]["note"] = ("MALL-resident re-write of an arena torch.zeros just wrote: not an HBM "
+                                      "rate (see bench.py extras.fill_GBps, 8 rotated arenas)")
+                out[label].pop("algorithmic_GBps_at_avg")
+                out[label]["algorithmic_GBps_at_avg_mall_resident"] = round(algo / float(d.mean()), 1)
     pipe = _pipelined(os.path.join(src, "prof_pipe_kt", "run_kernel_trace.csv"))
     if pipe:
         out["config2 verify, pipelined headline leg (bench.py default, streams round-robin)"] = pipe
@@ -162,8 +173,8 @@ def main(src, dst):
                 continue
             best = _by_kernel(csv.DictReader(open(p)), lambda r: float(r["Counter_Value"]))
             for k, (g, v) in best.items():
-                e = pmc.setdefault(WORKLOADS[k], {"kernel": k, "grid": int(g), "run": run,
-                                                  "algorithmic_bytes": ALGO_BYTES[k]})
+                label, algo = _label(k, run)
+                e = pmc.setdefault(label, {"kernel": k, "grid": int(g), "run": run, "algorithmic_bytes": algo})
                 if e["run"] != run or ctr + "_median" in e:
                     continue
                 e[ctr + "_median"] = float(np.median(v))
