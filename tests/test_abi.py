@@ -249,7 +249,8 @@ def _kernels(path):
 
 
 def test_product_library_carries_only_the_default_kernels():
-    """The .so compiles one kernel per path (verify 25, small-buffer 15, MediaStream 3, the fills), each for
+    """The .so compiles one kernel per path (verify 25, small-buffer 15, MediaStream 3, the fills: the 64 KiB fill in
+    piece order when a length hint is given, one workgroup or wave per buffer otherwise), each for
     nontemporal and plain loads, the small-buffer and MediaStream kernels' strided-ring forms, the MediaStream
     compact-status and frame-sum forms (descriptors and strided ring), the MediaStream fills (descriptors, and the ring
     for strides from 1024 and below it) for plain and nontemporal stores, the SYNC mailbox grid and the counter fold of
@@ -261,5 +262,7 @@ def test_product_library_carries_only_the_default_kernels():
     assert wg == ["_ZN3cts16verify_wg_kernelILb%dEEEvPKhmPK12cts_buf_descjP17cts_verify_resultPmPjj.kd" % nt
                   for nt in (0, 1)]
     assert not any("verify_wave" in k or "_nb_" in k for k in prod)
-    assert len(prod) == 31, sorted(prod)
+    assert len(prod) == 33, sorted(prod)
+    assert sorted(k for k in prod if "fill_pieces_kernel" in k) == [
+        "_ZN3cts18fill_pieces_kernelILb%dELj8192ELi16EEEvPhmPK12cts_buf_descjj.kd" % nts for nts in (0, 1)]
     assert any("mailbox_kernel" in k for k in prod) and any("counters_fold_kernel" in k for k in prod)
