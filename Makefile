@@ -19,7 +19,7 @@ SOFLAGS   := -shared -Wl,-Bsymbolic -Wl,--version-script=$(CSRC)/exports.map
 DEVICE_VERIFY := ctstraffic_amd/build/device_verify
 PROBES := tools/hbm_read_ceiling tools/verify_ablation tools/mailbox_probe tools/rw_mix_probe tools/write_shape_probe \
           tools/fill_bisect tools/fill_abi_probe tools/mailbox_bisect tools/ring_fill_probe tools/verify_timeline \
-          tools/verify_timeline_kp tools/sync_probe tools/deferred_ab tools/slab_verify_probe tools/write_ceiling_rot
+          tools/verify_timeline_kp tools/sync_probe tools/deferred_ab tools/slab_verify_probe tools/write_ceiling_rot tools/ring_order_probe
 BENCH_MULTI := tools/libcts_bench_multi.so
 
 all: $(ENGINE_SO) oracle $(DEVICE_VERIFY) $(BENCH_MULTI) tools/pattern_cpu_probe
@@ -64,6 +64,10 @@ tools/slab_verify_probe: tools/slab_verify_probe.hip $(CSRC)/cts_kernels.hip $(H
 
 # the HBM write ceiling on a rotated 4 GiB footprint beside the product fill kernel (diagnostic, profiles/r06/)
 tools/write_ceiling_rot: tools/write_ceiling_rot.hip $(CSRC)/cts_kernels.hip $(HDRS)
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -Iinclude -I$(CSRC) $< -o $@
+
+# the MediaStream ring fill in piece order beside the product's (diagnostic, profiles/r06/g/)
+tools/ring_order_probe: tools/ring_order_probe.hip $(CSRC)/cts_kernels.hip $(HDRS)
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -Iinclude -I$(CSRC) $< -o $@
 
 # the product MediaStream fill beside flat ring walks (diagnostic)
