@@ -160,3 +160,43 @@ def test_no_slot_array_no_count(engine):
     torch.cuda.synchronize()
     _, _, _, ecff = W.expected_results(w)
     assert engine.read_counters_ex(ctr)["connections_failed"] == _failed_conns(ecff[:100])
+
+
+def test_status_line_from_the_device_counters(engine):
+    """§8f-4 on the device-resident path ("device-resident receive"): two status ticks, each adding
+    what the GPU verified since the previous tick into the status counters (never SetValue), give the TCP status
+    line's RecvBps and DataError columns and the exit summary the oracle's totals: DataError = the failed connections
+    (ctsSocketState.cpp:221-228), counted once each although both ticks' batches carry failing buffers of the same
+    connections."""
+    from ctstraffic_amd import status as S
+
+    w = W.connection_streams(n_conns=64, buffers_per_conn=16, length=65536, corrupt_rate=5)
+    arena, _ = W.materialize(engine, w)
+    host = arena.cpu().numpy()
+    halves = [w.descs[0::2], w.descs[1::2]]  # every connection's stream, split over two batches
+    ctr, cff = engine.new_counters(), _slots(w.n_conns)
+    last = dict.fromkeys(("bytes_checked", "connections_failed"), 0)
+    recv, data_errors, lines = 0, 0, []
+    for tick, h in enumerate(halves):
+        engine.verify(arena, torch.from_numpy(np.ascontiguousarray(h).view(np.uint8).copy()).to(DEV),
+                      max_length_hint=65536, counters=ctr, conn_first_fail=cff)
+        torch.cuda.synchronize()
+        node = engine.read_counters_ex(ctr)
+        d_bytes = node["bytes_checked"] - last["bytes_checked"]
+        d_conns = node["connections_failed"] - last["connections_failed"]
+        last = node
+        recv += d_bytes
+        data_errors += d_conns
+        lines.append(S.line(S.CSV, current_time_ms=1000 * (tick + 1), start_time_ms=1000 * tick,
+                            end_time_ms=1000 * (tick + 1), bytes_sent=0, bytes_recv=d_bytes, active_connections=64,
+                            successful=0, connection_errors=0, protocol_errors=data_errors))
+    _, octr, ocff = oracle.verify_batch(host, w.descs, n_conns=w.n_conns, nthreads=8)
+    assert recv == octr["bytes_checked"]
+    assert data_errors == _failed_conns(ocff) > 0
+    for tick, (ln, h) in enumerate(zip(lines, halves)):
+        fields = ln.strip().split(",")
+        assert int(fields[2]) == int(h["length"].astype(np.int64).sum())  # RecvBps over a 1 s slice
+        assert int(fields[6]) <= data_errors
+    assert int(lines[-1].strip().split(",")[6]) == data_errors  # DataError is cumulative
+    s = S.summary(64 - data_errors, 0, data_errors, recv, 0)
+    assert "ProtocolErrors [%d]" % data_errors in s and "Total Bytes Recv : %d" % recv in s
