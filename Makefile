@@ -58,6 +58,14 @@ tools/verify_timeline_kp: tools/verify_timeline.hip $(CSRC)/cts_kernels.hip $(HD
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -Iinclude -I$(CSRC) -DCTS_TOOL_KERNARG_PRELOAD=1 \
 	  -mllvm -amdgpu-kernarg-preload-count=16 $< -o $@
 
+# the same with round 5's kernels (git show 236f346), for a same-box A/B of the verify (diagnostic, profiles/r06/h/)
+ctstraffic_amd/build/cts_kernels_r05.hip:
+	@mkdir -p ctstraffic_amd/build
+	git show 236f346:ctstraffic_amd/csrc/cts_kernels.hip > $@
+tools/verify_timeline_r05: tools/verify_timeline.hip ctstraffic_amd/build/cts_kernels_r05.hip $(HDRS)
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -Iinclude -I$(CSRC) -DCTS_TL_COUNTERS=5 \
+	  '-DCTS_KERNELS_FILE="../ctstraffic_amd/build/cts_kernels_r05.hip"' $< -o $@
+
 # a slim one-buffer-per-workgroup verify beside the product and the plain slab read (diagnostic, profiles/r05/d/)
 tools/slab_verify_probe: tools/slab_verify_probe.hip $(CSRC)/cts_kernels.hip $(HDRS)
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -Iinclude -I$(CSRC) -mllvm -amdgpu-kernarg-preload-count=16 $< -o $@

@@ -13,7 +13,16 @@
 //             after the counter flush; printed as percentiles over the 1024 workgroups and by XCC.
 // Built twice by the Makefile: tools/verify_timeline and tools/verify_timeline_kp (kernel arguments preloaded into
 // SGPRs: -mllvm -amdgpu-kernarg-preload-count=16), so one call compares both prologues. Diagnostic only.
+// CTS_KERNELS_FILE: another revision of the product kernels for an A/B on one box (CTS_TL_COUNTERS: its counter
+// count per shard row, 5 before round 6)
+#ifdef CTS_KERNELS_FILE
+#include CTS_KERNELS_FILE
+#else
 #include "../ctstraffic_amd/csrc/cts_kernels.hip"
+#endif
+#ifndef CTS_TL_COUNTERS
+#define CTS_TL_COUNTERS cts::kCounterCount
+#endif
 
 #include <algorithm>
 #include <cstdio>
@@ -86,7 +95,7 @@ __global__ void __launch_bounds__(256, 8)
                 uint32_t n, cts_verify_result* __restrict__ results, uint64_t* __restrict__ counters,
                 uint32_t* __restrict__ conn_first_fail, uint32_t n_conns)
 {
-    __shared__ uint64_t ctr[1][5];
+    __shared__ uint64_t ctr[1][CTS_TL_COUNTERS];
     const uint32_t lane = threadIdx.x;
     uint32_t i = blockIdx.x;
     const uint32_t step = gridDim.x;
@@ -121,7 +130,7 @@ __global__ void __launch_bounds__(256, 4)
                    uint32_t* __restrict__ conn_first_fail, uint32_t n_conns, uint64_t* __restrict__ st)
 {
     const uint64_t t_entry = STAMP ? stamp() : 0;
-    __shared__ uint64_t ctr[1][5];
+    __shared__ uint64_t ctr[1][CTS_TL_COUNTERS];
     const uint32_t lane = threadIdx.x;
     uint32_t i = blockIdx.x, k = 0;
     const uint32_t step = gridDim.x;
@@ -299,7 +308,7 @@ __global__ void __launch_bounds__(256, 4)
                 uint32_t* __restrict__ conn_first_fail, uint32_t n_conns, uint32_t main_grid, uint32_t full_rounds,
                 TailSlot* __restrict__ slots)
 {
-    __shared__ uint64_t ctr[1][5];
+    __shared__ uint64_t ctr[1][CTS_TL_COUNTERS];
     const uint32_t lane = threadIdx.x;
     cts::zero_counters<1>(ctr);
     if (blockIdx.x < main_grid) {
