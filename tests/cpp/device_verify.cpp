@@ -106,18 +106,32 @@ int main()
     cts_engine* const engines[1] = {e};
     const void* const blocks[1] = {ctr};
     void* const streams[1] = {stream};
+    // the RCCL clique built first, as ctsTraffic's start-up would (the status timer reads at t = 0)
+    CHECK(cts_counters_allreduce_prepare(engines, 1) == CTS_OK);
+    cts_allreduce_setup st{};
+    CHECK(cts_counters_allreduce_setup_times(&st) == CTS_OK && st.prepared == 1 && st.devices == 1);
     cts_counters folded{}, reduced{};
     CHECK(cts_counters_read_multi(engines, blocks, streams, 1, &folded) == CTS_OK);
     const int ar = cts_counters_allreduce(engines, blocks, streams, 1, &reduced);
     CHECK(ar == CTS_OK);
     CHECK(std::memcmp(&folded, &c, sizeof(c)) == 0 && std::memcmp(&reduced, &c, sizeof(c)) == 0);
+    // with the DataError count: one per connection holding a corrupted buffer (ctsSocketState.cpp:221-228)
+    uint64_t failed_conns = 0;
+    for (uint32_t cc = 0; cc < conns; ++cc) failed_conns += first_fail[cc] != ~0u;
+    cts_counters_ex cx{}, fx{}, rx{};
+    CHECK(cts_counters_read_ex(e, ctr, &cx, stream) == CTS_OK);
+    CHECK(cts_counters_read_multi_ex(engines, blocks, streams, 1, &fx) == CTS_OK);
+    CHECK(cts_counters_allreduce_ex(engines, blocks, streams, 1, &rx) == CTS_OK);
+    CHECK(failed_conns > 0 && cx.connections_failed == failed_conns);
+    CHECK(std::memcmp(&cx, &fx, sizeof(cx)) == 0 && std::memcmp(&cx, &rx, sizeof(cx)) == 0);
+    CHECK(cx.bytes_checked == c.bytes_checked && cx.buffers_failed == c.buffers_failed);
     CHECK(cts_counters_allreduce_release() == CTS_OK);
 
     CHECK(hipFree(arena) == hipSuccess && hipFree(descs) == hipSuccess && hipFree(results) == hipSuccess);
     CHECK(hipFree(ctr) == hipSuccess && hipFree(cff) == hipSuccess);
     CHECK(cts_engine_stream_destroy(e, stream) == CTS_OK);
     CHECK(cts_engine_destroy(e) == CTS_OK);
-    std::printf("device_verify: ok (%u buffers, %llu bytes, %llu corrupted)\n", n, (unsigned long long)total,
-                (unsigned long long)bad_buffers);
+    std::printf("device_verify: ok (%u buffers, %llu bytes, %llu corrupted, %llu connections failed)\n", n,
+                (unsigned long long)total, (unsigned long long)bad_buffers, (unsigned long long)failed_conns);
     return 0;
 }
