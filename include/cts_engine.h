@@ -221,12 +221,13 @@ int cts_counters_read(cts_engine* engine, const void* dev_counters, cts_counters
 int cts_counters_read_multi(cts_engine* const* engines, const void* const* dev_counters, void* const* streams,
                             uint32_t n, cts_counters* out);
 /* The same node-wide counters reduced on the GPUs over RCCL (ncclAllReduce, sum,
- * ncclUint64, count 5, over xGMI), for ctsTraffic's one-process host: each engine's block is folded on its own
+ * ncclUint64, over xGMI; count 6 since round 6: the five below and the DataError count of cts_counters_ex), for
+ * ctsTraffic's one-process host: each engine's block is folded on its own
  * device (engines sharing a device fold into one slot), then one ncclAllReduce per device runs inside
  * ncclGroupStart/End on that device's stream (the stream of its first engine in the list; streams may be NULL =
  * each engine's legacy stream; another engine's stream on the same device is synchronised first). Every device's
  * result is read back and must agree. The communicators (ncclCommInitAll over the distinct devices, in list
- * order) are created on the first call for a device set and reused. RCCL is loaded on first use (librccl.so.1,
+ * order) are created by cts_counters_allreduce_prepare, or else on the first call for a device set, and reused. RCCL is loaded on first use (librccl.so.1,
  * or the path in $CTS_RCCL_LIBRARY): CTS_E_UNAVAILABLE when it cannot be; CTS_E_HIP when an RCCL or HIP call
  * fails or the devices' results disagree. Thread-safe (calls are serialised). Replaces the reads behind
  * ctsConfig::TcpStatusDetails / ctsStatsTracking (ctsConfig.h:415-417, ctsStatistics.hpp:87-198). */
