@@ -1125,6 +1125,17 @@ def test_max_length_buffers(engine):
             got = int(arena[off + skip + rel].item())
             assert got == int(pat[(exp + rel) % 65536]), (b, rel)
         assert int(arena[off + ln].item()) == 0 if b == 1 else True  # the byte after the buffer is untouched
+    # the piece-order fill (a length hint above the datagram threshold) writes the same bytes: with a hint far
+    # below the lengths (the last piece of each buffer takes the rest) and with the exact one
+    ref = arena.clone()
+    for hint in (65536, L0):
+        arena.fill_(0x33)
+        engine.fill(arena, d, max_length_hint=hint)
+        torch.cuda.synchronize()
+        for off, ln, skip in ((0, L0, 0), (off1, L1, 26)):
+            assert torch.equal(arena[off + skip:off + ln], ref[off + skip:off + ln]), hint
+        assert int(arena[off1 + L1].item()) == 0x33 and int(arena[off1 + 25].item()) == 0x33  # neighbours, header
+    del ref
     # corrupt: buffer 0 at its last byte, buffer 1 at span byte 2^31 + 9 (past 2^31)
     c0, c1 = L0 - 1, 2**31 + 9
     arena[c0] ^= 0x5A
