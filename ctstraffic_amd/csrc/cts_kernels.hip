@@ -1205,34 +1205,17 @@ struct PieceJob {   // one piece, decoded by its lane of the batch
     uint32_t kind;  // 0 nothing to write, 1 whole 16-B chunks, 2 edge chunks in the range
 };
 
-// A piece's descriptor as loaded (raw: no use of it yet, so its load stays in flight under the stores issued
-// after it) and its decode into a PieceJob.
-struct PieceRaw {
-    cts_buf_desc d;
-    uint32_t pc;   // piece of its buffer
-    uint32_t ok;   // a piece exists at this lane's index
-};
-
-__device__ __forceinline__ PieceRaw load_piece(const cts_buf_desc* descs, uint64_t v, uint64_t total, uint32_t ppb,
-                                               bool mine)
-{
-    PieceRaw r{};
-    if (!mine || v >= total) return r;
-    const uint32_t i = (uint32_t)(v / ppb);
-    r.pc = (uint32_t)(v - (uint64_t)i * ppb);
-    r.d = descs[i];
-    r.ok = 1u;
-    return r;
-}
-
 template <uint32_t PIECE>
-__device__ __forceinline__ PieceJob decode_piece(uint8_t* arena, uint64_t arena_bytes, const PieceRaw& r, uint32_t ppb)
+__device__ __forceinline__ PieceJob decode_piece(uint8_t* arena, uint64_t arena_bytes, const cts_buf_desc* descs,
+                                                 uint64_t v, uint64_t total, uint32_t ppb, bool mine)
 {
     constexpr uint32_t kChunks = PIECE / 16;
     PieceJob j{};
-    const cts_buf_desc& d = r.d;
-    if (!r.ok || desc_bad(d, arena_bytes) || d.length == d.skip_head) return j;
-    const uint32_t len = d.length - d.skip_head, pc = r.pc;
+    if (!mine || v >= total) return j;
+    const uint32_t i = (uint32_t)(v / ppb), pc = (uint32_t)(v - (uint64_t)i * ppb);
+    const cts_buf_desc d = descs[i];
+    if (desc_bad(d, arena_bytes) || d.length == d.skip_head) return j;
+    const uint32_t len = d.length - d.skip_head;
     const uint64_t sp = (uint64_t)(uintptr_t)arena + d.byte_offset + d.skip_head;
     j.lo = (uint32_t)(sp & 15u);
     j.nchunks = (uint32_t)(((uint64_t)j.lo + len + 15u) >> 4);
@@ -1250,7 +1233,7 @@ __device__ __forceinline__ PieceJob decode_piece(uint8_t* arena, uint64_t arena_
 __device__ __forceinline__ uint32_t lane_u32(uint32_t x, int m) { return (uint32_t)__builtin_amdgcn_readlane((int)x, m); }
 
 // (PIECE and BATCH other than the defaults: tools/write_ceiling_rot.hip's sweep only)
-template <bool NTS, uint32_t PIECE = kFillPiece, int BATCH = kPieceBatch, bool LATE_DECODE = false>
+template <bool NTS, uint32_t PIECE = kFillPiece, int BATCH = kPieceBatch>
 __global__ void __launch_bounds__(kBlock) fill_pieces_kernel(uint8_t* __restrict__ arena, uint64_t arena_bytes,
                                                              const cts_buf_desc* __restrict__ descs, uint32_t n,
                                                              uint32_t ppb)
@@ -1262,15 +1245,13 @@ __global__ void __launch_bounds__(kBlock) fill_pieces_kernel(uint8_t* __restrict
     const uint32_t lane = threadIdx.x;
     const uint32_t m_own = lane & 63u;  // every wave decodes the batch for itself (readlane reads the own wave)
     const uint64_t G = gridDim.x;
-    const bool mine = m_own < (uint32_t)BATCH;
-    PieceJob cur = decode_piece<PIECE>(arena, arena_bytes,
-                                       load_piece(descs, blockIdx.x + (uint64_t)m_own * G, total, ppb, mine), ppb);
+    PieceJob cur = decode_piece<PIECE>(arena, arena_bytes, descs, blockIdx.x + (uint64_t)m_own * G, total, ppb,
+                                       m_own < (uint32_t)BATCH);
     for (uint64_t v0 = blockIdx.x; v0 < total; v0 += (uint64_t)BATCH * G) {
-        // the next batch's descriptors: loaded now, decoded after this batch's stores (LATE_DECODE), so the load
-        // is in flight under them; decoded at once, the batch's stores wait for it
-        PieceRaw nraw = load_piece(descs, v0 + (uint64_t)(BATCH + m_own) * G, total, ppb, mine);
-        PieceJob nxt{};
-        if constexpr (!LATE_DECODE) nxt = decode_piece<PIECE>(arena, arena_bytes, nraw, ppb);
+        // the next batch, decoded before this batch's stores: decoded after them, the wait for its load drains the
+        // whole batch's stores (vector loads and stores share one in-order counter), 7-8 % slower (profiles/r06/j)
+        const PieceJob nxt = decode_piece<PIECE>(arena, arena_bytes, descs, v0 + (uint64_t)(BATCH + m_own) * G, total,
+                                                 ppb, m_own < (uint32_t)BATCH);
 #pragma unroll 1
         for (int m = 0; m < BATCH; ++m) {
             const uint32_t kind = lane_u32(cur.kind, m);
@@ -1304,8 +1285,7 @@ __global__ void __launch_bounds__(kBlock) fill_pieces_kernel(uint8_t* __restrict
                 for (uint32_t c = cb + lane; c < ce; c += kBlock) fill_chunk<NTS>(p, c, nchunks, q0, lo, hi_last);
             }
         }
-        if constexpr (LATE_DECODE) cur = decode_piece<PIECE>(arena, arena_bytes, nraw, ppb);
-        else cur = nxt;
+        cur = nxt;
     }
 }
 

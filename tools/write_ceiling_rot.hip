@@ -275,12 +275,6 @@ int main()
                 emit("product_fill_pieces_kernel", wpc, g, rep, time_rot_us([&](int i) {
                          cts::fill_pieces_kernel<false><<<g, 256>>>(arena(i), kArena, d, n, 8u);
                      }));
-                emit("product_pieces_8k_b16_late_decode", wpc, g, rep, time_rot_us([&](int i) {
-                         cts::fill_pieces_kernel<false, 8192, 16, true><<<g, 256>>>(arena(i), kArena, d, n, 8u);
-                     }));
-                emit("product_pieces_8k_b32_late_decode", wpc, g, rep, time_rot_us([&](int i) {
-                         cts::fill_pieces_kernel<false, 8192, 32, true><<<g, 256>>>(arena(i), kArena, d, n, 8u);
-                     }));
                 emit("product_pieces_16k_b16", wpc, g, rep, time_rot_us([&](int i) {
                          cts::fill_pieces_kernel<false, 16384, 16><<<g, 256>>>(arena(i), kArena, d, n, 4u);
                      }));
