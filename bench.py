@@ -796,6 +796,9 @@ def main_engines(args, torch):
             red["allreduce_first_call_us"] = round((time.perf_counter() - t) * 1e6, 1)
             ph = counters_allreduce_setup_times()
             red["allreduce_first_call_phases_us"] = {k[5:]: round(ph[k], 1) for k in ph if k.startswith("last_")}
+            # the same call from entry to return inside the C ABI (what a C++ host's status timer pays); the rest of
+            # allreduce_first_call_us is this ctypes binding's first call
+            red["allreduce_first_call_c_abi_us"] = round(ph["last_total_us"], 1)
             red["allreduce_counters_us"] = round(_median_us(lambda: counters_allreduce_ex(engs, blocks), 20), 1)
             ph = counters_allreduce_setup_times()
             red["allreduce_last_call_phases_us"] = {k[5:]: round(ph[k], 1) for k in ph if k.startswith("last_")}

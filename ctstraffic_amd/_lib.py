@@ -99,6 +99,7 @@ class CtsAllreduceSetup(ctypes.Structure):
         ("last_fold_us", ctypes.c_double),
         ("last_allreduce_us", ctypes.c_double),
         ("last_readback_us", ctypes.c_double),
+        ("last_total_us", ctypes.c_double),
     ]
 
     def as_dict(self) -> dict:

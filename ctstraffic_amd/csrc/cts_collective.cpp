@@ -54,7 +54,7 @@ struct Clique {
 std::mutex g_mu;  // guards everything below
 Rccl g_rccl;
 std::vector<std::unique_ptr<Clique>> g_cliques;
-cts_allreduce_setup g_setup{0.0, 0.0, 0.0, 0.0, 0u, 0u, 0.0, 0.0, 0.0};  // the newest clique's set-up, the last call
+cts_allreduce_setup g_setup{0.0, 0.0, 0.0, 0.0, 0u, 0u, 0.0, 0.0, 0.0, 0.0};  // the newest clique's set-up, the last call
 
 double ms_since(std::chrono::steady_clock::time_point t0)
 {
@@ -146,7 +146,7 @@ int clique_for(const std::vector<int>& devices, double load_ms, bool prepared, C
             *out = c.get();
             return CTS_OK;
         }
-    cts_allreduce_setup t{load_ms, 0.0, 0.0, 0.0, (uint32_t)devices.size(), prepared ? 1u : 0u, 0.0, 0.0, 0.0};
+    cts_allreduce_setup t{load_ms, 0.0, 0.0, 0.0, (uint32_t)devices.size(), prepared ? 1u : 0u, 0.0, 0.0, 0.0, 0.0};
     std::unique_ptr<Clique> c(new (std::nothrow) Clique());
     if (!c) return CTS_E_NOMEM;
     c->devices = devices;
@@ -234,6 +234,7 @@ extern "C" {
 int cts_counters_allreduce_ex(cts_engine* const* engines, const void* const* dev_counters, void* const* streams,
                               uint32_t n, cts_counters_ex* out)
 {
+    const auto t_entry = std::chrono::steady_clock::now();
     if (out == nullptr || (n > 0 && (engines == nullptr || dev_counters == nullptr))) return CTS_E_INVALID;
     if (n == 0) {
         *out = cts_counters_ex{0, 0, 0, 0, 0, 0};
@@ -292,6 +293,7 @@ int cts_counters_allreduce_ex(cts_engine* const* engines, const void* const* dev
     g_setup.last_allreduce_us = allreduce_us;
     g_setup.last_readback_us = ms_since(t0) * 1e3;
     *out = cts::counters_ex_of(first_copy);
+    g_setup.last_total_us = ms_since(t_entry) * 1e3;
     return CTS_OK;
 }
 

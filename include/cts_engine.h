@@ -262,10 +262,12 @@ typedef struct cts_allreduce_setup {
     uint32_t devices;          /* ranks in that clique */
     uint32_t prepared;         /* 1 = built by cts_counters_allreduce_prepare, 0 = by a first all-reduce */
     /* the newest completed cts_counters_allreduce(_ex) call, in us: the folds launched (and other streams'
-     * synchronised), the grouped all-reduce enqueued, the copies back and their synchronisation */
+     * synchronised), the grouped all-reduce enqueued, the copies back and their synchronisation; and the whole call
+     * from entry to return (argument checks, the device grouping, the lock and the clique lookup included) */
     double last_fold_us;
     double last_allreduce_us;
     double last_readback_us;
+    double last_total_us;
 } cts_allreduce_setup;
 int cts_counters_allreduce_setup_times(cts_allreduce_setup* out);
 

@@ -318,7 +318,8 @@ int main(int argc, char** argv)
         // the set-up part unchanged; the last call's phases are the all-reduce's own
         CHECK(st2.rccl_load_ms == st.rccl_load_ms && st2.slots_ms == st.slots_ms && st2.comm_init_ms == st.comm_init_ms &&
               st2.first_allreduce_ms == st.first_allreduce_ms && st2.devices == st.devices && st2.prepared == 1);
-        CHECK(st2.last_fold_us >= 0.0 && st2.last_allreduce_us >= 0.0 && st2.last_readback_us >= 0.0);
+        CHECK(st2.last_fold_us >= 0.0 && st2.last_allreduce_us >= 0.0 && st2.last_readback_us >= 0.0 &&
+              st2.last_total_us >= st2.last_fold_us + st2.last_allreduce_us + st2.last_readback_us);
     }
     // a clique built lazily by a first all-reduce says so
     {

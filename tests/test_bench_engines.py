@@ -69,6 +69,9 @@ def test_engines_leg_native_threads(engines):
     ph = nc["allreduce_first_call_phases_us"]
     assert ph["fold_us"] + ph["allreduce_us"] + ph["readback_us"] < 1000, nc
     assert nc["allreduce_first_call_us"] < 50e3, nc
+    # the whole first call inside the C ABI (entry to return) holds its three phases
+    assert ph["total_us"] == nc["allreduce_first_call_c_abi_us"] >= ph["fold_us"] + ph["allreduce_us"] + ph["readback_us"]
+    assert nc["allreduce_first_call_c_abi_us"] < 1000, nc
 
 
 @pytest.mark.gpu

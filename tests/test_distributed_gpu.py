@@ -222,6 +222,7 @@ def test_counters_allreduce_ex_prepared_carries_data_errors():
     assert {k: v for k, v in after.items() if not k.startswith("last_")} == \
         {k: v for k, v in st.items() if not k.startswith("last_")}
     assert after["last_fold_us"] > 0 and after["last_readback_us"] > 0
+    assert after["last_total_us"] >= after["last_fold_us"] + after["last_allreduce_us"] + after["last_readback_us"]
     assert r["first_ex_us"] < 100e3, r["first_ex_us"]
     red, fold, exp = r["two"]
     assert red == fold == exp and exp["connections_failed"] > 0
