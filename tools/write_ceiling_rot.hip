@@ -128,7 +128,7 @@ __global__ void __launch_bounds__(256) fill_pieces_kernel(uint8_t* __restrict__ 
 // fill_pieces with the descriptors of M pieces fetched per batch (lane m loads piece m's, one round trip per batch,
 // the next batch's fetched before this batch's stores) and broadcast by readlane: the per-piece dependent
 // descriptor load that starved fill_pieces at one workgroup per CU is gone.
-template <int PIECE, int M>
+template <int PIECE, int M, int DRAIN = 0>
 __global__ void __launch_bounds__(256) fill_pieces_batched_kernel(uint8_t* __restrict__ arena,
                                                                   const cts_buf_desc* __restrict__ d, uint32_t n,
                                                                   uint32_t ppb)
@@ -161,9 +161,56 @@ __global__ void __launch_bounds__(256) fill_pieces_batched_kernel(uint8_t* __res
                 const uint32_t c = pc * kChunks + u * 256u + lane;
                 if (c < nchunks) q[c] = cts::expected_chunk((q0 + 16u * c) & 0xFFFFu, sh);
             }
+            // DRAIN > 0: every DRAIN pieces, wait for this wave's stores (the batch start drains them anyway)
+            if constexpr (DRAIN > 0)
+                if ((m + 1) % DRAIN == 0) __builtin_amdgcn_s_waitcnt(0x0F70);
         }
         cur = nxt;
     }
+}
+
+// fill_pieces_batched with the batch's pieces unrolled and every store unconditional (whole full batches; the
+// rest of the pieces one by one after them): the waitcnt pass can then count the stores issued after the next
+// batch's descriptor load and wait for that load alone (vmcnt(N) with N stores still in flight) instead of draining
+// them (vmcnt(0)), as it must when a runtime loop or a branch sits between the load and its use.
+template <int PIECE, int M>
+__global__ void __launch_bounds__(256) fill_pieces_nodrain_kernel(uint8_t* __restrict__ arena,
+                                                                  const cts_buf_desc* __restrict__ d, uint32_t n,
+                                                                  uint32_t ppb)
+{
+    typedef u32x4 __attribute__((address_space(1)))* gptr;
+    constexpr uint32_t kChunks = PIECE / 16, kU = kChunks / 256;
+    const uint64_t total = (uint64_t)n * ppb;
+    const uint32_t lane = threadIdx.x;
+    const uint64_t G = gridDim.x;
+    auto fetch = [&](uint64_t v0) {
+        const uint64_t v = v0 + (uint64_t)(lane & 63u & (M - 1)) * G;
+        return d[(uint32_t)((v < total ? v : total - 1) / ppb)];
+    };
+    auto piece = [&](const cts_buf_desc& c, int m, uint64_t v) {
+        const uint32_t off_lo = __builtin_amdgcn_readlane((int)(uint32_t)c.byte_offset, m);
+        const uint32_t off_hi = __builtin_amdgcn_readlane((int)(uint32_t)(c.byte_offset >> 32), m);
+        const uint32_t q0 = __builtin_amdgcn_readlane((int)c.expected_pattern_offset, m);
+        const uint32_t pc = (uint32_t)v % ppb;  // (pieces < 2^32 here; a 64-bit remainder branches per piece)
+        const gptr q = (gptr)(arena + (((uint64_t)off_hi << 32) | off_lo));
+#pragma unroll
+        for (uint32_t u = 0; u < kU; ++u) {
+            const uint32_t ch = pc * kChunks + u * 256u + lane;
+            q[ch] = cts::expected_chunk((q0 + 16u * ch) & 0xFFFFu, q0 & 1u);
+        }
+    };
+    uint64_t v0 = blockIdx.x;
+    cts_buf_desc cur = fetch(v0);
+    // the first batch's load complete before the loop: otherwise the loop header merges "that load pending, nothing
+    // after it" with the back edge's "32 stores pending" and waits as for the first, draining the stores every batch
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), expcnt and lgkmcnt unconstrained (gfx9 encoding)
+    for (; v0 + (uint64_t)(M - 1) * G < total; v0 += (uint64_t)M * G) {
+        const cts_buf_desc nxt = fetch(v0 + (uint64_t)M * G < total ? v0 + (uint64_t)M * G : v0);
+#pragma unroll
+        for (int m = 0; m < M; ++m) piece(cur, m, v0 + (uint64_t)m * G);
+        cur = nxt;
+    }
+    for (int m = 0; m < M && v0 + (uint64_t)m * G < total; ++m) piece(cur, m, v0 + (uint64_t)m * G);
 }
 
 // bytes of p[0, bytes) that differ from the ctsTraffic pattern P(j mod 65536) (every shape writes it)
@@ -264,7 +311,7 @@ int main()
                  dword_flat_kernel<2><<<g8, 256>>>(reinterpret_cast<uint32_t*>(arena(i)), kArena);
              }));
         if (sweep == 2) {  // the batched-descriptor piece order beside the flat stores it imitates
-            for (int wpc : {4, 8}) {
+            for (int wpc : {4, 8, 16}) {
                 const int g = cus * wpc / 4;
                 emit("b16_flat_u1", wpc, g, rep, time_rot_us([&](int i) {
                          b16_flat_kernel<1><<<g, 256>>>(reinterpret_cast<u32x4*>(arena(i)), kArena);
@@ -272,20 +319,26 @@ int main()
                 emit("fill_pieces_batched_8k_m16", wpc, g, rep, time_rot_us([&](int i) {
                          fill_pieces_batched_kernel<8192, 16><<<g, 256>>>(arena(i), d, n, 8u);
                      }));
+                emit("fill_pieces_batched_8k_m16_drain1", wpc, g, rep, time_rot_us([&](int i) {
+                         fill_pieces_batched_kernel<8192, 16, 1><<<g, 256>>>(arena(i), d, n, 8u);
+                     }));
+                emit("fill_pieces_batched_8k_m16_drain2", wpc, g, rep, time_rot_us([&](int i) {
+                         fill_pieces_batched_kernel<8192, 16, 2><<<g, 256>>>(arena(i), d, n, 8u);
+                     }));
+                emit("fill_pieces_batched_8k_m16_drain4", wpc, g, rep, time_rot_us([&](int i) {
+                         fill_pieces_batched_kernel<8192, 16, 4><<<g, 256>>>(arena(i), d, n, 8u);
+                     }));
+                emit("fill_pieces_batched_8k_m16_drain8", wpc, g, rep, time_rot_us([&](int i) {
+                         fill_pieces_batched_kernel<8192, 16, 8><<<g, 256>>>(arena(i), d, n, 8u);
+                     }));
+                emit("fill_pieces_nodrain_8k_m16", wpc, g, rep, time_rot_us([&](int i) {
+                         fill_pieces_nodrain_kernel<8192, 16><<<g, 256>>>(arena(i), d, n, 8u);
+                     }));
+                emit("fill_pieces_nodrain_8k_m8", wpc, g, rep, time_rot_us([&](int i) {
+                         fill_pieces_nodrain_kernel<8192, 8><<<g, 256>>>(arena(i), d, n, 8u);
+                     }));
                 emit("product_fill_pieces_kernel", wpc, g, rep, time_rot_us([&](int i) {
                          cts::fill_pieces_kernel<false><<<g, 256>>>(arena(i), kArena, d, n, 8u);
-                     }));
-                emit("product_pieces_16k_b16", wpc, g, rep, time_rot_us([&](int i) {
-                         cts::fill_pieces_kernel<false, 16384, 16><<<g, 256>>>(arena(i), kArena, d, n, 4u);
-                     }));
-                emit("product_pieces_8k_b32", wpc, g, rep, time_rot_us([&](int i) {
-                         cts::fill_pieces_kernel<false, 8192, 32><<<g, 256>>>(arena(i), kArena, d, n, 8u);
-                     }));
-                emit("product_pieces_16k_b32", wpc, g, rep, time_rot_us([&](int i) {
-                         cts::fill_pieces_kernel<false, 16384, 32><<<g, 256>>>(arena(i), kArena, d, n, 4u);
-                     }));
-                emit("product_pieces_4k_b32", wpc, g, rep, time_rot_us([&](int i) {
-                         cts::fill_pieces_kernel<false, 4096, 32><<<g, 256>>>(arena(i), kArena, d, n, 16u);
                      }));
             }
             continue;
