@@ -12,6 +12,8 @@
 //                  the product's grid (1 workgroup of 4 waves per CU) and at 2 and 4 per CU
 //   b16_flat     : 16-B stores grid-strided (second pass)
 //   fill_pieces  : the candidate fill order, buffers cut in 4/8/16 KiB pieces dealt round robin (second pass)
+//   SWEEP=2      : the batched piece order beside the product's fill_pieces_kernel, with the stores waited for
+//                  every 1-8 pieces or never (profiles/r06/l/)
 // Each (shape, waves) is timed over 32 launches (HIP events), the whole sweep three times, interleaved; one JSON
 // line per measurement. Diagnostic only (profiles/r06/a/write_ceiling_rotated.jsonl: SWEEP=0; SWEEP=1 the second).
 #include "../ctstraffic_amd/csrc/cts_kernels.hip"
