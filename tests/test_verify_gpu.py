@@ -266,6 +266,43 @@ def _fill_vs_oracle(engine):
         assert bad.size == 0, bad[:10]
 
 
+@pytest.mark.parametrize("hint", [0, 1472, 65536, 9000])
+def test_fill_skips_bad_descriptors(engine, hint):
+    """Descriptors the reference would FAIL_FAST on or that leave the arena (expected offset >= 65536,
+    ctsIOPattern.cpp:723-725; a skip longer than the buffer; a span past the arena's end, straddling it or wholly
+    beyond) write nothing on every fill path (hint 0: workgroup per buffer, 1472: the datagram path, 65536 / 9000: the
+    piece order), the bytes past the arena inside the same allocation included; the valid ones around them are filled
+    as the oracle fills them (it skips the same descriptors)."""
+    rng = np.random.default_rng(0xBAD)
+    n, N = 300, 0
+    descs = np.zeros(n, dtype=DESC_DTYPE)
+    big = hint in (65536, 9000)
+    for i in range(n):
+        ln = 65536 if big and rng.random() < 0.5 else int(rng.integers(1, 1473 if hint == 1472 else 70000))
+        descs[i] = (N, ln, int(rng.integers(0, 65536)), i, int(rng.integers(0, min(ln, 30) + 1)))
+        N += ln + int(rng.integers(0, 9))
+    arena_bytes = N - 5000  # the last buffers straddle or lie past the end
+    bad = rng.choice(n - 10, size=30, replace=False)
+    for k, i in enumerate(bad):
+        if k % 3 == 0:
+            descs[i]["expected_pattern_offset"] = 65536 + k
+        elif k % 3 == 1:
+            descs[i]["skip_head"] = int(descs[i]["length"]) + 1
+        else:
+            descs[i]["byte_offset"] = arena_bytes + 64 * k  # past the end
+    past = descs["byte_offset"].astype(np.int64) + descs["length"] > arena_bytes
+    assert past.sum() > 10 and (descs["byte_offset"][past] < arena_bytes).any()  # straddling ones too
+    init = rng.integers(0, 256, size=N + 4096, dtype=np.uint8)
+    exp = init.copy()
+    oracle.fill(exp[:arena_bytes], descs)
+    base = to_dev(init)
+    engine.fill(base[:arena_bytes], to_dev(descs), max_length_hint=hint)
+    torch.cuda.synchronize()
+    diff = np.nonzero(base.cpu().numpy() != exp)[0]
+    assert diff.size == 0, diff[:10]
+    assert not np.array_equal(exp, init)  # the valid buffers were written
+
+
 def test_counters_accumulate_and_reset(engine):
     w = W.tcp_resident(n_buffers=256, corrupt_rate=64)
     arena, descs = W.materialize(engine, w)
