@@ -5,6 +5,7 @@
 // deals the pieces of 64 KiB buffers), so the grid's concurrent stores cover adjacent pieces. A batch of 16 pieces'
 // datagram lengths and headers is staged in LDS (at most 10 datagrams touch a piece for strides >= 1024), the next
 // batch loaded into registers before this batch's stores; each wave writes 2 rounds of 64 chunks of every piece.
+// A second form (ring_wave_pieces_kernel, profiles/r06/q/) deals 2 KiB pieces to every wave, without LDS or barriers.
 // Every datagram's bytes are compared with the product's output; 16 M x 1472 B with 1 % of the lengths random.
 //   build: make tools/ring_order_probe     run: tools/ring_order_probe [datagrams] [reps]
 #include "../ctstraffic_amd/csrc/cts_kernels.hip"
