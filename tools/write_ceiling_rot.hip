@@ -215,6 +215,92 @@ __global__ void __launch_bounds__(256) fill_pieces_nodrain_kernel(uint8_t* __res
     for (int m = 0; m < M && v0 + (uint64_t)m * G < total; ++m) piece(cur, m, v0 + (uint64_t)m * G);
 }
 
+// The product's fill_pieces_kernel with the next batch's decode moved off the batch start: the descriptors are
+// loaded and waited for at the batch start as in the product (the once-per-batch wait that keeps the waves' stores
+// adjacent, profiles/r06/l/), but the ~60 VALU of the decode run after piece 0's stores are issued instead of between
+// the wait and the first store. (Probe copy of the product kernel; WAIT = false drops the explicit wait, so the
+// compiler places it at the decode.)
+template <bool WAIT>
+__global__ void __launch_bounds__(256) fill_pieces_deferred_kernel(uint8_t* __restrict__ arena, uint64_t arena_bytes,
+                                                                   const cts_buf_desc* __restrict__ descs, uint32_t n,
+                                                                   uint32_t ppb)
+{
+    typedef u32x4 __attribute__((address_space(1)))* gstore_ptr;
+    constexpr uint32_t kChunks = cts::kFillPiece / 16;
+    constexpr int BATCH = cts::kPieceBatch;
+    constexpr uint32_t kBlk = 256;
+    const uint64_t total = (uint64_t)n * ppb;
+    const uint32_t lane = threadIdx.x;
+    const uint32_t m_own = lane & 63u;
+    const uint64_t G = gridDim.x;
+    const bool mine = m_own < (uint32_t)BATCH;
+    struct Raw {
+        cts_buf_desc d;
+        uint64_t v;
+    };
+    auto load = [&](uint64_t v) {
+        Raw r{};
+        r.v = v;
+        if (mine && v < total) r.d = descs[(uint32_t)(v / ppb)];
+        return r;
+    };
+    auto decode = [&](const Raw& r) {
+        cts::PieceJob j{};
+        if (!mine || r.v >= total) return j;
+        const uint32_t i = (uint32_t)(r.v / ppb), pc = (uint32_t)(r.v - (uint64_t)i * ppb);
+        const cts_buf_desc& d = r.d;
+        if (cts::desc_bad(d, arena_bytes) || d.length == d.skip_head) return j;
+        const uint32_t len = d.length - d.skip_head;
+        const uint64_t sp = (uint64_t)(uintptr_t)arena + d.byte_offset + d.skip_head;
+        j.lo = (uint32_t)(sp & 15u);
+        j.nchunks = (uint32_t)(((uint64_t)j.lo + len + 15u) >> 4);
+        j.hi_last = (uint32_t)((uint64_t)j.lo + len - 16ull * (j.nchunks - 1u));
+        j.q0 = (d.expected_pattern_offset - j.lo) & 0xFFFFu;
+        j.base = sp - j.lo;
+        const uint64_t cb = (uint64_t)pc * kChunks;
+        if (cb >= j.nchunks) return j;
+        j.cb = (uint32_t)cb;
+        j.ce = pc + 1u == ppb ? j.nchunks : (uint32_t)(cb + kChunks < j.nchunks ? cb + kChunks : j.nchunks);
+        j.kind = (j.lo == 0u && j.hi_last == 16u) ? 1u : 2u;
+        return j;
+    };
+    auto piece = [&](const cts::PieceJob& cur, int m) {
+        const uint32_t kind = cts::lane_u32(cur.kind, m);
+        if (kind == 0u) return;
+        const uint64_t base = ((uint64_t)cts::lane_u32((uint32_t)(cur.base >> 32), m) << 32) |
+                              cts::lane_u32((uint32_t)cur.base, m);
+        const uint32_t q0 = cts::lane_u32(cur.q0, m), cb = cts::lane_u32(cur.cb, m), ce = cts::lane_u32(cur.ce, m);
+        if (kind == 1u) {
+            const gstore_ptr g = (gstore_ptr)base;
+            const uint32_t sh = q0 & 1u;
+            if (ce <= cb + kChunks) {
+#pragma unroll
+                for (uint32_t u = 0; u < kChunks / kBlk; ++u) {
+                    const uint32_t c = cb + u * kBlk + lane;
+                    if (c < ce) g[c] = cts::expected_chunk((q0 + 16u * c) & 0xFFFFu, sh);
+                }
+            } else {
+                for (uint32_t c = cb + lane; c < ce; c += kBlk) g[c] = cts::expected_chunk((q0 + 16u * c) & 0xFFFFu, sh);
+            }
+        } else {
+            const uint32_t nchunks = cts::lane_u32(cur.nchunks, m), lo = cts::lane_u32(cur.lo, m),
+                           hi_last = cts::lane_u32(cur.hi_last, m);
+            u32x4* p = reinterpret_cast<u32x4*>((uintptr_t)base);
+            for (uint32_t c = cb + lane; c < ce; c += kBlk) cts::fill_chunk<false>(p, c, nchunks, q0, lo, hi_last);
+        }
+    };
+    cts::PieceJob cur = decode(load(blockIdx.x + (uint64_t)m_own * G));
+    for (uint64_t v0 = blockIdx.x; v0 < total; v0 += (uint64_t)BATCH * G) {
+        const Raw raw = load(v0 + (uint64_t)(BATCH + m_own) * G);
+        if constexpr (WAIT) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the product's cadence
+        piece(cur, 0);
+        const cts::PieceJob nxt = decode(raw);
+#pragma unroll 1
+        for (int m = 1; m < BATCH; ++m) piece(cur, m);
+        cur = nxt;
+    }
+}
+
 // bytes of p[0, bytes) that differ from the ctsTraffic pattern P(j mod 65536) (every shape writes it)
 __global__ void __launch_bounds__(256) count_bad_kernel(const uint8_t* __restrict__ p, uint64_t bytes,
                                                         unsigned long long* bad)
@@ -320,6 +406,12 @@ int main()
                      }));
                 emit("fill_pieces_batched_8k_m16", wpc, g, rep, time_rot_us([&](int i) {
                          fill_pieces_batched_kernel<8192, 16><<<g, 256>>>(arena(i), d, n, 8u);
+                     }));
+                emit("product_fill_pieces_deferred_decode", wpc, g, rep, time_rot_us([&](int i) {
+                         fill_pieces_deferred_kernel<true><<<g, 256>>>(arena(i), kArena, d, n, 8u);
+                     }));
+                emit("product_fill_pieces_deferred_decode_nowait", wpc, g, rep, time_rot_us([&](int i) {
+                         fill_pieces_deferred_kernel<false><<<g, 256>>>(arena(i), kArena, d, n, 8u);
                      }));
                 emit("fill_pieces_batched_8k_m16_drain1", wpc, g, rep, time_rot_us([&](int i) {
                          fill_pieces_batched_kernel<8192, 16, 1><<<g, 256>>>(arena(i), d, n, 8u);
