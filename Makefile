@@ -19,7 +19,8 @@ SOFLAGS   := -shared -Wl,-Bsymbolic -Wl,--version-script=$(CSRC)/exports.map
 DEVICE_VERIFY := ctstraffic_amd/build/device_verify
 PROBES := tools/hbm_read_ceiling tools/verify_ablation tools/mailbox_probe tools/rw_mix_probe tools/write_shape_probe \
           tools/fill_bisect tools/fill_abi_probe tools/mailbox_bisect tools/ring_fill_probe tools/verify_timeline \
-          tools/verify_timeline_kp tools/sync_probe tools/deferred_ab tools/slab_verify_probe tools/write_ceiling_rot tools/ring_order_probe
+          tools/verify_timeline_kp tools/sync_probe tools/deferred_ab tools/slab_verify_probe tools/write_ceiling_rot tools/ring_order_probe \
+          tools/first_read_probe
 BENCH_MULTI := tools/libcts_bench_multi.so
 
 all: $(ENGINE_SO) oracle $(DEVICE_VERIFY) $(BENCH_MULTI) tools/pattern_cpu_probe
@@ -29,6 +30,10 @@ probes: $(PROBES)
 # bench.py's single-process leg (--engines N): the timed launches from one native thread per GPU
 $(BENCH_MULTI): tools/bench_multi.cpp $(ENGINE_SO) include/cts_engine.h
 	$(HIPCC) -O2 -std=c++17 -fPIC -shared -Iinclude $< -o $@ -Lctstraffic_amd -lcts_engine -Wl,-rpath,'$$ORIGIN/../ctstraffic_amd' -lpthread
+
+# the first counter read after cts_counters_allreduce_prepare, by thread and idle time (diagnostic)
+tools/first_read_probe: tools/first_read_probe.cpp $(ENGINE_SO) include/cts_engine.h
+	$(HIPCC) -O2 -std=c++17 -Iinclude $< -o $@ -Lctstraffic_amd -lcts_engine -Wl,-rpath,'$$ORIGIN/../ctstraffic_amd' -lpthread
 
 # SYNC-mode (per-completion) verify latency probe against the C ABI
 tools/sync_probe: tools/sync_probe.cpp $(ENGINE_SO) include/cts_engine.h
